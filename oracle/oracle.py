@@ -1,0 +1,192 @@
+"""ctypes wrapper for the CPU oracle (oracle/j2k_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker.  The product (grok_amd) never
+imports this module.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libj2k_oracle.so")
+_lib = None
+
+
+class CParams(ctypes.Structure):
+    _fields_ = [
+        ("numres", ctypes.c_uint32), ("cbw_exp", ctypes.c_uint32), ("cbh_exp", ctypes.c_uint32),
+        ("irreversible", ctypes.c_uint32), ("mct", ctypes.c_uint32), ("nlayers", ctypes.c_uint32),
+        ("write_com", ctypes.c_uint32),
+        ("prcw_exp", ctypes.c_uint32 * 33), ("prch_exp", ctypes.c_uint32 * 33),
+    ]
+
+
+class Block(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in
+                ("comp", "res", "band", "prc", "cblk", "x0", "y0", "x1", "y1", "numbps", "npasses", "len")] + \
+               [("data_off", ctypes.c_uint64)]
+
+
+def build():
+    """Compile the oracle with its Makefile (gcc only)."""
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.POINTER
+        _lib.orc_encode.restype = ctypes.c_size_t
+        _lib.orc_encode.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.c_uint32, ctypes.c_int, P(CParams), ctypes.c_void_p, ctypes.c_size_t]
+        _lib.orc_decode.restype = ctypes.c_int
+        _lib.orc_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p] + [P(ctypes.c_uint32)] * 4
+        _lib.orc_forward_coefs.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_int, P(CParams), P(ctypes.c_int32)]
+        _lib.orc_encode_blocks.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_int, P(CParams), ctypes.c_void_p,
+                                           P(ctypes.c_uint32), ctypes.c_void_p, P(ctypes.c_uint64)]
+        _lib.orc_t1_encode_cblk.restype = ctypes.c_int
+        _lib.orc_t1_encode_cblk.argtypes = [P(ctypes.c_int32)] + [ctypes.c_uint32] * 4 + [
+            ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_uint32), P(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_void_p]
+        _lib.orc_t1_decode_cblk.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [P(ctypes.c_int32)]
+        _lib.orc_default_params.argtypes = [P(CParams)]
+    return _lib
+
+
+def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None):
+    p = CParams()
+    lib().orc_default_params(ctypes.byref(p))
+    p.numres = numres
+    p.cbw_exp = int(cblk[0]).bit_length() - 1
+    p.cbh_exp = int(cblk[1]).bit_length() - 1
+    p.irreversible = int(irreversible)
+    p.mct = int(mct)
+    p.nlayers = nlayers
+    p.write_com = int(write_com)
+    if precincts:
+        # Grok CLI semantics: list of (w, h) from the highest resolution down; the last repeats
+        exps = [(int(w).bit_length() - 1, int(h).bit_length() - 1) for (w, h) in precincts]
+        for r in range(numres):
+            k = numres - 1 - r
+            e = exps[min(k, len(exps) - 1)]
+            if k >= len(exps):
+                # Grok halves the last specified precinct per lower resolution (min 1 = 2^1? keep >= cblk)
+                e = (max(exps[-1][0] - (k - len(exps) + 1), 1), max(exps[-1][1] - (k - len(exps) + 1), 1))
+            p.prcw_exp[r], p.prch_exp[r] = e
+    return p
+
+
+def _planes(img):
+    """img: (C, H, W) int32 array -> contiguous int32 planes."""
+    a = np.ascontiguousarray(img, dtype=np.int32)
+    assert a.ndim == 3
+    return a
+
+
+def encode(img, prec, signed=False, **kw):
+    a = _planes(img)
+    c, h, w = a.shape
+    p = params(**kw)
+    cap = a.nbytes * 2 + (1 << 16)
+    out = np.empty(cap, dtype=np.uint8)
+    n = lib().orc_encode(a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), w, h, c, prec, int(signed),
+                         ctypes.byref(p), out.ctypes.data, cap)
+    if n == 0:
+        raise RuntimeError("oracle encode failed")
+    return out[:n].tobytes()
+
+
+def decode(cs):
+    buf = np.frombuffer(cs, dtype=np.uint8).copy()
+    buf = np.concatenate([buf, np.zeros(8, np.uint8)])
+    W, H, NC, PREC = (ctypes.c_uint32() for _ in range(4))
+    rc = lib().orc_decode(buf.ctypes.data, len(cs), None, ctypes.byref(W), ctypes.byref(H), ctypes.byref(NC),
+                          ctypes.byref(PREC))
+    if rc != 0:
+        raise RuntimeError("oracle decode header failed: %d" % rc)
+    out = np.empty((NC.value, H.value, W.value), dtype=np.int32)
+    rc = lib().orc_decode(buf.ctypes.data, len(cs), out.ctypes.data, ctypes.byref(W), ctypes.byref(H),
+                          ctypes.byref(NC), ctypes.byref(PREC))
+    if rc != 0:
+        raise RuntimeError("oracle decode failed: %d" % rc)
+    return out, PREC.value
+
+
+def forward_coefs(img, prec, signed=False, **kw):
+    a = _planes(img)
+    c, h, w = a.shape
+    p = params(**kw)
+    out = np.empty_like(a)
+    lib().orc_forward_coefs(a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), w, h, c, prec, int(signed),
+                            ctypes.byref(p), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
+
+
+def encode_blocks(img, prec, signed=False, **kw):
+    """Per-block T1 results in canonical (comp, res, band, precinct, cblk) order."""
+    a = _planes(img)
+    c, h, w = a.shape
+    p = params(**kw)
+    nb = ctypes.c_uint32()
+    nbytes = ctypes.c_uint64()
+    ip = a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    lib().orc_encode_blocks(ip, w, h, c, prec, int(signed), ctypes.byref(p), None, ctypes.byref(nb), None,
+                            ctypes.byref(nbytes))
+    blocks = (Block * nb.value)()
+    data = np.empty(max(1, nbytes.value), dtype=np.uint8)
+    lib().orc_encode_blocks(ip, w, h, c, prec, int(signed), ctypes.byref(p), blocks, ctypes.byref(nb),
+                            data.ctypes.data, ctypes.byref(nbytes))
+    return blocks, data[:nbytes.value]
+
+
+def t1_encode_cblk(coef, orient):
+    a = np.ascontiguousarray(coef, dtype=np.int32)
+    h, w = a.shape
+    cap = w * h * 8 + 256
+    out = np.empty(cap, np.uint8)
+    nbps, npass = ctypes.c_uint32(), ctypes.c_uint32()
+    rates = np.zeros(256, np.uint32)
+    lens = np.zeros(256, np.uint32)
+    n = lib().orc_t1_encode_cblk(a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), w, h, w, orient, out.ctypes.data,
+                                 cap, ctypes.byref(nbps), ctypes.byref(npass), rates.ctypes.data, lens.ctypes.data)
+    return out[:n].tobytes(), nbps.value, npass.value, rates[:npass.value].copy(), lens[:npass.value].copy()
+
+
+def t1_decode_cblk(data, npasses, numbps, orient, w, h):
+    buf = np.frombuffer(data + b"\0" * 8, dtype=np.uint8).copy()
+    out = np.empty((h, w), np.int32)
+    lib().orc_t1_decode_cblk(buf.ctypes.data, len(data), npasses, numbps, orient, w, h,
+                             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
+
+
+# ---------------------------------------------------------------- PNM helpers
+def read_pnm(path):
+    with open(path, "rb") as f:
+        d = f.read()
+    toks, i = [], 0
+    while len(toks) < 4:
+        while d[i:i + 1].isspace():
+            i += 1
+        if d[i:i + 1] == b"#":
+            while d[i:i + 1] != b"\n":
+                i += 1
+            continue
+        j = i
+        while not d[j:j + 1].isspace():
+            j += 1
+        toks.append(d[i:j])
+        i = j
+    i += 1
+    w, h, m = int(toks[1]), int(toks[2]), int(toks[3])
+    c = 3 if toks[0] == b"P6" else 1
+    dt = np.dtype(np.uint8) if m < 256 else np.dtype(">u2")
+    a = np.frombuffer(d[i:i + w * h * c * dt.itemsize], dtype=dt).reshape(h, w, c)
+    return np.ascontiguousarray(a.transpose(2, 0, 1)).astype(np.int32), m
