@@ -1,0 +1,214 @@
+"""grok_amd — MI355X-native JPEG 2000 tile pipeline (host-side Python mirror).
+
+The product is the C-ABI library ``libgrok_amd.so`` (include/grok_amd.h):
+HIP kernels for gfx950 plus the native host engine (T2, codestream).  This
+module binds it with ctypes and mirrors the reference's compress/decompress
+call shape (grk_compress_* / grk_decompress_*, grok.h:1261-1451) for tests
+and the benchmark.  There is no CPU fallback: if the extension cannot be
+loaded, or no GPU is present, calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgrok_amd.so")
+
+GK_MAXRLVLS = 33
+GK_MAX_LAYERS = 100
+
+# Exported symbols declared in include/grok_amd.h (checked by tests/test_capi.py).
+EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_decode_header", "gk_decode",
+           "gk_get_timings", "gk_last_error", "gk_version")
+
+
+class CParameters(ctypes.Structure):
+    """gk_cparameters (include/grok_amd.h) — subset of grk_cparameters (grok.h:466-590)."""
+    _fields_ = [
+        ("numlayers", ctypes.c_uint16),
+        ("layer_rate", ctypes.c_double * GK_MAX_LAYERS),
+        ("numresolution", ctypes.c_uint8),
+        ("cblockw_init", ctypes.c_uint32), ("cblockh_init", ctypes.c_uint32),
+        ("cblk_sty", ctypes.c_uint8), ("irreversible", ctypes.c_uint8), ("mct", ctypes.c_uint8),
+        ("numgbits", ctypes.c_uint8), ("csty", ctypes.c_uint8),
+        ("res_spec", ctypes.c_uint32),
+        ("prcw_init", ctypes.c_uint32 * GK_MAXRLVLS), ("prch_init", ctypes.c_uint32 * GK_MAXRLVLS),
+        ("write_comment", ctypes.c_uint8),
+    ]
+
+
+class ImageInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("w", "h", "numcomps", "prec", "sgnd")]
+
+
+class Timings(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_float) for n in ("mct_ms", "dwt_ms", "t1_ms", "t2_ms", "assemble_ms", "total_ms")] + \
+               [("dwt_launches", ctypes.c_uint32), ("t1_blocks", ctypes.c_uint32), ("dwt_bytes", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def load_library(build_if_missing=True):
+    """Load the in-tree HIP extension (built by grok_amd.build / __graft_entry__.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        if not build_if_missing:
+            raise RuntimeError("libgrok_amd.so is missing: run __graft_entry__.build()")
+        from . import build as _b
+        _b.build()
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    lib.gk_create.restype = ctypes.c_void_p
+    lib.gk_create.argtypes = [ctypes.c_int]
+    lib.gk_destroy.argtypes = [ctypes.c_void_p]
+    lib.gk_set_default_params.argtypes = [P(CParameters)]
+    lib.gk_encode.restype = ctypes.c_int
+    lib.gk_encode.argtypes = [ctypes.c_void_p, P(ImageInfo), P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_int,
+                              P(CParameters), ctypes.c_void_p, ctypes.c_size_t, P(ctypes.c_size_t), ctypes.c_int]
+    lib.gk_decode_header.restype = ctypes.c_int
+    lib.gk_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ImageInfo)]
+    lib.gk_decode.restype = ctypes.c_int
+    lib.gk_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ctypes.c_void_p),
+                              P(ctypes.c_uint32), ctypes.c_int]
+    lib.gk_get_timings.restype = ctypes.c_int
+    lib.gk_get_timings.argtypes = [ctypes.c_void_p, P(Timings)]
+    lib.gk_last_error.restype = ctypes.c_char_p
+    lib.gk_last_error.argtypes = [ctypes.c_void_p]
+    lib.gk_version.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
+                   precincts=None, write_comment=True):
+    """grk_compress_set_default_params + the CLI options used by the benchmark configs."""
+    lib = load_library()
+    p = CParameters()
+    lib.gk_set_default_params(ctypes.byref(p))
+    p.numresolution = numresolution
+    p.cblockw_init, p.cblockh_init = cblk
+    p.irreversible = int(irreversible)
+    p.mct = int(mct)
+    p.numlayers = numlayers
+    if layer_rate:
+        for i, r in enumerate(layer_rate):
+            p.layer_rate[i] = r
+    if precincts:
+        p.csty |= 1
+        p.res_spec = len(precincts)
+        for i, (w, h) in enumerate(precincts):
+            p.prcw_init[i], p.prch_init[i] = w, h
+    p.write_comment = int(write_comment)
+    return p
+
+
+def _is_torch_cuda(x):
+    return hasattr(x, "is_cuda") and x.is_cuda
+
+
+class Engine:
+    """One MI355X, one HIP stream (grk_codec analogue)."""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        self.ctx = self.lib.gk_create(device)
+        if not self.ctx:
+            raise RuntimeError("gk_create failed: no HIP device %d" % device)
+
+    def close(self):
+        if self.ctx:
+            self.lib.gk_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, what):
+        raise RuntimeError("%s failed: %s" % (what, self.lib.gk_last_error(self.ctx).decode()))
+
+    def timings(self):
+        t = Timings()
+        self.lib.gk_get_timings(self.ctx, ctypes.byref(t))
+        return t
+
+    # ------------------------------------------------------------------ encode
+    def encode(self, planes, prec, signed=False, params=None, out=None):
+        """planes: (C, H, W) int32 numpy array (host) or torch cuda tensor (device).
+        Returns bytes (host) or, when ``out`` (a torch cuda uint8 tensor) is given,
+        the codestream length written into it on the device."""
+        if params is None:
+            params = default_params()
+        c, h, w = planes.shape
+        info = ImageInfo(w, h, c, prec, int(signed))
+        on_dev = _is_torch_cuda(planes)
+        if on_dev:
+            assert planes.dtype.__str__() == "torch.int32" and planes.is_contiguous()
+            base = planes.data_ptr()
+            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+        else:
+            planes = np.ascontiguousarray(planes, dtype=np.int32)
+            base = planes.ctypes.data
+            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+        strides = (ctypes.c_uint32 * c)(*([w] * c))
+        n = ctypes.c_size_t()
+        if out is not None:
+            rc = self.lib.gk_encode(self.ctx, ctypes.byref(info), ptrs, strides, int(on_dev), ctypes.byref(params),
+                                    ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(n), 1)
+            if rc != 0:
+                self._err("gk_encode")
+            return n.value
+        cap = c * h * w * 4 + (1 << 20)
+        buf = np.empty(cap, np.uint8)
+        rc = self.lib.gk_encode(self.ctx, ctypes.byref(info), ptrs, strides, int(on_dev), ctypes.byref(params),
+                                buf.ctypes.data, cap, ctypes.byref(n), 0)
+        if rc == -2:
+            buf = np.empty(n.value, np.uint8)
+            rc = self.lib.gk_encode(self.ctx, ctypes.byref(info), ptrs, strides, int(on_dev), ctypes.byref(params),
+                                    buf.ctypes.data, n.value, ctypes.byref(n), 0)
+        if rc != 0:
+            self._err("gk_encode")
+        return buf[:n.value].tobytes()
+
+    # ------------------------------------------------------------------ decode
+    def read_header(self, cs, length=None):
+        info = ImageInfo()
+        if _is_torch_cuda(cs):
+            rc = self.lib.gk_decode_header(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, ctypes.byref(info))
+        else:
+            b = np.frombuffer(cs, np.uint8)
+            rc = self.lib.gk_decode_header(self.ctx, b.ctypes.data, len(cs), 0, ctypes.byref(info))
+        if rc != 0:
+            self._err("gk_decode_header")
+        return info
+
+    def decode(self, cs, length=None, out=None):
+        """cs: bytes (host) or torch cuda uint8 tensor (+length).  Returns a
+        (C, H, W) int32 numpy array, or fills ``out`` (torch cuda int32) in place."""
+        on_dev = _is_torch_cuda(cs)
+        info = self.read_header(cs, length)
+        c, h, w = info.numcomps, info.h, info.w
+        strides = (ctypes.c_uint32 * c)(*([w] * c))
+        if out is not None:
+            base = out.data_ptr()
+            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+            res, out_dev = out, 1
+        else:
+            res = np.empty((c, h, w), np.int32)
+            base = res.ctypes.data
+            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+            out_dev = 0
+        if on_dev:
+            rc = self.lib.gk_decode(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, ptrs, strides, out_dev)
+        else:
+            b = np.frombuffer(cs, np.uint8)
+            rc = self.lib.gk_decode(self.ctx, b.ctypes.data, len(cs), 0, ptrs, strides, out_dev)
+        if rc != 0:
+            self._err("gk_decode")
+        return res

@@ -1,0 +1,48 @@
+// gk_common.h — descriptors shared by the host engine and the HIP kernels.
+//
+// Layout in HBM (DESIGN.md §Data layout):
+//   * a tile component is planar int32 (or f32 for 9/7), row stride = align32(width)
+//     samples (Grok's grkMakeAlignedWidth, cache/MemManager.cpp:35-43);
+//   * the forward DWT ping-pongs between two full-size work planes per component
+//     (A, B); level l writes its four subbands in Mallat placement into plane
+//     (l odd ? B : A), so every band is a (ptr, stride, w, h) window;
+//   * T1 reads/writes code-blocks straight out of those band windows.
+#pragma once
+#include <stdint.h>
+
+#define GK_MAX_RES 33
+#define GK_CTX 19
+
+// One code-block job (encode or decode).
+struct GkBlock {
+    uint64_t band_off;     // element offset of the block's top-left sample in the coefficient arena
+    uint32_t stride;       // row stride in elements
+    uint16_t w, h;         // block size (w <= 64, h <= 64 in this round)
+    uint8_t orient;        // 0 LL, 1 HL, 2 LH, 3 HH
+    uint8_t comp;
+    uint8_t band_numbps;   // Quantizer.cpp:45-49 (decode: numbps - k_msbs)
+    uint8_t flags;         // bit0: irreversible
+    float step;            // 9/7 encode: band stepsize (divisor, T1Part1.cpp:70-76); decode: stepsize/2 (ScaleFilter)
+    // encode outputs / decode inputs
+    uint64_t data_off;     // byte offset of the block's compressed data (slot) in the byte arena
+    uint32_t data_cap;     // slot capacity (encode)
+    uint32_t numbps;       // encode: output; decode: input (cblk->numbps)
+    uint32_t npasses;      // encode: output; decode: input
+    uint32_t len;          // encode: output bytes; decode: input bytes
+};
+
+// Pass information written by the encoder (max 3*31-2 passes per block).
+#define GK_MAX_PASSES 96
+struct GkPass {
+    uint32_t rate;
+    uint32_t len;
+    float dist;            // cumulative weighted distortion decrease (rate control)
+    uint32_t term;
+};
+
+// 2D window for DWT/MCT kernels.
+struct GkPlane {
+    uint64_t off;          // element offset in arena
+    uint32_t stride;
+    uint32_t w, h;
+};

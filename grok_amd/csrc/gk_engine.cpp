@@ -1,0 +1,1058 @@
+// gk_engine.cpp — host orchestration of the MI355X JPEG 2000 tile pipeline.
+//
+// Encode (TileProcessor::doCompress, TileProcessor.cpp:202-260):
+//   H2D (optional) -> DC shift + MCT -> 5/3 DWT levels -> T1 encode (one wave
+//   per code-block) -> D2H of per-block (numbps, passes, length) -> host T2
+//   packet headers (T2Compress.cpp:113-240) -> device gather of headers and
+//   code-block bytes into the codestream (-> D2H if the caller wants host bytes).
+// Decode (TileProcessor::decompressT2T1, TileProcessor.cpp:384-408):
+//   host T2 parse of packet headers (device-resident codestreams are read
+//   through a paged D2H reader) -> T1 decode -> inverse DWT -> inverse MCT.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/grok_amd.h"
+#include "gk_common.h"
+#include "gk_launch.h"
+
+namespace {
+
+static inline uint32_t ceildivpow2(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + (1ull << b) - 1) >> b); }
+static inline int floorlog2(uint32_t a) { int l = 0; while (a > 1) { a >>= 1; ++l; } return l; }
+static inline uint32_t align_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }
+
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { throw GkError(std::string(#x) + ": " + hipGetErrorString(e_)); } } while (0)
+
+struct GkError {
+    std::string msg;
+    explicit GkError(std::string m) : msg(std::move(m)) {}
+};
+
+// ---------------------------------------------------------------------------
+// Tile geometry (ISO 15444-1 Annex B; Grok Resolution.h:37-72,
+// Precinct.h:59-68).  Single tile anchored at the image origin.
+// ---------------------------------------------------------------------------
+struct Params {
+    uint32_t numres = 6, cbw = 6, cbh = 6, irrev = 0, mct = 1, numgbits = 2, nlayers = 1, write_com = 1;
+    uint32_t prcw[GK_MAXRLVLS], prch[GK_MAXRLVLS];
+    bool custom_prc = false;
+};
+
+struct BandG {
+    uint32_t orient, x0, y0, x1, y1;
+    uint32_t level;       // decomposition level (1..L), 0 for the final LL
+    uint32_t expn, mant, numbps;
+    float step_enc, step_dec;
+    uint32_t plane;       // 0 = A, 1 = B
+    uint32_t offx, offy;  // placement inside that plane
+    bool empty() const { return x1 <= x0 || y1 <= y0; }
+};
+struct PrecG {
+    uint32_t cw = 0, ch = 0;
+    uint32_t first_block = 0;   // index into Plan::blocks (canonical order)
+};
+struct ResG {
+    uint32_t w, h, pw, ph, cbw, cbh;
+    std::vector<BandG> bands;
+    std::vector<std::vector<PrecG>> prc;   // [band][precinct]
+};
+struct CompG {
+    std::vector<ResG> res;
+};
+
+struct Plan {
+    uint32_t w = 0, h = 0, nc = 0, prec = 0, sgnd = 0;
+    Params p;
+    uint32_t stride = 0;                 // work-plane stride (samples)
+    size_t plane_elems = 0;              // per plane
+    std::vector<CompG> comps;
+    std::vector<GkBlock> blocks;         // canonical order: comp, res, band, precinct, cblk
+    std::vector<uint32_t> resw, resh;    // resolution sizes by level l = 0..L (l=0: full)
+    uint64_t slot_bytes = 0;
+};
+
+static void assign_steps(Plan& P) {
+    for (auto& C : P.comps) {
+        for (uint32_t r = 0; r < P.p.numres; ++r) {
+            for (auto& B : C.res[r].bands) {
+                uint32_t level = P.p.numres - 1 - r;
+                uint32_t gain = P.p.irrev ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
+                // Part-1 QCD generation (HTParams.cpp:216-251)
+                static const double n97[4][10] = {
+                    {1.000, 1.965, 4.177, 8.403, 16.90, 33.84, 67.69, 135.3, 270.6, 540.9},
+                    {2.022, 3.989, 8.355, 17.04, 34.27, 68.63, 137.3, 274.6, 549.0},
+                    {2.022, 3.989, 8.355, 17.04, 34.27, 68.63, 137.3, 274.6, 549.0},
+                    {2.080, 3.865, 8.307, 17.18, 34.71, 69.59, 139.3, 278.6, 557.2}};
+                double stepsize = 1.0;
+                if (P.p.irrev) {
+                    uint32_t lv = level;
+                    if (B.orient == 0 && lv > 9) lv = 9; else if (B.orient > 0 && lv > 8) lv = 8;
+                    stepsize = (double)(1u << gain) / n97[B.orient][lv];
+                }
+                uint32_t step = (uint32_t)floor(stepsize * 8192.0);
+                int pp = floorlog2(step) - 13, n = 11 - floorlog2(step);
+                B.mant = (n < 0 ? step >> -n : step << n) & 0x7ff;
+                B.expn = (uint32_t)((int)(P.prec + gain) - pp);
+                // Quantizer::setBandStepSizeAndBps (Quantizer.cpp:26-66)
+                uint32_t lg_enc = B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1);
+                uint32_t lg_dec = P.p.irrev ? 0 : lg_enc;
+                B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
+                B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
+                int v = (int)B.expn + (int)P.p.numgbits - 1;
+                B.numbps = (uint32_t)std::max(0, v);
+            }
+        }
+    }
+}
+
+static void apply_qcd(Plan& P, const std::vector<std::pair<uint32_t, uint32_t>>& q) {
+    for (auto& C : P.comps) {
+        uint32_t bandno = 0;
+        for (uint32_t r = 0; r < P.p.numres; ++r)
+            for (auto& B : C.res[r].bands) {
+                size_t k = std::min<size_t>(bandno, q.size() - 1);
+                B.expn = q[k].first; B.mant = q[k].second;
+                uint32_t lg_enc = B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1);
+                uint32_t lg_dec = P.p.irrev ? 0 : lg_enc;
+                B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
+                B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
+                B.numbps = (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1);
+                ++bandno;
+            }
+    }
+}
+
+static void build_plan(Plan& P) {
+    const uint32_t L = P.p.numres - 1;
+    P.stride = align_up(std::max(P.w, 1u), 64);
+    P.plane_elems = (size_t)P.stride * P.h;
+    P.resw.resize(L + 1); P.resh.resize(L + 1);
+    for (uint32_t l = 0; l <= L; ++l) { P.resw[l] = ceildivpow2(P.w, l); P.resh[l] = ceildivpow2(P.h, l); }
+    P.comps.assign(P.nc, CompG());
+    P.blocks.clear();
+    for (uint32_t c = 0; c < P.nc; ++c) {
+        CompG& C = P.comps[c];
+        C.res.assign(P.p.numres, ResG());
+        for (uint32_t r = 0; r < P.p.numres; ++r) {
+            ResG& R = C.res[r];
+            uint32_t nb = L - r;
+            R.w = P.resw[nb]; R.h = P.resh[nb];
+            uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
+            R.pw = R.w ? ceildivpow2(R.w, pwe) : 0;
+            R.ph = R.h ? ceildivpow2(R.h, phe) : 0;
+            uint32_t bpw = r ? pwe - 1 : pwe, bph = r ? phe - 1 : phe;
+            R.cbw = std::min(P.p.cbw, bpw); R.cbh = std::min(P.p.cbh, bph);
+            uint32_t nbands = r ? 3 : 1;
+            R.bands.assign(nbands, BandG());
+            R.prc.assign(nbands, std::vector<PrecG>(R.pw * R.ph));
+            for (uint32_t bi = 0; bi < nbands; ++bi) {
+                BandG& B = R.bands[bi];
+                B.orient = r ? bi + 1 : 0;
+                if (!r) {
+                    B.x0 = 0; B.y0 = 0; B.x1 = R.w; B.y1 = R.h;
+                    B.level = L; B.offx = 0; B.offy = 0;
+                    B.plane = L == 0 ? 0 : ((L & 1) ? 1 : 0);
+                } else {
+                    uint32_t lev = P.p.numres - r;   // decomposition level of this band (1..L)
+                    uint32_t xo = B.orient & 1, yo = B.orient >> 1;
+                    uint64_t half = 1ull << (lev - 1);
+                    auto cb = [&](uint64_t t, uint32_t o) -> uint32_t {
+                        if (!o) return ceildivpow2((uint32_t)t, lev);
+                        return t <= half ? 0 : ceildivpow2((uint32_t)(t - half), lev);
+                    };
+                    B.x0 = cb(0, xo); B.y0 = cb(0, yo); B.x1 = cb(P.w, xo); B.y1 = cb(P.h, yo);
+                    B.level = lev;
+                    B.plane = (lev & 1) ? 1 : 0;
+                    B.offx = xo ? P.resw[lev] : 0;
+                    B.offy = yo ? P.resh[lev] : 0;
+                }
+            }
+        }
+    }
+    assign_steps(P);
+    // code-blocks, canonical order
+    for (uint32_t c = 0; c < P.nc; ++c) {
+        CompG& C = P.comps[c];
+        for (uint32_t r = 0; r < P.p.numres; ++r) {
+            ResG& R = C.res[r];
+            uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
+            uint32_t bpw = r ? pwe - 1 : pwe, bph = r ? phe - 1 : phe;
+            for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
+                BandG& B = R.bands[bi];
+                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                    PrecG& PG = R.prc[bi][pi];
+                    PG.first_block = (uint32_t)P.blocks.size();
+                    if (B.empty()) continue;
+                    uint32_t i = pi % R.pw, j = pi / R.pw;
+                    uint32_t cx0 = i << bpw, cy0 = j << bph;
+                    uint32_t px0 = std::max(cx0, B.x0), py0 = std::max(cy0, B.y0);
+                    uint32_t px1 = std::min(cx0 + (1u << bpw), B.x1), py1 = std::min(cy0 + (1u << bph), B.y1);
+                    if (px1 <= px0 || py1 <= py0) continue;
+                    uint32_t gx0 = (px0 >> R.cbw) << R.cbw, gy0 = (py0 >> R.cbh) << R.cbh;
+                    PG.cw = ((ceildivpow2(px1, R.cbw) << R.cbw) - gx0) >> R.cbw;
+                    PG.ch = ((ceildivpow2(py1, R.cbh) << R.cbh) - gy0) >> R.cbh;
+                    for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                        uint32_t a = k % PG.cw, b = k / PG.cw;
+                        uint32_t kx0 = gx0 + (a << R.cbw), ky0 = gy0 + (b << R.cbh);
+                        uint32_t x0 = std::max(kx0, px0), y0 = std::max(ky0, py0);
+                        uint32_t x1 = std::min(kx0 + (1u << R.cbw), px1), y1 = std::min(ky0 + (1u << R.cbh), py1);
+                        GkBlock G{};
+                        size_t plane_base = ((size_t)c * 2 + B.plane) * P.plane_elems;
+                        G.band_off = plane_base + (size_t)(B.offy + y0 - B.y0) * P.stride + (B.offx + x0 - B.x0);
+                        G.stride = P.stride;
+                        G.w = (uint16_t)(x1 - x0); G.h = (uint16_t)(y1 - y0);
+                        G.orient = (uint8_t)B.orient; G.comp = (uint8_t)c;
+                        G.band_numbps = (uint8_t)B.numbps;
+                        G.flags = P.p.irrev ? 1 : 0;
+                        G.step = B.step_enc;
+                        P.blocks.push_back(G);
+                    }
+                }
+            }
+        }
+    }
+    // encode slots: w*h*4 bytes + 16 (2-byte pad, alignment)
+    uint64_t off = 0;
+    for (auto& G : P.blocks) {
+        uint32_t cap = (uint32_t)G.w * G.h * 4 + 64;
+        G.data_off = off + 16;
+        G.data_cap = cap;
+        off += align_up(cap + 16, 64);
+    }
+    P.slot_bytes = off;
+}
+
+// ---------------------------------------------------------------------------
+// Packet-header bit writer / reader (t2/BitIO.cpp) and tag trees (t2/TagTree.h)
+// ---------------------------------------------------------------------------
+struct BitWriter {
+    std::vector<uint8_t>& o;
+    uint32_t buf = 0; int ct = 8;
+    explicit BitWriter(std::vector<uint8_t>& out) : o(out) {}
+    inline void wbyte() { o.push_back((uint8_t)buf); ct = (buf == 0xff) ? 7 : 8; buf = 0; }
+    inline void putbit(uint32_t b) { if (ct == 0) wbyte(); --ct; buf |= b << ct; }
+    inline void write(uint32_t v, int n) { for (int i = n - 1; i >= 0; --i) putbit((v >> i) & 1); }
+    void flush() { wbyte(); if (ct == 7) wbyte(); }
+    void commacode(uint32_t n) { for (uint32_t i = 0; i < n; ++i) putbit(1); putbit(0); }
+    void numpasses(uint32_t n) {
+        if (n == 1) write(0, 1);
+        else if (n == 2) write(2, 2);
+        else if (n <= 5) write(0xc | (n - 3), 4);
+        else if (n <= 36) write(0x1e0 | (n - 6), 9);
+        else write(0xff80 | (n - 37), 16);
+    }
+};
+
+struct TagTree {
+    std::vector<int32_t> parent;
+    std::vector<uint32_t> value, low;
+    std::vector<uint8_t> known;
+    void build(uint32_t nw, uint32_t nh) {
+        std::vector<uint32_t> lw{nw}, lh{nh};
+        size_t total = 0;
+        while (true) {
+            total += (size_t)lw.back() * lh.back();
+            if ((size_t)lw.back() * lh.back() <= 1) break;
+            lw.push_back((lw.back() + 1) / 2); lh.push_back((lh.back() + 1) / 2);
+        }
+        parent.assign(total, -1);
+        size_t base = 0;
+        for (size_t l = 0; l + 1 < lw.size(); ++l) {
+            size_t nbase = base + (size_t)lw[l] * lh[l];
+            for (uint32_t y = 0; y < lh[l]; ++y)
+                for (uint32_t x = 0; x < lw[l]; ++x)
+                    parent[base + (size_t)y * lw[l] + x] = (int32_t)(nbase + (size_t)(y / 2) * lw[l + 1] + x / 2);
+            base = nbase;
+        }
+        value.assign(total, 0xffffffffu); low.assign(total, 0); known.assign(total, 0);
+    }
+    void reset() {
+        std::fill(value.begin(), value.end(), 0xffffffffu);
+        std::fill(low.begin(), low.end(), 0u);
+        std::fill(known.begin(), known.end(), 0);
+    }
+    void setvalue(uint32_t leaf, uint32_t v) {
+        int32_t n = (int32_t)leaf;
+        while (n >= 0 && value[n] > v) { value[n] = v; n = parent[n]; }
+    }
+    void encode(BitWriter& bw, uint32_t leaf, uint32_t threshold) {
+        int32_t stk[40]; int sp = 0; int32_t n = (int32_t)leaf;
+        while (parent[n] >= 0) { stk[sp++] = n; n = parent[n]; }
+        uint32_t lo = 0;
+        while (true) {
+            if (low[n] < lo) low[n] = lo; else lo = low[n];
+            while (lo < threshold) {
+                if (lo >= value[n]) { if (!known[n]) { bw.putbit(1); known[n] = 1; } break; }
+                bw.putbit(0); ++lo;
+            }
+            low[n] = lo;
+            if (!sp) break;
+            n = stk[--sp];
+        }
+    }
+};
+
+// Random-access byte source for decode: host memory, or device memory read
+// through 64 KiB D2H pages.
+struct ByteSrc {
+    const uint8_t* host = nullptr;
+    const uint8_t* dev = nullptr;
+    size_t len = 0;
+    hipStream_t st = nullptr;
+    static const size_t PG = 1 << 16;
+    std::unordered_map<size_t, std::vector<uint8_t>> pages;
+    uint8_t at(size_t i) {
+        if (i >= len) return 0;
+        if (host) return host[i];
+        size_t pg = i / PG;
+        auto it = pages.find(pg);
+        if (it == pages.end()) {
+            size_t o = pg * PG, n = std::min(PG, len - o);
+            std::vector<uint8_t> v(n);
+            HIPCHK(hipMemcpyAsync(v.data(), dev + o, n, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            it = pages.emplace(pg, std::move(v)).first;
+        }
+        return it->second[i - pg * PG];
+    }
+    uint32_t be16(size_t i) { return ((uint32_t)at(i) << 8) | at(i + 1); }
+    uint32_t be32(size_t i) { return (be16(i) << 16) | be16(i + 2); }
+};
+
+struct BitReader {
+    ByteSrc& s; size_t off; size_t end; uint32_t buf = 0; int ct = 0;
+    BitReader(ByteSrc& src, size_t o, size_t e) : s(src), off(o), end(e) {}
+    inline void bytein() { ct = (buf == 0xff) ? 7 : 8; buf = off < end ? s.at(off) : 0; ++off; }
+    inline uint32_t getbit() { if (ct == 0) bytein(); --ct; return (buf >> ct) & 1; }
+    inline uint32_t read(int n) { uint32_t v = 0; for (int i = n - 1; i >= 0; --i) v |= getbit() << i; return v; }
+    void align() { if (buf == 0xff) bytein(); ct = 0; }
+    uint32_t numpasses() {
+        if (!read(1)) return 1;
+        if (!read(1)) return 2;
+        uint32_t n = read(2);
+        if (n != 3) return n + 3;
+        n = read(5);
+        if (n != 31) return n + 6;
+        return read(7) + 37;
+    }
+    uint32_t commacode() { uint32_t n = 0; while (read(1)) ++n; return n; }
+};
+
+struct DecTree {   // decoder-side tag tree
+    std::vector<int32_t> parent;
+    std::vector<uint32_t> value, low;
+    void build(uint32_t nw, uint32_t nh) {
+        TagTree t; t.build(nw, nh);
+        parent = t.parent; value.assign(parent.size(), 0xffffffffu); low.assign(parent.size(), 0);
+    }
+    uint32_t decode(BitReader& br, uint32_t leaf, uint32_t threshold) {
+        int32_t stk[40]; int sp = 0; int32_t n = (int32_t)leaf;
+        while (parent[n] >= 0) { stk[sp++] = n; n = parent[n]; }
+        uint32_t lo = 0;
+        while (true) {
+            if (low[n] < lo) low[n] = lo; else lo = low[n];
+            while (lo < threshold && lo < value[n]) {
+                if (br.read(1)) { value[n] = lo; break; }
+                ++lo;
+            }
+            low[n] = lo;
+            if (!sp) break;
+            n = stk[--sp];
+        }
+        return value[n];
+    }
+};
+
+static void put16(std::vector<uint8_t>& o, uint32_t v) { o.push_back((uint8_t)(v >> 8)); o.push_back((uint8_t)v); }
+static void put32(std::vector<uint8_t>& o, uint32_t v) { put16(o, v >> 16); put16(o, v & 0xffff); }
+
+// Main header: SOC SIZ COD QCD [COM]  (CodeStreamCompress.cpp:1054-1685 marker writers)
+static void write_main_header(std::vector<uint8_t>& o, const Plan& P) {
+    put16(o, 0xff4f);
+    put16(o, 0xff51); put16(o, 38 + 3 * P.nc);
+    put16(o, 0);
+    put32(o, P.w); put32(o, P.h); put32(o, 0); put32(o, 0);
+    put32(o, P.w); put32(o, P.h); put32(o, 0); put32(o, 0);
+    put16(o, P.nc);
+    for (uint32_t i = 0; i < P.nc; ++i) { o.push_back((uint8_t)((P.prec - 1) | (P.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
+    put16(o, 0xff52); put16(o, 12 + (P.p.custom_prc ? P.p.numres : 0));
+    o.push_back(P.p.custom_prc ? 1 : 0);
+    o.push_back(0);   // LRCP
+    put16(o, P.p.nlayers);
+    o.push_back((uint8_t)((P.p.mct && P.nc >= 3) ? 1 : 0));
+    o.push_back((uint8_t)(P.p.numres - 1));
+    o.push_back((uint8_t)(P.p.cbw - 2)); o.push_back((uint8_t)(P.p.cbh - 2));
+    o.push_back(0);
+    o.push_back(P.p.irrev ? 0 : 1);
+    if (P.p.custom_prc) for (uint32_t r = 0; r < P.p.numres; ++r) o.push_back((uint8_t)(P.p.prcw[r] | (P.p.prch[r] << 4)));
+    uint32_t nbands = 3 * P.p.numres - 2;
+    put16(o, 0xff5c);
+    const CompG& C = P.comps[0];
+    if (!P.p.irrev) {
+        put16(o, 3 + nbands);
+        o.push_back((uint8_t)(P.p.numgbits << 5));
+        for (uint32_t r = 0; r < P.p.numres; ++r) for (auto& B : C.res[r].bands) o.push_back((uint8_t)(B.expn << 3));
+    } else {
+        put16(o, 3 + 2 * nbands);
+        o.push_back((uint8_t)((P.p.numgbits << 5) | 2));
+        for (uint32_t r = 0; r < P.p.numres; ++r) for (auto& B : C.res[r].bands) put16(o, (B.expn << 11) | B.mant);
+    }
+    if (P.p.write_com) {
+        const char* txt = "Created by Grok     version 9.2.0";
+        put16(o, 0xff64); put16(o, 4 + (uint32_t)strlen(txt)); put16(o, 1);
+        o.insert(o.end(), txt, txt + strlen(txt));
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Context
+// ---------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr; size_t cap = 0;
+    void* get(size_t n) {
+        if (n > cap) {
+            if (p) (void)hipFree(p);
+            p = nullptr; cap = 0;
+            size_t c = std::max(n, (size_t)1 << 20);
+            HIPCHK(hipMalloc(&p, c));
+            cap = c;
+        }
+        return p;
+    }
+    ~DevBuf() { if (p) (void)hipFree(p); }
+};
+struct HostBuf {
+    void* p = nullptr; size_t cap = 0;
+    void* get(size_t n) {
+        if (n > cap) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr; cap = 0;
+            size_t c = std::max(n, (size_t)1 << 20);
+            HIPCHK(hipHostMalloc(&p, c, 0));
+            cap = c;
+        }
+        return p;
+    }
+    ~HostBuf() { if (p) (void)hipHostFree(p); }
+};
+
+struct gk_ctx {
+    int device = 0;
+    hipStream_t st = nullptr;
+    std::string err;
+    gk_timings tm{};
+    // cached plan
+    std::string plan_key;
+    Plan plan;
+    // device buffers
+    DevBuf arena;       // int32 work planes: nc * 2 * plane_elems
+    DevBuf bytes;       // encode slots + header staging / decode staging
+    DevBuf dblocks;     // GkBlock table
+    DevBuf dpasses;     // GkPass per block
+    DevBuf dinfo;       // 3 u32 per block
+    DevBuf dseg;        // gather segments
+    DevBuf dout;        // codestream (encode, when the caller wants host bytes) / input (decode from host)
+    DevBuf dplanes;     // component planes staged from host
+    DevBuf derr;
+    HostBuf hinfo, hseg, hhdr;
+    hipEvent_t ev[32];
+    bool blocks_uploaded = false;
+};
+
+static void set_params(Params& P, const gk_cparameters* cp) {
+    for (int i = 0; i < GK_MAXRLVLS; ++i) { P.prcw[i] = 15; P.prch[i] = 15; }
+    if (!cp) return;
+    P.numres = cp->numresolution ? cp->numresolution : 6;
+    P.cbw = (uint32_t)floorlog2(cp->cblockw_init ? cp->cblockw_init : 64);
+    P.cbh = (uint32_t)floorlog2(cp->cblockh_init ? cp->cblockh_init : 64);
+    P.irrev = cp->irreversible ? 1 : 0;
+    P.mct = cp->mct;
+    P.numgbits = cp->numgbits ? cp->numgbits : 2;
+    P.nlayers = cp->numlayers ? cp->numlayers : 1;
+    P.write_com = cp->write_comment;
+    if ((cp->csty & 1) && cp->res_spec) {   // CodeStreamCompress.cpp:542-590
+        P.custom_prc = true;
+        uint32_t p = 0;
+        for (int r = (int)P.numres - 1; r >= 0; --r, ++p) {
+            uint32_t pw, ph;
+            if (p < cp->res_spec) { pw = cp->prcw_init[p]; ph = cp->prch_init[p]; }
+            else {
+                pw = cp->prcw_init[cp->res_spec - 1] >> (p - (cp->res_spec - 1));
+                ph = cp->prch_init[cp->res_spec - 1] >> (p - (cp->res_spec - 1));
+            }
+            P.prcw[r] = pw < 1 ? 1 : (uint32_t)floorlog2(pw);
+            P.prch[r] = ph < 1 ? 1 : (uint32_t)floorlog2(ph);
+        }
+    }
+}
+
+static std::string plan_key(const Plan& P) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
+             P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0);
+    std::string k(buf);
+    for (uint32_t r = 0; r < P.p.numres; ++r) k += " " + std::to_string(P.p.prcw[r]) + "," + std::to_string(P.p.prch[r]);
+    return k;
+}
+
+static void ensure_plan(gk_ctx* ctx, const Plan& want) {
+    std::string k = plan_key(want);
+    if (k == ctx->plan_key) return;
+    ctx->plan = want;
+    build_plan(ctx->plan);
+    ctx->plan_key = k;
+    ctx->blocks_uploaded = false;
+}
+
+// Forward/inverse DWT over all components with the ping-pong placement of gk_common.h.
+static void run_dwt(gk_ctx* ctx, bool forward) {
+    Plan& P = ctx->plan;
+    int32_t* arena = (int32_t*)ctx->arena.p;
+    const uint32_t L = P.p.numres - 1;
+    ctx->tm.dwt_launches = 0; ctx->tm.dwt_bytes = 0;
+    for (uint32_t i = 0; i < L; ++i) {
+        uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
+        uint32_t w = P.resw[l - 1], h = P.resh[l - 1];
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            int32_t* A = arena + (size_t)c * 2 * P.plane_elems;
+            int32_t* B = A + P.plane_elems;
+            int32_t* src_l = (l & 1) ? A : B;     // D_{l-1}: level l input plane (l-1 odd -> B)
+            int32_t* dst_l = (l & 1) ? B : A;     // D_l
+            if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, P.stride, dst_l, P.stride, w, h);
+            else gk_launch_dwt53_inv(ctx->st, dst_l, P.stride, src_l, P.stride, w, h);
+            ctx->tm.dwt_launches++;
+            ctx->tm.dwt_bytes += (uint64_t)w * h * 8;
+        }
+    }
+}
+
+static float ev_ms(gk_ctx* ctx, int a, int b) {
+    float ms = 0; (void)hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]); return ms;
+}
+
+// ---------------------------------------------------------------------------
+// Encode
+// ---------------------------------------------------------------------------
+static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+                          int comps_on_device, const gk_cparameters* cp, uint8_t* out, size_t cap, int out_on_device,
+                          int* rc) {
+    Plan want;
+    want.w = info->w; want.h = info->h; want.nc = info->numcomps; want.prec = info->prec; want.sgnd = info->sgnd;
+    set_params(want.p, cp);
+    if (want.nc < 3) want.p.mct = 0;
+    if (want.p.irrev) throw GkError("9/7 irreversible encode is not implemented on the GPU path yet");
+    if (cp && cp->cblk_sty) throw GkError("code-block style mode switches are not supported");
+    if (want.p.nlayers != 1) throw GkError("only single-layer lossless encode is supported on the GPU path");
+    if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
+    if ((1u << want.p.cbw) > 64 || (1u << want.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
+    ensure_plan(ctx, want);
+    Plan& P = ctx->plan;
+    const uint32_t nb = (uint32_t)P.blocks.size();
+    hipStream_t st = ctx->st;
+
+    HIPCHK(hipEventRecord(ctx->ev[0], st));
+    int32_t* arena = (int32_t*)ctx->arena.get(P.plane_elems * P.nc * 2 * sizeof(int32_t));
+    // stage host planes
+    std::vector<const int32_t*> src(P.nc);
+    std::vector<uint32_t> sstr(P.nc);
+    if (!comps_on_device) {
+        int32_t* dp = (int32_t*)ctx->dplanes.get((size_t)P.w * P.h * P.nc * 4);
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * P.h, (size_t)P.w * 4, comps[c], (size_t)strides[c] * 4,
+                                    (size_t)P.w * 4, P.h, hipMemcpyHostToDevice, st));
+            src[c] = dp + (size_t)c * P.w * P.h; sstr[c] = P.w;
+        }
+    } else {
+        for (uint32_t c = 0; c < P.nc; ++c) { src[c] = comps[c]; sstr[c] = strides[c]; }
+    }
+    HIPCHK(hipEventRecord(ctx->ev[1], st));
+    // DC shift + MCT into plane A of each component
+    int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
+    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems; };
+    if (P.p.mct && P.nc >= 3) {
+        gk_launch_dc_rct_fwd(st, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), P.stride, P.w, P.h, shift);
+        for (uint32_t c = 3; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), P.stride, P.w, P.h, shift);
+    } else {
+        for (uint32_t c = 0; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), P.stride, P.w, P.h, shift);
+    }
+    HIPCHK(hipEventRecord(ctx->ev[2], st));
+    run_dwt(ctx, true);
+    HIPCHK(hipEventRecord(ctx->ev[3], st));
+    // T1
+    uint8_t* dbytes = (uint8_t*)ctx->bytes.get(P.slot_bytes + (64u << 20));
+    GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * std::max(nb, 1u));
+    GkPass* dps = (GkPass*)ctx->dpasses.get(sizeof(GkPass) * GK_MAX_PASSES * (size_t)std::max(nb, 1u));
+    uint32_t* dinfo = (uint32_t*)ctx->dinfo.get(12 * (size_t)std::max(nb, 1u));
+    int* derr = (int*)ctx->derr.get(64);
+    if (!ctx->blocks_uploaded) {
+        HIPCHK(hipMemcpyAsync(dblk, P.blocks.data(), sizeof(GkBlock) * nb, hipMemcpyHostToDevice, st));
+        ctx->blocks_uploaded = true;
+    }
+    HIPCHK(hipMemsetAsync(derr, 0, 4, st));
+    gk_launch_t1_encode(st, arena, dblk, dbytes, dps, dinfo, nb, derr);
+    HIPCHK(hipEventRecord(ctx->ev[4], st));
+    uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(12 * (size_t)nb + 16);
+    HIPCHK(hipMemcpyAsync(hinfo, dinfo, 12 * (size_t)nb, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hinfo + 3 * (size_t)nb, derr, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (hinfo[3 * (size_t)nb]) throw GkError("T1 code-block slot overflow");
+
+    // ---- host T2 (T2Compress.cpp:113-240), single layer / all passes
+    std::vector<uint8_t> H;
+    H.reserve(1 << 12);
+    write_main_header(H, P);
+    size_t sot = H.size();
+    put16(H, 0xff90); put16(H, 10); put16(H, 0); put32(H, 0); H.push_back(0); H.push_back(1);
+    put16(H, 0xff93);
+    // segments: (src_off in dbytes, dst_off in codestream, len); headers staged after the slots
+    std::vector<uint64_t> seg;
+    seg.reserve(3 * ((size_t)nb + 64));
+    std::vector<uint8_t> hdrs;   // all host bytes, in order, copied to staging
+    uint64_t pos = 0;            // codestream position
+    auto add_host = [&](const uint8_t* p, size_t n) {
+        if (!n) return;
+        seg.push_back(P.slot_bytes + hdrs.size()); seg.push_back(pos); seg.push_back(n);
+        hdrs.insert(hdrs.end(), p, p + n);
+        pos += n;
+    };
+    add_host(H.data(), H.size());
+    TagTree incl, imsb;
+    std::vector<uint8_t> ph;
+    ph.reserve(1 << 16);
+    for (uint32_t r = 0; r < P.p.numres; ++r)
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            ResG& R = P.comps[c].res[r];
+            for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                ph.clear();
+                BitWriter bw(ph);
+                bw.putbit(1);
+                for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
+                    PrecG& PG = R.prc[bi][pi];
+                    if (!PG.cw || !PG.ch) continue;
+                    const BandG& B = R.bands[bi];
+                    uint32_t n = PG.cw * PG.ch;
+                    incl.build(PG.cw, PG.ch); imsb.build(PG.cw, PG.ch);
+                    for (uint32_t k = 0; k < n; ++k) {
+                        const uint32_t* inf = hinfo + 3 * (size_t)(PG.first_block + k);
+                        imsb.setvalue(k, B.numbps - inf[0]);
+                        if (inf[1]) incl.setvalue(k, 0);
+                    }
+                    for (uint32_t k = 0; k < n; ++k) {
+                        const uint32_t* inf = hinfo + 3 * (size_t)(PG.first_block + k);
+                        uint32_t np = inf[1], len = inf[2];
+                        incl.encode(bw, k, 1);
+                        if (!np) continue;
+                        imsb.encode(bw, k, 0xffffffffu);
+                        bw.numpasses(np);
+                        int inc = std::max(0, floorlog2(len) + 1 - (3 + floorlog2(np)));
+                        bw.commacode((uint32_t)inc);
+                        bw.write(len, 3 + inc + floorlog2(np));
+                    }
+                }
+                bw.flush();
+                add_host(ph.data(), ph.size());
+                for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
+                    PrecG& PG = R.prc[bi][pi];
+                    for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                        uint32_t b = PG.first_block + k;
+                        uint32_t len = hinfo[3 * (size_t)b + 2];
+                        if (!hinfo[3 * (size_t)b + 1] || !len) continue;
+                        seg.push_back(P.blocks[b].data_off); seg.push_back(pos); seg.push_back(len);
+                        pos += len;
+                    }
+                }
+            }
+        }
+    uint8_t eoc[2] = {0xff, 0xd9};
+    // Psot patch: tile-part length from SOT to end of tile data
+    uint32_t psot = (uint32_t)(pos - sot);
+    hdrs[sot + 6] = (uint8_t)(psot >> 24); hdrs[sot + 7] = (uint8_t)(psot >> 16);
+    hdrs[sot + 8] = (uint8_t)(psot >> 8); hdrs[sot + 9] = (uint8_t)psot;
+    add_host(eoc, 2);
+    const size_t total = pos;
+    HIPCHK(hipEventRecord(ctx->ev[5], st));
+    if (total > cap) { *rc = -2; return total; }
+    // ---- device assembly
+    if (hdrs.size() > (64u << 20)) throw GkError("packet headers exceed staging");
+    uint8_t* hh = (uint8_t*)ctx->hhdr.get(hdrs.size());
+    memcpy(hh, hdrs.data(), hdrs.size());
+    HIPCHK(hipMemcpyAsync(dbytes + P.slot_bytes, hh, hdrs.size(), hipMemcpyHostToDevice, st));
+    uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8);
+    memcpy(hs, seg.data(), seg.size() * 8);
+    uint64_t* ds = (uint64_t*)ctx->dseg.get(seg.size() * 8);
+    HIPCHK(hipMemcpyAsync(ds, hs, seg.size() * 8, hipMemcpyHostToDevice, st));
+    uint8_t* dst = out_on_device ? out : (uint8_t*)ctx->dout.get(total);
+    gk_launch_gather(st, dbytes, dst, ds, (uint32_t)(seg.size() / 3));
+    HIPCHK(hipEventRecord(ctx->ev[6], st));
+    if (!out_on_device) HIPCHK(hipMemcpyAsync(out, dst, total, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(ctx->ev[7], st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->tm.mct_ms = ev_ms(ctx, 1, 2);
+    ctx->tm.dwt_ms = ev_ms(ctx, 2, 3);
+    ctx->tm.t1_ms = ev_ms(ctx, 3, 4);
+    ctx->tm.t2_ms = ev_ms(ctx, 4, 5);
+    ctx->tm.assemble_ms = ev_ms(ctx, 5, 7);
+    ctx->tm.total_ms = ev_ms(ctx, 0, 7);
+    ctx->tm.t1_blocks = nb;
+    *rc = 0;
+    return total;
+}
+
+// ---------------------------------------------------------------------------
+// Decode
+// ---------------------------------------------------------------------------
+struct Header {
+    Plan want;
+    std::vector<std::pair<uint32_t, uint32_t>> qcd;
+    size_t tile_data = 0, tile_end = 0;
+};
+
+static void parse_header(ByteSrc& S, Header& Hd) {
+    size_t i = 0;
+    if (S.len < 4 || S.be16(0) != 0xff4f) throw GkError("not a J2K codestream (no SOC)");
+    i = 2;
+    Plan& W = Hd.want;
+    for (int k = 0; k < GK_MAXRLVLS; ++k) { W.p.prcw[k] = 15; W.p.prch[k] = 15; }
+    bool have_siz = false, have_cod = false;
+    while (i + 4 <= S.len) {
+        uint32_t m = S.be16(i);
+        if (m == 0xff93) { Hd.tile_data = i + 2; break; }
+        uint32_t L = S.be16(i + 2);
+        size_t s = i + 4;
+        if (m == 0xff51) {
+            W.w = S.be32(s + 2) - S.be32(s + 10); W.h = S.be32(s + 6) - S.be32(s + 14);
+            if (S.be32(s + 10) || S.be32(s + 14)) throw GkError("image offsets not supported");
+            if (S.be32(s + 18) < S.be32(s + 2) || S.be32(s + 22) < S.be32(s + 6)) throw GkError("multi-tile codestreams not supported on this path yet");
+            W.nc = S.be16(s + 34);
+            uint32_t sz = S.at(s + 36);
+            W.prec = (sz & 0x7f) + 1; W.sgnd = (sz & 0x80) ? 1 : 0;
+            for (uint32_t c = 0; c < W.nc; ++c) {
+                if (S.at(s + 37 + 3 * c) != 1 || S.at(s + 38 + 3 * c) != 1) throw GkError("component subsampling not supported");
+                if (((S.at(s + 36 + 3 * c) & 0x7f) + 1) != W.prec) throw GkError("mixed component precision not supported");
+            }
+            have_siz = true;
+        } else if (m == 0xff52) {
+            uint32_t scod = S.at(s);
+            if (S.at(s + 1) != 0) throw GkError("only LRCP progression supported");
+            if (scod & 6) throw GkError("SOP/EPH markers not supported");
+            W.p.nlayers = S.be16(s + 2);
+            W.p.mct = S.at(s + 4);
+            W.p.numres = S.at(s + 5) + 1;
+            W.p.cbw = S.at(s + 6) + 2; W.p.cbh = S.at(s + 7) + 2;
+            if (S.at(s + 8)) throw GkError("code-block style mode switches not supported");
+            W.p.irrev = S.at(s + 9) == 0 ? 1 : 0;
+            if (scod & 1) {
+                W.p.custom_prc = true;
+                for (uint32_t r = 0; r < W.p.numres; ++r) { uint32_t v = S.at(s + 10 + r); W.p.prcw[r] = v & 15; W.p.prch[r] = v >> 4; }
+            }
+            have_cod = true;
+        } else if (m == 0xff5c) {
+            uint32_t sq = S.at(s);
+            W.p.numgbits = sq >> 5;
+            uint32_t qt = sq & 0x1f;
+            Hd.qcd.clear();
+            if (qt == 0) for (uint32_t k = 1; k < L - 2; ++k) Hd.qcd.push_back({(uint32_t)S.at(s + k) >> 3, 0u});
+            else if (qt == 2) for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = S.be16(s + k); Hd.qcd.push_back({v >> 11, v & 0x7ff}); }
+            else throw GkError("scalar-derived quantisation not supported");
+        } else if (m == 0xff90) {
+            uint32_t psot = S.be32(s + 2);
+            Hd.tile_end = psot ? i + psot : 0;
+        } else if (m == 0xff5d || m == 0xff53 || m == 0xff5e || m == 0xff5f) {
+            throw GkError("QCC/COC/RGN/POC markers not supported on this path yet");
+        }
+        i += 2 + L;
+    }
+    if (!have_siz || !have_cod || Hd.qcd.empty() || !Hd.tile_data) throw GkError("incomplete main header");
+    if (!Hd.tile_end || Hd.tile_end > S.len) Hd.tile_end = S.len >= 2 ? S.len - 2 : S.len;
+    if ((1u << W.p.cbw) > 64 || (1u << W.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
+}
+
+static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
+                        const uint32_t* strides, int out_on_device) {
+    hipStream_t st = ctx->st;
+    HIPCHK(hipEventRecord(ctx->ev[0], st));
+    ByteSrc S;
+    S.len = len; S.st = st;
+    if (cs_on_device) S.dev = cs; else S.host = cs;
+    Header Hd;
+    parse_header(S, Hd);
+    if (Hd.want.p.irrev) throw GkError("9/7 decode not implemented on the GPU path yet");
+    if (Hd.want.nc < 3) Hd.want.p.mct = 0;
+    ensure_plan(ctx, Hd.want);
+    Plan& P = ctx->plan;
+    apply_qcd(P, Hd.qcd);
+    const uint32_t nb = (uint32_t)P.blocks.size();
+    std::vector<GkBlock> blk = P.blocks;
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> chunks(nb);
+    std::vector<uint8_t> included(nb, 0);
+    std::vector<uint32_t> numlenbits(nb, 0);
+    for (auto& G : blk) { G.npasses = 0; G.numbps = 0; G.len = 0; }
+    // refresh band numbps from QCD (decoder semantics)
+    {
+        uint32_t b = 0;
+        for (uint32_t c = 0; c < P.nc; ++c)
+            for (uint32_t r = 0; r < P.p.numres; ++r) {
+                ResG& R = P.comps[c].res[r];
+                for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
+                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                        PrecG& PG = R.prc[bi][pi];
+                        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k, ++b) {
+                            blk[PG.first_block + k].band_numbps = (uint8_t)R.bands[bi].numbps;
+                            blk[PG.first_block + k].step = R.bands[bi].step_dec / 2.0f;
+                        }
+                    }
+            }
+    }
+    // ---- T2 (T2Decompress.cpp:216-570), LRCP
+    struct Trees { DecTree incl, imsb; };
+    std::vector<Trees> trees;
+    std::vector<size_t> tree_base;   // per (c, r, band, prc) index
+    // index trees by first_block of each precinct-band
+    std::unordered_map<uint32_t, size_t> tidx;
+    size_t pos = Hd.tile_data;
+    for (uint32_t l = 0; l < P.p.nlayers; ++l)
+        for (uint32_t r = 0; r < P.p.numres; ++r)
+            for (uint32_t c = 0; c < P.nc; ++c) {
+                ResG& R = P.comps[c].res[r];
+                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                    if (pos >= Hd.tile_end) goto t2done;
+                    BitReader br(S, pos, Hd.tile_end);
+                    std::vector<std::pair<uint32_t, uint32_t>> contrib;
+                    if (br.read(1)) {
+                        for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
+                            PrecG& PG = R.prc[bi][pi];
+                            if (!PG.cw || !PG.ch) continue;
+                            auto it = tidx.find(PG.first_block);
+                            if (it == tidx.end()) {
+                                trees.emplace_back();
+                                trees.back().incl.build(PG.cw, PG.ch);
+                                trees.back().imsb.build(PG.cw, PG.ch);
+                                it = tidx.emplace(PG.first_block, trees.size() - 1).first;
+                            }
+                            Trees& T = trees[it->second];
+                            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                                uint32_t b = PG.first_block + k;
+                                uint32_t inc;
+                                if (!included[b]) inc = T.incl.decode(br, k, l + 1) <= l ? 1 : 0;
+                                else inc = br.read(1);
+                                if (!inc) continue;
+                                if (!included[b]) {
+                                    uint32_t kmsbs = 0, v = T.imsb.decode(br, k, kmsbs);
+                                    while (v >= kmsbs) { ++kmsbs; if (kmsbs > 64) break; v = T.imsb.decode(br, k, kmsbs); }
+                                    kmsbs--;
+                                    uint32_t bnb = R.bands[bi].numbps;
+                                    blk[b].numbps = kmsbs > bnb ? 0 : bnb - kmsbs;
+                                    numlenbits[b] = 3;
+                                    included[b] = 1;
+                                }
+                                uint32_t np = br.numpasses();
+                                numlenbits[b] += br.commacode();
+                                uint32_t nbits = numlenbits[b] + floorlog2(np);
+                                if (nbits > 32) throw GkError("corrupt packet header (segment length)");
+                                uint32_t sl = br.read((int)nbits);
+                                blk[b].npasses += np;
+                                contrib.push_back({b, sl});
+                            }
+                        }
+                    }
+                    br.align();
+                    pos = br.off;
+                    for (auto& ct : contrib) {
+                        uint32_t n = (uint32_t)std::min<size_t>(ct.second, Hd.tile_end > pos ? Hd.tile_end - pos : 0);
+                        if (n) chunks[ct.first].push_back({pos, n});
+                        pos += ct.second;
+                    }
+                }
+            }
+t2done:
+    HIPCHK(hipEventRecord(ctx->ev[1], st));
+    // ---- stage compressed bytes on the device
+    const uint8_t* dcs = cs;
+    if (!cs_on_device) {
+        uint8_t* d = (uint8_t*)ctx->dout.get(len + 16);
+        HIPCHK(hipMemcpyAsync(d, cs, len, hipMemcpyHostToDevice, st));
+        dcs = d;
+    }
+    bool multi = false;
+    uint64_t tot = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        if (chunks[b].size() > 1) multi = true;
+        for (auto& ch : chunks[b]) tot += ch.second;
+    }
+    const uint8_t* src_bytes = dcs;
+    if (multi) {
+        uint8_t* stg = (uint8_t*)ctx->bytes.get(tot + 64);
+        std::vector<uint64_t> seg;
+        uint64_t o = 0;
+        for (uint32_t b = 0; b < nb; ++b) {
+            blk[b].data_off = o;
+            uint32_t L = 0;
+            for (auto& ch : chunks[b]) { seg.push_back(ch.first); seg.push_back(o); seg.push_back(ch.second); o += ch.second; L += ch.second; }
+            blk[b].len = L;
+        }
+        uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8 + 8);
+        memcpy(hs, seg.data(), seg.size() * 8);
+        uint64_t* ds = (uint64_t*)ctx->dseg.get(seg.size() * 8 + 8);
+        HIPCHK(hipMemcpyAsync(ds, hs, seg.size() * 8, hipMemcpyHostToDevice, st));
+        gk_launch_gather(st, dcs, stg, ds, (uint32_t)(seg.size() / 3));
+        src_bytes = stg;
+    } else {
+        for (uint32_t b = 0; b < nb; ++b) {
+            if (chunks[b].empty()) { blk[b].data_off = 0; blk[b].len = 0; blk[b].npasses = 0; continue; }
+            blk[b].data_off = chunks[b][0].first; blk[b].len = chunks[b][0].second;
+        }
+    }
+    GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * std::max(nb, 1u));
+    GkBlock* hblk = (GkBlock*)ctx->hinfo.get(sizeof(GkBlock) * std::max(nb, 1u));
+    memcpy(hblk, blk.data(), sizeof(GkBlock) * nb);
+    HIPCHK(hipMemcpyAsync(dblk, hblk, sizeof(GkBlock) * nb, hipMemcpyHostToDevice, st));
+    ctx->blocks_uploaded = false;   // the encode table must be re-uploaded
+    int32_t* arena = (int32_t*)ctx->arena.get(P.plane_elems * P.nc * 2 * sizeof(int32_t));
+    HIPCHK(hipEventRecord(ctx->ev[2], st));
+    gk_launch_t1_decode(st, src_bytes, dblk, arena, nb);
+    HIPCHK(hipEventRecord(ctx->ev[3], st));
+    run_dwt(ctx, false);
+    HIPCHK(hipEventRecord(ctx->ev[4], st));
+    // ---- inverse MCT + DC shift + clamp into the output planes
+    int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
+    int32_t mn = P.sgnd ? -(1 << (P.prec - 1)) : 0;
+    int32_t mx = P.sgnd ? (1 << (P.prec - 1)) - 1 : (int32_t)((1u << P.prec) - 1);
+    std::vector<int32_t*> dst(P.nc);
+    std::vector<uint32_t> dstr(P.nc);
+    int32_t* stage = nullptr;
+    if (!out_on_device) {
+        stage = (int32_t*)ctx->dplanes.get((size_t)P.w * P.h * P.nc * 4);
+        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = stage + (size_t)c * P.w * P.h; dstr[c] = P.w; }
+    } else {
+        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = comps[c]; dstr[c] = strides[c]; }
+    }
+    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems; };
+    if (P.p.mct && P.nc >= 3) {
+        gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w, P.h,
+                             shift, mn, mx);
+        for (uint32_t c = 3; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], P.w, P.h, shift, mn, mx);
+    } else {
+        for (uint32_t c = 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], P.w, P.h, shift, mn, mx);
+    }
+    HIPCHK(hipEventRecord(ctx->ev[5], st));
+    if (!out_on_device) {
+        for (uint32_t c = 0; c < P.nc; ++c)
+            HIPCHK(hipMemcpy2DAsync(comps[c], (size_t)strides[c] * 4, dst[c], (size_t)P.w * 4, (size_t)P.w * 4, P.h,
+                                    hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipEventRecord(ctx->ev[6], st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->tm.t2_ms = ev_ms(ctx, 0, 1);
+    ctx->tm.t1_ms = ev_ms(ctx, 2, 3);
+    ctx->tm.dwt_ms = ev_ms(ctx, 3, 4);
+    ctx->tm.mct_ms = ev_ms(ctx, 4, 5);
+    ctx->tm.assemble_ms = ev_ms(ctx, 1, 2);
+    ctx->tm.total_ms = ev_ms(ctx, 0, 6);
+    ctx->tm.t1_blocks = nb;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+gk_ctx* gk_create(int device_id) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device_id >= n) return nullptr;
+    if (hipSetDevice(device_id) != hipSuccess) return nullptr;
+    gk_ctx* ctx = new gk_ctx();
+    ctx->device = device_id;
+    if (hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) { delete ctx; return nullptr; }
+    for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+    return ctx;
+}
+
+void gk_destroy(gk_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->st);
+    for (auto& e : ctx->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(ctx->st);
+    delete ctx;
+}
+
+void gk_set_default_params(gk_cparameters* p) {
+    memset(p, 0, sizeof(*p));
+    p->numlayers = 1;
+    p->numresolution = 6;
+    p->cblockw_init = 64; p->cblockh_init = 64;
+    p->mct = 1;
+    p->numgbits = 2;
+    p->write_comment = 1;
+    for (int i = 0; i < GK_MAXRLVLS; ++i) { p->prcw_init[i] = 1u << 15; p->prch_init[i] = 1u << 15; }
+}
+
+int gk_encode(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+              int comps_on_device, const gk_cparameters* p, uint8_t* out, size_t cap, size_t* out_len,
+              int out_on_device) {
+    if (!ctx || !info || !comps || !strides || !out) return -1;
+    try {
+        (void)hipSetDevice(ctx->device);
+        int rc = 0;
+        size_t n = encode_impl(ctx, info, comps, strides, comps_on_device, p, out, cap, out_on_device, &rc);
+        if (out_len) *out_len = n;
+        if (rc == -2) ctx->err = "output capacity too small";
+        return rc;
+    } catch (const GkError& e) {
+        ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, gk_image_info* info) {
+    if (!ctx || !cs || !info) return -1;
+    try {
+        (void)hipSetDevice(ctx->device);
+        ByteSrc S; S.len = len; S.st = ctx->st;
+        if (cs_on_device) S.dev = cs; else S.host = cs;
+        Header Hd;
+        parse_header(S, Hd);
+        info->w = Hd.want.w; info->h = Hd.want.h; info->numcomps = Hd.want.nc; info->prec = Hd.want.prec;
+        info->sgnd = Hd.want.sgnd;
+        return 0;
+    } catch (const GkError& e) {
+        ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
+              const uint32_t* strides, int out_on_device) {
+    if (!ctx || !cs || !comps || !strides) return -1;
+    try {
+        (void)hipSetDevice(ctx->device);
+        decode_impl(ctx, cs, len, cs_on_device, comps, strides, out_on_device);
+        return 0;
+    } catch (const GkError& e) {
+        ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_get_timings(gk_ctx* ctx, gk_timings* t) {
+    if (!ctx || !t) return -1;
+    *t = ctx->tm;
+    return 0;
+}
+
+const char* gk_last_error(gk_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+const char* gk_version(void) { return "grok_amd 0.1.0 (MI355X gfx950; codestream-compatible with Grok 9.2.0)"; }
+
+}  // extern "C"

@@ -1,0 +1,24 @@
+// gk_launch.h — host-side launch wrappers for the kernels in gk_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gk_common.h"
+
+void gk_launch_dc_rct_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin,
+                          int32_t* y, int32_t* u, int32_t* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift);
+void gk_launch_dc_fwd(hipStream_t st, const int32_t* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+                      uint32_t h, int32_t shift);
+void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, const int32_t* v, uint32_t sin,
+                          int32_t* r, int32_t* g, int32_t* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift,
+                          int32_t mn, int32_t mx);
+void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+                      uint32_t h, int32_t shift, int32_t mn, int32_t mx);
+void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
+                         uint32_t w, uint32_t h);
+void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
+                         uint32_t w, uint32_t h);
+void gk_launch_t1_encode(hipStream_t st, const int32_t* coef, GkBlock* blocks, uint8_t* bytes, GkPass* passes,
+                         uint32_t* info, uint32_t nblocks, int* err);
+void gk_launch_t1_decode(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, int32_t* coef,
+                         uint32_t nblocks);
+void gk_launch_gather(hipStream_t st, const uint8_t* src, uint8_t* dst, const uint64_t* seg, uint32_t nseg);

@@ -1,0 +1,101 @@
+/*
+ * grok_amd.h — C ABI of the MI355X JPEG 2000 tile-pipeline engine.
+ *
+ * Drop-in boundary for Grok 9.2.0's hot path.  Plain C types,
+ * plain pointers and sizes; no torch/HIP types in any signature.  Every entry
+ * point cites the reference interface it replaces (paths relative to
+ * /root/reference/src/lib/jp2/).  INTEGRATION.md shows the reference-side
+ * binding (ctypes / C call sites) a maintainer would add.
+ *
+ * Conventions mirror grok.h: functions return 0 / non-NULL on success and a
+ * negative code on failure (grok.h returns bool false); messages are
+ * retrievable with gk_last_error() (grok.h routes them to grk_set_error_handler
+ * callbacks, grok.cpp:116-134).  Calls on one context are synchronous and
+ * single-threaded, like calls on one grk_codec (grok.cpp:71-86).
+ */
+#ifndef GROK_AMD_H
+#define GROK_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GK_MAXRLVLS 33
+#define GK_MAX_LAYERS 100
+
+/* Coding parameters: the subset of grk_cparameters (grok.h:466-590) the hot
+ * path consumes, with the same field names and meaning. */
+typedef struct gk_cparameters {
+    uint16_t numlayers;                  /* grk_cparameters::numlayers */
+    double layer_rate[GK_MAX_LAYERS];    /* grk_cparameters::layer_rate (compression ratio, 0 = lossless) */
+    uint8_t numresolution;               /* grk_cparameters::numresolution (default 6) */
+    uint32_t cblockw_init, cblockh_init; /* grk_cparameters::cblockw_init / cblockh_init (default 64) */
+    uint8_t cblk_sty;                    /* grk_cparameters::cblk_sty (only 0 supported this round) */
+    uint8_t irreversible;                /* grk_cparameters::irreversible */
+    uint8_t mct;                         /* grk_cparameters::mct (RCT/ICT for >= 3 components) */
+    uint8_t numgbits;                    /* grk_cparameters::numgbits (default 2) */
+    uint8_t csty;                        /* grk_cparameters::csty (bit0: user precincts) */
+    uint32_t res_spec;                   /* grk_cparameters::res_spec */
+    uint32_t prcw_init[GK_MAXRLVLS];     /* grk_cparameters::prcw_init */
+    uint32_t prch_init[GK_MAXRLVLS];     /* grk_cparameters::prch_init */
+    uint8_t write_comment;               /* write Grok's default COM marker (CodeStreamCompress.cpp:334) */
+} gk_cparameters;
+
+/* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to
+ * what the tile pipeline reads.  Component planes are int32 (grk_image_comp::data),
+ * row stride in samples (grk_image_comp::stride). */
+typedef struct gk_image_info {
+    uint32_t w, h;          /* grk_image::x1 - x0, y1 - y0 (single tile at the origin) */
+    uint32_t numcomps;      /* grk_image::numcomps */
+    uint32_t prec;          /* grk_image_comp::prec (same for every component) */
+    uint32_t sgnd;          /* grk_image_comp::sgnd */
+} gk_image_info;
+
+/* Per-stage device times of the last call (HIP events on the engine stream). */
+typedef struct gk_timings {
+    float mct_ms, dwt_ms, t1_ms, t2_ms, assemble_ms, total_ms;
+    uint32_t dwt_launches, t1_blocks;
+    uint64_t dwt_bytes;     /* algorithmic bytes moved by the DWT launches */
+} gk_timings;
+
+typedef struct gk_ctx gk_ctx;
+
+/* grk_initialize (grok.cpp:75-86): create an engine bound to one MI355X. */
+gk_ctx* gk_create(int device_id);
+/* grk_deinitialize / grk_object_unref(codec) */
+void gk_destroy(gk_ctx* ctx);
+/* grk_compress_set_default_params (grok.cpp:405-435) */
+void gk_set_default_params(gk_cparameters* p);
+
+/* grk_compress_init + grk_compress_start + grk_compress + grk_compress_end
+ * (grok.cpp:382-469; TileProcessor::doCompress TileProcessor.cpp:202-260) for a
+ * single-tile image.  comps[c] points at component c's int32 plane (device
+ * memory if comps_on_device, host otherwise).  The codestream is written to
+ * out (device memory if out_on_device); *out_len receives its size.
+ * Returns 0, or < 0 on error (-2: capacity too small, *out_len = needed). */
+int gk_encode(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+              int comps_on_device, const gk_cparameters* p, uint8_t* out, size_t cap, size_t* out_len,
+              int out_on_device);
+
+/* grk_decompress_read_header (grok.cpp:287-297, CodeStreamDecompress::readHeader) */
+int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, gk_image_info* info);
+
+/* grk_decompress (grok.cpp:287-297; TileProcessor::decompressT2T1 TileProcessor.cpp:384-408):
+ * full-tile decode into comps[c] (int32 planes, device memory if out_on_device). */
+int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
+              const uint32_t* strides, int out_on_device);
+
+/* Stage timings of the last gk_encode / gk_decode. */
+int gk_get_timings(gk_ctx* ctx, gk_timings* t);
+/* Last error message for this context (grk_set_error_handler equivalent). */
+const char* gk_last_error(gk_ctx* ctx);
+/* Engine version string (grk_version, grok.cpp). */
+const char* gk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GROK_AMD_H */
