@@ -125,7 +125,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_dwt53_fwd_level + k_dwt53_inv_level (all levels)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
-            "stages_ms": {"enc_mct": round(te.mct_ms, 3), "enc_dwt": round(te.dwt_ms, 3), "enc_t1": round(te.t1_ms, 3),
+            "stages_ms": {"enc_mct": round(te.mct_ms, 3), "enc_dwt": round(te.dwt_ms, 3), "enc_t1": round(te.t1_ms, 3), "enc_t1_cm": round(te.t1_cm_ms, 3),
                           "enc_t2_host": round(te.t2_ms, 3), "enc_assemble": round(te.assemble_ms, 3),
                           "dec_t2_host": round(td.t2_ms, 3), "dec_t1": round(td.t1_ms, 3), "dec_dwt": round(td.dwt_ms, 3),
                           "dec_mct": round(td.mct_ms, 3)},

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -78,6 +79,8 @@ struct Plan {
     std::vector<GkBlock> blocks;         // canonical order: comp, res, band, precinct, cblk
     std::vector<uint32_t> resw, resh;    // resolution sizes by level l = 0..L (l=0: full)
     uint64_t slot_bytes = 0;
+    std::vector<uint64_t> sym_off;       // T1 symbol-stream offsets (nblocks + 1)
+    std::vector<uint64_t> st_off;        // T1 decoder scratch offsets in uint64 words (nblocks + 1)
 };
 
 static void assign_steps(Plan& P) {
@@ -229,6 +232,22 @@ static void build_plan(Plan& P) {
         off += align_up(cap + 16, 64);
     }
     P.slot_bytes = off;
+    // symbol streams for the parallel context modeller: band numbps planes x 11264 symbols
+    P.sym_off.resize(P.blocks.size() + 1);
+    uint64_t so = 0;
+    for (size_t i = 0; i < P.blocks.size(); ++i) {
+        P.sym_off[i] = so;
+        so += (uint64_t)(P.blocks[i].band_numbps + 1) * 11264u;
+        so = (so + 255) & ~255ull;
+    }
+    P.sym_off[P.blocks.size()] = so;
+    P.st_off.resize(P.blocks.size() + 1);
+    uint64_t wo = 0;
+    for (size_t i = 0; i < P.blocks.size(); ++i) {
+        P.st_off[i] = wo;
+        wo += 260 + (uint64_t)(P.blocks[i].band_numbps + 1) * 64;
+    }
+    P.st_off[P.blocks.size()] = wo;
 }
 
 // ---------------------------------------------------------------------------
@@ -465,6 +484,8 @@ struct gk_ctx {
     DevBuf dout;        // codestream (encode, when the caller wants host bytes) / input (decode from host)
     DevBuf dplanes;     // component planes staged from host
     DevBuf derr;
+    DevBuf dsym, dsymoff, dpassend, dcminfo;
+    DevBuf dscratch, dstoff;
     HostBuf hinfo, hseg, hhdr;
     hipEvent_t ev[32];
     bool blocks_uploaded = false;
@@ -595,18 +616,29 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     GkPass* dps = (GkPass*)ctx->dpasses.get(sizeof(GkPass) * GK_MAX_PASSES * (size_t)std::max(nb, 1u));
     uint32_t* dinfo = (uint32_t*)ctx->dinfo.get(12 * (size_t)std::max(nb, 1u));
     int* derr = (int*)ctx->derr.get(64);
+    uint8_t* dsym = (uint8_t*)ctx->dsym.get(P.sym_off[nb] + 256);
+    uint64_t* dsymoff = (uint64_t*)ctx->dsymoff.get(8 * ((size_t)nb + 1));
+    uint32_t* dpe = (uint32_t*)ctx->dpassend.get(4 * GK_MAX_PASSES * (size_t)std::max(nb, 1u));
+    uint32_t* dcm = (uint32_t*)ctx->dcminfo.get(8 * (size_t)std::max(nb, 1u));
     if (!ctx->blocks_uploaded) {
         HIPCHK(hipMemcpyAsync(dblk, P.blocks.data(), sizeof(GkBlock) * nb, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(dsymoff, P.sym_off.data(), 8 * ((size_t)nb + 1), hipMemcpyHostToDevice, st));
         ctx->blocks_uploaded = true;
     }
     HIPCHK(hipMemsetAsync(derr, 0, 4, st));
-    gk_launch_t1_encode(st, arena, dblk, dbytes, dps, dinfo, nb, derr);
+    if (getenv("GK_T1_SERIAL")) {
+        gk_launch_t1_encode(st, arena, dblk, dbytes, dps, dinfo, nb, derr);
+    } else {
+        gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nb, derr);
+        HIPCHK(hipEventRecord(ctx->ev[8], st));
+        gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nb, derr);
+    }
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(12 * (size_t)nb + 16);
     HIPCHK(hipMemcpyAsync(hinfo, dinfo, 12 * (size_t)nb, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(hinfo + 3 * (size_t)nb, derr, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (hinfo[3 * (size_t)nb]) throw GkError("T1 code-block slot overflow");
+    if (hinfo[3 * (size_t)nb]) throw GkError(hinfo[3 * (size_t)nb] & 2 ? "T1 symbol buffer overflow" : "T1 code-block slot overflow");
 
     // ---- host T2 (T2Compress.cpp:113-240), single layer / all passes
     std::vector<uint8_t> H;
@@ -701,6 +733,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     ctx->tm.mct_ms = ev_ms(ctx, 1, 2);
     ctx->tm.dwt_ms = ev_ms(ctx, 2, 3);
     ctx->tm.t1_ms = ev_ms(ctx, 3, 4);
+    ctx->tm.t1_cm_ms = getenv("GK_T1_SERIAL") ? 0.f : ev_ms(ctx, 3, 8);
     ctx->tm.t2_ms = ev_ms(ctx, 4, 5);
     ctx->tm.assemble_ms = ev_ms(ctx, 5, 7);
     ctx->tm.total_ms = ev_ms(ctx, 0, 7);
@@ -884,35 +917,28 @@ t2done:
         HIPCHK(hipMemcpyAsync(d, cs, len, hipMemcpyHostToDevice, st));
         dcs = d;
     }
-    bool multi = false;
-    uint64_t tot = 0;
+    // gather every block's segments into a 16-byte aligned slot with >= 16 bytes of slack
+    // (the T1 decoder reads its bytes through aligned 8-byte windows)
+    std::vector<uint64_t> seg;
+    seg.reserve(3 * (size_t)nb);
+    uint64_t o = 0;
     for (uint32_t b = 0; b < nb; ++b) {
-        if (chunks[b].size() > 1) multi = true;
-        for (auto& ch : chunks[b]) tot += ch.second;
+        blk[b].data_off = o;
+        uint32_t L = 0;
+        for (auto& ch : chunks[b]) { seg.push_back(ch.first); seg.push_back(o + L); seg.push_back(ch.second); L += ch.second; }
+        blk[b].len = L;
+        if (!L) blk[b].npasses = 0;
+        o += ((uint64_t)L + 16 + 15) & ~15ull;
     }
-    const uint8_t* src_bytes = dcs;
-    if (multi) {
-        uint8_t* stg = (uint8_t*)ctx->bytes.get(tot + 64);
-        std::vector<uint64_t> seg;
-        uint64_t o = 0;
-        for (uint32_t b = 0; b < nb; ++b) {
-            blk[b].data_off = o;
-            uint32_t L = 0;
-            for (auto& ch : chunks[b]) { seg.push_back(ch.first); seg.push_back(o); seg.push_back(ch.second); o += ch.second; L += ch.second; }
-            blk[b].len = L;
-        }
+    uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 64);
+    if (!seg.empty()) {
         uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8 + 8);
         memcpy(hs, seg.data(), seg.size() * 8);
         uint64_t* ds = (uint64_t*)ctx->dseg.get(seg.size() * 8 + 8);
         HIPCHK(hipMemcpyAsync(ds, hs, seg.size() * 8, hipMemcpyHostToDevice, st));
         gk_launch_gather(st, dcs, stg, ds, (uint32_t)(seg.size() / 3));
-        src_bytes = stg;
-    } else {
-        for (uint32_t b = 0; b < nb; ++b) {
-            if (chunks[b].empty()) { blk[b].data_off = 0; blk[b].len = 0; blk[b].npasses = 0; continue; }
-            blk[b].data_off = chunks[b][0].first; blk[b].len = chunks[b][0].second;
-        }
     }
+    const uint8_t* src_bytes = stg;
     GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * std::max(nb, 1u));
     GkBlock* hblk = (GkBlock*)ctx->hinfo.get(sizeof(GkBlock) * std::max(nb, 1u));
     memcpy(hblk, blk.data(), sizeof(GkBlock) * nb);
@@ -920,7 +946,15 @@ t2done:
     ctx->blocks_uploaded = false;   // the encode table must be re-uploaded
     int32_t* arena = (int32_t*)ctx->arena.get(P.plane_elems * P.nc * 2 * sizeof(int32_t));
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    gk_launch_t1_decode(st, src_bytes, dblk, arena, nb);
+    if (getenv("GK_T1_SERIAL")) {
+        gk_launch_t1_decode(st, src_bytes, dblk, arena, nb);
+    } else {
+        uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * P.st_off[nb] + 64);
+        uint64_t* dsto = (uint64_t*)ctx->dstoff.get(8 * ((size_t)nb + 1));
+        HIPCHK(hipMemcpyAsync(dsto, P.st_off.data(), 8 * ((size_t)nb + 1), hipMemcpyHostToDevice, st));
+        gk_launch_t1_dec(st, src_bytes, dblk, dscr, dsto, nb);
+        gk_launch_t1_recon(st, dblk, dscr, dsto, arena, nb);
+    }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     run_dwt(ctx, false);
     HIPCHK(hipEventRecord(ctx->ev[4], st));

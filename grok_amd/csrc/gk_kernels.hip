@@ -244,64 +244,7 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
     }
 }
 
-// =============================================================================
-// EBCOT context tables (ISO 15444-1 Annex D, Tables D.1-D.3), built in LDS at
-// kernel start from the rules (no reference tables are copied).
-//   zc index: 9-bit neighbourhood  bit0 NW bit1 N bit2 NE bit3 W bit4 (self) bit5 E bit6 SW bit7 S bit8 SE
-//   sc index: 8-bit               bit0 W-neg bit1 W-sig bit2 E-neg bit3 E-sig bit4 N-neg bit5 N-sig bit6 S-neg bit7 S-sig
-// =============================================================================
-enum { CTX_ZC = 0, CTX_SC = 9, CTX_MAG = 14, CTX_AGG = 17, CTX_UNI = 18 };
-
-__device__ __forceinline__ uint8_t zc_rule(uint32_t orient, uint32_t f) {
-    int h = ((f >> 3) & 1) + ((f >> 5) & 1);
-    int v = ((f >> 1) & 1) + ((f >> 7) & 1);
-    int d = (f & 1) + ((f >> 2) & 1) + ((f >> 6) & 1) + ((f >> 8) & 1);
-    if (orient == 1) { int t = h; h = v; v = t; }
-    if (orient == 3) {
-        int hv = h + v;
-        if (d == 0) return hv == 0 ? 0 : (hv == 1 ? 1 : 2);
-        if (d == 1) return hv == 0 ? 3 : (hv == 1 ? 4 : 5);
-        if (d == 2) return hv == 0 ? 6 : 7;
-        return 8;
-    }
-    if (h == 0) {
-        if (v == 0) return d == 0 ? 0 : (d == 1 ? 1 : 2);
-        return v == 1 ? 3 : 4;
-    }
-    if (h == 1) return v == 0 ? (d == 0 ? 5 : 6) : 7;
-    return 8;
-}
-// returns (ctx offset in 0..4) | (xorbit << 4)
-__device__ __forceinline__ uint8_t sc_rule(uint32_t f) {
-    auto c = [&](int sigbit, int negbit) { return ((f >> sigbit) & 1) ? (((f >> negbit) & 1) ? -1 : 1) : 0; };
-    int H = c(1, 0) + c(3, 2), V = c(5, 4) + c(7, 6);
-    H = H < -1 ? -1 : (H > 1 ? 1 : H);
-    V = V < -1 ? -1 : (V > 1 ? 1 : V);
-    if (H == 0 && V == 0) return 0;
-    int xb = (H < 0 || (H == 0 && V < 0)) ? 1 : 0;
-    if (H < 0) { H = -H; V = -V; }
-    int ctx = (H == 0) ? 1 : (V == -1 ? 2 : (V == 0 ? 3 : 4));
-    return (uint8_t)(ctx | (xb << 4));
-}
-
-// MQ probability estimation table (Annex C, Table C.2): qe | nmps<<16 | nlps<<22 | switch<<28
-__constant__ uint32_t c_mq[47] = {
-    0x5601 | (1u << 16) | (1u << 22) | (1u << 28), 0x3401 | (2u << 16) | (6u << 22), 0x1801 | (3u << 16) | (9u << 22),
-    0x0AC1 | (4u << 16) | (12u << 22), 0x0521 | (5u << 16) | (29u << 22), 0x0221 | (38u << 16) | (33u << 22),
-    0x5601 | (7u << 16) | (6u << 22) | (1u << 28), 0x5401 | (8u << 16) | (14u << 22), 0x4801 | (9u << 16) | (14u << 22),
-    0x3801 | (10u << 16) | (14u << 22), 0x3001 | (11u << 16) | (17u << 22), 0x2401 | (12u << 16) | (18u << 22),
-    0x1C01 | (13u << 16) | (20u << 22), 0x1601 | (29u << 16) | (21u << 22), 0x5601 | (15u << 16) | (14u << 22) | (1u << 28),
-    0x5401 | (16u << 16) | (14u << 22), 0x5101 | (17u << 16) | (15u << 22), 0x4801 | (18u << 16) | (16u << 22),
-    0x3801 | (19u << 16) | (17u << 22), 0x3401 | (20u << 16) | (18u << 22), 0x3001 | (21u << 16) | (19u << 22),
-    0x2801 | (22u << 16) | (19u << 22), 0x2401 | (23u << 16) | (20u << 22), 0x2201 | (24u << 16) | (21u << 22),
-    0x1C01 | (25u << 16) | (22u << 22), 0x1801 | (26u << 16) | (23u << 22), 0x1601 | (27u << 16) | (24u << 22),
-    0x1401 | (28u << 16) | (25u << 22), 0x1201 | (29u << 16) | (26u << 22), 0x1101 | (30u << 16) | (27u << 22),
-    0x0AC1 | (31u << 16) | (28u << 22), 0x09C1 | (32u << 16) | (29u << 22), 0x08A1 | (33u << 16) | (30u << 22),
-    0x0521 | (34u << 16) | (31u << 22), 0x0441 | (35u << 16) | (32u << 22), 0x02A1 | (36u << 16) | (33u << 22),
-    0x0221 | (37u << 16) | (34u << 22), 0x0141 | (38u << 16) | (35u << 22), 0x0111 | (39u << 16) | (36u << 22),
-    0x0085 | (40u << 16) | (37u << 22), 0x0049 | (41u << 16) | (38u << 22), 0x0025 | (42u << 16) | (39u << 22),
-    0x0015 | (43u << 16) | (40u << 22), 0x0009 | (44u << 16) | (41u << 22), 0x0005 | (45u << 16) | (42u << 22),
-    0x0001 | (45u << 16) | (43u << 22), 0x5601 | (46u << 16) | (46u << 22)};
+#include "gk_t1_common.h"
 
 // Shared per-wave T1 state.  Row bitmaps: bit x = column x; rows are stored
 // with one guard row above and below (index y + 1).

@@ -22,3 +22,12 @@ void gk_launch_t1_encode(hipStream_t st, const int32_t* coef, GkBlock* blocks, u
 void gk_launch_t1_decode(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, int32_t* coef,
                          uint32_t nblocks);
 void gk_launch_gather(hipStream_t st, const uint8_t* src, uint8_t* dst, const uint64_t* seg, uint32_t nseg);
+void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks, const uint64_t* sym_off, uint8_t* sym,
+                     uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err);
+void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
+                     const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
+                     uint32_t nblocks, int* err);
+void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, uint64_t* scratch,
+                      const uint64_t* st_off, uint32_t nblocks);
+void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint64_t* scratch, const uint64_t* st_off,
+                        int32_t* coef, uint32_t nblocks);

@@ -1,0 +1,417 @@
+// gk_t1enc.hip — parallel Part-1 T1 encoder for CDNA4 (two kernels).
+//
+//  k_t1_cm  (one wave per code-block, lane = column): EBCOT context modelling.
+//           All three coding passes (T1.cpp:498-780) are evaluated for a whole
+//           4-row stripe at once with 64-bit column masks.  The only causal
+//           chain — significance propagation spreading left->right inside a
+//           stripe — is solved by a wave-wide fixpoint (monotone, converges to
+//           the sequential result); everything else is data-parallel because
+//           the encoder knows every magnitude bit up front.  Each stripe-pass
+//           emits its (context, decision) symbols in scan order through a wave
+//           prefix sum into a per-block symbol stream.
+//  k_t1_mq  (one lane per code-block): the MQ arithmetic coder (Annex C;
+//           mqc_enc.cpp:86-330) over that symbol stream, plus Grok's pass
+//           bookkeeping (rates, termination, monotone fix, FF back-off;
+//           T1.cpp:856-930).
+//
+// Symbol byte = (ctx << 1) | decision, ctx in 0..18 (T1_CTXNO_*).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gk_common.h"
+#include "gk_t1_common.h"
+
+#define SYM_PER_PLANE 11264u   // >= 2 symbols per sample + 3 per stripe column, per bit-plane
+
+__device__ __forceinline__ uint32_t win6(uint64_t col, uint32_t s) {
+    return (uint32_t)((s ? (col >> (4 * s - 1)) : (col << 1)) & 63u);
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
+    const int lane = threadIdx.x & 63;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
+    }
+    total = __shfl(inc, 63);
+    return inc - v;
+}
+
+// 9-bit neighbourhood pattern (bit0 NW bit1 N bit2 NE bit3 W bit5 E bit6 SW bit7 S bit8 SE) for
+// stripe row r given the left column (L), centre-above (CA), centre-below (CB), right column (R)
+// 6-bit windows (bit0 = row above the stripe, bit5 = row below).
+__device__ __forceinline__ uint32_t pat9(uint32_t L, uint32_t CA, uint32_t CB, uint32_t R, int r) {
+    return ((L >> r) & 1) | (((CA >> r) & 1) << 1) | (((R >> r) & 1) << 2) | (((L >> (r + 1)) & 1) << 3) |
+           (((R >> (r + 1)) & 1) << 5) | (((L >> (r + 2)) & 1) << 6) | (((CB >> (r + 2)) & 1) << 7) |
+           (((R >> (r + 2)) & 1) << 8);
+}
+// sign-context index (bit0 W-neg bit1 W-sig bit2 E-neg bit3 E-sig bit4 N-neg bit5 N-sig bit6 S-neg bit7 S-sig)
+__device__ __forceinline__ uint32_t scidx(uint32_t L, uint32_t NL, uint32_t CA, uint32_t CB, uint32_t NC, uint32_t R,
+                                          uint32_t NR, int r) {
+    uint32_t wv = (L >> (r + 1)) & 1, wn = (NL >> (r + 1)) & 1;
+    uint32_t ev = (R >> (r + 1)) & 1, en = (NR >> (r + 1)) & 1;
+    uint32_t nv = (CA >> r) & 1, nn = (NC >> r) & 1;
+    uint32_t sv = (CB >> (r + 2)) & 1, sn = (NC >> (r + 2)) & 1;
+    return wn | (wv << 1) | (en << 2) | (ev << 3) | (nn << 4) | (nv << 5) | (sn << 6) | (sv << 7);
+}
+
+struct CmLds {
+    uint8_t zc[512];
+    uint8_t sc[256];
+};
+
+__global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, const GkBlock* __restrict__ blocks,
+                                              const uint64_t* __restrict__ sym_off, uint8_t* __restrict__ sym,
+                                              uint32_t* __restrict__ pass_end, uint32_t* __restrict__ cm_info,
+                                              uint32_t nblocks, int* err) {
+    __shared__ CmLds L;
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks) return;
+    const int lane = threadIdx.x;
+    const GkBlock B = blocks[b];
+    const uint32_t w = B.w, h = B.h;
+    for (int i = lane; i < 512; i += 64) L.zc[i] = zc_rule(B.orient, (uint32_t)i);
+    for (int i = lane; i < 256; i += 64) L.sc[i] = sc_rule((uint32_t)i);
+    // ---- quantise + sign-magnitude (T1Part1.cpp:36-87), column `lane` into registers
+    const bool irrev = B.flags & 1;
+    uint32_t m[64];
+    uint64_t negcol = 0;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int y = 0; y < 64; ++y) {
+        int32_t v = 0;
+        if (y < (int)h && lane < (int)w) {
+            int32_t raw = coef[B.band_off + (size_t)y * B.stride + lane];
+            if (irrev) v = (int32_t)rintf((__int_as_float(raw) / B.step) * 64.0f);
+            else v = raw * 64;
+        }
+        uint32_t a = (uint32_t)(v < 0 ? -v : v);
+        m[y] = a;
+        mx = a > mx ? a : mx;
+        negcol |= (uint64_t)(v < 0) << y;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(mx, o); mx = t > mx ? t : mx; }
+    uint32_t numbps = 0;
+    if (mx) { uint32_t t = 32 - __clz(mx); numbps = t <= 6 ? 0 : t - 6; }
+    __syncthreads();
+    if (numbps == 0) {
+        if (lane == 0) { cm_info[2 * b] = 0; cm_info[2 * b + 1] = 0; }
+        return;
+    }
+    const uint64_t base_off = sym_off[b];
+    const uint64_t cap = sym_off[b + 1] - base_off;
+    if ((uint64_t)numbps * SYM_PER_PLANE > cap) {
+        if (lane == 0) { atomicOr(err, 2); cm_info[2 * b] = 0; cm_info[2 * b + 1] = 0; }
+        return;
+    }
+    uint8_t* S = sym + base_off;
+    uint32_t* PE = pass_end + (size_t)b * GK_MAX_PASSES;
+    const uint64_t validcol = (lane < (int)w) ? ((h >= 64) ? ~0ull : ((1ull << h) - 1)) : 0ull;
+    const uint32_t nstripes = (h + 3) >> 2;
+    uint64_t sig = 0, mu = 0;
+    uint32_t pos = 0, passno = 0;
+
+    for (int bpno = (int)numbps - 1; bpno >= 0; --bpno) {
+        uint64_t bitcol = 0;
+#pragma unroll
+        for (int y = 0; y < 64; ++y) bitcol |= (uint64_t)((m[y] >> (bpno + 6)) & 1u) << y;
+        uint64_t vis = 0;
+        const uint64_t sigPrev = sig;
+        if (bpno != (int)numbps - 1) {
+            // ================= significance propagation pass =================
+            for (uint32_t s = 0; s < nstripes; ++s) {
+                const uint32_t sh = 4 * s;
+                const uint32_t Wc = win6(sig, s), Nc = win6(negcol, s);
+                uint32_t pk = Wc | (Nc << 6);
+                uint32_t pL = __shfl_up(pk, 1), pR = __shfl_down(pk, 1);
+                if (lane == 0) pL = 0;
+                if (lane == 63) pR = 0;
+                const uint32_t WL = pL & 63, NL = (pL >> 6) & 63, WR = pR & 63, NR = (pR >> 6) & 63;
+                const uint32_t valid4 = (uint32_t)(validcol >> sh) & 15u;
+                const uint32_t cand = ~(Wc >> 1) & valid4;
+                const uint32_t bit4 = (uint32_t)(bitcol >> sh) & 15u;
+                const uint32_t A = ((WL | (WL >> 1) | (WL >> 2)) | (WR | (WR >> 1) | (WR >> 2)) | Wc | (Wc >> 2)) & 15u;
+                auto F = [&](uint32_t in, uint32_t& cd) -> uint32_t {
+                    uint32_t x = A | ((in | (in << 1) | (in >> 1)) & 15u);
+                    uint32_t c0 = cand & x & 1u, n0 = c0 & bit4;
+                    uint32_t c1 = cand & (x | (n0 << 1)) & 2u, n1 = c1 & bit4;
+                    uint32_t c2 = cand & (x | (n1 << 1)) & 4u, n2 = c2 & bit4;
+                    uint32_t c3 = cand & (x | (n2 << 1)) & 8u, n3 = c3 & bit4;
+                    cd = c0 | c1 | c2 | c3;
+                    return n0 | n1 | n2 | n3;
+                };
+                uint32_t cd, in = 0;
+                uint32_t ns = F(0, cd);
+                while (true) {
+                    uint32_t t = __shfl_up(ns, 1);
+                    in = (lane == 0) ? 0u : t;
+                    uint32_t cd2, ns2 = F(in, cd2);
+                    bool ch = ns2 != ns;
+                    ns = ns2; cd = cd2;
+                    if (!__any(ch)) break;
+                }
+                // symbols
+                const uint32_t Lt = WL | (in << 1), CA = Wc | (ns << 1), CB = Wc;
+                uint32_t cnt = __popc(cd) + __popc(ns);
+                uint32_t total, off = wave_excl_scan(cnt, total);
+                uint8_t* o = S + pos + off;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if ((cd >> r) & 1) {
+                        uint32_t d = (bit4 >> r) & 1;
+                        *o++ = (uint8_t)(((CTX_ZC + L.zc[pat9(Lt, CA, CB, WR, r)]) << 1) | d);
+                        if (d) {
+                            uint32_t e = L.sc[scidx(Lt, NL, CA, CB, Nc, WR, NR, r)];
+                            uint32_t sg = (Nc >> (r + 1)) & 1;
+                            *o++ = (uint8_t)(((CTX_SC + (e & 15)) << 1) | (sg ^ (e >> 4)));
+                        }
+                    }
+                }
+                pos += total;
+                sig |= (uint64_t)ns << sh;
+                vis |= (uint64_t)cd << sh;
+            }
+            if (lane == 0) PE[passno] = pos;
+            ++passno;
+            // ================= magnitude refinement pass =================
+            for (uint32_t s = 0; s < nstripes; ++s) {
+                const uint32_t sh = 4 * s;
+                const uint32_t Wc = win6(sig, s);
+                uint32_t pL = __shfl_up(Wc, 1), pR = __shfl_down(Wc, 1);
+                if (lane == 0) pL = 0;
+                if (lane == 63) pR = 0;
+                const uint32_t nb = ((pL | (pL >> 1) | (pL >> 2)) | (pR | (pR >> 1) | (pR >> 2)) | Wc | (Wc >> 2)) & 15u;
+                const uint32_t mr = (uint32_t)(sigPrev >> sh) & 15u;
+                const uint32_t mu4 = (uint32_t)(mu >> sh) & 15u;
+                const uint32_t bit4 = (uint32_t)(bitcol >> sh) & 15u;
+                uint32_t total, off = wave_excl_scan(__popc(mr), total);
+                uint8_t* o = S + pos + off;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if ((mr >> r) & 1) {
+                        uint32_t cx = ((mu4 >> r) & 1) ? CTX_MAG + 2 : (((nb >> r) & 1) ? CTX_MAG + 1 : CTX_MAG);
+                        *o++ = (uint8_t)((cx << 1) | ((bit4 >> r) & 1));
+                    }
+                }
+                pos += total;
+            }
+            mu |= sigPrev;
+            if (lane == 0) PE[passno] = pos;
+            ++passno;
+        }
+        // ================= cleanup pass =================
+        for (uint32_t s = 0; s < nstripes; ++s) {
+            const uint32_t sh = 4 * s;
+            const uint32_t Wc = win6(sig, s), Nc = win6(negcol, s);
+            const uint32_t valid4 = (uint32_t)(validcol >> sh) & 15u;
+            const uint32_t vis4 = (uint32_t)(vis >> sh) & 15u;
+            const uint32_t bit4 = (uint32_t)(bitcol >> sh) & 15u;
+            const uint32_t cl = ~(Wc >> 1) & ~vis4 & valid4;
+            const uint32_t nc = cl & bit4;
+            uint32_t pk = Wc | (Nc << 6) | (nc << 12);
+            uint32_t pL = __shfl_up(pk, 1), pR = __shfl_down(pk, 1);
+            if (lane == 0) pL = 0;
+            if (lane == 63) pR = 0;
+            const uint32_t WL = pL & 63, NL = (pL >> 6) & 63, ncL = (pL >> 12) & 15;
+            const uint32_t WR = pR & 63, NR = (pR >> 6) & 63;
+            const uint32_t Lt = WL | (ncL << 1), CA = Wc | (nc << 1), CB = Wc;
+            const bool agg = (valid4 == 15u) && (cl == 15u) && ((Lt | WR | (Wc & 0x21u)) == 0);
+            uint32_t rl = nc ? (uint32_t)__ffs(nc) - 1 : 4u;
+            uint32_t cnt;
+            uint32_t codemask;   // rows coded with ZC
+            if (agg) {
+                if (rl == 4) { cnt = 1; codemask = 0; }
+                else {
+                    codemask = cl & ~((2u << rl) - 1);   // rows after the run
+                    cnt = 3 + 1 + __popc(codemask) + __popc(nc & codemask);
+                }
+            } else {
+                codemask = cl;
+                cnt = __popc(cl) + __popc(nc);
+            }
+            uint32_t total, off = wave_excl_scan(cnt, total);
+            uint8_t* o = S + pos + off;
+            if (agg) {
+                *o++ = (uint8_t)((CTX_AGG << 1) | (rl != 4 ? 1 : 0));
+                if (rl != 4) {
+                    *o++ = (uint8_t)((CTX_UNI << 1) | (rl >> 1));
+                    *o++ = (uint8_t)((CTX_UNI << 1) | (rl & 1));
+                    uint32_t e = L.sc[scidx(Lt, NL, CA, CB, Nc, WR, NR, (int)rl)];
+                    uint32_t sg = (Nc >> (rl + 1)) & 1;
+                    *o++ = (uint8_t)(((CTX_SC + (e & 15)) << 1) | (sg ^ (e >> 4)));
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if ((codemask >> r) & 1) {
+                    uint32_t d = (bit4 >> r) & 1;
+                    *o++ = (uint8_t)(((CTX_ZC + L.zc[pat9(Lt, CA, CB, WR, r)]) << 1) | d);
+                    if (d) {
+                        uint32_t e = L.sc[scidx(Lt, NL, CA, CB, Nc, WR, NR, r)];
+                        uint32_t sg = (Nc >> (r + 1)) & 1;
+                        *o++ = (uint8_t)(((CTX_SC + (e & 15)) << 1) | (sg ^ (e >> 4)));
+                    }
+                }
+            }
+            pos += total;
+            sig |= (uint64_t)nc << sh;
+        }
+        if (lane == 0) PE[passno] = pos;
+        ++passno;
+    }
+    if (lane == 0) { cm_info[2 * b] = numbps; cm_info[2 * b + 1] = passno; }
+}
+
+// ---------------------------------------------------------------------------
+// MQ coder, one lane per code-block.  Context states live in registers
+// (5 x 32-bit words, one byte per context: state | mps << 6).
+// ---------------------------------------------------------------------------
+struct MqLane {
+    uint32_t a, c, ct;
+    int32_t bp;
+    uint32_t cur;
+    uint32_t wbuf;
+    uint8_t* out;
+    uint32_t cap;
+    uint32_t ovf;
+};
+
+__device__ __forceinline__ void mql_emit(MqLane& q, uint32_t nb) {
+    if (q.bp >= 0) {
+        if ((uint32_t)q.bp < q.cap) {
+            q.wbuf |= q.cur << (8 * (q.bp & 3));
+            if ((q.bp & 3) == 3) { *(uint32_t*)(q.out + (q.bp - 3)) = q.wbuf; q.wbuf = 0; }
+        } else q.ovf = 1;
+    }
+    q.bp++;
+    q.cur = nb & 0xff;
+}
+__device__ __forceinline__ void mql_byteout(MqLane& q) {
+    if (q.cur == 0xff) { mql_emit(q, q.c >> 20); q.c &= 0xfffff; q.ct = 7; }
+    else if ((q.c & 0x8000000) == 0) { mql_emit(q, q.c >> 19); q.c &= 0x7ffff; q.ct = 8; }
+    else {
+        q.cur++;
+        if (q.cur == 0xff) { q.c &= 0x7ffffff; mql_emit(q, q.c >> 20); q.c &= 0xfffff; q.ct = 7; }
+        else { mql_emit(q, q.c >> 19); q.c &= 0x7ffff; q.ct = 8; }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, const uint64_t* __restrict__ sym_off,
+                                              const uint32_t* __restrict__ pass_end, const uint32_t* __restrict__ cm_info,
+                                              const GkBlock* __restrict__ blocks, uint8_t* __restrict__ bytes,
+                                              GkPass* __restrict__ passes, uint32_t* __restrict__ info,
+                                              uint32_t nblocks, int* err) {
+    __shared__ uint32_t tab[47];
+    const int lane = threadIdx.x;
+    if (lane < 47) tab[lane] = c_mq[lane];
+    __syncthreads();
+    const uint32_t b = blockIdx.x * 64 + lane;
+    if (b >= nblocks) return;
+    const uint32_t numbps = cm_info[2 * b], npasses = cm_info[2 * b + 1];
+    if (npasses == 0) { info[3 * b] = 0; info[3 * b + 1] = 0; info[3 * b + 2] = 0; return; }
+    const GkBlock B = blocks[b];
+    const uint8_t* sp = sym + sym_off[b];
+    const uint32_t* PE = pass_end + (size_t)b * GK_MAX_PASSES;
+    GkPass* P = passes + (size_t)b * GK_MAX_PASSES;
+    MqLane q;
+    q.a = 0x8000; q.c = 0; q.ct = 12; q.bp = -1; q.cur = 0; q.wbuf = 0; q.out = bytes + B.data_off; q.cap = B.data_cap;
+    q.ovf = 0;
+    // initial context states (mqc_resetstates): ZC ctx0 -> 4, AGG -> 3, UNI -> 46
+    uint32_t cw[5] = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};   // ctx 17 = byte 1 of word 4, ctx 18 = byte 2
+    uint32_t i = 0;
+    // 16-byte symbol chunks, double-buffered so the next load is in flight while
+    // the current 16 symbols are coded (sym_off is 256-byte aligned).
+    uint4 cur4 = *(const uint4*)(sp), nxt4 = *(const uint4*)(sp + 16);
+    for (uint32_t p = 0; p < npasses; ++p) {
+        const uint32_t end = PE[p];
+        for (; i < end; ++i) {
+            const uint32_t j = i & 15;
+            const uint32_t wsel = j >> 2;
+            const uint32_t wv = wsel == 0 ? cur4.x : wsel == 1 ? cur4.y : wsel == 2 ? cur4.z : cur4.w;
+            const uint32_t s = (wv >> (8 * (j & 3))) & 0xff;
+            if (j == 15) { cur4 = nxt4; nxt4 = *(const uint4*)(sp + i + 17); }
+            const uint32_t cx = s >> 1, d = s & 1;
+            const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
+            uint32_t word = wi == 0 ? cw[0] : wi == 1 ? cw[1] : wi == 2 ? cw[2] : wi == 3 ? cw[3] : cw[4];
+            const uint32_t st = (word >> shb) & 0xff;
+            const uint32_t idx = st & 63, mps = st >> 6;
+            const uint32_t e = tab[idx];
+            const uint32_t qe = e & 0xffff;
+            uint32_t nst = st;
+            bool renorm = true;
+            q.a -= qe;
+            if (mps == d) {
+                if (q.a & 0x8000) { q.c += qe; renorm = false; }
+                else {
+                    if (q.a < qe) q.a = qe; else q.c += qe;
+                    nst = ((e >> 16) & 0x3f) | (mps << 6);
+                }
+            } else {
+                if (q.a < qe) q.c += qe; else q.a = qe;
+                nst = ((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6);
+            }
+            if (renorm) {
+                word = (word & ~(0xffu << shb)) | (nst << shb);
+                if (wi == 0) cw[0] = word; else if (wi == 1) cw[1] = word; else if (wi == 2) cw[2] = word;
+                else if (wi == 3) cw[3] = word; else cw[4] = word;
+                uint32_t n = __clz(q.a) - 16;
+                q.a <<= n;
+                while (n >= q.ct) { q.c <<= q.ct; n -= q.ct; mql_byteout(q); }
+                q.c <<= n; q.ct -= n;
+            }
+        }
+        // pass bookkeeping (T1.cpp:856-897); only the last pass is terminated (default style)
+        if (p == npasses - 1) {
+            uint32_t tempc = q.c + q.a;
+            q.c |= 0xffff;
+            if (q.c >= tempc) q.c -= 0x8000;
+            q.c <<= q.ct; mql_byteout(q);
+            q.c <<= q.ct; mql_byteout(q);
+            if (q.cur != 0xff) mql_emit(q, 0);
+            P[p].term = 1; P[p].rate = (uint32_t)q.bp;
+        } else {
+            P[p].term = 0; P[p].rate = (uint32_t)q.bp + 5 + (q.ct < 5 ? 1 : 0);
+        }
+        P[p].dist = 0.f;
+    }
+    // flush the partial output word (bytes [bp & ~3, bp) plus the pending byte)
+    if (q.bp >= 0 && (uint32_t)q.bp < q.cap) {
+        q.wbuf |= q.cur << (8 * (q.bp & 3));
+        *(uint32_t*)(q.out + (q.bp & ~3)) = q.wbuf;
+    }
+    __threadfence();
+    const uint32_t nbytes = (uint32_t)q.bp;
+    uint32_t last = nbytes;
+    for (int k = (int)npasses; k > 0;) {   // monotone rates (T1.cpp:907-919)
+        GkPass& ps = P[--k];
+        if (ps.rate > last) ps.rate = last; else last = ps.rate;
+    }
+    uint32_t prev = 0;
+    for (uint32_t k = 0; k < npasses; ++k) {   // FF back-off (T1.cpp:920-930)
+        GkPass& ps = P[k];
+        if (ps.rate > 0 && ps.rate <= q.cap && q.out[ps.rate - 1] == 0xff) ps.rate--;
+        ps.len = ps.rate - prev;
+        prev = ps.rate;
+    }
+    info[3 * b] = numbps;
+    info[3 * b + 1] = npasses;
+    info[3 * b + 2] = P[npasses - 1].rate;
+    if (q.ovf) atomicOr(err, 1);
+}
+
+#include "gk_launch.h"
+void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks, const uint64_t* sym_off, uint8_t* sym,
+                     uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(k_t1_cm, dim3(nblocks), dim3(64), 0, st, coef, blocks, sym_off, sym, pass_end, cm_info, nblocks,
+                       err);
+}
+void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
+                     const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
+                     uint32_t nblocks, int* err) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(k_t1_mq, dim3((nblocks + 63) / 64), dim3(64), 0, st, sym, sym_off, pass_end, cm_info, blocks,
+                       bytes, passes, info, nblocks, err);
+}

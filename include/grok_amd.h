@@ -57,6 +57,7 @@ typedef struct gk_image_info {
 /* Per-stage device times of the last call (HIP events on the engine stream). */
 typedef struct gk_timings {
     float mct_ms, dwt_ms, t1_ms, t2_ms, assemble_ms, total_ms;
+    float t1_cm_ms;         /* encode: context-modelling part of t1_ms */
     uint32_t dwt_launches, t1_blocks;
     uint64_t dwt_bytes;     /* algorithmic bytes moved by the DWT launches */
 } gk_timings;
