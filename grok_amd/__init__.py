@@ -9,6 +9,7 @@ loaded, or no GPU is present, calls raise.
 """
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -115,6 +116,15 @@ class Engine:
     """One MI355X, one HIP stream (grk_codec analogue)."""
 
     def __init__(self, device=0):
+        # PyTorch-ROCm bundles its own HIP/HSA runtime.  When both live in one
+        # process, torch's must initialise first or it later reports "No HIP
+        # GPUs"; device tensors are only exchanged with torch, so initialise it
+        # here when it is present.  The C ABI itself does not depend on torch.
+        if "torch" in sys.modules:
+            try:
+                sys.modules["torch"].cuda.init()
+            except Exception:
+                pass
         self.lib = load_library()
         self.ctx = self.lib.gk_create(device)
         if not self.ctx:
