@@ -95,7 +95,7 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
     p.cblockw_init, p.cblockh_init = cblk
     p.irreversible = int(irreversible)
     p.mct = int(mct)
-    p.numlayers = numlayers
+    p.numlayers = len(layer_rate) if layer_rate else numlayers
     if layer_rate:
         for i, r in enumerate(layer_rate):
             p.layer_rate[i] = r

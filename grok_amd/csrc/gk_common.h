@@ -21,8 +21,9 @@ struct GkBlock {
     uint8_t orient;        // 0 LL, 1 HL, 2 LH, 3 HH
     uint8_t comp;
     uint8_t band_numbps;   // Quantizer.cpp:45-49 (decode: numbps - k_msbs)
-    uint8_t flags;         // bit0: irreversible
+    uint8_t flags;         // bit0: irreversible, bit1: rate control (collect per-pass distortion)
     float step;            // 9/7 encode: band stepsize (divisor, T1Part1.cpp:70-76); decode: stepsize/2 (ScaleFilter)
+    double wmse;           // encode + rate control: w1 * w2 * stepsize of T1::getwmsedec (T1.cpp:418-436)
     // encode outputs / decode inputs
     uint64_t data_off;     // byte offset of the block's compressed data (slot) in the byte arena
     uint32_t data_cap;     // slot capacity (encode)
@@ -32,12 +33,12 @@ struct GkBlock {
 };
 
 // Pass information written by the encoder (max 3*31-2 passes per block).
+// Default code-block style: only the last pass is terminated (T1.cpp:437-458).
 #define GK_MAX_PASSES 96
 struct GkPass {
-    uint32_t rate;
-    uint32_t len;
-    float dist;            // cumulative weighted distortion decrease (rate control)
-    uint32_t term;
+    uint32_t rate;         // cumulative bytes after the pass (T1.cpp:856-930 rules)
+    uint32_t len;          // rate - previous rate
+    double dist;           // cumulative distortion decrease, Grok's distortiondec (rate control only)
 };
 
 // 2D window for DWT/MCT kernels.

@@ -1,0 +1,275 @@
+// gk_dwt97.hip — irreversible path kernels for gfx950: ICT, 9/7 DWT (fwd/inv),
+// and the irreversible DC/clamp stages.
+//
+// Bit-exactness: every lifting step is x_i = x_i + (x_{i-1} + x_{i+1}) * c with
+// no FMA contraction, the order Grok evaluates it in (dwt97::encode_step2 and
+// grk_v8dwt_encode_step2, WaveletFwd.cpp:135-163, 370-398; decompress_step2_97,
+// WaveletReverse.cpp:964-1022), so the GPU transform reproduces Grok's float
+// results bit for bit.  Boundaries use whole-sample symmetric extension of the
+// input (identical values to Grok's "2 * neighbour" edge rule).
+//
+// Tiling: one launch per decomposition level; a 256-thread workgroup owns a
+// 128 x 32 output tile, loads it with a 4-sample halo on every side into LDS,
+// runs the vertical then the horizontal lifting (forward) or horizontal then
+// vertical (inverse) in LDS, and scatters to the four Mallat quadrants.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gk_common.h"
+
+#pragma clang fp contract(off)
+
+#define T97_W 128
+#define T97_H 32
+#define T97_HALO 4
+#define T97_LW (T97_W + 2 * T97_HALO)
+#define T97_LH (T97_H + 2 * T97_HALO)
+
+// WaveletFwd.cpp:39-44 (float constants; invK computed in double then rounded)
+#define F97_A (-1.586134342f)
+#define F97_B (-0.052980118f)
+#define F97_G (0.882911075f)
+#define F97_D (0.443506852f)
+#define F97_K (1.230174105f)
+#define F97_INVK ((float)(1.0 / 1.230174105))
+// WaveletReverse.cpp:365-371
+#define I97_A (1.586134342f)
+#define I97_B (0.052980118f)
+#define I97_G (-0.882911075f)
+#define I97_D (-0.443506852f)
+#define I97_TWO_INVK (1.625732422f)
+
+__device__ __forceinline__ int mirror97(int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+// =============================================================================
+// DC shift + ICT forward (mct.cpp:147-219 CompressIrrev; TileProcessor.cpp:506-535).
+// Output: float written over int32 storage, as in Grok.
+// =============================================================================
+__global__ __launch_bounds__(256) void k_dc_ict_fwd(const int32_t* __restrict__ r_in, const int32_t* __restrict__ g_in,
+                                                    const int32_t* __restrict__ b_in, uint32_t sin,
+                                                    float* __restrict__ y_out, float* __restrict__ u_out,
+                                                    float* __restrict__ v_out, uint32_t sout, uint32_t w, uint32_t h,
+                                                    int32_t shift) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= w || y >= h) return;
+    const float a_r = 0.299f, a_g = 0.587f, a_b = 0.114f;
+    const float cb = 0.5f / (1.0f - a_b), cr = 0.5f / (1.0f - a_r);
+    const size_t i = (size_t)y * sin + x, o = (size_t)y * sout + x;
+    float r = (float)(r_in[i] - shift), g = (float)(g_in[i] - shift), b = (float)(b_in[i] - shift);
+    float t0 = a_r * r, t1 = a_g * g, t2 = a_b * b;
+    float Y = (t0 + t1) + t2;
+    y_out[o] = Y;
+    u_out[o] = cb * (b - Y);
+    v_out[o] = cr * (r - Y);
+}
+
+// DC shift to float without MCT (the standard behaviour; Grok's mono 9/7 path
+// multiplies by 2048 and reinterprets — R-BUG-1, not reproduced).
+__global__ __launch_bounds__(256) void k_dc_fwd_f(const int32_t* __restrict__ in, uint32_t sin, float* __restrict__ out,
+                                                  uint32_t sout, uint32_t w, uint32_t h, int32_t shift) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= w || y >= h) return;
+    out[(size_t)y * sout + x] = (float)(in[(size_t)y * sin + x] - shift);
+}
+
+// Inverse ICT + DC shift + clamp (mct.cpp:284-364 DecompressIrrev, lrintf rounding).
+__global__ __launch_bounds__(256) void k_ict_inv_dc(const float* __restrict__ y_in, const float* __restrict__ u_in,
+                                                    const float* __restrict__ v_in, uint32_t sin,
+                                                    int32_t* __restrict__ r_out, int32_t* __restrict__ g_out,
+                                                    int32_t* __restrict__ b_out, uint32_t sout, uint32_t w, uint32_t h,
+                                                    int32_t shift, int32_t mn, int32_t mx) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= w || y >= h) return;
+    const size_t i = (size_t)y * sin + x, o = (size_t)y * sout + x;
+    float Y = y_in[i], U = u_in[i], V = v_in[i];
+    float R = Y + 1.402f * V;
+    float G = (Y - 0.34413f * U) - 0.71414f * V;
+    float B = Y + 1.772f * U;
+    auto cl = [&](float f) { int32_t v = (int32_t)rintf(f) + shift; return v < mn ? mn : (v > mx ? mx : v); };
+    r_out[o] = cl(R); g_out[o] = cl(G); b_out[o] = cl(B);
+}
+
+__global__ __launch_bounds__(256) void k_dc_inv_f(const float* __restrict__ in, uint32_t sin, int32_t* __restrict__ out,
+                                                  uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
+                                                  int32_t mx) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= w || y >= h) return;
+    int32_t v = (int32_t)rintf(in[(size_t)y * sin + x]) + shift;
+    out[(size_t)y * sout + x] = v < mn ? mn : (v > mx ? mx : v);
+}
+
+// =============================================================================
+// Forward 9/7, one level (WaveletFwd.cpp:964-1025): vertical then horizontal.
+// =============================================================================
+__global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict__ src, uint32_t sstride,
+                                                         float* __restrict__ dst, uint32_t dstride, uint32_t w,
+                                                         uint32_t h) {
+    __shared__ float T[T97_LH][T97_LW + 1];
+    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < T97_LH * T97_LW; i += 256) {
+        int ly = i / T97_LW, lx = i % T97_LW;
+        int gy = mirror97(y0 - T97_HALO + ly, (int)h), gx = mirror97(x0 - T97_HALO + lx, (int)w);
+        T[ly][lx] = src[(size_t)gy * sstride + gx];
+    }
+    __syncthreads();
+    // local row ly <-> global y0 - 4 + ly; parity of global y == parity of ly (y0 even)
+    if (h > 1) {
+        const float cs[4] = {F97_A, F97_B, F97_G, F97_D};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int par = (s & 1) ? 0 : 1;          // alpha/gamma update odd rows, beta/delta even rows
+            const int lo = 1 + s, hi = T97_LH - 2 - s;  // rows with both neighbours still valid
+            const int first = lo + ((lo & 1) != par);
+            const int nrows = first > hi ? 0 : (hi - first) / 2 + 1;
+            for (int i = tid; i < nrows * T97_LW; i += 256) {
+                int ly = first + 2 * (i / T97_LW), lx = i % T97_LW;
+                float t = (T[ly - 1][lx] + T[ly + 1][lx]) * cs[s];
+                T[ly][lx] = T[ly][lx] + t;
+            }
+            __syncthreads();
+        }
+        for (int i = tid; i < T97_H * T97_LW; i += 256) {
+            int ly = T97_HALO + i / T97_LW, lx = i % T97_LW;
+            T[ly][lx] = T[ly][lx] * ((ly & 1) ? F97_K : F97_INVK);
+        }
+        __syncthreads();
+    }
+    if (w > 1) {
+        const float cs[4] = {F97_A, F97_B, F97_G, F97_D};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int par = (s & 1) ? 0 : 1;
+            const int lo = 1 + s, hi = T97_LW - 2 - s;
+            const int first = lo + ((lo & 1) != par);
+            const int ncols = first > hi ? 0 : (hi - first) / 2 + 1;
+            for (int i = tid; i < T97_H * ncols; i += 256) {
+                int ly = T97_HALO + i / ncols, lx = first + 2 * (i % ncols);
+                float t = (T[ly][lx - 1] + T[ly][lx + 1]) * cs[s];
+                T[ly][lx] = T[ly][lx] + t;
+            }
+            __syncthreads();
+        }
+        for (int i = tid; i < T97_H * T97_W; i += 256) {
+            int ly = T97_HALO + i / T97_W, lx = T97_HALO + i % T97_W;
+            T[ly][lx] = T[ly][lx] * ((lx & 1) ? F97_K : F97_INVK);
+        }
+        __syncthreads();
+    }
+    const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
+    for (int i = tid; i < T97_H * T97_W; i += 256) {
+        int ry = i / T97_W, rx = i % T97_W;
+        int q = rx / (T97_W / 2), k = rx % (T97_W / 2);
+        int gx = x0 + 2 * k + q, gy = y0 + ry;
+        if (gx >= (int)w || gy >= (int)h) continue;
+        float v = T[ry + T97_HALO][2 * k + q + T97_HALO];
+        int ox = (q == 0) ? (gx >> 1) : (snw + (gx >> 1));
+        int oy = ((gy & 1) == 0) ? (gy >> 1) : (snh + (gy >> 1));
+        dst[(size_t)oy * dstride + ox] = v;
+    }
+}
+
+// =============================================================================
+// Inverse 9/7, one level (WaveletReverse.cpp:1010-1022, 1272-1351):
+// horizontal then vertical, on the interleaved signal.
+// =============================================================================
+__global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict__ src, uint32_t sstride,
+                                                         float* __restrict__ dst, uint32_t dstride, uint32_t w,
+                                                         uint32_t h) {
+    __shared__ float T[T97_LH][T97_LW + 1];
+    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H;
+    const int tid = threadIdx.x;
+    const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
+    for (int i = tid; i < T97_LH * T97_LW; i += 256) {
+        int ly = i / T97_LW, lx = i % T97_LW;
+        int gy = mirror97(y0 - T97_HALO + ly, (int)h), gx = mirror97(x0 - T97_HALO + lx, (int)w);
+        int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
+        int sx = (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1);
+        T[ly][lx] = src[(size_t)sy * sstride + sx];
+    }
+    __syncthreads();
+    const float cs[4] = {I97_D, I97_G, I97_B, I97_A};
+    if (w > 1) {
+        for (int i = tid; i < T97_LH * T97_LW; i += 256) {
+            int ly = i / T97_LW, lx = i % T97_LW;
+            T[ly][lx] = T[ly][lx] * ((lx & 1) ? I97_TWO_INVK : F97_K);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int par = (s & 1) ? 1 : 0;            // delta/beta on even samples, gamma/alpha on odd
+            const int lo = 1 + s, hi = T97_LW - 2 - s;
+            const int first = lo + ((lo & 1) != par);
+            const int ncols = first > hi ? 0 : (hi - first) / 2 + 1;
+            for (int i = tid; i < T97_LH * ncols; i += 256) {
+                int ly = i / ncols, lx = first + 2 * (i % ncols);
+                float t = (T[ly][lx - 1] + T[ly][lx + 1]) * cs[s];
+                T[ly][lx] = T[ly][lx] + t;
+            }
+            __syncthreads();
+        }
+    }
+    if (h > 1) {
+        for (int i = tid; i < T97_LH * T97_W; i += 256) {
+            int ly = i / T97_W, lx = T97_HALO + i % T97_W;
+            T[ly][lx] = T[ly][lx] * ((ly & 1) ? I97_TWO_INVK : F97_K);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int par = (s & 1) ? 1 : 0;
+            const int lo = 1 + s, hi = T97_LH - 2 - s;
+            const int first = lo + ((lo & 1) != par);
+            const int nrows = first > hi ? 0 : (hi - first) / 2 + 1;
+            for (int i = tid; i < nrows * T97_W; i += 256) {
+                int ly = first + 2 * (i / T97_W), lx = T97_HALO + i % T97_W;
+                float t = (T[ly - 1][lx] + T[ly + 1][lx]) * cs[s];
+                T[ly][lx] = T[ly][lx] + t;
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = tid; i < T97_H * T97_W; i += 256) {
+        int ry = i / T97_W, rx = i % T97_W;
+        int gx = x0 + rx, gy = y0 + ry;
+        if (gx >= (int)w || gy >= (int)h) continue;
+        dst[(size_t)gy * dstride + gx] = T[ry + T97_HALO][rx + T97_HALO];
+    }
+}
+
+#include "gk_launch.h"
+
+void gk_launch_dc_ict_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin, float* y,
+                          float* u, float* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift) {
+    hipLaunchKernelGGL(k_dc_ict_fwd, dim3((w + 255) / 256, h), dim3(256), 0, st, r, g, b, sin, y, u, v, sout, w, h, shift);
+}
+void gk_launch_dc_fwd_f(hipStream_t st, const int32_t* in, uint32_t sin, float* out, uint32_t sout, uint32_t w,
+                        uint32_t h, int32_t shift) {
+    hipLaunchKernelGGL(k_dc_fwd_f, dim3((w + 255) / 256, h), dim3(256), 0, st, in, sin, out, sout, w, h, shift);
+}
+void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const float* v, uint32_t sin, int32_t* r,
+                          int32_t* g, int32_t* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
+                          int32_t mx) {
+    hipLaunchKernelGGL(k_ict_inv_dc, dim3((w + 255) / 256, h), dim3(256), 0, st, y, u, v, sin, r, g, b, sout, w, h,
+                       shift, mn, mx);
+}
+void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+                        uint32_t h, int32_t shift, int32_t mn, int32_t mx) {
+    hipLaunchKernelGGL(k_dc_inv_f, dim3((w + 255) / 256, h), dim3(256), 0, st, in, sin, out, sout, w, h, shift, mn, mx);
+}
+void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
+                         uint32_t h) {
+    dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H);
+    hipLaunchKernelGGL(k_dwt97_fwd_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h);
+}
+void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
+                         uint32_t h) {
+    dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H);
+    hipLaunchKernelGGL(k_dwt97_inv_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h);
+}

@@ -46,6 +46,11 @@ struct Params {
     uint32_t numres = 6, cbw = 6, cbh = 6, irrev = 0, mct = 1, numgbits = 2, nlayers = 1, write_com = 1;
     uint32_t prcw[GK_MAXRLVLS], prch[GK_MAXRLVLS];
     bool custom_prc = false;
+    double rates[GK_MAX_LAYERS] = {0};   // compression ratio per layer (0 = remaining passes)
+    bool rate_control() const {          // TileProcessor::needsRateControl (TileProcessor.cpp:952-967)
+        for (uint32_t l = 0; l < nlayers; ++l) if (rates[l] > 0.0) return true;
+        return false;
+    }
 };
 
 struct BandG {
@@ -60,6 +65,7 @@ struct BandG {
 struct PrecG {
     uint32_t cw = 0, ch = 0;
     uint32_t first_block = 0;   // index into Plan::blocks (canonical order)
+    uint32_t tree = 0;          // index of this precinct-band's tag trees
 };
 struct ResG {
     uint32_t w, h, pw, ph, cbw, cbh;
@@ -81,7 +87,25 @@ struct Plan {
     uint64_t slot_bytes = 0;
     std::vector<uint64_t> sym_off;       // T1 symbol-stream offsets (nblocks + 1)
     std::vector<uint64_t> st_off;        // T1 decoder scratch offsets in uint64 words (nblocks + 1)
+    uint32_t ntrees = 0;                 // precinct-bands with code-blocks
 };
+
+// DWT basis-function norms (T1.cpp:264-277 getnorm_53 / getnorm_97; ISO 15444-1 Annex E)
+static double band_norm(uint32_t level, uint32_t orient, bool rev) {
+    static const double n53[4][10] = {
+        {1.000, 1.500, 2.750, 5.375, 10.68, 21.34, 42.67, 85.33, 170.7, 341.3},
+        {1.038, 1.592, 2.919, 5.703, 11.33, 22.64, 45.25, 90.48, 180.9},
+        {1.038, 1.592, 2.919, 5.703, 11.33, 22.64, 45.25, 90.48, 180.9},
+        {.7186, .9218, 1.586, 3.043, 6.019, 12.01, 24.00, 47.97, 95.93}};
+    static const double n97[4][10] = {
+        {1.000, 1.965, 4.177, 8.403, 16.90, 33.84, 67.69, 135.3, 270.6, 540.9},
+        {2.022, 3.989, 8.355, 17.04, 34.27, 68.63, 137.3, 274.6, 549.0},
+        {2.022, 3.989, 8.355, 17.04, 34.27, 68.63, 137.3, 274.6, 549.0},
+        {2.080, 3.865, 8.307, 17.18, 34.71, 69.59, 139.3, 278.6, 557.2}};
+    if (orient == 0 && level > 9) level = 9;
+    else if (orient > 0 && level > 8) level = 8;
+    return rev ? n53[orient][level] : n97[orient][level];
+}
 
 static void assign_steps(Plan& P) {
     for (auto& C : P.comps) {
@@ -90,17 +114,8 @@ static void assign_steps(Plan& P) {
                 uint32_t level = P.p.numres - 1 - r;
                 uint32_t gain = P.p.irrev ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
                 // Part-1 QCD generation (HTParams.cpp:216-251)
-                static const double n97[4][10] = {
-                    {1.000, 1.965, 4.177, 8.403, 16.90, 33.84, 67.69, 135.3, 270.6, 540.9},
-                    {2.022, 3.989, 8.355, 17.04, 34.27, 68.63, 137.3, 274.6, 549.0},
-                    {2.022, 3.989, 8.355, 17.04, 34.27, 68.63, 137.3, 274.6, 549.0},
-                    {2.080, 3.865, 8.307, 17.18, 34.71, 69.59, 139.3, 278.6, 557.2}};
                 double stepsize = 1.0;
-                if (P.p.irrev) {
-                    uint32_t lv = level;
-                    if (B.orient == 0 && lv > 9) lv = 9; else if (B.orient > 0 && lv > 8) lv = 8;
-                    stepsize = (double)(1u << gain) / n97[B.orient][lv];
-                }
+                if (P.p.irrev) stepsize = (double)(1u << gain) / band_norm(level, B.orient, false);
                 uint32_t step = (uint32_t)floor(stepsize * 8192.0);
                 int pp = floorlog2(step) - 13, n = 11 - floorlog2(step);
                 B.mant = (n < 0 ? step >> -n : step << n) & 0x7ff;
@@ -142,6 +157,7 @@ static void build_plan(Plan& P) {
     for (uint32_t l = 0; l <= L; ++l) { P.resw[l] = ceildivpow2(P.w, l); P.resh[l] = ceildivpow2(P.h, l); }
     P.comps.assign(P.nc, CompG());
     P.blocks.clear();
+    P.ntrees = 0;
     for (uint32_t c = 0; c < P.nc; ++c) {
         CompG& C = P.comps[c];
         C.res.assign(P.p.numres, ResG());
@@ -194,6 +210,7 @@ static void build_plan(Plan& P) {
                 for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
                     PrecG& PG = R.prc[bi][pi];
                     PG.first_block = (uint32_t)P.blocks.size();
+                    PG.tree = P.ntrees;
                     if (B.empty()) continue;
                     uint32_t i = pi % R.pw, j = pi / R.pw;
                     uint32_t cx0 = i << bpw, cy0 = j << bph;
@@ -203,6 +220,7 @@ static void build_plan(Plan& P) {
                     uint32_t gx0 = (px0 >> R.cbw) << R.cbw, gy0 = (py0 >> R.cbh) << R.cbh;
                     PG.cw = ((ceildivpow2(px1, R.cbw) << R.cbw) - gx0) >> R.cbw;
                     PG.ch = ((ceildivpow2(py1, R.cbh) << R.cbh) - gy0) >> R.cbh;
+                    ++P.ntrees;
                     for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
                         uint32_t a = k % PG.cw, b = k / PG.cw;
                         uint32_t kx0 = gx0 + (a << R.cbw), ky0 = gy0 + (b << R.cbh);
@@ -215,8 +233,17 @@ static void build_plan(Plan& P) {
                         G.w = (uint16_t)(x1 - x0); G.h = (uint16_t)(y1 - y0);
                         G.orient = (uint8_t)B.orient; G.comp = (uint8_t)c;
                         G.band_numbps = (uint8_t)B.numbps;
-                        G.flags = P.p.irrev ? 1 : 0;
+                        G.flags = (P.p.irrev ? 1 : 0) | (P.p.rate_control() ? 2 : 0);
                         G.step = B.step_enc;
+                        // T1::getwmsedec weight w1 * w2 * stepsize (T1.cpp:418-436): w1 = MCT basis norm
+                        // (mct.cpp:689-704) when the MCT is on, w2 = DWT band norm (T1.cpp:264-277)
+                        {
+                            static const double norms_irrev[3] = {1.732, 1.805, 1.573};
+                            static const double norms_rev[3] = {1.732, .8292, .8292};
+                            const bool mct = P.p.mct && P.nc >= 3;
+                            double w1 = (mct && c < 3) ? (P.p.irrev ? norms_irrev[c] : norms_rev[c]) : 1.0;
+                            G.wmse = w1 * band_norm(P.p.numres - 1 - r, B.orient, !P.p.irrev) * (double)B.step_enc;
+                        }
                         P.blocks.push_back(G);
                     }
                 }
@@ -391,6 +418,204 @@ struct DecTree {   // decoder-side tag tree
     }
 };
 
+// ---------------------------------------------------------------------------
+// T2 packet encoding with quality layers and PCRD rate allocation.
+//   write_packet  — T2Compress::compressHeader + body (T2Compress.cpp:114-260,
+//                   compressPacketSimulate :347-430 for the byte budget);
+//   simulate      — compressPacketsSimulate (:59-112), LRCP;
+//   make_layer    — makeLayerSimple / makeLayerFinal (TileProcessor.cpp:1367-1515);
+//   allocate      — pcrdBisectSimple (:1196-1365) with updateRates
+//                   (CodeStreamCompress.cpp:951-1025).
+// Block k of the plan contributes lnp[k * nlayers + l] passes to layer l.
+// ---------------------------------------------------------------------------
+struct T2Enc {
+    const Plan& P;
+    const uint32_t* info;        // 4 u32 per block: numbps, npasses, bytes, pass offset
+    const GkPass* passes;        // packed pass records (only needed when passes split across layers)
+    uint32_t L;                  // layers
+    std::vector<uint16_t> lnp;   // passes per (block, layer)
+    std::vector<uint16_t> inprev;   // T2 state: passes already in packets (numPassesInPacket)
+    std::vector<uint8_t> nlb;       // T2 state: numlenbits
+    std::vector<TagTree> incl, imsb;
+    std::vector<uint8_t> hdr;
+    T2Enc(const Plan& plan, const uint32_t* inf, const GkPass* ps)
+        : P(plan), info(inf), passes(ps), L(plan.p.nlayers) {
+        size_t nb = P.blocks.size();
+        lnp.assign(nb * L, 0); inprev.assign(nb, 0); nlb.assign(nb, 0);
+        incl.resize(P.ntrees); imsb.resize(P.ntrees);
+        for (auto& C : P.comps)
+            for (auto& R : C.res)
+                for (size_t bi = 0; bi < R.bands.size(); ++bi)
+                    for (auto& PG : R.prc[bi])
+                        if (PG.cw && PG.ch) { incl[PG.tree].build(PG.cw, PG.ch); imsb[PG.tree].build(PG.cw, PG.ch); }
+    }
+    uint32_t npasses(uint32_t b) const { return info[4 * (size_t)b + 1]; }
+    uint32_t rate(uint32_t b, uint32_t q) const {   // cumulative bytes after pass q (q < npasses)
+        if (q + 1 == npasses(b)) return info[4 * (size_t)b + 2];
+        return passes[info[4 * (size_t)b + 3] + q].rate;
+    }
+    double dist(uint32_t b, uint32_t q) const { return passes[info[4 * (size_t)b + 3] + q].dist; }
+
+    // One packet.  budget: remaining bytes (nullptr = unbounded).  seg (optional) receives
+    // (block, first byte, length) body segments.  Returns false when the budget is exceeded.
+    bool write_packet(const ResG& R, uint32_t pi, uint32_t l, uint64_t* budget,
+                      std::vector<uint32_t>* seg) {
+        if (l == 0) {
+            for (size_t bi = 0; bi < R.bands.size(); ++bi) {
+                const PrecG& PG = R.prc[bi][pi];
+                if (!PG.cw || !PG.ch) continue;
+                incl[PG.tree].reset(); imsb[PG.tree].reset();
+                const uint32_t bnb = R.bands[bi].numbps;
+                for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                    uint32_t b = PG.first_block + k;
+                    inprev[b] = 0;
+                    imsb[PG.tree].setvalue(k, bnb - info[4 * (size_t)b]);
+                }
+            }
+        }
+        hdr.clear();
+        BitWriter bw(hdr);
+        bw.putbit(1);
+        for (size_t bi = 0; bi < R.bands.size(); ++bi) {
+            const PrecG& PG = R.prc[bi][pi];
+            if (!PG.cw || !PG.ch) continue;
+            const uint32_t n = PG.cw * PG.ch;
+            TagTree& IT = incl[PG.tree];
+            for (uint32_t k = 0; k < n; ++k) {
+                uint32_t b = PG.first_block + k;
+                if (!inprev[b] && lnp[(size_t)b * L + l]) IT.setvalue(k, l);
+            }
+            for (uint32_t k = 0; k < n; ++k) {
+                uint32_t b = PG.first_block + k;
+                uint32_t np = lnp[(size_t)b * L + l];
+                if (!inprev[b]) IT.encode(bw, k, l + 1);
+                else bw.putbit(np != 0);
+                if (!np) continue;
+                if (!inprev[b]) { nlb[b] = 3; imsb[PG.tree].encode(bw, k, 0xffffffffu); }
+                bw.numpasses(np);
+                // default style: one segment per contribution (only the last pass is terminated)
+                uint32_t r0 = inprev[b] ? rate(b, inprev[b] - 1) : 0;
+                uint32_t len = rate(b, inprev[b] + np - 1) - r0;
+                int inc = std::max(0, floorlog2(len) + 1 - ((int)nlb[b] + floorlog2(np)));
+                bw.commacode((uint32_t)inc);
+                nlb[b] = (uint8_t)(nlb[b] + inc);
+                bw.write(len, (int)nlb[b] + floorlog2(np));
+            }
+        }
+        bw.flush();
+        if (budget) {
+            if ((uint64_t)hdr.size() >= *budget) return false;   // bounded BitIO (BitIO.cpp:35-52)
+            *budget -= hdr.size();
+        }
+        for (size_t bi = 0; bi < R.bands.size(); ++bi) {
+            const PrecG& PG = R.prc[bi][pi];
+            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                uint32_t b = PG.first_block + k;
+                uint32_t np = lnp[(size_t)b * L + l];
+                if (!np) continue;
+                uint32_t r0 = inprev[b] ? rate(b, inprev[b] - 1) : 0;
+                uint32_t r1 = rate(b, inprev[b] + np - 1);
+                if (budget) {
+                    if ((uint64_t)(r1 - r0) > *budget) return false;
+                    *budget -= (r1 - r0);
+                }
+                if (seg) { seg->push_back(b); seg->push_back(r0); seg->push_back(r1 - r0); }
+                inprev[b] = (uint16_t)(inprev[b] + np);
+            }
+        }
+        return true;
+    }
+
+    bool simulate(uint32_t max_layers, uint64_t max_bytes) {
+        uint64_t budget = max_bytes;
+        uint64_t* bp = max_bytes == 0xffffffffull ? nullptr : &budget;
+        for (uint32_t l = 0; l < max_layers; ++l)
+            for (uint32_t r = 0; r < P.p.numres; ++r)
+                for (uint32_t c = 0; c < P.nc; ++c) {
+                    const ResG& R = P.comps[c].res[r];
+                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi)
+                        if (!write_packet(R, pi, l, bp, nullptr)) return false;
+                }
+        return true;
+    }
+
+    // makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0)
+    void make_layer(uint32_t l, double thresh, bool final_attempt, std::vector<uint16_t>& prev) {
+        const uint32_t nb = (uint32_t)P.blocks.size();
+        for (uint32_t b = 0; b < nb; ++b) {
+            if (l == 0) prev[b] = 0;
+            const uint32_t np = npasses(b);
+            uint32_t inc;
+            if (thresh < 0) inc = std::max<uint32_t>(prev[b], np);
+            else if (thresh == 0) inc = np;
+            else {
+                inc = prev[b];
+                for (uint32_t q = prev[b]; q < np; ++q) {
+                    uint32_t dr; double dd;
+                    if (inc == 0) { dr = rate(b, q); dd = dist(b, q); }
+                    else { dr = rate(b, q) - rate(b, inc - 1); dd = dist(b, q) - dist(b, inc - 1); }
+                    if (!dr) { if (dd != 0) inc = q + 1; continue; }
+                    double slope = dd / dr;
+                    if (thresh - slope < 2.220446049250313e-16) inc = q + 1;
+                }
+            }
+            lnp[(size_t)b * L + l] = (uint16_t)(inc - prev[b]);
+            if (final_attempt) prev[b] = (uint16_t)inc;
+        }
+    }
+
+    void allocate(size_t header_size) {
+        const uint32_t nb = (uint32_t)P.blocks.size();
+        std::vector<uint16_t> prev(nb, 0);
+        if (!P.p.rate_control()) {
+            for (uint32_t l = 0; l < L; ++l) make_layer(l, -1.0, true, prev);
+            return;
+        }
+        // updateRates: compression ratio -> cumulative byte budget per layer
+        double rates[GK_MAX_LAYERS];
+        const double size_pixel = (double)P.nc * P.prec, npix = (double)P.w * P.h;
+        for (uint32_t k = 0; k < L; ++k) rates[k] = P.p.rates[k] > 0.0 ? (size_pixel * npix) / (P.p.rates[k] * 8.0) : 0.0;
+        const double sot_adjust = (npix * (double)header_size) / npix;
+        if (rates[0] > 0.0) { rates[0] -= sot_adjust; if (rates[0] < 30.0f) rates[0] = 30.0f; }
+        for (uint32_t k = 1; k + 1 < L; ++k)
+            if (rates[k] > 0.0) { rates[k] -= sot_adjust; if (rates[k] < rates[k - 1] + 10.0) rates[k] = rates[k - 1] + 20.0; }
+        if (L > 1 && rates[L - 1] > 0.0) {
+            rates[L - 1] -= (sot_adjust + 2.0);
+            if (rates[L - 1] < rates[L - 2] + 10.0) rates[L - 1] = rates[L - 2] + 20.0;
+        }
+        double min_slope = 1.7976931348623157e308, max_slope = -1;
+        for (uint32_t b = 0; b < nb; ++b)
+            for (uint32_t q = 0; q < npasses(b); ++q) {
+                int32_t dr; double dd;
+                if (q == 0) { dr = (int32_t)rate(b, 0); dd = dist(b, 0); }
+                else { dr = (int32_t)(rate(b, q) - rate(b, q - 1)); dd = dist(b, q) - dist(b, q - 1); }
+                if (dr == 0) continue;
+                double sl = dd / dr;
+                if (sl < min_slope) min_slope = sl;
+                if (sl > max_slope) max_slope = sl;
+            }
+        double upper = max_slope;
+        for (uint32_t l = 0; l < L; ++l) {
+            uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
+            if (rates[l] > 0.0) {
+                double lower = min_slope, prevthresh = -1, thresh = 0;
+                for (uint32_t it = 0; it < 128; ++it) {
+                    thresh = (upper == -1) ? lower : (lower + upper) / 2;
+                    make_layer(l, thresh, false, prev);
+                    if (prevthresh != -1 && fabs(prevthresh - thresh) < 0.001) break;
+                    prevthresh = thresh;
+                    if (!simulate(l + 1, max_len)) { lower = thresh; continue; }
+                    upper = thresh;
+                }
+                make_layer(l, upper == -1 ? thresh : upper, true, prev);
+                upper = lower - 1;
+            } else {
+                make_layer(l, -1.0, true, prev);
+            }
+        }
+    }
+};
+
 static void put16(std::vector<uint8_t>& o, uint32_t v) { o.push_back((uint8_t)(v >> 8)); o.push_back((uint8_t)v); }
 static void put32(std::vector<uint8_t>& o, uint32_t v) { put16(o, v >> 16); put16(o, v & 0xffff); }
 
@@ -485,8 +710,9 @@ struct gk_ctx {
     DevBuf dplanes;     // component planes staged from host
     DevBuf derr;
     DevBuf dsym, dsymoff, dpassend, dcminfo;
-    DevBuf dscratch, dstoff;
-    HostBuf hinfo, hseg, hhdr;
+    DevBuf dscratch, dstoff, dnmse;
+    HostBuf hinfo, hseg, hhdr, hpasses;
+    int16_t* nmse_tab = nullptr;   // device copy of the nmsedec tables (4 x 128)
     hipEvent_t ev[32];
     bool blocks_uploaded = false;
 };
@@ -501,6 +727,8 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     P.mct = cp->mct;
     P.numgbits = cp->numgbits ? cp->numgbits : 2;
     P.nlayers = cp->numlayers ? cp->numlayers : 1;
+    if (P.nlayers > GK_MAX_LAYERS) P.nlayers = GK_MAX_LAYERS;
+    for (uint32_t l = 0; l < P.nlayers; ++l) P.rates[l] = cp->layer_rate[l] > 0.0 ? cp->layer_rate[l] : 0.0;
     P.write_com = cp->write_comment;
     if ((cp->csty & 1) && cp->res_spec) {   // CodeStreamCompress.cpp:542-590
         P.custom_prc = true;
@@ -520,8 +748,8 @@ static void set_params(Params& P, const gk_cparameters* cp) {
 
 static std::string plan_key(const Plan& P) {
     char buf[256];
-    snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
-             P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0);
+    snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
+             P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0, P.p.rate_control() ? 1 : 0);
     std::string k(buf);
     for (uint32_t r = 0; r < P.p.numres; ++r) k += " " + std::to_string(P.p.prcw[r]) + "," + std::to_string(P.p.prch[r]);
     return k;
@@ -550,8 +778,15 @@ static void run_dwt(gk_ctx* ctx, bool forward) {
             int32_t* B = A + P.plane_elems;
             int32_t* src_l = (l & 1) ? A : B;     // D_{l-1}: level l input plane (l-1 odd -> B)
             int32_t* dst_l = (l & 1) ? B : A;     // D_l
-            if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, P.stride, dst_l, P.stride, w, h);
-            else gk_launch_dwt53_inv(ctx->st, dst_l, P.stride, src_l, P.stride, w, h);
+            if (P.p.irrev) {
+                float* fs = reinterpret_cast<float*>(src_l);
+                float* fd = reinterpret_cast<float*>(dst_l);
+                if (forward) gk_launch_dwt97_fwd(ctx->st, fs, P.stride, fd, P.stride, w, h);
+                else gk_launch_dwt97_inv(ctx->st, fd, P.stride, fs, P.stride, w, h);
+            } else {
+                if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, P.stride, dst_l, P.stride, w, h);
+                else gk_launch_dwt53_inv(ctx->st, dst_l, P.stride, src_l, P.stride, w, h);
+            }
             ctx->tm.dwt_launches++;
             ctx->tm.dwt_bytes += (uint64_t)w * h * 8;
         }
@@ -572,9 +807,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     want.w = info->w; want.h = info->h; want.nc = info->numcomps; want.prec = info->prec; want.sgnd = info->sgnd;
     set_params(want.p, cp);
     if (want.nc < 3) want.p.mct = 0;
-    if (want.p.irrev) throw GkError("9/7 irreversible encode is not implemented on the GPU path yet");
     if (cp && cp->cblk_sty) throw GkError("code-block style mode switches are not supported");
-    if (want.p.nlayers != 1) throw GkError("only single-layer lossless encode is supported on the GPU path");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if ((1u << want.p.cbw) > 64 || (1u << want.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
     ensure_plan(ctx, want);
@@ -601,49 +834,62 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     // DC shift + MCT into plane A of each component
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
     auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems; };
-    if (P.p.mct && P.nc >= 3) {
-        gk_launch_dc_rct_fwd(st, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), P.stride, P.w, P.h, shift);
-        for (uint32_t c = 3; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), P.stride, P.w, P.h, shift);
+    auto planeAf = [&](uint32_t c) { return reinterpret_cast<float*>(planeA(c)); };
+    const bool mct3 = P.p.mct && P.nc >= 3;
+    if (!P.p.irrev) {
+        if (mct3) gk_launch_dc_rct_fwd(st, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), P.stride, P.w, P.h, shift);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), P.stride, P.w, P.h, shift);
     } else {
-        for (uint32_t c = 0; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), P.stride, P.w, P.h, shift);
+        if (mct3) gk_launch_dc_ict_fwd(st, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), P.stride, P.w, P.h, shift);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, src[c], sstr[c], planeAf(c), P.stride, P.w, P.h, shift);
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     run_dwt(ctx, true);
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // T1
+    const bool do_rc = P.p.rate_control();
     uint8_t* dbytes = (uint8_t*)ctx->bytes.get(P.slot_bytes + (64u << 20));
     GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * std::max(nb, 1u));
     GkPass* dps = (GkPass*)ctx->dpasses.get(sizeof(GkPass) * GK_MAX_PASSES * (size_t)std::max(nb, 1u));
-    uint32_t* dinfo = (uint32_t*)ctx->dinfo.get(12 * (size_t)std::max(nb, 1u));
+    uint32_t* dinfo = (uint32_t*)ctx->dinfo.get(16 * (size_t)std::max(nb, 1u) + 16);
     int* derr = (int*)ctx->derr.get(64);
+    uint32_t* dpcount = (uint32_t*)(derr + 4);
     uint8_t* dsym = (uint8_t*)ctx->dsym.get(P.sym_off[nb] + 256);
     uint64_t* dsymoff = (uint64_t*)ctx->dsymoff.get(8 * ((size_t)nb + 1));
     uint32_t* dpe = (uint32_t*)ctx->dpassend.get(4 * GK_MAX_PASSES * (size_t)std::max(nb, 1u));
     uint32_t* dcm = (uint32_t*)ctx->dcminfo.get(8 * (size_t)std::max(nb, 1u));
+    int32_t* dnmse = do_rc ? (int32_t*)ctx->dnmse.get(4 * GK_MAX_PASSES * (size_t)std::max(nb, 1u)) : nullptr;
     if (!ctx->blocks_uploaded) {
         HIPCHK(hipMemcpyAsync(dblk, P.blocks.data(), sizeof(GkBlock) * nb, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(dsymoff, P.sym_off.data(), 8 * ((size_t)nb + 1), hipMemcpyHostToDevice, st));
         ctx->blocks_uploaded = true;
     }
-    HIPCHK(hipMemsetAsync(derr, 0, 4, st));
-    if (getenv("GK_T1_SERIAL")) {
-        gk_launch_t1_encode(st, arena, dblk, dbytes, dps, dinfo, nb, derr);
-    } else {
-        gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nb, derr);
-        HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nb, derr);
-    }
+    HIPCHK(hipMemsetAsync(derr, 0, 64, st));
+    gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nb, derr, ctx->nmse_tab, dnmse);
+    HIPCHK(hipEventRecord(ctx->ev[8], st));
+    gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nb, derr, dnmse, dpcount);
     HIPCHK(hipEventRecord(ctx->ev[4], st));
-    uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(12 * (size_t)nb + 16);
-    HIPCHK(hipMemcpyAsync(hinfo, dinfo, 12 * (size_t)nb, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(hinfo + 3 * (size_t)nb, derr, 4, hipMemcpyDeviceToHost, st));
+    uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(16 * (size_t)nb + 64);
+    HIPCHK(hipMemcpyAsync(hinfo, dinfo, 16 * (size_t)nb, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hinfo + 4 * (size_t)nb, derr, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if (hinfo[3 * (size_t)nb]) throw GkError(hinfo[3 * (size_t)nb] & 2 ? "T1 symbol buffer overflow" : "T1 code-block slot overflow");
+    const uint32_t t1err = hinfo[4 * (size_t)nb], npass_total = hinfo[4 * (size_t)nb + 4];
+    if (t1err) throw GkError(t1err & 2 ? "T1 symbol buffer overflow" : "T1 code-block slot overflow");
+    const GkPass* hpasses = nullptr;
+    if (do_rc) {
+        GkPass* hp = (GkPass*)ctx->hpasses.get(sizeof(GkPass) * (size_t)std::max(npass_total, 1u));
+        HIPCHK(hipMemcpyAsync(hp, dps, sizeof(GkPass) * (size_t)npass_total, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        hpasses = hp;
+    }
 
-    // ---- host T2 (T2Compress.cpp:113-240), single layer / all passes
+    // ---- host T2 (T2Compress.cpp:113-240) with layer formation / rate allocation
     std::vector<uint8_t> H;
     H.reserve(1 << 12);
     write_main_header(H, P);
+    const size_t header_size = H.size();
+    T2Enc T2(P, hinfo, hpasses);
+    T2.allocate(header_size);
     size_t sot = H.size();
     put16(H, 0xff90); put16(H, 10); put16(H, 0); put32(H, 0); H.push_back(0); H.push_back(1);
     put16(H, 0xff93);
@@ -659,53 +905,24 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         pos += n;
     };
     add_host(H.data(), H.size());
-    TagTree incl, imsb;
-    std::vector<uint8_t> ph;
-    ph.reserve(1 << 16);
-    for (uint32_t r = 0; r < P.p.numres; ++r)
-        for (uint32_t c = 0; c < P.nc; ++c) {
-            ResG& R = P.comps[c].res[r];
-            for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                ph.clear();
-                BitWriter bw(ph);
-                bw.putbit(1);
-                for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
-                    PrecG& PG = R.prc[bi][pi];
-                    if (!PG.cw || !PG.ch) continue;
-                    const BandG& B = R.bands[bi];
-                    uint32_t n = PG.cw * PG.ch;
-                    incl.build(PG.cw, PG.ch); imsb.build(PG.cw, PG.ch);
-                    for (uint32_t k = 0; k < n; ++k) {
-                        const uint32_t* inf = hinfo + 3 * (size_t)(PG.first_block + k);
-                        imsb.setvalue(k, B.numbps - inf[0]);
-                        if (inf[1]) incl.setvalue(k, 0);
-                    }
-                    for (uint32_t k = 0; k < n; ++k) {
-                        const uint32_t* inf = hinfo + 3 * (size_t)(PG.first_block + k);
-                        uint32_t np = inf[1], len = inf[2];
-                        incl.encode(bw, k, 1);
-                        if (!np) continue;
-                        imsb.encode(bw, k, 0xffffffffu);
-                        bw.numpasses(np);
-                        int inc = std::max(0, floorlog2(len) + 1 - (3 + floorlog2(np)));
-                        bw.commacode((uint32_t)inc);
-                        bw.write(len, 3 + inc + floorlog2(np));
-                    }
-                }
-                bw.flush();
-                add_host(ph.data(), ph.size());
-                for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
-                    PrecG& PG = R.prc[bi][pi];
-                    for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                        uint32_t b = PG.first_block + k;
-                        uint32_t len = hinfo[3 * (size_t)b + 2];
-                        if (!hinfo[3 * (size_t)b + 1] || !len) continue;
-                        seg.push_back(P.blocks[b].data_off); seg.push_back(pos); seg.push_back(len);
-                        pos += len;
+    std::vector<uint32_t> body;
+    body.reserve(3 * 4096);
+    for (uint32_t l = 0; l < P.p.nlayers; ++l)
+        for (uint32_t r = 0; r < P.p.numres; ++r)
+            for (uint32_t c = 0; c < P.nc; ++c) {
+                const ResG& R = P.comps[c].res[r];
+                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                    body.clear();
+                    T2.write_packet(R, pi, l, nullptr, &body);
+                    add_host(T2.hdr.data(), T2.hdr.size());
+                    for (size_t i = 0; i < body.size(); i += 3) {
+                        if (!body[i + 2]) continue;
+                        seg.push_back(P.blocks[body[i]].data_off + body[i + 1]); seg.push_back(pos);
+                        seg.push_back(body[i + 2]);
+                        pos += body[i + 2];
                     }
                 }
             }
-        }
     uint8_t eoc[2] = {0xff, 0xd9};
     // Psot patch: tile-part length from SOT to end of tile data
     uint32_t psot = (uint32_t)(pos - sot);
@@ -733,7 +950,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     ctx->tm.mct_ms = ev_ms(ctx, 1, 2);
     ctx->tm.dwt_ms = ev_ms(ctx, 2, 3);
     ctx->tm.t1_ms = ev_ms(ctx, 3, 4);
-    ctx->tm.t1_cm_ms = getenv("GK_T1_SERIAL") ? 0.f : ev_ms(ctx, 3, 8);
+    ctx->tm.t1_cm_ms = ev_ms(ctx, 3, 8);
     ctx->tm.t2_ms = ev_ms(ctx, 4, 5);
     ctx->tm.assemble_ms = ev_ms(ctx, 5, 7);
     ctx->tm.total_ms = ev_ms(ctx, 0, 7);
@@ -820,7 +1037,6 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     if (cs_on_device) S.dev = cs; else S.host = cs;
     Header Hd;
     parse_header(S, Hd);
-    if (Hd.want.p.irrev) throw GkError("9/7 decode not implemented on the GPU path yet");
     if (Hd.want.nc < 3) Hd.want.p.mct = 0;
     ensure_plan(ctx, Hd.want);
     Plan& P = ctx->plan;
@@ -946,9 +1162,7 @@ t2done:
     ctx->blocks_uploaded = false;   // the encode table must be re-uploaded
     int32_t* arena = (int32_t*)ctx->arena.get(P.plane_elems * P.nc * 2 * sizeof(int32_t));
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    if (getenv("GK_T1_SERIAL")) {
-        gk_launch_t1_decode(st, src_bytes, dblk, arena, nb);
-    } else {
+    {
         uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * P.st_off[nb] + 64);
         uint64_t* dsto = (uint64_t*)ctx->dstoff.get(8 * ((size_t)nb + 1));
         HIPCHK(hipMemcpyAsync(dsto, P.st_off.data(), 8 * ((size_t)nb + 1), hipMemcpyHostToDevice, st));
@@ -972,12 +1186,16 @@ t2done:
         for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = comps[c]; dstr[c] = strides[c]; }
     }
     auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems; };
-    if (P.p.mct && P.nc >= 3) {
-        gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w, P.h,
-                             shift, mn, mx);
-        for (uint32_t c = 3; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], P.w, P.h, shift, mn, mx);
+    auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
+    const bool mct3 = P.p.mct && P.nc >= 3;
+    if (!P.p.irrev) {
+        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w, P.h,
+                                       shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], P.w, P.h, shift, mn, mx);
     } else {
-        for (uint32_t c = 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], P.w, P.h, shift, mn, mx);
+        if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w,
+                                       P.h, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv_f(st, planeAf(c), P.stride, dst[c], dstr[c], P.w, P.h, shift, mn, mx);
     }
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (!out_on_device) {
@@ -1009,6 +1227,23 @@ gk_ctx* gk_create(int device_id) {
     ctx->device = device_id;
     if (hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) { delete ctx; return nullptr; }
     for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+    // nmsedec lookup tables (t1_generate_luts.cpp:338-362): sig, sig0, ref, ref0
+    int16_t tab[4][128];
+    for (int i = 0; i < 128; ++i) {
+        const double F = 64.0;   // 2^T1_NMSEDEC_FRACBITS
+        double t = i / F, u = t, v = t - 1.5;
+        tab[0][i] = (int16_t)std::max(0, (int)(floor((u * u - v * v) * F + 0.5) / F * 8192.0));
+        tab[1][i] = (int16_t)std::max(0, (int)(floor((u * u) * F + 0.5) / F * 8192.0));
+        u = t - 1.0;
+        v = (i & 64) ? t - 1.5 : t - 0.5;
+        tab[2][i] = (int16_t)std::max(0, (int)(floor((u * u - v * v) * F + 0.5) / F * 8192.0));
+        tab[3][i] = (int16_t)std::max(0, (int)(floor((u * u) * F + 0.5) / F * 8192.0));
+    }
+    if (hipMalloc(&ctx->nmse_tab, sizeof tab) != hipSuccess ||
+        hipMemcpy(ctx->nmse_tab, tab, sizeof tab, hipMemcpyHostToDevice) != hipSuccess) {
+        gk_destroy(ctx);
+        return nullptr;
+    }
     return ctx;
 }
 
@@ -1017,6 +1252,7 @@ void gk_destroy(gk_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->st);
     for (auto& e : ctx->ev) (void)hipEventDestroy(e);
+    if (ctx->nmse_tab) (void)hipFree(ctx->nmse_tab);
     (void)hipStreamDestroy(ctx->st);
     delete ctx;
 }

@@ -17,17 +17,28 @@ void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, i
                          uint32_t w, uint32_t h);
 void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
                          uint32_t w, uint32_t h);
-void gk_launch_t1_encode(hipStream_t st, const int32_t* coef, GkBlock* blocks, uint8_t* bytes, GkPass* passes,
-                         uint32_t* info, uint32_t nblocks, int* err);
-void gk_launch_t1_decode(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, int32_t* coef,
-                         uint32_t nblocks);
 void gk_launch_gather(hipStream_t st, const uint8_t* src, uint8_t* dst, const uint64_t* seg, uint32_t nseg);
 void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks, const uint64_t* sym_off, uint8_t* sym,
-                     uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err);
+                     uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err, const int16_t* nmse_tab,
+                     int32_t* pass_nmse);
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
-                     uint32_t nblocks, int* err);
+                     uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter);
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, uint64_t* scratch,
                       const uint64_t* st_off, uint32_t nblocks);
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint64_t* scratch, const uint64_t* st_off,
                         int32_t* coef, uint32_t nblocks);
+// irreversible path (gk_dwt97.hip)
+void gk_launch_dc_ict_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin, float* y,
+                          float* u, float* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift);
+void gk_launch_dc_fwd_f(hipStream_t st, const int32_t* in, uint32_t sin, float* out, uint32_t sout, uint32_t w,
+                        uint32_t h, int32_t shift);
+void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const float* v, uint32_t sin, int32_t* r,
+                          int32_t* g, int32_t* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
+                          int32_t mx);
+void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+                        uint32_t h, int32_t shift, int32_t mn, int32_t mx);
+void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
+                         uint32_t h);
+void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
+                         uint32_t h);

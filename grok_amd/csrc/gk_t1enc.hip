@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include "gk_common.h"
 #include "gk_t1_common.h"
+#include <type_traits>
 
 #define SYM_PER_PLANE 11264u   // >= 2 symbols per sample + 3 per stripe column, per bit-plane
 
@@ -60,12 +61,30 @@ struct CmLds {
     uint8_t zc[512];
     uint8_t sc[256];
 };
+// Rate-control extras: the block's magnitudes (row-major, for per-sample
+// distortion lookups) and the nmsedec tables (t1_generate_luts.cpp:338-362:
+// sig, sig0, ref, ref0; 128 entries each, built on the host).
+struct CmRcLds {
+    uint32_t mag[64][64];
+    int16_t nm[4][128];
+};
 
+__device__ __forceinline__ int32_t wave_sum(int32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// RC: also accumulate Grok's per-pass nmsedec (T1.cpp:483-764 getnmsedec_sig/_ref)
+// into pass_nmse[b * GK_MAX_PASSES + pass].
+template <bool RC>
 __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, const GkBlock* __restrict__ blocks,
                                               const uint64_t* __restrict__ sym_off, uint8_t* __restrict__ sym,
                                               uint32_t* __restrict__ pass_end, uint32_t* __restrict__ cm_info,
-                                              uint32_t nblocks, int* err) {
+                                              uint32_t nblocks, int* err, const int16_t* __restrict__ nmse_tab,
+                                              int32_t* __restrict__ pass_nmse) {
     __shared__ CmLds L;
+    __shared__ typename std::conditional<RC, CmRcLds, char>::type R;
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
     const int lane = threadIdx.x;
@@ -90,6 +109,10 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
         m[y] = a;
         mx = a > mx ? a : mx;
         negcol |= (uint64_t)(v < 0) << y;
+        if constexpr (RC) R.mag[y][lane] = a;
+    }
+    if constexpr (RC) {
+        for (int i = lane; i < 512; i += 64) R.nm[i >> 7][i & 127] = nmse_tab[i];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(mx, o); mx = t > mx ? t : mx; }
@@ -112,6 +135,24 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
     const uint32_t nstripes = (h + 3) >> 2;
     uint64_t sig = 0, mu = 0;
     uint32_t pos = 0, passno = 0;
+    int32_t acc = 0;   // RC: this lane's nmsedec for the current pass
+    auto nm_sig = [&](uint32_t y, int bp) -> int32_t {
+        if constexpr (RC) { uint32_t x = R.mag[y][lane]; return bp > 0 ? R.nm[0][(x >> bp) & 127] : R.nm[1][x & 127]; }
+        return 0;
+    };
+    auto nm_ref = [&](uint32_t y, int bp) -> int32_t {
+        if constexpr (RC) { uint32_t x = R.mag[y][lane]; return bp > 0 ? R.nm[2][(x >> bp) & 127] : R.nm[3][x & 127]; }
+        return 0;
+    };
+    auto end_pass = [&]() {
+        if (lane == 0) PE[passno] = pos;
+        if constexpr (RC) {
+            int32_t t = wave_sum(acc);
+            if (lane == 0) pass_nmse[(size_t)b * GK_MAX_PASSES + passno] = t;
+            acc = 0;
+        }
+        ++passno;
+    };
 
     for (int bpno = (int)numbps - 1; bpno >= 0; --bpno) {
         uint64_t bitcol = 0;
@@ -172,9 +213,11 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                 pos += total;
                 sig |= (uint64_t)ns << sh;
                 vis |= (uint64_t)cd << sh;
+                if constexpr (RC) {
+                    for (int r = 0; r < 4; ++r) if ((ns >> r) & 1) acc += nm_sig(sh + r, bpno);
+                }
             }
-            if (lane == 0) PE[passno] = pos;
-            ++passno;
+            end_pass();
             // ================= magnitude refinement pass =================
             for (uint32_t s = 0; s < nstripes; ++s) {
                 const uint32_t sh = 4 * s;
@@ -196,10 +239,12 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                     }
                 }
                 pos += total;
+                if constexpr (RC) {
+                    for (int r = 0; r < 4; ++r) if ((mr >> r) & 1) acc += nm_ref(sh + r, bpno);
+                }
             }
             mu |= sigPrev;
-            if (lane == 0) PE[passno] = pos;
-            ++passno;
+            end_pass();
         }
         // ================= cleanup pass =================
         for (uint32_t s = 0; s < nstripes; ++s) {
@@ -257,9 +302,11 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
             }
             pos += total;
             sig |= (uint64_t)nc << sh;
+            if constexpr (RC) {
+                for (int r = 0; r < 4; ++r) if ((nc >> r) & 1) acc += nm_sig(sh + r, bpno);
+            }
         }
-        if (lane == 0) PE[passno] = pos;
-        ++passno;
+        end_pass();
     }
     if (lane == 0) { cm_info[2 * b] = numbps; cm_info[2 * b + 1] = passno; }
 }
@@ -298,11 +345,16 @@ __device__ __forceinline__ void mql_byteout(MqLane& q) {
     }
 }
 
+// Outputs: info[4b..4b+3] = (numbps, npasses, bytes, offset of the block's
+// passes in `passes`); pass records are packed (atomic offset allocation) so
+// the host copies only the passes that exist.  With rate control the
+// cumulative distortion follows T1::getwmsedec (T1.cpp:418-436, 836-842).
 __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, const uint64_t* __restrict__ sym_off,
                                               const uint32_t* __restrict__ pass_end, const uint32_t* __restrict__ cm_info,
                                               const GkBlock* __restrict__ blocks, uint8_t* __restrict__ bytes,
                                               GkPass* __restrict__ passes, uint32_t* __restrict__ info,
-                                              uint32_t nblocks, int* err) {
+                                              uint32_t nblocks, int* err, const int32_t* __restrict__ pass_nmse,
+                                              uint32_t* __restrict__ pass_counter) {
     __shared__ uint32_t tab[47];
     const int lane = threadIdx.x;
     if (lane < 47) tab[lane] = c_mq[lane];
@@ -310,11 +362,14 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
     const uint32_t b = blockIdx.x * 64 + lane;
     if (b >= nblocks) return;
     const uint32_t numbps = cm_info[2 * b], npasses = cm_info[2 * b + 1];
-    if (npasses == 0) { info[3 * b] = 0; info[3 * b + 1] = 0; info[3 * b + 2] = 0; return; }
+    if (npasses == 0) { info[4 * b] = 0; info[4 * b + 1] = 0; info[4 * b + 2] = 0; info[4 * b + 3] = 0; return; }
     const GkBlock B = blocks[b];
     const uint8_t* sp = sym + sym_off[b];
     const uint32_t* PE = pass_end + (size_t)b * GK_MAX_PASSES;
-    GkPass* P = passes + (size_t)b * GK_MAX_PASSES;
+    const uint32_t poff = atomicAdd(pass_counter, npasses);
+    GkPass* P = passes + poff;
+    const bool rc = (B.flags & 2) != 0;
+    double cum = 0.0;
     MqLane q;
     q.a = 0x8000; q.c = 0; q.ct = 12; q.bp = -1; q.cur = 0; q.wbuf = 0; q.out = bytes + B.data_off; q.cap = B.data_cap;
     q.ovf = 0;
@@ -370,11 +425,17 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
             q.c <<= q.ct; mql_byteout(q);
             q.c <<= q.ct; mql_byteout(q);
             if (q.cur != 0xff) mql_emit(q, 0);
-            P[p].term = 1; P[p].rate = (uint32_t)q.bp;
+            P[p].rate = (uint32_t)q.bp;
         } else {
-            P[p].term = 0; P[p].rate = (uint32_t)q.bp + 5 + (q.ct < 5 ? 1 : 0);
+            P[p].rate = (uint32_t)q.bp + 5 + (q.ct < 5 ? 1 : 0);
         }
-        P[p].dist = 0.f;
+        if (rc) {
+            const int bpno = p == 0 ? (int)numbps - 1 : (int)numbps - 2 - (int)(p - 1) / 3;
+            double wm = B.wmse * (double)(1 << bpno);
+            wm *= wm * (double)pass_nmse[(size_t)b * GK_MAX_PASSES + p] / 8192.0;
+            cum += wm;
+        }
+        P[p].dist = cum;
     }
     // flush the partial output word (bytes [bp & ~3, bp) plus the pending byte)
     if (q.bp >= 0 && (uint32_t)q.bp < q.cap) {
@@ -395,23 +456,29 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
         ps.len = ps.rate - prev;
         prev = ps.rate;
     }
-    info[3 * b] = numbps;
-    info[3 * b + 1] = npasses;
-    info[3 * b + 2] = P[npasses - 1].rate;
+    info[4 * b] = numbps;
+    info[4 * b + 1] = npasses;
+    info[4 * b + 2] = P[npasses - 1].rate;
+    info[4 * b + 3] = poff;
     if (q.ovf) atomicOr(err, 1);
 }
 
 #include "gk_launch.h"
 void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks, const uint64_t* sym_off, uint8_t* sym,
-                     uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err) {
+                     uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err, const int16_t* nmse_tab,
+                     int32_t* pass_nmse) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_t1_cm, dim3(nblocks), dim3(64), 0, st, coef, blocks, sym_off, sym, pass_end, cm_info, nblocks,
-                       err);
+    if (pass_nmse)
+        hipLaunchKernelGGL(k_t1_cm<true>, dim3(nblocks), dim3(64), 0, st, coef, blocks, sym_off, sym, pass_end, cm_info,
+                           nblocks, err, nmse_tab, pass_nmse);
+    else
+        hipLaunchKernelGGL(k_t1_cm<false>, dim3(nblocks), dim3(64), 0, st, coef, blocks, sym_off, sym, pass_end,
+                           cm_info, nblocks, err, nmse_tab, pass_nmse);
 }
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
-                     uint32_t nblocks, int* err) {
+                     uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter) {
     if (!nblocks) return;
     hipLaunchKernelGGL(k_t1_mq, dim3((nblocks + 63) / 64), dim3(64), 0, st, sym, sym_off, pass_end, cm_info, blocks,
-                       bytes, passes, info, nblocks, err);
+                       bytes, passes, info, nblocks, err, pass_nmse, pass_counter);
 }

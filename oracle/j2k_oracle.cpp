@@ -26,6 +26,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <functional>
 
 namespace orc {
 
@@ -44,6 +45,7 @@ struct Params {
     uint32_t numgbits = 2;
     uint32_t prcw_exp[33], prch_exp[33];  // per resolution
     uint32_t nlayers = 1;
+    double rates[100] = {0};    // grk_cparameters::layer_rate (compression ratios; 0 = all remaining passes)
     int write_com = 1;
     Params() { for (int i = 0; i < 33; ++i) { prcw_exp[i] = 15; prch_exp[i] = 15; } }
 };
@@ -63,6 +65,7 @@ struct Cblk {
     // T2 state
     uint32_t numlenbits = 0;
     uint32_t passes_in_prev = 0;  // passes included in previous layers (encoder)
+    std::vector<uint32_t> layer_np; // encoder: passes contributed to each layer (rate allocation)
     bool included_before = false;
     std::vector<uint32_t> seglens; // decoder: per segment lengths (one segment in default mode)
     std::vector<uint32_t> segpasses;
@@ -246,7 +249,8 @@ static void dc_rct_fwd(std::vector<std::vector<int32_t>>& planes, uint32_t prec,
     }
 }
 
-// ICT (mct.cpp:147-219): float result written into the int32 storage as float bits.
+// ICT (mct.cpp:147-219 CompressIrrev): y = a_r r + a_g g + a_b b, u = cb (b - y),
+// v = cr (r - y) in float, evaluated left to right without contraction.
 static void dc_ict_fwd(std::vector<std::vector<float>>& f, const std::vector<std::vector<int32_t>>& planes,
                        uint32_t prec, bool sgnd, bool mct) {
     int32_t shift = sgnd ? 0 : (1 << (prec - 1));
@@ -256,12 +260,15 @@ static void dc_ict_fwd(std::vector<std::vector<float>>& f, const std::vector<std
         for (size_t i = 0; i < planes[c].size(); ++i) f[c][i] = (float)(planes[c][i] - shift);
     }
     if (mct && planes.size() >= 3) {
+        const float a_r = 0.299f, a_g = 0.587f, a_b = 0.114f;
+        const float cb = 0.5f / (1.0f - a_b), cr = 0.5f / (1.0f - a_r);
         size_t n = f[0].size();
         for (size_t i = 0; i < n; ++i) {
             float r = f[0][i], g = f[1][i], b = f[2][i];
-            float y = 0.299f * r + 0.587f * g + 0.114f * b;
-            float u = -0.16875f * r - 0.331260f * g + 0.5f * b;
-            float v = 0.5f * r - 0.41869f * g - 0.08131f * b;
+            float t0 = a_r * r, t1 = a_g * g, t2 = a_b * b;
+            float y = (t0 + t1) + t2;
+            float u = cb * (b - y);
+            float v = cr * (r - y);
             f[0][i] = y; f[1][i] = u; f[2][i] = v;
         }
     }
@@ -313,7 +320,7 @@ static void inv53_1d(int32_t* x, uint32_t n, std::vector<int32_t>& tmp) {
 // WaveletReverse.cpp:882-1024, 1272-1351).  Float lifting.
 // ----------------------------------------------------------------------------
 static const float A97 = -1.586134342f, B97 = -0.052980118f, G97 = 0.882911075f, D97 = 0.443506852f;
-static const float K97 = 1.230174105f, INVK97 = 1.0f / 1.230174105f, TWO_INVK97 = 1.625732422f;
+static const float K97 = 1.230174105f, INVK97 = (float)(1.0 / 1.230174105), TWO_INVK97 = 1.625732422f;
 
 static void fwd97_1d(float* x, uint32_t n, std::vector<float>& tmp) {
     if (n < 2) return;
@@ -325,10 +332,10 @@ static void fwd97_1d(float* x, uint32_t n, std::vector<float>& tmp) {
         return x[i];
     };
     // work on a copy with lifting in place (odd = d, even = s)
-    for (int64_t i = 1; i < (int64_t)n; i += 2) x[i] += A97 * (X(i - 1) + X(i + 1));
-    for (int64_t i = 0; i < (int64_t)n; i += 2) x[i] += B97 * (X(i - 1) + X(i + 1));
-    for (int64_t i = 1; i < (int64_t)n; i += 2) x[i] += G97 * (X(i - 1) + X(i + 1));
-    for (int64_t i = 0; i < (int64_t)n; i += 2) x[i] += D97 * (X(i - 1) + X(i + 1));
+    auto lift = [&](int64_t start, float c) {
+        for (int64_t i = start; i < (int64_t)n; i += 2) { float t = (X(i - 1) + X(i + 1)) * c; x[i] = x[i] + t; }
+    };
+    lift(1, A97); lift(0, B97); lift(1, G97); lift(0, D97);
     for (uint32_t i = 0; i < sn; ++i) tmp[i] = x[2 * i] * INVK97;
     for (uint32_t i = 0; i < dn; ++i) tmp[sn + i] = x[2 * i + 1] * K97;
     memcpy(x, tmp.data(), n * sizeof(float));
@@ -962,40 +969,42 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
     }
 }
 
-// packet header + body for one (comp, res, precinct, layer), T2Compress.cpp:113-240
-static void encode_packet(std::vector<uint8_t>& o, Res& R, uint32_t pi, uint32_t layno,
-                          std::vector<std::vector<uint32_t>>& layer_np,  // unused placeholder
-                          std::vector<TagTree>& incl, std::vector<TagTree>& imsb,
-                          const std::vector<std::vector<std::vector<uint32_t>>>& npass_layer) {
-    (void)layer_np;
-    BitWriter bw; std::vector<uint8_t> hdr; bw.out = &hdr;
+// Packet header + body for one (comp, res, precinct, layer) (T2Compress.cpp:113-260,
+// compressPacket / compressPacketSimulate :262-430).  Block k contributes
+// K.layer_np[layno] passes.  With a byte budget, fails like Grok's bounded
+// BitIO (the header must stay below the budget) and body check.  Appends the
+// packet to *o when o is non-null.  Updates the per-block T2 state.
+struct PrecTrees { std::vector<TagTree> incl, imsb; };
+
+static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t layno, PrecTrees& T,
+                         uint64_t* budget) {
     if (layno == 0) {
         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
             Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
             if (B.empty() || P.cblks.empty()) continue;
-            incl[bi].reset(); imsb[bi].reset();
+            T.incl[bi].reset(); T.imsb[bi].reset();
             for (size_t k = 0; k < P.cblks.size(); ++k) {
                 P.cblks[k].passes_in_prev = 0;
-                imsb[bi].setvalue((uint32_t)k, B.numbps - P.cblks[k].numbps);
+                T.imsb[bi].setvalue((uint32_t)k, B.numbps - P.cblks[k].numbps);
             }
         }
     }
-    bw.write(1, 1);  // non-empty packet
+    BitWriter bw; std::vector<uint8_t> hdr; bw.out = &hdr;
+    bw.write(1, 1);  // non-empty packet (Grok always writes 1)
     for (size_t bi = 0; bi < R.bands.size(); ++bi) {
         Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
         if (B.empty() || P.cblks.empty()) continue;
-        const auto& nl = npass_layer[bi];
         for (size_t k = 0; k < P.cblks.size(); ++k) {
             Cblk& K = P.cblks[k];
-            if (!K.passes_in_prev && nl[k][layno]) incl[bi].setvalue((uint32_t)k, layno);
+            if (!K.passes_in_prev && K.layer_np[layno]) T.incl[bi].setvalue((uint32_t)k, layno);
         }
         for (size_t k = 0; k < P.cblks.size(); ++k) {
             Cblk& K = P.cblks[k];
-            uint32_t np = nl[k][layno];
-            if (!K.passes_in_prev) incl[bi].encode(bw, (uint32_t)k, layno + 1);
+            uint32_t np = K.layer_np[layno];
+            if (!K.passes_in_prev) T.incl[bi].encode(bw, (uint32_t)k, layno + 1);
             else bw.write(np != 0, 1);
             if (!np) continue;
-            if (!K.passes_in_prev) { K.numlenbits = 3; imsb[bi].encode(bw, (uint32_t)k, 0xffffffffu); }
+            if (!K.passes_in_prev) { K.numlenbits = 3; T.imsb[bi].encode(bw, (uint32_t)k, 0xffffffffu); }
             bw.numpasses(np);
             uint32_t first = K.passes_in_prev, last = first + np;
             int increment = 0; uint32_t len = 0, nump = 0;
@@ -1018,21 +1027,29 @@ static void encode_packet(std::vector<uint8_t>& o, Res& R, uint32_t pi, uint32_t
         }
     }
     bw.flush();
-    o.insert(o.end(), hdr.begin(), hdr.end());
+    if (budget) {
+        // BitIO::writeByte fails when the byte count reaches the budget (BitIO.cpp:35-52)
+        if ((uint64_t)hdr.size() >= *budget) return false;
+        *budget -= hdr.size();
+    }
+    if (o) o->insert(o->end(), hdr.begin(), hdr.end());
     for (size_t bi = 0; bi < R.bands.size(); ++bi) {   // packet body
         Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
         if (B.empty() || P.cblks.empty()) continue;
-        const auto& nl = npass_layer[bi];
-        for (size_t k = 0; k < P.cblks.size(); ++k) {
-            Cblk& K = P.cblks[k];
-            uint32_t np = nl[k][layno];
+        for (auto& K : P.cblks) {
+            uint32_t np = K.layer_np[layno];
             if (!np) continue;
             uint32_t r0 = K.passes_in_prev ? K.passes[K.passes_in_prev - 1].rate : 0;
             uint32_t r1 = K.passes[K.passes_in_prev + np - 1].rate;
-            o.insert(o.end(), K.data.begin() + r0, K.data.begin() + r1);
+            if (budget) {
+                if ((uint64_t)(r1 - r0) > *budget) return false;
+                *budget -= (r1 - r0);
+            }
+            if (o) o->insert(o->end(), K.data.begin() + r0, K.data.begin() + r1);
             K.passes_in_prev += np;
         }
     }
+    return true;
 }
 
 }  // namespace orc
@@ -1047,6 +1064,7 @@ extern "C" {
 typedef struct {
     uint32_t numres, cbw_exp, cbh_exp, irreversible, mct, nlayers, write_com;
     uint32_t prcw_exp[33], prch_exp[33];
+    double layer_rate[100];
 } orc_cparams;
 
 static Params to_params(const orc_cparams* cp) {
@@ -1055,6 +1073,7 @@ static Params to_params(const orc_cparams* cp) {
     p.numres = cp->numres; p.cbw_exp = cp->cbw_exp; p.cbh_exp = cp->cbh_exp;
     p.irreversible = cp->irreversible; p.mct = cp->mct; p.nlayers = cp->nlayers ? cp->nlayers : 1;
     p.write_com = (int)cp->write_com;
+    for (uint32_t i = 0; i < 100; ++i) p.rates[i] = i < p.nlayers ? cp->layer_rate[i] : 0.0;
     for (int i = 0; i < 33; ++i) { p.prcw_exp[i] = cp->prcw_exp[i] ? cp->prcw_exp[i] : 15; p.prch_exp[i] = cp->prch_exp[i] ? cp->prch_exp[i] : 15; }
     return p;
 }
@@ -1077,9 +1096,21 @@ struct EncodeState {
     Image im; Params p;
     std::vector<Comp> comps;
     std::vector<std::vector<int32_t>> coefs;   // reversible Mallat coefficients
+    std::vector<std::vector<float>> fcoefs;    // irreversible Mallat coefficients
+    size_t header_size = 0;
 };
 
+// Rate control is active when any layer has a target rate (TileProcessor.cpp:952-967).
+static bool needs_rate_control(const Params& p) {
+    for (uint32_t l = 0; l < p.nlayers; ++l) if (p.rates[l] > 0.0) return true;
+    return false;
+}
+
 static void t1_encode_all(EncodeState& E) {
+    const bool rc = needs_rate_control(E.p);
+    static const double norms_irrev[3] = {1.732, 1.805, 1.573};   // mct.cpp:689-704
+    static const double norms_rev[3] = {1.732, .8292, .8292};
+    const bool mct = E.p.mct && E.im.nc >= 3;
     for (uint32_t c = 0; c < E.im.nc; ++c) {
         Comp& C = E.comps[c];
         for (uint32_t r = 0; r < E.p.numres; ++r)
@@ -1090,13 +1121,20 @@ static void t1_encode_all(EncodeState& E) {
                         std::vector<uint32_t> mag(w * h); std::vector<uint8_t> neg(w * h);
                         for (uint32_t y = 0; y < h; ++y)
                             for (uint32_t x = 0; x < w; ++x) {
-                                int32_t v = E.coefs[c][(size_t)(B.offy + K.y0 - B.y0 + y) * C.w + (B.offx + K.x0 - B.x0 + x)];
-                                int64_t s = (int64_t)v * (1 << FRACBITS);
-                                neg[y * w + x] = s < 0;
-                                mag[y * w + x] = (uint32_t)(s < 0 ? -s : s);
+                                size_t o = (size_t)(B.offy + K.y0 - B.y0 + y) * C.w + (B.offx + K.x0 - B.x0 + x);
+                                int64_t sv;
+                                if (!E.p.irreversible) sv = (int64_t)E.coefs[c][o] * (1 << FRACBITS);
+                                else {   // T1Part1::preCompress (T1Part1.cpp:70-86)
+                                    float q = (E.fcoefs[c][o] / B.stepsize) * (float)(1 << FRACBITS);
+                                    sv = (int64_t)lrintf(q);
+                                }
+                                neg[y * w + x] = sv < 0;
+                                mag[y * w + x] = (uint32_t)(sv < 0 ? -sv : sv);
                             }
+                        DistCtx dc{c, E.p.numres - 1 - r, B.orient, E.p.irreversible ? 0u : 1u, (double)B.stepsize,
+                                   mct ? (E.p.irreversible ? norms_irrev : norms_rev) : nullptr, mct ? 3u : E.im.nc};
                         BlockEncResult res;
-                        t1_encode_block(mag.data(), neg.data(), w, h, B.orient, res, nullptr);
+                        t1_encode_block(mag.data(), neg.data(), w, h, B.orient, res, rc ? &dc : nullptr);
                         K.numbps = res.numbps; K.npasses = res.npasses; K.data = res.data; K.passes = res.passes;
                     }
     }
@@ -1111,28 +1149,55 @@ static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, ui
     for (uint32_t c = 0; c < nc; ++c) { build_geometry(E.comps[c], w, h, E.p); assign_steps(E.comps[c], E.p, prec, true, nullptr); }
     E.coefs.assign(nc, {});
     for (uint32_t c = 0; c < nc; ++c) E.coefs[c].assign(planes + (size_t)c * w * h, planes + (size_t)(c + 1) * w * h);
-    dc_rct_fwd(E.coefs, prec, sgnd != 0, E.p.mct != 0);
-    for (uint32_t c = 0; c < nc; ++c)
-        dwt2d<int32_t>(E.coefs[c].data(), w, E.comps[c], E.p.numres, true, fwd53_1d);
+    if (!E.p.irreversible) {
+        dc_rct_fwd(E.coefs, prec, sgnd != 0, E.p.mct != 0);
+        for (uint32_t c = 0; c < nc; ++c)
+            dwt2d<int32_t>(E.coefs[c].data(), w, E.comps[c], E.p.numres, true, fwd53_1d);
+    } else {
+        dc_ict_fwd(E.fcoefs, E.coefs, prec, sgnd != 0, E.p.mct != 0);
+        for (uint32_t c = 0; c < nc; ++c)
+            dwt2d<float>(E.fcoefs[c].data(), w, E.comps[c], E.p.numres, true, fwd97_1d);
+    }
 }
 
-static std::vector<uint8_t> assemble(EncodeState& E) {
-    std::vector<uint8_t> o;
-    write_main_header(o, E.im, E.p, E.comps[0]);
-    size_t sot = o.size();
-    put16(o, 0xff90); put16(o, 10); put16(o, 0); put32(o, 0); o.push_back(0); o.push_back(1);
-    put16(o, 0xff93);
-    // layer assignment: single layer, all passes (makeLayerFinal, TileProcessor.cpp:1460-1515)
-    // tag trees per (comp, res, band, precinct)
-    struct TT { std::vector<TagTree> incl, imsb; };
-    std::vector<std::vector<std::vector<TT>>> trees(E.im.nc);
+// ---------------------------------------------------------------------------
+// Layer formation and PCRD rate control (TileProcessor.cpp:1196-1515,
+// pcrdBisectSimple / makeLayerSimple / makeLayerFinal; rates from
+// CodeStreamCompress::updateRates :951-1025; T2 simulation
+// T2Compress.cpp:59-112, 114-260, 347-430).
+// ---------------------------------------------------------------------------
+static void for_blocks(EncodeState& E, const std::function<void(Cblk&)>& f) {
+    for (uint32_t c = 0; c < E.im.nc; ++c)
+        for (uint32_t r = 0; r < E.p.numres; ++r)
+            for (auto& B : E.comps[c].res[r].bands)
+                for (auto& P : B.prcs)
+                    for (auto& K : P.cblks) f(K);
+}
+
+// Passes included up to threshold `thresh` (makeLayerSimple's per-block rule).
+static uint32_t included_passes(const Cblk& K, uint32_t prev, double thresh) {
+    if (thresh == 0) return K.npasses;
+    uint32_t inc = prev;
+    for (uint32_t q = prev; q < K.npasses; ++q) {
+        uint32_t dr; double dd;
+        if (inc == 0) { dr = K.passes[q].rate; dd = K.passes[q].dist; }
+        else { dr = K.passes[q].rate - K.passes[inc - 1].rate; dd = K.passes[q].dist - K.passes[inc - 1].dist; }
+        if (!dr) { if (dd != 0) inc = q + 1; continue; }
+        double slope = dd / dr;
+        if (thresh - slope < 2.220446049250313e-16) inc = q + 1;
+    }
+    return inc;
+}
+
+static std::vector<std::vector<std::vector<PrecTrees>>> make_trees(EncodeState& E) {
+    std::vector<std::vector<std::vector<PrecTrees>>> trees(E.im.nc);
     for (uint32_t c = 0; c < E.im.nc; ++c) {
         trees[c].resize(E.p.numres);
         for (uint32_t r = 0; r < E.p.numres; ++r) {
             Res& R = E.comps[c].res[r];
             trees[c][r].resize(R.pw * R.ph);
             for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                TT& t = trees[c][r][pi];
+                PrecTrees& t = trees[c][r][pi];
                 t.incl.resize(R.bands.size()); t.imsb.resize(R.bands.size());
                 for (size_t bi = 0; bi < R.bands.size(); ++bi) {
                     Precinct& P = R.bands[bi].prcs[pi];
@@ -1141,23 +1206,113 @@ static std::vector<uint8_t> assemble(EncodeState& E) {
             }
         }
     }
+    return trees;
+}
+
+// T2Compress::compressPacketsSimulate: do layers [0, max_layers) fit in max_bytes?
+static bool simulate(EncodeState& E, uint32_t max_layers, uint64_t max_bytes) {
+    auto trees = make_trees(E);
+    uint64_t budget = max_bytes;
+    uint64_t* bp = (max_bytes == 0xffffffffull) ? nullptr : &budget;
+    for (uint32_t l = 0; l < max_layers; ++l)
+        for (uint32_t r = 0; r < E.p.numres; ++r)
+            for (uint32_t c = 0; c < E.im.nc; ++c) {
+                Res& R = E.comps[c].res[r];
+                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi)
+                    if (!write_packet(nullptr, R, pi, l, trees[c][r][pi], bp)) return false;
+            }
+    return true;
+}
+
+// makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0)
+static void make_layer(EncodeState& E, uint32_t layno, double thresh, bool final_attempt,
+                       std::vector<uint32_t>& prev) {
+    size_t i = 0;
+    for_blocks(E, [&](Cblk& K) {
+        if (layno == 0) prev[i] = 0;
+        uint32_t inc = thresh < 0 ? std::max(prev[i], K.npasses) : included_passes(K, prev[i], thresh);
+        K.layer_np[layno] = inc - prev[i];
+        if (final_attempt) prev[i] = inc;
+        ++i;
+    });
+}
+
+// CodeStreamCompress::updateRates: compression ratios -> cumulative byte budgets
+static void update_rates(const EncodeState& E, double* rates) {
+    const Params& p = E.p;
+    double size_pixel = (double)E.im.nc * E.im.prec, npix = (double)E.im.w * E.im.h, bits_empty = 8.0;
+    for (uint32_t k = 0; k < p.nlayers; ++k)
+        rates[k] = p.rates[k] > 0.0 ? (size_pixel * npix) / (p.rates[k] * bits_empty) : 0.0;
+    double sot_adjust = (npix * (double)E.header_size) / npix;
+    uint32_t k = 0;
+    if (rates[0] > 0.0) { rates[0] -= sot_adjust; if (rates[0] < 30.0f) rates[0] = 30.0f; }
+    for (k = 1; k + 1 < p.nlayers; ++k)
+        if (rates[k] > 0.0) { rates[k] -= sot_adjust; if (rates[k] < rates[k - 1] + 10.0) rates[k] = rates[k - 1] + 20.0; }
+    k = std::max(1u, p.nlayers - 1);
+    if (p.nlayers > 1 && rates[k] > 0.0) {
+        rates[k] -= (sot_adjust + 2.0);
+        if (rates[k] < rates[k - 1] + 10.0) rates[k] = rates[k - 1] + 20.0;
+    }
+}
+
+// TileProcessor::pcrdBisectSimple
+static void rate_allocate(EncodeState& E) {
+    size_t nb = 0;
+    for_blocks(E, [&](Cblk& K) { K.layer_np.assign(E.p.nlayers, 0); ++nb; });
+    std::vector<uint32_t> prev(nb, 0);
+    if (!needs_rate_control(E.p)) {
+        for (uint32_t l = 0; l < E.p.nlayers; ++l) make_layer(E, l, -1.0, true, prev);
+        return;
+    }
+    double rates[100];
+    update_rates(E, rates);
+    double min_slope = 1.7976931348623157e308, max_slope = -1;
+    for_blocks(E, [&](Cblk& K) {
+        for (uint32_t q = 0; q < K.npasses; ++q) {
+            int32_t dr; double dd;
+            if (q == 0) { dr = (int32_t)K.passes[q].rate; dd = K.passes[q].dist; }
+            else { dr = (int32_t)(K.passes[q].rate - K.passes[q - 1].rate); dd = K.passes[q].dist - K.passes[q - 1].dist; }
+            if (dr == 0) continue;
+            double sl = dd / dr;
+            min_slope = std::min(min_slope, sl); max_slope = std::max(max_slope, sl);
+        }
+    });
+    double upper = max_slope;
+    for (uint32_t l = 0; l < E.p.nlayers; ++l) {
+        uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
+        if (rates[l] > 0.0) {
+            double lower = min_slope, prevthresh = -1, thresh = 0;
+            for (uint32_t it = 0; it < 128; ++it) {
+                thresh = (upper == -1) ? lower : (lower + upper) / 2;
+                make_layer(E, l, thresh, false, prev);
+                if (prevthresh != -1 && fabs(prevthresh - thresh) < 0.001) break;
+                prevthresh = thresh;
+                if (!simulate(E, l + 1, max_len)) { lower = thresh; continue; }
+                upper = thresh;
+            }
+            double good = (upper == -1) ? thresh : upper;
+            make_layer(E, l, good, true, prev);
+            upper = lower - 1;
+        } else {
+            make_layer(E, l, -1.0, true, prev);
+        }
+    }
+}
+
+static std::vector<uint8_t> assemble(EncodeState& E) {
+    std::vector<uint8_t> o;
+    write_main_header(o, E.im, E.p, E.comps[0]);
+    E.header_size = o.size();
+    rate_allocate(E);
+    size_t sot = o.size();
+    put16(o, 0xff90); put16(o, 10); put16(o, 0); put32(o, 0); o.push_back(0); o.push_back(1);
+    put16(o, 0xff93);
+    auto trees = make_trees(E);
     for (uint32_t l = 0; l < E.p.nlayers; ++l)
         for (uint32_t r = 0; r < E.p.numres; ++r)
             for (uint32_t c = 0; c < E.im.nc; ++c) {
                 Res& R = E.comps[c].res[r];
-                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                    std::vector<std::vector<std::vector<uint32_t>>> npl(R.bands.size());
-                    for (size_t bi = 0; bi < R.bands.size(); ++bi) {
-                        Precinct& P = R.bands[bi].prcs[pi];
-                        npl[bi].resize(P.cblks.size());
-                        for (size_t k = 0; k < P.cblks.size(); ++k) {
-                            npl[bi][k].assign(E.p.nlayers, 0);
-                            npl[bi][k][0] = P.cblks[k].npasses;   // single lossless layer
-                        }
-                    }
-                    std::vector<std::vector<uint32_t>> dummy;
-                    encode_packet(o, R, pi, l, dummy, trees[c][r][pi].incl, trees[c][r][pi].imsb, npl);
-                }
+                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) write_packet(&o, R, pi, l, trees[c][r][pi], nullptr);
             }
     uint32_t psot = (uint32_t)(o.size() - sot);
     o[sot + 6] = (uint8_t)(psot >> 24); o[sot + 7] = (uint8_t)(psot >> 16); o[sot + 8] = (uint8_t)(psot >> 8); o[sot + 9] = (uint8_t)psot;
@@ -1165,13 +1320,12 @@ static std::vector<uint8_t> assemble(EncodeState& E) {
     return o;
 }
 
-// Full encode (5/3 lossless, single layer).  Returns the codestream size, or
-// 0 on failure / insufficient capacity (size still returned in *needed).
+// Full encode (5/3 or 9/7, any number of layers).  Returns the codestream
+// size, or 0 on failure / insufficient capacity.
 size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
                   const orc_cparams* cp, uint8_t* out, size_t cap) {
     EncodeState E;
     prepare_encode(E, planes, w, h, nc, prec, sgnd, cp);
-    if (E.p.irreversible) return 0;   // 9/7 encode: not in the oracle yet
     t1_encode_all(E);
     std::vector<uint8_t> o = assemble(E);
     if (o.size() > cap) return 0;

@@ -20,6 +20,7 @@ class CParams(ctypes.Structure):
         ("irreversible", ctypes.c_uint32), ("mct", ctypes.c_uint32), ("nlayers", ctypes.c_uint32),
         ("write_com", ctypes.c_uint32),
         ("prcw_exp", ctypes.c_uint32 * 33), ("prch_exp", ctypes.c_uint32 * 33),
+        ("layer_rate", ctypes.c_double * 100),
     ]
 
 
@@ -60,7 +61,8 @@ def lib():
     return _lib
 
 
-def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None):
+def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
+           layer_rate=None):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -70,6 +72,10 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
     p.mct = int(mct)
     p.nlayers = nlayers
     p.write_com = int(write_com)
+    if layer_rate:
+        p.nlayers = len(layer_rate)
+        for i, r in enumerate(layer_rate):
+            p.layer_rate[i] = r
     if precincts:
         # Grok CLI semantics: list of (w, h) from the highest resolution down; the last repeats
         exps = [(int(w).bit_length() - 1, int(h).bit_length() - 1) for (w, h) in precincts]

@@ -50,3 +50,29 @@ def test_fullsize_lossless_bit_exact(eng, name):
     eng.decode(out, length=n, out=y)
     torch.cuda.synchronize()
     assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("name", ["C3_l1", "C3_4k", "C3p"])
+def test_fullsize_97_vs_grok(eng, name):
+    """9/7 + ICT (+ PCRD layers): codestream SHA-256 equal to Grok's; our decode
+    within the stated tolerance of Grok's decode PSNR."""
+    import torch
+    import grok_amd as G
+    from conftest import parse_flags
+    cfg = FULL[name]
+    img = _img(cfg)
+    kw = parse_flags(cfg["flags"])
+    params = G.default_params(irreversible=True, precincts=kw.get("precincts"), layer_rate=kw.get("layer_rate"),
+                              numlayers=len(kw.get("layer_rate") or [0]))
+    x = torch.from_numpy(img).cuda()
+    out = torch.empty(img.nbytes + (1 << 24), dtype=torch.uint8, device="cuda")
+    n = eng.encode(x, cfg["bits"], params=params, out=out)
+    cs = out[:n].cpu().numpy().tobytes()
+    assert abs(n - cfg["bytes"]) <= 0.01 * cfg["bytes"]
+    assert hashlib.sha256(cs).hexdigest() == cfg["sha256"]
+    y = torch.empty_like(x)
+    eng.decode(out, length=n, out=y)
+    dec = y.cpu().numpy().astype(np.float64)
+    mse = np.mean((dec - img) ** 2)
+    psnr = 10 * np.log10(((1 << cfg["bits"]) - 1) ** 2 / mse)
+    assert abs(psnr - cfg["grok_psnr_db"]) <= 0.1

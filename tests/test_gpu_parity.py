@@ -14,6 +14,9 @@ import oracle as O
 pytestmark = pytest.mark.gpu
 
 PART1_LOSSLESS = [f for f in FIXTURES if f.lossless and not f.ht]
+PART1_LOSSY = [f for f in FIXTURES if not f.lossless and not f.ht]
+# 9/7 decode tolerance vs Grok's own decode: max-abs <= 1 LSB
+TOL_97_MAXABS = 1
 
 
 @pytest.fixture(scope="module")
@@ -138,3 +141,68 @@ def test_corrupt_stream_raises(eng):
         eng.decode(b"\x00\x01garbage")
     with pytest.raises(RuntimeError):
         eng.decode(fx.cs[:40])
+
+
+# ---------------------------------------------------------------- 9/7 + ICT
+@pytest.mark.parametrize("fx", PART1_LOSSY, ids=fixture_ids(PART1_LOSSY))
+def test_encode_97_bit_exact_vs_grok(eng, fx):
+    # Grok's float lifting order and PCRD rate allocation are reproduced exactly
+    cs = eng.encode(fx.img, fx.bits, params=gk_params(fx.kw))
+    assert len(cs) == len(fx.cs)
+    assert cs == fx.cs
+
+
+@pytest.mark.parametrize("fx", PART1_LOSSY, ids=fixture_ids(PART1_LOSSY))
+def test_decode_97_grok_stream_within_tolerance(eng, fx):
+    dec = eng.decode(fx.cs)
+    err = np.abs(dec.astype(np.int64) - fx.grok_decoded).max()
+    assert err <= TOL_97_MAXABS
+
+
+def _rand_97(seed):
+    rng = np.random.default_rng(100 + seed)
+    from grok_amd.synth import synth_image
+    c = int(rng.choice([1, 3]))
+    bits = int(rng.choice([8, 12]))
+    h, w = int(rng.integers(8, 400)), int(rng.integers(8, 400))
+    img = synth_image(h, w, c, bits, seed).astype(np.int32)
+    kw = {"numres": int(rng.integers(2, 7)), "cblk": [(64, 64), (32, 32), (16, 64)][seed % 3], "irreversible": True}
+    if seed % 2:
+        kw["layer_rate"] = [[40.0, 20.0, 10.0], [30.0, 8.0], [12.0], [50.0, 25.0, 12.0, 0.0]][seed % 4]
+    return img, bits, kw
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_97_vs_oracle(eng, seed):
+    img, bits, kw = _rand_97(seed)
+    if img.shape[0] == 1:
+        pytest.skip("mono 9/7: Grok's path is broken (R-BUG-1); covered by test_mono_97_quality")
+    ref = O.encode(img, bits, **kw)
+    cs = eng.encode(img, bits, params=gk_params(kw))
+    assert cs == ref
+    dref, _ = O.decode(ref)
+    assert np.abs(eng.decode(ref).astype(np.int64) - dref).max() <= TOL_97_MAXABS
+
+
+def test_mono_97_quality(eng):
+    # standard-correct mono 9/7 (Grok's own output is ~16 dB, R-BUG-1): check the
+    # round trip against the source image
+    from grok_amd.synth import synth_image
+    img = synth_image(300, 260, 1, 12, 4).astype(np.int32)
+    cs = eng.encode(img, 12, params=gk_params({"irreversible": True}))
+    dec = eng.decode(cs)
+    mse = np.mean((dec.astype(np.float64) - img) ** 2)
+    assert 10 * np.log10(4095.0 ** 2 / mse) > 60.0
+    dref, _ = O.decode(cs)   # the oracle decodes our stream to the same samples (+-1)
+    assert np.abs(dec.astype(np.int64) - dref).max() <= TOL_97_MAXABS
+
+
+@pytest.mark.parametrize("rates", [[20.0, 5.0, 0.0], [8.0], [40.0, 20.0, 10.0, 4.0, 2.0]])
+def test_lossless_layers_vs_oracle(eng, rates):
+    from grok_amd.synth import synth_image
+    img = synth_image(200, 300, 3, 8, 9).astype(np.int32)
+    kw = {"layer_rate": rates}
+    ref = O.encode(img, 8, **kw)
+    assert eng.encode(img, 8, params=gk_params(kw)) == ref
+    dec, _ = O.decode(ref)
+    np.testing.assert_array_equal(eng.decode(ref), dec)
