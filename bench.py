@@ -1,19 +1,23 @@
 """Benchmark: Mpixels/s encode+decode, JPEG 2000 tile pipeline on MI355X.
 
-Workload (BASELINE.json configs[1], "C2"): 8192x8192 8-bit RGB, 5/3 reversible
-lossless + RCT, 64x64 code-blocks, 6 resolutions, single tile, one quality
-layer — Grok's default coding parameters.  Synthetic input from the survey's
-seeded generator (grok_amd/synth.py, seed 10).
+Headline workload (BASELINE.json configs[1], "C2"): 8192x8192 8-bit RGB, 5/3
+reversible lossless + RCT, 64x64 code-blocks, 6 resolutions, single tile, one
+quality layer — Grok's default coding parameters.  Synthetic input from the
+survey's seeded generator (grok_amd/synth.py, seed 10 + rank).
 
 One step = encode (image resident in HBM -> codestream resident in HBM) +
-decode (codestream in HBM -> image in HBM), with the host doing T2 packet
-headers from per-block metadata.  value = pixels of all ranks / max-over-ranks
+decode (codestream in HBM -> image in HBM); host T2 (packet headers, rate
+allocation) runs inside the step.  value = pixels of all ranks / max-over-ranks
 wall time.  Single-tile configs shard as replicas (one image per GPU, no
-collective): scaling = "weak".
+collective on the data path): scaling = "weak".
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+The same JSON line carries an auxiliary measurement of configs[2] ("C3":
+8192x8192 12-bit RGB, 9/7 + ICT, 3 quality layers -r 40,20,10).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3] [--no-aux]
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -21,9 +25,18 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
+
+CONFIGS = {
+    "C2": dict(bits=8, seed=10, params=dict(), desc="8192x8192 8-bit RGB, 5/3 lossless + RCT, 64x64 code-blocks, "
+                                                   "6 resolutions, single tile, 1 layer"),
+    "C3": dict(bits=12, seed=11, params=dict(irreversible=True, layer_rate=[40.0, 20.0, 10.0]),
+               desc="8192x8192 12-bit RGB, 9/7 + ICT, 64x64 code-blocks, 6 resolutions, single tile, "
+                    "3 layers -r 40,20,10 (PCRD)"),
+}
 
 
 def parse():
@@ -32,26 +45,113 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-aux", action="store_true", help="skip the auxiliary C3 measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1024, help="side of the CPU-baseline crop")
+    ap.add_argument("--cpu-sample", type=int, default=2048, help="side of the CPU-baseline crop")
     return ap.parse_args()
 
 
-def cpu_baseline(img, side):
-    """Oracle (CPU restatement, bit-exact with Grok) on a bounded crop, 1 thread."""
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle"))
+def cpu_baseline(img, bits, side, params):
+    """The oracle (CPU restatement, byte-exact with Grok), one thread, on a bounded crop."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     crop = np.ascontiguousarray(img[:, :side, :side]).astype(np.int32)
+    kw = {}
+    if params.get("irreversible"):
+        kw = dict(irreversible=True, layer_rate=params.get("layer_rate"))
     t0 = time.perf_counter()
-    cs = O.encode(crop, 8)
+    cs = O.encode(crop, bits, **kw)
     t1 = time.perf_counter()
     dec, _ = O.decode(cs)
     t2 = time.perf_counter()
-    assert (dec == crop).all()
+    if not kw:
+        assert (dec == crop).all()
     mpix = side * side / 1e6
-    return {"value": mpix / (t2 - t0), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": "%dx%d RGB8 crop of the C2 image, oracle enc %.2fs + dec %.2fs, 1 thread" % (
+    return {"value": round(mpix / (t2 - t0), 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": "%dx%d crop of the same image, oracle/j2k_oracle.cpp encode %.2fs + decode %.2fs, 1 thread" % (
                 side, side, t1 - t0, t2 - t1)}
+
+
+def pmc_traffic(kernels):
+    """HBM bytes per launch of `kernels` from the newest committed PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py from rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this benchmark; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md's gfx950 note).  None if no summary exists."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    tot = 0.0
+    for k in kernels:
+        if k not in d:
+            return None
+        tot += d[k]["hbm_bytes_per_launch"]
+    return tot
+
+
+class Runner:
+    def __init__(self, name, size, rank, device):
+        import torch
+        import grok_amd as G
+        from grok_amd.synth import synth_image
+        cfg = CONFIGS[name]
+        self.name, self.cfg, self.size = name, cfg, size
+        self.img = synth_image(size, size, 3, cfg["bits"], cfg["seed"] + rank)
+        self.x = torch.from_numpy(self.img.astype(np.int32)).to(device).contiguous()
+        self.out = torch.empty(self.x.numel() * 4 + (1 << 24), dtype=torch.uint8, device=device)
+        self.y = torch.empty_like(self.x)
+        self.eng = G.Engine(device.index or 0)
+        self.params = G.default_params(**cfg["params"])
+        self.n = 0
+
+    def step(self):
+        self.n = self.eng.encode(self.x, self.cfg["bits"], params=self.params, out=self.out)
+        te = self.eng.timings()
+        self.eng.decode(self.out, length=self.n, out=self.y)
+        td = self.eng.timings()
+        return te, td
+
+    def check(self):
+        import torch
+        self.step()
+        torch.cuda.synchronize()
+        if "irreversible" not in self.cfg["params"]:
+            if not torch.equal(self.x, self.y):
+                raise SystemExit("lossless round trip FAILED (%s)" % self.name)
+        else:
+            d = (self.y - self.x).double()
+            mse = float((d * d).mean())
+            psnr = 10 * np.log10(((1 << self.cfg["bits"]) - 1) ** 2 / mse)
+            if psnr < 30.0:
+                raise SystemExit("9/7 round trip PSNR %.2f dB too low (%s)" % (psnr, self.name))
+            return psnr
+        return None
+
+
+def timed(r, steps, warmup, world, dist, device):
+    import torch
+    for _ in range(warmup):
+        r.step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acc = {}
+    for _ in range(steps):
+        te, td = r.step()
+        for pre, t in (("enc", te), ("dec", td)):
+            for f, _ in t._fields_:
+                acc[pre + "_" + f] = acc.get(pre + "_" + f, 0.0) + float(getattr(t, f))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, {k: v / steps for k, v in acc.items()}
 
 
 def main():
@@ -65,76 +165,70 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
-    import grok_amd as G
-    from grok_amd.synth import synth_image
+    device = torch.device("cuda", local)
 
     S = args.size
-    img = synth_image(S, S, 3, 8, 10 + rank)          # one independent image per rank (replicas)
-    x = torch.from_numpy(img.astype(np.int32)).to(f"cuda:{local}").contiguous()
-    out_cs = torch.empty(3 * S * S * 4 + (1 << 24), dtype=torch.uint8, device=f"cuda:{local}")
-    y = torch.empty_like(x)
-    eng = G.Engine(local)
-    params = G.default_params()
-
-    def step():
-        n = eng.encode(x, 8, params=params, out=out_cs)
-        te = eng.timings()
-        eng.decode(out_cs, length=n, out=y)
-        td = eng.timings()
-        return n, te, td
-
-    # correctness gate before timing
-    n, te, td = step()
-    torch.cuda.synchronize()
-    if not torch.equal(x, y):
-        raise SystemExit("lossless round trip FAILED on rank %d" % rank)
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    dwt_ms, dwt_bytes, t1e, t1d = 0.0, 0, 0.0, 0.0
-    for _ in range(args.steps):
-        n, te, td = step()
-        dwt_ms += te.dwt_ms + td.dwt_ms
-        dwt_bytes += te.dwt_bytes + td.dwt_bytes
-        t1e += te.t1_ms
-        t1d += td.t1_ms
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    r = Runner(args.config, S, rank, device)
+    r.check()
+    el, m = timed(r, args.steps, args.warmup, world, dist, device)
     ms = el * 1000.0 / args.steps
-    mpix = S * S / 1e6
-    value = mpix * world * args.steps / el
+    samples = S * S * 3
+    value = S * S / 1e6 * world * args.steps / el
+
+    aux = None
+    if not args.no_aux and args.config == "C2":
+        r3 = Runner("C3", S, rank, device)
+        psnr = r3.check()
+        el3, m3 = timed(r3, 2, 1, world, dist, device)
+        aux = {"config": "C3: " + CONFIGS["C3"]["desc"], "value": round(S * S / 1e6 * world * 2 / el3, 3),
+               "unit": "Mpixels/s", "ms_per_step": round(el3 * 500.0, 3), "psnr_db": round(psnr, 3),
+               "codestream_bytes": int(r3.n),
+               "stages_ms": {k: round(v, 3) for k, v in m3.items() if k.endswith("_ms") and v > 0}}
+        r3.eng.close()
+
     if rank == 0:
-        achieved = (dwt_bytes / 1e9) / (dwt_ms / 1e3) if dwt_ms > 0 else 0.0
+        # dominant kernel: the T1 stage with the largest average duration, measured with HIP
+        # events on the engine stream (encode: k_t1_cm + k_t1_mq, decode: k_t1_dec + k_t1_recon)
+        stages = {
+            "T1 decode (k_t1_dec + k_t1_recon)": (m["dec_t1_ms"], m["dec_t1_bytes"] + 4.0 * samples,
+                                                  ["k_t1_dec", "k_t1_recon"]),
+            "T1 encode (k_t1_cm + k_t1_mq)": (m["enc_t1_ms"], 4.0 * samples + m["enc_t1_bytes"],
+                                              ["k_t1_cm", "k_t1_mq"]),
+            "DWT 5/3 fwd+inv (all levels)": (m["enc_dwt_ms"] + m["dec_dwt_ms"], m["enc_dwt_bytes"] + m["dec_dwt_bytes"],
+                                             ["k_dwt53_fwd_level", "k_dwt53_inv_level"]),
+        }
+        dom = max(stages, key=lambda k: stages[k][0])
+        t_ms, nbytes, kern = stages[dom]
+        achieved = nbytes / 1e9 / (t_ms / 1e3)
+        traffic = pmc_traffic(kern)
+        dwt_gbs = (m["enc_dwt_bytes"] + m["dec_dwt_bytes"]) / 1e9 / ((m["enc_dwt_ms"] + m["dec_dwt_ms"]) / 1e3)
         res = {
             "metric": "Mpixels/s encode+decode, 8K RGB 5/3 lossless + 9/7 lossy, 1/2/4/8 GPU",
             "value": round(value, 3), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int32", "data": "synthetic (seeded survey generator, seed 10+rank)",
-            "config": {"workload": "C2: %dx%d 8-bit RGB, 5/3 lossless + RCT, 64x64 code-blocks, 6 resolutions, "
-                                   "single tile, 1 layer; encode+decode, image and codestream resident in HBM" % (S, S),
-                       "parallelism": "replicas x%d" % world, "codestream_bytes": int(n)},
-            "roofline": {"bound": "hbm", "kernel": "k_dwt53_fwd_level + k_dwt53_inv_level (all levels)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
-            "stages_ms": {"enc_mct": round(te.mct_ms, 3), "enc_dwt": round(te.dwt_ms, 3), "enc_t1": round(te.t1_ms, 3), "enc_t1_cm": round(te.t1_cm_ms, 3),
-                          "enc_t2_host": round(te.t2_ms, 3), "enc_assemble": round(te.assemble_ms, 3),
-                          "dec_t2_host": round(td.t2_ms, 3), "dec_t1": round(td.t1_ms, 3), "dec_dwt": round(td.dwt_ms, 3),
-                          "dec_mct": round(td.mct_ms, 3)},
-            "t1": {"blocks": te.t1_blocks, "enc_blocks_per_s": round(te.t1_blocks / (t1e / args.steps / 1e3), 1),
-                   "dec_blocks_per_s": round(td.t1_blocks / (t1d / args.steps / 1e3), 1)},
+            "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic (seeded survey generator grok_amd/synth.py, seed %d+rank)" % r.cfg["seed"],
+            "config": {"workload": "%s: %s; encode+decode, image and codestream resident in HBM" % (
+                args.config, r.cfg["desc"]), "parallelism": "replicas x%d (one image per GPU)" % world,
+                "codestream_bytes": int(r.n)},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": None if traffic is None else round(traffic),
+                         "bytes_per_launch": round(nbytes), "avg_ms": round(t_ms, 3),
+                         "note": "T1 is a serial MQ chain per code-block; bytes = compressed bytes + 4 B/sample"},
+            "dwt_roofline": {"achieved": round(dwt_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(dwt_gbs / HBM_PEAK_GBS, 4), "bytes_per_sample": 10.656},
+            "stages_ms": {k: round(v, 3) for k, v in m.items() if k.endswith("_ms") and v > 0},
+            "t1": {"blocks": int(m["enc_t1_blocks"]),
+                   "enc_blocks_per_s": round(m["enc_t1_blocks"] / (m["enc_t1_ms"] / 1e3)),
+                   "dec_blocks_per_s": round(m["dec_t1_blocks"] / (m["dec_t1_ms"] / 1e3))},
         }
+        if aux:
+            res["aux"] = aux
         if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(img, args.cpu_sample)
+            res["cpu_baseline"] = cpu_baseline(r.img, r.cfg["bits"], min(args.cpu_sample, S), r.cfg["params"])
         print(json.dumps(res), flush=True)
+    r.eng.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -45,8 +45,9 @@ class ImageInfo(ctypes.Structure):
 
 class Timings(ctypes.Structure):
     _fields_ = [(n, ctypes.c_float) for n in ("mct_ms", "dwt_ms", "t1_ms", "t2_ms", "assemble_ms", "total_ms",
-                                              "t1_cm_ms")] + \
-               [("dwt_launches", ctypes.c_uint32), ("t1_blocks", ctypes.c_uint32), ("dwt_bytes", ctypes.c_uint64)]
+                                              "t1_cm_ms", "t1_coder_ms")] + \
+               [("dwt_launches", ctypes.c_uint32), ("t1_blocks", ctypes.c_uint32)] + \
+               [(n, ctypes.c_uint64) for n in ("dwt_bytes", "cs_bytes", "t1_bytes")]
 
 
 _lib = None

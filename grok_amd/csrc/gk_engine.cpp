@@ -951,6 +951,13 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     ctx->tm.dwt_ms = ev_ms(ctx, 2, 3);
     ctx->tm.t1_ms = ev_ms(ctx, 3, 4);
     ctx->tm.t1_cm_ms = ev_ms(ctx, 3, 8);
+    ctx->tm.t1_coder_ms = ev_ms(ctx, 8, 4);
+    ctx->tm.cs_bytes = total;
+    {
+        uint64_t tb = 0;
+        for (uint32_t b = 0; b < nb; ++b) tb += hinfo[4 * (size_t)b + 2];
+        ctx->tm.t1_bytes = tb;
+    }
     ctx->tm.t2_ms = ev_ms(ctx, 4, 5);
     ctx->tm.assemble_ms = ev_ms(ctx, 5, 7);
     ctx->tm.total_ms = ev_ms(ctx, 0, 7);
@@ -1137,12 +1144,13 @@ t2done:
     // (the T1 decoder reads its bytes through aligned 8-byte windows)
     std::vector<uint64_t> seg;
     seg.reserve(3 * (size_t)nb);
-    uint64_t o = 0;
+    uint64_t o = 0, t1_bytes = 0;
     for (uint32_t b = 0; b < nb; ++b) {
         blk[b].data_off = o;
         uint32_t L = 0;
         for (auto& ch : chunks[b]) { seg.push_back(ch.first); seg.push_back(o + L); seg.push_back(ch.second); L += ch.second; }
         blk[b].len = L;
+        t1_bytes += L;
         if (!L) blk[b].npasses = 0;
         o += ((uint64_t)L + 16 + 15) & ~15ull;
     }
@@ -1167,6 +1175,7 @@ t2done:
         uint64_t* dsto = (uint64_t*)ctx->dstoff.get(8 * ((size_t)nb + 1));
         HIPCHK(hipMemcpyAsync(dsto, P.st_off.data(), 8 * ((size_t)nb + 1), hipMemcpyHostToDevice, st));
         gk_launch_t1_dec(st, src_bytes, dblk, dscr, dsto, nb);
+        HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_t1_recon(st, dblk, dscr, dsto, arena, nb);
     }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
@@ -1207,6 +1216,10 @@ t2done:
     HIPCHK(hipStreamSynchronize(st));
     ctx->tm.t2_ms = ev_ms(ctx, 0, 1);
     ctx->tm.t1_ms = ev_ms(ctx, 2, 3);
+    ctx->tm.t1_cm_ms = 0.f;
+    ctx->tm.t1_coder_ms = ev_ms(ctx, 2, 8);
+    ctx->tm.cs_bytes = len;
+    ctx->tm.t1_bytes = t1_bytes;
     ctx->tm.dwt_ms = ev_ms(ctx, 3, 4);
     ctx->tm.mct_ms = ev_ms(ctx, 4, 5);
     ctx->tm.assemble_ms = ev_ms(ctx, 1, 2);

@@ -57,9 +57,12 @@ typedef struct gk_image_info {
 /* Per-stage device times of the last call (HIP events on the engine stream). */
 typedef struct gk_timings {
     float mct_ms, dwt_ms, t1_ms, t2_ms, assemble_ms, total_ms;
-    float t1_cm_ms;         /* encode: context-modelling part of t1_ms */
+    float t1_cm_ms;         /* encode: context-modelling kernel (k_t1_cm) part of t1_ms */
+    float t1_coder_ms;      /* the arithmetic-coder kernel alone: k_t1_mq (encode) / k_t1_dec (decode) */
     uint32_t dwt_launches, t1_blocks;
     uint64_t dwt_bytes;     /* algorithmic bytes moved by the DWT launches */
+    uint64_t cs_bytes;      /* codestream bytes produced (encode) / consumed (decode) */
+    uint64_t t1_bytes;      /* compressed code-block bytes coded by T1 */
 } gk_timings;
 
 typedef struct gk_ctx gk_ctx;

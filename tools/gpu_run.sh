@@ -6,15 +6,17 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+OUT="$PWD/gpurun_out"
+REPO="$PWD"
 STEPS="${1:-test smoke bench}"
 TESTSEL="${TESTSEL:-tests}"
 run() {  # name timeout cmd...
     local name=$1 t=$2; shift 2
-    echo "== $name: $*" >> gpurun_out/steps.log
-    timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+    echo "== $name: $*" >> "$OUT/steps.log"
+    timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?
-    echo "== $name rc=$rc" >> gpurun_out/steps.log
-    if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)" >> gpurun_out/steps.log; exit $rc; fi
+    echo "== $name rc=$rc" >> "$OUT/steps.log"
+    if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)" >> "$OUT/steps.log"; exit $rc; fi
     return 0
 }
 for s in $STEPS; do
@@ -22,8 +24,8 @@ for s in $STEPS; do
         test) run pytest_gpu 900 python -m pytest $TESTSEL -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
-        prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}) || exit $? ;;
-        pmc) (cd /tmp && run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_fetch" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-} && run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_write" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 0 --no-cpu-baseline ${BENCH_ARGS:-}) || exit $? ;;
+        prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$REPO/gpurun_out/prof" -o run -- python "$REPO/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-aux ${PROF_ARGS:-}) || exit $? ;;
+        pmc) (cd /tmp && run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$REPO/gpurun_out/pmc_fetch" -o run -- python "$REPO/bench.py" --steps 2 --warmup 0 --no-cpu-baseline --no-aux ${PROF_ARGS:-} && run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$REPO/gpurun_out/pmc_write" -o run -- python "$REPO/bench.py" --steps 2 --warmup 0 --no-cpu-baseline --no-aux ${PROF_ARGS:-}) || exit $? ;;
     esac
 done
 exit 0
