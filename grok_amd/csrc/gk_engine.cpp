@@ -86,7 +86,6 @@ struct Plan {
     std::vector<uint32_t> resw, resh;    // resolution sizes by level l = 0..L (l=0: full)
     uint64_t slot_bytes = 0;
     std::vector<uint64_t> sym_off;       // T1 symbol-stream offsets (nblocks + 1)
-    std::vector<uint64_t> st_off;        // T1 decoder scratch offsets in uint64 words (nblocks + 1)
     uint32_t ntrees = 0;                 // precinct-bands with code-blocks
 };
 
@@ -268,13 +267,6 @@ static void build_plan(Plan& P) {
         so = (so + 255) & ~255ull;
     }
     P.sym_off[P.blocks.size()] = so;
-    P.st_off.resize(P.blocks.size() + 1);
-    uint64_t wo = 0;
-    for (size_t i = 0; i < P.blocks.size(); ++i) {
-        P.st_off[i] = wo;
-        wo += 260 + (uint64_t)(P.blocks[i].band_numbps + 1) * 64;
-    }
-    P.st_off[P.blocks.size()] = wo;
 }
 
 // ---------------------------------------------------------------------------
@@ -710,8 +702,8 @@ struct gk_ctx {
     DevBuf dplanes;     // component planes staged from host
     DevBuf derr;
     DevBuf dsym, dsymoff, dpassend, dcminfo;
-    DevBuf dscratch, dstoff, dnmse;
-    HostBuf hinfo, hseg, hhdr, hpasses;
+    DevBuf dscratch, dnmse, dord;
+    HostBuf hinfo, hseg, hhdr, hpasses, hord;
     int16_t* nmse_tab = nullptr;   // device copy of the nmsedec tables (4 x 128)
     hipEvent_t ev[32];
     bool blocks_uploaded = false;
@@ -1154,7 +1146,7 @@ t2done:
         if (!L) blk[b].npasses = 0;
         o += ((uint64_t)L + 16 + 15) & ~15ull;
     }
-    uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 64);
+    uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 256);   // decoder window loads read up to 48 B past a block
     if (!seg.empty()) {
         uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8 + 8);
         memcpy(hs, seg.data(), seg.size() * 8);
@@ -1171,12 +1163,39 @@ t2done:
     int32_t* arena = (int32_t*)ctx->arena.get(P.plane_elems * P.nc * 2 * sizeof(int32_t));
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     {
-        uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * P.st_off[nb] + 64);
-        uint64_t* dsto = (uint64_t*)ctx->dstoff.get(8 * ((size_t)nb + 1));
-        HIPCHK(hipMemcpyAsync(dsto, P.st_off.data(), 8 * ((size_t)nb + 1), hipMemcpyHostToDevice, st));
-        gk_launch_t1_dec(st, src_bytes, dblk, dscr, dsto, nb);
+        // lane assignment: blocks bucketed by pass count (descending), so the 64 lanes of a
+        // wave decode similar amounts of work and the longest waves start first
+        const uint32_t nw = (nb + 63) / 64;
+        uint32_t* hord = (uint32_t*)ctx->hord.get(4 * (2 * (size_t)nb + 2) + 8 * ((size_t)nw + 1));
+        uint32_t* hpos = hord + nb;
+        uint64_t* hwo = (uint64_t*)(hord + 2 * (size_t)nb + 2);
+        {
+            std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
+            for (uint32_t b = 0; b < nb; ++b) cnt[std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1)]++;
+            std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
+            uint32_t acc = 0;
+            for (int k = GK_MAX_PASSES + 1; k >= 0; --k) { start[k] = acc; acc += cnt[k]; }
+            for (uint32_t b = 0; b < nb; ++b) {
+                uint32_t k = std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1);
+                hord[start[k]] = b; hpos[b] = start[k]; start[k]++;
+            }
+            uint64_t wo = 0;
+            for (uint32_t wv = 0; wv < nw; ++wv) {
+                hwo[wv] = wo;
+                uint32_t mp = 0;
+                for (uint32_t i = wv * 64; i < std::min(nb, wv * 64 + 64); ++i) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
+                wo += (260 + (uint64_t)mp * 64) * 64;
+            }
+            hwo[nw] = wo;
+        }
+        uint32_t* dord = (uint32_t*)ctx->dord.get(4 * (2 * (size_t)nb + 2) + 8 * ((size_t)nw + 1));
+        HIPCHK(hipMemcpyAsync(dord, hord, 4 * (2 * (size_t)nb + 2) + 8 * ((size_t)nw + 1), hipMemcpyHostToDevice, st));
+        const uint32_t* dpos = dord + nb;
+        const uint64_t* dwo = (const uint64_t*)(dord + 2 * (size_t)nb + 2);
+        uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
+        gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nb);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_t1_recon(st, dblk, dscr, dsto, arena, nb);
+        gk_launch_t1_recon(st, dblk, dpos, dscr, dwo, arena, nb);
     }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     run_dwt(ctx, false);

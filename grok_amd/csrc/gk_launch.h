@@ -24,10 +24,10 @@ void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks,
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
                      uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter);
-void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, uint64_t* scratch,
-                      const uint64_t* st_off, uint32_t nblocks);
-void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint64_t* scratch, const uint64_t* st_off,
-                        int32_t* coef, uint32_t nblocks);
+void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
+                      uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks);
+void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* pos, const uint64_t* scratch,
+                        const uint64_t* wave_off, int32_t* coef, uint32_t nblocks);
 // irreversible path (gk_dwt97.hip)
 void gk_launch_dc_ict_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin, float* y,
                           float* u, float* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift);

@@ -1,277 +1,507 @@
-// gk_t1dec.hip — Part-1 T1 decoder for CDNA4, one lane per code-block.
+// gk_t1dec.hip — Part-1 T1 decoder for CDNA4: one lane per code-block,
+// stripe-synchronous waves.
 //
 // Decoding is a serial chain per code-block (every MQ decision feeds the next
-// context), so the parallelism is the code-blocks themselves: 64 blocks per
-// wave, each lane running T1::decompress_cblk (T1.cpp:934-1446) on its own
-// block.  Per-stripe state (6 significance rows, 6 sign rows, visited and
-// refinement rows) lives in 64-bit registers; the block's persistent row
-// bitmaps live in a per-block scratch slab (L2-resident).  Each bit-plane's
-// decoded magnitude bits are stored as row bitmaps; k_t1_recon (wave per block,
-// lane = column) then rebuilds Grok's pre-filter values (2M+1)<<q and applies
-// the ShiftFilter / ScaleFilter dequantisation (filters/PostDecompressFilters.h)
-// straight into the band window.
+// context; T1::decompress_cblk, T1.cpp:934-1446), so the parallelism is the
+// code-blocks: each lane of a wave decodes its own block.  To keep the 64
+// chains of a wave convergent, all lanes walk the same (bit-plane, pass,
+// stripe) sequence and, inside a stripe-pass, advance in lock-step *steps*:
+// every step each lane locates its next coding position, forms the context and
+// decodes exactly one MQ symbol.  Control flow is uniform per step; only data
+// differs between lanes.
+//
+// Per-lane stripe state (significance / sign / visited / refined / plane-bit
+// rows as 64-bit column masks) lives in VGPRs while a stripe is processed and
+// in a per-wave scratch slab between passes, laid out [row][lane] so every
+// stripe load/store is one coalesced 512-byte access.  The compressed bytes
+// stream through a 32-byte per-lane register window refilled at uniform step
+// intervals with a 16-byte look-ahead load, so no lane waits on memory inside
+// a step.  Blocks are assigned to lanes sorted by pass count (host), so the
+// lanes of a wave carry similar work.
+//
+// k_t1_recon (wave per block, lane = column) rebuilds Grok's pre-filter values
+// (2M+1)<<q from the decoded bit-planes and applies ShiftFilter / ScaleFilter
+// (filters/PostDecompressFilters.h) straight into the band window.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "gk_common.h"
 #include "gk_t1_common.h"
+#include <cstdio>
+#include <cstdlib>
 
-// scratch layout per block (uint64 words)
-#define ST_SIG 0      // 66 rows (row y at index y + 1)
-#define ST_NEG 66     // 66 rows
-#define ST_MU 132     // 64 rows
-#define ST_PI 196     // 64 rows
-#define ST_BITS 260   // numbps planes x 64 rows (plane 0 = first decoded plane)
+// per-wave scratch (uint64 words), row r of field F at (F + r) * 64 + lane
+#define WS_SIG 0      // 66 rows (row y at y + 1, guards 0 and 65)
+#define WS_NEG 66     // 66 rows
+#define WS_MU 132     // 64 rows: refined in an earlier plane
+#define WS_PI 196     // 64 rows: visited in the current plane
+#define WS_BITS 260   // numbps planes x 64 rows: bit of the plane (plane 0 = most significant)
+#define WS_FIXED 260
 
+// ------------------------------------------------------------------ MQ decoder
+// Compressed bytes reach the coder through a 128-byte per-lane ring in LDS
+// (dword-interleaved [dword][lane], conflict-free).  Refills happen only at
+// stripe-pass boundaries (uniform points outside the step loop): the 32 bytes
+// staged in VGPRs by the previous boundary are written and the next 32 are
+// requested, so no step waits on global memory.  A lane whose ring runs low
+// inside a very dense stripe-pass takes a synchronous top-up (rare).  At the
+// end of every step each lane reads the 4 bytes at its position (nb4) from the
+// ring, so BYTEIN itself never touches memory.
+#define RING_DW 32
 struct MqDec {
     uint32_t a, c, ct;
-    uint32_t bp, len;
-    const uint8_t* p;       // 16-byte aligned staging of this block's bytes
-    uint64_t w0, w1;        // bytes [8*k, 8*k+16) where k = bp >> 3
-    uint32_t wk;
+    uint32_t bp, len, fill;      // read position, block length, ring fill position (multiple of 16)
+    uint32_t nb4;                // bytes [bp, bp + 4)
+    uint32_t sbase;              // staged bytes cover [sbase, sbase + 32)
+    uint32_t T0, T1, T2, T3, T4, T5, T6, T7;
+    const uint8_t* p;            // block bytes (16-byte aligned slot, padded)
 };
 
-__device__ __forceinline__ uint32_t dec_byte(const MqDec& q, uint32_t i) {
-    if (i >= q.len) return 0xffu;
-    uint32_t k = i >> 3;
-    uint64_t w = (k == q.wk) ? q.w0 : q.w1;
-    return (uint32_t)(w >> (8 * (i & 7))) & 0xffu;
+__device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
+    // per-lane select through v_cndmask, as inline asm so the optimiser cannot turn a
+    // select tree over struct fields into a dynamically indexed (scratch) access
+    uint64_t m = __ballot(c);
+    uint32_t r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
 }
-__device__ __forceinline__ void dec_advance(MqDec& q) {
-    ++q.bp;
-    if ((q.bp >> 3) != q.wk) {
-        q.wk = q.bp >> 3;
-        q.w0 = q.w1;
-        q.w1 = *(const uint64_t*)(q.p + 8 * (q.wk + 1));
+
+__device__ __forceinline__ void ring_write16(uint32_t (*ring)[64], int lane, uint32_t pos, uint32_t a, uint32_t b,
+                                             uint32_t c, uint32_t d) {
+    const uint32_t j = (pos >> 2) & (RING_DW - 1);
+    ring[j][lane] = a; ring[j + 1][lane] = b; ring[j + 2][lane] = c; ring[j + 3][lane] = d;
+    if (j == 0) ring[RING_DW][lane] = a;   // mirror for wrap-around reads
+}
+__device__ __forceinline__ uint32_t ring_get4(uint32_t (*ring)[64], int lane, uint32_t bp) {
+    const uint32_t j = (bp >> 2) & (RING_DW - 1);
+    return __builtin_amdgcn_alignbyte(ring[j + 1][lane], ring[j][lane], bp & 3);
+}
+__device__ __forceinline__ void stage_load(MqDec& q) {
+    uint4 a = *(const uint4*)(q.p + q.sbase), b = *(const uint4*)(q.p + q.sbase + 16);
+    q.T0 = a.x; q.T1 = a.y; q.T2 = a.z; q.T3 = a.w; q.T4 = b.x; q.T5 = b.y; q.T6 = b.z; q.T7 = b.w;
+}
+// stripe-pass boundary: commit the staged 32 bytes when the ring has room, request the next 32
+__device__ __forceinline__ void ring_boundary(uint32_t (*ring)[64], int lane, MqDec& q) {
+    if (q.sbase != q.fill) { q.sbase = q.fill; stage_load(q); }   // after a synchronous top-up
+    if (q.fill + 32 - q.bp <= 4 * RING_DW) {
+        ring_write16(ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3);
+        ring_write16(ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7);
+        q.fill += 32;
+        q.sbase = q.fill;
+        stage_load(q);
     }
 }
-__device__ __forceinline__ void dec_bytein(MqDec& q) {
-    uint32_t cur = dec_byte(q, q.bp), nxt = dec_byte(q, q.bp + 1);
-    if (cur == 0xff) {
-        if (nxt > 0x8f) { q.c += 0xff00; q.ct = 8; }
-        else { dec_advance(q); q.c += nxt << 9; q.ct = 7; }
-    } else { dec_advance(q); q.c += nxt << 8; q.ct = 8; }
+// inside a step loop: synchronous top-up for a lane about to run dry
+__device__ __forceinline__ void ring_topup(uint32_t (*ring)[64], int lane, MqDec& q) {
+    if (q.fill - q.bp < 8) {
+        uint4 a = *(const uint4*)(q.p + q.fill);
+        ring_write16(ring, lane, q.fill, a.x, a.y, a.z, a.w);
+        q.fill += 16;
+    }
 }
 
-struct Ctx5 { uint32_t w[5]; };
+// BYTEIN (mqc_dec.cpp, Annex C.3.4), branch-free: bytes past the end read as 0xFF.
+__device__ __forceinline__ void mq_bytein(MqDec& q, bool en) {
+    const uint32_t cur = q.bp < q.len ? (q.nb4 & 0xff) : 0xffu;
+    const uint32_t nxt = q.bp + 1 < q.len ? ((q.nb4 >> 8) & 0xff) : 0xffu;
+    const bool ff = cur == 0xff, stuck = ff && nxt > 0x8f;
+    const uint32_t add = stuck ? 0xff00u : (nxt << (ff ? 9 : 8));
+    const bool adv = en && !stuck;
+    q.c += en ? add : 0u;
+    q.ct = en ? ((ff && !stuck) ? 7u : 8u) : q.ct;
+    q.bp += adv ? 1u : 0u;
+    q.nb4 = adv ? (q.nb4 >> 8) : q.nb4;
+}
 
-__device__ __forceinline__ uint32_t mq_dec(MqDec& q, Ctx5& cw, const uint32_t* tab, uint32_t cx) {
+struct Ctx5 { uint32_t w0, w1, w2, w3, w4; };   // one byte per context: state | mps << 6
+
+// DECODE (Annex C.3.2) for context cx; `en` predicates every state change.
+__device__ __forceinline__ uint32_t mq_decode(MqDec& q, Ctx5& cw, const uint32_t* tab, uint32_t cx, bool en) {
     const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
-    uint32_t word = wi == 0 ? cw.w[0] : wi == 1 ? cw.w[1] : wi == 2 ? cw.w[2] : wi == 3 ? cw.w[3] : cw.w[4];
+    uint32_t word = vsel(wi == 4, cw.w4, vsel(wi & 2, vsel(wi & 1, cw.w3, cw.w2), vsel(wi & 1, cw.w1, cw.w0)));
     const uint32_t st = (word >> shb) & 0xff;
     const uint32_t mps = st >> 6;
     const uint32_t e = tab[st & 63];
     const uint32_t qe = e & 0xffff;
-    uint32_t d, nst;
-    q.a -= qe;
-    if ((q.c >> 16) < qe) {
-        if (q.a < qe) { d = mps; nst = ((e >> 16) & 0x3f) | (mps << 6); }
-        else { d = mps ^ 1; nst = ((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6); }
-        q.a = qe;
-    } else {
-        q.c -= qe << 16;
-        if (q.a & 0x8000) return mps;
-        if (q.a < qe) { d = mps ^ 1; nst = ((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6); }
-        else { d = mps; nst = ((e >> 16) & 0x3f) | (mps << 6); }
-    }
+    const uint32_t a1 = q.a - qe;
+    const bool lower = (q.c >> 16) < qe;
+    const bool fast = !lower && (a1 & 0x8000);            // MPS, no renormalisation
+    const bool mps_path = lower ? (a1 < qe) : (a1 >= qe);  // exchange rule
+    const uint32_t d = (fast || mps_path) ? mps : (mps ^ 1);
+    const uint32_t nst = mps_path ? (((e >> 16) & 0x3f) | (mps << 6)) : (((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6));
+    const bool upd = en && !fast;
+    q.a = en ? (lower ? qe : a1) : q.a;
+    q.c = (en && !lower) ? q.c - (qe << 16) : q.c;
     word = (word & ~(0xffu << shb)) | (nst << shb);
-    if (wi == 0) cw.w[0] = word; else if (wi == 1) cw.w[1] = word; else if (wi == 2) cw.w[2] = word;
-    else if (wi == 3) cw.w[3] = word; else cw.w[4] = word;
-    uint32_t n = __clz(q.a) - 16;
-    while (n) {
-        if (q.ct == 0) dec_bytein(q);
-        uint32_t k = n < q.ct ? n : q.ct;
+    cw.w0 = vsel(upd && wi == 0, word, cw.w0); cw.w1 = vsel(upd && wi == 1, word, cw.w1);
+    cw.w2 = vsel(upd && wi == 2, word, cw.w2); cw.w3 = vsel(upd && wi == 3, word, cw.w3);
+    cw.w4 = vsel(upd && wi == 4, word, cw.w4);
+    // RENORMD: shift n bits, BYTEIN whenever ct reaches 0 before a shift
+    uint32_t n = upd ? __clz(q.a) - 16 : 0u;
+    while (__any(n != 0)) {
+        const bool need = n != 0;
+        mq_bytein(q, need && q.ct == 0);
+        const uint32_t k = n < q.ct ? n : q.ct;
         q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
     }
     return d;
 }
 
-__device__ __forceinline__ uint32_t w3(uint64_t row, uint32_t x) {
-    return (uint32_t)((x ? (row >> (x - 1)) : (row << 1)) & 7);
-}
-__device__ __forceinline__ uint32_t f9(uint64_t up, uint64_t mid, uint64_t dn, uint32_t x) {
-    return w3(up, x) | ((w3(mid, x) & 5) << 3) | (w3(dn, x) << 6);
-}
-__device__ __forceinline__ uint64_t dil(uint64_t u, uint64_t m, uint64_t d) {
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint64_t dil3(uint64_t u, uint64_t m, uint64_t d) {
     uint64_t t = u | m | d;
-    return u | d | (t << 1) | (t >> 1);
+    return t | (t << 1) | (t >> 1);
 }
-__device__ __forceinline__ uint32_t scx(uint64_t su, uint64_t nu, uint64_t sm, uint64_t nm, uint64_t sd, uint64_t nd,
-                                        uint32_t x) {
-    uint32_t wv = x ? (uint32_t)((sm >> (x - 1)) & 1) : 0, wn = x ? (uint32_t)((nm >> (x - 1)) & 1) : 0;
-    uint32_t ev = x < 63 ? (uint32_t)((sm >> (x + 1)) & 1) : 0, en = x < 63 ? (uint32_t)((nm >> (x + 1)) & 1) : 0;
-    uint32_t nv = (uint32_t)((su >> x) & 1), nn = (uint32_t)((nu >> x) & 1);
-    uint32_t sv = (uint32_t)((sd >> x) & 1), sn = (uint32_t)((nd >> x) & 1);
-    return (wn & wv) | (wv << 1) | ((en & ev) << 2) | (ev << 3) | ((nn & nv) << 4) | (nv << 5) | ((sn & sv) << 6) |
-           (sv << 7);
+// 3-bit window (x-1, x, x+1) of a row
+__device__ __forceinline__ uint32_t win3(uint64_t row, uint32_t x) {
+    return (uint32_t)((x ? (row >> (x - 1)) : (row << 1)) & 7u);
 }
+// 18-bit window of six rows: row i -> bits [3i, 3i+3)
+__device__ __forceinline__ uint32_t win18(uint64_t r0, uint64_t r1, uint64_t r2, uint64_t r3, uint64_t r4, uint64_t r5,
+                                          uint32_t x) {
+    return win3(r0, x) | (win3(r1, x) << 3) | (win3(r2, x) << 6) | (win3(r3, x) << 9) | (win3(r4, x) << 12) |
+           (win3(r5, x) << 15);
+}
+// bits of the four stripe rows at column x (bit r = row r)
+__device__ __forceinline__ uint32_t col4(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint32_t x) {
+    return (uint32_t)((a >> x) & 1) | ((uint32_t)((b >> x) & 1) << 1) | ((uint32_t)((c >> x) & 1) << 2) |
+           ((uint32_t)((d >> x) & 1) << 3);
+}
+// next coding position >= (x, r) in stripe scan order (column-major, rows 0..3);
+// returns false when the stripe has none.
+__device__ __forceinline__ bool next_pos(uint64_t c0, uint64_t c1, uint64_t c2, uint64_t c3, uint32_t& x, uint32_t& r) {
+    if (x < 64) {
+        uint32_t m = col4(c0, c1, c2, c3, x) & (0xfu << r);
+        if (m) { r = __ffs(m) - 1; return true; }
+    }
+    uint64_t any = c0 | c1 | c2 | c3;
+    any = (x >= 63) ? 0ull : (any & (~0ull << (x + 1)));
+    if (!any) return false;
+    x = (uint32_t)__ffsll((long long)any) - 1;
+    r = __ffs(col4(c0, c1, c2, c3, x)) - 1;
+    return true;
+}
+// sign-context index (bit0 W-neg bit1 W-sig bit2 E-neg bit3 E-sig bit4 N-neg bit5 N-sig bit6 S-neg bit7 S-sig)
+// from the 9-bit significance / sign neighbourhoods fs / fn of the sample
+__device__ __forceinline__ uint32_t sc_from9(uint32_t fs, uint32_t fn) {
+    uint32_t wv = (fs >> 3) & 1, ev = (fs >> 5) & 1, nv = (fs >> 1) & 1, sv = (fs >> 7) & 1;
+    uint32_t wn = (fn >> 3) & wv, en = (fn >> 5) & ev, nn = (fn >> 1) & nv, sn = (fn >> 7) & sv;
+    return wn | (wv << 1) | (en << 2) | (ev << 3) | (nn << 4) | (nv << 5) | (sn << 6) | (sv << 7);
+}
+__device__ __forceinline__ uint64_t rowsel(uint32_t r, uint32_t i, uint64_t v) { return r == i ? v : 0ull; }
 
 struct DecLds {
     uint32_t tab[47];
     uint8_t zc[4][512];
     uint8_t sc[256];
+    uint32_t ring[RING_DW + 1][64];
 };
 
-// significance decode of one sample (used by SP and CL)
-#define SIG_DECODE(UP, MID, DN, NUP, NMID, NDN, BT)                                             \
-    {                                                                                           \
-        uint32_t e_ = Ls.sc[scx(UP, NUP, MID, NMID, DN, NDN, x)];                               \
-        uint32_t sg_ = mq_dec(q, cw, Ls.tab, CTX_SC + (e_ & 15)) ^ (e_ >> 4);                   \
-        MID |= bx;                                                                              \
-        if (sg_) NMID |= bx;                                                                    \
-        BT |= bx;                                                                               \
+enum { PH_FIND = 0, PH_SIGN = 1, PH_UNI1 = 2, PH_UNI2 = 3 };
+
+// Everything one lane carries across stripe-passes.
+struct LaneDec {
+    MqDec q;
+    Ctx5 cw;
+    uint32_t step;
+    uint32_t nsym;
+};
+
+__device__ __forceinline__ void step_refill(LaneDec& L, uint32_t (*ring)[64], int lane) {
+    ++L.step;
+    if (__any(L.q.fill - L.q.bp < 8)) ring_topup(ring, lane, L.q);
+}
+__device__ __forceinline__ void step_prefetch(LaneDec& L, uint32_t (*ring)[64], int lane) {
+    L.q.nb4 = ring_get4(ring, lane, L.q.bp);
+}
+
+// Branch-free next coding position >= (x, r) (column-major, rows 0..3).  Returns
+// false (x, r unchanged) when the stripe has no further position.
+__device__ __forceinline__ bool find_next(uint64_t c0, uint64_t c1, uint64_t c2, uint64_t c3, uint32_t& x, uint32_t& r) {
+    const uint32_t xc = x & 63;
+    const uint32_t m = (x < 64) ? (col4(c0, c1, c2, c3, xc) & (0xfu << r)) : 0u;
+    const uint64_t any = (x >= 63) ? 0ull : ((c0 | c1 | c2 | c3) & (~0ull << (x + 1)));
+    const uint32_t xn = (uint32_t)__ffsll((long long)any) - 1;
+    const uint32_t mn = col4(c0, c1, c2, c3, xn & 63);
+    const bool here = m != 0, found = here || any != 0;
+    x = here ? x : (found ? xn : x);
+    r = here ? (uint32_t)(__ffs(m) - 1) : (found ? (uint32_t)(__ffs(mn) - 1) : r);
+    return found;
+}
+__device__ __forceinline__ uint64_t rsel(uint32_t r, uint32_t i, uint64_t v) { return r == i ? v : 0ull; }
+
+// ---- significance propagation on one stripe (T1.cpp:1182-1245)
+__device__ __forceinline__ void pass_sp(LaneDec& L, DecLds& Ls, const uint8_t* zc, int lane, bool on,
+                                        uint64_t S0, uint64_t& S1, uint64_t& S2, uint64_t& S3, uint64_t& S4, uint64_t S5,
+                                        uint64_t N0, uint64_t& N1, uint64_t& N2, uint64_t& N3, uint64_t& N4, uint64_t N5,
+                                        uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3, uint64_t& P0, uint64_t& P1,
+                                        uint64_t& P2, uint64_t& P3) {
+    uint64_t C0 = ~S1 & dil3(S0, S1, S2) & v0, C1 = ~S2 & dil3(S1, S2, S3) & v1;
+    uint64_t C2 = ~S3 & dil3(S2, S3, S4) & v2, C3 = ~S4 & dil3(S3, S4, S5) & v3;
+    uint32_t x = 0, r = 0;
+    bool sign = false, pend = on;
+    while (__any(pend)) {
+        step_refill(L, Ls.ring, lane);
+        if (!sign) pend = pend && find_next(C0, C1, C2, C3, x, r);
+        const uint32_t sh = 3 * r;
+        const uint32_t fs = (win18(S0, S1, S2, S3, S4, S5, x & 63) >> sh) & 0x1ff;
+        const uint32_t fn = (win18(N0, N1, N2, N3, N4, N5, x & 63) >> sh) & 0x1ff;
+        const uint32_t sce = Ls.sc[sc_from9(fs, fn)];
+        const uint32_t cx = sign ? CTX_SC + (sce & 15) : CTX_ZC + zc[fs];
+        const uint32_t d = mq_decode(L.q, L.cw, Ls.tab, cx, pend);
+        L.nsym += pend ? 1 : 0;
+        // sign decoded: the sample becomes significant
+        const bool sig = pend && sign;
+        const uint64_t bx = sig ? (1ull << (x & 63)) : 0ull, bn = bx << 1;
+        const uint64_t m0 = rsel(r, 0, bx), m1 = rsel(r, 1, bx), m2 = rsel(r, 2, bx), m3 = rsel(r, 3, bx);
+        S1 |= m0; S2 |= m1; S3 |= m2; S4 |= m3;
+        const uint64_t ng = (d ^ (sce >> 4)) ? ~0ull : 0ull;
+        N1 |= m0 & ng; N2 |= m1 & ng; N3 |= m2 & ng; N4 |= m3 & ng;
+        // later positions that gain a significant neighbour: (x, r+1) and column x+1 rows r-1..r+1
+        const uint64_t b0 = rsel(r, 0, bn), b1 = rsel(r, 1, bn), b2 = rsel(r, 2, bn), b3 = rsel(r, 3, bn);
+        C0 |= (b0 | b1) & ~S1 & v0;
+        C1 |= (m0 | b0 | b1 | b2) & ~S2 & v1;
+        C2 |= (m1 | b1 | b2 | b3) & ~S3 & v2;
+        C3 |= (m2 | b2 | b3) & ~S4 & v3;
+        // advance: after a zero ZC decision or a sign, move to the next row
+        const bool adv = pend && (sign || !d);
+        sign = pend && !sign && d;
+        r += adv ? 1 : 0;
+        x += (r == 4) ? 1 : 0;
+        r &= 3;
+        step_prefetch(L, Ls.ring, lane);
     }
+    // every candidate was visited and no visited position was added afterwards: visited = candidates
+    P0 = C0; P1 = C1; P2 = C2; P3 = C3;
+}
+
+// ---- magnitude refinement on one stripe (T1.cpp:1310-1364)
+__device__ __forceinline__ void pass_mr(LaneDec& L, DecLds& Ls, int lane, bool on, uint64_t S0, uint64_t S1, uint64_t S2,
+                                        uint64_t S3, uint64_t S4, uint64_t S5, uint64_t v0, uint64_t v1, uint64_t v2,
+                                        uint64_t v3, uint64_t P0, uint64_t P1, uint64_t P2, uint64_t P3, uint64_t& M0,
+                                        uint64_t& M1, uint64_t& M2, uint64_t& M3, uint64_t& B0, uint64_t& B1,
+                                        uint64_t& B2, uint64_t& B3) {
+    const uint64_t C0 = S1 & ~P0 & v0, C1 = S2 & ~P1 & v1, C2 = S3 & ~P2 & v2, C3 = S4 & ~P3 & v3;
+    uint32_t x = 0, r = 0;
+    bool pend = on;
+    while (__any(pend)) {
+        step_refill(L, Ls.ring, lane);
+        pend = pend && find_next(C0, C1, C2, C3, x, r);
+        const uint32_t xc = x & 63;
+        const uint32_t fs = (win18(S0, S1, S2, S3, S4, S5, xc) >> (3 * r)) & 0x1ef;
+        const uint64_t mu = rsel(r, 0, M0) | rsel(r, 1, M1) | rsel(r, 2, M2) | rsel(r, 3, M3);
+        const uint32_t cx = ((mu >> xc) & 1) ? CTX_MAG + 2 : (fs ? CTX_MAG + 1 : CTX_MAG);
+        const uint32_t d = mq_decode(L.q, L.cw, Ls.tab, cx, pend);
+        L.nsym += pend ? 1 : 0;
+        const uint64_t bx = (pend && d) ? (1ull << xc) : 0ull;
+        B0 |= rsel(r, 0, bx); B1 |= rsel(r, 1, bx); B2 |= rsel(r, 2, bx); B3 |= rsel(r, 3, bx);
+        r += pend ? 1 : 0;
+        x += (r == 4) ? 1 : 0;
+        r &= 3;
+        step_prefetch(L, Ls.ring, lane);
+    }
+    M0 |= C0; M1 |= C1; M2 |= C2; M3 |= C3;   // everything coded here is now refined
+}
+
+// ---- cleanup on one stripe (T1.cpp:974-1093)
+__device__ __forceinline__ void pass_cl(LaneDec& L, DecLds& Ls, const uint8_t* zc, int lane, bool on, uint32_t nr,
+                                        uint64_t S0, uint64_t& S1, uint64_t& S2, uint64_t& S3, uint64_t& S4, uint64_t S5,
+                                        uint64_t N0, uint64_t& N1, uint64_t& N2, uint64_t& N3, uint64_t& N4, uint64_t N5,
+                                        uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3, uint64_t P0, uint64_t P1,
+                                        uint64_t P2, uint64_t P3) {
+    const uint64_t C0 = ~S1 & ~P0 & v0, C1 = ~S2 & ~P1 & v1, C2 = ~S3 & ~P2 & v2, C3 = ~S4 & ~P3 & v3;
+    // run-length candidates: four coding positions, no significant neighbour at pass start
+    const uint64_t E = (nr == 4) ? (C0 & C1 & C2 & C3 & ~dil3(S0 | S1, S2 | S3, S4 | S5)) : 0ull;
+    uint64_t fresh = 0;   // samples that became significant during this pass
+    uint32_t x = 0, r = 0, ph = PH_FIND, colx = 0xffffffffu, rlhi = 0;
+    bool pend = on;
+    while (__any(pend)) {
+        step_refill(L, Ls.ring, lane);
+        const bool finding = ph == PH_FIND;
+        if (finding) pend = pend && find_next(C0, C1, C2, C3, x, r);
+        const uint32_t xc = x & 63;
+        // a new column starts in run-length mode when it was eligible at pass start and its
+        // left neighbour column gained no significance in this pass
+        const bool agg = finding && x != colx && ((E >> xc) & 1) && !(xc && ((fresh >> (xc - 1)) & 1));
+        colx = finding ? x : colx;
+        const uint32_t sh = 3 * r;
+        const uint32_t fs = (win18(S0, S1, S2, S3, S4, S5, xc) >> sh) & 0x1ff;
+        const uint32_t fn = (win18(N0, N1, N2, N3, N4, N5, xc) >> sh) & 0x1ff;
+        const uint32_t sce = Ls.sc[sc_from9(fs, fn)];
+        const uint32_t cx = agg ? CTX_AGG : (ph == PH_SIGN ? CTX_SC + (sce & 15) : (finding ? CTX_ZC + zc[fs] : CTX_UNI));
+        const uint32_t d = mq_decode(L.q, L.cw, Ls.tab, cx, pend);
+        L.nsym += pend ? 1 : 0;
+        const bool sig = pend && ph == PH_SIGN;
+        const uint64_t bx = sig ? (1ull << xc) : 0ull;
+        const uint64_t m0 = rsel(r, 0, bx), m1 = rsel(r, 1, bx), m2 = rsel(r, 2, bx), m3 = rsel(r, 3, bx);
+        S1 |= m0; S2 |= m1; S3 |= m2; S4 |= m3;
+        const uint64_t ng = (d ^ (sce >> 4)) ? ~0ull : 0ull;
+        N1 |= m0 & ng; N2 |= m1 & ng; N3 |= m2 & ng; N4 |= m3 & ng;
+        fresh |= bx;
+        // phase transitions
+        uint32_t nph = ph, nr2 = r;
+        bool col_done = false;
+        if (agg) { nph = d ? PH_UNI1 : PH_FIND; col_done = !d; }
+        else if (finding) { nph = d ? PH_SIGN : PH_FIND; nr2 = d ? r : r + 1; }
+        else if (ph == PH_UNI1) { rlhi = d; nph = PH_UNI2; }
+        else if (ph == PH_UNI2) { nr2 = (rlhi << 1) | d; nph = PH_SIGN; }
+        else { nph = PH_FIND; nr2 = r + 1; }
+        if (pend) {
+            ph = nph;
+            r = col_done ? 0 : nr2;
+            x += (col_done || r == 4) ? 1 : 0;
+            r &= 3;
+        }
+        step_prefetch(L, Ls.ring, lane);
+    }
+}
 
 __global__ __launch_bounds__(64) void k_t1_dec(const uint8_t* __restrict__ bytes, const GkBlock* __restrict__ blocks,
-                                               uint64_t* __restrict__ scratch, const uint64_t* __restrict__ st_off,
-                                               uint32_t nblocks) {
+                                               const uint32_t* __restrict__ order, uint64_t* __restrict__ scratch,
+                                               const uint64_t* __restrict__ wave_off, uint32_t nblocks,
+                                               unsigned long long* __restrict__ stats) {
     __shared__ DecLds Ls;
     const int lane = threadIdx.x;
     if (lane < 47) Ls.tab[lane] = c_mq[lane];
     for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
     for (int i = lane; i < 256; i += 64) Ls.sc[i] = sc_rule((uint32_t)i);
-    __syncthreads();
-    const uint32_t b = blockIdx.x * 64 + lane;
-    if (b >= nblocks) return;
-    const GkBlock B = blocks[b];
-    const uint32_t numbps = B.numbps, npasses = B.npasses;
-    uint64_t* ST = scratch + st_off[b];
+    const uint32_t slot = blockIdx.x * 64 + lane;
+    const bool has = slot < nblocks;
+    GkBlock B = {};
+    if (has) B = blocks[order[slot]];
+    uint64_t* WS = scratch + wave_off[blockIdx.x];
+    const uint32_t numbps = has ? B.numbps : 0, npasses = (has && B.numbps) ? B.npasses : 0;
     const uint32_t w = B.w, h = B.h;
-    for (int i = 0; i < 260; ++i) ST[i] = 0;
-    if (!npasses || !numbps) return;
-    const uint8_t* zc = Ls.zc[B.orient];
     const uint64_t colmask = w >= 64 ? ~0ull : ((1ull << w) - 1);
-    MqDec q;
-    q.p = bytes + B.data_off; q.len = B.len; q.bp = 0; q.wk = 0;
-    q.w0 = *(const uint64_t*)(q.p);
-    q.w1 = *(const uint64_t*)(q.p + 8);
-    q.c = (q.len == 0 ? 0xffu : dec_byte(q, 0)) << 16;
-    dec_bytein(q);
-    q.c <<= 7; q.ct -= 7; q.a = 0x8000;
-    Ctx5 cw;
-    cw.w[0] = 4u; cw.w[1] = 0; cw.w[2] = 0; cw.w[3] = 0; cw.w[4] = (3u << 8) | (46u << 16);
     const uint32_t nstripes = (h + 3) >> 2;
-    uint32_t pass = 0;
-    for (int bpno = (int)numbps - 1; bpno >= 0 && pass < npasses; --bpno) {
-        uint64_t* BITS = ST + ST_BITS + (size_t)(numbps - 1 - bpno) * 64;
-        const bool first = bpno == (int)numbps - 1;
-        if (!first) {
-            // ---------------- significance propagation (T1.cpp:1182-1245)
-            for (uint32_t s = 0; s < nstripes; ++s) {
-                const uint32_t y0 = 4 * s, nr = h - y0 < 4 ? h - y0 : 4;
-                uint64_t S0 = ST[ST_SIG + y0], S1 = ST[ST_SIG + y0 + 1], S2 = ST[ST_SIG + y0 + 2],
-                         S3 = ST[ST_SIG + y0 + 3], S4 = ST[ST_SIG + y0 + 4], S5 = ST[ST_SIG + y0 + 5];
-                uint64_t N0 = ST[ST_NEG + y0], N1 = ST[ST_NEG + y0 + 1], N2 = ST[ST_NEG + y0 + 2],
-                         N3 = ST[ST_NEG + y0 + 3], N4 = ST[ST_NEG + y0 + 4], N5 = ST[ST_NEG + y0 + 5];
-                uint64_t P0 = 0, P1 = nr > 1 ? 0 : ~0ull, P2 = nr > 2 ? 0 : ~0ull, P3 = nr > 3 ? 0 : ~0ull;
-                uint64_t B0 = 0, B1 = 0, B2 = 0, B3 = 0;
-                uint32_t x = 0;
-                while (x < 64) {
-                    uint64_t cand = (~S1 & ~P0 & dil(S0, S1, S2)) | (~S2 & ~P1 & dil(S1, S2, S3)) |
-                                    (~S3 & ~P2 & dil(S2, S3, S4)) | (~S4 & ~P3 & dil(S3, S4, S5));
-                    cand &= colmask & (~0ull << x);
-                    if (!cand) break;
-                    x = (uint32_t)__ffsll((long long)cand) - 1;
-                    const uint64_t bx = 1ull << x;
-                    if (!((S1 | P0) & bx)) { uint32_t f = f9(S0, S1, S2, x); if (f) { if (mq_dec(q, cw, Ls.tab, zc[f])) SIG_DECODE(S0, S1, S2, N0, N1, N2, B0); P0 |= bx; } }
-                    if (!((S2 | P1) & bx)) { uint32_t f = f9(S1, S2, S3, x); if (f) { if (mq_dec(q, cw, Ls.tab, zc[f])) SIG_DECODE(S1, S2, S3, N1, N2, N3, B1); P1 |= bx; } }
-                    if (!((S3 | P2) & bx)) { uint32_t f = f9(S2, S3, S4, x); if (f) { if (mq_dec(q, cw, Ls.tab, zc[f])) SIG_DECODE(S2, S3, S4, N2, N3, N4, B2); P2 |= bx; } }
-                    if (!((S4 | P3) & bx)) { uint32_t f = f9(S3, S4, S5, x); if (f) { if (mq_dec(q, cw, Ls.tab, zc[f])) SIG_DECODE(S3, S4, S5, N3, N4, N5, B3); P3 |= bx; } }
-                    ++x;
+    const uint8_t* zc = Ls.zc[B.orient & 3];
+    for (int r = 0; r < WS_FIXED; ++r) WS[r * 64 + lane] = 0;   // clear the state rows (coalesced)
+    LaneDec L;
+    L.cw = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};   // mqc_resetstates: ZC0=4, AGG=3, UNI=46
+    L.step = 0; L.nsym = 0;
+    MqDec& q = L.q;
+    q.p = npasses ? bytes + B.data_off : bytes;
+    q.len = npasses ? B.len : 0;
+    q.bp = 0; q.fill = 0; q.sbase = 0;
+    stage_load(q);
+    __syncthreads();
+    ring_boundary(Ls.ring, lane, q);
+    q.sbase = q.fill; stage_load(q);
+    ring_boundary(Ls.ring, lane, q);
+    ring_boundary(Ls.ring, lane, q);
+    q.nb4 = ring_get4(Ls.ring, lane, 0);
+    // INITDEC (mqc_dec.cpp:98-112)
+    q.c = (q.len ? (q.nb4 & 0xff) : 0xffu) << 16;
+    mq_bytein(q, true);
+    q.c <<= 7; q.ct -= 7; q.a = 0x8000;
+    // wave-uniform loop bounds
+    uint32_t maxplanes = numbps, maxst = nstripes;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        maxplanes = max(maxplanes, (uint32_t)__shfl_xor((int)maxplanes, o));
+        maxst = max(maxst, (uint32_t)__shfl_xor((int)maxst, o));
+    }
+    for (uint32_t k = 0; k < maxplanes; ++k) {
+        uint64_t* BITS = WS + (WS_BITS + (size_t)k * 64) * 64;
+        for (uint32_t t = (k == 0 ? 2u : 0u); t < 3; ++t) {
+            const uint32_t pidx = k == 0 ? 0 : 1 + 3 * (k - 1) + t;   // pass index within the block
+            const bool pass_on = k < numbps && pidx < npasses;
+            if (!__any(pass_on)) continue;
+            for (uint32_t s = 0; s < maxst; ++s) {
+                const bool on = pass_on && s < nstripes;
+                ring_boundary(Ls.ring, lane, L.q);
+                L.q.nb4 = ring_get4(Ls.ring, lane, L.q.bp);
+                const uint32_t y0 = 4 * s;
+                const uint32_t nr = on ? min(4u, h - y0) : 0;
+                const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
+                               v3 = nr > 3 ? colmask : 0;
+                uint64_t S0 = WS[(WS_SIG + y0) * 64 + lane], S1 = WS[(WS_SIG + y0 + 1) * 64 + lane],
+                         S2 = WS[(WS_SIG + y0 + 2) * 64 + lane], S3 = WS[(WS_SIG + y0 + 3) * 64 + lane],
+                         S4 = WS[(WS_SIG + y0 + 4) * 64 + lane], S5 = WS[(WS_SIG + y0 + 5) * 64 + lane];
+                if (t == 0) {
+                    uint64_t N0 = WS[(WS_NEG + y0) * 64 + lane], N1 = WS[(WS_NEG + y0 + 1) * 64 + lane],
+                             N2 = WS[(WS_NEG + y0 + 2) * 64 + lane], N3 = WS[(WS_NEG + y0 + 3) * 64 + lane],
+                             N4 = WS[(WS_NEG + y0 + 4) * 64 + lane], N5 = WS[(WS_NEG + y0 + 5) * 64 + lane];
+                    const uint64_t T1s = S1, T2s = S2, T3s = S3, T4s = S4;
+                    uint64_t P0, P1, P2, P3;
+                    pass_sp(L, Ls, zc, lane, on, S0, S1, S2, S3, S4, S5, N0, N1, N2, N3, N4, N5, v0, v1, v2, v3,
+                            P0, P1, P2, P3);
+                    if (on) {
+                        WS[(WS_SIG + y0 + 1) * 64 + lane] = S1; WS[(WS_SIG + y0 + 2) * 64 + lane] = S2;
+                        WS[(WS_SIG + y0 + 3) * 64 + lane] = S3; WS[(WS_SIG + y0 + 4) * 64 + lane] = S4;
+                        WS[(WS_NEG + y0 + 1) * 64 + lane] = N1; WS[(WS_NEG + y0 + 2) * 64 + lane] = N2;
+                        WS[(WS_NEG + y0 + 3) * 64 + lane] = N3; WS[(WS_NEG + y0 + 4) * 64 + lane] = N4;
+                        WS[(WS_PI + y0) * 64 + lane] = P0; WS[(WS_PI + y0 + 1) * 64 + lane] = P1;
+                        WS[(WS_PI + y0 + 2) * 64 + lane] = P2; WS[(WS_PI + y0 + 3) * 64 + lane] = P3;
+                        // plane bits: the newly significant samples
+                        BITS[(y0) * 64 + lane] = S1 & ~T1s; BITS[(y0 + 1) * 64 + lane] = S2 & ~T2s;
+                        BITS[(y0 + 2) * 64 + lane] = S3 & ~T3s; BITS[(y0 + 3) * 64 + lane] = S4 & ~T4s;
+                    }
+                } else if (t == 1) {
+                    const uint64_t P0 = WS[(WS_PI + y0) * 64 + lane], P1 = WS[(WS_PI + y0 + 1) * 64 + lane],
+                                   P2 = WS[(WS_PI + y0 + 2) * 64 + lane], P3 = WS[(WS_PI + y0 + 3) * 64 + lane];
+                    uint64_t M0 = WS[(WS_MU + y0) * 64 + lane], M1 = WS[(WS_MU + y0 + 1) * 64 + lane],
+                             M2 = WS[(WS_MU + y0 + 2) * 64 + lane], M3 = WS[(WS_MU + y0 + 3) * 64 + lane];
+                    uint64_t B0 = BITS[(y0) * 64 + lane], B1 = BITS[(y0 + 1) * 64 + lane],
+                             B2 = BITS[(y0 + 2) * 64 + lane], B3 = BITS[(y0 + 3) * 64 + lane];
+                    pass_mr(L, Ls, lane, on, S0, S1, S2, S3, S4, S5, v0, v1, v2, v3, P0, P1, P2, P3, M0, M1, M2, M3,
+                            B0, B1, B2, B3);
+                    if (on) {
+                        WS[(WS_MU + y0) * 64 + lane] = M0; WS[(WS_MU + y0 + 1) * 64 + lane] = M1;
+                        WS[(WS_MU + y0 + 2) * 64 + lane] = M2; WS[(WS_MU + y0 + 3) * 64 + lane] = M3;
+                        BITS[(y0) * 64 + lane] = B0; BITS[(y0 + 1) * 64 + lane] = B1;
+                        BITS[(y0 + 2) * 64 + lane] = B2; BITS[(y0 + 3) * 64 + lane] = B3;
+                    }
+                } else {
+                    uint64_t N0 = WS[(WS_NEG + y0) * 64 + lane], N1 = WS[(WS_NEG + y0 + 1) * 64 + lane],
+                             N2 = WS[(WS_NEG + y0 + 2) * 64 + lane], N3 = WS[(WS_NEG + y0 + 3) * 64 + lane],
+                             N4 = WS[(WS_NEG + y0 + 4) * 64 + lane], N5 = WS[(WS_NEG + y0 + 5) * 64 + lane];
+                    uint64_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, B0 = 0, B1 = 0, B2 = 0, B3 = 0;
+                    if (k) {
+                        P0 = WS[(WS_PI + y0) * 64 + lane]; P1 = WS[(WS_PI + y0 + 1) * 64 + lane];
+                        P2 = WS[(WS_PI + y0 + 2) * 64 + lane]; P3 = WS[(WS_PI + y0 + 3) * 64 + lane];
+                        B0 = BITS[(y0) * 64 + lane]; B1 = BITS[(y0 + 1) * 64 + lane];
+                        B2 = BITS[(y0 + 2) * 64 + lane]; B3 = BITS[(y0 + 3) * 64 + lane];
+                    }
+                    const uint64_t T1s = S1, T2s = S2, T3s = S3, T4s = S4;
+                    pass_cl(L, Ls, zc, lane, on, nr, S0, S1, S2, S3, S4, S5, N0, N1, N2, N3, N4, N5, v0, v1, v2, v3,
+                            P0, P1, P2, P3);
+                    if (on) {
+                        WS[(WS_SIG + y0 + 1) * 64 + lane] = S1; WS[(WS_SIG + y0 + 2) * 64 + lane] = S2;
+                        WS[(WS_SIG + y0 + 3) * 64 + lane] = S3; WS[(WS_SIG + y0 + 4) * 64 + lane] = S4;
+                        WS[(WS_NEG + y0 + 1) * 64 + lane] = N1; WS[(WS_NEG + y0 + 2) * 64 + lane] = N2;
+                        WS[(WS_NEG + y0 + 3) * 64 + lane] = N3; WS[(WS_NEG + y0 + 4) * 64 + lane] = N4;
+                        BITS[(y0) * 64 + lane] = B0 | (S1 & ~T1s); BITS[(y0 + 1) * 64 + lane] = B1 | (S2 & ~T2s);
+                        BITS[(y0 + 2) * 64 + lane] = B2 | (S3 & ~T3s); BITS[(y0 + 3) * 64 + lane] = B3 | (S4 & ~T4s);
+                    }
                 }
-                ST[ST_SIG + y0 + 1] = S1; ST[ST_NEG + y0 + 1] = N1; ST[ST_PI + y0] = P0; BITS[y0] = B0;
-                if (nr > 1) { ST[ST_SIG + y0 + 2] = S2; ST[ST_NEG + y0 + 2] = N2; ST[ST_PI + y0 + 1] = P1; BITS[y0 + 1] = B1; }
-                if (nr > 2) { ST[ST_SIG + y0 + 3] = S3; ST[ST_NEG + y0 + 3] = N3; ST[ST_PI + y0 + 2] = P2; BITS[y0 + 2] = B2; }
-                if (nr > 3) { ST[ST_SIG + y0 + 4] = S4; ST[ST_NEG + y0 + 4] = N4; ST[ST_PI + y0 + 3] = P3; BITS[y0 + 3] = B3; }
             }
-            if (++pass >= npasses) break;
-            // ---------------- magnitude refinement (T1.cpp:1310-1364)
-            for (uint32_t s = 0; s < nstripes; ++s) {
-                const uint32_t y0 = 4 * s, nr = h - y0 < 4 ? h - y0 : 4;
-                uint64_t S0 = ST[ST_SIG + y0], S1 = ST[ST_SIG + y0 + 1], S2 = ST[ST_SIG + y0 + 2],
-                         S3 = ST[ST_SIG + y0 + 3], S4 = ST[ST_SIG + y0 + 4], S5 = ST[ST_SIG + y0 + 5];
-                uint64_t M0 = ST[ST_MU + y0], M1 = ST[ST_MU + y0 + 1], M2 = ST[ST_MU + y0 + 2], M3 = ST[ST_MU + y0 + 3];
-                uint64_t P0 = ST[ST_PI + y0], P1 = ST[ST_PI + y0 + 1], P2 = ST[ST_PI + y0 + 2], P3 = ST[ST_PI + y0 + 3];
-                uint64_t B0 = BITS[y0], B1 = nr > 1 ? BITS[y0 + 1] : 0, B2 = nr > 2 ? BITS[y0 + 2] : 0,
-                         B3 = nr > 3 ? BITS[y0 + 3] : 0;
-                const uint64_t c0 = S1 & ~P0, c1 = nr > 1 ? S2 & ~P1 : 0, c2 = nr > 2 ? S3 & ~P2 : 0,
-                               c3 = nr > 3 ? S4 & ~P3 : 0;
-                uint64_t cols = (c0 | c1 | c2 | c3) & colmask;
-                while (cols) {
-                    const uint32_t x = (uint32_t)__ffsll((long long)cols) - 1;
-                    const uint64_t bx = 1ull << x;
-                    cols &= cols - 1;
-                    if (c0 & bx) { uint32_t cx = (M0 & bx) ? CTX_MAG + 2 : (f9(S0, S1, S2, x) ? CTX_MAG + 1 : CTX_MAG); if (mq_dec(q, cw, Ls.tab, cx)) B0 |= bx; M0 |= bx; }
-                    if (c1 & bx) { uint32_t cx = (M1 & bx) ? CTX_MAG + 2 : (f9(S1, S2, S3, x) ? CTX_MAG + 1 : CTX_MAG); if (mq_dec(q, cw, Ls.tab, cx)) B1 |= bx; M1 |= bx; }
-                    if (c2 & bx) { uint32_t cx = (M2 & bx) ? CTX_MAG + 2 : (f9(S2, S3, S4, x) ? CTX_MAG + 1 : CTX_MAG); if (mq_dec(q, cw, Ls.tab, cx)) B2 |= bx; M2 |= bx; }
-                    if (c3 & bx) { uint32_t cx = (M3 & bx) ? CTX_MAG + 2 : (f9(S3, S4, S5, x) ? CTX_MAG + 1 : CTX_MAG); if (mq_dec(q, cw, Ls.tab, cx)) B3 |= bx; M3 |= bx; }
-                }
-                ST[ST_MU + y0] = M0; BITS[y0] = B0;
-                if (nr > 1) { ST[ST_MU + y0 + 1] = M1; BITS[y0 + 1] = B1; }
-                if (nr > 2) { ST[ST_MU + y0 + 2] = M2; BITS[y0 + 2] = B2; }
-                if (nr > 3) { ST[ST_MU + y0 + 3] = M3; BITS[y0 + 3] = B3; }
-            }
-            if (++pass >= npasses) break;
         }
-        // ---------------- cleanup (T1.cpp:974-1093)
-        for (uint32_t s = 0; s < nstripes; ++s) {
-            const uint32_t y0 = 4 * s, nr = h - y0 < 4 ? h - y0 : 4;
-            uint64_t S0 = ST[ST_SIG + y0], S1 = ST[ST_SIG + y0 + 1], S2 = ST[ST_SIG + y0 + 2],
-                     S3 = ST[ST_SIG + y0 + 3], S4 = ST[ST_SIG + y0 + 4], S5 = ST[ST_SIG + y0 + 5];
-            uint64_t N0 = ST[ST_NEG + y0], N1 = ST[ST_NEG + y0 + 1], N2 = ST[ST_NEG + y0 + 2],
-                     N3 = ST[ST_NEG + y0 + 3], N4 = ST[ST_NEG + y0 + 4], N5 = ST[ST_NEG + y0 + 5];
-            uint64_t P0 = first ? 0 : ST[ST_PI + y0];
-            uint64_t P1 = nr > 1 ? (first ? 0 : ST[ST_PI + y0 + 1]) : ~0ull;
-            uint64_t P2 = nr > 2 ? (first ? 0 : ST[ST_PI + y0 + 2]) : ~0ull;
-            uint64_t P3 = nr > 3 ? (first ? 0 : ST[ST_PI + y0 + 3]) : ~0ull;
-            uint64_t B0 = first ? 0 : BITS[y0], B1 = (nr > 1 && !first) ? BITS[y0 + 1] : 0,
-                     B2 = (nr > 2 && !first) ? BITS[y0 + 2] : 0, B3 = (nr > 3 && !first) ? BITS[y0 + 3] : 0;
-            uint64_t cols = ((~S1 & ~P0) | (~S2 & ~P1) | (~S3 & ~P2) | (~S4 & ~P3)) & colmask;
-            while (cols) {
-                const uint32_t x = (uint32_t)__ffsll((long long)cols) - 1;
-                const uint64_t bx = 1ull << x;
-                cols &= cols - 1;
-                uint32_t start = 0;
-                if (nr == 4 && !((S1 | S2 | S3 | S4 | P0 | P1 | P2 | P3) & bx) && !f9(S0, S1, S2, x) &&
-                    !f9(S1, S2, S3, x) && !f9(S2, S3, S4, x) && !f9(S3, S4, S5, x)) {
-                    // run-length mode
-                    if (!mq_dec(q, cw, Ls.tab, CTX_AGG)) continue;
-                    uint32_t rl = mq_dec(q, cw, Ls.tab, CTX_UNI);
-                    rl = (rl << 1) | mq_dec(q, cw, Ls.tab, CTX_UNI);
-                    if (rl == 0) SIG_DECODE(S0, S1, S2, N0, N1, N2, B0)
-                    else if (rl == 1) SIG_DECODE(S1, S2, S3, N1, N2, N3, B1)
-                    else if (rl == 2) SIG_DECODE(S2, S3, S4, N2, N3, N4, B2)
-                    else SIG_DECODE(S3, S4, S5, N3, N4, N5, B3)
-                    start = rl + 1;
-                }
-                if (start <= 0 && !((S1 | P0) & bx)) { if (mq_dec(q, cw, Ls.tab, zc[f9(S0, S1, S2, x)])) SIG_DECODE(S0, S1, S2, N0, N1, N2, B0); }
-                if (start <= 1 && !((S2 | P1) & bx)) { if (mq_dec(q, cw, Ls.tab, zc[f9(S1, S2, S3, x)])) SIG_DECODE(S1, S2, S3, N1, N2, N3, B1); }
-                if (start <= 2 && !((S3 | P2) & bx)) { if (mq_dec(q, cw, Ls.tab, zc[f9(S2, S3, S4, x)])) SIG_DECODE(S2, S3, S4, N2, N3, N4, B2); }
-                if (start <= 3 && !((S4 | P3) & bx)) { if (mq_dec(q, cw, Ls.tab, zc[f9(S3, S4, S5, x)])) SIG_DECODE(S3, S4, S5, N3, N4, N5, B3); }
-            }
-            ST[ST_SIG + y0 + 1] = S1; ST[ST_NEG + y0 + 1] = N1; BITS[y0] = B0;
-            if (nr > 1) { ST[ST_SIG + y0 + 2] = S2; ST[ST_NEG + y0 + 2] = N2; BITS[y0 + 1] = B1; }
-            if (nr > 2) { ST[ST_SIG + y0 + 3] = S3; ST[ST_NEG + y0 + 3] = N3; BITS[y0 + 2] = B2; }
-            if (nr > 3) { ST[ST_SIG + y0 + 4] = S4; ST[ST_NEG + y0 + 4] = N4; BITS[y0 + 3] = B3; }
-        }
-        ++pass;
+    }
+    if (stats) {
+        unsigned long long tot = L.nsym;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        if (lane == 0) { atomicAdd(&stats[0], (unsigned long long)L.step); atomicAdd(&stats[1], tot);
+                         atomicMax(&stats[2], (unsigned long long)L.step); }
     }
 }
 
 // Reconstruction + dequantisation: wave per block, lane = column.
-__global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blocks,
+__global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blocks, const uint32_t* __restrict__ pos,
                                                  const uint64_t* __restrict__ scratch,
-                                                 const uint64_t* __restrict__ st_off, int32_t* __restrict__ coef,
+                                                 const uint64_t* __restrict__ wave_off, int32_t* __restrict__ coef,
                                                  uint32_t nblocks) {
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
     const int x = threadIdx.x;
     const GkBlock B = blocks[b];
     if (x >= (int)B.w) return;
-    const uint64_t* ST = scratch + st_off[b];
+    const uint32_t slot = pos[b], ln = slot & 63;
+    const uint64_t* WS = scratch + wave_off[slot >> 6];
     const bool irrev = B.flags & 1;
     float* fcoef = reinterpret_cast<float*>(coef);
     const uint32_t numbps = B.numbps, npasses = B.npasses;
-    // last decoded pass: k = npasses-1; pass k>0 belongs to plane P0-(k+2)/3, type (k+2)%3
+    // last decoded pass k = npasses-1: pass k>0 belongs to plane numbps-1-(k+2)/3, type (k+2)%3
     int bpl = 0, t = 2;
     if (npasses && numbps) {
         int k = (int)npasses - 1;
@@ -284,13 +514,13 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
         if (npasses && numbps) {
             uint32_t M = 0;
             for (int p = (int)numbps - 1; p >= bpl; --p) {
-                uint64_t row = ST[ST_BITS + (size_t)(numbps - 1 - p) * 64 + y];
+                uint64_t row = WS[(WS_BITS + (size_t)(numbps - 1 - p) * 64 + y) * 64 + ln];
                 M |= (uint32_t)((row >> x) & 1) << p;
             }
             if (M) {
                 int qq = (t == 0 && (M >> (bpl + 1)) != 0) ? bpl + 1 : bpl;
                 int32_t mag = (int32_t)(((M >> qq) << 1 | 1) << qq);
-                bool ng = (ST[ST_NEG + y + 1] >> x) & 1;
+                bool ng = (WS[(WS_NEG + y + 1) * 64 + ln] >> x) & 1;
                 v = ng ? -mag : mag;
             }
         }
@@ -301,13 +531,25 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
 }
 
 #include "gk_launch.h"
-void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, uint64_t* scratch,
-                      const uint64_t* st_off, uint32_t nblocks) {
+void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
+                      uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_t1_dec, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, scratch, st_off, nblocks);
+    static unsigned long long* stats = nullptr;
+    const bool want = getenv("GK_T1_STATS") != nullptr;
+    if (want && !stats) { (void)hipMalloc(&stats, 64); }
+    if (want) (void)hipMemsetAsync(stats, 0, 64, st);
+    hipLaunchKernelGGL(k_t1_dec, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch, wave_off,
+                       nblocks, want ? stats : nullptr);
+    if (want) {
+        unsigned long long h[3];
+        (void)hipMemcpyAsync(h, stats, 24, hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f\n",
+                (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]));
+    }
 }
-void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint64_t* scratch, const uint64_t* st_off,
-                        int32_t* coef, uint32_t nblocks) {
+void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* pos, const uint64_t* scratch,
+                        const uint64_t* wave_off, int32_t* coef, uint32_t nblocks) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_t1_recon, dim3(nblocks), dim3(64), 0, st, blocks, scratch, st_off, coef, nblocks);
+    hipLaunchKernelGGL(k_t1_recon, dim3(nblocks), dim3(64), 0, st, blocks, pos, scratch, wave_off, coef, nblocks);
 }

@@ -312,8 +312,13 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
 }
 
 // ---------------------------------------------------------------------------
-// MQ coder, one lane per code-block.  Context states live in registers
-// (5 x 32-bit words, one byte per context: state | mps << 6).
+// MQ coder (Annex C.2; mqc_enc.cpp:86-330), one lane per code-block.
+// Every lane codes exactly one symbol per step, so all lanes of a wave sit at
+// the same symbol index: the 16-symbol chunks of every lane are fetched at the
+// same (uniform) steps, two chunks ahead, and the loop is unrolled by 16 so a
+// fetch is consumed 32 steps after it was issued.  Pass boundaries come from a
+// per-lane copy of the pass-end table in LDS.  Context states live in VGPRs
+// (one byte per context: state | mps << 6).
 // ---------------------------------------------------------------------------
 struct MqLane {
     uint32_t a, c, ct;
@@ -324,6 +329,13 @@ struct MqLane {
     uint32_t cap;
     uint32_t ovf;
 };
+
+__device__ __forceinline__ uint32_t vsel_e(bool c, uint32_t a, uint32_t b) {
+    uint64_t m = __ballot(c);
+    uint32_t r;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
 
 __device__ __forceinline__ void mql_emit(MqLane& q, uint32_t nb) {
     if (q.bp >= 0) {
@@ -345,6 +357,46 @@ __device__ __forceinline__ void mql_byteout(MqLane& q) {
     }
 }
 
+struct Ctx5e { uint32_t w0, w1, w2, w3, w4; };
+
+// CODEMPS / CODELPS + RENORME for symbol s = (ctx << 1) | d, predicated on `en`
+__device__ __forceinline__ void mq_code(MqLane& q, Ctx5e& cw, const uint32_t* tab, uint32_t s, bool en) {
+    const uint32_t cx = s >> 1, d = s & 1;
+    const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
+    uint32_t word = vsel_e(wi == 4, cw.w4, vsel_e(wi & 2, vsel_e(wi & 1, cw.w3, cw.w2), vsel_e(wi & 1, cw.w1, cw.w0)));
+    const uint32_t st = (word >> shb) & 0xff;
+    const uint32_t mps = st >> 6;
+    const uint32_t e = tab[st & 63];
+    const uint32_t qe = e & 0xffff;
+    const uint32_t a1 = q.a - qe;
+    const bool is_mps = mps == d;
+    const bool fast = is_mps && (a1 & 0x8000);          // MPS without renormalisation
+    // CODEMPS: A < Qe ? A = Qe : C += Qe ; CODELPS: A < Qe ? C += Qe : A = Qe
+    const bool addc = fast || (is_mps ? !(a1 < qe) : (a1 < qe));
+    const uint32_t anew = fast ? a1 : (is_mps ? (a1 < qe ? qe : a1) : (a1 < qe ? a1 : qe));
+    const uint32_t nst = is_mps ? (((e >> 16) & 0x3f) | (mps << 6)) : (((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6));
+    const bool upd = en && !fast;
+    q.c += (en && addc) ? qe : 0u;
+    q.a = en ? anew : q.a;
+    word = (word & ~(0xffu << shb)) | (nst << shb);
+    cw.w0 = vsel_e(upd && wi == 0, word, cw.w0); cw.w1 = vsel_e(upd && wi == 1, word, cw.w1);
+    cw.w2 = vsel_e(upd && wi == 2, word, cw.w2); cw.w3 = vsel_e(upd && wi == 3, word, cw.w3);
+    cw.w4 = vsel_e(upd && wi == 4, word, cw.w4);
+    uint32_t n = upd ? __clz(q.a) - 16 : 0u;
+    while (__any(n != 0)) {
+        if (n) {
+            const uint32_t k = n < q.ct ? n : q.ct;
+            q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
+            if (q.ct == 0) mql_byteout(q);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t j) {
+    const uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
+    return (w >> (8 * (j & 3))) & 0xff;
+}
+
 // Outputs: info[4b..4b+3] = (numbps, npasses, bytes, offset of the block's
 // passes in `passes`); pass records are packed (atomic offset allocation) so
 // the host copies only the passes that exist.  With rate control the
@@ -356,17 +408,21 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
                                               uint32_t nblocks, int* err, const int32_t* __restrict__ pass_nmse,
                                               uint32_t* __restrict__ pass_counter) {
     __shared__ uint32_t tab[47];
+    __shared__ uint32_t pe_lds[GK_MAX_PASSES + 1][64];
     const int lane = threadIdx.x;
     if (lane < 47) tab[lane] = c_mq[lane];
-    __syncthreads();
     const uint32_t b = blockIdx.x * 64 + lane;
-    if (b >= nblocks) return;
-    const uint32_t numbps = cm_info[2 * b], npasses = cm_info[2 * b + 1];
-    if (npasses == 0) { info[4 * b] = 0; info[4 * b + 1] = 0; info[4 * b + 2] = 0; info[4 * b + 3] = 0; return; }
-    const GkBlock B = blocks[b];
-    const uint8_t* sp = sym + sym_off[b];
-    const uint32_t* PE = pass_end + (size_t)b * GK_MAX_PASSES;
-    const uint32_t poff = atomicAdd(pass_counter, npasses);
+    const bool has = b < nblocks;
+    const uint32_t numbps = has ? cm_info[2 * b] : 0, npasses = has ? cm_info[2 * b + 1] : 0;
+    const uint32_t* PE = pass_end + (size_t)(has ? b : 0) * GK_MAX_PASSES;
+    for (uint32_t p = 0; p < npasses; ++p) pe_lds[p][lane] = PE[p];
+    pe_lds[npasses][lane] = 0xffffffffu;
+    const uint32_t nsym = npasses ? PE[npasses - 1] : 0;
+    GkBlock B = {};
+    if (has) B = blocks[b];
+    const uint8_t* sp = sym + (has ? sym_off[b] : 0);
+    uint32_t poff = 0;
+    if (npasses) poff = atomicAdd(pass_counter, npasses);
     GkPass* P = passes + poff;
     const bool rc = (B.flags & 2) != 0;
     double cum = 0.0;
@@ -374,74 +430,62 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
     q.a = 0x8000; q.c = 0; q.ct = 12; q.bp = -1; q.cur = 0; q.wbuf = 0; q.out = bytes + B.data_off; q.cap = B.data_cap;
     q.ovf = 0;
     // initial context states (mqc_resetstates): ZC ctx0 -> 4, AGG -> 3, UNI -> 46
-    uint32_t cw[5] = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};   // ctx 17 = byte 1 of word 4, ctx 18 = byte 2
-    uint32_t i = 0;
-    // 16-byte symbol chunks, double-buffered so the next load is in flight while
-    // the current 16 symbols are coded (sym_off is 256-byte aligned).
-    uint4 cur4 = *(const uint4*)(sp), nxt4 = *(const uint4*)(sp + 16);
-    for (uint32_t p = 0; p < npasses; ++p) {
-        const uint32_t end = PE[p];
-        for (; i < end; ++i) {
-            const uint32_t j = i & 15;
-            const uint32_t wsel = j >> 2;
-            const uint32_t wv = wsel == 0 ? cur4.x : wsel == 1 ? cur4.y : wsel == 2 ? cur4.z : cur4.w;
-            const uint32_t s = (wv >> (8 * (j & 3))) & 0xff;
-            if (j == 15) { cur4 = nxt4; nxt4 = *(const uint4*)(sp + i + 17); }
-            const uint32_t cx = s >> 1, d = s & 1;
-            const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
-            uint32_t word = wi == 0 ? cw[0] : wi == 1 ? cw[1] : wi == 2 ? cw[2] : wi == 3 ? cw[3] : cw[4];
-            const uint32_t st = (word >> shb) & 0xff;
-            const uint32_t idx = st & 63, mps = st >> 6;
-            const uint32_t e = tab[idx];
-            const uint32_t qe = e & 0xffff;
-            uint32_t nst = st;
-            bool renorm = true;
-            q.a -= qe;
-            if (mps == d) {
-                if (q.a & 0x8000) { q.c += qe; renorm = false; }
-                else {
-                    if (q.a < qe) q.a = qe; else q.c += qe;
-                    nst = ((e >> 16) & 0x3f) | (mps << 6);
+    Ctx5e cw = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};
+    uint32_t maxsym = nsym;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) maxsym = max(maxsym, (uint32_t)__shfl_xor((int)maxsym, o));
+    __syncthreads();
+    uint32_t p = 0, next_end = pe_lds[0][lane];
+    // pass bookkeeping (T1.cpp:856-897); only the last pass is terminated (default style)
+    auto close_passes = [&](uint32_t i) {
+        while (__any(npasses && p < npasses && next_end == i)) {
+            if (npasses && p < npasses && next_end == i) {
+                if (p == npasses - 1) {
+                    uint32_t tempc = q.c + q.a;
+                    q.c |= 0xffff;
+                    if (q.c >= tempc) q.c -= 0x8000;
+                    q.c <<= q.ct; mql_byteout(q);
+                    q.c <<= q.ct; mql_byteout(q);
+                    if (q.cur != 0xff) mql_emit(q, 0);
+                    P[p].rate = (uint32_t)q.bp;
+                } else {
+                    P[p].rate = (uint32_t)q.bp + 5 + (q.ct < 5 ? 1 : 0);
                 }
-            } else {
-                if (q.a < qe) q.c += qe; else q.a = qe;
-                nst = ((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6);
-            }
-            if (renorm) {
-                word = (word & ~(0xffu << shb)) | (nst << shb);
-                if (wi == 0) cw[0] = word; else if (wi == 1) cw[1] = word; else if (wi == 2) cw[2] = word;
-                else if (wi == 3) cw[3] = word; else cw[4] = word;
-                uint32_t n = __clz(q.a) - 16;
-                q.a <<= n;
-                while (n >= q.ct) { q.c <<= q.ct; n -= q.ct; mql_byteout(q); }
-                q.c <<= n; q.ct -= n;
+                if (rc) {
+                    const int bpno = p == 0 ? (int)numbps - 1 : (int)numbps - 2 - (int)(p - 1) / 3;
+                    double wm = B.wmse * (double)(1 << bpno);
+                    wm *= wm * (double)pass_nmse[(size_t)b * GK_MAX_PASSES + p] / 8192.0;
+                    cum += wm;
+                }
+                P[p].dist = cum;
+                ++p;
+                next_end = pe_lds[p][lane];
             }
         }
-        // pass bookkeeping (T1.cpp:856-897); only the last pass is terminated (default style)
-        if (p == npasses - 1) {
-            uint32_t tempc = q.c + q.a;
-            q.c |= 0xffff;
-            if (q.c >= tempc) q.c -= 0x8000;
-            q.c <<= q.ct; mql_byteout(q);
-            q.c <<= q.ct; mql_byteout(q);
-            if (q.cur != 0xff) mql_emit(q, 0);
-            P[p].rate = (uint32_t)q.bp;
-        } else {
-            P[p].rate = (uint32_t)q.bp + 5 + (q.ct < 5 ? 1 : 0);
+    };
+    close_passes(0);   // passes without symbols before the first one
+    uint4 cur4 = make_uint4(0, 0, 0, 0), nxt4 = make_uint4(0, 0, 0, 0);
+    if (nsym) cur4 = *(const uint4*)(sp);
+    if (nsym > 16) nxt4 = *(const uint4*)(sp + 16);
+    for (uint32_t base = 0; base < maxsym; base += 16) {
+        uint4 pre = make_uint4(0, 0, 0, 0);
+        if (base + 32 < nsym) pre = *(const uint4*)(sp + base + 32);
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) {
+            const uint32_t i = base + j;
+            const bool en = i < nsym;
+            mq_code(q, cw, tab, byte_of(cur4, j), en);
+            close_passes(i + 1);
         }
-        if (rc) {
-            const int bpno = p == 0 ? (int)numbps - 1 : (int)numbps - 2 - (int)(p - 1) / 3;
-            double wm = B.wmse * (double)(1 << bpno);
-            wm *= wm * (double)pass_nmse[(size_t)b * GK_MAX_PASSES + p] / 8192.0;
-            cum += wm;
-        }
-        P[p].dist = cum;
+        cur4 = nxt4; nxt4 = pre;
     }
     // flush the partial output word (bytes [bp & ~3, bp) plus the pending byte)
-    if (q.bp >= 0 && (uint32_t)q.bp < q.cap) {
+    if (npasses && q.bp >= 0 && (uint32_t)q.bp < q.cap) {
         q.wbuf |= q.cur << (8 * (q.bp & 3));
         *(uint32_t*)(q.out + (q.bp & ~3)) = q.wbuf;
     }
+    if (!has) return;
+    if (npasses == 0) { info[4 * b] = 0; info[4 * b + 1] = 0; info[4 * b + 2] = 0; info[4 * b + 3] = 0; return; }
     __threadfence();
     const uint32_t nbytes = (uint32_t)q.bp;
     uint32_t last = nbytes;
