@@ -347,15 +347,21 @@ __device__ __forceinline__ void mql_emit(MqLane& q, uint32_t nb) {
     q.bp++;
     q.cur = nb & 0xff;
 }
-__device__ __forceinline__ void mql_byteout(MqLane& q) {
-    if (q.cur == 0xff) { mql_emit(q, q.c >> 20); q.c &= 0xfffff; q.ct = 7; }
-    else if ((q.c & 0x8000000) == 0) { mql_emit(q, q.c >> 19); q.c &= 0x7ffff; q.ct = 8; }
-    else {
-        q.cur++;
-        if (q.cur == 0xff) { q.c &= 0x7ffffff; mql_emit(q, q.c >> 20); q.c &= 0xfffff; q.ct = 7; }
-        else { mql_emit(q, q.c >> 19); q.c &= 0x7ffff; q.ct = 8; }
+// BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127), branch-free except the word store
+__device__ __forceinline__ void mql_byteout_if(MqLane& q, bool en) {
+    const bool carry = q.cur != 0xff && (q.c & 0x8000000);
+    const uint32_t cur = q.cur + (carry ? 1u : 0u);
+    const uint32_t c = carry ? (q.c & 0x7ffffff) : q.c;
+    const bool ff = cur == 0xff;
+    const uint32_t nb = ff ? (c >> 20) : (c >> 19);
+    if (en) {
+        q.cur = cur;
+        q.c = c & (ff ? 0xfffffu : 0x7ffffu);
+        q.ct = ff ? 7u : 8u;
+        mql_emit(q, nb);
     }
 }
+__device__ __forceinline__ void mql_byteout(MqLane& q) { mql_byteout_if(q, true); }
 
 struct Ctx5e { uint32_t w0, w1, w2, w3, w4; };
 
@@ -384,11 +390,9 @@ __device__ __forceinline__ void mq_code(MqLane& q, Ctx5e& cw, const uint32_t* ta
     cw.w4 = vsel_e(upd && wi == 4, word, cw.w4);
     uint32_t n = upd ? __clz(q.a) - 16 : 0u;
     while (__any(n != 0)) {
-        if (n) {
-            const uint32_t k = n < q.ct ? n : q.ct;
-            q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
-            if (q.ct == 0) mql_byteout(q);
-        }
+        const uint32_t k = n < q.ct ? n : q.ct;
+        q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
+        mql_byteout_if(q, k != 0 && q.ct == 0);
     }
 }
 
