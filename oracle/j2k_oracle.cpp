@@ -47,6 +47,8 @@ struct Params {
     uint32_t nlayers = 1;
     double rates[100] = {0};    // grk_cparameters::layer_rate (compression ratios; 0 = all remaining passes)
     int write_com = 1;
+    uint32_t cblk_sty = 0;      // 0x40 = HTJ2K block coder (GRK_CBLKSTY_HT, grok.h:104)
+    bool ht() const { return (cblk_sty & 0x40) != 0; }
     Params() { for (int i = 0; i < 33; ++i) { prcw_exp[i] = 15; prch_exp[i] = 15; } }
 };
 
@@ -196,6 +198,22 @@ static double getnorm(uint32_t level, uint32_t orient, bool rev) {  // T1.cpp:26
     return rev ? dwt_norms_53[orient][level] : dwt_norms_97[orient][level];
 }
 
+// BIBO gains of the 5/3 synthesis (HTParams.cpp:134-145), used by the HT
+// reversible QCD.
+static const float bibo53_l[16] = {1.0000f, 1.5000f, 1.6250f, 1.6875f, 1.6963f, 1.7067f, 1.7116f, 1.7129f,
+                                   1.7141f, 1.7145f, 1.7151f, 1.7152f, 1.7155f, 1.7155f, 1.7156f, 1.7156f};
+static const float bibo53_h[16] = {2.0000f, 2.5000f, 2.7500f, 2.8047f, 2.8198f, 2.8410f, 2.8558f, 2.8601f,
+                                   2.8628f, 2.8656f, 2.8662f, 2.8667f, 2.8669f, 2.8670f, 2.8671f, 2.8671f};
+static uint32_t ht_rev_expn(uint32_t B, uint32_t ndecomp, uint32_t r, uint32_t orient) {
+    auto L = [](uint32_t i) { return bibo53_l[std::min(i, 15u)]; };
+    auto H = [](uint32_t i) { return bibo53_h[std::min(i, 15u)]; };
+    auto X = [](float g) { return (int)ceil(log(g * 1.1f) / 0.69314718055994530942); };
+    if (r == 0) return (uint32_t)((int)B + X(L(ndecomp) * L(ndecomp)));
+    uint32_t d = ndecomp - r;   // OpenJPH level index of this resolution's bands
+    if (orient == 3) return (uint32_t)((int)B + X(H(d) * H(d)));
+    return (uint32_t)((int)B + X(H(d) * L(d + 1)));
+}
+
 static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress,
                          const std::vector<std::pair<uint32_t,uint32_t>>* qcd) {
     // qcd: per band (expn, mant) in band order LL, (HL,LH,HH) per resolution, when decoding.
@@ -211,6 +229,12 @@ static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress,
                     expn = (*qcd)[0].first - (p.numres - 1) + (nb - 1) + 0;  // rarely used
                     (void)nb;
                 }
+            } else if (p.ht() && !p.irreversible) {
+                // param_qcd::set_rev_quant (HTParams.cpp:253-272): B + ceil(log2(bibo^2 * 1.1)).
+                // Grok passes tcp->mct before it is assigned (CodeStreamCompress.cpp:382 vs the
+                // later mct setup), so the RCT bit is never added: B = precision.
+                expn = ht_rev_expn(prec, p.numres - 1, r, B.orient);
+                mant = 0;
             } else {
                 uint32_t level = p.numres - 1 - r;
                 uint32_t gain = p.irreversible ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
@@ -934,11 +958,17 @@ struct Image {
 static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Params& p, const Comp& c0) {
     put16(o, 0xff4f);                               // SOC
     put16(o, 0xff51); put16(o, 38 + 3 * im.nc);     // SIZ
-    put16(o, 0);                                    // Rsiz
+    put16(o, p.ht() ? 0x4000 : 0);                  // Rsiz (GRK_JPH_RSIZ_FLAG for HT, CodeStreamCompress.cpp:216-219)
     put32(o, im.w); put32(o, im.h); put32(o, 0); put32(o, 0);
     put32(o, im.w); put32(o, im.h); put32(o, 0); put32(o, 0);
     put16(o, im.nc);
     for (uint32_t i = 0; i < im.nc; ++i) { o.push_back((uint8_t)((im.prec - 1) | (im.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
+    if (p.ht()) {                                   // CAP (CodeStreamCompress::write_cap :1064-1111)
+        uint32_t B = 0;
+        for (uint32_t r = 0; r < p.numres; ++r) for (auto& Bd : c0.res[r].bands) B = std::max(B, Bd.expn + p.numgbits - 1);
+        uint32_t Bp = B <= 8 ? 0 : B < 28 ? B - 8 : B < 48 ? 13 + (B >> 2) : 31;
+        put16(o, 0xff50); put16(o, 8); put32(o, 0x00020000); put16(o, (p.irreversible ? 0x20 : 0) | Bp);
+    }
     bool custom_prc = false;
     for (uint32_t r = 0; r < p.numres; ++r) if (p.prcw_exp[r] != 15 || p.prch_exp[r] != 15) custom_prc = true;
     put16(o, 0xff52); put16(o, 12 + (custom_prc ? p.numres : 0));  // COD
@@ -948,7 +978,7 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
     o.push_back((uint8_t)((p.mct && im.nc >= 3) ? 1 : 0));
     o.push_back((uint8_t)(p.numres - 1));
     o.push_back((uint8_t)(p.cbw_exp - 2)); o.push_back((uint8_t)(p.cbh_exp - 2));
-    o.push_back(0);                                 // cblk style
+    o.push_back((uint8_t)p.cblk_sty);               // cblk style
     o.push_back(p.irreversible ? 0 : 1);
     if (custom_prc) for (uint32_t r = 0; r < p.numres; ++r) o.push_back((uint8_t)(p.prcw_exp[r] | (p.prch_exp[r] << 4)));
     uint32_t nbands = 3 * p.numres - 2;              // QCD
@@ -1052,6 +1082,362 @@ static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t 
     return true;
 }
 
+
+// ----------------------------------------------------------------------------
+// HTJ2K block coder, cleanup pass only (ISO/IEC 15444-15; Grok calls OpenJPH
+// 0.7.2: ojph_encode_codeblock ojph_block_encoder.cpp:470-947, decode
+// ojph_block_decoder.cpp:989-1700).  Restated from the standard's structure:
+// quads of 2x2 samples scanned in pairs along 2-row stripes; per quad the
+// significance pattern rho and the EMB pattern are CxtVLC coded (backward VLC
+// segment), the exponent offsets u_q are U-VLC coded (same segment), zero
+// contexts use the adaptive MEL run coder, magnitudes/signs go to the forward
+// MagSgn segment.  The segment layout and termination follow OpenJPH so the
+// bytes are identical to Grok's.
+// ----------------------------------------------------------------------------
+#include "ht_tables.h"
+
+static const int MEL_EXP[13] = {0, 0, 0, 1, 1, 1, 2, 2, 2, 3, 3, 4, 5};
+
+struct HtMelEnc {
+    std::vector<uint8_t> b; int rem = 8, tmp = 0, run = 0, k = 0, thr = 1;
+    void bit(int v) {
+        tmp = (tmp << 1) + v;
+        if (--rem == 0) { b.push_back((uint8_t)tmp); rem = (tmp == 0xFF) ? 7 : 8; tmp = 0; }
+    }
+    void code(bool e) {
+        if (!e) {
+            if (++run >= thr) { bit(1); run = 0; k = std::min(12, k + 1); thr = 1 << MEL_EXP[k]; }
+        } else {
+            bit(0);
+            for (int t = MEL_EXP[k]; t > 0;) bit((run >> --t) & 1);
+            run = 0; k = std::max(0, k - 1); thr = 1 << MEL_EXP[k];
+        }
+    }
+};
+struct HtVlcEnc {   // grows backward; b holds bytes in emission order
+    std::vector<uint8_t> b; int used = 4, tmp = 0xF; bool gt8f = true;
+    void code(int cwd, int len) {
+        while (len > 0) {
+            int avail = 8 - (gt8f ? 1 : 0) - used;
+            int t = std::min(avail, len);
+            tmp |= (cwd & ((1 << t) - 1)) << used;
+            used += t; avail -= t; len -= t; cwd >>= t;
+            if (avail == 0) {
+                if (gt8f && tmp != 0x7F) { gt8f = false; continue; }
+                b.push_back((uint8_t)tmp); gt8f = tmp > 0x8F; tmp = 0; used = 0;
+            }
+        }
+    }
+};
+struct HtMsEnc {
+    std::vector<uint8_t> b; int maxb = 8, used = 0; uint32_t tmp = 0;
+    void code(uint32_t cwd, int len) {
+        while (len > 0) {
+            int t = std::min(maxb - used, len);
+            tmp |= (cwd & ((1u << t) - 1)) << used;
+            used += t; cwd >>= t; len -= t;
+            if (used >= maxb) { b.push_back((uint8_t)tmp); maxb = (tmp == 0xFF) ? 7 : 8; tmp = 0; used = 0; }
+        }
+    }
+    void terminate() {
+        if (used) {
+            int t = maxb - used;
+            tmp |= (0xFFu & ((1u << t) - 1)) << used;
+            if (tmp != 0xFF) b.push_back((uint8_t)tmp);
+        } else if (maxb == 7) b.pop_back();
+    }
+};
+// U-VLC prefix/suffix codes for u in 0..32 (Annex C, OpenJPH uvlc tables)
+static void uvlc_code(int u, int& pre, int& pre_len, int& suf, int& suf_len) {
+    static const int P[5] = {0, 1, 2, 4, 4}, PL[5] = {0, 1, 2, 3, 3}, S[5] = {0, 0, 0, 0, 1}, SL[5] = {0, 0, 0, 1, 1};
+    if (u < 5) { pre = P[u]; pre_len = PL[u]; suf = S[u]; suf_len = SL[u]; }
+    else { pre = 0; pre_len = 3; suf = u - 5; suf_len = 5; }
+}
+
+// coef: signed integer coefficients (HT reversible: the full magnitude is coded)
+static std::vector<uint8_t> ht_encode_block(const int32_t* coef, uint32_t w, uint32_t h, uint32_t stride) {
+    HtMelEnc mel; HtVlcEnc vlc; HtMsEnc ms;
+    std::vector<uint8_t> e_val(w / 2 + 4, 0), cx_val(w / 2 + 4, 0);
+    auto sample = [&](uint32_t x, uint32_t y, int& rho, int bit, int& e, uint32_t& sv, int& emax) {
+        if (x >= w || y >= h) return;
+        int32_t v = coef[(size_t)y * stride + x];
+        uint32_t mu = (uint32_t)(v < 0 ? -v : v);
+        if (!mu) return;
+        rho |= bit;
+        e = 32 - __builtin_clz(2 * mu - 1);
+        emax = std::max(emax, e);
+        sv = 2 * mu - 2 + (v < 0 ? 1u : 0u);
+    };
+    auto uvlc = [&](int u) { int a, b, c, d; uvlc_code(u, a, b, c, d); vlc.code(a, b); };
+    auto uvlc_suf = [&](int u) { int a, b, c, d; uvlc_code(u, a, b, c, d); vlc.code(c, d); };
+    auto ms_quad = [&](int rho, int Uq, uint16_t tup, const uint32_t* sv) {
+        for (int n = 0; n < 4; ++n) {
+            int m = (rho >> n & 1) ? Uq - ((tup >> n) & 1) : 0;
+            ms.code(sv[n] & ((1u << m) - 1), m);
+        }
+    };
+    int c_q0 = 0;
+    for (uint32_t y = 0; y < h; y += 2) {
+        const bool first = y == 0;
+        const uint16_t* tbl = first ? HT_VLC_ENC0 : HT_VLC_ENC1;
+        int max_e = 0;
+        if (!first) { max_e = std::max(e_val[0], e_val[1]) - 1; e_val[0] = 0; c_q0 = cx_val[0] + (cx_val[1] << 2); cx_val[0] = 0; }
+        else { e_val[0] = 0; cx_val[0] = 0; }
+        size_t li = 0;   // line-state index (one entry per column pair)
+        for (uint32_t x = 0; x < w; x += 4) {
+            int rho[2] = {0, 0}, emax[2] = {0, 0}, e[8] = {0}; uint32_t sv[8] = {0};
+            sample(x, y, rho[0], 1, e[0], sv[0], emax[0]);
+            sample(x, y + 1, rho[0], 2, e[1], sv[1], emax[0]);
+            sample(x + 1, y, rho[0], 4, e[2], sv[2], emax[0]);
+            sample(x + 1, y + 1, rho[0], 8, e[3], sv[3], emax[0]);
+            int kappa0 = first ? 1 : ((rho[0] & (rho[0] - 1)) ? std::max(1, max_e) : 1);
+            int Uq0 = std::max(emax[0], kappa0), u0 = Uq0 - kappa0, u1 = 0;
+            int eps0 = 0;
+            if (u0 > 0) for (int n = 0; n < 4; ++n) eps0 |= (e[n] == emax[0]) << n;
+            e_val[li] = (uint8_t)std::max<int>(e_val[li], e[1]); ++li;
+            if (!first) max_e = std::max(e_val[li], e_val[li + 1]) - 1;
+            e_val[li] = (uint8_t)e[3];
+            cx_val[li - 1] = (uint8_t)(cx_val[li - 1] | ((rho[0] & 2) >> 1));
+            int c_q1 = first ? 0 : cx_val[li] + (cx_val[li + 1] << 2);
+            cx_val[li] = (uint8_t)((rho[0] & 8) >> 3);
+            uint16_t t0 = tbl[(c_q0 << 8) + (rho[0] << 4) + eps0];
+            vlc.code(t0 >> 8, (t0 >> 4) & 7);
+            if (c_q0 == 0) mel.code(rho[0] != 0);
+            ms_quad(rho[0], Uq0, t0, sv);
+            if (x + 2 < w) {
+                sample(x + 2, y, rho[1], 1, e[4], sv[4], emax[1]);
+                sample(x + 2, y + 1, rho[1], 2, e[5], sv[5], emax[1]);
+                sample(x + 3, y, rho[1], 4, e[6], sv[6], emax[1]);
+                sample(x + 3, y + 1, rho[1], 8, e[7], sv[7], emax[1]);
+                int kappa1 = first ? 1 : ((rho[1] & (rho[1] - 1)) ? std::max(1, max_e) : 1);
+                if (first) c_q1 = (rho[0] >> 1) | (rho[0] & 1);
+                else c_q1 |= ((rho[0] & 4) >> 1) | ((rho[0] & 8) >> 2);
+                int Uq1 = std::max(emax[1], kappa1);
+                u1 = Uq1 - kappa1;
+                int eps1 = 0;
+                if (u1 > 0) for (int n = 0; n < 4; ++n) eps1 |= (e[4 + n] == emax[1]) << n;
+                e_val[li] = (uint8_t)std::max<int>(e_val[li], e[5]); ++li;
+                if (!first) max_e = std::max(e_val[li], e_val[li + 1]) - 1;
+                e_val[li] = (uint8_t)e[7];
+                cx_val[li - 1] = (uint8_t)(cx_val[li - 1] | ((rho[1] & 2) >> 1));
+                if (!first) c_q0 = cx_val[li] + (cx_val[li + 1] << 2);
+                cx_val[li] = (uint8_t)((rho[1] & 8) >> 3);
+                uint16_t t1 = tbl[(c_q1 << 8) + (rho[1] << 4) + eps1];
+                vlc.code(t1 >> 8, (t1 >> 4) & 7);
+                if (c_q1 == 0) mel.code(rho[1] != 0);
+                ms_quad(rho[1], Uq1, t1, sv + 4);
+            }
+            if (first) {
+                if (u0 > 0 && u1 > 0) mel.code(std::min(u0, u1) > 2);
+                if (u0 > 2 && u1 > 2) { uvlc(u0 - 2); uvlc(u1 - 2); uvlc_suf(u0 - 2); uvlc_suf(u1 - 2); }
+                else if (u0 > 2 && u1 > 0) { uvlc(u0); vlc.code(u1 - 1, 1); uvlc_suf(u0); }
+                else { uvlc(u0); uvlc(u1); uvlc_suf(u0); uvlc_suf(u1); }
+                c_q0 = (rho[1] >> 1) | (rho[1] & 1);
+            } else {
+                uvlc(u0); uvlc(u1); uvlc_suf(u0); uvlc_suf(u1);
+                c_q0 |= ((rho[1] & 4) >> 1) | ((rho[1] & 8) >> 2);
+            }
+        }
+        if (first) e_val[li + 1] = 0;
+    }
+    // termination of MEL + VLC (terminate_mel_vlc) and MagSgn
+    if (mel.run > 0) mel.bit(1);
+    mel.tmp = mel.tmp << mel.rem;
+    int mel_mask = (0xFF << mel.rem) & 0xFF, vlc_mask = 0xFF >> (8 - vlc.used);
+    if ((mel_mask | vlc_mask) != 0) {
+        int fuse = mel.tmp | vlc.tmp;
+        if ((((fuse ^ mel.tmp) & mel_mask) | ((fuse ^ vlc.tmp) & vlc_mask)) == 0 && fuse != 0xFF && !vlc.b.empty())
+            mel.b.push_back((uint8_t)fuse);
+        else { mel.b.push_back((uint8_t)mel.tmp); vlc.b.push_back((uint8_t)vlc.tmp); }
+    }
+    ms.terminate();
+    std::vector<uint8_t> out(ms.b);
+    out.insert(out.end(), mel.b.begin(), mel.b.end());
+    for (size_t i = vlc.b.size(); i > 0; --i) out.push_back(vlc.b[i - 1]);
+    out.push_back(0xFF);
+    uint32_t scup = (uint32_t)(mel.b.size() + vlc.b.size() + 1);
+    size_t L = out.size();
+    out[L - 1] = (uint8_t)(scup >> 4);
+    out[L - 2] = (uint8_t)((out[L - 2] & 0xF0) | (scup & 0xF));
+    return out;
+}
+
+// HT cleanup-pass decoder (mirror of ht_encode_block; ISO/IEC 15444-15
+// clause 7; Grok: T1HT::decompress T1HT.cpp:134-187 -> ojph_decode_codeblock).
+// Writes signed coefficients.  Returns false on a malformed segment.
+struct HtMelDec {   // forward, MSB first, bit-unstuffing after 0xFF
+    const uint8_t* p; uint32_t n, pos = 0; int bits = 0; uint32_t cur = 0; bool ff = false;
+    int k = 0, run = 0; bool pending_one = false;
+    int bit() {
+        if (bits == 0) {
+            uint32_t b = pos < n ? p[pos] : 0xFF; ++pos;
+            bits = ff ? 7 : 8; cur = b & ((1u << bits) - 1); ff = b == 0xFF;
+        }
+        --bits; return (cur >> bits) & 1;
+    }
+    int event() {   // next MEL symbol (0 = no significance / "min(u) <= 2")
+        if (run > 0) { --run; return 0; }
+        if (pending_one) { pending_one = false; return 1; }
+        for (;;) {
+            if (bit()) {   // a full run of 2^e zeros
+                int r = 1 << MEL_EXP[k]; k = std::min(12, k + 1);
+                run = r - 1; return 0;
+            }
+            int e = MEL_EXP[k], r = 0;
+            for (int t = 0; t < e; ++t) r = (r << 1) | bit();
+            k = std::max(0, k - 1);
+            if (r == 0) return 1;
+            run = r - 1; pending_one = true; return 0;
+        }
+    }
+};
+struct HtVlcDec {   // backward from the end of the Scup region, LSB first
+    const uint8_t* p; int pos; uint64_t acc = 0; int nb = 0; bool gt8f;
+    void init(const uint8_t* base, uint32_t lcup) {
+        p = base; pos = (int)lcup - 2;
+        uint8_t d = base[lcup - 2];
+        int t = d >> 4;
+        int n = ((t & 7) == 7) ? 3 : 4;
+        acc = (uint64_t)(t & ((1 << n) - 1)); nb = n; gt8f = d > 0x8F;
+        --pos;
+    }
+    void fill() {
+        while (nb <= 56) {
+            uint8_t d = pos >= 0 ? p[pos] : 0; --pos;
+            int n = (gt8f && (d & 0x7F) == 0x7F) ? 7 : 8;
+            acc |= (uint64_t)(d & ((1 << n) - 1)) << nb; nb += n; gt8f = d > 0x8F;
+        }
+    }
+    uint32_t peek(int n) { fill(); return (uint32_t)(acc & ((1ull << n) - 1)); }
+    void skip(int n) { acc >>= n; nb -= n; }
+    uint32_t get(int n) { uint32_t v = peek(n); skip(n); return v; }
+};
+struct HtMsDec {    // forward, LSB first, unstuffing after 0xFF, 0xFF beyond the end
+    const uint8_t* p; uint32_t n, pos = 0; uint64_t acc = 0; int nb = 0; bool ff = false;
+    uint32_t get(int m) {
+        while (nb < m) {
+            uint8_t d = pos < n ? p[pos] : 0xFF; ++pos;
+            int k = ff ? 7 : 8;
+            acc |= (uint64_t)(d & ((1 << k) - 1)) << nb; nb += k; ff = d == 0xFF;
+        }
+        uint32_t v = (uint32_t)(acc & ((1ull << m) - 1)); acc >>= m; nb -= m; return v;
+    }
+};
+static int uvlc_decode_prefix(HtVlcDec& v) {   // returns 1,2,3(→3|4),5(→5+)
+    if (v.get(1)) return 1;
+    if (v.get(1)) return 2;
+    return v.get(1) ? 3 : 5;
+}
+static int uvlc_decode_suffix(HtVlcDec& v, int pre) {
+    if (pre == 3) return 3 + (int)v.get(1);
+    if (pre == 5) return 5 + (int)v.get(5);
+    return pre;
+}
+
+static bool ht_decode_block(const uint8_t* d, uint32_t lcup, uint32_t w, uint32_t h, uint32_t k_msbs,
+                            int32_t* out, uint32_t stride) {
+    for (uint32_t y = 0; y < h; ++y) for (uint32_t x = 0; x < w; ++x) out[(size_t)y * stride + x] = 0;
+    if (lcup < 2) return lcup == 0;
+    uint32_t scup = ((uint32_t)d[lcup - 1] << 4) | (d[lcup - 2] & 0xF);
+    if (scup < 2 || scup > lcup || scup > 4079) return false;
+    uint32_t pcup = lcup - scup;
+    HtMelDec mel; mel.p = d + pcup; mel.n = scup;
+    HtVlcDec vlc; vlc.init(d, lcup);
+    HtMsDec ms; ms.p = d; ms.n = pcup;
+    const int umax = (int)k_msbs + 2;
+    std::vector<uint8_t> e_val(w / 2 + 4, 0), cx_val(w / 2 + 4, 0);
+    auto emit = [&](uint32_t x, uint32_t y, int rho, int bit, int Uq, int ek, int e1, int& e) -> bool {
+        e = 0;
+        if (!(rho & bit)) return true;
+        int m = Uq - ((ek & bit) ? 1 : 0);
+        if (m < 0 || m > 31) return false;
+        uint32_t v = ms.get(m) | ((uint32_t)((e1 & bit) ? 1 : 0) << m);
+        uint32_t mu = (v >> 1) + 1;
+        e = 32 - __builtin_clz(2 * mu - 1);
+        if (x < w && y < h) out[(size_t)y * stride + x] = (v & 1) ? -(int32_t)mu : (int32_t)mu;
+        return true;
+    };
+    int c_q0 = 0;
+    for (uint32_t y = 0; y < h; y += 2) {
+        const bool first = y == 0;
+        const uint16_t* tbl = first ? HT_VLC_DEC0 : HT_VLC_DEC1;
+        int max_e = 0;
+        if (!first) { max_e = std::max(e_val[0], e_val[1]) - 1; e_val[0] = 0; c_q0 = cx_val[0] + (cx_val[1] << 2); cx_val[0] = 0; }
+        else { e_val[0] = 0; cx_val[0] = 0; }
+        size_t li = 0;
+        for (uint32_t x = 0; x < w; x += 4) {
+            int rho[2] = {0, 0}, uoff[2] = {0, 0}, ek[2] = {0, 0}, e1[2] = {0, 0}, u[2] = {0, 0};
+            const bool two = x + 2 < w;
+            // quad 0 significance + EMB
+            auto decode_quad = [&](int cq, int j) {
+                if (cq == 0 && !mel.event()) return;   // insignificant quad, no codeword
+                uint16_t t = tbl[(cq << 7) | vlc.peek(7)];
+                vlc.skip(t & 7);
+                rho[j] = (t >> 4) & 15; uoff[j] = (t >> 3) & 1; e1[j] = (t >> 8) & 15; ek[j] = (t >> 12) & 15;
+            };
+            decode_quad(c_q0, 0);
+            int c_q1 = 0;
+            if (!first) {
+                // context of quad 1 depends only on the previous row and on quad 0
+                c_q1 = cx_val[li + 1] + (cx_val[li + 2] << 2);
+            }
+            // the encoder updates the line state after each quad; replay that order
+            int e_q[8] = {0};
+            auto finish_row_state0 = [&]() {};
+            (void)finish_row_state0;
+            if (two) {
+                if (first) c_q1 = (rho[0] >> 1) | (rho[0] & 1);
+                else c_q1 |= ((rho[0] & 4) >> 1) | ((rho[0] & 8) >> 2);
+                decode_quad(c_q1, 1);
+            }
+            // U-VLC exponent offsets (clause 7.3.6)
+            if (first && uoff[0] && uoff[1]) {
+                if (mel.event()) {
+                    int p0 = uvlc_decode_prefix(vlc), p1 = uvlc_decode_prefix(vlc);
+                    u[0] = uvlc_decode_suffix(vlc, p0) + 2; u[1] = uvlc_decode_suffix(vlc, p1) + 2;
+                } else {
+                    int p0 = uvlc_decode_prefix(vlc);
+                    if (p0 > 2) { u[1] = (int)vlc.get(1) + 1; u[0] = uvlc_decode_suffix(vlc, p0); }
+                    else { int p1 = uvlc_decode_prefix(vlc); u[0] = uvlc_decode_suffix(vlc, p0); u[1] = uvlc_decode_suffix(vlc, p1); }
+                }
+            } else {
+                int p0 = uoff[0] ? uvlc_decode_prefix(vlc) : 0, p1 = uoff[1] ? uvlc_decode_prefix(vlc) : 0;
+                u[0] = uoff[0] ? uvlc_decode_suffix(vlc, p0) : 0; u[1] = uoff[1] ? uvlc_decode_suffix(vlc, p1) : 0;
+            }
+            // quad 0 magnitudes/signs, then line state, as the encoder orders them
+            int kappa0 = first ? 1 : ((rho[0] & (rho[0] - 1)) ? std::max(1, max_e) : 1);
+            int Uq0 = kappa0 + u[0];
+            if (Uq0 > umax && rho[0]) return false;
+            if (!emit(x, y, rho[0], 1, Uq0, ek[0], e1[0], e_q[0]) || !emit(x, y + 1, rho[0], 2, Uq0, ek[0], e1[0], e_q[1]) ||
+                !emit(x + 1, y, rho[0], 4, Uq0, ek[0], e1[0], e_q[2]) || !emit(x + 1, y + 1, rho[0], 8, Uq0, ek[0], e1[0], e_q[3]))
+                return false;
+            e_val[li] = (uint8_t)std::max<int>(e_val[li], e_q[1]); ++li;
+            if (!first) max_e = std::max(e_val[li], e_val[li + 1]) - 1;
+            e_val[li] = (uint8_t)e_q[3];
+            cx_val[li - 1] = (uint8_t)(cx_val[li - 1] | ((rho[0] & 2) >> 1));
+            cx_val[li] = (uint8_t)((rho[0] & 8) >> 3);
+            if (two) {
+                int kappa1 = first ? 1 : ((rho[1] & (rho[1] - 1)) ? std::max(1, max_e) : 1);
+                int Uq1 = kappa1 + u[1];
+                if (Uq1 > umax && rho[1]) return false;
+                if (!emit(x + 2, y, rho[1], 1, Uq1, ek[1], e1[1], e_q[4]) || !emit(x + 2, y + 1, rho[1], 2, Uq1, ek[1], e1[1], e_q[5]) ||
+                    !emit(x + 3, y, rho[1], 4, Uq1, ek[1], e1[1], e_q[6]) || !emit(x + 3, y + 1, rho[1], 8, Uq1, ek[1], e1[1], e_q[7]))
+                    return false;
+                e_val[li] = (uint8_t)std::max<int>(e_val[li], e_q[5]); ++li;
+                if (!first) max_e = std::max(e_val[li], e_val[li + 1]) - 1;
+                e_val[li] = (uint8_t)e_q[7];
+                cx_val[li - 1] = (uint8_t)(cx_val[li - 1] | ((rho[1] & 2) >> 1));
+                if (!first) c_q0 = cx_val[li] + (cx_val[li + 1] << 2);
+                cx_val[li] = (uint8_t)((rho[1] & 8) >> 3);
+            }
+            if (first) c_q0 = (rho[1] >> 1) | (rho[1] & 1);
+            else c_q0 |= ((rho[1] & 4) >> 1) | ((rho[1] & 8) >> 2);
+        }
+        if (first) e_val[li + 1] = 0;
+    }
+    return true;
+}
+
 }  // namespace orc
 
 using namespace orc;
@@ -1065,6 +1451,7 @@ typedef struct {
     uint32_t numres, cbw_exp, cbh_exp, irreversible, mct, nlayers, write_com;
     uint32_t prcw_exp[33], prch_exp[33];
     double layer_rate[100];
+    uint32_t cblk_sty;
 } orc_cparams;
 
 static Params to_params(const orc_cparams* cp) {
@@ -1073,6 +1460,8 @@ static Params to_params(const orc_cparams* cp) {
     p.numres = cp->numres; p.cbw_exp = cp->cbw_exp; p.cbh_exp = cp->cbh_exp;
     p.irreversible = cp->irreversible; p.mct = cp->mct; p.nlayers = cp->nlayers ? cp->nlayers : 1;
     p.write_com = (int)cp->write_com;
+    p.cblk_sty = cp->cblk_sty;
+    if (p.ht()) p.numgbits = 1;   // grk_compress.cpp:1123-1124
     for (uint32_t i = 0; i < 100; ++i) p.rates[i] = i < p.nlayers ? cp->layer_rate[i] : 0.0;
     for (int i = 0; i < 33; ++i) { p.prcw_exp[i] = cp->prcw_exp[i] ? cp->prcw_exp[i] : 15; p.prch_exp[i] = cp->prch_exp[i] ? cp->prch_exp[i] : 15; }
     return p;
@@ -1118,6 +1507,13 @@ static void t1_encode_all(EncodeState& E) {
                 for (auto& P : B.prcs)
                     for (auto& K : P.cblks) {
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
+                        if (E.p.ht()) {   // T1HT::compress (T1HT.cpp:109-133): one cleanup pass
+                            const int32_t* src = E.coefs[c].data() + (size_t)(B.offy + K.y0 - B.y0) * C.w + (B.offx + K.x0 - B.x0);
+                            K.data = ht_encode_block(src, w, h, C.w);
+                            uint32_t L = (uint32_t)K.data.size();
+                            K.numbps = 1; K.npasses = 1; K.passes.assign(1, PassInfo{L, L, 1, 0.0});
+                            continue;
+                        }
                         std::vector<uint32_t> mag(w * h); std::vector<uint8_t> neg(w * h);
                         for (uint32_t y = 0; y < h; ++y)
                             for (uint32_t x = 0; x < w; ++x) {
@@ -1392,6 +1788,17 @@ int orc_t1_encode_cblk(const int32_t* coef, uint32_t w, uint32_t h, uint32_t str
     return (int)r.data.size();
 }
 
+// Single code-block HT cleanup-pass encode / decode (signed coefficients).
+int orc_ht_encode_cblk(const int32_t* coef, uint32_t w, uint32_t h, uint32_t stride, uint8_t* out, uint32_t cap) {
+    std::vector<uint8_t> d = ht_encode_block(coef, w, h, stride);
+    if (d.size() > cap) return -1;
+    memcpy(out, d.data(), d.size());
+    return (int)d.size();
+}
+int orc_ht_decode_cblk(const uint8_t* data, uint32_t len, uint32_t w, uint32_t h, uint32_t k_msbs, int32_t* out) {
+    return ht_decode_block(data, len, w, h, k_msbs, out, w) ? 0 : -1;
+}
+
 // Single code-block T1 decode -> Grok's pre-filter values (2x magnitude with half bit).
 void orc_t1_decode_cblk(const uint8_t* data, uint32_t len, uint32_t npasses, uint32_t numbps, uint32_t orient,
                         uint32_t w, uint32_t h, int32_t* out) {
@@ -1423,7 +1830,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         } else if (m == 0xff52) {
             uint32_t scod = s[0]; prog = s[1]; nlayers = get16(s + 2); p.mct = s[4];
             p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
-            if (s[8] != 0) return -2;  // mode switches unsupported in the oracle
+            p.cblk_sty = s[8];
+            if (s[8] != 0 && s[8] != 0x40) return -2;  // other mode switches unsupported in the oracle
             if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
         } else if (m == 0xff5c) {
             uint32_t sq = s[0]; p.numgbits = sq >> 5;
@@ -1523,6 +1931,12 @@ t2done:
                     for (auto& K : P.cblks) {
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
                         std::vector<int32_t> blk(w * h);
+                        if (p.ht()) {   // T1HT::decompress: k_msbs = band numbps - cblk numbps
+                            if (K.npasses && !ht_decode_block(K.data.data(), (uint32_t)K.data.size(), w, h,
+                                                              B.numbps - K.numbps, blk.data(), w))
+                                return -4;
+                            if (!p.irreversible) for (auto& v : blk) v *= 2;   // same ShiftFilter below
+                        } else
                         t1_decode_block(K.data.data(), (uint32_t)K.data.size(), K.npasses, K.numbps, B.orient, w, h, blk.data());
                         for (uint32_t y = 0; y < h; ++y)
                             for (uint32_t x = 0; x < w; ++x) {

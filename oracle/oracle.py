@@ -21,6 +21,7 @@ class CParams(ctypes.Structure):
         ("write_com", ctypes.c_uint32),
         ("prcw_exp", ctypes.c_uint32 * 33), ("prch_exp", ctypes.c_uint32 * 33),
         ("layer_rate", ctypes.c_double * 100),
+        ("cblk_sty", ctypes.c_uint32),
     ]
 
 
@@ -58,11 +59,17 @@ def lib():
             ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_uint32), P(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_void_p]
         _lib.orc_t1_decode_cblk.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [P(ctypes.c_int32)]
         _lib.orc_default_params.argtypes = [P(CParams)]
+        _lib.orc_ht_encode_cblk.restype = ctypes.c_int
+        _lib.orc_ht_encode_cblk.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_uint32]
+        _lib.orc_ht_decode_cblk.restype = ctypes.c_int
+        _lib.orc_ht_decode_cblk.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_void_p]
     return _lib
 
 
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
-           layer_rate=None):
+           layer_rate=None, cblk_sty=0):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -72,6 +79,7 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
     p.mct = int(mct)
     p.nlayers = nlayers
     p.write_com = int(write_com)
+    p.cblk_sty = int(cblk_sty)
     if layer_rate:
         p.nlayers = len(layer_rate)
         for i, r in enumerate(layer_rate):
@@ -170,6 +178,26 @@ def t1_decode_cblk(data, npasses, numbps, orient, w, h):
     out = np.empty((h, w), np.int32)
     lib().orc_t1_decode_cblk(buf.ctypes.data, len(data), npasses, numbps, orient, w, h,
                              out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
+
+
+def ht_encode_cblk(coef):
+    """HTJ2K cleanup-pass encode of one code-block of signed coefficients -> bytes."""
+    a = np.ascontiguousarray(coef, dtype=np.int32)
+    h, w = a.shape
+    cap = w * h * 8 + 256
+    out = np.empty(cap, np.uint8)
+    n = lib().orc_ht_encode_cblk(a.ctypes.data, w, h, w, out.ctypes.data, cap)
+    assert n >= 0
+    return out[:n].tobytes()
+
+
+def ht_decode_cblk(data, w, h, k_msbs=30):
+    buf = np.frombuffer(data + b"\0" * 8, dtype=np.uint8).copy()
+    out = np.empty((h, w), np.int32)
+    rc = lib().orc_ht_decode_cblk(buf.ctypes.data, len(data), w, h, k_msbs, out.ctypes.data)
+    if rc != 0:
+        raise ValueError("HT block decode failed")
     return out
 
 
