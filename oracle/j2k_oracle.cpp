@@ -48,6 +48,8 @@ struct Params {
     double rates[100] = {0};    // grk_cparameters::layer_rate (compression ratios; 0 = all remaining passes)
     int write_com = 1;
     uint32_t cblk_sty = 0;      // 0x40 = HTJ2K block coder (GRK_CBLKSTY_HT, grok.h:104)
+    uint32_t tw = 0, th = 0;    // nominal tile size (0 = one tile covering the image), grk_cparameters::t_width/t_height
+    int tlm = 0, plt = 0;       // write TLM (-X) / PLT (-L) markers
     bool ht() const { return (cblk_sty & 0x40) != 0; }
     Params() { for (int i = 0; i < 33; ++i) { prcw_exp[i] = 15; prch_exp[i] = 15; } }
 };
@@ -102,14 +104,17 @@ struct Comp {
     std::vector<Res> res;
 };
 
-static void build_geometry(Comp& c, uint32_t w, uint32_t h, const Params& p) {
-    c.w = w; c.h = h;
+// Tile-component (tx0,ty0)-(tx1,ty1) in reference-grid coordinates (B.5).  The
+// sample buffer is tile-local (c.w x c.h); the band, precinct and code-block
+// grids are absolute, as in Grok's Resolution/Precinct setup.
+static void build_geometry(Comp& c, uint32_t tx0, uint32_t ty0, uint32_t tx1, uint32_t ty1, const Params& p) {
+    c.w = tx1 - tx0; c.h = ty1 - ty0;
     c.res.assign(p.numres, Res());
     for (uint32_t r = 0; r < p.numres; ++r) {
         Res& R = c.res[r];
         uint32_t nb = p.numres - 1 - r;
-        R.x0 = 0; R.y0 = 0;
-        R.x1 = ceildivpow2(w, nb); R.y1 = ceildivpow2(h, nb);
+        R.x0 = ceildivpow2(tx0, nb); R.y0 = ceildivpow2(ty0, nb);
+        R.x1 = ceildivpow2(tx1, nb); R.y1 = ceildivpow2(ty1, nb);
         R.prcw_exp = p.prcw_exp[r]; R.prch_exp = p.prch_exp[r];
         uint32_t px0 = floordivpow2(R.x0, R.prcw_exp) << R.prcw_exp;
         uint32_t py0 = floordivpow2(R.y0, R.prch_exp) << R.prch_exp;
@@ -140,8 +145,8 @@ static void build_geometry(Comp& c, uint32_t w, uint32_t h, const Params& p) {
                     if (t <= half) return 0;
                     return ceildivpow2((uint32_t)(t - half), nbb);
                 };
-                B.x0 = cb(0, xo); B.y0 = cb(0, yo);
-                B.x1 = cb(w, xo); B.y1 = cb(h, yo);
+                B.x0 = cb(tx0, xo); B.y0 = cb(ty0, yo);
+                B.x1 = cb(tx1, xo); B.y1 = cb(ty1, yo);
                 const Res& L = c.res[r - 1];
                 B.offx = xo ? (L.x1 - L.x0) : 0;
                 B.offy = yo ? (L.y1 - L.y0) : 0;
@@ -955,12 +960,29 @@ struct Image {
     uint32_t w, h, nc, prec; bool sgnd;
 };
 
-static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Params& p, const Comp& c0) {
+// Tile grid (B.3): nominal tile size (tw, th) anchored at the image origin.
+static uint32_t tile_count(const Params& p, uint32_t W, uint32_t H) {
+    uint32_t tw = p.tw ? p.tw : W, th = p.th ? p.th : H;
+    return ((W + tw - 1) / tw) * ((H + th - 1) / th);
+}
+static void tile_rect(const Params& p, uint32_t W, uint32_t H, uint32_t t, uint32_t& x0, uint32_t& y0, uint32_t& x1,
+                      uint32_t& y1) {
+    uint32_t tw = p.tw ? p.tw : W, th = p.th ? p.th : H;
+    uint32_t ntx = (W + tw - 1) / tw;
+    x0 = (t % ntx) * tw; y0 = (t / ntx) * th;
+    x1 = std::min(x0 + tw, W); y1 = std::min(y0 + th, H);
+}
+
+// Main header: SOC SIZ [CAP] COD QCD [TLM] [COM] (CodeStreamCompress::init_header_writing
+// :822-860).  *tlm_pos receives the offset of the first TLM entry (6 bytes per tile
+// part: Ttlm u16, Ptlm u32; Stlm = 0x60, LengthCache.cpp:437-482), patched later.
+static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Params& p, const Comp& c0,
+                              size_t* tlm_pos = nullptr) {
     put16(o, 0xff4f);                               // SOC
     put16(o, 0xff51); put16(o, 38 + 3 * im.nc);     // SIZ
     put16(o, p.ht() ? 0x4000 : 0);                  // Rsiz (GRK_JPH_RSIZ_FLAG for HT, CodeStreamCompress.cpp:216-219)
     put32(o, im.w); put32(o, im.h); put32(o, 0); put32(o, 0);
-    put32(o, im.w); put32(o, im.h); put32(o, 0); put32(o, 0);
+    put32(o, p.tw ? p.tw : im.w); put32(o, p.th ? p.th : im.h); put32(o, 0); put32(o, 0);
     put16(o, im.nc);
     for (uint32_t i = 0; i < im.nc; ++i) { o.push_back((uint8_t)((im.prec - 1) | (im.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
     if (p.ht()) {                                   // CAP (CodeStreamCompress::write_cap :1064-1111)
@@ -991,6 +1013,12 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
         put16(o, 3 + 2 * nbands);
         o.push_back((uint8_t)((p.numgbits << 5) | 2));
         for (uint32_t r = 0; r < p.numres; ++r) for (auto& B : c0.res[r].bands) put16(o, (B.expn << 11) | B.mant);
+    }
+    if (p.tlm) {                                     // TLM (TileLengthMarkers::writeBegin)
+        uint32_t nt = tile_count(p, im.w, im.h);
+        put16(o, 0xff55); put16(o, 4 + 6 * nt); o.push_back(0); o.push_back(0x60);
+        if (tlm_pos) *tlm_pos = o.size();
+        o.insert(o.end(), (size_t)6 * nt, 0);
     }
     if (p.write_com) {                               // COM (CodeStreamCompress.cpp:334, 1114)
         const char* txt = "Created by Grok     version 9.2.0";
@@ -1452,6 +1480,7 @@ typedef struct {
     uint32_t prcw_exp[33], prch_exp[33];
     double layer_rate[100];
     uint32_t cblk_sty;
+    uint32_t tile_w, tile_h, tlm, plt;
 } orc_cparams;
 
 static Params to_params(const orc_cparams* cp) {
@@ -1462,6 +1491,7 @@ static Params to_params(const orc_cparams* cp) {
     p.write_com = (int)cp->write_com;
     p.cblk_sty = cp->cblk_sty;
     if (p.ht()) p.numgbits = 1;   // grk_compress.cpp:1123-1124
+    p.tw = cp->tile_w; p.th = cp->tile_h; p.tlm = (int)cp->tlm; p.plt = (int)cp->plt;
     for (uint32_t i = 0; i < 100; ++i) p.rates[i] = i < p.nlayers ? cp->layer_rate[i] : 0.0;
     for (int i = 0; i < 33; ++i) { p.prcw_exp[i] = cp->prcw_exp[i] ? cp->prcw_exp[i] : 15; p.prch_exp[i] = cp->prch_exp[i] ? cp->prch_exp[i] : 15; }
     return p;
@@ -1483,6 +1513,7 @@ typedef struct {
 
 struct EncodeState {
     Image im; Params p;
+    uint32_t tile = 0, tx0 = 0, ty0 = 0, tx1 = 0, ty1 = 0;   // tile index and rectangle
     std::vector<Comp> comps;
     std::vector<std::vector<int32_t>> coefs;   // reversible Mallat coefficients
     std::vector<std::vector<float>> fcoefs;    // irreversible Mallat coefficients
@@ -1537,22 +1568,32 @@ static void t1_encode_all(EncodeState& E) {
 }
 
 static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc,
-                           uint32_t prec, int sgnd, const orc_cparams* cp) {
+                           uint32_t prec, int sgnd, const orc_cparams* cp, uint32_t tile = 0) {
     E.im = Image{w, h, nc, prec, sgnd != 0};
     E.p = to_params(cp);
     if (nc < 3) E.p.mct = 0;
+    E.tile = tile;
+    tile_rect(E.p, w, h, tile, E.tx0, E.ty0, E.tx1, E.ty1);
+    const uint32_t tw = E.tx1 - E.tx0, th = E.ty1 - E.ty0;
     E.comps.assign(nc, Comp());
-    for (uint32_t c = 0; c < nc; ++c) { build_geometry(E.comps[c], w, h, E.p); assign_steps(E.comps[c], E.p, prec, true, nullptr); }
+    for (uint32_t c = 0; c < nc; ++c) {
+        build_geometry(E.comps[c], E.tx0, E.ty0, E.tx1, E.ty1, E.p);
+        assign_steps(E.comps[c], E.p, prec, true, nullptr);
+    }
     E.coefs.assign(nc, {});
-    for (uint32_t c = 0; c < nc; ++c) E.coefs[c].assign(planes + (size_t)c * w * h, planes + (size_t)(c + 1) * w * h);
+    for (uint32_t c = 0; c < nc; ++c) {   // tile-local copy (TileProcessor::ingestImage, TileProcessor.cpp:410-431)
+        E.coefs[c].resize((size_t)tw * th);
+        for (uint32_t y = 0; y < th; ++y)
+            memcpy(&E.coefs[c][(size_t)y * tw], planes + (size_t)c * w * h + (size_t)(E.ty0 + y) * w + E.tx0, (size_t)tw * 4);
+    }
     if (!E.p.irreversible) {
         dc_rct_fwd(E.coefs, prec, sgnd != 0, E.p.mct != 0);
         for (uint32_t c = 0; c < nc; ++c)
-            dwt2d<int32_t>(E.coefs[c].data(), w, E.comps[c], E.p.numres, true, fwd53_1d);
+            dwt2d<int32_t>(E.coefs[c].data(), tw, E.comps[c], E.p.numres, true, fwd53_1d);
     } else {
         dc_ict_fwd(E.fcoefs, E.coefs, prec, sgnd != 0, E.p.mct != 0);
         for (uint32_t c = 0; c < nc; ++c)
-            dwt2d<float>(E.fcoefs[c].data(), w, E.comps[c], E.p.numres, true, fwd97_1d);
+            dwt2d<float>(E.fcoefs[c].data(), tw, E.comps[c], E.p.numres, true, fwd97_1d);
     }
 }
 
@@ -1695,35 +1736,72 @@ static void rate_allocate(EncodeState& E) {
     }
 }
 
-static std::vector<uint8_t> assemble(EncodeState& E) {
-    std::vector<uint8_t> o;
-    write_main_header(o, E.im, E.p, E.comps[0]);
-    E.header_size = o.size();
-    rate_allocate(E);
-    size_t sot = o.size();
-    put16(o, 0xff90); put16(o, 10); put16(o, 0); put32(o, 0); o.push_back(0); o.push_back(1);
-    put16(o, 0xff93);
+// One tile's packets in LRCP order (T2Compress::compressPackets); packet lengths
+// are recorded for PLT.
+static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector<uint32_t>& plens) {
     auto trees = make_trees(E);
     for (uint32_t l = 0; l < E.p.nlayers; ++l)
         for (uint32_t r = 0; r < E.p.numres; ++r)
             for (uint32_t c = 0; c < E.im.nc; ++c) {
                 Res& R = E.comps[c].res[r];
-                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) write_packet(&o, R, pi, l, trees[c][r][pi], nullptr);
+                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                    size_t before = body.size();
+                    write_packet(&body, R, pi, l, trees[c][r][pi], nullptr);
+                    plens.push_back((uint32_t)(body.size() - before));
+                }
             }
-    uint32_t psot = (uint32_t)(o.size() - sot);
-    o[sot + 6] = (uint8_t)(psot >> 24); o[sot + 7] = (uint8_t)(psot >> 16); o[sot + 8] = (uint8_t)(psot >> 8); o[sot + 9] = (uint8_t)psot;
-    put16(o, 0xffd9);
-    return o;
 }
 
-// Full encode (5/3 or 9/7, any number of layers).  Returns the codestream
-// size, or 0 on failure / insufficient capacity.
+// Tile part: SOT [PLT] SOD packets (CodeStreamCompress::writeTilePart :862-900; SOT with
+// TPsot = 0, TNsot = 1; PLT from PacketLengthMarkers::write, PacketLengthMarkers.cpp:107-175:
+// Zplt = 0, each length as 7-bit groups MSB first with a continuation bit).
+static uint32_t write_tile_part(std::vector<uint8_t>& o, EncodeState& E) {
+    std::vector<uint8_t> body; std::vector<uint32_t> plens;
+    tile_packets(E, body, plens);
+    size_t sot = o.size();
+    put16(o, 0xff90); put16(o, 10); put16(o, E.tile); put32(o, 0); o.push_back(0); o.push_back(1);
+    if (E.p.plt) {
+        std::vector<uint8_t> v;
+        for (uint32_t L : plens) {
+            int nbits = floorlog2(L) + 1, nbytes = (nbits + 6) / 7;
+            for (int k = nbytes - 1; k >= 0; --k) v.push_back((uint8_t)(((L >> (7 * k)) & 0x7F) | (k ? 0x80 : 0)));
+        }
+        put16(o, 0xff58); put16(o, (uint32_t)(3 + v.size())); o.push_back(0);
+        o.insert(o.end(), v.begin(), v.end());
+    }
+    put16(o, 0xff93);
+    o.insert(o.end(), body.begin(), body.end());
+    uint32_t psot = (uint32_t)(o.size() - sot);
+    o[sot + 6] = (uint8_t)(psot >> 24); o[sot + 7] = (uint8_t)(psot >> 16); o[sot + 8] = (uint8_t)(psot >> 8); o[sot + 9] = (uint8_t)psot;
+    return psot;
+}
+
+// Full encode (5/3 or 9/7, Part 1 or HT, any number of layers, one or more tiles).
+// Returns the codestream size, or 0 on failure / insufficient capacity.
 size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
                   const orc_cparams* cp, uint8_t* out, size_t cap) {
-    EncodeState E;
-    prepare_encode(E, planes, w, h, nc, prec, sgnd, cp);
-    t1_encode_all(E);
-    std::vector<uint8_t> o = assemble(E);
+    std::vector<uint8_t> o;
+    size_t tlm_pos = 0;
+    uint32_t nt = 0;
+    for (uint32_t t = 0;; ++t) {
+        EncodeState E;
+        prepare_encode(E, planes, w, h, nc, prec, sgnd, cp, t);
+        if (t == 0) {
+            nt = tile_count(E.p, w, h);
+            write_main_header(o, E.im, E.p, E.comps[0], &tlm_pos);
+        }
+        E.header_size = o.size();   // updateRates' SOT adjustment (single-tile semantics)
+        t1_encode_all(E);
+        rate_allocate(E);
+        uint32_t psot = write_tile_part(o, E);
+        if (E.p.tlm) {
+            size_t q = tlm_pos + (size_t)6 * t;
+            o[q] = (uint8_t)(t >> 8); o[q + 1] = (uint8_t)t;
+            o[q + 2] = (uint8_t)(psot >> 24); o[q + 3] = (uint8_t)(psot >> 16); o[q + 4] = (uint8_t)(psot >> 8); o[q + 5] = (uint8_t)psot;
+        }
+        if (t + 1 >= nt) break;
+    }
+    put16(o, 0xffd9);
     if (o.size() > cap) return 0;
     memcpy(out, o.data(), o.size());
     return o.size();
@@ -1806,52 +1884,20 @@ void orc_t1_decode_cblk(const uint8_t* data, uint32_t len, uint32_t npasses, uin
 }
 
 // ----------------------------------------------------------------------------
-// Decoder: main header + single tile, LRCP, any number of layers, default
-// code-block style.  Output planes are int32 at the image precision.
+// Decoder: main header, then one tile part per tile (SOT [PLT/other] SOD
+// packets), LRCP, any number of layers, Part-1 default style or HT.  Output
+// planes are int32 at the image precision.  (CodeStreamDecompress.cpp marker
+// handlers; T2Decompress.cpp:216-570; TileProcessor decompress path.)
 // ----------------------------------------------------------------------------
-int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_t* H, uint32_t* NC, uint32_t* PREC) {
-    size_t i = 0;
-    if (len < 4 || get16(cs) != 0xff4f) return -1;
-    i = 2;
-    Image im{}; Params p; p.write_com = 0;
-    std::vector<std::pair<uint32_t, uint32_t>> qcd;
-    uint32_t nlayers = 1, prog = 0;
-    size_t tile_end = 0;
-    bool in_tile = false;
-    while (i + 4 <= len) {
-        uint32_t m = get16(cs + i);
-        if (m == 0xff93) { i += 2; in_tile = true; break; }
-        uint32_t L = get16(cs + i + 2);
-        const uint8_t* s = cs + i + 4;
-        if (m == 0xff51) {
-            im.w = get32(s + 2); im.h = get32(s + 6);
-            im.nc = get16(s + 34);
-            im.prec = (s[36] & 0x7f) + 1; im.sgnd = (s[36] & 0x80) != 0;
-        } else if (m == 0xff52) {
-            uint32_t scod = s[0]; prog = s[1]; nlayers = get16(s + 2); p.mct = s[4];
-            p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
-            p.cblk_sty = s[8];
-            if (s[8] != 0 && s[8] != 0x40) return -2;  // other mode switches unsupported in the oracle
-            if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
-        } else if (m == 0xff5c) {
-            uint32_t sq = s[0]; p.numgbits = sq >> 5;
-            uint32_t qt = sq & 0x1f;
-            if (qt == 0) for (uint32_t k = 1; k + 0 < L - 2; ++k) qcd.push_back({(uint32_t)s[k] >> 3, 0u});
-            else for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = get16(s + k); qcd.push_back({v >> 11, v & 0x7ff}); }
-        } else if (m == 0xff90) {
-            uint32_t psot = get32(s + 2);
-            tile_end = i + psot;
-        }
-        i += 2 + L;
-    }
-    if (!in_tile) return -3;
-    (void)prog;
-    *W = im.w; *H = im.h; *NC = im.nc; *PREC = im.prec;
-    if (!out) return 0;
-    p.nlayers = nlayers;
-    if (tile_end == 0 || tile_end > len) tile_end = len - 2;
+static int decode_tile(const uint8_t* cs, size_t data, size_t tile_end, const Params& p, const Image& im,
+                       const std::vector<std::pair<uint32_t, uint32_t>>& qcd, uint32_t tile, int32_t* out) {
+    uint32_t tx0, ty0, tx1, ty1;
+    tile_rect(p, im.w, im.h, tile, tx0, ty0, tx1, ty1);
+    const uint32_t TW = tx1 - tx0, TH = ty1 - ty0;
+    const uint32_t nlayers = p.nlayers;
+    size_t i = data;
     std::vector<Comp> comps(im.nc);
-    for (uint32_t c = 0; c < im.nc; ++c) { build_geometry(comps[c], im.w, im.h, p); assign_steps(comps[c], p, im.prec, false, &qcd); }
+    for (uint32_t c = 0; c < im.nc; ++c) { build_geometry(comps[c], tx0, ty0, tx1, ty1, p); assign_steps(comps[c], p, im.prec, false, &qcd); }
     // T2 decode (LRCP)
     struct TT { std::vector<TagTree> incl, imsb; };
     std::vector<std::vector<std::vector<TT>>> trees(im.nc);
@@ -1924,7 +1970,7 @@ t2done:
     std::vector<std::vector<float>> fp(im.nc);
     for (uint32_t c = 0; c < im.nc; ++c) {
         Comp& C = comps[c];
-        if (!p.irreversible) ip[c].assign((size_t)im.w * im.h, 0); else fp[c].assign((size_t)im.w * im.h, 0.f);
+        if (!p.irreversible) ip[c].assign((size_t)TW * TH, 0); else fp[c].assign((size_t)TW * TH, 0.f);
         for (uint32_t r = 0; r < p.numres; ++r)
             for (auto& B : C.res[r].bands)
                 for (auto& P : B.prcs)
@@ -1940,18 +1986,21 @@ t2done:
                         t1_decode_block(K.data.data(), (uint32_t)K.data.size(), K.npasses, K.numbps, B.orient, w, h, blk.data());
                         for (uint32_t y = 0; y < h; ++y)
                             for (uint32_t x = 0; x < w; ++x) {
-                                size_t o = (size_t)(B.offy + K.y0 - B.y0 + y) * im.w + (B.offx + K.x0 - B.x0 + x);
+                                size_t o = (size_t)(B.offy + K.y0 - B.y0 + y) * TW + (B.offx + K.x0 - B.x0 + x);
                                 int32_t v = blk[y * w + x];
                                 if (!p.irreversible) ip[c][o] = v / 2;                 // ShiftFilter
                                 else fp[c][o] = (float)v * B.stepsize / 2.0f;          // ScaleFilter
                             }
                     }
-        if (!p.irreversible) dwt2d<int32_t>(ip[c].data(), im.w, C, p.numres, false, inv53_1d);
-        else dwt2d<float>(fp[c].data(), im.w, C, p.numres, false, inv97_1d);
+        if (!p.irreversible) dwt2d<int32_t>(ip[c].data(), TW, C, p.numres, false, inv53_1d);
+        else dwt2d<float>(fp[c].data(), TW, C, p.numres, false, inv97_1d);
     }
     int32_t shift = im.sgnd ? 0 : (1 << (im.prec - 1));
     int32_t mn = im.sgnd ? -(1 << (im.prec - 1)) : 0, mxv = im.sgnd ? (1 << (im.prec - 1)) - 1 : (1 << im.prec) - 1;
-    size_t n = (size_t)im.w * im.h;
+    const size_t n = (size_t)TW * TH, N = (size_t)im.w * im.h;
+    auto put = [&](uint32_t c, size_t k, int32_t v) {
+        out[c * N + (size_t)(ty0 + k / TW) * im.w + tx0 + k % TW] = std::min(mxv, std::max(mn, v + shift));
+    };
     if (!p.irreversible) {
         if (p.mct && im.nc >= 3)
             for (size_t k = 0; k < n; ++k) {
@@ -1960,7 +2009,7 @@ t2done:
                 ip[0][k] = rr; ip[1][k] = g; ip[2][k] = b;
             }
         for (uint32_t c = 0; c < im.nc; ++c)
-            for (size_t k = 0; k < n; ++k) out[c * n + k] = std::min(mxv, std::max(mn, ip[c][k] + shift));
+            for (size_t k = 0; k < n; ++k) put(c, k, ip[c][k]);
     } else {
         if (p.mct && im.nc >= 3)
             for (size_t k = 0; k < n; ++k) {
@@ -1970,7 +2019,63 @@ t2done:
                 fp[2][k] = y + 1.772f * u;
             }
         for (uint32_t c = 0; c < im.nc; ++c)
-            for (size_t k = 0; k < n; ++k) out[c * n + k] = std::min(mxv, std::max(mn, (int32_t)lrintf(fp[c][k]) + shift));
+            for (size_t k = 0; k < n; ++k) put(c, k, (int32_t)lrintf(fp[c][k]));
+    }
+    return 0;
+}
+
+int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_t* H, uint32_t* NC, uint32_t* PREC) {
+    size_t i = 0;
+    if (len < 4 || get16(cs) != 0xff4f) return -1;
+    i = 2;
+    Image im{}; Params p; p.write_com = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> qcd;
+    size_t first_sot = 0;
+    while (i + 4 <= len) {
+        uint32_t m = get16(cs + i);
+        if (m == 0xff90) { first_sot = i; break; }
+        uint32_t L = get16(cs + i + 2);
+        const uint8_t* s = cs + i + 4;
+        if (m == 0xff51) {
+            im.w = get32(s + 2) - get32(s + 10); im.h = get32(s + 6) - get32(s + 14);
+            if (get32(s + 10) || get32(s + 14) || get32(s + 26) || get32(s + 30)) return -2;  // origins unsupported
+            p.tw = get32(s + 18); p.th = get32(s + 22);
+            im.nc = get16(s + 34);
+            im.prec = (s[36] & 0x7f) + 1; im.sgnd = (s[36] & 0x80) != 0;
+        } else if (m == 0xff52) {
+            uint32_t scod = s[0];
+            p.nlayers = get16(s + 2); p.mct = s[4];
+            p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
+            p.cblk_sty = s[8];
+            if (s[1] != 0) return -2;                                // LRCP only
+            if (s[8] != 0 && s[8] != 0x40) return -2;  // other mode switches unsupported in the oracle
+            if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
+        } else if (m == 0xff5c) {
+            uint32_t sq = s[0]; p.numgbits = sq >> 5;
+            uint32_t qt = sq & 0x1f;
+            if (qt == 0) for (uint32_t k = 1; k + 0 < L - 2; ++k) qcd.push_back({(uint32_t)s[k] >> 3, 0u});
+            else for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = get16(s + k); qcd.push_back({v >> 11, v & 0x7ff}); }
+        }
+        i += 2 + L;   // CAP, TLM, COM and other main-header markers are skipped
+    }
+    if (!first_sot) return -3;
+    *W = im.w; *H = im.h; *NC = im.nc; *PREC = im.prec;
+    if (!out) return 0;
+    if (p.tw == im.w && p.th == im.h) p.tw = p.th = 0;
+    std::fill(out, out + (size_t)im.nc * im.w * im.h, 0);
+    const uint32_t nt = tile_count(p, im.w, im.h);
+    size_t pos = first_sot;
+    while (pos + 12 <= len && get16(cs + pos) == 0xff90) {
+        const uint8_t* s = cs + pos + 4;
+        uint32_t isot = get16(s), psot = get32(s + 2);
+        size_t tile_end = psot ? pos + psot : len - 2;
+        if (tile_end > len || isot >= nt) return -5;
+        size_t j = pos + 12;   // tile-part header markers (PLT, ...) until SOD
+        while (j + 2 <= tile_end && get16(cs + j) != 0xff93) j += 2 + get16(cs + j + 2);
+        if (j + 2 > tile_end) return -5;
+        int rc = decode_tile(cs, j + 2, tile_end, p, im, qcd, isot, out);
+        if (rc) return rc;
+        pos = tile_end;
     }
     return 0;
 }

@@ -22,6 +22,7 @@ class CParams(ctypes.Structure):
         ("prcw_exp", ctypes.c_uint32 * 33), ("prch_exp", ctypes.c_uint32 * 33),
         ("layer_rate", ctypes.c_double * 100),
         ("cblk_sty", ctypes.c_uint32),
+        ("tile_w", ctypes.c_uint32), ("tile_h", ctypes.c_uint32), ("tlm", ctypes.c_uint32), ("plt", ctypes.c_uint32),
     ]
 
 
@@ -69,7 +70,7 @@ def lib():
 
 
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
-           layer_rate=None, cblk_sty=0):
+           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -80,6 +81,9 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
     p.nlayers = nlayers
     p.write_com = int(write_com)
     p.cblk_sty = int(cblk_sty)
+    if tiles:
+        p.tile_w, p.tile_h = int(tiles[0]), int(tiles[1])
+    p.tlm, p.plt = int(tlm), int(plt)
     if layer_rate:
         p.nlayers = len(layer_rate)
         for i, r in enumerate(layer_rate):

@@ -43,6 +43,12 @@ def parse_flags(flags):
         kw["layer_rate"] = [float(v) for v in t[t.index("-r") + 1].split(",")]
     if "-M" in t:
         kw["cblk_sty"] = int(t[t.index("-M") + 1])
+    if "-t" in t:
+        kw["tiles"] = tuple(int(v) for v in t[t.index("-t") + 1].split(","))
+    if "-X" in t:
+        kw["tlm"] = True
+    if "-L" in t:
+        kw["plt"] = True
     return kw
 
 
@@ -64,6 +70,10 @@ class Fixture:
     @property
     def ht(self):
         return "-M" in self.flags
+
+    @property
+    def tiled(self):
+        return "-t" in self.flags
 
     def __repr__(self):
         return self.name

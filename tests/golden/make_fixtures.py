@@ -43,6 +43,12 @@ def cases():
     C.append(("rgb12_97_r", synth_image(384, 384, 3, 12, 11), 12, ["-I", "-r", "40,20,10"]))
     C.append(("mono16_ht", synth_image(256, 256, 1, 16, 20), 16, ["-M", "64"]))
     C.append(("rgb8_ht", synth_image(128, 128, 3, 8, 8), 8, ["-M", "64"]))
+    # multi-tile (tile origins are multiples of 2^(levels)), TLM (-X) and PLT (-L) markers
+    C.append(("rgb8_tiles", synth_image(300, 200, 3, 8, 41), 8, ["-t", "128,128"]))
+    C.append(("rgb8_tiles_xl", synth_image(300, 200, 3, 8, 42), 8, ["-t", "128,128", "-X", "-L"]))
+    C.append(("mono16_ht_tiles", synth_image(192, 256, 1, 16, 43), 16, ["-M", "64", "-t", "64,64", "-X", "-L"]))
+    C.append(("rgb12_97_tiles", synth_image(160, 256, 3, 12, 44), 12, ["-I", "-t", "128,128"]))
+    C.append(("mono8_tiles_n3", synth_image(77, 99, 1, 8, 45), 8, ["-t", "32,32", "-n", "3", "-b", "16,16"]))
     return C
 
 
@@ -55,12 +61,15 @@ def run(cmd, env):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--grok-bin", default="/tmp/grok-build/bin")
+    ap.add_argument("--only", nargs="*", help="regenerate only these fixture names")
     args = ap.parse_args()
     env = dict(os.environ, LD_LIBRARY_PATH=args.grok_bin)
     comp = os.path.join(args.grok_bin, "grk_compress")
     dec = os.path.join(args.grok_bin, "grk_decompress")
     with tempfile.TemporaryDirectory() as td:
         for name, img, bits, flags in cases():
+            if args.only and name not in args.only:
+                continue
             ext = "ppm" if img.shape[0] == 3 else "pgm"
             src = os.path.join(td, name + "." + ext)
             write_pnm(src, img, bits)

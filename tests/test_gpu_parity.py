@@ -13,8 +13,8 @@ import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-PART1_LOSSLESS = [f for f in FIXTURES if f.lossless and not f.ht]
-PART1_LOSSY = [f for f in FIXTURES if not f.lossless and not f.ht]
+PART1_LOSSLESS = [f for f in FIXTURES if f.lossless and not f.ht and not f.tiled]
+PART1_LOSSY = [f for f in FIXTURES if not f.lossless and not f.ht and not f.tiled]
 # 9/7 decode tolerance vs Grok's own decode: max-abs <= 1 LSB
 TOL_97_MAXABS = 1
 
