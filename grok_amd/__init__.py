@@ -87,8 +87,11 @@ def load_library(build_if_missing=True):
 
 
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
-                   precincts=None, write_comment=True):
-    """grk_compress_set_default_params + the CLI options used by the benchmark configs."""
+                   precincts=None, write_comment=True, cblk_sty=0):
+    """grk_compress_set_default_params + the CLI options used by the benchmark configs.
+
+    cblk_sty=0x40 selects the HTJ2K block coder; like grk_compress -M 64
+    (grk_compress.cpp:1120-1125) it also sets one guard bit."""
     lib = load_library()
     p = CParameters()
     lib.gk_set_default_params(ctypes.byref(p))
@@ -106,6 +109,9 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
         for i, (w, h) in enumerate(precincts):
             p.prcw_init[i], p.prch_init[i] = w, h
     p.write_comment = int(write_comment)
+    p.cblk_sty = int(cblk_sty)
+    if cblk_sty & 0x40:
+        p.numgbits = 1
     return p
 
 

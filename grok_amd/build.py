@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgrok_amd.so")
-SOURCES = ["gk_kernels.hip", "gk_dwt97.hip", "gk_t1enc.hip", "gk_t1dec.hip", "gk_engine.cpp"]
+SOURCES = ["gk_kernels.hip", "gk_dwt97.hip", "gk_t1enc.hip", "gk_t1dec.hip", "gk_ht.hip", "gk_engine.cpp"]
 
 
 def needs_build():

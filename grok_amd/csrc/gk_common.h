@@ -35,6 +35,7 @@ struct GkBlock {
 // Pass information written by the encoder (max 3*31-2 passes per block).
 // Default code-block style: only the last pass is terminated (T1.cpp:437-458).
 #define GK_MAX_PASSES 96
+#define GK_HT_MEL_CAP 1024   // MEL staging bytes per HT block (encoder)
 struct GkPass {
     uint32_t rate;         // cumulative bytes after the pass (T1.cpp:856-930 rules)
     uint32_t len;          // rate - previous rate

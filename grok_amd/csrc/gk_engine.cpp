@@ -47,6 +47,8 @@ struct Params {
     uint32_t prcw[GK_MAXRLVLS], prch[GK_MAXRLVLS];
     bool custom_prc = false;
     double rates[GK_MAX_LAYERS] = {0};   // compression ratio per layer (0 = remaining passes)
+    uint32_t cblk_sty = 0;               // 0 or GRK_CBLKSTY_HT (0x40, grok.h:104)
+    bool ht() const { return (cblk_sty & 0x40) != 0; }
     bool rate_control() const {          // TileProcessor::needsRateControl (TileProcessor.cpp:952-967)
         for (uint32_t l = 0; l < nlayers; ++l) if (rates[l] > 0.0) return true;
         return false;
@@ -106,11 +108,35 @@ static double band_norm(uint32_t level, uint32_t orient, bool rev) {
     return rev ? n53[orient][level] : n97[orient][level];
 }
 
+// HT reversible QCD: param_qcd::set_rev_quant (HTParams.cpp:253-272) —
+// exponent = B + ceil(log2(bibo_gain^2 * 1.1)) with the 5/3 BIBO gains
+// (HTParams.cpp:134-145).  Grok evaluates it before tcp->mct is set
+// (CodeStreamCompress.cpp:382 vs :396), so B is the sample precision.
+static uint32_t ht_rev_expn(uint32_t B, uint32_t ndecomp, uint32_t r, uint32_t orient) {
+    static const float gl[16] = {1.0000f, 1.5000f, 1.6250f, 1.6875f, 1.6963f, 1.7067f, 1.7116f, 1.7129f,
+                                 1.7141f, 1.7145f, 1.7151f, 1.7152f, 1.7155f, 1.7155f, 1.7156f, 1.7156f};
+    static const float gh[16] = {2.0000f, 2.5000f, 2.7500f, 2.8047f, 2.8198f, 2.8410f, 2.8558f, 2.8601f,
+                                 2.8628f, 2.8656f, 2.8662f, 2.8667f, 2.8669f, 2.8670f, 2.8671f, 2.8671f};
+    auto L = [&](uint32_t i) { return gl[std::min(i, 15u)]; };
+    auto H = [&](uint32_t i) { return gh[std::min(i, 15u)]; };
+    auto X = [](float g) { return (int)ceil(log(g * 1.1f) / 0.69314718055994530942); };
+    if (r == 0) return (uint32_t)((int)B + X(L(ndecomp) * L(ndecomp)));
+    const uint32_t d = ndecomp - r;
+    return (uint32_t)((int)B + (orient == 3 ? X(H(d) * H(d)) : X(H(d) * L(d + 1))));
+}
+
 static void assign_steps(Plan& P) {
     for (auto& C : P.comps) {
         for (uint32_t r = 0; r < P.p.numres; ++r) {
             for (auto& B : C.res[r].bands) {
                 uint32_t level = P.p.numres - 1 - r;
+                if (P.p.ht() && !P.p.irrev) {
+                    B.mant = 0;
+                    B.expn = ht_rev_expn(P.prec, P.p.numres - 1, r, B.orient);
+                    B.step_enc = B.step_dec = 1.0f;
+                    B.numbps = (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1);
+                    continue;
+                }
                 uint32_t gain = P.p.irrev ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
                 // Part-1 QCD generation (HTParams.cpp:216-251)
                 double stepsize = 1.0;
@@ -615,11 +641,18 @@ static void put32(std::vector<uint8_t>& o, uint32_t v) { put16(o, v >> 16); put1
 static void write_main_header(std::vector<uint8_t>& o, const Plan& P) {
     put16(o, 0xff4f);
     put16(o, 0xff51); put16(o, 38 + 3 * P.nc);
-    put16(o, 0);
+    put16(o, P.p.ht() ? 0x4000 : 0);   // Rsiz: GRK_JPH_RSIZ_FLAG for HT (CodeStreamCompress.cpp:216-219)
     put32(o, P.w); put32(o, P.h); put32(o, 0); put32(o, 0);
     put32(o, P.w); put32(o, P.h); put32(o, 0); put32(o, 0);
     put16(o, P.nc);
     for (uint32_t i = 0; i < P.nc; ++i) { o.push_back((uint8_t)((P.prec - 1) | (P.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
+    if (P.p.ht()) {   // CAP (CodeStreamCompress::write_cap :1064-1111): Pcap bit 15, Ccap = MAGBp code
+        uint32_t B = 0;
+        for (uint32_t r = 0; r < P.p.numres; ++r)
+            for (auto& Bd : P.comps[0].res[r].bands) B = std::max(B, Bd.expn + P.p.numgbits - 1);
+        uint32_t Bp = B <= 8 ? 0 : B < 28 ? B - 8 : B < 48 ? 13 + (B >> 2) : 31;
+        put16(o, 0xff50); put16(o, 8); put32(o, 0x00020000); put16(o, (P.p.irrev ? 0x20 : 0) | Bp);
+    }
     put16(o, 0xff52); put16(o, 12 + (P.p.custom_prc ? P.p.numres : 0));
     o.push_back(P.p.custom_prc ? 1 : 0);
     o.push_back(0);   // LRCP
@@ -627,7 +660,7 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P) {
     o.push_back((uint8_t)((P.p.mct && P.nc >= 3) ? 1 : 0));
     o.push_back((uint8_t)(P.p.numres - 1));
     o.push_back((uint8_t)(P.p.cbw - 2)); o.push_back((uint8_t)(P.p.cbh - 2));
-    o.push_back(0);
+    o.push_back((uint8_t)P.p.cblk_sty);
     o.push_back(P.p.irrev ? 0 : 1);
     if (P.p.custom_prc) for (uint32_t r = 0; r < P.p.numres; ++r) o.push_back((uint8_t)(P.p.prcw[r] | (P.p.prch[r] << 4)));
     uint32_t nbands = 3 * P.p.numres - 2;
@@ -722,6 +755,7 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     if (P.nlayers > GK_MAX_LAYERS) P.nlayers = GK_MAX_LAYERS;
     for (uint32_t l = 0; l < P.nlayers; ++l) P.rates[l] = cp->layer_rate[l] > 0.0 ? cp->layer_rate[l] : 0.0;
     P.write_com = cp->write_comment;
+    P.cblk_sty = cp->cblk_sty;
     if ((cp->csty & 1) && cp->res_spec) {   // CodeStreamCompress.cpp:542-590
         P.custom_prc = true;
         uint32_t p = 0;
@@ -743,6 +777,7 @@ static std::string plan_key(const Plan& P) {
     snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
              P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0, P.p.rate_control() ? 1 : 0);
     std::string k(buf);
+    k += " sty" + std::to_string(P.p.cblk_sty);
     for (uint32_t r = 0; r < P.p.numres; ++r) k += " " + std::to_string(P.p.prcw[r]) + "," + std::to_string(P.p.prch[r]);
     return k;
 }
@@ -799,7 +834,9 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     want.w = info->w; want.h = info->h; want.nc = info->numcomps; want.prec = info->prec; want.sgnd = info->sgnd;
     set_params(want.p, cp);
     if (want.nc < 3) want.p.mct = 0;
-    if (cp && cp->cblk_sty) throw GkError("code-block style mode switches are not supported");
+    if (want.p.cblk_sty != 0 && want.p.cblk_sty != 0x40) throw GkError("code-block style mode switches are not supported");
+    if (want.p.ht() && want.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
+    if (want.p.ht() && want.p.rate_control()) throw GkError("HTJ2K with rate control is not supported on this path yet");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if ((1u << want.p.cbw) > 64 || (1u << want.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
     ensure_plan(ctx, want);
@@ -846,7 +883,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     uint32_t* dinfo = (uint32_t*)ctx->dinfo.get(16 * (size_t)std::max(nb, 1u) + 16);
     int* derr = (int*)ctx->derr.get(64);
     uint32_t* dpcount = (uint32_t*)(derr + 4);
-    uint8_t* dsym = (uint8_t*)ctx->dsym.get(P.sym_off[nb] + 256);
+    uint8_t* dsym = P.p.ht() ? nullptr : (uint8_t*)ctx->dsym.get(P.sym_off[nb] + 256);
     uint64_t* dsymoff = (uint64_t*)ctx->dsymoff.get(8 * ((size_t)nb + 1));
     uint32_t* dpe = (uint32_t*)ctx->dpassend.get(4 * GK_MAX_PASSES * (size_t)std::max(nb, 1u));
     uint32_t* dcm = (uint32_t*)ctx->dcminfo.get(8 * (size_t)std::max(nb, 1u));
@@ -857,9 +894,16 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         ctx->blocks_uploaded = true;
     }
     HIPCHK(hipMemsetAsync(derr, 0, 64, st));
-    gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nb, derr, ctx->nmse_tab, dnmse);
-    HIPCHK(hipEventRecord(ctx->ev[8], st));
-    gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nb, derr, dnmse, dpcount);
+    if (P.p.ht()) {
+        // HT cleanup pass (T1HT::compress, T1HT.cpp:109-133); MEL bytes staged in the symbol buffer
+        uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nb * GK_HT_MEL_CAP + 256);
+        HIPCHK(hipEventRecord(ctx->ev[8], st));
+        gk_launch_ht_enc(st, arena, dblk, dbytes, mel, GK_HT_MEL_CAP, dinfo, nb, derr);
+    } else {
+        gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nb, derr, ctx->nmse_tab, dnmse);
+        HIPCHK(hipEventRecord(ctx->ev[8], st));
+        gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nb, derr, dnmse, dpcount);
+    }
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(16 * (size_t)nb + 64);
     HIPCHK(hipMemcpyAsync(hinfo, dinfo, 16 * (size_t)nb, hipMemcpyDeviceToHost, st));
@@ -867,6 +911,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t t1err = hinfo[4 * (size_t)nb], npass_total = hinfo[4 * (size_t)nb + 4];
     if (t1err) throw GkError(t1err & 2 ? "T1 symbol buffer overflow" : "T1 code-block slot overflow");
+    const bool ht = P.p.ht();
     const GkPass* hpasses = nullptr;
     if (do_rc) {
         GkPass* hp = (GkPass*)ctx->hpasses.get(sizeof(GkPass) * (size_t)std::max(npass_total, 1u));
@@ -909,7 +954,15 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
                     add_host(T2.hdr.data(), T2.hdr.size());
                     for (size_t i = 0; i < body.size(); i += 3) {
                         if (!body[i + 2]) continue;
-                        seg.push_back(P.blocks[body[i]].data_off + body[i + 1]); seg.push_back(pos);
+                        const GkBlock& G = P.blocks[body[i]];
+                        if (ht) {   // MagSgn head at the slot start, MEL+VLC tail at the slot end
+                            const uint32_t ms = hinfo[4 * (size_t)body[i] + 3], tl = body[i + 2] - ms;
+                            if (ms) { seg.push_back(G.data_off); seg.push_back(pos); seg.push_back(ms); pos += ms; }
+                            seg.push_back(G.data_off + G.data_cap - tl); seg.push_back(pos); seg.push_back(tl);
+                            pos += tl;
+                            continue;
+                        }
+                        seg.push_back(G.data_off + body[i + 1]); seg.push_back(pos);
                         seg.push_back(body[i + 2]);
                         pos += body[i + 2];
                     }
@@ -999,7 +1052,8 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             W.p.mct = S.at(s + 4);
             W.p.numres = S.at(s + 5) + 1;
             W.p.cbw = S.at(s + 6) + 2; W.p.cbh = S.at(s + 7) + 2;
-            if (S.at(s + 8)) throw GkError("code-block style mode switches not supported");
+            W.p.cblk_sty = S.at(s + 8);
+            if (W.p.cblk_sty != 0 && W.p.cblk_sty != 0x40) throw GkError("code-block style mode switches not supported");
             W.p.irrev = S.at(s + 9) == 0 ? 1 : 0;
             if (scod & 1) {
                 W.p.custom_prc = true;
@@ -1025,6 +1079,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     if (!have_siz || !have_cod || Hd.qcd.empty() || !Hd.tile_data) throw GkError("incomplete main header");
     if (!Hd.tile_end || Hd.tile_end > S.len) Hd.tile_end = S.len >= 2 ? S.len - 2 : S.len;
     if ((1u << W.p.cbw) > 64 || (1u << W.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
+    if (W.p.ht() && W.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
 }
 
 static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
@@ -1162,7 +1217,17 @@ t2done:
     ctx->blocks_uploaded = false;   // the encode table must be re-uploaded
     int32_t* arena = (int32_t*)ctx->arena.get(P.plane_elems * P.nc * 2 * sizeof(int32_t));
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    {
+    if (P.p.ht()) {
+        // HT cleanup pass decode straight into the band windows (T1HT::decompress, T1HT.cpp:134-187)
+        int* derr = (int*)ctx->derr.get(64);
+        HIPCHK(hipMemsetAsync(derr, 0, 64, st));
+        gk_launch_ht_dec(st, src_bytes, dblk, arena, nb, derr);
+        HIPCHK(hipEventRecord(ctx->ev[8], st));
+        int herr = 0;
+        HIPCHK(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (herr) throw GkError("corrupt HT code-block segment");
+    } else {
         // lane assignment: blocks bucketed by pass count (descending), so the 64 lanes of a
         // wave decode similar amounts of work and the longest waves start first
         const uint32_t nw = (nb + 63) / 64;

@@ -42,3 +42,8 @@ void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, flo
                          uint32_t h);
 void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
                          uint32_t h);
+// HTJ2K cleanup-pass block coder (gk_ht.hip)
+void gk_launch_ht_enc(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, uint8_t* mel_scratch,
+                      uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err);
+void gk_launch_ht_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, int32_t* coef, uint32_t nblocks,
+                      int* err);

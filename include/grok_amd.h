@@ -33,7 +33,7 @@ typedef struct gk_cparameters {
     double layer_rate[GK_MAX_LAYERS];    /* grk_cparameters::layer_rate (compression ratio, 0 = lossless) */
     uint8_t numresolution;               /* grk_cparameters::numresolution (default 6) */
     uint32_t cblockw_init, cblockh_init; /* grk_cparameters::cblockw_init / cblockh_init (default 64) */
-    uint8_t cblk_sty;                    /* grk_cparameters::cblk_sty (only 0 supported this round) */
+    uint8_t cblk_sty;                    /* grk_cparameters::cblk_sty: 0 (Part 1) or 0x40 (HTJ2K, GRK_CBLKSTY_HT) */
     uint8_t irreversible;                /* grk_cparameters::irreversible */
     uint8_t mct;                         /* grk_cparameters::mct (RCT/ICT for >= 3 components) */
     uint8_t numgbits;                    /* grk_cparameters::numgbits (default 2) */
