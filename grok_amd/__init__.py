@@ -36,6 +36,9 @@ class CParameters(ctypes.Structure):
         ("res_spec", ctypes.c_uint32),
         ("prcw_init", ctypes.c_uint32 * GK_MAXRLVLS), ("prch_init", ctypes.c_uint32 * GK_MAXRLVLS),
         ("write_comment", ctypes.c_uint8),
+        ("tile_size_on", ctypes.c_uint8),
+        ("t_width", ctypes.c_uint32), ("t_height", ctypes.c_uint32),
+        ("writeTLM", ctypes.c_uint8), ("writePLT", ctypes.c_uint8),
     ]
 
 
@@ -87,7 +90,7 @@ def load_library(build_if_missing=True):
 
 
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
-                   precincts=None, write_comment=True, cblk_sty=0):
+                   precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
     cblk_sty=0x40 selects the HTJ2K block coder; like grk_compress -M 64
@@ -112,6 +115,10 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
     p.cblk_sty = int(cblk_sty)
     if cblk_sty & 0x40:
         p.numgbits = 1
+    if tiles:   # grk_compress -t W,H
+        p.tile_size_on = 1
+        p.t_width, p.t_height = int(tiles[0]), int(tiles[1])
+    p.writeTLM, p.writePLT = int(bool(tlm)), int(bool(plt))
     return p
 
 

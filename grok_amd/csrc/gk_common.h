@@ -48,3 +48,14 @@ struct GkPlane {
     uint32_t stride;
     uint32_t w, h;
 };
+
+// A rectangular batch of equally-sized tiles for the level kernels (grid.z =
+// tile): tile z of the batch starts at row (j0 + z / nx) * dy, column
+// (i0 + z % nx) * dx of a plane; each tile is transformed independently.
+struct GkTiles {
+    uint32_t nx = 1, ny = 1, i0 = 0, j0 = 0, dx = 0, dy = 0;
+    __host__ __device__ uint32_t count() const { return nx * ny; }
+    __host__ __device__ uint64_t offset(uint32_t z, uint32_t stride) const {
+        return (uint64_t)((j0 + z / nx) * dy) * stride + (uint64_t)(i0 + z % nx) * dx;
+    }
+};

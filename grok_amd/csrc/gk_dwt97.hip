@@ -109,8 +109,9 @@ __global__ __launch_bounds__(256) void k_dc_inv_f(const float* __restrict__ in, 
 // =============================================================================
 __global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict__ src, uint32_t sstride,
                                                          float* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h) {
+                                                         uint32_t h, GkTiles tb) {
     __shared__ float T[T97_LH][T97_LW + 1];
+    src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
     const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H;
     const int tid = threadIdx.x;
     for (int i = tid; i < T97_LH * T97_LW; i += 256) {
@@ -181,8 +182,9 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict
 // =============================================================================
 __global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict__ src, uint32_t sstride,
                                                          float* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h) {
+                                                         uint32_t h, GkTiles tb) {
     __shared__ float T[T97_LH][T97_LW + 1];
+    src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
     const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H;
     const int tid = threadIdx.x;
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
@@ -264,12 +266,12 @@ void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int32_t* 
     hipLaunchKernelGGL(k_dc_inv_f, dim3((w + 255) / 256, h), dim3(256), 0, st, in, sin, out, sout, w, h, shift, mn, mx);
 }
 void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h) {
-    dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H);
-    hipLaunchKernelGGL(k_dwt97_fwd_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h);
+                         uint32_t h, GkTiles tb) {
+    dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
+    hipLaunchKernelGGL(k_dwt97_fwd_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h, tb);
 }
 void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h) {
-    dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H);
-    hipLaunchKernelGGL(k_dwt97_inv_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h);
+                         uint32_t h, GkTiles tb) {
+    dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
+    hipLaunchKernelGGL(k_dwt97_inv_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h, tb);
 }

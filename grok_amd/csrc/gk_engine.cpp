@@ -49,6 +49,8 @@ struct Params {
     double rates[GK_MAX_LAYERS] = {0};   // compression ratio per layer (0 = remaining passes)
     uint32_t cblk_sty = 0;               // 0 or GRK_CBLKSTY_HT (0x40, grok.h:104)
     bool ht() const { return (cblk_sty & 0x40) != 0; }
+    uint32_t tw = 0, th = 0;             // nominal tile size (grk_cparameters::t_width/t_height; 0 = image)
+    bool tlm = false, plt = false;       // grk_cparameters::writeTLM / writePLT
     bool rate_control() const {          // TileProcessor::needsRateControl (TileProcessor.cpp:952-967)
         for (uint32_t l = 0; l < nlayers; ++l) if (rates[l] > 0.0) return true;
         return false;
@@ -70,7 +72,9 @@ struct PrecG {
     uint32_t tree = 0;          // index of this precinct-band's tag trees
 };
 struct ResG {
+    uint32_t x0, y0;      // resolution origin on the reference grid (B.5)
     uint32_t w, h, pw, ph, cbw, cbh;
+    uint32_t px0, py0;    // precinct grid origin (resolution coordinates)
     std::vector<BandG> bands;
     std::vector<std::vector<PrecG>> prc;   // [band][precinct]
 };
@@ -78,14 +82,30 @@ struct CompG {
     std::vector<ResG> res;
 };
 
+// One tile (B.3).  Its samples live in the tile's rectangle of the image-sized
+// work planes, so DC/MCT run once over the image and every tile's DWT levels
+// and code-blocks are windows of the same planes.
+struct TileG {
+    uint32_t x0, y0, x1, y1;             // image coordinates
+    std::vector<CompG> comps;
+    uint32_t b0 = 0, b1 = 0;             // code-block range in Plan::blocks
+};
+// A rectangular batch of equally-sized tiles: one DWT launch per level (grid.z = tile).
+struct ShapeG {
+    uint32_t w, h;
+    std::vector<uint32_t> resw, resh;    // resolution sizes by level l = 0..L (l=0: full tile)
+    GkTiles tb;
+};
+
 struct Plan {
     uint32_t w = 0, h = 0, nc = 0, prec = 0, sgnd = 0;
     Params p;
     uint32_t stride = 0;                 // work-plane stride (samples)
     size_t plane_elems = 0;              // per plane
-    std::vector<CompG> comps;
-    std::vector<GkBlock> blocks;         // canonical order: comp, res, band, precinct, cblk
-    std::vector<uint32_t> resw, resh;    // resolution sizes by level l = 0..L (l=0: full)
+    uint32_t ntx = 1, nty = 1, tw = 0, th = 0;   // tile grid
+    std::vector<TileG> tiles;            // raster order
+    std::vector<ShapeG> shapes;
+    std::vector<GkBlock> blocks;         // tile order, then canonical: comp, res, band, precinct, cblk
     uint64_t slot_bytes = 0;
     std::vector<uint64_t> sym_off;       // T1 symbol-stream offsets (nblocks + 1)
     uint32_t ntrees = 0;                 // precinct-bands with code-blocks
@@ -125,8 +145,8 @@ static uint32_t ht_rev_expn(uint32_t B, uint32_t ndecomp, uint32_t r, uint32_t o
     return (uint32_t)((int)B + (orient == 3 ? X(H(d) * H(d)) : X(H(d) * L(d + 1))));
 }
 
-static void assign_steps(Plan& P) {
-    for (auto& C : P.comps) {
+static void assign_steps_tile(Plan& P, TileG& T) {
+    for (auto& C : T.comps) {
         for (uint32_t r = 0; r < P.p.numres; ++r) {
             for (auto& B : C.res[r].bands) {
                 uint32_t level = P.p.numres - 1 - r;
@@ -158,7 +178,8 @@ static void assign_steps(Plan& P) {
 }
 
 static void apply_qcd(Plan& P, const std::vector<std::pair<uint32_t, uint32_t>>& q) {
-    for (auto& C : P.comps) {
+    for (auto& T : P.tiles)
+    for (auto& C : T.comps) {
         uint32_t bandno = 0;
         for (uint32_t r = 0; r < P.p.numres; ++r)
             for (auto& B : C.res[r].bands) {
@@ -174,62 +195,60 @@ static void apply_qcd(Plan& P, const std::vector<std::pair<uint32_t, uint32_t>>&
     }
 }
 
-static void build_plan(Plan& P) {
+static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
     const uint32_t L = P.p.numres - 1;
-    P.stride = align_up(std::max(P.w, 1u), 64);
-    P.plane_elems = (size_t)P.stride * P.h;
-    P.resw.resize(L + 1); P.resh.resize(L + 1);
-    for (uint32_t l = 0; l <= L; ++l) { P.resw[l] = ceildivpow2(P.w, l); P.resh[l] = ceildivpow2(P.h, l); }
-    P.comps.assign(P.nc, CompG());
-    P.blocks.clear();
-    P.ntrees = 0;
+    T.comps.assign(P.nc, CompG());
+    T.b0 = (uint32_t)P.blocks.size();
     for (uint32_t c = 0; c < P.nc; ++c) {
-        CompG& C = P.comps[c];
+        CompG& C = T.comps[c];
         C.res.assign(P.p.numres, ResG());
         for (uint32_t r = 0; r < P.p.numres; ++r) {
             ResG& R = C.res[r];
-            uint32_t nb = L - r;
-            R.w = P.resw[nb]; R.h = P.resh[nb];
-            uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
-            R.pw = R.w ? ceildivpow2(R.w, pwe) : 0;
-            R.ph = R.h ? ceildivpow2(R.h, phe) : 0;
-            uint32_t bpw = r ? pwe - 1 : pwe, bph = r ? phe - 1 : phe;
+            const uint32_t nb = L - r;
+            R.x0 = ceildivpow2(T.x0, nb); R.y0 = ceildivpow2(T.y0, nb);
+            R.w = ceildivpow2(T.x1, nb) - R.x0; R.h = ceildivpow2(T.y1, nb) - R.y0;
+            const uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
+            R.px0 = (R.x0 >> pwe) << pwe; R.py0 = (R.y0 >> phe) << phe;
+            R.pw = R.w ? ((ceildivpow2(R.x0 + R.w, pwe) << pwe) - R.px0) >> pwe : 0;
+            R.ph = R.h ? ((ceildivpow2(R.y0 + R.h, phe) << phe) - R.py0) >> phe : 0;
+            const uint32_t bpw = r ? pwe - 1 : pwe, bph = r ? phe - 1 : phe;
             R.cbw = std::min(P.p.cbw, bpw); R.cbh = std::min(P.p.cbh, bph);
-            uint32_t nbands = r ? 3 : 1;
+            const uint32_t nbands = r ? 3 : 1;
             R.bands.assign(nbands, BandG());
             R.prc.assign(nbands, std::vector<PrecG>(R.pw * R.ph));
             for (uint32_t bi = 0; bi < nbands; ++bi) {
                 BandG& B = R.bands[bi];
                 B.orient = r ? bi + 1 : 0;
                 if (!r) {
-                    B.x0 = 0; B.y0 = 0; B.x1 = R.w; B.y1 = R.h;
+                    B.x0 = R.x0; B.y0 = R.y0; B.x1 = R.x0 + R.w; B.y1 = R.y0 + R.h;
                     B.level = L; B.offx = 0; B.offy = 0;
                     B.plane = L == 0 ? 0 : ((L & 1) ? 1 : 0);
                 } else {
-                    uint32_t lev = P.p.numres - r;   // decomposition level of this band (1..L)
-                    uint32_t xo = B.orient & 1, yo = B.orient >> 1;
-                    uint64_t half = 1ull << (lev - 1);
-                    auto cb = [&](uint64_t t, uint32_t o) -> uint32_t {
+                    const uint32_t lev = P.p.numres - r;   // decomposition level of this band (1..L)
+                    const uint32_t xo = B.orient & 1, yo = B.orient >> 1;
+                    const uint64_t half = 1ull << (lev - 1);
+                    auto cb = [&](uint64_t t, uint32_t o) -> uint32_t {   // B-15
                         if (!o) return ceildivpow2((uint32_t)t, lev);
                         return t <= half ? 0 : ceildivpow2((uint32_t)(t - half), lev);
                     };
-                    B.x0 = cb(0, xo); B.y0 = cb(0, yo); B.x1 = cb(P.w, xo); B.y1 = cb(P.h, yo);
+                    B.x0 = cb(T.x0, xo); B.y0 = cb(T.y0, yo); B.x1 = cb(T.x1, xo); B.y1 = cb(T.y1, yo);
                     B.level = lev;
                     B.plane = (lev & 1) ? 1 : 0;
-                    B.offx = xo ? P.resw[lev] : 0;
-                    B.offy = yo ? P.resh[lev] : 0;
+                    B.offx = xo ? S.resw[lev] : 0;   // Mallat placement inside the tile rectangle
+                    B.offy = yo ? S.resh[lev] : 0;
                 }
             }
         }
     }
-    assign_steps(P);
-    // code-blocks, canonical order
+    assign_steps_tile(P, T);
+    // code-blocks, canonical order (T1CompressScheduler.cpp:31-94); grids are absolute
     for (uint32_t c = 0; c < P.nc; ++c) {
-        CompG& C = P.comps[c];
+        CompG& C = T.comps[c];
         for (uint32_t r = 0; r < P.p.numres; ++r) {
             ResG& R = C.res[r];
-            uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
-            uint32_t bpw = r ? pwe - 1 : pwe, bph = r ? phe - 1 : phe;
+            const uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
+            const uint32_t bpw = r ? pwe - 1 : pwe, bph = r ? phe - 1 : phe;
+            const uint32_t tlx = r ? R.px0 >> 1 : R.px0, tly = r ? R.py0 >> 1 : R.py0;
             for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
                 BandG& B = R.bands[bi];
                 for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
@@ -237,23 +256,23 @@ static void build_plan(Plan& P) {
                     PG.first_block = (uint32_t)P.blocks.size();
                     PG.tree = P.ntrees;
                     if (B.empty()) continue;
-                    uint32_t i = pi % R.pw, j = pi / R.pw;
-                    uint32_t cx0 = i << bpw, cy0 = j << bph;
-                    uint32_t px0 = std::max(cx0, B.x0), py0 = std::max(cy0, B.y0);
-                    uint32_t px1 = std::min(cx0 + (1u << bpw), B.x1), py1 = std::min(cy0 + (1u << bph), B.y1);
+                    const uint32_t i = pi % R.pw, j = pi / R.pw;
+                    const uint32_t cx0 = tlx + (i << bpw), cy0 = tly + (j << bph);
+                    const uint32_t px0 = std::max(cx0, B.x0), py0 = std::max(cy0, B.y0);
+                    const uint32_t px1 = std::min(cx0 + (1u << bpw), B.x1), py1 = std::min(cy0 + (1u << bph), B.y1);
                     if (px1 <= px0 || py1 <= py0) continue;
-                    uint32_t gx0 = (px0 >> R.cbw) << R.cbw, gy0 = (py0 >> R.cbh) << R.cbh;
+                    const uint32_t gx0 = (px0 >> R.cbw) << R.cbw, gy0 = (py0 >> R.cbh) << R.cbh;
                     PG.cw = ((ceildivpow2(px1, R.cbw) << R.cbw) - gx0) >> R.cbw;
                     PG.ch = ((ceildivpow2(py1, R.cbh) << R.cbh) - gy0) >> R.cbh;
                     ++P.ntrees;
                     for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                        uint32_t a = k % PG.cw, b = k / PG.cw;
-                        uint32_t kx0 = gx0 + (a << R.cbw), ky0 = gy0 + (b << R.cbh);
-                        uint32_t x0 = std::max(kx0, px0), y0 = std::max(ky0, py0);
-                        uint32_t x1 = std::min(kx0 + (1u << R.cbw), px1), y1 = std::min(ky0 + (1u << R.cbh), py1);
+                        const uint32_t a = k % PG.cw, b = k / PG.cw;
+                        const uint32_t kx0 = gx0 + (a << R.cbw), ky0 = gy0 + (b << R.cbh);
+                        const uint32_t x0 = std::max(kx0, px0), y0 = std::max(ky0, py0);
+                        const uint32_t x1 = std::min(kx0 + (1u << R.cbw), px1), y1 = std::min(ky0 + (1u << R.cbh), py1);
                         GkBlock G{};
-                        size_t plane_base = ((size_t)c * 2 + B.plane) * P.plane_elems;
-                        G.band_off = plane_base + (size_t)(B.offy + y0 - B.y0) * P.stride + (B.offx + x0 - B.x0);
+                        const size_t plane_base = ((size_t)c * 2 + B.plane) * P.plane_elems;
+                        G.band_off = plane_base + (size_t)(T.y0 + B.offy + y0 - B.y0) * P.stride + (T.x0 + B.offx + x0 - B.x0);
                         G.stride = P.stride;
                         G.w = (uint16_t)(x1 - x0); G.h = (uint16_t)(y1 - y0);
                         G.orient = (uint8_t)B.orient; G.comp = (uint8_t)c;
@@ -274,6 +293,48 @@ static void build_plan(Plan& P) {
                 }
             }
         }
+    }
+    T.b1 = (uint32_t)P.blocks.size();
+}
+
+static void build_plan(Plan& P) {
+    const uint32_t L = P.p.numres - 1;
+    P.stride = align_up(std::max(P.w, 1u), 64);
+    P.plane_elems = (size_t)P.stride * P.h;
+    P.tw = P.p.tw ? std::min(P.p.tw, P.w) : P.w;
+    P.th = P.p.th ? std::min(P.p.th, P.h) : P.h;
+    P.ntx = (P.w + P.tw - 1) / P.tw; P.nty = (P.h + P.th - 1) / P.th;
+    // every tile origin must sit on the 2^L grid so each tile's DWT has even parity at all levels
+    if ((P.ntx > 1 && (P.tw & ((1u << L) - 1))) || (P.nty > 1 && (P.th & ((1u << L) - 1))))
+        throw GkError("tile sizes must be multiples of 2^(numresolution-1) on this path");
+    if ((size_t)P.ntx * P.nty > 65535) throw GkError("too many tiles");
+    // shape classes: {interior, last column} x {interior, last row}
+    const uint32_t lw = P.w - (P.ntx - 1) * P.tw, lh = P.h - (P.nty - 1) * P.th;
+    P.shapes.clear();
+    std::vector<int> shape_of((size_t)P.ntx * P.nty, -1);
+    for (int cj = 0; cj < 2; ++cj)
+        for (int ci = 0; ci < 2; ++ci) {
+            uint32_t i0 = ci ? P.ntx - 1 : 0, nx = ci ? 1 : P.ntx - 1;
+            uint32_t j0 = cj ? P.nty - 1 : 0, ny = cj ? 1 : P.nty - 1;
+            if (!nx || !ny) continue;
+            ShapeG S;
+            S.w = ci ? lw : P.tw; S.h = cj ? lh : P.th;
+            S.resw.resize(L + 1); S.resh.resize(L + 1);
+            for (uint32_t l = 0; l <= L; ++l) { S.resw[l] = ceildivpow2(S.w, l); S.resh[l] = ceildivpow2(S.h, l); }
+            S.tb.nx = nx; S.tb.ny = ny; S.tb.i0 = i0; S.tb.j0 = j0; S.tb.dx = P.tw; S.tb.dy = P.th;
+            for (uint32_t j = j0; j < j0 + ny; ++j)
+                for (uint32_t i = i0; i < i0 + nx; ++i) shape_of[(size_t)j * P.ntx + i] = (int)P.shapes.size();
+            P.shapes.push_back(S);
+        }
+    P.tiles.assign((size_t)P.ntx * P.nty, TileG());
+    P.blocks.clear();
+    P.ntrees = 0;
+    for (uint32_t t = 0; t < P.tiles.size(); ++t) {
+        TileG& T = P.tiles[t];
+        const uint32_t i = t % P.ntx, j = t / P.ntx;
+        T.x0 = i * P.tw; T.y0 = j * P.th;
+        T.x1 = std::min(T.x0 + P.tw, P.w); T.y1 = std::min(T.y0 + P.th, P.h);
+        build_tile(P, T, P.shapes[shape_of[t]]);
     }
     // encode slots: w*h*4 bytes + 16 (2-byte pad, alignment)
     uint64_t off = 0;
@@ -461,7 +522,8 @@ struct T2Enc {
         size_t nb = P.blocks.size();
         lnp.assign(nb * L, 0); inprev.assign(nb, 0); nlb.assign(nb, 0);
         incl.resize(P.ntrees); imsb.resize(P.ntrees);
-        for (auto& C : P.comps)
+        for (auto& T : P.tiles)
+        for (auto& C : T.comps)
             for (auto& R : C.res)
                 for (size_t bi = 0; bi < R.bands.size(); ++bi)
                     for (auto& PG : R.prc[bi])
@@ -550,7 +612,7 @@ struct T2Enc {
         for (uint32_t l = 0; l < max_layers; ++l)
             for (uint32_t r = 0; r < P.p.numres; ++r)
                 for (uint32_t c = 0; c < P.nc; ++c) {
-                    const ResG& R = P.comps[c].res[r];
+                    const ResG& R = P.tiles[0].comps[c].res[r];   // rate control: single tile
                     for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi)
                         if (!write_packet(R, pi, l, bp, nullptr)) return false;
                 }
@@ -637,19 +699,20 @@ struct T2Enc {
 static void put16(std::vector<uint8_t>& o, uint32_t v) { o.push_back((uint8_t)(v >> 8)); o.push_back((uint8_t)v); }
 static void put32(std::vector<uint8_t>& o, uint32_t v) { put16(o, v >> 16); put16(o, v & 0xffff); }
 
-// Main header: SOC SIZ COD QCD [COM]  (CodeStreamCompress.cpp:1054-1685 marker writers)
-static void write_main_header(std::vector<uint8_t>& o, const Plan& P) {
+// Main header: SOC SIZ [CAP] COD QCD [TLM] [COM]  (CodeStreamCompress::init_header_writing
+// :822-860; marker writers :1054-1685)
+static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tlm_pos = nullptr) {
     put16(o, 0xff4f);
     put16(o, 0xff51); put16(o, 38 + 3 * P.nc);
     put16(o, P.p.ht() ? 0x4000 : 0);   // Rsiz: GRK_JPH_RSIZ_FLAG for HT (CodeStreamCompress.cpp:216-219)
     put32(o, P.w); put32(o, P.h); put32(o, 0); put32(o, 0);
-    put32(o, P.w); put32(o, P.h); put32(o, 0); put32(o, 0);
+    put32(o, P.p.tw ? P.p.tw : P.w); put32(o, P.p.th ? P.p.th : P.h); put32(o, 0); put32(o, 0);   // XTsiz YTsiz XTOsiz YTOsiz
     put16(o, P.nc);
     for (uint32_t i = 0; i < P.nc; ++i) { o.push_back((uint8_t)((P.prec - 1) | (P.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
     if (P.p.ht()) {   // CAP (CodeStreamCompress::write_cap :1064-1111): Pcap bit 15, Ccap = MAGBp code
         uint32_t B = 0;
         for (uint32_t r = 0; r < P.p.numres; ++r)
-            for (auto& Bd : P.comps[0].res[r].bands) B = std::max(B, Bd.expn + P.p.numgbits - 1);
+            for (auto& Bd : P.tiles[0].comps[0].res[r].bands) B = std::max(B, Bd.expn + P.p.numgbits - 1);
         uint32_t Bp = B <= 8 ? 0 : B < 28 ? B - 8 : B < 48 ? 13 + (B >> 2) : 31;
         put16(o, 0xff50); put16(o, 8); put32(o, 0x00020000); put16(o, (P.p.irrev ? 0x20 : 0) | Bp);
     }
@@ -665,7 +728,7 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P) {
     if (P.p.custom_prc) for (uint32_t r = 0; r < P.p.numres; ++r) o.push_back((uint8_t)(P.p.prcw[r] | (P.p.prch[r] << 4)));
     uint32_t nbands = 3 * P.p.numres - 2;
     put16(o, 0xff5c);
-    const CompG& C = P.comps[0];
+    const CompG& C = P.tiles[0].comps[0];
     if (!P.p.irrev) {
         put16(o, 3 + nbands);
         o.push_back((uint8_t)(P.p.numgbits << 5));
@@ -674,6 +737,14 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P) {
         put16(o, 3 + 2 * nbands);
         o.push_back((uint8_t)((P.p.numgbits << 5) | 2));
         for (uint32_t r = 0; r < P.p.numres; ++r) for (auto& B : C.res[r].bands) put16(o, (B.expn << 11) | B.mant);
+    }
+    if (P.p.tlm) {   // TLM placeholder (TileLengthMarkers::writeBegin, LengthCache.cpp:437-463): Stlm 0x60,
+                     // 6 bytes (Ttlm u16, Ptlm u32) per tile part, filled in after the tiles are written
+        const uint32_t nt = (uint32_t)P.tiles.size();
+        if (4 + 6 * (size_t)nt > 65535) throw GkError("too many tiles for one TLM marker");
+        put16(o, 0xff55); put16(o, 4 + 6 * nt); o.push_back(0); o.push_back(0x60);
+        if (tlm_pos) *tlm_pos = o.size();
+        o.insert(o.end(), (size_t)6 * nt, 0);
     }
     if (P.p.write_com) {
         const char* txt = "Created by Grok     version 9.2.0";
@@ -756,6 +827,8 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     for (uint32_t l = 0; l < P.nlayers; ++l) P.rates[l] = cp->layer_rate[l] > 0.0 ? cp->layer_rate[l] : 0.0;
     P.write_com = cp->write_comment;
     P.cblk_sty = cp->cblk_sty;
+    if (cp->tile_size_on) { P.tw = cp->t_width; P.th = cp->t_height; }
+    P.tlm = cp->writeTLM != 0; P.plt = cp->writePLT != 0;
     if ((cp->csty & 1) && cp->res_spec) {   // CodeStreamCompress.cpp:542-590
         P.custom_prc = true;
         uint32_t p = 0;
@@ -777,14 +850,19 @@ static std::string plan_key(const Plan& P) {
     snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
              P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0, P.p.rate_control() ? 1 : 0);
     std::string k(buf);
-    k += " sty" + std::to_string(P.p.cblk_sty);
+    k += " sty" + std::to_string(P.p.cblk_sty) + " t" + std::to_string(P.p.tw) + "x" + std::to_string(P.p.th);
     for (uint32_t r = 0; r < P.p.numres; ++r) k += " " + std::to_string(P.p.prcw[r]) + "," + std::to_string(P.p.prch[r]);
     return k;
 }
 
 static void ensure_plan(gk_ctx* ctx, const Plan& want) {
     std::string k = plan_key(want);
-    if (k == ctx->plan_key) return;
+    if (k == ctx->plan_key) {
+        // same geometry: refresh the parameters that do not shape the plan (layers, rates,
+        // TLM/PLT, COM), which the cached plan would otherwise carry over from the last call
+        ctx->plan.p = want.p;
+        return;
+    }
     ctx->plan = want;
     build_plan(ctx->plan);
     ctx->plan_key = k;
@@ -799,23 +877,25 @@ static void run_dwt(gk_ctx* ctx, bool forward) {
     ctx->tm.dwt_launches = 0; ctx->tm.dwt_bytes = 0;
     for (uint32_t i = 0; i < L; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
-        uint32_t w = P.resw[l - 1], h = P.resh[l - 1];
-        for (uint32_t c = 0; c < P.nc; ++c) {
-            int32_t* A = arena + (size_t)c * 2 * P.plane_elems;
-            int32_t* B = A + P.plane_elems;
-            int32_t* src_l = (l & 1) ? A : B;     // D_{l-1}: level l input plane (l-1 odd -> B)
-            int32_t* dst_l = (l & 1) ? B : A;     // D_l
-            if (P.p.irrev) {
-                float* fs = reinterpret_cast<float*>(src_l);
-                float* fd = reinterpret_cast<float*>(dst_l);
-                if (forward) gk_launch_dwt97_fwd(ctx->st, fs, P.stride, fd, P.stride, w, h);
-                else gk_launch_dwt97_inv(ctx->st, fd, P.stride, fs, P.stride, w, h);
-            } else {
-                if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, P.stride, dst_l, P.stride, w, h);
-                else gk_launch_dwt53_inv(ctx->st, dst_l, P.stride, src_l, P.stride, w, h);
+        for (const ShapeG& S : P.shapes) {        // one launch per tile shape, grid.z = tiles of that shape
+            const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
+            for (uint32_t c = 0; c < P.nc; ++c) {
+                int32_t* A = arena + (size_t)c * 2 * P.plane_elems;
+                int32_t* B = A + P.plane_elems;
+                int32_t* src_l = (l & 1) ? A : B;     // D_{l-1}: level l input plane (l-1 odd -> B)
+                int32_t* dst_l = (l & 1) ? B : A;     // D_l
+                if (P.p.irrev) {
+                    float* fs = reinterpret_cast<float*>(src_l);
+                    float* fd = reinterpret_cast<float*>(dst_l);
+                    if (forward) gk_launch_dwt97_fwd(ctx->st, fs, P.stride, fd, P.stride, w, h, S.tb);
+                    else gk_launch_dwt97_inv(ctx->st, fd, P.stride, fs, P.stride, w, h, S.tb);
+                } else {
+                    if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, P.stride, dst_l, P.stride, w, h, S.tb);
+                    else gk_launch_dwt53_inv(ctx->st, dst_l, P.stride, src_l, P.stride, w, h, S.tb);
+                }
+                ctx->tm.dwt_launches++;
+                ctx->tm.dwt_bytes += (uint64_t)w * h * 8 * S.tb.count();
             }
-            ctx->tm.dwt_launches++;
-            ctx->tm.dwt_bytes += (uint64_t)w * h * 8;
         }
     }
 }
@@ -837,6 +917,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     if (want.p.cblk_sty != 0 && want.p.cblk_sty != 0x40) throw GkError("code-block style mode switches are not supported");
     if (want.p.ht() && want.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
     if (want.p.ht() && want.p.rate_control()) throw GkError("HTJ2K with rate control is not supported on this path yet");
+    if (want.p.tw && want.p.th && (want.p.tw < want.w || want.p.th < want.h) && want.p.rate_control())
+        throw GkError("rate control with more than one tile is not supported on this path yet");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if ((1u << want.p.cbw) > 64 || (1u << want.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
     ensure_plan(ctx, want);
@@ -923,16 +1005,14 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     // ---- host T2 (T2Compress.cpp:113-240) with layer formation / rate allocation
     std::vector<uint8_t> H;
     H.reserve(1 << 12);
-    write_main_header(H, P);
+    size_t tlm_pos = 0;
+    write_main_header(H, P, &tlm_pos);
     const size_t header_size = H.size();
     T2Enc T2(P, hinfo, hpasses);
     T2.allocate(header_size);
-    size_t sot = H.size();
-    put16(H, 0xff90); put16(H, 10); put16(H, 0); put32(H, 0); H.push_back(0); H.push_back(1);
-    put16(H, 0xff93);
-    // segments: (src_off in dbytes, dst_off in codestream, len); headers staged after the slots
+    // segments: (src_off in dbytes, dst_off in codestream, len); host bytes staged after the slots
     std::vector<uint64_t> seg;
-    seg.reserve(3 * ((size_t)nb + 64));
+    seg.reserve(3 * ((size_t)nb * (ht ? 2 : 1) + 64));
     std::vector<uint8_t> hdrs;   // all host bytes, in order, copied to staging
     uint64_t pos = 0;            // codestream position
     auto add_host = [&](const uint8_t* p, size_t n) {
@@ -942,37 +1022,74 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         pos += n;
     };
     add_host(H.data(), H.size());
-    std::vector<uint32_t> body;
-    body.reserve(3 * 4096);
-    for (uint32_t l = 0; l < P.p.nlayers; ++l)
-        for (uint32_t r = 0; r < P.p.numres; ++r)
-            for (uint32_t c = 0; c < P.nc; ++c) {
-                const ResG& R = P.comps[c].res[r];
-                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                    body.clear();
-                    T2.write_packet(R, pi, l, nullptr, &body);
-                    add_host(T2.hdr.data(), T2.hdr.size());
-                    for (size_t i = 0; i < body.size(); i += 3) {
-                        if (!body[i + 2]) continue;
-                        const GkBlock& G = P.blocks[body[i]];
-                        if (ht) {   // MagSgn head at the slot start, MEL+VLC tail at the slot end
-                            const uint32_t ms = hinfo[4 * (size_t)body[i] + 3], tl = body[i + 2] - ms;
-                            if (ms) { seg.push_back(G.data_off); seg.push_back(pos); seg.push_back(ms); pos += ms; }
-                            seg.push_back(G.data_off + G.data_cap - tl); seg.push_back(pos); seg.push_back(tl);
-                            pos += tl;
-                            continue;
+    std::vector<uint32_t> body, bsegs;   // bsegs: (block, first byte, length) of every packet body, tile order
+    std::vector<uint8_t> phdr;           // packet headers of the current tile
+    struct Pk { uint32_t hoff, hlen, s0, s1, len; };
+    std::vector<Pk> pk;
+    std::vector<uint8_t> tp;             // SOT [PLT] SOD bytes of the current tile
+    for (uint32_t t = 0; t < P.tiles.size(); ++t) {
+        const TileG& T = P.tiles[t];
+        pk.clear(); phdr.clear(); bsegs.clear();
+        for (uint32_t l = 0; l < P.p.nlayers; ++l)
+            for (uint32_t r = 0; r < P.p.numres; ++r)
+                for (uint32_t c = 0; c < P.nc; ++c) {
+                    const ResG& R = T.comps[c].res[r];
+                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                        body.clear();
+                        T2.write_packet(R, pi, l, nullptr, &body);
+                        Pk k{(uint32_t)phdr.size(), (uint32_t)T2.hdr.size(), (uint32_t)bsegs.size(), 0, (uint32_t)T2.hdr.size()};
+                        phdr.insert(phdr.end(), T2.hdr.begin(), T2.hdr.end());
+                        for (size_t q = 0; q < body.size(); q += 3) {
+                            if (!body[q + 2]) continue;
+                            bsegs.push_back(body[q]); bsegs.push_back(body[q + 1]); bsegs.push_back(body[q + 2]);
+                            k.len += body[q + 2];
                         }
-                        seg.push_back(G.data_off + body[i + 1]); seg.push_back(pos);
-                        seg.push_back(body[i + 2]);
-                        pos += body[i + 2];
+                        k.s1 = (uint32_t)bsegs.size();
+                        pk.push_back(k);
                     }
                 }
+        // tile part: SOT [PLT] SOD (CodeStreamCompress::writeTilePart :862-900)
+        tp.clear();
+        put16(tp, 0xff90); put16(tp, 10); put16(tp, t); put32(tp, 0); tp.push_back(0); tp.push_back(1);
+        if (P.p.plt) {   // PacketLengthMarkers::write (PacketLengthMarkers.cpp:107-175): Zplt 0, 7-bit groups MSB first
+            std::vector<uint8_t> v;
+            for (const Pk& k : pk) {
+                const int nbits = floorlog2(k.len) + 1, nbytes = (nbits + 6) / 7;
+                for (int q = nbytes - 1; q >= 0; --q) v.push_back((uint8_t)(((k.len >> (7 * q)) & 0x7F) | (q ? 0x80 : 0)));
             }
+            if (3 + v.size() > 65535) throw GkError("PLT marker overflow (too many packets in one tile)");
+            put16(tp, 0xff58); put16(tp, (uint32_t)(3 + v.size())); tp.push_back(0);
+            tp.insert(tp.end(), v.begin(), v.end());
+        }
+        put16(tp, 0xff93);
+        uint64_t psot = tp.size();
+        for (const Pk& k : pk) psot += k.len;
+        if (psot > 0xffffffffull) throw GkError("tile part exceeds 4 GiB");
+        tp[6] = (uint8_t)(psot >> 24); tp[7] = (uint8_t)(psot >> 16); tp[8] = (uint8_t)(psot >> 8); tp[9] = (uint8_t)psot;
+        if (P.p.tlm) {
+            uint8_t* e = hdrs.data() + tlm_pos + 6 * (size_t)t;   // the main header is hdrs[0 .. H.size())
+            e[0] = (uint8_t)(t >> 8); e[1] = (uint8_t)t;
+            e[2] = (uint8_t)(psot >> 24); e[3] = (uint8_t)(psot >> 16); e[4] = (uint8_t)(psot >> 8); e[5] = (uint8_t)psot;
+        }
+        add_host(tp.data(), tp.size());
+        for (const Pk& k : pk) {
+            add_host(phdr.data() + k.hoff, k.hlen);
+            for (uint32_t q = k.s0; q < k.s1; q += 3) {
+                const uint32_t b = bsegs[q], off = bsegs[q + 1], n = bsegs[q + 2];
+                const GkBlock& G = P.blocks[b];
+                if (ht) {   // MagSgn head at the slot start, MEL+VLC tail at the slot end
+                    const uint32_t ms = hinfo[4 * (size_t)b + 3], tl = n - ms;
+                    if (ms) { seg.push_back(G.data_off); seg.push_back(pos); seg.push_back(ms); pos += ms; }
+                    seg.push_back(G.data_off + G.data_cap - tl); seg.push_back(pos); seg.push_back(tl);
+                    pos += tl;
+                    continue;
+                }
+                seg.push_back(G.data_off + off); seg.push_back(pos); seg.push_back(n);
+                pos += n;
+            }
+        }
+    }
     uint8_t eoc[2] = {0xff, 0xd9};
-    // Psot patch: tile-part length from SOT to end of tile data
-    uint32_t psot = (uint32_t)(pos - sot);
-    hdrs[sot + 6] = (uint8_t)(psot >> 24); hdrs[sot + 7] = (uint8_t)(psot >> 16);
-    hdrs[sot + 8] = (uint8_t)(psot >> 8); hdrs[sot + 9] = (uint8_t)psot;
     add_host(eoc, 2);
     const size_t total = pos;
     HIPCHK(hipEventRecord(ctx->ev[5], st));
@@ -1014,10 +1131,12 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
 // ---------------------------------------------------------------------------
 // Decode
 // ---------------------------------------------------------------------------
+struct TilePart { uint32_t tile; size_t data, end; };   // packet bytes [data, end) of one tile part
 struct Header {
     Plan want;
     std::vector<std::pair<uint32_t, uint32_t>> qcd;
-    size_t tile_data = 0, tile_end = 0;
+    size_t first_sot = 0;
+    std::vector<TilePart> parts;
 };
 
 static void parse_header(ByteSrc& S, Header& Hd) {
@@ -1029,13 +1148,16 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     bool have_siz = false, have_cod = false;
     while (i + 4 <= S.len) {
         uint32_t m = S.be16(i);
-        if (m == 0xff93) { Hd.tile_data = i + 2; break; }
+        if (m == 0xff90) { Hd.first_sot = i; break; }
         uint32_t L = S.be16(i + 2);
         size_t s = i + 4;
         if (m == 0xff51) {
             W.w = S.be32(s + 2) - S.be32(s + 10); W.h = S.be32(s + 6) - S.be32(s + 14);
             if (S.be32(s + 10) || S.be32(s + 14)) throw GkError("image offsets not supported");
-            if (S.be32(s + 18) < S.be32(s + 2) || S.be32(s + 22) < S.be32(s + 6)) throw GkError("multi-tile codestreams not supported on this path yet");
+            if (S.be32(s + 26) || S.be32(s + 30)) throw GkError("tile grid offsets not supported");
+            W.p.tw = S.be32(s + 18); W.p.th = S.be32(s + 22);
+            if (!W.p.tw || !W.p.th) throw GkError("bad tile size");
+            if (W.p.tw >= W.w && W.p.th >= W.h) W.p.tw = W.p.th = 0;   // one tile
             W.nc = S.be16(s + 34);
             uint32_t sz = S.at(s + 36);
             W.prec = (sz & 0x7f) + 1; W.sgnd = (sz & 0x80) ? 1 : 0;
@@ -1068,16 +1190,27 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             if (qt == 0) for (uint32_t k = 1; k < L - 2; ++k) Hd.qcd.push_back({(uint32_t)S.at(s + k) >> 3, 0u});
             else if (qt == 2) for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = S.be16(s + k); Hd.qcd.push_back({v >> 11, v & 0x7ff}); }
             else throw GkError("scalar-derived quantisation not supported");
-        } else if (m == 0xff90) {
-            uint32_t psot = S.be32(s + 2);
-            Hd.tile_end = psot ? i + psot : 0;
         } else if (m == 0xff5d || m == 0xff53 || m == 0xff5e || m == 0xff5f) {
             throw GkError("QCC/COC/RGN/POC markers not supported on this path yet");
         }
         i += 2 + L;
     }
-    if (!have_siz || !have_cod || Hd.qcd.empty() || !Hd.tile_data) throw GkError("incomplete main header");
-    if (!Hd.tile_end || Hd.tile_end > S.len) Hd.tile_end = S.len >= 2 ? S.len - 2 : S.len;
+    if (!have_siz || !have_cod || Hd.qcd.empty() || !Hd.first_sot) throw GkError("incomplete main header");
+    // tile parts: SOT (Isot, Psot, TPsot, TNsot), tile-part header markers (PLT, ...), SOD, packets
+    // (CodeStreamDecompress SOT/SOD handlers; TLM and PLT are only needed for random access)
+    size_t pos = Hd.first_sot;
+    while (pos + 12 <= S.len && S.be16(pos) == 0xff90) {
+        const uint32_t isot = S.be16(pos + 4), psot = S.be32(pos + 6);
+        const size_t end = psot ? pos + psot : (S.len >= 2 ? S.len - 2 : S.len);
+        if (end > S.len || end < pos + 14) throw GkError("corrupt SOT (Psot)");
+        size_t j = pos + 12;
+        while (j + 4 <= end && S.be16(j) != 0xff93) j += 2 + S.be16(j + 2);
+        if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
+        if (S.at(pos + 10) != 0) throw GkError("multiple tile parts per tile not supported");
+        Hd.parts.push_back({isot, j + 2, end});
+        pos = end;
+    }
+    if (Hd.parts.empty()) throw GkError("no tile parts");
     if ((1u << W.p.cbw) > 64 || (1u << W.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
     if (W.p.ht() && W.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
 }
@@ -1102,83 +1235,86 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     std::vector<uint32_t> numlenbits(nb, 0);
     for (auto& G : blk) { G.npasses = 0; G.numbps = 0; G.len = 0; }
     // refresh band numbps from QCD (decoder semantics)
-    {
-        uint32_t b = 0;
+    for (auto& T : P.tiles)
         for (uint32_t c = 0; c < P.nc; ++c)
             for (uint32_t r = 0; r < P.p.numres; ++r) {
-                ResG& R = P.comps[c].res[r];
+                ResG& R = T.comps[c].res[r];
                 for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
                     for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
                         PrecG& PG = R.prc[bi][pi];
-                        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k, ++b) {
+                        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
                             blk[PG.first_block + k].band_numbps = (uint8_t)R.bands[bi].numbps;
                             blk[PG.first_block + k].step = R.bands[bi].step_dec / 2.0f;
                         }
                     }
             }
-    }
-    // ---- T2 (T2Decompress.cpp:216-570), LRCP
+    // ---- T2 (T2Decompress.cpp:216-570), LRCP, per tile part
     struct Trees { DecTree incl, imsb; };
     std::vector<Trees> trees;
-    std::vector<size_t> tree_base;   // per (c, r, band, prc) index
-    // index trees by first_block of each precinct-band
-    std::unordered_map<uint32_t, size_t> tidx;
-    size_t pos = Hd.tile_data;
-    for (uint32_t l = 0; l < P.p.nlayers; ++l)
-        for (uint32_t r = 0; r < P.p.numres; ++r)
-            for (uint32_t c = 0; c < P.nc; ++c) {
-                ResG& R = P.comps[c].res[r];
-                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                    if (pos >= Hd.tile_end) goto t2done;
-                    BitReader br(S, pos, Hd.tile_end);
-                    std::vector<std::pair<uint32_t, uint32_t>> contrib;
-                    if (br.read(1)) {
-                        for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
-                            PrecG& PG = R.prc[bi][pi];
-                            if (!PG.cw || !PG.ch) continue;
-                            auto it = tidx.find(PG.first_block);
-                            if (it == tidx.end()) {
-                                trees.emplace_back();
-                                trees.back().incl.build(PG.cw, PG.ch);
-                                trees.back().imsb.build(PG.cw, PG.ch);
-                                it = tidx.emplace(PG.first_block, trees.size() - 1).first;
-                            }
-                            Trees& T = trees[it->second];
-                            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                                uint32_t b = PG.first_block + k;
-                                uint32_t inc;
-                                if (!included[b]) inc = T.incl.decode(br, k, l + 1) <= l ? 1 : 0;
-                                else inc = br.read(1);
-                                if (!inc) continue;
-                                if (!included[b]) {
-                                    uint32_t kmsbs = 0, v = T.imsb.decode(br, k, kmsbs);
-                                    while (v >= kmsbs) { ++kmsbs; if (kmsbs > 64) break; v = T.imsb.decode(br, k, kmsbs); }
-                                    kmsbs--;
-                                    uint32_t bnb = R.bands[bi].numbps;
-                                    blk[b].numbps = kmsbs > bnb ? 0 : bnb - kmsbs;
-                                    numlenbits[b] = 3;
-                                    included[b] = 1;
+    std::unordered_map<uint32_t, size_t> tidx;   // trees by first_block of each precinct-band
+    std::vector<uint8_t> seen(P.tiles.size(), 0);
+    for (const TilePart& TPt : Hd.parts) {
+        if (TPt.tile >= P.tiles.size()) throw GkError("corrupt SOT (tile index)");
+        if (seen[TPt.tile]++) throw GkError("multiple tile parts per tile not supported");
+        const TileG& TG = P.tiles[TPt.tile];
+        const size_t tile_end = TPt.end;
+        size_t pos = TPt.data;
+        for (uint32_t l = 0; l < P.p.nlayers; ++l)
+            for (uint32_t r = 0; r < P.p.numres; ++r)
+                for (uint32_t c = 0; c < P.nc; ++c) {
+                    const ResG& R = TG.comps[c].res[r];
+                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                        if (pos >= tile_end) goto tile_done;
+                        BitReader br(S, pos, tile_end);
+                        std::vector<std::pair<uint32_t, uint32_t>> contrib;
+                        if (br.read(1)) {
+                            for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
+                                const PrecG& PG = R.prc[bi][pi];
+                                if (!PG.cw || !PG.ch) continue;
+                                auto it = tidx.find(PG.first_block);
+                                if (it == tidx.end()) {
+                                    trees.emplace_back();
+                                    trees.back().incl.build(PG.cw, PG.ch);
+                                    trees.back().imsb.build(PG.cw, PG.ch);
+                                    it = tidx.emplace(PG.first_block, trees.size() - 1).first;
                                 }
-                                uint32_t np = br.numpasses();
-                                numlenbits[b] += br.commacode();
-                                uint32_t nbits = numlenbits[b] + floorlog2(np);
-                                if (nbits > 32) throw GkError("corrupt packet header (segment length)");
-                                uint32_t sl = br.read((int)nbits);
-                                blk[b].npasses += np;
-                                contrib.push_back({b, sl});
+                                Trees& T = trees[it->second];
+                                for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                                    uint32_t b = PG.first_block + k;
+                                    uint32_t inc;
+                                    if (!included[b]) inc = T.incl.decode(br, k, l + 1) <= l ? 1 : 0;
+                                    else inc = br.read(1);
+                                    if (!inc) continue;
+                                    if (!included[b]) {
+                                        uint32_t kmsbs = 0, v = T.imsb.decode(br, k, kmsbs);
+                                        while (v >= kmsbs) { ++kmsbs; if (kmsbs > 64) break; v = T.imsb.decode(br, k, kmsbs); }
+                                        kmsbs--;
+                                        uint32_t bnb = R.bands[bi].numbps;
+                                        blk[b].numbps = kmsbs > bnb ? 0 : bnb - kmsbs;
+                                        numlenbits[b] = 3;
+                                        included[b] = 1;
+                                    }
+                                    uint32_t np = br.numpasses();
+                                    numlenbits[b] += br.commacode();
+                                    uint32_t nbits = numlenbits[b] + floorlog2(np);
+                                    if (nbits > 32) throw GkError("corrupt packet header (segment length)");
+                                    uint32_t sl = br.read((int)nbits);
+                                    blk[b].npasses += np;
+                                    contrib.push_back({b, sl});
+                                }
                             }
                         }
-                    }
-                    br.align();
-                    pos = br.off;
-                    for (auto& ct : contrib) {
-                        uint32_t n = (uint32_t)std::min<size_t>(ct.second, Hd.tile_end > pos ? Hd.tile_end - pos : 0);
-                        if (n) chunks[ct.first].push_back({pos, n});
-                        pos += ct.second;
+                        br.align();
+                        pos = br.off;
+                        for (auto& ct : contrib) {
+                            uint32_t n = (uint32_t)std::min<size_t>(ct.second, tile_end > pos ? tile_end - pos : 0);
+                            if (n) chunks[ct.first].push_back({pos, n});
+                            pos += ct.second;
+                        }
                     }
                 }
-            }
-t2done:
+    tile_done:;
+    }
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     // ---- stage compressed bytes on the device
     const uint8_t* dcs = cs;

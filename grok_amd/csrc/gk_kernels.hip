@@ -126,8 +126,9 @@ __device__ __forceinline__ int mirror(int i, int n) {
 
 __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restrict__ src, uint32_t sstride,
                                                          int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h) {
+                                                         uint32_t h, GkTiles tb) {
     __shared__ int32_t T[DWT_LH][DWT_LW + 1];
+    src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
     const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH;
     const int tid = threadIdx.x;
     // load rows y0-2 .. y0+TH, cols x0-2 .. x0+TW (mirrored)
@@ -191,8 +192,9 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
 #define IDWT_LH (DWT_TH + 3)
 __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restrict__ src, uint32_t sstride,
                                                          int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h) {
+                                                         uint32_t h, GkTiles tb) {
     __shared__ int32_t T[IDWT_LH][IDWT_LW + 1];
+    src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
     const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH;
     const int tid = threadIdx.x;
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
@@ -282,15 +284,15 @@ void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int32_t* 
     dim3 grid((w + 255) / 256, h);
     hipLaunchKernelGGL(k_dc_inv, grid, dim3(256), 0, st, in, sin, out, sout, w, h, shift, mn, mx);
 }
-void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
-                         uint32_t w, uint32_t h) {
-    dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH);
-    hipLaunchKernelGGL(k_dwt53_fwd_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h);
+void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
+                         uint32_t h, GkTiles tb) {
+    dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
+    hipLaunchKernelGGL(k_dwt53_fwd_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h, tb);
 }
-void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
-                         uint32_t w, uint32_t h) {
-    dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH);
-    hipLaunchKernelGGL(k_dwt53_inv_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h);
+void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
+                         uint32_t h, GkTiles tb) {
+    dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
+    hipLaunchKernelGGL(k_dwt53_inv_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h, tb);
 }
 void gk_launch_gather(hipStream_t st, const uint8_t* src, uint8_t* dst, const uint64_t* seg, uint32_t nseg) {
     if (!nseg) return;

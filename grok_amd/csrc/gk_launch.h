@@ -14,9 +14,11 @@ void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, co
 void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift, int32_t mn, int32_t mx);
 void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
-                         uint32_t w, uint32_t h);
+                         uint32_t w, uint32_t h,
+                         GkTiles tb = GkTiles());
 void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
-                         uint32_t w, uint32_t h);
+                         uint32_t w, uint32_t h,
+                         GkTiles tb = GkTiles());
 void gk_launch_gather(hipStream_t st, const uint8_t* src, uint8_t* dst, const uint64_t* seg, uint32_t nseg);
 void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks, const uint64_t* sym_off, uint8_t* sym,
                      uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err, const int16_t* nmse_tab,
@@ -39,9 +41,11 @@ void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const 
 void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
                         uint32_t h, int32_t shift, int32_t mn, int32_t mx);
 void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h);
+                         uint32_t h,
+                         GkTiles tb = GkTiles());
 void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h);
+                         uint32_t h,
+                         GkTiles tb = GkTiles());
 // HTJ2K cleanup-pass block coder (gk_ht.hip)
 void gk_launch_ht_enc(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, uint8_t* mel_scratch,
                       uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err);

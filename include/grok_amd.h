@@ -42,13 +42,17 @@ typedef struct gk_cparameters {
     uint32_t prcw_init[GK_MAXRLVLS];     /* grk_cparameters::prcw_init */
     uint32_t prch_init[GK_MAXRLVLS];     /* grk_cparameters::prch_init */
     uint8_t write_comment;               /* write Grok's default COM marker (CodeStreamCompress.cpp:334) */
+    uint8_t tile_size_on;                /* grk_cparameters::tile_size_on */
+    uint32_t t_width, t_height;          /* grk_cparameters::t_width / t_height (tile origins on the 2^levels grid) */
+    uint8_t writeTLM;                    /* grk_cparameters::writeTLM (grk_compress -X) */
+    uint8_t writePLT;                    /* grk_cparameters::writePLT (grk_compress -L) */
 } gk_cparameters;
 
 /* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to
  * what the tile pipeline reads.  Component planes are int32 (grk_image_comp::data),
  * row stride in samples (grk_image_comp::stride). */
 typedef struct gk_image_info {
-    uint32_t w, h;          /* grk_image::x1 - x0, y1 - y0 (single tile at the origin) */
+    uint32_t w, h;          /* grk_image::x1 - x0, y1 - y0 (image at the origin; tiles per gk_cparameters) */
     uint32_t numcomps;      /* grk_image::numcomps */
     uint32_t prec;          /* grk_image_comp::prec (same for every component) */
     uint32_t sgnd;          /* grk_image_comp::sgnd */
@@ -76,7 +80,7 @@ void gk_set_default_params(gk_cparameters* p);
 
 /* grk_compress_init + grk_compress_start + grk_compress + grk_compress_end
  * (grok.cpp:382-469; TileProcessor::doCompress TileProcessor.cpp:202-260) for a
- * single-tile image.  comps[c] points at component c's int32 plane (device
+ * single- or multi-tile image (all tiles in one pass; one tile part per tile).  comps[c] points at component c's int32 plane (device
  * memory if comps_on_device, host otherwise).  The codestream is written to
  * out (device memory if out_on_device); *out_len receives its size.
  * Returns 0, or < 0 on error (-2: capacity too small, *out_len = needed). */

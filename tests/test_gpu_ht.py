@@ -16,6 +16,7 @@ import oracle as O
 pytestmark = pytest.mark.gpu
 
 HT = [f for f in FIXTURES if f.ht and not f.tiled]
+HT_ALL = [f for f in FIXTURES if f.ht]
 
 
 @pytest.fixture(scope="module")
@@ -31,14 +32,15 @@ def ht_params(numres=6, cblk=(64, 64)):
     return G.default_params(numresolution=numres, cblk=cblk, cblk_sty=0x40)
 
 
-@pytest.mark.parametrize("fx", HT, ids=fixture_ids(HT))
+@pytest.mark.parametrize("fx", HT_ALL, ids=fixture_ids(HT_ALL))
 def test_ht_encode_bit_exact_vs_grok(eng, fx):
-    cs = eng.encode(fx.img, fx.bits, params=ht_params())
+    from test_gpu_parity import gk_params
+    cs = eng.encode(fx.img, fx.bits, params=gk_params(fx.kw))
     assert len(cs) == len(fx.cs)
     assert cs == fx.cs
 
 
-@pytest.mark.parametrize("fx", HT, ids=fixture_ids(HT))
+@pytest.mark.parametrize("fx", HT_ALL, ids=fixture_ids(HT_ALL))
 def test_ht_decode_grok_stream(eng, fx):
     np.testing.assert_array_equal(eng.decode(fx.cs), fx.grok_decoded)
     np.testing.assert_array_equal(eng.decode(fx.cs), fx.img)

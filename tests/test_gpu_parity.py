@@ -13,8 +13,8 @@ import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-PART1_LOSSLESS = [f for f in FIXTURES if f.lossless and not f.ht and not f.tiled]
-PART1_LOSSY = [f for f in FIXTURES if not f.lossless and not f.ht and not f.tiled]
+PART1_LOSSLESS = [f for f in FIXTURES if f.lossless and not f.ht]
+PART1_LOSSY = [f for f in FIXTURES if not f.lossless and not f.ht]
 # 9/7 decode tolerance vs Grok's own decode: max-abs <= 1 LSB
 TOL_97_MAXABS = 1
 
@@ -32,7 +32,7 @@ def gk_params(kw):
     k = {}
     if "numres" in kw:
         k["numresolution"] = kw["numres"]
-    for n in ("cblk", "precincts", "irreversible", "layer_rate"):
+    for n in ("cblk", "precincts", "irreversible", "layer_rate", "cblk_sty", "tiles", "tlm", "plt"):
         if n in kw:
             k[n] = kw[n]
     if "layer_rate" in kw:
