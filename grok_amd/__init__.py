@@ -75,6 +75,13 @@ def load_library(build_if_missing=True):
     lib.gk_encode.restype = ctypes.c_int
     lib.gk_encode.argtypes = [ctypes.c_void_p, P(ImageInfo), P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_int,
                               P(CParameters), ctypes.c_void_p, ctypes.c_size_t, P(ctypes.c_size_t), ctypes.c_int]
+    lib.gk_encode_tiles.restype = ctypes.c_int
+    lib.gk_encode_tiles.argtypes = [ctypes.c_void_p, P(ImageInfo), P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_int,
+                                    P(CParameters), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
+                                    P(ctypes.c_size_t), P(ctypes.c_uint32), ctypes.c_int]
+    lib.gk_main_header.restype = ctypes.c_int
+    lib.gk_main_header.argtypes = [ctypes.c_void_p, P(ImageInfo), P(CParameters), ctypes.c_void_p, ctypes.c_size_t,
+                                   P(ctypes.c_size_t), P(ctypes.c_size_t), P(ctypes.c_uint32)]
     lib.gk_decode_header.restype = ctypes.c_int
     lib.gk_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ImageInfo)]
     lib.gk_decode.restype = ctypes.c_int
@@ -200,6 +207,65 @@ class Engine:
         if rc != 0:
             self._err("gk_encode")
         return buf[:n.value].tobytes()
+
+    def _planes_ptrs(self, planes, row0=0):
+        """Component base pointers addressing image row 0 for a (C, rows, W) slab whose
+        first row is image row ``row0`` (only the slab's rows are ever read)."""
+        c, h, w = planes.shape
+        if _is_torch_cuda(planes):
+            assert str(planes.dtype) == "torch.int32" and planes.is_contiguous()
+            base, keep = planes.data_ptr(), planes
+        else:
+            keep = np.ascontiguousarray(planes, dtype=np.int32)
+            base = keep.ctypes.data
+        ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 - row0 * w * 4 for k in range(c)])
+        return ptrs, keep
+
+    def encode_tiles(self, planes, prec, tile_begin, tile_end, image_hw=None, row0=0, signed=False, params=None,
+                     out=None):
+        """gk_encode_tiles: tile parts of tiles [tile_begin, tile_end) only (tile sharding).
+        planes: (C, rows, W) slab starting at image row ``row0`` (the whole image by
+        default); image_hw = (H, W) of the full image.  Returns (bytes or length, part_lens)."""
+        if params is None:
+            params = default_params()
+        c, h, w = planes.shape
+        H, W = image_hw if image_hw else (h, w)
+        assert W == w
+        info = ImageInfo(W, H, c, prec, int(signed))
+        ptrs, keep = self._planes_ptrs(planes, row0)
+        on_dev = _is_torch_cuda(planes)
+        strides = (ctypes.c_uint32 * c)(*([w] * c))
+        lens = (ctypes.c_uint32 * (tile_end - tile_begin))()
+        n = ctypes.c_size_t()
+        if out is not None:
+            rc = self.lib.gk_encode_tiles(self.ctx, ctypes.byref(info), ptrs, strides, int(on_dev), ctypes.byref(params),
+                                          tile_begin, tile_end, ctypes.c_void_p(out.data_ptr()), out.numel(),
+                                          ctypes.byref(n), lens, 1)
+            if rc != 0:
+                self._err("gk_encode_tiles")
+            return n.value, list(lens)
+        cap = c * h * w * 4 + (1 << 20)
+        buf = np.empty(cap, np.uint8)
+        rc = self.lib.gk_encode_tiles(self.ctx, ctypes.byref(info), ptrs, strides, int(on_dev), ctypes.byref(params),
+                                      tile_begin, tile_end, buf.ctypes.data, cap, ctypes.byref(n), lens, 0)
+        if rc != 0:
+            self._err("gk_encode_tiles")
+        del keep
+        return buf[:n.value].tobytes(), list(lens)
+
+    def main_header(self, image_shape, prec, signed=False, params=None):
+        """gk_main_header: (header bytes, TLM entry offset or 0, number of tiles)."""
+        if params is None:
+            params = default_params()
+        c, h, w = image_shape
+        info = ImageInfo(w, h, c, prec, int(signed))
+        buf = np.empty(1 << 20, np.uint8)
+        n, tlm, nt = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_uint32()
+        rc = self.lib.gk_main_header(self.ctx, ctypes.byref(info), ctypes.byref(params), buf.ctypes.data, buf.size,
+                                     ctypes.byref(n), ctypes.byref(tlm), ctypes.byref(nt))
+        if rc != 0:
+            self._err("gk_main_header")
+        return buf[:n.value].tobytes(), tlm.value, nt.value
 
     # ------------------------------------------------------------------ decode
     def read_header(self, cs, length=None):

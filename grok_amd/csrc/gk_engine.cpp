@@ -870,14 +870,18 @@ static void ensure_plan(gk_ctx* ctx, const Plan& want) {
 }
 
 // Forward/inverse DWT over all components with the ping-pong placement of gk_common.h.
-static void run_dwt(gk_ctx* ctx, bool forward) {
+static void run_dwt(gk_ctx* ctx, bool forward, uint32_t jb = 0, uint32_t je = 0xffffffffu) {
     Plan& P = ctx->plan;
     int32_t* arena = (int32_t*)ctx->arena.p;
     const uint32_t L = P.p.numres - 1;
     ctx->tm.dwt_launches = 0; ctx->tm.dwt_bytes = 0;
     for (uint32_t i = 0; i < L; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
-        for (const ShapeG& S : P.shapes) {        // one launch per tile shape, grid.z = tiles of that shape
+        for (const ShapeG& S0 : P.shapes) {       // one launch per tile shape, grid.z = tiles of that shape
+            ShapeG S = S0;                        // restricted to tile rows [jb, je)
+            const uint32_t sj0 = std::max(S.tb.j0, jb), sj1 = std::min(S.tb.j0 + S.tb.ny, je);
+            if (sj0 >= sj1) continue;
+            S.tb.j0 = sj0; S.tb.ny = sj1 - sj0;
             const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
             for (uint32_t c = 0; c < P.nc; ++c) {
                 int32_t* A = arena + (size_t)c * 2 * P.plane_elems;
@@ -907,9 +911,10 @@ static float ev_ms(gk_ctx* ctx, int a, int b) {
 // ---------------------------------------------------------------------------
 // Encode
 // ---------------------------------------------------------------------------
-static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
-                          int comps_on_device, const gk_cparameters* cp, uint8_t* out, size_t cap, int out_on_device,
-                          int* rc) {
+// Encode tiles [tb, te) (te = 0: all).  with_header: SOC..main header + tile parts + EOC
+// (a complete codestream); otherwise only the tile parts, back to back, with their
+// lengths in part_lens (tile sharding across devices).
+static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparameters* cp) {
     Plan want;
     want.w = info->w; want.h = info->h; want.nc = info->numcomps; want.prec = info->prec; want.sgnd = info->sgnd;
     set_params(want.p, cp);
@@ -922,8 +927,21 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if ((1u << want.p.cbw) > 64 || (1u << want.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
     ensure_plan(ctx, want);
+}
+
+static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+                          int comps_on_device, const gk_cparameters* cp, uint8_t* out, size_t cap, int out_on_device,
+                          int* rc, uint32_t tb = 0, uint32_t te = 0, bool with_header = true,
+                          uint32_t* part_lens = nullptr) {
+    setup_plan(ctx, info, cp);
     Plan& P = ctx->plan;
+    const uint32_t ntiles = (uint32_t)P.tiles.size();
+    if (te == 0) { tb = 0; te = ntiles; }
+    if (tb >= te || te > ntiles) throw GkError("bad tile range");
     const uint32_t nb = (uint32_t)P.blocks.size();
+    const uint32_t b0 = P.tiles[tb].b0, b1 = P.tiles[te - 1].b1, nbr = b1 - b0;   // block range of the tiles
+    const uint32_t jb = tb / P.ntx, je = (te - 1) / P.ntx + 1;                     // tile rows touched
+    const uint32_t ry0 = P.tiles[jb * P.ntx].y0, ry1 = P.tiles[(je - 1) * P.ntx].y1;  // sample rows touched
     hipStream_t st = ctx->st;
 
     HIPCHK(hipEventRecord(ctx->ev[0], st));
@@ -934,28 +952,31 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     if (!comps_on_device) {
         int32_t* dp = (int32_t*)ctx->dplanes.get((size_t)P.w * P.h * P.nc * 4);
         for (uint32_t c = 0; c < P.nc; ++c) {
-            HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * P.h, (size_t)P.w * 4, comps[c], (size_t)strides[c] * 4,
-                                    (size_t)P.w * 4, P.h, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * P.h + (size_t)ry0 * P.w, (size_t)P.w * 4,
+                                    comps[c] + (size_t)ry0 * strides[c], (size_t)strides[c] * 4,
+                                    (size_t)P.w * 4, ry1 - ry0, hipMemcpyHostToDevice, st));
             src[c] = dp + (size_t)c * P.w * P.h; sstr[c] = P.w;
         }
     } else {
         for (uint32_t c = 0; c < P.nc; ++c) { src[c] = comps[c]; sstr[c] = strides[c]; }
     }
     HIPCHK(hipEventRecord(ctx->ev[1], st));
-    // DC shift + MCT into plane A of each component
+    // DC shift + MCT into plane A of each component (rows of the selected tiles)
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
-    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems; };
+    const uint32_t nrows = ry1 - ry0;
+    for (uint32_t c = 0; c < P.nc; ++c) src[c] += (size_t)ry0 * sstr[c];
+    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems + (size_t)ry0 * P.stride; };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
     if (!P.p.irrev) {
-        if (mct3) gk_launch_dc_rct_fwd(st, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), P.stride, P.w, P.h, shift);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), P.stride, P.w, P.h, shift);
+        if (mct3) gk_launch_dc_rct_fwd(st, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), P.stride, P.w, nrows, shift);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), P.stride, P.w, nrows, shift);
     } else {
-        if (mct3) gk_launch_dc_ict_fwd(st, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), P.stride, P.w, P.h, shift);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, src[c], sstr[c], planeAf(c), P.stride, P.w, P.h, shift);
+        if (mct3) gk_launch_dc_ict_fwd(st, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), P.stride, P.w, nrows, shift);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, src[c], sstr[c], planeAf(c), P.stride, P.w, nrows, shift);
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    run_dwt(ctx, true);
+    run_dwt(ctx, true, jb, je);
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // T1
     const bool do_rc = P.p.rate_control();
@@ -976,19 +997,23 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         ctx->blocks_uploaded = true;
     }
     HIPCHK(hipMemsetAsync(derr, 0, 64, st));
+    // the selected tiles' code-blocks are the contiguous range [b0, b1): per-block arrays are offset
+    const size_t MP = GK_MAX_PASSES;
     if (P.p.ht()) {
         // HT cleanup pass (T1HT::compress, T1HT.cpp:109-133); MEL bytes staged in the symbol buffer
         uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nb * GK_HT_MEL_CAP + 256);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_ht_enc(st, arena, dblk, dbytes, mel, GK_HT_MEL_CAP, dinfo, nb, derr);
+        gk_launch_ht_enc(st, arena, dblk + b0, dbytes, mel, GK_HT_MEL_CAP, dinfo + 4 * (size_t)b0, nbr, derr);
     } else {
-        gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nb, derr, ctx->nmse_tab, dnmse);
+        gk_launch_t1_cm(st, arena, dblk + b0, dsymoff + b0, dsym, dpe + MP * b0, dcm + 2 * (size_t)b0, nbr, derr,
+                        ctx->nmse_tab, dnmse ? dnmse + MP * b0 : nullptr);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nb, derr, dnmse, dpcount);
+        gk_launch_t1_mq(st, dsym, dsymoff + b0, dpe + MP * b0, dcm + 2 * (size_t)b0, dblk + b0, dbytes, dps,
+                        dinfo + 4 * (size_t)b0, nbr, derr, dnmse ? dnmse + MP * b0 : nullptr, dpcount);
     }
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(16 * (size_t)nb + 64);
-    HIPCHK(hipMemcpyAsync(hinfo, dinfo, 16 * (size_t)nb, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hinfo + 4 * (size_t)b0, dinfo + 4 * (size_t)b0, 16 * (size_t)nbr, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(hinfo + 4 * (size_t)nb, derr, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t t1err = hinfo[4 * (size_t)nb], npass_total = hinfo[4 * (size_t)nb + 4];
@@ -1008,6 +1033,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     size_t tlm_pos = 0;
     write_main_header(H, P, &tlm_pos);
     const size_t header_size = H.size();
+    if (!with_header) H.clear();
     T2Enc T2(P, hinfo, hpasses);
     T2.allocate(header_size);
     // segments: (src_off in dbytes, dst_off in codestream, len); host bytes staged after the slots
@@ -1027,7 +1053,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     struct Pk { uint32_t hoff, hlen, s0, s1, len; };
     std::vector<Pk> pk;
     std::vector<uint8_t> tp;             // SOT [PLT] SOD bytes of the current tile
-    for (uint32_t t = 0; t < P.tiles.size(); ++t) {
+    for (uint32_t t = tb; t < te; ++t) {
         const TileG& T = P.tiles[t];
         pk.clear(); phdr.clear(); bsegs.clear();
         for (uint32_t l = 0; l < P.p.nlayers; ++l)
@@ -1066,7 +1092,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         for (const Pk& k : pk) psot += k.len;
         if (psot > 0xffffffffull) throw GkError("tile part exceeds 4 GiB");
         tp[6] = (uint8_t)(psot >> 24); tp[7] = (uint8_t)(psot >> 16); tp[8] = (uint8_t)(psot >> 8); tp[9] = (uint8_t)psot;
-        if (P.p.tlm) {
+        if (part_lens) part_lens[t - tb] = (uint32_t)psot;
+        if (P.p.tlm && with_header) {
             uint8_t* e = hdrs.data() + tlm_pos + 6 * (size_t)t;   // the main header is hdrs[0 .. H.size())
             e[0] = (uint8_t)(t >> 8); e[1] = (uint8_t)t;
             e[2] = (uint8_t)(psot >> 24); e[3] = (uint8_t)(psot >> 16); e[4] = (uint8_t)(psot >> 8); e[5] = (uint8_t)psot;
@@ -1090,7 +1117,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         }
     }
     uint8_t eoc[2] = {0xff, 0xd9};
-    add_host(eoc, 2);
+    if (with_header) add_host(eoc, 2);
     const size_t total = pos;
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (total > cap) { *rc = -2; return total; }
@@ -1116,14 +1143,14 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     ctx->tm.t1_coder_ms = ev_ms(ctx, 8, 4);
     ctx->tm.cs_bytes = total;
     {
-        uint64_t tb = 0;
-        for (uint32_t b = 0; b < nb; ++b) tb += hinfo[4 * (size_t)b + 2];
-        ctx->tm.t1_bytes = tb;
+        uint64_t tbytes = 0;
+        for (uint32_t b = b0; b < b1; ++b) tbytes += hinfo[4 * (size_t)b + 2];
+        ctx->tm.t1_bytes = tbytes;
     }
     ctx->tm.t2_ms = ev_ms(ctx, 4, 5);
     ctx->tm.assemble_ms = ev_ms(ctx, 5, 7);
     ctx->tm.total_ms = ev_ms(ctx, 0, 7);
-    ctx->tm.t1_blocks = nb;
+    ctx->tm.t1_blocks = nbr;
     *rc = 0;
     return total;
 }
@@ -1315,6 +1342,12 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 }
     tile_done:;
     }
+    // decode only the tile rows whose tiles are present (sharded / windowed decode)
+    uint32_t jb = P.nty, je = 0;
+    for (uint32_t t = 0; t < P.tiles.size(); ++t)
+        if (seen[t]) { jb = std::min(jb, t / P.ntx); je = std::max(je, t / P.ntx + 1); }
+    const uint32_t b0 = P.tiles[jb * P.ntx].b0, b1 = P.tiles[je * P.ntx - 1].b1, nbr = b1 - b0;
+    const uint32_t ry0 = P.tiles[jb * P.ntx].y0, ry1 = P.tiles[(je - 1) * P.ntx].y1, nrows = ry1 - ry0;
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     // ---- stage compressed bytes on the device
     const uint8_t* dcs = cs;
@@ -1357,7 +1390,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // HT cleanup pass decode straight into the band windows (T1HT::decompress, T1HT.cpp:134-187)
         int* derr = (int*)ctx->derr.get(64);
         HIPCHK(hipMemsetAsync(derr, 0, 64, st));
-        gk_launch_ht_dec(st, src_bytes, dblk, arena, nb, derr);
+        gk_launch_ht_dec(st, src_bytes, dblk + b0, arena, nbr, derr);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         int herr = 0;
         HIPCHK(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st));
@@ -1366,40 +1399,40 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     } else {
         // lane assignment: blocks bucketed by pass count (descending), so the 64 lanes of a
         // wave decode similar amounts of work and the longest waves start first
-        const uint32_t nw = (nb + 63) / 64;
-        uint32_t* hord = (uint32_t*)ctx->hord.get(4 * (2 * (size_t)nb + 2) + 8 * ((size_t)nw + 1));
-        uint32_t* hpos = hord + nb;
-        uint64_t* hwo = (uint64_t*)(hord + 2 * (size_t)nb + 2);
+        const uint32_t nw = (nbr + 63) / 64;
+        uint32_t* hord = (uint32_t*)ctx->hord.get(4 * (2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
+        uint32_t* hpos = hord + nbr;                 // position of block b0 + k in the order
+        uint64_t* hwo = (uint64_t*)(hord + 2 * (size_t)nbr + 2);
         {
             std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
-            for (uint32_t b = 0; b < nb; ++b) cnt[std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1)]++;
+            for (uint32_t b = b0; b < b1; ++b) cnt[std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1)]++;
             std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
             uint32_t acc = 0;
             for (int k = GK_MAX_PASSES + 1; k >= 0; --k) { start[k] = acc; acc += cnt[k]; }
-            for (uint32_t b = 0; b < nb; ++b) {
+            for (uint32_t b = b0; b < b1; ++b) {
                 uint32_t k = std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1);
-                hord[start[k]] = b; hpos[b] = start[k]; start[k]++;
+                hord[start[k]] = b; hpos[b - b0] = start[k]; start[k]++;
             }
             uint64_t wo = 0;
             for (uint32_t wv = 0; wv < nw; ++wv) {
                 hwo[wv] = wo;
                 uint32_t mp = 0;
-                for (uint32_t i = wv * 64; i < std::min(nb, wv * 64 + 64); ++i) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
+                for (uint32_t i = wv * 64; i < std::min(nbr, wv * 64 + 64); ++i) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
                 wo += (260 + (uint64_t)mp * 64) * 64;
             }
             hwo[nw] = wo;
         }
-        uint32_t* dord = (uint32_t*)ctx->dord.get(4 * (2 * (size_t)nb + 2) + 8 * ((size_t)nw + 1));
-        HIPCHK(hipMemcpyAsync(dord, hord, 4 * (2 * (size_t)nb + 2) + 8 * ((size_t)nw + 1), hipMemcpyHostToDevice, st));
-        const uint32_t* dpos = dord + nb;
-        const uint64_t* dwo = (const uint64_t*)(dord + 2 * (size_t)nb + 2);
+        uint32_t* dord = (uint32_t*)ctx->dord.get(4 * (2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
+        HIPCHK(hipMemcpyAsync(dord, hord, 4 * (2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1), hipMemcpyHostToDevice, st));
+        const uint32_t* dpos = dord + nbr;
+        const uint64_t* dwo = (const uint64_t*)(dord + 2 * (size_t)nbr + 2);
         uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
-        gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nb);
+        gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nbr);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_t1_recon(st, dblk, dpos, dscr, dwo, arena, nb);
+        gk_launch_t1_recon(st, dblk + b0, dpos, dscr, dwo, arena, nbr);
     }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
-    run_dwt(ctx, false);
+    run_dwt(ctx, false, jb, je);
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     // ---- inverse MCT + DC shift + clamp into the output planes
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
@@ -1410,27 +1443,27 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     int32_t* stage = nullptr;
     if (!out_on_device) {
         stage = (int32_t*)ctx->dplanes.get((size_t)P.w * P.h * P.nc * 4);
-        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = stage + (size_t)c * P.w * P.h; dstr[c] = P.w; }
+        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = stage + (size_t)c * P.w * P.h + (size_t)ry0 * P.w; dstr[c] = P.w; }
     } else {
-        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = comps[c]; dstr[c] = strides[c]; }
+        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = comps[c] + (size_t)ry0 * strides[c]; dstr[c] = strides[c]; }
     }
-    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems; };
+    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems + (size_t)ry0 * P.stride; };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
     if (!P.p.irrev) {
-        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w, P.h,
+        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w, nrows,
                                        shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], P.w, P.h, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], P.w, nrows, shift, mn, mx);
     } else {
         if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w,
-                                       P.h, shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv_f(st, planeAf(c), P.stride, dst[c], dstr[c], P.w, P.h, shift, mn, mx);
+                                       nrows, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv_f(st, planeAf(c), P.stride, dst[c], dstr[c], P.w, nrows, shift, mn, mx);
     }
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (!out_on_device) {
         for (uint32_t c = 0; c < P.nc; ++c)
-            HIPCHK(hipMemcpy2DAsync(comps[c], (size_t)strides[c] * 4, dst[c], (size_t)P.w * 4, (size_t)P.w * 4, P.h,
-                                    hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpy2DAsync(comps[c] + (size_t)ry0 * strides[c], (size_t)strides[c] * 4, dst[c], (size_t)P.w * 4,
+                                    (size_t)P.w * 4, nrows, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipEventRecord(ctx->ev[6], st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1444,7 +1477,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     ctx->tm.mct_ms = ev_ms(ctx, 4, 5);
     ctx->tm.assemble_ms = ev_ms(ctx, 1, 2);
     ctx->tm.total_ms = ev_ms(ctx, 0, 6);
-    ctx->tm.t1_blocks = nb;
+    ctx->tm.t1_blocks = nbr;
 }
 
 // ---------------------------------------------------------------------------
@@ -1512,6 +1545,44 @@ int gk_encode(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comp
         if (out_len) *out_len = n;
         if (rc == -2) ctx->err = "output capacity too small";
         return rc;
+    } catch (const GkError& e) {
+        ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+                    int comps_on_device, const gk_cparameters* p, uint32_t tile_begin, uint32_t tile_end,
+                    uint8_t* out, size_t cap, size_t* out_len, uint32_t* part_lens, int out_on_device) {
+    if (!ctx || !info || !comps || !strides || !out || !part_lens || tile_end <= tile_begin) return -1;
+    try {
+        (void)hipSetDevice(ctx->device);
+        int rc = 0;
+        size_t n = encode_impl(ctx, info, comps, strides, comps_on_device, p, out, cap, out_on_device, &rc,
+                               tile_begin, tile_end, false, part_lens);
+        if (out_len) *out_len = n;
+        if (rc == -2) ctx->err = "output capacity too small";
+        return rc;
+    } catch (const GkError& e) {
+        ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_main_header(gk_ctx* ctx, const gk_image_info* info, const gk_cparameters* p, uint8_t* out, size_t cap,
+                   size_t* out_len, size_t* tlm_offset, uint32_t* num_tiles) {
+    if (!ctx || !info || !out) return -1;
+    try {
+        setup_plan(ctx, info, p);
+        std::vector<uint8_t> H;
+        size_t tlm = 0;
+        write_main_header(H, ctx->plan, &tlm);
+        if (out_len) *out_len = H.size();
+        if (tlm_offset) *tlm_offset = ctx->plan.p.tlm ? tlm : 0;
+        if (num_tiles) *num_tiles = (uint32_t)ctx->plan.tiles.size();
+        if (H.size() > cap) { ctx->err = "output capacity too small"; return -2; }
+        memcpy(out, H.data(), H.size());
+        return 0;
     } catch (const GkError& e) {
         ctx->err = e.msg;
         return -1;

@@ -40,3 +40,15 @@ def write_pnm(path, img, bits):
         f.write((b"P6" if c == 3 else b"P5") + b"\n%d %d\n%d\n" % (w, h, maxv))
         a = np.ascontiguousarray(img.transpose(1, 2, 0))
         f.write(a.astype(np.uint8).tobytes() if maxv < 256 else a.astype(">u2").tobytes())
+
+
+def synth_slab(y0, y1, h, w, c, bits, seed, chunk=1024):
+    """Rows [y0, y1) of synth_image(h, w, c, bits, seed) without building the rest
+    (each rank of a tile-sharded run generates only its own tile rows)."""
+    out = np.empty((c, y1 - y0, w), np.uint16)
+    for cy in range((y0 // chunk) * chunk, y1, chunk):
+        cy1 = min(h, cy + chunk)
+        rows = synth_rows(cy, cy1, w, c, bits, seed, h)
+        a, b = max(cy, y0), min(cy1, y1)
+        out[:, a - y0:b - y0, :] = rows[:, a - cy:b - cy, :]
+    return out

@@ -88,11 +88,31 @@ int gk_encode(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comp
               int comps_on_device, const gk_cparameters* p, uint8_t* out, size_t cap, size_t* out_len,
               int out_on_device);
 
+/* Tile sharding: encode only tiles [tile_begin, tile_end) of the
+ * image described by info / p — grk_compress_tile (grok.h:1082-1657) per tile, without
+ * the main header.  comps[c] addresses the image origin; only the sample rows of the
+ * selected tiles are read.  out receives their tile parts (SOT [PLT] SOD packets,
+ * CodeStreamCompress::writeTilePart :862-900) back to back; part_lens[i] = length
+ * of tile tile_begin + i (the TLM Ptlm value).  Returns 0 / < 0 like gk_encode. */
+int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+                    int comps_on_device, const gk_cparameters* p, uint32_t tile_begin, uint32_t tile_end,
+                    uint8_t* out, size_t cap, size_t* out_len, uint32_t* part_lens, int out_on_device);
+
+/* Main header alone (SOC SIZ [CAP] COD QCD [TLM] [COM]; CodeStreamCompress::
+ * init_header_writing :822-860) for assembling sharded tile parts: codestream =
+ * header + tile parts in tile order + EOC (0xFFD9).  With TLM, *tlm_offset is the
+ * offset of the first 6-byte entry (Ttlm u16 = tile index, Ptlm u32 = tile-part
+ * length, big-endian) for the caller to fill; *num_tiles = tiles in the grid. */
+int gk_main_header(gk_ctx* ctx, const gk_image_info* info, const gk_cparameters* p, uint8_t* out, size_t cap,
+                   size_t* out_len, size_t* tlm_offset, uint32_t* num_tiles);
+
 /* grk_decompress_read_header (grok.cpp:287-297, CodeStreamDecompress::readHeader) */
 int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, gk_image_info* info);
 
 /* grk_decompress (grok.cpp:287-297; TileProcessor::decompressT2T1 TileProcessor.cpp:384-408):
- * full-tile decode into comps[c] (int32 planes, device memory if out_on_device). */
+ * decode into comps[c] (int32 planes, device memory if out_on_device).  Every tile
+ * part present in cs is decoded; a stream holding the main header and only some
+ * tile parts (tile sharding, window decode) writes only those tiles' samples. */
 int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
               const uint32_t* strides, int out_on_device);
 

@@ -31,6 +31,9 @@ CONFIGS = {
     "C3_4k": dict(w=4096, h=4096, c=3, bits=12, seed=11, flags="-I -r 40,20,10"),
     "C3p": dict(w=8192, h=8192, c=3, bits=12, seed=11, flags="-I -r 40,20,10 -c [256,256]"),
     "C3_l1": dict(w=2048, h=2048, c=3, bits=12, seed=11, flags="-I"),
+    "C4": dict(w=16384, h=16384, c=1, bits=16, seed=20, flags="-M 64 -t 1024,1024 -X -L"),
+    "C4_4k": dict(w=4096, h=4096, c=1, bits=16, seed=20, flags="-M 64 -t 1024,1024 -X -L"),
+    "C4_p1": dict(w=4096, h=4096, c=1, bits=16, seed=20, flags="-t 1024,1024 -X -L"),
 }
 
 

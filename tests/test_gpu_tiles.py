@@ -102,3 +102,96 @@ def test_engine_reuse_refreshes_params(eng):
     for rates in ([40.0, 20.0], [20.0, 10.0], [40.0, 20.0]):
         kw = dict(irreversible=True, layer_rate=rates)
         assert eng.encode(img, 8, params=_params(**kw)) == O.encode(img, 8, **kw)
+
+
+def _c4_like(seed=3):
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 1 << 16, size=(1, 320, 288)).astype(np.int32)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_encode_tiles_assemble_equals_full(eng, world):
+    # each "rank" encodes its tile rows from its own slab; header + parts == one-shot encode
+    from grok_amd import shard
+    img = _c4_like()
+    kw = dict(tiles=(64, 64), cblk_sty=64, tlm=True, plt=True)
+    full = eng.encode(img, 16, params=_params(**kw))
+    assert full == O.encode(img, 16, **kw)
+    _, h, w = img.shape
+    ntx, nty = shard.tile_grid(h, w, 64, 64)
+    parts = []
+    for r in range(world):
+        tb, te, j0, j1 = shard.rank_tiles(ntx, nty, r, world)
+        y0, y1 = j0 * 64, min(h, j1 * 64)
+        blob, lens = eng.encode_tiles(img[:, y0:y1], 16, tb, te, image_hw=(h, w), row0=y0, params=_params(**kw))
+        parts += shard.split_parts(blob, lens, tb)
+    header, tlm, nt = eng.main_header(img.shape, 16, params=_params(**kw))
+    assert nt == ntx * nty
+    assert shard.assemble(header, tlm, parts) == full
+
+
+def test_decode_subset_of_tiles(eng):
+    from grok_amd import shard
+    img = _c4_like(4)
+    kw = dict(tiles=(64, 64), tlm=True)
+    cs = eng.encode(img, 16, params=_params(**kw))
+    header, parts = shard.split_codestream(cs)
+    ntx = (img.shape[2] + 63) // 64
+    sub = header + b"".join(b for t, b in parts if 2 * ntx <= t < 4 * ntx) + b"\xff\xd9"
+    dec = eng.decode(sub)
+    np.testing.assert_array_equal(dec[:, 128:256], img[:, 128:256])
+
+
+def _gpu_shard_worker(rank, world, port, q):
+    import os
+    import torch
+    import torch.distributed as dist
+    import grok_amd as G
+    from grok_amd import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.init()
+    dist.init_process_group("gloo", rank=rank, world_size=world)   # two ranks share the one GPU
+    try:
+        e = G.Engine(0)
+        img = _c4_like(5)
+        _, h, w = img.shape
+        kw = dict(tiles=(64, 64), cblk_sty=64, tlm=True, plt=True)
+        p = G.default_params(**kw)
+        ntx, nty = shard.tile_grid(h, w, 64, 64)
+
+        def enc(tb, te):
+            j0, j1 = tb // ntx, te // ntx
+            y0, y1 = j0 * 64, min(h, j1 * 64)
+            return e.encode_tiles(img[:, y0:y1], 16, tb, te, image_hw=(h, w), row0=y0, params=p)
+
+        def hdr():
+            hd, tlm, _ = e.main_header(img.shape, 16, params=p)
+            return hd, tlm
+
+        cs = shard.encode_sharded(dist, rank, world, enc, hdr, ntx, nty)
+        dec = shard.decode_sharded(dist, rank, world, cs, lambda sub: e.decode(sub), ntx, nty, 64)
+        if rank == 0:
+            q.put((cs == O.encode(img, 16, **kw), bool((dec == img).all())))
+        e.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_two_processes_one_gpu():
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == (True, True)
