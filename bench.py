@@ -11,8 +11,12 @@ allocation) runs inside the step.  value = pixels of all ranks / max-over-ranks
 wall time.  Single-tile configs shard as replicas (one image per GPU, no
 collective on the data path): scaling = "weak".
 
-The same JSON line carries an auxiliary measurement of configs[2] ("C3":
-8192x8192 12-bit RGB, 9/7 + ICT, 3 quality layers -r 40,20,10).
+The same JSON line carries auxiliary measurements of configs[2] ("C3":
+8192x8192 12-bit RGB, 9/7 + ICT, 3 quality layers -r 40,20,10) and configs[3]
+("C4": 16384x16384 16-bit mono, HTJ2K, 1024x1024 tiles, TLM + PLT).  With
+N > 1 ranks C4 is tile-sharded (strong scaling): each rank codes its tile rows
+from its own slab, rank 0 gathers the tile parts over RCCL and assembles the
+codestream; each rank then decodes its own tile parts.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3] [--no-aux]
 """
@@ -31,11 +35,14 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
 
 CONFIGS = {
-    "C2": dict(bits=8, seed=10, params=dict(), desc="8192x8192 8-bit RGB, 5/3 lossless + RCT, 64x64 code-blocks, "
-                                                   "6 resolutions, single tile, 1 layer"),
-    "C3": dict(bits=12, seed=11, params=dict(irreversible=True, layer_rate=[40.0, 20.0, 10.0]),
+    "C2": dict(size=8192, comps=3, bits=8, seed=10, params=dict(),
+               desc="8192x8192 8-bit RGB, 5/3 lossless + RCT, 64x64 code-blocks, 6 resolutions, single tile, 1 layer"),
+    "C3": dict(size=8192, comps=3, bits=12, seed=11, params=dict(irreversible=True, layer_rate=[40.0, 20.0, 10.0]),
                desc="8192x8192 12-bit RGB, 9/7 + ICT, 64x64 code-blocks, 6 resolutions, single tile, "
                     "3 layers -r 40,20,10 (PCRD)"),
+    "C4": dict(size=16384, comps=1, bits=16, seed=20,
+               params=dict(cblk_sty=0x40, tiles=(1024, 1024), tlm=True, plt=True),
+               desc="16384x16384 16-bit mono, HTJ2K, 5/3 lossless, 1024x1024 tiles, TLM + PLT (-M 64 -t 1024,1024 -X -L)"),
 }
 
 
@@ -44,7 +51,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--size", type=int, default=0, help="override the config's image side")
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--no-aux", action="store_true", help="skip the auxiliary C3 measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -96,8 +103,9 @@ class Runner:
         import grok_amd as G
         from grok_amd.synth import synth_image
         cfg = CONFIGS[name]
+        size = size or cfg["size"]
         self.name, self.cfg, self.size = name, cfg, size
-        self.img = synth_image(size, size, 3, cfg["bits"], cfg["seed"] + rank)
+        self.img = synth_image(size, size, cfg["comps"], cfg["bits"], cfg["seed"] + rank)
         self.x = torch.from_numpy(self.img.astype(np.int32)).to(device).contiguous()
         self.out = torch.empty(self.x.numel() * 4 + (1 << 24), dtype=torch.uint8, device=device)
         self.y = torch.empty_like(self.x)
@@ -116,7 +124,7 @@ class Runner:
         import torch
         self.step()
         torch.cuda.synchronize()
-        if "irreversible" not in self.cfg["params"]:
+        if not self.cfg["params"].get("irreversible"):
             if not torch.equal(self.x, self.y):
                 raise SystemExit("lossless round trip FAILED (%s)" % self.name)
         else:
@@ -126,6 +134,72 @@ class Runner:
             if psnr < 30.0:
                 raise SystemExit("9/7 round trip PSNR %.2f dB too low (%s)" % (psnr, self.name))
             return psnr
+        return None
+
+
+class ShardRunner:
+    """C4 on N ranks: tile rows split across ranks (grok_amd/shard.py).  One step =
+    every rank encodes its tiles from its slab (HBM -> tile parts in HBM), rank 0
+    gathers the tile parts (RCCL) and assembles the codestream in HBM, every rank
+    decodes its own tile parts back into its slab."""
+
+    def __init__(self, name, size, rank, world, device, dist):
+        import torch
+        import grok_amd as G
+        from grok_amd import shard
+        from grok_amd.synth import synth_slab
+        cfg = CONFIGS[name]
+        size = size or cfg["size"]
+        self.name, self.cfg, self.size, self.rank, self.world, self.dist = name, cfg, size, rank, world, dist
+        self.device = device
+        tw, th = cfg["params"]["tiles"]
+        self.ntx, self.nty = shard.tile_grid(size, size, th, tw)
+        self.tb, self.te, j0, j1 = shard.rank_tiles(self.ntx, self.nty, rank, world)
+        if self.te <= self.tb:
+            raise SystemExit("C4 sharding needs at least one tile row per rank")
+        self.y0, self.y1 = j0 * th, min(size, j1 * th)
+        slab = synth_slab(self.y0, self.y1, size, size, cfg["comps"], cfg["bits"], cfg["seed"])
+        self.x = torch.from_numpy(slab.astype(np.int32)).to(device).contiguous()
+        self.y = torch.empty_like(self.x)
+        self.eng = G.Engine(device.index or 0)
+        self.params = G.default_params(**cfg["params"])
+        hdr, self.tlm, _ = self.eng.main_header((cfg["comps"], size, size), cfg["bits"], params=self.params)
+        self.hdr = torch.frombuffer(bytearray(hdr), dtype=torch.uint8).to(device)
+        self.eoc = torch.tensor([0xFF, 0xD9], dtype=torch.uint8, device=device)
+        self.parts = torch.empty(self.x.numel() * 4 + (1 << 22), dtype=torch.uint8, device=device)
+        self.n = 0
+        self.cs = None
+
+    def step(self):
+        import torch
+        n, lens = self.eng.encode_tiles(self.x, self.cfg["bits"], self.tb, self.te, image_hw=(self.size, self.size),
+                                        row0=self.y0, params=self.params, out=self.parts)
+        te = self.eng.timings()
+        # gather tile parts to rank 0 (lengths, then padded payload) over RCCL
+        ln = torch.tensor([n], dtype=torch.int64, device=self.device)
+        lns = [torch.zeros_like(ln) for _ in range(self.world)]
+        self.dist.all_gather(lns, ln)
+        mx = int(max(int(v.item()) for v in lns))
+        payload = self.parts[:mx]
+        if self.rank == 0:
+            bufs = [torch.empty(mx, dtype=torch.uint8, device=self.device) for _ in range(self.world)]
+            self.dist.gather(payload, bufs, dst=0)
+            self.cs = torch.cat([self.hdr] + [b[:int(k.item())] for b, k in zip(bufs, lns)] + [self.eoc])
+            self.n = int(self.cs.numel())
+        else:
+            self.dist.gather(payload, None, dst=0)
+        # each rank decodes its own tile parts (main header + parts + EOC) into its slab
+        sub = torch.cat([self.hdr, self.parts[:n], self.eoc])
+        self.eng.decode(sub, length=int(sub.numel()), out=self.y, row0=self.y0)
+        td = self.eng.timings()
+        return te, td
+
+    def check(self):
+        import torch
+        self.step()
+        torch.cuda.synchronize()
+        if not torch.equal(self.x, self.y):
+            raise SystemExit("sharded lossless round trip FAILED (%s)" % self.name)
         return None
 
 
@@ -167,24 +241,44 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
 
-    S = args.size
-    r = Runner(args.config, S, rank, device)
+    r = Runner(args.config, args.size, rank, device)
+    S = r.size
     r.check()
     el, m = timed(r, args.steps, args.warmup, world, dist, device)
     ms = el * 1000.0 / args.steps
-    samples = S * S * 3
+    samples = S * S * r.cfg["comps"]
     value = S * S / 1e6 * world * args.steps / el
 
     aux = None
     if not args.no_aux and args.config == "C2":
-        r3 = Runner("C3", S, rank, device)
+        aux = {}
+        r.eng.close()
+        del r.x, r.y, r.out
+        torch.cuda.empty_cache()
+        r3 = Runner("C3", args.size, rank, device)
         psnr = r3.check()
         el3, m3 = timed(r3, 2, 1, world, dist, device)
-        aux = {"config": "C3: " + CONFIGS["C3"]["desc"], "value": round(S * S / 1e6 * world * 2 / el3, 3),
-               "unit": "Mpixels/s", "ms_per_step": round(el3 * 500.0, 3), "psnr_db": round(psnr, 3),
-               "codestream_bytes": int(r3.n),
-               "stages_ms": {k: round(v, 3) for k, v in m3.items() if k.endswith("_ms") and v > 0}}
+        S3 = r3.size
+        aux["C3"] = {"config": "C3: " + CONFIGS["C3"]["desc"], "value": round(S3 * S3 / 1e6 * world * 2 / el3, 3),
+                     "unit": "Mpixels/s", "ms_per_step": round(el3 * 500.0, 3), "psnr_db": round(psnr, 3),
+                     "codestream_bytes": int(r3.n), "parallelism": "replicas x%d" % world,
+                     "stages_ms": {k: round(v, 3) for k, v in m3.items() if k.endswith("_ms") and v > 0}}
         r3.eng.close()
+        del r3
+        torch.cuda.empty_cache()
+        r4 = ShardRunner("C4", 0, rank, world, device, dist) if world > 1 else Runner("C4", 0, rank, device)
+        r4.check()
+        el4, m4 = timed(r4, 3, 1, world, dist, device)
+        S4 = r4.size
+        aux["C4"] = {"config": "C4: " + CONFIGS["C4"]["desc"], "value": round(S4 * S4 / 1e6 * 3 / el4, 3),
+                     "unit": "Mpixels/s", "ms_per_step": round(el4 * 1000.0 / 3, 3),
+                     "codestream_bytes": int(r4.n),
+                     "parallelism": ("tile rows sharded over %d ranks, RCCL gather of tile parts to rank 0" % world)
+                     if world > 1 else "1 GPU, all 256 tiles batched",
+                     "scaling": "strong",
+                     "stages_ms": {k: round(v, 3) for k, v in m4.items() if k.endswith("_ms") and v > 0},
+                     "t1_blocks": int(m4.get("enc_t1_blocks", 0))}
+        r4.eng.close()
 
     if rank == 0:
         # dominant kernel: the T1 stage with the largest average duration, measured with HIP
@@ -228,7 +322,8 @@ def main():
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(r.img, r.cfg["bits"], min(args.cpu_sample, S), r.cfg["params"])
         print(json.dumps(res), flush=True)
-    r.eng.close()
+    if aux is None:
+        r.eng.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -279,16 +279,19 @@ class Engine:
             self._err("gk_decode_header")
         return info
 
-    def decode(self, cs, length=None, out=None):
+    def decode(self, cs, length=None, out=None, row0=0):
         """cs: bytes (host) or torch cuda uint8 tensor (+length).  Returns a
-        (C, H, W) int32 numpy array, or fills ``out`` (torch cuda int32) in place."""
+        (C, H, W) int32 numpy array, or fills ``out`` (torch cuda int32) in place.
+        ``out`` may be a (C, rows, W) slab holding image rows [row0, row0+rows) when
+        cs carries only the tile parts of those rows (sharded decode)."""
         on_dev = _is_torch_cuda(cs)
         info = self.read_header(cs, length)
         c, h, w = info.numcomps, info.h, info.w
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         if out is not None:
             base = out.data_ptr()
-            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+            rows = out.shape[1]
+            ptrs = (ctypes.c_void_p * c)(*[base + k * rows * w * 4 - row0 * w * 4 for k in range(c)])
             res, out_dev = out, 1
         else:
             res = np.empty((c, h, w), np.int32)

@@ -32,15 +32,18 @@ def eng():
     e.close()
 
 
-@pytest.mark.parametrize("name", ["C1", "C2", "C2p"])
+@pytest.mark.parametrize("name", ["C1", "C2", "C2p", "C4_4k", "C4_p1", "C4"])
 def test_fullsize_lossless_bit_exact(eng, name):
+    """C1/C2: Part 1 single tile; C4: 16384^2 16-bit HTJ2K, 1024^2 tiles, TLM + PLT
+    (C4_4k / C4_p1: 4096^2 crops, HT and Part 1)."""
     import torch
     import grok_amd as G
     from conftest import parse_flags
     cfg = FULL[name]
     img = _img(cfg)
     kw = parse_flags(cfg["flags"])
-    params = G.default_params(precincts=kw.get("precincts"))
+    params = G.default_params(precincts=kw.get("precincts"), cblk_sty=kw.get("cblk_sty", 0), tiles=kw.get("tiles"),
+                              tlm=kw.get("tlm", False), plt=kw.get("plt", False))
     x = torch.from_numpy(img).cuda()
     out = torch.empty(img.nbytes + (1 << 24), dtype=torch.uint8, device="cuda")
     n = eng.encode(x, cfg["bits"], params=params, out=out)
