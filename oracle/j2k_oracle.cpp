@@ -487,6 +487,7 @@ struct MqDec {
     uint32_t a, c, ct;
     uint8_t st[NUM_CTX], mps[NUM_CTX];
     std::vector<uint8_t> store;
+    uint64_t ndec = 0;           // decisions decoded (instrumentation for tools/t1_simt_stats.py)
     void reset_states() {
         for (int i = 0; i < NUM_CTX; ++i) { st[i] = 0; mps[i] = 0; }
         st[CTX_UNI] = 46; st[CTX_AGG] = 3; st[CTX_ZC] = 4;
@@ -507,6 +508,7 @@ struct MqDec {
     }
     void renorm() { do { if (ct == 0) bytein(); a <<= 1; c <<= 1; --ct; } while (a < 0x8000); }
     uint32_t decode(int cx) {
+        ++ndec;
         const QeEntry& q = QE[st[cx]];
         uint32_t d;
         a -= q.qe;
@@ -765,18 +767,24 @@ static void t1_encode_block(const uint32_t* mag, const uint8_t* neg, uint32_t w,
 // half-bit reconstruction (oneplushalf), sign applied, like Grok's
 // uncompressedData before PostDecompressFilters.
 // ----------------------------------------------------------------------------
+// stripe_counts (optional, instrumentation): decisions per (pass, stripe), pass-major.
 static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses, uint32_t numbps,
-                            uint32_t orient, uint32_t w, uint32_t h, int32_t* out) {
+                            uint32_t orient, uint32_t w, uint32_t h, int32_t* out, uint32_t* stripe_counts = nullptr) {
     std::fill(out, out + (size_t)w * h, 0);
     if (!npasses || !numbps) return;
     T1State S; S.init(w, h);
     MqDec mq; mq.reset_states(); mq.init(data, len);
+    const uint32_t ns = (h + 3) / 4;
+    auto tick = [&](uint32_t p, uint32_t k) {
+        if (stripe_counts) stripe_counts[p * ns + k / 4] = (uint32_t)mq.ndec;
+        return true;
+    };
     int bpno1 = (int)numbps;   // bpno_plus_one
     int passtype = 2;
     for (uint32_t p = 0; p < npasses && bpno1 >= 1; ++p) {
         int32_t one = 1 << bpno1, half = one >> 1, oph = one | half;
         if (passtype == 0) {
-            for (uint32_t k = 0; k < h; k += 4)
+            for (uint32_t k = 0; k < h && tick(p, k); k += 4)
                 for (uint32_t x = 0; x < w; ++x)
                     for (uint32_t y = k; y < std::min(k + 4, h); ++y) {
                         uint8_t& st = S.at(x, y);
@@ -793,7 +801,7 @@ static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses,
                     }
         } else if (passtype == 1) {
             int32_t poshalf = half;
-            for (uint32_t k = 0; k < h; k += 4)
+            for (uint32_t k = 0; k < h && tick(p, k); k += 4)
                 for (uint32_t x = 0; x < w; ++x)
                     for (uint32_t y = k; y < std::min(k + 4, h); ++y) {
                         uint8_t& st = S.at(x, y);
@@ -805,7 +813,7 @@ static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses,
                         st |= S_MU;
                     }
         } else {
-            for (uint32_t k = 0; k < h; k += 4)
+            for (uint32_t k = 0; k < h && tick(p, k); k += 4)
                 for (uint32_t x = 0; x < w; ++x) {
                     uint32_t ylim = std::min(k + 4, h);
                     uint32_t y = k;
@@ -843,6 +851,7 @@ static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses,
         }
         if (++passtype == 3) { passtype = 0; --bpno1; }
     }
+    if (stripe_counts) stripe_counts[(size_t)npasses * ns] = (uint32_t)mq.ndec;
 }
 
 // ----------------------------------------------------------------------------
@@ -1875,6 +1884,14 @@ int orc_ht_encode_cblk(const int32_t* coef, uint32_t w, uint32_t h, uint32_t str
 }
 int orc_ht_decode_cblk(const uint8_t* data, uint32_t len, uint32_t w, uint32_t h, uint32_t k_msbs, int32_t* out) {
     return ht_decode_block(data, len, w, h, k_msbs, out, w) ? 0 : -1;
+}
+
+// Instrumentation: decisions at the start of every (pass, stripe) of a block decode
+// (counts[npasses * nstripes] = total).  Used by tools/t1_simt_stats.py only.
+void orc_t1_decode_stripe_counts(const uint8_t* data, uint32_t len, uint32_t npasses, uint32_t numbps, uint32_t orient,
+                                 uint32_t w, uint32_t h, uint32_t* counts) {
+    std::vector<int32_t> out((size_t)w * h);
+    t1_decode_block(data, len, npasses, numbps, orient, w, h, out.data(), counts);
 }
 
 // Single code-block T1 decode -> Grok's pre-filter values (2x magnitude with half bit).
