@@ -25,6 +25,7 @@ for s in $STEPS; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
         prof) (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$REPO/gpurun_out/prof" -o run -- python "$REPO/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-aux ${PROF_ARGS:-}) || exit $? ;;
+        profaux) (cd /tmp && run profaux 900 rocprofv3 --kernel-trace --stats -d "$REPO/gpurun_out/profaux" -o run -- python "$REPO/bench.py" --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-}) || exit $? ;;
         pmc) (cd /tmp && run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$REPO/gpurun_out/pmc_fetch" -o run -- python "$REPO/bench.py" --steps 2 --warmup 0 --no-cpu-baseline --no-aux ${PROF_ARGS:-} && run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$REPO/gpurun_out/pmc_write" -o run -- python "$REPO/bench.py" --steps 2 --warmup 0 --no-cpu-baseline --no-aux ${PROF_ARGS:-}) || exit $? ;;
     esac
 done
