@@ -435,10 +435,9 @@ struct ByteSrc {
     hipStream_t st = nullptr;
     static const size_t PG = 1 << 16;
     std::unordered_map<size_t, std::vector<uint8_t>> pages;
-    uint8_t at(size_t i) {
-        if (i >= len) return 0;
-        if (host) return host[i];
-        size_t pg = i / PG;
+    size_t last_pg = ~(size_t)0;             // fast path: the page of the previous access
+    const uint8_t* last = nullptr;
+    const uint8_t* page(size_t pg) {
         auto it = pages.find(pg);
         if (it == pages.end()) {
             size_t o = pg * PG, n = std::min(PG, len - o);
@@ -447,12 +446,18 @@ struct ByteSrc {
             HIPCHK(hipStreamSynchronize(st));
             it = pages.emplace(pg, std::move(v)).first;
         }
-        return it->second[i - pg * PG];
+        return it->second.data();
+    }
+    inline uint8_t at(size_t i) {
+        if (i >= len) return 0;
+        if (host) return host[i];
+        const size_t pg = i / PG;
+        if (pg != last_pg) { last = page(pg); last_pg = pg; }
+        return last[i - pg * PG];
     }
     uint32_t be16(size_t i) { return ((uint32_t)at(i) << 8) | at(i + 1); }
     uint32_t be32(size_t i) { return (be16(i) << 16) | be16(i + 2); }
 };
-
 struct BitReader {
     ByteSrc& s; size_t off; size_t end; uint32_t buf = 0; int ct = 0;
     BitReader(ByteSrc& src, size_t o, size_t e) : s(src), off(o), end(e) {}

@@ -486,6 +486,252 @@ __global__ __launch_bounds__(64) void k_t1_dec(const uint8_t* __restrict__ bytes
     }
 }
 
+// =============================================================================
+// Lane-independent variant: every lane walks its own (plane, pass, stripe)
+// sequence.  A step decodes one MQ decision per active lane, whatever pass type
+// the lane is in (SP / MR / CL share the position search, the context
+// formation and the CL phase machine).  A lane whose stripe-pass has no further
+// coding position parks; parked lanes cross their stripe boundary together once
+// `kpark` of them wait (or nothing else is active), which amortises the
+// divergent boundary code.  The next stripe's rows are prefetched into VGPRs
+// when a stripe starts, so a boundary never waits on memory (blocks of fewer
+// than three stripes reload synchronously at pass boundaries — their next
+// pass starts with rows still being stored).  Measured by
+// tools/t1_simt_stats.py: the critical path drops from the sum over stripes of
+// the per-stripe maximum over lanes to roughly the heaviest block.
+// =============================================================================
+struct Rows22 {   // one stripe's rows: S1..S5 / N1..N5 (rows y0..y0+4), P/M/B (rows y0..y0+3)
+    uint64_t s1, s2, s3, s4, s5, n1, n2, n3, n4, n5, p0, p1, p2, p3, m0, m1, m2, m3, b0, b1, b2, b3;
+};
+__device__ __forceinline__ void load_rows(Rows22& R, const uint64_t* WS, const uint64_t* BITS, int lane, uint32_t y0) {
+    const uint64_t* sg = WS + (size_t)(WS_SIG + y0 + 1) * 64 + lane;
+    const uint64_t* ng = WS + (size_t)(WS_NEG + y0 + 1) * 64 + lane;
+    const uint64_t* pi = WS + (size_t)(WS_PI + y0) * 64 + lane;
+    const uint64_t* mu = WS + (size_t)(WS_MU + y0) * 64 + lane;
+    const uint64_t* bt = BITS + (size_t)y0 * 64 + lane;
+    R.s1 = sg[0]; R.s2 = sg[64]; R.s3 = sg[128]; R.s4 = sg[192]; R.s5 = sg[256];
+    R.n1 = ng[0]; R.n2 = ng[64]; R.n3 = ng[128]; R.n4 = ng[192]; R.n5 = ng[256];
+    R.p0 = pi[0]; R.p1 = pi[64]; R.p2 = pi[128]; R.p3 = pi[192];
+    R.m0 = mu[0]; R.m1 = mu[64]; R.m2 = mu[128]; R.m3 = mu[192];
+    R.b0 = bt[0]; R.b1 = bt[64]; R.b2 = bt[128]; R.b3 = bt[192];
+}
+
+// next (plane, pass type, stripe) after (k, t, s); pass types 0 SP, 1 MR, 2 CL
+__device__ __forceinline__ void next_pos3(uint32_t& k, uint32_t& t, uint32_t& s, uint32_t& pidx, uint32_t ns) {
+    if (++s == ns) {
+        s = 0; ++pidx;
+        if (t == 2) { ++k; t = 0; } else ++t;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ bytes, const GkBlock* __restrict__ blocks,
+                                                   const uint32_t* __restrict__ order, uint64_t* __restrict__ scratch,
+                                                   const uint64_t* __restrict__ wave_off, uint32_t nblocks,
+                                                   unsigned long long* __restrict__ stats, uint32_t kpark) {
+    __shared__ DecLds Ls;
+    const int lane = threadIdx.x;
+    if (lane < 47) Ls.tab[lane] = c_mq[lane];
+    for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
+    for (int i = lane; i < 256; i += 64) Ls.sc[i] = sc_rule((uint32_t)i);
+    const uint32_t slot = blockIdx.x * 64 + lane;
+    const bool has = slot < nblocks;
+    GkBlock B = {};
+    if (has) B = blocks[order[slot]];
+    uint64_t* WS = scratch + wave_off[blockIdx.x];
+    const uint32_t numbps = has ? B.numbps : 0, npasses = (has && B.numbps) ? B.npasses : 0;
+    const uint32_t h = B.h;
+    const uint64_t colmask = B.w >= 64 ? ~0ull : ((1ull << B.w) - 1);
+    const uint32_t ns = (h + 3) >> 2;
+    const uint8_t* zc = Ls.zc[B.orient & 3];
+    for (int r = 0; r < WS_FIXED; ++r) WS[r * 64 + lane] = 0;   // clear the state rows (coalesced)
+    LaneDec L;
+    L.cw = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};   // mqc_resetstates: ZC0=4, AGG=3, UNI=46
+    L.step = 0; L.nsym = 0;
+    MqDec& q = L.q;
+    q.p = npasses ? bytes + B.data_off : bytes;
+    q.len = npasses ? B.len : 0;
+    q.bp = 0; q.fill = 0; q.sbase = 0;
+    stage_load(q);
+    __syncthreads();
+    ring_boundary(Ls.ring, lane, q);
+    q.sbase = q.fill; stage_load(q);
+    ring_boundary(Ls.ring, lane, q);
+    ring_boundary(Ls.ring, lane, q);
+    q.nb4 = ring_get4(Ls.ring, lane, 0);
+    q.c = (q.len ? (q.nb4 & 0xff) : 0xffu) << 16;   // INITDEC (mqc_dec.cpp:98-112)
+    mq_bytein(q, true);
+    q.c <<= 7; q.ct -= 7; q.a = 0x8000;
+
+    // position: plane k (0 = top), pass type t, stripe s, pass index pidx; k = 0 has only CL
+    uint32_t k = 0, t = 2, s = 0, pidx = 0;
+    bool done = npasses == 0, parked = false;
+    // stripe state
+    uint64_t S0 = 0, S1 = 0, S2 = 0, S3 = 0, S4 = 0, S5 = 0, N0 = 0, N1 = 0, N2 = 0, N3 = 0, N4 = 0, N5 = 0;
+    uint64_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, M0 = 0, M1 = 0, M2 = 0, M3 = 0, B0 = 0, B1 = 0, B2 = 0, B3 = 0;
+    uint64_t C0, C1, C2, C3, E, fresh = 0;
+    uint32_t nr = min(4u, h), x = 0, r = 0, ph = PH_FIND, colx = 0xffffffffu, rlhi = 0;
+    {
+        const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
+                       v3 = nr > 3 ? colmask : 0;
+        C0 = v0; C1 = v1; C2 = v2; C3 = v3;   // first CL: nothing significant yet
+        E = (nr == 4) ? colmask : 0ull;
+    }
+    // prefetch of the next stripe (always valid: rows a later stripe of the same pass reads are not
+    // touched by the current stripe; at a pass change small blocks patch rows from registers)
+    Rows22 X = {};
+    {
+        uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
+        next_pos3(k2, t2, s2, p2, ns);
+        if (!done && p2 < npasses && k2 < numbps) load_rows(X, WS, WS + (WS_BITS + (size_t)k2 * 64) * 64, lane, 4 * s2);
+    }
+
+    while (__any(!done)) {
+        // ---------------- stripe boundary for parked lanes (batched)
+        const uint32_t nparked = __popcll(__ballot(parked));
+        const uint32_t nactive = __popcll(__ballot(!done && !parked));
+        if (nparked && (nparked >= kpark || nactive == 0)) {
+            // commit the bytes staged at the previous boundary first: they are older than this
+            // boundary's stores, so waiting for them does not wait for the stores
+            if (!done && q.fill + 32 - q.bp <= 4 * RING_DW) {
+                ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3);
+                ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7);
+                q.fill += 32;
+            }
+            if (parked) {
+                parked = false;
+                if (t == 0) { P0 = C0; P1 = C1; P2 = C2; P3 = C3; }            // visited = candidates
+                else if (t == 1) { M0 |= C0; M1 |= C1; M2 |= C2; M3 |= C3; }    // now refined
+                const uint32_t y0 = 4 * s;
+                uint64_t* sg = WS + (size_t)(WS_SIG + y0 + 1) * 64 + lane;
+                uint64_t* ng = WS + (size_t)(WS_NEG + y0 + 1) * 64 + lane;
+                uint64_t* pi = WS + (size_t)(WS_PI + y0) * 64 + lane;
+                uint64_t* mu = WS + (size_t)(WS_MU + y0) * 64 + lane;
+                uint64_t* bt = WS + (WS_BITS + (size_t)k * 64 + y0) * 64 + lane;
+                sg[0] = S1; sg[64] = S2; sg[128] = S3; sg[192] = S4;
+                ng[0] = N1; ng[64] = N2; ng[128] = N3; ng[192] = N4;
+                pi[0] = P0; pi[64] = P1; pi[128] = P2; pi[192] = P3;
+                mu[0] = M0; mu[64] = M1; mu[128] = M2; mu[192] = M3;
+                bt[0] = B0; bt[64] = B1; bt[128] = B2; bt[192] = B3;
+                const uint32_t ok = k;
+                next_pos3(k, t, s, pidx, ns);
+                done = pidx >= npasses || k >= numbps;
+                // new stripe rows: prefetched, except rows the finished stripe still held in
+                // registers when the prefetch was issued (1-stripe blocks: all; 2-stripe blocks at
+                // a pass change: row 4 = the finished stripe's first row)
+                const bool one = ns == 1, two = ns == 2 && s == 0;
+                const uint64_t nS0 = s ? S4 : 0ull, nN0 = s ? N4 : 0ull;
+                const uint64_t nS1 = one ? S1 : X.s1, nS2 = one ? S2 : X.s2, nS3 = one ? S3 : X.s3, nS4 = one ? S4 : X.s4;
+                const uint64_t nS5 = two ? S1 : X.s5;
+                const uint64_t nN1 = one ? N1 : X.n1, nN2 = one ? N2 : X.n2, nN3 = one ? N3 : X.n3, nN4 = one ? N4 : X.n4;
+                const uint64_t nN5 = two ? N1 : X.n5;
+                const uint64_t nP0 = one ? P0 : X.p0, nP1 = one ? P1 : X.p1, nP2 = one ? P2 : X.p2, nP3 = one ? P3 : X.p3;
+                const uint64_t nM0 = one ? M0 : X.m0, nM1 = one ? M1 : X.m1, nM2 = one ? M2 : X.m2, nM3 = one ? M3 : X.m3;
+                const bool same_plane = one && ok == k;
+                const uint64_t nB0 = same_plane ? B0 : X.b0, nB1 = same_plane ? B1 : X.b1, nB2 = same_plane ? B2 : X.b2,
+                               nB3 = same_plane ? B3 : X.b3;
+                S0 = nS0; S1 = nS1; S2 = nS2; S3 = nS3; S4 = nS4; S5 = nS5;
+                N0 = nN0; N1 = nN1; N2 = nN2; N3 = nN3; N4 = nN4; N5 = nN5;
+                const bool newplane = t == 0 || k == 0;
+                P0 = t == 0 ? 0ull : nP0; P1 = t == 0 ? 0ull : nP1; P2 = t == 0 ? 0ull : nP2; P3 = t == 0 ? 0ull : nP3;
+                M0 = nM0; M1 = nM1; M2 = nM2; M3 = nM3;
+                B0 = newplane ? 0ull : nB0; B1 = newplane ? 0ull : nB1; B2 = newplane ? 0ull : nB2;
+                B3 = newplane ? 0ull : nB3;
+                const uint32_t ny0 = 4 * s;
+                nr = done ? 0u : min(4u, h - ny0);
+                const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
+                               v3 = nr > 3 ? colmask : 0;
+                const uint64_t dS0 = dil3(S0, S1, S2), dS1 = dil3(S1, S2, S3), dS2 = dil3(S2, S3, S4),
+                               dS3 = dil3(S3, S4, S5);
+                const uint64_t q0 = t == 0 ? dS0 : ~P0, q1 = t == 0 ? dS1 : ~P1, q2 = t == 0 ? dS2 : ~P2,
+                               q3 = t == 0 ? dS3 : ~P3;
+                const uint64_t w0 = t == 1 ? S1 : ~S1, w1 = t == 1 ? S2 : ~S2, w2 = t == 1 ? S3 : ~S3,
+                               w3 = t == 1 ? S4 : ~S4;
+                C0 = w0 & q0 & v0; C1 = w1 & q1 & v1; C2 = w2 & q2 & v2; C3 = w3 & q3 & v3;
+                E = (t == 2 && nr == 4) ? (C0 & C1 & C2 & C3 & ~dil3(S0 | S1, S2 | S3, S4 | S5)) : 0ull;
+                fresh = 0; x = 0; r = 0; ph = PH_FIND; colx = 0xffffffffu;
+            }
+            // uniform part: stage the next ring bytes, prefetch every lane's next stripe
+            q.sbase = q.fill;
+            stage_load(q);
+            q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+            uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
+            next_pos3(k2, t2, s2, p2, ns);
+            const bool pf = !done && p2 < npasses && k2 < numbps;
+            load_rows(X, WS, WS + (WS_BITS + (size_t)(pf ? k2 : 0) * 64) * 64, lane, pf ? 4 * s2 : 0);
+        }
+        // ---------------- one decision per active lane
+        const bool act = !done && !parked;
+        step_refill(L, Ls.ring, lane);
+        const bool finding = ph == PH_FIND;
+        bool pend = act;
+        if (act && finding) {
+            const bool found = find_next(C0, C1, C2, C3, x, r);
+            pend = found;
+            parked = !found;
+        }
+        const uint32_t xc = x & 63;
+        const bool is_cl = t == 2, is_mr = t == 1, is_sp = t == 0;
+        const bool agg = is_cl && finding && x != colx && ((E >> xc) & 1) && !(xc && ((fresh >> (xc - 1)) & 1));
+        colx = (is_cl && finding) ? x : colx;
+        const uint32_t sh = 3 * r;
+        const uint32_t fs = (win18(S0, S1, S2, S3, S4, S5, xc) >> sh) & 0x1ff;
+        const uint32_t fn = (win18(N0, N1, N2, N3, N4, N5, xc) >> sh) & 0x1ff;
+        const uint32_t sce = Ls.sc[sc_from9(fs, fn)];
+        const uint64_t mu = rsel(r, 0, M0) | rsel(r, 1, M1) | rsel(r, 2, M2) | rsel(r, 3, M3);
+        const uint32_t cx_mr = ((mu >> xc) & 1) ? CTX_MAG + 2 : ((fs & 0x1ef) ? CTX_MAG + 1 : CTX_MAG);
+        const uint32_t cx = is_mr ? cx_mr
+                                  : (agg ? CTX_AGG
+                                         : (ph == PH_SIGN ? CTX_SC + (sce & 15)
+                                                          : (finding ? CTX_ZC + zc[fs] : CTX_UNI)));
+        const uint32_t d = mq_decode(q, L.cw, Ls.tab, cx, pend);
+        L.nsym += pend ? 1 : 0;
+        // a decoded sign makes the sample significant (SP / CL)
+        const bool sig = pend && !is_mr && ph == PH_SIGN;
+        const uint64_t bx = sig ? (1ull << xc) : 0ull;
+        const uint64_t m0 = rsel(r, 0, bx), m1 = rsel(r, 1, bx), m2 = rsel(r, 2, bx), m3 = rsel(r, 3, bx);
+        S1 |= m0; S2 |= m1; S3 |= m2; S4 |= m3;
+        const uint64_t ng = (d ^ (sce >> 4)) ? ~0ull : 0ull;
+        N1 |= m0 & ng; N2 |= m1 & ng; N3 |= m2 & ng; N4 |= m3 & ng;
+        fresh |= bx;
+        // plane bit: new significance, or a refinement bit of 1
+        const uint64_t pb = bx | ((pend && is_mr && d) ? (1ull << xc) : 0ull);
+        B0 |= rsel(r, 0, pb); B1 |= rsel(r, 1, pb); B2 |= rsel(r, 2, pb); B3 |= rsel(r, 3, pb);
+        if (is_sp) {   // later positions gaining a significant neighbour join the candidates
+            const uint64_t bn = bx << 1;
+            const uint64_t b0 = rsel(r, 0, bn), b1 = rsel(r, 1, bn), b2 = rsel(r, 2, bn), b3 = rsel(r, 3, bn);
+            const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
+                           v3 = nr > 3 ? colmask : 0;
+            C0 |= (b0 | b1) & ~S1 & v0;
+            C1 |= (m0 | b0 | b1 | b2) & ~S2 & v1;
+            C2 |= (m1 | b1 | b2 | b3) & ~S3 & v2;
+            C3 |= (m2 | b2 | b3) & ~S4 & v3;
+        }
+        // position / phase advance (SP and CL share the CL machine without run-length)
+        uint32_t nph = ph, nr2 = r;
+        bool col_done = false;
+        if (is_mr) { nr2 = r + 1; }
+        else if (agg) { nph = d ? PH_UNI1 : PH_FIND; col_done = !d; }
+        else if (finding) { nph = d ? PH_SIGN : PH_FIND; nr2 = d ? r : r + 1; }
+        else if (ph == PH_UNI1) { rlhi = d; nph = PH_UNI2; }
+        else if (ph == PH_UNI2) { nr2 = (rlhi << 1) | d; nph = PH_SIGN; }
+        else { nph = PH_FIND; nr2 = r + 1; }
+        if (pend) {
+            ph = nph;
+            r = col_done ? 0 : nr2;
+            x += (col_done || r == 4) ? 1 : 0;
+            r &= 3;
+        }
+        step_prefetch(L, Ls.ring, lane);
+    }
+    if (stats) {
+        unsigned long long tot = L.nsym;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        if (lane == 0) { atomicAdd(&stats[0], (unsigned long long)L.step); atomicAdd(&stats[1], tot);
+                         atomicMax(&stats[2], (unsigned long long)L.step); }
+    }
+}
+
 // Reconstruction + dequantisation: wave per block, lane = column.
 __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blocks, const uint32_t* __restrict__ pos,
                                                  const uint64_t* __restrict__ scratch,
@@ -538,8 +784,19 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     const bool want = getenv("GK_T1_STATS") != nullptr;
     if (want && !stats) { (void)hipMalloc(&stats, 64); }
     if (want) (void)hipMemsetAsync(stats, 0, 64, st);
-    hipLaunchKernelGGL(k_t1_dec, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch, wave_off,
-                       nblocks, want ? stats : nullptr);
+    static int variant = -1, kpark = 4;
+    if (variant < 0) {
+        const char* v = getenv("GK_T1DEC");       // 0: stripe-synchronous, 1 (default): lane-independent
+        variant = v ? atoi(v) : 1;
+        const char* kp = getenv("GK_T1DEC_PARK");
+        if (kp) kpark = atoi(kp);
+    }
+    if (variant == 0)
+        hipLaunchKernelGGL(k_t1_dec, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
+                           wave_off, nblocks, want ? stats : nullptr);
+    else
+        hipLaunchKernelGGL(k_t1_dec_ind, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
+                           wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
     if (want) {
         unsigned long long h[3];
         (void)hipMemcpyAsync(h, stats, 24, hipMemcpyDeviceToHost, st);
