@@ -579,6 +579,7 @@ __global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ b
     // prefetch of the next stripe (always valid: rows a later stripe of the same pass reads are not
     // touched by the current stripe; at a pass change small blocks patch rows from registers)
     Rows22 X = {};
+    uint32_t nevents = 0;
     {
         uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
         next_pos3(k2, t2, s2, p2, ns);
@@ -590,9 +591,11 @@ __global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ b
         const uint32_t nparked = __popcll(__ballot(parked));
         const uint32_t nactive = __popcll(__ballot(!done && !parked));
         if (nparked && (nparked >= kpark || nactive == 0)) {
+            ++nevents;
             // commit the bytes staged at the previous boundary first: they are older than this
             // boundary's stores, so waiting for them does not wait for the stores
-            if (!done && q.fill + 32 - q.bp <= 4 * RING_DW) {
+            // (only when no synchronous top-up moved the fill point since the bytes were staged)
+            if (!done && q.sbase == q.fill && q.fill + 32 - q.bp <= 4 * RING_DW) {
                 ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3);
                 ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7);
                 q.fill += 32;
@@ -664,10 +667,13 @@ __global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ b
         step_refill(L, Ls.ring, lane);
         const bool finding = ph == PH_FIND;
         bool pend = act;
-        if (act && finding) {
-            const bool found = find_next(C0, C1, C2, C3, x, r);
-            pend = found;
-            parked = !found;
+        {   // branch-free: every lane runs the search, only finding lanes take its result
+            uint32_t fx = x, fr = r;
+            const bool found = find_next(C0, C1, C2, C3, fx, fr);
+            const bool use = act && finding;
+            x = use ? fx : x; r = use ? fr : r;
+            pend = use ? found : act;
+            parked = parked || (use && !found);
         }
         const uint32_t xc = x & 63;
         const bool is_cl = t == 2, is_mr = t == 1, is_sp = t == 0;
@@ -696,37 +702,40 @@ __global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ b
         // plane bit: new significance, or a refinement bit of 1
         const uint64_t pb = bx | ((pend && is_mr && d) ? (1ull << xc) : 0ull);
         B0 |= rsel(r, 0, pb); B1 |= rsel(r, 1, pb); B2 |= rsel(r, 2, pb); B3 |= rsel(r, 3, pb);
-        if (is_sp) {   // later positions gaining a significant neighbour join the candidates
-            const uint64_t bn = bx << 1;
+        {   // SP: later positions gaining a significant neighbour join the candidates
+            const uint64_t bn = is_sp ? bx << 1 : 0ull;
             const uint64_t b0 = rsel(r, 0, bn), b1 = rsel(r, 1, bn), b2 = rsel(r, 2, bn), b3 = rsel(r, 3, bn);
             const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
                            v3 = nr > 3 ? colmask : 0;
+            const uint64_t sp = is_sp ? ~0ull : 0ull;
             C0 |= (b0 | b1) & ~S1 & v0;
-            C1 |= (m0 | b0 | b1 | b2) & ~S2 & v1;
-            C2 |= (m1 | b1 | b2 | b3) & ~S3 & v2;
-            C3 |= (m2 | b2 | b3) & ~S4 & v3;
+            C1 |= ((m0 & sp) | b0 | b1 | b2) & ~S2 & v1;
+            C2 |= ((m1 & sp) | b1 | b2 | b3) & ~S3 & v2;
+            C3 |= ((m2 & sp) | b2 | b3) & ~S4 & v3;
         }
         // position / phase advance (SP and CL share the CL machine without run-length)
-        uint32_t nph = ph, nr2 = r;
-        bool col_done = false;
-        if (is_mr) { nr2 = r + 1; }
-        else if (agg) { nph = d ? PH_UNI1 : PH_FIND; col_done = !d; }
-        else if (finding) { nph = d ? PH_SIGN : PH_FIND; nr2 = d ? r : r + 1; }
-        else if (ph == PH_UNI1) { rlhi = d; nph = PH_UNI2; }
-        else if (ph == PH_UNI2) { nr2 = (rlhi << 1) | d; nph = PH_SIGN; }
-        else { nph = PH_FIND; nr2 = r + 1; }
-        if (pend) {
-            ph = nph;
-            r = col_done ? 0 : nr2;
-            x += (col_done || r == 4) ? 1 : 0;
-            r &= 3;
-        }
+        // (selects, no branches: MR always advances; CL/SP run the phase machine)
+        const bool uni1 = ph == PH_UNI1, uni2 = ph == PH_UNI2, sgn = ph == PH_SIGN;
+        const bool col_done = !is_mr && agg && !d;
+        uint32_t nph = is_mr ? ph
+                             : (agg ? (d ? PH_UNI1 : PH_FIND)
+                                    : (finding ? (d ? PH_SIGN : PH_FIND) : (uni1 ? PH_UNI2 : (uni2 ? PH_SIGN : PH_FIND))));
+        uint32_t nr2 = is_mr ? r + 1
+                             : (agg ? r : (finding ? (d ? r : r + 1) : (uni1 ? r : (uni2 ? ((rlhi << 1) | d) : r + 1))));
+        (void)sgn;
+        rlhi = (pend && !is_mr && uni1) ? d : rlhi;
+        nph = pend ? nph : ph;
+        nr2 = pend ? (col_done ? 0u : nr2) : r;
+        x += (pend && (col_done || nr2 == 4)) ? 1 : 0;
+        ph = nph;
+        r = nr2 & 3;
         step_prefetch(L, Ls.ring, lane);
     }
     if (stats) {
         unsigned long long tot = L.nsym;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        if (lane == 0) atomicAdd(&stats[3], (unsigned long long)nevents);
         if (lane == 0) { atomicAdd(&stats[0], (unsigned long long)L.step); atomicAdd(&stats[1], tot);
                          atomicMax(&stats[2], (unsigned long long)L.step); }
     }
@@ -798,11 +807,12 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         hipLaunchKernelGGL(k_t1_dec_ind, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
     if (want) {
-        unsigned long long h[3];
-        (void)hipMemcpyAsync(h, stats, 24, hipMemcpyDeviceToHost, st);
+        unsigned long long h[4];
+        (void)hipMemcpyAsync(h, stats, 32, hipMemcpyDeviceToHost, st);
         (void)hipStreamSynchronize(st);
-        fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f\n",
-                (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]));
+        fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f events/wave %.0f\n",
+                (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]),
+                (double)h[3] / ((nblocks + 63) / 64));
     }
 }
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* pos, const uint64_t* scratch,
