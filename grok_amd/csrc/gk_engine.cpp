@@ -18,6 +18,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -437,6 +438,29 @@ struct ByteSrc {
     std::unordered_map<size_t, std::vector<uint8_t>> pages;
     size_t last_pg = ~(size_t)0;             // fast path: the page of the previous access
     const uint8_t* last = nullptr;
+    // host copies of scattered ranges fetched in one batch (tile-part and packet headers),
+    // sorted by start; a read outside them falls back to a page fetch
+    struct Region { size_t start, len; const uint8_t* p; };
+    std::vector<Region> regs;
+    size_t last_reg = ~(size_t)0;
+    void add_regions(const std::vector<Region>& rs) {
+        regs.insert(regs.end(), rs.begin(), rs.end());
+        std::sort(regs.begin(), regs.end(), [](const Region& a, const Region& b) { return a.start < b.start; });
+        last_reg = ~(size_t)0;
+    }
+    inline bool from_region(size_t i, uint8_t& v) {
+        if (last_reg < regs.size() && i - regs[last_reg].start < regs[last_reg].len) {
+            v = regs[last_reg].p[i - regs[last_reg].start];
+            return true;
+        }
+        size_t lo = 0, hi = regs.size();
+        while (lo < hi) { size_t m = (lo + hi) / 2; if (regs[m].start <= i) lo = m + 1; else hi = m; }
+        for (size_t k = lo; k > 0 && k + 2 > lo; --k) {   // the last two regions starting at or before i
+            const Region& R = regs[k - 1];
+            if (i - R.start < R.len) { last_reg = k - 1; v = R.p[i - R.start]; return true; }
+        }
+        return false;
+    }
     const uint8_t* page(size_t pg) {
         auto it = pages.find(pg);
         if (it == pages.end()) {
@@ -452,7 +476,10 @@ struct ByteSrc {
         if (i >= len) return 0;
         if (host) return host[i];
         const size_t pg = i / PG;
-        if (pg != last_pg) { last = page(pg); last_pg = pg; }
+        if (pg == last_pg) return last[i - pg * PG];
+        uint8_t v;
+        if (!regs.empty() && from_region(i, v)) return v;
+        last = page(pg); last_pg = pg;
         return last[i - pg * PG];
     }
     uint32_t be16(size_t i) { return ((uint32_t)at(i) << 8) | at(i + 1); }
@@ -545,6 +572,12 @@ struct T2Enc {
     // (block, first byte, length) body segments.  Returns false when the budget is exceeded.
     bool write_packet(const ResG& R, uint32_t pi, uint32_t l, uint64_t* budget,
                       std::vector<uint32_t>* seg) {
+        return write_packet(R, pi, l, budget, seg, hdr);
+    }
+    // hdr_out: the packet header bytes (a per-thread buffer when tiles are written in parallel;
+    // all other state touched is per code-block / per precinct, i.e. disjoint across tiles)
+    bool write_packet(const ResG& R, uint32_t pi, uint32_t l, uint64_t* budget,
+                      std::vector<uint32_t>* seg, std::vector<uint8_t>& hdr) {
         if (l == 0) {
             for (size_t bi = 0; bi < R.bands.size(); ++bi) {
                 const PrecG& PG = R.prc[bi][pi];
@@ -813,6 +846,8 @@ struct gk_ctx {
     DevBuf dsym, dsymoff, dpassend, dcminfo;
     DevBuf dscratch, dnmse, dord;
     HostBuf hinfo, hseg, hhdr, hpasses, hord;
+    DevBuf dstage1, dstage2;   // decode: batched tile-part / packet header fetches (device input)
+    HostBuf hstage1, hstage2;
     int16_t* nmse_tab = nullptr;   // device copy of the nmsedec tables (4 x 128)
     hipEvent_t ev[32];
     bool blocks_uploaded = false;
@@ -1053,38 +1088,45 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         pos += n;
     };
     add_host(H.data(), H.size());
-    std::vector<uint32_t> body, bsegs;   // bsegs: (block, first byte, length) of every packet body, tile order
-    std::vector<uint8_t> phdr;           // packet headers of the current tile
+    // per tile: packets (T2Compress::compressPackets) and the tile-part header; tiles are
+    // independent, so they are built in parallel host threads and appended in tile order
     struct Pk { uint32_t hoff, hlen, s0, s1, len; };
-    std::vector<Pk> pk;
-    std::vector<uint8_t> tp;             // SOT [PLT] SOD bytes of the current tile
-    for (uint32_t t = tb; t < te; ++t) {
+    struct TileOut {
+        std::vector<uint8_t> tp;     // SOT [PLT] SOD
+        std::vector<uint8_t> phdr;   // packet headers
+        std::vector<Pk> pk;
+        std::vector<uint32_t> bsegs; // (block, first byte, length) of every packet body
+        uint64_t psot = 0;
+    };
+    std::vector<TileOut> tout(te - tb);
+    auto build_tile_part = [&](uint32_t t, TileOut& O) {
         const TileG& T = P.tiles[t];
-        pk.clear(); phdr.clear(); bsegs.clear();
+        std::vector<uint32_t> body;
+        std::vector<uint8_t> hb;
         for (uint32_t l = 0; l < P.p.nlayers; ++l)
             for (uint32_t r = 0; r < P.p.numres; ++r)
                 for (uint32_t c = 0; c < P.nc; ++c) {
                     const ResG& R = T.comps[c].res[r];
                     for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
                         body.clear();
-                        T2.write_packet(R, pi, l, nullptr, &body);
-                        Pk k{(uint32_t)phdr.size(), (uint32_t)T2.hdr.size(), (uint32_t)bsegs.size(), 0, (uint32_t)T2.hdr.size()};
-                        phdr.insert(phdr.end(), T2.hdr.begin(), T2.hdr.end());
+                        T2.write_packet(R, pi, l, nullptr, &body, hb);
+                        Pk k{(uint32_t)O.phdr.size(), (uint32_t)hb.size(), (uint32_t)O.bsegs.size(), 0, (uint32_t)hb.size()};
+                        O.phdr.insert(O.phdr.end(), hb.begin(), hb.end());
                         for (size_t q = 0; q < body.size(); q += 3) {
                             if (!body[q + 2]) continue;
-                            bsegs.push_back(body[q]); bsegs.push_back(body[q + 1]); bsegs.push_back(body[q + 2]);
+                            O.bsegs.push_back(body[q]); O.bsegs.push_back(body[q + 1]); O.bsegs.push_back(body[q + 2]);
                             k.len += body[q + 2];
                         }
-                        k.s1 = (uint32_t)bsegs.size();
-                        pk.push_back(k);
+                        k.s1 = (uint32_t)O.bsegs.size();
+                        O.pk.push_back(k);
                     }
                 }
         // tile part: SOT [PLT] SOD (CodeStreamCompress::writeTilePart :862-900)
-        tp.clear();
+        std::vector<uint8_t>& tp = O.tp;
         put16(tp, 0xff90); put16(tp, 10); put16(tp, t); put32(tp, 0); tp.push_back(0); tp.push_back(1);
         if (P.p.plt) {   // PacketLengthMarkers::write (PacketLengthMarkers.cpp:107-175): Zplt 0, 7-bit groups MSB first
             std::vector<uint8_t> v;
-            for (const Pk& k : pk) {
+            for (const Pk& k : O.pk) {
                 const int nbits = floorlog2(k.len) + 1, nbytes = (nbits + 6) / 7;
                 for (int q = nbytes - 1; q >= 0; --q) v.push_back((uint8_t)(((k.len >> (7 * q)) & 0x7F) | (q ? 0x80 : 0)));
             }
@@ -1094,20 +1136,43 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         }
         put16(tp, 0xff93);
         uint64_t psot = tp.size();
-        for (const Pk& k : pk) psot += k.len;
+        for (const Pk& k : O.pk) psot += k.len;
         if (psot > 0xffffffffull) throw GkError("tile part exceeds 4 GiB");
         tp[6] = (uint8_t)(psot >> 24); tp[7] = (uint8_t)(psot >> 16); tp[8] = (uint8_t)(psot >> 8); tp[9] = (uint8_t)psot;
+        O.psot = psot;
+    };
+    {
+        const uint32_t ntl = te - tb;
+        const unsigned nthr = (unsigned)std::min<uint32_t>(ntl, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+        if (nthr <= 1 || do_rc) {
+            for (uint32_t t = tb; t < te; ++t) build_tile_part(t, tout[t - tb]);
+        } else {
+            std::vector<std::thread> th;
+            std::vector<std::string> errs(nthr);
+            for (unsigned w = 0; w < nthr; ++w)
+                th.emplace_back([&, w]() {
+                    try {
+                        for (uint32_t q = w; q < ntl; q += nthr) build_tile_part(tb + q, tout[q]);
+                    } catch (const GkError& e) { errs[w] = e.msg; }
+                });
+            for (auto& x : th) x.join();
+            for (auto& e : errs) if (!e.empty()) throw GkError(e);
+        }
+    }
+    for (uint32_t t = tb; t < te; ++t) {
+        TileOut& O = tout[t - tb];
+        const uint64_t psot = O.psot;
         if (part_lens) part_lens[t - tb] = (uint32_t)psot;
         if (P.p.tlm && with_header) {
             uint8_t* e = hdrs.data() + tlm_pos + 6 * (size_t)t;   // the main header is hdrs[0 .. H.size())
             e[0] = (uint8_t)(t >> 8); e[1] = (uint8_t)t;
             e[2] = (uint8_t)(psot >> 24); e[3] = (uint8_t)(psot >> 16); e[4] = (uint8_t)(psot >> 8); e[5] = (uint8_t)psot;
         }
-        add_host(tp.data(), tp.size());
-        for (const Pk& k : pk) {
-            add_host(phdr.data() + k.hoff, k.hlen);
+        add_host(O.tp.data(), O.tp.size());
+        for (const Pk& k : O.pk) {
+            add_host(O.phdr.data() + k.hoff, k.hlen);
             for (uint32_t q = k.s0; q < k.s1; q += 3) {
-                const uint32_t b = bsegs[q], off = bsegs[q + 1], n = bsegs[q + 2];
+                const uint32_t b = O.bsegs[q], off = O.bsegs[q + 1], n = O.bsegs[q + 2];
                 const GkBlock& G = P.blocks[b];
                 if (ht) {   // MagSgn head at the slot start, MEL+VLC tail at the slot end
                     const uint32_t ms = hinfo[4 * (size_t)b + 3], tl = n - ms;
@@ -1163,12 +1228,16 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
 // ---------------------------------------------------------------------------
 // Decode
 // ---------------------------------------------------------------------------
-struct TilePart { uint32_t tile; size_t data, end; };   // packet bytes [data, end) of one tile part
+struct TilePart {                  // packet bytes [data, end) of one tile part
+    uint32_t tile; size_t sot, data, end;
+    std::vector<uint32_t> plt;      // packet lengths from PLT markers (empty without PLT)
+};
 struct Header {
     Plan want;
     std::vector<std::pair<uint32_t, uint32_t>> qcd;
     size_t first_sot = 0;
     std::vector<TilePart> parts;
+    std::vector<std::pair<uint32_t, uint32_t>> tlm;   // (tile, tile-part length) from TLM markers
 };
 
 static void parse_header(ByteSrc& S, Header& Hd) {
@@ -1222,6 +1291,18 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             if (qt == 0) for (uint32_t k = 1; k < L - 2; ++k) Hd.qcd.push_back({(uint32_t)S.at(s + k) >> 3, 0u});
             else if (qt == 2) for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = S.be16(s + k); Hd.qcd.push_back({v >> 11, v & 0x7ff}); }
             else throw GkError("scalar-derived quantisation not supported");
+        } else if (m == 0xff55) {   // TLM (TileLengthMarkers::read, cache/LengthCache.cpp)
+            const uint32_t stlm = S.at(s + 1), st = (stlm >> 4) & 3, sp = (stlm >> 6) & 1;
+            const uint32_t esz = st + (sp ? 4 : 2);
+            size_t e = s + 2;
+            uint32_t tnext = Hd.tlm.empty() ? 0 : Hd.tlm.back().first + 1;
+            while (e + esz <= s + L - 2) {
+                uint32_t t = st == 0 ? tnext : (st == 1 ? S.at(e) : S.be16(e));
+                uint32_t len = sp ? S.be32(e + st) : S.be16(e + st);
+                Hd.tlm.push_back({t, len});
+                tnext = t + 1;
+                e += esz;
+            }
         } else if (m == 0xff5d || m == 0xff53 || m == 0xff5e || m == 0xff5f) {
             throw GkError("QCC/COC/RGN/POC markers not supported on this path yet");
         }
@@ -1231,20 +1312,109 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     // tile parts: SOT (Isot, Psot, TPsot, TNsot), tile-part header markers (PLT, ...), SOD, packets
     // (CodeStreamDecompress SOT/SOD handlers; TLM and PLT are only needed for random access)
     size_t pos = Hd.first_sot;
-    while (pos + 12 <= S.len && S.be16(pos) == 0xff90) {
-        const uint32_t isot = S.be16(pos + 4), psot = S.be32(pos + 6);
-        const size_t end = psot ? pos + psot : (S.len >= 2 ? S.len - 2 : S.len);
-        if (end > S.len || end < pos + 14) throw GkError("corrupt SOT (Psot)");
-        size_t j = pos + 12;
-        while (j + 4 <= end && S.be16(j) != 0xff93) j += 2 + S.be16(j + 2);
-        if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
-        if (S.at(pos + 10) != 0) throw GkError("multiple tile parts per tile not supported");
-        Hd.parts.push_back({isot, j + 2, end});
-        pos = end;
+    if (!Hd.tlm.empty() && S.dev) {
+        // device-resident stream with TLM: tile-part positions without walking the SOT chain;
+        // the tile-part headers are fetched in one batch by the decoder (data = 0 until then)
+        for (auto& tl : Hd.tlm) {
+            const size_t end = pos + tl.second;
+            if (tl.second < 14 || end > S.len) throw GkError("corrupt TLM");
+            Hd.parts.push_back({tl.first, pos, 0, end, {}});
+            pos = end;
+        }
+    } else {
+        while (pos + 12 <= S.len && S.be16(pos) == 0xff90) {
+            const uint32_t isot = S.be16(pos + 4), psot = S.be32(pos + 6);
+            const size_t end = psot ? pos + psot : (S.len >= 2 ? S.len - 2 : S.len);
+            if (end > S.len || end < pos + 14) throw GkError("corrupt SOT (Psot)");
+            size_t j = pos + 12;
+            while (j + 4 <= end && S.be16(j) != 0xff93) j += 2 + S.be16(j + 2);
+            if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
+            if (S.at(pos + 10) != 0) throw GkError("multiple tile parts per tile not supported");
+            Hd.parts.push_back({isot, pos, j + 2, end, {}});
+            pos = end;
+        }
     }
     if (Hd.parts.empty()) throw GkError("no tile parts");
     if ((1u << W.p.cbw) > 64 || (1u << W.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
     if (W.p.ht() && W.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
+}
+
+// Device-resident codestream: copy scattered ranges (tile-part headers, packet headers) to
+// the host with one gather launch and one D2H copy, and register them with the byte source.
+static void fetch_ranges(gk_ctx* ctx, ByteSrc& S, const std::vector<std::pair<size_t, size_t>>& rg, HostBuf& hb,
+                         DevBuf& db) {
+    if (rg.empty()) return;
+    size_t tot = 0;
+    for (auto& r : rg) tot += r.second;
+    uint8_t* dst = (uint8_t*)db.get(tot + 64);
+    uint64_t* hs = (uint64_t*)ctx->hseg.get(rg.size() * 24 + 8);
+    size_t o = 0;
+    for (size_t i = 0; i < rg.size(); ++i) { hs[3 * i] = rg[i].first; hs[3 * i + 1] = o; hs[3 * i + 2] = rg[i].second; o += rg[i].second; }
+    uint64_t* ds = (uint64_t*)ctx->dseg.get(rg.size() * 24 + 8);
+    HIPCHK(hipMemcpyAsync(ds, hs, rg.size() * 24, hipMemcpyHostToDevice, ctx->st));
+    gk_launch_gather(ctx->st, S.dev, dst, ds, (uint32_t)rg.size());
+    uint8_t* h = (uint8_t*)hb.get(tot + 64);
+    HIPCHK(hipMemcpyAsync(h, dst, tot, hipMemcpyDeviceToHost, ctx->st));
+    HIPCHK(hipStreamSynchronize(ctx->st));
+    std::vector<ByteSrc::Region> regs;
+    o = 0;
+    for (auto& r : rg) { regs.push_back({r.first, r.second, h + o}); o += r.second; }
+    S.add_regions(regs);
+}
+
+// Tile-part headers of parts located through TLM: SOD position and PLT packet lengths
+// (PacketLengthMarkers::readPLT: Zplt, then 7-bit groups MSB first, bit 7 = continuation).
+static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
+    std::vector<std::pair<size_t, size_t>> rg;
+    for (auto& TP : Hd.parts)
+        if (!TP.data) rg.push_back({TP.sot, std::min<size_t>(TP.end - TP.sot, 4096)});
+    fetch_ranges(ctx, S, rg, ctx->hstage1, ctx->dstage1);
+    for (auto& TP : Hd.parts) {
+        if (TP.data) continue;
+        if (S.be16(TP.sot) != 0xff90 || S.be16(TP.sot + 4) != TP.tile || S.be32(TP.sot + 6) != TP.end - TP.sot)
+            throw GkError("TLM does not match the SOT markers");
+        if (S.at(TP.sot + 10) != 0) throw GkError("multiple tile parts per tile not supported");
+        size_t j = TP.sot + 12;
+        while (j + 4 <= TP.end && S.be16(j) != 0xff93) {
+            const uint32_t m = S.be16(j), L = S.be16(j + 2);
+            if (m == 0xff58) {
+                uint32_t v = 0;
+                for (size_t q = j + 5; q < j + 2 + L; ++q) {
+                    const uint32_t b = S.at(q);
+                    v = (v << 7) | (b & 0x7f);
+                    if (!(b & 0x80)) { TP.plt.push_back(v); v = 0; }
+                }
+            }
+            j += 2 + L;
+        }
+        if (j + 2 > TP.end || S.be16(j) != 0xff93) throw GkError("missing SOD");
+        TP.data = j + 2;
+    }
+}
+
+// With PLT, every packet's start is known: fetch the first bytes of each packet (its header;
+// bound from the packet's code-block count) in one batch before T2 parses them.
+static void prefetch_packet_headers(gk_ctx* ctx, ByteSrc& S, const Plan& P, const Header& Hd) {
+    std::vector<std::pair<size_t, size_t>> rg;
+    for (const auto& TP : Hd.parts) {
+        if (TP.plt.empty() || TP.tile >= P.tiles.size()) continue;
+        const TileG& T = P.tiles[TP.tile];
+        size_t pos = TP.data, k = 0;
+        for (uint32_t l = 0; l < P.p.nlayers; ++l)
+            for (uint32_t r = 0; r < P.p.numres; ++r)
+                for (uint32_t c = 0; c < P.nc; ++c) {
+                    const ResG& R = T.comps[c].res[r];
+                    for (uint32_t pi = 0; pi < R.pw * R.ph && k < TP.plt.size(); ++pi, ++k) {
+                        size_t nblk = 0;
+                        for (uint32_t bi = 0; bi < R.bands.size(); ++bi) nblk += (size_t)R.prc[bi][pi].cw * R.prc[bi][pi].ch;
+                        const size_t len = TP.plt[k];
+                        if (pos + len > TP.end) return;   // inconsistent PLT: fall back to page fetches
+                        rg.push_back({pos, std::min(len, 64 + 16 * nblk)});
+                        pos += len;
+                    }
+                }
+    }
+    fetch_ranges(ctx, S, rg, ctx->hstage2, ctx->dstage2);
 }
 
 static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
@@ -1260,6 +1430,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     ensure_plan(ctx, Hd.want);
     Plan& P = ctx->plan;
     apply_qcd(P, Hd.qcd);
+    if (S.dev) {
+        read_tile_part_headers(ctx, S, Hd);
+        prefetch_packet_headers(ctx, S, P, Hd);
+    }
     const uint32_t nb = (uint32_t)P.blocks.size();
     std::vector<GkBlock> blk = P.blocks;
     std::vector<std::vector<std::pair<uint64_t, uint32_t>>> chunks(nb);
@@ -1280,14 +1454,17 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         }
                     }
             }
-    // ---- T2 (T2Decompress.cpp:216-570), LRCP, per tile part
-    struct Trees { DecTree incl, imsb; };
-    std::vector<Trees> trees;
-    std::unordered_map<uint32_t, size_t> tidx;   // trees by first_block of each precinct-band
+    // ---- T2 (T2Decompress.cpp:216-570), LRCP, per tile part.  Tile parts are independent
+    // (own precincts, tag trees and code-blocks), so they are parsed in parallel host threads.
     std::vector<uint8_t> seen(P.tiles.size(), 0);
     for (const TilePart& TPt : Hd.parts) {
         if (TPt.tile >= P.tiles.size()) throw GkError("corrupt SOT (tile index)");
         if (seen[TPt.tile]++) throw GkError("multiple tile parts per tile not supported");
+    }
+    auto t2_part = [&](const TilePart& TPt, ByteSrc& BS) {
+        struct Trees { DecTree incl, imsb; };
+        std::vector<Trees> trees;
+        std::unordered_map<uint32_t, size_t> tidx;   // trees by first_block of each precinct-band
         const TileG& TG = P.tiles[TPt.tile];
         const size_t tile_end = TPt.end;
         size_t pos = TPt.data;
@@ -1296,8 +1473,8 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 for (uint32_t c = 0; c < P.nc; ++c) {
                     const ResG& R = TG.comps[c].res[r];
                     for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                        if (pos >= tile_end) goto tile_done;
-                        BitReader br(S, pos, tile_end);
+                        if (pos >= tile_end) return;
+                        BitReader br(BS, pos, tile_end);
                         std::vector<std::pair<uint32_t, uint32_t>> contrib;
                         if (br.read(1)) {
                             for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
@@ -1345,7 +1522,25 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         }
                     }
                 }
-    tile_done:;
+    };
+    {
+        const size_t np = Hd.parts.size();
+        const unsigned nthr = (unsigned)std::min<size_t>(np, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+        if (nthr <= 1) {
+            for (const TilePart& TPt : Hd.parts) t2_part(TPt, S);
+        } else {
+            std::vector<std::thread> th;
+            std::vector<std::string> errs(nthr);
+            for (unsigned w = 0; w < nthr; ++w)
+                th.emplace_back([&, w]() {
+                    ByteSrc BS = S;   // per-thread cursor caches (regions shared read-only)
+                    try {
+                        for (size_t q = w; q < np; q += nthr) t2_part(Hd.parts[q], BS);
+                    } catch (const GkError& e) { errs[w] = e.msg; }
+                });
+            for (auto& t : th) t.join();
+            for (auto& e : errs) if (!e.empty()) throw GkError(e);
+        }
     }
     // decode only the tile rows whose tiles are present (sharded / windowed decode)
     uint32_t jb = P.nty, je = 0;

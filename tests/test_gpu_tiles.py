@@ -69,6 +69,12 @@ def test_tiled_random_vs_oracle(eng, seed):
     cs = eng.encode(img, bits, params=_params(**gkw))
     assert cs == ref, (w, h, tw, th, numres, ht)
     np.testing.assert_array_equal(eng.decode(cs), img)
+    # device-resident codestream: TLM-located tile parts, PLT-batched packet headers
+    import torch
+    d = torch.frombuffer(bytearray(cs), dtype=torch.uint8).cuda()
+    y = torch.empty((c, h, w), dtype=torch.int32, device="cuda")
+    eng.decode(d, length=len(cs), out=y)
+    np.testing.assert_array_equal(y.cpu().numpy(), img)
 
 
 def test_tiled_97(eng):
