@@ -18,6 +18,10 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -38,6 +42,74 @@ struct GkError {
     std::string msg;
     explicit GkError(std::string m) : msg(std::move(m)) {}
 };
+
+// Persistent host worker pool for the T2 stages (tiles, precinct chains, blocks).
+// run(n, f) calls f(0..n-1) across the workers and the caller, and returns when all
+// calls finished; the first GkError thrown by any call is rethrown.
+class HostPool {
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t)>* job_ = nullptr;
+    std::atomic<size_t> next_{0};
+    size_t n_ = 0;
+    int busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+    std::string err_;
+    void drain(const std::function<void(size_t)>& f, size_t n) {
+        for (;;) {
+            const size_t i = next_.fetch_add(1);
+            if (i >= n) break;
+            try { f(i); } catch (const GkError& e) {
+                std::lock_guard<std::mutex> lk(m_);
+                if (err_.empty()) err_ = e.msg;
+            }
+        }
+    }
+    void worker() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(size_t)>* f;
+            size_t n;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_; f = job_; n = n_;
+            }
+            drain(*f, n);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--busy_ == 0) done_.notify_all();
+        }
+    }
+
+public:
+    explicit HostPool(unsigned k) { for (unsigned i = 0; i < k; ++i) th_.emplace_back([this] { worker(); }); }
+    ~HostPool() {
+        { std::lock_guard<std::mutex> lk(m_); stop_ = true; }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    unsigned size() const { return (unsigned)th_.size() + 1; }
+    void run(size_t n, const std::function<void(size_t)>& f) {
+        if (n == 0) return;
+        if (n == 1 || th_.empty()) { for (size_t i = 0; i < n; ++i) f(i); return; }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &f; n_ = n; next_ = 0; busy_ = (int)th_.size(); ++gen_; err_.clear();
+        }
+        cv_.notify_all();
+        drain(f, n);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return busy_ == 0; });
+        if (!err_.empty()) throw GkError(err_);
+    }
+};
+static HostPool& host_pool() {   // one pool per process, sized to the CPU share (at most 16 threads)
+    static HostPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+    return pool;
+}
 
 // ---------------------------------------------------------------------------
 // Tile geometry (ISO 15444-1 Annex B; Grok Resolution.h:37-72,
@@ -441,14 +513,22 @@ struct ByteSrc {
     // host copies of scattered ranges fetched in one batch (tile-part and packet headers),
     // sorted by start; a read outside them falls back to a page fetch
     struct Region { size_t start, len; const uint8_t* p; };
-    std::vector<Region> regs;
+    std::shared_ptr<std::vector<Region>> regp = std::make_shared<std::vector<Region>>();
     size_t last_reg = ~(size_t)0;
     void add_regions(const std::vector<Region>& rs) {
+        auto& regs = *regp;
         regs.insert(regs.end(), rs.begin(), rs.end());
         std::sort(regs.begin(), regs.end(), [](const Region& a, const Region& b) { return a.start < b.start; });
         last_reg = ~(size_t)0;
     }
+    // a reader for another thread: shares the (read-only) regions, has its own page cache
+    ByteSrc fork() const {
+        ByteSrc b;
+        b.host = host; b.dev = dev; b.len = len; b.st = st; b.regp = regp;
+        return b;
+    }
     inline bool from_region(size_t i, uint8_t& v) {
+        const auto& regs = *regp;
         if (last_reg < regs.size() && i - regs[last_reg].start < regs[last_reg].len) {
             v = regs[last_reg].p[i - regs[last_reg].start];
             return true;
@@ -478,7 +558,7 @@ struct ByteSrc {
         const size_t pg = i / PG;
         if (pg == last_pg) return last[i - pg * PG];
         uint8_t v;
-        if (!regs.empty() && from_region(i, v)) return v;
+        if (!regp->empty() && from_region(i, v)) return v;
         last = page(pg); last_pg = pg;
         return last[i - pg * PG];
     }
@@ -577,7 +657,7 @@ struct T2Enc {
     // hdr_out: the packet header bytes (a per-thread buffer when tiles are written in parallel;
     // all other state touched is per code-block / per precinct, i.e. disjoint across tiles)
     bool write_packet(const ResG& R, uint32_t pi, uint32_t l, uint64_t* budget,
-                      std::vector<uint32_t>* seg, std::vector<uint8_t>& hdr) {
+                      std::vector<uint32_t>* seg, std::vector<uint8_t>& hdr, uint64_t* body_bytes = nullptr) {
         if (l == 0) {
             for (size_t bi = 0; bi < R.bands.size(); ++bi) {
                 const PrecG& PG = R.prc[bi][pi];
@@ -638,6 +718,7 @@ struct T2Enc {
                     *budget -= (r1 - r0);
                 }
                 if (seg) { seg->push_back(b); seg->push_back(r0); seg->push_back(r1 - r0); }
+                if (body_bytes) *body_bytes += r1 - r0;
                 inprev[b] = (uint16_t)(inprev[b] + np);
             }
         }
@@ -657,10 +738,72 @@ struct T2Enc {
         return true;
     }
 
-    // makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0)
+    // ---- fast simulation for the bisection of layer l (single tile).  Layers < l are final,
+    // so the T2 state after them is snapshotted once; every bisection step restores each
+    // precinct chain (its tag trees and code-blocks) and codes only layer l, chains in
+    // parallel.  compressPacketsSimulate's bounded writes fail iff, with S the running size
+    // over packets in LRCP order, some packet header reaches the remaining budget or some
+    // body exceeds it; sizes only grow, so that is decided by the last packet:
+    //   pass <=> S_(n-1) + hdr_n < budget  and  S_n <= budget.
+    struct Chain { uint32_t c, r, pi; };
+    std::vector<Chain> chains;              // one layer's packets in LRCP order
+    std::vector<TagTree> incl0, imsb0;      // snapshot after the final layers < l
+    std::vector<uint16_t> inprev0;
+    std::vector<uint8_t> nlb0;
+    uint64_t prior = 0;                     // bytes of the final layers < l
+    std::vector<uint64_t> csize, chdr;
+    void init_chains() {
+        chains.clear();
+        const TileG& T = P.tiles[0];
+        for (uint32_t r = 0; r < P.p.numres; ++r)
+            for (uint32_t c = 0; c < P.nc; ++c)
+                for (uint32_t pi = 0; pi < T.comps[c].res[r].pw * T.comps[c].res[r].ph; ++pi) chains.push_back({c, r, pi});
+        csize.assign(chains.size(), 0); chdr.assign(chains.size(), 0);
+        prior = 0;
+    }
+    void restore_chain(const Chain& ch) {
+        const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
+        for (size_t bi = 0; bi < R.bands.size(); ++bi) {
+            const PrecG& PG = R.prc[bi][ch.pi];
+            if (!PG.cw || !PG.ch) continue;
+            incl[PG.tree] = incl0[PG.tree]; imsb[PG.tree] = imsb0[PG.tree];
+            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                const uint32_t b = PG.first_block + k;
+                inprev[b] = inprev0[b]; nlb[b] = nlb0[b];
+            }
+        }
+    }
+    void code_layer(uint32_t l) {   // every chain of layer l from the snapshot, in parallel
+        host_pool().run(chains.size(), [&](size_t i) {
+            const Chain& ch = chains[i];
+            if (l) restore_chain(ch);
+            std::vector<uint8_t> hb;
+            uint64_t body = 0;
+            write_packet(P.tiles[0].comps[ch.c].res[ch.r], ch.pi, l, nullptr, nullptr, hb, &body);
+            chdr[i] = hb.size(); csize[i] = hb.size() + body;
+        });
+    }
+    bool simulate_layer(uint32_t l, uint64_t max_bytes) {
+        if (max_bytes == 0xffffffffull) return true;
+        code_layer(l);
+        uint64_t tot = prior;
+        for (uint64_t v : csize) tot += v;
+        const uint64_t last = csize.back(), lasth = chdr.back();
+        return tot - last + lasth < max_bytes && tot <= max_bytes;
+    }
+    void finish_layer(uint32_t l) {   // layer l is final: advance the snapshot past it
+        code_layer(l);
+        for (uint64_t v : csize) prior += v;
+        incl0 = incl; imsb0 = imsb; inprev0 = inprev; nlb0 = nlb;
+    }
+
+    // makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0), blocks in parallel
     void make_layer(uint32_t l, double thresh, bool final_attempt, std::vector<uint16_t>& prev) {
         const uint32_t nb = (uint32_t)P.blocks.size();
-        for (uint32_t b = 0; b < nb; ++b) {
+        const uint32_t chunk = 4096;
+        host_pool().run((nb + chunk - 1) / chunk, [&](size_t ci) {
+        const uint32_t bend = std::min<uint32_t>(nb, (uint32_t)(ci + 1) * chunk);
+        for (uint32_t b = (uint32_t)ci * chunk; b < bend; ++b) {
             if (l == 0) prev[b] = 0;
             const uint32_t np = npasses(b);
             uint32_t inc;
@@ -680,6 +823,7 @@ struct T2Enc {
             lnp[(size_t)b * L + l] = (uint16_t)(inc - prev[b]);
             if (final_attempt) prev[b] = (uint16_t)inc;
         }
+        });
     }
 
     void allocate(size_t header_size) {
@@ -713,6 +857,8 @@ struct T2Enc {
                 if (sl > max_slope) max_slope = sl;
             }
         double upper = max_slope;
+        const bool fast = P.tiles.size() == 1 && !getenv("GK_T2_SERIAL_SIM");
+        if (fast) init_chains();
         for (uint32_t l = 0; l < L; ++l) {
             uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
             if (rates[l] > 0.0) {
@@ -722,7 +868,7 @@ struct T2Enc {
                     make_layer(l, thresh, false, prev);
                     if (prevthresh != -1 && fabs(prevthresh - thresh) < 0.001) break;
                     prevthresh = thresh;
-                    if (!simulate(l + 1, max_len)) { lower = thresh; continue; }
+                    if (!(fast ? simulate_layer(l, max_len) : simulate(l + 1, max_len))) { lower = thresh; continue; }
                     upper = thresh;
                 }
                 make_layer(l, upper == -1 ? thresh : upper, true, prev);
@@ -730,6 +876,7 @@ struct T2Enc {
             } else {
                 make_layer(l, -1.0, true, prev);
             }
+            if (fast && l + 1 < L) finish_layer(l);
         }
     }
 };
@@ -1141,24 +1288,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         tp[6] = (uint8_t)(psot >> 24); tp[7] = (uint8_t)(psot >> 16); tp[8] = (uint8_t)(psot >> 8); tp[9] = (uint8_t)psot;
         O.psot = psot;
     };
-    {
-        const uint32_t ntl = te - tb;
-        const unsigned nthr = (unsigned)std::min<uint32_t>(ntl, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
-        if (nthr <= 1 || do_rc) {
-            for (uint32_t t = tb; t < te; ++t) build_tile_part(t, tout[t - tb]);
-        } else {
-            std::vector<std::thread> th;
-            std::vector<std::string> errs(nthr);
-            for (unsigned w = 0; w < nthr; ++w)
-                th.emplace_back([&, w]() {
-                    try {
-                        for (uint32_t q = w; q < ntl; q += nthr) build_tile_part(tb + q, tout[q]);
-                    } catch (const GkError& e) { errs[w] = e.msg; }
-                });
-            for (auto& x : th) x.join();
-            for (auto& e : errs) if (!e.empty()) throw GkError(e);
-        }
-    }
+    host_pool().run(te - tb, [&](size_t q) { build_tile_part(tb + (uint32_t)q, tout[q]); });
     for (uint32_t t = tb; t < te; ++t) {
         TileOut& O = tout[t - tb];
         const uint64_t psot = O.psot;
@@ -1523,24 +1653,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                     }
                 }
     };
-    {
-        const size_t np = Hd.parts.size();
-        const unsigned nthr = (unsigned)std::min<size_t>(np, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
-        if (nthr <= 1) {
-            for (const TilePart& TPt : Hd.parts) t2_part(TPt, S);
-        } else {
-            std::vector<std::thread> th;
-            std::vector<std::string> errs(nthr);
-            for (unsigned w = 0; w < nthr; ++w)
-                th.emplace_back([&, w]() {
-                    ByteSrc BS = S;   // per-thread cursor caches (regions shared read-only)
-                    try {
-                        for (size_t q = w; q < np; q += nthr) t2_part(Hd.parts[q], BS);
-                    } catch (const GkError& e) { errs[w] = e.msg; }
-                });
-            for (auto& t : th) t.join();
-            for (auto& e : errs) if (!e.empty()) throw GkError(e);
-        }
+    if (Hd.parts.size() == 1) {
+        t2_part(Hd.parts[0], S);
+    } else {
+        host_pool().run(Hd.parts.size(), [&](size_t q) {
+            ByteSrc BS = S.fork();   // per-call cursor caches (batched regions are shared read-only)
+            t2_part(Hd.parts[q], BS);
+        });
     }
     // decode only the tile rows whose tiles are present (sharded / windowed decode)
     uint32_t jb = P.nty, je = 0;
