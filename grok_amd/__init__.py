@@ -82,6 +82,9 @@ def load_library(build_if_missing=True):
     lib.gk_main_header.restype = ctypes.c_int
     lib.gk_main_header.argtypes = [ctypes.c_void_p, P(ImageInfo), P(CParameters), ctypes.c_void_p, ctypes.c_size_t,
                                    P(ctypes.c_size_t), P(ctypes.c_size_t), P(ctypes.c_uint32)]
+    lib.gk_decode_window.restype = ctypes.c_int
+    lib.gk_decode_window.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int] + \
+        [ctypes.c_uint32] * 4 + [P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_int]
     lib.gk_decode_header.restype = ctypes.c_int
     lib.gk_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ImageInfo)]
     lib.gk_decode.restype = ctypes.c_int
@@ -278,6 +281,30 @@ class Engine:
         if rc != 0:
             self._err("gk_decode_header")
         return info
+
+    def decode_window(self, cs, window, length=None, out=None):
+        """gk_decode_window: window = (x0, y0, x1, y1).  Returns a (C, y1-y0, x1-x0) int32
+        numpy array, or fills ``out`` (torch cuda int32 of that shape) in place."""
+        on_dev = _is_torch_cuda(cs)
+        info = self.read_header(cs, length)
+        x0, y0, x1, y1 = window
+        c, h, w = info.numcomps, y1 - y0, x1 - x0
+        strides = (ctypes.c_uint32 * c)(*([w] * c))
+        if out is not None:
+            base, res, out_dev = out.data_ptr(), out, 1
+        else:
+            res = np.empty((c, h, w), np.int32)
+            base, out_dev = res.ctypes.data, 0
+        ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+        if on_dev:
+            rc = self.lib.gk_decode_window(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, x0, y0, x1, y1, ptrs,
+                                           strides, out_dev)
+        else:
+            b = np.frombuffer(cs, np.uint8)
+            rc = self.lib.gk_decode_window(self.ctx, b.ctypes.data, len(cs), 0, x0, y0, x1, y1, ptrs, strides, out_dev)
+        if rc != 0:
+            self._err("gk_decode_window")
+        return res
 
     def decode(self, cs, length=None, out=None, row0=0):
         """cs: bytes (host) or torch cuda uint8 tensor (+length).  Returns a

@@ -1057,7 +1057,8 @@ static void ensure_plan(gk_ctx* ctx, const Plan& want) {
 }
 
 // Forward/inverse DWT over all components with the ping-pong placement of gk_common.h.
-static void run_dwt(gk_ctx* ctx, bool forward, uint32_t jb = 0, uint32_t je = 0xffffffffu) {
+static void run_dwt(gk_ctx* ctx, bool forward, uint32_t jb = 0, uint32_t je = 0xffffffffu, uint32_t ib = 0,
+                    uint32_t ie = 0xffffffffu) {
     Plan& P = ctx->plan;
     int32_t* arena = (int32_t*)ctx->arena.p;
     const uint32_t L = P.p.numres - 1;
@@ -1065,10 +1066,12 @@ static void run_dwt(gk_ctx* ctx, bool forward, uint32_t jb = 0, uint32_t je = 0x
     for (uint32_t i = 0; i < L; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
         for (const ShapeG& S0 : P.shapes) {       // one launch per tile shape, grid.z = tiles of that shape
-            ShapeG S = S0;                        // restricted to tile rows [jb, je)
+            ShapeG S = S0;                        // restricted to tile rows [jb, je), columns [ib, ie)
             const uint32_t sj0 = std::max(S.tb.j0, jb), sj1 = std::min(S.tb.j0 + S.tb.ny, je);
-            if (sj0 >= sj1) continue;
+            const uint32_t si0 = std::max(S.tb.i0, ib), si1 = std::min(S.tb.i0 + S.tb.nx, ie);
+            if (sj0 >= sj1 || si0 >= si1) continue;
             S.tb.j0 = sj0; S.tb.ny = sj1 - sj0;
+            S.tb.i0 = si0; S.tb.nx = si1 - si0;
             const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
             for (uint32_t c = 0; c < P.nc; ++c) {
                 int32_t* A = arena + (size_t)c * 2 * P.plane_elems;
@@ -1547,8 +1550,10 @@ static void prefetch_packet_headers(gk_ctx* ctx, ByteSrc& S, const Plan& P, cons
     fetch_ranges(ctx, S, rg, ctx->hstage2, ctx->dstage2);
 }
 
+// win (optional): x0, y0, x1, y1 — decode only the tiles intersecting the window and write
+// the window into comps (whose element 0 is the window's top-left sample).
 static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
-                        const uint32_t* strides, int out_on_device) {
+                        const uint32_t* strides, int out_on_device, const uint32_t* win = nullptr) {
     hipStream_t st = ctx->st;
     HIPCHK(hipEventRecord(ctx->ev[0], st));
     ByteSrc S;
@@ -1560,6 +1565,17 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     ensure_plan(ctx, Hd.want);
     Plan& P = ctx->plan;
     apply_qcd(P, Hd.qcd);
+    if (win) {   // keep only the tile parts of tiles intersecting the window
+        if (win[0] >= win[2] || win[1] >= win[3] || win[2] > P.w || win[3] > P.h) throw GkError("bad decode window");
+        std::vector<TilePart> keep;
+        for (auto& TP : Hd.parts) {
+            if (TP.tile >= P.tiles.size()) throw GkError("corrupt SOT (tile index)");
+            const TileG& T = P.tiles[TP.tile];
+            if (T.x0 < win[2] && win[0] < T.x1 && T.y0 < win[3] && win[1] < T.y1) keep.push_back(std::move(TP));
+        }
+        Hd.parts.swap(keep);
+        if (Hd.parts.empty()) throw GkError("no tile part intersects the window");
+    }
     if (S.dev) {
         read_tile_part_headers(ctx, S, Hd);
         prefetch_packet_headers(ctx, S, P, Hd);
@@ -1661,12 +1677,30 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             t2_part(Hd.parts[q], BS);
         });
     }
-    // decode only the tile rows whose tiles are present (sharded / windowed decode)
-    uint32_t jb = P.nty, je = 0;
+    // decode only the rectangle of tiles that are present (sharded / windowed decode)
+    uint32_t ib = P.ntx, ie = 0, jb = P.nty, je = 0;
     for (uint32_t t = 0; t < P.tiles.size(); ++t)
-        if (seen[t]) { jb = std::min(jb, t / P.ntx); je = std::max(je, t / P.ntx + 1); }
-    const uint32_t b0 = P.tiles[jb * P.ntx].b0, b1 = P.tiles[je * P.ntx - 1].b1, nbr = b1 - b0;
-    const uint32_t ry0 = P.tiles[jb * P.ntx].y0, ry1 = P.tiles[(je - 1) * P.ntx].y1, nrows = ry1 - ry0;
+        if (seen[t]) {
+            ib = std::min(ib, t % P.ntx); ie = std::max(ie, t % P.ntx + 1);
+            jb = std::min(jb, t / P.ntx); je = std::max(je, t / P.ntx + 1);
+        }
+    // code-blocks of the tiles in the rectangle (absent tiles decode as zero)
+    std::vector<uint32_t> sel;
+    for (uint32_t j = jb; j < je; ++j)
+        for (uint32_t i = ib; i < ie; ++i) {
+            const TileG& T = P.tiles[(size_t)j * P.ntx + i];
+            for (uint32_t b = T.b0; b < T.b1; ++b) sel.push_back(b);
+        }
+    const uint32_t nbr = (uint32_t)sel.size();
+    // output region (image coordinates) and the image position of comps[c][0]
+    uint32_t rx0 = P.tiles[(size_t)jb * P.ntx + ib].x0, ry0 = P.tiles[(size_t)jb * P.ntx + ib].y0;
+    uint32_t rx1 = P.tiles[(size_t)(je - 1) * P.ntx + ie - 1].x1, ry1 = P.tiles[(size_t)(je - 1) * P.ntx + ie - 1].y1;
+    uint32_t ox = 0, oy = 0;
+    if (win) {
+        rx0 = std::max(rx0, win[0]); ry0 = std::max(ry0, win[1]); rx1 = std::min(rx1, win[2]); ry1 = std::min(ry1, win[3]);
+        ox = win[0]; oy = win[1];
+    }
+    const uint32_t ncols = rx1 - rx0, nrows = ry1 - ry0;
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     // ---- stage compressed bytes on the device
     const uint8_t* dcs = cs;
@@ -1675,12 +1709,12 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipMemcpyAsync(d, cs, len, hipMemcpyHostToDevice, st));
         dcs = d;
     }
-    // gather every block's segments into a 16-byte aligned slot with >= 16 bytes of slack
-    // (the T1 decoder reads its bytes through aligned 8-byte windows)
+    // gather every selected block's segments into a 16-byte aligned slot with >= 16 bytes of
+    // slack (the T1 decoders read their bytes through aligned windows)
     std::vector<uint64_t> seg;
-    seg.reserve(3 * (size_t)nb);
+    seg.reserve(3 * (size_t)nbr);
     uint64_t o = 0, t1_bytes = 0;
-    for (uint32_t b = 0; b < nb; ++b) {
+    for (uint32_t b : sel) {
         blk[b].data_off = o;
         uint32_t L = 0;
         for (auto& ch : chunks[b]) { seg.push_back(ch.first); seg.push_back(o + L); seg.push_back(ch.second); L += ch.second; }
@@ -1707,9 +1741,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     if (P.p.ht()) {
         // HT cleanup pass decode straight into the band windows (T1HT::decompress, T1HT.cpp:134-187)
+        uint32_t* dsel = (uint32_t*)ctx->dord.get(4 * (size_t)nbr + 16);
+        uint32_t* hsel = (uint32_t*)ctx->hord.get(4 * (size_t)nbr + 16);
+        memcpy(hsel, sel.data(), 4 * (size_t)nbr);
+        HIPCHK(hipMemcpyAsync(dsel, hsel, 4 * (size_t)nbr, hipMemcpyHostToDevice, st));
         int* derr = (int*)ctx->derr.get(64);
         HIPCHK(hipMemsetAsync(derr, 0, 64, st));
-        gk_launch_ht_dec(st, src_bytes, dblk + b0, arena, nbr, derr);
+        gk_launch_ht_dec(st, src_bytes, dblk, dsel, arena, nbr, derr);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         int herr = 0;
         HIPCHK(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st));
@@ -1719,18 +1757,21 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // lane assignment: blocks bucketed by pass count (descending), so the 64 lanes of a
         // wave decode similar amounts of work and the longest waves start first
         const uint32_t nw = (nbr + 63) / 64;
-        uint32_t* hord = (uint32_t*)ctx->hord.get(4 * (2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
-        uint32_t* hpos = hord + nbr;                 // position of block b0 + k in the order
-        uint64_t* hwo = (uint64_t*)(hord + 2 * (size_t)nbr + 2);
+        uint32_t* hord = (uint32_t*)ctx->hord.get(4 * (3 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
+        uint32_t* hpos = hord + nbr;                 // position of block sel[k] in the order
+        uint32_t* hids = hord + 2 * (size_t)nbr;     // sel
+        uint64_t* hwo = (uint64_t*)(hord + 3 * (size_t)nbr + 2);
         {
             std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
-            for (uint32_t b = b0; b < b1; ++b) cnt[std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1)]++;
+            for (uint32_t b : sel) cnt[std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1)]++;
             std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
             uint32_t acc = 0;
             for (int k = GK_MAX_PASSES + 1; k >= 0; --k) { start[k] = acc; acc += cnt[k]; }
-            for (uint32_t b = b0; b < b1; ++b) {
+            for (uint32_t q = 0; q < nbr; ++q) {
+                const uint32_t b = sel[q];
                 uint32_t k = std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1);
-                hord[start[k]] = b; hpos[b - b0] = start[k]; start[k]++;
+                hord[start[k]] = b; hpos[q] = start[k]; start[k]++;
+                hids[q] = b;
             }
             uint64_t wo = 0;
             for (uint32_t wv = 0; wv < nw; ++wv) {
@@ -1741,48 +1782,52 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             }
             hwo[nw] = wo;
         }
-        uint32_t* dord = (uint32_t*)ctx->dord.get(4 * (2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
-        HIPCHK(hipMemcpyAsync(dord, hord, 4 * (2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1), hipMemcpyHostToDevice, st));
+        const size_t obytes = 4 * (3 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1);
+        uint32_t* dord = (uint32_t*)ctx->dord.get(obytes);
+        HIPCHK(hipMemcpyAsync(dord, hord, obytes, hipMemcpyHostToDevice, st));
         const uint32_t* dpos = dord + nbr;
-        const uint64_t* dwo = (const uint64_t*)(dord + 2 * (size_t)nbr + 2);
+        const uint32_t* dids = dord + 2 * (size_t)nbr;
+        const uint64_t* dwo = (const uint64_t*)(dord + 3 * (size_t)nbr + 2);
         uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
         gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nbr);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_t1_recon(st, dblk + b0, dpos, dscr, dwo, arena, nbr);
+        gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr);
     }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
-    run_dwt(ctx, false, jb, je);
+    run_dwt(ctx, false, jb, je, ib, ie);
     HIPCHK(hipEventRecord(ctx->ev[4], st));
-    // ---- inverse MCT + DC shift + clamp into the output planes
+    // ---- inverse MCT + DC shift + clamp of the output region into the output planes
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
     int32_t mn = P.sgnd ? -(1 << (P.prec - 1)) : 0;
     int32_t mx = P.sgnd ? (1 << (P.prec - 1)) - 1 : (int32_t)((1u << P.prec) - 1);
     std::vector<int32_t*> dst(P.nc);
     std::vector<uint32_t> dstr(P.nc);
-    int32_t* stage = nullptr;
     if (!out_on_device) {
-        stage = (int32_t*)ctx->dplanes.get((size_t)P.w * P.h * P.nc * 4);
-        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = stage + (size_t)c * P.w * P.h + (size_t)ry0 * P.w; dstr[c] = P.w; }
+        int32_t* stage = (int32_t*)ctx->dplanes.get((size_t)ncols * nrows * P.nc * 4 + 16);
+        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = stage + (size_t)c * ncols * nrows; dstr[c] = ncols; }
     } else {
-        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = comps[c] + (size_t)ry0 * strides[c]; dstr[c] = strides[c]; }
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            dst[c] = comps[c] + (size_t)(ry0 - oy) * strides[c] + (rx0 - ox);
+            dstr[c] = strides[c];
+        }
     }
-    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems + (size_t)ry0 * P.stride; };
+    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems + (size_t)ry0 * P.stride + rx0; };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
     if (!P.p.irrev) {
-        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w, nrows,
-                                       shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], P.w, nrows, shift, mn, mx);
-    } else {
-        if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), P.stride, dst[0], dst[1], dst[2], dstr[0], P.w,
+        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), P.stride, dst[0], dst[1], dst[2], dstr[0], ncols,
                                        nrows, shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv_f(st, planeAf(c), P.stride, dst[c], dstr[c], P.w, nrows, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
+    } else {
+        if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), P.stride, dst[0], dst[1], dst[2], dstr[0], ncols,
+                                       nrows, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv_f(st, planeAf(c), P.stride, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
     }
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (!out_on_device) {
         for (uint32_t c = 0; c < P.nc; ++c)
-            HIPCHK(hipMemcpy2DAsync(comps[c] + (size_t)ry0 * strides[c], (size_t)strides[c] * 4, dst[c], (size_t)P.w * 4,
-                                    (size_t)P.w * 4, nrows, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpy2DAsync(comps[c] + (size_t)(ry0 - oy) * strides[c] + (rx0 - ox), (size_t)strides[c] * 4, dst[c],
+                                    (size_t)ncols * 4, (size_t)ncols * 4, nrows, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipEventRecord(ctx->ev[6], st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1931,6 +1976,20 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int3
     try {
         (void)hipSetDevice(ctx->device);
         decode_impl(ctx, cs, len, cs_on_device, comps, strides, out_on_device);
+        return 0;
+    } catch (const GkError& e) {
+        ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_decode_window(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, uint32_t x0, uint32_t y0,
+                     uint32_t x1, uint32_t y1, int32_t* const* comps, const uint32_t* strides, int out_on_device) {
+    if (!ctx || !cs || !comps || !strides) return -1;
+    try {
+        (void)hipSetDevice(ctx->device);
+        const uint32_t win[4] = {x0, y0, x1, y1};
+        decode_impl(ctx, cs, len, cs_on_device, comps, strides, out_on_device, win);
         return 0;
     } catch (const GkError& e) {
         ctx->err = e.msg;

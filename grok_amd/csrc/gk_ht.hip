@@ -280,7 +280,8 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
 // Decoder
 // =============================================================================
 __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ bytes, const GkBlock* __restrict__ blocks,
-                                                  int32_t* __restrict__ coef, uint32_t nblocks, int* __restrict__ err) {
+                                                  const uint32_t* __restrict__ ids, int32_t* __restrict__ coef,
+                                                  uint32_t nblocks, int* __restrict__ err) {
     __shared__ uint16_t s_tab[2][1024];
     __shared__ uint8_t s_e[HT_LINE][HT_WG];
     __shared__ uint8_t s_cx[HT_LINE][HT_WG];
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     const uint32_t b = blockIdx.x * HT_WG + tid;
     if (b >= nblocks) return;
 
-    const GkBlock G = blocks[b];
+    const GkBlock G = blocks[ids ? ids[b] : b];
     int32_t* dst = coef + G.band_off;
     const uint32_t stride = G.stride, w = G.w, h = G.h;
     auto zero_block = [&]() {
@@ -502,9 +503,9 @@ void gk_launch_ht_enc(hipStream_t st, const int32_t* coef, const GkBlock* blocks
                        mel_scratch, mel_cap, info, nblocks, err);
 }
 
-void gk_launch_ht_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, int32_t* coef, uint32_t nblocks,
-                      int* err) {
+void gk_launch_ht_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* ids, int32_t* coef,
+                      uint32_t nblocks, int* err) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_ht_dec, dim3((nblocks + HT_WG - 1) / HT_WG), dim3(HT_WG), 0, st, bytes, blocks, coef, nblocks,
-                       err);
+    hipLaunchKernelGGL(k_ht_dec, dim3((nblocks + HT_WG - 1) / HT_WG), dim3(HT_WG), 0, st, bytes, blocks, ids, coef,
+                       nblocks, err);
 }

@@ -28,8 +28,8 @@ void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off
                      uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter);
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
                       uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks);
-void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* pos, const uint64_t* scratch,
-                        const uint64_t* wave_off, int32_t* coef, uint32_t nblocks);
+void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
+                        const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks);
 // irreversible path (gk_dwt97.hip)
 void gk_launch_dc_ict_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin, float* y,
                           float* u, float* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift);
@@ -49,5 +49,5 @@ void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, flo
 // HTJ2K cleanup-pass block coder (gk_ht.hip)
 void gk_launch_ht_enc(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, uint8_t* mel_scratch,
                       uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err);
-void gk_launch_ht_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, int32_t* coef, uint32_t nblocks,
-                      int* err);
+void gk_launch_ht_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* ids, int32_t* coef,
+                      uint32_t nblocks, int* err);

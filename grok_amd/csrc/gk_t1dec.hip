@@ -742,16 +742,18 @@ __global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ b
 }
 
 // Reconstruction + dequantisation: wave per block, lane = column.
-__global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blocks, const uint32_t* __restrict__ pos,
+// Job q reconstructs block ids[q], whose decoder lane was pos[q].
+__global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blocks, const uint32_t* __restrict__ ids,
+                                                 const uint32_t* __restrict__ pos,
                                                  const uint64_t* __restrict__ scratch,
                                                  const uint64_t* __restrict__ wave_off, int32_t* __restrict__ coef,
                                                  uint32_t nblocks) {
-    const uint32_t b = blockIdx.x;
-    if (b >= nblocks) return;
+    const uint32_t q = blockIdx.x;
+    if (q >= nblocks) return;
     const int x = threadIdx.x;
-    const GkBlock B = blocks[b];
+    const GkBlock B = blocks[ids[q]];
     if (x >= (int)B.w) return;
-    const uint32_t slot = pos[b], ln = slot & 63;
+    const uint32_t slot = pos[q], ln = slot & 63;
     const uint64_t* WS = scratch + wave_off[slot >> 6];
     const bool irrev = B.flags & 1;
     float* fcoef = reinterpret_cast<float*>(coef);
@@ -815,8 +817,8 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
                 (double)h[3] / ((nblocks + 63) / 64));
     }
 }
-void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* pos, const uint64_t* scratch,
-                        const uint64_t* wave_off, int32_t* coef, uint32_t nblocks) {
+void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
+                        const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_t1_recon, dim3(nblocks), dim3(64), 0, st, blocks, pos, scratch, wave_off, coef, nblocks);
+    hipLaunchKernelGGL(k_t1_recon, dim3(nblocks), dim3(64), 0, st, blocks, ids, pos, scratch, wave_off, coef, nblocks);
 }

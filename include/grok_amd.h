@@ -116,6 +116,14 @@ int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
 int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
               const uint32_t* strides, int out_on_device);
 
+/* grk_decompress_set_window + grk_decompress (grok.h:1082-1657; CodeStreamDecompress
+ * window decode): decode the window [x0, x1) x [y0, y1) of the image.
+ * Only the tile parts of tiles intersecting the window are read (located through TLM
+ * when present, their packet headers through PLT), decoded and inverse-transformed;
+ * comps[c][0] receives sample (x0, y0) of component c, row stride strides[c]. */
+int gk_decode_window(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, uint32_t x0, uint32_t y0,
+                     uint32_t x1, uint32_t y1, int32_t* const* comps, const uint32_t* strides, int out_on_device);
+
 /* Stage timings of the last gk_encode / gk_decode. */
 int gk_get_timings(gk_ctx* ctx, gk_timings* t);
 /* Last error message for this context (grk_set_error_handler equivalent). */

@@ -201,3 +201,42 @@ def test_sharded_two_processes_one_gpu():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == (True, True)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_decode_window_vs_full(eng, seed):
+    # random windows (aligned, unaligned, edge, whole image) of tiled Part-1 / HT / 9/7
+    # streams, host and device codestreams: window decode == crop of the full decode
+    import torch
+    rng = np.random.default_rng(900 + seed)
+    c = int(rng.choice([1, 3]))
+    bits = 8 if c == 3 else 16
+    h, w = int(rng.integers(64, 400)), int(rng.integers(64, 400))
+    img = rng.integers(0, 1 << bits, size=(c, h, w)).astype(np.int32)
+    kind = seed % 3
+    kw = dict(tiles=(64, 64), tlm=bool(seed % 2), plt=bool(seed % 2), numres=4)
+    if kind == 1:
+        kw["cblk_sty"] = 64
+    if kind == 2:
+        kw["irreversible"] = True
+    cs = eng.encode(img, bits, params=_params(**kw))
+    full = eng.decode(cs)
+    if kind != 2:
+        np.testing.assert_array_equal(full, img)
+    d = torch.frombuffer(bytearray(cs), dtype=torch.uint8).cuda()
+    for _ in range(4):
+        x0, y0 = int(rng.integers(0, w)), int(rng.integers(0, h))
+        x1, y1 = int(rng.integers(x0 + 1, w + 1)), int(rng.integers(y0 + 1, h + 1))
+        np.testing.assert_array_equal(eng.decode_window(cs, (x0, y0, x1, y1)), full[:, y0:y1, x0:x1])
+        y = torch.empty((c, y1 - y0, x1 - x0), dtype=torch.int32, device="cuda")
+        eng.decode_window(d, (x0, y0, x1, y1), length=len(cs), out=y)
+        np.testing.assert_array_equal(y.cpu().numpy(), full[:, y0:y1, x0:x1])
+    np.testing.assert_array_equal(eng.decode_window(cs, (0, 0, w, h)), full)
+
+
+def test_decode_window_single_tile(eng):
+    fx = [f for f in FIXTURES if f.name == "rgb8_odd"][0]
+    c, h, w = fx.img.shape
+    np.testing.assert_array_equal(eng.decode_window(fx.cs, (5, 7, w - 3, h - 11)), fx.img[:, 7:h - 11, 5:w - 3])
+    with pytest.raises(RuntimeError):
+        eng.decode_window(fx.cs, (0, 0, w + 1, h))
