@@ -1754,14 +1754,18 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipStreamSynchronize(st));
         if (herr) throw GkError("corrupt HT code-block segment");
     } else {
-        // lane assignment: blocks bucketed by pass count (descending), so the 64 lanes of a
-        // wave decode similar amounts of work and the longest waves start first
-        const uint32_t nw = (nbr + 63) / 64;
-        uint32_t* hord = (uint32_t*)ctx->hord.get(4 * (3 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
-        uint32_t* hpos = hord + nbr;                 // position of block sel[k] in the order
-        uint32_t* hids = hord + 2 * (size_t)nbr;     // sel
-        uint64_t* hwo = (uint64_t*)(hord + 3 * (size_t)nbr + 2);
+        // lane assignment: blocks bucketed by pass count (descending), so the lanes of a
+        // wave decode similar amounts of work and the longest waves start first.  Only
+        // `L` lanes of each 64-lane wave carry a block (gk_t1dec_lanes): fewer lanes per wave
+        // give more waves, so every SIMD of the chip holds waves and can hide latency.
+        const uint32_t L = gk_t1dec_lanes();
+        const uint32_t nw = (nbr + L - 1) / L, nslots = nw * 64;
+        uint32_t* hord = (uint32_t*)ctx->hord.get(4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
+        uint32_t* hpos = hord + nslots;               // slot of block sel[k]
+        uint32_t* hids = hpos + nbr;                  // sel
+        uint64_t* hwo = (uint64_t*)(hids + nbr + 2);
         {
+            std::fill(hord, hord + nslots, 0xffffffffu);
             std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
             for (uint32_t b : sel) cnt[std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1)]++;
             std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
@@ -1770,26 +1774,29 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             for (uint32_t q = 0; q < nbr; ++q) {
                 const uint32_t b = sel[q];
                 uint32_t k = std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1);
-                hord[start[k]] = b; hpos[q] = start[k]; start[k]++;
+                const uint32_t idx = start[k]++;
+                const uint32_t slot = (idx / L) * 64 + idx % L;
+                hord[slot] = b; hpos[q] = slot;
                 hids[q] = b;
             }
             uint64_t wo = 0;
             for (uint32_t wv = 0; wv < nw; ++wv) {
                 hwo[wv] = wo;
                 uint32_t mp = 0;
-                for (uint32_t i = wv * 64; i < std::min(nbr, wv * 64 + 64); ++i) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
+                for (uint32_t i = wv * 64; i < wv * 64 + L; ++i)
+                    if (hord[i] != 0xffffffffu) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
                 wo += (260 + (uint64_t)mp * 64) * 64;
             }
             hwo[nw] = wo;
         }
-        const size_t obytes = 4 * (3 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1);
+        const size_t obytes = 4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1);
         uint32_t* dord = (uint32_t*)ctx->dord.get(obytes);
         HIPCHK(hipMemcpyAsync(dord, hord, obytes, hipMemcpyHostToDevice, st));
-        const uint32_t* dpos = dord + nbr;
-        const uint32_t* dids = dord + 2 * (size_t)nbr;
-        const uint64_t* dwo = (const uint64_t*)(dord + 3 * (size_t)nbr + 2);
+        const uint32_t* dpos = dord + nslots;
+        const uint32_t* dids = dpos + nbr;
+        const uint64_t* dwo = (const uint64_t*)(dids + nbr + 2);
         uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
-        gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nbr);
+        gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nslots);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr);
     }

@@ -26,6 +26,7 @@ void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks,
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
                      uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter);
+uint32_t gk_t1dec_lanes();
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
                       uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks);
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,

@@ -75,12 +75,12 @@ __device__ __forceinline__ uint32_t ring_get4(uint32_t (*ring)[64], int lane, ui
     const uint32_t j = (bp >> 2) & (RING_DW - 1);
     return __builtin_amdgcn_alignbyte(ring[j + 1][lane], ring[j][lane], bp & 3);
 }
-__device__ __forceinline__ void stage_load(MqDec& q) {
+template <class Q> __device__ __forceinline__ void stage_load(Q& q) {
     uint4 a = *(const uint4*)(q.p + q.sbase), b = *(const uint4*)(q.p + q.sbase + 16);
     q.T0 = a.x; q.T1 = a.y; q.T2 = a.z; q.T3 = a.w; q.T4 = b.x; q.T5 = b.y; q.T6 = b.z; q.T7 = b.w;
 }
 // stripe-pass boundary: commit the staged 32 bytes when the ring has room, request the next 32
-__device__ __forceinline__ void ring_boundary(uint32_t (*ring)[64], int lane, MqDec& q) {
+template <class Q> __device__ __forceinline__ void ring_boundary(uint32_t (*ring)[64], int lane, Q& q) {
     if (q.sbase != q.fill) { q.sbase = q.fill; stage_load(q); }   // after a synchronous top-up
     if (q.fill + 32 - q.bp <= 4 * RING_DW) {
         ring_write16(ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3);
@@ -91,7 +91,7 @@ __device__ __forceinline__ void ring_boundary(uint32_t (*ring)[64], int lane, Mq
     }
 }
 // inside a step loop: synchronous top-up for a lane about to run dry
-__device__ __forceinline__ void ring_topup(uint32_t (*ring)[64], int lane, MqDec& q) {
+template <class Q> __device__ __forceinline__ void ring_topup(uint32_t (*ring)[64], int lane, Q& q) {
     if (q.fill - q.bp < 8) {
         uint4 a = *(const uint4*)(q.p + q.fill);
         ring_write16(ring, lane, q.fill, a.x, a.y, a.z, a.w);
@@ -365,9 +365,10 @@ __global__ __launch_bounds__(64) void k_t1_dec(const uint8_t* __restrict__ bytes
     for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
     for (int i = lane; i < 256; i += 64) Ls.sc[i] = sc_rule((uint32_t)i);
     const uint32_t slot = blockIdx.x * 64 + lane;
-    const bool has = slot < nblocks;
+    const uint32_t bid = slot < nblocks ? order[slot] : 0xffffffffu;   // empty slots: 0xffffffff
+    const bool has = bid != 0xffffffffu;
     GkBlock B = {};
-    if (has) B = blocks[order[slot]];
+    if (has) B = blocks[bid];
     uint64_t* WS = scratch + wave_off[blockIdx.x];
     const uint32_t numbps = has ? B.numbps : 0, npasses = (has && B.numbps) ? B.npasses : 0;
     const uint32_t w = B.w, h = B.h;
@@ -534,9 +535,10 @@ __global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ b
     for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
     for (int i = lane; i < 256; i += 64) Ls.sc[i] = sc_rule((uint32_t)i);
     const uint32_t slot = blockIdx.x * 64 + lane;
-    const bool has = slot < nblocks;
+    const uint32_t bid = slot < nblocks ? order[slot] : 0xffffffffu;   // empty slots: 0xffffffff
+    const bool has = bid != 0xffffffffu;
     GkBlock B = {};
-    if (has) B = blocks[order[slot]];
+    if (has) B = blocks[bid];
     uint64_t* WS = scratch + wave_off[blockIdx.x];
     const uint32_t numbps = has ? B.numbps : 0, npasses = (has && B.numbps) ? B.npasses : 0;
     const uint32_t h = B.h;
@@ -741,6 +743,363 @@ __global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ b
     }
 }
 
+// =============================================================================
+// Variant 2 (default): lane-independent stepping with the stripe state in LDS.
+//
+// Measured on variant 1 (SQ counters, C2): one wave per SIMD spends 72 % of its
+// cycles issuing ~600 instructions per decision, so the kernel is bound by the
+// instruction count of one step (a wave alone issues one VALU per 4 cycles).
+// This variant cuts the step to what the decision needs:
+//  * the stripe's significance and sign rows live in LDS, per lane, in a
+//    guarded layout (bit c+1 = column c, three dwords per row, [dword][lane]),
+//    so the 3x3 neighbourhood of (x, r) is three ds_read2st64 + alignbit, and a
+//    new significance is one ds_or_b32 - no per-row register selects;
+//  * refinement (mu) and plane-bit rows live in LDS too (read / or per step);
+//  * candidates are consumed: the next coding position is the first set bit of
+//    the candidate rows (one col4 per step); propagation in SP follows from the
+//    neighbourhood window already read;
+//  * the MQ code register is a 64-bit bit buffer (Chigh at bits 63:48, code
+//    bits pre-loaded below it, one byte inserted per step), so RENORMD is one
+//    shift with no byte loop (Annex C.3.3 / C.3.4 restated).
+// Stripe boundaries (batched, as in variant 1) move rows between scratch,
+// registers and LDS.
+// =============================================================================
+struct Mq2 {
+    uint64_t c;                  // bits 63:48 = Chigh; `avail` valid code bits below bit 48
+    uint32_t a, avail;
+    uint32_t bp, len, fill;      // byte position (last byte taken in), block length, ring fill position
+    uint32_t nb4;                // bytes [bp, bp + 4)
+    uint32_t sbase;              // staged bytes cover [sbase, sbase + 32)
+    uint32_t T0, T1, T2, T3, T4, T5, T6, T7;
+    const uint8_t* p;
+};
+
+// BYTEIN ahead of need (mqc_dec.cpp BYTEIN, Annex C.3.4): the byte after the last one taken
+// goes below the valid bits; after 0xFF it overlaps by one bit (B << 9), a marker feeds 1s.
+__device__ __forceinline__ void mq2_refill(Mq2& q, bool en) {
+    const uint32_t cur = q.bp < q.len ? (q.nb4 & 0xff) : 0xffu;
+    const uint32_t nxt = q.bp + 1 < q.len ? ((q.nb4 >> 8) & 0xff) : 0xffu;
+    const bool ff = cur == 0xff, stuck = ff && nxt > 0x8f;
+    const bool seven = ff && !stuck;
+    const uint32_t add = en ? (stuck ? 0xffu : nxt) : 0u;
+    const uint32_t sh = (40u + (seven ? 1u : 0u) - q.avail) & 63;
+    q.c += (uint64_t)add << sh;
+    q.avail += en ? (seven ? 7u : 8u) : 0u;
+    const bool adv = en && !stuck;
+    q.bp += adv ? 1u : 0u;
+    q.nb4 = adv ? (q.nb4 >> 8) : q.nb4;
+}
+
+// DECODE (Annex C.3.2) for context cx, predicated on `en`; needs avail >= 15.
+__device__ __forceinline__ uint32_t mq2_decode(Mq2& q, Ctx5& cw, const uint32_t* tab, uint32_t cx, bool en) {
+    const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
+    uint32_t word = vsel(wi == 4, cw.w4, vsel(wi & 2, vsel(wi & 1, cw.w3, cw.w2), vsel(wi & 1, cw.w1, cw.w0)));
+    const uint32_t st = (word >> shb) & 0xff;
+    const uint32_t mps = st >> 6;
+    const uint32_t e = tab[st & 63];
+    const uint32_t qe = e & 0xffff;
+    const uint32_t chi = (uint32_t)(q.c >> 32);
+    const uint32_t a1 = q.a - qe;
+    const bool lower = (chi >> 16) < qe;
+    const bool fast = !lower && (a1 & 0x8000);
+    const bool mps_path = lower ? (a1 < qe) : (a1 >= qe);
+    const uint32_t d = (fast || mps_path) ? mps : (mps ^ 1);
+    const uint32_t nst = mps_path ? (((e >> 16) & 0x3f) | (mps << 6)) : (((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6));
+    const bool upd = en && !fast;
+    const uint32_t an = en ? (lower ? qe : a1) : q.a;
+    const uint32_t ch = (en && !lower) ? chi - (qe << 16) : chi;
+    word = (word & ~(0xffu << shb)) | (nst << shb);
+    const uint32_t wu = upd ? wi : 7u;
+    cw.w0 = vsel(wu == 0, word, cw.w0); cw.w1 = vsel(wu == 1, word, cw.w1);
+    cw.w2 = vsel(wu == 2, word, cw.w2); cw.w3 = vsel(wu == 3, word, cw.w3);
+    cw.w4 = vsel(wu == 4, word, cw.w4);
+    const uint32_t n = upd ? __clz(an) - 16 : 0u;   // RENORMD: all shifts at once
+    q.a = an << n;
+    q.c = (((uint64_t)ch << 32) | (uint32_t)q.c) << n;
+    q.avail -= n;
+    return d;
+}
+
+struct Dec2Lds {
+    uint32_t tab[48];
+    uint8_t zc[4][512];
+    uint8_t sc[256];                 // index bit0 N-neg 1 N-sig 2 W-neg 3 W-sig 4 E-neg 5 E-sig 6 S-neg 7 S-sig
+    uint32_t ring[RING_DW + 1][64];
+    uint32_t sg[6 * 3][64];          // significance rows y0-1 .. y0+4, guarded: bit c+1 of the 96-bit row = column c
+    uint32_t ng[6 * 3][64];          // sign rows (bits only where significant), same layout
+    uint32_t mu[4 * 2][64];          // refined-in-an-earlier-plane rows y0 .. y0+3, plain 32-bit halves
+    uint32_t bt[4 * 2][64];          // plane-bit rows y0 .. y0+3
+};
+
+__device__ __forceinline__ void g_put(uint32_t (*g)[64], int row, int lane, uint64_t v) {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    g[row * 3][lane] = lo << 1;
+    g[row * 3 + 1][lane] = __builtin_amdgcn_alignbit(hi, lo, 31);
+    g[row * 3 + 2][lane] = hi >> 31;
+}
+__device__ __forceinline__ uint64_t g_get(uint32_t (*g)[64], int row, int lane) {
+    const uint32_t d0 = g[row * 3][lane], d1 = g[row * 3 + 1][lane], d2 = g[row * 3 + 2][lane];
+    return ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, 1) << 32) | __builtin_amdgcn_alignbit(d1, d0, 1);
+}
+__device__ __forceinline__ void h_put(uint32_t (*g)[64], int row, int lane, uint64_t v) {
+    g[row * 2][lane] = (uint32_t)v;
+    g[row * 2 + 1][lane] = (uint32_t)(v >> 32);
+}
+__device__ __forceinline__ uint64_t h_get(uint32_t (*g)[64], int row, int lane) {
+    return ((uint64_t)g[row * 2 + 1][lane] << 32) | g[row * 2][lane];
+}
+
+__global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ bytes, const GkBlock* __restrict__ blocks,
+                                                const uint32_t* __restrict__ order, uint64_t* __restrict__ scratch,
+                                                const uint64_t* __restrict__ wave_off, uint32_t nblocks,
+                                                unsigned long long* __restrict__ stats, uint32_t kpark) {
+    __shared__ Dec2Lds Ls;
+    const int lane = threadIdx.x;
+    if (lane < 47) Ls.tab[lane] = c_mq[lane];
+    for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
+    for (int i = lane; i < 256; i += 64)
+        Ls.sc[i] = sc_rule((uint32_t)(((i >> 2) & 0xf) | ((i & 3) << 4) | (i & 0xc0)));
+    const uint32_t slot = blockIdx.x * 64 + lane;
+    const uint32_t bid = slot < nblocks ? order[slot] : 0xffffffffu;   // empty slots: 0xffffffff
+    const bool has = bid != 0xffffffffu;
+    GkBlock B = {};
+    if (has) B = blocks[bid];
+    uint64_t* WS = scratch + wave_off[blockIdx.x];
+    const uint32_t numbps = has ? B.numbps : 0, npasses = (has && B.numbps) ? B.npasses : 0;
+    const uint32_t h = B.h, w = B.w;
+    const uint64_t colmask = w >= 64 ? ~0ull : ((1ull << w) - 1);
+    const uint32_t ns = (h + 3) >> 2;
+    const uint8_t* zc = Ls.zc[B.orient & 3];
+    for (int r = 0; r < WS_FIXED; ++r) WS[r * 64 + lane] = 0;   // clear the state rows (coalesced)
+    for (int i = 0; i < 18; ++i) { Ls.sg[i][lane] = 0; Ls.ng[i][lane] = 0; }
+    for (int i = 0; i < 8; ++i) { Ls.mu[i][lane] = 0; Ls.bt[i][lane] = 0; }
+    Ctx5 cw = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};   // mqc_resetstates: ZC0=4, AGG=3, UNI=46
+    uint32_t nstep = 0, nsym = 0, nevents = 0;
+    Mq2 q;
+    q.p = npasses ? bytes + B.data_off : bytes;
+    q.len = npasses ? B.len : 0;
+    q.bp = 0; q.fill = 0; q.sbase = 0;
+    stage_load(q);
+    __syncthreads();
+    ring_boundary(Ls.ring, lane, q);
+    ring_boundary(Ls.ring, lane, q);
+    ring_boundary(Ls.ring, lane, q);
+    // INITDEC (mqc_dec.cpp:98-112): C = B0 << 16, BYTEIN, C <<= 7, CT -= 7, A = 0x8000
+    q.nb4 = ring_get4(Ls.ring, lane, 0);
+    q.c = (uint64_t)(q.len ? (q.nb4 & 0xff) : 0xffu) << 48;
+    q.avail = 0;
+    mq2_refill(q, true);
+    q.c <<= 7; q.avail -= 7; q.a = 0x8000;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) { q.nb4 = ring_get4(Ls.ring, lane, q.bp); mq2_refill(q, q.avail <= 40); }
+    q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+
+    // position: plane k (0 = top), pass type t (0 SP, 1 MR, 2 CL), stripe s, pass index pidx
+    uint32_t k = 0, t = 2, s = 0, pidx = 0;
+    bool done = npasses == 0, parked = false;
+    uint32_t nr = min(4u, h), x = 0, r = 0, ph = PH_FIND, rlhi = 0;
+    uint32_t vr = (1u << nr) - 1;                 // valid rows of the stripe
+    uint64_t C0, C1, C2, C3, E, fresh = 0;        // candidates (consumed as coded), run-length columns
+    uint64_t P0 = 0, P1 = 0, P2 = 0, P3 = 0;      // visited in SP of this plane
+    uint64_t M0 = 0, M1 = 0, M2 = 0, M3 = 0;      // refined rows after this stripe-pass
+    {
+        const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
+                       v3 = nr > 3 ? colmask : 0;
+        C0 = v0; C1 = v1; C2 = v2; C3 = v3;      // first CL: nothing significant yet
+        E = (nr == 4) ? colmask : 0ull;
+    }
+    Rows22 X = {};
+    {
+        uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
+        next_pos3(k2, t2, s2, p2, ns);
+        if (!done && p2 < npasses && k2 < numbps) load_rows(X, WS, WS + (WS_BITS + (size_t)k2 * 64) * 64, lane, 4 * s2);
+    }
+
+    while (__any(!done)) {
+        // ---------------- stripe boundary for parked lanes (batched)
+        const uint32_t nparked = __popcll(__ballot(parked));
+        const uint32_t nactive = __popcll(__ballot(!done && !parked));
+        if (nparked && (nparked >= kpark || nactive == 0)) {
+            ++nevents;
+            if (!done && q.sbase == q.fill && q.fill + 32 - q.bp <= 4 * RING_DW) {
+                ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3);
+                ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7);
+                q.fill += 32;
+            }
+            if (parked) {
+                parked = false;
+                const uint32_t y0 = 4 * s;
+                // the finished stripe: rows back to scratch
+                const uint64_t S1 = g_get(Ls.sg, 1, lane), S2 = g_get(Ls.sg, 2, lane), S3 = g_get(Ls.sg, 3, lane),
+                               S4 = g_get(Ls.sg, 4, lane);
+                const uint64_t N1 = g_get(Ls.ng, 1, lane), N2 = g_get(Ls.ng, 2, lane), N3 = g_get(Ls.ng, 3, lane),
+                               N4 = g_get(Ls.ng, 4, lane);
+                const uint64_t B0 = h_get(Ls.bt, 0, lane), B1 = h_get(Ls.bt, 1, lane), B2 = h_get(Ls.bt, 2, lane),
+                               B3 = h_get(Ls.bt, 3, lane);
+                uint64_t* sgp = WS + (size_t)(WS_SIG + y0 + 1) * 64 + lane;
+                uint64_t* ngp = WS + (size_t)(WS_NEG + y0 + 1) * 64 + lane;
+                uint64_t* pip = WS + (size_t)(WS_PI + y0) * 64 + lane;
+                uint64_t* btp = WS + (WS_BITS + (size_t)k * 64 + y0) * 64 + lane;
+                sgp[0] = S1; sgp[64] = S2; sgp[128] = S3; sgp[192] = S4;
+                ngp[0] = N1; ngp[64] = N2; ngp[128] = N3; ngp[192] = N4;
+                if (t == 0) { pip[0] = P0; pip[64] = P1; pip[128] = P2; pip[192] = P3; }
+                btp[0] = B0; btp[64] = B1; btp[128] = B2; btp[192] = B3;
+                const uint32_t ok = k;
+                next_pos3(k, t, s, pidx, ns);
+                done = pidx >= npasses || k >= numbps;
+                // new stripe rows: prefetched, except rows the finished stripe still held when the
+                // prefetch was issued (1-stripe blocks: all; 2-stripe blocks at a pass change: row 4)
+                const bool one = ns == 1, two = ns == 2 && s == 0;
+                const uint64_t nS0 = s ? S4 : 0ull, nN0 = s ? N4 : 0ull;
+                const uint64_t nS1 = one ? S1 : X.s1, nS2 = one ? S2 : X.s2, nS3 = one ? S3 : X.s3, nS4 = one ? S4 : X.s4;
+                const uint64_t nS5 = two ? S1 : X.s5;
+                const uint64_t nN1 = one ? N1 : X.n1, nN2 = one ? N2 : X.n2, nN3 = one ? N3 : X.n3, nN4 = one ? N4 : X.n4;
+                const uint64_t nN5 = two ? N1 : X.n5;
+                const uint64_t nP0 = one ? P0 : X.p0, nP1 = one ? P1 : X.p1, nP2 = one ? P2 : X.p2, nP3 = one ? P3 : X.p3;
+                const uint64_t nM0 = one ? M0 : X.m0, nM1 = one ? M1 : X.m1, nM2 = one ? M2 : X.m2, nM3 = one ? M3 : X.m3;
+                const bool same_plane = one && ok == k;
+                const bool newplane = t == 0 || k == 0;
+                const uint64_t nB0 = newplane ? 0ull : (same_plane ? B0 : X.b0), nB1 = newplane ? 0ull : (same_plane ? B1 : X.b1),
+                               nB2 = newplane ? 0ull : (same_plane ? B2 : X.b2), nB3 = newplane ? 0ull : (same_plane ? B3 : X.b3);
+                const uint64_t pP0 = t == 0 ? 0ull : nP0, pP1 = t == 0 ? 0ull : nP1, pP2 = t == 0 ? 0ull : nP2,
+                               pP3 = t == 0 ? 0ull : nP3;
+                g_put(Ls.sg, 0, lane, nS0); g_put(Ls.sg, 1, lane, nS1); g_put(Ls.sg, 2, lane, nS2);
+                g_put(Ls.sg, 3, lane, nS3); g_put(Ls.sg, 4, lane, nS4); g_put(Ls.sg, 5, lane, nS5);
+                g_put(Ls.ng, 0, lane, nN0); g_put(Ls.ng, 1, lane, nN1); g_put(Ls.ng, 2, lane, nN2);
+                g_put(Ls.ng, 3, lane, nN3); g_put(Ls.ng, 4, lane, nN4); g_put(Ls.ng, 5, lane, nN5);
+                h_put(Ls.mu, 0, lane, nM0); h_put(Ls.mu, 1, lane, nM1); h_put(Ls.mu, 2, lane, nM2); h_put(Ls.mu, 3, lane, nM3);
+                h_put(Ls.bt, 0, lane, nB0); h_put(Ls.bt, 1, lane, nB1); h_put(Ls.bt, 2, lane, nB2); h_put(Ls.bt, 3, lane, nB3);
+                const uint32_t ny0 = 4 * s;
+                nr = done ? 0u : min(4u, h - ny0);
+                vr = (1u << nr) - 1;
+                const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
+                               v3 = nr > 3 ? colmask : 0;
+                const uint64_t dS0 = dil3(nS0, nS1, nS2), dS1 = dil3(nS1, nS2, nS3), dS2 = dil3(nS2, nS3, nS4),
+                               dS3 = dil3(nS3, nS4, nS5);
+                const uint64_t q0 = t == 0 ? dS0 : ~pP0, q1 = t == 0 ? dS1 : ~pP1, q2 = t == 0 ? dS2 : ~pP2,
+                               q3 = t == 0 ? dS3 : ~pP3;
+                const uint64_t w0 = t == 1 ? nS1 : ~nS1, w1 = t == 1 ? nS2 : ~nS2, w2 = t == 1 ? nS3 : ~nS3,
+                               w3 = t == 1 ? nS4 : ~nS4;
+                C0 = w0 & q0 & v0; C1 = w1 & q1 & v1; C2 = w2 & q2 & v2; C3 = w3 & q3 & v3;
+                E = (t == 2 && nr == 4) ? (C0 & C1 & C2 & C3 & ~dil3(nS0 | nS1, nS2 | nS3, nS4 | nS5)) : 0ull;
+                // SP: visited = its candidates (grown by propagation); MR: refined = old | coded now
+                P0 = t == 0 ? C0 : pP0; P1 = t == 0 ? C1 : pP1; P2 = t == 0 ? C2 : pP2; P3 = t == 0 ? C3 : pP3;
+                M0 = nM0 | (t == 1 ? C0 : 0ull); M1 = nM1 | (t == 1 ? C1 : 0ull);
+                M2 = nM2 | (t == 1 ? C2 : 0ull); M3 = nM3 | (t == 1 ? C3 : 0ull);
+                if (t == 1) {
+                    uint64_t* mup = WS + (size_t)(WS_MU + ny0) * 64 + lane;
+                    mup[0] = M0; mup[64] = M1; mup[128] = M2; mup[192] = M3;
+                }
+                fresh = 0; ph = PH_FIND;
+            }
+            q.sbase = q.fill;
+            stage_load(q);
+            uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
+            next_pos3(k2, t2, s2, p2, ns);
+            const bool pf = !done && p2 < npasses && k2 < numbps;
+            load_rows(X, WS, WS + (WS_BITS + (size_t)(pf ? k2 : 0) * 64) * 64, lane, pf ? 4 * s2 : 0);
+        }
+        // ---------------- one decision per active lane
+        const bool act = !done && !parked;
+        ++nstep;
+        if (__any(q.fill - q.bp < 8)) ring_topup(Ls.ring, lane, q);
+        mq2_refill(q, act && q.avail <= 40);
+        const bool finding = ph == PH_FIND;
+        // next coding position: first remaining candidate in stripe scan order
+        const uint64_t CU = C0 | C1 | C2 | C3;
+        const uint32_t xq = ((uint32_t)__ffsll((long long)CU) - 1) & 63;
+        const uint32_t c4 = col4(C0, C1, C2, C3, xq);
+        const bool use = act && finding;
+        const bool found = CU != 0;
+        x = (use && found) ? xq : x;
+        r = (use && found) ? (uint32_t)(__ffs(c4) - 1) : r;
+        const bool pend = use ? found : act;
+        parked = parked || (use && !found);
+        // neighbourhood of (x, r): guarded rows r .. r+2 (= stripe rows r-1 .. r+1)
+        const uint32_t dx = x >> 5, sx = x & 31;
+        const uint32_t o0 = (r * 3 + dx);
+        const uint32_t s0 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 1][lane], Ls.sg[o0][lane], sx) & 7;
+        const uint32_t s1 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 4][lane], Ls.sg[o0 + 3][lane], sx) & 7;
+        const uint32_t s2 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 7][lane], Ls.sg[o0 + 6][lane], sx) & 7;
+        const uint32_t n0 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 1][lane], Ls.ng[o0][lane], sx) & 7;
+        const uint32_t n1 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 4][lane], Ls.ng[o0 + 3][lane], sx) & 7;
+        const uint32_t n2 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 7][lane], Ls.ng[o0 + 6][lane], sx) & 7;
+        const uint32_t mub = (Ls.mu[r * 2 + dx][lane] >> sx) & 1;
+        const uint32_t fs = s0 | (s1 << 3) | (s2 << 6);
+        const uint32_t fn = n0 | (n1 << 3) | (n2 << 6);
+        const uint32_t sce = Ls.sc[(fs & 0xaa) | ((fn >> 1) & 0x55)];
+        const uint32_t zcx = zc[fs];
+        const bool is_cl = t == 2, is_mr = t == 1, is_sp = t == 0;
+        // a column starts in run-length mode when it was eligible at stripe start, is untouched
+        // and its left neighbour column gained no significance in this pass
+        // (bitwise, not short-circuit: keeps the step free of exec-mask branches)
+        const bool agg = is_cl & finding & (((E >> x) & 1) != 0) & (c4 == 0xf) & ((((fresh << 1) >> x) & 1) == 0);
+        const uint32_t cx_mr = vsel(mub != 0, CTX_MAG + 2, vsel((fs & 0x1ef) != 0, CTX_MAG + 1, CTX_MAG));
+        const uint32_t cx = vsel(is_mr, cx_mr,
+                                 vsel(agg, CTX_AGG,
+                                      vsel(ph == PH_SIGN, CTX_SC + (sce & 15), vsel(finding, CTX_ZC + zcx, CTX_UNI))));
+        while (__any(pend && q.avail < 16)) {   // rare: a burst of long renormalisations
+            mq2_refill(q, pend && q.avail < 16);
+            q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+        }
+        const uint32_t d = mq2_decode(q, cw, Ls.tab, cx, pend);
+        nsym += pend ? 1 : 0;
+        // ---- state updates
+        const bool sig = pend && !is_mr && ph == PH_SIGN;
+        const bool negs = sig && ((d ^ (sce >> 4)) & 1);
+        const uint32_t gx = x + 1, gd = gx >> 5, gb = 1u << (gx & 31);
+        atomicOr(&Ls.sg[(r + 1) * 3 + gd][lane], sig ? gb : 0u);
+        atomicOr(&Ls.ng[(r + 1) * 3 + gd][lane], negs ? gb : 0u);
+        const bool pb = sig || (pend && is_mr && d);
+        atomicOr(&Ls.bt[r * 2 + dx][lane], pb ? (1u << sx) : 0u);
+        fresh |= (uint64_t)(sig ? 1u : 0u) << x;
+        // SP: positions after (x, r) that gain a significant neighbour become candidates:
+        // (x, r+1) and column x+1 rows r-1 .. r+1, unless significant (window bits 7; 2, 5, 8)
+        const bool spn = sig && is_sp;
+        const uint32_t nf = ~fs;
+        const uint32_t ca = spn ? ((((nf >> 7) & 1) << (r + 1)) & vr) : 0u;
+        const uint32_t t3 = ((nf >> 2) & 1) | ((nf >> 4) & 2) | ((nf >> 6) & 4);
+        const uint32_t cb = (spn && gx < w) ? (((t3 << r) >> 1) & vr) : 0u;
+        // consumption: the coded position; a whole column after a zero run-length decision;
+        // rows 0 .. rr once the run-length index rr is known
+        const uint32_t rr = (rlhi << 1) | d;
+        const uint32_t crow_f = vsel(agg, vsel(d != 0, 0u, 0xfu), 1u << r);
+        const uint32_t crow = vsel(pend, vsel(finding, crow_f, vsel(ph == PH_UNI2, (2u << rr) - 1, 0u)), 0u);
+#define GK_CROW(Ci, Pi, i)                                                                                           \
+    {                                                                                                                \
+        const uint64_t add = (uint64_t)(((ca >> i) & 1) | (((cb >> i) & 1) << 1)) << x;                             \
+        const uint64_t clr = (uint64_t)((crow >> i) & 1) << x;                                                       \
+        Ci = (Ci & ~clr) | add;                                                                                      \
+        Pi |= add;                                                                                                   \
+    }
+        GK_CROW(C0, P0, 0) GK_CROW(C1, P1, 1) GK_CROW(C2, P2, 2) GK_CROW(C3, P3, 3)
+#undef GK_CROW
+        // phase machine: FIND -(ZC 1)-> SIGN -> FIND; FIND(run-length) -(1)-> UNI1 -> UNI2 -> SIGN
+        // next phase = table[ph][d][agg] (MR always stays in FIND), 2 bits per entry
+        //   FIND: agg ? (d ? UNI1 : FIND) : (d ? SIGN : FIND); SIGN -> FIND; UNI1 -> UNI2; UNI2 -> SIGN
+        const bool uni1 = ph == PH_UNI1, uni2 = ph == PH_UNI2;
+        const uint32_t key = (ph << 2) | (d << 1) | (agg ? 1u : 0u);
+        constexpr uint32_t kPhT = (0u << 0) | (0u << 2) | (PH_SIGN << 4) | (PH_UNI1 << 6)       // FIND
+                                | (PH_UNI2 << 16) | (PH_UNI2 << 18) | (PH_UNI2 << 20) | (PH_UNI2 << 22)  // UNI1
+                                | (PH_SIGN << 24) | (PH_SIGN << 26) | (PH_SIGN << 28) | (PH_SIGN << 30); // UNI2
+        const uint32_t nph = is_mr ? (uint32_t)PH_FIND : ((kPhT >> (2 * key)) & 3);
+        rlhi = vsel(pend & uni1, d, rlhi);
+        r = vsel(pend & uni2, rr, r);
+        ph = vsel(pend, nph, ph);
+        q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+    }
+    if (stats) {
+        unsigned long long tot = nsym;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        if (lane == 0) {
+            atomicAdd(&stats[3], (unsigned long long)nevents);
+            atomicAdd(&stats[0], (unsigned long long)nstep); atomicAdd(&stats[1], tot);
+            atomicMax(&stats[2], (unsigned long long)nstep);
+        }
+    }
+}
+
 // Reconstruction + dequantisation: wave per block, lane = column.
 // Job q reconstructs block ids[q], whose decoder lane was pos[q].
 __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blocks, const uint32_t* __restrict__ ids,
@@ -788,6 +1147,16 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
 }
 
 #include "gk_launch.h"
+// Blocks per 64-lane wave (GK_T1DEC_LANES, 1..64).
+uint32_t gk_t1dec_lanes() {
+    static uint32_t lanes = 0;
+    if (!lanes) {
+        const char* v = getenv("GK_T1DEC_LANES");
+        int n = v ? atoi(v) : 64;
+        lanes = (uint32_t)(n < 1 ? 1 : (n > 64 ? 64 : n));
+    }
+    return lanes;
+}
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
                       uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks) {
     if (!nblocks) return;
@@ -797,14 +1166,17 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     if (want) (void)hipMemsetAsync(stats, 0, 64, st);
     static int variant = -1, kpark = 4;
     if (variant < 0) {
-        const char* v = getenv("GK_T1DEC");       // 0: stripe-synchronous, 1 (default): lane-independent
-        variant = v ? atoi(v) : 1;
+        const char* v = getenv("GK_T1DEC");   // 0: stripe-synchronous, 1: lane-independent, 2 (default): LDS state
+        variant = v ? atoi(v) : 2;
         const char* kp = getenv("GK_T1DEC_PARK");
         if (kp) kpark = atoi(kp);
     }
     if (variant == 0)
         hipLaunchKernelGGL(k_t1_dec, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, want ? stats : nullptr);
+    else if (variant == 2)
+        hipLaunchKernelGGL(k_t1_dec2, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
+                           wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
     else
         hipLaunchKernelGGL(k_t1_dec_ind, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);

@@ -20,6 +20,7 @@
 #include "gk_common.h"
 #include "gk_t1_common.h"
 #include <type_traits>
+#include <cstdlib>
 
 #define SYM_PER_PLANE 11264u   // >= 2 symbols per sample + 3 per stripe column, per bit-plane
 
@@ -410,17 +411,20 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
                                               const GkBlock* __restrict__ blocks, uint8_t* __restrict__ bytes,
                                               GkPass* __restrict__ passes, uint32_t* __restrict__ info,
                                               uint32_t nblocks, int* err, const int32_t* __restrict__ pass_nmse,
-                                              uint32_t* __restrict__ pass_counter) {
+                                              uint32_t* __restrict__ pass_counter, uint32_t nl) {
+    // nl = blocks per wave (lanes >= nl idle; gk_t1enc_lanes); pass ends staged in LDS [pass][lane]
     __shared__ uint32_t tab[47];
-    __shared__ uint32_t pe_lds[GK_MAX_PASSES + 1][64];
+    extern __shared__ uint32_t pe_dyn[];
     const int lane = threadIdx.x;
     if (lane < 47) tab[lane] = c_mq[lane];
-    const uint32_t b = blockIdx.x * 64 + lane;
-    const bool has = b < nblocks;
+    const uint32_t b = blockIdx.x * nl + lane;
+    const bool has = (uint32_t)lane < nl && b < nblocks;
+    uint32_t* pe_col = pe_dyn + (lane < (int)nl ? lane : 0);
+#define pe_lds_at(p) pe_col[(size_t)(p) * nl]
     const uint32_t numbps = has ? cm_info[2 * b] : 0, npasses = has ? cm_info[2 * b + 1] : 0;
     const uint32_t* PE = pass_end + (size_t)(has ? b : 0) * GK_MAX_PASSES;
-    for (uint32_t p = 0; p < npasses; ++p) pe_lds[p][lane] = PE[p];
-    pe_lds[npasses][lane] = 0xffffffffu;
+    for (uint32_t p = 0; p < npasses; ++p) pe_lds_at(p) = PE[p];
+    if (has) pe_lds_at(npasses) = 0xffffffffu;
     const uint32_t nsym = npasses ? PE[npasses - 1] : 0;
     GkBlock B = {};
     if (has) B = blocks[b];
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxsym = max(maxsym, (uint32_t)__shfl_xor((int)maxsym, o));
     __syncthreads();
-    uint32_t p = 0, next_end = pe_lds[0][lane];
+    uint32_t p = 0, next_end = has ? pe_lds_at(0) : 0xffffffffu;
     // pass bookkeeping (T1.cpp:856-897); only the last pass is terminated (default style)
     auto close_passes = [&](uint32_t i) {
         while (__any(npasses && p < npasses && next_end == i)) {
@@ -463,7 +467,7 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
                 }
                 P[p].dist = cum;
                 ++p;
-                next_end = pe_lds[p][lane];
+                next_end = pe_lds_at(p);
             }
         }
     };
@@ -509,6 +513,7 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
     info[4 * b + 2] = P[npasses - 1].rate;
     info[4 * b + 3] = poff;
     if (q.ovf) atomicOr(err, 1);
+#undef pe_lds_at
 }
 
 #include "gk_launch.h"
@@ -527,6 +532,13 @@ void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
                      uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_t1_mq, dim3((nblocks + 63) / 64), dim3(64), 0, st, sym, sym_off, pass_end, cm_info, blocks,
-                       bytes, passes, info, nblocks, err, pass_nmse, pass_counter);
+    static uint32_t nl = 0;
+    if (!nl) {   // blocks per 64-lane wave (GK_T1ENC_LANES, 1..64)
+        const char* v = getenv("GK_T1ENC_LANES");
+        const int n = v ? atoi(v) : 64;
+        nl = (uint32_t)(n < 1 ? 1 : (n > 64 ? 64 : n));
+    }
+    const size_t lds = (size_t)(GK_MAX_PASSES + 1) * nl * 4;
+    hipLaunchKernelGGL(k_t1_mq, dim3((nblocks + nl - 1) / nl), dim3(64), lds, st, sym, sym_off, pass_end, cm_info,
+                       blocks, bytes, passes, info, nblocks, err, pass_nmse, pass_counter, nl);
 }
