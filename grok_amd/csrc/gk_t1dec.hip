@@ -65,8 +65,15 @@ __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
     return r;
 }
 
+// bytes at or past the block length read as 0xFF (the MQ decoder's end-of-data rule,
+// mqc_dec.cpp BYTEIN), so the per-step byte fetch needs no length test
+__device__ __forceinline__ uint32_t ff_past(uint32_t v, uint32_t at, uint32_t len) {
+    const int k = (int)len - (int)at;
+    return k <= 0 ? 0xffffffffu : (k >= 4 ? v : (v | (0xffffffffu << (8 * k))));
+}
 __device__ __forceinline__ void ring_write16(uint32_t (*ring)[64], int lane, uint32_t pos, uint32_t a, uint32_t b,
-                                             uint32_t c, uint32_t d) {
+                                             uint32_t c, uint32_t d, uint32_t len) {
+    a = ff_past(a, pos, len); b = ff_past(b, pos + 4, len); c = ff_past(c, pos + 8, len); d = ff_past(d, pos + 12, len);
     const uint32_t j = (pos >> 2) & (RING_DW - 1);
     ring[j][lane] = a; ring[j + 1][lane] = b; ring[j + 2][lane] = c; ring[j + 3][lane] = d;
     if (j == 0) ring[RING_DW][lane] = a;   // mirror for wrap-around reads
@@ -83,8 +90,8 @@ template <class Q> __device__ __forceinline__ void stage_load(Q& q) {
 template <class Q> __device__ __forceinline__ void ring_boundary(uint32_t (*ring)[64], int lane, Q& q) {
     if (q.sbase != q.fill) { q.sbase = q.fill; stage_load(q); }   // after a synchronous top-up
     if (q.fill + 32 - q.bp <= 4 * RING_DW) {
-        ring_write16(ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3);
-        ring_write16(ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7);
+        ring_write16(ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3, q.len);
+        ring_write16(ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7, q.len);
         q.fill += 32;
         q.sbase = q.fill;
         stage_load(q);
@@ -94,7 +101,7 @@ template <class Q> __device__ __forceinline__ void ring_boundary(uint32_t (*ring
 template <class Q> __device__ __forceinline__ void ring_topup(uint32_t (*ring)[64], int lane, Q& q) {
     if (q.fill - q.bp < 8) {
         uint4 a = *(const uint4*)(q.p + q.fill);
-        ring_write16(ring, lane, q.fill, a.x, a.y, a.z, a.w);
+        ring_write16(ring, lane, q.fill, a.x, a.y, a.z, a.w, q.len);
         q.fill += 16;
     }
 }
@@ -598,8 +605,8 @@ __global__ __launch_bounds__(64) void k_t1_dec_ind(const uint8_t* __restrict__ b
             // boundary's stores, so waiting for them does not wait for the stores
             // (only when no synchronous top-up moved the fill point since the bytes were staged)
             if (!done && q.sbase == q.fill && q.fill + 32 - q.bp <= 4 * RING_DW) {
-                ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3);
-                ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7);
+                ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3, q.len);
+                ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7, q.len);
                 q.fill += 32;
             }
             if (parked) {
@@ -777,10 +784,9 @@ struct Mq2 {
 // BYTEIN ahead of need (mqc_dec.cpp BYTEIN, Annex C.3.4): the byte after the last one taken
 // goes below the valid bits; after 0xFF it overlaps by one bit (B << 9), a marker feeds 1s.
 __device__ __forceinline__ void mq2_refill(Mq2& q, bool en) {
-    const uint32_t cur = q.bp < q.len ? (q.nb4 & 0xff) : 0xffu;
-    const uint32_t nxt = q.bp + 1 < q.len ? ((q.nb4 >> 8) & 0xff) : 0xffu;
-    const bool ff = cur == 0xff, stuck = ff && nxt > 0x8f;
-    const bool seven = ff && !stuck;
+    const uint32_t cur = q.nb4 & 0xff, nxt = (q.nb4 >> 8) & 0xff;   // ring bytes past the end are 0xFF
+    const bool ff = cur == 0xff, stuck = ff & (nxt > 0x8f);
+    const bool seven = ff & !stuck;
     const uint32_t add = en ? (stuck ? 0xffu : nxt) : 0u;
     const uint32_t sh = (40u + (seven ? 1u : 0u) - q.avail) & 63;
     q.c += (uint64_t)add << sh;
@@ -922,8 +928,8 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         if (nparked && (nparked >= kpark || nactive == 0)) {
             ++nevents;
             if (!done && q.sbase == q.fill && q.fill + 32 - q.bp <= 4 * RING_DW) {
-                ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3);
-                ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7);
+                ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3, q.len);
+                ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7, q.len);
                 q.fill += 32;
             }
             if (parked) {

@@ -477,12 +477,18 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
     if (nsym > 16) nxt4 = *(const uint4*)(sp + 16);
     for (uint32_t base = 0; base < maxsym; base += 16) {
         uint4 pre = make_uint4(0, 0, 0, 0);
-        if (base + 32 < nsym) pre = *(const uint4*)(sp + base + 32);
 #pragma unroll
         for (uint32_t j = 0; j < 16; ++j) {
             const uint32_t i = base + j;
             const bool en = i < nsym;
             mq_code(q, cw, tab, byte_of(cur4, j), en);
+            // the prefetch two chunks ahead is issued after the first symbol has consumed this
+            // chunk's bytes, so the wait for them does not also wait for the prefetch
+            if (j == 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (base + 32 < nsym) pre = *(const uint4*)(sp + base + 32);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             close_passes(i + 1);
         }
         cur4 = nxt4; nxt4 = pre;
