@@ -397,6 +397,69 @@ __device__ __forceinline__ void mq_code(MqLane& q, Ctx5e& cw, const uint32_t* ta
     }
 }
 
+// Branch-free BYTEOUT for the symbol loop: every value is computed for all lanes and
+// committed with selects; only the word store is predicated (`en` lanes that complete
+// a 4-byte word).  Same arithmetic as mql_byteout_if (Annex C.2.6).
+__device__ __forceinline__ void mql_byteout_sel(MqLane& q, bool en) {
+    const uint32_t carry = (q.cur != 0xff) ? ((q.c >> 27) & 1) : 0u;
+    const uint32_t cur = q.cur + carry;
+    const uint32_t c = q.c & ~(carry << 27);
+    const bool ff = cur == 0xff;
+    const uint32_t nb = ff ? (c >> 20) : (c >> 19);
+    // emit `cur` at bp (bp = -1 is the encoder's dummy byte before the buffer)
+    const bool inb = (q.bp >= 0) & ((uint32_t)q.bp < q.cap);
+    const bool put = en & inb;
+    const uint32_t wb = q.wbuf | (put ? cur << (8 * (q.bp & 3)) : 0u);
+    const bool full = put & ((q.bp & 3) == 3);
+    if (full) *(uint32_t*)(q.out + (q.bp - 3)) = wb;
+    q.wbuf = vsel_e(en, full ? 0u : wb, q.wbuf);
+    q.ovf |= (en & (q.bp >= 0) & !inb) ? 1u : 0u;
+    q.bp += en ? 1 : 0;
+    q.cur = vsel_e(en, nb & 0xff, q.cur);
+    q.c = vsel_e(en, c & (ff ? 0xfffffu : 0x7ffffu), q.c);
+    q.ct = vsel_e(en, ff ? 7u : 8u, q.ct);
+}
+
+// CODEMPS / CODELPS + RENORME (Annex C.2.4-C.2.7), branch-free.  With x = (MPS symbol) xor
+// (A - Qe < Qe): the coder adds Qe to C iff x and keeps A - Qe iff x, else A = Qe.
+// RENORME's n shifts run as at most two segments that end at a byte boundary (CT = 0),
+// each followed by a predicated BYTEOUT; a third boundary (two 0xFF bytes in one
+// renormalisation) falls back to the loop.
+__device__ __forceinline__ void mq_code2(MqLane& q, Ctx5e& cw, const uint32_t* tab, uint32_t s, bool en) {
+    const uint32_t cx = s >> 1, d = s & 1;
+    const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
+    uint32_t word = vsel_e(wi == 4, cw.w4, vsel_e(wi & 2, vsel_e(wi & 1, cw.w3, cw.w2), vsel_e(wi & 1, cw.w1, cw.w0)));
+    const uint32_t st = (word >> shb) & 0xff;
+    const uint32_t mps = st >> 6;
+    const uint32_t e = tab[st & 63];
+    const uint32_t qe = e & 0xffff;
+    const uint32_t a1 = q.a - qe;
+    const bool is_mps = mps == d;
+    const bool fast = is_mps & ((a1 & 0x8000) != 0);   // MPS without renormalisation
+    const bool x = is_mps ^ (a1 < qe);
+    const uint32_t nst = is_mps ? (((e >> 16) & 0x3f) | (mps << 6)) : (((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6));
+    const bool upd = en & !fast;
+    q.c += (en & x) ? qe : 0u;
+    q.a = vsel_e(en, x ? a1 : qe, q.a);
+    word = (word & ~(0xffu << shb)) | (nst << shb);
+    const uint32_t wu = upd ? wi : 7u;
+    cw.w0 = vsel_e(wu == 0, word, cw.w0); cw.w1 = vsel_e(wu == 1, word, cw.w1);
+    cw.w2 = vsel_e(wu == 2, word, cw.w2); cw.w3 = vsel_e(wu == 3, word, cw.w3);
+    cw.w4 = vsel_e(wu == 4, word, cw.w4);
+    uint32_t n = upd ? __clz(q.a) - 16 : 0u;
+    uint32_t k = min(n, q.ct);
+    q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
+    mql_byteout_sel(q, q.ct == 0);
+    k = min(n, q.ct);
+    q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
+    mql_byteout_sel(q, q.ct == 0);
+    while (__any(n != 0)) {
+        k = min(n, q.ct);
+        q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
+        mql_byteout_if(q, k != 0 && q.ct == 0);
+    }
+}
+
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t j) {
     const uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
     return (w >> (8 * (j & 3))) & 0xff;
@@ -481,7 +544,7 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
         for (uint32_t j = 0; j < 16; ++j) {
             const uint32_t i = base + j;
             const bool en = i < nsym;
-            mq_code(q, cw, tab, byte_of(cur4, j), en);
+            mq_code2(q, cw, tab, byte_of(cur4, j), en);
             // the prefetch two chunks ahead is issued after the first symbol has consumed this
             // chunk's bytes, so the wait for them does not also wait for the prefetch
             if (j == 0) {
