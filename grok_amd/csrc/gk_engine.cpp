@@ -19,6 +19,7 @@
 #include <memory>
 #include <string>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -564,13 +565,47 @@ struct ByteSrc {
     }
     uint32_t be16(size_t i) { return ((uint32_t)at(i) << 8) | at(i + 1); }
     uint32_t be32(size_t i) { return (be16(i) << 16) | be16(i + 2); }
+    // contiguous bytes [lo, hi) around i, for readers that scan forward (packet headers)
+    const uint8_t* span(size_t i, size_t& lo, size_t& hi) {
+        if (host) { lo = 0; hi = len; return host; }
+        if (!regp->empty()) {
+            uint8_t v;
+            if (from_region(i, v)) {
+                const Region& R = (*regp)[last_reg];
+                lo = R.start; hi = R.start + R.len; return R.p;
+            }
+        }
+        const size_t pg = i / PG;
+        if (pg != last_pg) { last = page(pg); last_pg = pg; }
+        lo = pg * PG; hi = std::min(len, lo + PG);
+        return last;
+    }
 };
+// Packet-header bit reader (T2Decompress / BitIO: a byte after 0xFF carries 7 bits).  Bytes
+// come from a cached contiguous span of the source; bits are taken several at a time.
 struct BitReader {
     ByteSrc& s; size_t off; size_t end; uint32_t buf = 0; int ct = 0;
+    const uint8_t* wp = nullptr; size_t wlo = 0, whi = 0;   // empty window
     BitReader(ByteSrc& src, size_t o, size_t e) : s(src), off(o), end(e) {}
-    inline void bytein() { ct = (buf == 0xff) ? 7 : 8; buf = off < end ? s.at(off) : 0; ++off; }
+    inline uint8_t byte_at(size_t i) {
+        if (i - wlo >= whi - wlo) {
+            if (i >= s.len) return 0;
+            wp = s.span(i, wlo, whi);
+        }
+        return wp[i - wlo];
+    }
+    inline void bytein() { ct = (buf == 0xff) ? 7 : 8; buf = off < end ? byte_at(off) : 0; ++off; }
     inline uint32_t getbit() { if (ct == 0) bytein(); --ct; return (buf >> ct) & 1; }
-    inline uint32_t read(int n) { uint32_t v = 0; for (int i = n - 1; i >= 0; --i) v |= getbit() << i; return v; }
+    inline uint32_t read(int n) {
+        uint32_t v = 0;
+        while (n > 0) {
+            if (ct == 0) bytein();
+            const int k = n < ct ? n : ct;
+            v = (v << k) | ((buf >> (ct - k)) & ((1u << k) - 1));
+            ct -= k; n -= k;
+        }
+        return v;
+    }
     void align() { if (buf == 0xff) bytein(); ct = 0; }
     uint32_t numpasses() {
         if (!read(1)) return 1;
@@ -1249,28 +1284,57 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         uint64_t psot = 0;
     };
     std::vector<TileOut> tout(te - tb);
+    const bool par_chains = te - tb == 1;   // one tile: its precinct chains run in parallel instead
     auto build_tile_part = [&](uint32_t t, TileOut& O) {
         const TileG& T = P.tiles[t];
-        std::vector<uint32_t> body;
-        std::vector<uint8_t> hb;
-        for (uint32_t l = 0; l < P.p.nlayers; ++l)
-            for (uint32_t r = 0; r < P.p.numres; ++r)
-                for (uint32_t c = 0; c < P.nc; ++c) {
-                    const ResG& R = T.comps[c].res[r];
-                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                        body.clear();
-                        T2.write_packet(R, pi, l, nullptr, &body, hb);
-                        Pk k{(uint32_t)O.phdr.size(), (uint32_t)hb.size(), (uint32_t)O.bsegs.size(), 0, (uint32_t)hb.size()};
-                        O.phdr.insert(O.phdr.end(), hb.begin(), hb.end());
-                        for (size_t q = 0; q < body.size(); q += 3) {
-                            if (!body[q + 2]) continue;
-                            O.bsegs.push_back(body[q]); O.bsegs.push_back(body[q + 1]); O.bsegs.push_back(body[q + 2]);
-                            k.len += body[q + 2];
-                        }
-                        k.s1 = (uint32_t)O.bsegs.size();
-                        O.pk.push_back(k);
-                    }
+        // A (resolution, component, precinct) chain owns its code-blocks and tag trees, so chains
+        // are independent; within a chain the layers are sequential (T2 state carries over).
+        struct Chain { uint32_t r, c, pi; };
+        std::vector<Chain> chains;
+        for (uint32_t r = 0; r < P.p.numres; ++r)
+            for (uint32_t c = 0; c < P.nc; ++c)
+                for (uint32_t pi = 0; pi < T.comps[c].res[r].pw * T.comps[c].res[r].ph; ++pi) chains.push_back({r, c, pi});
+        const uint32_t L = P.p.nlayers;
+        std::vector<TileOut> co(chains.size());   // per chain: headers, body segments, one Pk per layer
+        auto run_chain = [&](size_t q) {
+            const Chain& ch = chains[q];
+            const ResG& R = T.comps[ch.c].res[ch.r];
+            TileOut& C = co[q];
+            std::vector<uint32_t> body;
+            std::vector<uint8_t> hb;
+            for (uint32_t l = 0; l < L; ++l) {
+                body.clear();
+                T2.write_packet(R, ch.pi, l, nullptr, &body, hb);
+                Pk k{(uint32_t)C.phdr.size(), (uint32_t)hb.size(), (uint32_t)C.bsegs.size(), 0, (uint32_t)hb.size()};
+                C.phdr.insert(C.phdr.end(), hb.begin(), hb.end());
+                for (size_t i = 0; i < body.size(); i += 3) {
+                    if (!body[i + 2]) continue;
+                    C.bsegs.push_back(body[i]); C.bsegs.push_back(body[i + 1]); C.bsegs.push_back(body[i + 2]);
+                    k.len += body[i + 2];
                 }
+                k.s1 = (uint32_t)C.bsegs.size();
+                C.pk.push_back(k);
+            }
+        };
+        if (par_chains && chains.size() > 1) {
+            // largest chains (highest resolutions) first for the dynamic schedule
+            std::vector<size_t> ord(chains.size());
+            for (size_t i = 0; i < ord.size(); ++i) ord[i] = ord.size() - 1 - i;
+            host_pool().run(ord.size(), [&](size_t i) { run_chain(ord[i]); });
+        } else {
+            for (size_t q = 0; q < chains.size(); ++q) run_chain(q);
+        }
+        // LRCP order: layer, then chains in (resolution, component, precinct) order
+        for (uint32_t l = 0; l < L; ++l)
+            for (size_t q = 0; q < chains.size(); ++q) {
+                const TileOut& C = co[q];
+                Pk k = C.pk[l];
+                const uint32_t h0 = (uint32_t)O.phdr.size(), s0 = (uint32_t)O.bsegs.size();
+                O.phdr.insert(O.phdr.end(), C.phdr.begin() + k.hoff, C.phdr.begin() + k.hoff + k.hlen);
+                O.bsegs.insert(O.bsegs.end(), C.bsegs.begin() + k.s0, C.bsegs.begin() + k.s1);
+                k.hoff = h0; k.s1 = s0 + (k.s1 - k.s0); k.s0 = s0;
+                O.pk.push_back(k);
+            }
         // tile part: SOT [PLT] SOD (CodeStreamCompress::writeTilePart :862-900)
         std::vector<uint8_t>& tp = O.tp;
         put16(tp, 0xff90); put16(tp, 10); put16(tp, t); put32(tp, 0); tp.push_back(0); tp.push_back(1);
@@ -1291,7 +1355,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         tp[6] = (uint8_t)(psot >> 24); tp[7] = (uint8_t)(psot >> 16); tp[8] = (uint8_t)(psot >> 8); tp[9] = (uint8_t)psot;
         O.psot = psot;
     };
-    host_pool().run(te - tb, [&](size_t q) { build_tile_part(tb + (uint32_t)q, tout[q]); });
+    if (par_chains) build_tile_part(tb, tout[0]);   // (its chains use the pool: no nested pool call)
+    else host_pool().run(te - tb, [&](size_t q) { build_tile_part(tb + (uint32_t)q, tout[q]); });
     for (uint32_t t = tb; t < te; ++t) {
         TileOut& O = tout[t - tb];
         const uint64_t psot = O.psot;
@@ -1556,6 +1621,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         const uint32_t* strides, int out_on_device, const uint32_t* win = nullptr) {
     hipStream_t st = ctx->st;
     HIPCHK(hipEventRecord(ctx->ev[0], st));
+    // GK_PROFILE=1: host phase times of the decode (stderr)
+    static const bool prof = getenv("GK_PROFILE") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto h0 = now();
     ByteSrc S;
     S.len = len; S.st = st;
     if (cs_on_device) S.dev = cs; else S.host = cs;
@@ -1582,7 +1654,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     }
     const uint32_t nb = (uint32_t)P.blocks.size();
     std::vector<GkBlock> blk = P.blocks;
-    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> chunks(nb);
+    // code-block segments in stream order, one list per tile part (parts parse in parallel)
+    struct Chunk { uint64_t pos; uint32_t b, len; };
+    std::vector<std::vector<Chunk>> part_chunks(Hd.parts.size());
     std::vector<uint8_t> included(nb, 0);
     std::vector<uint32_t> numlenbits(nb, 0);
     for (auto& G : blk) { G.npasses = 0; G.numbps = 0; G.len = 0; }
@@ -1607,7 +1681,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         if (TPt.tile >= P.tiles.size()) throw GkError("corrupt SOT (tile index)");
         if (seen[TPt.tile]++) throw GkError("multiple tile parts per tile not supported");
     }
-    auto t2_part = [&](const TilePart& TPt, ByteSrc& BS) {
+    auto t2_part = [&](const TilePart& TPt, ByteSrc& BS, std::vector<Chunk>& chunks) {
         struct Trees { DecTree incl, imsb; };
         std::vector<Trees> trees;
         std::unordered_map<uint32_t, size_t> tidx;   // trees by first_block of each precinct-band
@@ -1641,9 +1715,12 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                     else inc = br.read(1);
                                     if (!inc) continue;
                                     if (!included[b]) {
-                                        uint32_t kmsbs = 0, v = T.imsb.decode(br, k, kmsbs);
-                                        while (v >= kmsbs) { ++kmsbs; if (kmsbs > 64) break; v = T.imsb.decode(br, k, kmsbs); }
-                                        kmsbs--;
+                                        // zero bit-planes: Grok raises the threshold one plane at a time
+                                        // until the leaf is known; a tag tree reads a node's bits only
+                                        // once its parent is known, so one walk with threshold 64 reads
+                                        // exactly the same bits
+                                        const uint32_t v = T.imsb.decode(br, k, 64);
+                                        const uint32_t kmsbs = v < 64 ? v : 64;
                                         uint32_t bnb = R.bands[bi].numbps;
                                         blk[b].numbps = kmsbs > bnb ? 0 : bnb - kmsbs;
                                         numlenbits[b] = 3;
@@ -1663,20 +1740,23 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         pos = br.off;
                         for (auto& ct : contrib) {
                             uint32_t n = (uint32_t)std::min<size_t>(ct.second, tile_end > pos ? tile_end - pos : 0);
-                            if (n) chunks[ct.first].push_back({pos, n});
+                            if (n) chunks.push_back({pos, ct.first, n});
                             pos += ct.second;
                         }
                     }
                 }
     };
+    const auto h1 = now();
     if (Hd.parts.size() == 1) {
-        t2_part(Hd.parts[0], S);
+        part_chunks[0].reserve(nb);
+        t2_part(Hd.parts[0], S, part_chunks[0]);
     } else {
         host_pool().run(Hd.parts.size(), [&](size_t q) {
             ByteSrc BS = S.fork();   // per-call cursor caches (batched regions are shared read-only)
-            t2_part(Hd.parts[q], BS);
+            t2_part(Hd.parts[q], BS, part_chunks[q]);
         });
     }
+    const auto h2 = now();
     // decode only the rectangle of tiles that are present (sharded / windowed decode)
     uint32_t ib = P.ntx, ie = 0, jb = P.nty, je = 0;
     for (uint32_t t = 0; t < P.tiles.size(); ++t)
@@ -1712,16 +1792,30 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // gather every selected block's segments into a 16-byte aligned slot with >= 16 bytes of
     // slack (the T1 decoders read their bytes through aligned windows)
     std::vector<uint64_t> seg;
-    seg.reserve(3 * (size_t)nbr);
     uint64_t o = 0, t1_bytes = 0;
-    for (uint32_t b : sel) {
-        blk[b].data_off = o;
-        uint32_t L = 0;
-        for (auto& ch : chunks[b]) { seg.push_back(ch.first); seg.push_back(o + L); seg.push_back(ch.second); L += ch.second; }
-        blk[b].len = L;
-        t1_bytes += L;
-        if (!L) blk[b].npasses = 0;
-        o += ((uint64_t)L + 16 + 15) & ~15ull;
+    {
+        size_t nch = 0;
+        for (auto& pc : part_chunks) {
+            nch += pc.size();
+            for (const Chunk& ch : pc) blk[ch.b].len += ch.len;
+        }
+        for (uint32_t b : sel) {
+            blk[b].data_off = o;
+            const uint32_t L = blk[b].len;
+            t1_bytes += L;
+            if (!L) blk[b].npasses = 0;
+            o += ((uint64_t)L + 16 + 15) & ~15ull;
+            blk[b].len = 0;   // reused as the fill cursor below
+        }
+        seg.resize(3 * nch);
+        size_t k = 0;
+        for (auto& pc : part_chunks)
+            for (const Chunk& ch : pc) {   // stream order = layer order within a block
+                GkBlock& G = blk[ch.b];
+                seg[k] = ch.pos; seg[k + 1] = G.data_off + G.len; seg[k + 2] = ch.len;
+                G.len += ch.len;
+                k += 3;
+            }
     }
     uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 256);   // decoder window loads read up to 48 B past a block
     if (!seg.empty()) {
@@ -1732,6 +1826,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         gk_launch_gather(st, dcs, stg, ds, (uint32_t)(seg.size() / 3));
     }
     const uint8_t* src_bytes = stg;
+    if (prof)
+        fprintf(stderr, "decode host: headers+setup %.3f ms, packet headers %.3f ms, segments %.3f ms (%zu parts)\n",
+                ms(h0, h1), ms(h1, h2), ms(h2, now()), Hd.parts.size());
     GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * std::max(nb, 1u));
     GkBlock* hblk = (GkBlock*)ctx->hinfo.get(sizeof(GkBlock) * std::max(nb, 1u));
     memcpy(hblk, blk.data(), sizeof(GkBlock) * nb);

@@ -535,6 +535,14 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
         }
     };
     close_passes(0);   // passes without symbols before the first one
+    // earliest pass end of the wave (uniform), so the per-symbol test is one scalar compare
+    auto wave_next_end = [&]() -> uint32_t {
+        uint32_t m = (npasses && p < npasses) ? next_end : 0xffffffffu;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+        return __builtin_amdgcn_readfirstlane(m);
+    };
+    uint32_t wnext = wave_next_end();
     uint4 cur4 = make_uint4(0, 0, 0, 0), nxt4 = make_uint4(0, 0, 0, 0);
     if (nsym) cur4 = *(const uint4*)(sp);
     if (nsym > 16) nxt4 = *(const uint4*)(sp + 16);
@@ -552,7 +560,7 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
                 if (base + 32 < nsym) pre = *(const uint4*)(sp + base + 32);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            close_passes(i + 1);
+            if (i + 1 == wnext) { close_passes(i + 1); wnext = wave_next_end(); }
         }
         cur4 = nxt4; nxt4 = pre;
     }
