@@ -405,17 +405,15 @@ __device__ __forceinline__ void mql_byteout_sel(MqLane& q, bool en) {
     const uint32_t cur = q.cur + carry;
     const uint32_t c = q.c & ~(carry << 27);
     const bool ff = cur == 0xff;
-    const uint32_t nb = ff ? (c >> 20) : (c >> 19);
-    // emit `cur` at bp (bp = -1 is the encoder's dummy byte before the buffer)
-    const bool inb = (q.bp >= 0) & ((uint32_t)q.bp < q.cap);
-    const bool put = en & inb;
+    // emit `cur` at bp; bp = -1 is the encoder's dummy byte before the buffer, which the one
+    // unsigned compare also excludes (overflow past `cap` is detected from the final bp)
+    const bool put = en & ((uint32_t)q.bp < q.cap);
     const uint32_t wb = q.wbuf | (put ? cur << (8 * (q.bp & 3)) : 0u);
     const bool full = put & ((q.bp & 3) == 3);
     if (full) *(uint32_t*)(q.out + (q.bp - 3)) = wb;
-    q.wbuf = vsel_e(en, full ? 0u : wb, q.wbuf);
-    q.ovf |= (en & (q.bp >= 0) & !inb) ? 1u : 0u;
+    q.wbuf = full ? 0u : wb;
     q.bp += en ? 1 : 0;
-    q.cur = vsel_e(en, nb & 0xff, q.cur);
+    q.cur = vsel_e(en, (ff ? (c >> 20) : (c >> 19)) & 0xff, q.cur);
     q.c = vsel_e(en, c & (ff ? 0xfffffu : 0x7ffffu), q.c);
     q.ct = vsel_e(en, ff ? 7u : 8u, q.ct);
 }
@@ -450,9 +448,11 @@ __device__ __forceinline__ void mq_code2(MqLane& q, Ctx5e& cw, const uint32_t* t
     uint32_t k = min(n, q.ct);
     q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
     mql_byteout_sel(q, q.ct == 0);
-    k = min(n, q.ct);
-    q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
-    mql_byteout_sel(q, q.ct == 0);
+    if (__any(n != 0)) {   // a second byte boundary in this renormalisation (large shifts)
+        k = min(n, q.ct);
+        q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
+        mql_byteout_sel(q, q.ct == 0);
+    }
     while (__any(n != 0)) {
         k = min(n, q.ct);
         q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
     info[4 * b + 1] = npasses;
     info[4 * b + 2] = P[npasses - 1].rate;
     info[4 * b + 3] = poff;
-    if (q.ovf) atomicOr(err, 1);
+    if (q.ovf || (q.bp > 0 && (uint32_t)q.bp > q.cap)) atomicOr(err, 1);
 #undef pe_lds_at
 }
 
