@@ -855,6 +855,9 @@ __device__ __forceinline__ uint64_t h_get(uint32_t (*g)[64], int row, int lane) 
     return ((uint64_t)g[row * 2 + 1][lane] << 32) | g[row * 2][lane];
 }
 
+// TIMING (diagnostic build, GK_T1_STATS=2): shader-clock cycles spent in stripe-boundary
+// events vs decision steps, summed into stats[4] / stats[5].
+template <bool TIMING>
 __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ bytes, const GkBlock* __restrict__ blocks,
                                                 const uint32_t* __restrict__ order, uint64_t* __restrict__ scratch,
                                                 const uint64_t* __restrict__ wave_off, uint32_t nblocks,
@@ -881,6 +884,7 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
     for (int i = 0; i < 8; ++i) { Ls.mu[i][lane] = 0; Ls.bt[i][lane] = 0; }
     Ctx5 cw = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};   // mqc_resetstates: ZC0=4, AGG=3, UNI=46
     uint32_t nstep = 0, nsym = 0, nevents = 0;
+    unsigned long long cyc_ev = 0, cyc_step = 0;
     Mq2 q;
     q.p = npasses ? bytes + B.data_off : bytes;
     q.len = npasses ? B.len : 0;
@@ -925,8 +929,10 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         // ---------------- stripe boundary for parked lanes (batched)
         const uint32_t nparked = __popcll(__ballot(parked));
         const uint32_t nactive = __popcll(__ballot(!done && !parked));
+        uint64_t tev = 0;
         if (nparked && (nparked >= kpark || nactive == 0)) {
             ++nevents;
+            if (TIMING) tev = __builtin_amdgcn_s_memtime();
             if (!done && q.sbase == q.fill && q.fill + 32 - q.bp <= 4 * RING_DW) {
                 ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3, q.len);
                 ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7, q.len);
@@ -1004,7 +1010,9 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
             next_pos3(k2, t2, s2, p2, ns);
             const bool pf = !done && p2 < npasses && k2 < numbps;
             load_rows(X, WS, WS + (WS_BITS + (size_t)(pf ? k2 : 0) * 64) * 64, lane, pf ? 4 * s2 : 0);
+            if (TIMING) { const uint64_t t1 = __builtin_amdgcn_s_memtime(); cyc_ev += t1 - tev; tev = t1; }
         }
+        if (TIMING && !tev) tev = __builtin_amdgcn_s_memtime();
         // ---------------- one decision per active lane
         const bool act = !done && !parked;
         ++nstep;
@@ -1093,12 +1101,14 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         r = vsel(pend & uni2, rr, r);
         ph = vsel(pend, nph, ph);
         q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+        if (TIMING) cyc_step += __builtin_amdgcn_s_memtime() - tev;
     }
     if (stats) {
         unsigned long long tot = nsym;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
         if (lane == 0) {
+            if (TIMING) { atomicAdd(&stats[4], cyc_ev); atomicAdd(&stats[5], cyc_step); }
             atomicAdd(&stats[3], (unsigned long long)nevents);
             atomicAdd(&stats[0], (unsigned long long)nstep); atomicAdd(&stats[1], tot);
             atomicMax(&stats[2], (unsigned long long)nstep);
@@ -1167,7 +1177,8 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
                       uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks) {
     if (!nblocks) return;
     static unsigned long long* stats = nullptr;
-    const bool want = getenv("GK_T1_STATS") != nullptr;
+    const char* sv = getenv("GK_T1_STATS");
+    const bool want = sv != nullptr, timing = sv && atoi(sv) == 2;
     if (want && !stats) { (void)hipMalloc(&stats, 64); }
     if (want) (void)hipMemsetAsync(stats, 0, 64, st);
     static int variant = -1, kpark = 4;
@@ -1180,19 +1191,26 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     if (variant == 0)
         hipLaunchKernelGGL(k_t1_dec, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, want ? stats : nullptr);
+    else if (variant == 2 && timing)
+        hipLaunchKernelGGL(k_t1_dec2<true>, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
+                           wave_off, nblocks, stats, (uint32_t)kpark);
     else if (variant == 2)
-        hipLaunchKernelGGL(k_t1_dec2, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
+        hipLaunchKernelGGL(k_t1_dec2<false>, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
     else
         hipLaunchKernelGGL(k_t1_dec_ind, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
     if (want) {
-        unsigned long long h[4];
-        (void)hipMemcpyAsync(h, stats, 32, hipMemcpyDeviceToHost, st);
+        unsigned long long h[8];
+        (void)hipMemcpyAsync(h, stats, 64, hipMemcpyDeviceToHost, st);
         (void)hipStreamSynchronize(st);
         fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f events/wave %.0f\n",
                 (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]),
                 (double)h[3] / ((nblocks + 63) / 64));
+        if (timing)
+            fprintf(stderr, "t1dec timing: cycles/event %.0f cycles/step %.0f (event share %.3f)\n",
+                    (double)h[4] / (double)(h[3] ? h[3] : 1), (double)h[5] / (double)(h[0] ? h[0] : 1),
+                    (double)h[4] / (double)(h[4] + h[5] ? h[4] + h[5] : 1));
     }
 }
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
