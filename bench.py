@@ -282,12 +282,12 @@ def main():
 
     if rank == 0:
         # dominant kernel: the T1 stage with the largest average duration, measured with HIP
-        # events on the engine stream (encode: k_t1_cm + k_t1_mq, decode: k_t1_dec + k_t1_recon)
+        # events on the engine stream (encode: k_t1_cm + k_t1_mq, decode: k_t1_dec2 + k_t1_recon)
         stages = {
-            "T1 decode (k_t1_dec + k_t1_recon)": (m["dec_t1_ms"], m["dec_t1_bytes"] + 4.0 * samples,
-                                                  ["k_t1_dec", "k_t1_recon"]),
+            "T1 decode (k_t1_dec2 + k_t1_recon)": (m["dec_t1_ms"], m["dec_t1_bytes"] + 4.0 * samples,
+                                                   ["void k_t1_dec2<false>", "k_t1_recon"]),
             "T1 encode (k_t1_cm + k_t1_mq)": (m["enc_t1_ms"], 4.0 * samples + m["enc_t1_bytes"],
-                                              ["k_t1_cm", "k_t1_mq"]),
+                                              ["void k_t1_cm<false>", "k_t1_mq"]),
             "DWT 5/3 fwd+inv (all levels)": (m["enc_dwt_ms"] + m["dec_dwt_ms"], m["enc_dwt_bytes"] + m["dec_dwt_bytes"],
                                              ["k_dwt53_fwd_level", "k_dwt53_inv_level"]),
         }

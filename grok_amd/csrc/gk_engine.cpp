@@ -1893,6 +1893,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         const uint32_t* dids = dpos + nbr;
         const uint64_t* dwo = (const uint64_t*)(dids + nbr + 2);
         uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
+        HIPCHK(hipMemsetAsync(dscr, 0, 8 * hwo[nw], st));   // decoder state rows start at zero
         gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nslots);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr);
