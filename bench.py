@@ -137,6 +137,36 @@ class Runner:
         return None
 
 
+class BatchRunner:
+    """`nimg` images in flight on one GPU: each has its own engine (own HIP stream and
+    buffers) and is driven from its own host thread, so one image's host T2 and
+    chain-bound T1 kernels overlap with the other's (ctypes releases the GIL).  One
+    step = every image encoded and decoded once.  Image i uses seed cfg.seed + rank
+    + 1000 * i (same generator, same statistics)."""
+
+    def __init__(self, name, nimg, rank, device):
+        from concurrent.futures import ThreadPoolExecutor
+        self.rs = [Runner(name, 0, rank + 1000 * i, device) for i in range(nimg)]
+        self.size, self.cfg, self.name = self.rs[0].size, self.rs[0].cfg, name
+        self.n = self.rs[0].n
+        self.pool = ThreadPoolExecutor(nimg)
+
+    def step(self):
+        res = [f.result() for f in [self.pool.submit(r.step) for r in self.rs]]
+        self.n = self.rs[0].n
+        return res[0]
+
+    def check(self):
+        for r in self.rs:
+            r.check()
+        self.n = self.rs[0].n
+
+    def close(self):
+        self.pool.shutdown()
+        for r in self.rs:
+            r.eng.close()
+
+
 class ShardRunner:
     """C4 on N ranks: tile rows split across ranks (grok_amd/shard.py).  One step =
     every rank encodes its tiles from its slab (HBM -> tile parts in HBM), rank 0
@@ -265,6 +295,19 @@ def main():
                      "stages_ms": {k: round(v, 3) for k, v in m3.items() if k.endswith("_ms") and v > 0}}
         r3.eng.close()
         del r3
+        torch.cuda.empty_cache()
+        # C2 with two images in flight per GPU (throughput of overlapped independent jobs)
+        rb = BatchRunner("C2", 2, rank, device)
+        rb.check()
+        elb, mb = timed(rb, 3, 1, world, dist, device)
+        Sb = rb.size
+        aux["C2_batch2"] = {"config": "C2 with 2 images in flight per GPU (2 engines / HIP streams, one host thread "
+                                      "each); one step = 2 images encoded + decoded",
+                            "value": round(2 * Sb * Sb / 1e6 * world * 3 / elb, 3), "unit": "Mpixels/s",
+                            "ms_per_step": round(elb * 1000.0 / 3, 3), "images_per_step": 2,
+                            "parallelism": "replicas x%d" % world}
+        rb.close()
+        del rb
         torch.cuda.empty_cache()
         r4 = ShardRunner("C4", 0, rank, world, device, dist) if world > 1 else Runner("C4", 0, rank, device)
         r4.check()

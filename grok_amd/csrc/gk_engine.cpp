@@ -58,6 +58,7 @@ class HostPool {
     uint64_t gen_ = 0;
     bool stop_ = false;
     std::string err_;
+    std::mutex run_m_;
     void drain(const std::function<void(size_t)>& f, size_t n) {
         for (;;) {
             const size_t i = next_.fetch_add(1);
@@ -93,9 +94,12 @@ public:
         for (auto& t : th_) t.join();
     }
     unsigned size() const { return (unsigned)th_.size() + 1; }
+    // One job at a time: a caller that finds the pool busy (another engine context on
+    // another host thread) runs its items inline.
     void run(size_t n, const std::function<void(size_t)>& f) {
         if (n == 0) return;
-        if (n == 1 || th_.empty()) { for (size_t i = 0; i < n; ++i) f(i); return; }
+        std::unique_lock<std::mutex> own(run_m_, std::try_to_lock);
+        if (n == 1 || th_.empty() || !own.owns_lock()) { for (size_t i = 0; i < n; ++i) f(i); return; }
         {
             std::lock_guard<std::mutex> lk(m_);
             job_ = &f; n_ = n; next_ = 0; busy_ = (int)th_.size(); ++gen_; err_.clear();
