@@ -104,7 +104,6 @@ template <class Q> __device__ __forceinline__ void ring_topup(uint32_t (*ring)[6
     }
 }
 
-struct Ctx5 { uint32_t w0, w1, w2, w3, w4; };   // one byte per context: state | mps << 6
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint64_t dil3(uint64_t u, uint64_t m, uint64_t d) {
@@ -169,28 +168,29 @@ __device__ __forceinline__ void mq2_refill(Mq2& q, bool en) {
 }
 
 // DECODE (Annex C.3.2) for context cx, predicated on `en`; needs avail >= 15.
-__device__ __forceinline__ uint32_t mq2_decode(Mq2& q, Ctx5& cw, const uint32_t* tab, uint32_t cx, bool en) {
-    const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
-    uint32_t word = vsel(wi == 4, cw.w4, vsel(wi & 2, vsel(wi & 1, cw.w3, cw.w2), vsel(wi & 1, cw.w1, cw.w0)));
-    const uint32_t st = (word >> shb) & 0xff;
-    const uint32_t mps = st >> 6;
-    const uint32_t e = tab[st & 63];
+// DECODE (Annex C.3.2) for context cx, predicated on `en`; needs avail >= 15.
+// Context states live in LDS per lane as their probability-table entry
+// (Qe | NMPS << 16 | NLPS << 22 | SWITCH << 28) with the MPS in bit 31, so one read
+// yields everything the decision needs; the new state's entry is looked up and
+// written back off the decision's dependency chain.
+__device__ __forceinline__ uint32_t mq2_decode(Mq2& q, uint32_t (*ctx)[64], int lane, const uint32_t* tab,
+                                               uint32_t cx, bool en) {
+    const uint32_t e = ctx[cx][lane];
+    const uint32_t mps = e >> 31;
     const uint32_t qe = e & 0xffff;
     const uint32_t chi = (uint32_t)(q.c >> 32);
     const uint32_t a1 = q.a - qe;
     const bool lower = (chi >> 16) < qe;
-    const bool fast = !lower && (a1 & 0x8000);
-    const bool mps_path = lower ? (a1 < qe) : (a1 >= qe);
-    const uint32_t d = (fast || mps_path) ? mps : (mps ^ 1);
-    const uint32_t nst = mps_path ? (((e >> 16) & 0x3f) | (mps << 6)) : (((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6));
-    const bool upd = en && !fast;
+    const bool fast = !lower & ((a1 & 0x8000) != 0);
+    const bool mps_path = lower ^ (a1 >= qe);                // exchange rule
+    const uint32_t d = (fast | mps_path) ? mps : (mps ^ 1);
+    const uint32_t nidx = mps_path ? ((e >> 16) & 0x3f) : ((e >> 22) & 0x3f);
+    const uint32_t nmps = mps_path ? mps : (mps ^ ((e >> 28) & 1));
+    const bool upd = en & !fast;
     const uint32_t an = en ? (lower ? qe : a1) : q.a;
-    const uint32_t ch = (en && !lower) ? chi - (qe << 16) : chi;
-    word = (word & ~(0xffu << shb)) | (nst << shb);
-    const uint32_t wu = upd ? wi : 7u;
-    cw.w0 = vsel(wu == 0, word, cw.w0); cw.w1 = vsel(wu == 1, word, cw.w1);
-    cw.w2 = vsel(wu == 2, word, cw.w2); cw.w3 = vsel(wu == 3, word, cw.w3);
-    cw.w4 = vsel(wu == 4, word, cw.w4);
+    const uint32_t ch = (en & !lower) ? chi - (qe << 16) : chi;
+    const uint32_t ne = tab[nidx] | (nmps << 31);
+    if (upd) ctx[cx][lane] = ne;
     const uint32_t n = upd ? __clz(an) - 16 : 0u;   // RENORMD: all shifts at once
     q.a = an << n;
     q.c = (((uint64_t)ch << 32) | (uint32_t)q.c) << n;
@@ -200,6 +200,7 @@ __device__ __forceinline__ uint32_t mq2_decode(Mq2& q, Ctx5& cw, const uint32_t*
 
 struct Dec2Lds {
     uint32_t tab[48];
+    uint32_t ctx[19][64];            // per-lane context states as table entries (| MPS << 31)
     uint8_t zc[4][512];
     uint8_t sc[256];                 // index bit0 N-neg 1 N-sig 2 W-neg 3 W-sig 4 E-neg 5 E-sig 6 S-neg 7 S-sig
     uint32_t ring[RING_DW + 1][64];
@@ -256,7 +257,9 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
     const uint8_t* zc = Ls.zc[B.orient & 3];
     for (int i = 0; i < 18; ++i) { Ls.sg[i][lane] = 0; Ls.ng[i][lane] = 0; }
     for (int i = 0; i < 8; ++i) { Ls.mu[i][lane] = 0; Ls.bt[i][lane] = 0; }
-    Ctx5 cw = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};   // mqc_resetstates: ZC0=4, AGG=3, UNI=46
+    // mqc_resetstates (mqc_dec.cpp:121-130): every context at state 0 except ZC0 = 4, AGG = 3, UNI = 46
+    for (int c = 0; c < 19; ++c)
+        Ls.ctx[c][lane] = c_mq[c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))];
     uint32_t nstep = 0, nsym = 0, nevents = 0;
     unsigned long long cyc_ev = 0, cyc_step = 0;
     Mq2 q;
@@ -433,7 +436,7 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
             mq2_refill(q, pend && q.avail < 16);
             q.nb4 = ring_get4(Ls.ring, lane, q.bp);
         }
-        const uint32_t d = mq2_decode(q, cw, Ls.tab, cx, pend);
+        const uint32_t d = mq2_decode(q, Ls.ctx, lane, Ls.tab, cx, pend);
         nsym += pend ? 1 : 0;
         // ---- state updates
         const bool sig = pend && !is_mr && ph == PH_SIGN;
