@@ -1793,8 +1793,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipMemcpyAsync(d, cs, len, hipMemcpyHostToDevice, st));
         dcs = d;
     }
-    // gather every selected block's segments into a 16-byte aligned slot with >= 16 bytes of
-    // slack (the T1 decoders read their bytes through aligned windows)
+    // gather every selected block's segments into a 16-byte aligned slot followed by >= 32
+    // bytes of 0xFF (the T1 decoders read their bytes through aligned windows; the Part-1
+    // decoder takes the padding as the MQ end-of-data bytes)
     std::vector<uint64_t> seg;
     uint64_t o = 0, t1_bytes = 0;
     {
@@ -1808,7 +1809,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             const uint32_t L = blk[b].len;
             t1_bytes += L;
             if (!L) blk[b].npasses = 0;
-            o += ((uint64_t)L + 16 + 15) & ~15ull;
+            o += (((uint64_t)L + 15) & ~15ull) + 32;
             blk[b].len = 0;   // reused as the fill cursor below
         }
         seg.resize(3 * nch);
@@ -1822,6 +1823,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             }
     }
     uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 256);   // decoder window loads read up to 48 B past a block
+    if (!P.p.ht()) HIPCHK(hipMemsetAsync(stg, 0xff, o, st));
     if (!seg.empty()) {
         uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8 + 8);
         memcpy(hs, seg.data(), seg.size() * 8);
@@ -1886,7 +1888,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 uint32_t mp = 0;
                 for (uint32_t i = wv * 64; i < wv * 64 + L; ++i)
                     if (hord[i] != 0xffffffffu) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
-                wo += (260 + (uint64_t)mp * 64) * 64;
+                wo += (262 + (uint64_t)mp * 64) * 64;   // per-lane slab: WS_FIXED + planes (gk_t1dec.hip)
             }
             hwo[nw] = wo;
         }

@@ -39,12 +39,13 @@
 #include <cstdlib>
 
 // per-lane scratch (uint64 words, one contiguous slab per lane): field F row r at F + r
-#define WS_SIG 0      // 66 rows (row y at y + 1, guards 0 and 65)
-#define WS_NEG 66     // 66 rows
-#define WS_MU 132     // 64 rows: refined in an earlier plane
-#define WS_PI 196     // 64 rows: visited in the current plane
-#define WS_BITS 260   // numbps planes x 64 rows: bit of the plane (plane 0 = most significant)
-#define WS_FIXED 260
+// (offsets chosen so every stripe's first row is 16-byte aligned: rows move in pairs)
+#define WS_SIG 1      // 66 rows (row y at y + 1, guards 0 and 65)
+#define WS_NEG 67     // 66 rows
+#define WS_MU 134     // 64 rows: refined in an earlier plane
+#define WS_PI 198     // 64 rows: visited in the current plane
+#define WS_BITS 262   // numbps planes x 64 rows: bit of the plane (plane 0 = most significant)
+#define WS_FIXED 262
 
 // ------------------------------------------------------------------ MQ byte ring
 // Compressed bytes reach the coder through a 128-byte per-lane ring in LDS
@@ -63,33 +64,34 @@ __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
     return r;
 }
 
-// bytes at or past the block length read as 0xFF (the MQ decoder's end-of-data rule,
-// mqc_dec.cpp BYTEIN), so the per-step byte fetch needs no length test
-__device__ __forceinline__ uint32_t ff_past(uint32_t v, uint32_t at, uint32_t len) {
-    const int k = (int)len - (int)at;
-    return k <= 0 ? 0xffffffffu : (k >= 4 ? v : (v | (0xffffffffu << (8 * k))));
+// Bytes at or past the block length read as 0xFF (the MQ decoder's end-of-data rule,
+// mqc_dec.cpp BYTEIN).  The host pads every staged block with >= 32 bytes of 0xFF after its
+// data, and windows that start at or past the length read this constant instead, so the
+// ring needs no per-byte length tests.
+__device__ uint4 g_ff32[2] = {{~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}};
+__device__ __forceinline__ const uint4* win(const uint8_t* p, uint32_t at, uint32_t len) {
+    return at < len ? (const uint4*)(p + at) : g_ff32;
 }
-__device__ __forceinline__ void ring_write16(uint32_t (*ring)[64], int lane, uint32_t pos, uint32_t a, uint32_t b,
-                                             uint32_t c, uint32_t d, uint32_t len) {
-    a = ff_past(a, pos, len); b = ff_past(b, pos + 4, len); c = ff_past(c, pos + 8, len); d = ff_past(d, pos + 12, len);
+__device__ __forceinline__ void ring_write16(uint32_t (*ring)[64], int lane, uint32_t pos, uint4 v) {
     const uint32_t j = (pos >> 2) & (RING_DW - 1);
-    ring[j][lane] = a; ring[j + 1][lane] = b; ring[j + 2][lane] = c; ring[j + 3][lane] = d;
-    if (j == 0) ring[RING_DW][lane] = a;   // mirror for wrap-around reads
+    ring[j][lane] = v.x; ring[j + 1][lane] = v.y; ring[j + 2][lane] = v.z; ring[j + 3][lane] = v.w;
+    if (j == 0) ring[RING_DW][lane] = v.x;   // mirror for wrap-around reads
 }
 __device__ __forceinline__ uint32_t ring_get4(uint32_t (*ring)[64], int lane, uint32_t bp) {
     const uint32_t j = (bp >> 2) & (RING_DW - 1);
     return __builtin_amdgcn_alignbyte(ring[j + 1][lane], ring[j][lane], bp & 3);
 }
+// the 32 staged bytes land in two register quads (no copies, so no wait after the issue)
 template <class Q> __device__ __forceinline__ void stage_load(Q& q) {
-    uint4 a = *(const uint4*)(q.p + q.sbase), b = *(const uint4*)(q.p + q.sbase + 16);
-    q.T0 = a.x; q.T1 = a.y; q.T2 = a.z; q.T3 = a.w; q.T4 = b.x; q.T5 = b.y; q.T6 = b.z; q.T7 = b.w;
+    const uint4* w = win(q.p, q.sbase, q.len);
+    q.Ta = w[0]; q.Tb = w[1];
 }
 // stripe-pass boundary: commit the staged 32 bytes when the ring has room, request the next 32
 template <class Q> __device__ __forceinline__ void ring_boundary(uint32_t (*ring)[64], int lane, Q& q) {
     if (q.sbase != q.fill) { q.sbase = q.fill; stage_load(q); }   // after a synchronous top-up
     if (q.fill + 32 - q.bp <= 4 * RING_DW) {
-        ring_write16(ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3, q.len);
-        ring_write16(ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7, q.len);
+        ring_write16(ring, lane, q.fill, q.Ta);
+        ring_write16(ring, lane, q.fill + 16, q.Tb);
         q.fill += 32;
         q.sbase = q.fill;
         stage_load(q);
@@ -98,8 +100,7 @@ template <class Q> __device__ __forceinline__ void ring_boundary(uint32_t (*ring
 // inside a step loop: synchronous top-up for a lane about to run dry
 template <class Q> __device__ __forceinline__ void ring_topup(uint32_t (*ring)[64], int lane, Q& q) {
     if (q.fill - q.bp < 8) {
-        uint4 a = *(const uint4*)(q.p + q.fill);
-        ring_write16(ring, lane, q.fill, a.x, a.y, a.z, a.w, q.len);
+        ring_write16(ring, lane, q.fill, *win(q.p, q.fill, q.len));
         q.fill += 16;
     }
 }
@@ -121,17 +122,22 @@ struct Rows22 {   // one stripe's rows: S1..S5 / N1..N5 (rows y0..y0+4), P/M/B (
     uint64_t s1, s2, s3, s4, s5, n1, n2, n3, n4, n5, p0, p1, p2, p3, m0, m1, m2, m3, b0, b1, b2, b3;
 };
 // rows of stripe y0 / plane `k` from the lane's scratch slab (consecutive words per field)
+__device__ __forceinline__ void ld2(const uint64_t* p, uint64_t& a, uint64_t& b) {   // 16-byte aligned pair
+    const ulonglong2 v = *(const ulonglong2*)p;
+    a = v.x; b = v.y;
+}
+__device__ __forceinline__ void st2(uint64_t* p, uint64_t a, uint64_t b) { *(ulonglong2*)p = make_ulonglong2(a, b); }
 __device__ __forceinline__ void load_rows(Rows22& R, const uint64_t* WS, uint32_t k, uint32_t y0) {
     const uint64_t* sg = WS + WS_SIG + y0 + 1;
     const uint64_t* ng = WS + WS_NEG + y0 + 1;
     const uint64_t* pi = WS + WS_PI + y0;
     const uint64_t* mu = WS + WS_MU + y0;
     const uint64_t* bt = WS + WS_BITS + (size_t)k * 64 + y0;
-    R.s1 = sg[0]; R.s2 = sg[1]; R.s3 = sg[2]; R.s4 = sg[3]; R.s5 = sg[4];
-    R.n1 = ng[0]; R.n2 = ng[1]; R.n3 = ng[2]; R.n4 = ng[3]; R.n5 = ng[4];
-    R.p0 = pi[0]; R.p1 = pi[1]; R.p2 = pi[2]; R.p3 = pi[3];
-    R.m0 = mu[0]; R.m1 = mu[1]; R.m2 = mu[2]; R.m3 = mu[3];
-    R.b0 = bt[0]; R.b1 = bt[1]; R.b2 = bt[2]; R.b3 = bt[3];
+    ld2(sg, R.s1, R.s2); ld2(sg + 2, R.s3, R.s4); R.s5 = sg[4];
+    ld2(ng, R.n1, R.n2); ld2(ng + 2, R.n3, R.n4); R.n5 = ng[4];
+    ld2(pi, R.p0, R.p1); ld2(pi + 2, R.p2, R.p3);
+    ld2(mu, R.m0, R.m1); ld2(mu + 2, R.m2, R.m3);
+    ld2(bt, R.b0, R.b1); ld2(bt + 2, R.b2, R.b3);
 }
 
 // next (plane, pass type, stripe) after (k, t, s); pass types 0 SP, 1 MR, 2 CL
@@ -148,7 +154,7 @@ struct Mq2 {
     uint32_t bp, len, fill;      // byte position (last byte taken in), block length, ring fill position
     uint32_t nb4;                // bytes [bp, bp + 4)
     uint32_t sbase;              // staged bytes cover [sbase, sbase + 32)
-    uint32_t T0, T1, T2, T3, T4, T5, T6, T7;
+    uint4 Ta, Tb;
     const uint8_t* p;
 };
 
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
     for (int c = 0; c < 19; ++c)
         Ls.ctx[c][lane] = c_mq[c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))];
     uint32_t nstep = 0, nsym = 0, nevents = 0;
-    unsigned long long cyc_ev = 0, cyc_step = 0;
+    unsigned long long cyc_ev = 0, cyc_step = 0, cyc_p[6] = {0, 0, 0, 0, 0, 0};
     Mq2 q;
     q.p = npasses ? bytes + B.data_off : bytes;
     q.len = npasses ? B.len : 0;
@@ -288,7 +294,6 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
     uint32_t vr = (1u << nr) - 1;                 // valid rows of the stripe
     uint64_t C0, C1, C2, C3, E, fresh = 0;        // candidates (consumed as coded), run-length columns
     uint64_t P0 = 0, P1 = 0, P2 = 0, P3 = 0;      // visited in SP of this plane
-    uint64_t M0 = 0, M1 = 0, M2 = 0, M3 = 0;      // refined rows after this stripe-pass
     {
         const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
                        v3 = nr > 3 ? colmask : 0;
@@ -310,12 +315,29 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         if (nparked && (nparked >= kpark || nactive == 0)) {
             ++nevents;
             if (TIMING) tev = __builtin_amdgcn_s_memtime();
+            // everything the previous event issued has long landed: one explicit wait here
+            // (seen by the compiler's counter model) keeps it from placing conservative waits
+            // behind this event's own loads and stores
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
             if (!done && q.sbase == q.fill && q.fill + 32 - q.bp <= 4 * RING_DW) {
-                ring_write16(Ls.ring, lane, q.fill, q.T0, q.T1, q.T2, q.T3, q.len);
-                ring_write16(Ls.ring, lane, q.fill + 16, q.T4, q.T5, q.T6, q.T7, q.len);
+                ring_write16(Ls.ring, lane, q.fill, q.Ta);
+                ring_write16(Ls.ring, lane, q.fill + 16, q.Tb);
                 q.fill += 32;
             }
-            bool switched = false;
+            // Write-back order.  The wave's vector memory counter covers loads and stores alike,
+            // so a wait for a load issued after stores also waits for those stores.  Lanes of
+            // blocks with >= 4 stripes therefore issue this event's loads (staged bytes, next
+            // stripe prefetch) first and the write-back stores last; their prefetch never reads
+            // rows written back in the same event.  Blocks with <= 3 stripes (prefetch rows that
+            // overlap the finished stripe) store first, as program order then orders the reads.
+            bool switched = false, late = false;
+            uint64_t W0 = 0, W1 = 0, W2 = 0, W3 = 0, W4 = 0, W5 = 0, W6 = 0, W7 = 0;   // finished stripe S1..S4, N1..N4
+            uint64_t WB0 = 0, WB1 = 0, WB2 = 0, WB3 = 0, WP0 = 0, WP1 = 0, WP2 = 0, WP3 = 0;
+            uint64_t WM0 = 0, WM1 = 0, WM2 = 0, WM3 = 0;
+            uint32_t wy0 = 0, wk = 0, wt = 0, wmy = 0;
+            bool wmu = false;
+            uint64_t tp0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+            if (TIMING) cyc_p[3] += tp0 - tev;
             if (parked) {
                 parked = false;
                 switched = true;
@@ -327,39 +349,48 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
                                N4 = g_get(Ls.ng, 4, lane);
                 const uint64_t B0 = h_get(Ls.bt, 0, lane), B1 = h_get(Ls.bt, 1, lane), B2 = h_get(Ls.bt, 2, lane),
                                B3 = h_get(Ls.bt, 3, lane);
-                uint64_t* sgp = WS + WS_SIG + y0 + 1;
-                uint64_t* ngp = WS + WS_NEG + y0 + 1;
-                uint64_t* pip = WS + WS_PI + y0;
-                uint64_t* btp = WS + WS_BITS + (size_t)k * 64 + y0;
-                sgp[0] = S1; sgp[1] = S2; sgp[2] = S3; sgp[3] = S4;
-                ngp[0] = N1; ngp[1] = N2; ngp[2] = N3; ngp[3] = N4;
-                if (t == 0) { pip[0] = P0; pip[1] = P1; pip[2] = P2; pip[3] = P3; }
-                btp[0] = B0; btp[1] = B1; btp[2] = B2; btp[3] = B3;
-                const uint32_t ok = k;
+                late = ns > 3;
+                W0 = S1; W1 = S2; W2 = S3; W3 = S4; W4 = N1; W5 = N2; W6 = N3; W7 = N4;
+                WB0 = B0; WB1 = B1; WB2 = B2; WB3 = B3; WP0 = P0; WP1 = P1; WP2 = P2; WP3 = P3;
+                wy0 = y0; wk = k; wt = t;
+                if (!late) {
+                    uint64_t* sgp = WS + WS_SIG + y0 + 1;
+                    uint64_t* ngp = WS + WS_NEG + y0 + 1;
+                    uint64_t* pip = WS + WS_PI + y0;
+                    uint64_t* btp = WS + WS_BITS + (size_t)k * 64 + y0;
+                    st2(sgp, S1, S2); st2(sgp + 2, S3, S4);
+                    st2(ngp, N1, N2); st2(ngp + 2, N3, N4);
+                    if (t == 0) { st2(pip, P0, P1); st2(pip + 2, P2, P3); }
+                    st2(btp, B0, B1); st2(btp + 2, B2, B3);
+                }
+                if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[0] += t - tp0; tp0 = t; }
                 next_pos3(k, t, s, pidx, ns);
                 done = pidx >= npasses || k >= numbps;
-                // new stripe rows: prefetched, except rows the finished stripe still held when the
-                // prefetch was issued (1-stripe blocks: all; 2-stripe blocks at a pass change: row 4)
-                const bool one = ns == 1, two = ns == 2 && s == 0;
-                const uint64_t nS0 = s ? S4 : 0ull, nN0 = s ? N4 : 0ull;
-                const uint64_t nS1 = one ? S1 : X.s1, nS2 = one ? S2 : X.s2, nS3 = one ? S3 : X.s3, nS4 = one ? S4 : X.s4;
-                const uint64_t nS5 = two ? S1 : X.s5;
-                const uint64_t nN1 = one ? N1 : X.n1, nN2 = one ? N2 : X.n2, nN3 = one ? N3 : X.n3, nN4 = one ? N4 : X.n4;
-                const uint64_t nN5 = two ? N1 : X.n5;
-                const uint64_t nP0 = one ? P0 : X.p0, nP1 = one ? P1 : X.p1, nP2 = one ? P2 : X.p2, nP3 = one ? P3 : X.p3;
-                const uint64_t nM0 = one ? M0 : X.m0, nM1 = one ? M1 : X.m1, nM2 = one ? M2 : X.m2, nM3 = one ? M3 : X.m3;
-                const bool same_plane = one && ok == k;
+                // New stripe rows come from the prefetch X, issued when the finished stripe
+                // started.  For 1-stripe blocks (and 2-stripe blocks at a pass change) that
+                // prefetch overlapped the finished stripe's rows, so those lanes reload them
+                // now, after the write-back above (rare: only the smallest bands).
+                const bool resync = !done && (ns == 1 || (ns == 2 && s == 0));
+                if (__any(resync)) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (resync) load_rows(X, WS, k, 4 * s);
+                }
                 const bool newplane = t == 0 || k == 0;
-                const uint64_t nB0 = newplane ? 0ull : (same_plane ? B0 : X.b0), nB1 = newplane ? 0ull : (same_plane ? B1 : X.b1),
-                               nB2 = newplane ? 0ull : (same_plane ? B2 : X.b2), nB3 = newplane ? 0ull : (same_plane ? B3 : X.b3);
-                const uint64_t pP0 = t == 0 ? 0ull : nP0, pP1 = t == 0 ? 0ull : nP1, pP2 = t == 0 ? 0ull : nP2,
-                               pP3 = t == 0 ? 0ull : nP3;
+                const uint64_t nS0 = s ? S4 : 0ull, nN0 = s ? N4 : 0ull;
+                const uint64_t nS1 = X.s1, nS2 = X.s2, nS3 = X.s3, nS4 = X.s4, nS5 = X.s5;
+                const uint64_t nN1 = X.n1, nN2 = X.n2, nN3 = X.n3, nN4 = X.n4, nN5 = X.n5;
+                const uint64_t nM0 = X.m0, nM1 = X.m1, nM2 = X.m2, nM3 = X.m3;
+                const uint64_t nB0 = newplane ? 0ull : X.b0, nB1 = newplane ? 0ull : X.b1,
+                               nB2 = newplane ? 0ull : X.b2, nB3 = newplane ? 0ull : X.b3;
+                const uint64_t pP0 = t == 0 ? 0ull : X.p0, pP1 = t == 0 ? 0ull : X.p1, pP2 = t == 0 ? 0ull : X.p2,
+                               pP3 = t == 0 ? 0ull : X.p3;
                 g_put(Ls.sg, 0, lane, nS0); g_put(Ls.sg, 1, lane, nS1); g_put(Ls.sg, 2, lane, nS2);
                 g_put(Ls.sg, 3, lane, nS3); g_put(Ls.sg, 4, lane, nS4); g_put(Ls.sg, 5, lane, nS5);
                 g_put(Ls.ng, 0, lane, nN0); g_put(Ls.ng, 1, lane, nN1); g_put(Ls.ng, 2, lane, nN2);
                 g_put(Ls.ng, 3, lane, nN3); g_put(Ls.ng, 4, lane, nN4); g_put(Ls.ng, 5, lane, nN5);
                 h_put(Ls.mu, 0, lane, nM0); h_put(Ls.mu, 1, lane, nM1); h_put(Ls.mu, 2, lane, nM2); h_put(Ls.mu, 3, lane, nM3);
                 h_put(Ls.bt, 0, lane, nB0); h_put(Ls.bt, 1, lane, nB1); h_put(Ls.bt, 2, lane, nB2); h_put(Ls.bt, 3, lane, nB3);
+                if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[1] += t - tp0; tp0 = t; }
                 const uint32_t ny0 = 4 * s;
                 nr = done ? 0u : min(4u, h - ny0);
                 vr = (1u << nr) - 1;
@@ -375,21 +406,40 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
                 E = (t == 2 && nr == 4) ? (C0 & C1 & C2 & C3 & ~dil3(nS0 | nS1, nS2 | nS3, nS4 | nS5)) : 0ull;
                 // SP: visited = its candidates (grown by propagation); MR: refined = old | coded now
                 P0 = t == 0 ? C0 : pP0; P1 = t == 0 ? C1 : pP1; P2 = t == 0 ? C2 : pP2; P3 = t == 0 ? C3 : pP3;
-                M0 = nM0 | (t == 1 ? C0 : 0ull); M1 = nM1 | (t == 1 ? C1 : 0ull);
-                M2 = nM2 | (t == 1 ? C2 : 0ull); M3 = nM3 | (t == 1 ? C3 : 0ull);
-                if (t == 1) {
+                // MR refines every candidate: the rows after this pass, stored with the write-back
+                wmu = t == 1; wmy = ny0;
+                WM0 = nM0 | C0; WM1 = nM1 | C1; WM2 = nM2 | C2; WM3 = nM3 | C3;
+                if (wmu && !late) {
                     uint64_t* mup = WS + WS_MU + ny0;
-                    mup[0] = M0; mup[1] = M1; mup[2] = M2; mup[3] = M3;
+                    st2(mup, WM0, WM1); st2(mup + 2, WM2, WM3);
                 }
                 fresh = 0; ph = PH_FIND;
+                if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[2] += t - tp0; tp0 = t; }
             }
             // stage the next ring bytes (lanes whose fill point moved) and prefetch the next
             // stripe of the lanes that switched (the others keep theirs): no re-reads
+            uint64_t tq0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
             if (q.sbase != q.fill) { q.sbase = q.fill; stage_load(q); }
+            if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[4] += t - tq0; tq0 = t; }
             uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
             next_pos3(k2, t2, s2, p2, ns);
             if (switched && !done && p2 < npasses && k2 < numbps)
                 load_rows(X, WS, k2, 4 * s2);
+            if (late) {
+                uint64_t* sgp = WS + WS_SIG + wy0 + 1;
+                uint64_t* ngp = WS + WS_NEG + wy0 + 1;
+                uint64_t* pip = WS + WS_PI + wy0;
+                uint64_t* btp = WS + WS_BITS + (size_t)wk * 64 + wy0;
+                st2(sgp, W0, W1); st2(sgp + 2, W2, W3);
+                st2(ngp, W4, W5); st2(ngp + 2, W6, W7);
+                if (wt == 0) { st2(pip, WP0, WP1); st2(pip + 2, WP2, WP3); }
+                st2(btp, WB0, WB1); st2(btp + 2, WB2, WB3);
+                if (wmu && !done) {
+                    uint64_t* mup = WS + WS_MU + wmy;
+                    st2(mup, WM0, WM1); st2(mup + 2, WM2, WM3);
+                }
+            }
+            if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[5] += t - tq0; }
             if (TIMING) { const uint64_t t1 = __builtin_amdgcn_s_memtime(); cyc_ev += t1 - tev; tev = t1; }
         }
         if (TIMING && !tev) tev = __builtin_amdgcn_s_memtime();
@@ -483,12 +533,23 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         q.nb4 = ring_get4(Ls.ring, lane, q.bp);
         if (TIMING) cyc_step += __builtin_amdgcn_s_memtime() - tev;
     }
+    unsigned long long cp[6] = {0, 0, 0, 0, 0, 0};
+    if (TIMING) {   // the parked block runs on the parked lanes only: take the max over lanes per event
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            cp[i] = cyc_p[i];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) cp[i] = max(cp[i], (unsigned long long)__shfl_xor(cp[i], o));
+        }
+    }
     if (stats) {
         unsigned long long tot = nsym;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
         if (lane == 0) {
             if (TIMING) { atomicAdd(&stats[4], cyc_ev); atomicAdd(&stats[5], cyc_step); }
+            if (TIMING)
+                for (int i = 0; i < 6; ++i) atomicAdd(&stats[6 + i], cp[i]);
             atomicAdd(&stats[3], (unsigned long long)nevents);
             atomicAdd(&stats[0], (unsigned long long)nstep); atomicAdd(&stats[1], tot);
             atomicMax(&stats[2], (unsigned long long)nstep);
@@ -560,8 +621,8 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     static unsigned long long* stats = nullptr;
     const char* sv = getenv("GK_T1_STATS");
     const bool want = sv != nullptr, timing = sv && atoi(sv) == 2;
-    if (want && !stats) { (void)hipMalloc(&stats, 64); }
-    if (want) (void)hipMemsetAsync(stats, 0, 64, st);
+    if (want && !stats) { (void)hipMalloc(&stats, 128); }
+    if (want) (void)hipMemsetAsync(stats, 0, 128, st);
     static int kpark = -1;
     if (kpark < 0) {
         const char* kp = getenv("GK_T1DEC_PARK");   // parked lanes that trigger a stripe boundary
@@ -574,8 +635,8 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         hipLaunchKernelGGL(k_t1_dec2<false>, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
     if (want) {
-        unsigned long long h[8];
-        (void)hipMemcpyAsync(h, stats, 64, hipMemcpyDeviceToHost, st);
+        unsigned long long h[16];
+        (void)hipMemcpyAsync(h, stats, 128, hipMemcpyDeviceToHost, st);
         (void)hipStreamSynchronize(st);
         fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f events/wave %.0f\n",
                 (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]),
@@ -584,6 +645,12 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
             fprintf(stderr, "t1dec timing: cycles/event %.0f cycles/step %.0f (event share %.3f)\n",
                     (double)h[4] / (double)(h[3] ? h[3] : 1), (double)h[5] / (double)(h[0] ? h[0] : 1),
                     (double)h[4] / (double)(h[4] + h[5] ? h[4] + h[5] : 1));
+        if (timing)
+            fprintf(stderr, "t1dec event parts (max-lane sums / events): ring commit %.0f, write-back %.0f, select+LDS %.0f, "
+                            "candidates %.0f, stage %.0f, prefetch %.0f\n",
+                    (double)h[9] / (double)(h[3] ? h[3] : 1), (double)h[6] / (double)(h[3] ? h[3] : 1),
+                    (double)h[7] / (double)(h[3] ? h[3] : 1), (double)h[8] / (double)(h[3] ? h[3] : 1),
+                    (double)h[10] / (double)(h[3] ? h[3] : 1), (double)h[11] / (double)(h[3] ? h[3] : 1));
     }
 }
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
