@@ -487,7 +487,7 @@ struct TagTree {
         int32_t n = (int32_t)leaf;
         while (n >= 0 && value[n] > v) { value[n] = v; n = parent[n]; }
     }
-    void encode(BitWriter& bw, uint32_t leaf, uint32_t threshold) {
+    template <class W> void encode(W& bw, uint32_t leaf, uint32_t threshold) {
         int32_t stk[40]; int sp = 0; int32_t n = (int32_t)leaf;
         while (parent[n] >= 0) { stk[sp++] = n; n = parent[n]; }
         uint32_t lo = 0;
@@ -501,6 +501,42 @@ struct TagTree {
             if (!sp) break;
             n = stk[--sp];
         }
+    }
+};
+
+// Raw (unstuffed) packet-header bits, MSB first in left-aligned 64-bit words, with BitWriter's
+// interface: the rate-control simulation codes each band of a packet on its own and counts
+// the stuffed length of the concatenation afterwards (T2Enc::stuffed_len).
+struct RawBits {
+    std::vector<uint64_t> w;
+    uint64_t acc = 0;   // pending bits, right-aligned
+    uint32_t nacc = 0;
+    uint64_t n = 0;     // bits written
+    void clear() { w.clear(); acc = 0; nacc = 0; n = 0; }
+    inline void put(uint32_t v, uint32_t k) {   // the low k <= 32 bits of v (higher bits zero)
+        n += k;
+        if (nacc + k < 64) { acc = (acc << k) | v; nacc += k; return; }
+        const uint32_t k1 = 64 - nacc, k2 = k - k1;   // k1 in 1..32, k2 in 0..31
+        w.push_back((acc << k1) | ((uint64_t)v >> k2));
+        acc = (uint64_t)v & ((1ull << k2) - 1);
+        nacc = k2;
+    }
+    void finish() { if (nacc) w.push_back(acc << (64 - nacc)); acc = 0; nacc = 0; }
+    inline void putbit(uint32_t b) { put(b, 1); }
+    inline void write(uint32_t v, int k) {
+        if (k > 32) { put(0, (uint32_t)k - 32); k = 32; }
+        put(k == 32 ? v : (v & ((1u << k) - 1)), (uint32_t)k);
+    }
+    void commacode(uint32_t c) {
+        while (c >= 31) { put(0x7fffffffu, 31); c -= 31; }
+        put(((1u << c) - 1) << 1, c + 1);
+    }
+    void numpasses(uint32_t np) {
+        if (np == 1) put(0, 1);
+        else if (np == 2) put(2, 2);
+        else if (np <= 5) put(0xc | (np - 3), 4);
+        else if (np <= 36) put(0x1e0 | (np - 6), 9);
+        else put(0xff80 | (np - 37), 16);
     }
 };
 
@@ -687,6 +723,54 @@ struct T2Enc {
     }
     double dist(uint32_t b, uint32_t q) const { return passes[info[4 * (size_t)b + 3] + q].dist; }
 
+    // l == 0: fresh tag trees, every code-block's zero-bit-plane count in its tree
+    void band_init(const PrecG& PG, uint32_t bnb) {
+        incl[PG.tree].reset(); imsb[PG.tree].reset();
+        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+            const uint32_t b = PG.first_block + k;
+            inprev[b] = 0;
+            imsb[PG.tree].setvalue(k, bnb - info[4 * (size_t)b]);
+        }
+    }
+    // one band's part of a packet header (T2Compress::compressHeader, T2Compress.cpp:114-240)
+    template <class W> void band_header(const PrecG& PG, uint32_t l, W& bw) {
+        const uint32_t n = PG.cw * PG.ch;
+        TagTree& IT = incl[PG.tree];
+        for (uint32_t k = 0; k < n; ++k) {
+            uint32_t b = PG.first_block + k;
+            if (!inprev[b] && lnp[(size_t)b * L + l]) IT.setvalue(k, l);
+        }
+        for (uint32_t k = 0; k < n; ++k) {
+            uint32_t b = PG.first_block + k;
+            uint32_t np = lnp[(size_t)b * L + l];
+            if (!inprev[b]) IT.encode(bw, k, l + 1);
+            else bw.putbit(np != 0);
+            if (!np) continue;
+            if (!inprev[b]) { nlb[b] = 3; imsb[PG.tree].encode(bw, k, 0xffffffffu); }
+            bw.numpasses(np);
+            // default style: one segment per contribution (only the last pass is terminated)
+            uint32_t r0 = inprev[b] ? rate(b, inprev[b] - 1) : 0;
+            uint32_t len = rate(b, inprev[b] + np - 1) - r0;
+            int inc = std::max(0, floorlog2(len) + 1 - ((int)nlb[b] + floorlog2(np)));
+            bw.commacode((uint32_t)inc);
+            nlb[b] = (uint8_t)(nlb[b] + inc);
+            bw.write(len, (int)nlb[b] + floorlog2(np));
+        }
+    }
+    // one band's packet body bytes; advances its code-blocks' pass counts
+    uint64_t band_body(const PrecG& PG, uint32_t l) {
+        uint64_t sum = 0;
+        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+            const uint32_t b = PG.first_block + k;
+            const uint32_t np = lnp[(size_t)b * L + l];
+            if (!np) continue;
+            const uint32_t r0 = inprev[b] ? rate(b, inprev[b] - 1) : 0;
+            sum += rate(b, inprev[b] + np - 1) - r0;
+            inprev[b] = (uint16_t)(inprev[b] + np);
+        }
+        return sum;
+    }
+
     // One packet.  budget: remaining bytes (nullptr = unbounded).  seg (optional) receives
     // (block, first byte, length) body segments.  Returns false when the budget is exceeded.
     bool write_packet(const ResG& R, uint32_t pi, uint32_t l, uint64_t* budget,
@@ -697,47 +781,17 @@ struct T2Enc {
     // all other state touched is per code-block / per precinct, i.e. disjoint across tiles)
     bool write_packet(const ResG& R, uint32_t pi, uint32_t l, uint64_t* budget,
                       std::vector<uint32_t>* seg, std::vector<uint8_t>& hdr, uint64_t* body_bytes = nullptr) {
-        if (l == 0) {
+        if (l == 0)
             for (size_t bi = 0; bi < R.bands.size(); ++bi) {
                 const PrecG& PG = R.prc[bi][pi];
-                if (!PG.cw || !PG.ch) continue;
-                incl[PG.tree].reset(); imsb[PG.tree].reset();
-                const uint32_t bnb = R.bands[bi].numbps;
-                for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                    uint32_t b = PG.first_block + k;
-                    inprev[b] = 0;
-                    imsb[PG.tree].setvalue(k, bnb - info[4 * (size_t)b]);
-                }
+                if (PG.cw && PG.ch) band_init(PG, R.bands[bi].numbps);
             }
-        }
         hdr.clear();
         BitWriter bw(hdr);
         bw.putbit(1);
         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
             const PrecG& PG = R.prc[bi][pi];
-            if (!PG.cw || !PG.ch) continue;
-            const uint32_t n = PG.cw * PG.ch;
-            TagTree& IT = incl[PG.tree];
-            for (uint32_t k = 0; k < n; ++k) {
-                uint32_t b = PG.first_block + k;
-                if (!inprev[b] && lnp[(size_t)b * L + l]) IT.setvalue(k, l);
-            }
-            for (uint32_t k = 0; k < n; ++k) {
-                uint32_t b = PG.first_block + k;
-                uint32_t np = lnp[(size_t)b * L + l];
-                if (!inprev[b]) IT.encode(bw, k, l + 1);
-                else bw.putbit(np != 0);
-                if (!np) continue;
-                if (!inprev[b]) { nlb[b] = 3; imsb[PG.tree].encode(bw, k, 0xffffffffu); }
-                bw.numpasses(np);
-                // default style: one segment per contribution (only the last pass is terminated)
-                uint32_t r0 = inprev[b] ? rate(b, inprev[b] - 1) : 0;
-                uint32_t len = rate(b, inprev[b] + np - 1) - r0;
-                int inc = std::max(0, floorlog2(len) + 1 - ((int)nlb[b] + floorlog2(np)));
-                bw.commacode((uint32_t)inc);
-                nlb[b] = (uint8_t)(nlb[b] + inc);
-                bw.write(len, (int)nlb[b] + floorlog2(np));
-            }
+            if (PG.cw && PG.ch) band_header(PG, l, bw);
         }
         bw.flush();
         if (budget) {
@@ -779,48 +833,137 @@ struct T2Enc {
 
     // ---- fast simulation for the bisection of layer l (single tile).  Layers < l are final,
     // so the T2 state after them is snapshotted once; every bisection step restores each
-    // precinct chain (its tag trees and code-blocks) and codes only layer l, chains in
-    // parallel.  compressPacketsSimulate's bounded writes fail iff, with S the running size
-    // over packets in LRCP order, some packet header reaches the remaining budget or some
-    // body exceeds it; sizes only grow, so that is decided by the last packet:
+    // band of each packet (its tag trees and code-blocks) and codes only layer l.  A packet
+    // header is the bit 1 followed by its bands' bits, and bands share no coding state, so
+    // every (packet, band) is coded on its own into raw bits, in parallel, and the header
+    // length is counted from the concatenation (stuffed_len).  compressPacketsSimulate's
+    // bounded writes fail iff, with S the running size over packets in LRCP order, some
+    // packet header reaches the remaining budget or some body exceeds it; sizes only grow,
+    // so that is decided by the last packet:
     //   pass <=> S_(n-1) + hdr_n < budget  and  S_n <= budget.
     struct Chain { uint32_t c, r, pi; };
+    struct Unit { uint32_t chain, band, nblk; };
     std::vector<Chain> chains;              // one layer's packets in LRCP order
+    std::vector<Unit> units;                // (packet, band) pieces
+    std::vector<uint32_t> uorder;           // units, largest first (dynamic schedule)
+    std::vector<std::vector<uint32_t>> cunits;   // per packet: its units in band order
+    std::vector<RawBits> ubits;
+    std::vector<uint64_t> ubody;
     std::vector<TagTree> incl0, imsb0;      // snapshot after the final layers < l
     std::vector<uint16_t> inprev0;
     std::vector<uint8_t> nlb0;
     uint64_t prior = 0;                     // bytes of the final layers < l
     std::vector<uint64_t> csize, chdr;
     void init_chains() {
-        chains.clear();
+        chains.clear(); units.clear();
         const TileG& T = P.tiles[0];
         for (uint32_t r = 0; r < P.p.numres; ++r)
             for (uint32_t c = 0; c < P.nc; ++c)
                 for (uint32_t pi = 0; pi < T.comps[c].res[r].pw * T.comps[c].res[r].ph; ++pi) chains.push_back({c, r, pi});
+        cunits.assign(chains.size(), {});
+        for (uint32_t i = 0; i < (uint32_t)chains.size(); ++i) {
+            const ResG& R = T.comps[chains[i].c].res[chains[i].r];
+            for (uint32_t bi = 0; bi < (uint32_t)R.bands.size(); ++bi) {
+                const PrecG& PG = R.prc[bi][chains[i].pi];
+                if (!PG.cw || !PG.ch) continue;
+                cunits[i].push_back((uint32_t)units.size());
+                units.push_back({i, bi, PG.cw * PG.ch});
+            }
+        }
+        uorder.resize(units.size());
+        for (uint32_t u = 0; u < (uint32_t)units.size(); ++u) uorder[u] = u;
+        std::stable_sort(uorder.begin(), uorder.end(), [&](uint32_t x, uint32_t y) { return units[x].nblk > units[y].nblk; });
+        ubits.assign(units.size(), RawBits());
+        ubody.assign(units.size(), 0);
         csize.assign(chains.size(), 0); chdr.assign(chains.size(), 0);
         prior = 0;
     }
-    void restore_chain(const Chain& ch) {
-        const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
-        for (size_t bi = 0; bi < R.bands.size(); ++bi) {
-            const PrecG& PG = R.prc[bi][ch.pi];
-            if (!PG.cw || !PG.ch) continue;
-            incl[PG.tree] = incl0[PG.tree]; imsb[PG.tree] = imsb0[PG.tree];
-            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                const uint32_t b = PG.first_block + k;
-                inprev[b] = inprev0[b]; nlb[b] = nlb0[b];
-            }
+    void restore_band(const PrecG& PG) {
+        incl[PG.tree] = incl0[PG.tree]; imsb[PG.tree] = imsb0[PG.tree];
+        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+            const uint32_t b = PG.first_block + k;
+            inprev[b] = inprev0[b]; nlb[b] = nlb0[b];
         }
     }
-    void code_layer(uint32_t l) {   // every chain of layer l from the snapshot, in parallel
-        host_pool().run(chains.size(), [&](size_t i) {
-            const Chain& ch = chains[i];
-            if (l) restore_chain(ch);
-            std::vector<uint8_t> hb;
-            uint64_t body = 0;
-            write_packet(P.tiles[0].comps[ch.c].res[ch.r], ch.pi, l, nullptr, nullptr, hb, &body);
-            chdr[i] = hb.size(); csize[i] = hb.size() + body;
+    // Bytes BitIO writes for the bit 1, the units' raw bits and a flush (BitIO.cpp): bytes
+    // are 8-bit chunks of the raw bits, except that the chunk after an 0xFF byte carries 7
+    // bits, and a final 0xFF byte is followed by one more.  Only chunk-grid positions where 8
+    // ones start give 0xFF, so those positions are found word-wise and the rest is counted.
+    uint64_t stuffed_len(const std::vector<uint32_t>& us, std::vector<uint64_t>& sb) const {
+        sb.clear();
+        uint64_t cur = 1ull << 63, N = 1;
+        uint32_t cn = 1;
+        auto app = [&](uint64_t x, uint32_t k) {   // the top k bits of x (bits below them zero)
+            cur |= x >> cn;
+            if (cn + k >= 64) { sb.push_back(cur); cur = cn ? x << (64 - cn) : 0; cn = cn + k - 64; }
+            else cn += k;
+        };
+        for (uint32_t u : us) {
+            const RawBits& rb = ubits[u];
+            const size_t full = (size_t)(rb.n / 64);
+            const uint32_t rem = (uint32_t)(rb.n % 64);
+            for (size_t i = 0; i < full; ++i) app(rb.w[i], 64);
+            if (rem) app(rb.w[full], rem);
+            N += rb.n;
+        }
+        if (cn) sb.push_back(cur);
+        sb.push_back(0);
+        uint64_t pos = 0, bytes = 0;
+        bool last_ff = false, end = false;
+        for (size_t j = 0; j + 1 < sb.size() && !end; ++j) {
+            const uint64_t x = sb[j], nx = sb[j + 1];
+            uint64_t ones = x;
+            for (int d = 1; d < 8; ++d) ones &= (x << d) | (nx >> (64 - d));
+            while (ones && !end) {
+                const int z = __builtin_clzll(ones);
+                ones &= ~(1ull << (63 - z));
+                const uint64_t p = (uint64_t)j * 64 + (uint64_t)z;   // bits p .. p+7 are ones
+                if (p < pos || ((p - pos) & 7)) continue;
+                bytes += (p - pos) / 8 + 1;                         // chunks up to the 0xFF one
+                if (p + 8 >= N) { last_ff = true; pos = N; end = true; break; }
+                bytes += 1;                                         // the 7-bit chunk after it
+                pos = p + 15;
+                if (pos >= N) { pos = N; end = true; }
+            }
+        }
+        if (pos < N) bytes += (N - pos + 7) / 8;
+        if (last_ff) ++bytes;
+        return bytes;
+    }
+    void code_layer(uint32_t l) {   // every (packet, band) of layer l from the snapshot, in parallel
+        host_pool().run(uorder.size(), [&](size_t j) {
+            const uint32_t u = uorder[j];
+            const Unit& U = units[u];
+            const Chain& ch = chains[U.chain];
+            const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
+            const PrecG& PG = R.prc[U.band][ch.pi];
+            if (l) restore_band(PG); else band_init(PG, R.bands[U.band].numbps);
+            RawBits& rb = ubits[u];
+            rb.clear();
+            band_header(PG, l, rb);
+            rb.finish();
+            ubody[u] = band_body(PG, l);
         });
+        host_pool().run(chains.size(), [&](size_t i) {
+            thread_local std::vector<uint64_t> sbuf;
+            uint64_t body = 0;
+            for (uint32_t u : cunits[i]) body += ubody[u];
+            const uint64_t h = stuffed_len(cunits[i], sbuf);
+            chdr[i] = h; csize[i] = h + body;
+        });
+        static const bool check = getenv("GK_T2_CHECK_SIM") != nullptr;
+        if (check) {   // debug: the packets' real sizes (write_packet) must match
+            std::vector<uint8_t> hb;
+            for (size_t i = 0; i < chains.size(); ++i) {
+                const Chain& ch = chains[i];
+                const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
+                if (l) for (uint32_t u : cunits[i]) restore_band(R.prc[units[u].band][ch.pi]);
+                uint64_t body = 0;
+                write_packet(R, ch.pi, l, nullptr, nullptr, hb, &body);
+                if (hb.size() != chdr[i] || hb.size() + body != csize[i])
+                    throw GkError("rate-control simulation: packet size mismatch");
+            }
+        }
     }
     bool simulate_layer(uint32_t l, uint64_t max_bytes) {
         if (max_bytes == 0xffffffffull) return true;
@@ -836,33 +979,61 @@ struct T2Enc {
         incl0 = incl; imsb0 = imsb; inprev0 = inprev; nlb0 = nlb;
     }
 
-    // makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0), blocks in parallel
-    void make_layer(uint32_t l, double thresh, bool final_attempt, std::vector<uint16_t>& prev) {
+    // makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0) (TileProcessor.cpp:1367-1515),
+    // blocks in parallel.  During one layer's bisection prev[] is fixed, so each block keeps
+    // the threshold its pass count was last computed at (mref) and half the distance from it
+    // to the nearest slope it was compared with (mrad): a threshold closer than that takes
+    // every comparison of the greedy scan the same way, so the count is reused exactly.
+    // Returns a hash of the layer's pass counts (equal counts => equal simulation outcome).
+    std::vector<double> mref, mrad;
+    static uint64_t mix64(uint64_t x) {
+        x += 0x9e3779b97f4a7c15ull;
+        x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+        x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+        return x ^ (x >> 31);
+    }
+    uint64_t make_layer(uint32_t l, double thresh, bool final_attempt, std::vector<uint16_t>& prev) {
         const uint32_t nb = (uint32_t)P.blocks.size();
-        const uint32_t chunk = 4096;
-        host_pool().run((nb + chunk - 1) / chunk, [&](size_t ci) {
+        const uint32_t chunk = 2048, nch = (nb + chunk - 1) / chunk;
+        if (mref.size() != nb) { mref.assign(nb, 0.0); mrad.assign(nb, -1.0); }
+        std::vector<uint64_t> hs(nch, 0);
+        host_pool().run(nch, [&](size_t ci) {
+        uint64_t hsum = 0;
         const uint32_t bend = std::min<uint32_t>(nb, (uint32_t)(ci + 1) * chunk);
         for (uint32_t b = (uint32_t)ci * chunk; b < bend; ++b) {
             if (l == 0) prev[b] = 0;
             const uint32_t np = npasses(b);
             uint32_t inc;
-            if (thresh < 0) inc = std::max<uint32_t>(prev[b], np);
-            else if (thresh == 0) inc = np;
+            if (thresh < 0) { inc = std::max<uint32_t>(prev[b], np); mrad[b] = -1.0; }
+            else if (thresh == 0) { inc = np; mrad[b] = -1.0; }
+            else if (mrad[b] > 0 && fabs(thresh - mref[b]) < mrad[b]) inc = prev[b] + lnp[(size_t)b * L + l];
             else {
                 inc = prev[b];
+                double m = HUGE_VAL;
                 for (uint32_t q = prev[b]; q < np; ++q) {
                     uint32_t dr; double dd;
                     if (inc == 0) { dr = rate(b, q); dd = dist(b, q); }
                     else { dr = rate(b, q) - rate(b, inc - 1); dd = dist(b, q) - dist(b, inc - 1); }
                     if (!dr) { if (dd != 0) inc = q + 1; continue; }
                     double slope = dd / dr;
-                    if (thresh - slope < 2.220446049250313e-16) inc = q + 1;
+                    const double diff = thresh - slope;
+                    if (diff < 2.220446049250313e-16) inc = q + 1;
+                    m = std::min(m, fabs(diff));
                 }
+                // reuse only with a radius far above rounding (relative 1e-9) and eps
+                mref[b] = thresh;
+                mrad[b] = (m > 1e-9 * fabs(thresh) && m > 1e-12) ? 0.5 * m : 0.0;
             }
-            lnp[(size_t)b * L + l] = (uint16_t)(inc - prev[b]);
-            if (final_attempt) prev[b] = (uint16_t)inc;
+            const uint16_t v = (uint16_t)(inc - prev[b]);
+            lnp[(size_t)b * L + l] = v;
+            hsum += mix64(((uint64_t)b << 16) | v);
+            if (final_attempt) { prev[b] = (uint16_t)inc; mrad[b] = -1.0; }
         }
+        hs[ci] = hsum;
         });
+        uint64_t h = 0;
+        for (uint64_t v : hs) h += v;
+        return h;
     }
 
     void allocate(size_t header_size) {
@@ -897,18 +1068,39 @@ struct T2Enc {
             }
         double upper = max_slope;
         const bool fast = P.tiles.size() == 1 && !getenv("GK_T2_SERIAL_SIM");
+        static const bool prof = getenv("GK_PROFILE") != nullptr;
+        using clk = std::chrono::steady_clock;
+        auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        double t_make = 0, t_sim = 0;
+        uint32_t n_it = 0, n_sim = 0;
         if (fast) init_chains();
         for (uint32_t l = 0; l < L; ++l) {
             uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
             if (rates[l] > 0.0) {
                 double lower = min_slope, prevthresh = -1, thresh = 0;
+                // pass counts equal to those at an end of the bisection interval give that end's
+                // outcome (the simulation depends on nothing else): the simulation is skipped
+                bool has_lo = false, has_hi = false;
+                uint64_t h_lo = 0, h_hi = 0;
                 for (uint32_t it = 0; it < 128; ++it) {
                     thresh = (upper == -1) ? lower : (lower + upper) / 2;
-                    make_layer(l, thresh, false, prev);
+                    const auto t0 = clk::now();
+                    const uint64_t h = make_layer(l, thresh, false, prev);
+                    const auto t1 = clk::now();
+                    t_make += msd(t0, t1);
+                    ++n_it;
                     if (prevthresh != -1 && fabs(prevthresh - thresh) < 0.001) break;
                     prevthresh = thresh;
-                    if (!(fast ? simulate_layer(l, max_len) : simulate(l + 1, max_len))) { lower = thresh; continue; }
-                    upper = thresh;
+                    bool ok;
+                    if (has_hi && h == h_hi) ok = true;
+                    else if (has_lo && h == h_lo) ok = false;
+                    else {
+                        ok = fast ? simulate_layer(l, max_len) : simulate(l + 1, max_len);
+                        t_sim += msd(t1, clk::now());
+                        ++n_sim;
+                    }
+                    if (!ok) { lower = thresh; h_lo = h; has_lo = true; continue; }
+                    upper = thresh; h_hi = h; has_hi = true;
                 }
                 make_layer(l, upper == -1 ? thresh : upper, true, prev);
                 upper = lower - 1;
@@ -917,6 +1109,9 @@ struct T2Enc {
             }
             if (fast && l + 1 < L) finish_layer(l);
         }
+        if (prof)
+            fprintf(stderr, "pcrd: %u bisection steps, %u simulated; make_layer %.2f ms, simulation %.2f ms\n", n_it,
+                    n_sim, t_make, t_sim);
     }
 };
 

@@ -366,64 +366,26 @@ __device__ __forceinline__ void mql_byteout(MqLane& q) { mql_byteout_if(q, true)
 
 struct Ctx5e { uint32_t w0, w1, w2, w3, w4; };
 
-// CODEMPS / CODELPS + RENORME for symbol s = (ctx << 1) | d, predicated on `en`
-__device__ __forceinline__ void mq_code(MqLane& q, Ctx5e& cw, const uint32_t* tab, uint32_t s, bool en) {
-    const uint32_t cx = s >> 1, d = s & 1;
-    const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
-    uint32_t word = vsel_e(wi == 4, cw.w4, vsel_e(wi & 2, vsel_e(wi & 1, cw.w3, cw.w2), vsel_e(wi & 1, cw.w1, cw.w0)));
-    const uint32_t st = (word >> shb) & 0xff;
-    const uint32_t mps = st >> 6;
-    const uint32_t e = tab[st & 63];
-    const uint32_t qe = e & 0xffff;
-    const uint32_t a1 = q.a - qe;
-    const bool is_mps = mps == d;
-    const bool fast = is_mps && (a1 & 0x8000);          // MPS without renormalisation
-    // CODEMPS: A < Qe ? A = Qe : C += Qe ; CODELPS: A < Qe ? C += Qe : A = Qe
-    const bool addc = fast || (is_mps ? !(a1 < qe) : (a1 < qe));
-    const uint32_t anew = fast ? a1 : (is_mps ? (a1 < qe ? qe : a1) : (a1 < qe ? a1 : qe));
-    const uint32_t nst = is_mps ? (((e >> 16) & 0x3f) | (mps << 6)) : (((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6));
-    const bool upd = en && !fast;
-    q.c += (en && addc) ? qe : 0u;
-    q.a = en ? anew : q.a;
-    word = (word & ~(0xffu << shb)) | (nst << shb);
-    cw.w0 = vsel_e(upd && wi == 0, word, cw.w0); cw.w1 = vsel_e(upd && wi == 1, word, cw.w1);
-    cw.w2 = vsel_e(upd && wi == 2, word, cw.w2); cw.w3 = vsel_e(upd && wi == 3, word, cw.w3);
-    cw.w4 = vsel_e(upd && wi == 4, word, cw.w4);
-    uint32_t n = upd ? __clz(q.a) - 16 : 0u;
-    while (__any(n != 0)) {
-        const uint32_t k = n < q.ct ? n : q.ct;
-        q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
-        mql_byteout_if(q, k != 0 && q.ct == 0);
-    }
-}
-
-// Branch-free BYTEOUT for the symbol loop: every value is computed for all lanes and
-// committed with selects; only the word store is predicated (`en` lanes that complete
-// a 4-byte word).  Same arithmetic as mql_byteout_if (Annex C.2.6).
-__device__ __forceinline__ void mql_byteout_sel(MqLane& q, bool en) {
-    const uint32_t carry = (q.cur != 0xff) ? ((q.c >> 27) & 1) : 0u;
-    const uint32_t cur = q.cur + carry;
-    const uint32_t c = q.c & ~(carry << 27);
-    const bool ff = cur == 0xff;
-    // emit `cur` at bp; bp = -1 is the encoder's dummy byte before the buffer, which the one
-    // unsigned compare also excludes (overflow past `cap` is detected from the final bp)
+// Byte emission for the symbol loop: `cur` goes to position bp (bp = -1 is the encoder's
+// dummy byte before the buffer, which the one unsigned compare also excludes; overflow past
+// `cap` is detected from the final bp).  Branch-free except the predicated word store.
+__device__ __forceinline__ void mql_put_sel(MqLane& q, bool en, uint32_t cur) {
     const bool put = en & ((uint32_t)q.bp < q.cap);
     const uint32_t wb = q.wbuf | (put ? cur << (8 * (q.bp & 3)) : 0u);
     const bool full = put & ((q.bp & 3) == 3);
     if (full) *(uint32_t*)(q.out + (q.bp - 3)) = wb;
     q.wbuf = full ? 0u : wb;
     q.bp += en ? 1 : 0;
-    q.cur = vsel_e(en, (ff ? (c >> 20) : (c >> 19)) & 0xff, q.cur);
-    q.c = vsel_e(en, c & (ff ? 0xfffffu : 0x7ffffu), q.c);
-    q.ct = vsel_e(en, ff ? 7u : 8u, q.ct);
 }
 
 // CODEMPS / CODELPS + RENORME (Annex C.2.4-C.2.7), branch-free.  With x = (MPS symbol) xor
 // (A - Qe < Qe): the coder adds Qe to C iff x and keeps A - Qe iff x, else A = Qe.
-// RENORME's n shifts run as at most two segments that end at a byte boundary (CT = 0),
-// each followed by a predicated BYTEOUT; a third boundary (two 0xFF bytes in one
-// renormalisation) falls back to the loop.
-__device__ __forceinline__ void mq_code2(MqLane& q, Ctx5e& cw, const uint32_t* tab, uint32_t s, bool en) {
+// RENORME shifts A and C by the whole renormalisation at once (C as 64 bits).  When the byte
+// boundary (CT = 0) falls inside the shift, BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127) runs on
+// C >> e, e = the bits shifted past the boundary; they stay below the new byte, whose CT
+// (8, or 7 after 0xFF) is reduced by e.  A second boundary in one renormalisation (e >= 8)
+// repeats the BYTEOUT (rare; at most two for shifts <= 15).
+__device__ __forceinline__ void mq_code3(MqLane& q, Ctx5e& cw, const uint32_t* tab, uint32_t s, bool en) {
     const uint32_t cx = s >> 1, d = s & 1;
     const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
     uint32_t word = vsel_e(wi == 4, cw.w4, vsel_e(wi & 2, vsel_e(wi & 1, cw.w3, cw.w2), vsel_e(wi & 1, cw.w1, cw.w0)));
@@ -437,27 +399,33 @@ __device__ __forceinline__ void mq_code2(MqLane& q, Ctx5e& cw, const uint32_t* t
     const bool x = is_mps ^ (a1 < qe);
     const uint32_t nst = is_mps ? (((e >> 16) & 0x3f) | (mps << 6)) : (((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6));
     const bool upd = en & !fast;
-    q.c += (en & x) ? qe : 0u;
-    q.a = vsel_e(en, x ? a1 : qe, q.a);
+    const uint32_t an = vsel_e(en, x ? a1 : qe, q.a);
     word = (word & ~(0xffu << shb)) | (nst << shb);
     const uint32_t wu = upd ? wi : 7u;
     cw.w0 = vsel_e(wu == 0, word, cw.w0); cw.w1 = vsel_e(wu == 1, word, cw.w1);
     cw.w2 = vsel_e(wu == 2, word, cw.w2); cw.w3 = vsel_e(wu == 3, word, cw.w3);
     cw.w4 = vsel_e(wu == 4, word, cw.w4);
-    uint32_t n = upd ? __clz(q.a) - 16 : 0u;
-    uint32_t k = min(n, q.ct);
-    q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
-    mql_byteout_sel(q, q.ct == 0);
-    if (__any(n != 0)) {   // a second byte boundary in this renormalisation (large shifts)
-        k = min(n, q.ct);
-        q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
-        mql_byteout_sel(q, q.ct == 0);
+    const uint32_t n = upd ? __clz(an) - 16 : 0u;
+    q.a = an << n;
+    uint64_t c = (uint64_t)(q.c + ((en & x) ? qe : 0u)) << n;
+    int ct = (int)q.ct - (int)n;
+    bool bo = ct <= 0;
+    while (__any(bo)) {
+        const uint32_t sh = bo ? (uint32_t)(-ct) : 0u;
+        const uint32_t carry = (bo & (q.cur != 0xff)) ? (uint32_t)(c >> (27 + sh)) & 1u : 0u;
+        const uint32_t cur = q.cur + carry;
+        c &= ~((uint64_t)carry << (27 + sh));
+        const bool ff = cur == 0xff;
+        const uint32_t nb = (uint32_t)(c >> ((ff ? 20u : 19u) + sh)) & 0xffu;
+        mql_put_sel(q, bo, cur);
+        q.cur = vsel_e(bo, nb, q.cur);
+        const uint64_t keep = ((uint64_t)(ff ? 0x100000u : 0x80000u) << sh) - 1;
+        c = bo ? (c & keep) : c;
+        ct = bo ? (ff ? 7 : 8) - (int)sh : ct;
+        bo = ct <= 0;
     }
-    while (__any(n != 0)) {
-        k = min(n, q.ct);
-        q.a <<= k; q.c <<= k; q.ct -= k; n -= k;
-        mql_byteout_if(q, k != 0 && q.ct == 0);
-    }
+    q.c = (uint32_t)c;
+    q.ct = (uint32_t)ct;
 }
 
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t j) {
@@ -552,7 +520,7 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
         for (uint32_t j = 0; j < 16; ++j) {
             const uint32_t i = base + j;
             const bool en = i < nsym;
-            mq_code2(q, cw, tab, byte_of(cur4, j), en);
+            mq_code3(q, cw, tab, byte_of(cur4, j), en);
             // the prefetch two chunks ahead is issued after the first symbol has consumed this
             // chunk's bytes, so the wait for them does not also wait for the prefetch
             if (j == 0) {
