@@ -131,57 +131,65 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
     src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
     const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH;
     const int tid = threadIdx.x;
-    // load rows y0-2 .. y0+TH, cols x0-2 .. x0+TW (mirrored)
-    for (int i = tid; i < DWT_LH * DWT_LW; i += 256) {
-        int ly = i / DWT_LW, lx = i % DWT_LW;
-        int gy = mirror(y0 - 2 + ly, (int)h), gx = mirror(x0 - 2 + lx, (int)w);
-        T[ly][lx] = src[(size_t)gy * sstride + gx];
+    // 4 waves x 64 lanes: lane tx walks columns tx, tx+64, tx+128 of rows ty, ty+4, ... (no
+    // index division: the level is bound by instruction count before HBM)
+    const int tx = tid & 63, ty = tid >> 6;
+    // load rows y0-2 .. y0+TH, cols x0-2 .. x0+TW (mirrored at the resolution border)
+    if (x0 >= 2 && y0 >= 2 && x0 + DWT_TW < (int)w && y0 + DWT_TH < (int)h) {   // interior tile
+        const int32_t* s0 = src + (size_t)(y0 - 2) * sstride + (x0 - 2);
+        for (int ly = ty; ly < DWT_LH; ly += 4) {
+            const int32_t* sr = s0 + (size_t)ly * sstride;
+            T[ly][tx] = sr[tx];
+            T[ly][tx + 64] = sr[tx + 64];
+            if (tx < DWT_LW - 128) T[ly][tx + 128] = sr[tx + 128];
+        }
+    } else {
+        for (int i = tid; i < DWT_LH * DWT_LW; i += 256) {
+            int ly = i / DWT_LW, lx = i % DWT_LW;
+            int gy = mirror(y0 - 2 + ly, (int)h), gx = mirror(x0 - 2 + lx, (int)w);
+            T[ly][lx] = src[(size_t)gy * sstride + gx];
+        }
     }
     LDS_BARRIER();
     if (h > 1) {
         // vertical predict: odd absolute rows y in [y0-1, y0+TH-1]  (local ly = y - y0 + 2, odd y <=> ly odd)
-        for (int i = tid; i < (DWT_TH / 2 + 1) * DWT_LW; i += 256) {
-            int k = i / DWT_LW, lx = i % DWT_LW;
-            int ly = 1 + 2 * k;   // y = y0 - 1 + 2k
-            T[ly][lx] -= (T[ly - 1][lx] + T[ly + 1][lx]) >> 1;
+        for (int k = ty; k <= DWT_TH / 2; k += 4) {
+            const int ly = 1 + 2 * k;   // y = y0 - 1 + 2k
+            for (int lx = tx; lx < DWT_LW; lx += 64) T[ly][lx] -= (T[ly - 1][lx] + T[ly + 1][lx]) >> 1;
         }
         LDS_BARRIER();
         // vertical update: even rows y in [y0, y0+TH-2]: ly = 2 + 2k
-        for (int i = tid; i < (DWT_TH / 2) * DWT_LW; i += 256) {
-            int k = i / DWT_LW, lx = i % DWT_LW;
-            int ly = 2 + 2 * k;
-            T[ly][lx] += (T[ly - 1][lx] + T[ly + 1][lx] + 2) >> 2;
+        for (int k = ty; k < DWT_TH / 2; k += 4) {
+            const int ly = 2 + 2 * k;
+            for (int lx = tx; lx < DWT_LW; lx += 64) T[ly][lx] += (T[ly - 1][lx] + T[ly + 1][lx] + 2) >> 2;
         }
         LDS_BARRIER();
     }
     if (w > 1) {
-        // horizontal predict on rows ly in [2, TH+2): odd cols lx = 1 + 2k
-        for (int i = tid; i < DWT_TH * (DWT_TW / 2 + 1); i += 256) {
-            int ly = 2 + i / (DWT_TW / 2 + 1), k = i % (DWT_TW / 2 + 1);
-            int lx = 1 + 2 * k;
-            T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1]) >> 1;
-        }
+        // horizontal predict on rows ly in [2, TH+2): odd cols lx = 1 + 2k, k in [0, TW/2]
+        for (int ly = 2 + ty; ly < DWT_TH + 2; ly += 4)
+            for (int k = tx; k <= DWT_TW / 2; k += 64) {
+                const int lx = 1 + 2 * k;
+                T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1]) >> 1;
+            }
         LDS_BARRIER();
-        for (int i = tid; i < DWT_TH * (DWT_TW / 2); i += 256) {
-            int ly = 2 + i / (DWT_TW / 2), k = i % (DWT_TW / 2);
-            int lx = 2 + 2 * k;
+        for (int ly = 2 + ty; ly < DWT_TH + 2; ly += 4) {
+            const int lx = 2 + 2 * tx;   // k = tx in [0, TW/2)
             T[ly][lx] += (T[ly][lx - 1] + T[ly][lx + 1] + 2) >> 2;
         }
         LDS_BARRIER();
     }
-    // scatter to quadrants
+    // scatter to quadrants: lane tx writes L and H sample k = tx of each row (coalesced rows)
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
-    for (int i = tid; i < DWT_TH * DWT_TW; i += 256) {
-        int ry = i / DWT_TW, rx = i % DWT_TW;
-        // iterate so that consecutive threads write consecutive outputs of one quadrant row:
-        int q = rx / (DWT_TW / 2);           // 0: even columns (L), 1: odd columns (H)
-        int k = rx % (DWT_TW / 2);
-        int gx = x0 + 2 * k + q, gy = y0 + ry;
-        if (gx >= (int)w || gy >= (int)h) continue;
-        int32_t v = T[ry + 2][2 + 2 * k + q];
-        int ox = (q == 0) ? (gx >> 1) : (snw + (gx >> 1));
-        int oy = ((gy & 1) == 0) ? (gy >> 1) : (snh + (gy >> 1));
-        dst[(size_t)oy * dstride + ox] = v;
+    const bool full = x0 + DWT_TW <= (int)w && y0 + DWT_TH <= (int)h;
+    for (int ry = ty; ry < DWT_TH; ry += 4) {
+        const int gy = y0 + ry;
+        if (!full && gy >= (int)h) break;
+        const int oy = ((gy & 1) == 0) ? (gy >> 1) : (snh + (gy >> 1));
+        int32_t* drow = dst + (size_t)oy * dstride;
+        const int gxl = x0 + 2 * tx;
+        if (full || gxl < (int)w) drow[gxl >> 1] = T[ry + 2][2 + 2 * tx];
+        if (full || gxl + 1 < (int)w) drow[snw + (gxl >> 1)] = T[ry + 2][3 + 2 * tx];
     }
 }
 
@@ -197,50 +205,62 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
     src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
     const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH;
     const int tid = threadIdx.x;
+    const int tx = tid & 63, ty = tid >> 6;   // as in the forward level
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
-    for (int i = tid; i < IDWT_LH * IDWT_LW; i += 256) {
-        int ly = i / IDWT_LW, lx = i % IDWT_LW;
-        int gy = mirror(y0 - 1 + ly, (int)h), gx = mirror(x0 - 1 + lx, (int)w);
-        int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
-        int sx = (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1);
-        T[ly][lx] = src[(size_t)sy * sstride + sx];
+    if (x0 >= 1 && y0 >= 1 && x0 + DWT_TW + 1 < (int)w && y0 + DWT_TH + 1 < (int)h) {   // interior tile
+        // interleaved column gx = x0 - 1 + lx: odd lx <=> even gx (L sample x0/2 + k, lx = 1 + 2k),
+        // even lx <=> odd gx (H sample x0/2 - 1 + k, lx = 2k); both reads are contiguous
+        for (int ly = ty; ly < IDWT_LH; ly += 4) {
+            const int gy = y0 - 1 + ly;
+            const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
+            const int32_t* sr = src + (size_t)sy * sstride;
+            for (int k = tx; k <= DWT_TW / 2; k += 64) T[ly][1 + 2 * k] = sr[(x0 >> 1) + k];
+            for (int k = tx; k <= DWT_TW / 2 + 1; k += 64) T[ly][2 * k] = sr[snw + (x0 >> 1) - 1 + k];
+        }
+    } else {
+        for (int i = tid; i < IDWT_LH * IDWT_LW; i += 256) {
+            int ly = i / IDWT_LW, lx = i % IDWT_LW;
+            int gy = mirror(y0 - 1 + ly, (int)h), gx = mirror(x0 - 1 + lx, (int)w);
+            int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
+            int sx = (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1);
+            T[ly][lx] = src[(size_t)sy * sstride + sx];
+        }
     }
     LDS_BARRIER();
     if (w > 1) {
         // horizontal step 1: even interleaved cols x (lx = x - x0 + 1): x even <=> lx odd, lx in [1, TW+1]
-        for (int i = tid; i < IDWT_LH * (DWT_TW / 2 + 1); i += 256) {
-            int ly = i / (DWT_TW / 2 + 1), k = i % (DWT_TW / 2 + 1);
-            int lx = 1 + 2 * k;
-            T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1] + 2) >> 2;
-        }
+        for (int ly = ty; ly < IDWT_LH; ly += 4)
+            for (int k = tx; k <= DWT_TW / 2; k += 64) {
+                const int lx = 1 + 2 * k;
+                T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1] + 2) >> 2;
+            }
         LDS_BARRIER();
-        // step 2: odd cols x in [x0+1, x0+TW-1]: lx = 2 + 2k
-        for (int i = tid; i < IDWT_LH * (DWT_TW / 2); i += 256) {
-            int ly = i / (DWT_TW / 2), k = i % (DWT_TW / 2);
-            int lx = 2 + 2 * k;
+        // step 2: odd cols x in [x0+1, x0+TW-1]: lx = 2 + 2k, k = tx
+        for (int ly = ty; ly < IDWT_LH; ly += 4) {
+            const int lx = 2 + 2 * tx;
             T[ly][lx] += (T[ly][lx - 1] + T[ly][lx + 1]) >> 1;
         }
         LDS_BARRIER();
     }
     if (h > 1) {
-        for (int i = tid; i < (DWT_TH / 2 + 1) * DWT_TW; i += 256) {
-            int k = i / DWT_TW, lx = 1 + i % DWT_TW;
-            int ly = 1 + 2 * k;
-            T[ly][lx] -= (T[ly - 1][lx] + T[ly + 1][lx] + 2) >> 2;
+        for (int k = ty; k <= DWT_TH / 2; k += 4) {
+            const int ly = 1 + 2 * k;
+            for (int lx = 1 + tx; lx <= DWT_TW; lx += 64) T[ly][lx] -= (T[ly - 1][lx] + T[ly + 1][lx] + 2) >> 2;
         }
         LDS_BARRIER();
-        for (int i = tid; i < (DWT_TH / 2) * DWT_TW; i += 256) {
-            int k = i / DWT_TW, lx = 1 + i % DWT_TW;
-            int ly = 2 + 2 * k;
-            T[ly][lx] += (T[ly - 1][lx] + T[ly + 1][lx]) >> 1;
+        for (int k = ty; k < DWT_TH / 2; k += 4) {
+            const int ly = 2 + 2 * k;
+            for (int lx = 1 + tx; lx <= DWT_TW; lx += 64) T[ly][lx] += (T[ly - 1][lx] + T[ly + 1][lx]) >> 1;
         }
         LDS_BARRIER();
     }
-    for (int i = tid; i < DWT_TH * DWT_TW; i += 256) {
-        int ry = i / DWT_TW, rx = i % DWT_TW;
-        int gx = x0 + rx, gy = y0 + ry;
-        if (gx >= (int)w || gy >= (int)h) continue;
-        dst[(size_t)gy * dstride + gx] = T[ry + 1][rx + 1];
+    const bool full = x0 + DWT_TW <= (int)w && y0 + DWT_TH <= (int)h;
+    for (int ry = ty; ry < DWT_TH; ry += 4) {
+        const int gy = y0 + ry;
+        if (!full && gy >= (int)h) break;
+        int32_t* drow = dst + (size_t)gy * dstride + x0;
+        for (int c = tx; c < DWT_TW; c += 64)
+            if (full || x0 + c < (int)w) drow[c] = T[ry + 1][c + 1];
     }
 }
 
