@@ -141,7 +141,10 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
             const int32_t* sr = s0 + (size_t)ly * sstride;
             T[ly][tx] = sr[tx];
             T[ly][tx + 64] = sr[tx + 64];
-            if (tx < DWT_LW - 128) T[ly][tx + 128] = sr[tx + 128];
+        }
+        for (int i = tid; i < 3 * DWT_LH; i += 256) {   // columns 128..130
+            const int ly = i / 3, lx = 128 + i % 3;
+            T[ly][lx] = s0[(size_t)ly * sstride + lx];
         }
     } else {
         for (int i = tid; i < DWT_LH * DWT_LW; i += 256) {
@@ -153,25 +156,38 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
     LDS_BARRIER();
     if (h > 1) {
         // vertical predict: odd absolute rows y in [y0-1, y0+TH-1]  (local ly = y - y0 + 2, odd y <=> ly odd)
+        // (columns 0..127 by every lane, the halo columns 128..130 as one extra pass: a loop
+        // tail that only a few lanes enter would cost a full pass per row)
         for (int k = ty; k <= DWT_TH / 2; k += 4) {
             const int ly = 1 + 2 * k;   // y = y0 - 1 + 2k
-            for (int lx = tx; lx < DWT_LW; lx += 64) T[ly][lx] -= (T[ly - 1][lx] + T[ly + 1][lx]) >> 1;
+            for (int lx = tx; lx < 128; lx += 64) T[ly][lx] -= (T[ly - 1][lx] + T[ly + 1][lx]) >> 1;
+        }
+        if (tid < 3 * (DWT_TH / 2 + 1)) {
+            const int ly = 1 + 2 * (tid / 3), lx = 128 + tid % 3;
+            T[ly][lx] -= (T[ly - 1][lx] + T[ly + 1][lx]) >> 1;
         }
         LDS_BARRIER();
         // vertical update: even rows y in [y0, y0+TH-2]: ly = 2 + 2k
         for (int k = ty; k < DWT_TH / 2; k += 4) {
             const int ly = 2 + 2 * k;
-            for (int lx = tx; lx < DWT_LW; lx += 64) T[ly][lx] += (T[ly - 1][lx] + T[ly + 1][lx] + 2) >> 2;
+            for (int lx = tx; lx < 128; lx += 64) T[ly][lx] += (T[ly - 1][lx] + T[ly + 1][lx] + 2) >> 2;
+        }
+        if (tid < 3 * (DWT_TH / 2)) {
+            const int ly = 2 + 2 * (tid / 3), lx = 128 + tid % 3;
+            T[ly][lx] += (T[ly - 1][lx] + T[ly + 1][lx] + 2) >> 2;
         }
         LDS_BARRIER();
     }
     if (w > 1) {
         // horizontal predict on rows ly in [2, TH+2): odd cols lx = 1 + 2k, k in [0, TW/2]
-        for (int ly = 2 + ty; ly < DWT_TH + 2; ly += 4)
-            for (int k = tx; k <= DWT_TW / 2; k += 64) {
-                const int lx = 1 + 2 * k;
-                T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1]) >> 1;
-            }
+        for (int ly = 2 + ty; ly < DWT_TH + 2; ly += 4) {
+            const int lx = 1 + 2 * tx;
+            T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1]) >> 1;
+        }
+        if (tid < DWT_TH) {   // k = TW/2 (lx = TW + 1) of every row
+            const int ly = 2 + tid, lx = DWT_TW + 1;
+            T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1]) >> 1;
+        }
         LDS_BARRIER();
         for (int ly = 2 + ty; ly < DWT_TH + 2; ly += 4) {
             const int lx = 2 + 2 * tx;   // k = tx in [0, TW/2)
@@ -214,8 +230,14 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
             const int gy = y0 - 1 + ly;
             const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
             const int32_t* sr = src + (size_t)sy * sstride;
-            for (int k = tx; k <= DWT_TW / 2; k += 64) T[ly][1 + 2 * k] = sr[(x0 >> 1) + k];
-            for (int k = tx; k <= DWT_TW / 2 + 1; k += 64) T[ly][2 * k] = sr[snw + (x0 >> 1) - 1 + k];
+            T[ly][1 + 2 * tx] = sr[(x0 >> 1) + tx];
+            T[ly][2 * tx] = sr[snw + (x0 >> 1) - 1 + tx];
+        }
+        for (int i = tid; i < 3 * IDWT_LH; i += 256) {   // lx 128 (H), 129 (L), 130 (H)
+            const int ly = i / 3, j = i % 3, gy = y0 - 1 + ly;
+            const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
+            const int32_t* sr = src + (size_t)sy * sstride;
+            T[ly][128 + j] = (j == 1) ? sr[(x0 >> 1) + 64] : sr[snw + (x0 >> 1) + 63 + (j >> 1)];
         }
     } else {
         for (int i = tid; i < IDWT_LH * IDWT_LW; i += 256) {
@@ -229,11 +251,14 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
     LDS_BARRIER();
     if (w > 1) {
         // horizontal step 1: even interleaved cols x (lx = x - x0 + 1): x even <=> lx odd, lx in [1, TW+1]
-        for (int ly = ty; ly < IDWT_LH; ly += 4)
-            for (int k = tx; k <= DWT_TW / 2; k += 64) {
-                const int lx = 1 + 2 * k;
-                T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1] + 2) >> 2;
-            }
+        for (int ly = ty; ly < IDWT_LH; ly += 4) {
+            const int lx = 1 + 2 * tx;
+            T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1] + 2) >> 2;
+        }
+        if (tid < IDWT_LH) {   // k = TW/2 (lx = TW + 1) of every row
+            const int ly = tid, lx = DWT_TW + 1;
+            T[ly][lx] -= (T[ly][lx - 1] + T[ly][lx + 1] + 2) >> 2;
+        }
         LDS_BARRIER();
         // step 2: odd cols x in [x0+1, x0+TW-1]: lx = 2 + 2k, k = tx
         for (int ly = ty; ly < IDWT_LH; ly += 4) {
