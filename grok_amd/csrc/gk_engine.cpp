@@ -582,14 +582,18 @@ struct ByteSrc {
         }
         return false;
     }
+    static std::atomic<uint64_t> fetch_ns, fetch_cnt;   // GK_PROFILE: synchronous page fetches
     const uint8_t* page(size_t pg) {
         auto it = pages.find(pg);
         if (it == pages.end()) {
+            const auto t0 = std::chrono::steady_clock::now();
             size_t o = pg * PG, n = std::min(PG, len - o);
             std::vector<uint8_t> v(n);
             HIPCHK(hipMemcpyAsync(v.data(), dev + o, n, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             it = pages.emplace(pg, std::move(v)).first;
+            fetch_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+            ++fetch_cnt;
         }
         return it->second.data();
     }
@@ -621,6 +625,7 @@ struct ByteSrc {
         return last;
     }
 };
+std::atomic<uint64_t> ByteSrc::fetch_ns{0}, ByteSrc::fetch_cnt{0};
 // Packet-header bit reader (T2Decompress / BitIO: a byte after 0xFF carries 7 bits).  Bytes
 // come from a cached contiguous span of the source; bits are taken several at a time.
 struct BitReader {
@@ -666,21 +671,31 @@ struct DecTree {   // decoder-side tag tree
         TagTree t; t.build(nw, nh);
         parent = t.parent; value.assign(parent.size(), 0xffffffffu); low.assign(parent.size(), 0);
     }
+    // TagTree::decode (TagTree.h): walk from the root to the leaf reading bits until each
+    // node's value or the threshold is reached.  A node with nothing left to read at this
+    // threshold (low >= min(threshold, value)) has only such nodes above it — a node is
+    // processed only after its parent, and thresholds never decrease — and its final `lo` is
+    // its `low`, so the walk starts below the first such node met going up from the leaf
+    // (for raster-order leaves that is usually the leaf's parent).
     uint32_t decode(BitReader& br, uint32_t leaf, uint32_t threshold) {
         int32_t stk[40]; int sp = 0; int32_t n = (int32_t)leaf;
-        while (parent[n] >= 0) { stk[sp++] = n; n = parent[n]; }
         uint32_t lo = 0;
         while (true) {
+            if (low[n] >= std::min(threshold, value[n])) { lo = low[n]; break; }
+            stk[sp++] = n;
+            if (parent[n] < 0) break;
+            n = parent[n];
+        }
+        while (sp) {
+            n = stk[--sp];
             if (low[n] < lo) low[n] = lo; else lo = low[n];
             while (lo < threshold && lo < value[n]) {
                 if (br.read(1)) { value[n] = lo; break; }
                 ++lo;
             }
             low[n] = lo;
-            if (!sp) break;
-            n = stk[--sp];
         }
-        return value[n];
+        return value[leaf];
     }
 };
 
@@ -2028,8 +2043,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     }
     const uint8_t* src_bytes = stg;
     if (prof)
-        fprintf(stderr, "decode host: headers+setup %.3f ms, packet headers %.3f ms, segments %.3f ms (%zu parts)\n",
-                ms(h0, h1), ms(h1, h2), ms(h2, now()), Hd.parts.size());
+        fprintf(stderr, "decode host: headers+setup %.3f ms, packet headers %.3f ms, segments %.3f ms (%zu parts); "
+                        "%llu page fetches %.3f ms (cumulative)\n",
+                ms(h0, h1), ms(h1, h2), ms(h2, now()), Hd.parts.size(), (unsigned long long)ByteSrc::fetch_cnt.load(),
+                ByteSrc::fetch_ns.load() * 1e-6);
     GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * std::max(nb, 1u));
     GkBlock* hblk = (GkBlock*)ctx->hinfo.get(sizeof(GkBlock) * std::max(nb, 1u));
     memcpy(hblk, blk.data(), sizeof(GkBlock) * nb);
