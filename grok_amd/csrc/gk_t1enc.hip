@@ -384,7 +384,7 @@ __device__ __forceinline__ void mql_put_sel(MqLane& q, bool en, uint32_t cur) {
 // boundary (CT = 0) falls inside the shift, BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127) runs on
 // C >> e, e = the bits shifted past the boundary; they stay below the new byte, whose CT
 // (8, or 7 after 0xFF) is reduced by e.  A second boundary in one renormalisation (e >= 8)
-// repeats the BYTEOUT (rare; at most two for shifts <= 15).
+// repeats the BYTEOUT (rare; at most two for shifts <= 15: after the first, e <= 14 - 7).
 __device__ __forceinline__ void mq_code3(MqLane& q, Ctx5e& cw, const uint32_t* tab, uint32_t s, bool en) {
     const uint32_t cx = s >> 1, d = s & 1;
     const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
@@ -409,8 +409,7 @@ __device__ __forceinline__ void mq_code3(MqLane& q, Ctx5e& cw, const uint32_t* t
     q.a = an << n;
     uint64_t c = (uint64_t)(q.c + ((en & x) ? qe : 0u)) << n;
     int ct = (int)q.ct - (int)n;
-    bool bo = ct <= 0;
-    while (__any(bo)) {
+    auto byteout = [&](bool bo) {
         const uint32_t sh = bo ? (uint32_t)(-ct) : 0u;
         const uint32_t carry = (bo & (q.cur != 0xff)) ? (uint32_t)(c >> (27 + sh)) & 1u : 0u;
         const uint32_t cur = q.cur + carry;
@@ -422,8 +421,11 @@ __device__ __forceinline__ void mq_code3(MqLane& q, Ctx5e& cw, const uint32_t* t
         const uint64_t keep = ((uint64_t)(ff ? 0x100000u : 0x80000u) << sh) - 1;
         c = bo ? (c & keep) : c;
         ct = bo ? (ff ? 7 : 8) - (int)sh : ct;
-        bo = ct <= 0;
-    }
+    };
+    // straight-line: some lane of the wave crosses a byte boundary at almost every symbol, and
+    // a loop here costs register copies at its head; a second boundary (shift > CT + 7) is rare
+    byteout(ct <= 0);
+    if (__any(ct <= 0)) byteout(ct <= 0);
     q.c = (uint32_t)c;
     q.ct = (uint32_t)ct;
 }
