@@ -482,9 +482,11 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         const uint32_t cx = vsel(is_mr, cx_mr,
                                  vsel(agg, CTX_AGG,
                                       vsel(ph == PH_SIGN, CTX_SC + (sce & 15), vsel(finding, CTX_ZC + zcx, CTX_UNI))));
-        while (__any(pend && q.avail < 16)) {   // rare: a burst of long renormalisations
-            mq2_refill(q, pend && q.avail < 16);
-            q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+        if (__any(pend && q.avail < 16)) {   // rare: a burst of long renormalisations (a loop
+            do {                              // here would put its head's copies on every step)
+                mq2_refill(q, pend && q.avail < 16);
+                q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+            } while (__any(pend && q.avail < 16));
         }
         const uint32_t d = mq2_decode(q, Ls.ctx, lane, Ls.tab, cx, pend);
         nsym += pend ? 1 : 0;
