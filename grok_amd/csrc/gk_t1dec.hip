@@ -196,7 +196,7 @@ __device__ __forceinline__ uint32_t mq2_decode(Mq2& q, uint32_t (*ctx)[64], int 
     const uint32_t an = en ? (lower ? qe : a1) : q.a;
     const uint32_t ch = (en & !lower) ? chi - (qe << 16) : chi;
     const uint32_t ne = tab[nidx] | (nmps << 31);
-    if (upd) ctx[cx][lane] = ne;
+    ctx[cx][lane] = upd ? ne : e;   // unconditional: a branch here would wait on the table read
     const uint32_t n = upd ? __clz(an) - 16 : 0u;   // RENORMD: all shifts at once
     q.a = an << n;
     q.c = (((uint64_t)ch << 32) | (uint32_t)q.c) << n;
