@@ -55,6 +55,9 @@
 // ring runs low inside a dense stripe-pass takes a synchronous top-up (rare).
 // At the end of every step each lane reads the 4 bytes at its position (nb4).
 #define RING_DW 32
+#ifndef T1DEC_UNROLL
+#define T1DEC_UNROLL 8   // decision steps per stripe-boundary test (C2: 1 -> 33.5 ms, 2 -> 32.3, 4 -> 30.7, 8 -> 29.5, 16 -> 30.0)
+#endif
 __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
     // per-lane select through v_cndmask, as inline asm so the optimiser cannot turn a
     // select tree over struct fields into a dynamically indexed (scratch) access
@@ -443,96 +446,102 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
             if (TIMING) { const uint64_t t1 = __builtin_amdgcn_s_memtime(); cyc_ev += t1 - tev; tev = t1; }
         }
         if (TIMING && !tev) tev = __builtin_amdgcn_s_memtime();
-        // ---------------- one decision per active lane
-        const bool act = !done && !parked;
-        ++nstep;
-        if (__any(q.fill - q.bp < 8)) ring_topup(Ls.ring, lane, q);
-        mq2_refill(q, act && q.avail <= 40);
-        const bool finding = ph == PH_FIND;
-        // next coding position: first remaining candidate in stripe scan order
-        const uint64_t CU = C0 | C1 | C2 | C3;
-        const uint32_t xq = ((uint32_t)__ffsll((long long)CU) - 1) & 63;
-        const uint32_t c4 = col4(C0, C1, C2, C3, xq);
-        const bool use = act && finding;
-        const bool found = CU != 0;
-        x = (use && found) ? xq : x;
-        r = (use && found) ? (uint32_t)(__ffs(c4) - 1) : r;
-        const bool pend = use ? found : act;
-        parked = parked || (use && !found);
-        // neighbourhood of (x, r): guarded rows r .. r+2 (= stripe rows r-1 .. r+1)
-        const uint32_t dx = x >> 5, sx = x & 31;
-        const uint32_t o0 = (r * 3 + dx);
-        const uint32_t s0 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 1][lane], Ls.sg[o0][lane], sx) & 7;
-        const uint32_t s1 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 4][lane], Ls.sg[o0 + 3][lane], sx) & 7;
-        const uint32_t s2 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 7][lane], Ls.sg[o0 + 6][lane], sx) & 7;
-        const uint32_t n0 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 1][lane], Ls.ng[o0][lane], sx) & 7;
-        const uint32_t n1 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 4][lane], Ls.ng[o0 + 3][lane], sx) & 7;
-        const uint32_t n2 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 7][lane], Ls.ng[o0 + 6][lane], sx) & 7;
-        const uint32_t mub = (Ls.mu[r * 2 + dx][lane] >> sx) & 1;
-        const uint32_t fs = s0 | (s1 << 3) | (s2 << 6);
-        const uint32_t fn = n0 | (n1 << 3) | (n2 << 6);
-        const uint32_t sce = Ls.sc[(fs & 0xaa) | ((fn >> 1) & 0x55)];
-        const uint32_t zcx = zc[fs];
-        const bool is_cl = t == 2, is_mr = t == 1, is_sp = t == 0;
-        // a column starts in run-length mode when it was eligible at stripe start, is untouched
-        // and its left neighbour column gained no significance in this pass
-        // (bitwise, not short-circuit: keeps the step free of exec-mask branches)
-        const bool agg = is_cl & finding & (((E >> x) & 1) != 0) & (c4 == 0xf) & ((((fresh << 1) >> x) & 1) == 0);
-        const uint32_t cx_mr = vsel(mub != 0, CTX_MAG + 2, vsel((fs & 0x1ef) != 0, CTX_MAG + 1, CTX_MAG));
-        const uint32_t cx = vsel(is_mr, cx_mr,
-                                 vsel(agg, CTX_AGG,
-                                      vsel(ph == PH_SIGN, CTX_SC + (sce & 15), vsel(finding, CTX_ZC + zcx, CTX_UNI))));
-        if (__any(pend && q.avail < 16)) {   // rare: a burst of long renormalisations (a loop
-            do {                              // here would put its head's copies on every step)
-                mq2_refill(q, pend && q.avail < 16);
-                q.nb4 = ring_get4(Ls.ring, lane, q.bp);
-            } while (__any(pend && q.avail < 16));
-        }
-        const uint32_t d = mq2_decode(q, Ls.ctx, lane, Ls.tab, cx, pend);
-        nsym += pend ? 1 : 0;
-        // ---- state updates
-        const bool sig = pend && !is_mr && ph == PH_SIGN;
-        const bool negs = sig && ((d ^ (sce >> 4)) & 1);
-        const uint32_t gx = x + 1, gd = gx >> 5, gb = 1u << (gx & 31);
-        atomicOr(&Ls.sg[(r + 1) * 3 + gd][lane], sig ? gb : 0u);
-        atomicOr(&Ls.ng[(r + 1) * 3 + gd][lane], negs ? gb : 0u);
-        const bool pb = sig || (pend && is_mr && d);
-        atomicOr(&Ls.bt[r * 2 + dx][lane], pb ? (1u << sx) : 0u);
-        fresh |= (uint64_t)(sig ? 1u : 0u) << x;
-        // SP: positions after (x, r) that gain a significant neighbour become candidates:
-        // (x, r+1) and column x+1 rows r-1 .. r+1, unless significant (window bits 7; 2, 5, 8)
-        const bool spn = sig && is_sp;
-        const uint32_t nf = ~fs;
-        const uint32_t ca = spn ? ((((nf >> 7) & 1) << (r + 1)) & vr) : 0u;
-        const uint32_t t3 = ((nf >> 2) & 1) | ((nf >> 4) & 2) | ((nf >> 6) & 4);
-        const uint32_t cb = (spn && gx < w) ? (((t3 << r) >> 1) & vr) : 0u;
-        // consumption: the coded position; a whole column after a zero run-length decision;
-        // rows 0 .. rr once the run-length index rr is known
-        const uint32_t rr = (rlhi << 1) | d;
-        const uint32_t crow_f = vsel(agg, vsel(d != 0, 0u, 0xfu), 1u << r);
-        const uint32_t crow = vsel(pend, vsel(finding, crow_f, vsel(ph == PH_UNI2, (2u << rr) - 1, 0u)), 0u);
+        // ---------------- decisions: T1DEC_UNROLL steps per loop iteration.  The stripe-boundary
+        // test at the loop head then runs once per group, and more lanes are parked when it does,
+        // so events are fewer and larger (C2: 3325 -> 1891 per wave); parked lanes idle meanwhile
+#pragma unroll
+        for (int us = 0; us < T1DEC_UNROLL; ++us) {
+            // ---------------- one decision per active lane
+            const bool act = !done && !parked;
+            ++nstep;
+            if (__any(q.fill - q.bp < 8)) ring_topup(Ls.ring, lane, q);
+            mq2_refill(q, act && q.avail <= 40);
+            const bool finding = ph == PH_FIND;
+            // next coding position: first remaining candidate in stripe scan order
+            const uint64_t CU = C0 | C1 | C2 | C3;
+            const uint32_t xq = ((uint32_t)__ffsll((long long)CU) - 1) & 63;
+            const uint32_t c4 = col4(C0, C1, C2, C3, xq);
+            const bool use = act && finding;
+            const bool found = CU != 0;
+            x = (use && found) ? xq : x;
+            r = (use && found) ? (uint32_t)(__ffs(c4) - 1) : r;
+            const bool pend = use ? found : act;
+            parked = parked || (use && !found);
+            // neighbourhood of (x, r): guarded rows r .. r+2 (= stripe rows r-1 .. r+1)
+            const uint32_t dx = x >> 5, sx = x & 31;
+            const uint32_t o0 = (r * 3 + dx);
+            const uint32_t s0 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 1][lane], Ls.sg[o0][lane], sx) & 7;
+            const uint32_t s1 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 4][lane], Ls.sg[o0 + 3][lane], sx) & 7;
+            const uint32_t s2 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 7][lane], Ls.sg[o0 + 6][lane], sx) & 7;
+            const uint32_t n0 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 1][lane], Ls.ng[o0][lane], sx) & 7;
+            const uint32_t n1 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 4][lane], Ls.ng[o0 + 3][lane], sx) & 7;
+            const uint32_t n2 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 7][lane], Ls.ng[o0 + 6][lane], sx) & 7;
+            const uint32_t mub = (Ls.mu[r * 2 + dx][lane] >> sx) & 1;
+            const uint32_t fs = s0 | (s1 << 3) | (s2 << 6);
+            const uint32_t fn = n0 | (n1 << 3) | (n2 << 6);
+            const uint32_t sce = Ls.sc[(fs & 0xaa) | ((fn >> 1) & 0x55)];
+            const uint32_t zcx = zc[fs];
+            const bool is_cl = t == 2, is_mr = t == 1, is_sp = t == 0;
+            // a column starts in run-length mode when it was eligible at stripe start, is untouched
+            // and its left neighbour column gained no significance in this pass
+            // (bitwise, not short-circuit: keeps the step free of exec-mask branches)
+            const bool agg = is_cl & finding & (((E >> x) & 1) != 0) & (c4 == 0xf) & ((((fresh << 1) >> x) & 1) == 0);
+            const uint32_t cx_mr = vsel(mub != 0, CTX_MAG + 2, vsel((fs & 0x1ef) != 0, CTX_MAG + 1, CTX_MAG));
+            const uint32_t cx = vsel(is_mr, cx_mr,
+                                     vsel(agg, CTX_AGG,
+                                          vsel(ph == PH_SIGN, CTX_SC + (sce & 15), vsel(finding, CTX_ZC + zcx, CTX_UNI))));
+            if (__any(pend && q.avail < 16)) {   // rare: a burst of long renormalisations (a loop
+                do {                              // here would put its head's copies on every step)
+                    mq2_refill(q, pend && q.avail < 16);
+                    q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+                } while (__any(pend && q.avail < 16));
+            }
+            const uint32_t d = mq2_decode(q, Ls.ctx, lane, Ls.tab, cx, pend);
+            nsym += pend ? 1 : 0;
+            // ---- state updates
+            const bool sig = pend && !is_mr && ph == PH_SIGN;
+            const bool negs = sig && ((d ^ (sce >> 4)) & 1);
+            const uint32_t gx = x + 1, gd = gx >> 5, gb = 1u << (gx & 31);
+            atomicOr(&Ls.sg[(r + 1) * 3 + gd][lane], sig ? gb : 0u);
+            atomicOr(&Ls.ng[(r + 1) * 3 + gd][lane], negs ? gb : 0u);
+            const bool pb = sig || (pend && is_mr && d);
+            atomicOr(&Ls.bt[r * 2 + dx][lane], pb ? (1u << sx) : 0u);
+            fresh |= (uint64_t)(sig ? 1u : 0u) << x;
+            // SP: positions after (x, r) that gain a significant neighbour become candidates:
+            // (x, r+1) and column x+1 rows r-1 .. r+1, unless significant (window bits 7; 2, 5, 8)
+            const bool spn = sig && is_sp;
+            const uint32_t nf = ~fs;
+            const uint32_t ca = spn ? ((((nf >> 7) & 1) << (r + 1)) & vr) : 0u;
+            const uint32_t t3 = ((nf >> 2) & 1) | ((nf >> 4) & 2) | ((nf >> 6) & 4);
+            const uint32_t cb = (spn && gx < w) ? (((t3 << r) >> 1) & vr) : 0u;
+            // consumption: the coded position; a whole column after a zero run-length decision;
+            // rows 0 .. rr once the run-length index rr is known
+            const uint32_t rr = (rlhi << 1) | d;
+            const uint32_t crow_f = vsel(agg, vsel(d != 0, 0u, 0xfu), 1u << r);
+            const uint32_t crow = vsel(pend, vsel(finding, crow_f, vsel(ph == PH_UNI2, (2u << rr) - 1, 0u)), 0u);
 #define GK_CROW(Ci, Pi, i)                                                                                           \
-    {                                                                                                                \
-        const uint64_t add = (uint64_t)(((ca >> i) & 1) | (((cb >> i) & 1) << 1)) << x;                             \
-        const uint64_t clr = (uint64_t)((crow >> i) & 1) << x;                                                       \
-        Ci = (Ci & ~clr) | add;                                                                                      \
-        Pi |= add;                                                                                                   \
-    }
-        GK_CROW(C0, P0, 0) GK_CROW(C1, P1, 1) GK_CROW(C2, P2, 2) GK_CROW(C3, P3, 3)
+        {                                                                                                                \
+            const uint64_t add = (uint64_t)(((ca >> i) & 1) | (((cb >> i) & 1) << 1)) << x;                             \
+            const uint64_t clr = (uint64_t)((crow >> i) & 1) << x;                                                       \
+            Ci = (Ci & ~clr) | add;                                                                                      \
+            Pi |= add;                                                                                                   \
+        }
+            GK_CROW(C0, P0, 0) GK_CROW(C1, P1, 1) GK_CROW(C2, P2, 2) GK_CROW(C3, P3, 3)
 #undef GK_CROW
-        // phase machine: FIND -(ZC 1)-> SIGN -> FIND; FIND(run-length) -(1)-> UNI1 -> UNI2 -> SIGN
-        // next phase = table[ph][d][agg] (MR always stays in FIND), 2 bits per entry
-        //   FIND: agg ? (d ? UNI1 : FIND) : (d ? SIGN : FIND); SIGN -> FIND; UNI1 -> UNI2; UNI2 -> SIGN
-        const bool uni1 = ph == PH_UNI1, uni2 = ph == PH_UNI2;
-        const uint32_t key = (ph << 2) | (d << 1) | (agg ? 1u : 0u);
-        constexpr uint32_t kPhT = (0u << 0) | (0u << 2) | (PH_SIGN << 4) | (PH_UNI1 << 6)       // FIND
-                                | (PH_UNI2 << 16) | (PH_UNI2 << 18) | (PH_UNI2 << 20) | (PH_UNI2 << 22)  // UNI1
-                                | (PH_SIGN << 24) | (PH_SIGN << 26) | (PH_SIGN << 28) | (PH_SIGN << 30); // UNI2
-        const uint32_t nph = is_mr ? (uint32_t)PH_FIND : ((kPhT >> (2 * key)) & 3);
-        rlhi = vsel(pend & uni1, d, rlhi);
-        r = vsel(pend & uni2, rr, r);
-        ph = vsel(pend, nph, ph);
-        q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+            // phase machine: FIND -(ZC 1)-> SIGN -> FIND; FIND(run-length) -(1)-> UNI1 -> UNI2 -> SIGN
+            // next phase = table[ph][d][agg] (MR always stays in FIND), 2 bits per entry
+            //   FIND: agg ? (d ? UNI1 : FIND) : (d ? SIGN : FIND); SIGN -> FIND; UNI1 -> UNI2; UNI2 -> SIGN
+            const bool uni1 = ph == PH_UNI1, uni2 = ph == PH_UNI2;
+            const uint32_t key = (ph << 2) | (d << 1) | (agg ? 1u : 0u);
+            constexpr uint32_t kPhT = (0u << 0) | (0u << 2) | (PH_SIGN << 4) | (PH_UNI1 << 6)       // FIND
+                                    | (PH_UNI2 << 16) | (PH_UNI2 << 18) | (PH_UNI2 << 20) | (PH_UNI2 << 22)  // UNI1
+                                    | (PH_SIGN << 24) | (PH_SIGN << 26) | (PH_SIGN << 28) | (PH_SIGN << 30); // UNI2
+            const uint32_t nph = is_mr ? (uint32_t)PH_FIND : ((kPhT >> (2 * key)) & 3);
+            rlhi = vsel(pend & uni1, d, rlhi);
+            r = vsel(pend & uni2, rr, r);
+            ph = vsel(pend, nph, ph);
+            q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+        }
         if (TIMING) cyc_step += __builtin_amdgcn_s_memtime() - tev;
     }
     unsigned long long cp[6] = {0, 0, 0, 0, 0, 0};
