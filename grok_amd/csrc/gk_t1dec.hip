@@ -101,8 +101,8 @@ template <class Q> __device__ __forceinline__ void ring_boundary(uint32_t (*ring
     }
 }
 // inside a step loop: synchronous top-up for a lane about to run dry
-template <class Q> __device__ __forceinline__ void ring_topup(uint32_t (*ring)[64], int lane, Q& q) {
-    if (q.fill - q.bp < 8) {
+template <class Q> __device__ __forceinline__ void ring_topup(uint32_t (*ring)[64], int lane, Q& q, uint32_t low) {
+    if (q.fill - q.bp < low) {
         ring_write16(ring, lane, q.fill, *win(q.p, q.fill, q.len));
         q.fill += 16;
     }
@@ -449,12 +449,18 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         // ---------------- decisions: T1DEC_UNROLL steps per loop iteration.  The stripe-boundary
         // test at the loop head then runs once per group, and more lanes are parked when it does,
         // so events are fewer and larger (C2: 3325 -> 1891 per wave); parked lanes idle meanwhile
+        // a step takes at most 3 ring bytes (one refill, two in a renormalisation burst), and
+        // ring_get4 looks 4 ahead: 3 * T1DEC_UNROLL + 4 <= 32 bytes must be staged per group
+        static_assert(3 * T1DEC_UNROLL + 4 <= 32, "ring top-up margin");
+        if (__any(q.fill - q.bp < 32)) {
+            ring_topup(Ls.ring, lane, q, 32);
+            if (__any(q.fill - q.bp < 32)) ring_topup(Ls.ring, lane, q, 32);
+        }
 #pragma unroll
         for (int us = 0; us < T1DEC_UNROLL; ++us) {
             // ---------------- one decision per active lane
             const bool act = !done && !parked;
             ++nstep;
-            if (__any(q.fill - q.bp < 8)) ring_topup(Ls.ring, lane, q);
             mq2_refill(q, act && q.avail <= 40);
             const bool finding = ph == PH_FIND;
             // next coding position: first remaining candidate in stripe scan order
