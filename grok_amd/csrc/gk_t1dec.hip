@@ -449,19 +449,24 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         // ---------------- decisions: T1DEC_UNROLL steps per loop iteration.  The stripe-boundary
         // test at the loop head then runs once per group, and more lanes are parked when it does,
         // so events are fewer and larger (C2: 3325 -> 1891 per wave); parked lanes idle meanwhile
-        // a step takes at most 3 ring bytes (one refill, two in a renormalisation burst), and
-        // ring_get4 looks 4 ahead: 3 * T1DEC_UNROLL + 4 <= 32 bytes must be staged per group
-        static_assert(3 * T1DEC_UNROLL + 4 <= 32, "ring top-up margin");
+        // The code register is refilled to > 40 bits once per group (at most 6 bytes); a step
+        // then takes ring bytes only in a renormalisation burst (at most 2: a decision needs 16
+        // bits and leaves at least 1), and ring_get4 looks 4 ahead: 6 + 2 * T1DEC_UNROLL + 4
+        // <= 32 bytes must be staged per group.  q.nb4 stays valid while bp does not move.
+        static_assert(6 + 2 * T1DEC_UNROLL + 4 <= 32, "ring top-up margin");
         if (__any(q.fill - q.bp < 32)) {
             ring_topup(Ls.ring, lane, q, 32);
             if (__any(q.fill - q.bp < 32)) ring_topup(Ls.ring, lane, q, 32);
+        }
+        while (__any(!done && q.avail <= 40)) {
+            mq2_refill(q, !done && q.avail <= 40);
+            q.nb4 = ring_get4(Ls.ring, lane, q.bp);
         }
 #pragma unroll
         for (int us = 0; us < T1DEC_UNROLL; ++us) {
             // ---------------- one decision per active lane
             const bool act = !done && !parked;
             ++nstep;
-            mq2_refill(q, act && q.avail <= 40);
             const bool finding = ph == PH_FIND;
             // next coding position: first remaining candidate in stripe scan order
             const uint64_t CU = C0 | C1 | C2 | C3;
@@ -546,7 +551,6 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
             rlhi = vsel(pend & uni1, d, rlhi);
             r = vsel(pend & uni2, rr, r);
             ph = vsel(pend, nph, ph);
-            q.nb4 = ring_get4(Ls.ring, lane, q.bp);
         }
         if (TIMING) cyc_step += __builtin_amdgcn_s_memtime() - tev;
     }
