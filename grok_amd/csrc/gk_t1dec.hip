@@ -56,7 +56,7 @@
 // At the end of every step each lane reads the 4 bytes at its position (nb4).
 #define RING_DW 32
 #ifndef T1DEC_UNROLL
-#define T1DEC_UNROLL 8   // decision steps per stripe-boundary test (C2: 1 -> 33.5 ms, 2 -> 32.3, 4 -> 30.7, 8 -> 29.5, 16 -> 30.0)
+#define T1DEC_UNROLL 12   // decision steps per stripe-boundary test (C2 decoder: 1 -> 33.5 ms, 8 -> 26.4, 12 -> 25.8, 16 -> 26.3)
 #endif
 __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
     // per-lane select through v_cndmask, as inline asm so the optimiser cannot turn a
@@ -452,12 +452,10 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
         // The code register is refilled to > 40 bits once per group (at most 6 bytes); a step
         // then takes ring bytes only in a renormalisation burst (at most 2: a decision needs 16
         // bits and leaves at least 1), and ring_get4 looks 4 ahead: 6 + 2 * T1DEC_UNROLL + 4
-        // <= 32 bytes must be staged per group.  q.nb4 stays valid while bp does not move.
-        static_assert(6 + 2 * T1DEC_UNROLL + 4 <= 32, "ring top-up margin");
-        if (__any(q.fill - q.bp < 32)) {
-            ring_topup(Ls.ring, lane, q, 32);
-            if (__any(q.fill - q.bp < 32)) ring_topup(Ls.ring, lane, q, 32);
-        }
+        // bytes must be staged per group (kMargin).  q.nb4 stays valid while bp does not move.
+        constexpr uint32_t kMargin = (6 + 2 * T1DEC_UNROLL + 4 + 15) / 16 * 16;
+        static_assert(kMargin + 16 + 32 <= 4 * RING_DW, "ring top-up margin");
+        while (__any(q.fill - q.bp < kMargin)) ring_topup(Ls.ring, lane, q, kMargin);
         while (__any(!done && q.avail <= 40)) {
             mq2_refill(q, !done && q.avail <= 40);
             q.nb4 = ring_get4(Ls.ring, lane, q.bp);
