@@ -34,7 +34,7 @@
 namespace {
 
 static inline uint32_t ceildivpow2(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + (1ull << b) - 1) >> b); }
-static inline int floorlog2(uint32_t a) { int l = 0; while (a > 1) { a >>= 1; ++l; } return l; }
+static inline int floorlog2(uint32_t a) { return a > 1 ? 31 - __builtin_clz(a) : 0; }
 static inline uint32_t align_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { throw GkError(std::string(#x) + ": " + hipGetErrorString(e_)); } } while (0)
@@ -444,6 +444,7 @@ struct BitWriter {
     inline void wbyte() { o.push_back((uint8_t)buf); ct = (buf == 0xff) ? 7 : 8; buf = 0; }
     inline void putbit(uint32_t b) { if (ct == 0) wbyte(); --ct; buf |= b << ct; }
     inline void write(uint32_t v, int n) { for (int i = n - 1; i >= 0; --i) putbit((v >> i) & 1); }
+    inline void put(uint32_t v, uint32_t k) { write(v, (int)k); }
     void flush() { wbyte(); if (ct == 7) wbyte(); }
     void commacode(uint32_t n) { for (uint32_t i = 0; i < n; ++i) putbit(1); putbit(0); }
     void numpasses(uint32_t n) {
@@ -487,20 +488,45 @@ struct TagTree {
         int32_t n = (int32_t)leaf;
         while (n >= 0 && value[n] > v) { value[n] = v; n = parent[n]; }
     }
+    // TagTree::encode (TagTree.h): from the root to the leaf, each node emits a 0 per unit its
+    // low rises below min(value, threshold) and a 1 when it reaches a value below the
+    // threshold the first time.  A node with nothing left to emit (low >= min(value,
+    // threshold), and known if value < threshold) only has such nodes above it, and its low
+    // bounds theirs, so the walk starts below the first one met going up from the leaf
+    // (usually the leaf's parent, visited by the previous leaf); runs of bits go out at once.
     template <class W> void encode(W& bw, uint32_t leaf, uint32_t threshold) {
+        uint32_t* lw = low.data();
+        uint8_t* kn = known.data();
         int32_t stk[40]; int sp = 0; int32_t n = (int32_t)leaf;
-        while (parent[n] >= 0) { stk[sp++] = n; n = parent[n]; }
         uint32_t lo = 0;
         while (true) {
-            if (low[n] < lo) low[n] = lo; else lo = low[n];
-            while (lo < threshold) {
-                if (lo >= value[n]) { if (!known[n]) { bw.putbit(1); known[n] = 1; } break; }
-                bw.putbit(0); ++lo;
-            }
-            low[n] = lo;
-            if (!sp) break;
-            n = stk[--sp];
+            const uint32_t v = value[n];
+            if (lw[n] >= std::min(v, threshold) && (v >= threshold || kn[n])) { lo = lw[n]; break; }
+            stk[sp++] = n;
+            if (parent[n] < 0) break;
+            n = parent[n];
         }
+        while (sp) {
+            n = stk[--sp];
+            if (lw[n] < lo) lw[n] = lo; else lo = lw[n];
+            const uint32_t v = value[n];
+            if (v < threshold) {
+                const uint32_t z = v > lo ? v - lo : 0;
+                const uint32_t one = kn[n] ? 0u : 1u;
+                put_run(bw, z, one);
+                kn[n] = 1;
+                if (lo < v) lo = v;
+            } else if (lo < threshold) {
+                put_run(bw, threshold - lo, 0);
+                lo = threshold;
+            }
+            lw[n] = lo;
+        }
+    }
+    // z zero bits, then a 1 if one
+    template <class W> static inline void put_run(W& bw, uint32_t z, uint32_t one) {
+        for (; z >= 31; z -= 31) bw.put(0u, 31);
+        if (z + one) bw.put(one, z + one);
     }
 };
 
@@ -737,6 +763,15 @@ struct T2Enc {
         return passes[info[4 * (size_t)b + 3] + q].rate;
     }
     double dist(uint32_t b, uint32_t q) const { return passes[info[4 * (size_t)b + 3] + q].dist; }
+    // The pass records (tens of MB) are read one or two per code-block in block order, each
+    // a cache miss: prefetch those of the block PF ahead (its first pass not yet in packets
+    // and the last one layer l would take).
+    static constexpr uint32_t PF = 8;
+    inline void prefetch_rates(uint32_t b, uint32_t l) const {
+        const GkPass* p = passes + info[4 * (size_t)b + 3] + inprev[b];
+        __builtin_prefetch(p - 1);
+        __builtin_prefetch(p + lnp[(size_t)b * L + l] - 1);
+    }
 
     // l == 0: fresh tag trees, every code-block's zero-bit-plane count in its tree
     void band_init(const PrecG& PG, uint32_t bnb) {
@@ -757,6 +792,7 @@ struct T2Enc {
         }
         for (uint32_t k = 0; k < n; ++k) {
             uint32_t b = PG.first_block + k;
+            if (passes && k + PF < n) prefetch_rates(b + PF, l);
             uint32_t np = lnp[(size_t)b * L + l];
             if (!inprev[b]) IT.encode(bw, k, l + 1);
             else bw.putbit(np != 0);
@@ -945,20 +981,31 @@ struct T2Enc {
         if (last_ff) ++bytes;
         return bytes;
     }
+    const PrecG& unit_prec(const Unit& U, uint32_t* numbps = nullptr) const {
+        const Chain& ch = chains[U.chain];
+        const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
+        if (numbps) *numbps = R.bands[U.band].numbps;
+        return R.prc[U.band][ch.pi];
+    }
     void code_layer(uint32_t l) {   // every (packet, band) of layer l from the snapshot, in parallel
+        const auto tc0 = std::chrono::steady_clock::now();
         host_pool().run(uorder.size(), [&](size_t j) {
             const uint32_t u = uorder[j];
             const Unit& U = units[u];
-            const Chain& ch = chains[U.chain];
-            const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
-            const PrecG& PG = R.prc[U.band][ch.pi];
-            if (l) restore_band(PG); else band_init(PG, R.bands[U.band].numbps);
-            RawBits& rb = ubits[u];
+            uint32_t numbps;
+            const PrecG& PG = unit_prec(U, &numbps);
+            if (l) restore_band(PG); else band_init(PG, numbps);
+            // bits go to a thread-local writer and are swapped in at the end: units' writers
+            // sit next to each other in ubits, and a bit-at-a-time writer shared a cache line
+            // with its neighbours' (false sharing cost ~5x)
+            thread_local RawBits rb;
             rb.clear();
             band_header(PG, l, rb);
             rb.finish();
+            std::swap(rb, ubits[u]);
             ubody[u] = band_body(PG, l);
         });
+        const auto tc2 = std::chrono::steady_clock::now();
         host_pool().run(chains.size(), [&](size_t i) {
             thread_local std::vector<uint64_t> sbuf;
             uint64_t body = 0;
@@ -966,9 +1013,17 @@ struct T2Enc {
             const uint64_t h = stuffed_len(cunits[i], sbuf);
             chdr[i] = h; csize[i] = h + body;
         });
+        const auto tc3 = std::chrono::steady_clock::now();
+        auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count(); };
+        prof_code += us(tc0, tc2); prof_stuff += us(tc2, tc3);
         static const bool check = getenv("GK_T2_CHECK_SIM") != nullptr;
         if (check) {   // debug: the packets' real sizes (write_packet) must match
             std::vector<uint8_t> hb;
+            // and the coding state the simulation left must be the packets'
+            const std::vector<TagTree> sim_incl = incl, sim_imsb = imsb;
+            const std::vector<uint16_t> sim_inprev = inprev;
+            const std::vector<uint8_t> sim_nlb = nlb;
             for (size_t i = 0; i < chains.size(); ++i) {
                 const Chain& ch = chains[i];
                 const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
@@ -978,8 +1033,16 @@ struct T2Enc {
                 if (hb.size() != chdr[i] || hb.size() + body != csize[i])
                     throw GkError("rate-control simulation: packet size mismatch");
             }
+            auto same = [](const std::vector<TagTree>& a, const std::vector<TagTree>& b) {
+                for (size_t t = 0; t < a.size(); ++t)
+                    if (a[t].value != b[t].value || a[t].low != b[t].low || a[t].known != b[t].known) return false;
+                return true;
+            };
+            if (!same(sim_incl, incl) || !same(sim_imsb, imsb) || sim_inprev != inprev || sim_nlb != nlb)
+                throw GkError("rate-control simulation: coding state mismatch");
         }
     }
+    uint64_t prof_code = 0, prof_stuff = 0;   // GK_PROFILE: code_layer phases (us)
     bool simulate_layer(uint32_t l, uint64_t max_bytes) {
         if (max_bytes == 0xffffffffull) return true;
         code_layer(l);
@@ -1016,6 +1079,7 @@ struct T2Enc {
         uint64_t hsum = 0;
         const uint32_t bend = std::min<uint32_t>(nb, (uint32_t)(ci + 1) * chunk);
         for (uint32_t b = (uint32_t)ci * chunk; b < bend; ++b) {
+            if (passes && b + PF < bend) __builtin_prefetch(passes + info[4 * (size_t)(b + PF) + 3] + prev[b + PF]);
             if (l == 0) prev[b] = 0;
             const uint32_t np = npasses(b);
             uint32_t inc;
@@ -1127,6 +1191,9 @@ struct T2Enc {
         if (prof)
             fprintf(stderr, "pcrd: %u bisection steps, %u simulated; make_layer %.2f ms, simulation %.2f ms\n", n_it,
                     n_sim, t_make, t_sim);
+        if (prof)
+            fprintf(stderr, "pcrd code_layer: units %.2f ms, packet lengths %.2f ms (%zu units, %zu packets)\n",
+                    prof_code / 1e3, prof_stuff / 1e3, units.size(), chains.size());
     }
 };
 

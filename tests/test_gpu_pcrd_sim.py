@@ -4,7 +4,8 @@ against real packet writes.
 GK_T2_CHECK_SIM=1 makes the engine write every simulated packet for real and raise on any size
 difference, at every bisection step (TileProcessor.cpp:1196-1365 pcrdBisectSimple + T2Compress
 compressPacketsSimulate).  The variable is read once per process, so the cases run in a child
-process; each codestream must also equal the oracle's byte for byte.
+process; each codestream must also equal the oracle's byte for byte.  The check also compares the
+coding state the simulation leaves (tag trees, pass counts, length indicators) with the packets'.
 """
 import os
 import subprocess

@@ -1,0 +1,38 @@
+// Host-only timing harness for T2Enc::allocate (PCRD rate control) on the C3 geometry
+// (8192x8192, 3 components, 12-bit, 9/7, 3 layers -r 40,20,10) with synthetic pass
+// records.  No GPU call is made.  Build: tools/pcrd_bench.sh
+#include "../grok_amd/csrc/gk_engine.cpp"
+#include <random>
+
+int main(int argc, char** argv) {
+    Plan P;
+    P.w = P.h = argc > 1 ? (uint32_t)atoi(argv[1]) : 8192;
+    P.nc = 3; P.prec = 12; P.sgnd = 0;
+    P.p.irrev = 1; P.p.nlayers = 3; P.p.rates[0] = 40; P.p.rates[1] = 20; P.p.rates[2] = 10;
+    for (int i = 0; i < GK_MAXRLVLS; ++i) { P.p.prcw[i] = 15; P.p.prch[i] = 15; }
+    build_plan(P);
+    const uint32_t nb = (uint32_t)P.blocks.size();
+    std::mt19937 rng(7);
+    std::vector<uint32_t> info(4 * (size_t)nb);
+    std::vector<GkPass> passes;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint32_t bnb = P.blocks[b].band_numbps;
+        const uint32_t nbps = bnb > 4 ? bnb - 4 + rng() % 5 : bnb;
+        const uint32_t np = nbps ? 3 * nbps - 2 : 0;
+        info[4 * b] = nbps; info[4 * b + 1] = np; info[4 * b + 3] = (uint32_t)passes.size();
+        uint32_t r = 0; double d = 0, sd = 1e6 * (1 + rng() % 100);
+        for (uint32_t q = 0; q < np; ++q) {
+            const uint32_t dr = (q < 3 * nbps / 2) ? 1 + rng() % 8 : 40 + rng() % 200;
+            r += dr; d += sd * dr; sd *= 0.55 + 0.1 * (rng() % 100) / 100.0;
+            passes.push_back({r, dr, d});
+        }
+        info[4 * b + 2] = r;
+    }
+    printf("blocks %u passes %zu\n", nb, passes.size());
+    for (int it = 0; it < 5; ++it) {
+        T2Enc T2(P, info.data(), passes.data());
+        const auto t0 = std::chrono::steady_clock::now();
+        T2.allocate(200);
+        printf("allocate %.2f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+}
