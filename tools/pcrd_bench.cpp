@@ -33,6 +33,9 @@ int main(int argc, char** argv) {
         T2Enc T2(P, info.data(), passes.data());
         const auto t0 = std::chrono::steady_clock::now();
         T2.allocate(200);
-        printf("allocate %.2f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        uint64_t h = 0;
+        for (size_t i = 0; i < T2.lnp.size(); ++i) h = h * 1000003u + T2.lnp[i];
+        printf("allocate %.2f ms (layer pass counts hash %016llx)\n",
+               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), (unsigned long long)h);
     }
 }
