@@ -687,7 +687,24 @@ struct BitReader {
         if (n != 31) return n + 6;
         return read(7) + 37;
     }
-    uint32_t commacode() { uint32_t n = 0; while (read(1)) ++n; return n; }
+    // Up to `limit` bits equal to `bit`, counted a byte at a time; when a different bit comes
+    // first it is consumed too and `ended` is set (what a read(1) loop would have read).
+    uint32_t run(uint32_t bit, uint32_t limit, bool& ended) {
+        uint32_t n = 0;
+        ended = false;
+        while (n < limit) {
+            if (ct == 0) bytein();
+            const uint32_t mask = (1u << ct) - 1;
+            const uint32_t r = (bit ? ~buf : buf) & mask;   // differing bits in the unread window
+            if (!r) { const uint32_t k = std::min<uint32_t>((uint32_t)ct, limit - n); n += k; ct -= (int)k; continue; }
+            const uint32_t z = (uint32_t)ct - 1 - (uint32_t)floorlog2(r);
+            if (n + z >= limit) { ct -= (int)(limit - n); return limit; }
+            n += z; ct -= (int)z + 1; ended = true;
+            return n;
+        }
+        return n;
+    }
+    uint32_t commacode() { bool e; return run(1, 0xffffffffu, e); }
 };
 
 struct DecTree {   // decoder-side tag tree
@@ -715,9 +732,11 @@ struct DecTree {   // decoder-side tag tree
         while (sp) {
             n = stk[--sp];
             if (low[n] < lo) low[n] = lo; else lo = low[n];
-            while (lo < threshold && lo < value[n]) {
-                if (br.read(1)) { value[n] = lo; break; }
-                ++lo;
+            const uint32_t lim = std::min(threshold, value[n]);
+            if (lo < lim) {   // zeros up to the node's value (a 1) or the threshold
+                bool one;
+                lo += br.run(0, lim - lo, one);
+                if (one) value[n] = lo;
             }
             low[n] = lo;
         }
