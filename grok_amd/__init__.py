@@ -39,6 +39,7 @@ class CParameters(ctypes.Structure):
         ("tile_size_on", ctypes.c_uint8),
         ("t_width", ctypes.c_uint32), ("t_height", ctypes.c_uint32),
         ("writeTLM", ctypes.c_uint8), ("writePLT", ctypes.c_uint8),
+        ("cod_format", ctypes.c_int32),
     ]
 
 

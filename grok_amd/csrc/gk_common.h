@@ -50,12 +50,14 @@ struct GkPlane {
 };
 
 // A rectangular batch of equally-sized tiles for the level kernels (grid.z =
-// tile): tile z of the batch starts at row (j0 + z / nx) * dy, column
-// (i0 + z % nx) * dx of a plane; each tile is transformed independently.
+// tile): tile z of the batch starts at image row (j0 + z / nx) * dy, column
+// (i0 + z % nx) * dx; each tile is transformed independently.  The work plane
+// holds the image region whose top-left sample is (ox, oy) (a tile rectangle
+// for sharded / windowed calls, the whole image otherwise).
 struct GkTiles {
-    uint32_t nx = 1, ny = 1, i0 = 0, j0 = 0, dx = 0, dy = 0;
+    uint32_t nx = 1, ny = 1, i0 = 0, j0 = 0, dx = 0, dy = 0, ox = 0, oy = 0;
     __host__ __device__ uint32_t count() const { return nx * ny; }
     __host__ __device__ uint64_t offset(uint32_t z, uint32_t stride) const {
-        return (uint64_t)((j0 + z / nx) * dy) * stride + (uint64_t)(i0 + z % nx) * dx;
+        return (uint64_t)((j0 + z / nx) * dy - oy) * stride + (uint64_t)((i0 + z % nx) * dx - ox);
     }
 };

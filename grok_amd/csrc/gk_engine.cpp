@@ -66,6 +66,12 @@ class HostPool {
             try { f(i); } catch (const GkError& e) {
                 std::lock_guard<std::mutex> lk(m_);
                 if (err_.empty()) err_ = e.msg;
+            } catch (const std::exception& e) {   // e.g. std::bad_alloc: recorded, never escapes a worker
+                std::lock_guard<std::mutex> lk(m_);
+                if (err_.empty()) err_ = std::string("host worker: ") + e.what();
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(m_);
+                if (err_.empty()) err_ = "host worker: unknown exception";
             }
         }
     }
@@ -129,6 +135,7 @@ struct Params {
     bool ht() const { return (cblk_sty & 0x40) != 0; }
     uint32_t tw = 0, th = 0;             // nominal tile size (grk_cparameters::t_width/t_height; 0 = image)
     bool tlm = false, plt = false;       // grk_cparameters::writeTLM / writePLT
+    bool jp2 = false;                    // grk_cparameters::cod_format == GRK_CODEC_JP2 (file format boxes)
     bool rate_control() const {          // TileProcessor::needsRateControl (TileProcessor.cpp:952-967)
         for (uint32_t l = 0; l < nlayers; ++l) if (rates[l] > 0.0) return true;
         return false;
@@ -184,10 +191,32 @@ struct Plan {
     std::vector<TileG> tiles;            // raster order
     std::vector<ShapeG> shapes;
     std::vector<GkBlock> blocks;         // tile order, then canonical: comp, res, band, precinct, cblk
+    std::vector<uint32_t> bxy;           // per block: top-left (x, y) in its band's coordinates
     uint64_t slot_bytes = 0;
     std::vector<uint64_t> sym_off;       // T1 symbol-stream offsets (nblocks + 1)
     uint32_t ntrees = 0;                 // precinct-bands with code-blocks
 };
+
+// The image rectangle the work planes hold during one call.  A plan's block offsets
+// (GkBlock::band_off) address planes covering the whole image; a call that touches only
+// some tiles (tile-range encode, sharded or windowed decode) allocates planes for the
+// rectangle of those tiles alone and relocates the offsets of the blocks it codes.
+struct Region {
+    uint32_t x0 = 0, y0 = 0, w = 0, h = 0, stride = 0;
+    size_t plane = 0;                    // elements per work plane
+};
+static Region make_region(uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    Region R;
+    R.x0 = x0; R.y0 = y0; R.w = x1 - x0; R.h = y1 - y0;
+    R.stride = align_up(std::max(R.w, 1u), 64);
+    R.plane = (size_t)R.stride * R.h;
+    return R;
+}
+static inline uint64_t relocate(const Plan& P, const Region& R, uint64_t band_off) {
+    const uint64_t q = band_off / P.plane_elems, rem = band_off % P.plane_elems;
+    const uint64_t y = rem / P.stride, x = rem % P.stride;
+    return q * R.plane + (y - R.y0) * R.stride + (x - R.x0);
+}
 
 // DWT basis-function norms (T1.cpp:264-277 getnorm_53 / getnorm_97; ISO 15444-1 Annex E)
 static double band_norm(uint32_t level, uint32_t orient, bool rev) {
@@ -367,6 +396,7 @@ static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
                             G.wmse = w1 * band_norm(P.p.numres - 1 - r, B.orient, !P.p.irrev) * (double)B.step_enc;
                         }
                         P.blocks.push_back(G);
+                        P.bxy.push_back(x0); P.bxy.push_back(y0);
                     }
                 }
             }
@@ -406,6 +436,7 @@ static void build_plan(Plan& P) {
         }
     P.tiles.assign((size_t)P.ntx * P.nty, TileG());
     P.blocks.clear();
+    P.bxy.clear();
     P.ntrees = 0;
     for (uint32_t t = 0; t < P.tiles.size(); ++t) {
         TileG& T = P.tiles[t];
@@ -764,13 +795,15 @@ struct T2Enc {
     std::vector<uint8_t> nlb;       // T2 state: numlenbits
     std::vector<TagTree> incl, imsb;
     std::vector<uint8_t> hdr;
-    T2Enc(const Plan& plan, const uint32_t* inf, const GkPass* ps)
+    uint32_t b0 = 0, b1 = 0;     // code-blocks of the tiles being written (tiles [tb, te))
+    T2Enc(const Plan& plan, const uint32_t* inf, const GkPass* ps, uint32_t tb, uint32_t te)
         : P(plan), info(inf), passes(ps), L(plan.p.nlayers) {
         size_t nb = P.blocks.size();
+        b0 = P.tiles[tb].b0; b1 = P.tiles[te - 1].b1;
         lnp.assign(nb * L, 0); inprev.assign(nb, 0); nlb.assign(nb, 0);
         incl.resize(P.ntrees); imsb.resize(P.ntrees);
-        for (auto& T : P.tiles)
-        for (auto& C : T.comps)
+        for (uint32_t t = tb; t < te; ++t)
+        for (auto& C : P.tiles[t].comps)
             for (auto& R : C.res)
                 for (size_t bi = 0; bi < R.bands.size(); ++bi)
                     for (auto& PG : R.prc[bi])
@@ -1091,13 +1124,13 @@ struct T2Enc {
     }
     uint64_t make_layer(uint32_t l, double thresh, bool final_attempt, std::vector<uint16_t>& prev) {
         const uint32_t nb = (uint32_t)P.blocks.size();
-        const uint32_t chunk = 2048, nch = (nb + chunk - 1) / chunk;
+        const uint32_t chunk = 2048, nch = (b1 - b0 + chunk - 1) / chunk;
         if (mref.size() != nb) { mref.assign(nb, 0.0); mrad.assign(nb, -1.0); }
         std::vector<uint64_t> hs(nch, 0);
         host_pool().run(nch, [&](size_t ci) {
         uint64_t hsum = 0;
-        const uint32_t bend = std::min<uint32_t>(nb, (uint32_t)(ci + 1) * chunk);
-        for (uint32_t b = (uint32_t)ci * chunk; b < bend; ++b) {
+        const uint32_t bend = std::min<uint32_t>(b1, b0 + (uint32_t)(ci + 1) * chunk);
+        for (uint32_t b = b0 + (uint32_t)ci * chunk; b < bend; ++b) {
             if (passes && b + PF < bend) __builtin_prefetch(passes + info[4 * (size_t)(b + PF) + 3] + prev[b + PF]);
             if (l == 0) prev[b] = 0;
             const uint32_t np = npasses(b);
@@ -1154,7 +1187,7 @@ struct T2Enc {
             if (rates[L - 1] < rates[L - 2] + 10.0) rates[L - 1] = rates[L - 2] + 20.0;
         }
         double min_slope = 1.7976931348623157e308, max_slope = -1;
-        for (uint32_t b = 0; b < nb; ++b)
+        for (uint32_t b = b0; b < b1; ++b)
             for (uint32_t q = 0; q < npasses(b); ++q) {
                 int32_t dr; double dd;
                 if (q == 0) { dr = (int32_t)rate(b, 0); dd = dist(b, 0); }
@@ -1180,6 +1213,12 @@ struct T2Enc {
                 // outcome (the simulation depends on nothing else): the simulation is skipped
                 bool has_lo = false, has_hi = false;
                 uint64_t h_lo = 0, h_hi = 0;
+                // the hash only nominates a match: the layer's pass counts are compared exactly
+                std::vector<uint16_t> c_lo, c_hi, c_now;
+                auto counts = [&](std::vector<uint16_t>& v) {
+                    v.resize(b1 - b0);
+                    for (uint32_t b = b0; b < b1; ++b) v[b - b0] = lnp[(size_t)b * L + l];
+                };
                 for (uint32_t it = 0; it < 128; ++it) {
                     thresh = (upper == -1) ? lower : (lower + upper) / 2;
                     const auto t0 = clk::now();
@@ -1190,15 +1229,16 @@ struct T2Enc {
                     if (prevthresh != -1 && fabs(prevthresh - thresh) < 0.001) break;
                     prevthresh = thresh;
                     bool ok;
-                    if (has_hi && h == h_hi) ok = true;
-                    else if (has_lo && h == h_lo) ok = false;
+                    if ((has_hi && h == h_hi) || (has_lo && h == h_lo)) counts(c_now);
+                    if (has_hi && h == h_hi && c_now == c_hi) ok = true;
+                    else if (has_lo && h == h_lo && c_now == c_lo) ok = false;
                     else {
                         ok = fast ? simulate_layer(l, max_len) : simulate(l + 1, max_len);
                         t_sim += msd(t1, clk::now());
                         ++n_sim;
                     }
-                    if (!ok) { lower = thresh; h_lo = h; has_lo = true; continue; }
-                    upper = thresh; h_hi = h; has_hi = true;
+                    if (!ok) { lower = thresh; h_lo = h; has_lo = true; counts(c_lo); continue; }
+                    upper = thresh; h_hi = h; has_hi = true; counts(c_hi);
                 }
                 make_layer(l, upper == -1 ? thresh : upper, true, prev);
                 upper = lower - 1;
@@ -1273,6 +1313,63 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
     }
 }
 
+// ---------------------------------------------------------------------------
+// JP2 file format (ISO 15444-1 Annex I): the boxes Grok writes around the codestream
+// (FileFormatCompress.cpp:43-265, 619-665, 936-953) and the box walk that finds it
+// (FileFormatDecompress.cpp:632-672).  No colour conversion is applied (sRGB / greyscale
+// enumerated spaces, as grk_compress records for PNM input, PNMFormat.cpp:439-442).
+// ---------------------------------------------------------------------------
+static const uint32_t BOX_JP = 0x6a502020, BOX_FTYP = 0x66747970, BOX_JP2H = 0x6a703268, BOX_IHDR = 0x69686472,
+                      BOX_COLR = 0x636f6c72, BOX_JP2C = 0x6a703263, BRAND_JP2 = 0x6a703220;
+// FileFormatCompress::startCompress: the jp2c box carries an 8-byte XLBox when the raw image
+// exceeds 2^30 bytes (the codestream may pass 4 GiB)
+static bool jp2_needs_xl(const Plan& P) {
+    return (uint64_t)P.nc * P.w * P.h * ((P.prec + 7) / 8) > (1ull << 30);
+}
+static size_t jp2_prefix_size(const Plan& P) { return 12 + 20 + 45 + (jp2_needs_xl(P) ? 16 : 8); }
+// signature, file type, JP2 header (ihdr + colr) and the jp2c box header for a codestream of cs_len bytes
+static void write_jp2_prefix(std::vector<uint8_t>& o, const Plan& P, uint64_t cs_len) {
+    put32(o, 12); put32(o, BOX_JP); put32(o, 0x0d0a870a);
+    put32(o, 20); put32(o, BOX_FTYP); put32(o, BRAND_JP2); put32(o, 0); put32(o, BRAND_JP2);
+    put32(o, 8 + 22 + 15); put32(o, BOX_JP2H);
+    put32(o, 22); put32(o, BOX_IHDR); put32(o, P.h); put32(o, P.w); put16(o, P.nc);
+    o.push_back((uint8_t)((P.prec - 1) | (P.sgnd ? 0x80 : 0)));   // BPC (one precision for all components)
+    o.push_back(7); o.push_back(0); o.push_back(0);                 // C = 7, UnkC = 0, IPR = 0
+    put32(o, 15); put32(o, BOX_COLR); o.push_back(1); o.push_back(0); o.push_back(0);   // METH 1, PREC, APPROX
+    put32(o, P.nc < 3 ? 17 : 16);                                   // EnumCS: greyscale / sRGB
+    if (jp2_needs_xl(P)) {
+        put32(o, 1); put32(o, BOX_JP2C); put32(o, (uint32_t)((cs_len + 16) >> 32)); put32(o, (uint32_t)(cs_len + 16));
+    } else {
+        const uint64_t L = cs_len + 8;
+        put32(o, L < (1ull << 32) ? (uint32_t)L : 0); put32(o, BOX_JP2C);
+    }
+}
+// JP2 file -> [off, off + len) of its contiguous codestream box; false for a raw codestream
+static bool jp2_locate(ByteSrc& S, size_t& off, size_t& len) {
+    if (S.len < 12 || S.be32(0) != 12 || S.be32(4) != BOX_JP) return false;
+    if (S.be32(8) != 0x0d0a870a) throw GkError("corrupt JP2 signature box");
+    size_t pos = 12;
+    bool ftyp = false;
+    while (pos + 8 <= S.len) {
+        uint64_t L = S.be32(pos);
+        const uint32_t T = S.be32(pos + 4);
+        size_t hdr = 8;
+        if (L == 1) {
+            if (pos + 16 > S.len) throw GkError("corrupt JP2 box header");
+            L = ((uint64_t)S.be32(pos + 8) << 32) | S.be32(pos + 12);
+            hdr = 16;
+        } else if (L == 0) {
+            L = S.len - pos;   // last box
+        }
+        if (L < hdr || L > S.len - pos) throw GkError("corrupt JP2 box length");
+        if (!ftyp && T != BOX_FTYP) throw GkError("malformed JP2: second box must be the file type box");
+        ftyp = true;
+        if (T == BOX_JP2C) { off = pos + hdr; len = (size_t)L - hdr; return true; }
+        pos += (size_t)L;
+    }
+    throw GkError("JP2 file without a contiguous codestream box");
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1333,11 +1430,18 @@ struct gk_ctx {
     int16_t* nmse_tab = nullptr;   // device copy of the nmsedec tables (4 x 128)
     hipEvent_t ev[32];
     bool blocks_uploaded = false;
+    uint32_t enc_b0 = 0, enc_b1 = 0;   // block range of the uploaded encode table
+    // band quantisation held by the cached plan's bands: the plan's own (encoder, native_qcd)
+    // or that of the last decoded stream (band_qcd)
+    std::vector<std::pair<uint32_t, uint32_t>> native_qcd, band_qcd;
 };
 
 static void set_params(Params& P, const gk_cparameters* cp) {
     for (int i = 0; i < GK_MAXRLVLS; ++i) { P.prcw[i] = 15; P.prch[i] = 15; }
     if (!cp) return;
+    // CodeStreamCompress.cpp:159: 1..33 resolutions; res_spec indexes the 33-entry precinct arrays
+    if (cp->numresolution > GK_MAXRLVLS) throw GkError("numresolution must be at most 33");
+    if (cp->res_spec > GK_MAXRLVLS) throw GkError("res_spec must be at most 33");
     P.numres = cp->numresolution ? cp->numresolution : 6;
     P.cbw = (uint32_t)floorlog2(cp->cblockw_init ? cp->cblockw_init : 64);
     P.cbh = (uint32_t)floorlog2(cp->cblockh_init ? cp->cblockh_init : 64);
@@ -1351,6 +1455,8 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     P.cblk_sty = cp->cblk_sty;
     if (cp->tile_size_on) { P.tw = cp->t_width; P.th = cp->t_height; }
     P.tlm = cp->writeTLM != 0; P.plt = cp->writePLT != 0;
+    if (cp->cod_format != 0 && cp->cod_format != 2) throw GkError("cod_format must be GRK_CODEC_J2K (0) or GRK_CODEC_JP2 (2)");
+    P.jp2 = cp->cod_format == 2;
     if ((cp->csty & 1) && cp->res_spec) {   // CodeStreamCompress.cpp:542-590
         P.custom_prc = true;
         uint32_t p = 0;
@@ -1389,11 +1495,21 @@ static void ensure_plan(gk_ctx* ctx, const Plan& want) {
     build_plan(ctx->plan);
     ctx->plan_key = k;
     ctx->blocks_uploaded = false;
+    ctx->native_qcd.clear();
+    for (const ResG& R : ctx->plan.tiles[0].comps[0].res)
+        for (const BandG& B : R.bands) ctx->native_qcd.push_back({B.expn, B.mant});
+    ctx->band_qcd = ctx->native_qcd;
+}
+// Encode uses the plan's own quantisation: undo a decoded stream's QCD if one was applied.
+static void restore_native_qcd(gk_ctx* ctx) {
+    if (ctx->band_qcd == ctx->native_qcd) return;
+    for (TileG& T : ctx->plan.tiles) assign_steps_tile(ctx->plan, T);
+    ctx->band_qcd = ctx->native_qcd;
 }
 
 // Forward/inverse DWT over all components with the ping-pong placement of gk_common.h.
-static void run_dwt(gk_ctx* ctx, bool forward, uint32_t jb = 0, uint32_t je = 0xffffffffu, uint32_t ib = 0,
-                    uint32_t ie = 0xffffffffu) {
+static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0, uint32_t je = 0xffffffffu,
+                    uint32_t ib = 0, uint32_t ie = 0xffffffffu) {
     Plan& P = ctx->plan;
     int32_t* arena = (int32_t*)ctx->arena.p;
     const uint32_t L = P.p.numres - 1;
@@ -1407,20 +1523,21 @@ static void run_dwt(gk_ctx* ctx, bool forward, uint32_t jb = 0, uint32_t je = 0x
             if (sj0 >= sj1 || si0 >= si1) continue;
             S.tb.j0 = sj0; S.tb.ny = sj1 - sj0;
             S.tb.i0 = si0; S.tb.nx = si1 - si0;
+            S.tb.ox = RG.x0; S.tb.oy = RG.y0;
             const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
             for (uint32_t c = 0; c < P.nc; ++c) {
-                int32_t* A = arena + (size_t)c * 2 * P.plane_elems;
-                int32_t* B = A + P.plane_elems;
+                int32_t* A = arena + (size_t)c * 2 * RG.plane;
+                int32_t* B = A + RG.plane;
                 int32_t* src_l = (l & 1) ? A : B;     // D_{l-1}: level l input plane (l-1 odd -> B)
                 int32_t* dst_l = (l & 1) ? B : A;     // D_l
                 if (P.p.irrev) {
                     float* fs = reinterpret_cast<float*>(src_l);
                     float* fd = reinterpret_cast<float*>(dst_l);
-                    if (forward) gk_launch_dwt97_fwd(ctx->st, fs, P.stride, fd, P.stride, w, h, S.tb);
-                    else gk_launch_dwt97_inv(ctx->st, fd, P.stride, fs, P.stride, w, h, S.tb);
+                    if (forward) gk_launch_dwt97_fwd(ctx->st, fs, RG.stride, fd, RG.stride, w, h, S.tb);
+                    else gk_launch_dwt97_inv(ctx->st, fd, RG.stride, fs, RG.stride, w, h, S.tb);
                 } else {
-                    if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, P.stride, dst_l, P.stride, w, h, S.tb);
-                    else gk_launch_dwt53_inv(ctx->st, dst_l, P.stride, src_l, P.stride, w, h, S.tb);
+                    if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, RG.stride, dst_l, RG.stride, w, h, S.tb);
+                    else gk_launch_dwt53_inv(ctx->st, dst_l, RG.stride, src_l, RG.stride, w, h, S.tb);
                 }
                 ctx->tm.dwt_launches++;
                 ctx->tm.dwt_bytes += (uint64_t)w * h * 8 * S.tb.count();
@@ -1450,8 +1567,11 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     if (want.p.tw && want.p.th && (want.p.tw < want.w || want.p.th < want.h) && want.p.rate_control())
         throw GkError("rate control with more than one tile is not supported on this path yet");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
+    if (want.prec == 0 || want.prec > 31) throw GkError("component precision must be 1..31 bits");
+    if (want.w == 0 || want.h == 0) throw GkError("empty image");
     if ((1u << want.p.cbw) > 64 || (1u << want.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
     ensure_plan(ctx, want);
+    restore_native_qcd(ctx);
 }
 
 static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
@@ -1470,75 +1590,87 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     hipStream_t st = ctx->st;
 
     HIPCHK(hipEventRecord(ctx->ev[0], st));
-    int32_t* arena = (int32_t*)ctx->arena.get(P.plane_elems * P.nc * 2 * sizeof(int32_t));
-    // stage host planes
+    // work planes for the sample rows of the selected tiles only
+    const Region RG = make_region(0, ry0, P.w, ry1);
+    int32_t* arena = (int32_t*)ctx->arena.get(RG.plane * P.nc * 2 * sizeof(int32_t));
+    const uint32_t nrows = ry1 - ry0;
+    // stage host planes (those rows only)
     std::vector<const int32_t*> src(P.nc);
     std::vector<uint32_t> sstr(P.nc);
     if (!comps_on_device) {
-        int32_t* dp = (int32_t*)ctx->dplanes.get((size_t)P.w * P.h * P.nc * 4);
+        int32_t* dp = (int32_t*)ctx->dplanes.get((size_t)P.w * nrows * P.nc * 4);
         for (uint32_t c = 0; c < P.nc; ++c) {
-            HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * P.h + (size_t)ry0 * P.w, (size_t)P.w * 4,
+            HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * nrows, (size_t)P.w * 4,
                                     comps[c] + (size_t)ry0 * strides[c], (size_t)strides[c] * 4,
-                                    (size_t)P.w * 4, ry1 - ry0, hipMemcpyHostToDevice, st));
-            src[c] = dp + (size_t)c * P.w * P.h; sstr[c] = P.w;
+                                    (size_t)P.w * 4, nrows, hipMemcpyHostToDevice, st));
+            src[c] = dp + (size_t)c * P.w * nrows; sstr[c] = P.w;
         }
     } else {
-        for (uint32_t c = 0; c < P.nc; ++c) { src[c] = comps[c]; sstr[c] = strides[c]; }
+        for (uint32_t c = 0; c < P.nc; ++c) { src[c] = comps[c] + (size_t)ry0 * strides[c]; sstr[c] = strides[c]; }
     }
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     // DC shift + MCT into plane A of each component (rows of the selected tiles)
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
-    const uint32_t nrows = ry1 - ry0;
-    for (uint32_t c = 0; c < P.nc; ++c) src[c] += (size_t)ry0 * sstr[c];
-    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems + (size_t)ry0 * P.stride; };
+    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * RG.plane; };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
     if (!P.p.irrev) {
-        if (mct3) gk_launch_dc_rct_fwd(st, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), P.stride, P.w, nrows, shift);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), P.stride, P.w, nrows, shift);
+        if (mct3) gk_launch_dc_rct_fwd(st, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), RG.stride, P.w, nrows, shift);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), RG.stride, P.w, nrows, shift);
     } else {
-        if (mct3) gk_launch_dc_ict_fwd(st, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), P.stride, P.w, nrows, shift);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, src[c], sstr[c], planeAf(c), P.stride, P.w, nrows, shift);
+        if (mct3) gk_launch_dc_ict_fwd(st, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), RG.stride, P.w, nrows, shift);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, src[c], sstr[c], planeAf(c), RG.stride, P.w, nrows, shift);
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    run_dwt(ctx, true, jb, je);
+    run_dwt(ctx, RG, true, jb, je);
     HIPCHK(hipEventRecord(ctx->ev[3], st));
-    // T1
+    // T1 over the block range [b0, b1): every per-block device array is range-local
     const bool do_rc = P.p.rate_control();
-    uint8_t* dbytes = (uint8_t*)ctx->bytes.get(P.slot_bytes + (64u << 20));
-    GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * std::max(nb, 1u));
-    GkPass* dps = (GkPass*)ctx->dpasses.get(sizeof(GkPass) * GK_MAX_PASSES * (size_t)std::max(nb, 1u));
-    uint32_t* dinfo = (uint32_t*)ctx->dinfo.get(16 * (size_t)std::max(nb, 1u) + 16);
+    const uint64_t slot0 = P.blocks[b0].data_off - 16;
+    const uint64_t slot1 = b1 < nb ? P.blocks[b1].data_off - 16 : P.slot_bytes;
+    const uint64_t slot_span = slot1 - slot0;    // the range's slots; host bytes are staged after them
+    uint8_t* dbytes = (uint8_t*)ctx->bytes.get(slot_span + (64u << 20));
+    const uint32_t nbx = std::max(nbr, 1u);
+    GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * nbx);
+    GkPass* dps = (GkPass*)ctx->dpasses.get(sizeof(GkPass) * GK_MAX_PASSES * (size_t)nbx);
+    uint32_t* dinfo = (uint32_t*)ctx->dinfo.get(16 * (size_t)nbx + 16);
     int* derr = (int*)ctx->derr.get(64);
     uint32_t* dpcount = (uint32_t*)(derr + 4);
-    uint8_t* dsym = P.p.ht() ? nullptr : (uint8_t*)ctx->dsym.get(P.sym_off[nb] + 256);
-    uint64_t* dsymoff = (uint64_t*)ctx->dsymoff.get(8 * ((size_t)nb + 1));
-    uint32_t* dpe = (uint32_t*)ctx->dpassend.get(4 * GK_MAX_PASSES * (size_t)std::max(nb, 1u));
-    uint32_t* dcm = (uint32_t*)ctx->dcminfo.get(8 * (size_t)std::max(nb, 1u));
-    int32_t* dnmse = do_rc ? (int32_t*)ctx->dnmse.get(4 * GK_MAX_PASSES * (size_t)std::max(nb, 1u)) : nullptr;
-    if (!ctx->blocks_uploaded) {
-        HIPCHK(hipMemcpyAsync(dblk, P.blocks.data(), sizeof(GkBlock) * nb, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(dsymoff, P.sym_off.data(), 8 * ((size_t)nb + 1), hipMemcpyHostToDevice, st));
-        ctx->blocks_uploaded = true;
+    uint8_t* dsym = P.p.ht() ? nullptr : (uint8_t*)ctx->dsym.get(P.sym_off[b1] - P.sym_off[b0] + 256);
+    uint64_t* dsymoff = (uint64_t*)ctx->dsymoff.get(8 * ((size_t)nbr + 1));
+    uint32_t* dpe = (uint32_t*)ctx->dpassend.get(4 * GK_MAX_PASSES * (size_t)nbx);
+    uint32_t* dcm = (uint32_t*)ctx->dcminfo.get(8 * (size_t)nbx);
+    int32_t* dnmse = do_rc ? (int32_t*)ctx->dnmse.get(4 * GK_MAX_PASSES * (size_t)nbx) : nullptr;
+    if (!ctx->blocks_uploaded || ctx->enc_b0 != b0 || ctx->enc_b1 != b1) {
+        // the range's blocks with offsets into this call's planes and slots
+        GkBlock* hb = (GkBlock*)ctx->hpasses.get(sizeof(GkBlock) * nbx + 8 * ((size_t)nbr + 1));
+        uint64_t* hso = (uint64_t*)(hb + nbx);
+        for (uint32_t i = 0; i < nbr; ++i) {
+            hb[i] = P.blocks[b0 + i];
+            hb[i].band_off = relocate(P, RG, hb[i].band_off);
+            hb[i].stride = RG.stride;
+            hb[i].data_off -= slot0;
+        }
+        for (uint32_t i = 0; i <= nbr; ++i) hso[i] = P.sym_off[b0 + i] - P.sym_off[b0];
+        HIPCHK(hipMemcpyAsync(dblk, hb, sizeof(GkBlock) * nbr, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(dsymoff, hso, 8 * ((size_t)nbr + 1), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));   // the staging buffer is reused below
+        ctx->blocks_uploaded = true; ctx->enc_b0 = b0; ctx->enc_b1 = b1;
     }
     HIPCHK(hipMemsetAsync(derr, 0, 64, st));
-    // the selected tiles' code-blocks are the contiguous range [b0, b1): per-block arrays are offset
-    const size_t MP = GK_MAX_PASSES;
     if (P.p.ht()) {
         // HT cleanup pass (T1HT::compress, T1HT.cpp:109-133); MEL bytes staged in the symbol buffer
-        uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nb * GK_HT_MEL_CAP + 256);
+        uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nbx * GK_HT_MEL_CAP + 256);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_ht_enc(st, arena, dblk + b0, dbytes, mel, GK_HT_MEL_CAP, dinfo + 4 * (size_t)b0, nbr, derr);
+        gk_launch_ht_enc(st, arena, dblk, dbytes, mel, GK_HT_MEL_CAP, dinfo, nbr, derr);
     } else {
-        gk_launch_t1_cm(st, arena, dblk + b0, dsymoff + b0, dsym, dpe + MP * b0, dcm + 2 * (size_t)b0, nbr, derr,
-                        ctx->nmse_tab, dnmse ? dnmse + MP * b0 : nullptr);
+        gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nbr, derr, ctx->nmse_tab, dnmse);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_t1_mq(st, dsym, dsymoff + b0, dpe + MP * b0, dcm + 2 * (size_t)b0, dblk + b0, dbytes, dps,
-                        dinfo + 4 * (size_t)b0, nbr, derr, dnmse ? dnmse + MP * b0 : nullptr, dpcount);
+        gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount);
     }
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(16 * (size_t)nb + 64);
-    HIPCHK(hipMemcpyAsync(hinfo + 4 * (size_t)b0, dinfo + 4 * (size_t)b0, 16 * (size_t)nbr, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hinfo + 4 * (size_t)b0, dinfo, 16 * (size_t)nbr, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(hinfo + 4 * (size_t)nb, derr, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t t1err = hinfo[4 * (size_t)nb], npass_total = hinfo[4 * (size_t)nb + 4];
@@ -1559,7 +1691,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     write_main_header(H, P, &tlm_pos);
     const size_t header_size = H.size();
     if (!with_header) H.clear();
-    T2Enc T2(P, hinfo, hpasses);
+    T2Enc T2(P, hinfo, hpasses, tb, te);
     T2.allocate(header_size);
     // segments: (src_off in dbytes, dst_off in codestream, len); host bytes staged after the slots
     std::vector<uint64_t> seg;
@@ -1568,10 +1700,16 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     uint64_t pos = 0;            // codestream position
     auto add_host = [&](const uint8_t* p, size_t n) {
         if (!n) return;
-        seg.push_back(P.slot_bytes + hdrs.size()); seg.push_back(pos); seg.push_back(n);
+        seg.push_back(slot_span + hdrs.size()); seg.push_back(pos); seg.push_back(n);
         hdrs.insert(hdrs.end(), p, p + n);
         pos += n;
     };
+    // JP2 boxes before the codestream; the jp2c length is written once the size is known
+    std::vector<uint8_t> J;
+    const bool jp2 = P.p.jp2 && with_header;
+    if (jp2) write_jp2_prefix(J, P, 0);
+    add_host(J.data(), J.size());
+    const size_t main_at = J.size();   // the main header's position in hdrs
     add_host(H.data(), H.size());
     // per tile: packets (T2Compress::compressPackets) and the tile-part header; tiles are
     // independent, so they are built in parallel host threads and appended in tile order
@@ -1662,7 +1800,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
         const uint64_t psot = O.psot;
         if (part_lens) part_lens[t - tb] = (uint32_t)psot;
         if (P.p.tlm && with_header) {
-            uint8_t* e = hdrs.data() + tlm_pos + 6 * (size_t)t;   // the main header is hdrs[0 .. H.size())
+            uint8_t* e = hdrs.data() + main_at + tlm_pos + 6 * (size_t)t;   // the main header is hdrs[main_at ..)
             e[0] = (uint8_t)(t >> 8); e[1] = (uint8_t)t;
             e[2] = (uint8_t)(psot >> 24); e[3] = (uint8_t)(psot >> 16); e[4] = (uint8_t)(psot >> 8); e[5] = (uint8_t)psot;
         }
@@ -1672,14 +1810,15 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
             for (uint32_t q = k.s0; q < k.s1; q += 3) {
                 const uint32_t b = O.bsegs[q], off = O.bsegs[q + 1], n = O.bsegs[q + 2];
                 const GkBlock& G = P.blocks[b];
+                const uint64_t so = G.data_off - slot0;   // the block's slot in this call's byte arena
                 if (ht) {   // MagSgn head at the slot start, MEL+VLC tail at the slot end
                     const uint32_t ms = hinfo[4 * (size_t)b + 3], tl = n - ms;
-                    if (ms) { seg.push_back(G.data_off); seg.push_back(pos); seg.push_back(ms); pos += ms; }
-                    seg.push_back(G.data_off + G.data_cap - tl); seg.push_back(pos); seg.push_back(tl);
+                    if (ms) { seg.push_back(so); seg.push_back(pos); seg.push_back(ms); pos += ms; }
+                    seg.push_back(so + G.data_cap - tl); seg.push_back(pos); seg.push_back(tl);
                     pos += tl;
                     continue;
                 }
-                seg.push_back(G.data_off + off); seg.push_back(pos); seg.push_back(n);
+                seg.push_back(so + off); seg.push_back(pos); seg.push_back(n);
                 pos += n;
             }
         }
@@ -1687,13 +1826,18 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     uint8_t eoc[2] = {0xff, 0xd9};
     if (with_header) add_host(eoc, 2);
     const size_t total = pos;
+    if (jp2) {
+        J.clear();
+        write_jp2_prefix(J, P, total - jp2_prefix_size(P));
+        memcpy(hdrs.data(), J.data(), J.size());
+    }
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (total > cap) { *rc = -2; return total; }
     // ---- device assembly
     if (hdrs.size() > (64u << 20)) throw GkError("packet headers exceed staging");
     uint8_t* hh = (uint8_t*)ctx->hhdr.get(hdrs.size());
     memcpy(hh, hdrs.data(), hdrs.size());
-    HIPCHK(hipMemcpyAsync(dbytes + P.slot_bytes, hh, hdrs.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dbytes + slot_span, hh, hdrs.size(), hipMemcpyHostToDevice, st));
     uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8);
     memcpy(hs, seg.data(), seg.size() * 8);
     uint64_t* ds = (uint64_t*)ctx->dseg.get(seg.size() * 8);
@@ -1750,7 +1894,9 @@ static void parse_header(ByteSrc& S, Header& Hd) {
         if (m == 0xff90) { Hd.first_sot = i; break; }
         uint32_t L = S.be16(i + 2);
         size_t s = i + 4;
+        if (L < 2 || i + 2 + L > S.len) throw GkError("corrupt main header (marker length)");
         if (m == 0xff51) {
+            if (L < 41) throw GkError("corrupt SIZ marker");
             W.w = S.be32(s + 2) - S.be32(s + 10); W.h = S.be32(s + 6) - S.be32(s + 14);
             if (S.be32(s + 10) || S.be32(s + 14)) throw GkError("image offsets not supported");
             if (S.be32(s + 26) || S.be32(s + 30)) throw GkError("tile grid offsets not supported");
@@ -1758,30 +1904,39 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             if (!W.p.tw || !W.p.th) throw GkError("bad tile size");
             if (W.p.tw >= W.w && W.p.th >= W.h) W.p.tw = W.p.th = 0;   // one tile
             W.nc = S.be16(s + 34);
+            if (W.nc == 0 || W.nc > 255 || L < 38 + 3 * W.nc) throw GkError("corrupt SIZ marker (component count)");
+            if (!W.w || !W.h) throw GkError("corrupt SIZ marker (empty image)");
             uint32_t sz = S.at(s + 36);
             W.prec = (sz & 0x7f) + 1; W.sgnd = (sz & 0x80) ? 1 : 0;
+            if (W.prec > 31) throw GkError("component precision > 31 bits not supported");
             for (uint32_t c = 0; c < W.nc; ++c) {
                 if (S.at(s + 37 + 3 * c) != 1 || S.at(s + 38 + 3 * c) != 1) throw GkError("component subsampling not supported");
                 if (((S.at(s + 36 + 3 * c) & 0x7f) + 1) != W.prec) throw GkError("mixed component precision not supported");
             }
             have_siz = true;
         } else if (m == 0xff52) {
+            if (L < 12) throw GkError("corrupt COD marker");
             uint32_t scod = S.at(s);
             if (S.at(s + 1) != 0) throw GkError("only LRCP progression supported");
             if (scod & 6) throw GkError("SOP/EPH markers not supported");
             W.p.nlayers = S.be16(s + 2);
             W.p.mct = S.at(s + 4);
             W.p.numres = S.at(s + 5) + 1;
+            // at most 32 decomposition levels (CodeStreamDecompress.cpp:1733)
+            if (W.p.numres > GK_MAXRLVLS) throw GkError("corrupt COD marker (more than 32 decomposition levels)");
             W.p.cbw = S.at(s + 6) + 2; W.p.cbh = S.at(s + 7) + 2;
+            if (W.p.cbw > 10 || W.p.cbh > 10 || W.p.cbw + W.p.cbh > 12) throw GkError("corrupt COD marker (code-block size)");
             W.p.cblk_sty = S.at(s + 8);
             if (W.p.cblk_sty != 0 && W.p.cblk_sty != 0x40) throw GkError("code-block style mode switches not supported");
             W.p.irrev = S.at(s + 9) == 0 ? 1 : 0;
             if (scod & 1) {
+                if (L < 12 + W.p.numres) throw GkError("corrupt COD marker (precinct sizes)");
                 W.p.custom_prc = true;
                 for (uint32_t r = 0; r < W.p.numres; ++r) { uint32_t v = S.at(s + 10 + r); W.p.prcw[r] = v & 15; W.p.prch[r] = v >> 4; }
             }
             have_cod = true;
         } else if (m == 0xff5c) {
+            if (L < 4) throw GkError("corrupt QCD marker");
             uint32_t sq = S.at(s);
             W.p.numgbits = sq >> 5;
             uint32_t qt = sq & 0x1f;
@@ -1931,12 +2086,20 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     ByteSrc S;
     S.len = len; S.st = st;
     if (cs_on_device) S.dev = cs; else S.host = cs;
+    {
+        size_t joff = 0, jlen = 0;
+        if (jp2_locate(S, joff, jlen)) {   // JP2 file: decode its codestream box
+            cs += joff; len = jlen;
+            S = ByteSrc(); S.len = len; S.st = st;
+            if (cs_on_device) S.dev = cs; else S.host = cs;
+        }
+    }
     Header Hd;
     parse_header(S, Hd);
     if (Hd.want.nc < 3) Hd.want.p.mct = 0;
     ensure_plan(ctx, Hd.want);
     Plan& P = ctx->plan;
-    apply_qcd(P, Hd.qcd);
+    if (Hd.qcd != ctx->band_qcd) { apply_qcd(P, Hd.qcd); ctx->band_qcd = Hd.qcd; }
     if (win) {   // keep only the tile parts of tiles intersecting the window
         if (win[0] >= win[2] || win[1] >= win[3] || win[2] > P.w || win[3] > P.h) throw GkError("bad decode window");
         std::vector<TilePart> keep;
@@ -1952,48 +2115,122 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         read_tile_part_headers(ctx, S, Hd);
         prefetch_packet_headers(ctx, S, P, Hd);
     }
-    const uint32_t nb = (uint32_t)P.blocks.size();
-    std::vector<GkBlock> blk = P.blocks;
-    // code-block segments in stream order, one list per tile part (parts parse in parallel)
-    struct Chunk { uint64_t pos; uint32_t b, len; };
-    std::vector<std::vector<Chunk>> part_chunks(Hd.parts.size());
-    std::vector<uint8_t> included(nb, 0);
-    std::vector<uint32_t> numlenbits(nb, 0);
-    for (auto& G : blk) { G.npasses = 0; G.numbps = 0; G.len = 0; }
-    // refresh band numbps from QCD (decoder semantics)
-    for (auto& T : P.tiles)
+    // ---- tiles present, their rectangle, and the code-blocks that reach the output
+    std::vector<int32_t> part_of(P.tiles.size(), -1);
+    for (size_t q = 0; q < Hd.parts.size(); ++q) {
+        const TilePart& TPt = Hd.parts[q];
+        if (TPt.tile >= P.tiles.size()) throw GkError("corrupt SOT (tile index)");
+        if (part_of[TPt.tile] >= 0) throw GkError("multiple tile parts per tile not supported");
+        part_of[TPt.tile] = (int32_t)q;
+    }
+    uint32_t ib = P.ntx, ie = 0, jb = P.nty, je = 0;
+    for (const TilePart& TPt : Hd.parts) {
+        const uint32_t t = TPt.tile;
+        ib = std::min(ib, t % P.ntx); ie = std::max(ie, t % P.ntx + 1);
+        jb = std::min(jb, t / P.ntx); je = std::max(je, t / P.ntx + 1);
+    }
+    // work planes cover the tile rectangle only (tiles of the rectangle without a tile part
+    // decode as zero); the output region is the rectangle, clipped to the window
+    const TileG& Tfirst = P.tiles[(size_t)jb * P.ntx + ib];
+    const TileG& Tlast = P.tiles[(size_t)(je - 1) * P.ntx + ie - 1];
+    const Region RG = make_region(Tfirst.x0, Tfirst.y0, Tlast.x1, Tlast.y1);
+    uint32_t rx0 = RG.x0, ry0 = RG.y0, rx1 = RG.x0 + RG.w, ry1 = RG.y0 + RG.h, ox = 0, oy = 0;
+    if (win) {
+        rx0 = std::max(rx0, win[0]); ry0 = std::max(ry0, win[1]); rx1 = std::min(rx1, win[2]); ry1 = std::min(ry1, win[3]);
+        ox = win[0]; oy = win[1];
+    }
+    const uint32_t ncols = rx1 - rx0, nrows = ry1 - ry0;
+    // Per tile: which code-blocks reach [rx0, rx1) x [ry0, ry1).  Inverse lifting reconstructs
+    // sample n of a level from low/high coefficients within a few positions of n/2 (5/3: the
+    // update/predict steps reach one neighbour each; 9/7: four steps), so the coefficients a
+    // window needs at each level are its projection padded by that reach, clamped to the band
+    // (the padded band window of TileComponentWindowBuffer / T2Decompress.cpp:55-116).  Blocks
+    // outside are not decoded (their samples only feed outputs outside the window), and with
+    // PLT a packet none of whose blocks is needed is skipped unparsed.
+    const uint32_t Lv = P.p.numres - 1, pad = P.p.irrev ? 4 : 2;
+    auto block_needed = [&](const TileG& T, std::vector<uint8_t>& need) {
+        need.assign(T.b1 - T.b0, 1);
+        if (!win || (rx0 <= T.x0 && T.x1 <= rx1 && ry0 <= T.y0 && T.y1 <= ry1)) return;
+        // lo[a][l], hi[a][l]: needed [begin, end) in level-l low / high band coordinates, axis a
+        uint32_t lo[2][GK_MAXRLVLS + 1][2], hi[2][GK_MAXRLVLS + 1][2];
+        const CompG& C0 = T.comps[0];
+        for (int ax = 0; ax < 2; ++ax) {
+            uint32_t s0 = ax ? std::max(ry0, T.y0) : std::max(rx0, T.x0);
+            uint32_t s1 = ax ? std::min(ry1, T.y1) : std::min(rx1, T.x1);
+            lo[ax][0][0] = s0; lo[ax][0][1] = s1;
+            for (uint32_t l = 1; l <= Lv; ++l) {
+                const ResG& Rl = C0.res[P.p.numres - l];       // resolution holding level-l bands
+                const ResG& Rlow = C0.res[P.p.numres - 1 - l]; // its low-pass image
+                const uint32_t c0 = s0 / 2 > pad ? s0 / 2 - pad : 0, c1 = (s1 + 1) / 2 + pad;
+                const uint32_t lx0 = ax ? Rlow.y0 : Rlow.x0, lx1 = lx0 + (ax ? Rlow.h : Rlow.w);
+                const BandG& Bh = Rl.bands[ax ? 1 : 0];       // HL (high in x) / LH (high in y)
+                const uint32_t hx0 = ax ? Bh.y0 : Bh.x0, hx1 = ax ? Bh.y1 : Bh.x1;
+                lo[ax][l][0] = std::max(c0, lx0); lo[ax][l][1] = std::min(c1, lx1);
+                hi[ax][l][0] = std::max(c0, hx0); hi[ax][l][1] = std::min(c1, hx1);
+                s0 = lo[ax][l][0]; s1 = std::max(lo[ax][l][0], lo[ax][l][1]);
+            }
+        }
         for (uint32_t c = 0; c < P.nc; ++c)
             for (uint32_t r = 0; r < P.p.numres; ++r) {
-                ResG& R = T.comps[c].res[r];
-                for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
+                const ResG& R = T.comps[c].res[r];
+                const uint32_t lev = r ? P.p.numres - r : Lv;
+                for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
+                    const uint32_t o = R.bands[bi].orient;
+                    const uint32_t* nx = (o & 1) ? hi[0][lev] : lo[0][lev];
+                    const uint32_t* ny = (o & 2) ? hi[1][lev] : lo[1][lev];
                     for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                        PrecG& PG = R.prc[bi][pi];
+                        const PrecG& PG = R.prc[bi][pi];
                         for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                            blk[PG.first_block + k].band_numbps = (uint8_t)R.bands[bi].numbps;
-                            blk[PG.first_block + k].step = R.bands[bi].step_dec / 2.0f;
+                            const uint32_t bb = PG.first_block + k;
+                            const GkBlock& G = P.blocks[bb];
+                            const uint32_t x = P.bxy[2 * (size_t)bb], y = P.bxy[2 * (size_t)bb + 1];
+                            need[bb - T.b0] = x < nx[1] && nx[0] < x + G.w && y < ny[1] && ny[0] < y + G.h;
                         }
                     }
+                }
             }
+    };
+    std::vector<std::vector<uint8_t>> part_need(Hd.parts.size());
+    host_pool().run(Hd.parts.size(), [&](size_t q) { block_needed(P.tiles[Hd.parts[q].tile], part_need[q]); });
     // ---- T2 (T2Decompress.cpp:216-570), LRCP, per tile part.  Tile parts are independent
-    // (own precincts, tag trees and code-blocks), so they are parsed in parallel host threads.
-    std::vector<uint8_t> seen(P.tiles.size(), 0);
-    for (const TilePart& TPt : Hd.parts) {
-        if (TPt.tile >= P.tiles.size()) throw GkError("corrupt SOT (tile index)");
-        if (seen[TPt.tile]++) throw GkError("multiple tile parts per tile not supported");
-    }
-    auto t2_part = [&](const TilePart& TPt, ByteSrc& BS, std::vector<Chunk>& chunks) {
+    // (own precincts, tag trees and code-blocks), so they are parsed in parallel host threads
+    // into tile-local state (index = block - tile's first block).
+    struct Chunk { uint64_t pos; uint32_t b, len; };
+    struct PartState {
+        std::vector<Chunk> chunks;
+        std::vector<uint8_t> included, numbps;
+        std::vector<uint16_t> npasses;
+        std::vector<uint32_t> numlenbits, len;
+    };
+    std::vector<PartState> ps(Hd.parts.size());
+    auto t2_part = [&](size_t q, ByteSrc& BS) {
+        const TilePart& TPt = Hd.parts[q];
+        PartState& st2 = ps[q];
+        const std::vector<uint8_t>& need = part_need[q];
         struct Trees { DecTree incl, imsb; };
         std::vector<Trees> trees;
         std::unordered_map<uint32_t, size_t> tidx;   // trees by first_block of each precinct-band
         const TileG& TG = P.tiles[TPt.tile];
+        const uint32_t tb0 = TG.b0, ntb = TG.b1 - TG.b0;
+        st2.included.assign(ntb, 0); st2.numbps.assign(ntb, 0); st2.npasses.assign(ntb, 0);
+        st2.numlenbits.assign(ntb, 0); st2.len.assign(ntb, 0);
+        st2.chunks.reserve(ntb);
         const size_t tile_end = TPt.end;
-        size_t pos = TPt.data;
+        size_t pos = TPt.data, pk = 0;
         for (uint32_t l = 0; l < P.p.nlayers; ++l)
             for (uint32_t r = 0; r < P.p.numres; ++r)
                 for (uint32_t c = 0; c < P.nc; ++c) {
                     const ResG& R = TG.comps[c].res[r];
-                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi, ++pk) {
                         if (pos >= tile_end) return;
+                        if (pk < TPt.plt.size()) {   // PLT: a packet with no needed block is skipped unread
+                            bool any = false;
+                            for (uint32_t bi = 0; bi < R.bands.size() && !any; ++bi) {
+                                const PrecG& PG = R.prc[bi][pi];
+                                for (uint32_t k = 0; k < PG.cw * PG.ch && !any; ++k) any = need[PG.first_block + k - tb0];
+                            }
+                            if (!any) { pos += TPt.plt[pk]; continue; }
+                        }
                         BitReader br(BS, pos, tile_end);
                         std::vector<std::pair<uint32_t, uint32_t>> contrib;
                         if (br.read(1)) {
@@ -2009,29 +2246,30 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                 }
                                 Trees& T = trees[it->second];
                                 for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                                    uint32_t b = PG.first_block + k;
+                                    const uint32_t b = PG.first_block + k - tb0;
                                     uint32_t inc;
-                                    if (!included[b]) inc = T.incl.decode(br, k, l + 1) <= l ? 1 : 0;
+                                    if (!st2.included[b]) inc = T.incl.decode(br, k, l + 1) <= l ? 1 : 0;
                                     else inc = br.read(1);
                                     if (!inc) continue;
-                                    if (!included[b]) {
+                                    if (!st2.included[b]) {
                                         // zero bit-planes: Grok raises the threshold one plane at a time
                                         // until the leaf is known; a tag tree reads a node's bits only
                                         // once its parent is known, so one walk with threshold 64 reads
                                         // exactly the same bits
                                         const uint32_t v = T.imsb.decode(br, k, 64);
                                         const uint32_t kmsbs = v < 64 ? v : 64;
-                                        uint32_t bnb = R.bands[bi].numbps;
-                                        blk[b].numbps = kmsbs > bnb ? 0 : bnb - kmsbs;
-                                        numlenbits[b] = 3;
-                                        included[b] = 1;
+                                        const uint32_t bnb = R.bands[bi].numbps;
+                                        st2.numbps[b] = (uint8_t)(kmsbs > bnb ? 0 : bnb - kmsbs);
+                                        st2.numlenbits[b] = 3;
+                                        st2.included[b] = 1;
                                     }
-                                    uint32_t np = br.numpasses();
-                                    numlenbits[b] += br.commacode();
-                                    uint32_t nbits = numlenbits[b] + floorlog2(np);
+                                    const uint32_t np = br.numpasses();
+                                    st2.numlenbits[b] += br.commacode();
+                                    const uint32_t nbits = st2.numlenbits[b] + floorlog2(np);
                                     if (nbits > 32) throw GkError("corrupt packet header (segment length)");
-                                    uint32_t sl = br.read((int)nbits);
-                                    blk[b].npasses += np;
+                                    const uint32_t sl = br.read((int)nbits);
+                                    if (st2.npasses[b] + np > GK_MAX_PASSES) throw GkError("corrupt packet header (pass count)");
+                                    st2.npasses[b] = (uint16_t)(st2.npasses[b] + np);
                                     contrib.push_back({b, sl});
                                 }
                             }
@@ -2039,8 +2277,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         br.align();
                         pos = br.off;
                         for (auto& ct : contrib) {
-                            uint32_t n = (uint32_t)std::min<size_t>(ct.second, tile_end > pos ? tile_end - pos : 0);
-                            if (n) chunks.push_back({pos, ct.first, n});
+                            const uint32_t n = (uint32_t)std::min<size_t>(ct.second, tile_end > pos ? tile_end - pos : 0);
+                            if (n && need[ct.first]) {
+                                st2.chunks.push_back({pos, ct.first, n});
+                                st2.len[ct.first] += n;
+                            }
                             pos += ct.second;
                         }
                     }
@@ -2048,39 +2289,56 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     };
     const auto h1 = now();
     if (Hd.parts.size() == 1) {
-        part_chunks[0].reserve(nb);
-        t2_part(Hd.parts[0], S, part_chunks[0]);
+        t2_part(0, S);
     } else {
         host_pool().run(Hd.parts.size(), [&](size_t q) {
             ByteSrc BS = S.fork();   // per-call cursor caches (batched regions are shared read-only)
-            t2_part(Hd.parts[q], BS, part_chunks[q]);
+            t2_part(q, BS);
         });
     }
     const auto h2 = now();
-    // decode only the rectangle of tiles that are present (sharded / windowed decode)
-    uint32_t ib = P.ntx, ie = 0, jb = P.nty, je = 0;
-    for (uint32_t t = 0; t < P.tiles.size(); ++t)
-        if (seen[t]) {
-            ib = std::min(ib, t % P.ntx); ie = std::max(ie, t % P.ntx + 1);
-            jb = std::min(jb, t / P.ntx); je = std::max(je, t / P.ntx + 1);
-        }
-    // code-blocks of the tiles in the rectangle (absent tiles decode as zero)
-    std::vector<uint32_t> sel;
+    // ---- the decode table: the needed blocks of the rectangle's tiles, compacted, with offsets
+    // into this call's planes and staging slots, band quantisation from QCD (decoder semantics)
+    std::vector<GkBlock> blk;
+    std::vector<std::vector<int32_t>> part_idx(Hd.parts.size());   // tile-local block -> table entry
+    uint64_t o = 0, t1_bytes = 0;
     for (uint32_t j = jb; j < je; ++j)
         for (uint32_t i = ib; i < ie; ++i) {
+            const int32_t q = part_of[(size_t)j * P.ntx + i];
+            if (q < 0) continue;
             const TileG& T = P.tiles[(size_t)j * P.ntx + i];
-            for (uint32_t b = T.b0; b < T.b1; ++b) sel.push_back(b);
+            const PartState& st2 = ps[q];
+            const std::vector<uint8_t>& need = part_need[q];
+            std::vector<int32_t>& idx = part_idx[q];
+            idx.assign(T.b1 - T.b0, -1);
+            for (uint32_t c = 0; c < P.nc; ++c)
+                for (uint32_t r = 0; r < P.p.numres; ++r) {
+                    const ResG& R = T.comps[c].res[r];
+                    for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
+                        for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                            const PrecG& PG = R.prc[bi][pi];
+                            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                                const uint32_t lb = PG.first_block + k - T.b0;
+                                if (!need[lb]) continue;
+                                GkBlock G = P.blocks[T.b0 + lb];
+                                G.band_off = relocate(P, RG, G.band_off);
+                                G.stride = RG.stride;
+                                G.band_numbps = (uint8_t)R.bands[bi].numbps;
+                                G.step = R.bands[bi].step_dec / 2.0f;
+                                G.numbps = st2.numbps[lb];
+                                G.len = st2.len[lb];
+                                G.npasses = G.len ? st2.npasses[lb] : 0;
+                                G.data_off = o;
+                                t1_bytes += G.len;
+                                o += (((uint64_t)G.len + 15) & ~15ull) + 32;
+                                G.len = 0;   // reused as the fill cursor below
+                                idx[lb] = (int32_t)blk.size();
+                                blk.push_back(G);
+                            }
+                        }
+                }
         }
-    const uint32_t nbr = (uint32_t)sel.size();
-    // output region (image coordinates) and the image position of comps[c][0]
-    uint32_t rx0 = P.tiles[(size_t)jb * P.ntx + ib].x0, ry0 = P.tiles[(size_t)jb * P.ntx + ib].y0;
-    uint32_t rx1 = P.tiles[(size_t)(je - 1) * P.ntx + ie - 1].x1, ry1 = P.tiles[(size_t)(je - 1) * P.ntx + ie - 1].y1;
-    uint32_t ox = 0, oy = 0;
-    if (win) {
-        rx0 = std::max(rx0, win[0]); ry0 = std::max(ry0, win[1]); rx1 = std::min(rx1, win[2]); ry1 = std::min(ry1, win[3]);
-        ox = win[0]; oy = win[1];
-    }
-    const uint32_t ncols = rx1 - rx0, nrows = ry1 - ry0;
+    const uint32_t nbr = (uint32_t)blk.size(), nbx = std::max(nbr, 1u);
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     // ---- stage compressed bytes on the device
     const uint8_t* dcs = cs;
@@ -2093,29 +2351,18 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // bytes of 0xFF (the T1 decoders read their bytes through aligned windows; the Part-1
     // decoder takes the padding as the MQ end-of-data bytes)
     std::vector<uint64_t> seg;
-    uint64_t o = 0, t1_bytes = 0;
     {
         size_t nch = 0;
-        for (auto& pc : part_chunks) {
-            nch += pc.size();
-            for (const Chunk& ch : pc) blk[ch.b].len += ch.len;
-        }
-        for (uint32_t b : sel) {
-            blk[b].data_off = o;
-            const uint32_t L = blk[b].len;
-            t1_bytes += L;
-            if (!L) blk[b].npasses = 0;
-            o += (((uint64_t)L + 15) & ~15ull) + 32;
-            blk[b].len = 0;   // reused as the fill cursor below
-        }
-        seg.resize(3 * nch);
-        size_t k = 0;
-        for (auto& pc : part_chunks)
-            for (const Chunk& ch : pc) {   // stream order = layer order within a block
-                GkBlock& G = blk[ch.b];
-                seg[k] = ch.pos; seg[k + 1] = G.data_off + G.len; seg[k + 2] = ch.len;
+        for (auto& p2 : ps) nch += p2.chunks.size();
+        seg.reserve(3 * nch);
+        for (size_t q = 0; q < ps.size(); ++q)
+            for (const Chunk& ch : ps[q].chunks) {   // stream order = layer order within a block
+                if (part_idx[q].empty()) continue;
+                const int32_t k = part_idx[q][ch.b];
+                if (k < 0) continue;
+                GkBlock& G = blk[k];
+                seg.push_back(ch.pos); seg.push_back(G.data_off + G.len); seg.push_back(ch.len);
                 G.len += ch.len;
-                k += 3;
             }
     }
     uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 256);   // decoder window loads read up to 48 B past a block
@@ -2129,22 +2376,28 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     }
     const uint8_t* src_bytes = stg;
     if (prof)
-        fprintf(stderr, "decode host: headers+setup %.3f ms, packet headers %.3f ms, segments %.3f ms (%zu parts); "
-                        "%llu page fetches %.3f ms (cumulative)\n",
-                ms(h0, h1), ms(h1, h2), ms(h2, now()), Hd.parts.size(), (unsigned long long)ByteSrc::fetch_cnt.load(),
-                ByteSrc::fetch_ns.load() * 1e-6);
-    GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * std::max(nb, 1u));
-    GkBlock* hblk = (GkBlock*)ctx->hinfo.get(sizeof(GkBlock) * std::max(nb, 1u));
-    memcpy(hblk, blk.data(), sizeof(GkBlock) * nb);
-    HIPCHK(hipMemcpyAsync(dblk, hblk, sizeof(GkBlock) * nb, hipMemcpyHostToDevice, st));
+        fprintf(stderr, "decode host: headers+setup %.3f ms, packet headers %.3f ms, segments %.3f ms (%zu parts, "
+                        "%u blocks); %llu page fetches %.3f ms (cumulative)\n",
+                ms(h0, h1), ms(h1, h2), ms(h2, now()), Hd.parts.size(), nbr,
+                (unsigned long long)ByteSrc::fetch_cnt.load(), ByteSrc::fetch_ns.load() * 1e-6);
+    GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * nbx);
+    GkBlock* hblk = (GkBlock*)ctx->hinfo.get(sizeof(GkBlock) * nbx);
+    memcpy(hblk, blk.data(), sizeof(GkBlock) * nbr);
+    HIPCHK(hipMemcpyAsync(dblk, hblk, sizeof(GkBlock) * nbr, hipMemcpyHostToDevice, st));
     ctx->blocks_uploaded = false;   // the encode table must be re-uploaded
-    int32_t* arena = (int32_t*)ctx->arena.get(P.plane_elems * P.nc * 2 * sizeof(int32_t));
+    int32_t* arena = (int32_t*)ctx->arena.get(RG.plane * P.nc * 2 * sizeof(int32_t));
+    // tiles of the rectangle without a tile part decode as zero; blocks skipped by the window
+    // need no clearing (they only feed samples outside the output region)
+    if (Hd.parts.size() < (size_t)(ie - ib) * (je - jb))
+        HIPCHK(hipMemsetAsync(arena, 0, RG.plane * P.nc * 2 * sizeof(int32_t), st));
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    if (P.p.ht()) {
+    if (nbr == 0) {
+        // nothing to decode (all-zero tiles)
+    } else if (P.p.ht()) {
         // HT cleanup pass decode straight into the band windows (T1HT::decompress, T1HT.cpp:134-187)
-        uint32_t* dsel = (uint32_t*)ctx->dord.get(4 * (size_t)nbr + 16);
-        uint32_t* hsel = (uint32_t*)ctx->hord.get(4 * (size_t)nbr + 16);
-        memcpy(hsel, sel.data(), 4 * (size_t)nbr);
+        uint32_t* dsel = (uint32_t*)ctx->dord.get(4 * (size_t)nbx + 16);
+        uint32_t* hsel = (uint32_t*)ctx->hord.get(4 * (size_t)nbx + 16);
+        for (uint32_t k = 0; k < nbr; ++k) hsel[k] = k;
         HIPCHK(hipMemcpyAsync(dsel, hsel, 4 * (size_t)nbr, hipMemcpyHostToDevice, st));
         int* derr = (int*)ctx->derr.get(64);
         HIPCHK(hipMemsetAsync(derr, 0, 64, st));
@@ -2162,23 +2415,22 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         const uint32_t L = gk_t1dec_lanes();
         const uint32_t nw = (nbr + L - 1) / L, nslots = nw * 64;
         uint32_t* hord = (uint32_t*)ctx->hord.get(4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
-        uint32_t* hpos = hord + nslots;               // slot of block sel[k]
-        uint32_t* hids = hpos + nbr;                  // sel
+        uint32_t* hpos = hord + nslots;               // slot of block k
+        uint32_t* hids = hpos + nbr;                  // identity (compact table)
         uint64_t* hwo = (uint64_t*)(hids + nbr + 2);
         {
             std::fill(hord, hord + nslots, 0xffffffffu);
             std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
-            for (uint32_t b : sel) cnt[std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1)]++;
+            for (const GkBlock& G : blk) cnt[std::min<uint32_t>(G.npasses, GK_MAX_PASSES + 1)]++;
             std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
             uint32_t acc = 0;
             for (int k = GK_MAX_PASSES + 1; k >= 0; --k) { start[k] = acc; acc += cnt[k]; }
             for (uint32_t q = 0; q < nbr; ++q) {
-                const uint32_t b = sel[q];
-                uint32_t k = std::min<uint32_t>(blk[b].npasses, GK_MAX_PASSES + 1);
+                const uint32_t k = std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1);
                 const uint32_t idx = start[k]++;
                 const uint32_t slot = (idx / L) * 64 + idx % L;
-                hord[slot] = b; hpos[q] = slot;
-                hids[q] = b;
+                hord[slot] = q; hpos[q] = slot;
+                hids[q] = q;
             }
             uint64_t wo = 0;
             for (uint32_t wv = 0; wv < nw; ++wv) {
@@ -2203,7 +2455,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr);
     }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
-    run_dwt(ctx, false, jb, je, ib, ie);
+    run_dwt(ctx, RG, false, jb, je, ib, ie);
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     // ---- inverse MCT + DC shift + clamp of the output region into the output planes
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
@@ -2220,17 +2472,19 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             dstr[c] = strides[c];
         }
     }
-    auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * P.plane_elems + (size_t)ry0 * P.stride + rx0; };
+    auto planeA = [&](uint32_t c) {
+        return arena + (size_t)c * 2 * RG.plane + (size_t)(ry0 - RG.y0) * RG.stride + (rx0 - RG.x0);
+    };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
     if (!P.p.irrev) {
-        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), P.stride, dst[0], dst[1], dst[2], dstr[0], ncols,
+        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, dst[0], dst[1], dst[2], dstr[0], ncols,
                                        nrows, shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), P.stride, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), RG.stride, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
     } else {
-        if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), P.stride, dst[0], dst[1], dst[2], dstr[0], ncols,
+        if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, dst[0], dst[1], dst[2], dstr[0], ncols,
                                        nrows, shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv_f(st, planeAf(c), P.stride, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv_f(st, planeAf(c), RG.stride, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
     }
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (!out_on_device) {
@@ -2301,7 +2555,7 @@ void gk_set_default_params(gk_cparameters* p) {
     p->numlayers = 1;
     p->numresolution = 6;
     p->cblockw_init = 64; p->cblockh_init = 64;
-    p->mct = 1;
+    p->mct = 0;   // API default (memset in grk_compress_set_default_params, grok.cpp:409); the CLI sets 1 for RGB
     p->numgbits = 2;
     p->write_comment = 1;
     for (int i = 0; i < GK_MAXRLVLS; ++i) { p->prcw_init[i] = 1u << 15; p->prch_init[i] = 1u << 15; }
@@ -2368,6 +2622,11 @@ int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
         (void)hipSetDevice(ctx->device);
         ByteSrc S; S.len = len; S.st = ctx->st;
         if (cs_on_device) S.dev = cs; else S.host = cs;
+        size_t joff = 0, jlen = 0;
+        if (jp2_locate(S, joff, jlen)) {
+            S = ByteSrc(); S.len = jlen; S.st = ctx->st;
+            if (cs_on_device) S.dev = cs + joff; else S.host = cs + joff;
+        }
         Header Hd;
         parse_header(S, Hd);
         info->w = Hd.want.w; info->h = Hd.want.h; info->numcomps = Hd.want.nc; info->prec = Hd.want.prec;
@@ -2375,6 +2634,41 @@ int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
         return 0;
     } catch (const GkError& e) {
         ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_jp2_header(gk_ctx* ctx, const gk_image_info* info, uint64_t cs_len, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!ctx || !info || !out) return -1;
+    try {
+        Plan P;
+        P.w = info->w; P.h = info->h; P.nc = info->numcomps; P.prec = info->prec; P.sgnd = info->sgnd;
+        if (!P.w || !P.h || !P.nc || P.nc > 255 || !P.prec || P.prec > 31) throw GkError("bad image info");
+        std::vector<uint8_t> J;
+        write_jp2_prefix(J, P, cs_len);
+        if (out_len) *out_len = J.size();
+        if (J.size() > cap) { ctx->err = "output capacity too small"; return -2; }
+        memcpy(out, J.data(), J.size());
+        return 0;
+    } catch (const GkError& e) {
+        ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, char* msg, size_t msg_cap) {
+    if (!cs || !info) return -1;
+    try {
+        ByteSrc S; S.len = len; S.host = cs;
+        size_t joff = 0, jlen = 0;
+        if (jp2_locate(S, joff, jlen)) { S = ByteSrc(); S.len = jlen; S.host = cs + joff; }
+        Header Hd;
+        parse_header(S, Hd);
+        info->w = Hd.want.w; info->h = Hd.want.h; info->numcomps = Hd.want.nc; info->prec = Hd.want.prec;
+        info->sgnd = Hd.want.sgnd;
+        return 0;
+    } catch (const GkError& e) {
+        if (msg && msg_cap) snprintf(msg, msg_cap, "%s", e.msg.c_str());
         return -1;
     }
 }

@@ -46,6 +46,8 @@ typedef struct gk_cparameters {
     uint32_t t_width, t_height;          /* grk_cparameters::t_width / t_height (tile origins on the 2^levels grid) */
     uint8_t writeTLM;                    /* grk_cparameters::writeTLM (grk_compress -X) */
     uint8_t writePLT;                    /* grk_cparameters::writePLT (grk_compress -L) */
+    int32_t cod_format;                  /* grk_cparameters::cod_format: GRK_CODEC_J2K (0, raw codestream) or
+                                            GRK_CODEC_JP2 (2, JP2 file boxes around it; FileFormatCompress.cpp) */
 } gk_cparameters;
 
 /* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to
@@ -106,8 +108,19 @@ int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const int32_t* const
 int gk_main_header(gk_ctx* ctx, const gk_image_info* info, const gk_cparameters* p, uint8_t* out, size_t cap,
                    size_t* out_len, size_t* tlm_offset, uint32_t* num_tiles);
 
-/* grk_decompress_read_header (grok.cpp:287-297, CodeStreamDecompress::readHeader) */
+/* JP2 boxes for a file wrapping a codestream of cs_len bytes (signature, ftyp, jp2h with
+ * ihdr + colr, jp2c box header; FileFormatCompress::startCompress / write_jp2c,
+ * FileFormatCompress.cpp:666-693, 59-102): JP2 file = these bytes + the codestream.  Used to
+ * assemble sharded tile parts into a .jp2.  Returns 0, -2 if cap is too small (*out_len = needed). */
+int gk_jp2_header(gk_ctx* ctx, const gk_image_info* info, uint64_t cs_len, uint8_t* out, size_t cap, size_t* out_len);
+
+/* grk_decompress_read_header (grok.cpp:287-297, CodeStreamDecompress::readHeader) of a raw
+ * codestream or a JP2 file (its jp2c box; FileFormatDecompress::read_box_hdr :632-672). */
 int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, gk_image_info* info);
+
+/* The same header parse on host bytes without an engine (no device needed): image info of a
+ * codestream / JP2 file, or < 0 with the reason in msg. */
+int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, char* msg, size_t msg_cap);
 
 /* grk_decompress (grok.cpp:287-297; TileProcessor::decompressT2T1 TileProcessor.cpp:384-408):
  * decode into comps[c] (int32 planes, device memory if out_on_device).  Every tile
