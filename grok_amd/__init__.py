@@ -20,8 +20,9 @@ GK_MAXRLVLS = 33
 GK_MAX_LAYERS = 100
 
 # Exported symbols declared in include/grok_amd.h (checked by tests/test_capi.py).
-EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_decode_header", "gk_decode",
-           "gk_get_timings", "gk_last_error", "gk_version")
+EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_encode_tiles", "gk_main_header",
+           "gk_jp2_header", "gk_decode_header", "gk_probe_header", "gk_decode", "gk_decode_window", "gk_get_timings",
+           "gk_last_error", "gk_version")
 
 
 class CParameters(ctypes.Structure):
@@ -44,7 +45,8 @@ class CParameters(ctypes.Structure):
 
 
 class ImageInfo(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_uint32) for n in ("w", "h", "numcomps", "prec", "sgnd")]
+    """gk_image_info; sample_bytes: 0/4 = int32 planes, 1/2 = planar 8/16-bit samples."""
+    _fields_ = [(n, ctypes.c_uint32) for n in ("w", "h", "numcomps", "prec", "sgnd", "sample_bytes")]
 
 
 class Timings(ctypes.Structure):
@@ -83,14 +85,19 @@ def load_library(build_if_missing=True):
     lib.gk_main_header.restype = ctypes.c_int
     lib.gk_main_header.argtypes = [ctypes.c_void_p, P(ImageInfo), P(CParameters), ctypes.c_void_p, ctypes.c_size_t,
                                    P(ctypes.c_size_t), P(ctypes.c_size_t), P(ctypes.c_uint32)]
+    lib.gk_jp2_header.restype = ctypes.c_int
+    lib.gk_jp2_header.argtypes = [ctypes.c_void_p, P(ImageInfo), ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t,
+                                  P(ctypes.c_size_t)]
+    lib.gk_probe_header.restype = ctypes.c_int
+    lib.gk_probe_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, P(ImageInfo), ctypes.c_char_p, ctypes.c_size_t]
     lib.gk_decode_window.restype = ctypes.c_int
     lib.gk_decode_window.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int] + \
-        [ctypes.c_uint32] * 4 + [P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_int]
+        [ctypes.c_uint32] * 4 + [P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_int]
     lib.gk_decode_header.restype = ctypes.c_int
     lib.gk_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ImageInfo)]
     lib.gk_decode.restype = ctypes.c_int
     lib.gk_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ctypes.c_void_p),
-                              P(ctypes.c_uint32), ctypes.c_int]
+                              P(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_int]
     lib.gk_get_timings.restype = ctypes.c_int
     lib.gk_get_timings.argtypes = [ctypes.c_void_p, P(Timings)]
     lib.gk_last_error.restype = ctypes.c_char_p
@@ -101,7 +108,7 @@ def load_library(build_if_missing=True):
 
 
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
-                   precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False):
+                   precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
     cblk_sty=0x40 selects the HTJ2K block coder; like grk_compress -M 64
@@ -130,7 +137,39 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
         p.tile_size_on = 1
         p.t_width, p.t_height = int(tiles[0]), int(tiles[1])
     p.writeTLM, p.writePLT = int(bool(tlm)), int(bool(plt))
+    p.cod_format = 2 if jp2 else 0   # GRK_CODEC_JP2 / GRK_CODEC_J2K
     return p
+
+
+def probe_header(cs):
+    """gk_probe_header: image info of host codestream / JP2 bytes, no engine or GPU needed."""
+    lib = load_library()
+    b = np.frombuffer(bytes(cs), np.uint8)
+    info = ImageInfo()
+    msg = ctypes.create_string_buffer(256)
+    if lib.gk_probe_header(b.ctypes.data, len(b), ctypes.byref(info), msg, 256) != 0:
+        raise ValueError(msg.value.decode())
+    return info
+
+
+def _sample_bytes(x):
+    """gk_image_info::sample_bytes of a plane array (numpy or torch): 0 for 32-bit, else its item size."""
+    n = x.element_size() if hasattr(x, "element_size") else x.dtype.itemsize
+    return 0 if n == 4 else n
+
+
+def _host_planes(a, prec):
+    """Host planes as passed when their 8/16-bit type fits the precision ((prec + 7) // 8 bytes,
+    grk_compress_tile's raw buffer), int32 otherwise."""
+    if a.dtype.kind in "ui" and a.dtype.itemsize in (1, 2) and a.dtype.itemsize == (prec + 7) // 8:
+        return np.ascontiguousarray(a)
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _np_sample_dtype(sample_bytes, info):
+    if sample_bytes in (0, 4):
+        return np.int32
+    return {(1, 0): np.uint8, (1, 1): np.int8, (2, 0): np.uint16, (2, 1): np.int16}[(sample_bytes, int(info.sgnd))]
 
 
 def _is_torch_cuda(x):
@@ -182,16 +221,17 @@ class Engine:
         if params is None:
             params = default_params()
         c, h, w = planes.shape
-        info = ImageInfo(w, h, c, prec, int(signed))
         on_dev = _is_torch_cuda(planes)
         if on_dev:
-            assert planes.dtype.__str__() == "torch.int32" and planes.is_contiguous()
+            assert planes.is_contiguous() and planes.element_size() in (1, 2, 4)
             base = planes.data_ptr()
-            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
         else:
-            planes = np.ascontiguousarray(planes, dtype=np.int32)
+            planes = _host_planes(planes, prec)
             base = planes.ctypes.data
-            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+        sb = _sample_bytes(planes)
+        es = sb or 4
+        info = ImageInfo(w, h, c, prec, int(signed), sb)
+        ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * es for k in range(c)])
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         n = ctypes.c_size_t()
         if out is not None:
@@ -212,17 +252,18 @@ class Engine:
             self._err("gk_encode")
         return buf[:n.value].tobytes()
 
-    def _planes_ptrs(self, planes, row0=0):
+    def _planes_ptrs(self, planes, row0=0, prec=32):
         """Component base pointers addressing image row 0 for a (C, rows, W) slab whose
         first row is image row ``row0`` (only the slab's rows are ever read)."""
         c, h, w = planes.shape
         if _is_torch_cuda(planes):
-            assert str(planes.dtype) == "torch.int32" and planes.is_contiguous()
+            assert planes.is_contiguous() and planes.element_size() in (1, 2, 4)
             base, keep = planes.data_ptr(), planes
         else:
-            keep = np.ascontiguousarray(planes, dtype=np.int32)
+            keep = _host_planes(planes, prec)
             base = keep.ctypes.data
-        ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 - row0 * w * 4 for k in range(c)])
+        es = _sample_bytes(keep) or 4
+        ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * es - row0 * w * es for k in range(c)])
         return ptrs, keep
 
     def encode_tiles(self, planes, prec, tile_begin, tile_end, image_hw=None, row0=0, signed=False, params=None,
@@ -235,8 +276,8 @@ class Engine:
         c, h, w = planes.shape
         H, W = image_hw if image_hw else (h, w)
         assert W == w
-        info = ImageInfo(W, H, c, prec, int(signed))
-        ptrs, keep = self._planes_ptrs(planes, row0)
+        ptrs, keep = self._planes_ptrs(planes, row0, prec)
+        info = ImageInfo(W, H, c, prec, int(signed), _sample_bytes(keep))
         on_dev = _is_torch_cuda(planes)
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         lens = (ctypes.c_uint32 * (tile_end - tile_begin))()
@@ -257,12 +298,22 @@ class Engine:
         del keep
         return buf[:n.value].tobytes(), list(lens)
 
+    def jp2_header(self, image_shape, prec, cs_len, signed=False):
+        """gk_jp2_header: the JP2 boxes in front of a codestream of cs_len bytes."""
+        c, h, w = image_shape
+        info = ImageInfo(w, h, c, prec, int(signed), 0)
+        buf = np.empty(256, np.uint8)
+        n = ctypes.c_size_t()
+        if self.lib.gk_jp2_header(self.ctx, ctypes.byref(info), cs_len, buf.ctypes.data, buf.size, ctypes.byref(n)) != 0:
+            self._err("gk_jp2_header")
+        return buf[:n.value].tobytes()
+
     def main_header(self, image_shape, prec, signed=False, params=None):
         """gk_main_header: (header bytes, TLM entry offset or 0, number of tiles)."""
         if params is None:
             params = default_params()
         c, h, w = image_shape
-        info = ImageInfo(w, h, c, prec, int(signed))
+        info = ImageInfo(w, h, c, prec, int(signed), 0)
         buf = np.empty(1 << 20, np.uint8)
         n, tlm, nt = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_uint32()
         rc = self.lib.gk_main_header(self.ctx, ctypes.byref(info), ctypes.byref(params), buf.ctypes.data, buf.size,
@@ -283,9 +334,10 @@ class Engine:
             self._err("gk_decode_header")
         return info
 
-    def decode_window(self, cs, window, length=None, out=None):
-        """gk_decode_window: window = (x0, y0, x1, y1).  Returns a (C, y1-y0, x1-x0) int32
-        numpy array, or fills ``out`` (torch cuda int32 of that shape) in place."""
+    def decode_window(self, cs, window, length=None, out=None, sample_bytes=0):
+        """gk_decode_window: window = (x0, y0, x1, y1).  Returns a (C, y1-y0, x1-x0) numpy
+        array (int32, or 8/16-bit with sample_bytes 1/2), or fills ``out`` (a torch cuda
+        tensor of that shape; its element size selects the sample type) in place."""
         on_dev = _is_torch_cuda(cs)
         info = self.read_header(cs, length)
         x0, y0, x1, y1 = window
@@ -293,44 +345,52 @@ class Engine:
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         if out is not None:
             base, res, out_dev = out.data_ptr(), out, 1
+            sample_bytes = _sample_bytes(out)
         else:
-            res = np.empty((c, h, w), np.int32)
+            res = np.empty((c, h, w), _np_sample_dtype(sample_bytes, info))
             base, out_dev = res.ctypes.data, 0
-        ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+        es = sample_bytes or 4
+        ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * es for k in range(c)])
         if on_dev:
             rc = self.lib.gk_decode_window(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, x0, y0, x1, y1, ptrs,
-                                           strides, out_dev)
+                                           strides, sample_bytes, out_dev)
         else:
             b = np.frombuffer(cs, np.uint8)
-            rc = self.lib.gk_decode_window(self.ctx, b.ctypes.data, len(cs), 0, x0, y0, x1, y1, ptrs, strides, out_dev)
+            rc = self.lib.gk_decode_window(self.ctx, b.ctypes.data, len(cs), 0, x0, y0, x1, y1, ptrs, strides,
+                                           sample_bytes, out_dev)
         if rc != 0:
             self._err("gk_decode_window")
         return res
 
-    def decode(self, cs, length=None, out=None, row0=0):
-        """cs: bytes (host) or torch cuda uint8 tensor (+length).  Returns a
-        (C, H, W) int32 numpy array, or fills ``out`` (torch cuda int32) in place.
-        ``out`` may be a (C, rows, W) slab holding image rows [row0, row0+rows) when
-        cs carries only the tile parts of those rows (sharded decode)."""
+    def decode(self, cs, length=None, out=None, row0=0, sample_bytes=0):
+        """cs: bytes (host) or torch cuda uint8 tensor (+length).  Returns a (C, H, W)
+        numpy array (int32, or 8/16-bit with sample_bytes 1/2), or fills ``out`` (torch
+        cuda tensor; its element size selects the sample type) in place.  ``out`` may be
+        a (C, rows, W) slab holding image rows [row0, row0+rows) when cs carries only the
+        tile parts of those rows (sharded decode)."""
         on_dev = _is_torch_cuda(cs)
         info = self.read_header(cs, length)
         c, h, w = info.numcomps, info.h, info.w
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         if out is not None:
+            sample_bytes = _sample_bytes(out)
+            es = sample_bytes or 4
             base = out.data_ptr()
             rows = out.shape[1]
-            ptrs = (ctypes.c_void_p * c)(*[base + k * rows * w * 4 - row0 * w * 4 for k in range(c)])
+            ptrs = (ctypes.c_void_p * c)(*[base + k * rows * w * es - row0 * w * es for k in range(c)])
             res, out_dev = out, 1
         else:
-            res = np.empty((c, h, w), np.int32)
+            es = sample_bytes or 4
+            res = np.empty((c, h, w), _np_sample_dtype(sample_bytes, info))
             base = res.ctypes.data
-            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * 4 for k in range(c)])
+            ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * es for k in range(c)])
             out_dev = 0
         if on_dev:
-            rc = self.lib.gk_decode(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, ptrs, strides, out_dev)
+            rc = self.lib.gk_decode(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, ptrs, strides, sample_bytes,
+                                    out_dev)
         else:
             b = np.frombuffer(cs, np.uint8)
-            rc = self.lib.gk_decode(self.ctx, b.ctypes.data, len(cs), 0, ptrs, strides, out_dev)
+            rc = self.lib.gk_decode(self.ctx, b.ctypes.data, len(cs), 0, ptrs, strides, sample_bytes, out_dev)
         if rc != 0:
             self._err("gk_decode")
         return res

@@ -13,6 +13,12 @@
 #define GK_MAX_RES 33
 #define GK_CTX 19
 
+// Caller sample types of the image planes (gk_image_info::sample_bytes + sgnd):
+// Grok's int32 image components, or the planar 8/16-bit buffers of
+// TileProcessor::ingestUncompressedData (TileProcessor.cpp:779-835).
+enum GkSample { GK_S32 = 0, GK_U8 = 1, GK_S8 = 2, GK_U16 = 3, GK_S16 = 4 };
+static inline __host__ __device__ uint32_t gk_sample_size(int t) { return t == GK_S32 ? 4 : (t <= GK_S8 ? 1 : 2); }
+
 // One code-block job (encode or decode).
 struct GkBlock {
     uint64_t band_off;     // element offset of the block's top-left sample in the coefficient arena

@@ -51,8 +51,9 @@ __device__ __forceinline__ int mirror97(int i, int n) {
 // DC shift + ICT forward (mct.cpp:147-219 CompressIrrev; TileProcessor.cpp:506-535).
 // Output: float written over int32 storage, as in Grok.
 // =============================================================================
-__global__ __launch_bounds__(256) void k_dc_ict_fwd(const int32_t* __restrict__ r_in, const int32_t* __restrict__ g_in,
-                                                    const int32_t* __restrict__ b_in, uint32_t sin,
+template <class TI>
+__global__ __launch_bounds__(256) void k_dc_ict_fwd(const TI* __restrict__ r_in, const TI* __restrict__ g_in,
+                                                    const TI* __restrict__ b_in, uint32_t sin,
                                                     float* __restrict__ y_out, float* __restrict__ u_out,
                                                     float* __restrict__ v_out, uint32_t sout, uint32_t w, uint32_t h,
                                                     int32_t shift) {
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(256) void k_dc_ict_fwd(const int32_t* __restrict__ 
     const float a_r = 0.299f, a_g = 0.587f, a_b = 0.114f;
     const float cb = 0.5f / (1.0f - a_b), cr = 0.5f / (1.0f - a_r);
     const size_t i = (size_t)y * sin + x, o = (size_t)y * sout + x;
-    float r = (float)(r_in[i] - shift), g = (float)(g_in[i] - shift), b = (float)(b_in[i] - shift);
+    float r = (float)((int32_t)r_in[i] - shift), g = (float)((int32_t)g_in[i] - shift), b = (float)((int32_t)b_in[i] - shift);
     float t0 = a_r * r, t1 = a_g * g, t2 = a_b * b;
     float Y = (t0 + t1) + t2;
     y_out[o] = Y;
@@ -71,18 +72,20 @@ __global__ __launch_bounds__(256) void k_dc_ict_fwd(const int32_t* __restrict__ 
 
 // DC shift to float without MCT (the standard behaviour; Grok's mono 9/7 path
 // multiplies by 2048 and reinterprets — R-BUG-1, not reproduced).
-__global__ __launch_bounds__(256) void k_dc_fwd_f(const int32_t* __restrict__ in, uint32_t sin, float* __restrict__ out,
+template <class TI>
+__global__ __launch_bounds__(256) void k_dc_fwd_f(const TI* __restrict__ in, uint32_t sin, float* __restrict__ out,
                                                   uint32_t sout, uint32_t w, uint32_t h, int32_t shift) {
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (x >= w || y >= h) return;
-    out[(size_t)y * sout + x] = (float)(in[(size_t)y * sin + x] - shift);
+    out[(size_t)y * sout + x] = (float)((int32_t)in[(size_t)y * sin + x] - shift);
 }
 
 // Inverse ICT + DC shift + clamp (mct.cpp:284-364 DecompressIrrev, lrintf rounding).
+template <class TO>
 __global__ __launch_bounds__(256) void k_ict_inv_dc(const float* __restrict__ y_in, const float* __restrict__ u_in,
                                                     const float* __restrict__ v_in, uint32_t sin,
-                                                    int32_t* __restrict__ r_out, int32_t* __restrict__ g_out,
-                                                    int32_t* __restrict__ b_out, uint32_t sout, uint32_t w, uint32_t h,
+                                                    TO* __restrict__ r_out, TO* __restrict__ g_out,
+                                                    TO* __restrict__ b_out, uint32_t sout, uint32_t w, uint32_t h,
                                                     int32_t shift, int32_t mn, int32_t mx) {
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (x >= w || y >= h) return;
@@ -91,17 +94,18 @@ __global__ __launch_bounds__(256) void k_ict_inv_dc(const float* __restrict__ y_
     float R = Y + 1.402f * V;
     float G = (Y - 0.34413f * U) - 0.71414f * V;
     float B = Y + 1.772f * U;
-    auto cl = [&](float f) { int32_t v = (int32_t)rintf(f) + shift; return v < mn ? mn : (v > mx ? mx : v); };
+    auto cl = [&](float f) { int32_t v = (int32_t)rintf(f) + shift; return (TO)(v < mn ? mn : (v > mx ? mx : v)); };
     r_out[o] = cl(R); g_out[o] = cl(G); b_out[o] = cl(B);
 }
 
-__global__ __launch_bounds__(256) void k_dc_inv_f(const float* __restrict__ in, uint32_t sin, int32_t* __restrict__ out,
+template <class TO>
+__global__ __launch_bounds__(256) void k_dc_inv_f(const float* __restrict__ in, uint32_t sin, TO* __restrict__ out,
                                                   uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
                                                   int32_t mx) {
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (x >= w || y >= h) return;
     int32_t v = (int32_t)rintf(in[(size_t)y * sin + x]) + shift;
-    out[(size_t)y * sout + x] = v < mn ? mn : (v > mx ? mx : v);
+    out[(size_t)y * sout + x] = (TO)(v < mn ? mn : (v > mx ? mx : v));
 }
 
 // =============================================================================
@@ -247,23 +251,30 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict
 
 #include "gk_launch.h"
 
-void gk_launch_dc_ict_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin, float* y,
+void gk_launch_dc_ict_fwd(hipStream_t st, int stype, const void* r, const void* g, const void* b, uint32_t sin, float* y,
                           float* u, float* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift) {
-    hipLaunchKernelGGL(k_dc_ict_fwd, dim3((w + 255) / 256, h), dim3(256), 0, st, r, g, b, sin, y, u, v, sout, w, h, shift);
+    GK_SAMPLE_DISPATCH(stype, T,
+        hipLaunchKernelGGL(k_dc_ict_fwd<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, (const T*)r, (const T*)g,
+                           (const T*)b, sin, y, u, v, sout, w, h, shift))
 }
-void gk_launch_dc_fwd_f(hipStream_t st, const int32_t* in, uint32_t sin, float* out, uint32_t sout, uint32_t w,
+void gk_launch_dc_fwd_f(hipStream_t st, int stype, const void* in, uint32_t sin, float* out, uint32_t sout, uint32_t w,
                         uint32_t h, int32_t shift) {
-    hipLaunchKernelGGL(k_dc_fwd_f, dim3((w + 255) / 256, h), dim3(256), 0, st, in, sin, out, sout, w, h, shift);
+    GK_SAMPLE_DISPATCH(stype, T,
+        hipLaunchKernelGGL(k_dc_fwd_f<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, (const T*)in, sin, out, sout, w, h,
+                           shift))
 }
-void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const float* v, uint32_t sin, int32_t* r,
-                          int32_t* g, int32_t* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
+void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const float* v, uint32_t sin, int stype, void* r,
+                          void* g, void* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
                           int32_t mx) {
-    hipLaunchKernelGGL(k_ict_inv_dc, dim3((w + 255) / 256, h), dim3(256), 0, st, y, u, v, sin, r, g, b, sout, w, h,
-                       shift, mn, mx);
+    GK_SAMPLE_DISPATCH(stype, T,
+        hipLaunchKernelGGL(k_ict_inv_dc<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, y, u, v, sin, (T*)r, (T*)g, (T*)b,
+                           sout, w, h, shift, mn, mx))
 }
-void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                         uint32_t h, int32_t shift, int32_t mn, int32_t mx) {
-    hipLaunchKernelGGL(k_dc_inv_f, dim3((w + 255) / 256, h), dim3(256), 0, st, in, sin, out, sout, w, h, shift, mn, mx);
+    GK_SAMPLE_DISPATCH(stype, T,
+        hipLaunchKernelGGL(k_dc_inv_f<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, in, sin, (T*)out, sout, w, h, shift,
+                           mn, mx))
 }
 void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb) {

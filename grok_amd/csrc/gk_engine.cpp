@@ -197,6 +197,14 @@ struct Plan {
     uint32_t ntrees = 0;                 // precinct-bands with code-blocks
 };
 
+// Caller sample type (GkSample) of planes described by (sample_bytes, sgnd).
+static int sample_type(uint32_t sample_bytes, uint32_t prec, bool sgnd) {
+    if (sample_bytes == 0 || sample_bytes == 4) return GK_S32;
+    if (sample_bytes != (prec + 7) / 8) throw GkError("sample_bytes must be 4 or (prec + 7) / 8");
+    if (sample_bytes == 1) return sgnd ? GK_S8 : GK_U8;
+    return sgnd ? GK_S16 : GK_U16;
+}
+
 // The image rectangle the work planes hold during one call.  A plan's block offsets
 // (GkBlock::band_off) address planes covering the whole image; a call that touches only
 // some tiles (tile-range encode, sharded or windowed decode) allocates planes for the
@@ -1574,7 +1582,7 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     restore_native_qcd(ctx);
 }
 
-static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, const uint32_t* strides,
                           int comps_on_device, const gk_cparameters* cp, uint8_t* out, size_t cap, int out_on_device,
                           int* rc, uint32_t tb = 0, uint32_t te = 0, bool with_header = true,
                           uint32_t* part_lens = nullptr) {
@@ -1594,19 +1602,23 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     const Region RG = make_region(0, ry0, P.w, ry1);
     int32_t* arena = (int32_t*)ctx->arena.get(RG.plane * P.nc * 2 * sizeof(int32_t));
     const uint32_t nrows = ry1 - ry0;
-    // stage host planes (those rows only)
-    std::vector<const int32_t*> src(P.nc);
+    // the caller's planes (int32 or 8/16-bit samples); host planes are staged (those rows only)
+    const int stype = sample_type(info->sample_bytes, P.prec, P.sgnd != 0);
+    const size_t es = gk_sample_size(stype);
+    std::vector<const void*> src(P.nc);
     std::vector<uint32_t> sstr(P.nc);
     if (!comps_on_device) {
-        int32_t* dp = (int32_t*)ctx->dplanes.get((size_t)P.w * nrows * P.nc * 4);
+        uint8_t* dp = (uint8_t*)ctx->dplanes.get((size_t)P.w * nrows * P.nc * es);
         for (uint32_t c = 0; c < P.nc; ++c) {
-            HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * nrows, (size_t)P.w * 4,
-                                    comps[c] + (size_t)ry0 * strides[c], (size_t)strides[c] * 4,
-                                    (size_t)P.w * 4, nrows, hipMemcpyHostToDevice, st));
-            src[c] = dp + (size_t)c * P.w * nrows; sstr[c] = P.w;
+            HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * nrows * es, (size_t)P.w * es,
+                                    (const uint8_t*)comps[c] + (size_t)ry0 * strides[c] * es, (size_t)strides[c] * es,
+                                    (size_t)P.w * es, nrows, hipMemcpyHostToDevice, st));
+            src[c] = dp + (size_t)c * P.w * nrows * es; sstr[c] = P.w;
         }
     } else {
-        for (uint32_t c = 0; c < P.nc; ++c) { src[c] = comps[c] + (size_t)ry0 * strides[c]; sstr[c] = strides[c]; }
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            src[c] = (const uint8_t*)comps[c] + (size_t)ry0 * strides[c] * es; sstr[c] = strides[c];
+        }
     }
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     // DC shift + MCT into plane A of each component (rows of the selected tiles)
@@ -1614,12 +1626,13 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const int32_t*
     auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * RG.plane; };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
+    if (mct3 && (sstr[1] != sstr[0] || sstr[2] != sstr[0])) throw GkError("the first three components must share a stride");
     if (!P.p.irrev) {
-        if (mct3) gk_launch_dc_rct_fwd(st, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), RG.stride, P.w, nrows, shift);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, src[c], sstr[c], planeA(c), RG.stride, P.w, nrows, shift);
+        if (mct3) gk_launch_dc_rct_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), RG.stride, P.w, nrows, shift);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, stype, src[c], sstr[c], planeA(c), RG.stride, P.w, nrows, shift);
     } else {
-        if (mct3) gk_launch_dc_ict_fwd(st, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), RG.stride, P.w, nrows, shift);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, src[c], sstr[c], planeAf(c), RG.stride, P.w, nrows, shift);
+        if (mct3) gk_launch_dc_ict_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), RG.stride, P.w, nrows, shift);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, stype, src[c], sstr[c], planeAf(c), RG.stride, P.w, nrows, shift);
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     run_dwt(ctx, RG, true, jb, je);
@@ -2072,8 +2085,8 @@ static void prefetch_packet_headers(gk_ctx* ctx, ByteSrc& S, const Plan& P, cons
 
 // win (optional): x0, y0, x1, y1 — decode only the tiles intersecting the window and write
 // the window into comps (whose element 0 is the window's top-left sample).
-static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
-                        const uint32_t* strides, int out_on_device, const uint32_t* win = nullptr) {
+static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void* const* comps,
+                        const uint32_t* strides, uint32_t sample_bytes, int out_on_device, const uint32_t* win = nullptr) {
     hipStream_t st = ctx->st;
     HIPCHK(hipEventRecord(ctx->ev[0], st));
     // GK_PROFILE=1: host phase times of the decode (stderr)
@@ -2461,14 +2474,16 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
     int32_t mn = P.sgnd ? -(1 << (P.prec - 1)) : 0;
     int32_t mx = P.sgnd ? (1 << (P.prec - 1)) - 1 : (int32_t)((1u << P.prec) - 1);
-    std::vector<int32_t*> dst(P.nc);
+    const int stype = sample_type(sample_bytes, P.prec, P.sgnd != 0);
+    const size_t es = gk_sample_size(stype);
+    std::vector<void*> dst(P.nc);
     std::vector<uint32_t> dstr(P.nc);
     if (!out_on_device) {
-        int32_t* stage = (int32_t*)ctx->dplanes.get((size_t)ncols * nrows * P.nc * 4 + 16);
-        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = stage + (size_t)c * ncols * nrows; dstr[c] = ncols; }
+        uint8_t* stage = (uint8_t*)ctx->dplanes.get((size_t)ncols * nrows * P.nc * es + 16);
+        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = stage + (size_t)c * ncols * nrows * es; dstr[c] = ncols; }
     } else {
         for (uint32_t c = 0; c < P.nc; ++c) {
-            dst[c] = comps[c] + (size_t)(ry0 - oy) * strides[c] + (rx0 - ox);
+            dst[c] = (uint8_t*)comps[c] + ((size_t)(ry0 - oy) * strides[c] + (rx0 - ox)) * es;
             dstr[c] = strides[c];
         }
     }
@@ -2478,19 +2493,22 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
     if (!P.p.irrev) {
-        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, dst[0], dst[1], dst[2], dstr[0], ncols,
-                                       nrows, shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv(st, planeA(c), RG.stride, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
+        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
+                                       ncols, nrows, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
+            gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
     } else {
-        if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, dst[0], dst[1], dst[2], dstr[0], ncols,
-                                       nrows, shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_inv_f(st, planeAf(c), RG.stride, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
+        if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
+                                       ncols, nrows, shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
+            gk_launch_dc_inv_f(st, planeAf(c), RG.stride, stype, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
     }
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (!out_on_device) {
         for (uint32_t c = 0; c < P.nc; ++c)
-            HIPCHK(hipMemcpy2DAsync(comps[c] + (size_t)(ry0 - oy) * strides[c] + (rx0 - ox), (size_t)strides[c] * 4, dst[c],
-                                    (size_t)ncols * 4, (size_t)ncols * 4, nrows, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)(ry0 - oy) * strides[c] + (rx0 - ox)) * es,
+                                    (size_t)strides[c] * es, dst[c], (size_t)ncols * es, (size_t)ncols * es, nrows,
+                                    hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipEventRecord(ctx->ev[6], st));
     HIPCHK(hipStreamSynchronize(st));
@@ -2561,7 +2579,7 @@ void gk_set_default_params(gk_cparameters* p) {
     for (int i = 0; i < GK_MAXRLVLS; ++i) { p->prcw_init[i] = 1u << 15; p->prch_init[i] = 1u << 15; }
 }
 
-int gk_encode(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+int gk_encode(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, const uint32_t* strides,
               int comps_on_device, const gk_cparameters* p, uint8_t* out, size_t cap, size_t* out_len,
               int out_on_device) {
     if (!ctx || !info || !comps || !strides || !out) return -1;
@@ -2578,7 +2596,7 @@ int gk_encode(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comp
     }
 }
 
-int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, const uint32_t* strides,
                     int comps_on_device, const gk_cparameters* p, uint32_t tile_begin, uint32_t tile_end,
                     uint8_t* out, size_t cap, size_t* out_len, uint32_t* part_lens, int out_on_device) {
     if (!ctx || !info || !comps || !strides || !out || !part_lens || tile_end <= tile_begin) return -1;
@@ -2673,12 +2691,12 @@ int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, char* ms
     }
 }
 
-int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
-              const uint32_t* strides, int out_on_device) {
+int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void* const* comps,
+              const uint32_t* strides, uint32_t sample_bytes, int out_on_device) {
     if (!ctx || !cs || !comps || !strides) return -1;
     try {
         (void)hipSetDevice(ctx->device);
-        decode_impl(ctx, cs, len, cs_on_device, comps, strides, out_on_device);
+        decode_impl(ctx, cs, len, cs_on_device, comps, strides, sample_bytes, out_on_device);
         return 0;
     } catch (const GkError& e) {
         ctx->err = e.msg;
@@ -2687,12 +2705,13 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int3
 }
 
 int gk_decode_window(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, uint32_t x0, uint32_t y0,
-                     uint32_t x1, uint32_t y1, int32_t* const* comps, const uint32_t* strides, int out_on_device) {
+                     uint32_t x1, uint32_t y1, void* const* comps, const uint32_t* strides, uint32_t sample_bytes,
+                     int out_on_device) {
     if (!ctx || !cs || !comps || !strides) return -1;
     try {
         (void)hipSetDevice(ctx->device);
         const uint32_t win[4] = {x0, y0, x1, y1};
-        decode_impl(ctx, cs, len, cs_on_device, comps, strides, out_on_device, win);
+        decode_impl(ctx, cs, len, cs_on_device, comps, strides, sample_bytes, out_on_device, win);
         return 0;
     } catch (const GkError& e) {
         ctx->err = e.msg;

@@ -15,25 +15,43 @@
 #define LDS_BARRIER() __syncthreads()
 
 // =============================================================================
-// DC level shift + RCT (forward).  In: 3 planes (int32, stride sin), out: 3
-// planes (stride sout).  mct.cpp:99-146, TileProcessor.cpp:506-535.
+// Sample access for the caller's planes: int32 (Grok image components) or the
+// planar 8/16-bit buffers of grk_compress_tile (TileProcessor.cpp:779-835).
+// Four consecutive samples move as one vector access (16 B int32, 4 B u8,
+// 8 B u16) when the host found every pointer and stride aligned (vec != 0).
 // =============================================================================
-__global__ __launch_bounds__(256) void k_dc_rct_fwd(const int32_t* __restrict__ r_in, const int32_t* __restrict__ g_in,
-                                                    const int32_t* __restrict__ b_in, uint32_t sin,
+__device__ __forceinline__ int4 ld4(const int32_t* p) { return *(const int4*)p; }
+__device__ __forceinline__ int4 ld4(const uint8_t* p) { const uchar4 v = *(const uchar4*)p; return make_int4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ int4 ld4(const int8_t* p) { const char4 v = *(const char4*)p; return make_int4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ int4 ld4(const uint16_t* p) { const ushort4 v = *(const ushort4*)p; return make_int4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ int4 ld4(const int16_t* p) { const short4 v = *(const short4*)p; return make_int4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ void st4(int32_t* p, int4 v) { *(int4*)p = v; }
+__device__ __forceinline__ void st4(uint8_t* p, int4 v) { *(uchar4*)p = make_uchar4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ void st4(int8_t* p, int4 v) { *(char4*)p = make_char4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ void st4(uint16_t* p, int4 v) { *(ushort4*)p = make_ushort4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ void st4(int16_t* p, int4 v) { *(short4*)p = make_short4(v.x, v.y, v.z, v.w); }
+
+// =============================================================================
+// DC level shift + RCT (forward).  In: 3 caller planes (stride sin), out: 3
+// int32 work planes (stride sout).  mct.cpp:99-146, TileProcessor.cpp:506-535.
+// =============================================================================
+template <class TI>
+__global__ __launch_bounds__(256) void k_dc_rct_fwd(const TI* __restrict__ r_in, const TI* __restrict__ g_in,
+                                                    const TI* __restrict__ b_in, uint32_t sin,
                                                     int32_t* __restrict__ y_out, int32_t* __restrict__ u_out,
                                                     int32_t* __restrict__ v_out, uint32_t sout, uint32_t w, uint32_t h,
-                                                    int32_t shift) {
+                                                    int32_t shift, int vec) {
     uint32_t x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
     uint32_t y = blockIdx.y;
     if (y >= h || x4 >= w) return;
-    const int32_t* rp = r_in + (size_t)y * sin;
-    const int32_t* gp = g_in + (size_t)y * sin;
-    const int32_t* bp = b_in + (size_t)y * sin;
+    const TI* rp = r_in + (size_t)y * sin;
+    const TI* gp = g_in + (size_t)y * sin;
+    const TI* bp = b_in + (size_t)y * sin;
     int32_t* yp = y_out + (size_t)y * sout;
     int32_t* up = u_out + (size_t)y * sout;
     int32_t* vp = v_out + (size_t)y * sout;
-    if (x4 + 3 < w && ((sin | sout) & 3) == 0) {
-        int4 r = *(const int4*)(rp + x4), g = *(const int4*)(gp + x4), b = *(const int4*)(bp + x4);
+    if (vec && x4 + 3 < w) {
+        int4 r = ld4(rp + x4), g = ld4(gp + x4), b = ld4(bp + x4);
         r.x -= shift; r.y -= shift; r.z -= shift; r.w -= shift;
         g.x -= shift; g.y -= shift; g.z -= shift; g.w -= shift;
         b.x -= shift; b.y -= shift; b.z -= shift; b.w -= shift;
@@ -42,65 +60,68 @@ __global__ __launch_bounds__(256) void k_dc_rct_fwd(const int32_t* __restrict__ 
         Y.z = (r.z + 2 * g.z + b.z) >> 2; Y.w = (r.w + 2 * g.w + b.w) >> 2;
         U.x = b.x - g.x; U.y = b.y - g.y; U.z = b.z - g.z; U.w = b.w - g.w;
         V.x = r.x - g.x; V.y = r.y - g.y; V.z = r.z - g.z; V.w = r.w - g.w;
-        *(int4*)(yp + x4) = Y; *(int4*)(up + x4) = U; *(int4*)(vp + x4) = V;
+        st4(yp + x4, Y); st4(up + x4, U); st4(vp + x4, V);
     } else {
         for (uint32_t x = x4; x < w && x < x4 + 4; ++x) {
-            int32_t r = rp[x] - shift, g = gp[x] - shift, b = bp[x] - shift;
+            int32_t r = (int32_t)rp[x] - shift, g = (int32_t)gp[x] - shift, b = (int32_t)bp[x] - shift;
             yp[x] = (r + 2 * g + b) >> 2; up[x] = b - g; vp[x] = r - g;
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_dc_fwd(const int32_t* __restrict__ in, uint32_t sin, int32_t* __restrict__ out,
+template <class TI>
+__global__ __launch_bounds__(256) void k_dc_fwd(const TI* __restrict__ in, uint32_t sin, int32_t* __restrict__ out,
                                                 uint32_t sout, uint32_t w, uint32_t h, int32_t shift) {
     uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t y = blockIdx.y;
     if (y >= h || x >= w) return;
-    out[(size_t)y * sout + x] = in[(size_t)y * sin + x] - shift;
+    out[(size_t)y * sout + x] = (int32_t)in[(size_t)y * sin + x] - shift;
 }
 
-// Inverse RCT + DC shift + clamp (mct.cpp:221-283).
+// Inverse RCT + DC shift + clamp (mct.cpp:221-283) into the caller's planes.
+template <class TO>
 __global__ __launch_bounds__(256) void k_rct_inv_dc(const int32_t* __restrict__ y_in, const int32_t* __restrict__ u_in,
                                                     const int32_t* __restrict__ v_in, uint32_t sin,
-                                                    int32_t* __restrict__ r_out, int32_t* __restrict__ g_out,
-                                                    int32_t* __restrict__ b_out, uint32_t sout, uint32_t w, uint32_t h,
-                                                    int32_t shift, int32_t mn, int32_t mx) {
+                                                    TO* __restrict__ r_out, TO* __restrict__ g_out,
+                                                    TO* __restrict__ b_out, uint32_t sout, uint32_t w, uint32_t h,
+                                                    int32_t shift, int32_t mn, int32_t mx, int vec) {
     uint32_t x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
     uint32_t y = blockIdx.y;
     if (y >= h || x4 >= w) return;
     const int32_t* Yp = y_in + (size_t)y * sin;
     const int32_t* Up = u_in + (size_t)y * sin;
     const int32_t* Vp = v_in + (size_t)y * sin;
-    int32_t* rp = r_out + (size_t)y * sout;
-    int32_t* gp = g_out + (size_t)y * sout;
-    int32_t* bp = b_out + (size_t)y * sout;
+    TO* rp = r_out + (size_t)y * sout;
+    TO* gp = g_out + (size_t)y * sout;
+    TO* bp = b_out + (size_t)y * sout;
     auto cl = [&](int32_t v) { return v < mn ? mn : (v > mx ? mx : v); };
-    if (x4 + 3 < w && ((sin | sout) & 3) == 0) {
-        int4 Y = *(const int4*)(Yp + x4), U = *(const int4*)(Up + x4), V = *(const int4*)(Vp + x4);
+    if (vec && x4 + 3 < w) {
+        int4 Y = ld4(Yp + x4), U = ld4(Up + x4), V = ld4(Vp + x4);
         int4 R, G, B;
         G.x = Y.x - ((U.x + V.x) >> 2); G.y = Y.y - ((U.y + V.y) >> 2);
         G.z = Y.z - ((U.z + V.z) >> 2); G.w = Y.w - ((U.w + V.w) >> 2);
         R.x = cl(V.x + G.x + shift); R.y = cl(V.y + G.y + shift); R.z = cl(V.z + G.z + shift); R.w = cl(V.w + G.w + shift);
         B.x = cl(U.x + G.x + shift); B.y = cl(U.y + G.y + shift); B.z = cl(U.z + G.z + shift); B.w = cl(U.w + G.w + shift);
         G.x = cl(G.x + shift); G.y = cl(G.y + shift); G.z = cl(G.z + shift); G.w = cl(G.w + shift);
-        *(int4*)(rp + x4) = R; *(int4*)(gp + x4) = G; *(int4*)(bp + x4) = B;
+        st4(rp + x4, R); st4(gp + x4, G); st4(bp + x4, B);
     } else {
         for (uint32_t x = x4; x < w && x < x4 + 4; ++x) {
             int32_t Y = Yp[x], U = Up[x], V = Vp[x];
             int32_t G = Y - ((U + V) >> 2);
-            rp[x] = cl(V + G + shift); gp[x] = cl(G + shift); bp[x] = cl(U + G + shift);
+            rp[x] = (TO)cl(V + G + shift); gp[x] = (TO)cl(G + shift); bp[x] = (TO)cl(U + G + shift);
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_dc_inv(const int32_t* __restrict__ in, uint32_t sin, int32_t* __restrict__ out,
+template <class TO>
+__global__ __launch_bounds__(256) void k_dc_inv(const int32_t* __restrict__ in, uint32_t sin, TO* __restrict__ out,
                                                 uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
                                                 int32_t mx) {
     uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t y = blockIdx.y;
     if (y >= h || x >= w) return;
     int32_t v = in[(size_t)y * sin + x] + shift;
-    out[(size_t)y * sout + x] = v < mn ? mn : (v > mx ? mx : v);
+    out[(size_t)y * sout + x] = (TO)(v < mn ? mn : (v > mx ? mx : v));
 }
 
 // =============================================================================
@@ -308,26 +329,41 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ src,
 // =============================================================================
 #include "gk_launch.h"
 
-void gk_launch_dc_rct_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin,
+// vector path: every plane pointer aligned to 4 samples of its type, strides multiples of 4
+static int vec_ok(uint32_t es_a, const void* a0, const void* a1, const void* a2, uint32_t sa, uint32_t es_b,
+                  const void* b0, const void* b1, const void* b2, uint32_t sb) {
+    auto al = [](const void* p, uint32_t es) { return ((uintptr_t)p % (4 * es)) == 0; };
+    return al(a0, es_a) && al(a1, es_a) && al(a2, es_a) && al(b0, es_b) && al(b1, es_b) && al(b2, es_b) &&
+           (sa & 3) == 0 && (sb & 3) == 0;
+}
+void gk_launch_dc_rct_fwd(hipStream_t st, int stype, const void* r, const void* g, const void* b, uint32_t sin,
                           int32_t* y, int32_t* u, int32_t* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift) {
     dim3 grid((w + 1023) / 1024, h);
-    hipLaunchKernelGGL(k_dc_rct_fwd, grid, dim3(256), 0, st, r, g, b, sin, y, u, v, sout, w, h, shift);
+    const int vec = vec_ok(gk_sample_size(stype), r, g, b, sin, 4, y, u, v, sout);
+    GK_SAMPLE_DISPATCH(stype, T,
+        hipLaunchKernelGGL(k_dc_rct_fwd<T>, grid, dim3(256), 0, st, (const T*)r, (const T*)g, (const T*)b, sin, y, u, v,
+                           sout, w, h, shift, vec))
 }
-void gk_launch_dc_fwd(hipStream_t st, const int32_t* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+void gk_launch_dc_fwd(hipStream_t st, int stype, const void* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift) {
     dim3 grid((w + 255) / 256, h);
-    hipLaunchKernelGGL(k_dc_fwd, grid, dim3(256), 0, st, in, sin, out, sout, w, h, shift);
+    GK_SAMPLE_DISPATCH(stype, T,
+        hipLaunchKernelGGL(k_dc_fwd<T>, grid, dim3(256), 0, st, (const T*)in, sin, out, sout, w, h, shift))
 }
-void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, const int32_t* v, uint32_t sin,
-                          int32_t* r, int32_t* g, int32_t* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift,
+void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, const int32_t* v, uint32_t sin, int stype,
+                          void* r, void* g, void* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift,
                           int32_t mn, int32_t mx) {
     dim3 grid((w + 1023) / 1024, h);
-    hipLaunchKernelGGL(k_rct_inv_dc, grid, dim3(256), 0, st, y, u, v, sin, r, g, b, sout, w, h, shift, mn, mx);
+    const int vec = vec_ok(4, y, u, v, sin, gk_sample_size(stype), r, g, b, sout);
+    GK_SAMPLE_DISPATCH(stype, T,
+        hipLaunchKernelGGL(k_rct_inv_dc<T>, grid, dim3(256), 0, st, y, u, v, sin, (T*)r, (T*)g, (T*)b, sout, w, h, shift,
+                           mn, mx, vec))
 }
-void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift, int32_t mn, int32_t mx) {
     dim3 grid((w + 255) / 256, h);
-    hipLaunchKernelGGL(k_dc_inv, grid, dim3(256), 0, st, in, sin, out, sout, w, h, shift, mn, mx);
+    GK_SAMPLE_DISPATCH(stype, T,
+        hipLaunchKernelGGL(k_dc_inv<T>, grid, dim3(256), 0, st, in, sin, (T*)out, sout, w, h, shift, mn, mx))
 }
 void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb) {

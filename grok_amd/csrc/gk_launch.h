@@ -4,14 +4,25 @@
 #include <stdint.h>
 #include "gk_common.h"
 
-void gk_launch_dc_rct_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin,
+// Dispatch on the caller's sample type (GkSample): T names the element type in the body.
+#define GK_SAMPLE_DISPATCH(t, T, ...)                            \
+    switch (t) {                                                 \
+        case GK_U8: { typedef uint8_t T; __VA_ARGS__; break; }   \
+        case GK_S8: { typedef int8_t T; __VA_ARGS__; break; }    \
+        case GK_U16: { typedef uint16_t T; __VA_ARGS__; break; } \
+        case GK_S16: { typedef int16_t T; __VA_ARGS__; break; }  \
+        default: { typedef int32_t T; __VA_ARGS__; break; }      \
+    }
+
+// DC shift / MCT between the caller's planes (sample type stype, GkSample) and the int32 work planes
+void gk_launch_dc_rct_fwd(hipStream_t st, int stype, const void* r, const void* g, const void* b, uint32_t sin,
                           int32_t* y, int32_t* u, int32_t* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift);
-void gk_launch_dc_fwd(hipStream_t st, const int32_t* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+void gk_launch_dc_fwd(hipStream_t st, int stype, const void* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift);
-void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, const int32_t* v, uint32_t sin,
-                          int32_t* r, int32_t* g, int32_t* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift,
+void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, const int32_t* v, uint32_t sin, int stype,
+                          void* r, void* g, void* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift,
                           int32_t mn, int32_t mx);
-void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift, int32_t mn, int32_t mx);
 void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
                          uint32_t w, uint32_t h,
@@ -32,14 +43,14 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
                         const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks);
 // irreversible path (gk_dwt97.hip)
-void gk_launch_dc_ict_fwd(hipStream_t st, const int32_t* r, const int32_t* g, const int32_t* b, uint32_t sin, float* y,
+void gk_launch_dc_ict_fwd(hipStream_t st, int stype, const void* r, const void* g, const void* b, uint32_t sin, float* y,
                           float* u, float* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift);
-void gk_launch_dc_fwd_f(hipStream_t st, const int32_t* in, uint32_t sin, float* out, uint32_t sout, uint32_t w,
+void gk_launch_dc_fwd_f(hipStream_t st, int stype, const void* in, uint32_t sin, float* out, uint32_t sout, uint32_t w,
                         uint32_t h, int32_t shift);
-void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const float* v, uint32_t sin, int32_t* r,
-                          int32_t* g, int32_t* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
+void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const float* v, uint32_t sin, int stype, void* r,
+                          void* g, void* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
                           int32_t mx);
-void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
+void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                         uint32_t h, int32_t shift, int32_t mn, int32_t mx);
 void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
                          uint32_t h,

@@ -58,6 +58,10 @@ typedef struct gk_image_info {
     uint32_t numcomps;      /* grk_image::numcomps */
     uint32_t prec;          /* grk_image_comp::prec (same for every component) */
     uint32_t sgnd;          /* grk_image_comp::sgnd */
+    uint32_t sample_bytes;  /* the caller's planes: 0 or 4 = int32 (grk_image_comp::data); 1 / 2 = planar
+                               8 / 16-bit samples, signed iff sgnd, as grk_compress_tile's buffer
+                               (TileProcessor::ingestUncompressedData, TileProcessor.cpp:779-835);
+                               must be 4 or (prec + 7) / 8.  Decode writes the same type. */
 } gk_image_info;
 
 /* Per-stage device times of the last call (HIP events on the engine stream). */
@@ -82,11 +86,11 @@ void gk_set_default_params(gk_cparameters* p);
 
 /* grk_compress_init + grk_compress_start + grk_compress + grk_compress_end
  * (grok.cpp:382-469; TileProcessor::doCompress TileProcessor.cpp:202-260) for a
- * single- or multi-tile image (all tiles in one pass; one tile part per tile).  comps[c] points at component c's int32 plane (device
+ * single- or multi-tile image (all tiles in one pass; one tile part per tile).  comps[c] points at component c's plane (device
  * memory if comps_on_device, host otherwise).  The codestream is written to
  * out (device memory if out_on_device); *out_len receives its size.
  * Returns 0, or < 0 on error (-2: capacity too small, *out_len = needed). */
-int gk_encode(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+int gk_encode(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, const uint32_t* strides,
               int comps_on_device, const gk_cparameters* p, uint8_t* out, size_t cap, size_t* out_len,
               int out_on_device);
 
@@ -96,7 +100,7 @@ int gk_encode(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comp
  * selected tiles are read.  out receives their tile parts (SOT [PLT] SOD packets,
  * CodeStreamCompress::writeTilePart :862-900) back to back; part_lens[i] = length
  * of tile tile_begin + i (the TLM Ptlm value).  Returns 0 / < 0 like gk_encode. */
-int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const int32_t* const* comps, const uint32_t* strides,
+int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, const uint32_t* strides,
                     int comps_on_device, const gk_cparameters* p, uint32_t tile_begin, uint32_t tile_end,
                     uint8_t* out, size_t cap, size_t* out_len, uint32_t* part_lens, int out_on_device);
 
@@ -123,11 +127,12 @@ int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
 int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, char* msg, size_t msg_cap);
 
 /* grk_decompress (grok.cpp:287-297; TileProcessor::decompressT2T1 TileProcessor.cpp:384-408):
- * decode into comps[c] (int32 planes, device memory if out_on_device).  Every tile
+ * decode into comps[c] (device memory if out_on_device): int32 planes (sample_bytes 0 / 4) or planar
+ * (prec + 7) / 8-byte samples (sample_bytes 1 / 2, signed iff the image is; gk_image_info).  Every tile
  * part present in cs is decoded; a stream holding the main header and only some
  * tile parts (tile sharding, window decode) writes only those tiles' samples. */
-int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int32_t* const* comps,
-              const uint32_t* strides, int out_on_device);
+int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void* const* comps,
+              const uint32_t* strides, uint32_t sample_bytes, int out_on_device);
 
 /* grk_decompress_set_window + grk_decompress (grok.h:1082-1657; CodeStreamDecompress
  * window decode): decode the window [x0, x1) x [y0, y1) of the image.
@@ -135,7 +140,8 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, int3
  * when present, their packet headers through PLT), decoded and inverse-transformed;
  * comps[c][0] receives sample (x0, y0) of component c, row stride strides[c]. */
 int gk_decode_window(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, uint32_t x0, uint32_t y0,
-                     uint32_t x1, uint32_t y1, int32_t* const* comps, const uint32_t* strides, int out_on_device);
+                     uint32_t x1, uint32_t y1, void* const* comps, const uint32_t* strides, uint32_t sample_bytes,
+                     int out_on_device);
 
 /* Stage timings of the last gk_encode / gk_decode. */
 int gk_get_timings(gk_ctx* ctx, gk_timings* t);

@@ -8,8 +8,14 @@
 // not include, link or call anything in this directory.
 //
 // Parity pin: the outputs of this restatement are checked byte-for-byte
-// against codestreams produced by reference Grok 9.2.0 (the binaries built by
-// the survey stage; see tests/golden/make_fixtures.sh and DESIGN.md §Oracle).
+// against codestreams produced by reference Grok 9.2.0 (the binaries the survey
+// stage built with cmake; fixtures made by
+// tests/golden/make_fixtures.py and make_fullsize.py).  The JP2
+// box wrapper (FileFormatCompress.cpp) is restated but not pinned by a Grok
+// output: Grok needs cmake-generated headers, so it is not rebuilt here.
+//
+// Threads (orc_set_threads): code-blocks of a tile, and tiles of a multi-tile
+// image, are coded on worker threads; the result does not depend on the count.
 //
 // Every stage cites the reference function it restates (paths relative to
 // /root/reference/src/lib/jp2/).  The code is written from the JPEG 2000
@@ -26,9 +32,32 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <atomic>
 #include <functional>
+#include <thread>
 
 namespace orc {
+
+// ----------------------------------------------------------------------------
+// Worker threads: par_for(n, f) runs f(0..n-1) on up to g_threads threads
+// (nested calls run serially on the calling thread).
+// ----------------------------------------------------------------------------
+static unsigned g_threads = 1;
+static thread_local bool t_in_par = false;
+template <class F> static void par_for(size_t n, F f) {
+    const unsigned T = (unsigned)std::min<size_t>(g_threads, n);
+    if (T <= 1 || t_in_par) { for (size_t i = 0; i < n; ++i) f(i); return; }
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        t_in_par = true;
+        for (;;) { const size_t i = next++; if (i >= n) break; f(i); }
+        t_in_par = false;
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+}
 
 static inline uint32_t ceildivpow2(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + (1ull << b) - 1) >> b); }
 static inline uint32_t floordivpow2(uint32_t a, uint32_t b) { return a >> b; }
@@ -1490,7 +1519,11 @@ typedef struct {
     double layer_rate[100];
     uint32_t cblk_sty;
     uint32_t tile_w, tile_h, tlm, plt;
+    uint32_t cod_format;   // 0 = raw codestream (GRK_CODEC_J2K), 2 = JP2 file (GRK_CODEC_JP2)
 } orc_cparams;
+
+void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
+unsigned orc_get_threads(void) { return g_threads; }
 
 static Params to_params(const orc_cparams* cp) {
     Params p;
@@ -1540,19 +1573,25 @@ static void t1_encode_all(EncodeState& E) {
     static const double norms_irrev[3] = {1.732, 1.805, 1.573};   // mct.cpp:689-704
     static const double norms_rev[3] = {1.732, .8292, .8292};
     const bool mct = E.p.mct && E.im.nc >= 3;
-    for (uint32_t c = 0; c < E.im.nc; ++c) {
-        Comp& C = E.comps[c];
+    struct Job { uint32_t c, r; Band* B; Cblk* K; };
+    std::vector<Job> jobs;
+    for (uint32_t c = 0; c < E.im.nc; ++c)
         for (uint32_t r = 0; r < E.p.numres; ++r)
-            for (auto& B : C.res[r].bands)
+            for (auto& B : E.comps[c].res[r].bands)
                 for (auto& P : B.prcs)
-                    for (auto& K : P.cblks) {
+                    for (auto& K : P.cblks) jobs.push_back({c, r, &B, &K});
+    par_for(jobs.size(), [&](size_t ji) {
+                        const uint32_t c = jobs[ji].c, r = jobs[ji].r;
+                        Comp& C = E.comps[c];
+                        Band& B = *jobs[ji].B;
+                        Cblk& K = *jobs[ji].K;
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
                         if (E.p.ht()) {   // T1HT::compress (T1HT.cpp:109-133): one cleanup pass
                             const int32_t* src = E.coefs[c].data() + (size_t)(B.offy + K.y0 - B.y0) * C.w + (B.offx + K.x0 - B.x0);
                             K.data = ht_encode_block(src, w, h, C.w);
                             uint32_t L = (uint32_t)K.data.size();
                             K.numbps = 1; K.npasses = 1; K.passes.assign(1, PassInfo{L, L, 1, 0.0});
-                            continue;
+                            return;
                         }
                         std::vector<uint32_t> mag(w * h); std::vector<uint8_t> neg(w * h);
                         for (uint32_t y = 0; y < h; ++y)
@@ -1572,12 +1611,15 @@ static void t1_encode_all(EncodeState& E) {
                         BlockEncResult res;
                         t1_encode_block(mag.data(), neg.data(), w, h, B.orient, res, rc ? &dc : nullptr);
                         K.numbps = res.numbps; K.npasses = res.npasses; K.data = res.data; K.passes = res.passes;
-                    }
-    }
+    });
 }
 
+// planes: nc planes of `rows` rows (row stride w) holding image rows [row0, row0 + rows);
+// rows = 0 means the whole image
 static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc,
-                           uint32_t prec, int sgnd, const orc_cparams* cp, uint32_t tile = 0) {
+                           uint32_t prec, int sgnd, const orc_cparams* cp, uint32_t tile = 0, uint32_t row0 = 0,
+                           uint32_t rows = 0) {
+    if (!rows) rows = h;
     E.im = Image{w, h, nc, prec, sgnd != 0};
     E.p = to_params(cp);
     if (nc < 3) E.p.mct = 0;
@@ -1593,7 +1635,8 @@ static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, ui
     for (uint32_t c = 0; c < nc; ++c) {   // tile-local copy (TileProcessor::ingestImage, TileProcessor.cpp:410-431)
         E.coefs[c].resize((size_t)tw * th);
         for (uint32_t y = 0; y < th; ++y)
-            memcpy(&E.coefs[c][(size_t)y * tw], planes + (size_t)c * w * h + (size_t)(E.ty0 + y) * w + E.tx0, (size_t)tw * 4);
+            memcpy(&E.coefs[c][(size_t)y * tw], planes + (size_t)c * w * rows + (size_t)(E.ty0 - row0 + y) * w + E.tx0,
+                   (size_t)tw * 4);
     }
     if (!E.p.irreversible) {
         dc_rct_fwd(E.coefs, prec, sgnd != 0, E.p.mct != 0);
@@ -1787,11 +1830,50 @@ static uint32_t write_tile_part(std::vector<uint8_t>& o, EncodeState& E) {
 
 // Full encode (5/3 or 9/7, Part 1 or HT, any number of layers, one or more tiles).
 // Returns the codestream size, or 0 on failure / insufficient capacity.
+static void jp2_prefix(std::vector<uint8_t>& o, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
+                       uint64_t cs_len);
+
 size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
                   const orc_cparams* cp, uint8_t* out, size_t cap) {
     std::vector<uint8_t> o;
     size_t tlm_pos = 0;
     uint32_t nt = 0;
+    const Params p0 = to_params(cp);
+    if (!needs_rate_control(p0) && tile_count(p0, w, h) > 1) {
+        // independent tiles coded in parallel, written in tile order
+        nt = tile_count(p0, w, h);
+        {
+            EncodeState E0;
+            E0.im = Image{w, h, nc, prec, sgnd != 0};
+            E0.p = p0;
+            if (nc < 3) E0.p.mct = 0;
+            E0.comps.assign(1, Comp());
+            uint32_t x0, y0, x1, y1;
+            tile_rect(E0.p, w, h, 0, x0, y0, x1, y1);
+            build_geometry(E0.comps[0], x0, y0, x1, y1, E0.p);
+            assign_steps(E0.comps[0], E0.p, prec, true, nullptr);
+            write_main_header(o, E0.im, E0.p, E0.comps[0], &tlm_pos);
+        }
+        std::vector<std::vector<uint8_t>> parts(nt);
+        par_for(nt, [&](size_t t) {
+            EncodeState E;
+            prepare_encode(E, planes, w, h, nc, prec, sgnd, cp, (uint32_t)t);
+            t1_encode_all(E);
+            rate_allocate(E);
+            write_tile_part(parts[t], E);
+        });
+        for (uint32_t t = 0; t < nt; ++t) {
+            const uint32_t psot = (uint32_t)parts[t].size();
+            if (p0.tlm) {
+                size_t q = tlm_pos + (size_t)6 * t;
+                o[q] = (uint8_t)(t >> 8); o[q + 1] = (uint8_t)t;
+                o[q + 2] = (uint8_t)(psot >> 24); o[q + 3] = (uint8_t)(psot >> 16); o[q + 4] = (uint8_t)(psot >> 8); o[q + 5] = (uint8_t)psot;
+            }
+            o.insert(o.end(), parts[t].begin(), parts[t].end());
+            std::vector<uint8_t>().swap(parts[t]);
+        }
+        put16(o, 0xffd9);
+    } else
     for (uint32_t t = 0;; ++t) {
         EncodeState E;
         prepare_encode(E, planes, w, h, nc, prec, sgnd, cp, t);
@@ -1808,12 +1890,88 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
             o[q] = (uint8_t)(t >> 8); o[q + 1] = (uint8_t)t;
             o[q + 2] = (uint8_t)(psot >> 24); o[q + 3] = (uint8_t)(psot >> 16); o[q + 4] = (uint8_t)(psot >> 8); o[q + 5] = (uint8_t)psot;
         }
-        if (t + 1 >= nt) break;
+        if (t + 1 >= nt) { put16(o, 0xffd9); break; }
     }
-    put16(o, 0xffd9);
+    std::vector<uint8_t> J;
+    if (cp && cp->cod_format == 2) jp2_prefix(J, w, h, nc, prec, sgnd, o.size());
+    if (J.size() + o.size() > cap) return 0;
+    memcpy(out, J.data(), J.size());
+    memcpy(out + J.size(), o.data(), o.size());
+    return J.size() + o.size();
+}
+
+// ----------------------------------------------------------------------------
+// JP2 file format (ISO 15444-1 Annex I) as Grok writes it for PNM input:
+// signature box, ftyp (brand/compat 'jp2 '), jp2h = ihdr (22 B) + colr (15 B,
+// METH 1, EnumCS sRGB 16 / greyscale 17), then the jp2c box, whose header has an
+// 8-byte XLBox when the raw image exceeds 2^30 bytes (FileFormatCompress.cpp:
+// write_jp :43-58, write_ftyp :103-148, write_jp2h :176-264, write_colr :344-403,
+// write_ihdr :619-665, startCompress :678-686, write_jp2c :59-102).
+// ----------------------------------------------------------------------------
+static void jp2_prefix(std::vector<uint8_t>& o, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
+                       uint64_t cs_len) {
+    auto box = [&](uint32_t len, const char* type) { put32(o, len); o.insert(o.end(), type, type + 4); };
+    box(12, "jP  "); put32(o, 0x0d0a870a);
+    box(20, "ftyp"); o.insert(o.end(), {'j', 'p', '2', ' '}); put32(o, 0); o.insert(o.end(), {'j', 'p', '2', ' '});
+    box(45, "jp2h");
+    box(22, "ihdr"); put32(o, h); put32(o, w); put16(o, nc);
+    o.push_back((uint8_t)((prec - 1) + (sgnd ? 128 : 0))); o.push_back(7); o.push_back(0); o.push_back(0);
+    box(15, "colr"); o.push_back(1); o.push_back(0); o.push_back(0); put32(o, nc < 3 ? 17 : 16);
+    const bool xl = (uint64_t)nc * w * h * ((prec + 7) / 8) > (1ull << 30);
+    if (xl) { box(1, "jp2c"); put32(o, (uint32_t)((cs_len + 16) >> 32)); put32(o, (uint32_t)(cs_len + 16)); }
+    else box(cs_len + 8 < (1ull << 32) ? (uint32_t)(cs_len + 8) : 0, "jp2c");
+}
+
+size_t orc_jp2_header(uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd, uint64_t cs_len, uint8_t* out) {
+    std::vector<uint8_t> J;
+    jp2_prefix(J, w, h, nc, prec, sgnd, cs_len);
+    if (out) memcpy(out, J.data(), J.size());
+    return J.size();
+}
+
+// Main header alone (SOC .. TLM placeholder .. COM), for assembling tile parts coded separately.
+size_t orc_main_header(uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd, const orc_cparams* cp, uint8_t* out,
+                       size_t cap, size_t* tlm_offset) {
+    EncodeState E0;
+    E0.im = Image{w, h, nc, prec, sgnd != 0};
+    E0.p = to_params(cp);
+    if (nc < 3) E0.p.mct = 0;
+    E0.comps.assign(1, Comp());
+    uint32_t x0, y0, x1, y1;
+    tile_rect(E0.p, w, h, 0, x0, y0, x1, y1);
+    build_geometry(E0.comps[0], x0, y0, x1, y1, E0.p);
+    assign_steps(E0.comps[0], E0.p, prec, true, nullptr);
+    std::vector<uint8_t> o;
+    size_t tlm = 0;
+    write_main_header(o, E0.im, E0.p, E0.comps[0], &tlm);
+    if (tlm_offset) *tlm_offset = E0.p.tlm ? tlm : 0;
     if (o.size() > cap) return 0;
     memcpy(out, o.data(), o.size());
     return o.size();
+}
+
+// Tile parts of tiles [tb, te) (no rate control) from a slab holding image rows
+// [row0, row0 + rows) of every component (component stride w * rows); part_lens[i]
+// = Psot of tile tb + i.  Returns the bytes written, 0 if cap is too small.
+size_t orc_encode_tile_parts(const int32_t* slab, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
+                             const orc_cparams* cp, uint32_t row0, uint32_t rows, uint32_t tb, uint32_t te,
+                             uint8_t* out, size_t cap, uint32_t* part_lens) {
+    std::vector<std::vector<uint8_t>> parts(te - tb);
+    par_for(te - tb, [&](size_t q) {
+        EncodeState E;
+        prepare_encode(E, slab, w, h, nc, prec, sgnd, cp, tb + (uint32_t)q, row0, rows);
+        t1_encode_all(E);
+        rate_allocate(E);
+        write_tile_part(parts[q], E);
+    });
+    size_t n = 0;
+    for (size_t q = 0; q < parts.size(); ++q) {
+        if (n + parts[q].size() > cap) return 0;
+        memcpy(out + n, parts[q].data(), parts[q].size());
+        part_lens[q] = (uint32_t)parts[q].size();
+        n += parts[q].size();
+    }
+    return n;
 }
 
 // Stage dump: forward DC+RCT+DWT coefficients (Mallat, stride w), nc planes.
@@ -1985,19 +2143,28 @@ t2done:
     // T1 decode + dequantisation + inverse DWT + inverse MCT
     std::vector<std::vector<int32_t>> ip(im.nc);
     std::vector<std::vector<float>> fp(im.nc);
+    struct Job { uint32_t c; Band* B; Cblk* K; };
+    std::vector<Job> jobs;
     for (uint32_t c = 0; c < im.nc; ++c) {
-        Comp& C = comps[c];
         if (!p.irreversible) ip[c].assign((size_t)TW * TH, 0); else fp[c].assign((size_t)TW * TH, 0.f);
         for (uint32_t r = 0; r < p.numres; ++r)
-            for (auto& B : C.res[r].bands)
+            for (auto& B : comps[c].res[r].bands)
                 for (auto& P : B.prcs)
-                    for (auto& K : P.cblks) {
+                    for (auto& K : P.cblks) jobs.push_back({c, &B, &K});
+    }
+    std::vector<int> jrc(jobs.size(), 0);
+    par_for(jobs.size(), [&](size_t ji) {
+                        const uint32_t c = jobs[ji].c;
+                        Band& B = *jobs[ji].B;
+                        Cblk& K = *jobs[ji].K;
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
                         std::vector<int32_t> blk(w * h);
                         if (p.ht()) {   // T1HT::decompress: k_msbs = band numbps - cblk numbps
                             if (K.npasses && !ht_decode_block(K.data.data(), (uint32_t)K.data.size(), w, h,
-                                                              B.numbps - K.numbps, blk.data(), w))
-                                return -4;
+                                                              B.numbps - K.numbps, blk.data(), w)) {
+                                jrc[ji] = -4;
+                                return;
+                            }
                             if (!p.irreversible) for (auto& v : blk) v *= 2;   // same ShiftFilter below
                         } else
                         t1_decode_block(K.data.data(), (uint32_t)K.data.size(), K.npasses, K.numbps, B.orient, w, h, blk.data());
@@ -2008,7 +2175,10 @@ t2done:
                                 if (!p.irreversible) ip[c][o] = v / 2;                 // ShiftFilter
                                 else fp[c][o] = (float)v * B.stepsize / 2.0f;          // ScaleFilter
                             }
-                    }
+    });
+    for (int rc : jrc) if (rc) return rc;
+    for (uint32_t c = 0; c < im.nc; ++c) {
+        Comp& C = comps[c];
         if (!p.irreversible) dwt2d<int32_t>(ip[c].data(), TW, C, p.numres, false, inv53_1d);
         else dwt2d<float>(fp[c].data(), TW, C, p.numres, false, inv97_1d);
     }
@@ -2043,6 +2213,20 @@ t2done:
 
 int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_t* H, uint32_t* NC, uint32_t* PREC) {
     size_t i = 0;
+    if (len >= 12 && get32(cs) == 12 && get32(cs + 4) == 0x6a502020) {   // JP2: find the jp2c box
+        size_t pos = 12;
+        bool found = false;
+        while (pos + 8 <= len) {
+            uint64_t L = get32(cs + pos);
+            size_t hdr = 8;
+            if (L == 1) { L = ((uint64_t)get32(cs + pos + 8) << 32) | get32(cs + pos + 12); hdr = 16; }
+            else if (L == 0) L = len - pos;
+            if (L < hdr || L > len - pos) return -6;
+            if (get32(cs + pos + 4) == 0x6a703263) { cs += pos + hdr; len = (size_t)L - hdr; found = true; break; }
+            pos += (size_t)L;
+        }
+        if (!found) return -6;
+    }
     if (len < 4 || get16(cs) != 0xff4f) return -1;
     i = 2;
     Image im{}; Params p; p.write_com = 0;
@@ -2082,6 +2266,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     std::fill(out, out + (size_t)im.nc * im.w * im.h, 0);
     const uint32_t nt = tile_count(p, im.w, im.h);
     size_t pos = first_sot;
+    struct Part { size_t data, end; uint32_t tile; };
+    std::vector<Part> parts;
     while (pos + 12 <= len && get16(cs + pos) == 0xff90) {
         const uint8_t* s = cs + pos + 4;
         uint32_t isot = get16(s), psot = get32(s + 2);
@@ -2090,10 +2276,12 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         size_t j = pos + 12;   // tile-part header markers (PLT, ...) until SOD
         while (j + 2 <= tile_end && get16(cs + j) != 0xff93) j += 2 + get16(cs + j + 2);
         if (j + 2 > tile_end) return -5;
-        int rc = decode_tile(cs, j + 2, tile_end, p, im, qcd, isot, out);
-        if (rc) return rc;
+        parts.push_back({j + 2, tile_end, isot});
         pos = tile_end;
     }
+    std::vector<int> rcs(parts.size(), 0);   // tiles write disjoint rectangles of out
+    par_for(parts.size(), [&](size_t q) { rcs[q] = decode_tile(cs, parts[q].data, parts[q].end, p, im, qcd, parts[q].tile, out); });
+    for (int rc : rcs) if (rc) return rc;
     return 0;
 }
 

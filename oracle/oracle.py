@@ -23,6 +23,7 @@ class CParams(ctypes.Structure):
         ("layer_rate", ctypes.c_double * 100),
         ("cblk_sty", ctypes.c_uint32),
         ("tile_w", ctypes.c_uint32), ("tile_h", ctypes.c_uint32), ("tlm", ctypes.c_uint32), ("plt", ctypes.c_uint32),
+        ("cod_format", ctypes.c_uint32),
     ]
 
 
@@ -60,6 +61,16 @@ def lib():
             ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_uint32), P(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_void_p]
         _lib.orc_t1_decode_cblk.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [P(ctypes.c_int32)]
         _lib.orc_default_params.argtypes = [P(CParams)]
+        _lib.orc_set_threads.argtypes = [ctypes.c_uint]
+        _lib.orc_get_threads.restype = ctypes.c_uint
+        _lib.orc_jp2_header.restype = ctypes.c_size_t
+        _lib.orc_jp2_header.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p]
+        _lib.orc_main_header.restype = ctypes.c_size_t
+        _lib.orc_main_header.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_int, P(CParams), ctypes.c_void_p,
+                                                                ctypes.c_size_t, P(ctypes.c_size_t)]
+        _lib.orc_encode_tile_parts.restype = ctypes.c_size_t
+        _lib.orc_encode_tile_parts.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 4 + [ctypes.c_int, P(CParams)] + \
+            [ctypes.c_uint32] * 4 + [ctypes.c_void_p, ctypes.c_size_t, P(ctypes.c_uint32)]
         _lib.orc_ht_encode_cblk.restype = ctypes.c_int
         _lib.orc_ht_encode_cblk.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_void_p, ctypes.c_uint32]
@@ -69,8 +80,17 @@ def lib():
     return _lib
 
 
+def set_threads(n):
+    """Worker threads for code-blocks / tiles (results do not depend on the count)."""
+    lib().orc_set_threads(int(n))
+
+
+def get_threads():
+    return int(lib().orc_get_threads())
+
+
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
-           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False):
+           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -84,6 +104,7 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
     if tiles:
         p.tile_w, p.tile_h = int(tiles[0]), int(tiles[1])
     p.tlm, p.plt = int(tlm), int(plt)
+    p.cod_format = 2 if jp2 else 0
     if layer_rate:
         p.nlayers = len(layer_rate)
         for i, r in enumerate(layer_rate):
@@ -119,6 +140,43 @@ def encode(img, prec, signed=False, **kw):
     if n == 0:
         raise RuntimeError("oracle encode failed")
     return out[:n].tobytes()
+
+
+def jp2_header(w, h, nc, prec, cs_len, signed=False):
+    """JP2 boxes in front of a codestream of cs_len bytes (file = header + codestream)."""
+    buf = np.empty(128, np.uint8)
+    n = lib().orc_jp2_header(w, h, nc, prec, int(signed), cs_len, buf.ctypes.data)
+    return buf[:n].tobytes()
+
+
+def main_header(w, h, nc, prec, signed=False, **kw):
+    """(main header bytes, TLM entry offset or 0) for assembling separately coded tile parts."""
+    p = params(**kw)
+    buf = np.empty(1 << 20, np.uint8)
+    tlm = ctypes.c_size_t()
+    n = lib().orc_main_header(w, h, nc, prec, int(signed), ctypes.byref(p), buf.ctypes.data, buf.size,
+                              ctypes.byref(tlm))
+    if n == 0:
+        raise RuntimeError("oracle main header failed")
+    return buf[:n].tobytes(), tlm.value
+
+
+def encode_tile_parts(slab, row0, image_hw, prec, tile_begin, tile_end, signed=False, **kw):
+    """Tile parts of tiles [tile_begin, tile_end) from a (C, rows, W) slab holding image rows
+    [row0, row0 + rows).  Returns (bytes, [Psot per tile])."""
+    a = _planes(slab)
+    c, rows, w = a.shape
+    H, W = image_hw
+    assert W == w
+    p = params(**kw)
+    cap = a.nbytes * 2 + (1 << 20)
+    out = np.empty(cap, np.uint8)
+    lens = (ctypes.c_uint32 * (tile_end - tile_begin))()
+    n = lib().orc_encode_tile_parts(a.ctypes.data, W, H, c, prec, int(signed), ctypes.byref(p), row0, rows,
+                                    tile_begin, tile_end, out.ctypes.data, cap, lens)
+    if n == 0:
+        raise RuntimeError("oracle tile-part encode failed")
+    return out[:n].tobytes(), list(lens)
 
 
 def decode(cs):

@@ -46,14 +46,16 @@ def test_every_declared_symbol_is_exported():
 def test_struct_layout_matches_header(tmp_path):
     src = tmp_path / "layout.c"
     src.write_text('#include "grok_amd.h"\n#include <stdio.h>\n#include <stddef.h>\n'
-                   'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(gk_cparameters), sizeof(gk_image_info),'
-                   ' sizeof(gk_timings), offsetof(gk_cparameters, write_comment), offsetof(gk_timings, dwt_bytes));'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(gk_cparameters), sizeof(gk_image_info),'
+                   ' sizeof(gk_timings), offsetof(gk_cparameters, write_comment), offsetof(gk_timings, dwt_bytes),'
+                   ' offsetof(gk_cparameters, cod_format), offsetof(gk_image_info, sample_bytes));'
                    'return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
     got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
     want = [ctypes.sizeof(G.CParameters), ctypes.sizeof(G.ImageInfo), ctypes.sizeof(G.Timings),
-            G.CParameters.write_comment.offset, G.Timings.dwt_bytes.offset]
+            G.CParameters.write_comment.offset, G.Timings.dwt_bytes.offset, G.CParameters.cod_format.offset,
+            G.ImageInfo.sample_bytes.offset]
     assert got == want
 
 
@@ -70,3 +72,7 @@ def test_default_params_mirror_grok_defaults():
     p = G.default_params()
     assert p.numresolution == 6 and p.cblockw_init == 64 and p.cblockh_init == 64
     assert p.numlayers == 1 and p.numgbits == 2 and p.irreversible == 0
+    # the C API default leaves the MCT off (memset, grok.cpp:409); the CLI switches it on for RGB
+    raw = G.CParameters()
+    G.load_library().gk_set_default_params(ctypes.byref(raw))
+    assert raw.mct == 0 and raw.cod_format == 0 and raw.numresolution == 6
