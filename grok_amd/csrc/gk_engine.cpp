@@ -2353,9 +2353,12 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         }
     const uint32_t nbr = (uint32_t)blk.size(), nbx = std::max(nbr, 1u);
     HIPCHK(hipEventRecord(ctx->ev[1], st));
-    // ---- stage compressed bytes on the device
+    // ---- stage compressed bytes on the device.  A host stream of which the selected blocks
+    // use a small part (window decode of a large file) is gathered on the host and only those
+    // bytes cross PCIe; otherwise the whole stream is copied and gathered on the device.
+    const bool host_gather = !cs_on_device && o * 2 < len;
     const uint8_t* dcs = cs;
-    if (!cs_on_device) {
+    if (!cs_on_device && !host_gather) {
         uint8_t* d = (uint8_t*)ctx->dout.get(len + 16);
         HIPCHK(hipMemcpyAsync(d, cs, len, hipMemcpyHostToDevice, st));
         dcs = d;
@@ -2379,6 +2382,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             }
     }
     uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 256);   // decoder window loads read up to 48 B past a block
+    if (host_gather) {
+        HIPCHK(hipStreamSynchronize(st));   // the pinned staging buffer may still feed an earlier copy
+        uint8_t* hst = (uint8_t*)ctx->hstage2.get(o + 256);
+        if (!P.p.ht()) memset(hst, 0xff, o);
+        for (size_t k = 0; k < seg.size(); k += 3) memcpy(hst + seg[k + 1], cs + seg[k], seg[k + 2]);
+        HIPCHK(hipMemcpyAsync(stg, hst, o, hipMemcpyHostToDevice, st));
+    } else {
     if (!P.p.ht()) HIPCHK(hipMemsetAsync(stg, 0xff, o, st));
     if (!seg.empty()) {
         uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8 + 8);
@@ -2386,6 +2396,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         uint64_t* ds = (uint64_t*)ctx->dseg.get(seg.size() * 8 + 8);
         HIPCHK(hipMemcpyAsync(ds, hs, seg.size() * 8, hipMemcpyHostToDevice, st));
         gk_launch_gather(st, dcs, stg, ds, (uint32_t)(seg.size() / 3));
+    }
     }
     const uint8_t* src_bytes = stg;
     if (prof)
