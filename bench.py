@@ -8,22 +8,32 @@ survey's seeded generator (grok_amd/synth.py, seed 10 + rank).
 One step = encode (image resident in HBM -> codestream resident in HBM) +
 decode (codestream in HBM -> image in HBM); host T2 (packet headers, rate
 allocation) runs inside the step.  value = pixels of all ranks / max-over-ranks
-wall time.  Single-tile configs shard as replicas (one image per GPU, no
+wall time.  Single-tile configs run as replicas (one image per GPU, no
 collective on the data path): scaling = "weak".
 
-The same JSON line carries auxiliary measurements of configs[2] ("C3":
-8192x8192 12-bit RGB, 9/7 + ICT, 3 quality layers -r 40,20,10) and configs[3]
-("C4": 16384x16384 16-bit mono, HTJ2K, 1024x1024 tiles, TLM + PLT).  With
-N > 1 ranks C4 is tile-sharded (strong scaling): each rank codes its tile rows
-from its own slab, rank 0 gathers the tile parts over RCCL and assembles the
-codestream; each rank then decodes its own tile parts.
+The same JSON line carries auxiliary measurements:
+  C3  configs[2]: 8192^2 12-bit RGB, 9/7 + ICT, 3 quality layers -r 40,20,10;
+  C4  configs[3]: 16384^2 16-bit mono, HTJ2K, 1024^2 tiles, TLM + PLT — with N > 1
+      ranks tile rows are sharded (strong scaling): each rank codes its tile rows,
+      rank 0 gathers the tile parts over RCCL, each rank decodes its own parts;
+  C5  configs[4]: decode-only random windows of a 32768^2 RGB8 tiled .jp2 (1024^2
+      tiles, TLM + PLT): the four SURVEY windows per step; with N > 1 ranks each
+      window's tile rows are split over the ranks and rank 0 gathers the rows;
+  C2_batch2: two C2 images in flight per GPU (serving throughput, never `value`).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3] [--no-aux]
+`cpu_baseline`: the oracle (CPU restatement, byte-exact with Grok by the fixtures)
+on bounded crops of C2 / C3 / C4, median of 3 runs, at 1 and N host threads.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4] [--no-aux]
+With --gpus N > 1 and no WORLD_SIZE in the environment the script starts N rank
+processes itself (torch.distributed.run) before touching the GPU.
 """
 import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +43,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
+METRIC = "Mpixels/s encode+decode, 8K RGB 5/3 lossless + 9/7 lossy, 1/2/4/8 GPU"
+# Grok 9.2.0 on the survey container (8 vCPU), enc+dec Mpix/s
+GROK_CPU = {"C2p_8t": 5.99, "C2p_1t": 1.11, "C3p_8t": 2.87, "C3p_1t": 0.93, "C4_8t": 51.9, "C4_1t": 19.3,
+            "C5_w16k_8t": 12.8}
 
 CONFIGS = {
     "C2": dict(size=8192, comps=3, bits=8, seed=10, params=dict(),
@@ -43,7 +57,13 @@ CONFIGS = {
     "C4": dict(size=16384, comps=1, bits=16, seed=20,
                params=dict(cblk_sty=0x40, tiles=(1024, 1024), tlm=True, plt=True),
                desc="16384x16384 16-bit mono, HTJ2K, 5/3 lossless, 1024x1024 tiles, TLM + PLT (-M 64 -t 1024,1024 -X -L)"),
+    "C5": dict(size=32768, comps=3, bits=8, seed=30, params=dict(tiles=(1024, 1024), tlm=True, plt=True, jp2=True),
+               desc="decode-only random windows of a 32768x32768 8-bit RGB tiled .jp2 (5/3, 1024x1024 tiles, TLM + "
+                    "PLT; -t 1024,1024 -X -L): windows 0,0,1024,1024 / 12345,23456,16441,27552 / "
+                    "30000,30000,32768,32768 / 8000,8000,24384,24384, decoded to u8 planes in HBM"),
 }
+C5_WINDOWS = [(0, 0, 1024, 1024), (12345, 23456, 16441, 27552), (30000, 30000, 32768, 32768),
+              (8000, 8000, 24384, 24384)]
 
 
 def parse():
@@ -52,51 +72,100 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size", type=int, default=0, help="override the config's image side")
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
-    ap.add_argument("--no-aux", action="store_true", help="skip the auxiliary C3 measurement")
+    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4"])
+    ap.add_argument("--no-aux", action="store_true", help="skip the auxiliary C3/C4/C5/batch measurements")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 window-decode measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=2048, help="side of the CPU-baseline crop")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="N for the N-thread CPU baseline (0: the host share)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group / timing plumbing only (CPU, gloo, no engine): for tests")
     return ap.parse_args()
 
 
-def cpu_baseline(img, bits, side, params):
-    """The oracle (CPU restatement, byte-exact with Grok), one thread, on a bounded crop."""
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args):
+    """Start --gpus rank processes (one per GPU) with torch.distributed.run and return its
+    exit code.  Called before this process touches the GPU; the ranks find WORLD_SIZE set."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+def host_threads(args):
+    if args.cpu_threads:
+        return args.cpu_threads
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count() or 1, 16))
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(nthreads):
+    """The oracle (CPU restatement, byte-exact with Grok by the committed fixtures) timed on
+    bounded crops of the same synthetic images: encode + decode, median of 3 runs, at 1 and
+    nthreads threads (code-blocks / tiles on worker threads)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    crop = np.ascontiguousarray(img[:, :side, :side]).astype(np.int32)
-    kw = {}
-    if params.get("irreversible"):
-        kw = dict(irreversible=True, layer_rate=params.get("layer_rate"))
-    t0 = time.perf_counter()
-    cs = O.encode(crop, bits, **kw)
-    t1 = time.perf_counter()
-    dec, _ = O.decode(cs)
-    t2 = time.perf_counter()
-    if not kw:
-        assert (dec == crop).all()
-    mpix = side * side / 1e6
-    return {"value": round(mpix / (t2 - t0), 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": "%dx%d crop of the same image, oracle/j2k_oracle.cpp encode %.2fs + decode %.2fs, 1 thread" % (
-                side, side, t1 - t0, t2 - t1)}
+    from grok_amd.synth import synth_image
+    cases = {
+        "C2": (synth_image(2048, 2048, 3, 8, 10).astype(np.int32), 8, dict(), "2048x2048 crop of C2 (RGB8 5/3)"),
+        "C3": (synth_image(1024, 1024, 3, 12, 11).astype(np.int32), 12,
+               dict(irreversible=True, layer_rate=[40.0, 20.0, 10.0]), "1024x1024 crop of C3 (RGB12 9/7 -r 40,20,10)"),
+        "C4": (synth_image(2048, 2048, 1, 16, 20).astype(np.int32), 16,
+               dict(cblk_sty=0x40, tiles=(1024, 1024), tlm=True, plt=True), "2048x2048 crop of C4 (mono16 HT tiles)"),
+    }
+    per = {}
+    for name, (img, bits, kw, desc) in cases.items():
+        c, h, w = img.shape
+        per[name] = {"sample": desc}
+        for th in sorted({1, nthreads}):
+            O.set_threads(th)
+            runs = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                cs = O.encode(img, bits, **kw)
+                dec, _ = O.decode(cs)
+                runs.append(time.perf_counter() - t0)
+            if not kw.get("irreversible"):
+                assert (dec == img).all()
+            per[name]["%dt" % th] = round(h * w / 1e6 / float(np.median(runs)), 4)
+    O.set_threads(1)
+    return {"value": per["C2"]["%dt" % nthreads], "unit": "Mpixels/s", "cores": nthreads, "cores_list": sorted({1, nthreads}),
+            "kind": "port",
+            "sample": "oracle/j2k_oracle.cpp encode+decode, median of 3, on crops: C2 2048^2, C3 1024^2, C4 2048^2; "
+                      "value = C2 crop at %d threads" % nthreads,
+            "per_config": per,
+            "grok_container_8vcpu": {"note": "BASELINE.md section 2, Grok 9.2.0 CLI on the survey container (8 vCPU), "
+                                             "enc+dec Mpix/s; C2p/C3p = -c [256,256] variants (Grok cannot decode the "
+                                             "single-precinct 8K streams)", **GROK_CPU}}
 
 
 def pmc_traffic(kernels):
     """HBM bytes per launch of `kernels` from the newest committed PMC summary
     (profiles/*_pmc.json, written by tools/pmc_summary.py from rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes of this benchmark; FETCH_SIZE doubled per
-    MI355X_MICROARCH.md's gfx950 note).  None if no summary exists."""
+    MI355X_MICROARCH.md's gfx950 note).  (None, None) if no summary exists."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     if not files:
-        return None
+        return None, None
     d = json.load(open(files[-1]))
     tot = 0.0
     for k in kernels:
         if k not in d:
-            return None
+            return None, None
         tot += d[k]["hbm_bytes_per_launch"]
-    return tot
+    return tot, os.path.basename(files[-1])
 
 
+# ----------------------------------------------------------------------------- runners
 class Runner:
     def __init__(self, name, size, rank, device):
         import torch
@@ -112,6 +181,7 @@ class Runner:
         self.eng = G.Engine(device.index or 0)
         self.params = G.default_params(**cfg["params"])
         self.n = 0
+        self.pixels = size * size
 
     def step(self):
         self.n = self.eng.encode(self.x, self.cfg["bits"], params=self.params, out=self.out)
@@ -135,6 +205,9 @@ class Runner:
                 raise SystemExit("9/7 round trip PSNR %.2f dB too low (%s)" % (psnr, self.name))
             return psnr
         return None
+
+    def close(self):
+        self.eng.close()
 
 
 class BatchRunner:
@@ -169,9 +242,10 @@ class BatchRunner:
 
 class ShardRunner:
     """C4 on N ranks: tile rows split across ranks (grok_amd/shard.py).  One step =
-    every rank encodes its tiles from its slab (HBM -> tile parts in HBM), rank 0
-    gathers the tile parts (RCCL) and assembles the codestream in HBM, every rank
-    decodes its own tile parts back into its slab."""
+    every rank encodes its tiles from its slab (HBM -> tile parts in HBM); the tile-part
+    lengths are all-gathered; rank 0 gathers the payloads (RCCL) and assembles the
+    codestream in HBM under the main header with its TLM filled; every rank decodes its
+    own tile parts (main header with a TLM listing just those parts) back into its slab."""
 
     def __init__(self, name, size, rank, world, device, dist):
         import torch
@@ -187,39 +261,56 @@ class ShardRunner:
         self.tb, self.te, j0, j1 = shard.rank_tiles(self.ntx, self.nty, rank, world)
         if self.te <= self.tb:
             raise SystemExit("C4 sharding needs at least one tile row per rank")
+        self.maxt = max(shard.rank_tiles(self.ntx, self.nty, r, world)[1] - shard.rank_tiles(self.ntx, self.nty, r, world)[0]
+                        for r in range(world))
         self.y0, self.y1 = j0 * th, min(size, j1 * th)
         slab = synth_slab(self.y0, self.y1, size, size, cfg["comps"], cfg["bits"], cfg["seed"])
         self.x = torch.from_numpy(slab.astype(np.int32)).to(device).contiguous()
         self.y = torch.empty_like(self.x)
         self.eng = G.Engine(device.index or 0)
         self.params = G.default_params(**cfg["params"])
-        hdr, self.tlm, _ = self.eng.main_header((cfg["comps"], size, size), cfg["bits"], params=self.params)
-        self.hdr = torch.frombuffer(bytearray(hdr), dtype=torch.uint8).to(device)
+        self.hdr, self.tlm, _ = self.eng.main_header((cfg["comps"], size, size), cfg["bits"], params=self.params)
         self.eoc = torch.tensor([0xFF, 0xD9], dtype=torch.uint8, device=device)
         self.parts = torch.empty(self.x.numel() * 4 + (1 << 22), dtype=torch.uint8, device=device)
         self.n = 0
         self.cs = None
+        self.pixels = size * size
 
     def step(self):
+        import struct
         import torch
+        from grok_amd import shard
         n, lens = self.eng.encode_tiles(self.x, self.cfg["bits"], self.tb, self.te, image_hw=(self.size, self.size),
                                         row0=self.y0, params=self.params, out=self.parts)
         te = self.eng.timings()
-        # gather tile parts to rank 0 (lengths, then padded payload) over RCCL
-        ln = torch.tensor([n], dtype=torch.int64, device=self.device)
+        # tile-part lengths of every rank (padded to the largest tile count), then payloads to rank 0
+        ln = torch.zeros(self.maxt + 1, dtype=torch.int64, device=self.device)
+        ln[0] = n
+        ln[1:1 + len(lens)] = torch.tensor(lens, dtype=torch.int64)
         lns = [torch.zeros_like(ln) for _ in range(self.world)]
         self.dist.all_gather(lns, ln)
-        mx = int(max(int(v.item()) for v in lns))
+        lns = [v.cpu().tolist() for v in lns]
+        mx = int(max(v[0] for v in lns))
         payload = self.parts[:mx]
         if self.rank == 0:
             bufs = [torch.empty(mx, dtype=torch.uint8, device=self.device) for _ in range(self.world)]
             self.dist.gather(payload, bufs, dst=0)
-            self.cs = torch.cat([self.hdr] + [b[:int(k.item())] for b, k in zip(bufs, lns)] + [self.eoc])
+            h = bytearray(self.hdr)
+            if self.tlm:
+                for r in range(self.world):
+                    rtb, rte, _, _ = shard.rank_tiles(self.ntx, self.nty, r, self.world)
+                    for k in range(rte - rtb):
+                        t = rtb + k
+                        h[self.tlm + 6 * t:self.tlm + 6 * t + 6] = struct.pack(">HI", t, int(lns[r][1 + k]))
+            hd = torch.frombuffer(h, dtype=torch.uint8).to(self.device)
+            self.cs = torch.cat([hd] + [b[:int(v[0])] for b, v in zip(bufs, lns)] + [self.eoc])
             self.n = int(self.cs.numel())
         else:
             self.dist.gather(payload, None, dst=0)
-        # each rank decodes its own tile parts (main header + parts + EOC) into its slab
-        sub = torch.cat([self.hdr, self.parts[:n], self.eoc])
+        # each rank decodes its own tile parts: main header with a TLM of just those parts
+        sub_hdr = shard.retlm(self.hdr, [(self.tb + k, int(v)) for k, v in enumerate(lens)])
+        sh = torch.frombuffer(bytearray(sub_hdr), dtype=torch.uint8).to(self.device)
+        sub = torch.cat([sh, self.parts[:n], self.eoc])
         self.eng.decode(sub, length=int(sub.numel()), out=self.y, row0=self.y0)
         td = self.eng.timings()
         return te, td
@@ -230,61 +321,198 @@ class ShardRunner:
         torch.cuda.synchronize()
         if not torch.equal(self.x, self.y):
             raise SystemExit("sharded lossless round trip FAILED (%s)" % self.name)
+        if self.rank == 0 and self.tlm:
+            # the assembled stream is a valid codestream: decode a few tiles from it through its TLM
+            probe = torch.empty((self.x.shape[0], 64, 64), dtype=torch.int32, device=self.device)
+            self.eng.decode_window(self.cs, (0, 0, 64, 64), length=self.n, out=probe)
+            if not torch.equal(probe, self.x[:, :64, :64]):
+                raise SystemExit("assembled sharded codestream does not decode (%s)" % self.name)
         return None
 
+    def close(self):
+        self.eng.close()
 
-def timed(r, steps, warmup, world, dist, device):
+
+class C5Runner:
+    """C5: decode-only random windows of a 32768^2 RGB8 tiled .jp2 held in HBM.  Rank 0
+    builds the file on its GPU from tile-row slabs (grok_amd.bigimage) and broadcasts it
+    (a shared file); one step decodes the four SURVEY windows.  With N ranks the tile rows
+    of each window are split into contiguous ranges, each rank decodes its band of the
+    window (TLM finds the tiles, PLT the packets, out-of-reach code-blocks are skipped)
+    into u8 planes, and rank 0 gathers the bands."""
+
+    def __init__(self, rank, world, device, dist):
+        import torch
+        import grok_amd as G
+        from grok_amd import bigimage
+        cfg = CONFIGS["C5"]
+        self.cfg, self.rank, self.world, self.device, self.dist = cfg, rank, world, device, dist
+        S = cfg["size"]
+        self.eng = G.Engine(device.index or 0)
+        p = G.default_params(**cfg["params"])
+        self.crops = None
+        t0 = time.perf_counter()
+        if rank == 0:
+            it = bigimage.slabs(S, S, cfg["comps"], cfg["bits"], cfg["seed"], 1024, threads=16)
+            crops = {k: w for k, w in enumerate(C5_WINDOWS)}
+            self.file, self.n, self.crops = bigimage.encode_tiled(self.eng, (cfg["comps"], S, S), cfg["bits"], p, it,
+                                                                  device, crops=crops)
+        self.build_s = time.perf_counter() - t0
+        if world > 1:
+            n = torch.tensor([self.n if rank == 0 else 0], dtype=torch.int64, device=device)
+            dist.broadcast(n, 0)
+            if rank != 0:
+                self.n = int(n.item())
+                self.file = torch.empty(self.n, dtype=torch.uint8, device=device)
+            dist.broadcast(self.file[:self.n], 0)
+        self.pixels = sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in C5_WINDOWS)
+        self.outs = [torch.empty((3, y1 - y0, x1 - x0), dtype=torch.uint8, device=device)
+                     for x0, y0, x1, y1 in C5_WINDOWS]
+        self.bands = [self._band(w) for w in C5_WINDOWS]
+
+    def _band(self, win):
+        x0, y0, x1, y1 = win
+        j0, j1 = y0 // 1024, (y1 - 1) // 1024 + 1
+        per, extra = divmod(j1 - j0, self.world)
+        rows = []
+        for r in range(self.world):
+            a = j0 + r * per + min(r, extra)
+            b = a + per + (1 if r < extra else 0)
+            rows.append((max(y0, a * 1024), min(y1, b * 1024)) if b > a else (y0, y0))
+        return rows
+
+    def step(self):
+        import torch
+        acc = {}
+        for k, (x0, y0, x1, y1) in enumerate(C5_WINDOWS):
+            ry0, ry1 = self.bands[k][self.rank]
+            out = self.outs[k]
+            if ry1 > ry0:
+                self.eng.decode_window(self.file, (x0, ry0, x1, ry1), length=self.n, out=out[:, ry0 - y0:ry1 - y0])
+                t = self.eng.timings()
+                for f in ("t1_ms", "dwt_ms", "mct_ms", "t2_ms", "total_ms"):
+                    acc["dec_" + f] = acc.get("dec_" + f, 0.0) + float(getattr(t, f))
+            if self.world > 1:
+                # rank 0 gathers the window's row bands (padded to the tallest band)
+                hmax = max(b - a for a, b in self.bands[k])
+                pad = torch.zeros((3, hmax, x1 - x0), dtype=torch.uint8, device=self.device)
+                if ry1 > ry0:
+                    pad[:, :ry1 - ry0] = out[:, ry0 - y0:ry1 - y0]
+                if self.rank == 0:
+                    bufs = [torch.empty_like(pad) for _ in range(self.world)]
+                    self.dist.gather(pad, bufs, dst=0)
+                    for r, (a, b) in enumerate(self.bands[k]):
+                        if b > a and r:
+                            out[:, a - y0:b - y0] = bufs[r][:, :b - a]
+                else:
+                    self.dist.gather(pad, None, dst=0)
+        return acc
+
+    def check(self):
+        import torch
+        self.step()
+        torch.cuda.synchronize()
+        if self.rank == 0:
+            for k, o in enumerate(self.outs):
+                if not np.array_equal(o.cpu().numpy(), self.crops[k]):
+                    raise SystemExit("C5 window %s decode differs from the source" % (C5_WINDOWS[k],))
+
+    def close(self):
+        self.eng.close()
+
+
+def timed(r, steps, warmup, world, dist, device, sync=True):
     import torch
     for _ in range(warmup):
         r.step()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    if sync:
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     acc = {}
     for _ in range(steps):
-        te, td = r.step()
+        out = r.step()
+        if isinstance(out, dict):
+            for k, v in out.items():
+                acc[k] = acc.get(k, 0.0) + v
+            continue
+        te, td = out
         for pre, t in (("enc", te), ("dec", td)):
             for f, _ in t._fields_:
                 acc[pre + "_" + f] = acc.get(pre + "_" + f, 0.0) + float(getattr(t, f))
-    torch.cuda.synchronize()
+    if sync:
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device=device)
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el, {k: v / steps for k, v in acc.items()}
 
 
+class DryRunner:
+    """--dry-run: a fixed host computation per step, no engine (launcher/timing plumbing)."""
+    pixels = 1 << 20
+
+    def step(self):
+        a = np.arange(1 << 16, dtype=np.float64)
+        return {"work": float(np.sqrt(a).sum()) * 0.0}
+
+
+def dry_main(args, world, rank, dist):
+    import torch
+    el, _ = timed(DryRunner(), args.steps, args.warmup, world, dist, torch.device("cpu"), sync=False)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "value": round(DryRunner.pixels / 1e6 * world * args.steps / el, 3),
+                          "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el * 1000.0 / args.steps, 3), "higher_is_better": True,
+                          "scaling": "weak"}), flush=True)
+
+
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch(args))   # this process has not touched the GPU
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group("gloo" if args.dry_run else "nccl")
+    if args.dry_run:
+        dry_main(args, world, rank, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
 
-    r = Runner(args.config, args.size, rank, device)
+    r = Runner(args.config, args.size, rank, device) if args.config != "C4" or world == 1 else \
+        ShardRunner("C4", args.size, rank, world, device, dist)
     S = r.size
     r.check()
     el, m = timed(r, args.steps, args.warmup, world, dist, device)
     ms = el * 1000.0 / args.steps
     samples = S * S * r.cfg["comps"]
-    value = S * S / 1e6 * world * args.steps / el
+    per_rank = world if isinstance(r, Runner) else 1   # replicas: every rank codes its own image
+    value = S * S / 1e6 * per_rank * args.steps / el
+    codestream_bytes = int(r.n)
+    r.close()
+    del r
+    torch.cuda.empty_cache()
 
     aux = None
     if not args.no_aux and args.config == "C2":
         aux = {}
-        r.eng.close()
-        del r.x, r.y, r.out
-        torch.cuda.empty_cache()
         r3 = Runner("C3", args.size, rank, device)
         psnr = r3.check()
         el3, m3 = timed(r3, 2, 1, world, dist, device)
@@ -293,7 +521,7 @@ def main():
                      "unit": "Mpixels/s", "ms_per_step": round(el3 * 500.0, 3), "psnr_db": round(psnr, 3),
                      "codestream_bytes": int(r3.n), "parallelism": "replicas x%d" % world,
                      "stages_ms": {k: round(v, 3) for k, v in m3.items() if k.endswith("_ms") and v > 0}}
-        r3.eng.close()
+        r3.close()
         del r3
         torch.cuda.empty_cache()
         # C2 with two images in flight per GPU (throughput of overlapped independent jobs)
@@ -321,7 +549,25 @@ def main():
                      "scaling": "strong",
                      "stages_ms": {k: round(v, 3) for k, v in m4.items() if k.endswith("_ms") and v > 0},
                      "t1_blocks": int(m4.get("enc_t1_blocks", 0))}
-        r4.eng.close()
+        r4.close()
+        del r4
+        torch.cuda.empty_cache()
+        if not args.no_c5:
+            r5 = C5Runner(rank, world, device, dist)
+            r5.check()
+            el5, m5 = timed(r5, 3, 1, world, dist, device)
+            aux["C5"] = {"config": "C5: " + CONFIGS["C5"]["desc"], "value": round(r5.pixels / 1e6 * 3 / el5, 3),
+                         "unit": "Mpixels/s (window output samples)", "ms_per_step": round(el5 * 1000.0 / 3, 3),
+                         "window_mpix_per_step": round(r5.pixels / 1e6, 3), "file_bytes": int(r5.n),
+                         "parallelism": ("each window's tile rows split over %d ranks, RCCL gather of the rows" % world)
+                         if world > 1 else "1 GPU",
+                         "scaling": "strong", "build_s": round(r5.build_s, 1),
+                         "stages_ms_rank0": {k: round(v, 3) for k, v in m5.items() if v > 0},
+                         "vs_grok_8vcpu_w16k": "Grok -H 8 decodes the 16384^2 window at %.1f Mpix/s (BASELINE.md)"
+                                               % GROK_CPU["C5_w16k_8t"]}
+            r5.close()
+            del r5
+            torch.cuda.empty_cache()
 
     if rank == 0:
         # dominant kernel: the T1 stage with the largest average duration, measured with HIP
@@ -337,20 +583,26 @@ def main():
         dom = max(stages, key=lambda k: stages[k][0])
         t_ms, nbytes, kern = stages[dom]
         achieved = nbytes / 1e9 / (t_ms / 1e3)
-        traffic = pmc_traffic(kern)
+        traffic, traffic_src = pmc_traffic(kern)
         dwt_gbs = (m["enc_dwt_bytes"] + m["dec_dwt_bytes"]) / 1e9 / ((m["enc_dwt_ms"] + m["dec_dwt_ms"]) / 1e3)
         res = {
-            "metric": "Mpixels/s encode+decode, 8K RGB 5/3 lossless + 9/7 lossy, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": round(value, 3), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int32",
-            "data": "synthetic (seeded survey generator grok_amd/synth.py, seed %d+rank)" % r.cfg["seed"],
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak" if args.config != "C4" else "strong",
+            "vs_baseline": round(value / GROK_CPU["C2p_8t"], 2) if args.config == "C2" else None,
+            "vs_baseline_ref": "Grok 9.2.0 CPU enc+dec of C2' (-c [256,256]) on 8 vCPU, 5.99 Mpix/s (BASELINE.md "
+                               "section 2; no published GPU number exists)",
+            "dtype": "int32",
+            "data": "synthetic (seeded survey generator grok_amd/synth.py, seed %d+rank)" % CONFIGS[args.config]["seed"],
             "config": {"workload": "%s: %s; encode+decode, image and codestream resident in HBM" % (
-                args.config, r.cfg["desc"]), "parallelism": "replicas x%d (one image per GPU)" % world,
-                "codestream_bytes": int(r.n)},
+                args.config, CONFIGS[args.config]["desc"]),
+                "parallelism": "replicas x%d (one image per GPU)" % world if args.config != "C4" or world == 1 else
+                "C4 tile rows sharded over %d ranks" % world,
+                "codestream_bytes": codestream_bytes},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None if traffic is None else round(traffic),
+                         "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src,
                          "bytes_per_launch": round(nbytes), "avg_ms": round(t_ms, 3),
                          "note": "T1 is a serial MQ chain per code-block; bytes = compressed bytes + 4 B/sample"},
             "dwt_roofline": {"achieved": round(dwt_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -363,10 +615,8 @@ def main():
         if aux:
             res["aux"] = aux
         if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(r.img, r.cfg["bits"], min(args.cpu_sample, S), r.cfg["params"])
+            res["cpu_baseline"] = cpu_baseline(host_threads(args))
         print(json.dumps(res), flush=True)
-    if aux is None:
-        r.eng.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -342,15 +342,20 @@ class Engine:
         info = self.read_header(cs, length)
         x0, y0, x1, y1 = window
         c, h, w = info.numcomps, y1 - y0, x1 - x0
-        strides = (ctypes.c_uint32 * c)(*([w] * c))
         if out is not None:
+            # any (C, h, w) view with unit column stride (e.g. a row band of a larger window)
+            assert tuple(out.shape) == (c, h, w) and out.stride(2) == 1
             base, res, out_dev = out.data_ptr(), out, 1
             sample_bytes = _sample_bytes(out)
+            es = sample_bytes or 4
+            cstride, rstride = out.stride(0), out.stride(1)
         else:
             res = np.empty((c, h, w), _np_sample_dtype(sample_bytes, info))
             base, out_dev = res.ctypes.data, 0
-        es = sample_bytes or 4
-        ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * es for k in range(c)])
+            es = sample_bytes or 4
+            cstride, rstride = h * w, w
+        strides = (ctypes.c_uint32 * c)(*([rstride] * c))
+        ptrs = (ctypes.c_void_p * c)(*[base + k * cstride * es for k in range(c)])
         if on_dev:
             rc = self.lib.gk_decode_window(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, x0, y0, x1, y1, ptrs,
                                            strides, sample_bytes, out_dev)

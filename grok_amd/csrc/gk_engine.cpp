@@ -1978,16 +1978,21 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     // tile parts: SOT (Isot, Psot, TPsot, TNsot), tile-part header markers (PLT, ...), SOD, packets
     // (CodeStreamDecompress SOT/SOD handlers; TLM and PLT are only needed for random access)
     size_t pos = Hd.first_sot;
-    if (!Hd.tlm.empty() && S.dev) {
+    bool tlm_ok = !Hd.tlm.empty() && S.dev;
+    if (tlm_ok) {
         // device-resident stream with TLM: tile-part positions without walking the SOT chain;
-        // the tile-part headers are fetched in one batch by the decoder (data = 0 until then)
+        // the tile-part headers are fetched in one batch by the decoder (data = 0 until then).
+        // A TLM that does not fit the stream (e.g. a full-image TLM in front of a subset of
+        // the tile parts) is ignored and the SOT chain is walked instead.
         for (auto& tl : Hd.tlm) {
             const size_t end = pos + tl.second;
-            if (tl.second < 14 || end > S.len) throw GkError("corrupt TLM");
+            if (tl.second < 14 || end > S.len) { tlm_ok = false; break; }
             Hd.parts.push_back({tl.first, pos, 0, end, {}});
             pos = end;
         }
-    } else {
+        if (!tlm_ok) { Hd.parts.clear(); pos = Hd.first_sot; }
+    }
+    if (!tlm_ok) {
         while (pos + 12 <= S.len && S.be16(pos) == 0xff90) {
             const uint32_t isot = S.be16(pos + 4), psot = S.be32(pos + 6);
             const size_t end = psot ? pos + psot : (S.len >= 2 ? S.len - 2 : S.len);

@@ -5,8 +5,9 @@ Encode: every rank codes its tiles (gk_encode_tiles) into tile parts; rank 0
 gathers (lengths, then payload) and writes main header + TLM + tile parts in
 tile order + EOC — the codestream is byte-identical to a one-GPU encode.
 Decode: rank 0 splits the codestream into tile parts (SOT/Psot walk, what TLM
-records), each rank receives the main header + its tile parts and decodes only
-those tile rows; rank 0 gathers the decoded rows.
+records) and scatters to each rank the main header (TLM rewritten to that rank's
+parts) + its tile parts; each rank decodes only those tile rows; rank 0 gathers
+the decoded row slabs as tensors.
 
 The collectives are plain torch.distributed calls (RCCL on MI355X, gloo on CPU
 for the world-size-2 tests); the codestream logic here is pure Python.
@@ -123,31 +124,93 @@ def encode_sharded(dist, rank, world, encode_tiles, main_header, ntx, nty, devic
     return assemble(header, tlm, parts)
 
 
-def decode_sharded(dist, rank, world, cs, decode, ntx, nty, th):
-    """Rank 0 holds the codestream; every rank decodes header + its tile parts with
-    decode(substream) -> (C, H, W) array (rows of other tiles untouched / zero).
-    Returns the full decoded image on rank 0 (rows gathered per rank)."""
+def retlm(header, entries):
+    """The main header with its TLM marker rewritten to list exactly `entries` [(tile, Psot)]
+    (Ttlm u16, Ptlm u32: Stlm = 0x60, TileLengthMarkers::writeBegin).  A rank's sub-stream
+    (main header + its own tile parts) then carries a TLM that matches it.  Headers without
+    TLM are returned unchanged."""
+    h = bytes(header)
+    i = 2
+    while i + 4 <= len(h):
+        m, L = struct.unpack(">HH", h[i:i + 4])
+        if m == TLM:
+            seg = struct.pack(">HHBB", TLM, 4 + 6 * len(entries), 0, 0x60) + \
+                b"".join(struct.pack(">HI", t, n) for t, n in entries)
+            return h[:i] + seg + h[i + 2 + L:]
+        i += 2 + L
+    return h
+
+
+def _scatter_bytes(dist, rank, world, payloads, device):
+    """Rank 0's per-rank byte strings to every rank (lengths, then payloads padded to the
+    longest) with two scatter collectives.  Returns this rank's bytes as a uint8 tensor."""
     import torch
-    objs = [None]
+    n = torch.zeros(1, dtype=torch.int64, device=device)
+    if rank == 0:
+        ns = [torch.tensor([len(p)], dtype=torch.int64, device=device) for p in payloads]
+        dist.scatter(n, ns, src=0)
+    else:
+        dist.scatter(n, None, src=0)
+    mx = torch.tensor([int(n.item())], dtype=torch.int64, device=device)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    mx = max(int(mx.item()), 1)
+    buf = torch.empty(mx, dtype=torch.uint8, device=device)
+    if rank == 0:
+        srcs = []
+        for p in payloads:
+            t = torch.zeros(mx, dtype=torch.uint8)
+            if len(p):
+                t[:len(p)] = torch.frombuffer(bytearray(p), dtype=torch.uint8)
+            srcs.append(t.to(device))
+        dist.scatter(buf, srcs, src=0)
+    else:
+        dist.scatter(buf, None, src=0)
+    return buf[:int(n.item())]
+
+
+def decode_sharded(dist, rank, world, cs, decode, ntx, nty, th, shape, device=None):
+    """Rank 0 holds the codestream (host bytes).  It cuts the tile parts (SOT walk) and
+    scatters to every rank its main header (TLM rewritten to its own parts) + tile parts +
+    EOC; each rank decodes its tile rows with decode(sub_tensor, y0, y1) -> (C, y1-y0, W)
+    tensor; rank 0 gathers the row slabs (padded to the tallest) and returns the (C, H, W)
+    image.  Every transfer is a torch.distributed collective on uint8 / sample tensors
+    (RCCL over xGMI with device tensors; gloo with CPU tensors in the tests)."""
+    import torch
+    C, H, W = shape
+    device = device or torch.device("cpu")
+    subs = None
     if rank == 0:
         header, parts = split_codestream(cs)
-        per_rank = []
+        pl = dict(parts)
+        subs = []
         for r in range(world):
             tb, te, _, _ = rank_tiles(ntx, nty, r, world)
-            per_rank.append(header + b"".join(b for t, b in parts if tb <= t < te) + struct.pack(">H", EOC))
-        objs = [per_rank]
-    dist.broadcast_object_list(objs, src=0)
-    tb, te, _, _ = rank_tiles(ntx, nty, rank, world)
-    img = decode(objs[0][rank]) if te > tb else None   # ranks without tiles stay idle
-    out = [None] * world if rank == 0 else None
-    dist.gather_object(img, out, dst=0)
-    if rank != 0:
-        return None
-    full = np.zeros_like(next(o for o in out if o is not None))
-    for r in range(world):
-        _, _, j0, j1 = rank_tiles(ntx, nty, r, world)
-        if j1 <= j0:
-            continue
-        y0, y1 = j0 * th, min(full.shape[1], j1 * th)
-        full[:, y0:y1] = out[r][:, y0:y1]
-    return full
+            mine = [(t, pl[t]) for t in range(tb, te) if t in pl]
+            subs.append(retlm(header, [(t, len(b)) for t, b in mine]) + b"".join(b for _, b in mine) +
+                        struct.pack(">H", EOC) if mine else b"")
+    sub = _scatter_bytes(dist, rank, world, subs, device)
+    _, _, j0, j1 = rank_tiles(ntx, nty, rank, world)
+    y0, y1 = min(H, j0 * th), min(H, j1 * th)
+    rows_max = max(min(H, rank_tiles(ntx, nty, r, world)[3] * th) - min(H, rank_tiles(ntx, nty, r, world)[2] * th)
+                   for r in range(world))
+    slab = None
+    if y1 > y0:
+        slab = decode(sub, y0, y1)
+        if not isinstance(slab, torch.Tensor):
+            slab = torch.from_numpy(np.ascontiguousarray(slab))
+    dtype = slab.dtype if slab is not None else torch.int32
+    pad = torch.zeros((C, max(rows_max, 1), W), dtype=dtype, device=device)
+    if slab is not None:
+        pad[:, :y1 - y0] = slab.to(device)
+    if rank == 0:
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.gather(pad, bufs, dst=0)
+        full = torch.empty((C, H, W), dtype=dtype, device=device)
+        for r in range(world):
+            _, _, a, b = rank_tiles(ntx, nty, r, world)
+            ry0, ry1 = min(H, a * th), min(H, b * th)
+            if ry1 > ry0:
+                full[:, ry0:ry1] = bufs[r][:, :ry1 - ry0]
+        return full
+    dist.gather(pad, None, dst=0)
+    return None

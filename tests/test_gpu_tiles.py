@@ -176,7 +176,14 @@ def _gpu_shard_worker(rank, world, port, q):
             return hd, tlm
 
         cs = shard.encode_sharded(dist, rank, world, enc, hdr, ntx, nty)
-        dec = shard.decode_sharded(dist, rank, world, cs, lambda sub: e.decode(sub), ntx, nty, 64)
+        def dec_rows(sub, y0, y1):   # the rank's sub-stream (header with its own TLM + parts) into its slab
+            d = sub.cuda()
+            out = torch.empty((img.shape[0], y1 - y0, w), dtype=torch.int32, device="cuda")
+            e.decode(d, length=d.numel(), out=out, row0=y0)
+            return out.cpu()
+
+        dec = shard.decode_sharded(dist, rank, world, cs, dec_rows, ntx, nty, 64, img.shape)
+        dec = dec.numpy() if dec is not None else None
         if rank == 0:
             q.put((cs == O.encode(img, 16, **kw), bool((dec == img).all())))
         e.close()

@@ -60,10 +60,14 @@ def _worker(rank, world, port, case, q):
             return header, tlm
 
         cs = shard.encode_sharded(dist, rank, world, encode_tiles, main_header, ntx, nty)
-        dec = shard.decode_sharded(dist, rank, world, full if rank == 0 else None,
-                                   lambda sub: O.decode(sub)[0], ntx, nty, th)
+
+        def dec_rows(sub, y0, y1):   # stand-in for gk_decode of the rank's sub-stream into its slab
+            d, _ = O.decode(sub.numpy().tobytes())
+            return d[:, y0:y1]
+
+        dec = shard.decode_sharded(dist, rank, world, full if rank == 0 else None, dec_rows, ntx, nty, th, (c, h, w))
         if rank == 0:
-            q.put((cs == full, bool((dec == img).all())))
+            q.put((cs == full, bool((dec.numpy() == img).all())))
     finally:
         dist.destroy_process_group()
 
@@ -91,6 +95,21 @@ def test_rank_tiles_cover_grid():
             assert te - tb == (j1 - j0) * ntx
             seen += list(range(tb, te))
         assert seen == list(range(ntx * nty))
+
+
+def test_retlm_lists_only_given_parts():
+    rng = np.random.default_rng(4)
+    img = rng.integers(0, 256, size=(1, 96, 160)).astype(np.int32)
+    cs = O.encode(img, 8, tiles=(32, 32), tlm=True, plt=True)
+    header, parts = shard.split_codestream(cs)
+    mine = parts[5:10]
+    sub = shard.retlm(header, [(t, len(b)) for t, b in mine]) + b"".join(b for _, b in mine) + b"\xff\xd9"
+    d, _ = O.decode(sub)
+    np.testing.assert_array_equal(d[:, 32:64], img[:, 32:64])
+    i = sub.index(b"\xff\x55")
+    assert int.from_bytes(sub[i + 2:i + 4], "big") == 4 + 6 * 5
+    plain = shard.split_codestream(O.encode(img, 8, tiles=(32, 32)))[0]   # no TLM: header unchanged
+    assert shard.retlm(plain, [(0, 10)]) == plain
 
 
 def test_assemble_roundtrip():
