@@ -79,3 +79,25 @@ def test_fullsize_97_vs_grok(eng, name):
     mse = np.mean((dec - img) ** 2)
     psnr = 10 * np.log10(((1 << cfg["bits"]) - 1) ** 2 / mse)
     assert abs(psnr - cfg["grok_psnr_db"]) <= 0.1
+
+
+def test_fullsize_c3_exact_config_vs_oracle(eng):
+    """C3 exactly as BASELINE configures it (8192^2 RGB12, -I -r 40,20,10, single precinct):
+    no Grok hash exists here (Grok is not rebuilt; its decoder is broken on this stream,
+    SURVEY R-BUG-3), so the reference is the Grok-pinned oracle's stream
+    (full_size.json oracle_fullsize.C3, make_oracle_fullsize.py)."""
+    import torch
+    import grok_amd as G
+    cfg = FULL["oracle_fullsize"]["C3"]
+    img = _img(cfg)
+    params = G.default_params(irreversible=True, layer_rate=[40.0, 20.0, 10.0])
+    x = torch.from_numpy(img).cuda()
+    out = torch.empty(img.nbytes + (1 << 24), dtype=torch.uint8, device="cuda")
+    n = eng.encode(x, cfg["bits"], params=params, out=out)
+    assert n == cfg["bytes"]
+    assert hashlib.sha256(out[:n].cpu().numpy().tobytes()).hexdigest() == cfg["sha256"]
+    y = torch.empty_like(x)
+    eng.decode(out, length=n, out=y)
+    dec = y.cpu().numpy().astype(np.float64)
+    psnr = 10 * np.log10(4095.0 ** 2 / np.mean((dec - img) ** 2))
+    assert psnr > 33.0   # the 3-layer stream decodes to ~33.4 dB (Grok's own decoder gives 17.9 dB here)
