@@ -89,7 +89,8 @@ def load_library(build_if_missing=True):
     lib.gk_jp2_header.argtypes = [ctypes.c_void_p, P(ImageInfo), ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t,
                                   P(ctypes.c_size_t)]
     lib.gk_probe_header.restype = ctypes.c_int
-    lib.gk_probe_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, P(ImageInfo), ctypes.c_char_p, ctypes.c_size_t]
+    lib.gk_probe_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, P(ImageInfo), P(CParameters), ctypes.c_char_p,
+                                    ctypes.c_size_t]
     lib.gk_decode_window.restype = ctypes.c_int
     lib.gk_decode_window.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int] + \
         [ctypes.c_uint32] * 4 + [P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_int]
@@ -147,7 +148,7 @@ def probe_header(cs):
     b = np.frombuffer(bytes(cs), np.uint8)
     info = ImageInfo()
     msg = ctypes.create_string_buffer(256)
-    if lib.gk_probe_header(b.ctypes.data, len(b), ctypes.byref(info), msg, 256) != 0:
+    if lib.gk_probe_header(b.ctypes.data, len(b), ctypes.byref(info), None, msg, 256) != 0:
         raise ValueError(msg.value.decode())
     return info
 

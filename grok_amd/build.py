@@ -6,14 +6,15 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgrok_amd.so")
-SOURCES = ["gk_kernels.hip", "gk_dwt97.hip", "gk_t1enc.hip", "gk_t1dec.hip", "gk_ht.hip", "gk_engine.cpp"]
+SOURCES = ["gk_kernels.hip", "gk_dwt97.hip", "gk_t1enc.hip", "gk_t1dec.hip", "gk_ht.hip", "gk_engine.cpp", "grk_shim.cpp"]
 
 
 def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(HERE, "..", "include", "grok_amd.h")]
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + \
+        [os.path.join(HERE, "..", "include", f) for f in ("grok_amd.h", "grk_abi.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 

@@ -2690,16 +2690,41 @@ int gk_jp2_header(gk_ctx* ctx, const gk_image_info* info, uint64_t cs_len, uint8
     }
 }
 
-int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, char* msg, size_t msg_cap) {
+int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, gk_cparameters* coding, char* msg,
+                    size_t msg_cap) {
     if (!cs || !info) return -1;
     try {
         ByteSrc S; S.len = len; S.host = cs;
         size_t joff = 0, jlen = 0;
-        if (jp2_locate(S, joff, jlen)) { S = ByteSrc(); S.len = jlen; S.host = cs + joff; }
+        const bool jp2 = jp2_locate(S, joff, jlen);
+        if (jp2) { S = ByteSrc(); S.len = jlen; S.host = cs + joff; }
         Header Hd;
         parse_header(S, Hd);
         info->w = Hd.want.w; info->h = Hd.want.h; info->numcomps = Hd.want.nc; info->prec = Hd.want.prec;
         info->sgnd = Hd.want.sgnd;
+        info->sample_bytes = 0;
+        if (coding) {
+            const Params& p = Hd.want.p;
+            gk_set_default_params(coding);
+            coding->numlayers = (uint16_t)p.nlayers;
+            coding->numresolution = (uint8_t)p.numres;
+            coding->cblockw_init = 1u << p.cbw; coding->cblockh_init = 1u << p.cbh;
+            coding->cblk_sty = (uint8_t)p.cblk_sty;
+            coding->irreversible = (uint8_t)p.irrev;
+            coding->mct = (uint8_t)p.mct;
+            coding->numgbits = (uint8_t)p.numgbits;
+            coding->csty = p.custom_prc ? 1 : 0;
+            coding->res_spec = p.custom_prc ? p.numres : 0;
+            for (uint32_t r = 0; r < p.numres; ++r) {   // highest resolution first, as grk_cparameters
+                coding->prcw_init[r] = 1u << p.prcw[p.numres - 1 - r];
+                coding->prch_init[r] = 1u << p.prch[p.numres - 1 - r];
+            }
+            coding->tile_size_on = p.tw != 0;
+            coding->t_width = p.tw ? p.tw : Hd.want.w; coding->t_height = p.th ? p.th : Hd.want.h;
+            coding->writeTLM = !Hd.tlm.empty();
+            coding->writePLT = 0;
+            coding->cod_format = jp2 ? 2 : 0;
+        }
         return 0;
     } catch (const GkError& e) {
         if (msg && msg_cap) snprintf(msg, msg_cap, "%s", e.msg.c_str());

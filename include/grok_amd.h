@@ -123,8 +123,11 @@ int gk_jp2_header(gk_ctx* ctx, const gk_image_info* info, uint64_t cs_len, uint8
 int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, gk_image_info* info);
 
 /* The same header parse on host bytes without an engine (no device needed): image info of a
- * codestream / JP2 file, or < 0 with the reason in msg. */
-int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, char* msg, size_t msg_cap);
+ * codestream / JP2 file and, when coding != NULL, its coding style in gk_cparameters terms
+ * (CodeStreamDecompress main-header markers; what grk_decompress_read_header reports in
+ * grk_header_info), or < 0 with the reason in msg. */
+int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, gk_cparameters* coding, char* msg,
+                    size_t msg_cap);
 
 /* grk_decompress (grok.cpp:287-297; TileProcessor::decompressT2T1 TileProcessor.cpp:384-408):
  * decode into comps[c] (device memory if out_on_device): int32 planes (sample_bytes 0 / 4) or planar
