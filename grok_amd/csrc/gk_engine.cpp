@@ -453,13 +453,13 @@ static void build_plan(Plan& P) {
         T.x1 = std::min(T.x0 + P.tw, P.w); T.y1 = std::min(T.y0 + P.th, P.h);
         build_tile(P, T, P.shapes[shape_of[t]]);
     }
-    // encode slots: w*h*4 bytes + 16 (2-byte pad, alignment)
+    // encode slots: w*h*4 + 64 bytes each, 64-byte aligned (the MQ coder stores whole 64-byte lines)
     uint64_t off = 0;
     for (auto& G : P.blocks) {
         uint32_t cap = (uint32_t)G.w * G.h * 4 + 64;
-        G.data_off = off + 16;
+        G.data_off = off;
         G.data_cap = cap;
-        off += align_up(cap + 16, 64);
+        off += align_up(cap, 64);
     }
     P.slot_bytes = off;
     // symbol streams for the parallel context modeller: band numbps planes x 11264 symbols
@@ -1639,8 +1639,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // T1 over the block range [b0, b1): every per-block device array is range-local
     const bool do_rc = P.p.rate_control();
-    const uint64_t slot0 = P.blocks[b0].data_off - 16;
-    const uint64_t slot1 = b1 < nb ? P.blocks[b1].data_off - 16 : P.slot_bytes;
+    const uint64_t slot0 = P.blocks[b0].data_off;
+    const uint64_t slot1 = b1 < nb ? P.blocks[b1].data_off : P.slot_bytes;
     const uint64_t slot_span = slot1 - slot0;    // the range's slots; host bytes are staged after them
     uint8_t* dbytes = (uint8_t*)ctx->bytes.get(slot_span + (64u << 20));
     const uint32_t nbx = std::max(nbr, 1u);

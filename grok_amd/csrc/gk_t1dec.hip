@@ -130,17 +130,19 @@ __device__ __forceinline__ void ld2(const uint64_t* p, uint64_t& a, uint64_t& b)
     a = v.x; b = v.y;
 }
 __device__ __forceinline__ void st2(uint64_t* p, uint64_t a, uint64_t b) { *(ulonglong2*)p = make_ulonglong2(a, b); }
-__device__ __forceinline__ void load_rows(Rows22& R, const uint64_t* WS, uint32_t k, uint32_t y0) {
+// Only the rows the stripe-pass of type t (0 SP, 1 MR, 2 CL) reads are fetched: SP starts a
+// plane (no plane-bit or visited rows) and ignores refinement rows; MR ignores signs; CL
+// ignores refinement rows; the first cleanup pass (k == 0) has no plane or visited rows yet.
+__device__ __forceinline__ void load_rows(Rows22& R, const uint64_t* WS, uint32_t k, uint32_t t, uint32_t y0) {
     const uint64_t* sg = WS + WS_SIG + y0 + 1;
     const uint64_t* ng = WS + WS_NEG + y0 + 1;
     const uint64_t* pi = WS + WS_PI + y0;
     const uint64_t* mu = WS + WS_MU + y0;
     const uint64_t* bt = WS + WS_BITS + (size_t)k * 64 + y0;
     ld2(sg, R.s1, R.s2); ld2(sg + 2, R.s3, R.s4); R.s5 = sg[4];
-    ld2(ng, R.n1, R.n2); ld2(ng + 2, R.n3, R.n4); R.n5 = ng[4];
-    ld2(pi, R.p0, R.p1); ld2(pi + 2, R.p2, R.p3);
-    ld2(mu, R.m0, R.m1); ld2(mu + 2, R.m2, R.m3);
-    ld2(bt, R.b0, R.b1); ld2(bt + 2, R.b2, R.b3);
+    if (t != 1) { ld2(ng, R.n1, R.n2); ld2(ng + 2, R.n3, R.n4); R.n5 = ng[4]; }
+    if (t != 0 && k != 0) { ld2(pi, R.p0, R.p1); ld2(pi + 2, R.p2, R.p3); ld2(bt, R.b0, R.b1); ld2(bt + 2, R.b2, R.b3); }
+    if (t == 1) { ld2(mu, R.m0, R.m1); ld2(mu + 2, R.m2, R.m3); }
 }
 
 // next (plane, pass type, stripe) after (k, t, s); pass types 0 SP, 1 MR, 2 CL
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
     {
         uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
         next_pos3(k2, t2, s2, p2, ns);
-        if (!done && p2 < npasses && k2 < numbps) load_rows(X, WS, k2, 4 * s2);
+        if (!done && p2 < npasses && k2 < numbps) load_rows(X, WS, k2, t2, 4 * s2);
     }
 
     while (__any(!done)) {
@@ -361,8 +363,10 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
                     uint64_t* ngp = WS + WS_NEG + y0 + 1;
                     uint64_t* pip = WS + WS_PI + y0;
                     uint64_t* btp = WS + WS_BITS + (size_t)k * 64 + y0;
-                    st2(sgp, S1, S2); st2(sgp + 2, S3, S4);
-                    st2(ngp, N1, N2); st2(ngp + 2, N3, N4);
+                    if (t != 1) {   // MR changes neither significance nor signs
+                        st2(sgp, S1, S2); st2(sgp + 2, S3, S4);
+                        st2(ngp, N1, N2); st2(ngp + 2, N3, N4);
+                    }
                     if (t == 0) { st2(pip, P0, P1); st2(pip + 2, P2, P3); }
                     st2(btp, B0, B1); st2(btp + 2, B2, B3);
                 }
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
                 const bool resync = !done && (ns == 1 || (ns == 2 && s == 0));
                 if (__any(resync)) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (resync) load_rows(X, WS, k, 4 * s);
+                    if (resync) load_rows(X, WS, k, t, 4 * s);
                 }
                 const bool newplane = t == 0 || k == 0;
                 const uint64_t nS0 = s ? S4 : 0ull, nN0 = s ? N4 : 0ull;
@@ -427,14 +431,16 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
             uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
             next_pos3(k2, t2, s2, p2, ns);
             if (switched && !done && p2 < npasses && k2 < numbps)
-                load_rows(X, WS, k2, 4 * s2);
+                load_rows(X, WS, k2, t2, 4 * s2);
             if (late) {
                 uint64_t* sgp = WS + WS_SIG + wy0 + 1;
                 uint64_t* ngp = WS + WS_NEG + wy0 + 1;
                 uint64_t* pip = WS + WS_PI + wy0;
                 uint64_t* btp = WS + WS_BITS + (size_t)wk * 64 + wy0;
-                st2(sgp, W0, W1); st2(sgp + 2, W2, W3);
-                st2(ngp, W4, W5); st2(ngp + 2, W6, W7);
+                if (wt != 1) {
+                    st2(sgp, W0, W1); st2(sgp + 2, W2, W3);
+                    st2(ngp, W4, W5); st2(ngp + 2, W6, W7);
+                }
                 if (wt == 0) { st2(pip, WP0, WP1); st2(pip + 2, WP2, WP3); }
                 st2(btp, WB0, WB1); st2(btp + 2, WB2, WB3);
                 if (wmu && !done) {

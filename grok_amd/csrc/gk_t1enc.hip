@@ -318,9 +318,15 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
 // the same symbol index: the 16-symbol chunks of every lane are fetched at the
 // same (uniform) steps, two chunks ahead, and the loop is unrolled by 16 so a
 // fetch is consumed 32 steps after it was issued.  Pass boundaries come from a
-// per-lane copy of the pass-end table in LDS.  Context states live in VGPRs
-// (one byte per context: state | mps << 6).
+// per-lane copy of the pass-end table in LDS.
+// Context states live in LDS per lane as their probability-table entry with the
+// MPS in bit 31 (one read gives Qe, NMPS, NLPS and SWITCH; the next entry is
+// written back off the symbol's dependency chain), as in the decoder.
+// Output bytes gather into dwords in a VGPR and the dwords into a 64-byte line per
+// lane in LDS; a full line leaves as four 16-byte stores, so HBM sees whole lines
+// instead of one 4-byte write per lane-dword (scattered over 64 slots).
 // ---------------------------------------------------------------------------
+#define MQ_LINE_DW 16
 struct MqLane {
     uint32_t a, c, ct;
     int32_t bp;
@@ -330,6 +336,11 @@ struct MqLane {
     uint32_t cap;
     uint32_t ovf;
 };
+struct MqLds {
+    uint32_t tab[48];
+    uint32_t ctx[19][64];                 // per-lane context states (table entry | MPS << 31)
+    uint32_t line[64][MQ_LINE_DW + 1];    // per-lane output line (row padded: conflict-free columns)
+};
 
 __device__ __forceinline__ uint32_t vsel_e(bool c, uint32_t a, uint32_t b) {
     uint64_t m = __ballot(c);
@@ -338,42 +349,61 @@ __device__ __forceinline__ uint32_t vsel_e(bool c, uint32_t a, uint32_t b) {
     return r;
 }
 
-__device__ __forceinline__ void mql_emit(MqLane& q, uint32_t nb) {
+// the line holding stream bytes [64k, 64k + 64) goes out when its last dword is complete
+__device__ __forceinline__ void mql_line_out(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane, uint32_t first_byte,
+                                             uint32_t ndw) {
+    uint8_t* dst = q.out + first_byte;
+    if (ndw == MQ_LINE_DW) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            *(uint4*)(dst + 16 * i) = make_uint4(line[lane][4 * i], line[lane][4 * i + 1], line[lane][4 * i + 2],
+                                                 line[lane][4 * i + 3]);
+    } else {
+        for (uint32_t i = 0; i < ndw; ++i) *(uint32_t*)(dst + 4 * i) = line[lane][i];
+    }
+}
+
+// one completed dword (stream bytes [bp - 3, bp]) into the lane's line; a full line is stored
+__device__ __forceinline__ void mql_dword(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane, bool full, uint32_t wb) {
+    const uint32_t k = ((uint32_t)(q.bp - 3) >> 2) & (MQ_LINE_DW - 1);
+    if (full) line[lane][k] = wb;
+    const bool flush = full & (k == MQ_LINE_DW - 1);
+    if (__any(flush)) {
+        if (flush) mql_line_out(q, line, lane, (uint32_t)(q.bp - 3) & ~63u, MQ_LINE_DW);
+    }
+}
+
+__device__ __forceinline__ void mql_emit(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane, uint32_t nb) {
     if (q.bp >= 0) {
         if ((uint32_t)q.bp < q.cap) {
             q.wbuf |= q.cur << (8 * (q.bp & 3));
-            if ((q.bp & 3) == 3) { *(uint32_t*)(q.out + (q.bp - 3)) = q.wbuf; q.wbuf = 0; }
+            if ((q.bp & 3) == 3) { mql_dword(q, line, lane, true, q.wbuf); q.wbuf = 0; }
         } else q.ovf = 1;
     }
     q.bp++;
     q.cur = nb & 0xff;
 }
-// BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127), branch-free except the word store
-__device__ __forceinline__ void mql_byteout_if(MqLane& q, bool en) {
+// BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127), used at the flush only
+__device__ __forceinline__ void mql_byteout(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane) {
     const bool carry = q.cur != 0xff && (q.c & 0x8000000);
     const uint32_t cur = q.cur + (carry ? 1u : 0u);
     const uint32_t c = carry ? (q.c & 0x7ffffff) : q.c;
     const bool ff = cur == 0xff;
     const uint32_t nb = ff ? (c >> 20) : (c >> 19);
-    if (en) {
-        q.cur = cur;
-        q.c = c & (ff ? 0xfffffu : 0x7ffffu);
-        q.ct = ff ? 7u : 8u;
-        mql_emit(q, nb);
-    }
+    q.cur = cur;
+    q.c = c & (ff ? 0xfffffu : 0x7ffffu);
+    q.ct = ff ? 7u : 8u;
+    mql_emit(q, line, lane, nb);
 }
-__device__ __forceinline__ void mql_byteout(MqLane& q) { mql_byteout_if(q, true); }
-
-struct Ctx5e { uint32_t w0, w1, w2, w3, w4; };
 
 // Byte emission for the symbol loop: `cur` goes to position bp (bp = -1 is the encoder's
 // dummy byte before the buffer, which the one unsigned compare also excludes; overflow past
-// `cap` is detected from the final bp).  Branch-free except the predicated word store.
-__device__ __forceinline__ void mql_put_sel(MqLane& q, bool en, uint32_t cur) {
+// `cap` is detected from the final bp).  Branch-free except the line store.
+__device__ __forceinline__ void mql_put_sel(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane, bool en, uint32_t cur) {
     const bool put = en & ((uint32_t)q.bp < q.cap);
     const uint32_t wb = q.wbuf | (put ? cur << (8 * (q.bp & 3)) : 0u);
     const bool full = put & ((q.bp & 3) == 3);
-    if (full) *(uint32_t*)(q.out + (q.bp - 3)) = wb;
+    mql_dword(q, line, lane, full, wb);
     q.wbuf = full ? 0u : wb;
     q.bp += en ? 1 : 0;
 }
@@ -385,26 +415,21 @@ __device__ __forceinline__ void mql_put_sel(MqLane& q, bool en, uint32_t cur) {
 // C >> e, e = the bits shifted past the boundary; they stay below the new byte, whose CT
 // (8, or 7 after 0xFF) is reduced by e.  A second boundary in one renormalisation (e >= 8)
 // repeats the BYTEOUT (rare; at most two for shifts <= 15: after the first, e <= 14 - 7).
-__device__ __forceinline__ void mq_code3(MqLane& q, Ctx5e& cw, const uint32_t* tab, uint32_t s, bool en) {
+__device__ __forceinline__ void mq_code4(MqLane& q, MqLds& L, int lane, uint32_t s, bool en) {
     const uint32_t cx = s >> 1, d = s & 1;
-    const uint32_t wi = cx >> 2, shb = (cx & 3) * 8;
-    uint32_t word = vsel_e(wi == 4, cw.w4, vsel_e(wi & 2, vsel_e(wi & 1, cw.w3, cw.w2), vsel_e(wi & 1, cw.w1, cw.w0)));
-    const uint32_t st = (word >> shb) & 0xff;
-    const uint32_t mps = st >> 6;
-    const uint32_t e = tab[st & 63];
+    const uint32_t e = L.ctx[cx][lane];
+    const uint32_t mps = e >> 31;
     const uint32_t qe = e & 0xffff;
     const uint32_t a1 = q.a - qe;
     const bool is_mps = mps == d;
     const bool fast = is_mps & ((a1 & 0x8000) != 0);   // MPS without renormalisation
     const bool x = is_mps ^ (a1 < qe);
-    const uint32_t nst = is_mps ? (((e >> 16) & 0x3f) | (mps << 6)) : (((e >> 22) & 0x3f) | ((mps ^ (e >> 28)) << 6));
+    const uint32_t nidx = is_mps ? ((e >> 16) & 0x3f) : ((e >> 22) & 0x3f);
+    const uint32_t nmps = is_mps ? mps : (mps ^ ((e >> 28) & 1));
     const bool upd = en & !fast;
+    const uint32_t ne = L.tab[nidx] | (nmps << 31);
+    L.ctx[cx][lane] = upd ? ne : e;   // unconditional: a branch here would wait on the table read
     const uint32_t an = vsel_e(en, x ? a1 : qe, q.a);
-    word = (word & ~(0xffu << shb)) | (nst << shb);
-    const uint32_t wu = upd ? wi : 7u;
-    cw.w0 = vsel_e(wu == 0, word, cw.w0); cw.w1 = vsel_e(wu == 1, word, cw.w1);
-    cw.w2 = vsel_e(wu == 2, word, cw.w2); cw.w3 = vsel_e(wu == 3, word, cw.w3);
-    cw.w4 = vsel_e(wu == 4, word, cw.w4);
     const uint32_t n = upd ? __clz(an) - 16 : 0u;
     q.a = an << n;
     uint64_t c = (uint64_t)(q.c + ((en & x) ? qe : 0u)) << n;
@@ -416,7 +441,7 @@ __device__ __forceinline__ void mq_code3(MqLane& q, Ctx5e& cw, const uint32_t* t
         c &= ~((uint64_t)carry << (27 + sh));
         const bool ff = cur == 0xff;
         const uint32_t nb = (uint32_t)(c >> ((ff ? 20u : 19u) + sh)) & 0xffu;
-        mql_put_sel(q, bo, cur);
+        mql_put_sel(q, L.line, lane, bo, cur);
         q.cur = vsel_e(bo, nb, q.cur);
         const uint64_t keep = ((uint64_t)(ff ? 0x100000u : 0x80000u) << sh) - 1;
         c = bo ? (c & keep) : c;
@@ -446,10 +471,10 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
                                               uint32_t nblocks, int* err, const int32_t* __restrict__ pass_nmse,
                                               uint32_t* __restrict__ pass_counter, uint32_t nl) {
     // nl = blocks per wave (lanes >= nl idle; gk_t1enc_lanes); pass ends staged in LDS [pass][lane]
-    __shared__ uint32_t tab[47];
+    __shared__ MqLds L;
     extern __shared__ uint32_t pe_dyn[];
     const int lane = threadIdx.x;
-    if (lane < 47) tab[lane] = c_mq[lane];
+    if (lane < 47) L.tab[lane] = c_mq[lane];
     const uint32_t b = blockIdx.x * nl + lane;
     const bool has = (uint32_t)lane < nl && b < nblocks;
     uint32_t* pe_col = pe_dyn + (lane < (int)nl ? lane : 0);
@@ -470,8 +495,9 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
     MqLane q;
     q.a = 0x8000; q.c = 0; q.ct = 12; q.bp = -1; q.cur = 0; q.wbuf = 0; q.out = bytes + B.data_off; q.cap = B.data_cap;
     q.ovf = 0;
-    // initial context states (mqc_resetstates): ZC ctx0 -> 4, AGG -> 3, UNI -> 46
-    Ctx5e cw = {4u, 0u, 0u, 0u, (3u << 8) | (46u << 16)};
+    // initial context states (mqc_resetstates): every context at state 0 except ZC0 = 4, AGG = 3, UNI = 46
+    for (int c = 0; c < 19; ++c)
+        L.ctx[c][lane] = c_mq[c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))];
     uint32_t maxsym = nsym;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxsym = max(maxsym, (uint32_t)__shfl_xor((int)maxsym, o));
@@ -485,9 +511,9 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
                     uint32_t tempc = q.c + q.a;
                     q.c |= 0xffff;
                     if (q.c >= tempc) q.c -= 0x8000;
-                    q.c <<= q.ct; mql_byteout(q);
-                    q.c <<= q.ct; mql_byteout(q);
-                    if (q.cur != 0xff) mql_emit(q, 0);
+                    q.c <<= q.ct; mql_byteout(q, L.line, lane);
+                    q.c <<= q.ct; mql_byteout(q, L.line, lane);
+                    if (q.cur != 0xff) mql_emit(q, L.line, lane, 0);
                     P[p].rate = (uint32_t)q.bp;
                 } else {
                     P[p].rate = (uint32_t)q.bp + 5 + (q.ct < 5 ? 1 : 0);
@@ -522,7 +548,7 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
         for (uint32_t j = 0; j < 16; ++j) {
             const uint32_t i = base + j;
             const bool en = i < nsym;
-            mq_code3(q, cw, tab, byte_of(cur4, j), en);
+            mq_code4(q, L, lane, byte_of(cur4, j), en);
             // the prefetch two chunks ahead is issued after the first symbol has consumed this
             // chunk's bytes, so the wait for them does not also wait for the prefetch
             if (j == 0) {
@@ -534,10 +560,11 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
         }
         cur4 = nxt4; nxt4 = pre;
     }
-    // flush the partial output word (bytes [bp & ~3, bp) plus the pending byte)
+    // the partial last line: whole dwords before bp, then the dword holding bp (pending byte)
     if (npasses && q.bp >= 0 && (uint32_t)q.bp < q.cap) {
-        q.wbuf |= q.cur << (8 * (q.bp & 3));
-        *(uint32_t*)(q.out + (q.bp & ~3)) = q.wbuf;
+        const uint32_t k = ((uint32_t)q.bp >> 2) & (MQ_LINE_DW - 1);
+        L.line[lane][k] = q.wbuf | (q.cur << (8 * (q.bp & 3)));
+        mql_line_out(q, L.line, lane, (uint32_t)q.bp & ~63u, k + 1);
     }
     if (!has) return;
     if (npasses == 0) { info[4 * b] = 0; info[4 * b + 1] = 0; info[4 * b + 2] = 0; info[4 * b + 3] = 0; return; }
