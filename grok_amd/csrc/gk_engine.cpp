@@ -1442,6 +1442,11 @@ struct gk_ctx {
     // band quantisation held by the cached plan's bands: the plan's own (encoder, native_qcd)
     // or that of the last decoded stream (band_qcd)
     std::vector<std::pair<uint32_t, uint32_t>> native_qcd, band_qcd;
+    // results of the last gk_encode_blocks
+    std::vector<gk_band_result> rb_bands;
+    std::vector<gk_block_result> rb_blocks;
+    std::vector<gk_pass_result> rb_passes;
+    std::vector<uint8_t> rb_data;
 };
 
 static void set_params(Params& P, const gk_cparameters* cp) {
@@ -1582,10 +1587,75 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     restore_native_qcd(ctx);
 }
 
+// gk_encode_blocks: the T1 results of the (single) tile in canonical order, the block bytes
+// compacted on the device (the HT pieces joined: MagSgn head, then MEL + VLC tail) and copied out.
+static void dump_blocks(gk_ctx* ctx, const uint32_t* hinfo, const GkPass* dps, uint32_t npass_total,
+                        uint8_t* dbytes, uint64_t slot0) {
+    const Plan& P = ctx->plan;
+    hipStream_t st = ctx->st;
+    const bool ht = P.p.ht();
+    std::vector<GkPass> hp(std::max(npass_total, 1u));
+    if (!ht && npass_total)
+        HIPCHK(hipMemcpyAsync(hp.data(), dps, sizeof(GkPass) * npass_total, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ctx->rb_bands.clear(); ctx->rb_blocks.clear(); ctx->rb_passes.clear();
+    std::vector<uint64_t> seg;
+    uint64_t pos = 0;
+    const TileG& T = P.tiles[0];
+    for (uint32_t c = 0; c < P.nc; ++c)
+        for (uint32_t r = 0; r < P.p.numres; ++r) {
+            const ResG& R = T.comps[c].res[r];
+            for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
+                const BandG& B = R.bands[bi];
+                ctx->rb_bands.push_back({c, r, bi, B.orient, R.pw * R.ph, B.step_enc});
+                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                    const PrecG& PG = R.prc[bi][pi];
+                    for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                        const uint32_t b = PG.first_block + k;
+                        const GkBlock& G = P.blocks[b];
+                        gk_block_result o{};
+                        o.comp = c; o.res = r; o.band = bi; o.precinct = pi; o.cblk = k;
+                        o.x0 = P.bxy[2 * (size_t)b]; o.y0 = P.bxy[2 * (size_t)b + 1];
+                        o.x1 = o.x0 + G.w; o.y1 = o.y0 + G.h;
+                        o.numbps = hinfo[4 * (size_t)b]; o.npasses = hinfo[4 * (size_t)b + 1];
+                        o.len = hinfo[4 * (size_t)b + 2];
+                        o.pass_off = (uint32_t)ctx->rb_passes.size();
+                        o.data_off = pos;
+                        const uint64_t so = G.data_off - slot0;
+                        if (ht && o.npasses) {
+                            const uint32_t ms = hinfo[4 * (size_t)b + 3], tl = o.len - ms;
+                            if (ms) { seg.push_back(so); seg.push_back(pos); seg.push_back(ms); }
+                            seg.push_back(so + G.data_cap - tl); seg.push_back(pos + ms); seg.push_back(tl);
+                            ctx->rb_passes.push_back({o.len, o.len, 0.0});
+                        } else if (o.npasses) {
+                            seg.push_back(so); seg.push_back(pos); seg.push_back(o.len);
+                            const GkPass* ps = hp.data() + hinfo[4 * (size_t)b + 3];
+                            for (uint32_t q = 0; q < o.npasses; ++q)
+                                ctx->rb_passes.push_back({q + 1 == o.npasses ? o.len : ps[q].rate, ps[q].len, ps[q].dist});
+                        }
+                        pos += o.len;
+                        ctx->rb_blocks.push_back(o);
+                    }
+                }
+            }
+        }
+    ctx->rb_data.resize(pos);
+    if (pos) {
+        uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8);
+        memcpy(hs, seg.data(), seg.size() * 8);
+        uint64_t* ds = (uint64_t*)ctx->dseg.get(seg.size() * 8);
+        HIPCHK(hipMemcpyAsync(ds, hs, seg.size() * 8, hipMemcpyHostToDevice, st));
+        uint8_t* dst = (uint8_t*)ctx->dout.get(pos);
+        gk_launch_gather(st, dbytes, dst, ds, (uint32_t)(seg.size() / 3));
+        HIPCHK(hipMemcpyAsync(ctx->rb_data.data(), dst, pos, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+}
+
 static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, const uint32_t* strides,
                           int comps_on_device, const gk_cparameters* cp, uint8_t* out, size_t cap, int out_on_device,
                           int* rc, uint32_t tb = 0, uint32_t te = 0, bool with_header = true,
-                          uint32_t* part_lens = nullptr) {
+                          uint32_t* part_lens = nullptr, bool blocks_only = false) {
     setup_plan(ctx, info, cp);
     Plan& P = ctx->plan;
     const uint32_t ntiles = (uint32_t)P.tiles.size();
@@ -1695,6 +1765,11 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         HIPCHK(hipMemcpyAsync(hp, dps, sizeof(GkPass) * (size_t)npass_total, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         hpasses = hp;
+    }
+    if (blocks_only) {   // gk_encode_blocks: T1 results only (the host of a T1 plugin runs T2)
+        dump_blocks(ctx, hinfo, dps, npass_total, dbytes, slot0);
+        *rc = 0;
+        return 0;
     }
 
     // ---- host T2 (T2Compress.cpp:113-240) with layer formation / rate allocation
@@ -2467,7 +2542,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 uint32_t mp = 0;
                 for (uint32_t i = wv * 64; i < wv * 64 + L; ++i)
                     if (hord[i] != 0xffffffffu) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
-                wo += (262 + (uint64_t)mp * 64) * 64;   // per-lane slab: WS_FIXED + planes (gk_t1dec.hip)
+                wo += (272 + (uint64_t)mp * 64) * 64;   // per-lane slab: WS_FIXED + planes (gk_t1dec.hip), 128 B lines
             }
             hwo[nw] = wo;
         }
@@ -2628,6 +2703,38 @@ int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const void* const* c
         ctx->err = e.msg;
         return -1;
     }
+}
+
+int gk_encode_blocks(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, const uint32_t* strides,
+                     int comps_on_device, const gk_cparameters* p, uint32_t* nbands, uint32_t* nblocks,
+                     uint64_t* nbytes, uint32_t* npasses) {
+    if (!ctx || !info || !comps || !strides) return -1;
+    try {
+        (void)hipSetDevice(ctx->device);
+        if (p && p->tile_size_on && (p->t_width < info->w || p->t_height < info->h))
+            throw GkError("code-block results are produced for single-tile images only (Grok's plugin tile is one tile)");
+        int rc = 0;
+        uint8_t dummy = 0;
+        encode_impl(ctx, info, comps, strides, comps_on_device, p, &dummy, 0, 0, &rc, 0, 0, true, nullptr, true);
+        if (nbands) *nbands = (uint32_t)ctx->rb_bands.size();
+        if (nblocks) *nblocks = (uint32_t)ctx->rb_blocks.size();
+        if (nbytes) *nbytes = ctx->rb_data.size();
+        if (npasses) *npasses = (uint32_t)ctx->rb_passes.size();
+        return rc;
+    } catch (const GkError& e) {
+        ctx->err = e.msg;
+        return -1;
+    }
+}
+
+int gk_encode_blocks_get(gk_ctx* ctx, gk_band_result* bands, gk_block_result* blocks, uint8_t* data,
+                         gk_pass_result* passes) {
+    if (!ctx) return -1;
+    if (bands) std::copy(ctx->rb_bands.begin(), ctx->rb_bands.end(), bands);
+    if (blocks) std::copy(ctx->rb_blocks.begin(), ctx->rb_blocks.end(), blocks);
+    if (data && !ctx->rb_data.empty()) memcpy(data, ctx->rb_data.data(), ctx->rb_data.size());
+    if (passes) std::copy(ctx->rb_passes.begin(), ctx->rb_passes.end(), passes);
+    return 0;
 }
 
 int gk_main_header(gk_ctx* ctx, const gk_image_info* info, const gk_cparameters* p, uint8_t* out, size_t cap,

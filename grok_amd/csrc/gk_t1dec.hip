@@ -38,14 +38,17 @@
 #include <cstdio>
 #include <cstdlib>
 
-// per-lane scratch (uint64 words, one contiguous slab per lane): field F row r at F + r
-// (offsets chosen so every stripe's first row is 16-byte aligned: rows move in pairs)
-#define WS_SIG 1      // 66 rows (row y at y + 1, guards 0 and 65)
-#define WS_NEG 67     // 66 rows
-#define WS_MU 134     // 64 rows: refined in an earlier plane
-#define WS_PI 198     // 64 rows: visited in the current plane
-#define WS_BITS 262   // numbps planes x 64 rows: bit of the plane (plane 0 = most significant)
-#define WS_FIXED 262
+// per-lane scratch (uint64 words, one contiguous slab per lane, 128-byte aligned).  A stripe's
+// state rows are one 128-byte line: stripe s at 16 s holds significance, sign, visited (SP of the
+// current plane) and refined-in-an-earlier-plane rows 4s .. 4s+3, four words each, so a stripe
+// boundary moves whole lines (plus the first rows of the next stripe's line: the row below).
+// Stripe 16 is an all-zero guard.  The decoded bit-plane rows follow, plane-major.
+#define WS_S 0        // + 16 s + (y & 3): significance of row y = 4 s + (y & 3)
+#define WS_N 4        // sign (set where significant)
+#define WS_P 8        // visited in SP of the current plane
+#define WS_M 12       // refined in an earlier plane
+#define WS_BITS 272   // numbps planes x 64 rows: bit of the plane (plane 0 = most significant)
+#define WS_FIXED 272
 
 // ------------------------------------------------------------------ MQ byte ring
 // Compressed bytes reach the coder through a 128-byte per-lane ring in LDS
@@ -134,15 +137,12 @@ __device__ __forceinline__ void st2(uint64_t* p, uint64_t a, uint64_t b) { *(ulo
 // plane (no plane-bit or visited rows) and ignores refinement rows; MR ignores signs; CL
 // ignores refinement rows; the first cleanup pass (k == 0) has no plane or visited rows yet.
 __device__ __forceinline__ void load_rows(Rows22& R, const uint64_t* WS, uint32_t k, uint32_t t, uint32_t y0) {
-    const uint64_t* sg = WS + WS_SIG + y0 + 1;
-    const uint64_t* ng = WS + WS_NEG + y0 + 1;
-    const uint64_t* pi = WS + WS_PI + y0;
-    const uint64_t* mu = WS + WS_MU + y0;
+    const uint64_t* st = WS + 4 * y0;   // this stripe's line (y0 = 4 s)
     const uint64_t* bt = WS + WS_BITS + (size_t)k * 64 + y0;
-    ld2(sg, R.s1, R.s2); ld2(sg + 2, R.s3, R.s4); R.s5 = sg[4];
-    if (t != 1) { ld2(ng, R.n1, R.n2); ld2(ng + 2, R.n3, R.n4); R.n5 = ng[4]; }
-    if (t != 0 && k != 0) { ld2(pi, R.p0, R.p1); ld2(pi + 2, R.p2, R.p3); ld2(bt, R.b0, R.b1); ld2(bt + 2, R.b2, R.b3); }
-    if (t == 1) { ld2(mu, R.m0, R.m1); ld2(mu + 2, R.m2, R.m3); }
+    ld2(st + WS_S, R.s1, R.s2); ld2(st + WS_S + 2, R.s3, R.s4); R.s5 = st[16 + WS_S];
+    if (t != 1) { ld2(st + WS_N, R.n1, R.n2); ld2(st + WS_N + 2, R.n3, R.n4); R.n5 = st[16 + WS_N]; }
+    if (t != 0 && k != 0) { ld2(st + WS_P, R.p0, R.p1); ld2(st + WS_P + 2, R.p2, R.p3); ld2(bt, R.b0, R.b1); ld2(bt + 2, R.b2, R.b3); }
+    if (t == 1) { ld2(st + WS_M, R.m0, R.m1); ld2(st + WS_M + 2, R.m2, R.m3); }
 }
 
 // next (plane, pass type, stripe) after (k, t, s); pass types 0 SP, 1 MR, 2 CL
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
             // stripe prefetch) first and the write-back stores last; their prefetch never reads
             // rows written back in the same event.  Blocks with <= 3 stripes (prefetch rows that
             // overlap the finished stripe) store first, as program order then orders the reads.
-            bool switched = false, late = false;
+            bool switched = false, late = false, wdirty = false;
             uint64_t W0 = 0, W1 = 0, W2 = 0, W3 = 0, W4 = 0, W5 = 0, W6 = 0, W7 = 0;   // finished stripe S1..S4, N1..N4
             uint64_t WB0 = 0, WB1 = 0, WB2 = 0, WB3 = 0, WP0 = 0, WP1 = 0, WP2 = 0, WP3 = 0;
             uint64_t WM0 = 0, WM1 = 0, WM2 = 0, WM3 = 0;
@@ -355,20 +355,25 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
                 const uint64_t B0 = h_get(Ls.bt, 0, lane), B1 = h_get(Ls.bt, 1, lane), B2 = h_get(Ls.bt, 2, lane),
                                B3 = h_get(Ls.bt, 3, lane);
                 late = ns > 3;
+                // rows a stripe-pass left unchanged are not stored: `fresh` marks the columns that
+                // gained a 1 bit in this plane's bit rows (a new significance in SP / CL, a
+                // refinement 1 in MR); scratch starts zero-filled and SP is the first pass to touch
+                // a plane's bit rows
+                wdirty = fresh != 0;
                 W0 = S1; W1 = S2; W2 = S3; W3 = S4; W4 = N1; W5 = N2; W6 = N3; W7 = N4;
                 WB0 = B0; WB1 = B1; WB2 = B2; WB3 = B3; WP0 = P0; WP1 = P1; WP2 = P2; WP3 = P3;
                 wy0 = y0; wk = k; wt = t;
                 if (!late) {
-                    uint64_t* sgp = WS + WS_SIG + y0 + 1;
-                    uint64_t* ngp = WS + WS_NEG + y0 + 1;
-                    uint64_t* pip = WS + WS_PI + y0;
+                    uint64_t* sgp = WS + 4 * y0 + WS_S;
+                    uint64_t* ngp = WS + 4 * y0 + WS_N;
+                    uint64_t* pip = WS + 4 * y0 + WS_P;
                     uint64_t* btp = WS + WS_BITS + (size_t)k * 64 + y0;
-                    if (t != 1) {   // MR changes neither significance nor signs
+                    if (t != 1 && wdirty) {   // MR changes neither significance nor signs
                         st2(sgp, S1, S2); st2(sgp + 2, S3, S4);
                         st2(ngp, N1, N2); st2(ngp + 2, N3, N4);
                     }
                     if (t == 0) { st2(pip, P0, P1); st2(pip + 2, P2, P3); }
-                    st2(btp, B0, B1); st2(btp + 2, B2, B3);
+                    if (wdirty) { st2(btp, B0, B1); st2(btp + 2, B2, B3); }
                 }
                 if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[0] += t - tp0; tp0 = t; }
                 next_pos3(k, t, s, pidx, ns);
@@ -417,7 +422,7 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
                 wmu = t == 1; wmy = ny0;
                 WM0 = nM0 | C0; WM1 = nM1 | C1; WM2 = nM2 | C2; WM3 = nM3 | C3;
                 if (wmu && !late) {
-                    uint64_t* mup = WS + WS_MU + ny0;
+                    uint64_t* mup = WS + 4 * ny0 + WS_M;
                     st2(mup, WM0, WM1); st2(mup + 2, WM2, WM3);
                 }
                 fresh = 0; ph = PH_FIND;
@@ -433,18 +438,18 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
             if (switched && !done && p2 < npasses && k2 < numbps)
                 load_rows(X, WS, k2, t2, 4 * s2);
             if (late) {
-                uint64_t* sgp = WS + WS_SIG + wy0 + 1;
-                uint64_t* ngp = WS + WS_NEG + wy0 + 1;
-                uint64_t* pip = WS + WS_PI + wy0;
+                uint64_t* sgp = WS + 4 * wy0 + WS_S;
+                uint64_t* ngp = WS + 4 * wy0 + WS_N;
+                uint64_t* pip = WS + 4 * wy0 + WS_P;
                 uint64_t* btp = WS + WS_BITS + (size_t)wk * 64 + wy0;
-                if (wt != 1) {
+                if (wt != 1 && wdirty) {
                     st2(sgp, W0, W1); st2(sgp + 2, W2, W3);
                     st2(ngp, W4, W5); st2(ngp + 2, W6, W7);
                 }
                 if (wt == 0) { st2(pip, WP0, WP1); st2(pip + 2, WP2, WP3); }
-                st2(btp, WB0, WB1); st2(btp + 2, WB2, WB3);
+                if (wdirty) { st2(btp, WB0, WB1); st2(btp + 2, WB2, WB3); }
                 if (wmu && !done) {
-                    uint64_t* mup = WS + WS_MU + wmy;
+                    uint64_t* mup = WS + 4 * wmy + WS_M;
                     st2(mup, WM0, WM1); st2(mup + 2, WM2, WM3);
                 }
             }
@@ -521,7 +526,7 @@ __global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ byte
             atomicOr(&Ls.ng[(r + 1) * 3 + gd][lane], negs ? gb : 0u);
             const bool pb = sig || (pend && is_mr && d);
             atomicOr(&Ls.bt[r * 2 + dx][lane], pb ? (1u << sx) : 0u);
-            fresh |= (uint64_t)(sig ? 1u : 0u) << x;
+            fresh |= (uint64_t)(pb ? 1u : 0u) << x;   // pb == sig outside MR (run-length test in CL)
             // SP: positions after (x, r) that gain a significant neighbour become candidates:
             // (x, r+1) and column x+1 rows r-1 .. r+1, unless significant (window bits 7; 2, 5, 8)
             const bool spn = sig && is_sp;
@@ -619,7 +624,7 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
             if (M) {
                 int qq = (t == 0 && (M >> (bpl + 1)) != 0) ? bpl + 1 : bpl;
                 int32_t mag = (int32_t)(((M >> qq) << 1 | 1) << qq);
-                bool ng = (WS[WS_NEG + y + 1] >> x) & 1;
+                bool ng = (WS[4 * (y & ~3u) + WS_N + (y & 3)] >> x) & 1;
                 v = ng ? -mag : mag;
             }
         }
