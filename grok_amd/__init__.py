@@ -14,7 +14,8 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgrok_amd.so")
+# GROK_AMD_LIB: another in-tree build of the library (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("GROK_AMD_LIB") or os.path.join(HERE, "libgrok_amd.so")
 
 GK_MAXRLVLS = 33
 GK_MAX_LAYERS = 100

@@ -6,22 +6,25 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgrok_amd.so")
-SOURCES = ["gk_kernels.hip", "gk_dwt97.hip", "gk_t1enc.hip", "gk_t1dec.hip", "gk_ht.hip", "gk_engine.cpp", "grk_shim.cpp"]
+# Grok's plugin loader opens <pluginPath>/libgrokj2k_plugin.so (grok.cpp:579-605)
+PLUGIN = os.path.join(HERE, "libgrokj2k_plugin.so")
+ENGINE = ["gk_kernels.hip", "gk_dwt97.hip", "gk_t1enc.hip", "gk_t1dec.hip", "gk_ht.hip", "gk_engine.cpp"]
+SOURCES = ENGINE + ["grk_shim.cpp", "grk_plugin.cpp"]
 
 
 def needs_build():
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(PLUGIN):
         return True
-    t = os.path.getmtime(LIB)
+    t = min(os.path.getmtime(LIB), os.path.getmtime(PLUGIN))
     deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + \
-        [os.path.join(HERE, "..", "include", f) for f in ("grok_amd.h", "grk_abi.h")]
+        [os.path.join(HERE, "..", "include", f) for f in ("grok_amd.h", "grk_abi.h", "grk_plugin_abi.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
 def build(force=False, verbose=False):
     if not force and not needs_build():
         return LIB
-    objs = []
+    objs = {}
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(CSRC, s.rsplit(".", 1)[0] + ".o")
@@ -29,10 +32,14 @@ def build(force=False, verbose=False):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
-        objs.append(obj)
-    cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB] + objs
-    subprocess.check_call(cmd)
-    for o in objs:
+        objs[s] = obj
+    engine = [objs[s] for s in ENGINE]
+    # the grk_* drop-in, and the T1 plugin a Grok host loads (its own copy of the engine: a
+    # host process already holds Grok's grk_* symbols)
+    for lib, extra in ((LIB, "grk_shim.cpp"), (PLUGIN, "grk_plugin.cpp")):
+        cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + engine + [objs[extra]]
+        subprocess.check_call(cmd)
+    for o in objs.values():
         os.remove(o)
     return LIB
 

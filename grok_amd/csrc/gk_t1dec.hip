@@ -62,12 +62,9 @@
 #define T1DEC_UNROLL 12   // decision steps per stripe-boundary test (C2 decoder: 1 -> 33.5 ms, 8 -> 26.4, 12 -> 25.8, 16 -> 26.3)
 #endif
 __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
-    // per-lane select through v_cndmask, as inline asm so the optimiser cannot turn a
-    // select tree over struct fields into a dynamically indexed (scratch) access
-    uint64_t m = __ballot(c);
-    uint32_t r;
-    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
-    return r;
+    // per-lane select; a plain ternary lets the compiler keep c as the compare's lane mask (an
+    // explicit ballot made it rebuild the mask from a 0/1 value: two extra instructions each)
+    return c ? a : b;
 }
 
 // Bytes at or past the block length read as 0xFF (the MQ decoder's end-of-data rule,

@@ -520,9 +520,11 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
                 }
                 if (rc) {
                     const int bpno = p == 0 ? (int)numbps - 1 : (int)numbps - 2 - (int)(p - 1) / 3;
-                    double wm = B.wmse * (double)(1 << bpno);
-                    wm *= wm * (double)pass_nmse[(size_t)b * GK_MAX_PASSES + p] / 8192.0;
-                    cum += wm;
+                    // Grok's roundings, one per operation (no fused multiply-add): the values feed
+                    // PCRD on the host and the plugin tree's distortionDecrease
+                    double wm = __dmul_rn(B.wmse, (double)(1 << bpno));
+                    wm = __dmul_rn(wm, __dmul_rn(wm, (double)pass_nmse[(size_t)b * GK_MAX_PASSES + p]) / 8192.0);
+                    cum = __dadd_rn(cum, wm);
                 }
                 P[p].dist = cum;
                 ++p;

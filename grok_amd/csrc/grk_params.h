@@ -1,0 +1,58 @@
+// grk_params.h — grk_cparameters (grok.h:466-590) -> gk_cparameters, shared by the grk_*
+// shim (grk_shim.cpp) and the T1 plugin (grk_plugin.cpp).
+//
+// Follows CodeStreamCompress::initCompress (CodeStreamCompress.cpp:150-610).  Features outside
+// the GPU path are refused with a reason, never approximated.
+#pragma once
+#include <cstdio>
+#include <string>
+
+#include "../../include/grk_abi.h"
+#include "../../include/grok_amd.h"
+
+inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters& p, std::string& why) {
+    char msg[256];
+    auto refuse = [&](const char* m) { why = m; return false; };
+    gk_set_default_params(&p);
+    if (g.numresolution < 1 || g.numresolution > GRK_J2K_MAXRLVLS) {
+        snprintf(msg, sizeof msg, "Invalid number of resolutions : %u not in range [1,%u]", g.numresolution,
+                 GRK_J2K_MAXRLVLS);
+        return refuse(msg);
+    }
+    if (g.prog_order != GRK_LRCP || g.numpocs) return refuse("only the LRCP progression is supported on this path");
+    if (g.roi_compno >= 0) return refuse("region of interest (RGN) is not supported on this path");
+    if (g.tx0 || g.ty0 || g.image_offset_x0 || g.image_offset_y0) return refuse("image/tile offsets are not supported");
+    if (g.enableTilePartGeneration) return refuse("multiple tile parts per tile are not supported");
+    // mct 255 = not set on the command line: grk_compress resolves it from the component count
+    // once the image is loaded (grk_compress.cpp:1977-1981), as the engine does (>= 3 -> RCT/ICT)
+    if (g.mct_data || (g.mct > 1 && g.mct != 255)) return refuse("Part-2 array MCT is not supported");
+    if (g.allocationByQuality && g.numlayers) return refuse("fixed-quality layers are not supported (use rates)");
+    if (g.num_comments) return refuse("custom COM markers are not supported (the default comment is written)");
+    if (g.csty & ~1u) return refuse("SOP/EPH markers are not supported");
+    const uint32_t sty = (g.isHT ? GRK_CBLKSTY_HT : 0) | g.cblk_sty;
+    if (sty != 0 && sty != GRK_CBLKSTY_HT) {
+        snprintf(msg, sizeof msg, "code-block style 0x%x is not supported on this path", sty);
+        return refuse(msg);
+    }
+    if ((g.rsiz & ~GRK_JPH_RSIZ_FLAG) != GRK_PROFILE_NONE) {
+        snprintf(msg, sizeof msg, "profile 0x%x is not supported", g.rsiz);
+        return refuse(msg);
+    }
+    p.numlayers = g.numlayers ? g.numlayers : 1;
+    for (uint32_t l = 0; l < p.numlayers && l < GRK_MAX_LAYERS; ++l) p.layer_rate[l] = g.numlayers ? g.layer_rate[l] : 0.0;
+    p.numresolution = g.numresolution;
+    p.cblockw_init = g.cblockw_init; p.cblockh_init = g.cblockh_init;
+    p.cblk_sty = (uint8_t)sty;
+    p.irreversible = g.irreversible ? 1 : 0;
+    p.mct = g.mct == 255 ? 1 : g.mct;
+    p.numgbits = g.numgbits;
+    p.csty = g.csty;
+    p.res_spec = g.res_spec;
+    for (int r = 0; r < GK_MAXRLVLS; ++r) { p.prcw_init[r] = g.prcw_init[r]; p.prch_init[r] = g.prch_init[r]; }
+    p.write_comment = 1;
+    p.tile_size_on = g.tile_size_on;
+    p.t_width = g.t_width; p.t_height = g.t_height;
+    p.writeTLM = g.writeTLM; p.writePLT = g.writePLT;
+    p.cod_format = jp2 ? 2 : 0;
+    return true;
+}

@@ -23,6 +23,7 @@
 
 #include "../../include/grk_abi.h"
 #include "../../include/grok_amd.h"
+#include "grk_params.h"
 
 namespace {
 
@@ -214,42 +215,12 @@ struct CodecObj : Obj {
 };
 CodecObj* codec_of(grk_codec* c) { return c ? dynamic_cast<CodecObj*>(obj_of(c)) : nullptr; }
 
-// grk_cparameters -> gk_cparameters (CodeStreamCompress::initCompress, CodeStreamCompress.cpp:
-// 150-610).  Features outside the GPU path are refused with a message, never approximated.
+// grk_cparameters -> gk_cparameters (grk_params.h); a refusal goes to the error callback
 bool to_gk(const grk_cparameters& g, GRK_CODEC_FORMAT fmt, gk_cparameters& p) {
-    gk_set_default_params(&p);
-    if (g.numresolution < 1 || g.numresolution > GRK_J2K_MAXRLVLS) {
-        error("Invalid number of resolutions : %u not in range [1,%u]", g.numresolution, GRK_J2K_MAXRLVLS);
-        return false;
-    }
-    if (g.prog_order != GRK_LRCP || g.numpocs) { error("only the LRCP progression is supported on this path"); return false; }
-    if (g.roi_compno >= 0) { error("region of interest (RGN) is not supported on this path"); return false; }
-    if (g.tx0 || g.ty0 || g.image_offset_x0 || g.image_offset_y0) { error("image/tile offsets are not supported"); return false; }
-    if (g.enableTilePartGeneration) { error("multiple tile parts per tile are not supported"); return false; }
-    if (g.mct_data || g.mct > 1) { error("Part-2 array MCT is not supported"); return false; }
-    if (g.allocationByQuality && g.numlayers) { error("fixed-quality layers are not supported (use rates)"); return false; }
-    if (g.num_comments) { error("custom COM markers are not supported (the default comment is written)"); return false; }
-    if (g.csty & ~1u) { error("SOP/EPH markers are not supported"); return false; }
-    const uint32_t sty = (g.isHT ? GRK_CBLKSTY_HT : 0) | g.cblk_sty;
-    if (sty != 0 && sty != GRK_CBLKSTY_HT) { error("code-block style 0x%x is not supported on this path", sty); return false; }
-    if ((g.rsiz & ~GRK_JPH_RSIZ_FLAG) != GRK_PROFILE_NONE) { error("profile 0x%x is not supported", g.rsiz); return false; }
-    p.numlayers = g.numlayers ? g.numlayers : 1;
-    for (uint32_t l = 0; l < p.numlayers && l < GRK_MAX_LAYERS; ++l) p.layer_rate[l] = g.numlayers ? g.layer_rate[l] : 0.0;
-    p.numresolution = g.numresolution;
-    p.cblockw_init = g.cblockw_init; p.cblockh_init = g.cblockh_init;
-    p.cblk_sty = (uint8_t)sty;
-    p.irreversible = g.irreversible ? 1 : 0;
-    p.mct = g.mct;
-    p.numgbits = g.numgbits;
-    p.csty = g.csty;
-    p.res_spec = g.res_spec;
-    for (int r = 0; r < GK_MAXRLVLS; ++r) { p.prcw_init[r] = g.prcw_init[r]; p.prch_init[r] = g.prch_init[r]; }
-    p.write_comment = 1;
-    p.tile_size_on = g.tile_size_on;
-    p.t_width = g.t_width; p.t_height = g.t_height;
-    p.writeTLM = g.writeTLM; p.writePLT = g.writePLT;
-    p.cod_format = fmt == GRK_CODEC_JP2 ? 2 : 0;
-    return true;
+    std::string why;
+    if (grk_params_to_gk(g, fmt == GRK_CODEC_JP2, p, why)) return true;
+    error("%s", why.c_str());
+    return false;
 }
 
 bool image_geometry(const grk_image* im, gk_image_info& info) {

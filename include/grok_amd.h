@@ -146,6 +146,44 @@ int gk_decode_window(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
                      uint32_t x1, uint32_t y1, void* const* comps, const uint32_t* strides, uint32_t sample_bytes,
                      int out_on_device);
 
+/* Code-block results of a single-tile encode, for Grok's T1 plugin interface (SURVEY.md
+ * §8(b) B2: grk_plugin_tile -> ... -> grk_plugin_code_block, grok.h:995-1077): what the host
+ * takes from the plugin in compress_synch_with_plugin (plugin/plugin_bridge.cpp:146-270).
+ * Order is canonical: component, resolution, band, precinct, code-block
+ * (T1CompressScheduler.cpp:31-94). */
+typedef struct gk_band_result {
+    uint32_t comp, res, band;   /* position in the tile tree */
+    uint32_t orient;            /* 0 LL, 1 HL, 2 LH, 3 HH (grk_plugin_band::orientation) */
+    uint32_t num_precincts;     /* grk_plugin_band::numPrecincts (precinct grid of the resolution) */
+    float stepsize;             /* the band's quantisation step (Subband::stepsize) */
+} gk_band_result;
+typedef struct gk_block_result {
+    uint32_t comp, res, band, precinct, cblk;   /* position; cblk = raster index in the precinct */
+    uint32_t x0, y0, x1, y1;                    /* code-block rectangle in band coordinates */
+    uint32_t numbps;                            /* Codeblock::numbps */
+    uint32_t npasses;                           /* CompressCodeblock::numPassesTotal */
+    uint32_t len;                               /* compressed bytes */
+    uint32_t pass_off;                          /* first pass record in the pass array */
+    uint64_t data_off;                          /* first byte in the byte array */
+} gk_block_result;
+typedef struct gk_pass_result {
+    uint32_t rate;     /* cumulative bytes after the pass (CodePass::rate, T1.cpp:856-930 rules) */
+    uint32_t len;      /* rate - previous rate (CodePass::len) */
+    double dist;       /* cumulative distortion decrease (CodePass::distortiondec); 0 unless the
+                          parameters ask for rate control (TileProcessor::needsRateControl) */
+} gk_pass_result;
+
+/* TileProcessor::doCompress up to and including T1 (TileProcessor.cpp:202-232: DC shift, MCT,
+ * DWT, t1_encode) of a single-tile image; the results stay in the context and *nbands,
+ * *nblocks, *nbytes, *npasses receive their counts.  Returns 0 / < 0 (error). */
+int gk_encode_blocks(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, const uint32_t* strides,
+                     int comps_on_device, const gk_cparameters* p, uint32_t* nbands, uint32_t* nblocks,
+                     uint64_t* nbytes, uint32_t* npasses);
+/* Copies the results of the last gk_encode_blocks into caller arrays of the reported sizes
+ * (any pointer may be NULL to skip that array). */
+int gk_encode_blocks_get(gk_ctx* ctx, gk_band_result* bands, gk_block_result* blocks, uint8_t* data,
+                         gk_pass_result* passes);
+
 /* Stage timings of the last gk_encode / gk_decode. */
 int gk_get_timings(gk_ctx* ctx, gk_timings* t);
 /* Last error message for this context (grk_set_error_handler equivalent). */

@@ -2014,6 +2014,28 @@ int orc_encode_blocks(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc
     return 0;
 }
 
+// Per-pass rates and cumulative distortion decreases of every code-block, concatenated in
+// the canonical order of orc_encode_blocks (CodePass::rate / distortiondec after
+// T1::compress_cblk's rate rules, T1.cpp:856-930).  rates / dists may be NULL (count only).
+int orc_encode_block_passes(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
+                            const orc_cparams* cp, uint32_t* rates, double* dists, uint64_t* npasses) {
+    EncodeState E;
+    prepare_encode(E, planes, w, h, nc, prec, sgnd, cp);
+    t1_encode_all(E);
+    uint64_t n = 0;
+    for (uint32_t c = 0; c < nc; ++c)
+        for (uint32_t r = 0; r < E.p.numres; ++r)
+            for (auto& B : E.comps[c].res[r].bands)
+                for (auto& P : B.prcs)
+                    for (auto& K : P.cblks)
+                        for (uint32_t q = 0; q < K.npasses; ++q, ++n) {
+                            if (rates) rates[n] = K.passes[q].rate;
+                            if (dists) dists[n] = K.passes[q].dist;
+                        }
+    *npasses = n;
+    return 0;
+}
+
 // Single code-block T1 encode from signed integer coefficients (reversible
 // convention: value << 6 to SMR).  Returns the byte length; pass rates in rates[].
 int orc_t1_encode_cblk(const int32_t* coef, uint32_t w, uint32_t h, uint32_t stride, uint32_t orient,

@@ -56,6 +56,9 @@ def lib():
         _lib.orc_encode_blocks.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_int, P(CParams), ctypes.c_void_p,
                                            P(ctypes.c_uint32), ctypes.c_void_p, P(ctypes.c_uint64)]
+        _lib.orc_encode_block_passes.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_int, P(CParams), ctypes.c_void_p,
+                                                 ctypes.c_void_p, P(ctypes.c_uint64)]
         _lib.orc_t1_encode_cblk.restype = ctypes.c_int
         _lib.orc_t1_encode_cblk.argtypes = [P(ctypes.c_int32)] + [ctypes.c_uint32] * 4 + [
             ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_uint32), P(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_void_p]
@@ -220,6 +223,22 @@ def encode_blocks(img, prec, signed=False, **kw):
     lib().orc_encode_blocks(ip, w, h, c, prec, int(signed), ctypes.byref(p), blocks, ctypes.byref(nb),
                             data.ctypes.data, ctypes.byref(nbytes))
     return blocks, data[:nbytes.value]
+
+
+def encode_block_passes(img, prec, signed=False, **kw):
+    """Pass rates (uint32) and cumulative distortion decreases (float64) of every code-block,
+    concatenated in encode_blocks order (each block contributes its npasses entries)."""
+    a = _planes(img)
+    c, h, w = a.shape
+    p = params(**kw)
+    n = ctypes.c_uint64()
+    ip = a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    lib().orc_encode_block_passes(ip, w, h, c, prec, int(signed), ctypes.byref(p), None, None, ctypes.byref(n))
+    rates = np.zeros(max(1, n.value), np.uint32)
+    dists = np.zeros(max(1, n.value), np.float64)
+    lib().orc_encode_block_passes(ip, w, h, c, prec, int(signed), ctypes.byref(p), rates.ctypes.data,
+                                  dists.ctypes.data, ctypes.byref(n))
+    return rates[:n.value], dists[:n.value]
 
 
 def t1_encode_cblk(coef, orient):
