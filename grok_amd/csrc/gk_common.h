@@ -66,4 +66,24 @@ struct GkTiles {
     __host__ __device__ uint64_t offset(uint32_t z, uint32_t stride) const {
         return (uint64_t)((j0 + z / nx) * dy - oy) * stride + (uint64_t)((i0 + z % nx) * dx - ox);
     }
+    // top-left of tile z in work-plane (region) coordinates
+    __host__ __device__ void origin(uint32_t z, int32_t& x, int32_t& y) const {
+        x = (int32_t)((i0 + z % nx) * dx - ox);
+        y = (int32_t)((j0 + z / nx) * dy - oy);
+    }
+};
+
+// Components of one level launch: component c's plane at base + c * cstride elements,
+// grid.z = component * tiles + tile.
+struct GkComps {
+    uint64_t cstride = 0;
+    uint32_t n = 1;
+};
+// Caller planes of up to three components (fused level-1 kernels).
+struct GkPtr3 {
+    const void* p[3] = {nullptr, nullptr, nullptr};
+};
+// Output window of a fused last inverse level, in work-plane (region) coordinates.
+struct GkWin {
+    int32_t x0 = 0, y0 = 0, x1 = 0, y1 = 0;
 };

@@ -110,20 +110,21 @@ __global__ __launch_bounds__(256) void k_dc_inv_f(const float* __restrict__ in, 
 
 // =============================================================================
 // Forward 9/7, one level (WaveletFwd.cpp:964-1025): vertical then horizontal.
+// Components in grid.z (GkComps); level 1 fused with DC + ICT (k_dwt97_fwd_l1) and the
+// last inverse level with the inverse ICT + DC + clamp (k_dwt97_inv_l1), as for the 5/3.
 // =============================================================================
-__global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict__ src, uint32_t sstride,
-                                                         float* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h, GkTiles tb) {
-    __shared__ float T[T97_LH][T97_LW + 1];
-    src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
-    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H;
-    const int tid = threadIdx.x;
+typedef float Lds97[T97_LH][T97_LW + 1];
+
+// f(ly, lx, gy, gx): the sample at mirrored input position (gy, gx) into LDS (ly, lx)
+template <class F>
+__device__ __forceinline__ void fwd97_fill(int x0, int y0, int w, int h, int tid, F f) {
     for (int i = tid; i < T97_LH * T97_LW; i += 256) {
-        int ly = i / T97_LW, lx = i % T97_LW;
-        int gy = mirror97(y0 - T97_HALO + ly, (int)h), gx = mirror97(x0 - T97_HALO + lx, (int)w);
-        T[ly][lx] = src[(size_t)gy * sstride + gx];
+        const int ly = i / T97_LW, lx = i % T97_LW;
+        f(ly, lx, mirror97(y0 - T97_HALO + ly, h), mirror97(x0 - T97_HALO + lx, w));
     }
-    __syncthreads();
+}
+
+__device__ __forceinline__ void fwd97_lift(Lds97& T, int w, int h, int tid) {
     // local row ly <-> global y0 - 4 + ly; parity of global y == parity of ly (y0 even)
     if (h > 1) {
         const float cs[4] = {F97_A, F97_B, F97_G, F97_D};
@@ -167,12 +168,16 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict
         }
         __syncthreads();
     }
+}
+
+__device__ __forceinline__ void fwd97_store(const Lds97& T, float* __restrict__ dst, uint32_t dstride, int x0, int y0,
+                                            int w, int h, int tid) {
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
     for (int i = tid; i < T97_H * T97_W; i += 256) {
         int ry = i / T97_W, rx = i % T97_W;
         int q = rx / (T97_W / 2), k = rx % (T97_W / 2);
         int gx = x0 + 2 * k + q, gy = y0 + ry;
-        if (gx >= (int)w || gy >= (int)h) continue;
+        if (gx >= w || gy >= h) continue;
         float v = T[ry + T97_HALO][2 * k + q + T97_HALO];
         int ox = (q == 0) ? (gx >> 1) : (snw + (gx >> 1));
         int oy = ((gy & 1) == 0) ? (gy >> 1) : (snh + (gy >> 1));
@@ -180,26 +185,97 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict
     }
 }
 
+__global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict__ src, uint32_t sstride,
+                                                         float* __restrict__ dst, uint32_t dstride, uint32_t w,
+                                                         uint32_t h, GkTiles tb, GkComps cs) {
+    __shared__ Lds97 T;
+    const uint32_t tile = blockIdx.z % tb.count(), comp = blockIdx.z / tb.count();
+    src += tb.offset(tile, sstride) + comp * cs.cstride;
+    dst += tb.offset(tile, dstride) + comp * cs.cstride;
+    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H, tid = threadIdx.x;
+    fwd97_fill(x0, y0, (int)w, (int)h, tid,
+               [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; });
+    __syncthreads();
+    fwd97_lift(T, (int)w, (int)h, tid);
+    fwd97_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
+}
+
+// Level 1 from the caller's planes: DC shift and, for NC = 3, the ICT (mct.cpp:147-219) on load.
+// One LDS tile: Y goes first while each thread keeps U and V of its positions in registers
+// (22 slots = ceil(40 x 136 / 256)), then U, then V (as k_dwt53_fwd_l1).
+#define L97_SLOTS 22
+template <class F>   // f(slot, ly, lx, gy, gx) over fwd97_fill's positions
+__device__ __forceinline__ void fwd97_fill_slots(int x0, int y0, int w, int h, int tid, F f) {
+#pragma unroll
+    for (int k = 0; k < L97_SLOTS; ++k) {
+        const int i = tid + 256 * k;
+        if (i < T97_LH * T97_LW) {
+            const int ly = i / T97_LW, lx = i % T97_LW;
+            f(k, ly, lx, mirror97(y0 - T97_HALO + ly, h), mirror97(x0 - T97_HALO + lx, w));
+        }
+    }
+}
+
+template <class TI, int NC>
+__global__ __launch_bounds__(256) void k_dwt97_fwd_l1(GkPtr3 in, uint32_t sin, float* __restrict__ dst, uint64_t cstride,
+                                                      uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb,
+                                                      int32_t shift) {
+    __shared__ Lds97 T;
+    const uint32_t tile = blockIdx.z;
+    const uint64_t io = tb.offset(tile, sin);
+    const TI* p0 = (const TI*)in.p[0] + io;
+    const TI* p1 = (const TI*)in.p[NC == 3 ? 1 : 0] + io;
+    const TI* p2 = (const TI*)in.p[NC == 3 ? 2 : 0] + io;
+    dst += tb.offset(tile, dstride);
+    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H, tid = threadIdx.x;
+    float U[L97_SLOTS], V[L97_SLOTS];
+    fwd97_fill_slots(x0, y0, (int)w, (int)h, tid, [&](int k, int ly, int lx, int gy, int gx) {
+        const size_t i = (size_t)gy * sin + gx;
+        if (NC == 3) {
+            const float a_r = 0.299f, a_g = 0.587f, a_b = 0.114f;
+            const float cb = 0.5f / (1.0f - a_b), cr = 0.5f / (1.0f - a_r);
+            const float r = (float)((int32_t)p0[i] - shift), g = (float)((int32_t)p1[i] - shift),
+                        b = (float)((int32_t)p2[i] - shift);
+            const float t0 = a_r * r, t1 = a_g * g, t2 = a_b * b;
+            const float Y = (t0 + t1) + t2;
+            T[ly][lx] = Y;
+            U[k] = cb * (b - Y);
+            V[k] = cr * (r - Y);
+        } else {
+            T[ly][lx] = (float)((int32_t)p0[i] - shift);
+        }
+    });
+    __syncthreads();
+    fwd97_lift(T, (int)w, (int)h, tid);
+    fwd97_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
+    if (NC == 3) {
+#pragma unroll
+        for (int c = 1; c < 3; ++c) {
+            __syncthreads();
+            fwd97_fill_slots(x0, y0, (int)w, (int)h, tid,
+                             [&](int k, int ly, int lx, int, int) { T[ly][lx] = c == 1 ? U[k] : V[k]; });
+            __syncthreads();
+            fwd97_lift(T, (int)w, (int)h, tid);
+            fwd97_store(T, dst + c * cstride, dstride, x0, y0, (int)w, (int)h, tid);
+        }
+    }
+}
+
 // =============================================================================
 // Inverse 9/7, one level (WaveletReverse.cpp:1010-1022, 1272-1351):
 // horizontal then vertical, on the interleaved signal.
 // =============================================================================
-__global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict__ src, uint32_t sstride,
-                                                         float* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h, GkTiles tb) {
-    __shared__ float T[T97_LH][T97_LW + 1];
-    src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
-    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H;
-    const int tid = threadIdx.x;
+template <class F>
+__device__ __forceinline__ void inv97_fill(int x0, int y0, int w, int h, int tid, F f) {
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
     for (int i = tid; i < T97_LH * T97_LW; i += 256) {
         int ly = i / T97_LW, lx = i % T97_LW;
-        int gy = mirror97(y0 - T97_HALO + ly, (int)h), gx = mirror97(x0 - T97_HALO + lx, (int)w);
-        int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
-        int sx = (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1);
-        T[ly][lx] = src[(size_t)sy * sstride + sx];
+        int gy = mirror97(y0 - T97_HALO + ly, h), gx = mirror97(x0 - T97_HALO + lx, w);
+        f(ly, lx, (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1), (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1));
     }
-    __syncthreads();
+}
+
+__device__ __forceinline__ void inv97_lift(Lds97& T, int w, int h, int tid) {
     const float cs[4] = {I97_D, I97_G, I97_B, I97_A};
     if (w > 1) {
         for (int i = tid; i < T97_LH * T97_LW; i += 256) {
@@ -241,11 +317,79 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict
             __syncthreads();
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict__ src, uint32_t sstride,
+                                                         float* __restrict__ dst, uint32_t dstride, uint32_t w,
+                                                         uint32_t h, GkTiles tb, GkComps cs) {
+    __shared__ Lds97 T;
+    const uint32_t tile = blockIdx.z % tb.count(), comp = blockIdx.z / tb.count();
+    src += tb.offset(tile, sstride) + comp * cs.cstride;
+    dst += tb.offset(tile, dstride) + comp * cs.cstride;
+    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H, tid = threadIdx.x;
+    inv97_fill(x0, y0, (int)w, (int)h, tid,
+               [&](int ly, int lx, int sy, int sx) { T[ly][lx] = src[(size_t)sy * sstride + sx]; });
+    __syncthreads();
+    inv97_lift(T, (int)w, (int)h, tid);
     for (int i = tid; i < T97_H * T97_W; i += 256) {
         int ry = i / T97_W, rx = i % T97_W;
         int gx = x0 + rx, gy = y0 + ry;
         if (gx >= (int)w || gy >= (int)h) continue;
         dst[(size_t)gy * dstride + gx] = T[ry + T97_HALO][rx + T97_HALO];
+    }
+}
+
+// Last inverse level into the caller's planes: inverse ICT for NC = 3 (mct.cpp:284-364,
+// lrintf rounding), DC shift and clamp, only inside the output window (GkWin).  One LDS
+// tile; the Y and U results of each thread's 16 output samples wait in registers.
+template <class TO, int NC>
+__global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ src, uint64_t cstride, uint32_t sstride,
+                                                      GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h,
+                                                      GkTiles tb, int32_t shift, int32_t mn, int32_t mx) {
+    __shared__ Lds97 T;
+    const uint32_t tile = blockIdx.z;
+    src += tb.offset(tile, sstride);
+    int32_t ox, oy;
+    tb.origin(tile, ox, oy);
+    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H, tid = threadIdx.x;
+    float R0[16], R1[16];   // sample i = tid + 256 k of the 32 x 128 output tile
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (c) __syncthreads();
+        const float* sc = src + c * cstride;
+        inv97_fill(x0, y0, (int)w, (int)h, tid,
+                   [&](int ly, int lx, int sy, int sx) { T[ly][lx] = sc[(size_t)sy * sstride + sx]; });
+        __syncthreads();
+        inv97_lift(T, (int)w, (int)h, tid);
+        if (c + 1 < NC) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int i = tid + 256 * k;
+                (c == 0 ? R0 : R1)[k] = T[i / T97_W + T97_HALO][i % T97_W + T97_HALO];
+            }
+        }
+    }
+    TO* o0 = (TO*)out.p[0];
+    TO* o1 = (TO*)out.p[NC == 3 ? 1 : 0];
+    TO* o2 = (TO*)out.p[NC == 3 ? 2 : 0];
+    auto cl = [&](float f) { int32_t v = (int32_t)rintf(f) + shift; return (TO)(v < mn ? mn : (v > mx ? mx : v)); };
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int i = tid + 256 * k;
+        const int ry = i / T97_W, rx = i % T97_W;
+        const int gx = x0 + rx, gy = y0 + ry, X = ox + gx, Y = oy + gy;
+        if (gx >= (int)w || gy >= (int)h || X < win.x0 || X >= win.x1 || Y < win.y0 || Y >= win.y1) continue;
+        const size_t o = (size_t)(Y - win.y0) * ostride + (X - win.x0);
+        const float last = T[ry + T97_HALO][rx + T97_HALO];
+        if (NC == 3) {
+            const float Yv = R0[k], U = R1[k], V = last;
+            const float R = Yv + 1.402f * V;
+            const float G = (Yv - 0.34413f * U) - 0.71414f * V;
+            const float B = Yv + 1.772f * U;
+            o0[o] = cl(R); o1[o] = cl(G); o2[o] = cl(B);
+        } else {
+            o0[o] = cl(last);
+        }
     }
 }
 
@@ -276,13 +420,45 @@ void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int stype
         hipLaunchKernelGGL(k_dc_inv_f<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, in, sin, (T*)out, sout, w, h, shift,
                            mn, mx))
 }
+static uint32_t comps_in_grid97(GkTiles tb, GkComps cs) { return tb.count() * cs.n <= 65535u ? cs.n : 1u; }
 void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h, GkTiles tb) {
-    dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
-    hipLaunchKernelGGL(k_dwt97_fwd_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h, tb);
+                         uint32_t h, GkTiles tb, GkComps cs) {
+    const uint32_t ng = comps_in_grid97(tb, cs);
+    for (uint32_t c = 0; c < cs.n; c += ng) {
+        GkComps g = cs; g.n = ng;
+        dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count() * ng);
+        hipLaunchKernelGGL(k_dwt97_fwd_level, grid, dim3(256), 0, st, src + c * cs.cstride, sstride, dst + c * cs.cstride,
+                           dstride, w, h, tb, g);
+    }
 }
 void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h, GkTiles tb) {
+                         uint32_t h, GkTiles tb, GkComps cs) {
+    const uint32_t ng = comps_in_grid97(tb, cs);
+    for (uint32_t c = 0; c < cs.n; c += ng) {
+        GkComps g = cs; g.n = ng;
+        dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count() * ng);
+        hipLaunchKernelGGL(k_dwt97_inv_level, grid, dim3(256), 0, st, src + c * cs.cstride, sstride, dst + c * cs.cstride,
+                           dstride, w, h, tb, g);
+    }
+}
+void gk_launch_dwt97_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32_t sin, float* dst, uint64_t cstride,
+                            uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb, int32_t shift) {
     dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
-    hipLaunchKernelGGL(k_dwt97_inv_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h, tb);
+    if (nc == 3)
+        GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_fwd_l1<T, 3>), grid, dim3(256), 0, st, in, sin, dst,
+                                                        cstride, dstride, w, h, tb, shift))
+    else
+        GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_fwd_l1<T, 1>), grid, dim3(256), 0, st, in, sin, dst,
+                                                        cstride, dstride, w, h, tb, shift))
+}
+void gk_launch_dwt97_inv_l1(hipStream_t st, int stype, int nc, const float* src, uint64_t cstride, uint32_t sstride,
+                            GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
+                            int32_t mn, int32_t mx) {
+    dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
+    if (nc == 3)
+        GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_inv_l1<T, 3>), grid, dim3(256), 0, st, src, cstride,
+                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx))
+    else
+        GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_inv_l1<T, 1>), grid, dim3(256), 0, st, src, cstride,
+                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx))
 }

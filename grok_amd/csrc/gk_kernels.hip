@@ -130,11 +130,17 @@ __global__ __launch_bounds__(256) void k_dc_inv(const int32_t* __restrict__ in, 
 // on a (TH+3) x (TW+3) LDS tile (2-sample halo before, 1 after, whole-sample
 // symmetric extension at the resolution border), outputs written straight into
 // the four Mallat quadrants.  Parity 0 (resolution origin even).
+// Components run in grid.z (z = component * tiles + tile, GkComps).  Level 1 is
+// fused with the sample stage: the forward kernel reads the caller's planes with
+// the DC shift and RCT applied on load (k_dwt53_fwd_l1), the inverse kernel writes
+// them through the inverse RCT, DC shift and clamp (k_dwt53_inv_l1), so the image
+// never makes a separate pass through HBM.
 // =============================================================================
 #define DWT_TW 128
 #define DWT_TH 32
 #define DWT_LW (DWT_TW + 3)
 #define DWT_LH (DWT_TH + 3)
+typedef int32_t Lds53[DWT_LH][DWT_LW + 1];
 
 __device__ __forceinline__ int mirror(int i, int n) {
     if (n == 1) return 0;
@@ -145,36 +151,34 @@ __device__ __forceinline__ int mirror(int i, int n) {
     return i;
 }
 
-__global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restrict__ src, uint32_t sstride,
-                                                         int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h, GkTiles tb) {
-    __shared__ int32_t T[DWT_LH][DWT_LW + 1];
-    src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
-    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH;
-    const int tid = threadIdx.x;
-    // 4 waves x 64 lanes: lane tx walks columns tx, tx+64, tx+128 of rows ty, ty+4, ... (no
-    // index division: the level is bound by instruction count before HBM)
+// Visit the forward tile's input positions: rows y0-2 .. y0+TH, cols x0-2 .. x0+TW,
+// f(ly, lx, gy, gx) with (gy, gx) mirrored at the resolution border.  4 waves x 64 lanes:
+// lane tx walks columns tx, tx+64 of rows ty, ty+4, ..., the halo columns 128..130 as
+// one extra pass (no index division on the interior path).
+template <class F>
+__device__ __forceinline__ void fwd53_fill(int x0, int y0, int w, int h, int tid, F f) {
     const int tx = tid & 63, ty = tid >> 6;
-    // load rows y0-2 .. y0+TH, cols x0-2 .. x0+TW (mirrored at the resolution border)
-    if (x0 >= 2 && y0 >= 2 && x0 + DWT_TW < (int)w && y0 + DWT_TH < (int)h) {   // interior tile
-        const int32_t* s0 = src + (size_t)(y0 - 2) * sstride + (x0 - 2);
+    if (x0 >= 2 && y0 >= 2 && x0 + DWT_TW < w && y0 + DWT_TH < h) {   // interior tile
         for (int ly = ty; ly < DWT_LH; ly += 4) {
-            const int32_t* sr = s0 + (size_t)ly * sstride;
-            T[ly][tx] = sr[tx];
-            T[ly][tx + 64] = sr[tx + 64];
+            const int gy = y0 - 2 + ly;
+            f(ly, tx, gy, x0 - 2 + tx);
+            f(ly, tx + 64, gy, x0 + 62 + tx);
         }
         for (int i = tid; i < 3 * DWT_LH; i += 256) {   // columns 128..130
             const int ly = i / 3, lx = 128 + i % 3;
-            T[ly][lx] = s0[(size_t)ly * sstride + lx];
+            f(ly, lx, y0 - 2 + ly, x0 - 2 + lx);
         }
     } else {
         for (int i = tid; i < DWT_LH * DWT_LW; i += 256) {
-            int ly = i / DWT_LW, lx = i % DWT_LW;
-            int gy = mirror(y0 - 2 + ly, (int)h), gx = mirror(x0 - 2 + lx, (int)w);
-            T[ly][lx] = src[(size_t)gy * sstride + gx];
+            const int ly = i / DWT_LW, lx = i % DWT_LW;
+            f(ly, lx, mirror(y0 - 2 + ly, h), mirror(x0 - 2 + lx, w));
         }
     }
-    LDS_BARRIER();
+}
+
+// Forward lifting of one loaded tile (barriers inside: every thread of the block calls it).
+__device__ __forceinline__ void fwd53_lift(Lds53& T, int w, int h, int tid) {
+    const int tx = tid & 63, ty = tid >> 6;
     if (h > 1) {
         // vertical predict: odd absolute rows y in [y0-1, y0+TH-1]  (local ly = y - y0 + 2, odd y <=> ly odd)
         // (columns 0..127 by every lane, the halo columns 128..130 as one extra pass: a loop
@@ -216,17 +220,112 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
         }
         LDS_BARRIER();
     }
-    // scatter to quadrants: lane tx writes L and H sample k = tx of each row (coalesced rows)
+}
+
+// scatter to quadrants: lane tx writes L and H sample k = tx of each row (coalesced rows)
+__device__ __forceinline__ void fwd53_store(const Lds53& T, int32_t* __restrict__ dst, uint32_t dstride, int x0, int y0,
+                                            int w, int h, int tid) {
+    const int tx = tid & 63, ty = tid >> 6;
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
-    const bool full = x0 + DWT_TW <= (int)w && y0 + DWT_TH <= (int)h;
+    const bool full = x0 + DWT_TW <= w && y0 + DWT_TH <= h;
     for (int ry = ty; ry < DWT_TH; ry += 4) {
         const int gy = y0 + ry;
-        if (!full && gy >= (int)h) break;
+        if (!full && gy >= h) break;
         const int oy = ((gy & 1) == 0) ? (gy >> 1) : (snh + (gy >> 1));
         int32_t* drow = dst + (size_t)oy * dstride;
         const int gxl = x0 + 2 * tx;
-        if (full || gxl < (int)w) drow[gxl >> 1] = T[ry + 2][2 + 2 * tx];
-        if (full || gxl + 1 < (int)w) drow[snw + (gxl >> 1)] = T[ry + 2][3 + 2 * tx];
+        if (full || gxl < w) drow[gxl >> 1] = T[ry + 2][2 + 2 * tx];
+        if (full || gxl + 1 < w) drow[snw + (gxl >> 1)] = T[ry + 2][3 + 2 * tx];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restrict__ src, uint32_t sstride,
+                                                         int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
+                                                         uint32_t h, GkTiles tb, GkComps cs) {
+    __shared__ Lds53 T;
+    const uint32_t tile = blockIdx.z % tb.count(), comp = blockIdx.z / tb.count();
+    src += tb.offset(tile, sstride) + comp * cs.cstride;
+    dst += tb.offset(tile, dstride) + comp * cs.cstride;
+    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
+    fwd53_fill(x0, y0, (int)w, (int)h, tid,
+               [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; });
+    LDS_BARRIER();
+    fwd53_lift(T, (int)w, (int)h, tid);
+    fwd53_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
+}
+
+// Level 1 from the caller's planes: DC shift (TileProcessor.cpp:506-535) and, for NC = 3,
+// the RCT (mct.cpp:99-146) on load; outputs into the level-1 planes of the NC components
+// (dst + c * cstride).  One LDS tile: Y is transformed first while each thread keeps the U
+// and V of its input positions in registers (19 slots), then U, then V go through the same
+// tile, so a workgroup needs 18 KB of LDS, not 55 (occupancy).
+#define L1_SLOTS 19
+template <class F>   // f(slot, ly, lx, gy, gx): the positions of fwd53_fill, slot = compile-time index
+__device__ __forceinline__ void fwd53_fill_slots(int x0, int y0, int w, int h, int tid, F f) {
+    const int tx = tid & 63, ty = tid >> 6;
+    if (x0 >= 2 && y0 >= 2 && x0 + DWT_TW < w && y0 + DWT_TH < h) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int ly = ty + 4 * k;
+            if (ly < DWT_LH) {
+                const int gy = y0 - 2 + ly;
+                f(2 * k, ly, tx, gy, x0 - 2 + tx);
+                f(2 * k + 1, ly, tx + 64, gy, x0 + 62 + tx);
+            }
+        }
+        if (tid < 3 * DWT_LH) {
+            const int ly = tid / 3, lx = 128 + tid % 3;
+            f(18, ly, lx, y0 - 2 + ly, x0 - 2 + lx);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 18; ++k) {   // 18 x 256 >= 35 x 131
+            const int i = tid + 256 * k;
+            if (i < DWT_LH * DWT_LW) {
+                const int ly = i / DWT_LW, lx = i % DWT_LW;
+                f(k, ly, lx, mirror(y0 - 2 + ly, h), mirror(x0 - 2 + lx, w));
+            }
+        }
+    }
+}
+
+template <class TI, int NC>
+__global__ __launch_bounds__(256) void k_dwt53_fwd_l1(GkPtr3 in, uint32_t sin, int32_t* __restrict__ dst,
+                                                      uint64_t cstride, uint32_t dstride, uint32_t w, uint32_t h,
+                                                      GkTiles tb, int32_t shift) {
+    __shared__ Lds53 T;
+    const uint32_t tile = blockIdx.z;
+    const uint64_t io = tb.offset(tile, sin);
+    const TI* p0 = (const TI*)in.p[0] + io;
+    const TI* p1 = (const TI*)in.p[NC == 3 ? 1 : 0] + io;
+    const TI* p2 = (const TI*)in.p[NC == 3 ? 2 : 0] + io;
+    dst += tb.offset(tile, dstride);
+    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
+    int32_t U[L1_SLOTS], V[L1_SLOTS];
+    fwd53_fill_slots(x0, y0, (int)w, (int)h, tid, [&](int k, int ly, int lx, int gy, int gx) {
+        const size_t i = (size_t)gy * sin + gx;
+        if (NC == 3) {
+            const int32_t r = (int32_t)p0[i] - shift, g = (int32_t)p1[i] - shift, b = (int32_t)p2[i] - shift;
+            T[ly][lx] = (r + 2 * g + b) >> 2;
+            U[k] = b - g;
+            V[k] = r - g;
+        } else {
+            T[ly][lx] = (int32_t)p0[i] - shift;
+        }
+    });
+    LDS_BARRIER();
+    fwd53_lift(T, (int)w, (int)h, tid);
+    fwd53_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
+    if (NC == 3) {
+#pragma unroll
+        for (int c = 1; c < 3; ++c) {
+            LDS_BARRIER();   // the previous component's stores have read the tile
+            fwd53_fill_slots(x0, y0, (int)w, (int)h, tid,
+                             [&](int k, int ly, int lx, int, int) { T[ly][lx] = c == 1 ? U[k] : V[k]; });
+            LDS_BARRIER();
+            fwd53_lift(T, (int)w, (int)h, tid);
+            fwd53_store(T, dst + c * cstride, dstride, x0, y0, (int)w, (int)h, tid);
+        }
     }
 }
 
@@ -235,41 +334,38 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
 // y0..y0+TH-1; needs interleaved rows y0-1..y0+TH+1 and cols x0-1..x0+TW+1.
 #define IDWT_LW (DWT_TW + 3)
 #define IDWT_LH (DWT_TH + 3)
-__global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restrict__ src, uint32_t sstride,
-                                                         int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h, GkTiles tb) {
-    __shared__ int32_t T[IDWT_LH][IDWT_LW + 1];
-    src += tb.offset(blockIdx.z, sstride); dst += tb.offset(blockIdx.z, dstride);
-    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH;
-    const int tid = threadIdx.x;
-    const int tx = tid & 63, ty = tid >> 6;   // as in the forward level
+
+// Visit the inverse tile's input: interleaved position (ly, lx) = (y0-1+ly, x0-1+lx) comes
+// from Mallat position (sy, sx): f(ly, lx, sy, sx).
+template <class F>
+__device__ __forceinline__ void inv53_fill(int x0, int y0, int w, int h, int tid, F f) {
+    const int tx = tid & 63, ty = tid >> 6;
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
-    if (x0 >= 1 && y0 >= 1 && x0 + DWT_TW + 1 < (int)w && y0 + DWT_TH + 1 < (int)h) {   // interior tile
+    if (x0 >= 1 && y0 >= 1 && x0 + DWT_TW + 1 < w && y0 + DWT_TH + 1 < h) {   // interior tile
         // interleaved column gx = x0 - 1 + lx: odd lx <=> even gx (L sample x0/2 + k, lx = 1 + 2k),
         // even lx <=> odd gx (H sample x0/2 - 1 + k, lx = 2k); both reads are contiguous
         for (int ly = ty; ly < IDWT_LH; ly += 4) {
             const int gy = y0 - 1 + ly;
             const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
-            const int32_t* sr = src + (size_t)sy * sstride;
-            T[ly][1 + 2 * tx] = sr[(x0 >> 1) + tx];
-            T[ly][2 * tx] = sr[snw + (x0 >> 1) - 1 + tx];
+            f(ly, 1 + 2 * tx, sy, (x0 >> 1) + tx);
+            f(ly, 2 * tx, sy, snw + (x0 >> 1) - 1 + tx);
         }
         for (int i = tid; i < 3 * IDWT_LH; i += 256) {   // lx 128 (H), 129 (L), 130 (H)
             const int ly = i / 3, j = i % 3, gy = y0 - 1 + ly;
             const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
-            const int32_t* sr = src + (size_t)sy * sstride;
-            T[ly][128 + j] = (j == 1) ? sr[(x0 >> 1) + 64] : sr[snw + (x0 >> 1) + 63 + (j >> 1)];
+            f(ly, 128 + j, sy, (j == 1) ? (x0 >> 1) + 64 : snw + (x0 >> 1) + 63 + (j >> 1));
         }
     } else {
         for (int i = tid; i < IDWT_LH * IDWT_LW; i += 256) {
-            int ly = i / IDWT_LW, lx = i % IDWT_LW;
-            int gy = mirror(y0 - 1 + ly, (int)h), gx = mirror(x0 - 1 + lx, (int)w);
-            int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
-            int sx = (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1);
-            T[ly][lx] = src[(size_t)sy * sstride + sx];
+            const int ly = i / IDWT_LW, lx = i % IDWT_LW;
+            const int gy = mirror(y0 - 1 + ly, h), gx = mirror(x0 - 1 + lx, w);
+            f(ly, lx, (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1), (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1));
         }
     }
-    LDS_BARRIER();
+}
+
+__device__ __forceinline__ void inv53_lift(Lds53& T, int w, int h, int tid) {
+    const int tx = tid & 63, ty = tid >> 6;
     if (w > 1) {
         // horizontal step 1: even interleaved cols x (lx = x - x0 + 1): x even <=> lx odd, lx in [1, TW+1]
         for (int ly = ty; ly < IDWT_LH; ly += 4) {
@@ -300,6 +396,21 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
         }
         LDS_BARRIER();
     }
+}
+
+__global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restrict__ src, uint32_t sstride,
+                                                         int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
+                                                         uint32_t h, GkTiles tb, GkComps cs) {
+    __shared__ Lds53 T;
+    const uint32_t tile = blockIdx.z % tb.count(), comp = blockIdx.z / tb.count();
+    src += tb.offset(tile, sstride) + comp * cs.cstride;
+    dst += tb.offset(tile, dstride) + comp * cs.cstride;
+    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
+    const int tx = tid & 63, ty = tid >> 6;
+    inv53_fill(x0, y0, (int)w, (int)h, tid,
+               [&](int ly, int lx, int sy, int sx) { T[ly][lx] = src[(size_t)sy * sstride + sx]; });
+    LDS_BARRIER();
+    inv53_lift(T, (int)w, (int)h, tid);
     const bool full = x0 + DWT_TW <= (int)w && y0 + DWT_TH <= (int)h;
     for (int ry = ty; ry < DWT_TH; ry += 4) {
         const int gy = y0 + ry;
@@ -307,6 +418,58 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
         int32_t* drow = dst + (size_t)gy * dstride + x0;
         for (int c = tx; c < DWT_TW; c += 64)
             if (full || x0 + c < (int)w) drow[c] = T[ry + 1][c + 1];
+    }
+}
+
+// Last inverse level into the caller's planes: inverse RCT for NC = 3 (mct.cpp:221-283),
+// DC shift and clamp (TileProcessor.cpp:457-504), samples of type TO, only inside the
+// output window (region coordinates [wx0, wx1) x [wy0, wy1); out.p[c] addresses (wx0, wy0)).
+// One LDS tile: the Y and U results of each thread's 16 output samples wait in registers
+// while the next component goes through the tile.
+template <class TO, int NC>
+__global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict__ src, uint64_t cstride, uint32_t sstride,
+                                                      GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h,
+                                                      GkTiles tb, int32_t shift, int32_t mn, int32_t mx) {
+    __shared__ Lds53 T;
+    const uint32_t tile = blockIdx.z;
+    src += tb.offset(tile, sstride);
+    int32_t ox, oy;
+    tb.origin(tile, ox, oy);
+    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
+    const int tx = tid & 63, ty = tid >> 6;
+    int32_t R0[16], R1[16];   // this thread's samples (ry = ty + 4 (k >> 1), column tx + 64 (k & 1))
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (c) LDS_BARRIER();   // the previous component's samples have been read
+        const int32_t* sc = src + c * cstride;
+        inv53_fill(x0, y0, (int)w, (int)h, tid,
+                   [&](int ly, int lx, int sy, int sx) { T[ly][lx] = sc[(size_t)sy * sstride + sx]; });
+        LDS_BARRIER();
+        inv53_lift(T, (int)w, (int)h, tid);
+        if (c + 1 < NC) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) (c == 0 ? R0 : R1)[k] = T[ty + 4 * (k >> 1) + 1][tx + 64 * (k & 1) + 1];
+        }
+    }
+    TO* o0 = (TO*)out.p[0];
+    TO* o1 = (TO*)out.p[NC == 3 ? 1 : 0];
+    TO* o2 = (TO*)out.p[NC == 3 ? 2 : 0];
+    auto cl = [&](int32_t v) { return (TO)(v < mn ? mn : (v > mx ? mx : v)); };
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int ry = ty + 4 * (k >> 1), cx = tx + 64 * (k & 1);
+        const int gy = y0 + ry, Y = oy + gy, gx = x0 + cx, X = ox + gx;
+        if (gy >= (int)h || gx >= (int)w || Y < win.y0 || Y >= win.y1 || X < win.x0 || X >= win.x1) continue;
+        const size_t o = (size_t)(Y - win.y0) * ostride + (X - win.x0);
+        const int32_t last = T[ry + 1][cx + 1];
+        if (NC == 3) {
+            const int32_t G = R0[k] - ((R1[k] + last) >> 2);
+            o0[o] = cl(last + G + shift);
+            o1[o] = cl(G + shift);
+            o2[o] = cl(R1[k] + G + shift);
+        } else {
+            o0[o] = cl(last + shift);
+        }
     }
 }
 
@@ -365,15 +528,47 @@ void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int stype
     GK_SAMPLE_DISPATCH(stype, T,
         hipLaunchKernelGGL(k_dc_inv<T>, grid, dim3(256), 0, st, in, sin, (T*)out, sout, w, h, shift, mn, mx))
 }
+static uint32_t comps_in_grid(GkTiles tb, GkComps cs) { return tb.count() * cs.n <= 65535u ? cs.n : 1u; }
 void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h, GkTiles tb) {
-    dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
-    hipLaunchKernelGGL(k_dwt53_fwd_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h, tb);
+                         uint32_t h, GkTiles tb, GkComps cs) {
+    const uint32_t ng = comps_in_grid(tb, cs);   // components per launch
+    for (uint32_t c = 0; c < cs.n; c += ng) {
+        GkComps g = cs; g.n = ng;
+        dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count() * ng);
+        hipLaunchKernelGGL(k_dwt53_fwd_level, grid, dim3(256), 0, st, src + c * cs.cstride, sstride, dst + c * cs.cstride,
+                           dstride, w, h, tb, g);
+    }
 }
 void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h, GkTiles tb) {
+                         uint32_t h, GkTiles tb, GkComps cs) {
+    const uint32_t ng = comps_in_grid(tb, cs);
+    for (uint32_t c = 0; c < cs.n; c += ng) {
+        GkComps g = cs; g.n = ng;
+        dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count() * ng);
+        hipLaunchKernelGGL(k_dwt53_inv_level, grid, dim3(256), 0, st, src + c * cs.cstride, sstride, dst + c * cs.cstride,
+                           dstride, w, h, tb, g);
+    }
+}
+void gk_launch_dwt53_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32_t sin, int32_t* dst, uint64_t cstride,
+                            uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb, int32_t shift) {
     dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
-    hipLaunchKernelGGL(k_dwt53_inv_level, grid, dim3(256), 0, st, src, sstride, dst, dstride, w, h, tb);
+    if (nc == 3)
+        GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_fwd_l1<T, 3>), grid, dim3(256), 0, st, in, sin, dst,
+                                                        cstride, dstride, w, h, tb, shift))
+    else
+        GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_fwd_l1<T, 1>), grid, dim3(256), 0, st, in, sin, dst,
+                                                        cstride, dstride, w, h, tb, shift))
+}
+void gk_launch_dwt53_inv_l1(hipStream_t st, int stype, int nc, const int32_t* src, uint64_t cstride, uint32_t sstride,
+                            GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
+                            int32_t mn, int32_t mx) {
+    dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
+    if (nc == 3)
+        GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_inv_l1<T, 3>), grid, dim3(256), 0, st, src, cstride,
+                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx))
+    else
+        GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_inv_l1<T, 1>), grid, dim3(256), 0, st, src, cstride,
+                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx))
 }
 void gk_launch_gather(hipStream_t st, const uint8_t* src, uint8_t* dst, const uint64_t* seg, uint32_t nseg) {
     if (!nseg) return;

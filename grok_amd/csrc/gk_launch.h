@@ -24,19 +24,29 @@ void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, co
                           int32_t mn, int32_t mx);
 void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift, int32_t mn, int32_t mx);
+// one DWT level of cs.n components (planes cs.cstride apart), every tile of tb
 void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
-                         uint32_t w, uint32_t h,
-                         GkTiles tb = GkTiles());
+                         uint32_t w, uint32_t h, GkTiles tb = GkTiles(), GkComps cs = GkComps());
 void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
-                         uint32_t w, uint32_t h,
-                         GkTiles tb = GkTiles());
+                         uint32_t w, uint32_t h, GkTiles tb = GkTiles(), GkComps cs = GkComps());
+// level 1 fused with the sample stage: nc = 3 (DC + RCT of three components) or 1 (DC of one)
+void gk_launch_dwt53_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32_t sin, int32_t* dst, uint64_t cstride,
+                            uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb, int32_t shift);
+void gk_launch_dwt53_inv_l1(hipStream_t st, int stype, int nc, const int32_t* src, uint64_t cstride, uint32_t sstride,
+                            GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
+                            int32_t mn, int32_t mx);
 void gk_launch_gather(hipStream_t st, const uint8_t* src, uint8_t* dst, const uint64_t* seg, uint32_t nseg);
+// T1 encode of `count` blocks: positions [base, base + count) of `order` (block ids), or blocks
+// [base, base + count) without one; count = ~0u: all nblocks
 void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks, const uint64_t* sym_off, uint8_t* sym,
                      uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err, const int16_t* nmse_tab,
-                     int32_t* pass_nmse);
+                     int32_t* pass_nmse, const uint32_t* order = nullptr, uint32_t base = 0, uint32_t count = 0xffffffffu);
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
-                     uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter);
+                     uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter,
+                     const uint32_t* order = nullptr, uint32_t base = 0, uint32_t count = 0xffffffffu);
+// per-block coded bit-plane count (weight of the chunked CM / MQ overlap)
+void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* weight, uint32_t nblocks);
 uint32_t gk_t1dec_lanes();
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
                       uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks);
@@ -53,11 +63,15 @@ void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const 
 void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                         uint32_t h, int32_t shift, int32_t mn, int32_t mx);
 void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h,
-                         GkTiles tb = GkTiles());
+                         uint32_t h, GkTiles tb = GkTiles(), GkComps cs = GkComps());
 void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
-                         uint32_t h,
-                         GkTiles tb = GkTiles());
+                         uint32_t h, GkTiles tb = GkTiles(), GkComps cs = GkComps());
+// level 1 fused with the sample stage: nc = 3 (DC + ICT) or 1 (DC)
+void gk_launch_dwt97_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32_t sin, float* dst, uint64_t cstride,
+                            uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb, int32_t shift);
+void gk_launch_dwt97_inv_l1(hipStream_t st, int stype, int nc, const float* src, uint64_t cstride, uint32_t sstride,
+                            GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
+                            int32_t mn, int32_t mx);
 // HTJ2K cleanup-pass block coder (gk_ht.hip)
 void gk_launch_ht_enc(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, uint8_t* mel_scratch,
                       uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err);
