@@ -43,6 +43,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
+CLOCK_GHZ = 2.4            # MI355X max engine clock (MI355X_MICROARCH.md)
+DEC_INSTR_PER_STEP = 262   # k_t1_dec2 decision step, gfx950 ISA (python tools/isa_step_count.py)
 METRIC = "Mpixels/s encode+decode, 8K RGB 5/3 lossless + 9/7 lossy, 1/2/4/8 GPU"
 # Grok 9.2.0 on the survey container (8 vCPU), enc+dec Mpix/s
 GROK_CPU = {"C2p_8t": 5.99, "C2p_1t": 1.11, "C3p_8t": 2.87, "C3p_1t": 0.93, "C4_8t": 51.9, "C4_1t": 19.3,
@@ -506,6 +508,16 @@ def main():
     per_rank = world if isinstance(r, Runner) else 1   # replicas: every rank codes its own image
     value = S * S / 1e6 * per_rank * args.steps / el
     codestream_bytes = int(r.n)
+    # the T1 decoder's chain length: one more (untimed) decode with the step counters on
+    dec_steps = None
+    if isinstance(r, Runner) and not r.cfg["params"].get("cblk_sty"):
+        os.environ["GK_T1_STATS"] = "1"
+        try:
+            r.eng.decode(r.out, length=r.n, out=r.y)
+            t = r.eng.timings()
+            dec_steps = (int(t.t1_steps_max), int(t.t1_steps_total), int(t.t1_symbols))
+        finally:
+            del os.environ["GK_T1_STATS"]
     r.close()
     del r
     torch.cuda.empty_cache()
@@ -605,13 +617,28 @@ def main():
                          "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src,
                          "bytes_per_launch": round(nbytes), "avg_ms": round(t_ms, 3),
                          "note": "T1 is a serial MQ chain per code-block; bytes = compressed bytes + 4 B/sample"},
-            "dwt_roofline": {"achieved": round(dwt_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(dwt_gbs / HBM_PEAK_GBS, 4), "bytes_per_sample": 10.656},
+            "dwt_roofline": {"stage": "DC shift + MCT + DWT, encode and decode (level 1 fused with the sample "
+                                      "stage, all levels)",
+                             "achieved": round(dwt_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(dwt_gbs / HBM_PEAK_GBS, 4),
+                             "bytes_per_sample": round((m["enc_dwt_bytes"] + m["dec_dwt_bytes"]) / (2.0 * samples), 3)},
             "stages_ms": {k: round(v, 3) for k, v in m.items() if k.endswith("_ms") and v > 0},
             "t1": {"blocks": int(m["enc_t1_blocks"]),
                    "enc_blocks_per_s": round(m["enc_t1_blocks"] / (m["enc_t1_ms"] / 1e3)),
                    "dec_blocks_per_s": round(m["dec_t1_blocks"] / (m["dec_t1_ms"] / 1e3))},
         }
+        if dec_steps and dec_steps[0]:
+            # issue roofline of the chain-bound decoder: one wave per SIMD issues one instruction
+            # per 4 cycles, so the kernel takes at least (steps of its longest wave) x
+            # (instructions per step) x 4 cycles; DEC_INSTR_PER_STEP from tools/isa_step_count.py
+            floor_ms = dec_steps[0] * DEC_INSTR_PER_STEP * 4 / (CLOCK_GHZ * 1e6)
+            dec2_ms = m.get("dec_t1_coder_ms", m["dec_t1_ms"])
+            res["issue_roofline"] = {
+                "kernel": "k_t1_dec2 (T1 decode chain)", "bound": "instruction issue of the longest wave",
+                "max_steps_per_wave": dec_steps[0], "instructions_per_step": DEC_INSTR_PER_STEP,
+                "clock_ghz": CLOCK_GHZ, "floor_ms": round(floor_ms, 3), "measured_ms": round(dec2_ms, 3),
+                "frac": round(floor_ms / dec2_ms, 3), "steps_total": dec_steps[1], "symbols": dec_steps[2],
+                "lane_efficiency": round(dec_steps[2] / (64.0 * dec_steps[1]), 3) if dec_steps[1] else None}
         if aux:
             res["aux"] = aux
         if not args.no_cpu_baseline:

@@ -54,7 +54,8 @@ class Timings(ctypes.Structure):
     _fields_ = [(n, ctypes.c_float) for n in ("mct_ms", "dwt_ms", "t1_ms", "t2_ms", "assemble_ms", "total_ms",
                                               "t1_cm_ms", "t1_coder_ms")] + \
                [("dwt_launches", ctypes.c_uint32), ("t1_blocks", ctypes.c_uint32)] + \
-               [(n, ctypes.c_uint64) for n in ("dwt_bytes", "cs_bytes", "t1_bytes")]
+               [(n, ctypes.c_uint64) for n in ("dwt_bytes", "cs_bytes", "t1_bytes", "t1_steps_max", "t1_steps_total",
+                                               "t1_symbols")]
 
 
 _lib = None

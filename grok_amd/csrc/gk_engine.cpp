@@ -1520,12 +1520,27 @@ static void restore_native_qcd(gk_ctx* ctx) {
     ctx->band_qcd = ctx->native_qcd;
 }
 
-// Forward/inverse DWT over all components with the ping-pong placement of gk_common.h.
+// Level 1 fused with the sample stage: the caller's planes (sample type stype) are read by the
+// first forward level through the DC shift (+ RCT / ICT for the first three components when
+// mct3) and written by the last inverse level through the inverse MCT, DC shift and clamp, only
+// inside the window (region coordinates; planes[c] addresses the window origin).
+struct L1Io {
+    int stype = GK_S32;
+    bool mct3 = false;
+    std::vector<const void*> planes;
+    std::vector<uint32_t> strides;
+    int32_t shift = 0, mn = 0, mx = 0;
+    GkWin win;
+};
+
+// Forward/inverse DWT over all components with the ping-pong placement of gk_common.h; every
+// level is one launch per tile shape with the components in grid.z.
 static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0, uint32_t je = 0xffffffffu,
-                    uint32_t ib = 0, uint32_t ie = 0xffffffffu) {
+                    uint32_t ib = 0, uint32_t ie = 0xffffffffu, const L1Io* io = nullptr) {
     Plan& P = ctx->plan;
     int32_t* arena = (int32_t*)ctx->arena.p;
     const uint32_t L = P.p.numres - 1;
+    const uint64_t cst = 2 * (uint64_t)RG.plane;   // component plane pairs
     ctx->tm.dwt_launches = 0; ctx->tm.dwt_bytes = 0;
     for (uint32_t i = 0; i < L; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
@@ -1538,23 +1553,53 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
             S.tb.i0 = si0; S.tb.nx = si1 - si0;
             S.tb.ox = RG.x0; S.tb.oy = RG.y0;
             const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
-            for (uint32_t c = 0; c < P.nc; ++c) {
-                int32_t* A = arena + (size_t)c * 2 * RG.plane;
-                int32_t* B = A + RG.plane;
-                int32_t* src_l = (l & 1) ? A : B;     // D_{l-1}: level l input plane (l-1 odd -> B)
-                int32_t* dst_l = (l & 1) ? B : A;     // D_l
-                if (P.p.irrev) {
-                    float* fs = reinterpret_cast<float*>(src_l);
-                    float* fd = reinterpret_cast<float*>(dst_l);
-                    if (forward) gk_launch_dwt97_fwd(ctx->st, fs, RG.stride, fd, RG.stride, w, h, S.tb);
-                    else gk_launch_dwt97_inv(ctx->st, fd, RG.stride, fs, RG.stride, w, h, S.tb);
-                } else {
-                    if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, RG.stride, dst_l, RG.stride, w, h, S.tb);
-                    else gk_launch_dwt53_inv(ctx->st, dst_l, RG.stride, src_l, RG.stride, w, h, S.tb);
+            const uint64_t area = (uint64_t)w * h * S.tb.count();
+            int32_t* A = arena;
+            int32_t* B = A + RG.plane;
+            int32_t* src_l = (l & 1) ? A : B;     // D_{l-1}: level l input plane (l-1 odd -> B)
+            int32_t* dst_l = (l & 1) ? B : A;     // D_l
+            if (l == 1 && io) {
+                // fused level 1: three components through the MCT, the others one by one
+                const uint64_t es = gk_sample_size(io->stype);
+                for (uint32_t c = 0; c < P.nc;) {
+                    const int nc = (io->mct3 && c == 0) ? 3 : 1;
+                    GkPtr3 pp;
+                    for (int k = 0; k < nc; ++k) pp.p[k] = io->planes[c + k];
+                    if (forward) {
+                        if (P.p.irrev)
+                            gk_launch_dwt97_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c],
+                                                   reinterpret_cast<float*>(dst_l + c * cst), cst, RG.stride, w, h, S.tb,
+                                                   io->shift);
+                        else
+                            gk_launch_dwt53_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c], dst_l + c * cst, cst,
+                                                   RG.stride, w, h, S.tb, io->shift);
+                    } else {
+                        if (P.p.irrev)
+                            gk_launch_dwt97_inv_l1(ctx->st, io->stype, nc, reinterpret_cast<const float*>(dst_l + c * cst),
+                                                   cst, RG.stride, pp, io->strides[c], io->win, w, h, S.tb, io->shift,
+                                                   io->mn, io->mx);
+                        else
+                            gk_launch_dwt53_inv_l1(ctx->st, io->stype, nc, dst_l + c * cst, cst, RG.stride, pp,
+                                                   io->strides[c], io->win, w, h, S.tb, io->shift, io->mn, io->mx);
+                    }
+                    ctx->tm.dwt_launches++;
+                    ctx->tm.dwt_bytes += area * (4 + es) * nc;
+                    c += nc;
                 }
-                ctx->tm.dwt_launches++;
-                ctx->tm.dwt_bytes += (uint64_t)w * h * 8 * S.tb.count();
+                continue;
             }
+            const GkComps cs{cst, P.nc};
+            if (P.p.irrev) {
+                float* fs = reinterpret_cast<float*>(src_l);
+                float* fd = reinterpret_cast<float*>(dst_l);
+                if (forward) gk_launch_dwt97_fwd(ctx->st, fs, RG.stride, fd, RG.stride, w, h, S.tb, cs);
+                else gk_launch_dwt97_inv(ctx->st, fd, RG.stride, fs, RG.stride, w, h, S.tb, cs);
+            } else {
+                if (forward) gk_launch_dwt53_fwd(ctx->st, src_l, RG.stride, dst_l, RG.stride, w, h, S.tb, cs);
+                else gk_launch_dwt53_inv(ctx->st, dst_l, RG.stride, src_l, RG.stride, w, h, S.tb, cs);
+            }
+            ctx->tm.dwt_launches++;
+            ctx->tm.dwt_bytes += area * 8 * P.nc;
         }
     }
 }
@@ -1691,13 +1736,18 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         }
     }
     HIPCHK(hipEventRecord(ctx->ev[1], st));
-    // DC shift + MCT into plane A of each component (rows of the selected tiles)
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
     auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * RG.plane; };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
     if (mct3 && (sstr[1] != sstr[0] || sstr[2] != sstr[0])) throw GkError("the first three components must share a stride");
-    if (!P.p.irrev) {
+    L1Io io;
+    const bool fused = P.p.numres > 1;   // DC shift + MCT run inside the first DWT level
+    if (fused) {
+        io.stype = stype; io.mct3 = mct3; io.shift = shift;
+        io.planes.assign(src.begin(), src.end());
+        io.strides = sstr;
+    } else if (!P.p.irrev) {   // no decomposition: DC shift + MCT into plane A of each component
         if (mct3) gk_launch_dc_rct_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), RG.stride, P.w, nrows, shift);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, stype, src[c], sstr[c], planeA(c), RG.stride, P.w, nrows, shift);
     } else {
@@ -1705,7 +1755,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, stype, src[c], sstr[c], planeAf(c), RG.stride, P.w, nrows, shift);
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    run_dwt(ctx, RG, true, jb, je);
+    run_dwt(ctx, RG, true, jb, je, 0, 0xffffffffu, fused ? &io : nullptr);
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // T1 over the block range [b0, b1): every per-block device array is range-local
     const bool do_rc = P.p.rate_control();
@@ -2555,13 +2605,18 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
         HIPCHK(hipMemsetAsync(dscr, 0, 8 * hwo[nw], st));   // decoder state rows start at zero
         gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nslots);
+        ctx->tm.t1_steps_max = ctx->tm.t1_steps_total = ctx->tm.t1_symbols = 0;
+        if (getenv("GK_T1_STATS")) {
+            uint64_t sv[3];
+            gk_t1dec_stats(sv);
+            ctx->tm.t1_steps_max = sv[0]; ctx->tm.t1_steps_total = sv[1]; ctx->tm.t1_symbols = sv[2];
+        }
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr);
     }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
-    run_dwt(ctx, RG, false, jb, je, ib, ie);
-    HIPCHK(hipEventRecord(ctx->ev[4], st));
-    // ---- inverse MCT + DC shift + clamp of the output region into the output planes
+    // ---- inverse DWT; its last level writes the output region through the inverse MCT + DC
+    // shift + clamp into the output planes (without decomposition levels a separate pass does)
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
     int32_t mn = P.sgnd ? -(1 << (P.prec - 1)) : 0;
     int32_t mx = P.sgnd ? (1 << (P.prec - 1)) - 1 : (int32_t)((1u << P.prec) - 1);
@@ -2583,12 +2638,24 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
-    if (!P.p.irrev) {
+    if (P.p.numres > 1) {
+        L1Io io;
+        io.stype = stype; io.mct3 = mct3; io.shift = shift; io.mn = mn; io.mx = mx;
+        io.planes.assign(dst.begin(), dst.end());
+        io.strides = dstr;
+        io.win.x0 = (int32_t)(rx0 - RG.x0); io.win.y0 = (int32_t)(ry0 - RG.y0);
+        io.win.x1 = io.win.x0 + (int32_t)ncols; io.win.y1 = io.win.y0 + (int32_t)nrows;
+        if (mct3 && (dstr[1] != dstr[0] || dstr[2] != dstr[0])) throw GkError("the first three components must share a stride");
+        run_dwt(ctx, RG, false, jb, je, ib, ie, &io);
+        HIPCHK(hipEventRecord(ctx->ev[4], st));
+    } else if (!P.p.irrev) {
+        HIPCHK(hipEventRecord(ctx->ev[4], st));
         if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
                                        ncols, nrows, shift, mn, mx);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
             gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
     } else {
+        HIPCHK(hipEventRecord(ctx->ev[4], st));
         if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
                                        ncols, nrows, shift, mn, mx);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
@@ -2652,10 +2719,10 @@ gk_ctx* gk_create(int device_id) {
 void gk_destroy(gk_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->st);
-    for (auto& e : ctx->ev) (void)hipEventDestroy(e);
+    if (ctx->st) (void)hipStreamSynchronize(ctx->st);
+    for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
     if (ctx->nmse_tab) (void)hipFree(ctx->nmse_tab);
-    (void)hipStreamDestroy(ctx->st);
+    if (ctx->st) (void)hipStreamDestroy(ctx->st);
     delete ctx;
 }
 

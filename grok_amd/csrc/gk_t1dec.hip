@@ -642,6 +642,8 @@ uint32_t gk_t1dec_lanes() {
     }
     return lanes;
 }
+static uint64_t g_last_stats[3] = {0, 0, 0};   // max steps per wave, steps, symbols (GK_T1_STATS)
+void gk_t1dec_stats(uint64_t out[3]) { out[0] = g_last_stats[0]; out[1] = g_last_stats[1]; out[2] = g_last_stats[2]; }
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
                       uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks) {
     if (!nblocks) return;
@@ -665,6 +667,7 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         unsigned long long h[16];
         (void)hipMemcpyAsync(h, stats, 128, hipMemcpyDeviceToHost, st);
         (void)hipStreamSynchronize(st);
+        g_last_stats[0] = h[2]; g_last_stats[1] = h[0]; g_last_stats[2] = h[1];
         fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f events/wave %.0f\n",
                 (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]),
                 (double)h[3] / ((nblocks + 63) / 64));

@@ -83,10 +83,13 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                                               const uint64_t* __restrict__ sym_off, uint8_t* __restrict__ sym,
                                               uint32_t* __restrict__ pass_end, uint32_t* __restrict__ cm_info,
                                               uint32_t nblocks, int* err, const int16_t* __restrict__ nmse_tab,
-                                              int32_t* __restrict__ pass_nmse) {
+                                              int32_t* __restrict__ pass_nmse, const uint32_t* __restrict__ order,
+                                              uint32_t base, uint32_t count) {
     __shared__ CmLds L;
     __shared__ typename std::conditional<RC, CmRcLds, char>::type R;
-    const uint32_t b = blockIdx.x;
+    // workgroup j codes block order[base + j] (all blocks in index order without an order)
+    if (blockIdx.x >= count) return;
+    const uint32_t b = order ? order[base + blockIdx.x] : base + blockIdx.x;
     if (b >= nblocks) return;
     const int lane = threadIdx.x;
     const GkBlock B = blocks[b];
@@ -335,10 +338,13 @@ struct MqLane {
     uint8_t* out;
     uint32_t cap;
     uint32_t ovf;
+    // context-state updates of the last two symbols, not yet in LDS (cx 19 = none), and the
+    // entry of the next symbol's context read ahead of time (see mq_code4)
+    uint32_t pcx1, pne1, pcx2, pne2, epref;
 };
 struct MqLds {
     uint32_t tab[48];
-    uint32_t ctx[19][64];                 // per-lane context states (table entry | MPS << 31)
+    uint32_t ctx[20][64];                 // per-lane context states (table entry | MPS << 31); row 19 spare
     uint32_t line[64][MQ_LINE_DW + 1];    // per-lane output line (row padded: conflict-free columns)
 };
 
@@ -415,9 +421,18 @@ __device__ __forceinline__ void mql_put_sel(MqLane& q, uint32_t (*line)[MQ_LINE_
 // C >> e, e = the bits shifted past the boundary; they stay below the new byte, whose CT
 // (8, or 7 after 0xFF) is reduced by e.  A second boundary in one renormalisation (e >= 8)
 // repeats the BYTEOUT (rare; at most two for shifts <= 15: after the first, e <= 14 - 7).
-__device__ __forceinline__ void mq_code4(MqLane& q, MqLds& L, int lane, uint32_t s, bool en) {
-    const uint32_t cx = s >> 1, d = s & 1;
-    const uint32_t e = L.ctx[cx][lane];
+// One symbol (cx = s >> 1, decision s & 1).  Context states reach LDS two symbols late: the
+// entry of the next symbol's context is read here, right after the update from two symbols back
+// is written, and the next symbol takes the updates of the last two symbols from registers when
+// its context matches.  So neither the context read nor the probability-table read of an update
+// sits on the chain between consecutive symbols (except for back-to-back symbols of one context,
+// which wait for the table read).
+__device__ __forceinline__ void mq_code4(MqLane& q, MqLds& L, int lane, uint32_t s, uint32_t s_next, bool en) {
+    // bytes past a block's symbols are arbitrary: their context is the spare row 19
+    const uint32_t cx = min(s >> 1, 19u), d = s & 1;
+    const uint32_t e = cx == q.pcx1 ? q.pne1 : (cx == q.pcx2 ? q.pne2 : q.epref);
+    L.ctx[q.pcx2][lane] = q.pne2;
+    q.epref = L.ctx[min(s_next >> 1, 19u)][lane];
     const uint32_t mps = e >> 31;
     const uint32_t qe = e & 0xffff;
     const uint32_t a1 = q.a - qe;
@@ -428,7 +443,8 @@ __device__ __forceinline__ void mq_code4(MqLane& q, MqLds& L, int lane, uint32_t
     const uint32_t nmps = is_mps ? mps : (mps ^ ((e >> 28) & 1));
     const bool upd = en & !fast;
     const uint32_t ne = L.tab[nidx] | (nmps << 31);
-    L.ctx[cx][lane] = upd ? ne : e;   // unconditional: a branch here would wait on the table read
+    q.pcx2 = q.pcx1; q.pne2 = q.pne1;
+    q.pcx1 = cx; q.pne1 = upd ? ne : e;
     const uint32_t an = vsel_e(en, x ? a1 : qe, q.a);
     const uint32_t n = upd ? __clz(an) - 16 : 0u;
     q.a = an << n;
@@ -469,14 +485,18 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
                                               const GkBlock* __restrict__ blocks, uint8_t* __restrict__ bytes,
                                               GkPass* __restrict__ passes, uint32_t* __restrict__ info,
                                               uint32_t nblocks, int* err, const int32_t* __restrict__ pass_nmse,
-                                              uint32_t* __restrict__ pass_counter, uint32_t nl) {
+                                              uint32_t* __restrict__ pass_counter, uint32_t nl,
+                                              const uint32_t* __restrict__ order, uint32_t base, uint32_t count) {
     // nl = blocks per wave (lanes >= nl idle; gk_t1enc_lanes); pass ends staged in LDS [pass][lane]
     __shared__ MqLds L;
     extern __shared__ uint32_t pe_dyn[];
     const int lane = threadIdx.x;
     if (lane < 47) L.tab[lane] = c_mq[lane];
-    const uint32_t b = blockIdx.x * nl + lane;
-    const bool has = (uint32_t)lane < nl && b < nblocks;
+    // lane slot j = position base + j of `order` (index order without one)
+    const uint32_t j = blockIdx.x * nl + lane;
+    const bool inr = (uint32_t)lane < nl && j < count;
+    const uint32_t b = inr ? (order ? order[base + j] : base + j) : 0xffffffffu;
+    const bool has = inr && b < nblocks;
     uint32_t* pe_col = pe_dyn + (lane < (int)nl ? lane : 0);
 #define pe_lds_at(p) pe_col[(size_t)(p) * nl]
     const uint32_t numbps = has ? cm_info[2 * b] : 0, npasses = has ? cm_info[2 * b + 1] : 0;
@@ -544,13 +564,15 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
     uint4 cur4 = make_uint4(0, 0, 0, 0), nxt4 = make_uint4(0, 0, 0, 0);
     if (nsym) cur4 = *(const uint4*)(sp);
     if (nsym > 16) nxt4 = *(const uint4*)(sp + 16);
+    q.pcx1 = q.pcx2 = 19; q.pne1 = q.pne2 = 0;
+    q.epref = L.ctx[min(byte_of(cur4, 0) >> 1, 19u)][lane];
     for (uint32_t base = 0; base < maxsym; base += 16) {
         uint4 pre = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (uint32_t j = 0; j < 16; ++j) {
             const uint32_t i = base + j;
             const bool en = i < nsym;
-            mq_code4(q, L, lane, byte_of(cur4, j), en);
+            mq_code4(q, L, lane, byte_of(cur4, j), byte_of(j < 15 ? cur4 : nxt4, (j + 1) & 15), en);
             // the prefetch two chunks ahead is issued after the first symbol has consumed this
             // chunk's bytes, so the wait for them does not also wait for the prefetch
             if (j == 0) {
@@ -595,19 +617,25 @@ __global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, c
 #include "gk_launch.h"
 void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks, const uint64_t* sym_off, uint8_t* sym,
                      uint32_t* pass_end, uint32_t* cm_info, uint32_t nblocks, int* err, const int16_t* nmse_tab,
-                     int32_t* pass_nmse) {
+                     int32_t* pass_nmse, const uint32_t* order, uint32_t base, uint32_t count) {
     if (!nblocks) return;
+    if (count == 0xffffffffu) count = nblocks;
+    if (!count) return;
     if (pass_nmse)
-        hipLaunchKernelGGL(k_t1_cm<true>, dim3(nblocks), dim3(64), 0, st, coef, blocks, sym_off, sym, pass_end, cm_info,
-                           nblocks, err, nmse_tab, pass_nmse);
+        hipLaunchKernelGGL(k_t1_cm<true>, dim3(count), dim3(64), 0, st, coef, blocks, sym_off, sym, pass_end, cm_info,
+                           nblocks, err, nmse_tab, pass_nmse, order, base, count);
     else
-        hipLaunchKernelGGL(k_t1_cm<false>, dim3(nblocks), dim3(64), 0, st, coef, blocks, sym_off, sym, pass_end,
-                           cm_info, nblocks, err, nmse_tab, pass_nmse);
+        hipLaunchKernelGGL(k_t1_cm<false>, dim3(count), dim3(64), 0, st, coef, blocks, sym_off, sym, pass_end,
+                           cm_info, nblocks, err, nmse_tab, pass_nmse, order, base, count);
 }
+
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
-                     uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter) {
+                     uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter, const uint32_t* order,
+                     uint32_t base, uint32_t count) {
     if (!nblocks) return;
+    if (count == 0xffffffffu) count = nblocks;
+    if (!count) return;
     static uint32_t nl = 0;
     if (!nl) {   // blocks per 64-lane wave (GK_T1ENC_LANES, 1..64)
         const char* v = getenv("GK_T1ENC_LANES");
@@ -615,6 +643,6 @@ void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off
         nl = (uint32_t)(n < 1 ? 1 : (n > 64 ? 64 : n));
     }
     const size_t lds = (size_t)(GK_MAX_PASSES + 1) * nl * 4;
-    hipLaunchKernelGGL(k_t1_mq, dim3((nblocks + nl - 1) / nl), dim3(64), lds, st, sym, sym_off, pass_end, cm_info,
-                       blocks, bytes, passes, info, nblocks, err, pass_nmse, pass_counter, nl);
+    hipLaunchKernelGGL(k_t1_mq, dim3((count + nl - 1) / nl), dim3(64), lds, st, sym, sym_off, pass_end, cm_info,
+                       blocks, bytes, passes, info, nblocks, err, pass_nmse, pass_counter, nl, order, base, count);
 }

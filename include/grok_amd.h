@@ -73,6 +73,9 @@ typedef struct gk_timings {
     uint64_t dwt_bytes;     /* algorithmic bytes moved by the DWT launches */
     uint64_t cs_bytes;      /* codestream bytes produced (encode) / consumed (decode) */
     uint64_t t1_bytes;      /* compressed code-block bytes coded by T1 */
+    /* Part-1 decode with GK_T1_STATS set in the environment (0 otherwise): decision steps of
+       the longest-running wave, all steps issued, symbols decoded (the T1 chain's work) */
+    uint64_t t1_steps_max, t1_steps_total, t1_symbols;
 } gk_timings;
 
 typedef struct gk_ctx gk_ctx;
