@@ -1415,6 +1415,8 @@ struct HostBuf {
 struct gk_ctx {
     int device = 0;
     hipStream_t st = nullptr;
+    hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // encode T1: MQ chunks overlapping context modelling
+    hipEvent_t xev[6];
     std::string err;
     gk_timings tm{};
     // cached plan
@@ -1431,8 +1433,8 @@ struct gk_ctx {
     DevBuf dplanes;     // component planes staged from host
     DevBuf derr;
     DevBuf dsym, dsymoff, dpassend, dcminfo;
-    DevBuf dscratch, dnmse, dord;
-    HostBuf hinfo, hseg, hhdr, hpasses, hord;
+    DevBuf dscratch, dnmse, dord, dweight, dord_enc;
+    HostBuf hinfo, hseg, hhdr, hpasses, hord, hweight, hord_enc;
     DevBuf dstage1, dstage2;   // decode: batched tile-part / packet header fetches (device input)
     HostBuf hstage1, hstage2;
     int16_t* nmse_tab = nullptr;   // device copy of the nmsedec tables (4 x 128)
@@ -1796,10 +1798,66 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nbx * GK_HT_MEL_CAP + 256);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_ht_enc(st, arena, dblk, dbytes, mel, GK_HT_MEL_CAP, dinfo, nbr, derr);
-    } else {
+    } else if (nbr < 8192 || getenv("GK_T1ENC_SERIAL")) {
         gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nbr, derr, ctx->nmse_tab, dnmse);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount);
+    } else {
+        // Context modelling and MQ coding overlap.  Blocks go heaviest first (most coded
+        // bit-planes, k_t1_weight) in three chunks; chunk i's MQ kernel starts on its own stream
+        // once chunk i is modelled, so the longest MQ chains run while the lighter blocks are
+        // still being modelled.  An MQ workgroup fills its CU's LDS, so the modelling waves never
+        // share a SIMD with an MQ chain (sharing one slowed the chains more than the overlap
+        // gained).  Each block is coded exactly as in one pass; only the launch order changes.
+        uint8_t* dw = (uint8_t*)ctx->dweight.get(nbr);
+        gk_launch_t1_weight(st, arena, dblk, dw, nbr);
+        uint8_t* hw = (uint8_t*)ctx->hweight.get(nbr);
+        HIPCHK(hipMemcpyAsync(hw, dw, nbr, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        uint32_t start[34] = {0};
+        for (uint32_t i = 0; i < nbr; ++i) start[32 - std::min<uint32_t>(hw[i], 32)]++;   // descending weight
+        for (uint32_t k = 0, acc = 0; k < 34; ++k) { const uint32_t c = start[k]; start[k] = acc; acc += c; }
+        uint32_t* ho = (uint32_t*)ctx->hord_enc.get(4 * (size_t)nbr);
+        for (uint32_t i = 0; i < nbr; ++i) ho[start[32 - std::min<uint32_t>(hw[i], 32)]++] = i;
+        uint32_t* dord = (uint32_t*)ctx->dord_enc.get(4 * (size_t)nbr);
+        HIPCHK(hipMemcpyAsync(dord, ho, 4 * (size_t)nbr, hipMemcpyHostToDevice, st));
+        // chunk ends as fractions of the blocks (GK_T1ENC_CUTS, up to three), rounded to whole MQ
+        // workgroups (4 x 64 blocks); the last chunk's MQ runs on the main stream
+        static std::vector<double> fr;
+        if (fr.empty()) {
+            const char* cv = getenv("GK_T1ENC_CUTS");
+            std::string cs = cv ? cv : "0.125,0.375";
+            for (size_t q = 0; q < cs.size();) {
+                size_t e = cs.find(',', q);
+                if (e == std::string::npos) e = cs.size();
+                const double f = atof(cs.substr(q, e - q).c_str());
+                if (f > 0 && f < 1 && fr.size() < 3) fr.push_back(f);
+                q = e + 1;
+            }
+        }
+        std::vector<uint32_t> cut(1, 0);
+        for (double f : fr) {
+            const uint32_t c = (uint32_t)(nbr * f) / 256 * 256;
+            if (c > cut.back() && c < nbr) cut.push_back(c);
+        }
+        cut.push_back(nbr);
+        const int nch = (int)cut.size() - 1;
+        for (int k = 0; k < nch; ++k) {
+            const uint32_t base = cut[k], cnt = cut[k + 1] - cut[k];
+            gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nbr, derr, ctx->nmse_tab, dnmse, dord, base, cnt);
+            if (k + 1 < nch) {
+                HIPCHK(hipEventRecord(ctx->xev[k], st));
+                HIPCHK(hipStreamWaitEvent(ctx->aux[k], ctx->xev[k], 0));
+                gk_launch_t1_mq(ctx->aux[k], dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount,
+                                dord, base, cnt);
+                HIPCHK(hipEventRecord(ctx->xev[3 + k], ctx->aux[k]));
+            } else {
+                HIPCHK(hipEventRecord(ctx->ev[8], st));
+                gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount, dord,
+                                base, cnt);
+            }
+        }
+        for (int k = 0; k + 1 < nch; ++k) HIPCHK(hipStreamWaitEvent(st, ctx->xev[3 + k], 0));
     }
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(16 * (size_t)nb + 64);
@@ -2695,7 +2753,10 @@ gk_ctx* gk_create(int device_id) {
     gk_ctx* ctx = new gk_ctx();
     ctx->device = device_id;
     if (hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) { delete ctx; return nullptr; }
+    for (auto& a : ctx->aux)
+        if (hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) { gk_destroy(ctx); return nullptr; }
     for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+    for (auto& e : ctx->xev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
     // nmsedec lookup tables (t1_generate_luts.cpp:338-362): sig, sig0, ref, ref0
     int16_t tab[4][128];
     for (int i = 0; i < 128; ++i) {
@@ -2720,7 +2781,10 @@ void gk_destroy(gk_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
+    for (auto& a : ctx->aux)
+        if (a) { (void)hipStreamSynchronize(a); (void)hipStreamDestroy(a); }
     for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : ctx->xev) if (e) (void)hipEventDestroy(e);
     if (ctx->nmse_tab) (void)hipFree(ctx->nmse_tab);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     delete ctx;

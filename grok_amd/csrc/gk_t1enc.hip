@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include "gk_common.h"
 #include "gk_t1_common.h"
+#include <algorithm>
 #include <type_traits>
 #include <cstdlib>
 
@@ -480,24 +481,27 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t j) {
 // passes in `passes`); pass records are packed (atomic offset allocation) so
 // the host copies only the passes that exist.  With rate control the
 // cumulative distortion follows T1::getwmsedec (T1.cpp:418-436, 836-842).
-__global__ __launch_bounds__(64) void k_t1_mq(const uint8_t* __restrict__ sym, const uint64_t* __restrict__ sym_off,
+__global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, const uint64_t* __restrict__ sym_off,
                                               const uint32_t* __restrict__ pass_end, const uint32_t* __restrict__ cm_info,
                                               const GkBlock* __restrict__ blocks, uint8_t* __restrict__ bytes,
                                               GkPass* __restrict__ passes, uint32_t* __restrict__ info,
                                               uint32_t nblocks, int* err, const int32_t* __restrict__ pass_nmse,
                                               uint32_t* __restrict__ pass_counter, uint32_t nl,
                                               const uint32_t* __restrict__ order, uint32_t base, uint32_t count) {
-    // nl = blocks per wave (lanes >= nl idle; gk_t1enc_lanes); pass ends staged in LDS [pass][lane]
-    __shared__ MqLds L;
+    // nl = blocks per wave (lanes >= nl idle; gk_t1enc_lanes); pass ends staged in LDS [pass][lane].
+    // A workgroup is four independent waves (one per SIMD) and takes a whole CU's LDS (the
+    // launch pads it), so no other kernel's waves share a SIMD with an MQ chain.
+    __shared__ MqLds Lw[4];
     extern __shared__ uint32_t pe_dyn[];
-    const int lane = threadIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    MqLds& L = Lw[wave];
     if (lane < 47) L.tab[lane] = c_mq[lane];
     // lane slot j = position base + j of `order` (index order without one)
-    const uint32_t j = blockIdx.x * nl + lane;
+    const uint32_t j = (blockIdx.x * 4 + wave) * nl + lane;
     const bool inr = (uint32_t)lane < nl && j < count;
     const uint32_t b = inr ? (order ? order[base + j] : base + j) : 0xffffffffu;
     const bool has = inr && b < nblocks;
-    uint32_t* pe_col = pe_dyn + (lane < (int)nl ? lane : 0);
+    uint32_t* pe_col = pe_dyn + (size_t)wave * (GK_MAX_PASSES + 1) * nl + (lane < (int)nl ? lane : 0);
 #define pe_lds_at(p) pe_col[(size_t)(p) * nl]
     const uint32_t numbps = has ? cm_info[2 * b] : 0, npasses = has ? cm_info[2 * b + 1] : 0;
     const uint32_t* PE = pass_end + (size_t)(has ? b : 0) * GK_MAX_PASSES;
@@ -629,6 +633,34 @@ void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks,
                            cm_info, nblocks, err, nmse_tab, pass_nmse, order, base, count);
 }
 
+// Per block the bit-plane count T1 will code (the magnitude test of k_t1_cm's load), as the
+// weight that orders the chunked context-modelling / MQ overlap: one wave per block.
+__global__ __launch_bounds__(64) void k_t1_weight(const int32_t* __restrict__ coef, const GkBlock* __restrict__ blocks,
+                                                  uint8_t* __restrict__ weight, uint32_t nblocks) {
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks) return;
+    const int lane = threadIdx.x;
+    const GkBlock B = blocks[b];
+    const bool irrev = B.flags & 1;
+    uint32_t mx = 0;
+    if (lane < (int)B.w)
+        for (uint32_t y = 0; y < B.h; ++y) {
+            const int32_t raw = coef[B.band_off + (size_t)y * B.stride + lane];
+            const uint32_t a = irrev ? (uint32_t)fabsf(rintf((__int_as_float(raw) / B.step) * 64.0f))
+                                     : (uint32_t)(raw < 0 ? -raw : raw) * 64u;
+            mx = a > mx ? a : mx;
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { const uint32_t t = __shfl_xor(mx, o); mx = t > mx ? t : mx; }
+    if (lane == 0) {
+        const uint32_t t = mx ? 32 - __clz(mx) : 0;
+        weight[b] = (uint8_t)(t <= 6 ? 0 : t - 6);
+    }
+}
+void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* weight, uint32_t nblocks) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(k_t1_weight, dim3(nblocks), dim3(64), 0, st, coef, blocks, weight, nblocks);
+}
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
                      uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter, const uint32_t* order,
@@ -642,7 +674,9 @@ void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off
         const int n = v ? atoi(v) : 64;
         nl = (uint32_t)(n < 1 ? 1 : (n > 64 ? 64 : n));
     }
-    const size_t lds = (size_t)(GK_MAX_PASSES + 1) * nl * 4;
-    hipLaunchKernelGGL(k_t1_mq, dim3((count + nl - 1) / nl), dim3(64), lds, st, sym, sym_off, pass_end, cm_info,
-                       blocks, bytes, passes, info, nblocks, err, pass_nmse, pass_counter, nl, order, base, count);
+    // dynamic LDS: the four waves' pass ends, padded so one workgroup fills the CU's 160 KiB
+    const size_t pe = (size_t)(GK_MAX_PASSES + 1) * nl * 4 * 4;
+    const size_t lds = std::max(pe, (size_t)163840 - 4 * sizeof(MqLds));
+    hipLaunchKernelGGL(k_t1_mq, dim3((count + 4 * nl - 1) / (4 * nl)), dim3(256), lds, st, sym, sym_off, pass_end,
+                       cm_info, blocks, bytes, passes, info, nblocks, err, pass_nmse, pass_counter, nl, order, base, count);
 }
