@@ -239,25 +239,33 @@ __device__ __forceinline__ uint64_t h_get(uint32_t (*g)[64], int row, int lane) 
 // TIMING (diagnostic build, GK_T1_STATS=2): shader-clock cycles spent in stripe-boundary
 // events vs decision steps, summed into stats[4] / stats[5].
 template <bool TIMING>
-__global__ __launch_bounds__(64) void k_t1_dec2(const uint8_t* __restrict__ bytes, const GkBlock* __restrict__ blocks,
+// A workgroup is DEC_WAVES independent waves (one per SIMD) and the launch pads its LDS to the
+// CU's 160 KiB, so every decoding wave has its SIMD to itself (single waves per workgroup were
+// placed two to a SIMD on some CUs while other SIMDs idled).
+#define DEC_WAVES 4
+__global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __restrict__ bytes,
+                                                const GkBlock* __restrict__ blocks,
                                                 const uint32_t* __restrict__ order, uint64_t* __restrict__ scratch,
                                                 const uint64_t* __restrict__ wave_off, uint32_t nblocks,
                                                 unsigned long long* __restrict__ stats, uint32_t kpark) {
-    __shared__ Dec2Lds Ls;
-    const int lane = threadIdx.x;
+    __shared__ Dec2Lds Lw[DEC_WAVES];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    Dec2Lds& Ls = Lw[wv];
+    const uint32_t gw = blockIdx.x * DEC_WAVES + wv;          // global wave: 64 slots
+    const uint32_t nwaves = (nblocks + 63) / 64;
     if (lane < 47) Ls.tab[lane] = c_mq[lane];
     for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
     for (int i = lane; i < 256; i += 64)
         Ls.sc[i] = sc_rule((uint32_t)(((i >> 2) & 0xf) | ((i & 3) << 4) | (i & 0xc0)));
-    const uint32_t slot = blockIdx.x * 64 + lane;
+    const uint32_t slot = gw * 64 + lane;
     const uint32_t bid = slot < nblocks ? order[slot] : 0xffffffffu;   // empty slots: 0xffffffff
     const bool has = bid != 0xffffffffu;
     GkBlock B = {};
     if (has) B = blocks[bid];
     // this lane's scratch slab: the wave's region split into 64 equal slabs (host sizes
     // it for the wave's largest numbps and zero-fills it)
-    const uint64_t lstride = (wave_off[blockIdx.x + 1] - wave_off[blockIdx.x]) / 64;
-    uint64_t* WS = scratch + wave_off[blockIdx.x] + (size_t)lane * lstride;
+    const uint64_t lstride = gw < nwaves ? (wave_off[gw + 1] - wave_off[gw]) / 64 : 0;
+    uint64_t* WS = scratch + (gw < nwaves ? wave_off[gw] : 0) + (size_t)lane * lstride;
     const uint32_t numbps = has ? B.numbps : 0, npasses = (has && B.numbps) ? B.npasses : 0;
     const uint32_t h = B.h, w = B.w;
     const uint64_t colmask = w >= 64 ? ~0ull : ((1ull << w) - 1);
@@ -657,12 +665,14 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         const char* kp = getenv("GK_T1DEC_PARK");   // parked lanes that trigger a stripe boundary
         kpark = kp ? atoi(kp) : 4;
     }
+    const uint32_t nwaves = (nblocks + 63) / 64, ngroups = (nwaves + DEC_WAVES - 1) / DEC_WAVES;
+    const size_t pad = DEC_WAVES * sizeof(Dec2Lds) < 163840 ? 163840 - DEC_WAVES * sizeof(Dec2Lds) : 0;
     if (timing)
-        hipLaunchKernelGGL(k_t1_dec2<true>, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
+        hipLaunchKernelGGL(k_t1_dec2<true>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, stats, (uint32_t)kpark);
     else
-        hipLaunchKernelGGL(k_t1_dec2<false>, dim3((nblocks + 63) / 64), dim3(64), 0, st, bytes, blocks, order, scratch,
-                           wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
+        hipLaunchKernelGGL(k_t1_dec2<false>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order,
+                           scratch, wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
     if (want) {
         unsigned long long h[16];
         (void)hipMemcpyAsync(h, stats, 128, hipMemcpyDeviceToHost, st);
