@@ -477,13 +477,35 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
 // Byte gather for codestream assembly and decode staging.
 // seg: (src_off, dst_off, len) triples; one wave per segment.
 // =============================================================================
+// Bytes up to the next 16-byte boundary of the destination go one per lane; then every lane
+// stores 16 aligned bytes per iteration, built from the covering source dwords with alignbyte
+// (a source offset need not share the destination's alignment); the tail goes one per lane.
 __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                 const uint64_t* __restrict__ seg, uint32_t nseg) {
     uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= nseg) return;
-    uint64_t so = seg[3 * s], d = seg[3 * s + 1], n = seg[3 * s + 2];
+    const uint64_t so = seg[3 * s], d = seg[3 * s + 1];
+    uint64_t n = seg[3 * s + 2];
     const int lane = threadIdx.x & 63;
-    for (uint64_t i = lane; i < n; i += 64) dst[d + i] = src[so + i];
+    const uint8_t* sp = src + so;
+    uint8_t* dp = dst + d;
+    const uint64_t head = min(n, (uint64_t)((16 - (d & 15)) & 15));
+    if ((uint64_t)lane < head) dp[lane] = sp[lane];
+    sp += head; dp += head; n -= head;
+    const uint64_t nch = n / 16;
+    const uint32_t sh = (uint32_t)((uintptr_t)sp & 3);
+    const uint32_t* sw = (const uint32_t*)((uintptr_t)sp & ~(uintptr_t)3);
+    for (uint64_t c = lane; c < nch; c += 64) {
+        const uint32_t* w = sw + 4 * c;
+        const uint32_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3], a4 = sh ? w[4] : 0u;
+        uint4 v;
+        v.x = __builtin_amdgcn_alignbyte(a1, a0, sh);
+        v.y = __builtin_amdgcn_alignbyte(a2, a1, sh);
+        v.z = __builtin_amdgcn_alignbyte(a3, a2, sh);
+        v.w = __builtin_amdgcn_alignbyte(a4, a3, sh);
+        *(uint4*)(dp + 16 * c) = v;
+    }
+    for (uint64_t i = nch * 16 + lane; i < n; i += 64) dp[i] = sp[i];
 }
 
 // =============================================================================
