@@ -1117,6 +1117,99 @@ struct T2Enc {
         incl0 = incl; imsb0 = imsb; inprev0 = inprev; nlb0 = nlb;
     }
 
+    // ---- bisection steps decided without coding the packets.  A layer's header bits, all
+    // but the stuffing, follow from its pass counts: per code-block the inclusion bit (blocks
+    // already in packets), number of passes, comma code and length (make_layer caches them
+    // with the count); the inclusion tag tree codes exactly one bit for every node with no
+    // block included before l whose parent has one included by l (the root always: a node's
+    // low is l when its parent lets it be coded, so it emits one 0 or one 1), and the
+    // zero-bit-plane tree codes every node whose first block enters at l, from the parent's
+    // value up to its own and a 1.  A header of R raw bits takes ceil(R/8) .. ceil(R/7)+2
+    // bytes (a 7-bit chunk after each 0xFF, a final 0xFF doubled), so the layer's size is
+    // known to a few parts in 10^4 and a step that range decides is not simulated.
+    std::vector<uint32_t> bbits, blen;      // per code-block: header bits, body bytes at its count
+    std::vector<uint32_t> ccount;           // per code-block: the count bbits/blen belong to
+    std::vector<std::vector<uint8_t>> tA;   // per tree: a block of the subtree is in packets before l
+    std::vector<std::vector<uint32_t>> tV;  // per tree: zero-bit-plane tag values (subtree minimum)
+    std::vector<uint64_t> ubitn;            // per unit: raw header bits
+    static uint32_t numpasses_bits(uint32_t n) { return n == 1 ? 1 : n == 2 ? 2 : n <= 5 ? 4 : n <= 36 ? 9 : 16; }
+    // header bits (past the tag trees) and body bytes of block b taking passes [p0, inc)
+    void block_cost(uint32_t b, uint32_t p0, uint32_t inc) {
+        ccount[b] = inc;
+        if (inc == p0) { bbits[b] = 0; blen[b] = 0; return; }
+        const uint32_t np = inc - p0;
+        const uint32_t len = rate(b, inc - 1) - (p0 ? rate(b, p0 - 1) : 0);
+        const int nl = p0 ? (int)nlb0[b] : 3;
+        const int c = std::max(0, floorlog2(len) + 1 - (nl + floorlog2(np)));
+        bbits[b] = numpasses_bits(np) + (uint32_t)c + 1 + (uint32_t)(nl + c + floorlog2(np));
+        blen[b] = len;
+    }
+    void bounds_prep(const std::vector<uint16_t>& prev) {   // once per layer, after the snapshot
+        const uint32_t nb = (uint32_t)P.blocks.size();
+        if (bbits.size() != nb) { bbits.assign(nb, 0); blen.assign(nb, 0); ccount.assign(nb, 0xffffffffu); }
+        std::fill(ccount.begin(), ccount.end(), 0xffffffffu);
+        tA.resize(P.ntrees); tV.resize(P.ntrees);
+        ubitn.assign(units.size(), 0);
+        for (const Unit& U : units) {
+            uint32_t bnb;
+            const PrecG& PG = unit_prec(U, &bnb);
+            const std::vector<int32_t>& par = incl[PG.tree].parent;
+            std::vector<uint8_t>& A = tA[PG.tree];
+            A.assign(par.size(), 0);
+            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) A[k] = prev[PG.first_block + k] != 0;
+            for (size_t n = 0; n < par.size(); ++n) if (A[n] && par[n] >= 0) A[par[n]] = 1;
+            std::vector<uint32_t>& V = tV[PG.tree];
+            if (V.size() != par.size()) {
+                V.assign(par.size(), 0xffffffffu);
+                for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) V[k] = bnb - info[4 * (size_t)(PG.first_block + k)];
+                for (size_t n = 0; n < par.size(); ++n) if (par[n] >= 0) V[par[n]] = std::min(V[par[n]], V[n]);
+            }
+        }
+    }
+    // -1: the layer's packets overrun max_bytes, 1: they fit, 0: too close to call
+    std::vector<uint64_t> clo, chi, cbody;   // per packet: header byte bounds, body bytes
+    int decide(uint32_t l, uint64_t max_bytes, const std::vector<uint16_t>& prev) {
+        if (max_bytes == 0xffffffffull) return 1;
+        host_pool().run(uorder.size(), [&](size_t j) {
+            const uint32_t u = uorder[j];
+            const PrecG& PG = unit_prec(units[u]);
+            const std::vector<int32_t>& par = incl[PG.tree].parent;
+            const std::vector<uint8_t>& A = tA[PG.tree];
+            const std::vector<uint32_t>& V = tV[PG.tree];
+            thread_local std::vector<uint8_t> N;
+            N.assign(par.size(), 0);
+            uint64_t bits = 0, body = 0;
+            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                const uint32_t b = PG.first_block + k;
+                const bool in = lnp[(size_t)b * L + l] != 0;
+                if (prev[b]) bits += 1;
+                else if (in) N[k] = 1;
+                if (in) { bits += bbits[b]; body += blen[b]; }
+            }
+            for (size_t n = 0; n < par.size(); ++n) if (N[n] && par[n] >= 0) N[par[n]] = 1;
+            for (size_t n = 0; n < par.size(); ++n) {
+                if (A[n]) continue;
+                const int32_t p = par[n];
+                if (p < 0 || A[p] || N[p]) bits += 1;
+                if (N[n]) bits += V[n] - (p < 0 ? 0u : V[p]) + 1;
+            }
+            ubitn[u] = bits; ubody[u] = body;
+        });
+        uint64_t lo = prior, hi = prior, last_body = 0;
+        clo.resize(chains.size()); chi.resize(chains.size()); cbody.resize(chains.size());
+        for (size_t i = 0; i < chains.size(); ++i) {
+            uint64_t R = 1, body = 0;
+            for (uint32_t u : cunits[i]) { R += ubitn[u]; body += ubody[u]; }
+            clo[i] = (R + 7) / 8; chi[i] = (R + 6) / 7 + 2; cbody[i] = body;
+            lo += clo[i] + body; hi += chi[i] + body;
+            last_body = body;
+        }
+        // pass <=> S_(n-1) + hdr_n < max_bytes and S_n <= max_bytes, S_n - body_n = S_(n-1) + hdr_n
+        if (hi <= max_bytes && hi - last_body < max_bytes) return 1;
+        if (lo > max_bytes || lo - last_body >= max_bytes) return -1;
+        return 0;
+    }
+
     // makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0) (TileProcessor.cpp:1367-1515),
     // blocks in parallel.  During one layer's bisection prev[] is fixed, so each block keeps
     // the threshold its pass count was last computed at (mref) and half the distance from it
@@ -1130,6 +1223,8 @@ struct T2Enc {
         x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
         return x ^ (x >> 31);
     }
+    bool bounds = false;      // bisection steps decided by header-size bounds (fast path)
+    bool bounds_on = false;   // ... during this layer's bisection (make_layer caches block costs)
     uint64_t make_layer(uint32_t l, double thresh, bool final_attempt, std::vector<uint16_t>& prev) {
         const uint32_t nb = (uint32_t)P.blocks.size();
         const uint32_t chunk = 2048, nch = (b1 - b0 + chunk - 1) / chunk;
@@ -1164,6 +1259,7 @@ struct T2Enc {
                 mrad[b] = (m > 1e-9 * fabs(thresh) && m > 1e-12) ? 0.5 * m : 0.0;
             }
             const uint16_t v = (uint16_t)(inc - prev[b]);
+            if (bounds_on && ccount[b] != inc) block_cost(b, prev[b], inc);
             lnp[(size_t)b * L + l] = v;
             hsum += mix64(((uint64_t)b << 16) | v);
             if (final_attempt) { prev[b] = (uint16_t)inc; mrad[b] = -1.0; }
@@ -1210,11 +1306,16 @@ struct T2Enc {
         static const bool prof = getenv("GK_PROFILE") != nullptr;
         using clk = std::chrono::steady_clock;
         auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        double t_make = 0, t_sim = 0;
+        double t_make = 0, t_sim = 0, t_prep = 0;
         uint32_t n_it = 0, n_sim = 0;
         if (fast) init_chains();
+        static const bool check = getenv("GK_T2_CHECK_SIM") != nullptr;
+        bounds = fast && !getenv("GK_T2_NO_BOUNDS");
+        uint32_t n_bound = 0;
         for (uint32_t l = 0; l < L; ++l) {
             uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
+            bounds_on = bounds && rates[l] > 0.0;
+            if (bounds_on) { const auto tp = clk::now(); bounds_prep(prev); t_prep += msd(tp, clk::now()); }
             if (rates[l] > 0.0) {
                 double lower = min_slope, prevthresh = -1, thresh = 0;
                 // pass counts equal to those at an end of the bisection interval give that end's
@@ -1241,13 +1342,24 @@ struct T2Enc {
                     if (has_hi && h == h_hi && c_now == c_hi) ok = true;
                     else if (has_lo && h == h_lo && c_now == c_lo) ok = false;
                     else {
-                        ok = fast ? simulate_layer(l, max_len) : simulate(l + 1, max_len);
+                        const int d = bounds_on ? decide(l, max_len, prev) : 0;
+                        if (d && !check) { ok = d > 0; ++n_bound; }
+                        else {
+                            ok = fast ? simulate_layer(l, max_len) : simulate(l + 1, max_len);
+                            ++n_sim;
+                            if (bounds_on && check && max_len != 0xffffffffull) {
+                                for (size_t i = 0; i < chains.size(); ++i)
+                                    if (chdr[i] < clo[i] || chdr[i] > chi[i] || csize[i] - chdr[i] != cbody[i])
+                                        throw GkError("rate-control bounds: packet size outside its bounds");
+                                if (d && ok != (d > 0)) throw GkError("rate-control bounds: decision differs from the simulation");
+                            }
+                        }
                         t_sim += msd(t1, clk::now());
-                        ++n_sim;
                     }
                     if (!ok) { lower = thresh; h_lo = h; has_lo = true; counts(c_lo); continue; }
                     upper = thresh; h_hi = h; has_hi = true; counts(c_hi);
                 }
+                bounds_on = false;
                 make_layer(l, upper == -1 ? thresh : upper, true, prev);
                 upper = lower - 1;
             } else {
@@ -1256,8 +1368,8 @@ struct T2Enc {
             if (fast && l + 1 < L) finish_layer(l);
         }
         if (prof)
-            fprintf(stderr, "pcrd: %u bisection steps, %u simulated; make_layer %.2f ms, simulation %.2f ms\n", n_it,
-                    n_sim, t_make, t_sim);
+            fprintf(stderr, "pcrd: %u bisection steps, %u simulated, %u decided by bounds; make_layer %.2f ms, simulation %.2f ms, bounds setup %.2f ms\n",
+                    n_it, n_sim, n_bound, t_make, t_sim, t_prep);
         if (prof)
             fprintf(stderr, "pcrd code_layer: units %.2f ms, packet lengths %.2f ms (%zu units, %zu packets)\n",
                     prof_code / 1e3, prof_stuff / 1e3, units.size(), chains.size());

@@ -593,43 +593,54 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
 }
 
 // Reconstruction + dequantisation: wave per block, lane = column.
-// Job q reconstructs block ids[q], whose decoder lane was pos[q].
+// Job q reconstructs block ids[q], whose decoder lane was pos[q]. The block's
+// significant bit-plane rows and sign rows are staged once through LDS with
+// coalesced row loads (lane = row); the column extraction then reads them as
+// LDS broadcasts instead of one uniform global load per (row, plane).
 __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blocks, const uint32_t* __restrict__ ids,
                                                  const uint32_t* __restrict__ pos,
                                                  const uint64_t* __restrict__ scratch,
                                                  const uint64_t* __restrict__ wave_off, int32_t* __restrict__ coef,
                                                  uint32_t nblocks) {
+    __shared__ uint64_t Lr[32 * 64];
+    __shared__ uint64_t Ls[64];
     const uint32_t q = blockIdx.x;
     if (q >= nblocks) return;
     const int x = threadIdx.x;
     const GkBlock B = blocks[ids[q]];
-    if (x >= (int)B.w) return;
     const uint32_t slot = pos[q], ln = slot & 63;
     const uint64_t lstride = (wave_off[(slot >> 6) + 1] - wave_off[slot >> 6]) / 64;
     const uint64_t* WS = scratch + wave_off[slot >> 6] + (size_t)ln * lstride;
     const bool irrev = B.flags & 1;
     float* fcoef = reinterpret_cast<float*>(coef);
-    const uint32_t numbps = B.numbps, npasses = B.npasses;
+    const uint32_t numbps = B.numbps, npasses = B.npasses, h = B.h;
     // last decoded pass k = npasses-1: pass k>0 belongs to plane numbps-1-(k+2)/3, type (k+2)%3
     int bpl = 0, t = 2;
-    if (npasses && numbps) {
+    const bool any = npasses && numbps;
+    if (any) {
         int k = (int)npasses - 1;
         if (k > 3 * (int)numbps - 3) k = 3 * (int)numbps - 3;
         bpl = (int)numbps - 1 - (k + 2) / 3;
         t = (k + 2) % 3;
+        const int np = min((int)numbps - bpl, 32);   // planes numbps-1 .. bpl, row i = numbps-1-p
+        if (x < (int)h) {
+#pragma unroll 4
+            for (int i = 0; i < np; ++i) Lr[i * 64 + x] = WS[WS_BITS + (size_t)i * 64 + x];
+            Ls[x] = WS[4 * (x & ~3) + WS_N + (x & 3)];
+        }
     }
-    for (uint32_t y = 0; y < B.h; ++y) {
+    __syncthreads();
+    if (x >= (int)B.w) return;
+    const int np = min((int)numbps - bpl, 32);
+    for (uint32_t y = 0; y < h; ++y) {
         int32_t v = 0;
-        if (npasses && numbps) {
+        if (any) {
             uint32_t M = 0;
-            for (int p = (int)numbps - 1; p >= bpl; --p) {
-                uint64_t row = WS[WS_BITS + (size_t)(numbps - 1 - p) * 64 + y];
-                M |= (uint32_t)((row >> x) & 1) << p;
-            }
+            for (int i = 0; i < np; ++i) M |= (uint32_t)((Lr[i * 64 + y] >> x) & 1) << ((int)numbps - 1 - i);
             if (M) {
                 int qq = (t == 0 && (M >> (bpl + 1)) != 0) ? bpl + 1 : bpl;
                 int32_t mag = (int32_t)(((M >> qq) << 1 | 1) << qq);
-                bool ng = (WS[4 * (y & ~3u) + WS_N + (y & 3)] >> x) & 1;
+                bool ng = (Ls[y] >> x) & 1;
                 v = ng ? -mag : mag;
             }
         }
