@@ -1290,23 +1290,34 @@ struct T2Enc {
             rates[L - 1] -= (sot_adjust + 2.0);
             if (rates[L - 1] < rates[L - 2] + 10.0) rates[L - 1] = rates[L - 2] + 20.0;
         }
+        // slope range over every pass of the tile(s), blocks in parallel chunks
+        const auto ta0 = std::chrono::steady_clock::now();
+        const uint32_t schunk = 2048, nsch = (b1 - b0 + schunk - 1) / schunk;
+        std::vector<double> smin(nsch, 1.7976931348623157e308), smax(nsch, -1);
+        host_pool().run(nsch, [&](size_t ci) {
+            double mn = 1.7976931348623157e308, mx = -1;
+            const uint32_t bend = std::min<uint32_t>(b1, b0 + (uint32_t)(ci + 1) * schunk);
+            for (uint32_t b = b0 + (uint32_t)ci * schunk; b < bend; ++b)
+                for (uint32_t q = 0; q < npasses(b); ++q) {
+                    int32_t dr; double dd;
+                    if (q == 0) { dr = (int32_t)rate(b, 0); dd = dist(b, 0); }
+                    else { dr = (int32_t)(rate(b, q) - rate(b, q - 1)); dd = dist(b, q) - dist(b, q - 1); }
+                    if (dr == 0) continue;
+                    double sl = dd / dr;
+                    if (sl < mn) mn = sl;
+                    if (sl > mx) mx = sl;
+                }
+            smin[ci] = mn; smax[ci] = mx;
+        });
         double min_slope = 1.7976931348623157e308, max_slope = -1;
-        for (uint32_t b = b0; b < b1; ++b)
-            for (uint32_t q = 0; q < npasses(b); ++q) {
-                int32_t dr; double dd;
-                if (q == 0) { dr = (int32_t)rate(b, 0); dd = dist(b, 0); }
-                else { dr = (int32_t)(rate(b, q) - rate(b, q - 1)); dd = dist(b, q) - dist(b, q - 1); }
-                if (dr == 0) continue;
-                double sl = dd / dr;
-                if (sl < min_slope) min_slope = sl;
-                if (sl > max_slope) max_slope = sl;
-            }
+        for (uint32_t ci = 0; ci < nsch; ++ci) { min_slope = std::min(min_slope, smin[ci]); max_slope = std::max(max_slope, smax[ci]); }
         double upper = max_slope;
         const bool fast = P.tiles.size() == 1 && !getenv("GK_T2_SERIAL_SIM");
         static const bool prof = getenv("GK_PROFILE") != nullptr;
         using clk = std::chrono::steady_clock;
         auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        double t_make = 0, t_sim = 0, t_prep = 0;
+        double t_make = 0, t_sim = 0, t_prep = 0, t_fin = 0;
+        const double t_slopes = msd(ta0, clk::now());
         uint32_t n_it = 0, n_sim = 0;
         if (fast) init_chains();
         static const bool check = getenv("GK_T2_CHECK_SIM") != nullptr;
@@ -1365,11 +1376,11 @@ struct T2Enc {
             } else {
                 make_layer(l, -1.0, true, prev);
             }
-            if (fast && l + 1 < L) finish_layer(l);
+            if (fast && l + 1 < L) { const auto tf = clk::now(); finish_layer(l); t_fin += msd(tf, clk::now()); }
         }
         if (prof)
-            fprintf(stderr, "pcrd: %u bisection steps, %u simulated, %u decided by bounds; make_layer %.2f ms, simulation %.2f ms, bounds setup %.2f ms\n",
-                    n_it, n_sim, n_bound, t_make, t_sim, t_prep);
+            fprintf(stderr, "pcrd: %u bisection steps, %u simulated, %u decided by bounds; make_layer %.2f ms, simulation %.2f ms, bounds setup %.2f ms, "
+                    "slope range %.2f ms, layer snapshots %.2f ms\n", n_it, n_sim, n_bound, t_make, t_sim, t_prep, t_slopes, t_fin);
         if (prof)
             fprintf(stderr, "pcrd code_layer: units %.2f ms, packet lengths %.2f ms (%zu units, %zu packets)\n",
                     prof_code / 1e3, prof_stuff / 1e3, units.size(), chains.size());
@@ -1972,6 +1983,11 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         for (int k = 0; k + 1 < nch; ++k) HIPCHK(hipStreamWaitEvent(st, ctx->xev[3 + k], 0));
     }
     HIPCHK(hipEventRecord(ctx->ev[4], st));
+    // GK_PROFILE=1: host phase times of the encode's T2 (stderr)
+    static const bool eprof = getenv("GK_PROFILE") != nullptr;
+    using eclk = std::chrono::steady_clock;
+    auto ems = [](eclk::time_point a, eclk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto te0 = eclk::now();
     uint32_t* hinfo = (uint32_t*)ctx->hinfo.get(16 * (size_t)nb + 64);
     HIPCHK(hipMemcpyAsync(hinfo + 4 * (size_t)b0, dinfo, 16 * (size_t)nbr, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(hinfo + 4 * (size_t)nb, derr, 32, hipMemcpyDeviceToHost, st));
@@ -1999,8 +2015,19 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     write_main_header(H, P, &tlm_pos);
     const size_t header_size = H.size();
     if (!with_header) H.clear();
+    const auto te1 = eclk::now();
+    if (const char* dp = getenv("GK_DUMP_PASSES")) {   // debug: pass records for tools/pcrd_bench
+        if (FILE* f = fopen(dp, "wb")) {
+            const uint32_t hdr[2] = {nb, npass_total};
+            fwrite(hdr, 4, 2, f);
+            fwrite(hinfo, 16, nb, f);
+            if (hpasses) fwrite(hpasses, sizeof(GkPass), npass_total, f);
+            fclose(f);
+        }
+    }
     T2Enc T2(P, hinfo, hpasses, tb, te);
     T2.allocate(header_size);
+    const auto te2 = eclk::now();
     // segments: (src_off in dbytes, dst_off in codestream, len); host bytes staged after the slots
     std::vector<uint64_t> seg;
     seg.reserve(3 * ((size_t)nb * (ht ? 2 : 1) + 64));
@@ -2103,6 +2130,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     };
     if (par_chains) build_tile_part(tb, tout[0]);   // (its chains use the pool: no nested pool call)
     else host_pool().run(te - tb, [&](size_t q) { build_tile_part(tb + (uint32_t)q, tout[q]); });
+    const auto te3 = eclk::now();
     for (uint32_t t = tb; t < te; ++t) {
         TileOut& O = tout[t - tb];
         const uint64_t psot = O.psot;
@@ -2140,6 +2168,9 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         memcpy(hdrs.data(), J.data(), J.size());
     }
     HIPCHK(hipEventRecord(ctx->ev[5], st));
+    if (eprof)
+        fprintf(stderr, "encode t2: fetch %.2f ms, allocate %.2f ms, packets %.2f ms, segments %.2f ms\n", ems(te0, te1),
+                ems(te1, te2), ems(te2, te3), ems(te3, eclk::now()));
     if (total > cap) { *rc = -2; return total; }
     // ---- device assembly
     if (hdrs.size() > (64u << 20)) throw GkError("packet headers exceed staging");

@@ -28,6 +28,14 @@ int main(int argc, char** argv) {
         }
         info[4 * b + 2] = r;
     }
+    if (argc > 2) {   // pass records dumped by the engine (GK_DUMP_PASSES) for this geometry
+        FILE* f = fopen(argv[2], "rb");
+        uint32_t hdr[2];
+        if (!f || fread(hdr, 4, 2, f) != 2 || hdr[0] != nb) { fprintf(stderr, "bad dump\n"); return 1; }
+        passes.resize(hdr[1]);
+        if (fread(info.data(), 16, nb, f) != nb || fread(passes.data(), sizeof(GkPass), hdr[1], f) != hdr[1]) return 1;
+        fclose(f);
+    }
     printf("blocks %u passes %zu\n", nb, passes.size());
     for (int it = 0; it < 5; ++it) {
         T2Enc T2(P, info.data(), passes.data(), 0, 1);
