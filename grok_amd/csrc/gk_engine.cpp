@@ -804,9 +804,16 @@ struct T2Enc {
     std::vector<TagTree> incl, imsb;
     std::vector<uint8_t> hdr;
     uint32_t b0 = 0, b1 = 0;     // code-blocks of the tiles being written (tiles [tb, te))
+    uint32_t t0 = 0, t1 = 0;     // those tiles; rate control runs on one tile (t1 == t0 + 1)
+    bool serial = false;         // run on the calling thread (tiles allocated in parallel)
+    template <class F> void prun(size_t n, const F& f) {
+        if (serial) { for (size_t i = 0; i < n; ++i) f(i); return; }
+        prun(n, f);
+    }
     T2Enc(const Plan& plan, const uint32_t* inf, const GkPass* ps, uint32_t tb, uint32_t te)
         : P(plan), info(inf), passes(ps), L(plan.p.nlayers) {
         size_t nb = P.blocks.size();
+        t0 = tb; t1 = te;
         b0 = P.tiles[tb].b0; b1 = P.tiles[te - 1].b1;
         lnp.assign(nb * L, 0); inprev.assign(nb, 0); nlb.assign(nb, 0);
         incl.resize(P.ntrees); imsb.resize(P.ntrees);
@@ -935,7 +942,7 @@ struct T2Enc {
         for (uint32_t l = 0; l < max_layers; ++l)
             for (uint32_t r = 0; r < P.p.numres; ++r)
                 for (uint32_t c = 0; c < P.nc; ++c) {
-                    const ResG& R = P.tiles[0].comps[c].res[r];   // rate control: single tile
+                    const ResG& R = P.tiles[t0].comps[c].res[r];   // rate control: one tile
                     for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi)
                         if (!write_packet(R, pi, l, bp, nullptr)) return false;
                 }
@@ -967,7 +974,7 @@ struct T2Enc {
     std::vector<uint64_t> csize, chdr;
     void init_chains() {
         chains.clear(); units.clear();
-        const TileG& T = P.tiles[0];
+        const TileG& T = P.tiles[t0];
         for (uint32_t r = 0; r < P.p.numres; ++r)
             for (uint32_t c = 0; c < P.nc; ++c)
                 for (uint32_t pi = 0; pi < T.comps[c].res[r].pw * T.comps[c].res[r].ph; ++pi) chains.push_back({c, r, pi});
@@ -1043,13 +1050,13 @@ struct T2Enc {
     }
     const PrecG& unit_prec(const Unit& U, uint32_t* numbps = nullptr) const {
         const Chain& ch = chains[U.chain];
-        const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
+        const ResG& R = P.tiles[t0].comps[ch.c].res[ch.r];
         if (numbps) *numbps = R.bands[U.band].numbps;
         return R.prc[U.band][ch.pi];
     }
     void code_layer(uint32_t l) {   // every (packet, band) of layer l from the snapshot, in parallel
         const auto tc0 = std::chrono::steady_clock::now();
-        host_pool().run(uorder.size(), [&](size_t j) {
+        prun(uorder.size(), [&](size_t j) {
             const uint32_t u = uorder[j];
             const Unit& U = units[u];
             uint32_t numbps;
@@ -1066,7 +1073,7 @@ struct T2Enc {
             ubody[u] = band_body(PG, l);
         });
         const auto tc2 = std::chrono::steady_clock::now();
-        host_pool().run(chains.size(), [&](size_t i) {
+        prun(chains.size(), [&](size_t i) {
             thread_local std::vector<uint64_t> sbuf;
             uint64_t body = 0;
             for (uint32_t u : cunits[i]) body += ubody[u];
@@ -1086,7 +1093,7 @@ struct T2Enc {
             const std::vector<uint8_t> sim_nlb = nlb;
             for (size_t i = 0; i < chains.size(); ++i) {
                 const Chain& ch = chains[i];
-                const ResG& R = P.tiles[0].comps[ch.c].res[ch.r];
+                const ResG& R = P.tiles[t0].comps[ch.c].res[ch.r];
                 if (l) for (uint32_t u : cunits[i]) restore_band(R.prc[units[u].band][ch.pi]);
                 uint64_t body = 0;
                 write_packet(R, ch.pi, l, nullptr, nullptr, hb, &body);
@@ -1170,7 +1177,7 @@ struct T2Enc {
     std::vector<uint64_t> clo, chi, cbody;   // per packet: header byte bounds, body bytes
     int decide(uint32_t l, uint64_t max_bytes, const std::vector<uint16_t>& prev) {
         if (max_bytes == 0xffffffffull) return 1;
-        host_pool().run(uorder.size(), [&](size_t j) {
+        prun(uorder.size(), [&](size_t j) {
             const uint32_t u = uorder[j];
             const PrecG& PG = unit_prec(units[u]);
             const std::vector<int32_t>& par = incl[PG.tree].parent;
@@ -1230,7 +1237,7 @@ struct T2Enc {
         const uint32_t chunk = 2048, nch = (b1 - b0 + chunk - 1) / chunk;
         if (mref.size() != nb) { mref.assign(nb, 0.0); mrad.assign(nb, -1.0); }
         std::vector<uint64_t> hs(nch, 0);
-        host_pool().run(nch, [&](size_t ci) {
+        prun(nch, [&](size_t ci) {
         uint64_t hsum = 0;
         const uint32_t bend = std::min<uint32_t>(b1, b0 + (uint32_t)(ci + 1) * chunk);
         for (uint32_t b = b0 + (uint32_t)ci * chunk; b < bend; ++b) {
@@ -1280,9 +1287,13 @@ struct T2Enc {
         }
         // updateRates: compression ratio -> cumulative byte budget per layer
         double rates[GK_MAX_LAYERS];
-        const double size_pixel = (double)P.nc * P.prec, npix = (double)P.w * P.h;
+        // per tile (CodeStreamCompress.cpp:965-1024): budgets from the tile's pixel count, the header
+        // bytes before the first tile shared by area
+        if (t1 != t0 + 1) throw GkError("rate control runs on one tile at a time");
+        const TileG& TT = P.tiles[t0];
+        const double size_pixel = (double)P.nc * P.prec, npix = (double)((uint64_t)(TT.x1 - TT.x0) * (TT.y1 - TT.y0));
         for (uint32_t k = 0; k < L; ++k) rates[k] = P.p.rates[k] > 0.0 ? (size_pixel * npix) / (P.p.rates[k] * 8.0) : 0.0;
-        const double sot_adjust = (npix * (double)header_size) / npix;
+        const double sot_adjust = (npix * (double)header_size) / ((double)P.w * (double)P.h);
         if (rates[0] > 0.0) { rates[0] -= sot_adjust; if (rates[0] < 30.0f) rates[0] = 30.0f; }
         for (uint32_t k = 1; k + 1 < L; ++k)
             if (rates[k] > 0.0) { rates[k] -= sot_adjust; if (rates[k] < rates[k - 1] + 10.0) rates[k] = rates[k - 1] + 20.0; }
@@ -1294,7 +1305,7 @@ struct T2Enc {
         const auto ta0 = std::chrono::steady_clock::now();
         const uint32_t schunk = 2048, nsch = (b1 - b0 + schunk - 1) / schunk;
         std::vector<double> smin(nsch, 1.7976931348623157e308), smax(nsch, -1);
-        host_pool().run(nsch, [&](size_t ci) {
+        prun(nsch, [&](size_t ci) {
             double mn = 1.7976931348623157e308, mx = -1;
             const uint32_t bend = std::min<uint32_t>(b1, b0 + (uint32_t)(ci + 1) * schunk);
             for (uint32_t b = b0 + (uint32_t)ci * schunk; b < bend; ++b)
@@ -1312,7 +1323,7 @@ struct T2Enc {
         double min_slope = 1.7976931348623157e308, max_slope = -1;
         for (uint32_t ci = 0; ci < nsch; ++ci) { min_slope = std::min(min_slope, smin[ci]); max_slope = std::max(max_slope, smax[ci]); }
         double upper = max_slope;
-        const bool fast = P.tiles.size() == 1 && !getenv("GK_T2_SERIAL_SIM");
+        const bool fast = t1 == t0 + 1 && !getenv("GK_T2_SERIAL_SIM");
         static const bool prof = getenv("GK_PROFILE") != nullptr;
         using clk = std::chrono::steady_clock;
         auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1747,8 +1758,6 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     if (want.p.cblk_sty != 0 && want.p.cblk_sty != 0x40) throw GkError("code-block style mode switches are not supported");
     if (want.p.ht() && want.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
     if (want.p.ht() && want.p.rate_control()) throw GkError("HTJ2K with rate control is not supported on this path yet");
-    if (want.p.tw && want.p.th && (want.p.tw < want.w || want.p.th < want.h) && want.p.rate_control())
-        throw GkError("rate control with more than one tile is not supported on this path yet");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if (want.prec == 0 || want.prec > 31) throw GkError("component precision must be 1..31 bits");
     if (want.w == 0 || want.h == 0) throw GkError("empty image");
@@ -2013,7 +2022,9 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     H.reserve(1 << 12);
     size_t tlm_pos = 0;
     write_main_header(H, P, &tlm_pos);
-    const size_t header_size = H.size();
+    // updateRates' header bytes: the stream position after the main header (JP2 boxes and the
+    // jp2c box header come first in a .jp2), CodeStreamCompress.cpp:963
+    const size_t rc_header_size = H.size() + (P.p.jp2 ? jp2_prefix_size(P) : 0);
     if (!with_header) H.clear();
     const auto te1 = eclk::now();
     if (const char* dp = getenv("GK_DUMP_PASSES")) {   // debug: pass records for tools/pcrd_bench
@@ -2026,7 +2037,23 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         }
     }
     T2Enc T2(P, hinfo, hpasses, tb, te);
-    T2.allocate(header_size);
+    if (te - tb == 1 || !P.p.rate_control()) T2.allocate(rc_header_size);
+    else {
+        // rate control per tile (TileProcessor::pcrdBisectSimple runs per tile): many tiles run
+        // side by side on one thread each, a few run one after the other on the whole pool
+        const bool par = te - tb >= host_pool().size();
+        auto one = [&](size_t q) {
+            const uint32_t t = tb + (uint32_t)q;
+            T2Enc Tt(P, hinfo, hpasses, t, t + 1);
+            Tt.serial = par;
+            Tt.allocate(rc_header_size);
+            const TileG& TG = P.tiles[t];
+            std::copy(Tt.lnp.begin() + (size_t)TG.b0 * T2.L, Tt.lnp.begin() + (size_t)TG.b1 * T2.L,
+                      T2.lnp.begin() + (size_t)TG.b0 * T2.L);
+        };
+        if (par) host_pool().run(te - tb, one);
+        else for (uint32_t q = 0; q < te - tb; ++q) one(q);
+    }
     const auto te2 = eclk::now();
     // segments: (src_off in dbytes, dst_off in codestream, len); host bytes staged after the slots
     std::vector<uint64_t> seg;

@@ -1726,13 +1726,16 @@ static void make_layer(EncodeState& E, uint32_t layno, double thresh, bool final
     });
 }
 
-// CodeStreamCompress::updateRates: compression ratios -> cumulative byte budgets
+// CodeStreamCompress::updateRates (:951-1025): compression ratios -> cumulative byte budgets of
+// the tile, from its pixel count; the SOT adjustment shares the header bytes written before the
+// first tile (JP2 boxes, jp2c box header, main header: the stream position) by tile area.
 static void update_rates(const EncodeState& E, double* rates) {
     const Params& p = E.p;
-    double size_pixel = (double)E.im.nc * E.im.prec, npix = (double)E.im.w * E.im.h, bits_empty = 8.0;
+    const double size_pixel = (double)E.im.nc * E.im.prec, bits_empty = 8.0;
+    const double npix = (double)((uint64_t)(E.tx1 - E.tx0) * (E.ty1 - E.ty0));
     for (uint32_t k = 0; k < p.nlayers; ++k)
         rates[k] = p.rates[k] > 0.0 ? (size_pixel * npix) / (p.rates[k] * bits_empty) : 0.0;
-    double sot_adjust = (npix * (double)E.header_size) / npix;
+    double sot_adjust = (npix * (double)E.header_size) / ((double)E.im.w * (double)E.im.h);
     uint32_t k = 0;
     if (rates[0] > 0.0) { rates[0] -= sot_adjust; if (rates[0] < 30.0f) rates[0] = 30.0f; }
     for (k = 1; k + 1 < p.nlayers; ++k)
@@ -1873,15 +1876,22 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
             std::vector<uint8_t>().swap(parts[t]);
         }
         put16(o, 0xffd9);
-    } else
+    } else {
+    size_t header_size = 0;
     for (uint32_t t = 0;; ++t) {
         EncodeState E;
         prepare_encode(E, planes, w, h, nc, prec, sgnd, cp, t);
         if (t == 0) {
             nt = tile_count(E.p, w, h);
             write_main_header(o, E.im, E.p, E.comps[0], &tlm_pos);
+            header_size = o.size();   // updateRates runs once, after the main header
+            if (cp && cp->cod_format == 2) {
+                std::vector<uint8_t> J0;
+                jp2_prefix(J0, w, h, nc, prec, sgnd, 0);
+                header_size += J0.size();
+            }
         }
-        E.header_size = o.size();   // updateRates' SOT adjustment (single-tile semantics)
+        E.header_size = header_size;
         t1_encode_all(E);
         rate_allocate(E);
         uint32_t psot = write_tile_part(o, E);
@@ -1891,6 +1901,7 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
             o[q + 2] = (uint8_t)(psot >> 24); o[q + 3] = (uint8_t)(psot >> 16); o[q + 4] = (uint8_t)(psot >> 8); o[q + 5] = (uint8_t)psot;
         }
         if (t + 1 >= nt) { put16(o, 0xffd9); break; }
+    }
     }
     std::vector<uint8_t> J;
     if (cp && cp->cod_format == 2) jp2_prefix(J, w, h, nc, prec, sgnd, o.size());

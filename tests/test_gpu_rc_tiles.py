@@ -1,0 +1,120 @@
+"""Rate control (PCRD layers) on tiled images and in .jp2 files, HIP path vs the oracle.
+
+Grok runs the PCRD bisection per tile (TileProcessor::pcrdBisectSimple,
+TileProcessor.cpp:1196-1357): each tile's layer budgets come from its own pixel count, and
+the header bytes written before the first tile (JP2 boxes + jp2c box header + main header:
+the stream position when CodeStreamCompress::updateRates runs, :951-1025) are shared among
+the tiles by area.  The engine allocates each tile with its own T2 state (in parallel when
+there are many tiles); the oracle restates the same rule tile by tile.
+
+Parity: byte-identical codestreams to the oracle.  Multi-tile rate control and .jp2 + rate
+control are pinned by the oracle's restatement of updateRates only: no Grok fixture holds
+such a stream (the single-tile `-r` fixture rgb12_97_r pins the single-tile budget rule).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import grok_amd as G
+    e = G.Engine(0)
+    yield e
+    e.close()
+
+
+def _params(**kw):
+    import grok_amd as G
+    numres = kw.pop("numres", 6)
+    if "layer_rate" in kw:
+        kw["numlayers"] = len(kw["layer_rate"])
+    return G.default_params(numresolution=numres, **kw)
+
+
+def _img(seed, c, h, w, bits):
+    from grok_amd.synth import synth_image
+    return synth_image(h, w, c, bits, seed).astype(np.int32)
+
+
+CASES = [
+    # (seed, comps, h, w, bits, kw)
+    (1, 3, 256, 256, 12, dict(irreversible=True, layer_rate=[40.0, 20.0, 10.0], tiles=(128, 128))),
+    (2, 3, 200, 330, 8, dict(irreversible=True, layer_rate=[30.0, 8.0], tiles=(128, 64), tlm=True, plt=True)),
+    (3, 1, 300, 260, 16, dict(layer_rate=[20.0, 5.0, 0.0], tiles=(64, 128), numres=4)),
+    (4, 3, 192, 192, 8, dict(irreversible=True, layer_rate=[12.0], tiles=(64, 64), cblk=(32, 32), numres=5)),
+    (5, 3, 160, 520, 12, dict(irreversible=True, layer_rate=[50.0, 25.0, 12.0, 0.0], tiles=(256, 32), numres=3)),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[str(c[0]) for c in CASES])
+def test_tiled_rate_control_vs_oracle(eng, case):
+    seed, c, h, w, bits, kw = case
+    img = _img(40 + seed, c, h, w, bits)
+    ref = O.encode(img, bits, **kw)
+    cs = eng.encode(img, bits, params=_params(**dict(kw)))
+    assert cs == ref
+    dec_o, _ = O.decode(cs)
+    dec = eng.decode(cs)
+    if kw.get("irreversible"):
+        assert np.abs(dec.astype(np.int64) - dec_o).max() <= 1
+    else:
+        np.testing.assert_array_equal(dec, dec_o)
+
+
+def test_many_tiles_rate_control_parallel(eng):
+    # more tiles than host threads: tiles are allocated side by side, one thread each
+    img = _img(90, 3, 384, 384, 8)
+    kw = dict(irreversible=True, layer_rate=[40.0, 10.0], tiles=(32, 32), numres=3, cblk=(16, 16))
+    assert eng.encode(img, 8, params=_params(**dict(kw))) == O.encode(img, 8, **kw)
+
+
+def test_tiled_rate_control_budgets(eng):
+    # each tile's layers fit its own budget: the tile part (minus its SOT/SOD markers) stays
+    # within the last layer's rate
+    img = _img(77, 3, 256, 256, 12)
+    kw = dict(irreversible=True, layer_rate=[40.0, 20.0], tiles=(128, 128))
+    cs = eng.encode(img, 12, params=_params(**dict(kw)))
+    pos = cs.find(b"\xff\x90")
+    sizes = []
+    while pos >= 0 and pos + 10 <= len(cs):
+        psot = int.from_bytes(cs[pos + 6:pos + 10], "big")
+        sizes.append(psot)
+        pos = pos + psot if cs[pos + psot:pos + psot + 2] == b"\xff\x90" else -1
+    assert len(sizes) == 4
+    budget = 3 * 12 * 128 * 128 / (20.0 * 8)
+    assert all(s - 14 <= budget for s in sizes), (sizes, budget)
+
+
+@pytest.mark.parametrize("tiles", [None, (128, 128)])
+def test_jp2_rate_control_vs_oracle(eng, tiles):
+    # .jp2: the boxes before the codestream count in updateRates' header size
+    img = _img(55, 3, 256, 256, 12)
+    kw = dict(irreversible=True, layer_rate=[40.0, 20.0, 10.0], jp2=True)
+    if tiles:
+        kw["tiles"] = tiles
+    ref = O.encode(img, 12, **kw)
+    assert ref[4:8] == b"jP  "
+    assert eng.encode(img, 12, params=_params(**dict(kw))) == ref
+
+
+def test_sharded_tile_rows_with_rate_control(eng):
+    # per-tile budgets make a tile-row shard's parts equal to the one-shot encode's
+    from grok_amd import shard
+    img = _img(66, 3, 256, 192, 8)
+    kw = dict(irreversible=True, layer_rate=[30.0, 10.0], tiles=(64, 64), tlm=True)
+    full = eng.encode(img, 8, params=_params(**dict(kw)))
+    assert full == O.encode(img, 8, **kw)
+    _, h, w = img.shape
+    ntx, nty = shard.tile_grid(h, w, 64, 64)
+    parts = []
+    for r in range(2):
+        tb, te, j0, j1 = shard.rank_tiles(ntx, nty, r, 2)
+        y0, y1 = j0 * 64, min(h, j1 * 64)
+        blob, lens = eng.encode_tiles(img[:, y0:y1], 8, tb, te, image_hw=(h, w), row0=y0, params=_params(**dict(kw)))
+        parts += shard.split_parts(blob, lens, tb)
+    header, tlm, _ = eng.main_header(img.shape, 8, params=_params(**dict(kw)))
+    assert shard.assemble(header, tlm, parts) == full
