@@ -829,7 +829,9 @@ struct T2Enc {
         if (q + 1 == npasses(b)) return info[4 * (size_t)b + 2];
         return passes[info[4 * (size_t)b + 3] + q].rate;
     }
-    double dist(uint32_t b, uint32_t q) const { return passes[info[4 * (size_t)b + 3] + q].dist; }
+    // HT code-blocks have one pass and no distortion record (T1HT::compress sets only its
+    // rate; CodePass zero-initialises distortiondec, Codeblock.h:47)
+    double dist(uint32_t b, uint32_t q) const { return passes ? passes[info[4 * (size_t)b + 3] + q].dist : 0.0; }
     // The pass records (tens of MB) are read one or two per code-block in block order, each
     // a cache miss: prefetch those of the block PF ahead (its first pass not yet in packets
     // and the last one layer l would take).
@@ -1757,7 +1759,6 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     if (want.nc < 3) want.p.mct = 0;
     if (want.p.cblk_sty != 0 && want.p.cblk_sty != 0x40) throw GkError("code-block style mode switches are not supported");
     if (want.p.ht() && want.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
-    if (want.p.ht() && want.p.rate_control()) throw GkError("HTJ2K with rate control is not supported on this path yet");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if (want.prec == 0 || want.prec > 31) throw GkError("component precision must be 1..31 bits");
     if (want.w == 0 || want.h == 0) throw GkError("empty image");
@@ -2005,7 +2006,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     if (t1err) throw GkError(t1err & 2 ? "T1 symbol buffer overflow" : "T1 code-block slot overflow");
     const bool ht = P.p.ht();
     const GkPass* hpasses = nullptr;
-    if (do_rc) {
+    if (do_rc && !ht) {
         GkPass* hp = (GkPass*)ctx->hpasses.get(sizeof(GkPass) * (size_t)std::max(npass_total, 1u));
         HIPCHK(hipMemcpyAsync(hp, dps, sizeof(GkPass) * (size_t)npass_total, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));

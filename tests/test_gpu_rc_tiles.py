@@ -118,3 +118,18 @@ def test_sharded_tile_rows_with_rate_control(eng):
         parts += shard.split_parts(blob, lens, tb)
     header, tlm, _ = eng.main_header(img.shape, 8, params=_params(**dict(kw)))
     assert shard.assemble(header, tlm, parts) == full
+
+
+@pytest.mark.parametrize("tiles", [None, (64, 64)])
+def test_ht_rate_control_vs_oracle(eng, tiles):
+    # HTJ2K code-blocks carry one pass and no distortion record (T1HT::compress), so every
+    # slope is 0: the bisection's first threshold (0) puts each block whole into layer 0 and
+    # the later layers stay empty (TileProcessor.cpp:1303-1343, makeLayerSimple :1389-1392)
+    img = _img(33, 3, 192, 160, 8)
+    kw = dict(cblk_sty=64, layer_rate=[20.0, 10.0])
+    if tiles:
+        kw["tiles"] = tiles
+    ref = O.encode(img, 8, **kw)
+    cs = eng.encode(img, 8, params=_params(**dict(kw)))
+    assert cs == ref
+    np.testing.assert_array_equal(eng.decode(cs), img)
