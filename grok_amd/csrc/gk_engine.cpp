@@ -808,7 +808,7 @@ struct T2Enc {
     bool serial = false;         // run on the calling thread (tiles allocated in parallel)
     template <class F> void prun(size_t n, const F& f) {
         if (serial) { for (size_t i = 0; i < n; ++i) f(i); return; }
-        prun(n, f);
+        host_pool().run(n, f);
     }
     T2Enc(const Plan& plan, const uint32_t* inf, const GkPass* ps, uint32_t tb, uint32_t te)
         : P(plan), info(inf), passes(ps), L(plan.p.nlayers) {

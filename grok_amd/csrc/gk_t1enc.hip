@@ -63,11 +63,10 @@ struct CmLds {
     uint8_t zc[512];
     uint8_t sc[256];
 };
-// Rate-control extras: the block's magnitudes (row-major, for per-sample
-// distortion lookups) and the nmsedec tables (t1_generate_luts.cpp:338-362:
-// sig, sig0, ref, ref0; 128 entries each, built on the host).
+// Rate-control extras: the nmsedec tables (t1_generate_luts.cpp:338-362: sig, sig0, ref,
+// ref0; 128 entries each, built on the host).  The magnitudes the lookups index stay in the
+// lane's registers: a pass's samples are summed after it from a 64-row mask.
 struct CmRcLds {
-    uint32_t mag[64][64];
     int16_t nm[4][128];
 };
 
@@ -114,7 +113,6 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
         m[y] = a;
         mx = a > mx ? a : mx;
         negcol |= (uint64_t)(v < 0) << y;
-        if constexpr (RC) R.mag[y][lane] = a;
     }
     if constexpr (RC) {
         for (int i = lane; i < 512; i += 64) R.nm[i >> 7][i & 127] = nmse_tab[i];
@@ -141,13 +139,19 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
     uint64_t sig = 0, mu = 0;
     uint32_t pos = 0, passno = 0;
     int32_t acc = 0;   // RC: this lane's nmsedec for the current pass
-    auto nm_sig = [&](uint32_t y, int bp) -> int32_t {
-        if constexpr (RC) { uint32_t x = R.mag[y][lane]; return bp > 0 ? R.nm[0][(x >> bp) & 127] : R.nm[1][x & 127]; }
-        return 0;
-    };
-    auto nm_ref = [&](uint32_t y, int bp) -> int32_t {
-        if constexpr (RC) { uint32_t x = R.mag[y][lane]; return bp > 0 ? R.nm[2][(x >> bp) & 127] : R.nm[3][x & 127]; }
-        return 0;
+    // RC: nmsedec of the rows in mask (getnmsedec_sig: table 0/1, getnmsedec_ref: table 2/3)
+    auto nm_rows = [&](uint64_t mask, int t, int bp) __attribute__((always_inline)) {
+        if constexpr (RC) {
+            if (bp > 0) {
+#pragma unroll
+                for (int y = 0; y < 64; ++y)
+                    if ((mask >> y) & 1) acc += R.nm[t][(m[y] >> bp) & 127];
+            } else {
+#pragma unroll
+                for (int y = 0; y < 64; ++y)
+                    if ((mask >> y) & 1) acc += R.nm[t + 1][m[y] & 127];
+            }
+        }
     };
     auto end_pass = [&]() {
         if (lane == 0) PE[passno] = pos;
@@ -218,10 +222,8 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                 pos += total;
                 sig |= (uint64_t)ns << sh;
                 vis |= (uint64_t)cd << sh;
-                if constexpr (RC) {
-                    for (int r = 0; r < 4; ++r) if ((ns >> r) & 1) acc += nm_sig(sh + r, bpno);
-                }
             }
+            nm_rows(sig & ~sigPrev, 0, bpno);
             end_pass();
             // ================= magnitude refinement pass =================
             for (uint32_t s = 0; s < nstripes; ++s) {
@@ -244,14 +246,13 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                     }
                 }
                 pos += total;
-                if constexpr (RC) {
-                    for (int r = 0; r < 4; ++r) if ((mr >> r) & 1) acc += nm_ref(sh + r, bpno);
-                }
             }
+            nm_rows(sigPrev, 2, bpno);
             mu |= sigPrev;
             end_pass();
         }
         // ================= cleanup pass =================
+        const uint64_t sigCu = sig;
         for (uint32_t s = 0; s < nstripes; ++s) {
             const uint32_t sh = 4 * s;
             const uint32_t Wc = win6(sig, s), Nc = win6(negcol, s);
@@ -307,10 +308,8 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
             }
             pos += total;
             sig |= (uint64_t)nc << sh;
-            if constexpr (RC) {
-                for (int r = 0; r < 4; ++r) if ((nc >> r) & 1) acc += nm_sig(sh + r, bpno);
-            }
         }
+        nm_rows(sig & ~sigCu, 0, bpno);
         end_pass();
     }
     if (lane == 0) { cm_info[2 * b] = numbps; cm_info[2 * b + 1] = passno; }
