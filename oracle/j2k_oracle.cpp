@@ -509,6 +509,46 @@ struct MqEnc {
         if (B(bp) != 0xff) ++bp;
     }
     uint32_t numbytes() const { return (uint32_t)bp; }  // wraps for bp == -1 as in the reference
+    // ---- mode switches (mqc_enc.cpp:229-330).  In raw (bypass) mode bp indexes the next byte
+    // to write; BYPASS_CT_INIT marks "no raw bit written yet" (mqc_inl.h:24).
+    static constexpr uint32_t CT_INIT = 0xDEADBEEFu;
+    void bypass_init() { c = 0; ct = CT_INIT; }                                 // :229-246
+    void bypass_encode(uint32_t d) {                                           // mqc_enc_inl.h:104-124
+        if (ct == CT_INIT) ct = 8;
+        --ct;
+        c += d << ct;
+        if (ct == 0) {
+            B(bp) = (uint8_t)c;
+            ct = (B(bp) == 0xff) ? 7 : 8;
+            ++bp; c = 0;
+        }
+    }
+    uint32_t bypass_extra_bytes(bool erterm) {                                 // :247-250
+        return (ct < 7 || (ct == 7 && (erterm || B(bp - 1) != 0xff))) ? 2 : 1;
+    }
+    void bypass_flush(bool erterm) {                                           // :251-292
+        if (ct < 7 || (ct == 7 && (erterm || B(bp - 1) != 0xff))) {
+            uint32_t bit = 0;
+            while (ct > 0) { --ct; c += bit << ct; bit = 1 - bit; }
+            B(bp) = (uint8_t)c;
+            ++bp;
+        } else if (ct == 7 && B(bp - 1) == 0xff) {
+            --bp;
+        } else if (ct == 8 && !erterm && B(bp - 1) == 0x7f && B(bp - 2) == 0xff) {
+            bp -= 2;
+        }
+    }
+    void restart_init() {                                                      // :294-310
+        a = 0x8000; c = 0; ct = 12;
+        --bp;
+        if (B(bp) == 0xff) ct = 13;
+    }
+    void erterm() {                                                            // :312-325
+        int32_t k = (int32_t)(11 - ct + 1);
+        while (k > 0) { c <<= ct; ct = 0; byteout(); k -= (int32_t)ct; }
+        if (B(bp) != 0xff) byteout();
+    }
+    void segmark() { for (uint32_t i = 1; i < 5; ++i) encode(CTX_UNI, i % 2); }   // :327-330
 };
 
 struct MqDec {
@@ -534,6 +574,17 @@ struct MqDec {
         c = (uint32_t)(((n == 0) ? 0xff : at(0)) << 16);
         bytein();
         c <<= 7; ct -= 7; a = 0x8000;
+    }
+    void raw_init(const uint8_t* b, uint32_t n) { buf = b; len = n; bp = 0; c = 0; ct = 0; }   // mqc_dec.cpp:108-113
+    uint32_t raw_decode() {                                                    // mqc_dec_inl.h:61-91
+        if (ct == 0) {
+            if (c == 0xff) {
+                if (at(bp) > 0x8f) { c = 0xff; ct = 8; }
+                else { c = at(bp); ++bp; ct = 7; }
+            } else { c = at(bp); ++bp; ct = 8; }
+        }
+        --ct;
+        return (c >> ct) & 1u;
     }
     void renorm() { do { if (ct == 0) bytein(); a <<= 1; c <<= 1; --ct; } while (a < 0x8000); }
     uint32_t decode(int cx) {
@@ -594,27 +645,33 @@ static void sc_ctx(int H, int V, int& ctx, int& xorbit) {
 // into 32-bit flag words per 4-row column, T1.cpp:45-130).
 enum { S_SIG = 1, S_NEG = 2, S_PI = 4, S_MU = 8 };
 
+// VSC (GRK_CBLKSTY_VSC): a stripe's first row does not update the flags of the row above it
+// (update_flags, T1.cpp:209-232, `ci == 0 && !vsc`), i.e. the last row of a stripe sees the
+// next stripe's samples as insignificant.
 struct T1State {
     uint32_t w, h, sw;  // sw = w + 2
+    bool vsc = false;
     std::vector<uint8_t> s;
-    void init(uint32_t W, uint32_t H) { w = W; h = H; sw = W + 2; s.assign((size_t)(W + 2) * (H + 2), 0); }
+    void init(uint32_t W, uint32_t H, bool VSC = false) { w = W; h = H; sw = W + 2; vsc = VSC; s.assign((size_t)(W + 2) * (H + 2), 0); }
     uint8_t& at(int x, int y) { return s[(size_t)(y + 1) * sw + (x + 1)]; }
     uint8_t get(int x, int y) const { return s[(size_t)(y + 1) * sw + (x + 1)]; }
+    // neighbour (xx, yy) of sample row y
+    uint8_t nbr(int xx, int yy, int y) const { return (vsc && yy == y + 1 && (y & 3) == 3) ? 0 : get(xx, yy); }
     void counts(int x, int y, int& hh, int& vv, int& dd) const {
-        auto sg = [&](int xx, int yy) { return (get(xx, yy) & S_SIG) ? 1 : 0; };
+        auto sg = [&](int xx, int yy) { return (nbr(xx, yy, y) & S_SIG) ? 1 : 0; };
         hh = sg(x - 1, y) + sg(x + 1, y);
         vv = sg(x, y - 1) + sg(x, y + 1);
         dd = sg(x - 1, y - 1) + sg(x + 1, y - 1) + sg(x - 1, y + 1) + sg(x + 1, y + 1);
     }
     bool any_sig_nbr(int x, int y) const { int a, b, c; counts(x, y, a, b, c); return (a + b + c) != 0; }
-    int contrib(int x, int y) const {
-        uint8_t v = get(x, y);
+    int contrib(int x, int y, int yc) const {
+        uint8_t v = nbr(x, y, yc);
         if (!(v & S_SIG)) return 0;
         return (v & S_NEG) ? -1 : 1;
     }
     void sign_ctx(int x, int y, int& ctx, int& xorbit) const {
-        int H = contrib(x - 1, y) + contrib(x + 1, y);
-        int V = contrib(x, y - 1) + contrib(x, y + 1);
+        int H = contrib(x - 1, y, y) + contrib(x + 1, y, y);
+        int V = contrib(x, y - 1, y) + contrib(x, y + 1, y);
         H = std::max(-1, std::min(1, H)); V = std::max(-1, std::min(1, V));
         sc_ctx(H, V, ctx, xorbit);
     }
@@ -622,8 +679,8 @@ struct T1State {
 
 // ----------------------------------------------------------------------------
 // T1 encoder (T1.cpp:498-932 enc_sigpass / enc_refpass / enc_clnpass /
-// compress_cblk; T1Part1.cpp:36-127 preCompress).  Default code-block style
-// (no mode switches): one terminated segment, the last cleanup pass.
+// compress_cblk; T1Part1.cpp:36-127 preCompress), with the code-block style mode
+// switches (BYPASS/LAZY, RESET, TERMALL, VSC, PTERM, SEGSYM; mqc_enc.cpp:229-330).
 // coef: SMR magnitudes already shifted by T1_NMSEDEC_FRACBITS (6).
 // ----------------------------------------------------------------------------
 static const int FRACBITS = 6;
@@ -663,8 +720,22 @@ static double getwmsedec(int nmsedec, const DistCtx& dc, int bpno) {
     return wm;
 }
 
+// Code-block style bits (grok.h:98-104)
+enum { STY_LAZY = 0x01, STY_RESET = 0x02, STY_TERMALL = 0x04, STY_VSC = 0x08, STY_PTERM = 0x10, STY_SEGSYM = 0x20 };
+
+// T1::enc_is_term_pass (T1.cpp:437-458)
+static bool enc_is_term_pass(uint32_t sty, int numbps, int bpno, int passtype) {
+    if (passtype == 2 && bpno == 0) return true;
+    if (sty & STY_TERMALL) return true;
+    if (sty & STY_LAZY) {
+        if (bpno == numbps - 4 && passtype == 2) return true;   // the 4th cleanup pass
+        if (bpno < numbps - 4 && passtype > 0) return true;     // later MR (raw) and CL (MQ) passes
+    }
+    return false;
+}
+
 static void t1_encode_block(const uint32_t* mag, const uint8_t* neg, uint32_t w, uint32_t h, uint32_t orient,
-                            BlockEncResult& out, const DistCtx* dctx) {
+                            BlockEncResult& out, const DistCtx* dctx, uint32_t sty = 0) {
     uint32_t mx = 0;
     for (uint32_t i = 0; i < w * h; ++i) mx = std::max(mx, mag[i]);
     out.numbps = 0; out.npasses = 0; out.passes.clear(); out.data.clear();
@@ -673,7 +744,7 @@ static void t1_encode_block(const uint32_t* mag, const uint8_t* neg, uint32_t w,
         out.numbps = (t <= (uint32_t)FRACBITS) ? 0 : t - FRACBITS;
     }
     if (out.numbps == 0) return;
-    T1State S; S.init(w, h);
+    T1State S; S.init(w, h, (sty & STY_VSC) != 0);
     // generous buffer: 2-byte left pad (Codeblock.h:156-170)
     std::vector<uint8_t> buf(64 + (size_t)w * h * 4 + (size_t)out.numbps * 3 * 64, 0);
     MqEnc mq; mq.reset_states(); mq.init(buf.data() + 2);
@@ -682,9 +753,16 @@ static void t1_encode_block(const uint32_t* mag, const uint8_t* neg, uint32_t w,
     int bpno = (int)out.numbps - 1;
     int passtype = 2;
     double cum = 0;
+    const int nbp = (int)out.numbps;
     for (uint32_t passno = 0; bpno >= 0; ++passno) {
         uint32_t one = 1u << (bpno + FRACBITS);
         int nmsedec = 0;
+        // BYPASS: SP and MR passes below the 4th bit-plane are raw (T1.cpp:820-824)
+        const bool raw = (sty & STY_LAZY) && bpno < nbp - 4 && passtype < 2;
+        if (passno > 0 && out.passes[passno - 1].term) {   // T1.cpp:826-833
+            if (raw) mq.bypass_init(); else mq.restart_init();
+        }
+        auto code = [&](int cx, uint32_t d) { if (raw) mq.bypass_encode(d); else mq.encode(cx, d); };
         auto bit = [&](uint32_t x, uint32_t y) { return (mag[y * w + x] & one) ? 1u : 0u; };
         if (passtype == 0) {            // significance propagation
             for (uint32_t k = 0; k < h; k += 4)
@@ -695,12 +773,12 @@ static void t1_encode_block(const uint32_t* mag, const uint8_t* neg, uint32_t w,
                         int hh, vv, dd; S.counts(x, y, hh, vv, dd);
                         if (hh + vv + dd == 0) continue;
                         uint32_t v = bit(x, y);
-                        mq.encode(CTX_ZC + zc_ctx(orient, hh, vv, dd), v);
+                        code(CTX_ZC + zc_ctx(orient, hh, vv, dd), v);
                         if (v) {
                             int cx, xb; S.sign_ctx(x, y, cx, xb);
                             uint32_t sg = neg[y * w + x];
                             if (dctx) nmsedec += nmse_sig(mag[y * w + x], bpno);
-                            mq.encode(CTX_SC + cx, sg ^ (uint32_t)xb);
+                            code(CTX_SC + cx, raw ? sg : (sg ^ (uint32_t)xb));   // raw signs are not predicted
                             st |= S_SIG | (sg ? S_NEG : 0);
                         }
                         st |= S_PI;
@@ -713,10 +791,10 @@ static void t1_encode_block(const uint32_t* mag, const uint8_t* neg, uint32_t w,
                         if ((st & (S_SIG | S_PI)) != S_SIG) continue;
                         int cx = (st & S_MU) ? 2 : (S.any_sig_nbr(x, y) ? 1 : 0);
                         if (dctx) nmsedec += nmse_ref(mag[y * w + x], bpno);
-                        mq.encode(CTX_MAG + cx, bit(x, y));
+                        code(CTX_MAG + cx, bit(x, y));
                         st |= S_MU;
                     }
-        } else {                        // cleanup
+        } else {                        // cleanup (always MQ)
             for (uint32_t k = 0; k < h; k += 4)
                 for (uint32_t x = 0; x < w; ++x) {
                     uint32_t ylim = std::min(k + 4, h);
@@ -761,19 +839,23 @@ static void t1_encode_block(const uint32_t* mag, const uint8_t* neg, uint32_t w,
                     }
                     for (uint32_t yy = k; yy < ylim; ++yy) S.at(x, yy) &= (uint8_t)~S_PI;
                 }
+            if (sty & STY_SEGSYM) mq.segmark();
         }
         PassInfo& P = out.passes[passno];
         if (dctx) { cum += getwmsedec(nmsedec, *dctx, bpno); P.dist = cum; } else P.dist = 0;
-        bool term = (passtype == 2 && bpno == 0);   // enc_is_term_pass, T1.cpp:437-458
-        if (term) {
-            mq.flush();
+        if (enc_is_term_pass(sty, nbp, bpno, passtype)) {   // T1.cpp:856-869
+            if (raw) mq.bypass_flush((sty & STY_PTERM) != 0);
+            else if (sty & STY_PTERM) mq.erterm();
+            else mq.flush();
             P.term = 1; P.rate = mq.numbytes();
         } else {
-            uint32_t extra = 4 + 1;                   // T1.cpp:883-896
-            if (mq.ct < 5) extra++;
+            uint32_t extra;                           // T1.cpp:870-897
+            if (raw) extra = mq.bypass_extra_bytes((sty & STY_PTERM) != 0);
+            else { extra = 4 + 1; if (mq.ct < 5) extra++; }
             P.term = 0; P.rate = mq.numbytes() + extra;
         }
         if (++passtype == 3) { passtype = 0; --bpno; }
+        if (sty & STY_RESET) mq.reset_states();
         out.npasses = passno + 1;
     }
     out.passes.resize(out.npasses);
@@ -797,12 +879,24 @@ static void t1_encode_block(const uint32_t* mag, const uint8_t* neg, uint32_t w,
 // uncompressedData before PostDecompressFilters.
 // ----------------------------------------------------------------------------
 // stripe_counts (optional, instrumentation): decisions per (pass, stripe), pass-major.
+// Passes of codeword segment `seg` (T2Decompress::initSegment, T2Decompress.cpp:28-54):
+// TERMALL one pass each; BYPASS 10, then alternately 2 (raw SP + MR) and 1 (MQ CL);
+// otherwise one segment of every pass.
+static uint32_t seg_maxpasses(uint32_t sty, uint32_t seg) {
+    if (sty & STY_TERMALL) return 1;
+    if (sty & STY_LAZY) return seg == 0 ? 10 : ((seg & 1) ? 2 : 1);
+    return 0xffffffffu;
+}
+
+// seglens: byte length of each codeword segment (concatenated in `data`); empty = one
+// segment of `len` bytes.
 static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses, uint32_t numbps,
-                            uint32_t orient, uint32_t w, uint32_t h, int32_t* out, uint32_t* stripe_counts = nullptr) {
+                            uint32_t orient, uint32_t w, uint32_t h, int32_t* out, uint32_t* stripe_counts = nullptr,
+                            uint32_t sty = 0, const std::vector<uint32_t>* seglens = nullptr) {
     std::fill(out, out + (size_t)w * h, 0);
     if (!npasses || !numbps) return;
-    T1State S; S.init(w, h);
-    MqDec mq; mq.reset_states(); mq.init(data, len);
+    T1State S; S.init(w, h, (sty & STY_VSC) != 0);
+    MqDec mq; mq.reset_states();
     const uint32_t ns = (h + 3) / 4;
     auto tick = [&](uint32_t p, uint32_t k) {
         if (stripe_counts) stripe_counts[p * ns + k / 4] = (uint32_t)mq.ndec;
@@ -810,8 +904,20 @@ static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses,
     };
     int bpno1 = (int)numbps;   // bpno_plus_one
     int passtype = 2;
-    for (uint32_t p = 0; p < npasses && bpno1 >= 1; ++p) {
+    uint32_t p = 0, segno = 0, off = 0, seg_left = 0;
+    bool raw = false;
+    for (; p < npasses && bpno1 >= 1; ++p) {
+        if (seg_left == 0) {   // next codeword segment (T1::decompress_cblk, T1.cpp:1380-1400)
+            const uint32_t sl = seglens ? (segno < seglens->size() ? (*seglens)[segno] : 0) : len;
+            const uint32_t sb = std::min(sl, len - std::min(off, len));
+            raw = (sty & STY_LAZY) && bpno1 <= (int)numbps - 4 && passtype < 2;
+            if (raw) mq.raw_init(data + off, sb); else mq.init(data + off, sb);
+            off += sb;
+            seg_left = seg_maxpasses(sty, segno++);
+        }
+        --seg_left;
         int32_t one = 1 << bpno1, half = one >> 1, oph = one | half;
+        auto dec = [&](int cx) { return raw ? mq.raw_decode() : mq.decode(cx); };
         if (passtype == 0) {
             for (uint32_t k = 0; k < h && tick(p, k); k += 4)
                 for (uint32_t x = 0; x < w; ++x)
@@ -820,9 +926,9 @@ static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses,
                         if (st & (S_SIG | S_PI)) continue;
                         int hh, vv, dd; S.counts(x, y, hh, vv, dd);
                         if (hh + vv + dd == 0) continue;
-                        if (mq.decode(CTX_ZC + zc_ctx(orient, hh, vv, dd))) {
+                        if (dec(CTX_ZC + zc_ctx(orient, hh, vv, dd))) {
                             int cx, xb; S.sign_ctx(x, y, cx, xb);
-                            uint32_t sg = mq.decode(CTX_SC + cx) ^ (uint32_t)xb;
+                            uint32_t sg = raw ? mq.raw_decode() : (mq.decode(CTX_SC + cx) ^ (uint32_t)xb);
                             out[y * w + x] = sg ? -oph : oph;
                             st |= S_SIG | (sg ? S_NEG : 0);
                         }
@@ -836,7 +942,7 @@ static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses,
                         uint8_t& st = S.at(x, y);
                         if ((st & (S_SIG | S_PI)) != S_SIG) continue;
                         int cx = (st & S_MU) ? 2 : (S.any_sig_nbr(x, y) ? 1 : 0);
-                        uint32_t v = mq.decode(CTX_MAG + cx);
+                        uint32_t v = dec(CTX_MAG + cx);
                         int32_t& o = out[y * w + x];
                         o += (v ^ (o < 0 ? 1u : 0u)) ? poshalf : -poshalf;
                         st |= S_MU;
@@ -877,7 +983,10 @@ static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses,
                     }
                     for (uint32_t yy = k; yy < ylim; ++yy) S.at(x, yy) &= (uint8_t)~S_PI;
                 }
+            if (sty & STY_SEGSYM)   // dec_clnpass_check_segsym: four UNIFORM decisions
+                for (int i = 0; i < 4; ++i) mq.decode(CTX_UNI);
         }
+        if ((sty & STY_RESET) && !raw) mq.reset_states();   // T1.cpp:1420-1421
         if (++passtype == 3) { passtype = 0; --bpno1; }
     }
     if (stripe_counts) stripe_counts[(size_t)npasses * ns] = (uint32_t)mq.ndec;
@@ -1609,7 +1718,7 @@ static void t1_encode_all(EncodeState& E) {
                         DistCtx dc{c, E.p.numres - 1 - r, B.orient, E.p.irreversible ? 0u : 1u, (double)B.stepsize,
                                    mct ? (E.p.irreversible ? norms_irrev : norms_rev) : nullptr, mct ? 3u : E.im.nc};
                         BlockEncResult res;
-                        t1_encode_block(mag.data(), neg.data(), w, h, B.orient, res, rc ? &dc : nullptr);
+                        t1_encode_block(mag.data(), neg.data(), w, h, B.orient, res, rc ? &dc : nullptr, E.p.cblk_sty);
                         K.numbps = res.numbps; K.npasses = res.npasses; K.data = res.data; K.passes = res.passes;
     });
 }
@@ -2156,8 +2265,19 @@ static int decode_tile(const uint8_t* cs, size_t data, size_t tile_end, const Pa
                                 }
                                 uint32_t np = br.numpasses();
                                 K.numlenbits += br.commacode();
-                                // default mode: a single segment of unbounded passes
-                                uint32_t nb = br.read((int)K.numlenbits + floorlog2(np));
+                                // codeword segments (T2Decompress.cpp:388-466): a new segment starts
+                                // when the last one holds its maximum pass count
+                                uint32_t nb = 0, left = np;
+                                while (left) {
+                                    if (K.segpasses.empty() || K.segpasses.back() == seg_maxpasses(p.cblk_sty, (uint32_t)K.segpasses.size() - 1)) {
+                                        K.segpasses.push_back(0); K.seglens.push_back(0);
+                                    }
+                                    const uint32_t room = seg_maxpasses(p.cblk_sty, (uint32_t)K.segpasses.size() - 1) - K.segpasses.back();
+                                    const uint32_t n = std::min(room, left);
+                                    const uint32_t sl = br.read((int)K.numlenbits + floorlog2(n));
+                                    K.segpasses.back() += n; K.seglens.back() += sl;
+                                    nb += sl; left -= n;
+                                }
                                 K.npasses += np;
                                 contrib.push_back({&K, nb});
                             }
@@ -2200,7 +2320,8 @@ t2done:
                             }
                             if (!p.irreversible) for (auto& v : blk) v *= 2;   // same ShiftFilter below
                         } else
-                        t1_decode_block(K.data.data(), (uint32_t)K.data.size(), K.npasses, K.numbps, B.orient, w, h, blk.data());
+                        t1_decode_block(K.data.data(), (uint32_t)K.data.size(), K.npasses, K.numbps, B.orient, w, h, blk.data(),
+                                        nullptr, p.cblk_sty, &K.seglens);
                         for (uint32_t y = 0; y < h; ++y)
                             for (uint32_t x = 0; x < w; ++x) {
                                 size_t o = (size_t)(B.offy + K.y0 - B.y0 + y) * TW + (B.offx + K.x0 - B.x0 + x);
@@ -2282,7 +2403,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
             p.cblk_sty = s[8];
             if (s[1] != 0) return -2;                                // LRCP only
-            if (s[8] != 0 && s[8] != 0x40) return -2;  // other mode switches unsupported in the oracle
+            if ((s[8] & 0x40) && s[8] != 0x40) return -2;  // HT with Part-1 mode switches (CodeStreamDecompress.cpp:1781)
+            if (s[8] & 0x80) return -2;
             if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
         } else if (m == 0xff5c) {
             uint32_t sq = s[0]; p.numgbits = sq >> 5;
