@@ -793,6 +793,22 @@ struct DecTree {   // decoder-side tag tree
 //                   (CodeStreamCompress.cpp:951-1025).
 // Block k of the plan contributes lnp[k * nlayers + l] passes to layer l.
 // ---------------------------------------------------------------------------
+// Code-block style bits (grok.h:98-104) and T1::enc_is_term_pass (T1.cpp:437-458) for pass q
+// of a block with nbp bit-planes: pass 0 is the first cleanup pass, then SP, MR, CL per plane.
+enum { GK_STY_LAZY = 0x01, GK_STY_RESET = 0x02, GK_STY_TERMALL = 0x04, GK_STY_VSC = 0x08, GK_STY_PTERM = 0x10,
+       GK_STY_SEGSYM = 0x20, GK_STY_HT = 0x40 };
+static inline bool term_pass(uint32_t sty, uint32_t nbp, uint32_t q) {
+    const int bpno = q == 0 ? (int)nbp - 1 : (int)nbp - 2 - (int)(q - 1) / 3;
+    const int type = q == 0 ? 2 : (int)(q - 1) % 3;
+    if (type == 2 && bpno == 0) return true;
+    if (sty & GK_STY_TERMALL) return true;
+    if (sty & GK_STY_LAZY) {
+        if (bpno == (int)nbp - 4 && type == 2) return true;
+        if (bpno < (int)nbp - 4 && type > 0) return true;
+    }
+    return false;
+}
+
 struct T2Enc {
     const Plan& P;
     const uint32_t* info;        // 4 u32 per block: numbps, npasses, bytes, pass offset
@@ -868,13 +884,34 @@ struct T2Enc {
             if (!np) continue;
             if (!inprev[b]) { nlb[b] = 3; imsb[PG.tree].encode(bw, k, 0xffffffffu); }
             bw.numpasses(np);
-            // default style: one segment per contribution (only the last pass is terminated)
             uint32_t r0 = inprev[b] ? rate(b, inprev[b] - 1) : 0;
-            uint32_t len = rate(b, inprev[b] + np - 1) - r0;
-            int inc = std::max(0, floorlog2(len) + 1 - ((int)nlb[b] + floorlog2(np)));
+            if (!(P.p.cblk_sty & (GK_STY_LAZY | GK_STY_TERMALL))) {
+                // default style: one segment per contribution (only the last pass is terminated)
+                uint32_t len = rate(b, inprev[b] + np - 1) - r0;
+                int inc = std::max(0, floorlog2(len) + 1 - ((int)nlb[b] + floorlog2(np)));
+                bw.commacode((uint32_t)inc);
+                nlb[b] = (uint8_t)(nlb[b] + inc);
+                bw.write(len, (int)nlb[b] + floorlog2(np));
+                continue;
+            }
+            // one length per codeword segment: a segment ends at a terminated pass or at the
+            // contribution's last pass (T2Compress.cpp:210-248)
+            const uint32_t q0 = inprev[b], q1 = q0 + np, nbp = info[4 * (size_t)b];
+            int inc = 0;
+            for (uint32_t q = q0, s0 = q0, rs = r0; q < q1; ++q)
+                if (term_pass(P.p.cblk_sty, nbp, q) || q + 1 == q1) {
+                    const uint32_t re = rate(b, q);
+                    inc = std::max(inc, floorlog2(re - rs) + 1 - ((int)nlb[b] + floorlog2(q + 1 - s0)));
+                    s0 = q + 1; rs = re;
+                }
             bw.commacode((uint32_t)inc);
             nlb[b] = (uint8_t)(nlb[b] + inc);
-            bw.write(len, (int)nlb[b] + floorlog2(np));
+            for (uint32_t q = q0, s0 = q0, rs = r0; q < q1; ++q)
+                if (term_pass(P.p.cblk_sty, nbp, q) || q + 1 == q1) {
+                    const uint32_t re = rate(b, q);
+                    bw.write(re - rs, (int)nlb[b] + floorlog2(q + 1 - s0));
+                    s0 = q + 1; rs = re;
+                }
         }
     }
     // one band's packet body bytes; advances its code-blocks' pass counts
@@ -1334,7 +1371,8 @@ struct T2Enc {
         uint32_t n_it = 0, n_sim = 0;
         if (fast) init_chains();
         static const bool check = getenv("GK_T2_CHECK_SIM") != nullptr;
-        bounds = fast && !getenv("GK_T2_NO_BOUNDS");
+        // the header-size bounds assume one codeword segment per contribution
+        bounds = fast && !getenv("GK_T2_NO_BOUNDS") && !(P.p.cblk_sty & (GK_STY_LAZY | GK_STY_TERMALL));
         uint32_t n_bound = 0;
         for (uint32_t l = 0; l < L; ++l) {
             uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
@@ -1569,6 +1607,7 @@ struct gk_ctx {
     DevBuf dplanes;     // component planes staged from host
     DevBuf derr;
     DevBuf dsym, dsymoff, dpassend, dcminfo;
+    DevBuf dmsstate, dseglen;      // mode-switch T1 state slabs, decode segment lengths
     DevBuf dscratch, dnmse, dord, dweight, dord_enc;
     HostBuf hinfo, hseg, hhdr, hpasses, hord, hweight, hord_enc;
     DevBuf dstage1, dstage2;   // decode: batched tile-part / packet header fetches (device input)
@@ -1757,7 +1796,9 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     want.w = info->w; want.h = info->h; want.nc = info->numcomps; want.prec = info->prec; want.sgnd = info->sgnd;
     set_params(want.p, cp);
     if (want.nc < 3) want.p.mct = 0;
-    if (want.p.cblk_sty != 0 && want.p.cblk_sty != 0x40) throw GkError("code-block style mode switches are not supported");
+    if ((want.p.cblk_sty & GK_STY_HT) && want.p.cblk_sty != GK_STY_HT)
+        throw GkError("HTJ2K cannot be combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781
+    if (want.p.cblk_sty > 0x7f) throw GkError("unknown code-block style bits");
     if (want.p.ht() && want.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if (want.prec == 0 || want.prec > 31) throw GkError("component precision must be 1..31 bits");
@@ -1931,6 +1972,11 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nbx * GK_HT_MEL_CAP + 256);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_ht_enc(st, arena, dblk, dbytes, mel, GK_HT_MEL_CAP, dinfo, nbr, derr);
+    } else if (P.p.cblk_sty & 0x3f) {
+        // mode switches: lane-per-block coder with per-pass termination rules (gk_t1ms.hip)
+        uint8_t* mst = (uint8_t*)ctx->dmsstate.get(gk_t1ms_state_bytes(nbx));
+        HIPCHK(hipEventRecord(ctx->ev[8], st));
+        gk_launch_t1_enc_ms(st, arena, dblk, dbytes, dps, dinfo, nbr, derr, ctx->nmse_tab, dpcount, mst, P.p.cblk_sty & 0x3f);
     } else if (nbr < 8192 || getenv("GK_T1ENC_SERIAL")) {
         gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nbr, derr, ctx->nmse_tab, dnmse);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
@@ -2006,7 +2052,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     if (t1err) throw GkError(t1err & 2 ? "T1 symbol buffer overflow" : "T1 code-block slot overflow");
     const bool ht = P.p.ht();
     const GkPass* hpasses = nullptr;
-    if (do_rc && !ht) {
+    // pass records: rate control, and BYPASS / TERMALL (a length per codeword segment)
+    if ((do_rc || (P.p.cblk_sty & (GK_STY_LAZY | GK_STY_TERMALL))) && !ht) {
         GkPass* hp = (GkPass*)ctx->hpasses.get(sizeof(GkPass) * (size_t)std::max(npass_total, 1u));
         HIPCHK(hipMemcpyAsync(hp, dps, sizeof(GkPass) * (size_t)npass_total, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -2294,7 +2341,9 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             W.p.cbw = S.at(s + 6) + 2; W.p.cbh = S.at(s + 7) + 2;
             if (W.p.cbw > 10 || W.p.cbh > 10 || W.p.cbw + W.p.cbh > 12) throw GkError("corrupt COD marker (code-block size)");
             W.p.cblk_sty = S.at(s + 8);
-            if (W.p.cblk_sty != 0 && W.p.cblk_sty != 0x40) throw GkError("code-block style mode switches not supported");
+            if ((W.p.cblk_sty & GK_STY_HT) && W.p.cblk_sty != GK_STY_HT)
+                throw GkError("HTJ2K combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781-1788
+            if (W.p.cblk_sty > 0x7f) throw GkError("unknown code-block style bits");
             W.p.irrev = S.at(s + 9) == 0 ? 1 : 0;
             if (scod & 1) {
                 if (L < 12 + W.p.numres) throw GkError("corrupt COD marker (precinct sizes)");
@@ -2573,6 +2622,15 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         std::vector<uint8_t> included, numbps;
         std::vector<uint16_t> npasses;
         std::vector<uint32_t> numlenbits, len;
+        // BYPASS / TERMALL: per block the byte length of each codeword segment and the passes
+        // of its last segment (T2Decompress::initSegment, T2Decompress.cpp:28-54)
+        std::vector<std::vector<uint32_t>> seglens;
+        std::vector<uint16_t> segp;
+    };
+    const bool multiseg = (P.p.cblk_sty & (GK_STY_LAZY | GK_STY_TERMALL)) != 0;
+    auto seg_max = [&](uint32_t sg) -> uint32_t {
+        if (P.p.cblk_sty & GK_STY_TERMALL) return 1;
+        return sg == 0 ? 10 : ((sg & 1) ? 2 : 1);
     };
     std::vector<PartState> ps(Hd.parts.size());
     auto t2_part = [&](size_t q, ByteSrc& BS) {
@@ -2586,6 +2644,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         const uint32_t tb0 = TG.b0, ntb = TG.b1 - TG.b0;
         st2.included.assign(ntb, 0); st2.numbps.assign(ntb, 0); st2.npasses.assign(ntb, 0);
         st2.numlenbits.assign(ntb, 0); st2.len.assign(ntb, 0);
+        if (multiseg) { st2.seglens.assign(ntb, {}); st2.segp.assign(ntb, 0); }
         st2.chunks.reserve(ntb);
         const size_t tile_end = TPt.end;
         size_t pos = TPt.data, pk = 0;
@@ -2637,9 +2696,29 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                     }
                                     const uint32_t np = br.numpasses();
                                     st2.numlenbits[b] += br.commacode();
-                                    const uint32_t nbits = st2.numlenbits[b] + floorlog2(np);
-                                    if (nbits > 32) throw GkError("corrupt packet header (segment length)");
-                                    const uint32_t sl = br.read((int)nbits);
+                                    uint32_t sl = 0;
+                                    if (!multiseg) {
+                                        const uint32_t nbits = st2.numlenbits[b] + floorlog2(np);
+                                        if (nbits > 32) throw GkError("corrupt packet header (segment length)");
+                                        sl = br.read((int)nbits);
+                                    } else {
+                                        // one length per segment part; a segment continues across
+                                        // packets until it holds its maximum pass count
+                                        std::vector<uint32_t>& SL = st2.seglens[b];
+                                        for (uint32_t left = np; left;) {
+                                            if (SL.empty() || st2.segp[b] == seg_max((uint32_t)SL.size() - 1)) {
+                                                if (SL.size() >= GK_MAX_PASSES) throw GkError("corrupt packet header (segments)");
+                                                SL.push_back(0); st2.segp[b] = 0;
+                                            }
+                                            const uint32_t n = std::min(seg_max((uint32_t)SL.size() - 1) - st2.segp[b], left);
+                                            const uint32_t nbits = st2.numlenbits[b] + floorlog2(n);
+                                            if (nbits > 32) throw GkError("corrupt packet header (segment length)");
+                                            const uint32_t part = br.read((int)nbits);
+                                            SL.back() += part; sl += part;
+                                            st2.segp[b] = (uint16_t)(st2.segp[b] + n);
+                                            left -= n;
+                                        }
+                                    }
                                     if (st2.npasses[b] + np > GK_MAX_PASSES) throw GkError("corrupt packet header (pass count)");
                                     st2.npasses[b] = (uint16_t)(st2.npasses[b] + np);
                                     contrib.push_back({b, sl});
@@ -2672,6 +2751,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // ---- the decode table: the needed blocks of the rectangle's tiles, compacted, with offsets
     // into this call's planes and staging slots, band quantisation from QCD (decoder semantics)
     std::vector<GkBlock> blk;
+    std::vector<uint32_t> hseglen;   // BYPASS / TERMALL: segment lengths, a block's at G.data_cap
     std::vector<std::vector<int32_t>> part_idx(Hd.parts.size());   // tile-local block -> table entry
     uint64_t o = 0, t1_bytes = 0;
     for (uint32_t j = jb; j < je; ++j)
@@ -2700,6 +2780,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                 G.numbps = st2.numbps[lb];
                                 G.len = st2.len[lb];
                                 G.npasses = G.len ? st2.npasses[lb] : 0;
+                                if (multiseg) {
+                                    G.data_cap = (uint32_t)hseglen.size();
+                                    hseglen.insert(hseglen.end(), st2.seglens[lb].begin(), st2.seglens[lb].end());
+                                }
                                 G.data_off = o;
                                 t1_bytes += G.len;
                                 o += (((uint64_t)G.len + 15) & ~15ull) + 32;
@@ -2790,6 +2874,19 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (herr) throw GkError("corrupt HT code-block segment");
+    } else if (P.p.cblk_sty & 0x3f) {
+        // mode switches: lane-per-block decoder over the codeword segments (gk_t1ms.hip)
+        uint32_t* dsl = nullptr;
+        if (multiseg && !hseglen.empty()) {
+            uint32_t* hsl = (uint32_t*)ctx->hord.get(4 * hseglen.size());
+            memcpy(hsl, hseglen.data(), 4 * hseglen.size());
+            dsl = (uint32_t*)ctx->dseglen.get(4 * hseglen.size());
+            HIPCHK(hipMemcpyAsync(dsl, hsl, 4 * hseglen.size(), hipMemcpyHostToDevice, st));
+        }
+        uint8_t* mst = (uint8_t*)ctx->dmsstate.get(gk_t1ms_state_bytes(nbx));
+        gk_launch_t1_dec_ms(st, src_bytes, dblk, dsl, arena, nbr, mst, P.p.cblk_sty & 0x3f);
+        HIPCHK(hipEventRecord(ctx->ev[8], st));
+        if (multiseg && !hseglen.empty()) HIPCHK(hipStreamSynchronize(st));   // the pinned table is reused
     } else {
         // lane assignment: blocks bucketed by pass count (descending), so the lanes of a
         // wave decode similar amounts of work and the longest waves start first.  Only

@@ -299,6 +299,10 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
             for (uint32_t x = 0; x < w; ++x) dst[(size_t)y * stride + x] = 0;
     };
     const uint32_t lcup = G.len;
+    // Grok hands every byte to the cleanup pass (T1HT::decompress, T1HT.cpp:169-173: lengths1 =
+    // all bytes, lengths2 = 0), so a block with SigProp / MagRef passes is an error
+    // (ojph_block_decoder.cpp:1014-1019), as here
+    if (G.npasses > 1 && lcup) { atomicOr(err, 4); zero_block(); return; }
     if (!G.npasses || lcup < 2) {
         if (lcup == 1 || (G.npasses && lcup)) atomicOr(err, 4);
         zero_block();

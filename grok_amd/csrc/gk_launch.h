@@ -55,6 +55,13 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
                         const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks);
 // irreversible path (gk_dwt97.hip)
+// code-blocks with mode switches (gk_t1ms.hip)
+void gk_launch_t1_enc_ms(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, GkPass* passes,
+                         uint32_t* info, uint32_t nblocks, int* err, const int16_t* nmse_tab, uint32_t* pass_counter,
+                         uint8_t* state, uint32_t sty);
+void gk_launch_t1_dec_ms(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* seglen, int32_t* coef,
+                         uint32_t nblocks, uint8_t* state, uint32_t sty);
+size_t gk_t1ms_state_bytes(uint32_t nblocks);
 void gk_launch_dc_ict_fwd(hipStream_t st, int stype, const void* r, const void* g, const void* b, uint32_t sin, float* y,
                           float* u, float* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift);
 void gk_launch_dc_fwd_f(hipStream_t st, int stype, const void* in, uint32_t sin, float* out, uint32_t sout, uint32_t w,

@@ -2313,6 +2313,9 @@ t2done:
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
                         std::vector<int32_t> blk(w * h);
                         if (p.ht()) {   // T1HT::decompress: k_msbs = band numbps - cblk numbps
+                            // refinement passes: Grok passes lengths2 = 0 (T1HT.cpp:169-173), which
+                            // ojph_decode_codeblock rejects (ojph_block_decoder.cpp:1014-1019)
+                            if (K.npasses > 1 && !K.data.empty()) { jrc[ji] = -4; return; }
                             if (K.npasses && !ht_decode_block(K.data.data(), (uint32_t)K.data.size(), w, h,
                                                               B.numbps - K.numbps, blk.data(), w)) {
                                 jrc[ji] = -4;

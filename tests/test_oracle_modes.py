@@ -1,0 +1,26 @@
+"""Oracle self-consistency for the code-block mode switches (CPU): every combination of
+the reference's non-regression list round-trips losslessly through the oracle's encoder
+and segment-aware decoder, with one and several quality layers.  (Parity with Grok for
+these modes is unpinned: no reference-held fixture carries such a codestream.)"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+
+@pytest.mark.parametrize("sty", [1, 2, 4, 8, 16, 32, 5, 17, 20, 38, 63])
+@pytest.mark.parametrize("layers", [None, [10, 0]])
+def test_oracle_modes_roundtrip(sty, layers):
+    rng = np.random.default_rng(sty)
+    img = rng.integers(0, 4096, size=(1, 70, 90)).astype(np.int32)
+    img = (img // 8 + np.arange(90)[None, None, :] * 40) % 4096
+    cs = O.encode(img.astype(np.int32), 12, numres=3, cblk=(32, 32), cblk_sty=sty, layer_rate=layers)
+    np.testing.assert_array_equal(O.decode(cs)[0], img)
+
+
+def test_oracle_modes_change_stream():
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, size=(1, 64, 64)).astype(np.int32)
+    base = O.encode(img, 8, numres=3, cblk=(32, 32))
+    for sty in (1, 2, 4, 8, 16, 32):
+        assert O.encode(img, 8, numres=3, cblk=(32, 32), cblk_sty=sty) != base
