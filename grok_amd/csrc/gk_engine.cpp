@@ -260,6 +260,33 @@ static uint32_t ht_rev_expn(uint32_t B, uint32_t ndecomp, uint32_t r, uint32_t o
     return (uint32_t)((int)B + (orient == 3 ? X(H(d) * H(d)) : X(H(d) * L(d + 1))));
 }
 
+// HT irreversible QCD: param_qcd::set_irrev_quant (HTParams.cpp:273-317), base_delta =
+// 2^-(bit depth + signed) (:211-212), 9/7 synthesis energy gains (sqrt_energy_gains,
+// HTParams.cpp:75-86: constant data of the 9/7 filter bank).
+static void ht_irrev_quant(uint32_t prec, bool sgnd, uint32_t nd, uint32_t r, uint32_t orient, uint32_t& expn,
+                           uint32_t& mant) {
+    static const float L97[34] = {
+        1.0000e+00f, 1.4021e+00f, 2.0304e+00f, 2.9012e+00f, 4.1153e+00f, 5.8245e+00f, 8.2388e+00f, 1.1652e+01f, 1.6479e+01f,
+        2.3304e+01f, 3.2957e+01f, 4.6609e+01f, 6.5915e+01f, 9.3217e+01f, 1.3183e+02f, 1.8643e+02f, 2.6366e+02f, 3.7287e+02f,
+        5.2732e+02f, 7.4574e+02f, 1.0546e+03f, 1.4915e+03f, 2.1093e+03f, 2.9830e+03f, 4.2185e+03f, 5.9659e+03f, 8.4371e+03f,
+        1.1932e+04f, 1.6874e+04f, 2.3864e+04f, 3.3748e+04f, 4.7727e+04f, 6.7496e+04f, 9.5454e+04f};
+    static const float H97[34] = {
+        1.4425e+00f, 1.9669e+00f, 2.8839e+00f, 4.1475e+00f, 5.8946e+00f, 8.3472e+00f, 1.1809e+01f, 1.6701e+01f, 2.3620e+01f,
+        3.3403e+01f, 4.7240e+01f, 6.6807e+01f, 9.4479e+01f, 1.3361e+02f, 1.8896e+02f, 2.6723e+02f, 3.7792e+02f, 5.3446e+02f,
+        7.5583e+02f, 1.0689e+03f, 1.5117e+03f, 2.1378e+03f, 3.0233e+03f, 4.2756e+03f, 6.0467e+03f, 8.5513e+03f, 1.2093e+04f,
+        1.7103e+04f, 2.4187e+04f, 3.4205e+04f, 4.8373e+04f, 6.8410e+04f, 9.6747e+04f, 1.3682e+05f};
+    const float base_delta = 1.0f / (float)(1u << (prec + (sgnd ? 1 : 0)));
+    float gl, gh;
+    if (r == 0) { gl = L97[nd]; gh = gl; }
+    else { const uint32_t d = nd - r; gl = orient == 3 ? H97[d] : L97[d + 1]; gh = H97[d]; }
+    float delta_b = base_delta / (gl * gh);
+    uint32_t e = 0;
+    while (delta_b < 1.0f) { e++; delta_b *= 2.0f; }
+    const uint32_t m = (uint32_t)round(delta_b * (float)(1 << 11)) - (1 << 11);
+    mant = m < (1u << 11) ? m : 0x7ff;
+    expn = e;
+}
+
 static void assign_steps_tile(Plan& P, TileG& T) {
     for (auto& C : T.comps) {
         for (uint32_t r = 0; r < P.p.numres; ++r) {
@@ -273,6 +300,9 @@ static void assign_steps_tile(Plan& P, TileG& T) {
                     continue;
                 }
                 uint32_t gain = P.p.irrev ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
+                if (P.p.ht()) {
+                    ht_irrev_quant(P.prec, P.sgnd != 0, P.p.numres - 1, r, B.orient, B.expn, B.mant);
+                } else {
                 // Part-1 QCD generation (HTParams.cpp:216-251)
                 double stepsize = 1.0;
                 if (P.p.irrev) stepsize = (double)(1u << gain) / band_norm(level, B.orient, false);
@@ -280,6 +310,7 @@ static void assign_steps_tile(Plan& P, TileG& T) {
                 int pp = floorlog2(step) - 13, n = 11 - floorlog2(step);
                 B.mant = (n < 0 ? step >> -n : step << n) & 0x7ff;
                 B.expn = (uint32_t)((int)(P.prec + gain) - pp);
+                }
                 // Quantizer::setBandStepSizeAndBps (Quantizer.cpp:26-66)
                 uint32_t lg_enc = B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1);
                 uint32_t lg_dec = P.p.irrev ? 0 : lg_enc;
@@ -1453,8 +1484,13 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
     for (uint32_t i = 0; i < P.nc; ++i) { o.push_back((uint8_t)((P.prec - 1) | (P.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
     if (P.p.ht()) {   // CAP (CodeStreamCompress::write_cap :1064-1111): Pcap bit 15, Ccap = MAGBp code
         uint32_t B = 0;
+        // param_qcd::get_MAGBp (HTParams.cpp:318-336): scalar expounded bands count from their
+        // decomposition level (LL: num_decomps), in unsigned arithmetic as there
         for (uint32_t r = 0; r < P.p.numres; ++r)
-            for (auto& Bd : P.tiles[0].comps[0].res[r].bands) B = std::max(B, Bd.expn + P.p.numgbits - 1);
+            for (auto& Bd : P.tiles[0].comps[0].res[r].bands) {
+                const uint32_t nb = P.p.irrev ? (P.p.numres - 1) - (r ? r - 1 : 0) : 1u;
+                B = std::max(B, Bd.expn + P.p.numgbits - nb);
+            }
         uint32_t Bp = B <= 8 ? 0 : B < 28 ? B - 8 : B < 48 ? 13 + (B >> 2) : 31;
         put16(o, 0xff50); put16(o, 8); put32(o, 0x00020000); put16(o, (P.p.irrev ? 0x20 : 0) | Bp);
     }
@@ -1799,7 +1835,6 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     if ((want.p.cblk_sty & GK_STY_HT) && want.p.cblk_sty != GK_STY_HT)
         throw GkError("HTJ2K cannot be combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781
     if (want.p.cblk_sty > 0x7f) throw GkError("unknown code-block style bits");
-    if (want.p.ht() && want.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if (want.prec == 0 || want.prec > 31) throw GkError("component precision must be 1..31 bits");
     if (want.w == 0 || want.h == 0) throw GkError("empty image");
@@ -2410,7 +2445,6 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     }
     if (Hd.parts.empty()) throw GkError("no tile parts");
     if ((1u << W.p.cbw) > 64 || (1u << W.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
-    if (W.p.ht() && W.p.irrev) throw GkError("HTJ2K with the 9/7 transform is not supported on this path yet");
 }
 
 // Device-resident codestream: copy scattered ranges (tile-part headers, packet headers) to
@@ -2777,6 +2811,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                 G.stride = RG.stride;
                                 G.band_numbps = (uint8_t)R.bands[bi].numbps;
                                 G.step = R.bands[bi].step_dec / 2.0f;
+                                if (P.p.ht() && P.p.irrev) {   // ScaleHTFilter: stepsize / 2^(31 - numbps) (Quantizer.cpp:52-62)
+                                    if (R.bands[bi].numbps > 31) throw GkError("unsupported number of band bit-planes");
+                                    G.step = R.bands[bi].step_dec / (float)(1u << (31 - R.bands[bi].numbps));
+                                }
                                 G.numbps = st2.numbps[lb];
                                 G.len = st2.len[lb];
                                 G.npasses = G.len ? st2.npasses[lb] : 0;

@@ -120,7 +120,15 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
         }
     };
 
-    auto ld = [&](uint32_t x, uint32_t y) -> int32_t { return (x < w && y < h) ? src[(size_t)y * stride + x] : 0; };
+    // 9/7: the quantisation index of T1HT::preCompress (T1HT.cpp:88-104) taken from the float
+    // coefficient, trunc(x * (1 / stepsize)) (R-BUG-2: Grok reads the float bits as an int)
+    const bool irrev = G.flags & 1;
+    const float inv_step = irrev ? 1.0f / G.step : 0.0f;
+    auto ld = [&](uint32_t x, uint32_t y) -> int32_t {
+        if (x >= w || y >= h) return 0;
+        const int32_t raw = src[(size_t)y * stride + x];
+        return irrev ? (int32_t)(__int_as_float(raw) * inv_step) : raw;
+    };
     // one quad: samples (x,y) (x,y+1) (x+1,y) (x+1,y+1) -> rho, exponents, MagSgn values
     auto quad = [&](uint32_t x, uint32_t y, int& rho, int* e, uint32_t* sv, int& emax) {
         int32_t v[4] = {ld(x, y), ld(x, y + 1), ld(x + 1, y), ld(x + 1, y + 1)};
@@ -303,6 +311,14 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     // all bytes, lengths2 = 0), so a block with SigProp / MagRef passes is an error
     // (ojph_block_decoder.cpp:1014-1019), as here
     if (G.npasses > 1 && lcup) { atomicOr(err, 4); zero_block(); return; }
+    // 9/7: ScaleHTFilter (PostDecompressFilters.h:161-176) on the decoder's 32-bit sample, whose
+    // magnitude LSB sits at p = 30 - k_msbs (ojph_block_decoder.cpp:1222); G.step = stepsize /
+    // 2^(31 - band numbps).  k_msbs > 29 does not fit 32 bits (:1028-1030).
+    const bool irrev = G.flags & 1;
+    const uint32_t kmsbs = (uint32_t)G.band_numbps - (uint32_t)G.numbps;
+    if (G.npasses && lcup && kmsbs > 29) { atomicOr(err, 4); zero_block(); return; }
+    const uint32_t pbit = 30 - kmsbs;
+    float* fdst = reinterpret_cast<float*>(dst);
     if (!G.npasses || lcup < 2) {
         if (lcup == 1 || (G.npasses && lcup)) atomicOr(err, 4);
         zero_block();
@@ -416,7 +432,13 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
                 e[n] = 32 - __clz(2 * mu - 1);
                 val = (v & 1) ? -(int32_t)mu : (int32_t)mu;
             }
-            if (xx < w && yy < h) dst[(size_t)yy * stride + xx] = val;
+            if (xx < w && yy < h) {
+                if (irrev) {
+                    const uint32_t mag = ((uint32_t)(val < 0 ? -val : val) << pbit) & 0x7fffffffu;
+                    const float f = (float)mag * G.step;
+                    fdst[(size_t)yy * stride + xx] = val < 0 ? -f : f;
+                } else dst[(size_t)yy * stride + xx] = val;
+            }
         }
     };
 

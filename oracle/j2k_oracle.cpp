@@ -248,8 +248,38 @@ static uint32_t ht_rev_expn(uint32_t B, uint32_t ndecomp, uint32_t r, uint32_t o
     return (uint32_t)((int)B + X(H(d) * L(d + 1)));
 }
 
+// HT irreversible QCD: param_qcd::set_irrev_quant (HTParams.cpp:273-317) with base_delta =
+// 2^-(bit depth + signed) (:211-212) and the 9/7 synthesis energy gains (sqrt_energy_gains,
+// HTParams.cpp:75-86; constant data of the 9/7 filter bank).
+static const float HT_G97_L[34] = {
+    1.0000e+00f, 1.4021e+00f, 2.0304e+00f, 2.9012e+00f, 4.1153e+00f, 5.8245e+00f, 8.2388e+00f, 1.1652e+01f, 1.6479e+01f,
+    2.3304e+01f, 3.2957e+01f, 4.6609e+01f, 6.5915e+01f, 9.3217e+01f, 1.3183e+02f, 1.8643e+02f, 2.6366e+02f, 3.7287e+02f,
+    5.2732e+02f, 7.4574e+02f, 1.0546e+03f, 1.4915e+03f, 2.1093e+03f, 2.9830e+03f, 4.2185e+03f, 5.9659e+03f, 8.4371e+03f,
+    1.1932e+04f, 1.6874e+04f, 2.3864e+04f, 3.3748e+04f, 4.7727e+04f, 6.7496e+04f, 9.5454e+04f};
+static const float HT_G97_H[34] = {
+    1.4425e+00f, 1.9669e+00f, 2.8839e+00f, 4.1475e+00f, 5.8946e+00f, 8.3472e+00f, 1.1809e+01f, 1.6701e+01f, 2.3620e+01f,
+    3.3403e+01f, 4.7240e+01f, 6.6807e+01f, 9.4479e+01f, 1.3361e+02f, 1.8896e+02f, 2.6723e+02f, 3.7792e+02f, 5.3446e+02f,
+    7.5583e+02f, 1.0689e+03f, 1.5117e+03f, 2.1378e+03f, 3.0233e+03f, 4.2756e+03f, 6.0467e+03f, 8.5513e+03f, 1.2093e+04f,
+    1.7103e+04f, 2.4187e+04f, 3.4205e+04f, 4.8373e+04f, 6.8410e+04f, 9.6747e+04f, 1.3682e+05f};
+static void ht_irrev_quant(uint32_t prec, int sgnd, uint32_t nd, uint32_t r, uint32_t orient, uint32_t& expn, uint32_t& mant) {
+    const float base_delta = 1.0f / (float)(1u << (prec + (sgnd ? 1 : 0)));
+    float gl, gh;
+    if (r == 0) { gl = HT_G97_L[nd]; gh = gl; }
+    else {
+        const uint32_t d = nd - r;
+        gl = orient == 3 ? HT_G97_H[d] : HT_G97_L[d + 1];
+        gh = HT_G97_H[d];
+    }
+    float delta_b = base_delta / (gl * gh);
+    uint32_t e = 0;
+    while (delta_b < 1.0f) { e++; delta_b *= 2.0f; }
+    uint32_t m = (uint32_t)round(delta_b * (float)(1 << 11)) - (1 << 11);
+    mant = m < (1u << 11) ? m : 0x7ff;
+    expn = e;
+}
+
 static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress,
-                         const std::vector<std::pair<uint32_t,uint32_t>>* qcd) {
+                         const std::vector<std::pair<uint32_t,uint32_t>>* qcd, int sgnd = 0) {
     // qcd: per band (expn, mant) in band order LL, (HL,LH,HH) per resolution, when decoding.
     uint32_t bandno = 0;
     for (uint32_t r = 0; r < p.numres; ++r) {
@@ -263,6 +293,8 @@ static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress,
                     expn = (*qcd)[0].first - (p.numres - 1) + (nb - 1) + 0;  // rarely used
                     (void)nb;
                 }
+            } else if (p.ht() && p.irreversible) {
+                ht_irrev_quant(prec, sgnd, p.numres - 1, r, B.orient, expn, mant);
             } else if (p.ht() && !p.irreversible) {
                 // param_qcd::set_rev_quant (HTParams.cpp:253-272): B + ceil(log2(bibo^2 * 1.1)).
                 // Grok passes tcp->mct before it is assigned (CodeStreamCompress.cpp:382 vs the
@@ -1134,7 +1166,14 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
     for (uint32_t i = 0; i < im.nc; ++i) { o.push_back((uint8_t)((im.prec - 1) | (im.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
     if (p.ht()) {                                   // CAP (CodeStreamCompress::write_cap :1064-1111)
         uint32_t B = 0;
-        for (uint32_t r = 0; r < p.numres; ++r) for (auto& Bd : c0.res[r].bands) B = std::max(B, Bd.expn + p.numgbits - 1);
+        // param_qcd::get_MAGBp (HTParams.cpp:318-336): reversible expn + guard - 1; scalar
+        // expounded expn + guard - nb, nb = the band's decomposition level (LL: num_decomps),
+        // in unsigned arithmetic as there
+        for (uint32_t r = 0; r < p.numres; ++r)
+            for (auto& Bd : c0.res[r].bands) {
+                const uint32_t nb = p.irreversible ? (p.numres - 1) - (r ? r - 1 : 0) : 1u;
+                B = std::max(B, Bd.expn + p.numgbits - nb);
+            }
         uint32_t Bp = B <= 8 ? 0 : B < 28 ? B - 8 : B < 48 ? 13 + (B >> 2) : 31;
         put16(o, 0xff50); put16(o, 8); put32(o, 0x00020000); put16(o, (p.irreversible ? 0x20 : 0) | Bp);
     }
@@ -1696,8 +1735,18 @@ static void t1_encode_all(EncodeState& E) {
                         Cblk& K = *jobs[ji].K;
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
                         if (E.p.ht()) {   // T1HT::compress (T1HT.cpp:109-133): one cleanup pass
-                            const int32_t* src = E.coefs[c].data() + (size_t)(B.offy + K.y0 - B.y0) * C.w + (B.offx + K.x0 - B.x0);
-                            K.data = ht_encode_block(src, w, h, C.w);
+                            const size_t o0 = (size_t)(B.offy + K.y0 - B.y0) * C.w + (B.offx + K.x0 - B.x0);
+                            if (E.p.irreversible) {
+                                // T1HT::preCompress irreversible branch (T1HT.cpp:88-104) on the 9/7
+                                // coefficients as floats (R-BUG-2: Grok reads the float bits as
+                                // int32): index = trunc(x * (1 / stepsize))
+                                const float inv = 1.0f / B.stepsize;
+                                std::vector<int32_t> q((size_t)w * h);
+                                for (uint32_t y = 0; y < h; ++y)
+                                    for (uint32_t x = 0; x < w; ++x) q[(size_t)y * w + x] = (int32_t)(E.fcoefs[c][o0 + (size_t)y * C.w + x] * inv);
+                                K.data = ht_encode_block(q.data(), w, h, w);
+                            } else
+                            K.data = ht_encode_block(E.coefs[c].data() + o0, w, h, C.w);
                             uint32_t L = (uint32_t)K.data.size();
                             K.numbps = 1; K.npasses = 1; K.passes.assign(1, PassInfo{L, L, 1, 0.0});
                             return;
@@ -1738,7 +1787,7 @@ static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, ui
     E.comps.assign(nc, Comp());
     for (uint32_t c = 0; c < nc; ++c) {
         build_geometry(E.comps[c], E.tx0, E.ty0, E.tx1, E.ty1, E.p);
-        assign_steps(E.comps[c], E.p, prec, true, nullptr);
+        assign_steps(E.comps[c], E.p, prec, true, nullptr, sgnd);
     }
     E.coefs.assign(nc, {});
     for (uint32_t c = 0; c < nc; ++c) {   // tile-local copy (TileProcessor::ingestImage, TileProcessor.cpp:410-431)
@@ -1963,7 +2012,7 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
             uint32_t x0, y0, x1, y1;
             tile_rect(E0.p, w, h, 0, x0, y0, x1, y1);
             build_geometry(E0.comps[0], x0, y0, x1, y1, E0.p);
-            assign_steps(E0.comps[0], E0.p, prec, true, nullptr);
+            assign_steps(E0.comps[0], E0.p, prec, true, nullptr, sgnd);
             write_main_header(o, E0.im, E0.p, E0.comps[0], &tlm_pos);
         }
         std::vector<std::vector<uint8_t>> parts(nt);
@@ -2060,7 +2109,7 @@ size_t orc_main_header(uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int s
     uint32_t x0, y0, x1, y1;
     tile_rect(E0.p, w, h, 0, x0, y0, x1, y1);
     build_geometry(E0.comps[0], x0, y0, x1, y1, E0.p);
-    assign_steps(E0.comps[0], E0.p, prec, true, nullptr);
+    assign_steps(E0.comps[0], E0.p, prec, true, nullptr, sgnd);
     std::vector<uint8_t> o;
     size_t tlm = 0;
     write_main_header(o, E0.im, E0.p, E0.comps[0], &tlm);
@@ -2316,12 +2365,31 @@ t2done:
                             // refinement passes: Grok passes lengths2 = 0 (T1HT.cpp:169-173), which
                             // ojph_decode_codeblock rejects (ojph_block_decoder.cpp:1014-1019)
                             if (K.npasses > 1 && !K.data.empty()) { jrc[ji] = -4; return; }
+                            // missing_msbs > 29: 32 bits cannot hold the samples (ojph_block_decoder.cpp:1028-1030)
+                            if (K.npasses && !K.data.empty() && B.numbps - K.numbps > 29) { jrc[ji] = -4; return; }
                             if (K.npasses && !ht_decode_block(K.data.data(), (uint32_t)K.data.size(), w, h,
                                                               B.numbps - K.numbps, blk.data(), w)) {
                                 jrc[ji] = -4;
                                 return;
                             }
                             if (!p.irreversible) for (auto& v : blk) v *= 2;   // same ShiftFilter below
+                            else {
+                                // ScaleHTFilter (PostDecompressFilters.h:161-176): the decoder's 32-bit
+                                // sample (magnitude LSB at p = 30 - k_msbs, ojph_block_decoder.cpp:1222)
+                                // times stepsize / 2^(31 - band numbps) (Quantizer.cpp:52-62)
+                                if (B.numbps > 31) { jrc[ji] = -4; return; }
+                                const uint32_t kmsbs = B.numbps - K.numbps, pp = 30 - kmsbs;
+                                const float scale = B.stepsize / (float)(1u << (31 - B.numbps));
+                                for (uint32_t y = 0; y < h; ++y)
+                                    for (uint32_t x = 0; x < w; ++x) {
+                                        const int32_t v = blk[y * w + x];
+                                        const uint32_t mag = ((uint32_t)(v < 0 ? -v : v) << pp) & 0x7fffffffu;
+                                        const float f = (float)mag * scale;
+                                        const size_t o = (size_t)(B.offy + K.y0 - B.y0 + y) * TW + (B.offx + K.x0 - B.x0 + x);
+                                        fp[c][o] = v < 0 ? -f : f;
+                                    }
+                                return;
+                            }
                         } else
                         t1_decode_block(K.data.data(), (uint32_t)K.data.size(), K.npasses, K.numbps, B.orient, w, h, blk.data(),
                                         nullptr, p.cblk_sty, &K.seglens);

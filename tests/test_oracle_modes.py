@@ -24,3 +24,17 @@ def test_oracle_modes_change_stream():
     base = O.encode(img, 8, numres=3, cblk=(32, 32))
     for sty in (1, 2, 4, 8, 16, 32):
         assert O.encode(img, 8, numres=3, cblk=(32, 32), cblk_sty=sty) != base
+
+
+@pytest.mark.parametrize("bits,c", [(8, 3), (12, 1), (16, 1)])
+def test_oracle_ht97_roundtrip(bits, c):
+    """HT + 9/7 (standard-correct in place of R-BUG-2): decodes close to the source."""
+    rng = np.random.default_rng(bits)
+    yy, xx = np.mgrid[0:90, 0:110]
+    base = (np.sin(xx / 9.0) * np.cos(yy / 7.0) + 1) * (1 << (bits - 2))
+    img = np.clip(base[None].repeat(c, 0) + rng.integers(0, 1 << (bits - 4), size=(c, 90, 110)), 0,
+                  (1 << bits) - 1).astype(np.int32)
+    cs = O.encode(img, bits, numres=5, cblk_sty=0x40, irreversible=True)
+    dec = O.decode(cs)[0]
+    mse = np.mean((dec.astype(np.float64) - img) ** 2)
+    assert 10 * np.log10(((1 << bits) - 1) ** 2 / max(mse, 1e-12)) >= 45.0
