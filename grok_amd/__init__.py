@@ -23,7 +23,7 @@ GK_MAX_LAYERS = 100
 # Exported symbols declared in include/grok_amd.h (checked by tests/test_capi.py).
 EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_encode_tiles", "gk_main_header",
            "gk_jp2_header", "gk_decode_header", "gk_probe_header", "gk_decode", "gk_decode_window", "gk_get_timings",
-           "gk_last_error", "gk_version")
+           "gk_last_error", "gk_version", "gk_set_decode_layers")
 
 
 class CParameters(ctypes.Structure):
@@ -41,7 +41,7 @@ class CParameters(ctypes.Structure):
         ("tile_size_on", ctypes.c_uint8),
         ("t_width", ctypes.c_uint32), ("t_height", ctypes.c_uint32),
         ("writeTLM", ctypes.c_uint8), ("writePLT", ctypes.c_uint8),
-        ("cod_format", ctypes.c_int32),
+        ("cod_format", ctypes.c_int32), ("prog_order", ctypes.c_int32),
     ]
 
 
@@ -98,6 +98,8 @@ def load_library(build_if_missing=True):
         [ctypes.c_uint32] * 4 + [P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_int]
     lib.gk_decode_header.restype = ctypes.c_int
     lib.gk_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ImageInfo)]
+    lib.gk_set_decode_layers.restype = ctypes.c_int
+    lib.gk_set_decode_layers.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     lib.gk_decode.restype = ctypes.c_int
     lib.gk_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ctypes.c_void_p),
                               P(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_int]
@@ -110,10 +112,15 @@ def load_library(build_if_missing=True):
     return lib
 
 
+PROG_ORDERS = ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"]   # GRK_PROG_ORDER (grok.h)
+
+
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
-                   precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False):
+                   precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False,
+                   prog_order="LRCP"):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
+    prog_order: "LRCP", "RLCP", "RPCL", "PCRL", "CPRL" or 0..4 (grk_compress -p).
     cblk_sty=0x40 selects the HTJ2K block coder; like grk_compress -M 64
     (grk_compress.cpp:1120-1125) it also sets one guard bit."""
     lib = load_library()
@@ -141,6 +148,7 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
         p.t_width, p.t_height = int(tiles[0]), int(tiles[1])
     p.writeTLM, p.writePLT = int(bool(tlm)), int(bool(plt))
     p.cod_format = 2 if jp2 else 0   # GRK_CODEC_JP2 / GRK_CODEC_J2K
+    p.prog_order = PROG_ORDERS.index(prog_order) if isinstance(prog_order, str) else int(prog_order)
     return p
 
 
@@ -369,6 +377,12 @@ class Engine:
         if rc != 0:
             self._err("gk_decode_window")
         return res
+
+    def set_decode_layers(self, max_layers):
+        """gk_set_decode_layers: decode only the first max_layers quality layers (0 = all),
+        as grk_decompress -l (grk_dparameters::cp_layer)."""
+        if self.lib.gk_set_decode_layers(self.ctx, int(max_layers)) != 0:
+            self._err("gk_set_decode_layers")
 
     def decode(self, cs, length=None, out=None, row0=0, sample_bytes=0):
         """cs: bytes (host) or torch cuda uint8 tensor (+length).  Returns a (C, H, W)

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <tuple>
 #include <cmath>
 #include <cstdarg>
 #include <cstdlib>
@@ -131,7 +132,8 @@ struct Params {
     uint32_t prcw[GK_MAXRLVLS], prch[GK_MAXRLVLS];
     bool custom_prc = false;
     double rates[GK_MAX_LAYERS] = {0};   // compression ratio per layer (0 = remaining passes)
-    uint32_t cblk_sty = 0;               // 0 or GRK_CBLKSTY_HT (0x40, grok.h:104)
+    uint32_t cblk_sty = 0;               // Part-1 mode switches or GRK_CBLKSTY_HT (0x40, grok.h:98-104)
+    uint32_t prog = 0;                   // progression order: GRK_LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4
     bool ht() const { return (cblk_sty & 0x40) != 0; }
     uint32_t tw = 0, th = 0;             // nominal tile size (grk_cparameters::t_width/t_height; 0 = image)
     bool tlm = false, plt = false;       // grk_cparameters::writeTLM / writePLT
@@ -824,6 +826,56 @@ struct DecTree {   // decoder-side tag tree
 //                   (CodeStreamCompress.cpp:951-1025).
 // Block k of the plan contributes lnp[k * nlayers + l] passes to layer l.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Packet order of one tile (ISO 15444-1 B.12; PacketIter::next_lrcp .. next_cprl,
+// PacketIter.cpp:100-266).  For the position-driven orders the iterator walks x, y over the
+// tile in steps of the smallest precinct (reference grid), starting at the tile origin and
+// then at multiples of the step, and emits a precinct where the position is its first
+// sample (generatePrecinctIndex, :287-335): with tile origins on the 2^levels grid that is
+// the tile origin for a resolution's first precinct column / row and the precinct's own
+// origin (a multiple of 2^(PP + level)) for the others.  So the walk is a sort by (anchor
+// y, anchor x) with the order's other indices around it.
+// ---------------------------------------------------------------------------
+struct PacketRef { uint32_t l, r, c, pi; };
+static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32_t L) {
+    std::vector<PacketRef> out;
+    const uint32_t nr = P.p.numres, nc = P.nc;
+    auto np = [&](uint32_t c, uint32_t r) { const ResG& R = T.comps[c].res[r]; return R.w && R.h ? R.pw * R.ph : 0u; };
+    if (P.p.prog == 0 || P.p.prog == 1) {   // LRCP / RLCP
+        for (uint32_t a = 0; a < (P.p.prog == 0 ? L : nr); ++a)
+            for (uint32_t b = 0; b < (P.p.prog == 0 ? nr : L); ++b)
+                for (uint32_t c = 0; c < nc; ++c) {
+                    const uint32_t l = P.p.prog == 0 ? a : b, r = P.p.prog == 0 ? b : a;
+                    for (uint32_t pi = 0; pi < np(c, r); ++pi) out.push_back({l, r, c, pi});
+                }
+        return out;
+    }
+    struct Pr { uint64_t ay, ax; uint32_t r, c, pi; };
+    std::vector<Pr> v;
+    for (uint32_t c = 0; c < nc; ++c)
+        for (uint32_t r = 0; r < nr; ++r) {
+            const ResG& R = T.comps[c].res[r];
+            const uint32_t n = np(c, r), lv = nr - 1 - r, pwe = P.p.prcw[r], phe = P.p.prch[r];
+            for (uint32_t pi = 0; pi < n; ++pi) {
+                const uint32_t i = pi % R.pw, j = pi / R.pw;
+                const uint64_t ax = i ? ((uint64_t)(R.px0 >> pwe) + i) << (pwe + lv) : T.x0;
+                const uint64_t ay = j ? ((uint64_t)(R.py0 >> phe) + j) << (phe + lv) : T.y0;
+                v.push_back({ay, ax, r, c, pi});
+            }
+        }
+    auto key = [&](const Pr& a) {
+        // RPCL: r, y, x, c; PCRL: y, x, c, r; CPRL: c, y, x, r (layers innermost)
+        if (P.p.prog == 2) return std::make_tuple((uint64_t)a.r, a.ay, a.ax, (uint64_t)a.c);
+        if (P.p.prog == 3) return std::make_tuple(a.ay, a.ax, (uint64_t)a.c, (uint64_t)a.r);
+        return std::make_tuple((uint64_t)a.c, a.ay, a.ax, (uint64_t)a.r);
+    };
+    std::stable_sort(v.begin(), v.end(), [&](const Pr& a, const Pr& b) { return key(a) < key(b); });
+    out.reserve(v.size() * L);
+    for (const Pr& q : v)
+        for (uint32_t l = 0; l < L; ++l) out.push_back({l, q.r, q.c, q.pi});
+    return out;
+}
+
 // Code-block style bits (grok.h:98-104) and T1::enc_is_term_pass (T1.cpp:437-458) for pass q
 // of a block with nbp bit-planes: pass 0 is the first cleanup pass, then SP, MR, CL per plane.
 enum { GK_STY_LAZY = 0x01, GK_STY_RESET = 0x02, GK_STY_TERMALL = 0x04, GK_STY_VSC = 0x08, GK_STY_PTERM = 0x10,
@@ -1009,13 +1061,8 @@ struct T2Enc {
     bool simulate(uint32_t max_layers, uint64_t max_bytes) {
         uint64_t budget = max_bytes;
         uint64_t* bp = max_bytes == 0xffffffffull ? nullptr : &budget;
-        for (uint32_t l = 0; l < max_layers; ++l)
-            for (uint32_t r = 0; r < P.p.numres; ++r)
-                for (uint32_t c = 0; c < P.nc; ++c) {
-                    const ResG& R = P.tiles[t0].comps[c].res[r];   // rate control: one tile
-                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi)
-                        if (!write_packet(R, pi, l, bp, nullptr)) return false;
-                }
+        for (const PacketRef& pr : packet_order(P, P.tiles[t0], max_layers))   // rate control: one tile
+            if (!write_packet(P.tiles[t0].comps[pr.c].res[pr.r], pr.pi, pr.l, bp, nullptr)) return false;
         return true;
     }
 
@@ -1042,12 +1089,21 @@ struct T2Enc {
     std::vector<uint8_t> nlb0;
     uint64_t prior = 0;                     // bytes of the final layers < l
     std::vector<uint64_t> csize, chdr;
+    uint32_t last_chain = 0;                // chain of the layer's last packet in progression order
     void init_chains() {
         chains.clear(); units.clear();
         const TileG& T = P.tiles[t0];
         for (uint32_t r = 0; r < P.p.numres; ++r)
             for (uint32_t c = 0; c < P.nc; ++c)
                 for (uint32_t pi = 0; pi < T.comps[c].res[r].pw * T.comps[c].res[r].ph; ++pi) chains.push_back({c, r, pi});
+        // the packet the progression order writes last decides the budget test
+        last_chain = chains.empty() ? 0 : (uint32_t)chains.size() - 1;
+        {
+            const std::vector<PacketRef> ord = packet_order(P, T, 1);
+            if (!ord.empty())
+                for (uint32_t i = 0; i < (uint32_t)chains.size(); ++i)
+                    if (chains[i].r == ord.back().r && chains[i].c == ord.back().c && chains[i].pi == ord.back().pi) last_chain = i;
+        }
         cunits.assign(chains.size(), {});
         for (uint32_t i = 0; i < (uint32_t)chains.size(); ++i) {
             const ResG& R = T.comps[chains[i].c].res[chains[i].r];
@@ -1185,7 +1241,7 @@ struct T2Enc {
         code_layer(l);
         uint64_t tot = prior;
         for (uint64_t v : csize) tot += v;
-        const uint64_t last = csize.back(), lasth = chdr.back();
+        const uint64_t last = csize[last_chain], lasth = chdr[last_chain];
         return tot - last + lasth < max_bytes && tot <= max_bytes;
     }
     void finish_layer(uint32_t l) {   // layer l is final: advance the snapshot past it
@@ -1279,7 +1335,7 @@ struct T2Enc {
             for (uint32_t u : cunits[i]) { R += ubitn[u]; body += ubody[u]; }
             clo[i] = (R + 7) / 8; chi[i] = (R + 6) / 7 + 2; cbody[i] = body;
             lo += clo[i] + body; hi += chi[i] + body;
-            last_body = body;
+            if (i == last_chain) last_body = body;
         }
         // pass <=> S_(n-1) + hdr_n < max_bytes and S_n <= max_bytes, S_n - body_n = S_(n-1) + hdr_n
         if (hi <= max_bytes && hi - last_body < max_bytes) return 1;
@@ -1496,7 +1552,7 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
     }
     put16(o, 0xff52); put16(o, 12 + (P.p.custom_prc ? P.p.numres : 0));
     o.push_back(P.p.custom_prc ? 1 : 0);
-    o.push_back(0);   // LRCP
+    o.push_back((uint8_t)P.p.prog);   // progression order
     put16(o, P.p.nlayers);
     o.push_back((uint8_t)((P.p.mct && P.nc >= 3) ? 1 : 0));
     o.push_back((uint8_t)(P.p.numres - 1));
@@ -1623,6 +1679,7 @@ struct HostBuf {
 };
 
 struct gk_ctx {
+    uint32_t dec_layers = 0;   // quality layers to decode (0 = all; grk_dparameters::cp_layer)
     int device = 0;
     hipStream_t st = nullptr;
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // encode T1: MQ chunks overlapping context modelling
@@ -1679,6 +1736,8 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     for (uint32_t l = 0; l < P.nlayers; ++l) P.rates[l] = cp->layer_rate[l] > 0.0 ? cp->layer_rate[l] : 0.0;
     P.write_com = cp->write_comment;
     P.cblk_sty = cp->cblk_sty;
+    if (cp->prog_order < 0 || cp->prog_order > 4) throw GkError("unknown progression order");
+    P.prog = (uint32_t)cp->prog_order;
     if (cp->tile_size_on) { P.tw = cp->t_width; P.th = cp->t_height; }
     P.tlm = cp->writeTLM != 0; P.plt = cp->writePLT != 0;
     if (cp->cod_format != 0 && cp->cod_format != 2) throw GkError("cod_format must be GRK_CODEC_J2K (0) or GRK_CODEC_JP2 (2)");
@@ -2207,9 +2266,14 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         } else {
             for (size_t q = 0; q < chains.size(); ++q) run_chain(q);
         }
-        // LRCP order: layer, then chains in (resolution, component, precinct) order
-        for (uint32_t l = 0; l < L; ++l)
-            for (size_t q = 0; q < chains.size(); ++q) {
+        // packets in the progression order (chains are numbered in (resolution, component,
+        // precinct) order)
+        std::vector<uint32_t> chain_at(P.p.numres * P.nc + 1, 0);
+        for (uint32_t r = 0, q = 0; r < P.p.numres; ++r)
+            for (uint32_t c = 0; c < P.nc; ++c) { chain_at[r * P.nc + c] = q; q += T.comps[c].res[r].pw * T.comps[c].res[r].ph; }
+        for (const PacketRef& pr : packet_order(P, T, L)) {
+                const size_t q = chain_at[pr.r * P.nc + pr.c] + pr.pi;
+                const uint32_t l = pr.l;
                 const TileOut& C = co[q];
                 Pk k = C.pk[l];
                 const uint32_t h0 = (uint32_t)O.phdr.size(), s0 = (uint32_t)O.bsegs.size();
@@ -2366,7 +2430,8 @@ static void parse_header(ByteSrc& S, Header& Hd) {
         } else if (m == 0xff52) {
             if (L < 12) throw GkError("corrupt COD marker");
             uint32_t scod = S.at(s);
-            if (S.at(s + 1) != 0) throw GkError("only LRCP progression supported");
+            if (S.at(s + 1) > 4) throw GkError("corrupt COD marker (progression order)");
+            W.p.prog = S.at(s + 1);
             if (scod & 6) throw GkError("SOP/EPH markers not supported");
             W.p.nlayers = S.be16(s + 2);
             W.p.mct = S.at(s + 4);
@@ -2682,12 +2747,17 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         st2.chunks.reserve(ntb);
         const size_t tile_end = TPt.end;
         size_t pos = TPt.data, pk = 0;
-        for (uint32_t l = 0; l < P.p.nlayers; ++l)
-            for (uint32_t r = 0; r < P.p.numres; ++r)
-                for (uint32_t c = 0; c < P.nc; ++c) {
-                    const ResG& R = TG.comps[c].res[r];
-                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi, ++pk) {
+        const std::vector<PacketRef> order = packet_order(P, TG, P.p.nlayers);
+        // layer limit (tcp->numLayersToDecompress): packets of later layers are skipped through
+        // PLT or parsed without their data (T2Decompress::processPacket, T2Decompress.cpp:55-116)
+        const uint32_t maxl = ctx->dec_layers ? std::min(ctx->dec_layers, P.p.nlayers) : P.p.nlayers;
+        for (size_t oi = 0; oi < order.size(); ++oi, ++pk) {
+                        const uint32_t l = order[oi].l, r = order[oi].r, c = order[oi].c, pi = order[oi].pi;
+                        const ResG& R = TG.comps[c].res[r];
+                        (void)r;
                         if (pos >= tile_end) return;
+                        const bool skip_l = l >= maxl;
+                        if (skip_l && pk < TPt.plt.size()) { pos += TPt.plt[pk]; continue; }
                         if (pk < TPt.plt.size()) {   // PLT: a packet with no needed block is skipped unread
                             bool any = false;
                             for (uint32_t bi = 0; bi < R.bands.size() && !any; ++bi) {
@@ -2748,13 +2818,14 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                             const uint32_t nbits = st2.numlenbits[b] + floorlog2(n);
                                             if (nbits > 32) throw GkError("corrupt packet header (segment length)");
                                             const uint32_t part = br.read((int)nbits);
-                                            SL.back() += part; sl += part;
+                                            if (!skip_l) SL.back() += part;
+                                            sl += part;
                                             st2.segp[b] = (uint16_t)(st2.segp[b] + n);
                                             left -= n;
                                         }
                                     }
                                     if (st2.npasses[b] + np > GK_MAX_PASSES) throw GkError("corrupt packet header (pass count)");
-                                    st2.npasses[b] = (uint16_t)(st2.npasses[b] + np);
+                                    if (!skip_l) st2.npasses[b] = (uint16_t)(st2.npasses[b] + np);
                                     contrib.push_back({b, sl});
                                 }
                             }
@@ -2763,14 +2834,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         pos = br.off;
                         for (auto& ct : contrib) {
                             const uint32_t n = (uint32_t)std::min<size_t>(ct.second, tile_end > pos ? tile_end - pos : 0);
-                            if (n && need[ct.first]) {
+                            if (n && need[ct.first] && !skip_l) {
                                 st2.chunks.push_back({pos, ct.first, n});
                                 st2.len[ct.first] += n;
                             }
                             pos += ct.second;
                         }
-                    }
-                }
+        }
     };
     const auto h1 = now();
     if (Hd.parts.size() == 1) {
@@ -3268,6 +3338,7 @@ int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, gk_cpara
             coding->writeTLM = !Hd.tlm.empty();
             coding->writePLT = 0;
             coding->cod_format = jp2 ? 2 : 0;
+            coding->prog_order = (int32_t)p.prog;
         }
         return 0;
     } catch (const GkError& e) {
@@ -3287,6 +3358,12 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void
         ctx->err = e.msg;
         return -1;
     }
+}
+
+int gk_set_decode_layers(gk_ctx* ctx, uint32_t max_layers) {
+    if (!ctx) return -1;
+    ctx->dec_layers = max_layers;
+    return 0;
 }
 
 int gk_decode_window(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, uint32_t x0, uint32_t y0,

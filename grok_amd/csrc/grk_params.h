@@ -19,7 +19,8 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
                  GRK_J2K_MAXRLVLS);
         return refuse(msg);
     }
-    if (g.prog_order != GRK_LRCP || g.numpocs) return refuse("only the LRCP progression is supported on this path");
+    if (g.numpocs) return refuse("progression order changes (POC) are not supported on this path");
+    if (g.prog_order < GRK_LRCP || g.prog_order > GRK_CPRL) return refuse("unknown progression order");
     if (g.roi_compno >= 0) return refuse("region of interest (RGN) is not supported on this path");
     if (g.tx0 || g.ty0 || g.image_offset_x0 || g.image_offset_y0) return refuse("image/tile offsets are not supported");
     if (g.enableTilePartGeneration) return refuse("multiple tile parts per tile are not supported");
@@ -30,7 +31,7 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     if (g.num_comments) return refuse("custom COM markers are not supported (the default comment is written)");
     if (g.csty & ~1u) return refuse("SOP/EPH markers are not supported");
     const uint32_t sty = (g.isHT ? GRK_CBLKSTY_HT : 0) | g.cblk_sty;
-    if (sty != 0 && sty != GRK_CBLKSTY_HT) {
+    if (sty > 0x7f || ((sty & GRK_CBLKSTY_HT) && sty != GRK_CBLKSTY_HT)) {
         snprintf(msg, sizeof msg, "code-block style 0x%x is not supported on this path", sty);
         return refuse(msg);
     }
@@ -54,5 +55,6 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     p.t_width = g.t_width; p.t_height = g.t_height;
     p.writeTLM = g.writeTLM; p.writePLT = g.writePLT;
     p.cod_format = jp2 ? 2 : 0;
+    p.prog_order = (int32_t)g.prog_order;
     return true;
 }

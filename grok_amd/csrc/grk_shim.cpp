@@ -276,6 +276,7 @@ bool run_decode(CodecObj* C, ImageObj* o, const uint32_t* w) {
     std::vector<void*> planes(o->img.numcomps);
     std::vector<uint32_t> strides(o->img.numcomps);
     for (uint16_t i = 0; i < o->img.numcomps; ++i) { planes[i] = o->comps[i].data; strides[i] = o->comps[i].stride; }
+    gk_set_decode_layers(e, C->dp.cp_layer);   // 0 = every layer
     int rc = w ? gk_decode_window(e, C->data.data(), C->data.size(), 0, w[0], w[1], w[2], w[3], planes.data(),
                                   strides.data(), 0, 0)
                : gk_decode(e, C->data.data(), C->data.size(), 0, planes.data(), strides.data(), 0, 0);
@@ -539,10 +540,6 @@ bool grk_decompress_read_header(grk_codec* codec, grk_header_info* hi) {
         char msg[256];
         if (gk_probe_header(C->data.data(), C->data.size(), &C->info, &C->coding, msg, sizeof msg) != 0) {
             error("%s", msg);
-            return false;
-        }
-        if (C->dp.cp_layer && C->dp.cp_layer < C->coding.numlayers) {
-            error("decoding fewer quality layers than the stream holds is not supported on this path");
             return false;
         }
         C->header_read = true;

@@ -33,7 +33,8 @@ typedef struct gk_cparameters {
     double layer_rate[GK_MAX_LAYERS];    /* grk_cparameters::layer_rate (compression ratio, 0 = lossless) */
     uint8_t numresolution;               /* grk_cparameters::numresolution (default 6) */
     uint32_t cblockw_init, cblockh_init; /* grk_cparameters::cblockw_init / cblockh_init (default 64) */
-    uint8_t cblk_sty;                    /* grk_cparameters::cblk_sty: 0 (Part 1) or 0x40 (HTJ2K, GRK_CBLKSTY_HT) */
+    uint8_t cblk_sty;                    /* grk_cparameters::cblk_sty: Part-1 mode switches (LAZY 1, RESET 2, TERMALL 4,
+                                            VSC 8, PTERM 0x10, SEGSYM 0x20) or 0x40 alone (HTJ2K, GRK_CBLKSTY_HT) */
     uint8_t irreversible;                /* grk_cparameters::irreversible */
     uint8_t mct;                         /* grk_cparameters::mct (RCT/ICT for >= 3 components) */
     uint8_t numgbits;                    /* grk_cparameters::numgbits (default 2) */
@@ -48,6 +49,7 @@ typedef struct gk_cparameters {
     uint8_t writePLT;                    /* grk_cparameters::writePLT (grk_compress -L) */
     int32_t cod_format;                  /* grk_cparameters::cod_format: GRK_CODEC_J2K (0, raw codestream) or
                                             GRK_CODEC_JP2 (2, JP2 file boxes around it; FileFormatCompress.cpp) */
+    int32_t prog_order;                  /* grk_cparameters::prog_order: GRK_LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4 */
 } gk_cparameters;
 
 /* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to
@@ -139,6 +141,11 @@ int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, gk_cpara
  * tile parts (tile sharding, window decode) writes only those tiles' samples. */
 int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void* const* comps,
               const uint32_t* strides, uint32_t sample_bytes, int out_on_device);
+
+/* grk_dparameters::cp_layer (CodeStreamDecompress.cpp:2570-2579): later gk_decode /
+ * gk_decode_window calls decode only the first max_layers quality layers (0 = all); packets of
+ * later layers are skipped through PLT or parsed without their data (T2Decompress.cpp:55-116). */
+int gk_set_decode_layers(gk_ctx* ctx, uint32_t max_layers);
 
 /* grk_decompress_set_window + grk_decompress (grok.h:1082-1657; CodeStreamDecompress
  * window decode): decode the window [x0, x1) x [y0, y1) of the image.

@@ -43,6 +43,7 @@ namespace orc {
 // (nested calls run serially on the calling thread).
 // ----------------------------------------------------------------------------
 static unsigned g_threads = 1;
+static uint32_t g_dec_layers = 0;   // decode: quality layers to use (0 = all; grk_dparameters::cp_layer)
 static thread_local bool t_in_par = false;
 template <class F> static void par_for(size_t n, F f) {
     const unsigned T = (unsigned)std::min<size_t>(g_threads, n);
@@ -76,7 +77,8 @@ struct Params {
     uint32_t nlayers = 1;
     double rates[100] = {0};    // grk_cparameters::layer_rate (compression ratios; 0 = all remaining passes)
     int write_com = 1;
-    uint32_t cblk_sty = 0;      // 0x40 = HTJ2K block coder (GRK_CBLKSTY_HT, grok.h:104)
+    uint32_t cblk_sty = 0;      // mode switches (grok.h:98-103) or 0x40 = HTJ2K block coder (GRK_CBLKSTY_HT, grok.h:104)
+    uint32_t prog = 0;          // progression order (GRK_PROG_ORDER): LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4
     uint32_t tw = 0, th = 0;    // nominal tile size (0 = one tile covering the image), grk_cparameters::t_width/t_height
     int tlm = 0, plt = 0;       // write TLM (-X) / PLT (-L) markers
     bool ht() const { return (cblk_sty & 0x40) != 0; }
@@ -1181,7 +1183,7 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
     for (uint32_t r = 0; r < p.numres; ++r) if (p.prcw_exp[r] != 15 || p.prch_exp[r] != 15) custom_prc = true;
     put16(o, 0xff52); put16(o, 12 + (custom_prc ? p.numres : 0));  // COD
     o.push_back(custom_prc ? 1 : 0);                // Scod
-    o.push_back(0);                                 // LRCP
+    o.push_back((uint8_t)p.prog);                   // progression order
     put16(o, p.nlayers);
     o.push_back((uint8_t)((p.mct && im.nc >= 3) ? 1 : 0));
     o.push_back((uint8_t)(p.numres - 1));
@@ -1218,6 +1220,80 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
 // K.layer_np[layno] passes.  With a byte budget, fails like Grok's bounded
 // BitIO (the header must stay below the budget) and body check.  Appends the
 // packet to *o when o is non-null.  Updates the per-block T2 state.
+// Packet iterator (ISO 15444-1 B.12.1; PacketIter::next_* PacketIter.cpp:100-266): the
+// position-driven orders walk y, x from the tile origin in steps of the smallest precinct
+// (then at the step's multiples, `y += dy - y % dy`) and emit a precinct of resolution r
+// where the position is a multiple of its size, or the tile origin when the resolution's
+// origin is not (generatePrecinctIndex, :287-335).  Each packet at most once.
+struct PktRef { uint32_t l, r, c, pi; };
+static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Params& p, uint32_t tx0, uint32_t ty0,
+                                       uint32_t tx1, uint32_t ty1, uint32_t nlayers) {
+    std::vector<PktRef> v;
+    const uint32_t nc = (uint32_t)comps.size(), nr = p.numres;
+    auto nprc = [&](uint32_t c, uint32_t r) {
+        const Res& R = comps[c].res[r];
+        return (R.x1 > R.x0 && R.y1 > R.y0) ? R.pw * R.ph : 0u;
+    };
+    if (p.prog == 0 || p.prog == 1) {
+        for (uint32_t a = 0; a < (p.prog == 0 ? nlayers : nr); ++a)
+            for (uint32_t b = 0; b < (p.prog == 0 ? nr : nlayers); ++b)
+                for (uint32_t c = 0; c < nc; ++c) {
+                    const uint32_t l = p.prog == 0 ? a : b, r = p.prog == 0 ? b : a;
+                    for (uint32_t pi = 0; pi < nprc(c, r); ++pi) v.push_back({l, r, c, pi});
+                }
+        return v;
+    }
+    uint64_t dx = ~0ull, dy = ~0ull;
+    for (uint32_t c = 0; c < nc; ++c)
+        for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t lv = nr - 1 - r;
+            dx = std::min<uint64_t>(dx, 1ull << (comps[c].res[r].prcw_exp + lv));
+            dy = std::min<uint64_t>(dy, 1ull << (comps[c].res[r].prch_exp + lv));
+        }
+    std::vector<uint8_t> seen;
+    std::vector<uint32_t> base(nc * nr + 1, 0);
+    for (uint32_t c = 0, k = 0; c < nc; ++c)
+        for (uint32_t r = 0; r < nr; ++r, ++k) base[k + 1] = base[k] + nprc(c, r);
+    seen.assign(base[nc * nr], 0);
+    auto prc_at = [&](uint32_t c, uint32_t r, uint64_t x, uint64_t y, uint32_t& pi) {
+        const Res& R = comps[c].res[r];
+        if (!nprc(c, r)) return false;
+        const uint32_t lv = nr - 1 - r;
+        const uint64_t rpx = R.prcw_exp + lv, rpy = R.prch_exp + lv;
+        if (!((x % (1ull << rpx)) == 0 || (x == tx0 && (((uint64_t)R.x0 << lv) % (1ull << rpx)) != 0))) return false;
+        if (!((y % (1ull << rpy)) == 0 || (y == ty0 && (((uint64_t)R.y0 << lv) % (1ull << rpy)) != 0))) return false;
+        const uint64_t i = (((x + (1ull << lv) - 1) >> lv) >> R.prcw_exp) - (R.x0 >> R.prcw_exp);
+        const uint64_t j = (((y + (1ull << lv) - 1) >> lv) >> R.prch_exp) - (R.y0 >> R.prch_exp);
+        if (i >= R.pw || j >= R.ph) return false;
+        pi = (uint32_t)(i + j * R.pw);
+        return true;
+    };
+    auto emit = [&](uint32_t c, uint32_t r, uint64_t x, uint64_t y) {
+        uint32_t pi;
+        if (!prc_at(c, r, x, y, pi)) return;
+        uint8_t& s = seen[base[c * nr + r] + pi];
+        if (s) return;
+        s = 1;
+        for (uint32_t l = 0; l < nlayers; ++l) v.push_back({l, r, c, pi});
+    };
+    auto walk = [&](const std::function<void(uint64_t, uint64_t)>& f) {
+        for (uint64_t y = ty0; y < ty1; y += dy - (y % dy))
+            for (uint64_t x = tx0; x < tx1; x += dx - (x % dx)) f(x, y);
+    };
+    if (p.prog == 2) {          // RPCL
+        for (uint32_t r = 0; r < nr; ++r)
+            walk([&](uint64_t x, uint64_t y) { for (uint32_t c = 0; c < nc; ++c) emit(c, r, x, y); });
+    } else if (p.prog == 3) {   // PCRL
+        walk([&](uint64_t x, uint64_t y) {
+            for (uint32_t c = 0; c < nc; ++c) for (uint32_t r = 0; r < nr; ++r) emit(c, r, x, y);
+        });
+    } else {                    // CPRL
+        for (uint32_t c = 0; c < nc; ++c)
+            walk([&](uint64_t x, uint64_t y) { for (uint32_t r = 0; r < nr; ++r) emit(c, r, x, y); });
+    }
+    return v;
+}
+
 struct PrecTrees { std::vector<TagTree> incl, imsb; };
 
 static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t layno, PrecTrees& T,
@@ -1668,9 +1744,11 @@ typedef struct {
     uint32_t cblk_sty;
     uint32_t tile_w, tile_h, tlm, plt;
     uint32_t cod_format;   // 0 = raw codestream (GRK_CODEC_J2K), 2 = JP2 file (GRK_CODEC_JP2)
+    uint32_t prog_order;   // GRK_PROG_ORDER
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
+void orc_set_decode_layers(uint32_t n) { g_dec_layers = n; }
 unsigned orc_get_threads(void) { return g_threads; }
 
 static Params to_params(const orc_cparams* cp) {
@@ -1680,6 +1758,7 @@ static Params to_params(const orc_cparams* cp) {
     p.irreversible = cp->irreversible; p.mct = cp->mct; p.nlayers = cp->nlayers ? cp->nlayers : 1;
     p.write_com = (int)cp->write_com;
     p.cblk_sty = cp->cblk_sty;
+    p.prog = cp->prog_order;
     if (p.ht()) p.numgbits = 1;   // grk_compress.cpp:1123-1124
     p.tw = cp->tile_w; p.th = cp->tile_h; p.tlm = (int)cp->tlm; p.plt = (int)cp->plt;
     for (uint32_t i = 0; i < 100; ++i) p.rates[i] = i < p.nlayers ? cp->layer_rate[i] : 0.0;
@@ -1861,13 +1940,8 @@ static bool simulate(EncodeState& E, uint32_t max_layers, uint64_t max_bytes) {
     auto trees = make_trees(E);
     uint64_t budget = max_bytes;
     uint64_t* bp = (max_bytes == 0xffffffffull) ? nullptr : &budget;
-    for (uint32_t l = 0; l < max_layers; ++l)
-        for (uint32_t r = 0; r < E.p.numres; ++r)
-            for (uint32_t c = 0; c < E.im.nc; ++c) {
-                Res& R = E.comps[c].res[r];
-                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi)
-                    if (!write_packet(nullptr, R, pi, l, trees[c][r][pi], bp)) return false;
-            }
+    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, max_layers))
+        if (!write_packet(nullptr, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], bp)) return false;
     return true;
 }
 
@@ -1953,16 +2027,11 @@ static void rate_allocate(EncodeState& E) {
 // are recorded for PLT.
 static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector<uint32_t>& plens) {
     auto trees = make_trees(E);
-    for (uint32_t l = 0; l < E.p.nlayers; ++l)
-        for (uint32_t r = 0; r < E.p.numres; ++r)
-            for (uint32_t c = 0; c < E.im.nc; ++c) {
-                Res& R = E.comps[c].res[r];
-                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                    size_t before = body.size();
-                    write_packet(&body, R, pi, l, trees[c][r][pi], nullptr);
-                    plens.push_back((uint32_t)(body.size() - before));
-                }
-            }
+    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, E.p.nlayers)) {
+        size_t before = body.size();
+        write_packet(&body, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], nullptr);
+        plens.push_back((uint32_t)(body.size() - before));
+    }
 }
 
 // Tile part: SOT [PLT] SOD packets (CodeStreamCompress::writeTilePart :862-900; SOT with
@@ -2283,11 +2352,13 @@ static int decode_tile(const uint8_t* cs, size_t data, size_t tile_end, const Pa
         }
     }
     size_t pos = i;
-    for (uint32_t l = 0; l < nlayers; ++l)
-        for (uint32_t r = 0; r < p.numres; ++r)
-            for (uint32_t c = 0; c < im.nc; ++c) {
+    for (const PktRef& pk : packet_iter(comps, p, tx0, ty0, tx1, ty1, nlayers)) {
+                const uint32_t l = pk.l, r = pk.r, c = pk.c, pi = pk.pi;
                 Res& R = comps[c].res[r];
-                for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                // layers past the limit: header parsed for the coding state, data skipped
+                // (T2Decompress::processPacket, T2Decompress.cpp:55-116)
+                const bool skip_l = g_dec_layers && l >= g_dec_layers;
+                {
                     if (pos >= tile_end) goto t2done;
                     BitReader br; br.p = cs + pos; br.len = tile_end - pos;
                     std::vector<std::pair<Cblk*, uint32_t>> contrib;  // block, bytes in this packet
@@ -2324,19 +2395,22 @@ static int decode_tile(const uint8_t* cs, size_t data, size_t tile_end, const Pa
                                     const uint32_t room = seg_maxpasses(p.cblk_sty, (uint32_t)K.segpasses.size() - 1) - K.segpasses.back();
                                     const uint32_t n = std::min(room, left);
                                     const uint32_t sl = br.read((int)K.numlenbits + floorlog2(n));
-                                    K.segpasses.back() += n; K.seglens.back() += sl;
+                                    K.segpasses.back() += n;
+                                    if (!skip_l) K.seglens.back() += sl;
                                     nb += sl; left -= n;
                                 }
-                                K.npasses += np;
-                                contrib.push_back({&K, nb});
+                                if (!skip_l) K.npasses += np;
+                                contrib.push_back({&K, skip_l ? ~0u - nb : nb});
                             }
                         }
                     }
                     br.align();
                     pos += br.off;
                     for (auto& ct : contrib) {
-                        uint32_t nb = (uint32_t)std::min<size_t>(ct.second, tile_end - pos);
-                        ct.first->data.insert(ct.first->data.end(), cs + pos, cs + pos + nb);
+                        const bool skip = ct.second > 0x7fffffffu;   // skipped layer: ~bytes
+                        const uint32_t want = skip ? ~ct.second : ct.second;
+                        uint32_t nb = (uint32_t)std::min<size_t>(want, tile_end - pos);
+                        if (!skip) ct.first->data.insert(ct.first->data.end(), cs + pos, cs + pos + nb);
                         pos += nb;
                     }
                 }
@@ -2473,7 +2547,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             p.nlayers = get16(s + 2); p.mct = s[4];
             p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
             p.cblk_sty = s[8];
-            if (s[1] != 0) return -2;                                // LRCP only
+            if (s[1] > 4) return -2;                                 // progression order
+            p.prog = s[1];
             if ((s[8] & 0x40) && s[8] != 0x40) return -2;  // HT with Part-1 mode switches (CodeStreamDecompress.cpp:1781)
             if (s[8] & 0x80) return -2;
             if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }

@@ -23,7 +23,7 @@ class CParams(ctypes.Structure):
         ("layer_rate", ctypes.c_double * 100),
         ("cblk_sty", ctypes.c_uint32),
         ("tile_w", ctypes.c_uint32), ("tile_h", ctypes.c_uint32), ("tlm", ctypes.c_uint32), ("plt", ctypes.c_uint32),
-        ("cod_format", ctypes.c_uint32),
+        ("cod_format", ctypes.c_uint32), ("prog_order", ctypes.c_uint32),
     ]
 
 
@@ -93,7 +93,7 @@ def get_threads():
 
 
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
-           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False):
+           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -104,6 +104,8 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
     p.nlayers = nlayers
     p.write_com = int(write_com)
     p.cblk_sty = int(cblk_sty)
+    p.prog_order = ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"].index(prog_order) if isinstance(prog_order, str) \
+        else int(prog_order)
     if tiles:
         p.tile_w, p.tile_h = int(tiles[0]), int(tiles[1])
     p.tlm, p.plt = int(tlm), int(plt)
@@ -180,6 +182,11 @@ def encode_tile_parts(slab, row0, image_hw, prec, tile_begin, tile_end, signed=F
     if n == 0:
         raise RuntimeError("oracle tile-part encode failed")
     return out[:n].tobytes(), list(lens)
+
+
+def set_decode_layers(n):
+    """Decode only the first n quality layers from now on (0 = all; grk_decompress -l)."""
+    lib().orc_set_decode_layers(ctypes.c_uint32(int(n)))
 
 
 def decode(cs):

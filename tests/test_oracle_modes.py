@@ -38,3 +38,29 @@ def test_oracle_ht97_roundtrip(bits, c):
     dec = O.decode(cs)[0]
     mse = np.mean((dec.astype(np.float64) - img) ** 2)
     assert 10 * np.log10(((1 << bits) - 1) ** 2 / max(mse, 1e-12)) >= 45.0
+
+
+@pytest.mark.parametrize("prog", ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"])
+def test_oracle_progressions_roundtrip(prog):
+    """Every progression order round-trips (precincts, tiles) and changes the packet order."""
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, size=(3, 100, 120)).astype(np.int32)
+    kw = dict(numres=4, cblk=(16, 16), precincts=[(32, 32)], tiles=(64, 64))
+    cs = O.encode(img, 8, prog_order=prog, **kw)
+    np.testing.assert_array_equal(O.decode(cs)[0], img)
+    if prog != "LRCP":
+        assert cs != O.encode(img, 8, **kw)
+
+
+def test_oracle_layer_limit():
+    rng = np.random.default_rng(6)
+    img = (rng.integers(0, 64, size=(1, 96, 96)) + np.arange(96)[None, None, :]).astype(np.int32)
+    cs = O.encode(img, 8, numres=3, cblk=(32, 32), layer_rate=[30, 8, 0])
+    errs = []
+    try:
+        for n in (1, 2, 3):
+            O.set_decode_layers(n)
+            errs.append(np.abs(O.decode(cs)[0].astype(np.int64) - img).mean())
+    finally:
+        O.set_decode_layers(0)
+    assert errs[0] > errs[1] > errs[2] == 0
