@@ -2386,6 +2386,11 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
 struct TilePart {                  // packet bytes [data, end) of one tile part
     uint32_t tile; size_t sot, data, end;
     std::vector<uint32_t> plt;      // packet lengths from PLT markers (empty without PLT)
+    // a tile's later tile parts (TPsot 1, 2, ...), merged behind its first: their packet
+    // ranges continue the tile's packet sequence (B.10.4 / T2Decompress over the tile's
+    // parts in order); their PLT lengths are appended to plt
+    std::vector<std::pair<size_t, size_t>> more;
+    uint32_t tpsot = 0;
 };
 struct Header {
     Plan want;
@@ -2503,8 +2508,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             size_t j = pos + 12;
             while (j + 4 <= end && S.be16(j) != 0xff93) j += 2 + S.be16(j + 2);
             if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
-            if (S.at(pos + 10) != 0) throw GkError("multiple tile parts per tile not supported");
-            Hd.parts.push_back({isot, pos, j + 2, end, {}});
+            Hd.parts.push_back({isot, pos, j + 2, end, {}, {}, S.at(pos + 10)});
             pos = end;
         }
     }
@@ -2546,7 +2550,7 @@ static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
         if (TP.data) continue;
         if (S.be16(TP.sot) != 0xff90 || S.be16(TP.sot + 4) != TP.tile || S.be32(TP.sot + 6) != TP.end - TP.sot)
             throw GkError("TLM does not match the SOT markers");
-        if (S.at(TP.sot + 10) != 0) throw GkError("multiple tile parts per tile not supported");
+        TP.tpsot = S.at(TP.sot + 10);
         size_t j = TP.sot + 12;
         while (j + 4 <= TP.end && S.be16(j) != 0xff93) {
             const uint32_t m = S.be16(j), L = S.be16(j + 2);
@@ -2572,26 +2576,45 @@ static void prefetch_packet_headers(gk_ctx* ctx, ByteSrc& S, const Plan& P, cons
     for (const auto& TP : Hd.parts) {
         if (TP.plt.empty() || TP.tile >= P.tiles.size()) continue;
         const TileG& T = P.tiles[TP.tile];
-        size_t pos = TP.data, k = 0;
-        for (uint32_t l = 0; l < P.p.nlayers; ++l)
-            for (uint32_t r = 0; r < P.p.numres; ++r)
-                for (uint32_t c = 0; c < P.nc; ++c) {
-                    const ResG& R = T.comps[c].res[r];
-                    for (uint32_t pi = 0; pi < R.pw * R.ph && k < TP.plt.size(); ++pi, ++k) {
-                        size_t nblk = 0;
-                        for (uint32_t bi = 0; bi < R.bands.size(); ++bi) nblk += (size_t)R.prc[bi][pi].cw * R.prc[bi][pi].ch;
-                        const size_t len = TP.plt[k];
-                        if (pos + len > TP.end) return;   // inconsistent PLT: fall back to page fetches
-                        rg.push_back({pos, std::min(len, 64 + 16 * nblk)});
-                        pos += len;
-                    }
-                }
+        size_t pos = TP.data, end = TP.end, k = 0, nextp = 0;
+        for (const PacketRef& pr : packet_order(P, T, P.p.nlayers)) {
+            if (k >= TP.plt.size()) break;
+            const ResG& R = T.comps[pr.c].res[pr.r];
+            while (pos >= end && nextp < TP.more.size()) { pos = TP.more[nextp].first; end = TP.more[nextp].second; ++nextp; }
+            size_t nblk = 0;
+            for (uint32_t bi = 0; bi < R.bands.size(); ++bi) nblk += (size_t)R.prc[bi][pr.pi].cw * R.prc[bi][pr.pi].ch;
+            const size_t len = TP.plt[k++];
+            if (pos + len > end) return;   // inconsistent PLT: fall back to page fetches
+            rg.push_back({pos, std::min(len, 64 + 16 * nblk)});
+            pos += len;
+        }
     }
     fetch_ranges(ctx, S, rg, ctx->hstage2, ctx->dstage2);
 }
 
 // win (optional): x0, y0, x1, y1 — decode only the tiles intersecting the window and write
 // the window into comps (whose element 0 is the window's top-left sample).
+// A tile's tile parts in TPsot order become one entry: the first part's range, the others
+// in `more`, PLT lengths concatenated (packets never straddle tile parts, A.4.2).
+static void merge_tile_parts(Header& Hd) {
+    std::unordered_map<uint32_t, size_t> first;
+    std::vector<TilePart> out;
+    for (TilePart& TP : Hd.parts) {
+        auto it = first.find(TP.tile);
+        if (it == first.end()) {
+            if (TP.tpsot != 0) throw GkError("tile parts out of order (first TPsot is not 0)");
+            first.emplace(TP.tile, out.size());
+            out.push_back(std::move(TP));
+            continue;
+        }
+        TilePart& H = out[it->second];
+        if (TP.tpsot != H.more.size() + 1) throw GkError("tile parts out of order (TPsot)");
+        H.more.push_back({TP.data, TP.end});
+        H.plt.insert(H.plt.end(), TP.plt.begin(), TP.plt.end());
+    }
+    Hd.parts.swap(out);
+}
+
 static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void* const* comps,
                         const uint32_t* strides, uint32_t sample_bytes, int out_on_device, const uint32_t* win = nullptr) {
     hipStream_t st = ctx->st;
@@ -2631,16 +2654,15 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         Hd.parts.swap(keep);
         if (Hd.parts.empty()) throw GkError("no tile part intersects the window");
     }
-    if (S.dev) {
-        read_tile_part_headers(ctx, S, Hd);
-        prefetch_packet_headers(ctx, S, P, Hd);
-    }
+    if (S.dev) read_tile_part_headers(ctx, S, Hd);
+    merge_tile_parts(Hd);
+    if (S.dev) prefetch_packet_headers(ctx, S, P, Hd);
     // ---- tiles present, their rectangle, and the code-blocks that reach the output
     std::vector<int32_t> part_of(P.tiles.size(), -1);
     for (size_t q = 0; q < Hd.parts.size(); ++q) {
         const TilePart& TPt = Hd.parts[q];
         if (TPt.tile >= P.tiles.size()) throw GkError("corrupt SOT (tile index)");
-        if (part_of[TPt.tile] >= 0) throw GkError("multiple tile parts per tile not supported");
+        if (part_of[TPt.tile] >= 0) throw GkError("corrupt stream (tile parts of one tile merged twice)");
         part_of[TPt.tile] = (int32_t)q;
     }
     uint32_t ib = P.ntx, ie = 0, jb = P.nty, je = 0;
@@ -2745,8 +2767,8 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         st2.numlenbits.assign(ntb, 0); st2.len.assign(ntb, 0);
         if (multiseg) { st2.seglens.assign(ntb, {}); st2.segp.assign(ntb, 0); }
         st2.chunks.reserve(ntb);
-        const size_t tile_end = TPt.end;
-        size_t pos = TPt.data, pk = 0;
+        size_t tile_end = TPt.end;
+        size_t pos = TPt.data, pk = 0, nextp = 0;
         const std::vector<PacketRef> order = packet_order(P, TG, P.p.nlayers);
         // layer limit (tcp->numLayersToDecompress): packets of later layers are skipped through
         // PLT or parsed without their data (T2Decompress::processPacket, T2Decompress.cpp:55-116)
@@ -2755,6 +2777,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         const uint32_t l = order[oi].l, r = order[oi].r, c = order[oi].c, pi = order[oi].pi;
                         const ResG& R = TG.comps[c].res[r];
                         (void)r;
+                        while (pos >= tile_end && nextp < TPt.more.size()) {   // the tile's next tile part
+                            pos = TPt.more[nextp].first; tile_end = TPt.more[nextp].second; ++nextp;
+                        }
                         if (pos >= tile_end) return;
                         const bool skip_l = l >= maxl;
                         if (skip_l && pk < TPt.plt.size()) { pos += TPt.plt[pk]; continue; }
