@@ -20,6 +20,7 @@ The same JSON line carries auxiliary measurements:
       tiles, TLM + PLT): the four SURVEY windows per step; with N > 1 ranks each
       window's tile rows are split over the ranks and rank 0 gathers the rows;
   C2_batch2: two C2 images in flight per GPU (serving throughput, never `value`).
+  C3_batch2: two C3 images in flight per GPU (host PCRD overlapped with GPU work).
 
 `cpu_baseline`: the oracle (CPU restatement, byte-exact with Grok by the fixtures)
 on bounded crops of C2 / C3 / C4, median of 3 runs, at 1 and N host threads.
@@ -548,6 +549,21 @@ def main():
                             "parallelism": "replicas x%d" % world}
         rb.close()
         del rb
+        torch.cuda.empty_cache()
+        # C3 with two images in flight: one image's host PCRD + T2 runs while the other's
+        # DWT / T1 kernels occupy the GPU
+        rb3 = BatchRunner("C3", 2, rank, device)
+        rb3.check()
+        elb3, _ = timed(rb3, 2, 1, world, dist, device)
+        Sb3 = rb3.size
+        aux["C3_batch2"] = {"config": "C3 with 2 images in flight per GPU (2 engines / HIP streams, one host thread "
+                                      "each: host PCRD of one image overlaps the other's GPU stages); one step = 2 "
+                                      "images encoded + decoded",
+                            "value": round(2 * Sb3 * Sb3 / 1e6 * world * 2 / elb3, 3), "unit": "Mpixels/s",
+                            "ms_per_step": round(elb3 * 1000.0 / 2, 3), "images_per_step": 2,
+                            "parallelism": "replicas x%d" % world}
+        rb3.close()
+        del rb3
         torch.cuda.empty_cache()
         r4 = ShardRunner("C4", 0, rank, world, device, dist) if world > 1 else Runner("C4", 0, rank, device)
         r4.check()

@@ -23,7 +23,7 @@ GK_MAX_LAYERS = 100
 # Exported symbols declared in include/grok_amd.h (checked by tests/test_capi.py).
 EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_encode_tiles", "gk_main_header",
            "gk_jp2_header", "gk_decode_header", "gk_probe_header", "gk_decode", "gk_decode_window", "gk_get_timings",
-           "gk_last_error", "gk_version", "gk_set_decode_layers")
+           "gk_last_error", "gk_version", "gk_set_decode_layers", "gk_set_decode_reduce")
 
 
 class CParameters(ctypes.Structure):
@@ -98,6 +98,8 @@ def load_library(build_if_missing=True):
         [ctypes.c_uint32] * 4 + [P(ctypes.c_void_p), P(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_int]
     lib.gk_decode_header.restype = ctypes.c_int
     lib.gk_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ImageInfo)]
+    lib.gk_set_decode_reduce.restype = ctypes.c_int
+    lib.gk_set_decode_reduce.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     lib.gk_set_decode_layers.restype = ctypes.c_int
     lib.gk_set_decode_layers.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     lib.gk_decode.restype = ctypes.c_int
@@ -384,6 +386,13 @@ class Engine:
         if self.lib.gk_set_decode_layers(self.ctx, int(max_layers)) != 0:
             self._err("gk_set_decode_layers")
 
+    def set_decode_reduce(self, reduce):
+        """gk_set_decode_reduce: discard the `reduce` highest resolutions (grk_decompress -r,
+        grk_dparameters::cp_reduce); decode() then returns ceil(H / 2^reduce) x ceil(W / 2^reduce)."""
+        if self.lib.gk_set_decode_reduce(self.ctx, int(reduce)) != 0:
+            self._err("gk_set_decode_reduce")
+        self._reduce = int(reduce)
+
     def decode(self, cs, length=None, out=None, row0=0, sample_bytes=0):
         """cs: bytes (host) or torch cuda uint8 tensor (+length).  Returns a (C, H, W)
         numpy array (int32, or 8/16-bit with sample_bytes 1/2), or fills ``out`` (torch
@@ -393,6 +402,9 @@ class Engine:
         on_dev = _is_torch_cuda(cs)
         info = self.read_header(cs, length)
         c, h, w = info.numcomps, info.h, info.w
+        red = getattr(self, "_reduce", 0)
+        if red:   # reduced-resolution output: ceil(size / 2^reduce)
+            h, w = -(-h // (1 << red)), -(-w // (1 << red))
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         if out is not None:
             sample_bytes = _sample_bytes(out)

@@ -1680,6 +1680,7 @@ struct HostBuf {
 
 struct gk_ctx {
     uint32_t dec_layers = 0;   // quality layers to decode (0 = all; grk_dparameters::cp_layer)
+    uint32_t dec_reduce = 0;   // highest resolutions discarded on decode (grk_dparameters::cp_reduce)
     int device = 0;
     hipStream_t st = nullptr;
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // encode T1: MQ chunks overlapping context modelling
@@ -1807,14 +1808,17 @@ struct L1Io {
 
 // Forward/inverse DWT over all components with the ping-pong placement of gk_common.h; every
 // level is one launch per tile shape with the components in grid.z.
+// lstop (inverse only): the last level undone (1 = full resolution; reduced-resolution decode
+// stops at reduce + 1, leaving resolution numres - 1 - reduce at the tiles' corners)
 static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0, uint32_t je = 0xffffffffu,
-                    uint32_t ib = 0, uint32_t ie = 0xffffffffu, const L1Io* io = nullptr) {
+                    uint32_t ib = 0, uint32_t ie = 0xffffffffu, const L1Io* io = nullptr, uint32_t lstop = 1) {
     Plan& P = ctx->plan;
     int32_t* arena = (int32_t*)ctx->arena.p;
     const uint32_t L = P.p.numres - 1;
     const uint64_t cst = 2 * (uint64_t)RG.plane;   // component plane pairs
     ctx->tm.dwt_launches = 0; ctx->tm.dwt_bytes = 0;
-    for (uint32_t i = 0; i < L; ++i) {
+    const uint32_t nlev = forward ? L : (L + 1 > lstop ? L + 1 - lstop : 0);
+    for (uint32_t i = 0; i < nlev; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
         for (const ShapeG& S0 : P.shapes) {       // one launch per tile shape, grid.z = tiles of that shape
             ShapeG S = S0;                        // restricted to tile rows [jb, je), columns [ib, ie)
@@ -2643,6 +2647,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     ensure_plan(ctx, Hd.want);
     Plan& P = ctx->plan;
     if (Hd.qcd != ctx->band_qcd) { apply_qcd(P, Hd.qcd); ctx->band_qcd = Hd.qcd; }
+    const uint32_t red = ctx->dec_reduce;
+    if (red >= P.p.numres) throw GkError("reduce must be less than the number of resolutions");
+    if (red && win) throw GkError("reduced-resolution decode of a window is not supported");
     if (win) {   // keep only the tile parts of tiles intersecting the window
         if (win[0] >= win[2] || win[1] >= win[3] || win[2] > P.w || win[3] > P.h) throw GkError("bad decode window");
         std::vector<TilePart> keep;
@@ -2773,15 +2780,15 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // layer limit (tcp->numLayersToDecompress): packets of later layers are skipped through
         // PLT or parsed without their data (T2Decompress::processPacket, T2Decompress.cpp:55-116)
         const uint32_t maxl = ctx->dec_layers ? std::min(ctx->dec_layers, P.p.nlayers) : P.p.nlayers;
+        const uint32_t rmax = P.p.numres - ctx->dec_reduce;   // resolutions decoded
         for (size_t oi = 0; oi < order.size(); ++oi, ++pk) {
                         const uint32_t l = order[oi].l, r = order[oi].r, c = order[oi].c, pi = order[oi].pi;
                         const ResG& R = TG.comps[c].res[r];
-                        (void)r;
                         while (pos >= tile_end && nextp < TPt.more.size()) {   // the tile's next tile part
                             pos = TPt.more[nextp].first; tile_end = TPt.more[nextp].second; ++nextp;
                         }
                         if (pos >= tile_end) return;
-                        const bool skip_l = l >= maxl;
+                        const bool skip_l = l >= maxl || r >= rmax;
                         if (skip_l && pk < TPt.plt.size()) { pos += TPt.plt[pk]; continue; }
                         if (pk < TPt.plt.size()) {   // PLT: a packet with no needed block is skipped unread
                             bool any = false;
@@ -3081,6 +3088,61 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     int32_t mx = P.sgnd ? (1 << (P.prec - 1)) - 1 : (int32_t)((1u << P.prec) - 1);
     const int stype = sample_type(sample_bytes, P.prec, P.sgnd != 0);
     const size_t es = gk_sample_size(stype);
+    const bool mct3r = P.p.mct && P.nc >= 3;
+    if (red) {
+        // reduced resolution: undo levels L .. red+1; resolution numres-1-red of each tile is
+        // then at the tile's corner of plane (red odd ? B : A); the inverse MCT + DC + clamp
+        // writes it per tile into the ceil(size / 2^red) output (tile origins lie on the
+        // 2^levels grid, so a tile's reduced origin is its origin >> red)
+        run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr, red + 1);
+        HIPCHK(hipEventRecord(ctx->ev[4], st));
+        const uint32_t qx0 = RG.x0 >> red, qy0 = RG.y0 >> red;
+        const uint32_t qcols = ceildivpow2(RG.x0 + RG.w, red) - qx0, qrows = ceildivpow2(RG.y0 + RG.h, red) - qy0;
+        std::vector<uint8_t*> qd(P.nc);
+        std::vector<uint32_t> qs(P.nc);
+        if (!out_on_device) {
+            uint8_t* stage = (uint8_t*)ctx->dplanes.get((size_t)qcols * qrows * P.nc * es + 16);
+            for (uint32_t c = 0; c < P.nc; ++c) { qd[c] = stage + (size_t)c * qcols * qrows * es; qs[c] = qcols; }
+        } else {
+            for (uint32_t c = 0; c < P.nc; ++c) { qd[c] = (uint8_t*)comps[c] + ((size_t)qy0 * strides[c] + qx0) * es; qs[c] = strides[c]; }
+        }
+        for (uint32_t j = jb; j < je; ++j)
+            for (uint32_t i = ib; i < ie; ++i) {
+                const TileG& T = P.tiles[(size_t)j * P.ntx + i];
+                const uint32_t tx0 = T.x0 >> red, ty0 = T.y0 >> red;
+                const uint32_t tw = ceildivpow2(T.x1, red) - tx0, th = ceildivpow2(T.y1, red) - ty0;
+                auto src = [&](uint32_t c) {
+                    return arena + (size_t)c * 2 * RG.plane + ((red & 1) ? RG.plane : 0) +
+                           (size_t)(T.y0 - RG.y0) * RG.stride + (T.x0 - RG.x0);
+                };
+                auto srcf = [&](uint32_t c) { return reinterpret_cast<const float*>(src(c)); };
+                auto dst = [&](uint32_t c) { return qd[c] + ((size_t)(ty0 - qy0) * qs[c] + (tx0 - qx0)) * es; };
+                if (!P.p.irrev) {
+                    if (mct3r) gk_launch_rct_inv_dc(st, src(0), src(1), src(2), RG.stride, stype, dst(0), dst(1), dst(2), qs[0],
+                                                    tw, th, shift, mn, mx);
+                    for (uint32_t c = mct3r ? 3 : 0; c < P.nc; ++c)
+                        gk_launch_dc_inv(st, src(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
+                } else {
+                    if (mct3r) gk_launch_ict_inv_dc(st, srcf(0), srcf(1), srcf(2), RG.stride, stype, dst(0), dst(1), dst(2),
+                                                    qs[0], tw, th, shift, mn, mx);
+                    for (uint32_t c = mct3r ? 3 : 0; c < P.nc; ++c)
+                        gk_launch_dc_inv_f(st, srcf(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
+                }
+            }
+        if (mct3r && (qs[1] != qs[0] || qs[2] != qs[0])) throw GkError("the first three components must share a stride");
+        HIPCHK(hipEventRecord(ctx->ev[5], st));
+        if (!out_on_device)
+            for (uint32_t c = 0; c < P.nc; ++c)
+                HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)qy0 * strides[c] + qx0) * es, (size_t)strides[c] * es,
+                                        qd[c], (size_t)qcols * es, (size_t)qcols * es, qrows, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(ctx->ev[6], st));
+        HIPCHK(hipStreamSynchronize(st));
+        ctx->tm.t2_ms = ev_ms(ctx, 0, 1); ctx->tm.t1_ms = ev_ms(ctx, 2, 3); ctx->tm.t1_cm_ms = 0.f;
+        ctx->tm.t1_coder_ms = ev_ms(ctx, 2, 8); ctx->tm.cs_bytes = len; ctx->tm.t1_bytes = t1_bytes;
+        ctx->tm.dwt_ms = ev_ms(ctx, 3, 4); ctx->tm.mct_ms = ev_ms(ctx, 4, 5); ctx->tm.assemble_ms = ev_ms(ctx, 1, 2);
+        ctx->tm.total_ms = ev_ms(ctx, 0, 6); ctx->tm.t1_blocks = nbr;
+        return;
+    }
     std::vector<void*> dst(P.nc);
     std::vector<uint32_t> dstr(P.nc);
     if (!out_on_device) {
@@ -3383,6 +3445,12 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void
         ctx->err = e.msg;
         return -1;
     }
+}
+
+int gk_set_decode_reduce(gk_ctx* ctx, uint32_t reduce) {
+    if (!ctx || reduce >= GK_MAXRLVLS) return -1;
+    ctx->dec_reduce = reduce;
+    return 0;
 }
 
 int gk_set_decode_layers(gk_ctx* ctx, uint32_t max_layers) {

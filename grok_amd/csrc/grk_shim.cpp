@@ -277,6 +277,7 @@ bool run_decode(CodecObj* C, ImageObj* o, const uint32_t* w) {
     std::vector<uint32_t> strides(o->img.numcomps);
     for (uint16_t i = 0; i < o->img.numcomps; ++i) { planes[i] = o->comps[i].data; strides[i] = o->comps[i].stride; }
     gk_set_decode_layers(e, C->dp.cp_layer);   // 0 = every layer
+    gk_set_decode_reduce(e, C->dp.cp_reduce);   // the engine refuses it with a window
     int rc = w ? gk_decode_window(e, C->data.data(), C->data.size(), 0, w[0], w[1], w[2], w[3], planes.data(),
                                   strides.data(), 0, 0)
                : gk_decode(e, C->data.data(), C->data.size(), 0, planes.data(), strides.data(), 0, 0);
@@ -521,7 +522,6 @@ void grk_decompress_set_default_params(grk_dparameters* p) {
 bool grk_decompress_init(grk_codec* codec, grk_dparameters* parameters) {
     CodecObj* C = codec_of(codec);
     if (!C || C->compress || !parameters) return false;
-    if (parameters->cp_reduce) { error("reduced-resolution decode is not supported on this path"); return false; }
     C->dp = *parameters;
     if (parameters->DA_x1 > parameters->DA_x0 && parameters->DA_y1 > parameters->DA_y0) {
         C->win[0] = parameters->DA_x0; C->win[1] = parameters->DA_y0;
@@ -543,7 +543,19 @@ bool grk_decompress_read_header(grk_codec* codec, grk_header_info* hi) {
             return false;
         }
         C->header_read = true;
-        C->out = region_image(C, 0, 0, C->info.w, C->info.h);
+        if (C->dp.cp_reduce >= C->coding.numresolution) {
+            error("reduce %u must be less than the number of resolutions %u", C->dp.cp_reduce, C->coding.numresolution);
+            return false;
+        }
+        if (C->dp.cp_reduce && C->has_win) {
+            error("reduced-resolution decode of a window is not supported on this path");
+            return false;
+        }
+        {   // cp_reduce: the composited image is ceil(size / 2^reduce)
+            const uint32_t r = C->dp.cp_reduce;
+            C->out = region_image(C, 0, 0, (uint32_t)(((uint64_t)C->info.w + (1ull << r) - 1) >> r),
+                                  (uint32_t)(((uint64_t)C->info.h + (1ull << r) - 1) >> r));
+        }
         if (!C->out) return false;
     }
     if (hi) {

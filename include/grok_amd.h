@@ -147,6 +147,12 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void
  * later layers are skipped through PLT or parsed without their data (T2Decompress.cpp:55-116). */
 int gk_set_decode_layers(gk_ctx* ctx, uint32_t max_layers);
 
+/* grk_dparameters::cp_reduce (CodeStreamDecompress / TileComponent resolutions_to_decompress):
+ * later gk_decode calls discard the `reduce` highest resolutions: packets of those resolutions
+ * are skipped, the inverse DWT stops `reduce` levels early and the output planes are
+ * ceil(w / 2^reduce) x ceil(h / 2^reduce) (0 = full resolution; not with gk_decode_window). */
+int gk_set_decode_reduce(gk_ctx* ctx, uint32_t reduce);
+
 /* grk_decompress_set_window + grk_decompress (grok.h:1082-1657; CodeStreamDecompress
  * window decode): decode the window [x0, x1) x [y0, y1) of the image.
  * Only the tile parts of tiles intersecting the window are read (located through TLM

@@ -44,6 +44,7 @@ namespace orc {
 // ----------------------------------------------------------------------------
 static unsigned g_threads = 1;
 static uint32_t g_dec_layers = 0;   // decode: quality layers to use (0 = all; grk_dparameters::cp_layer)
+static uint32_t g_dec_reduce = 0;   // decode: resolutions discarded (grk_dparameters::cp_reduce)
 static thread_local bool t_in_par = false;
 template <class F> static void par_for(size_t n, F f) {
     const unsigned T = (unsigned)std::min<size_t>(g_threads, n);
@@ -1749,6 +1750,7 @@ typedef struct {
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
 void orc_set_decode_layers(uint32_t n) { g_dec_layers = n; }
+void orc_set_decode_reduce(uint32_t n) { g_dec_reduce = n; }
 unsigned orc_get_threads(void) { return g_threads; }
 
 static Params to_params(const orc_cparams* cp) {
@@ -2330,6 +2332,7 @@ static int decode_tile(const uint8_t* cs, size_t data, size_t tile_end, const Pa
     tile_rect(p, im.w, im.h, tile, tx0, ty0, tx1, ty1);
     const uint32_t TW = tx1 - tx0, TH = ty1 - ty0;
     const uint32_t nlayers = p.nlayers;
+    const uint32_t red = g_dec_reduce;   // grk_dparameters::cp_reduce
     size_t i = data;
     std::vector<Comp> comps(im.nc);
     for (uint32_t c = 0; c < im.nc; ++c) { build_geometry(comps[c], tx0, ty0, tx1, ty1, p); assign_steps(comps[c], p, im.prec, false, &qcd); }
@@ -2355,9 +2358,9 @@ static int decode_tile(const uint8_t* cs, size_t data, size_t tile_end, const Pa
     for (const PktRef& pk : packet_iter(comps, p, tx0, ty0, tx1, ty1, nlayers)) {
                 const uint32_t l = pk.l, r = pk.r, c = pk.c, pi = pk.pi;
                 Res& R = comps[c].res[r];
-                // layers past the limit: header parsed for the coding state, data skipped
-                // (T2Decompress::processPacket, T2Decompress.cpp:55-116)
-                const bool skip_l = g_dec_layers && l >= g_dec_layers;
+                // layers past the limit and resolutions past the reduction: header parsed for
+                // the coding state, data skipped (T2Decompress::processPacket, T2Decompress.cpp:55-116)
+                const bool skip_l = (g_dec_layers && l >= g_dec_layers) || r + red >= p.numres;
                 {
                     if (pos >= tile_end) goto t2done;
                     BitReader br; br.p = cs + pos; br.len = tile_end - pos;
@@ -2478,14 +2481,21 @@ t2done:
     for (int rc : jrc) if (rc) return rc;
     for (uint32_t c = 0; c < im.nc; ++c) {
         Comp& C = comps[c];
-        if (!p.irreversible) dwt2d<int32_t>(ip[c].data(), TW, C, p.numres, false, inv53_1d);
-        else dwt2d<float>(fp[c].data(), TW, C, p.numres, false, inv97_1d);
+        // reduced-resolution decode: the inverse transform stops at resolution numres-1-reduce,
+        // whose samples sit at the tile buffer's corner (resolutions_to_decompress)
+        if (!p.irreversible) dwt2d<int32_t>(ip[c].data(), TW, C, p.numres - red, false, inv53_1d);
+        else dwt2d<float>(fp[c].data(), TW, C, p.numres - red, false, inv97_1d);
     }
     int32_t shift = im.sgnd ? 0 : (1 << (im.prec - 1));
     int32_t mn = im.sgnd ? -(1 << (im.prec - 1)) : 0, mxv = im.sgnd ? (1 << (im.prec - 1)) - 1 : (1 << im.prec) - 1;
-    const size_t n = (size_t)TW * TH, N = (size_t)im.w * im.h;
+    const uint32_t Wr = ceildivpow2(im.w, red), Hr = ceildivpow2(im.h, red);
+    const uint32_t tx0r = ceildivpow2(tx0, red), ty0r = ceildivpow2(ty0, red);
+    const uint32_t TWr = ceildivpow2(tx1, red) - tx0r, THr = ceildivpow2(ty1, red) - ty0r;
+    const size_t n = (size_t)TW * TH, N = (size_t)Wr * Hr;
     auto put = [&](uint32_t c, size_t k, int32_t v) {
-        out[c * N + (size_t)(ty0 + k / TW) * im.w + tx0 + k % TW] = std::min(mxv, std::max(mn, v + shift));
+        const uint32_t x = (uint32_t)(k % TW), y = (uint32_t)(k / TW);
+        if (x >= TWr || y >= THr) return;
+        out[c * N + (size_t)(ty0r + y) * Wr + tx0r + x] = std::min(mxv, std::max(mn, v + shift));
     };
     if (!p.irreversible) {
         if (p.mct && im.nc >= 3)
@@ -2561,10 +2571,11 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         i += 2 + L;   // CAP, TLM, COM and other main-header markers are skipped
     }
     if (!first_sot) return -3;
-    *W = im.w; *H = im.h; *NC = im.nc; *PREC = im.prec;
+    if (g_dec_reduce >= p.numres) return -7;   // reduce must leave one resolution
+    *W = ceildivpow2(im.w, g_dec_reduce); *H = ceildivpow2(im.h, g_dec_reduce); *NC = im.nc; *PREC = im.prec;
     if (!out) return 0;
     if (p.tw == im.w && p.th == im.h) p.tw = p.th = 0;
-    std::fill(out, out + (size_t)im.nc * im.w * im.h, 0);
+    std::fill(out, out + (size_t)im.nc * *W * *H, 0);
     const uint32_t nt = tile_count(p, im.w, im.h);
     size_t pos = first_sot;
     struct Part { size_t data, end; uint32_t tile; };

@@ -189,6 +189,11 @@ def set_decode_layers(n):
     lib().orc_set_decode_layers(ctypes.c_uint32(int(n)))
 
 
+def set_decode_reduce(n):
+    """Discard the n highest resolutions from now on (grk_decompress -r / cp_reduce)."""
+    lib().orc_set_decode_reduce(ctypes.c_uint32(int(n)))
+
+
 def decode(cs):
     buf = np.frombuffer(cs, dtype=np.uint8).copy()
     buf = np.concatenate([buf, np.zeros(8, np.uint8)])
