@@ -42,6 +42,7 @@ class CParameters(ctypes.Structure):
         ("t_width", ctypes.c_uint32), ("t_height", ctypes.c_uint32),
         ("writeTLM", ctypes.c_uint8), ("writePLT", ctypes.c_uint8),
         ("cod_format", ctypes.c_int32), ("prog_order", ctypes.c_int32),
+        ("enableTilePartGeneration", ctypes.c_uint8), ("newTilePartProgressionDivider", ctypes.c_char),
     ]
 
 
@@ -119,7 +120,7 @@ PROG_ORDERS = ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"]   # GRK_PROG_ORDER (grok.
 
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
                    precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False,
-                   prog_order="LRCP"):
+                   prog_order="LRCP", tile_parts=None):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
     prog_order: "LRCP", "RLCP", "RPCL", "PCRL", "CPRL" or 0..4 (grk_compress -p).
@@ -151,6 +152,9 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
     p.writeTLM, p.writePLT = int(bool(tlm)), int(bool(plt))
     p.cod_format = 2 if jp2 else 0   # GRK_CODEC_JP2 / GRK_CODEC_J2K
     p.prog_order = PROG_ORDERS.index(prog_order) if isinstance(prog_order, str) else int(prog_order)
+    if tile_parts:   # grk_compress -u L|R|C: a new tile part whenever that index changes
+        p.enableTilePartGeneration = 1
+        p.newTilePartProgressionDivider = tile_parts.encode()
     return p
 
 

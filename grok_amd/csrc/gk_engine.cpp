@@ -134,6 +134,7 @@ struct Params {
     double rates[GK_MAX_LAYERS] = {0};   // compression ratio per layer (0 = remaining passes)
     uint32_t cblk_sty = 0;               // Part-1 mode switches or GRK_CBLKSTY_HT (0x40, grok.h:98-104)
     uint32_t prog = 0;                   // progression order: GRK_LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4
+    char tp_div = 0;                     // tile-part divider 'L' / 'R' / 'C' (grk_compress -u), 0 = one part per tile
     bool ht() const { return (cblk_sty & 0x40) != 0; }
     uint32_t tw = 0, th = 0;             // nominal tile size (grk_cparameters::t_width/t_height; 0 = image)
     bool tlm = false, plt = false;       // grk_cparameters::writeTLM / writePLT
@@ -876,6 +877,43 @@ static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32
     return out;
 }
 
+// Tile parts per tile (CodeStreamCompress::getNumTilePartsForProgression,
+// CodeStreamCompress.cpp:1899-1958): with divider D the indices of the progression string up
+// to D (layers L, resolutions R, components C) each start a new tile part, so a tile has the
+// product of their ranges and part k holds the packets whose leading indices form the k-th
+// combination; those are contiguous in the packet order.  A divider behind the position
+// index (P) is refused.  tp_key(pr) = the part of packet pr.
+struct TilePartSplit {
+    uint32_t n = 1;
+    int depth = -1;   // last progression-string position that splits
+    const char* prog = "LRCP";
+    uint32_t L = 1, R = 1, C = 1;
+    uint32_t key(const PacketRef& pr) const {
+        uint32_t k = 0;
+        for (int j = 0; j <= depth; ++j) {
+            const char ch = prog[j];
+            if (ch == 'L') k = k * L + pr.l;
+            else if (ch == 'R') k = k * R + pr.r;
+            else k = k * C + pr.c;
+        }
+        return k;
+    }
+};
+static TilePartSplit tile_part_split(const Plan& P) {
+    static const char* names[5] = {"LRCP", "RLCP", "RPCL", "PCRL", "CPRL"};
+    TilePartSplit S;
+    S.prog = names[P.p.prog]; S.L = P.p.nlayers; S.R = P.p.numres; S.C = P.nc;
+    if (!P.p.tp_div) return S;
+    for (int j = 0; j < 4; ++j) {
+        const char ch = S.prog[j];
+        if (ch == 'P') throw GkError("a tile-part divider behind the position index is not supported");
+        S.n *= ch == 'L' ? S.L : ch == 'R' ? S.R : S.C;
+        if (ch == P.p.tp_div) { S.depth = j; break; }
+    }
+    if (S.n > 255) throw GkError("more than 255 tile parts per tile");
+    return S;
+}
+
 // Code-block style bits (grok.h:98-104) and T1::enc_is_term_pass (T1.cpp:437-458) for pass q
 // of a block with nbp bit-planes: pass 0 is the first cleanup pass, then SP, MR, CL per plane.
 enum { GK_STY_LAZY = 0x01, GK_STY_RESET = 0x02, GK_STY_TERMALL = 0x04, GK_STY_VSC = 0x08, GK_STY_PTERM = 0x10,
@@ -1418,7 +1456,10 @@ struct T2Enc {
         if (t1 != t0 + 1) throw GkError("rate control runs on one tile at a time");
         const TileG& TT = P.tiles[t0];
         const double size_pixel = (double)P.nc * P.prec, npix = (double)((uint64_t)(TT.x1 - TT.x0) * (TT.y1 - TT.y0));
-        for (uint32_t k = 0; k < L; ++k) rates[k] = P.p.rates[k] > 0.0 ? (size_pixel * npix) / (P.p.rates[k] * 8.0) : 0.0;
+        // tile-part generation: 14 bytes (SOT + SOD) per extra part, spread over the layers
+        const double tp_offset = (double)((tile_part_split(P).n - 1) * 14) / (double)L;
+        for (uint32_t k = 0; k < L; ++k)
+            rates[k] = P.p.rates[k] > 0.0 ? (size_pixel * npix) / (P.p.rates[k] * 8.0) - tp_offset : 0.0;
         const double sot_adjust = (npix * (double)header_size) / ((double)P.w * (double)P.h);
         if (rates[0] > 0.0) { rates[0] -= sot_adjust; if (rates[0] < 30.0f) rates[0] = 30.0f; }
         for (uint32_t k = 1; k + 1 < L; ++k)
@@ -1576,9 +1617,11 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
                      // 6 bytes (Ttlm u16, Ptlm u32) per tile part, filled in after the tiles are written
         const uint32_t nt = (uint32_t)P.tiles.size();
         if (4 + 6 * (size_t)nt > 65535) throw GkError("too many tiles for one TLM marker");
-        put16(o, 0xff55); put16(o, 4 + 6 * nt); o.push_back(0); o.push_back(0x60);
+        const uint64_t ne = (uint64_t)nt * tile_part_split(P).n;   // one entry per tile part
+        if (4 + 6 * ne > 65535) throw GkError("TLM marker overflow (too many tile parts)");
+        put16(o, 0xff55); put16(o, (uint32_t)(4 + 6 * ne)); o.push_back(0); o.push_back(0x60);
         if (tlm_pos) *tlm_pos = o.size();
-        o.insert(o.end(), (size_t)6 * nt, 0);
+        o.insert(o.end(), (size_t)(6 * ne), 0);
     }
     if (P.p.write_com) {
         const char* txt = "Created by Grok     version 9.2.0";
@@ -1739,6 +1782,9 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     P.cblk_sty = cp->cblk_sty;
     if (cp->prog_order < 0 || cp->prog_order > 4) throw GkError("unknown progression order");
     P.prog = (uint32_t)cp->prog_order;
+    P.tp_div = cp->enableTilePartGeneration ? cp->newTilePartProgressionDivider : 0;
+    if (P.tp_div && P.tp_div != 'L' && P.tp_div != 'R' && P.tp_div != 'C')
+        throw GkError("tile-part divider must be L, R or C");
     if (cp->tile_size_on) { P.tw = cp->t_width; P.th = cp->t_height; }
     P.tlm = cp->writeTLM != 0; P.plt = cp->writePLT != 0;
     if (cp->cod_format != 0 && cp->cod_format != 2) throw GkError("cod_format must be GRK_CODEC_J2K (0) or GRK_CODEC_JP2 (2)");
@@ -2223,12 +2269,17 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     // independent, so they are built in parallel host threads and appended in tile order
     struct Pk { uint32_t hoff, hlen, s0, s1, len; };
     struct TileOut {
-        std::vector<uint8_t> tp;     // SOT [PLT] SOD
+        std::vector<uint8_t> tp;     // SOT [PLT] SOD (every tile part's, concatenated)
         std::vector<uint8_t> phdr;   // packet headers
         std::vector<Pk> pk;
         std::vector<uint32_t> bsegs; // (block, first byte, length) of every packet body
         uint64_t psot = 0;
+        std::vector<uint32_t> pkey;  // tile part of each packet
+        std::vector<uint32_t> tp_off, pk_first;   // per tile part: header offset in tp, first packet
+        std::vector<uint64_t> psots;
     };
+    const TilePartSplit TPS = tile_part_split(P);
+    if (part_lens && TPS.n > 1) throw GkError("tile-part generation is not supported with tile sharding");
     std::vector<TileOut> tout(te - tb);
     const bool par_chains = te - tb == 1;   // one tile: its precinct chains run in parallel instead
     auto build_tile_part = [&](uint32_t t, TileOut& O) {
@@ -2276,6 +2327,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         for (uint32_t r = 0, q = 0; r < P.p.numres; ++r)
             for (uint32_t c = 0; c < P.nc; ++c) { chain_at[r * P.nc + c] = q; q += T.comps[c].res[r].pw * T.comps[c].res[r].ph; }
         for (const PacketRef& pr : packet_order(P, T, L)) {
+                O.pkey.push_back(TPS.key(pr));
                 const size_t q = chain_at[pr.r * P.nc + pr.c] + pr.pi;
                 const uint32_t l = pr.l;
                 const TileOut& C = co[q];
@@ -2286,40 +2338,56 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
                 k.hoff = h0; k.s1 = s0 + (k.s1 - k.s0); k.s0 = s0;
                 O.pk.push_back(k);
             }
-        // tile part: SOT [PLT] SOD (CodeStreamCompress::writeTilePart :862-900)
+        // tile parts: SOT [PLT] SOD (CodeStreamCompress::writeTilePart :858-900); the PLT of every
+        // packet of the tile goes into the first part's header (TileProcessor::writeTilePartT2)
         std::vector<uint8_t>& tp = O.tp;
-        put16(tp, 0xff90); put16(tp, 10); put16(tp, t); put32(tp, 0); tp.push_back(0); tp.push_back(1);
-        if (P.p.plt) {   // PacketLengthMarkers::write (PacketLengthMarkers.cpp:107-175): Zplt 0, 7-bit groups MSB first
-            std::vector<uint8_t> v;
-            for (const Pk& k : O.pk) {
-                const int nbits = floorlog2(k.len) + 1, nbytes = (nbits + 6) / 7;
-                for (int q = nbytes - 1; q >= 0; --q) v.push_back((uint8_t)(((k.len >> (7 * q)) & 0x7F) | (q ? 0x80 : 0)));
+        size_t pk0 = 0;
+        for (uint32_t part = 0; part < TPS.n; ++part) {
+            size_t pk1 = pk0;
+            while (pk1 < O.pk.size() && O.pkey[pk1] == part) ++pk1;
+            const size_t h0 = tp.size();
+            O.tp_off.push_back((uint32_t)h0); O.pk_first.push_back((uint32_t)pk0);
+            put16(tp, 0xff90); put16(tp, 10); put16(tp, t); put32(tp, 0); tp.push_back((uint8_t)part);
+            tp.push_back((uint8_t)TPS.n);
+            if (P.p.plt && part == 0) {   // PacketLengthMarkers::write (PacketLengthMarkers.cpp:107-175): Zplt 0, 7-bit groups MSB first
+                std::vector<uint8_t> v;
+                for (const Pk& k : O.pk) {
+                    const int nbits = floorlog2(k.len) + 1, nbytes = (nbits + 6) / 7;
+                    for (int q = nbytes - 1; q >= 0; --q) v.push_back((uint8_t)(((k.len >> (7 * q)) & 0x7F) | (q ? 0x80 : 0)));
+                }
+                if (3 + v.size() > 65535) throw GkError("PLT marker overflow (too many packets in one tile)");
+                put16(tp, 0xff58); put16(tp, (uint32_t)(3 + v.size())); tp.push_back(0);
+                tp.insert(tp.end(), v.begin(), v.end());
             }
-            if (3 + v.size() > 65535) throw GkError("PLT marker overflow (too many packets in one tile)");
-            put16(tp, 0xff58); put16(tp, (uint32_t)(3 + v.size())); tp.push_back(0);
-            tp.insert(tp.end(), v.begin(), v.end());
+            put16(tp, 0xff93);
+            uint64_t psot = tp.size() - h0;
+            for (size_t q = pk0; q < pk1; ++q) psot += O.pk[q].len;
+            if (psot > 0xffffffffull) throw GkError("tile part exceeds 4 GiB");
+            tp[h0 + 6] = (uint8_t)(psot >> 24); tp[h0 + 7] = (uint8_t)(psot >> 16); tp[h0 + 8] = (uint8_t)(psot >> 8);
+            tp[h0 + 9] = (uint8_t)psot;
+            O.psots.push_back(psot);
+            pk0 = pk1;
         }
-        put16(tp, 0xff93);
-        uint64_t psot = tp.size();
-        for (const Pk& k : O.pk) psot += k.len;
-        if (psot > 0xffffffffull) throw GkError("tile part exceeds 4 GiB");
-        tp[6] = (uint8_t)(psot >> 24); tp[7] = (uint8_t)(psot >> 16); tp[8] = (uint8_t)(psot >> 8); tp[9] = (uint8_t)psot;
-        O.psot = psot;
+        if (pk0 != O.pk.size()) throw GkError("tile-part split out of packet order");
+        O.tp_off.push_back((uint32_t)tp.size()); O.pk_first.push_back((uint32_t)pk0);
+        O.psot = O.psots[0];
     };
     if (par_chains) build_tile_part(tb, tout[0]);   // (its chains use the pool: no nested pool call)
     else host_pool().run(te - tb, [&](size_t q) { build_tile_part(tb + (uint32_t)q, tout[q]); });
     const auto te3 = eclk::now();
     for (uint32_t t = tb; t < te; ++t) {
         TileOut& O = tout[t - tb];
-        const uint64_t psot = O.psot;
-        if (part_lens) part_lens[t - tb] = (uint32_t)psot;
-        if (P.p.tlm && with_header) {
-            uint8_t* e = hdrs.data() + main_at + tlm_pos + 6 * (size_t)t;   // the main header is hdrs[main_at ..)
+        if (part_lens) part_lens[t - tb] = (uint32_t)O.psot;
+        for (uint32_t part = 0; part < TPS.n; ++part) {
+        const uint64_t psot = O.psots[part];
+        if (P.p.tlm && with_header) {   // one TLM entry per tile part, in stream order
+            uint8_t* e = hdrs.data() + main_at + tlm_pos + 6 * ((size_t)t * TPS.n + part);   // the main header is hdrs[main_at ..)
             e[0] = (uint8_t)(t >> 8); e[1] = (uint8_t)t;
             e[2] = (uint8_t)(psot >> 24); e[3] = (uint8_t)(psot >> 16); e[4] = (uint8_t)(psot >> 8); e[5] = (uint8_t)psot;
         }
-        add_host(O.tp.data(), O.tp.size());
-        for (const Pk& k : O.pk) {
+        add_host(O.tp.data() + O.tp_off[part], O.tp_off[part + 1] - O.tp_off[part]);
+        for (uint32_t pq = O.pk_first[part]; pq < O.pk_first[part + 1]; ++pq) {
+            const Pk& k = O.pk[pq];
             add_host(O.phdr.data() + k.hoff, k.hlen);
             for (uint32_t q = k.s0; q < k.s1; q += 3) {
                 const uint32_t b = O.bsegs[q], off = O.bsegs[q + 1], n = O.bsegs[q + 2];
@@ -2335,6 +2403,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
                 seg.push_back(so + off); seg.push_back(pos); seg.push_back(n);
                 pos += n;
             }
+        }
         }
     }
     uint8_t eoc[2] = {0xff, 0xd9};

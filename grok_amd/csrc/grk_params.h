@@ -23,7 +23,6 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     if (g.prog_order < GRK_LRCP || g.prog_order > GRK_CPRL) return refuse("unknown progression order");
     if (g.roi_compno >= 0) return refuse("region of interest (RGN) is not supported on this path");
     if (g.tx0 || g.ty0 || g.image_offset_x0 || g.image_offset_y0) return refuse("image/tile offsets are not supported");
-    if (g.enableTilePartGeneration) return refuse("multiple tile parts per tile are not supported");
     // mct 255 = not set on the command line: grk_compress resolves it from the component count
     // once the image is loaded (grk_compress.cpp:1977-1981), as the engine does (>= 3 -> RCT/ICT)
     if (g.mct_data || (g.mct > 1 && g.mct != 255)) return refuse("Part-2 array MCT is not supported");
@@ -56,5 +55,7 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     p.writeTLM = g.writeTLM; p.writePLT = g.writePLT;
     p.cod_format = jp2 ? 2 : 0;
     p.prog_order = (int32_t)g.prog_order;
+    p.enableTilePartGeneration = g.enableTilePartGeneration ? 1 : 0;
+    p.newTilePartProgressionDivider = g.newTilePartProgressionDivider;
     return true;
 }

@@ -50,6 +50,8 @@ typedef struct gk_cparameters {
     int32_t cod_format;                  /* grk_cparameters::cod_format: GRK_CODEC_J2K (0, raw codestream) or
                                             GRK_CODEC_JP2 (2, JP2 file boxes around it; FileFormatCompress.cpp) */
     int32_t prog_order;                  /* grk_cparameters::prog_order: GRK_LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4 */
+    uint8_t enableTilePartGeneration;    /* grk_cparameters::enableTilePartGeneration (grk_compress -u) */
+    char newTilePartProgressionDivider;  /* grk_cparameters::newTilePartProgressionDivider: 'L', 'R' or 'C' */
 } gk_cparameters;
 
 /* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to

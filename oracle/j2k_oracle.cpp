@@ -80,6 +80,7 @@ struct Params {
     int write_com = 1;
     uint32_t cblk_sty = 0;      // mode switches (grok.h:98-103) or 0x40 = HTJ2K block coder (GRK_CBLKSTY_HT, grok.h:104)
     uint32_t prog = 0;          // progression order (GRK_PROG_ORDER): LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4
+    char tp_div = 0;            // tile-part divider 'L' / 'R' / 'C' (grk_compress -u), 0 = one part per tile
     uint32_t tw = 0, th = 0;    // nominal tile size (0 = one tile covering the image), grk_cparameters::t_width/t_height
     int tlm = 0, plt = 0;       // write TLM (-X) / PLT (-L) markers
     bool ht() const { return (cblk_sty & 0x40) != 0; }
@@ -1158,6 +1159,7 @@ static void tile_rect(const Params& p, uint32_t W, uint32_t H, uint32_t t, uint3
 // Main header: SOC SIZ [CAP] COD QCD [TLM] [COM] (CodeStreamCompress::init_header_writing
 // :822-860).  *tlm_pos receives the offset of the first TLM entry (6 bytes per tile
 // part: Ttlm u16, Ptlm u32; Stlm = 0x60, LengthCache.cpp:437-482), patched later.
+static int tile_parts(const Params& p, uint32_t nc);   // tile parts per tile (below)
 static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Params& p, const Comp& c0,
                               size_t* tlm_pos = nullptr) {
     put16(o, 0xff4f);                               // SOC
@@ -1204,7 +1206,7 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
         for (uint32_t r = 0; r < p.numres; ++r) for (auto& B : c0.res[r].bands) put16(o, (B.expn << 11) | B.mant);
     }
     if (p.tlm) {                                     // TLM (TileLengthMarkers::writeBegin)
-        uint32_t nt = tile_count(p, im.w, im.h);
+        uint32_t nt = tile_count(p, im.w, im.h) * (uint32_t)std::max(1, tile_parts(p, im.nc));   // entries per tile part
         put16(o, 0xff55); put16(o, 4 + 6 * nt); o.push_back(0); o.push_back(0x60);
         if (tlm_pos) *tlm_pos = o.size();
         o.insert(o.end(), (size_t)6 * nt, 0);
@@ -1291,6 +1293,33 @@ static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Par
     } else {                    // CPRL
         for (uint32_t c = 0; c < nc; ++c)
             walk([&](uint64_t x, uint64_t y) { for (uint32_t r = 0; r < nr; ++r) emit(c, r, x, y); });
+    }
+    return v;
+}
+
+// Tile parts (CodeStreamCompress::getNumTilePartsForProgression, :1899-1958): the indices
+// of the progression string up to the divider each open a new part; part count = product of
+// their ranges (-1: unsupported divider, one behind P).
+static int tile_parts(const Params& p, uint32_t nc) {
+    if (!p.tp_div) return 1;
+    static const char* names[5] = {"LRCP", "RLCP", "RPCL", "PCRL", "CPRL"};
+    int n = 1;
+    for (const char* q = names[p.prog]; *q; ++q) {
+        if (*q == 'P') return -1;
+        n *= *q == 'L' ? (int)p.nlayers : *q == 'R' ? (int)p.numres : (int)nc;
+        if (*q == p.tp_div) return n;
+    }
+    return -1;
+}
+static uint32_t tile_part_of(const Params& p, uint32_t nc, const PktRef& k) {
+    if (!p.tp_div) return 0;
+    static const char* names[5] = {"LRCP", "RLCP", "RPCL", "PCRL", "CPRL"};
+    uint32_t v = 0;
+    for (const char* q = names[p.prog]; *q; ++q) {
+        if (*q == 'L') v = v * p.nlayers + k.l;
+        else if (*q == 'R') v = v * p.numres + k.r;
+        else if (*q == 'C') v = v * nc + k.c;
+        if (*q == p.tp_div) break;
     }
     return v;
 }
@@ -1746,6 +1775,7 @@ typedef struct {
     uint32_t tile_w, tile_h, tlm, plt;
     uint32_t cod_format;   // 0 = raw codestream (GRK_CODEC_J2K), 2 = JP2 file (GRK_CODEC_JP2)
     uint32_t prog_order;   // GRK_PROG_ORDER
+    uint32_t tp_div;       // tile-part divider character ('L', 'R', 'C') or 0
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -1761,6 +1791,7 @@ static Params to_params(const orc_cparams* cp) {
     p.write_com = (int)cp->write_com;
     p.cblk_sty = cp->cblk_sty;
     p.prog = cp->prog_order;
+    p.tp_div = (char)cp->tp_div;
     if (p.ht()) p.numgbits = 1;   // grk_compress.cpp:1123-1124
     p.tw = cp->tile_w; p.th = cp->tile_h; p.tlm = (int)cp->tlm; p.plt = (int)cp->plt;
     for (uint32_t i = 0; i < 100; ++i) p.rates[i] = i < p.nlayers ? cp->layer_rate[i] : 0.0;
@@ -1967,8 +1998,10 @@ static void update_rates(const EncodeState& E, double* rates) {
     const Params& p = E.p;
     const double size_pixel = (double)E.im.nc * E.im.prec, bits_empty = 8.0;
     const double npix = (double)((uint64_t)(E.tx1 - E.tx0) * (E.ty1 - E.ty0));
+    // tile-part generation: (parts - 1) x 14 bytes of SOT + SOD, spread over the layers
+    const double offset = (double)((std::max(1, tile_parts(p, E.im.nc)) - 1) * 14) / (double)p.nlayers;
     for (uint32_t k = 0; k < p.nlayers; ++k)
-        rates[k] = p.rates[k] > 0.0 ? (size_pixel * npix) / (p.rates[k] * bits_empty) : 0.0;
+        rates[k] = p.rates[k] > 0.0 ? (size_pixel * npix) / (p.rates[k] * bits_empty) - offset : 0.0;
     double sot_adjust = (npix * (double)E.header_size) / ((double)E.im.w * (double)E.im.h);
     uint32_t k = 0;
     if (rates[0] > 0.0) { rates[0] -= sot_adjust; if (rates[0] < 30.0f) rates[0] = 30.0f; }
@@ -2027,37 +2060,51 @@ static void rate_allocate(EncodeState& E) {
 
 // One tile's packets in LRCP order (T2Compress::compressPackets); packet lengths
 // are recorded for PLT.
-static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector<uint32_t>& plens) {
+static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector<uint32_t>& plens,
+                         std::vector<uint32_t>* pparts = nullptr) {
     auto trees = make_trees(E);
     for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, E.p.nlayers)) {
         size_t before = body.size();
         write_packet(&body, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], nullptr);
         plens.push_back((uint32_t)(body.size() - before));
+        if (pparts) pparts->push_back(tile_part_of(E.p, E.im.nc, k));
     }
 }
 
 // Tile part: SOT [PLT] SOD packets (CodeStreamCompress::writeTilePart :862-900; SOT with
 // TPsot = 0, TNsot = 1; PLT from PacketLengthMarkers::write, PacketLengthMarkers.cpp:107-175:
 // Zplt = 0, each length as 7-bit groups MSB first with a continuation bit).
-static uint32_t write_tile_part(std::vector<uint8_t>& o, EncodeState& E) {
-    std::vector<uint8_t> body; std::vector<uint32_t> plens;
-    tile_packets(E, body, plens);
-    size_t sot = o.size();
-    put16(o, 0xff90); put16(o, 10); put16(o, E.tile); put32(o, 0); o.push_back(0); o.push_back(1);
-    if (E.p.plt) {
-        std::vector<uint8_t> v;
-        for (uint32_t L : plens) {
-            int nbits = floorlog2(L) + 1, nbytes = (nbits + 6) / 7;
-            for (int k = nbytes - 1; k >= 0; --k) v.push_back((uint8_t)(((L >> (7 * k)) & 0x7F) | (k ? 0x80 : 0)));
+// The tile's tile parts (CodeStreamCompress::writeTileParts / writeTilePart, :858-946): SOT
+// (TPsot = part, TNsot = parts) [PLT of every packet of the tile, first part only
+// (TileProcessor::writeTilePartT2)] SOD, packets.  Returns each part's Psot.
+static std::vector<uint32_t> write_tile_part(std::vector<uint8_t>& o, EncodeState& E) {
+    std::vector<uint8_t> body; std::vector<uint32_t> plens, pparts;
+    tile_packets(E, body, plens, &pparts);
+    const int np = tile_parts(E.p, E.im.nc);
+    std::vector<uint32_t> psots;
+    size_t pk = 0, boff = 0;
+    for (int part = 0; part < np; ++part) {
+        size_t sot = o.size();
+        put16(o, 0xff90); put16(o, 10); put16(o, E.tile); put32(o, 0); o.push_back((uint8_t)part); o.push_back((uint8_t)np);
+        if (E.p.plt && part == 0) {
+            std::vector<uint8_t> v;
+            for (uint32_t L : plens) {
+                int nbits = floorlog2(L) + 1, nbytes = (nbits + 6) / 7;
+                for (int k = nbytes - 1; k >= 0; --k) v.push_back((uint8_t)(((L >> (7 * k)) & 0x7F) | (k ? 0x80 : 0)));
+            }
+            put16(o, 0xff58); put16(o, (uint32_t)(3 + v.size())); o.push_back(0);
+            o.insert(o.end(), v.begin(), v.end());
         }
-        put16(o, 0xff58); put16(o, (uint32_t)(3 + v.size())); o.push_back(0);
-        o.insert(o.end(), v.begin(), v.end());
+        put16(o, 0xff93);
+        size_t bl = 0;
+        while (pk < plens.size() && pparts[pk] == (uint32_t)part) bl += plens[pk++];
+        o.insert(o.end(), body.begin() + boff, body.begin() + boff + bl);
+        boff += bl;
+        uint32_t psot = (uint32_t)(o.size() - sot);
+        o[sot + 6] = (uint8_t)(psot >> 24); o[sot + 7] = (uint8_t)(psot >> 16); o[sot + 8] = (uint8_t)(psot >> 8); o[sot + 9] = (uint8_t)psot;
+        psots.push_back(psot);
     }
-    put16(o, 0xff93);
-    o.insert(o.end(), body.begin(), body.end());
-    uint32_t psot = (uint32_t)(o.size() - sot);
-    o[sot + 6] = (uint8_t)(psot >> 24); o[sot + 7] = (uint8_t)(psot >> 16); o[sot + 8] = (uint8_t)(psot >> 8); o[sot + 9] = (uint8_t)psot;
-    return psot;
+    return psots;
 }
 
 // Full encode (5/3 or 9/7, Part 1 or HT, any number of layers, one or more tiles).
@@ -2087,17 +2134,18 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
             write_main_header(o, E0.im, E0.p, E0.comps[0], &tlm_pos);
         }
         std::vector<std::vector<uint8_t>> parts(nt);
+        std::vector<std::vector<uint32_t>> psl(nt);
         par_for(nt, [&](size_t t) {
             EncodeState E;
             prepare_encode(E, planes, w, h, nc, prec, sgnd, cp, (uint32_t)t);
             t1_encode_all(E);
             rate_allocate(E);
-            write_tile_part(parts[t], E);
+            psl[t] = write_tile_part(parts[t], E);
         });
         for (uint32_t t = 0; t < nt; ++t) {
-            const uint32_t psot = (uint32_t)parts[t].size();
-            if (p0.tlm) {
-                size_t q = tlm_pos + (size_t)6 * t;
+            for (size_t k = 0; p0.tlm && k < psl[t].size(); ++k) {
+                const uint32_t psot = psl[t][k];
+                size_t q = tlm_pos + (size_t)6 * (t * psl[t].size() + k);
                 o[q] = (uint8_t)(t >> 8); o[q + 1] = (uint8_t)t;
                 o[q + 2] = (uint8_t)(psot >> 24); o[q + 3] = (uint8_t)(psot >> 16); o[q + 4] = (uint8_t)(psot >> 8); o[q + 5] = (uint8_t)psot;
             }
@@ -2123,9 +2171,10 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
         E.header_size = header_size;
         t1_encode_all(E);
         rate_allocate(E);
-        uint32_t psot = write_tile_part(o, E);
-        if (E.p.tlm) {
-            size_t q = tlm_pos + (size_t)6 * t;
+        const std::vector<uint32_t> psl = write_tile_part(o, E);
+        for (size_t k = 0; E.p.tlm && k < psl.size(); ++k) {
+            const uint32_t psot = psl[k];
+            size_t q = tlm_pos + (size_t)6 * (t * psl.size() + k);
             o[q] = (uint8_t)(t >> 8); o[q + 1] = (uint8_t)t;
             o[q + 2] = (uint8_t)(psot >> 24); o[q + 3] = (uint8_t)(psot >> 16); o[q + 4] = (uint8_t)(psot >> 8); o[q + 5] = (uint8_t)psot;
         }
@@ -2326,8 +2375,12 @@ void orc_t1_decode_cblk(const uint8_t* data, uint32_t len, uint32_t npasses, uin
 // planes are int32 at the image precision.  (CodeStreamDecompress.cpp marker
 // handlers; T2Decompress.cpp:216-570; TileProcessor decompress path.)
 // ----------------------------------------------------------------------------
-static int decode_tile(const uint8_t* cs, size_t data, size_t tile_end, const Params& p, const Image& im,
-                       const std::vector<std::pair<uint32_t, uint32_t>>& qcd, uint32_t tile, int32_t* out) {
+// ranges: the packet bytes [data, end) of the tile's tile parts in TPsot order (a tile's
+// packet sequence continues across its parts, A.4.2)
+static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, size_t>>& ranges, const Params& p,
+                       const Image& im, const std::vector<std::pair<uint32_t, uint32_t>>& qcd, uint32_t tile,
+                       int32_t* out) {
+    size_t data = ranges[0].first, tile_end = ranges[0].second, next_range = 1;
     uint32_t tx0, ty0, tx1, ty1;
     tile_rect(p, im.w, im.h, tile, tx0, ty0, tx1, ty1);
     const uint32_t TW = tx1 - tx0, TH = ty1 - ty0;
@@ -2362,6 +2415,9 @@ static int decode_tile(const uint8_t* cs, size_t data, size_t tile_end, const Pa
                 // the coding state, data skipped (T2Decompress::processPacket, T2Decompress.cpp:55-116)
                 const bool skip_l = (g_dec_layers && l >= g_dec_layers) || r + red >= p.numres;
                 {
+                    while (pos >= tile_end && next_range < ranges.size()) {
+                        pos = ranges[next_range].first; tile_end = ranges[next_range].second; ++next_range;
+                    }
                     if (pos >= tile_end) goto t2done;
                     BitReader br; br.p = cs + pos; br.len = tile_end - pos;
                     std::vector<std::pair<Cblk*, uint32_t>> contrib;  // block, bytes in this packet
@@ -2578,7 +2634,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     std::fill(out, out + (size_t)im.nc * *W * *H, 0);
     const uint32_t nt = tile_count(p, im.w, im.h);
     size_t pos = first_sot;
-    struct Part { size_t data, end; uint32_t tile; };
+    struct Part { size_t data, end; uint32_t tile, tpsot; };
     std::vector<Part> parts;
     while (pos + 12 <= len && get16(cs + pos) == 0xff90) {
         const uint8_t* s = cs + pos + 4;
@@ -2588,11 +2644,22 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         size_t j = pos + 12;   // tile-part header markers (PLT, ...) until SOD
         while (j + 2 <= tile_end && get16(cs + j) != 0xff93) j += 2 + get16(cs + j + 2);
         if (j + 2 > tile_end) return -5;
-        parts.push_back({j + 2, tile_end, isot});
+        parts.push_back({j + 2, tile_end, isot, s[6]});
         pos = tile_end;
     }
-    std::vector<int> rcs(parts.size(), 0);   // tiles write disjoint rectangles of out
-    par_for(parts.size(), [&](size_t q) { rcs[q] = decode_tile(cs, parts[q].data, parts[q].end, p, im, qcd, parts[q].tile, out); });
+    // a tile's parts in order (TPsot 0, 1, ...)
+    std::vector<uint32_t> tiles;
+    std::vector<std::vector<std::pair<size_t, size_t>>> ranges;
+    std::vector<int> slot(nt, -1);
+    for (const Part& q : parts) {
+        if (slot[q.tile] < 0) {
+            if (q.tpsot != 0) return -5;
+            slot[q.tile] = (int)tiles.size(); tiles.push_back(q.tile); ranges.emplace_back();
+        } else if (q.tpsot != ranges[slot[q.tile]].size()) return -5;
+        ranges[slot[q.tile]].push_back({q.data, q.end});
+    }
+    std::vector<int> rcs(tiles.size(), 0);   // tiles write disjoint rectangles of out
+    par_for(tiles.size(), [&](size_t q) { rcs[q] = decode_tile(cs, ranges[q], p, im, qcd, tiles[q], out); });
     for (int rc : rcs) if (rc) return rc;
     return 0;
 }

@@ -109,3 +109,35 @@ def test_split_tile_parts_device_stream(eng):
     sp = split_tile_parts(cs, 3, True)
     dev = torch.frombuffer(bytearray(sp), dtype=torch.uint8).cuda()
     np.testing.assert_array_equal(eng.decode(dev, length=len(sp)), img)
+
+
+GEN = [("LRCP", "L"), ("LRCP", "R"), ("RLCP", "R"), ("RPCL", "R"), ("CPRL", "C"), ("LRCP", "C")]
+
+
+@pytest.mark.parametrize("prog,div", GEN)
+def test_tile_part_generation_vs_oracle(eng, prog, div):
+    """grk_compress -u L|R|C (enableTilePartGeneration): a new tile part whenever the
+    progression's index up to the divider changes (getNumTilePartsForProgression), PLT in
+    the first part, TLM with one entry per part, 14 bytes per extra part off the rate
+    budget (updateRates).  Encode byte-identical to the oracle; decodes equal."""
+    import oracle as O
+    import grok_amd as G
+    img = _img(8, 3, 150, 170)
+    for kw in (dict(tiles=(64, 96), tlm=True, plt=True), dict(layer_rate=[30, 8, 2], precincts=[(64, 64)])):
+        gkw = dict(kw)
+        if "layer_rate" in gkw:
+            gkw["numlayers"] = len(gkw["layer_rate"])
+        cs = eng.encode(img, 8, params=G.default_params(numresolution=4, cblk=(16, 16), prog_order=prog,
+                                                        tile_parts=div, **gkw))
+        ref = O.encode(img, 8, numres=4, cblk=(16, 16), prog_order=prog, tile_parts=div, **kw)
+        assert cs == ref
+        np.testing.assert_array_equal(eng.decode(cs), O.decode(ref)[0])
+        if "tiles" in kw:
+            np.testing.assert_array_equal(eng.decode_window(cs, (20, 30, 150, 140)), img[:, 30:140, 20:150])
+
+
+def test_tile_part_divider_behind_position_refused(eng):
+    import grok_amd as G
+    img = _img(9, 1, 64, 64)
+    with pytest.raises(Exception):
+        eng.encode(img, 8, params=G.default_params(numresolution=3, prog_order="PCRL", tile_parts="C"))

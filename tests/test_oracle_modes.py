@@ -64,3 +64,13 @@ def test_oracle_layer_limit():
     finally:
         O.set_decode_layers(0)
     assert errs[0] > errs[1] > errs[2] == 0
+
+
+@pytest.mark.parametrize("prog,div", [("LRCP", "L"), ("LRCP", "R"), ("RPCL", "R"), ("CPRL", "C")])
+def test_oracle_tile_part_generation(prog, div):
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 256, size=(3, 90, 100)).astype(np.int32)
+    cs = O.encode(img, 8, numres=3, cblk=(16, 16), prog_order=prog, tile_parts=div, tiles=(64, 64), tlm=True, plt=True,
+                  layer_rate=[10, 0])
+    assert cs.count(b"\xff\x90") > 4   # several SOT markers per tile
+    np.testing.assert_array_equal(O.decode(cs)[0], img)
