@@ -26,6 +26,12 @@ EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_
            "gk_last_error", "gk_version", "gk_set_decode_layers", "gk_set_decode_reduce")
 
 
+class Poc(ctypes.Structure):
+    """gk_poc (include/grok_amd.h): one progression order change."""
+    _fields_ = [("resS", ctypes.c_uint32), ("compS", ctypes.c_uint32), ("layE", ctypes.c_uint32),
+                ("resE", ctypes.c_uint32), ("compE", ctypes.c_uint32), ("prog", ctypes.c_int32)]
+
+
 class CParameters(ctypes.Structure):
     """gk_cparameters (include/grok_amd.h) — subset of grk_cparameters (grok.h:466-590)."""
     _fields_ = [
@@ -43,6 +49,7 @@ class CParameters(ctypes.Structure):
         ("writeTLM", ctypes.c_uint8), ("writePLT", ctypes.c_uint8),
         ("cod_format", ctypes.c_int32), ("prog_order", ctypes.c_int32),
         ("enableTilePartGeneration", ctypes.c_uint8), ("newTilePartProgressionDivider", ctypes.c_char),
+        ("numpocs", ctypes.c_uint32), ("pocs", Poc * 32),
     ]
 
 
@@ -120,7 +127,7 @@ PROG_ORDERS = ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"]   # GRK_PROG_ORDER (grok.
 
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
                    precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False,
-                   prog_order="LRCP", tile_parts=None):
+                   prog_order="LRCP", tile_parts=None, pocs=None):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
     prog_order: "LRCP", "RLCP", "RPCL", "PCRL", "CPRL" or 0..4 (grk_compress -p).
@@ -152,6 +159,10 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
     p.writeTLM, p.writePLT = int(bool(tlm)), int(bool(plt))
     p.cod_format = 2 if jp2 else 0   # GRK_CODEC_JP2 / GRK_CODEC_J2K
     p.prog_order = PROG_ORDERS.index(prog_order) if isinstance(prog_order, str) else int(prog_order)
+    if pocs:   # [(resS, compS, layE, resE, compE, "PROG"), ...] (grk_compress -P)
+        p.numpocs = len(pocs)
+        for i, (rs, cs, le, re_, ce, pr) in enumerate(pocs):
+            p.pocs[i] = Poc(rs, cs, le, re_, ce, PROG_ORDERS.index(pr) if isinstance(pr, str) else int(pr))
     if tile_parts:   # grk_compress -u L|R|C: a new tile part whenever that index changes
         p.enableTilePartGeneration = 1
         p.newTilePartProgressionDivider = tile_parts.encode()

@@ -127,6 +127,10 @@ static HostPool& host_pool() {   // one pool per process, sized to the CPU share
 // Tile geometry (ISO 15444-1 Annex B; Grok Resolution.h:37-72,
 // Precinct.h:59-68).  Single tile anchored at the image origin.
 // ---------------------------------------------------------------------------
+// One progression order change (POC marker, A.6.6): layers [0, lye), resolutions [rs, re),
+// components [cs, ce) in progression prog.
+struct Poc { uint32_t rs = 0, cs = 0, lye = 0, re = 0, ce = 0, prog = 0; };
+
 struct Params {
     uint32_t numres = 6, cbw = 6, cbh = 6, irrev = 0, mct = 1, numgbits = 2, nlayers = 1, write_com = 1;
     uint32_t prcw[GK_MAXRLVLS], prch[GK_MAXRLVLS];
@@ -135,6 +139,7 @@ struct Params {
     uint32_t cblk_sty = 0;               // Part-1 mode switches or GRK_CBLKSTY_HT (0x40, grok.h:98-104)
     uint32_t prog = 0;                   // progression order: GRK_LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4
     char tp_div = 0;                     // tile-part divider 'L' / 'R' / 'C' (grk_compress -u), 0 = one part per tile
+    std::vector<Poc> pocs;               // progression order changes (every tile; empty = prog)
     bool ht() const { return (cblk_sty & 0x40) != 0; }
     uint32_t tw = 0, th = 0;             // nominal tile size (grk_cparameters::t_width/t_height; 0 = image)
     bool tlm = false, plt = false;       // grk_cparameters::writeTLM / writePLT
@@ -838,23 +843,24 @@ struct DecTree {   // decoder-side tag tree
 // y, anchor x) with the order's other indices around it.
 // ---------------------------------------------------------------------------
 struct PacketRef { uint32_t l, r, c, pi; };
-static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32_t L) {
-    std::vector<PacketRef> out;
-    const uint32_t nr = P.p.numres, nc = P.nc;
+// One progression over layers [0, L), resolutions [r0, r1), components [c0, c1).
+static void order_ranges(const Plan& P, const TileG& T, uint32_t prog, uint32_t L, uint32_t r0, uint32_t r1, uint32_t c0,
+                         uint32_t c1, std::vector<PacketRef>& out) {
+    const uint32_t nr = P.p.numres;
     auto np = [&](uint32_t c, uint32_t r) { const ResG& R = T.comps[c].res[r]; return R.w && R.h ? R.pw * R.ph : 0u; };
-    if (P.p.prog == 0 || P.p.prog == 1) {   // LRCP / RLCP
-        for (uint32_t a = 0; a < (P.p.prog == 0 ? L : nr); ++a)
-            for (uint32_t b = 0; b < (P.p.prog == 0 ? nr : L); ++b)
-                for (uint32_t c = 0; c < nc; ++c) {
-                    const uint32_t l = P.p.prog == 0 ? a : b, r = P.p.prog == 0 ? b : a;
+    if (prog == 0 || prog == 1) {   // LRCP / RLCP
+        for (uint32_t a = (prog == 0 ? 0 : r0); a < (prog == 0 ? L : r1); ++a)
+            for (uint32_t b = (prog == 0 ? r0 : 0); b < (prog == 0 ? r1 : L); ++b)
+                for (uint32_t c = c0; c < c1; ++c) {
+                    const uint32_t l = prog == 0 ? a : b, r = prog == 0 ? b : a;
                     for (uint32_t pi = 0; pi < np(c, r); ++pi) out.push_back({l, r, c, pi});
                 }
-        return out;
+        return;
     }
     struct Pr { uint64_t ay, ax; uint32_t r, c, pi; };
     std::vector<Pr> v;
-    for (uint32_t c = 0; c < nc; ++c)
-        for (uint32_t r = 0; r < nr; ++r) {
+    for (uint32_t c = c0; c < c1; ++c)
+        for (uint32_t r = r0; r < r1; ++r) {
             const ResG& R = T.comps[c].res[r];
             const uint32_t n = np(c, r), lv = nr - 1 - r, pwe = P.p.prcw[r], phe = P.p.prch[r];
             for (uint32_t pi = 0; pi < n; ++pi) {
@@ -866,14 +872,44 @@ static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32
         }
     auto key = [&](const Pr& a) {
         // RPCL: r, y, x, c; PCRL: y, x, c, r; CPRL: c, y, x, r (layers innermost)
-        if (P.p.prog == 2) return std::make_tuple((uint64_t)a.r, a.ay, a.ax, (uint64_t)a.c);
-        if (P.p.prog == 3) return std::make_tuple(a.ay, a.ax, (uint64_t)a.c, (uint64_t)a.r);
+        if (prog == 2) return std::make_tuple((uint64_t)a.r, a.ay, a.ax, (uint64_t)a.c);
+        if (prog == 3) return std::make_tuple(a.ay, a.ax, (uint64_t)a.c, (uint64_t)a.r);
         return std::make_tuple((uint64_t)a.c, a.ay, a.ax, (uint64_t)a.r);
     };
     std::stable_sort(v.begin(), v.end(), [&](const Pr& a, const Pr& b) { return key(a) < key(b); });
-    out.reserve(v.size() * L);
     for (const Pr& q : v)
         for (uint32_t l = 0; l < L; ++l) out.push_back({l, q.r, q.c, q.pi});
+}
+
+// The tile's packet order: its progression, or with progression order changes (POC marker,
+// A.6.6; PacketIter over the tile's progressions, each packet at most once: update_include)
+// the concatenation of every entry's progression over its ranges, clamped to the stream's
+// layers / resolutions / components, skipping packets an earlier entry already emitted.
+static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32_t L,
+                                           const std::vector<Poc>* pocs = nullptr) {
+    std::vector<PacketRef> out;
+    if (!pocs || pocs->empty()) {
+        order_ranges(P, T, P.p.prog, L, 0, P.p.numres, 0, P.nc, out);
+        return out;
+    }
+    // packet id: ((c * numres + r) * maxprc + pi) * L + l
+    uint32_t maxprc = 1;
+    for (uint32_t c = 0; c < P.nc; ++c)
+        for (uint32_t r = 0; r < P.p.numres; ++r) maxprc = std::max(maxprc, T.comps[c].res[r].pw * T.comps[c].res[r].ph);
+    std::vector<uint8_t> seen((size_t)P.nc * P.p.numres * maxprc * L, 0);
+    std::vector<PacketRef> sub;
+    for (const Poc& q : *pocs) {
+        sub.clear();
+        const uint32_t le = std::min(q.lye, L), r1 = std::min(q.re, P.p.numres), c1 = std::min(q.ce, P.nc);
+        if (q.rs >= r1 || q.cs >= c1 || !le) continue;
+        order_ranges(P, T, q.prog, le, q.rs, r1, q.cs, c1, sub);
+        for (const PacketRef& pr : sub) {
+            uint8_t& sflag = seen[(((size_t)pr.c * P.p.numres + pr.r) * maxprc + pr.pi) * L + pr.l];
+            if (sflag) continue;
+            sflag = 1;
+            out.push_back(pr);
+        }
+    }
     return out;
 }
 
@@ -904,6 +940,7 @@ static TilePartSplit tile_part_split(const Plan& P) {
     TilePartSplit S;
     S.prog = names[P.p.prog]; S.L = P.p.nlayers; S.R = P.p.numres; S.C = P.nc;
     if (!P.p.tp_div) return S;
+    if (!P.p.pocs.empty()) throw GkError("tile-part generation with progression order changes is not supported");
     for (int j = 0; j < 4; ++j) {
         const char ch = S.prog[j];
         if (ch == 'P') throw GkError("a tile-part divider behind the position index is not supported");
@@ -1099,7 +1136,7 @@ struct T2Enc {
     bool simulate(uint32_t max_layers, uint64_t max_bytes) {
         uint64_t budget = max_bytes;
         uint64_t* bp = max_bytes == 0xffffffffull ? nullptr : &budget;
-        for (const PacketRef& pr : packet_order(P, P.tiles[t0], max_layers))   // rate control: one tile
+        for (const PacketRef& pr : packet_order(P, P.tiles[t0], max_layers, &P.p.pocs))   // rate control: one tile
             if (!write_packet(P.tiles[t0].comps[pr.c].res[pr.r], pr.pi, pr.l, bp, nullptr)) return false;
         return true;
     }
@@ -1490,7 +1527,9 @@ struct T2Enc {
         double min_slope = 1.7976931348623157e308, max_slope = -1;
         for (uint32_t ci = 0; ci < nsch; ++ci) { min_slope = std::min(min_slope, smin[ci]); max_slope = std::max(max_slope, smax[ci]); }
         double upper = max_slope;
-        const bool fast = t1 == t0 + 1 && !getenv("GK_T2_SERIAL_SIM");
+        // (with progression order changes the last packet of a layer's budget test is not
+        // known per chain: every bisection step runs the serial simulation)
+        const bool fast = t1 == t0 + 1 && !getenv("GK_T2_SERIAL_SIM") && P.p.pocs.empty();
         static const bool prof = getenv("GK_PROFILE") != nullptr;
         using clk = std::chrono::steady_clock;
         auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1782,6 +1821,16 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     P.cblk_sty = cp->cblk_sty;
     if (cp->prog_order < 0 || cp->prog_order > 4) throw GkError("unknown progression order");
     P.prog = (uint32_t)cp->prog_order;
+    if (cp->numpocs > 32) throw GkError("at most 32 progression order changes");
+    P.pocs.clear();
+    for (uint32_t i = 0; i < cp->numpocs; ++i) {
+        const gk_poc& g = cp->pocs[i];
+        if (g.prog < 0 || g.prog > 4 || g.resE > GK_MAXRLVLS || g.resS >= g.resE || g.compS >= g.compE || !g.layE ||
+            g.layE > 65535 || g.compE > 16384)
+            throw GkError("bad progression order change");
+        Poc e; e.rs = g.resS; e.cs = g.compS; e.lye = g.layE; e.re = g.resE; e.ce = g.compE; e.prog = (uint32_t)g.prog;
+        P.pocs.push_back(e);
+    }
     P.tp_div = cp->enableTilePartGeneration ? cp->newTilePartProgressionDivider : 0;
     if (P.tp_div && P.tp_div != 'L' && P.tp_div != 'R' && P.tp_div != 'C')
         throw GkError("tile-part divider must be L, R or C");
@@ -2326,7 +2375,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         std::vector<uint32_t> chain_at(P.p.numres * P.nc + 1, 0);
         for (uint32_t r = 0, q = 0; r < P.p.numres; ++r)
             for (uint32_t c = 0; c < P.nc; ++c) { chain_at[r * P.nc + c] = q; q += T.comps[c].res[r].pw * T.comps[c].res[r].ph; }
-        for (const PacketRef& pr : packet_order(P, T, L)) {
+        for (const PacketRef& pr : packet_order(P, T, L, &P.p.pocs)) {
                 O.pkey.push_back(TPS.key(pr));
                 const size_t q = chain_at[pr.r * P.nc + pr.c] + pr.pi;
                 const uint32_t l = pr.l;
@@ -2349,6 +2398,18 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             O.tp_off.push_back((uint32_t)h0); O.pk_first.push_back((uint32_t)pk0);
             put16(tp, 0xff90); put16(tp, 10); put16(tp, t); put32(tp, 0); tp.push_back((uint8_t)part);
             tp.push_back((uint8_t)TPS.n);
+            if (part == 0 && !P.p.pocs.empty()) {   // POC in the first tile part (CodeStreamCompress::writePoc :1278-1340)
+                const uint32_t cw = P.nc <= 256 ? 1 : 2;
+                put16(tp, 0xff5f); put16(tp, 2 + (uint32_t)P.p.pocs.size() * (5 + 2 * cw));
+                for (const Poc& e : P.p.pocs) {
+                    tp.push_back((uint8_t)e.rs);
+                    if (cw == 1) tp.push_back((uint8_t)e.cs); else put16(tp, e.cs);
+                    put16(tp, e.lye);
+                    tp.push_back((uint8_t)e.re);
+                    if (cw == 1) tp.push_back((uint8_t)e.ce); else put16(tp, e.ce);
+                    tp.push_back((uint8_t)e.prog);
+                }
+            }
             if (P.p.plt && part == 0) {   // PacketLengthMarkers::write (PacketLengthMarkers.cpp:107-175): Zplt 0, 7-bit groups MSB first
                 std::vector<uint8_t> v;
                 for (const Pk& k : O.pk) {
@@ -2464,7 +2525,28 @@ struct TilePart {                  // packet bytes [data, end) of one tile part
     // parts in order); their PLT lengths are appended to plt
     std::vector<std::pair<size_t, size_t>> more;
     uint32_t tpsot = 0;
+    std::vector<Poc> pocs;          // POC in the tile's first tile-part header (overrides the main header's)
 };
+// POC marker body (A.6.6): per entry RSpoc, CSpoc (1 or 2 bytes), LYEpoc (2), REpoc, CEpoc
+// (1 or 2; 0 = 256 with one byte), Ppoc (CodeStreamDecompress::read_poc)
+template <class Src>
+static void parse_poc(Src& S, size_t s, uint32_t L, uint32_t nc, std::vector<Poc>& out) {
+    const uint32_t cw = nc <= 256 ? 1 : 2, esz = 5 + 2 * cw;
+    if (L < 2 + esz || (L - 2) % esz) throw GkError("corrupt POC marker");
+    out.clear();
+    for (size_t q = s; q + esz <= s + L - 2; q += esz) {
+        Poc e;
+        e.rs = S.at(q);
+        e.cs = cw == 1 ? S.at(q + 1) : S.be16(q + 1);
+        e.lye = S.be16(q + 1 + cw);
+        e.re = S.at(q + 3 + cw);
+        e.ce = cw == 1 ? S.at(q + 4 + cw) : S.be16(q + 4 + cw);
+        if (cw == 1 && e.ce == 0) e.ce = 256;
+        e.prog = S.at(q + 4 + 2 * cw);
+        if (e.prog > 4 || e.re > 33) throw GkError("corrupt POC marker");
+        out.push_back(e);
+    }
+}
 struct Header {
     Plan want;
     std::vector<std::pair<uint32_t, uint32_t>> qcd;
@@ -2550,8 +2632,10 @@ static void parse_header(ByteSrc& S, Header& Hd) {
                 tnext = t + 1;
                 e += esz;
             }
-        } else if (m == 0xff5d || m == 0xff53 || m == 0xff5e || m == 0xff5f) {
-            throw GkError("QCC/COC/RGN/POC markers not supported on this path yet");
+        } else if (m == 0xff5f) {   // POC in the main header: every tile's packet order
+            parse_poc(S, s, L, W.nc, W.p.pocs);
+        } else if (m == 0xff5d || m == 0xff53 || m == 0xff5e) {
+            throw GkError("QCC/COC/RGN markers not supported on this path yet");
         }
         i += 2 + L;
     }
@@ -2579,9 +2663,13 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             const size_t end = psot ? pos + psot : (S.len >= 2 ? S.len - 2 : S.len);
             if (end > S.len || end < pos + 14) throw GkError("corrupt SOT (Psot)");
             size_t j = pos + 12;
-            while (j + 4 <= end && S.be16(j) != 0xff93) j += 2 + S.be16(j + 2);
+            std::vector<Poc> tpoc;
+            while (j + 4 <= end && S.be16(j) != 0xff93) {
+                if (S.be16(j) == 0xff5f) parse_poc(S, j + 4, S.be16(j + 2), W.nc, tpoc);   // tile-part POC
+                j += 2 + S.be16(j + 2);
+            }
             if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
-            Hd.parts.push_back({isot, pos, j + 2, end, {}, {}, S.at(pos + 10)});
+            Hd.parts.push_back({isot, pos, j + 2, end, {}, {}, S.at(pos + 10), std::move(tpoc)});
             pos = end;
         }
     }
@@ -2615,6 +2703,7 @@ static void fetch_ranges(gk_ctx* ctx, ByteSrc& S, const std::vector<std::pair<si
 // Tile-part headers of parts located through TLM: SOD position and PLT packet lengths
 // (PacketLengthMarkers::readPLT: Zplt, then 7-bit groups MSB first, bit 7 = continuation).
 static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
+    const uint32_t nc = Hd.want.nc;
     std::vector<std::pair<size_t, size_t>> rg;
     for (auto& TP : Hd.parts)
         if (!TP.data) rg.push_back({TP.sot, std::min<size_t>(TP.end - TP.sot, 4096)});
@@ -2627,6 +2716,7 @@ static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
         size_t j = TP.sot + 12;
         while (j + 4 <= TP.end && S.be16(j) != 0xff93) {
             const uint32_t m = S.be16(j), L = S.be16(j + 2);
+            if (m == 0xff5f) parse_poc(S, j + 4, L, nc, TP.pocs);   // tile-part POC
             if (m == 0xff58) {
                 uint32_t v = 0;
                 for (size_t q = j + 5; q < j + 2 + L; ++q) {
@@ -2650,7 +2740,7 @@ static void prefetch_packet_headers(gk_ctx* ctx, ByteSrc& S, const Plan& P, cons
         if (TP.plt.empty() || TP.tile >= P.tiles.size()) continue;
         const TileG& T = P.tiles[TP.tile];
         size_t pos = TP.data, end = TP.end, k = 0, nextp = 0;
-        for (const PacketRef& pr : packet_order(P, T, P.p.nlayers)) {
+        for (const PacketRef& pr : packet_order(P, T, P.p.nlayers, TP.pocs.empty() ? &P.p.pocs : &TP.pocs)) {
             if (k >= TP.plt.size()) break;
             const ResG& R = T.comps[pr.c].res[pr.r];
             while (pos >= end && nextp < TP.more.size()) { pos = TP.more[nextp].first; end = TP.more[nextp].second; ++nextp; }
@@ -2845,7 +2935,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         st2.chunks.reserve(ntb);
         size_t tile_end = TPt.end;
         size_t pos = TPt.data, pk = 0, nextp = 0;
-        const std::vector<PacketRef> order = packet_order(P, TG, P.p.nlayers);
+        const std::vector<PacketRef> order = packet_order(P, TG, P.p.nlayers, TPt.pocs.empty() ? &P.p.pocs : &TPt.pocs);
         // layer limit (tcp->numLayersToDecompress): packets of later layers are skipped through
         // PLT or parsed without their data (T2Decompress::processPacket, T2Decompress.cpp:55-116)
         const uint32_t maxl = ctx->dec_layers ? std::min(ctx->dec_layers, P.p.nlayers) : P.p.nlayers;

@@ -26,6 +26,13 @@ extern "C" {
 #define GK_MAXRLVLS 33
 #define GK_MAX_LAYERS 100
 
+/* One progression order change (grk_progression's resS, compS, layE, resE, compE, progression;
+ * POC marker A.6.6): layers [0, layE), resolutions [resS, resE), components [compS, compE). */
+typedef struct gk_poc {
+    uint32_t resS, compS, layE, resE, compE;
+    int32_t prog;                        /* GRK_PROG_ORDER */
+} gk_poc;
+
 /* Coding parameters: the subset of grk_cparameters (grok.h:466-590) the hot
  * path consumes, with the same field names and meaning. */
 typedef struct gk_cparameters {
@@ -52,6 +59,9 @@ typedef struct gk_cparameters {
     int32_t prog_order;                  /* grk_cparameters::prog_order: GRK_LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4 */
     uint8_t enableTilePartGeneration;    /* grk_cparameters::enableTilePartGeneration (grk_compress -u) */
     char newTilePartProgressionDivider;  /* grk_cparameters::newTilePartProgressionDivider: 'L', 'R' or 'C' */
+    uint32_t numpocs;                    /* progression order changes, written as a POC marker in each tile's
+                                            first tile-part header (CodeStreamCompress::writePoc) */
+    gk_poc pocs[32];
 } gk_cparameters;
 
 /* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to

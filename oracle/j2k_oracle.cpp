@@ -68,6 +68,8 @@ static inline int floorlog2(uint32_t a) { int l = 0; while (a > 1) { a >>= 1; ++
 // ----------------------------------------------------------------------------
 // Coding parameters (subset of grk_cparameters, grok.h:466-590)
 // ----------------------------------------------------------------------------
+struct PocE { uint32_t rs, cs, lye, re, ce, prog; };   // progression order change (POC marker, A.6.6)
+
 struct Params {
     uint32_t numres = 6;        // grok.cpp:405-435 default: 6 resolutions
     uint32_t cbw_exp = 6, cbh_exp = 6;  // 64x64
@@ -81,6 +83,7 @@ struct Params {
     uint32_t cblk_sty = 0;      // mode switches (grok.h:98-103) or 0x40 = HTJ2K block coder (GRK_CBLKSTY_HT, grok.h:104)
     uint32_t prog = 0;          // progression order (GRK_PROG_ORDER): LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4
     char tp_div = 0;            // tile-part divider 'L' / 'R' / 'C' (grk_compress -u), 0 = one part per tile
+    std::vector<PocE> pocs;     // progression order changes (encode: every tile; decode: main header)
     uint32_t tw = 0, th = 0;    // nominal tile size (0 = one tile covering the image), grk_cparameters::t_width/t_height
     int tlm = 0, plt = 0;       // write TLM (-X) / PLT (-L) markers
     bool ht() const { return (cblk_sty & 0x40) != 0; }
@@ -1160,6 +1163,37 @@ static void tile_rect(const Params& p, uint32_t W, uint32_t H, uint32_t t, uint3
 // :822-860).  *tlm_pos receives the offset of the first TLM entry (6 bytes per tile
 // part: Ttlm u16, Ptlm u32; Stlm = 0x60, LengthCache.cpp:437-482), patched later.
 static int tile_parts(const Params& p, uint32_t nc);   // tile parts per tile (below)
+
+// POC marker (A.6.6): RSpoc, CSpoc, LYEpoc (16 bit), REpoc, CEpoc, Ppoc per entry; CSpoc /
+// CEpoc take two bytes when there are more than 256 components, CEpoc 0 means 256.
+static bool read_poc(const uint8_t* s, uint32_t L, uint32_t nc, std::vector<PocE>& out) {
+    const uint32_t cw = nc <= 256 ? 1 : 2, esz = 5 + 2 * cw;
+    if (L < 2 + esz || (L - 2) % esz) return false;
+    out.clear();
+    for (uint32_t q = 0; q + esz <= L - 2; q += esz) {
+        const uint8_t* e = s + q;
+        PocE v;
+        v.rs = e[0]; v.cs = cw == 1 ? e[1] : get16(e + 1); v.lye = get16(e + 1 + cw); v.re = e[3 + cw];
+        v.ce = cw == 1 ? e[4 + cw] : get16(e + 4 + cw);
+        if (cw == 1 && v.ce == 0) v.ce = 256;
+        v.prog = e[4 + 2 * cw];
+        if (v.prog > 4) return false;
+        out.push_back(v);
+    }
+    return true;
+}
+static void write_poc(std::vector<uint8_t>& o, const std::vector<PocE>& pocs, uint32_t nc) {   // CodeStreamCompress::writePoc
+    const uint32_t cw = nc <= 256 ? 1 : 2;
+    put16(o, 0xff5f); put16(o, 2 + (uint32_t)pocs.size() * (5 + 2 * cw));
+    for (const PocE& e : pocs) {
+        o.push_back((uint8_t)e.rs);
+        if (cw == 1) o.push_back((uint8_t)e.cs); else put16(o, e.cs);
+        put16(o, e.lye);
+        o.push_back((uint8_t)e.re);
+        if (cw == 1) o.push_back((uint8_t)e.ce); else put16(o, e.ce);
+        o.push_back((uint8_t)e.prog);
+    }
+}
 static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Params& p, const Comp& c0,
                               size_t* tlm_pos = nullptr) {
     put16(o, 0xff4f);                               // SOC
@@ -1229,22 +1263,31 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
 // where the position is a multiple of its size, or the tile origin when the resolution's
 // origin is not (generatePrecinctIndex, :287-335).  Each packet at most once.
 struct PktRef { uint32_t l, r, c, pi; };
-static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Params& p, uint32_t tx0, uint32_t ty0,
-                                       uint32_t tx1, uint32_t ty1, uint32_t nlayers) {
-    std::vector<PktRef> v;
+// One progression over layers [0, nlayers), resolutions [r0, r1), components [c0, c1); packets
+// already in `seen` (per (c, r, pi, l)) are skipped (PacketIter::update_include).
+static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uint32_t prog, uint32_t tx0, uint32_t ty0,
+                            uint32_t tx1, uint32_t ty1, uint32_t nlayers, uint32_t L, uint32_t r0, uint32_t r1,
+                            uint32_t c0, uint32_t c1, std::vector<uint8_t>& seen, const std::vector<uint32_t>& base,
+                            std::vector<PktRef>& v) {
     const uint32_t nc = (uint32_t)comps.size(), nr = p.numres;
     auto nprc = [&](uint32_t c, uint32_t r) {
         const Res& R = comps[c].res[r];
         return (R.x1 > R.x0 && R.y1 > R.y0) ? R.pw * R.ph : 0u;
     };
-    if (p.prog == 0 || p.prog == 1) {
-        for (uint32_t a = 0; a < (p.prog == 0 ? nlayers : nr); ++a)
-            for (uint32_t b = 0; b < (p.prog == 0 ? nr : nlayers); ++b)
-                for (uint32_t c = 0; c < nc; ++c) {
-                    const uint32_t l = p.prog == 0 ? a : b, r = p.prog == 0 ? b : a;
-                    for (uint32_t pi = 0; pi < nprc(c, r); ++pi) v.push_back({l, r, c, pi});
+    auto put = [&](uint32_t l, uint32_t r, uint32_t c, uint32_t pi) {
+        uint8_t& f = seen[((size_t)base[c * nr + r] + pi) * L + l];
+        if (f) return;
+        f = 1;
+        v.push_back({l, r, c, pi});
+    };
+    if (prog == 0 || prog == 1) {
+        for (uint32_t a = (prog == 0 ? 0 : r0); a < (prog == 0 ? nlayers : r1); ++a)
+            for (uint32_t b = (prog == 0 ? r0 : 0); b < (prog == 0 ? r1 : nlayers); ++b)
+                for (uint32_t c = c0; c < c1; ++c) {
+                    const uint32_t l = prog == 0 ? a : b, r = prog == 0 ? b : a;
+                    for (uint32_t pi = 0; pi < nprc(c, r); ++pi) put(l, r, c, pi);
                 }
-        return v;
+        return;
     }
     uint64_t dx = ~0ull, dy = ~0ull;
     for (uint32_t c = 0; c < nc; ++c)
@@ -1253,11 +1296,6 @@ static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Par
             dx = std::min<uint64_t>(dx, 1ull << (comps[c].res[r].prcw_exp + lv));
             dy = std::min<uint64_t>(dy, 1ull << (comps[c].res[r].prch_exp + lv));
         }
-    std::vector<uint8_t> seen;
-    std::vector<uint32_t> base(nc * nr + 1, 0);
-    for (uint32_t c = 0, k = 0; c < nc; ++c)
-        for (uint32_t r = 0; r < nr; ++r, ++k) base[k + 1] = base[k] + nprc(c, r);
-    seen.assign(base[nc * nr], 0);
     auto prc_at = [&](uint32_t c, uint32_t r, uint64_t x, uint64_t y, uint32_t& pi) {
         const Res& R = comps[c].res[r];
         if (!nprc(c, r)) return false;
@@ -1274,25 +1312,47 @@ static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Par
     auto emit = [&](uint32_t c, uint32_t r, uint64_t x, uint64_t y) {
         uint32_t pi;
         if (!prc_at(c, r, x, y, pi)) return;
-        uint8_t& s = seen[base[c * nr + r] + pi];
-        if (s) return;
-        s = 1;
-        for (uint32_t l = 0; l < nlayers; ++l) v.push_back({l, r, c, pi});
+        for (uint32_t l = 0; l < nlayers; ++l) put(l, r, c, pi);
     };
     auto walk = [&](const std::function<void(uint64_t, uint64_t)>& f) {
         for (uint64_t y = ty0; y < ty1; y += dy - (y % dy))
             for (uint64_t x = tx0; x < tx1; x += dx - (x % dx)) f(x, y);
     };
-    if (p.prog == 2) {          // RPCL
-        for (uint32_t r = 0; r < nr; ++r)
-            walk([&](uint64_t x, uint64_t y) { for (uint32_t c = 0; c < nc; ++c) emit(c, r, x, y); });
-    } else if (p.prog == 3) {   // PCRL
+    if (prog == 2) {          // RPCL
+        for (uint32_t r = r0; r < r1; ++r)
+            walk([&](uint64_t x, uint64_t y) { for (uint32_t c = c0; c < c1; ++c) emit(c, r, x, y); });
+    } else if (prog == 3) {   // PCRL
         walk([&](uint64_t x, uint64_t y) {
-            for (uint32_t c = 0; c < nc; ++c) for (uint32_t r = 0; r < nr; ++r) emit(c, r, x, y);
+            for (uint32_t c = c0; c < c1; ++c) for (uint32_t r = r0; r < r1; ++r) emit(c, r, x, y);
         });
-    } else {                    // CPRL
-        for (uint32_t c = 0; c < nc; ++c)
-            walk([&](uint64_t x, uint64_t y) { for (uint32_t r = 0; r < nr; ++r) emit(c, r, x, y); });
+    } else {                  // CPRL
+        for (uint32_t c = c0; c < c1; ++c)
+            walk([&](uint64_t x, uint64_t y) { for (uint32_t r = r0; r < r1; ++r) emit(c, r, x, y); });
+    }
+}
+
+// The tile's packet sequence: its progression, or the POC entries' progressions in turn
+// (layers clamped to the stream's, each packet once).
+static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Params& p, uint32_t tx0, uint32_t ty0,
+                                       uint32_t tx1, uint32_t ty1, uint32_t nlayers,
+                                       const std::vector<PocE>* pocs = nullptr) {
+    std::vector<PktRef> v;
+    const uint32_t nc = (uint32_t)comps.size(), nr = p.numres;
+    std::vector<uint32_t> base(nc * nr + 1, 0);
+    for (uint32_t c = 0, k = 0; c < nc; ++c)
+        for (uint32_t r = 0; r < nr; ++r, ++k) {
+            const Res& R = comps[c].res[r];
+            base[k + 1] = base[k] + ((R.x1 > R.x0 && R.y1 > R.y0) ? R.pw * R.ph : 0u);
+        }
+    std::vector<uint8_t> seen((size_t)base[nc * nr] * nlayers + 1, 0);
+    if (!pocs || pocs->empty()) {
+        packet_iter_one(comps, p, p.prog, tx0, ty0, tx1, ty1, nlayers, nlayers, 0, nr, 0, nc, seen, base, v);
+        return v;
+    }
+    for (const PocE& e : *pocs) {
+        const uint32_t le = std::min(e.lye, nlayers), r1 = std::min(e.re, nr), c1 = std::min(e.ce, nc);
+        if (e.rs >= r1 || e.cs >= c1 || !le) continue;
+        packet_iter_one(comps, p, e.prog, tx0, ty0, tx1, ty1, le, nlayers, e.rs, r1, e.cs, c1, seen, base, v);
     }
     return v;
 }
@@ -1776,6 +1836,8 @@ typedef struct {
     uint32_t cod_format;   // 0 = raw codestream (GRK_CODEC_J2K), 2 = JP2 file (GRK_CODEC_JP2)
     uint32_t prog_order;   // GRK_PROG_ORDER
     uint32_t tp_div;       // tile-part divider character ('L', 'R', 'C') or 0
+    uint32_t numpocs;      // progression order changes: pocs[i] = resS, compS, layE, resE, compE, prog
+    uint32_t pocs[32][6];
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -1792,6 +1854,8 @@ static Params to_params(const orc_cparams* cp) {
     p.cblk_sty = cp->cblk_sty;
     p.prog = cp->prog_order;
     p.tp_div = (char)cp->tp_div;
+    for (uint32_t i = 0; i < cp->numpocs && i < 32; ++i)
+        p.pocs.push_back({cp->pocs[i][0], cp->pocs[i][1], cp->pocs[i][2], cp->pocs[i][3], cp->pocs[i][4], cp->pocs[i][5]});
     if (p.ht()) p.numgbits = 1;   // grk_compress.cpp:1123-1124
     p.tw = cp->tile_w; p.th = cp->tile_h; p.tlm = (int)cp->tlm; p.plt = (int)cp->plt;
     for (uint32_t i = 0; i < 100; ++i) p.rates[i] = i < p.nlayers ? cp->layer_rate[i] : 0.0;
@@ -1973,7 +2037,7 @@ static bool simulate(EncodeState& E, uint32_t max_layers, uint64_t max_bytes) {
     auto trees = make_trees(E);
     uint64_t budget = max_bytes;
     uint64_t* bp = (max_bytes == 0xffffffffull) ? nullptr : &budget;
-    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, max_layers))
+    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, max_layers, &E.p.pocs))
         if (!write_packet(nullptr, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], bp)) return false;
     return true;
 }
@@ -2063,7 +2127,7 @@ static void rate_allocate(EncodeState& E) {
 static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector<uint32_t>& plens,
                          std::vector<uint32_t>* pparts = nullptr) {
     auto trees = make_trees(E);
-    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, E.p.nlayers)) {
+    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, E.p.nlayers, &E.p.pocs)) {
         size_t before = body.size();
         write_packet(&body, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], nullptr);
         plens.push_back((uint32_t)(body.size() - before));
@@ -2086,6 +2150,7 @@ static std::vector<uint32_t> write_tile_part(std::vector<uint8_t>& o, EncodeStat
     for (int part = 0; part < np; ++part) {
         size_t sot = o.size();
         put16(o, 0xff90); put16(o, 10); put16(o, E.tile); put32(o, 0); o.push_back((uint8_t)part); o.push_back((uint8_t)np);
+        if (part == 0 && !E.p.pocs.empty()) write_poc(o, E.p.pocs, E.im.nc);   // POC in the first tile part
         if (E.p.plt && part == 0) {
             std::vector<uint8_t> v;
             for (uint32_t L : plens) {
@@ -2379,7 +2444,7 @@ void orc_t1_decode_cblk(const uint8_t* data, uint32_t len, uint32_t npasses, uin
 // packet sequence continues across its parts, A.4.2)
 static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, size_t>>& ranges, const Params& p,
                        const Image& im, const std::vector<std::pair<uint32_t, uint32_t>>& qcd, uint32_t tile,
-                       int32_t* out) {
+                       int32_t* out, const std::vector<PocE>* tpocs = nullptr) {
     size_t data = ranges[0].first, tile_end = ranges[0].second, next_range = 1;
     uint32_t tx0, ty0, tx1, ty1;
     tile_rect(p, im.w, im.h, tile, tx0, ty0, tx1, ty1);
@@ -2408,7 +2473,7 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
         }
     }
     size_t pos = i;
-    for (const PktRef& pk : packet_iter(comps, p, tx0, ty0, tx1, ty1, nlayers)) {
+    for (const PktRef& pk : packet_iter(comps, p, tx0, ty0, tx1, ty1, nlayers, tpocs && !tpocs->empty() ? tpocs : &p.pocs)) {
                 const uint32_t l = pk.l, r = pk.r, c = pk.c, pi = pk.pi;
                 Res& R = comps[c].res[r];
                 // layers past the limit and resolutions past the reduction: header parsed for
@@ -2618,6 +2683,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             if ((s[8] & 0x40) && s[8] != 0x40) return -2;  // HT with Part-1 mode switches (CodeStreamDecompress.cpp:1781)
             if (s[8] & 0x80) return -2;
             if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
+        } else if (m == 0xff5f) {
+            if (!read_poc(s, L, im.nc, p.pocs)) return -2;
         } else if (m == 0xff5c) {
             uint32_t sq = s[0]; p.numgbits = sq >> 5;
             uint32_t qt = sq & 0x1f;
@@ -2634,32 +2701,38 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     std::fill(out, out + (size_t)im.nc * *W * *H, 0);
     const uint32_t nt = tile_count(p, im.w, im.h);
     size_t pos = first_sot;
-    struct Part { size_t data, end; uint32_t tile, tpsot; };
+    struct Part { size_t data, end; uint32_t tile, tpsot; std::vector<PocE> pocs; };
     std::vector<Part> parts;
     while (pos + 12 <= len && get16(cs + pos) == 0xff90) {
         const uint8_t* s = cs + pos + 4;
         uint32_t isot = get16(s), psot = get32(s + 2);
         size_t tile_end = psot ? pos + psot : len - 2;
         if (tile_end > len || isot >= nt) return -5;
-        size_t j = pos + 12;   // tile-part header markers (PLT, ...) until SOD
-        while (j + 2 <= tile_end && get16(cs + j) != 0xff93) j += 2 + get16(cs + j + 2);
+        size_t j = pos + 12;   // tile-part header markers (PLT, POC, ...) until SOD
+        std::vector<PocE> tp_pocs;
+        while (j + 2 <= tile_end && get16(cs + j) != 0xff93) {
+            if (get16(cs + j) == 0xff5f && !read_poc(cs + j + 4, get16(cs + j + 2), im.nc, tp_pocs)) return -5;
+            j += 2 + get16(cs + j + 2);
+        }
         if (j + 2 > tile_end) return -5;
-        parts.push_back({j + 2, tile_end, isot, s[6]});
+        parts.push_back({j + 2, tile_end, isot, s[6], std::move(tp_pocs)});
         pos = tile_end;
     }
     // a tile's parts in order (TPsot 0, 1, ...)
     std::vector<uint32_t> tiles;
     std::vector<std::vector<std::pair<size_t, size_t>>> ranges;
+    std::vector<std::vector<PocE>> tpocs;   // POC of the tile's first tile-part header
     std::vector<int> slot(nt, -1);
-    for (const Part& q : parts) {
+    for (Part& q : parts) {
         if (slot[q.tile] < 0) {
             if (q.tpsot != 0) return -5;
             slot[q.tile] = (int)tiles.size(); tiles.push_back(q.tile); ranges.emplace_back();
+            tpocs.push_back(std::move(q.pocs));
         } else if (q.tpsot != ranges[slot[q.tile]].size()) return -5;
         ranges[slot[q.tile]].push_back({q.data, q.end});
     }
     std::vector<int> rcs(tiles.size(), 0);   // tiles write disjoint rectangles of out
-    par_for(tiles.size(), [&](size_t q) { rcs[q] = decode_tile(cs, ranges[q], p, im, qcd, tiles[q], out); });
+    par_for(tiles.size(), [&](size_t q) { rcs[q] = decode_tile(cs, ranges[q], p, im, qcd, tiles[q], out, &tpocs[q]); });
     for (int rc : rcs) if (rc) return rc;
     return 0;
 }

@@ -106,3 +106,30 @@ def test_layer_limited_decode(eng, prog, plt):
         O.set_decode_layers(0)
     np.testing.assert_array_equal(dec, full)
     assert errs[0] > errs[1] > errs[2]
+
+
+POCS = [
+    [(0, 0, 1, 3, 3, "RLCP"), (0, 0, 3, 4, 3, "LRCP")],
+    [(0, 0, 2, 4, 2, "CPRL"), (0, 2, 2, 4, 3, "RPCL"), (0, 0, 3, 4, 3, "PCRL")],
+    [(1, 0, 3, 4, 3, "RPCL"), (0, 0, 3, 1, 3, "LRCP")],
+]
+
+
+@pytest.mark.parametrize("pi", range(len(POCS)))
+def test_progression_order_changes(eng, pi):
+    """POC (A.6.6; PacketIter over the tile's progressions, update_include): a POC marker in
+    each tile's first tile-part header (CodeStreamCompress::writePoc), packets ordered entry
+    by entry, each once.  Encode byte-identical to the oracle, decodes equal (whole, window,
+    PCRD layers through the serial simulation)."""
+    import grok_amd as G
+    img = _img(20 + pi, 3, 150, 170)
+    for kw in (dict(tiles=(64, 96), plt=True, tlm=True), dict(precincts=[(32, 32)], layer_rate=[20, 5, 0])):
+        gkw = dict(kw)
+        if "layer_rate" in gkw:
+            gkw["numlayers"] = len(gkw["layer_rate"])
+        cs = eng.encode(img, 8, params=G.default_params(numresolution=4, cblk=(16, 16), pocs=POCS[pi], **gkw))
+        ref = O.encode(img, 8, numres=4, cblk=(16, 16), pocs=POCS[pi], **kw)
+        assert cs == ref
+        np.testing.assert_array_equal(eng.decode(cs), img)
+        if "tiles" in kw:
+            np.testing.assert_array_equal(eng.decode_window(cs, (30, 20, 160, 120)), img[:, 20:120, 30:160])
