@@ -14,6 +14,12 @@
 // box wrapper (FileFormatCompress.cpp) is restated but not pinned by a Grok
 // output: Grok needs cmake-generated headers, so it is not rebuilt here.
 //
+// Restated from the reference sources with no Grok-produced fixture, so PARITY UNPINNED
+// for them (the engine is tested byte-/sample-exact against these restatements): code-block
+// mode switches (T1.cpp, mqc_enc.cpp, T2 segments), progression orders other than LRCP and
+// POC (PacketIter.cpp), HT with 9/7 (the standard-correct fix of R-BUG-2), layer-limited and
+// reduced-resolution decode, tiles in several tile parts and tile-part generation.
+//
 // Threads (orc_set_threads): code-blocks of a tile, and tiles of a multi-tile
 // image, are coded on worker threads; the result does not depend on the count.
 //
