@@ -49,6 +49,7 @@ class CParameters(ctypes.Structure):
         ("writeTLM", ctypes.c_uint8), ("writePLT", ctypes.c_uint8),
         ("cod_format", ctypes.c_int32), ("prog_order", ctypes.c_int32),
         ("enableTilePartGeneration", ctypes.c_uint8), ("newTilePartProgressionDivider", ctypes.c_char),
+        ("roi_compno", ctypes.c_int32), ("roi_shift", ctypes.c_uint32),
         ("numpocs", ctypes.c_uint32), ("pocs", Poc * 32),
     ]
 
@@ -127,7 +128,7 @@ PROG_ORDERS = ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"]   # GRK_PROG_ORDER (grok.
 
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
                    precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False,
-                   prog_order="LRCP", tile_parts=None, pocs=None):
+                   prog_order="LRCP", tile_parts=None, pocs=None, roi=None):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
     prog_order: "LRCP", "RLCP", "RPCL", "PCRL", "CPRL" or 0..4 (grk_compress -p).
@@ -159,6 +160,7 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
     p.writeTLM, p.writePLT = int(bool(tlm)), int(bool(plt))
     p.cod_format = 2 if jp2 else 0   # GRK_CODEC_JP2 / GRK_CODEC_J2K
     p.prog_order = PROG_ORDERS.index(prog_order) if isinstance(prog_order, str) else int(prog_order)
+    p.roi_compno, p.roi_shift = (int(roi[0]), int(roi[1])) if roi else (-1, 0)   # grk_compress -ROI c=..,U=..
     if pocs:   # [(resS, compS, layE, resE, compE, "PROG"), ...] (grk_compress -P)
         p.numpocs = len(pocs)
         for i, (rs, cs, le, re_, ce, pr) in enumerate(pocs):

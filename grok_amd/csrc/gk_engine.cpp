@@ -140,6 +140,8 @@ struct Params {
     uint32_t prog = 0;                   // progression order: GRK_LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4
     char tp_div = 0;                     // tile-part divider 'L' / 'R' / 'C' (grk_compress -u), 0 = one part per tile
     std::vector<Poc> pocs;               // progression order changes (every tile; empty = prog)
+    std::vector<uint8_t> roishift;       // per component ROI shift (RGN, maxshift; empty = none)
+    uint32_t roi(uint32_t c) const { return c < roishift.size() ? roishift[c] : 0u; }
     bool ht() const { return (cblk_sty & 0x40) != 0; }
     uint32_t tw = 0, th = 0;             // nominal tile size (grk_cparameters::t_width/t_height; 0 = image)
     bool tlm = false, plt = false;       // grk_cparameters::writeTLM / writePLT
@@ -296,7 +298,8 @@ static void ht_irrev_quant(uint32_t prec, bool sgnd, uint32_t nd, uint32_t r, ui
 }
 
 static void assign_steps_tile(Plan& P, TileG& T) {
-    for (auto& C : T.comps) {
+    for (uint32_t ci = 0; ci < (uint32_t)T.comps.size(); ++ci) {
+        CompG& C = T.comps[ci];
         for (uint32_t r = 0; r < P.p.numres; ++r) {
             for (auto& B : C.res[r].bands) {
                 uint32_t level = P.p.numres - 1 - r;
@@ -304,7 +307,7 @@ static void assign_steps_tile(Plan& P, TileG& T) {
                     B.mant = 0;
                     B.expn = ht_rev_expn(P.prec, P.p.numres - 1, r, B.orient);
                     B.step_enc = B.step_dec = 1.0f;
-                    B.numbps = (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1);
+                    B.numbps = (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1) + P.p.roi(ci);
                     continue;
                 }
                 uint32_t gain = P.p.irrev ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
@@ -325,7 +328,9 @@ static void assign_steps_tile(Plan& P, TileG& T) {
                 B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
                 B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
                 int v = (int)B.expn + (int)P.p.numgbits - 1;
-                B.numbps = (uint32_t)std::max(0, v);
+                B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, v);   // Quantizer.cpp:47: roishift + ...
+                // ROI-scaled indices keep 6 fractional bits below them in a 31-bit magnitude
+                if (P.p.roi(ci) && B.numbps > 25) throw GkError("ROI shift too large for this precision");
             }
         }
     }
@@ -333,7 +338,8 @@ static void assign_steps_tile(Plan& P, TileG& T) {
 
 static void apply_qcd(Plan& P, const std::vector<std::pair<uint32_t, uint32_t>>& q) {
     for (auto& T : P.tiles)
-    for (auto& C : T.comps) {
+    for (uint32_t ci = 0; ci < (uint32_t)T.comps.size(); ++ci) {
+        CompG& C = T.comps[ci];
         uint32_t bandno = 0;
         for (uint32_t r = 0; r < P.p.numres; ++r)
             for (auto& B : C.res[r].bands) {
@@ -343,7 +349,7 @@ static void apply_qcd(Plan& P, const std::vector<std::pair<uint32_t, uint32_t>>&
                 uint32_t lg_dec = P.p.irrev ? 0 : lg_enc;
                 B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
                 B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
-                B.numbps = (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1);
+                B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1);
                 ++bandno;
             }
     }
@@ -431,7 +437,8 @@ static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
                         G.w = (uint16_t)(x1 - x0); G.h = (uint16_t)(y1 - y0);
                         G.orient = (uint8_t)B.orient; G.comp = (uint8_t)c;
                         G.band_numbps = (uint8_t)B.numbps;
-                        G.flags = (P.p.irrev ? 1 : 0) | (P.p.rate_control() ? 2 : 0);
+                        // bits 3..7: the component's ROI shift (RGN; RoiShiftFilter on decode)
+                        G.flags = (P.p.irrev ? 1 : 0) | (P.p.rate_control() ? 2 : 0) | (uint8_t)(P.p.roi(c) << 3);
                         G.step = B.step_enc;
                         // T1::getwmsedec weight w1 * w2 * stepsize (T1.cpp:418-436): w1 = MCT basis norm
                         // (mct.cpp:689-704) when the MCT is on, w2 = DWT band norm (T1.cpp:264-277)
@@ -1662,6 +1669,14 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
         if (tlm_pos) *tlm_pos = o.size();
         o.insert(o.end(), (size_t)(6 * ne), 0);
     }
+    for (uint32_t c = 0; c < P.nc; ++c)   // RGN (CodeStreamCompress::write_regions / write_rgn :746-780, 1397-1410)
+        if (P.p.roi(c)) {
+            const uint32_t cw = P.nc <= 256 ? 1 : 2;
+            put16(o, 0xff5e); put16(o, 4 + cw);
+            if (cw == 1) o.push_back((uint8_t)c); else put16(o, c);
+            o.push_back(0);   // Srgn: implicit (maxshift)
+            o.push_back((uint8_t)P.p.roi(c));
+        }
     if (P.p.write_com) {
         const char* txt = "Created by Grok     version 9.2.0";
         put16(o, 0xff64); put16(o, 4 + (uint32_t)strlen(txt)); put16(o, 1);
@@ -1821,6 +1836,12 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     P.cblk_sty = cp->cblk_sty;
     if (cp->prog_order < 0 || cp->prog_order > 4) throw GkError("unknown progression order");
     P.prog = (uint32_t)cp->prog_order;
+    P.roishift.clear();
+    if (cp->roi_compno >= 0 && cp->roi_shift) {   // CodeStreamCompress.cpp:538-541: roishift on one component
+        if (cp->roi_shift >= 32) throw GkError("ROI shift must be below 32");
+        P.roishift.assign((size_t)cp->roi_compno + 1, 0);
+        P.roishift[(size_t)cp->roi_compno] = (uint8_t)cp->roi_shift;
+    }
     if (cp->numpocs > 32) throw GkError("at most 32 progression order changes");
     P.pocs.clear();
     for (uint32_t i = 0; i < cp->numpocs; ++i) {
@@ -1860,6 +1881,7 @@ static std::string plan_key(const Plan& P) {
              P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0, P.p.rate_control() ? 1 : 0);
     std::string k(buf);
     k += " sty" + std::to_string(P.p.cblk_sty) + " t" + std::to_string(P.p.tw) + "x" + std::to_string(P.p.th);
+    for (uint8_t v : P.p.roishift) k += " roi" + std::to_string(v);
     for (uint32_t r = 0; r < P.p.numres; ++r) k += " " + std::to_string(P.p.prcw[r]) + "," + std::to_string(P.p.prch[r]);
     return k;
 }
@@ -1992,6 +2014,8 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     if (want.nc < 3) want.p.mct = 0;
     if ((want.p.cblk_sty & GK_STY_HT) && want.p.cblk_sty != GK_STY_HT)
         throw GkError("HTJ2K cannot be combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781
+    for (uint8_t v : want.p.roishift)
+        if (v && want.p.ht()) throw GkError("ROI with HTJ2K is not supported on this path");
     if (want.p.cblk_sty > 0x7f) throw GkError("unknown code-block style bits");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if (want.prec == 0 || want.prec > 31) throw GkError("component precision must be 1..31 bits");
@@ -2634,8 +2658,18 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             }
         } else if (m == 0xff5f) {   // POC in the main header: every tile's packet order
             parse_poc(S, s, L, W.nc, W.p.pocs);
-        } else if (m == 0xff5d || m == 0xff53 || m == 0xff5e) {
-            throw GkError("QCC/COC/RGN markers not supported on this path yet");
+        } else if (m == 0xff5e) {   // RGN (CodeStreamDecompress::read_rgn :1480-1520)
+            const uint32_t cw = W.nc <= 256 ? 1 : 2;
+            if (L != 4 + cw) throw GkError("corrupt RGN marker");
+            const uint32_t c = cw == 1 ? S.at(s) : S.be16(s);
+            if (c >= W.nc) throw GkError("bad component number in RGN");
+            if (S.at(s + cw) != 0) throw GkError("only the implicit (maxshift) ROI style is defined");
+            const uint32_t shift = S.at(s + cw + 1);
+            if (shift >= 32) throw GkError("unsupported ROI shift");
+            if (W.p.roishift.size() < W.nc) W.p.roishift.resize(W.nc, 0);
+            W.p.roishift[c] = (uint8_t)shift;
+        } else if (m == 0xff5d || m == 0xff53) {
+            throw GkError("QCC/COC markers not supported on this path yet");
         }
         i += 2 + L;
     }
@@ -2674,6 +2708,8 @@ static void parse_header(ByteSrc& S, Header& Hd) {
         }
     }
     if (Hd.parts.empty()) throw GkError("no tile parts");
+    for (uint8_t v : W.p.roishift)   // Grok's RoiShiftHTFilter keeps only the sign of a shifted sample
+        if (v && W.p.ht()) throw GkError("ROI with HTJ2K is not supported on this path");
     if ((1u << W.p.cbw) > 64 || (1u << W.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
 }
 

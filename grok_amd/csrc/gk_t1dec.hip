@@ -612,6 +612,7 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
     const uint64_t lstride = (wave_off[(slot >> 6) + 1] - wave_off[slot >> 6]) / 64;
     const uint64_t* WS = scratch + wave_off[slot >> 6] + (size_t)ln * lstride;
     const bool irrev = B.flags & 1;
+    const uint32_t rs = B.flags >> 3;   // ROI shift of the component (RGN)
     float* fcoef = reinterpret_cast<float*>(coef);
     const uint32_t numbps = B.numbps, npasses = B.npasses, h = B.h;
     // last decoded pass k = npasses-1: pass k>0 belongs to plane numbps-1-(k+2)/3, type (k+2)%3
@@ -645,6 +646,10 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
             }
         }
         size_t o = B.band_off + (size_t)y * B.stride + x;
+        if (rs) {   // RoiShiftFilter / RoiScaleFilter (PostDecompressFilters.h:7-72)
+            const int32_t m = v < 0 ? -v : v;
+            if (m >= (1 << rs)) v = v < 0 ? -(m >> rs) : (m >> rs);
+        }
         if (irrev) fcoef[o] = (float)v * B.step;
         else coef[o] = v / 2;
     }

@@ -108,6 +108,11 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
             int32_t raw = coef[B.band_off + (size_t)y * B.stride + lane];
             if (irrev) v = (int32_t)rintf((__int_as_float(raw) / B.step) * 64.0f);
             else v = raw * 64;
+            if (B.flags >> 3) {   // ROI maxshift (the component is the region): integer part of the index up
+                const uint32_t rs = B.flags >> 3, a0 = (uint32_t)(v < 0 ? -v : v);
+                const uint32_t a1 = ((a0 >> 6) << (6 + rs)) | (a0 & 63u);
+                v = v < 0 ? -(int32_t)a1 : (int32_t)a1;
+            }
         }
         uint32_t a = (uint32_t)(v < 0 ? -v : v);
         m[y] = a;
@@ -645,8 +650,9 @@ __global__ __launch_bounds__(64) void k_t1_weight(const int32_t* __restrict__ co
     if (lane < (int)B.w)
         for (uint32_t y = 0; y < B.h; ++y) {
             const int32_t raw = coef[B.band_off + (size_t)y * B.stride + lane];
-            const uint32_t a = irrev ? (uint32_t)fabsf(rintf((__int_as_float(raw) / B.step) * 64.0f))
-                                     : (uint32_t)(raw < 0 ? -raw : raw) * 64u;
+            const uint32_t a0 = irrev ? (uint32_t)fabsf(rintf((__int_as_float(raw) / B.step) * 64.0f))
+                                      : (uint32_t)(raw < 0 ? -raw : raw) * 64u;
+            const uint32_t a = ((a0 >> 6) << (6 + (B.flags >> 3))) | (a0 & 63u);   // ROI maxshift
             mx = a > mx ? a : mx;
         }
 #pragma unroll

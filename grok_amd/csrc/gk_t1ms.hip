@@ -172,7 +172,11 @@ __global__ __launch_bounds__(64) void k_t1_enc_ms(const int32_t* __restrict__ co
     const bool irrev = G.flags & 1, rc = (G.flags & 2) != 0;
     auto smr = [&](int x, int y) -> int32_t {   // T1Part1::preCompress (T1Part1.cpp:36-87)
         const int32_t raw = coef[G.band_off + (size_t)y * G.stride + x];
-        return irrev ? (int32_t)rintf((__int_as_float(raw) / G.step) * 64.0f) : raw * 64;
+        const int32_t v = irrev ? (int32_t)rintf((__int_as_float(raw) / G.step) * 64.0f) : raw * 64;
+        if (!(G.flags >> 3)) return v;
+        // ROI maxshift (the component is the region): the index's integer part scaled up
+        const uint32_t a0 = (uint32_t)(v < 0 ? -v : v), a1 = ((a0 >> 6) << (6 + (G.flags >> 3))) | (a0 & 63u);
+        return v < 0 ? -(int32_t)a1 : (int32_t)a1;
     };
     uint32_t mx = 0;
     for (int y = 0; y < h; ++y)
@@ -502,11 +506,16 @@ __global__ __launch_bounds__(64) void k_t1_dec_ms(const uint8_t* __restrict__ by
         }
     }
     const bool irrev = G.flags & 1;
+    const uint32_t rs = G.flags >> 3;   // ROI shift (RoiShiftFilter / RoiScaleFilter)
     float* fo = reinterpret_cast<float*>(o);
     for (int y = 0; y < h; ++y)
         for (int x = 0; x < w; ++x) {
             const size_t i = (size_t)y * os + x;
-            const int32_t v = o[i];
+            int32_t v = o[i];
+            if (rs) {
+                const int32_t m = v < 0 ? -v : v;
+                if (m >= (1 << rs)) v = v < 0 ? -(m >> rs) : (m >> rs);
+            }
             if (irrev) fo[i] = (float)v * G.step;
             else o[i] = v / 2;
         }

@@ -21,7 +21,6 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     }
     if (g.numpocs) return refuse("progression order changes (POC) are not supported on this path");
     if (g.prog_order < GRK_LRCP || g.prog_order > GRK_CPRL) return refuse("unknown progression order");
-    if (g.roi_compno >= 0) return refuse("region of interest (RGN) is not supported on this path");
     if (g.tx0 || g.ty0 || g.image_offset_x0 || g.image_offset_y0) return refuse("image/tile offsets are not supported");
     // mct 255 = not set on the command line: grk_compress resolves it from the component count
     // once the image is loaded (grk_compress.cpp:1977-1981), as the engine does (>= 3 -> RCT/ICT)
@@ -55,6 +54,7 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     p.writeTLM = g.writeTLM; p.writePLT = g.writePLT;
     p.cod_format = jp2 ? 2 : 0;
     p.prog_order = (int32_t)g.prog_order;
+    p.roi_compno = g.roi_compno; p.roi_shift = g.roi_shift;
     p.enableTilePartGeneration = g.enableTilePartGeneration ? 1 : 0;
     p.newTilePartProgressionDivider = g.newTilePartProgressionDivider;
     return true;

@@ -59,6 +59,8 @@ typedef struct gk_cparameters {
     int32_t prog_order;                  /* grk_cparameters::prog_order: GRK_LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4 */
     uint8_t enableTilePartGeneration;    /* grk_cparameters::enableTilePartGeneration (grk_compress -u) */
     char newTilePartProgressionDivider;  /* grk_cparameters::newTilePartProgressionDivider: 'L', 'R' or 'C' */
+    int32_t roi_compno;                  /* grk_cparameters::roi_compno (-1: none) */
+    uint32_t roi_shift;                  /* grk_cparameters::roi_shift: RGN maxshift of that component (Part-1) */
     uint32_t numpocs;                    /* progression order changes, written as a POC marker in each tile's
                                             first tile-part header (CodeStreamCompress::writePoc) */
     gk_poc pocs[32];

@@ -90,6 +90,8 @@ struct Params {
     uint32_t prog = 0;          // progression order (GRK_PROG_ORDER): LRCP 0, RLCP 1, RPCL 2, PCRL 3, CPRL 4
     char tp_div = 0;            // tile-part divider 'L' / 'R' / 'C' (grk_compress -u), 0 = one part per tile
     std::vector<PocE> pocs;     // progression order changes (encode: every tile; decode: main header)
+    std::vector<uint32_t> roishift;   // per component ROI maxshift (RGN); empty = none
+    uint32_t roi(uint32_t c) const { return c < roishift.size() ? roishift[c] : 0u; }
     uint32_t tw = 0, th = 0;    // nominal tile size (0 = one tile covering the image), grk_cparameters::t_width/t_height
     int tlm = 0, plt = 0;       // write TLM (-X) / PLT (-L) markers
     bool ht() const { return (cblk_sty & 0x40) != 0; }
@@ -292,7 +294,7 @@ static void ht_irrev_quant(uint32_t prec, int sgnd, uint32_t nd, uint32_t r, uin
 }
 
 static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress,
-                         const std::vector<std::pair<uint32_t,uint32_t>>* qcd, int sgnd = 0) {
+                         const std::vector<std::pair<uint32_t,uint32_t>>* qcd, int sgnd = 0, uint32_t roishift = 0) {
     // qcd: per band (expn, mant) in band order LL, (HL,LH,HH) per resolution, when decoding.
     uint32_t bandno = 0;
     for (uint32_t r = 0; r < p.numres; ++r) {
@@ -329,7 +331,7 @@ static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress,
             uint32_t nbps = prec + log2_gain;
             B.stepsize = (float)((1.0 + mant / 2048.0) * pow(2.0, (int)nbps - (int)expn));
             int v = (int)expn + (int)p.numgbits - 1;
-            B.numbps = (uint32_t)std::max(0, v);
+            B.numbps = roishift + (uint32_t)std::max(0, v);   // Quantizer.cpp:47: roishift + expn + guard - 1
             ++bandno;
         }
     }
@@ -1251,6 +1253,13 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
         if (tlm_pos) *tlm_pos = o.size();
         o.insert(o.end(), (size_t)6 * nt, 0);
     }
+    for (uint32_t c = 0; c < im.nc; ++c)            // RGN (CodeStreamCompress::write_rgn :746-780)
+        if (p.roi(c)) {
+            const uint32_t cw = im.nc <= 256 ? 1 : 2;
+            put16(o, 0xff5e); put16(o, 4 + cw);
+            if (cw == 1) o.push_back((uint8_t)c); else put16(o, c);
+            o.push_back(0); o.push_back((uint8_t)p.roi(c));
+        }
     if (p.write_com) {                               // COM (CodeStreamCompress.cpp:334, 1114)
         const char* txt = "Created by Grok     version 9.2.0";
         put16(o, 0xff64); put16(o, 4 + (uint32_t)strlen(txt)); put16(o, 1);
@@ -1844,6 +1853,8 @@ typedef struct {
     uint32_t tp_div;       // tile-part divider character ('L', 'R', 'C') or 0
     uint32_t numpocs;      // progression order changes: pocs[i] = resS, compS, layE, resE, compE, prog
     uint32_t pocs[32][6];
+    int32_t roi_compno;    // grk_cparameters::roi_compno (-1 none) / roi_shift
+    uint32_t roi_shift;
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -1860,6 +1871,10 @@ static Params to_params(const orc_cparams* cp) {
     p.cblk_sty = cp->cblk_sty;
     p.prog = cp->prog_order;
     p.tp_div = (char)cp->tp_div;
+    if (cp->roi_compno >= 0 && cp->roi_shift) {
+        p.roishift.assign((size_t)cp->roi_compno + 1, 0);
+        p.roishift[(size_t)cp->roi_compno] = cp->roi_shift;
+    }
     for (uint32_t i = 0; i < cp->numpocs && i < 32; ++i)
         p.pocs.push_back({cp->pocs[i][0], cp->pocs[i][1], cp->pocs[i][2], cp->pocs[i][3], cp->pocs[i][4], cp->pocs[i][5]});
     if (p.ht()) p.numgbits = 1;   // grk_compress.cpp:1123-1124
@@ -1943,8 +1958,14 @@ static void t1_encode_all(EncodeState& E) {
                                     float q = (E.fcoefs[c][o] / B.stepsize) * (float)(1 << FRACBITS);
                                     sv = (int64_t)lrintf(q);
                                 }
+                                // ROI maxshift (standard-correct: the whole component is the region,
+                                // the integer part of its indices scaled up by 2^shift, the six
+                                // fractional distortion bits kept below; Grok's encoder only raises
+                                // the band bit-plane count, CodeStreamCompress.cpp:538-541)
+                                const uint64_t a0 = (uint64_t)(sv < 0 ? -sv : sv);
+                                const uint64_t a1 = ((a0 >> FRACBITS) << (FRACBITS + E.p.roi(c))) | (a0 & 63u);
                                 neg[y * w + x] = sv < 0;
-                                mag[y * w + x] = (uint32_t)(sv < 0 ? -sv : sv);
+                                mag[y * w + x] = (uint32_t)a1;
                             }
                         DistCtx dc{c, E.p.numres - 1 - r, B.orient, E.p.irreversible ? 0u : 1u, (double)B.stepsize,
                                    mct ? (E.p.irreversible ? norms_irrev : norms_rev) : nullptr, mct ? 3u : E.im.nc};
@@ -1969,7 +1990,7 @@ static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, ui
     E.comps.assign(nc, Comp());
     for (uint32_t c = 0; c < nc; ++c) {
         build_geometry(E.comps[c], E.tx0, E.ty0, E.tx1, E.ty1, E.p);
-        assign_steps(E.comps[c], E.p, prec, true, nullptr, sgnd);
+        assign_steps(E.comps[c], E.p, prec, true, nullptr, sgnd, E.p.roi(c));
     }
     E.coefs.assign(nc, {});
     for (uint32_t c = 0; c < nc; ++c) {   // tile-local copy (TileProcessor::ingestImage, TileProcessor.cpp:410-431)
@@ -2459,7 +2480,7 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
     const uint32_t red = g_dec_reduce;   // grk_dparameters::cp_reduce
     size_t i = data;
     std::vector<Comp> comps(im.nc);
-    for (uint32_t c = 0; c < im.nc; ++c) { build_geometry(comps[c], tx0, ty0, tx1, ty1, p); assign_steps(comps[c], p, im.prec, false, &qcd); }
+    for (uint32_t c = 0; c < im.nc; ++c) { build_geometry(comps[c], tx0, ty0, tx1, ty1, p); assign_steps(comps[c], p, im.prec, false, &qcd, 0, p.roi(c)); }
     // T2 decode (LRCP)
     struct TT { std::vector<TagTree> incl, imsb; };
     std::vector<std::vector<std::vector<TT>>> trees(im.nc);
@@ -2597,10 +2618,12 @@ t2done:
                         } else
                         t1_decode_block(K.data.data(), (uint32_t)K.data.size(), K.npasses, K.numbps, B.orient, w, h, blk.data(),
                                         nullptr, p.cblk_sty, &K.seglens);
+                        const uint32_t rs = p.roi(c);   // RoiShiftFilter / RoiScaleFilter (PostDecompressFilters.h:7-72)
                         for (uint32_t y = 0; y < h; ++y)
                             for (uint32_t x = 0; x < w; ++x) {
                                 size_t o = (size_t)(B.offy + K.y0 - B.y0 + y) * TW + (B.offx + K.x0 - B.x0 + x);
                                 int32_t v = blk[y * w + x];
+                                if (rs && std::abs(v) >= (1 << rs)) v = v < 0 ? -(std::abs(v) >> rs) : (v >> rs);
                                 if (!p.irreversible) ip[c][o] = v / 2;                 // ShiftFilter
                                 else fp[c][o] = (float)v * B.stepsize / 2.0f;          // ScaleFilter
                             }
@@ -2691,6 +2714,12 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
         } else if (m == 0xff5f) {
             if (!read_poc(s, L, im.nc, p.pocs)) return -2;
+        } else if (m == 0xff5e) {                          // RGN: Crgn, Srgn (0), SPrgn
+            const uint32_t cw = im.nc <= 256 ? 1 : 2;
+            const uint32_t c = cw == 1 ? s[0] : get16(s);
+            if (L != 4 + cw || c >= im.nc || s[cw] != 0 || s[cw + 1] >= 32) return -2;
+            if (p.roishift.size() < im.nc) p.roishift.resize(im.nc, 0);
+            p.roishift[c] = s[cw + 1];
         } else if (m == 0xff5c) {
             uint32_t sq = s[0]; p.numgbits = sq >> 5;
             uint32_t qt = sq & 0x1f;

@@ -25,6 +25,7 @@ class CParams(ctypes.Structure):
         ("tile_w", ctypes.c_uint32), ("tile_h", ctypes.c_uint32), ("tlm", ctypes.c_uint32), ("plt", ctypes.c_uint32),
         ("cod_format", ctypes.c_uint32), ("prog_order", ctypes.c_uint32), ("tp_div", ctypes.c_uint32),
         ("numpocs", ctypes.c_uint32), ("pocs", (ctypes.c_uint32 * 6) * 32),
+        ("roi_compno", ctypes.c_int32), ("roi_shift", ctypes.c_uint32),
     ]
 
 
@@ -94,7 +95,7 @@ def get_threads():
 
 
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
-           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None):
+           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None, roi=None):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -112,6 +113,7 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
     for i, e in enumerate(pocs or []):
         p.pocs[i][:] = list(e[:5]) + [progs.index(e[5]) if isinstance(e[5], str) else int(e[5])]
     p.numpocs = len(pocs or [])
+    p.roi_compno, p.roi_shift = (int(roi[0]), int(roi[1])) if roi else (-1, 0)
     if tiles:
         p.tile_w, p.tile_h = int(tiles[0]), int(tiles[1])
     p.tlm, p.plt = int(tlm), int(plt)
