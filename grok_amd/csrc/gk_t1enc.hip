@@ -108,16 +108,19 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
             int32_t raw = coef[B.band_off + (size_t)y * B.stride + lane];
             if (irrev) v = (int32_t)rintf((__int_as_float(raw) / B.step) * 64.0f);
             else v = raw * 64;
-            if (B.flags >> 3) {   // ROI maxshift (the component is the region): integer part of the index up
-                const uint32_t rs = B.flags >> 3, a0 = (uint32_t)(v < 0 ? -v : v);
-                const uint32_t a1 = ((a0 >> 6) << (6 + rs)) | (a0 & 63u);
-                v = v < 0 ? -(int32_t)a1 : (int32_t)a1;
-            }
         }
         uint32_t a = (uint32_t)(v < 0 ? -v : v);
         m[y] = a;
         mx = a > mx ? a : mx;
         negcol |= (uint64_t)(v < 0) << y;
+    }
+    if (const uint32_t rs = B.flags >> 3) {   // ROI maxshift (the component is the region): index integer part up
+        mx = 0;
+#pragma unroll
+        for (int y = 0; y < 64; ++y) {
+            m[y] = ((m[y] >> 6) << (6 + rs)) | (m[y] & 63u);
+            mx = m[y] > mx ? m[y] : mx;
+        }
     }
     if constexpr (RC) {
         for (int i = lane; i < 512; i += 64) R.nm[i >> 7][i & 127] = nmse_tab[i];
