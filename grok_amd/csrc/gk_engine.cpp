@@ -350,6 +350,9 @@ static void apply_qcd(Plan& P, const std::vector<std::pair<uint32_t, uint32_t>>&
                 B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
                 B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
                 B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1);
+                // the Part-1 decoders hold twice the magnitude plus the half-bit, (2M+1) << q, in
+                // an int32: a band (ROI shift included) of more than 30 bit-planes cannot be held
+                if (!P.p.ht() && B.numbps > 30) throw GkError("more than 30 band bit-planes (ROI shift included) not supported");
                 ++bandno;
             }
     }
@@ -1817,7 +1820,7 @@ struct gk_ctx {
     std::vector<uint8_t> rb_data;
 };
 
-static void set_params(Params& P, const gk_cparameters* cp) {
+static void set_params(Params& P, const gk_cparameters* cp, uint32_t nc) {
     for (int i = 0; i < GK_MAXRLVLS; ++i) { P.prcw[i] = 15; P.prch[i] = 15; }
     if (!cp) return;
     // CodeStreamCompress.cpp:159: 1..33 resolutions; res_spec indexes the 33-entry precinct arrays
@@ -1837,9 +1840,11 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     if (cp->prog_order < 0 || cp->prog_order > 4) throw GkError("unknown progression order");
     P.prog = (uint32_t)cp->prog_order;
     P.roishift.clear();
-    if (cp->roi_compno >= 0 && cp->roi_shift) {   // CodeStreamCompress.cpp:538-541: roishift on one component
+    // CodeStreamCompress.cpp:538-541: roishift on the component whose index equals roi_compno;
+    // an index past the last component matches none (no ROI), as in Grok
+    if (cp->roi_compno >= 0 && (uint32_t)cp->roi_compno < nc && cp->roi_shift) {
         if (cp->roi_shift >= 32) throw GkError("ROI shift must be below 32");
-        P.roishift.assign((size_t)cp->roi_compno + 1, 0);
+        P.roishift.assign(nc, 0);
         P.roishift[(size_t)cp->roi_compno] = (uint8_t)cp->roi_shift;
     }
     if (cp->numpocs > 32) throw GkError("at most 32 progression order changes");
@@ -1855,7 +1860,10 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     P.tp_div = cp->enableTilePartGeneration ? cp->newTilePartProgressionDivider : 0;
     if (P.tp_div && P.tp_div != 'L' && P.tp_div != 'R' && P.tp_div != 'C')
         throw GkError("tile-part divider must be L, R or C");
-    if (cp->tile_size_on) { P.tw = cp->t_width; P.th = cp->t_height; }
+    if (cp->tile_size_on) {
+        if (!cp->t_width || !cp->t_height) throw GkError("tile size must be non-zero when tiling is on");
+        P.tw = cp->t_width; P.th = cp->t_height;
+    }
     P.tlm = cp->writeTLM != 0; P.plt = cp->writePLT != 0;
     if (cp->cod_format != 0 && cp->cod_format != 2) throw GkError("cod_format must be GRK_CODEC_J2K (0) or GRK_CODEC_JP2 (2)");
     P.jp2 = cp->cod_format == 2;
@@ -1875,13 +1883,30 @@ static void set_params(Params& P, const gk_cparameters* cp) {
     }
 }
 
+// CodeStreamCompress::validateProgressionOrders (CodeStreamCompress.cpp:1685-1747): the POC
+// entries, clamped to the stream's layers / resolutions / components, must cover every
+// (layer, resolution, component); a list that leaves a packet out is refused ("POC: missing
+// packets") rather than dropping its code-blocks from the codestream.
+static void check_poc_coverage(const Params& P, uint32_t nc) {
+    if (P.pocs.empty()) return;
+    const uint32_t L = P.nlayers, R = P.numres;
+    std::vector<uint8_t> seen((size_t)L * R * nc, 0);
+    for (const Poc& q : P.pocs)
+        for (uint32_t r = q.rs; r < std::min(q.re, R); ++r)
+            for (uint32_t c = q.cs; c < std::min(q.ce, nc); ++c)
+                for (uint32_t l = 0; l < std::min(q.lye, L); ++l) seen[((size_t)l * R + r) * nc + c] = 1;
+    for (uint8_t v : seen)
+        if (!v) throw GkError("POC: missing packets (the progression order changes do not cover every packet)");
+}
+
 static std::string plan_key(const Plan& P) {
     char buf[256];
     snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
              P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0, P.p.rate_control() ? 1 : 0);
     std::string k(buf);
     k += " sty" + std::to_string(P.p.cblk_sty) + " t" + std::to_string(P.p.tw) + "x" + std::to_string(P.p.th);
-    for (uint8_t v : P.p.roishift) k += " roi" + std::to_string(v);
+    for (size_t c = 0; c < P.p.roishift.size(); ++c)   // non-zero (component, shift) pairs only
+        if (P.p.roishift[c]) k += " roi" + std::to_string(c) + ":" + std::to_string(P.p.roishift[c]);
     for (uint32_t r = 0; r < P.p.numres; ++r) k += " " + std::to_string(P.p.prcw[r]) + "," + std::to_string(P.p.prch[r]);
     return k;
 }
@@ -2010,8 +2035,9 @@ static float ev_ms(gk_ctx* ctx, int a, int b) {
 static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparameters* cp) {
     Plan want;
     want.w = info->w; want.h = info->h; want.nc = info->numcomps; want.prec = info->prec; want.sgnd = info->sgnd;
-    set_params(want.p, cp);
+    set_params(want.p, cp, want.nc);
     if (want.nc < 3) want.p.mct = 0;
+    check_poc_coverage(want.p, want.nc);
     if ((want.p.cblk_sty & GK_STY_HT) && want.p.cblk_sty != GK_STY_HT)
         throw GkError("HTJ2K cannot be combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781
     for (uint8_t v : want.p.roishift)
@@ -2571,6 +2597,14 @@ static void parse_poc(Src& S, size_t s, uint32_t L, uint32_t nc, std::vector<Poc
         out.push_back(e);
     }
 }
+// Tile-part header markers that would change how the tile decodes (CodeStreamDecompress's
+// tile-part handlers: COD :1725, COC, QCD, QCC, RGN read_rgn :1480-1520) are refused here
+// rather than skipped, so a stream that carries them fails instead of decoding wrongly.
+static void check_tile_part_marker(uint32_t m) {
+    if (m == 0xff52 || m == 0xff53 || m == 0xff5c || m == 0xff5d)
+        throw GkError("COD/COC/QCD/QCC in a tile-part header are not supported on this path");
+    if (m == 0xff5e) throw GkError("RGN in a tile-part header is not supported on this path");
+}
 struct Header {
     Plan want;
     std::vector<std::pair<uint32_t, uint32_t>> qcd;
@@ -2700,6 +2734,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             std::vector<Poc> tpoc;
             while (j + 4 <= end && S.be16(j) != 0xff93) {
                 if (S.be16(j) == 0xff5f) parse_poc(S, j + 4, S.be16(j + 2), W.nc, tpoc);   // tile-part POC
+                check_tile_part_marker(S.be16(j));
                 j += 2 + S.be16(j + 2);
             }
             if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
@@ -2753,6 +2788,7 @@ static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
         while (j + 4 <= TP.end && S.be16(j) != 0xff93) {
             const uint32_t m = S.be16(j), L = S.be16(j + 2);
             if (m == 0xff5f) parse_poc(S, j + 4, L, nc, TP.pocs);   // tile-part POC
+            check_tile_part_marker(m);
             if (m == 0xff58) {
                 uint32_t v = 0;
                 for (size_t q = j + 5; q < j + 2 + L; ++q) {
@@ -2841,7 +2877,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     if (Hd.want.nc < 3) Hd.want.p.mct = 0;
     ensure_plan(ctx, Hd.want);
     Plan& P = ctx->plan;
-    if (Hd.qcd != ctx->band_qcd) { apply_qcd(P, Hd.qcd); ctx->band_qcd = Hd.qcd; }
+    if (Hd.qcd != ctx->band_qcd) { ctx->band_qcd.clear(); apply_qcd(P, Hd.qcd); ctx->band_qcd = Hd.qcd; }
     const uint32_t red = ctx->dec_reduce;
     if (red >= P.p.numres) throw GkError("reduce must be less than the number of resolutions");
     if (red && win) throw GkError("reduced-resolution decode of a window is not supported");

@@ -465,6 +465,7 @@ bool grk_compress_tile(grk_codec* codec, uint16_t tileIndex, uint8_t* data, uint
     if (!image_geometry(C->image, info)) return false;
     const uint32_t es = (info.prec + 7) / 8;
     if (es > 2) { error("raw tiles of more than 16 bits per sample are not supported"); return false; }
+    if (C->cp.tile_size_on && (!C->cp.t_width || !C->cp.t_height)) { error("tile size must be non-zero"); return false; }
     const uint32_t tw = C->cp.tile_size_on ? std::min(C->cp.t_width, info.w) : info.w;
     const uint32_t th = C->cp.tile_size_on ? std::min(C->cp.t_height, info.h) : info.h;
     const uint32_t ntx = (info.w + tw - 1) / tw, nty = (info.h + th - 1) / th;

@@ -133,3 +133,21 @@ def test_progression_order_changes(eng, pi):
         np.testing.assert_array_equal(eng.decode(cs), img)
         if "tiles" in kw:
             np.testing.assert_array_equal(eng.decode_window(cs, (30, 20, 160, 120)), img[:, 20:120, 30:160])
+
+
+def test_incomplete_poc_refused(eng):
+    """CodeStreamCompress::validateProgressionOrders (CodeStreamCompress.cpp:1685-1747): POC
+    entries that leave a (layer, resolution, component) packet uncovered are refused ("POC:
+    missing packets") instead of silently dropping the packet's code-blocks."""
+    import grok_amd as G
+    img = _img(30, 3, 64, 80)
+    for pocs in ([(0, 0, 1, 4, 3, "LRCP")],                              # layers 1.. of 2 missing
+                 [(0, 0, 2, 3, 3, "RLCP")],                              # resolution 3 missing
+                 [(0, 0, 2, 4, 2, "CPRL"), (1, 2, 2, 4, 3, "RPCL")]):    # (r 0, c 2) missing
+        p = G.default_params(numresolution=4, cblk=(16, 16), layer_rate=[20, 0], pocs=pocs)
+        with pytest.raises(RuntimeError, match="POC: missing packets"):
+            eng.encode(img, 8, params=p)
+    # the engine stays usable and a covering list still encodes
+    p = G.default_params(numresolution=4, cblk=(16, 16), layer_rate=[20, 0], pocs=[(0, 0, 2, 4, 3, "RLCP")])
+    assert eng.encode(img, 8, params=p) == O.encode(img, 8, numres=4, cblk=(16, 16), layer_rate=[20, 0],
+                                                    pocs=[(0, 0, 2, 4, 3, "RLCP")])

@@ -48,3 +48,60 @@ def test_roi_mode_switch_path(eng):
     cs = eng.encode(img, 8, params=G.default_params(numresolution=3, cblk_sty=5, roi=(0, 4)))
     assert cs == O.encode(img, 8, numres=3, cblk_sty=5, roi=(0, 4))
     np.testing.assert_array_equal(eng.decode(cs), img)
+
+
+def test_roi_component_past_last_is_ignored(eng):
+    """grk_cparameters::roi_compno past the last component matches no component
+    (CodeStreamCompress.cpp:538-541 compares it with each index), so no RGN is written."""
+    import grok_amd as G
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, size=(3, 48, 40)).astype(np.int32)
+    plain = eng.encode(img, 8, params=G.default_params(numresolution=3))
+    for c in (3, 1 << 30):
+        cs = eng.encode(img, 8, params=G.default_params(numresolution=3, roi=(c, 7)))
+        assert cs == plain and b"\xff\x5e" not in cs
+
+
+def _split_marker(cs, code):
+    """(offset, length incl. marker) of the first main-header marker `code`"""
+    i = 2
+    while True:
+        m, L = int.from_bytes(cs[i:i + 2], "big"), int.from_bytes(cs[i + 2:i + 4], "big")
+        if m == code:
+            return i, 2 + L
+        assert m != 0xff90
+        i += 2 + L
+
+
+def test_rgn_in_tile_part_header_refused(eng):
+    """RGN in a tile-part header (read_rgn accepts it there) would change the tile's samples;
+    the decoder refuses it instead of skipping it."""
+    import grok_amd as G
+    rng = np.random.default_rng(6)
+    img = rng.integers(0, 256, size=(1, 40, 48)).astype(np.int32)
+    cs = eng.encode(img, 8, params=G.default_params(numresolution=3, roi=(0, 4)))
+    o, n = _split_marker(cs, 0xff5e)
+    rgn = cs[o:o + n]
+    body = cs[:o] + cs[o + n:]
+    sot = body.index(b"\xff\x90")
+    psot = int.from_bytes(body[sot + 6:sot + 10], "big")
+    sot_new = body[sot:sot + 6] + ((psot + n) if psot else 0).to_bytes(4, "big") + body[sot + 10:sot + 12]
+    spliced = body[:sot] + sot_new + rgn + body[sot + 12:]
+    with pytest.raises(RuntimeError, match="RGN in a tile-part header"):
+        eng.decode(spliced)
+    np.testing.assert_array_equal(eng.decode(cs), img)
+
+
+def test_band_bitplanes_over_30_refused(eng):
+    """A Part-1 stream whose band bit-plane count (QCD exponent + guard bits - 1, plus the ROI
+    shift) exceeds 30 cannot be held as (2M+1) << q in an int32: refused, not decoded."""
+    import grok_amd as G
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 256, size=(1, 40, 48)).astype(np.int32)
+    cs = eng.encode(img, 8, params=G.default_params(numresolution=3, roi=(0, 10)))
+    np.testing.assert_array_equal(eng.decode(cs), img)
+    o, n = _split_marker(cs, 0xff5e)
+    bad = cs[:o + n - 1] + bytes([29]) + cs[o + n:]   # shift 29: HH numbps 29 + 11 > 30
+    with pytest.raises(RuntimeError, match="30 band bit-planes"):
+        eng.decode(bad)
+    np.testing.assert_array_equal(eng.decode(cs), img)
