@@ -329,8 +329,6 @@ static void assign_steps_tile(Plan& P, TileG& T) {
                 B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
                 int v = (int)B.expn + (int)P.p.numgbits - 1;
                 B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, v);   // Quantizer.cpp:47: roishift + ...
-                // ROI-scaled indices keep 6 fractional bits below them in a 31-bit magnitude
-                if (P.p.roi(ci) && B.numbps > 25) throw GkError("ROI shift too large for this precision");
             }
         }
     }
@@ -350,9 +348,6 @@ static void apply_qcd(Plan& P, const std::vector<std::pair<uint32_t, uint32_t>>&
                 B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
                 B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
                 B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1);
-                // the Part-1 decoders hold twice the magnitude plus the half-bit, (2M+1) << q, in
-                // an int32: a band (ROI shift included) of more than 30 bit-planes cannot be held
-                if (!P.p.ht() && B.numbps > 30) throw GkError("more than 30 band bit-planes (ROI shift included) not supported");
                 ++bandno;
             }
     }
@@ -2049,6 +2044,14 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     if ((1u << want.p.cbw) > 64 || (1u << want.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
     ensure_plan(ctx, want);
     restore_native_qcd(ctx);
+    // encode: ROI-scaled indices keep 6 fractional bits below them in a 31-bit magnitude
+    // (the decoders take up to 30 band bit-planes, checked where a stream's QCD is applied)
+    if (!ctx->plan.p.roishift.empty())
+    for (const TileG& T : ctx->plan.tiles)
+        for (uint32_t ci = 0; ci < (uint32_t)T.comps.size(); ++ci)
+            for (const ResG& R : T.comps[ci].res)
+                for (const auto& B : R.bands)
+                    if (ctx->plan.p.roi(ci) && B.numbps > 25) throw GkError("ROI shift too large for this precision");
 }
 
 // gk_encode_blocks: the T1 results of the (single) tile in canonical order, the block bytes
@@ -2877,7 +2880,15 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     if (Hd.want.nc < 3) Hd.want.p.mct = 0;
     ensure_plan(ctx, Hd.want);
     Plan& P = ctx->plan;
-    if (Hd.qcd != ctx->band_qcd) { ctx->band_qcd.clear(); apply_qcd(P, Hd.qcd); ctx->band_qcd = Hd.qcd; }
+    if (Hd.qcd != ctx->band_qcd) { apply_qcd(P, Hd.qcd); ctx->band_qcd = Hd.qcd; }
+    // the Part-1 decoders hold twice the magnitude plus the half-bit, (2M+1) << q, in an int32:
+    // a band (ROI shift included) of more than 30 bit-planes cannot be held (every tile has the
+    // same bands as tile 0)
+    if (!P.p.ht())
+        for (const CompG& C : P.tiles[0].comps)
+            for (const ResG& R : C.res)
+                for (const BandG& B : R.bands)
+                    if (B.numbps > 30) throw GkError("more than 30 band bit-planes (ROI shift included) not supported");
     const uint32_t red = ctx->dec_reduce;
     if (red >= P.p.numres) throw GkError("reduce must be less than the number of resolutions");
     if (red && win) throw GkError("reduced-resolution decode of a window is not supported");

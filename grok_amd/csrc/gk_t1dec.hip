@@ -67,6 +67,32 @@ __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
     return c ? a : b;
 }
 
+// Lane conditions as VGPR masks (0 or 0xffffffff) combined with VALU logic and v_bfi selects.
+// Measured on gfx950 with one wave per SIMD: a VALU compare feeding SALU mask logic (s_and_b64
+// of lane masks) or a branch stalls the wave ~14-40 cycles per hop, a v_cndmask reading VCC can
+// take ~14 cycles, while a VALU op issues every ~4.5 cycles; the decoder's step keeps its
+// conditions in VGPRs.  opq() hides a value from the optimiser so it cannot turn the arithmetic
+// back into compares on lane masks.
+__device__ __forceinline__ uint32_t opq(uint32_t v) { asm volatile("" : "+v"(v)); return v; }
+__device__ __forceinline__ uint32_t mbit(uint32_t v, uint32_t k) { return opq((uint32_t)__builtin_amdgcn_sbfe((int32_t)v, k, 1)); }
+__device__ __forceinline__ uint32_t mneg(uint32_t v) { return mbit(v, 31); }   // sign -> mask
+__device__ __forceinline__ uint32_t mlt(uint32_t a, uint32_t b) { return mneg(a - b); }   // a < b (|a - b| < 2^31)
+__device__ __forceinline__ uint32_t mnz(uint32_t v) { return mneg(0u - v); }              // v != 0 (v < 2^31)
+
+__device__ __forceinline__ uint32_t ffbh(uint32_t v) {   // leading zeros, 0xffffffff for 0
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+__device__ __forceinline__ uint32_t ffbl(uint32_t v) {   // lowest set bit, 0xffffffff for 0
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+// m ? a : b bitwise (v_bfi_b32 / v_bitop3_b32); m comes from the helpers above, so the optimiser
+// cannot see it as a compare result and turn the select into a VCC select
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+
 // Bytes at or past the block length read as 0xFF (the MQ decoder's end-of-data rule,
 // mqc_dec.cpp BYTEIN).  The host pads every staged block with >= 32 bytes of 0xFF after its
 // data, and windows that start at or past the length read this constant instead, so the
@@ -119,7 +145,7 @@ __device__ __forceinline__ uint32_t col4(uint64_t a, uint64_t b, uint64_t c, uin
     return (uint32_t)((a >> x) & 1) | ((uint32_t)((b >> x) & 1) << 1) | ((uint32_t)((c >> x) & 1) << 2) |
            ((uint32_t)((d >> x) & 1) << 3);
 }
-enum { PH_FIND = 0, PH_SIGN = 1, PH_UNI1 = 2, PH_UNI2 = 3 };
+enum { PH_FIND = 1, PH_SIGN = 2, PH_UNI1 = 4, PH_UNI2 = 8 };   // one-hot: the step tests bits
 
 struct Rows22 {   // one stripe's rows: S1..S5 / N1..N5 (rows y0..y0+4), P/M/B (rows y0..y0+3)
     uint64_t s1, s2, s3, s4, s5, n1, n2, n3, n4, n5, p0, p1, p2, p3, m0, m1, m2, m3, b0, b1, b2, b3;
@@ -182,7 +208,7 @@ __device__ __forceinline__ void mq2_refill(Mq2& q, bool en) {
 // yields everything the decision needs; the new state's entry is looked up and
 // written back off the decision's dependency chain.
 __device__ __forceinline__ uint32_t mq2_decode(Mq2& q, uint32_t (*ctx)[64], int lane, const uint32_t* tab,
-                                               uint32_t cx, bool en) {
+                                               uint32_t cx, bool en, uint32_t& wb) {
     const uint32_t e = ctx[cx][lane];
     const uint32_t mps = e >> 31;
     const uint32_t qe = e & 0xffff;
@@ -198,7 +224,9 @@ __device__ __forceinline__ uint32_t mq2_decode(Mq2& q, uint32_t (*ctx)[64], int 
     const uint32_t an = en ? (lower ? qe : a1) : q.a;
     const uint32_t ch = (en & !lower) ? chi - (qe << 16) : chi;
     const uint32_t ne = tab[nidx] | (nmps << 31);
-    ctx[cx][lane] = upd ? ne : e;   // unconditional: a branch here would wait on the table read
+    // written back by the caller at the end of the step (unconditionally: a branch would wait
+    // on the table read), so the table read's latency hides behind the step's state updates
+    wb = upd ? ne : e;
     const uint32_t n = upd ? __clz(an) - 16 : 0u;   // RENORMD: all shifts at once
     q.a = an << n;
     q.c = (((uint64_t)ch << 32) | (uint32_t)q.c) << n;
@@ -212,10 +240,11 @@ struct Dec2Lds {
     uint8_t zc[4][512];
     uint8_t sc[256];                 // index bit0 N-neg 1 N-sig 2 W-neg 3 W-sig 4 E-neg 5 E-sig 6 S-neg 7 S-sig
     uint32_t ring[RING_DW + 1][64];
-    uint32_t sg[6 * 3][64];          // significance rows y0-1 .. y0+4, guarded: bit c+1 of the 96-bit row = column c
-    uint32_t ng[6 * 3][64];          // sign rows (bits only where significant), same layout
+    uint32_t sg[7 * 3][64];          // significance rows y0-1 .. y0+4 (+ a zero row), guarded: bit c+1 of the 96-bit row = column c
+    uint32_t ng[7 * 3][64];          // sign rows (bits only where significant), same layout
     uint32_t mu[4 * 2][64];          // refined-in-an-earlier-plane rows y0 .. y0+3, plain 32-bit halves
     uint32_t bt[4 * 2][64];          // plane-bit rows y0 .. y0+3
+    uint32_t pv[4 * 2][64];          // visited in SP of this plane, rows y0 .. y0+3 (SP stripe-passes)
 };
 
 __device__ __forceinline__ void g_put(uint32_t (*g)[64], int row, int lane, uint64_t v) {
@@ -271,8 +300,8 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
     const uint64_t colmask = w >= 64 ? ~0ull : ((1ull << w) - 1);
     const uint32_t ns = (h + 3) >> 2;
     const uint8_t* zc = Ls.zc[B.orient & 3];
-    for (int i = 0; i < 18; ++i) { Ls.sg[i][lane] = 0; Ls.ng[i][lane] = 0; }
-    for (int i = 0; i < 8; ++i) { Ls.mu[i][lane] = 0; Ls.bt[i][lane] = 0; }
+    for (int i = 0; i < 21; ++i) { Ls.sg[i][lane] = 0; Ls.ng[i][lane] = 0; }
+    for (int i = 0; i < 8; ++i) { Ls.mu[i][lane] = 0; Ls.bt[i][lane] = 0; Ls.pv[i][lane] = 0; }
     // mqc_resetstates (mqc_dec.cpp:121-130): every context at state 0 except ZC0 = 4, AGG = 3, UNI = 46
     for (int c = 0; c < 19; ++c)
         Ls.ctx[c][lane] = c_mq[c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))];
@@ -300,22 +329,77 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
     // position: plane k (0 = top), pass type t (0 SP, 1 MR, 2 CL), stripe s, pass index pidx
     uint32_t k = 0, t = 2, s = 0, pidx = 0;
     bool done = npasses == 0, parked = false;
-    uint32_t nr = min(4u, h), x = 0, r = 0, ph = PH_FIND, rlhi = 0;
+    // Candidates: C0..C3 are the stripe-pass's candidate rows at its start (static); the lane
+    // walks them column by column: x = current column, nib = its rows still to code (the current
+    // position included while in FIND), nn = rows of column x + 1 that SP propagation made
+    // candidates.
+    uint32_t nr = min(4u, h), x = 0xffffffffu, r = 0, ph = PH_FIND, rlhi = 0, nib = 0, nn = 0;
     uint32_t vr = (1u << nr) - 1;                 // valid rows of the stripe
-    uint64_t C0, C1, C2, C3, E, fresh = 0;        // candidates (consumed as coded), run-length columns
-    uint64_t P0 = 0, P1 = 0, P2 = 0, P3 = 0;      // visited in SP of this plane
+    uint64_t C0, C1, C2, C3, CU, E, fresh = 0;    // candidate rows, their union, run-length columns
     {
         const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
                        v3 = nr > 3 ? colmask : 0;
         C0 = v0; C1 = v1; C2 = v2; C3 = v3;      // first CL: nothing significant yet
+        CU = v0;
         E = (nr == 4) ? colmask : 0ull;
     }
+    // The current decision's context cx and its state entry e are ready when a step starts; so
+    // are, for the current position, the run-length flag, the 3x3 significance window fs and
+    // the sign-context entry sce (for the SIGN decision that may follow).
+    uint32_t cx = 0, e = 0, fs = 0, sce = 0;
+    bool agg = false;
+    // the entries of the two possible next contexts, read by the last step; the next step's R2
+    // takes the one its decision selected (pend_b) when that step decided (pend_v)
+    uint32_t eAp = 0, eBp = 0;
+    uint32_t pend_v = 0, pend_b = 0, slow = 0, aggm = 0;   // lane masks
+    // First position of column x + 1 or later (the next column with a stripe-start candidate, or
+    // x + 1 when propagation gave it rows nn0), given the current column's rows nib0 still to code.
+    auto next_position = [&](uint32_t nib0, uint32_t nn0, uint32_t& xA, uint32_t& nibA, uint32_t& nnA) {
+        const uint32_t x1 = x + 1;
+        const uint64_t rest = (CU >> (x1 & 63)) & (0ull - (uint64_t)(x1 < 64));
+        const uint32_t xs = rest ? x1 + (uint32_t)__ffsll((long long)rest) - 1 : 64u;
+        const uint32_t xadv = nn0 ? x1 : xs;
+        const uint32_t nibadv = (col4(C0, C1, C2, C3, xadv & 63) & (0u - (uint32_t)(xadv < 64))) | nn0;
+        const bool stay = nib0 != 0;
+        xA = stay ? x : xadv;
+        nibA = stay ? nib0 : nibadv;
+        nnA = stay ? nn0 : 0u;
+    };
+    // The first position of a stripe-pass (lanes that `sel`): its window, contexts and entry.
+    auto prep_stripe = [&](bool sel) {
+        x = sel ? 0xffffffffu : x;
+        uint32_t xA, nibA, nnA;
+        next_position(0u, 0u, xA, nibA, nnA);
+        const uint32_t rA = ((uint32_t)__ffs(nibA) - 1) & 3;
+        const uint32_t Xc = xA & 63, dx = Xc >> 5, sx = Xc & 31, o0 = rA * 3 + dx;
+        const uint32_t s0 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 1][lane], Ls.sg[o0][lane], sx) & 7;
+        const uint32_t s1 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 4][lane], Ls.sg[o0 + 3][lane], sx) & 7;
+        const uint32_t s2 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 7][lane], Ls.sg[o0 + 6][lane], sx) & 7;
+        const uint32_t n0 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 1][lane], Ls.ng[o0][lane], sx) & 7;
+        const uint32_t n1 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 4][lane], Ls.ng[o0 + 3][lane], sx) & 7;
+        const uint32_t n2 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 7][lane], Ls.ng[o0 + 6][lane], sx) & 7;
+        const uint32_t mub = (Ls.mu[rA * 2 + dx][lane] >> sx) & 1;
+        const uint32_t fsA = s0 | (s1 << 3) | (s2 << 6), fnA = n0 | (n1 << 3) | (n2 << 6);
+        const uint32_t scA = Ls.sc[(fsA & 0xaa) | ((fnA >> 1) & 0x55)];
+        const bool aggA = (t == 2) & (((E >> Xc) & 1) != 0) & (nibA == 0xf);
+        const uint32_t cxF = t == 1 ? (mub ? CTX_MAG + 2 : ((fsA & 0x1ef) ? CTX_MAG + 1 : CTX_MAG))
+                                    : (aggA ? CTX_AGG : CTX_ZC + zc[fsA]);
+        const uint32_t eF = Ls.ctx[cxF][lane];
+        if (sel) {
+            x = xA; r = rA; nib = nibA; nn = nnA; ph = PH_FIND; agg = aggA; fs = fsA; sce = scA; cx = cxF; e = eF;
+            aggm = aggA ? ~0u : 0u;
+            pend_v = 0; slow = 0;
+            parked = parked || nibA == 0;   // a stripe-pass without candidates ends at once
+        }
+    };
     Rows22 X = {};
     {
         uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
         next_pos3(k2, t2, s2, p2, ns);
         if (!done && p2 < npasses && k2 < numbps) load_rows(X, WS, k2, t2, 4 * s2);
     }
+
+    prep_stripe(!done);
 
     while (__any(!done)) {
         // ---------------- stripe boundary for parked lanes (batched)
@@ -366,7 +450,10 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
                 // a plane's bit rows
                 wdirty = fresh != 0;
                 W0 = S1; W1 = S2; W2 = S3; W3 = S4; W4 = N1; W5 = N2; W6 = N3; W7 = N4;
-                WB0 = B0; WB1 = B1; WB2 = B2; WB3 = B3; WP0 = P0; WP1 = P1; WP2 = P2; WP3 = P3;
+                WB0 = B0; WB1 = B1; WB2 = B2; WB3 = B3;
+                const uint64_t P0 = h_get(Ls.pv, 0, lane), P1 = h_get(Ls.pv, 1, lane), P2 = h_get(Ls.pv, 2, lane),
+                               P3 = h_get(Ls.pv, 3, lane);
+                WP0 = P0; WP1 = P1; WP2 = P2; WP3 = P3;
                 wy0 = y0; wk = k; wt = t;
                 if (!late) {
                     uint64_t* sgp = WS + 4 * y0 + WS_S;
@@ -407,6 +494,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
                 g_put(Ls.ng, 3, lane, nN3); g_put(Ls.ng, 4, lane, nN4); g_put(Ls.ng, 5, lane, nN5);
                 h_put(Ls.mu, 0, lane, nM0); h_put(Ls.mu, 1, lane, nM1); h_put(Ls.mu, 2, lane, nM2); h_put(Ls.mu, 3, lane, nM3);
                 h_put(Ls.bt, 0, lane, nB0); h_put(Ls.bt, 1, lane, nB1); h_put(Ls.bt, 2, lane, nB2); h_put(Ls.bt, 3, lane, nB3);
+                h_put(Ls.pv, 0, lane, 0); h_put(Ls.pv, 1, lane, 0); h_put(Ls.pv, 2, lane, 0); h_put(Ls.pv, 3, lane, 0);
                 if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[1] += t - tp0; tp0 = t; }
                 const uint32_t ny0 = 4 * s;
                 nr = done ? 0u : min(4u, h - ny0);
@@ -420,9 +508,9 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
                 const uint64_t w0 = t == 1 ? nS1 : ~nS1, w1 = t == 1 ? nS2 : ~nS2, w2 = t == 1 ? nS3 : ~nS3,
                                w3 = t == 1 ? nS4 : ~nS4;
                 C0 = w0 & q0 & v0; C1 = w1 & q1 & v1; C2 = w2 & q2 & v2; C3 = w3 & q3 & v3;
+                CU = C0 | C1 | C2 | C3;
                 E = (t == 2 && nr == 4) ? (C0 & C1 & C2 & C3 & ~dil3(nS0 | nS1, nS2 | nS3, nS4 | nS5)) : 0ull;
-                // SP: visited = its candidates (grown by propagation); MR: refined = old | coded now
-                P0 = t == 0 ? C0 : pP0; P1 = t == 0 ? C1 : pP1; P2 = t == 0 ? C2 : pP2; P3 = t == 0 ? C3 : pP3;
+                // SP: visited = the positions it codes (pv rows in LDS); MR: refined = old | coded now
                 // MR refines every candidate: the rows after this pass, stored with the write-back
                 wmu = t == 1; wmy = ny0;
                 WM0 = nM0 | C0; WM1 = nM1 | C1; WM2 = nM2 | C2; WM3 = nM3 | C3;
@@ -430,9 +518,10 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
                     uint64_t* mup = WS + 4 * ny0 + WS_M;
                     st2(mup, WM0, WM1); st2(mup + 2, WM2, WM3);
                 }
-                fresh = 0; ph = PH_FIND;
+                fresh = 0; nn = 0; ph = PH_FIND;
                 if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[2] += t - tp0; tp0 = t; }
             }
+            prep_stripe(switched && !done);
             // stage the next ring bytes (lanes whose fill point moved) and prefetch the next
             // stripe of the lanes that switched (the others keep theirs): no re-reads
             uint64_t tq0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
@@ -476,96 +565,166 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             mq2_refill(q, !done && q.avail <= 40);
             q.nb4 = ring_get4(Ls.ring, lane, q.bp);
         }
+        // lane masks constant over the group: active, pass type (t: 0 SP, 1 MR, 2 CL)
+        uint32_t actm = (!done && !parked) ? ~0u : 0u;
+        const uint32_t mSP = mlt(t, 1), mMR = mbit(t, 0), mCL = mbit(t, 1);
+        uint32_t parkm = 0;
+        // need: some lane must refill its code register or fetch a SIGN context after UNI2 before
+        // its next decision (computed at the end of the previous step, so the branch does not wait)
+        bool need = __any(((actm != 0) & (q.avail < 16)) | (slow != 0));
 #pragma unroll
         for (int us = 0; us < T1DEC_UNROLL; ++us) {
-            // ---------------- one decision per active lane
-            const bool act = !done && !parked;
+            // ---------------- one decision per active lane.  While it is decoded, the next step's
+            // context is fetched for both outcomes: A, the next FIND position (where a 0 leads, or
+            // where MR and SIGN lead anyway) with its significance window, LUT entry and context
+            // entry, and B (SIGN after a ZC 1, UNI1 after a run-length 1) with its entry.  The
+            // decision then only selects, so the LDS round trips are off the chain from one
+            // decision to the next.  The step is one basic block cut into regions by scheduling
+            // fences, ordered so that a region's LDS reads land while the next region computes:
+            //   R1 position A, window reads | R2 this decision | R3 windows -> LUT reads |
+            //   R4 state updates, context write-back | R5 contexts of A and B, entry reads |
+            //   R6 next state (the entry is selected in the next step's R2)
+            // SIGN after UNI2 (a run-length interruption, rare) fetches its context before the step.
             ++nstep;
-            const bool finding = ph == PH_FIND;
-            // next coding position: first remaining candidate in stripe scan order
-            const uint64_t CU = C0 | C1 | C2 | C3;
-            const uint32_t xq = ((uint32_t)__ffsll((long long)CU) - 1) & 63;
-            const uint32_t c4 = col4(C0, C1, C2, C3, xq);
-            const bool use = act && finding;
-            const bool found = CU != 0;
-            x = (use && found) ? xq : x;
-            r = (use && found) ? (uint32_t)(__ffs(c4) - 1) : r;
-            const bool pend = use ? found : act;
-            parked = parked || (use && !found);
-            // neighbourhood of (x, r): guarded rows r .. r+2 (= stripe rows r-1 .. r+1)
-            const uint32_t dx = x >> 5, sx = x & 31;
-            const uint32_t o0 = (r * 3 + dx);
-            const uint32_t s0 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 1][lane], Ls.sg[o0][lane], sx) & 7;
-            const uint32_t s1 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 4][lane], Ls.sg[o0 + 3][lane], sx) & 7;
-            const uint32_t s2 = __builtin_amdgcn_alignbit(Ls.sg[o0 + 7][lane], Ls.sg[o0 + 6][lane], sx) & 7;
-            const uint32_t n0 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 1][lane], Ls.ng[o0][lane], sx) & 7;
-            const uint32_t n1 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 4][lane], Ls.ng[o0 + 3][lane], sx) & 7;
-            const uint32_t n2 = __builtin_amdgcn_alignbit(Ls.ng[o0 + 7][lane], Ls.ng[o0 + 6][lane], sx) & 7;
-            const uint32_t mub = (Ls.mu[r * 2 + dx][lane] >> sx) & 1;
-            const uint32_t fs = s0 | (s1 << 3) | (s2 << 6);
-            const uint32_t fn = n0 | (n1 << 3) | (n2 << 6);
-            const uint32_t sce = Ls.sc[(fs & 0xaa) | ((fn >> 1) & 0x55)];
-            const uint32_t zcx = zc[fs];
-            const bool is_cl = t == 2, is_mr = t == 1, is_sp = t == 0;
+            if (__builtin_expect(need, 0)) {
+                while (__any((actm != 0) & (q.avail < 16))) {   // a burst of long renormalisations
+                    mq2_refill(q, (actm != 0) & (q.avail < 16));
+                    q.nb4 = ring_get4(Ls.ring, lane, q.bp);
+                }
+                if (__any(slow != 0)) {   // SIGN at row rr after UNI2: its window, sign context and entry
+                    const uint32_t dxs = (x >> 5) & 1, sxs = x & 31, os = r * 3 + dxs;
+                    const uint32_t fss = (__builtin_amdgcn_alignbit(Ls.sg[os + 1][lane], Ls.sg[os][lane], sxs) & 7) |
+                                         ((__builtin_amdgcn_alignbit(Ls.sg[os + 4][lane], Ls.sg[os + 3][lane], sxs) & 7) << 3) |
+                                         ((__builtin_amdgcn_alignbit(Ls.sg[os + 7][lane], Ls.sg[os + 6][lane], sxs) & 7) << 6);
+                    const uint32_t fns = (__builtin_amdgcn_alignbit(Ls.ng[os + 1][lane], Ls.ng[os][lane], sxs) & 7) |
+                                         ((__builtin_amdgcn_alignbit(Ls.ng[os + 4][lane], Ls.ng[os + 3][lane], sxs) & 7) << 3) |
+                                         ((__builtin_amdgcn_alignbit(Ls.ng[os + 7][lane], Ls.ng[os + 6][lane], sxs) & 7) << 6);
+                    const uint32_t cxs = CTX_SC + (Ls.sc[(fss & 0xaa) | ((fns >> 1) & 0x55)] & 15);
+                    const uint32_t es = Ls.ctx[cxs][lane];
+                    fs = bsel(slow, fss, fs);
+                    cx = bsel(slow, cxs, cx);
+                    e = bsel(slow, es, e);
+                    slow = 0;
+                }
+            }
+            // ---- R1
+            const uint32_t mF = mbit(ph, 0), mS = mbit(ph, 1), mU1 = mbit(ph, 2), mU2 = mbit(ph, 3);
+            // SIGN: the sample becomes significant now (its sign bit follows the decision)
+            const uint32_t gx = x + 1, gd = (gx >> 5) & 3, gb = 1u << (gx & 31);
+            const uint32_t sgn = actm & mS;
+            atomicOr(&Ls.sg[(r + 1) * 3 + gd][lane], gb & sgn);
+            const uint32_t spn = sgn & mSP;   // SP propagation from the new significance
+            const uint32_t nf = ~fs;
+            const uint32_t ca = (((nf >> 7) & 1) << (r + 1)) & vr & spn;
+            const uint32_t t3 = ((nf >> 2) & 1) | ((nf >> 4) & 2) | ((nf >> 6) & 4);
+            const uint32_t cb = ((t3 << r) >> 1) & vr & spn & mlt(gx, w);
+            const uint32_t nib0 = bsel(mF, nib & ~(1u << r) & ~aggm, nib | ca);
+            const uint32_t nn0 = nn | cb;
+            const uint64_t fresh0 = fresh | ((uint64_t)(sgn & 1) << (x & 63));
+            // next position: the current column's next row, else x + 1 (propagated rows) or the
+            // next column with a stripe-start candidate
+            const uint32_t x1 = x + 1;
+            const uint64_t rest = CU >> (x1 & 63);
+            const uint32_t in64 = mlt(x1, 64);
+            const uint32_t frel = min(ffbl((uint32_t)rest & in64),   // first set bit, ~0 if none
+                                      min(ffbl((uint32_t)(rest >> 32) & in64), 0xffffffdfu) + 32u);
+            const uint32_t xs = min(x1 + min(frel, 64u), 64u);
+            const uint32_t xadv = bsel(mnz(nn0), x1, xs);
+            const uint32_t nibadv = (col4(C0, C1, C2, C3, xadv & 63) & mlt(xadv, 64)) | nn0;
+            const uint32_t stay = mnz(nib0);
+            const uint32_t xA = bsel(stay, x, xadv), nibA = bsel(stay, nib0, nibadv), nnA = nn0 & stay;
+            const uint32_t rA = (uint32_t)ffbl(nibA) & 3;
+            // significance window of A; sign window of the current position (its sign context)
+            const uint32_t XA = xA & 63, dA = XA >> 5, sA = XA & 31, oA = rA * 3 + dA;
+            const uint32_t g0a = Ls.sg[oA][lane], g0b = Ls.sg[oA + 1][lane], g1a = Ls.sg[oA + 3][lane],
+                           g1b = Ls.sg[oA + 4][lane], g2a = Ls.sg[oA + 6][lane], g2b = Ls.sg[oA + 7][lane];
+            const uint32_t muw = Ls.mu[rA * 2 + dA][lane];
+            const uint32_t Xc = x & 63, dC = Xc >> 5, sC = Xc & 31, oC = r * 3 + dC;
+            const uint32_t h0a = Ls.ng[oC][lane], h0b = Ls.ng[oC + 1][lane], h1a = Ls.ng[oC + 3][lane],
+                           h1b = Ls.ng[oC + 4][lane], h2a = Ls.ng[oC + 6][lane], h2b = Ls.ng[oC + 7][lane];
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- R2: the entry selected by the last decision; DECODE (Annex C.3.2; RENORMD as one shift)
+            e = bsel(pend_v, bsel(pend_b, eBp, eAp), e);
+            const uint32_t tM = Ls.tab[(e >> 16) & 0x3f], tL = Ls.tab[(e >> 22) & 0x3f];   // MPS / LPS successors
+            const uint32_t mps = e >> 31, qe = e & 0xffff;
+            const uint32_t chi = (uint32_t)(q.c >> 32);
+            const uint32_t a1 = q.a - qe;
+            const uint32_t lower = mlt(chi >> 16, qe);
+            const uint32_t fast = ~lower & mbit(a1, 15);
+            const uint32_t mpsp = lower ^ ~mlt(a1, qe);      // exchange rule
+            const uint32_t d = mps ^ (~(fast | mpsp) & 1);
+            const uint32_t upd = actm & ~fast;
+            const uint32_t an = bsel(actm, bsel(lower, qe, a1), q.a);
+            const uint32_t ch = chi - ((qe << 16) & actm & ~lower);
+            const uint32_t nsh = (ffbh(an) - 16) & upd;   // an != 0
+            q.a = an << nsh;
+            q.c = (((uint64_t)ch << 32) | (uint32_t)q.c) << nsh;
+            q.avail -= nsh;
+            nsym += actm & 1;
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- R3: windows -> LUT reads (zero coding of A, sign context of the current position)
+            const uint32_t fsA = (__builtin_amdgcn_alignbit(g0b, g0a, sA) & 7) | ((__builtin_amdgcn_alignbit(g1b, g1a, sA) & 7) << 3) |
+                                 ((__builtin_amdgcn_alignbit(g2b, g2a, sA) & 7) << 6);
+            const uint32_t fnC = (__builtin_amdgcn_alignbit(h0b, h0a, sC) & 7) | ((__builtin_amdgcn_alignbit(h1b, h1a, sC) & 7) << 3) |
+                                 ((__builtin_amdgcn_alignbit(h2b, h2a, sC) & 7) << 6);
+            const uint32_t zcA = zc[fsA];
+            const uint32_t sce = Ls.sc[(fs & 0xaa) | ((fnC >> 1) & 0x55)];
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- R4: state updates: plane bit (significance or refinement 1), visited in SP; the
+            // context's new entry written back (the reads of R5 come after it)
+            const uint32_t md = mbit(d, 0);
+            const uint32_t pb = sgn | (actm & mF & mMR & md);
+            const uint32_t dx0 = (x >> 5) & 1, bx = 1u << (x & 31);
+            atomicOr(&Ls.bt[r * 2 + dx0][lane], bx & pb);
+            atomicOr(&Ls.pv[r * 2 + dx0][lane], bx & actm & mF & mSP);
+            fresh |= (uint64_t)(pb & 1) << (x & 63);
+            // next state: FIND at A after a 0 (FIND), always after MR and SIGN; SIGN after a ZC 1;
+            // UNI1 after a run-length 1; UNI2 after UNI1; SIGN at row 2 rlhi + d after UNI2
+            const uint32_t takeB = mF & ~mMR & md;
+            const uint32_t toA = (mF & ~takeB) | mS;
+            const uint32_t rr = (rlhi << 1) | d;
+            const uint32_t nph = bsel(toA, PH_FIND, bsel(mF, bsel(aggm, PH_UNI1, PH_SIGN), bsel(mU1, PH_UNI2, PH_SIGN)));
+            const uint32_t consumed = bsel(mF & ~aggm, 1u << r, ((2u << rr) - 1) & mU2);
+            const uint32_t ne = bsel(mpsp, tM | (mps << 31), tL | ((mps ^ ((e >> 28) & 1)) << 31));
+            Ls.ctx[cx][lane] = bsel(upd, ne, e);
+            // some lane must refill its code register, or fetch a SIGN context after UNI2, before its
+            // next decision: decided here so the next step's branch does not wait for the compare
+            need = __any((actm & (mlt(q.avail, 16) | mU2)) != 0);
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- R5: the sign, the contexts of A and B and their entries
+            const uint32_t negs = sgn & mbit(d ^ (sce >> 4), 0);
+            atomicOr(&Ls.ng[(r + 1) * 3 + gd][lane], gb & negs);
             // a column starts in run-length mode when it was eligible at stripe start, is untouched
             // and its left neighbour column gained no significance in this pass
-            // (bitwise, not short-circuit: keeps the step free of exec-mask branches)
-            const bool agg = is_cl & finding & (((E >> x) & 1) != 0) & (c4 == 0xf) & ((((fresh << 1) >> x) & 1) == 0);
-            const uint32_t cx_mr = vsel(mub != 0, CTX_MAG + 2, vsel((fs & 0x1ef) != 0, CTX_MAG + 1, CTX_MAG));
-            const uint32_t cx = vsel(is_mr, cx_mr,
-                                     vsel(agg, CTX_AGG,
-                                          vsel(ph == PH_SIGN, CTX_SC + (sce & 15), vsel(finding, CTX_ZC + zcx, CTX_UNI))));
-            if (__any(pend && q.avail < 16)) {   // rare: a burst of long renormalisations (a loop
-                do {                              // here would put its head's copies on every step)
-                    mq2_refill(q, pend && q.avail < 16);
-                    q.nb4 = ring_get4(Ls.ring, lane, q.bp);
-                } while (__any(pend && q.avail < 16));
-            }
-            const uint32_t d = mq2_decode(q, Ls.ctx, lane, Ls.tab, cx, pend);
-            nsym += pend ? 1 : 0;
-            // ---- state updates
-            const bool sig = pend && !is_mr && ph == PH_SIGN;
-            const bool negs = sig && ((d ^ (sce >> 4)) & 1);
-            const uint32_t gx = x + 1, gd = gx >> 5, gb = 1u << (gx & 31);
-            atomicOr(&Ls.sg[(r + 1) * 3 + gd][lane], sig ? gb : 0u);
-            atomicOr(&Ls.ng[(r + 1) * 3 + gd][lane], negs ? gb : 0u);
-            const bool pb = sig || (pend && is_mr && d);
-            atomicOr(&Ls.bt[r * 2 + dx][lane], pb ? (1u << sx) : 0u);
-            fresh |= (uint64_t)(pb ? 1u : 0u) << x;   // pb == sig outside MR (run-length test in CL)
-            // SP: positions after (x, r) that gain a significant neighbour become candidates:
-            // (x, r+1) and column x+1 rows r-1 .. r+1, unless significant (window bits 7; 2, 5, 8)
-            const bool spn = sig && is_sp;
-            const uint32_t nf = ~fs;
-            const uint32_t ca = spn ? ((((nf >> 7) & 1) << (r + 1)) & vr) : 0u;
-            const uint32_t t3 = ((nf >> 2) & 1) | ((nf >> 4) & 2) | ((nf >> 6) & 4);
-            const uint32_t cb = (spn && gx < w) ? (((t3 << r) >> 1) & vr) : 0u;
-            // consumption: the coded position; a whole column after a zero run-length decision;
-            // rows 0 .. rr once the run-length index rr is known
-            const uint32_t rr = (rlhi << 1) | d;
-            const uint32_t crow_f = vsel(agg, vsel(d != 0, 0u, 0xfu), 1u << r);
-            const uint32_t crow = vsel(pend, vsel(finding, crow_f, vsel(ph == PH_UNI2, (2u << rr) - 1, 0u)), 0u);
-#define GK_CROW(Ci, Pi, i)                                                                                           \
-        {                                                                                                                \
-            const uint64_t add = (uint64_t)(((ca >> i) & 1) | (((cb >> i) & 1) << 1)) << x;                             \
-            const uint64_t clr = (uint64_t)((crow >> i) & 1) << x;                                                       \
-            Ci = (Ci & ~clr) | add;                                                                                      \
-            Pi |= add;                                                                                                   \
+            const uint32_t aggA = mCL & mbit((uint32_t)(E >> XA), 0) & mbit(nibA + 1, 4) &
+                                  ~mbit((uint32_t)((fresh0 << 1) >> XA), 0);
+            const uint32_t cxM = bsel(mbit(muw, sA), CTX_MAG + 2, bsel(mnz(fsA & 0x1ef), CTX_MAG + 1, CTX_MAG));
+            const uint32_t cxF = bsel(mMR, cxM, bsel(aggA, CTX_AGG, CTX_ZC + zcA));
+            const uint32_t cxA = bsel(mU1, CTX_UNI, cxF);
+            const uint32_t cxB = bsel(aggm, CTX_UNI, CTX_SC + (sce & 15));
+            eAp = Ls.ctx[cxA][lane];
+            eBp = Ls.ctx[cxB][lane];
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- R6: next state (lanes that did not decide keep cx / e and are parked or done, so
+            // their other fields are rebuilt at the next stripe boundary)
+            fs = bsel(toA, fsA, fs);
+            aggm = bsel(toA, aggA, aggm);
+            x = bsel(toA, xA, x);
+            r = bsel(toA, rA, bsel(mU2, rr, r));
+            nn = bsel(toA, nnA, nn);
+            nib = bsel(toA, nibA, nib & ~consumed);
+            rlhi = bsel(mU1, d, rlhi);
+            ph = nph;
+            const uint32_t np = actm & toA & ~mnz(nibA);   // no position left: the stripe-pass ends
+            parkm |= np;
+            cx = bsel(actm, bsel(takeB, cxB, cxA), cx);
+            pend_v = actm & ~mU2; pend_b = takeB;
+            slow = actm & mU2;
+            actm &= ~np;
+            __builtin_amdgcn_sched_barrier(0);
         }
-            GK_CROW(C0, P0, 0) GK_CROW(C1, P1, 1) GK_CROW(C2, P2, 2) GK_CROW(C3, P3, 3)
-#undef GK_CROW
-            // phase machine: FIND -(ZC 1)-> SIGN -> FIND; FIND(run-length) -(1)-> UNI1 -> UNI2 -> SIGN
-            // next phase = table[ph][d][agg] (MR always stays in FIND), 2 bits per entry
-            //   FIND: agg ? (d ? UNI1 : FIND) : (d ? SIGN : FIND); SIGN -> FIND; UNI1 -> UNI2; UNI2 -> SIGN
-            const bool uni1 = ph == PH_UNI1, uni2 = ph == PH_UNI2;
-            const uint32_t key = (ph << 2) | (d << 1) | (agg ? 1u : 0u);
-            constexpr uint32_t kPhT = (0u << 0) | (0u << 2) | (PH_SIGN << 4) | (PH_UNI1 << 6)       // FIND
-                                    | (PH_UNI2 << 16) | (PH_UNI2 << 18) | (PH_UNI2 << 20) | (PH_UNI2 << 22)  // UNI1
-                                    | (PH_SIGN << 24) | (PH_SIGN << 26) | (PH_SIGN << 28) | (PH_SIGN << 30); // UNI2
-            const uint32_t nph = is_mr ? (uint32_t)PH_FIND : ((kPhT >> (2 * key)) & 3);
-            rlhi = vsel(pend & uni1, d, rlhi);
-            r = vsel(pend & uni2, rr, r);
-            ph = vsel(pend, nph, ph);
-        }
+        parked = parked || parkm != 0;
+        agg = aggm != 0;
         if (TIMING) cyc_step += __builtin_amdgcn_s_memtime() - tev;
     }
     unsigned long long cp[6] = {0, 0, 0, 0, 0, 0};

@@ -12,10 +12,11 @@ cp -r include "$T/"
 cp grok_amd/csrc/* "$T/grok_amd/csrc/"
 cp "$REPL" "$T/grok_amd/csrc/$NAME"
 cd "$T/grok_amd/csrc"
-for f in gk_kernels.hip gk_dwt97.hip gk_t1enc.hip gk_t1dec.hip gk_ht.hip gk_engine.cpp grk_shim.cpp; do
+SRCS="gk_kernels.hip gk_dwt97.hip gk_t1enc.hip gk_t1dec.hip gk_t1ms.hip gk_ht.hip gk_engine.cpp grk_shim.cpp"
+for f in $SRCS; do
     hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -c $f -o ${f%.*}.o &
 done
 wait
-hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" gk_kernels.o gk_dwt97.o gk_t1enc.o gk_t1dec.o gk_ht.o gk_engine.o grk_shim.o
+hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" $(for f in $SRCS; do echo ${f%.*}.o; done)
 rm -rf "$T"
 echo "$OUT"

@@ -1,4 +1,5 @@
-"""Print per-kernel SQ counter averages from tools/sq_counters.sh output."""
+"""Print per-kernel SQ counter averages from a rocprofv3 PMC pass (tools/sq_counters*.sh):
+per-wave instruction counts and the cycle buckets as fractions of SQ_WAVE_CYCLES."""
 import sqlite3
 import sys
 
@@ -7,9 +8,17 @@ d = {}
 for k, cn, v in c.execute("select kernel_name, counter_name, avg(value) from counters_collection group by kernel_name, counter_name"):
     d.setdefault(k.split("(")[0], {})[cn] = v
 for k, v in d.items():
-    if any(t in k for t in ("t1", "dwt", "rct", "ht")):
-        w = v.get("SQ_WAVES", 1)
-        print("%-22s waves %6d  VALU/wave %10.0f SALU/wave %9.0f LDS/wave %8.0f  active %5.2f wait %5.2f waitinst %5.2f" % (
-            k[:22], w, v["SQ_INSTS_VALU"] / w, v["SQ_INSTS_SALU"] / w, v["SQ_INSTS_LDS"] / w,
-            v["SQ_ACTIVE_INST_ANY"] / v["SQ_WAVE_CYCLES"], v["SQ_WAIT_ANY"] / v["SQ_WAVE_CYCLES"],
-            v["SQ_WAIT_INST_ANY"] / v["SQ_WAVE_CYCLES"]))
+    if not any(t in k for t in ("t1", "dwt", "rct", "ht", "gather")):
+        continue
+    w = v.get("SQ_WAVES", 1) or 1
+    cyc = v.get("SQ_WAVE_CYCLES", 0) or 1
+    parts = ["waves %d" % w]
+    for n, x in sorted(v.items()):
+        if n in ("SQ_WAVES", "SQ_WAVE_CYCLES"):
+            continue
+        if n.startswith("SQ_INSTS"):
+            parts.append("%s/wave %.0f" % (n[8:], x / w))
+        else:
+            parts.append("%s %.3f" % (n[3:], x / cyc))
+    parts.append("WAVE_CYCLES/wave %.0f" % (cyc / w))
+    print("%-26s %s" % (k[:26], "  ".join(parts)))
