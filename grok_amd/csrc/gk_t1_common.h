@@ -11,6 +11,33 @@
 // =============================================================================
 enum { CTX_ZC = 0, CTX_SC = 9, CTX_MAG = 14, CTX_AGG = 17, CTX_UNI = 18 };
 
+// Lane conditions as VGPR masks (0 or 0xffffffff) combined with VALU logic and v_bfi selects.
+// Measured on gfx950 with one wave per SIMD: a VALU compare feeding SALU mask logic (s_and_b64
+// of lane masks) or a branch stalls the wave ~14-40 cycles per hop, a v_cndmask reading VCC can
+// take ~14 cycles, while a VALU op issues every ~4.5 cycles; the decoder's step keeps its
+// conditions in VGPRs.  opq() hides a value from the optimiser so it cannot turn the arithmetic
+// back into compares on lane masks.
+__device__ __forceinline__ uint32_t opq(uint32_t v) { asm volatile("" : "+v"(v)); return v; }
+__device__ __forceinline__ uint32_t mbit(uint32_t v, uint32_t k) { return opq((uint32_t)__builtin_amdgcn_sbfe((int32_t)v, k, 1)); }
+__device__ __forceinline__ uint32_t mneg(uint32_t v) { return mbit(v, 31); }   // sign -> mask
+__device__ __forceinline__ uint32_t mlt(uint32_t a, uint32_t b) { return mneg(a - b); }   // a < b (|a - b| < 2^31)
+__device__ __forceinline__ uint32_t mnz(uint32_t v) { return mneg(0u - v); }              // v != 0 (v < 2^31)
+
+__device__ __forceinline__ uint32_t ffbh(uint32_t v) {   // leading zeros, 0xffffffff for 0
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+__device__ __forceinline__ uint32_t ffbl(uint32_t v) {   // lowest set bit, 0xffffffff for 0
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+// m ? a : b bitwise (v_bfi_b32 / v_bitop3_b32); m comes from the helpers above, so the optimiser
+// cannot see it as a compare result and turn the select into a VCC select
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+
+
 __device__ __forceinline__ uint8_t zc_rule(uint32_t orient, uint32_t f) {
     int h = ((f >> 3) & 1) + ((f >> 5) & 1);
     int v = ((f >> 1) & 1) + ((f >> 7) & 1);

@@ -67,32 +67,6 @@ __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
     return c ? a : b;
 }
 
-// Lane conditions as VGPR masks (0 or 0xffffffff) combined with VALU logic and v_bfi selects.
-// Measured on gfx950 with one wave per SIMD: a VALU compare feeding SALU mask logic (s_and_b64
-// of lane masks) or a branch stalls the wave ~14-40 cycles per hop, a v_cndmask reading VCC can
-// take ~14 cycles, while a VALU op issues every ~4.5 cycles; the decoder's step keeps its
-// conditions in VGPRs.  opq() hides a value from the optimiser so it cannot turn the arithmetic
-// back into compares on lane masks.
-__device__ __forceinline__ uint32_t opq(uint32_t v) { asm volatile("" : "+v"(v)); return v; }
-__device__ __forceinline__ uint32_t mbit(uint32_t v, uint32_t k) { return opq((uint32_t)__builtin_amdgcn_sbfe((int32_t)v, k, 1)); }
-__device__ __forceinline__ uint32_t mneg(uint32_t v) { return mbit(v, 31); }   // sign -> mask
-__device__ __forceinline__ uint32_t mlt(uint32_t a, uint32_t b) { return mneg(a - b); }   // a < b (|a - b| < 2^31)
-__device__ __forceinline__ uint32_t mnz(uint32_t v) { return mneg(0u - v); }              // v != 0 (v < 2^31)
-
-__device__ __forceinline__ uint32_t ffbh(uint32_t v) {   // leading zeros, 0xffffffff for 0
-    uint32_t r;
-    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(v));
-    return r;
-}
-__device__ __forceinline__ uint32_t ffbl(uint32_t v) {   // lowest set bit, 0xffffffff for 0
-    uint32_t r;
-    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(v));
-    return r;
-}
-// m ? a : b bitwise (v_bfi_b32 / v_bitop3_b32); m comes from the helpers above, so the optimiser
-// cannot see it as a compare result and turn the select into a VCC select
-__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
-
 // Bytes at or past the block length read as 0xFF (the MQ decoder's end-of-data rule,
 // mqc_dec.cpp BYTEIN).  The host pads every staged block with >= 32 bytes of 0xFF after its
 // data, and windows that start at or past the length read this constant instead, so the
@@ -399,14 +373,26 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
         if (!done && p2 < npasses && k2 < numbps) load_rows(X, WS, k2, t2, 4 * s2);
     }
 
+    // the lane with the most stripe-passes left (the wave lasts as long as it does), wave-uniform
+    auto critical_lane = [&]() -> uint32_t {
+        const uint32_t rem = done ? 0u : (npasses - pidx) * ns - s;
+        uint32_t key = (rem << 6) | (uint32_t)lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, o));
+        return __builtin_amdgcn_readfirstlane(key) & 63;
+    };
     prep_stripe(!done);
+    uint32_t crit_lane = critical_lane();
 
     while (__any(!done)) {
         // ---------------- stripe boundary for parked lanes (batched)
-        const uint32_t nparked = __popcll(__ballot(parked));
+        const uint64_t parkedm = __ballot(parked);
+        const uint32_t nparked = __popcll(parkedm);
         const uint32_t nactive = __popcll(__ballot(!done && !parked));
         uint64_t tev = 0;
-        if (nparked && (nparked >= kpark || nactive == 0)) {
+        // a boundary event runs once kpark lanes wait, or at once when the lane with the most work
+        // left is waiting: the wave's time is that lane's (it used to wait ~9 % of its steps)
+        if (nparked && (nparked >= (kpark & 0xff) || nactive == 0 || ((parkedm >> crit_lane) & (kpark >> 8) & 1))) {
             ++nevents;
             if (TIMING) tev = __builtin_amdgcn_s_memtime();
             // everything the previous event issued has long landed: one explicit wait here
@@ -522,6 +508,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
                 if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[2] += t - tp0; tp0 = t; }
             }
             prep_stripe(switched && !done);
+            crit_lane = critical_lane();
             // stage the next ring bytes (lanes whose fill point moved) and prefetch the next
             // stripe of the lanes that switched (the others keep theirs): no re-reads
             uint64_t tq0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
@@ -748,6 +735,12 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             atomicAdd(&stats[0], (unsigned long long)nstep); atomicAdd(&stats[1], tot);
             atomicMax(&stats[2], (unsigned long long)nstep);
         }
+        if (stats) {   // the busiest lane of the kernel: its decisions, and the steps of its wave
+            unsigned long long mx = nsym;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned long long)__shfl_xor(mx, o));
+            if (lane == 0) atomicMax(&stats[12], (mx << 32) | nstep);
+        }
     }
 }
 
@@ -839,6 +832,9 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     if (kpark < 0) {
         const char* kp = getenv("GK_T1DEC_PARK");   // parked lanes that trigger a stripe boundary
         kpark = kp ? atoi(kp) : 4;
+        // GK_T1DEC_CRIT=0: no event for the lane with the most work left alone (bit 8 of kpark)
+        const char* kc = getenv("GK_T1DEC_CRIT");
+        if (!kc || atoi(kc)) kpark |= 0x100;
     }
     const uint32_t nwaves = (nblocks + 63) / 64, ngroups = (nwaves + DEC_WAVES - 1) / DEC_WAVES;
     const size_t pad = DEC_WAVES * sizeof(Dec2Lds) < 163840 ? 163840 - DEC_WAVES * sizeof(Dec2Lds) : 0;
@@ -853,9 +849,10 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         (void)hipMemcpyAsync(h, stats, 128, hipMemcpyDeviceToHost, st);
         (void)hipStreamSynchronize(st);
         g_last_stats[0] = h[2]; g_last_stats[1] = h[0]; g_last_stats[2] = h[1];
-        fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f events/wave %.0f\n",
+        fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f events/wave %.0f"
+                        " busiest lane %llu decisions in a wave of %llu steps\n",
                 (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]),
-                (double)h[3] / ((nblocks + 63) / 64));
+                (double)h[3] / ((nblocks + 63) / 64), h[12] >> 32, h[12] & 0xffffffffull);
         if (timing)
             fprintf(stderr, "t1dec timing: cycles/event %.0f cycles/step %.0f (event share %.3f)\n",
                     (double)h[4] / (double)(h[3] ? h[3] : 1), (double)h[5] / (double)(h[0] ? h[0] : 1),
