@@ -29,16 +29,25 @@ __device__ __forceinline__ uint32_t win6(uint64_t col, uint32_t s) {
     return (uint32_t)((s ? (col >> (4 * s - 1)) : (col << 1)) & 63u);
 }
 
+// Cross-lane moves through DPP (a few cycles) instead of LDS permutes (~50-cycle round trips,
+// which made the modelling of a stripe a chain of dependent LDS latencies).
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v) {   // lane - 1's value, 0 at lane 0 (wave_shr:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane_next(uint32_t v) {   // lane + 1's value, 0 at lane 63 (wave_shl:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+// exclusive prefix sum over the wave (row_shr 1/2/4/8 within rows of 16, then row_bcast 15 / 31)
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
-    const int lane = threadIdx.x & 63;
-    uint32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(inc, o);
-        if (lane >= o) inc += t;
-    }
-    total = __shfl(inc, 63);
-    return inc - v;
+    int inc = (int)v;
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x111, 0xf, 0xf, false);
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x112, 0xf, 0xf, false);
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x114, 0xf, 0xf, false);
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x118, 0xf, 0xf, false);
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x142, 0xa, 0xf, false);
+    inc += __builtin_amdgcn_update_dpp(0, inc, 0x143, 0xc, 0xf, false);
+    total = (uint32_t)__builtin_amdgcn_readlane(inc, 63);
+    return (uint32_t)inc - v;
 }
 
 // 9-bit neighbourhood pattern (bit0 NW bit1 N bit2 NE bit3 W bit5 E bit6 SW bit7 S bit8 SE) for
@@ -183,9 +192,7 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                 const uint32_t sh = 4 * s;
                 const uint32_t Wc = win6(sig, s), Nc = win6(negcol, s);
                 uint32_t pk = Wc | (Nc << 6);
-                uint32_t pL = __shfl_up(pk, 1), pR = __shfl_down(pk, 1);
-                if (lane == 0) pL = 0;
-                if (lane == 63) pR = 0;
+                const uint32_t pL = lane_prev(pk), pR = lane_next(pk);
                 const uint32_t WL = pL & 63, NL = (pL >> 6) & 63, WR = pR & 63, NR = (pR >> 6) & 63;
                 const uint32_t valid4 = (uint32_t)(validcol >> sh) & 15u;
                 const uint32_t cand = ~(Wc >> 1) & valid4;
@@ -203,8 +210,7 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                 uint32_t cd, in = 0;
                 uint32_t ns = F(0, cd);
                 while (true) {
-                    uint32_t t = __shfl_up(ns, 1);
-                    in = (lane == 0) ? 0u : t;
+                    in = lane_prev(ns);
                     uint32_t cd2, ns2 = F(in, cd2);
                     bool ch = ns2 != ns;
                     ns = ns2; cd = cd2;
@@ -237,9 +243,7 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
             for (uint32_t s = 0; s < nstripes; ++s) {
                 const uint32_t sh = 4 * s;
                 const uint32_t Wc = win6(sig, s);
-                uint32_t pL = __shfl_up(Wc, 1), pR = __shfl_down(Wc, 1);
-                if (lane == 0) pL = 0;
-                if (lane == 63) pR = 0;
+                const uint32_t pL = lane_prev(Wc), pR = lane_next(Wc);
                 const uint32_t nb = ((pL | (pL >> 1) | (pL >> 2)) | (pR | (pR >> 1) | (pR >> 2)) | Wc | (Wc >> 2)) & 15u;
                 const uint32_t mr = (uint32_t)(sigPrev >> sh) & 15u;
                 const uint32_t mu4 = (uint32_t)(mu >> sh) & 15u;
@@ -270,9 +274,7 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
             const uint32_t cl = ~(Wc >> 1) & ~vis4 & valid4;
             const uint32_t nc = cl & bit4;
             uint32_t pk = Wc | (Nc << 6) | (nc << 12);
-            uint32_t pL = __shfl_up(pk, 1), pR = __shfl_down(pk, 1);
-            if (lane == 0) pL = 0;
-            if (lane == 63) pR = 0;
+            const uint32_t pL = lane_prev(pk), pR = lane_next(pk);
             const uint32_t WL = pL & 63, NL = (pL >> 6) & 63, ncL = (pL >> 12) & 15;
             const uint32_t WR = pR & 63, NR = (pR >> 6) & 63;
             const uint32_t Lt = WL | (ncL << 1), CA = Wc | (nc << 1), CB = Wc;
