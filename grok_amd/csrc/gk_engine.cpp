@@ -972,6 +972,9 @@ static inline bool term_pass(uint32_t sty, uint32_t nbp, uint32_t q) {
     return false;
 }
 
+#ifdef PCRD_TRACE
+static std::atomic<uint64_t> g_scans{0}, g_scan_passes{0};
+#endif
 struct T2Enc {
     const Plan& P;
     const uint32_t* info;        // 4 u32 per block: numbps, npasses, bytes, pass offset
@@ -1262,8 +1265,16 @@ struct T2Enc {
     }
     void code_layer(uint32_t l) {   // every (packet, band) of layer l from the snapshot, in parallel
         const auto tc0 = std::chrono::steady_clock::now();
+        // during a bounds_on bisection a unit none of whose counts changed since it was last
+        // coded at this layer keeps its bits, body and coding state (they follow from the counts)
+        const bool skip = skip_clean;
+        if (skip) {
+            cdirty.assign(chains.size(), 0);
+            for (uint32_t u = 0; u < (uint32_t)units.size(); ++u) cdirty[units[u].chain] |= udirty[u];
+        }
         prun(uorder.size(), [&](size_t j) {
             const uint32_t u = uorder[j];
+            if (skip) { if (!udirty[u]) return; udirty[u] = 0; }
             const Unit& U = units[u];
             uint32_t numbps;
             const PrecG& PG = unit_prec(U, &numbps);
@@ -1280,6 +1291,7 @@ struct T2Enc {
         });
         const auto tc2 = std::chrono::steady_clock::now();
         prun(chains.size(), [&](size_t i) {
+            if (skip && !cdirty[i]) return;
             thread_local std::vector<uint64_t> sbuf;
             uint64_t body = 0;
             for (uint32_t u : cunits[i]) body += ubody[u];
@@ -1316,6 +1328,8 @@ struct T2Enc {
         }
     }
     uint64_t prof_code = 0, prof_stuff = 0;   // GK_PROFILE: code_layer phases (us)
+    bool skip_clean = false;
+    std::vector<uint8_t> cdirty;
     bool simulate_layer(uint32_t l, uint64_t max_bytes) {
         if (max_bytes == 0xffffffffull) return true;
         code_layer(l);
@@ -1357,15 +1371,17 @@ struct T2Enc {
         bbits[b] = numpasses_bits(np) + (uint32_t)c + 1 + (uint32_t)(nl + c + floorlog2(np));
         blen[b] = len;
     }
-    void bounds_prep(const std::vector<uint16_t>& prev) {   // once per layer, after the snapshot
+    void bounds_prep(uint32_t l, const std::vector<uint16_t>& prev) {   // once per layer, after the snapshot
         const uint32_t nb = (uint32_t)P.blocks.size();
         if (bbits.size() != nb) { bbits.assign(nb, 0); blen.assign(nb, 0); ccount.assign(nb, 0xffffffffu); }
-        std::fill(ccount.begin(), ccount.end(), 0xffffffffu);
-        tA.resize(P.ntrees); tV.resize(P.ntrees);
+        tA.resize(P.ntrees); tV.resize(P.ntrees); tN.resize(P.ntrees); tC.resize(P.ntrees);
         ubitn.assign(units.size(), 0);
-        for (const Unit& U : units) {
+        ibits.assign(units.size(), 0); ibody.assign(units.size(), 0);
+        udirty.assign(units.size(), 1);
+        prun(uorder.size(), [&](size_t j) {   // units own disjoint trees and blocks
+            const uint32_t u = uorder[j];
             uint32_t bnb;
-            const PrecG& PG = unit_prec(U, &bnb);
+            const PrecG& PG = unit_prec(units[u], &bnb);
             const std::vector<int32_t>& par = incl[PG.tree].parent;
             std::vector<uint8_t>& A = tA[PG.tree];
             A.assign(par.size(), 0);
@@ -1377,7 +1393,41 @@ struct T2Enc {
                 for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) V[k] = bnb - info[4 * (size_t)(PG.first_block + k)];
                 for (size_t n = 0; n < par.size(); ++n) if (par[n] >= 0) V[par[n]] = std::min(V[par[n]], V[n]);
             }
+            // incremental state with no block included at l (see make_layer_inc)
+            tN[PG.tree].assign(par.size(), 0);
+            std::vector<uint32_t>& C = tC[PG.tree];
+            C.assign(par.size(), 0);
+            uint64_t bits = 0;
+            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                const uint32_t b = PG.first_block + k;
+                bits += prev[b] != 0;
+                lnp[(size_t)b * L + l] = 0;
+                ccount[b] = prev[b]; bbits[b] = 0; blen[b] = 0;
+            }
+            for (size_t n = 0; n < par.size(); ++n) {
+                if (A[n]) continue;
+                if (par[n] < 0 || A[par[n]]) bits += 1;
+                if (par[n] >= 0) C[par[n]] += 1;
+            }
+            ibits[u] = bits;
+        });
+        // work chunks: pieces of one unit's blocks, the unit's changes applied under its lock
+        if (chunks.empty())
+            for (uint32_t u = 0; u < (uint32_t)units.size(); ++u) {
+                const uint32_t fb = unit_prec(units[u]).first_block;
+                for (uint32_t k = 0; k < units[u].nblk; k += kChunk)
+                    chunks.push_back({u, fb + k, fb + std::min(units[u].nblk, k + kChunk), {}, {}, 0});
+            }
+        if (ulock.size() != units.size()) ulock = std::vector<std::mutex>(units.size());
+        nact = 0;
+        for (ChunkI& C : chunks) {
+            C.act.resize(C.e - C.s);
+            for (uint32_t b = C.s; b < C.e; ++b) C.act[b - C.s] = b;
+            nact += C.act.size();
         }
+        lay_hash = 0;
+        jlog.clear();
+        if (jstamp.size() != nb) { jstamp.assign(nb, 0); jgen = 0; }
     }
     // -1: the layer's packets overrun max_bytes, 1: they fit, 0: too close to call
     std::vector<uint64_t> clo, chi, cbody;   // per packet: header byte bounds, body bytes
@@ -1422,26 +1472,198 @@ struct T2Enc {
         if (lo > max_bytes || lo - last_body >= max_bytes) return -1;
         return 0;
     }
+    // decide() from the per-unit sums make_layer_inc keeps (same arithmetic, no pass over blocks)
+    int decide_inc(uint64_t max_bytes) {
+        if (max_bytes == 0xffffffffull) return 1;
+        for (uint32_t u = 0; u < (uint32_t)units.size(); ++u) { ubitn[u] = ibits[u]; ubody[u] = ibody[u]; }
+        uint64_t lo = prior, hi = prior, last_body = 0;
+        clo.resize(chains.size()); chi.resize(chains.size()); cbody.resize(chains.size());
+        for (size_t i = 0; i < chains.size(); ++i) {
+            uint64_t R = 1, body = 0;
+            for (uint32_t u : cunits[i]) { R += ibits[u]; body += ibody[u]; }
+            clo[i] = (R + 7) / 8; chi[i] = (R + 6) / 7 + 2; cbody[i] = body;
+            lo += clo[i] + body; hi += chi[i] + body;
+            if (i == last_chain) last_body = body;
+        }
+        if (hi <= max_bytes && hi - last_body < max_bytes) return 1;
+        if (lo > max_bytes || lo - last_body >= max_bytes) return -1;
+        return 0;
+    }
+
+    // ---- incremental bisection (bounds_on layers).  prev[] is fixed while layer l is
+    // bisected and every later threshold lies between the interval's two ends, so a block
+    // whose reuse test (count_at below) holds at both ends keeps its count to the end of
+    // the bisection and leaves the active list.  The rest are recounted per step; a count
+    // that changes updates the hash, the block's cached cost and its unit's header bits and
+    // body bytes, and - when the block enters or leaves the layer with nothing in packets
+    // before - the inclusion tree's per-node counts of such blocks.  A node's count turning
+    // non-zero adds its zero-bit-plane bits (V[n] - V[parent] + 1) and one bit for each
+    // child with no block in packets (decide()'s two tree terms), and the walk stops at the
+    // first ancestor already counting one.  A step is one parallel pass over chunks of a
+    // unit's blocks (recount in parallel; changes applied under the unit's lock, since units
+    // own disjoint trees and sums).
+    // act: blocks whose count may still change; log: this step's changes (block, old count)
+    struct ChunkI { uint32_t u, s, e; std::vector<uint32_t> act, log; uint64_t hd; };
+    static constexpr uint32_t kChunk = 512;
+    std::vector<ChunkI> chunks;
+    std::vector<std::mutex> ulock;               // per unit
+    size_t nact = 0;                             // active blocks over all chunks
+    std::vector<std::vector<uint32_t>> tN, tC;   // per tree node: included new blocks below; children with A == 0
+    std::vector<uint64_t> ibits, ibody;          // per unit: header bits (tag trees + blocks), body bytes
+    std::vector<uint8_t> udirty;                 // per unit: counts changed since it was last coded
+    uint64_t lay_hash = 0, prof_act = 0;
+    void tree_toggle(uint32_t tree, uint32_t k, bool enter, uint64_t& bits) {
+        const std::vector<int32_t>& par = incl[tree].parent;
+        const std::vector<uint8_t>& A = tA[tree];
+        const std::vector<uint32_t>& V = tV[tree];
+        const std::vector<uint32_t>& C = tC[tree];
+        std::vector<uint32_t>& N = tN[tree];
+        for (int32_t n = (int32_t)k; n >= 0 && !A[n]; n = par[n]) {
+            const uint64_t w = (uint64_t)(V[n] - (par[n] < 0 ? 0u : V[par[n]]) + 1) + C[n];
+            if (enter) { if (N[n]++) break; bits += w; }
+            else { if (--N[n]) break; bits -= w; }
+        }
+    }
+    uint64_t make_layer_inc(uint32_t l, double thresh, double lo, double hi, const std::vector<uint16_t>& prev) {
+        prof_act += nact;
+#ifdef PCRD_TRACE
+        fprintf(stderr, "l %u t %.6g [%.6g, %.6g] active %zu\n", l, thresh, lo, hi, nact);
+#endif
+        auto run_chunk = [&](size_t c) {
+            ChunkI& C = chunks[c];
+            C.hd = 0;
+            if (C.act.empty()) return;
+            thread_local std::vector<uint32_t> chg;   // (block, new count) pairs
+            chg.clear();
+            size_t w = 0;
+            const size_t n = C.act.size();
+            for (size_t i = 0; i < n; ++i) {
+                const uint32_t b = C.act[i];
+                // the reuse test holds on an interval: at both ends, for every later threshold
+                // (thresholds <= 0 take count_at's special cases)
+                if (lo > 0 && reusable(b, lo) && reusable(b, hi)) continue;
+                C.act[w++] = b;
+                if (passes && i + PF < n) {
+                    const uint32_t bp = C.act[i + PF];
+                    __builtin_prefetch(passes + info[4 * (size_t)bp + 3] + prev[bp]);
+                }
+                const uint32_t cur = lnp[(size_t)b * L + l], inc = count_at(b, thresh, prev[b], cur);
+                if (inc != prev[b] + cur) { chg.push_back(b); chg.push_back(inc); }
+            }
+            C.act.resize(w);
+            if (chg.empty()) return;
+            const PrecG& PG = unit_prec(units[C.u]);
+            std::lock_guard<std::mutex> lk(ulock[C.u]);
+            uint64_t hd = 0, bits = ibits[C.u], body = ibody[C.u];
+            for (size_t j = 0; j < chg.size(); j += 2) {
+                const uint32_t b = chg[j], inc = chg[j + 1];
+                const uint16_t vo = lnp[(size_t)b * L + l], vn = (uint16_t)(inc - prev[b]);
+                hd += mix64(((uint64_t)b << 16) | vn) - mix64(((uint64_t)b << 16) | vo);
+                C.log.push_back(b); C.log.push_back(vo);
+                if (vo) { bits -= bbits[b]; body -= blen[b]; }
+                block_cost(b, prev[b], inc);
+                if (vn) { bits += bbits[b]; body += blen[b]; }
+                lnp[(size_t)b * L + l] = vn;
+                if (!prev[b] && (vo == 0) != (vn == 0)) tree_toggle(PG.tree, b - PG.first_block, vn != 0, bits);
+            }
+            ibits[C.u] = bits; ibody[C.u] = body; udirty[C.u] = 1;
+            C.hd = hd;
+        };
+        if (nact >= 2048) prun(chunks.size(), run_chunk);
+        else for (size_t c = 0; c < chunks.size(); ++c) run_chunk(c);
+        nact = 0;
+        for (ChunkI& C : chunks) {
+            lay_hash += C.hd; nact += C.act.size();
+            jlog.insert(jlog.end(), C.log.begin(), C.log.end());
+            C.log.clear();
+        }
+        return lay_hash;
+    }
+    // the change journal of this layer's bisection: the counts now equal those when the
+    // journal held pos entries iff every block changed since has its count from then (the
+    // old count of its first change after pos)
+    std::vector<uint32_t> jlog, jstamp;
+    uint32_t jgen = 0;
+    bool same_counts_since(size_t pos, uint32_t l) {
+        if (++jgen == 0) { std::fill(jstamp.begin(), jstamp.end(), 0); jgen = 1; }
+        for (size_t i = pos; i < jlog.size(); i += 2) {
+            const uint32_t b = jlog[i];
+            if (jstamp[b] == jgen) continue;
+            jstamp[b] = jgen;
+            if (lnp[(size_t)b * L + l] != jlog[i + 1]) return false;
+        }
+        return true;
+    }
 
     // makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0) (TileProcessor.cpp:1367-1515),
-    // blocks in parallel.  During one layer's bisection prev[] is fixed, so each block keeps
-    // the threshold its pass count was last computed at (mref) and half the distance from it
-    // to the nearest slope it was compared with (mrad): a threshold closer than that takes
-    // every comparison of the greedy scan the same way, so the count is reused exactly.
+    // blocks in parallel.  During one layer's bisection prev[] is fixed, and a block's greedy
+    // scan is a chain of comparisons thresh - slope < DBL_EPSILON; the scan (so the count)
+    // repeats exactly for every threshold that takes each comparison the same way.  The
+    // floating-point difference is monotone in both operands, so that set is
+    //   thresh - shi < eps  and  !(thresh - slo < eps)
+    // with shi the smallest slope that added passes and slo the largest that did not: the
+    // block keeps (slo, shi) and reuses its count while both hold (vld: they are current).
     // Returns a hash of the layer's pass counts (equal counts => equal simulation outcome).
-    std::vector<double> mref, mrad;
+    std::vector<double> slo, shi;
+    std::vector<uint8_t> vld;
+    static constexpr double kEps = 2.220446049250313e-16;
     static uint64_t mix64(uint64_t x) {
         x += 0x9e3779b97f4a7c15ull;
         x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
         x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
         return x ^ (x >> 31);
     }
+    inline bool reusable(uint32_t b, double t) const { return vld[b] && t - shi[b] < kEps && !(t - slo[b] < kEps); }
+    // block b's pass count (cumulative) at threshold thresh, p0 passes in before this layer,
+    // cur = its current count for the layer (kept while the comparisons repeat)
+    inline uint32_t count_at(uint32_t b, double thresh, uint32_t p0, uint32_t cur) {
+        const uint32_t np = npasses(b);
+        if (thresh < 0) { vld[b] = 0; return std::max<uint32_t>(p0, np); }
+        if (thresh == 0) { vld[b] = 0; return np; }
+        if (reusable(b, thresh)) return p0 + cur;
+        uint32_t inc = p0;
+        double lo = -HUGE_VAL, hi = HUGE_VAL;
+#ifdef PCRD_TRACE
+        g_scans.fetch_add(1, std::memory_order_relaxed); g_scan_passes.fetch_add(np - p0, std::memory_order_relaxed);
+#endif
+        if (passes && np) {
+            // the same arithmetic with the last included pass's rate and distortion in registers
+            // (x - 0 == x exactly, so inc == 0 needs no case of its own)
+            const GkPass* ps = passes + info[4 * (size_t)b + 3];
+            uint32_t rb = p0 ? rate(b, p0 - 1) : 0;
+            double db = p0 ? ps[p0 - 1].dist : 0.0;
+            for (uint32_t q = p0; q < np; ++q) {
+                const uint32_t r = q + 1 == np ? info[4 * (size_t)b + 2] : ps[q].rate;
+                const double d = ps[q].dist;
+                const uint32_t dr = r - rb;
+                const double dd = d - db;
+                if (!dr) { if (dd != 0) { inc = q + 1; rb = r; db = d; } continue; }
+                const double slope = dd / dr;
+                if (thresh - slope < kEps) { inc = q + 1; rb = r; db = d; hi = std::min(hi, slope); }
+                else lo = std::max(lo, slope);
+            }
+            slo[b] = lo; shi[b] = hi; vld[b] = 1;
+            return inc;
+        }
+        for (uint32_t q = p0; q < np; ++q) {
+            uint32_t dr; double dd;
+            if (inc == 0) { dr = rate(b, q); dd = dist(b, q); }
+            else { dr = rate(b, q) - rate(b, inc - 1); dd = dist(b, q) - dist(b, inc - 1); }
+            if (!dr) { if (dd != 0) inc = q + 1; continue; }
+            const double slope = dd / dr;
+            if (thresh - slope < kEps) { inc = q + 1; hi = std::min(hi, slope); }
+            else lo = std::max(lo, slope);
+        }
+        slo[b] = lo; shi[b] = hi; vld[b] = 1;
+        return inc;
+    }
+    void count_state(uint32_t nb) { if (vld.size() != nb) { slo.assign(nb, 0.0); shi.assign(nb, 0.0); vld.assign(nb, 0); } }
     bool bounds = false;      // bisection steps decided by header-size bounds (fast path)
     bool bounds_on = false;   // ... during this layer's bisection (make_layer caches block costs)
     uint64_t make_layer(uint32_t l, double thresh, bool final_attempt, std::vector<uint16_t>& prev) {
         const uint32_t nb = (uint32_t)P.blocks.size();
         const uint32_t chunk = 2048, nch = (b1 - b0 + chunk - 1) / chunk;
-        if (mref.size() != nb) { mref.assign(nb, 0.0); mrad.assign(nb, -1.0); }
+        count_state(nb);
         std::vector<uint64_t> hs(nch, 0);
         prun(nch, [&](size_t ci) {
         uint64_t hsum = 0;
@@ -1449,33 +1671,12 @@ struct T2Enc {
         for (uint32_t b = b0 + (uint32_t)ci * chunk; b < bend; ++b) {
             if (passes && b + PF < bend) __builtin_prefetch(passes + info[4 * (size_t)(b + PF) + 3] + prev[b + PF]);
             if (l == 0) prev[b] = 0;
-            const uint32_t np = npasses(b);
-            uint32_t inc;
-            if (thresh < 0) { inc = std::max<uint32_t>(prev[b], np); mrad[b] = -1.0; }
-            else if (thresh == 0) { inc = np; mrad[b] = -1.0; }
-            else if (mrad[b] > 0 && fabs(thresh - mref[b]) < mrad[b]) inc = prev[b] + lnp[(size_t)b * L + l];
-            else {
-                inc = prev[b];
-                double m = HUGE_VAL;
-                for (uint32_t q = prev[b]; q < np; ++q) {
-                    uint32_t dr; double dd;
-                    if (inc == 0) { dr = rate(b, q); dd = dist(b, q); }
-                    else { dr = rate(b, q) - rate(b, inc - 1); dd = dist(b, q) - dist(b, inc - 1); }
-                    if (!dr) { if (dd != 0) inc = q + 1; continue; }
-                    double slope = dd / dr;
-                    const double diff = thresh - slope;
-                    if (diff < 2.220446049250313e-16) inc = q + 1;
-                    m = std::min(m, fabs(diff));
-                }
-                // reuse only with a radius far above rounding (relative 1e-9) and eps
-                mref[b] = thresh;
-                mrad[b] = (m > 1e-9 * fabs(thresh) && m > 1e-12) ? 0.5 * m : 0.0;
-            }
+            const uint32_t inc = count_at(b, thresh, prev[b], lnp[(size_t)b * L + l]);
             const uint16_t v = (uint16_t)(inc - prev[b]);
             if (bounds_on && ccount[b] != inc) block_cost(b, prev[b], inc);
             lnp[(size_t)b * L + l] = v;
             hsum += mix64(((uint64_t)b << 16) | v);
-            if (final_attempt) { prev[b] = (uint16_t)inc; mrad[b] = -1.0; }
+            if (final_attempt) { prev[b] = (uint16_t)inc; vld[b] = 0; }
         }
         hs[ci] = hsum;
         });
@@ -1549,13 +1750,19 @@ struct T2Enc {
         for (uint32_t l = 0; l < L; ++l) {
             uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
             bounds_on = bounds && rates[l] > 0.0;
-            if (bounds_on) { const auto tp = clk::now(); bounds_prep(prev); t_prep += msd(tp, clk::now()); }
+            if (bounds_on) {
+                const auto tp = clk::now();
+                count_state(nb);
+                bounds_prep(l, prev);
+                t_prep += msd(tp, clk::now());
+            }
             if (rates[l] > 0.0) {
                 double lower = min_slope, prevthresh = -1, thresh = 0;
                 // pass counts equal to those at an end of the bisection interval give that end's
                 // outcome (the simulation depends on nothing else): the simulation is skipped
                 bool has_lo = false, has_hi = false;
                 uint64_t h_lo = 0, h_hi = 0;
+                size_t j_lo = 0, j_hi = 0;   // journal positions of the counts at lower / upper
                 // the hash only nominates a match: the layer's pass counts are compared exactly
                 std::vector<uint16_t> c_lo, c_hi, c_now;
                 auto counts = [&](std::vector<uint16_t>& v) {
@@ -1565,21 +1772,36 @@ struct T2Enc {
                 for (uint32_t it = 0; it < 128; ++it) {
                     thresh = (upper == -1) ? lower : (lower + upper) / 2;
                     const auto t0 = clk::now();
-                    const uint64_t h = make_layer(l, thresh, false, prev);
+                    // every later threshold lies between lower and upper (just lower while upper is unset)
+                    const double hu = upper == -1 ? lower : upper;
+                    const uint64_t h = bounds_on ? make_layer_inc(l, thresh, std::min(lower, hu), std::max(lower, hu), prev)
+                                                 : make_layer(l, thresh, false, prev);
                     const auto t1 = clk::now();
                     t_make += msd(t0, t1);
                     ++n_it;
                     if (prevthresh != -1 && fabs(prevthresh - thresh) < 0.001) break;
                     prevthresh = thresh;
                     bool ok;
-                    if ((has_hi && h == h_hi) || (has_lo && h == h_lo)) counts(c_now);
-                    if (has_hi && h == h_hi && c_now == c_hi) ok = true;
-                    else if (has_lo && h == h_lo && c_now == c_lo) ok = false;
+                    // (bounds_on: the exact compare from the change journal, no count copies)
+                    auto same = [&](const std::vector<uint16_t>& c, size_t pos) {
+                        if (bounds_on) return same_counts_since(pos, l);
+                        counts(c_now);
+                        return c_now == c;
+                    };
+                    if (has_hi && h == h_hi && same(c_hi, j_hi)) ok = true;
+                    else if (has_lo && h == h_lo && same(c_lo, j_lo)) ok = false;
                     else {
-                        const int d = bounds_on ? decide(l, max_len, prev) : 0;
+                        int d = bounds_on ? decide_inc(max_len) : 0;
+                        if (bounds_on && check) {   // debug: the incremental sums must equal a full pass
+                            const std::vector<uint64_t> b0v = ubitn, b1v = ubody;
+                            if (decide(l, max_len, prev) != d || ubitn != b0v || ubody != b1v)
+                                throw GkError("rate-control bounds: incremental layer sums differ");
+                        }
                         if (d && !check) { ok = d > 0; ++n_bound; }
                         else {
+                            skip_clean = bounds_on;
                             ok = fast ? simulate_layer(l, max_len) : simulate(l + 1, max_len);
+                            skip_clean = false;
                             ++n_sim;
                             if (bounds_on && check && max_len != 0xffffffffull) {
                                 for (size_t i = 0; i < chains.size(); ++i)
@@ -1590,20 +1812,39 @@ struct T2Enc {
                         }
                         t_sim += msd(t1, clk::now());
                     }
-                    if (!ok) { lower = thresh; h_lo = h; has_lo = true; counts(c_lo); continue; }
-                    upper = thresh; h_hi = h; has_hi = true; counts(c_hi);
+                    if (!ok) {
+                        lower = thresh; h_lo = h; has_lo = true;
+                        if (bounds_on) j_lo = jlog.size(); else counts(c_lo);
+                        continue;
+                    }
+                    upper = thresh; h_hi = h; has_hi = true;
+                    if (bounds_on) j_hi = jlog.size(); else counts(c_hi);
                 }
-                bounds_on = false;
-                make_layer(l, upper == -1 ? thresh : upper, true, prev);
+                const double fin = upper == -1 ? thresh : upper;
+                if (bounds_on) {   // incrementally too (fin is an end of the interval), then final
+                    const double hu = upper == -1 ? lower : upper;
+                    const auto tm = clk::now();
+                    make_layer_inc(l, fin, std::min(lower, hu), std::max(lower, hu), prev);
+                    for (uint32_t b = b0; b < b1; ++b) { prev[b] = (uint16_t)(prev[b] + lnp[(size_t)b * L + l]); vld[b] = 0; }
+                    t_make += msd(tm, clk::now());
+                } else make_layer(l, fin, true, prev);
                 upper = lower - 1;
             } else {
                 make_layer(l, -1.0, true, prev);
             }
-            if (fast && l + 1 < L) { const auto tf = clk::now(); finish_layer(l); t_fin += msd(tf, clk::now()); }
+            if (fast && l + 1 < L) {
+                const auto tf = clk::now();
+                skip_clean = bounds_on;   // units coded at these counts keep their bits and state
+                finish_layer(l);
+                skip_clean = false;
+                t_fin += msd(tf, clk::now());
+            }
+            bounds_on = false;
         }
         if (prof)
             fprintf(stderr, "pcrd: %u bisection steps, %u simulated, %u decided by bounds; make_layer %.2f ms, simulation %.2f ms, bounds setup %.2f ms, "
-                    "slope range %.2f ms, layer snapshots %.2f ms\n", n_it, n_sim, n_bound, t_make, t_sim, t_prep, t_slopes, t_fin);
+                    "slope range %.2f ms, layer snapshots %.2f ms; %llu block recounts\n", n_it, n_sim, n_bound, t_make, t_sim, t_prep, t_slopes, t_fin,
+                    (unsigned long long)prof_act);
         if (prof)
             fprintf(stderr, "pcrd code_layer: units %.2f ms, packet lengths %.2f ms (%zu units, %zu packets)\n",
                     prof_code / 1e3, prof_stuff / 1e3, units.size(), chains.size());

@@ -376,10 +376,15 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
     // the lane with the most stripe-passes left (the wave lasts as long as it does), wave-uniform
     auto critical_lane = [&]() -> uint32_t {
         const uint32_t rem = done ? 0u : (npasses - pidx) * ns - s;
+        // wave max through DPP (row_shr 1/2/4/8, row_bcast 15/31): lane 63 ends with it
         uint32_t key = (rem << 6) | (uint32_t)lane;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, o));
-        return __builtin_amdgcn_readfirstlane(key) & 63;
+        key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x111, 0xf, 0xf, false));
+        key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x112, 0xf, 0xf, false));
+        key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x114, 0xf, 0xf, false));
+        key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x118, 0xf, 0xf, false));
+        key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x142, 0xa, 0xf, false));
+        key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x143, 0xc, 0xf, false));
+        return (uint32_t)__builtin_amdgcn_readlane((int)key, 63) & 63;
     };
     prep_stripe(!done);
     uint32_t crit_lane = critical_lane();
@@ -831,7 +836,7 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     static int kpark = -1;
     if (kpark < 0) {
         const char* kp = getenv("GK_T1DEC_PARK");   // parked lanes that trigger a stripe boundary
-        kpark = kp ? atoi(kp) : 4;
+        kpark = kp ? atoi(kp) : 16;
         // GK_T1DEC_CRIT=0: no event for the lane with the most work left alone (bit 8 of kpark)
         const char* kc = getenv("GK_T1DEC_CRIT");
         if (!kc || atoi(kc)) kpark |= 0x100;

@@ -1,7 +1,10 @@
 // Host-only timing harness for T2Enc::allocate (PCRD rate control) on the C3 geometry
 // (8192x8192, 3 components, 12-bit, 9/7, 3 layers -r 40,20,10) with synthetic pass
 // records.  No GPU call is made.  Build: tools/pcrd_bench.sh
-#include "../grok_amd/csrc/gk_engine.cpp"
+#ifndef ENGINE_SRC
+#define ENGINE_SRC "../grok_amd/csrc/gk_engine.cpp"
+#endif
+#include ENGINE_SRC
 #include <random>
 
 int main(int argc, char** argv) {
@@ -43,6 +46,9 @@ int main(int argc, char** argv) {
         T2.allocate(200);
         uint64_t h = 0;
         for (size_t i = 0; i < T2.lnp.size(); ++i) h = h * 1000003u + T2.lnp[i];
+#ifdef PCRD_TRACE
+        printf("scans %llu passes %llu\n", (unsigned long long)g_scans.load(), (unsigned long long)g_scan_passes.load());
+#endif
         printf("allocate %.2f ms (layer pass counts hash %016llx)\n",
                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), (unsigned long long)h);
     }
