@@ -1511,7 +1511,8 @@ struct T2Enc {
     std::vector<std::vector<uint32_t>> tN, tC;   // per tree node: included new blocks below; children with A == 0
     std::vector<uint64_t> ibits, ibody;          // per unit: header bits (tag trees + blocks), body bytes
     std::vector<uint8_t> udirty;                 // per unit: counts changed since it was last coded
-    uint64_t lay_hash = 0, prof_act = 0;
+    uint64_t lay_hash = 0, prof_act = 0, prof_npar = 0;
+    double prof_par_ms = 0, prof_ser_ms = 0;
     void tree_toggle(uint32_t tree, uint32_t k, bool enter, uint64_t& bits) {
         const std::vector<int32_t>& par = incl[tree].parent;
         const std::vector<uint8_t>& A = tA[tree];
@@ -1569,8 +1570,13 @@ struct T2Enc {
             ibits[C.u] = bits; ibody[C.u] = body; udirty[C.u] = 1;
             C.hd = hd;
         };
-        if (nact >= 2048) prun(chunks.size(), run_chunk);
+        const auto tp0 = std::chrono::steady_clock::now();
+        const bool par = nact >= 2048;
+        if (par) prun(chunks.size(), run_chunk);
         else for (size_t c = 0; c < chunks.size(); ++c) run_chunk(c);
+        const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();
+        (par ? prof_par_ms : prof_ser_ms) += dt;
+        prof_npar += par;
         nact = 0;
         for (ChunkI& C : chunks) {
             lay_hash += C.hd; nact += C.act.size();
@@ -1843,8 +1849,9 @@ struct T2Enc {
         }
         if (prof)
             fprintf(stderr, "pcrd: %u bisection steps, %u simulated, %u decided by bounds; make_layer %.2f ms, simulation %.2f ms, bounds setup %.2f ms, "
-                    "slope range %.2f ms, layer snapshots %.2f ms; %llu block recounts\n", n_it, n_sim, n_bound, t_make, t_sim, t_prep, t_slopes, t_fin,
-                    (unsigned long long)prof_act);
+                    "slope range %.2f ms, layer snapshots %.2f ms; %llu block recounts, %llu parallel steps %.2f ms, serial %.2f ms\n",
+                    n_it, n_sim, n_bound, t_make, t_sim, t_prep, t_slopes, t_fin,
+                    (unsigned long long)prof_act, (unsigned long long)prof_npar, prof_par_ms, prof_ser_ms);
         if (prof)
             fprintf(stderr, "pcrd code_layer: units %.2f ms, packet lengths %.2f ms (%zu units, %zu packets)\n",
                     prof_code / 1e3, prof_stuff / 1e3, units.size(), chains.size());
@@ -2562,6 +2569,17 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const size_t rc_header_size = H.size() + (P.p.jp2 ? jp2_prefix_size(P) : 0);
     if (!with_header) H.clear();
     const auto te1 = eclk::now();
+    if (const char* ds = getenv("GK_DUMP_SYMS"); ds && dsym && !(P.p.cblk_sty & 0x3f)) {
+        // debug: per-block MQ symbol counts (decisions) and coded bit-planes, u32 pairs
+        std::vector<uint32_t> pe((size_t)GK_MAX_PASSES * nbr), cm(2 * (size_t)nbr), out(2 * (size_t)nbr);
+        HIPCHK(hipMemcpy(pe.data(), dpe, 4 * pe.size(), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(cm.data(), dcm, 4 * cm.size(), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < nbr; ++i) {
+            out[2 * i] = cm[2 * i + 1] ? pe[(size_t)GK_MAX_PASSES * i + cm[2 * i + 1] - 1] : 0;
+            out[2 * i + 1] = cm[2 * i];
+        }
+        if (FILE* f = fopen(ds, "wb")) { fwrite(out.data(), 4, out.size(), f); fclose(f); }
+    }
     if (const char* dp = getenv("GK_DUMP_PASSES")) {   // debug: pass records for tools/pcrd_bench
         if (FILE* f = fopen(dp, "wb")) {
             const uint32_t hdr[2] = {nb, npass_total};

@@ -42,6 +42,7 @@ int main(int argc, char** argv) {
     printf("blocks %u passes %zu\n", nb, passes.size());
     for (int it = 0; it < 5; ++it) {
         T2Enc T2(P, info.data(), passes.data(), 0, 1);
+        T2.serial = getenv("PCRD_SERIAL") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
         T2.allocate(200);
         uint64_t h = 0;
