@@ -22,6 +22,7 @@ __device__ __forceinline__ uint32_t mbit(uint32_t v, uint32_t k) { return opq((u
 __device__ __forceinline__ uint32_t mneg(uint32_t v) { return mbit(v, 31); }   // sign -> mask
 __device__ __forceinline__ uint32_t mlt(uint32_t a, uint32_t b) { return mneg(a - b); }   // a < b (|a - b| < 2^31)
 __device__ __forceinline__ uint32_t mnz(uint32_t v) { return mneg(0u - v); }              // v != 0 (v < 2^31)
+__device__ __forceinline__ uint32_t mz(uint32_t v) { return ~mnz(v); }                     // v == 0 (v < 2^31)
 
 __device__ __forceinline__ uint32_t ffbh(uint32_t v) {   // leading zeros, 0xffffffff for 0
     uint32_t r;

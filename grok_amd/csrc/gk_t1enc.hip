@@ -335,11 +335,15 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
 // Context states live in LDS per lane as their probability-table entry with the
 // MPS in bit 31 (one read gives Qe, NMPS, NLPS and SWITCH; the next entry is
 // written back off the symbol's dependency chain), as in the decoder.
-// Output bytes gather into dwords in a VGPR and the dwords into a 64-byte line per
-// lane in LDS; a full line leaves as four 16-byte stores, so HBM sees whole lines
-// instead of one 4-byte write per lane-dword (scattered over 64 slots).
+// Output bytes gather into dwords in a VGPR; every emission stores the dword it touched into a
+// per-lane 128-byte ring (two 64-byte lines) in LDS, unconditionally (a later store of the same
+// dword supersedes it), and a completed line leaves as four 16-byte stores at the next 16-symbol
+// group boundary (a symbol emits at most two bytes, so a group crosses at most one line end), so
+// HBM sees whole lines instead of one 4-byte write per lane-dword (scattered over 64 slots).
+// Lane conditions are 0 / -1 VGPR values combined with VALU logic (gk_t1_common.h), not compare
+// masks in SGPRs: a compare feeding SALU mask logic stalls a lone wave ~14 cycles per hop.
 // ---------------------------------------------------------------------------
-#define MQ_LINE_DW 16
+#define MQ_RING_DW 32
 struct MqLane {
     uint32_t a, c, ct;
     int32_t bp;
@@ -347,138 +351,109 @@ struct MqLane {
     uint32_t wbuf;
     uint8_t* out;
     uint32_t cap;
-    uint32_t ovf;
+    uint32_t lf;             // first line of the stream not yet stored to HBM
     // context-state updates of the last two symbols, not yet in LDS (cx 19 = none), and the
-    // entry of the next symbol's context read ahead of time (see mq_code4)
+    // entry of the next symbol's context read ahead of time (see mq_code5)
     uint32_t pcx1, pne1, pcx2, pne2, epref;
 };
 struct MqLds {
     uint32_t tab[48];
     uint32_t ctx[20][64];                 // per-lane context states (table entry | MPS << 31); row 19 spare
-    uint32_t line[64][MQ_LINE_DW + 1];    // per-lane output line (row padded: conflict-free columns)
+    uint32_t ring[64][MQ_RING_DW + 1];    // per-lane output ring (row padded: conflict-free columns)
 };
 
-__device__ __forceinline__ uint32_t vsel_e(bool c, uint32_t a, uint32_t b) {
-    uint64_t m = __ballot(c);
-    uint32_t r;
-    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
-    return r;
-}
-
-// the line holding stream bytes [64k, 64k + 64) goes out when its last dword is complete
-__device__ __forceinline__ void mql_line_out(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane, uint32_t first_byte,
-                                             uint32_t ndw) {
-    uint8_t* dst = q.out + first_byte;
-    if (ndw == MQ_LINE_DW) {
+// stream line `li` (64 bytes from the lane's ring) to HBM; only whole lines inside the slot
+__device__ __forceinline__ void mq_line_store(MqLane& q, MqLds& L, int lane, uint32_t li) {
+    const uint32_t o = (li & 1) * 16;
+    uint8_t* dst = q.out + (size_t)li * 64;
+    if ((li + 1) * 64 <= q.cap) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            *(uint4*)(dst + 16 * i) = make_uint4(line[lane][4 * i], line[lane][4 * i + 1], line[lane][4 * i + 2],
-                                                 line[lane][4 * i + 3]);
+            *(uint4*)(dst + 16 * i) = make_uint4(L.ring[lane][o + 4 * i], L.ring[lane][o + 4 * i + 1],
+                                                 L.ring[lane][o + 4 * i + 2], L.ring[lane][o + 4 * i + 3]);
     } else {
-        for (uint32_t i = 0; i < ndw; ++i) *(uint32_t*)(dst + 4 * i) = line[lane][i];
+        for (uint32_t i = 0; i < 16 && li * 64 + 4 * i + 4 <= q.cap; ++i) *(uint32_t*)(dst + 4 * i) = L.ring[lane][o + i];
+    }
+}
+// the lines the stream has passed (at most one per 16-symbol group) go out
+__device__ __forceinline__ void mq_lines_out(MqLane& q, MqLds& L, int lane) {
+    const uint32_t cl = (uint32_t)max(q.bp, 0) >> 6;
+    if (__any(cl > q.lf)) {
+        if (cl > q.lf) { mq_line_store(q, L, lane, q.lf); q.lf++; }
     }
 }
 
-// one completed dword (stream bytes [bp - 3, bp]) into the lane's line; a full line is stored
-__device__ __forceinline__ void mql_dword(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane, bool full, uint32_t wb) {
-    const uint32_t k = ((uint32_t)(q.bp - 3) >> 2) & (MQ_LINE_DW - 1);
-    if (full) line[lane][k] = wb;
-    const bool flush = full & (k == MQ_LINE_DW - 1);
-    if (__any(flush)) {
-        if (flush) mql_line_out(q, line, lane, (uint32_t)(q.bp - 3) & ~63u, MQ_LINE_DW);
-    }
+// byte `cur` to stream position bp where bo (a lane mask), bp advances
+__device__ __forceinline__ void mq_put5(MqLane& q, MqLds& L, int lane, uint32_t bo, uint32_t cur) {
+    const uint32_t bp = (uint32_t)q.bp;
+    const uint32_t put = bo & mlt(bp, q.cap) & ~mneg(bp);
+    const uint32_t wb = q.wbuf | ((cur << (8 * (bp & 3))) & put);
+    L.ring[lane][(bp >> 2) & (MQ_RING_DW - 1)] = wb;
+    q.wbuf = wb & ~(put & mz((bp & 3) ^ 3u));
+    q.bp += (int32_t)(bo & 1u);
 }
-
-__device__ __forceinline__ void mql_emit(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane, uint32_t nb) {
-    if (q.bp >= 0) {
-        if ((uint32_t)q.bp < q.cap) {
-            q.wbuf |= q.cur << (8 * (q.bp & 3));
-            if ((q.bp & 3) == 3) { mql_dword(q, line, lane, true, q.wbuf); q.wbuf = 0; }
-        } else q.ovf = 1;
-    }
-    q.bp++;
-    q.cur = nb & 0xff;
-}
-// BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127), used at the flush only
-__device__ __forceinline__ void mql_byteout(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane) {
-    const bool carry = q.cur != 0xff && (q.c & 0x8000000);
-    const uint32_t cur = q.cur + (carry ? 1u : 0u);
-    const uint32_t c = carry ? (q.c & 0x7ffffff) : q.c;
-    const bool ff = cur == 0xff;
-    const uint32_t nb = ff ? (c >> 20) : (c >> 19);
-    q.cur = cur;
-    q.c = c & (ff ? 0xfffffu : 0x7ffffu);
-    q.ct = ff ? 7u : 8u;
-    mql_emit(q, line, lane, nb);
-}
-
-// Byte emission for the symbol loop: `cur` goes to position bp (bp = -1 is the encoder's
-// dummy byte before the buffer, which the one unsigned compare also excludes; overflow past
-// `cap` is detected from the final bp).  Branch-free except the line store.
-__device__ __forceinline__ void mql_put_sel(MqLane& q, uint32_t (*line)[MQ_LINE_DW + 1], int lane, bool en, uint32_t cur) {
-    const bool put = en & ((uint32_t)q.bp < q.cap);
-    const uint32_t wb = q.wbuf | (put ? cur << (8 * (q.bp & 3)) : 0u);
-    const bool full = put & ((q.bp & 3) == 3);
-    mql_dword(q, line, lane, full, wb);
-    q.wbuf = full ? 0u : wb;
-    q.bp += en ? 1 : 0;
+// BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127) where bo (a lane mask; CT has reached 0 there).
+// The finished byte (cur plus the carry) goes to position bp: into the dword buffer and,
+// unconditionally, into the ring (bp = -1 is the coder's dummy byte before the buffer, and
+// bytes at or past cap are dropped: the final bp reports the overflow).
+__device__ __forceinline__ void mq_byteout5(MqLane& q, MqLds& L, int lane, uint32_t bo, uint32_t& c, uint32_t& ct) {
+    const uint32_t carry = (c >> 27) & 1u & bo & ~mz(q.cur ^ 0xffu);
+    const uint32_t cur = q.cur + carry;
+    c &= ~(carry << 27);
+    const uint32_t ffm = mz(cur ^ 0xffu);
+    const uint32_t nb = (c >> (19u + (ffm & 1u))) & 0xffu;
+    mq_put5(q, L, lane, bo, cur);
+    q.cur = bsel(bo, nb, q.cur);
+    c &= bsel(bo, bsel(ffm, 0xfffffu, 0x7ffffu), ~0u);
+    ct = bsel(bo, 8u - (ffm & 1u), ct);
 }
 
 // CODEMPS / CODELPS + RENORME (Annex C.2.4-C.2.7), branch-free.  With x = (MPS symbol) xor
 // (A - Qe < Qe): the coder adds Qe to C iff x and keeps A - Qe iff x, else A = Qe.
-// RENORME shifts A and C by the whole renormalisation at once (C as 64 bits).  When the byte
-// boundary (CT = 0) falls inside the shift, BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127) runs on
-// C >> e, e = the bits shifted past the boundary; they stay below the new byte, whose CT
-// (8, or 7 after 0xFF) is reduced by e.  A second boundary in one renormalisation (e >= 8)
-// repeats the BYTEOUT (rare; at most two for shifts <= 15: after the first, e <= 14 - 7).
-// One symbol (cx = s >> 1, decision s & 1).  Context states reach LDS two symbols late: the
-// entry of the next symbol's context is read here, right after the update from two symbols back
-// is written, and the next symbol takes the updates of the last two symbols from registers when
-// its context matches.  So neither the context read nor the probability-table read of an update
-// sits on the chain between consecutive symbols (except for back-to-back symbols of one context,
-// which wait for the table read).
-__device__ __forceinline__ void mq_code4(MqLane& q, MqLds& L, int lane, uint32_t s, uint32_t s_next, bool en) {
+// RENORME's n = clz shifts run as at most three straight shifts: up to the byte boundary
+// (CT = 0), BYTEOUT there, then the rest; C stays below 2^28 before a shift of at most CT, so
+// 32 bits hold it.  A second boundary needs n >= CT + 7 (rare; never a third for n <= 15).
+// One symbol (cx = s >> 1, decision s & 1); enm: 0 / -1, the lane has it.
+// Context states reach LDS two symbols late: the entry of the next symbol's context is read
+// here, right after the update from two symbols back is written, and the next symbol takes the
+// updates of the last two symbols from registers when its context matches.  So neither the
+// context read nor the probability-table read of an update sits on the chain between
+// consecutive symbols (except for back-to-back symbols of one context, which wait for the
+// table read).
+__device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t s, uint32_t s_next, uint32_t enm) {
     // bytes past a block's symbols are arbitrary: their context is the spare row 19
-    const uint32_t cx = min(s >> 1, 19u), d = s & 1;
-    const uint32_t e = cx == q.pcx1 ? q.pne1 : (cx == q.pcx2 ? q.pne2 : q.epref);
+    const uint32_t cx = min(s >> 1, 19u);
+    const uint32_t e = bsel(mz(cx ^ q.pcx1), q.pne1, bsel(mz(cx ^ q.pcx2), q.pne2, q.epref));
     L.ctx[q.pcx2][lane] = q.pne2;
     q.epref = L.ctx[min(s_next >> 1, 19u)][lane];
-    const uint32_t mps = e >> 31;
-    const uint32_t qe = e & 0xffff;
+    const uint32_t mpsm = mneg(e), qe = e & 0xffff;
     const uint32_t a1 = q.a - qe;
-    const bool is_mps = mps == d;
-    const bool fast = is_mps & ((a1 & 0x8000) != 0);   // MPS without renormalisation
-    const bool x = is_mps ^ (a1 < qe);
-    const uint32_t nidx = is_mps ? ((e >> 16) & 0x3f) : ((e >> 22) & 0x3f);
-    const uint32_t nmps = is_mps ? mps : (mps ^ ((e >> 28) & 1));
-    const bool upd = en & !fast;
-    const uint32_t ne = L.tab[nidx] | (nmps << 31);
+    const uint32_t ism = ~(mpsm ^ mbit(s, 0));            // the symbol is the MPS
+    const uint32_t fast = ism & mbit(a1, 15);             // MPS without renormalisation
+    const uint32_t x = ism ^ mlt(a1, qe);
+    const uint32_t nidx = bsel(ism, (e >> 16) & 0x3f, (e >> 22) & 0x3f);
+    const uint32_t nmps = bsel(ism, mpsm, mpsm ^ mbit(e, 28));
+    const uint32_t upd = enm & ~fast;
+    const uint32_t ne = L.tab[nidx] | (nmps & 0x80000000u);
     q.pcx2 = q.pcx1; q.pne2 = q.pne1;
-    q.pcx1 = cx; q.pne1 = upd ? ne : e;
-    const uint32_t an = vsel_e(en, x ? a1 : qe, q.a);
-    const uint32_t n = upd ? __clz(an) - 16 : 0u;
+    q.pcx1 = cx; q.pne1 = bsel(upd, ne, e);
+    const uint32_t an = bsel(enm, bsel(x, a1, qe), q.a);
+    const uint32_t n = (ffbh(an) - 16u) & upd;           // an != 0
     q.a = an << n;
-    uint64_t c = (uint64_t)(q.c + ((en & x) ? qe : 0u)) << n;
-    int ct = (int)q.ct - (int)n;
-    auto byteout = [&](bool bo) {
-        const uint32_t sh = bo ? (uint32_t)(-ct) : 0u;
-        const uint32_t carry = (bo & (q.cur != 0xff)) ? (uint32_t)(c >> (27 + sh)) & 1u : 0u;
-        const uint32_t cur = q.cur + carry;
-        c &= ~((uint64_t)carry << (27 + sh));
-        const bool ff = cur == 0xff;
-        const uint32_t nb = (uint32_t)(c >> ((ff ? 20u : 19u) + sh)) & 0xffu;
-        mql_put_sel(q, L.line, lane, bo, cur);
-        q.cur = vsel_e(bo, nb, q.cur);
-        const uint64_t keep = ((uint64_t)(ff ? 0x100000u : 0x80000u) << sh) - 1;
-        c = bo ? (c & keep) : c;
-        ct = bo ? (ff ? 7 : 8) - (int)sh : ct;
-    };
-    // straight-line: some lane of the wave crosses a byte boundary at almost every symbol, and
-    // a loop here costs register copies at its head; a second boundary (shift > CT + 7) is rare
-    byteout(ct <= 0);
-    if (__any(ct <= 0)) byteout(ct <= 0);
-    q.c = (uint32_t)c;
-    q.ct = (uint32_t)ct;
+    uint32_t c = q.c + (qe & enm & x);
+    const uint32_t n1 = min(n, q.ct);
+    uint32_t n2 = n - n1;
+    const bool two = __any(n2 >= 7u);                      // known before the first BYTEOUT
+    c <<= n1;
+    uint32_t ct = q.ct - n1;
+    mq_byteout5(q, L, lane, mz(ct), c, ct);
+    if (two) {
+        const uint32_t n2a = min(n2, ct);
+        c <<= n2a; ct -= n2a; n2 -= n2a;
+        mq_byteout5(q, L, lane, mz(ct), c, ct);
+    }
+    q.c = c << n2;
+    q.ct = ct - n2;
 }
 
 __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t j) {
@@ -527,7 +502,7 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
     double cum = 0.0;
     MqLane q;
     q.a = 0x8000; q.c = 0; q.ct = 12; q.bp = -1; q.cur = 0; q.wbuf = 0; q.out = bytes + B.data_off; q.cap = B.data_cap;
-    q.ovf = 0;
+    q.lf = 0;
     // initial context states (mqc_resetstates): every context at state 0 except ZC0 = 4, AGG = 3, UNI = 46
     for (int c = 0; c < 19; ++c)
         L.ctx[c][lane] = c_mq[c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))];
@@ -540,13 +515,16 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
     auto close_passes = [&](uint32_t i) {
         while (__any(npasses && p < npasses && next_end == i)) {
             if (npasses && p < npasses && next_end == i) {
-                if (p == npasses - 1) {
+                if (p == npasses - 1) {   // FLUSH (Annex C.2.9, mqc_enc.cpp:229-247), C as 32 bits
                     uint32_t tempc = q.c + q.a;
-                    q.c |= 0xffff;
-                    if (q.c >= tempc) q.c -= 0x8000;
-                    q.c <<= q.ct; mql_byteout(q, L.line, lane);
-                    q.c <<= q.ct; mql_byteout(q, L.line, lane);
-                    if (q.cur != 0xff) mql_emit(q, L.line, lane, 0);
+                    uint32_t c32 = q.c | 0xffff;
+                    if (c32 >= tempc) c32 -= 0x8000;
+                    uint32_t c = c32 << q.ct, ct = 0;
+                    mq_byteout5(q, L, lane, ~0u, c, ct);
+                    c <<= ct; ct = 0;
+                    mq_byteout5(q, L, lane, ~0u, c, ct);
+                    q.c = c; q.ct = ct;
+                    if (q.cur != 0xff) { mq_put5(q, L, lane, ~0u, q.cur); q.cur = 0; }
                     P[p].rate = (uint32_t)q.bp;
                 } else {
                     P[p].rate = (uint32_t)q.bp + 5 + (q.ct < 5 ? 1 : 0);
@@ -584,8 +562,7 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
 #pragma unroll
         for (uint32_t j = 0; j < 16; ++j) {
             const uint32_t i = base + j;
-            const bool en = i < nsym;
-            mq_code4(q, L, lane, byte_of(cur4, j), byte_of(j < 15 ? cur4 : nxt4, (j + 1) & 15), en);
+            mq_code5(q, L, lane, byte_of(cur4, j), byte_of(j < 15 ? cur4 : nxt4, (j + 1) & 15), mlt(i, nsym));
             // the prefetch two chunks ahead is issued after the first symbol has consumed this
             // chunk's bytes, so the wait for them does not also wait for the prefetch
             if (j == 0) {
@@ -596,12 +573,15 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
             if (i + 1 == wnext) { close_passes(i + 1); wnext = wave_next_end(); }
         }
         cur4 = nxt4; nxt4 = pre;
+        mq_lines_out(q, L, lane);
     }
     // the partial last line: whole dwords before bp, then the dword holding bp (pending byte)
     if (npasses && q.bp >= 0 && (uint32_t)q.bp < q.cap) {
-        const uint32_t k = ((uint32_t)q.bp >> 2) & (MQ_LINE_DW - 1);
-        L.line[lane][k] = q.wbuf | (q.cur << (8 * (q.bp & 3)));
-        mql_line_out(q, L.line, lane, (uint32_t)q.bp & ~63u, k + 1);
+        const uint32_t bp = (uint32_t)q.bp, cl = bp >> 6;
+        L.ring[lane][(bp >> 2) & (MQ_RING_DW - 1)] = q.wbuf | (q.cur << (8 * (bp & 3)));
+        if (cl > q.lf) mq_line_store(q, L, lane, q.lf);
+        const uint32_t o = (cl & 1) * 16, k = (bp >> 2) & 15;
+        for (uint32_t i = 0; i <= k; ++i) *(uint32_t*)(q.out + (size_t)cl * 64 + 4 * i) = L.ring[lane][o + i];
     }
     if (!has) return;
     if (npasses == 0) { info[4 * b] = 0; info[4 * b + 1] = 0; info[4 * b + 2] = 0; info[4 * b + 3] = 0; return; }
@@ -623,7 +603,7 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
     info[4 * b + 1] = npasses;
     info[4 * b + 2] = P[npasses - 1].rate;
     info[4 * b + 3] = poff;
-    if (q.ovf || (q.bp > 0 && (uint32_t)q.bp > q.cap)) atomicOr(err, 1);
+    if (q.bp > 0 && (uint32_t)q.bp > q.cap) atomicOr(err, 1);
 #undef pe_lds_at
 }
 
