@@ -383,13 +383,15 @@ __device__ __forceinline__ void mq_lines_out(MqLane& q, MqLds& L, int lane) {
     }
 }
 
-// byte `cur` to stream position bp where bo (a lane mask), bp advances
+// byte `cur` to stream position bp where bo (a lane mask), bp advances.  The coder's dummy
+// byte at bp = -1 lands in the top byte of a dword that is dropped (it completes, so the
+// buffer restarts, and its ring slot is rewritten before its line goes out); bytes at or past
+// cap enter the ring but never HBM (line stores stop at cap; the final bp reports overflow).
 __device__ __forceinline__ void mq_put5(MqLane& q, MqLds& L, int lane, uint32_t bo, uint32_t cur) {
     const uint32_t bp = (uint32_t)q.bp;
-    const uint32_t put = bo & mlt(bp, q.cap) & ~mneg(bp);
-    const uint32_t wb = q.wbuf | ((cur << (8 * (bp & 3))) & put);
+    const uint32_t wb = q.wbuf | ((cur << (8 * (bp & 3))) & bo);
     L.ring[lane][(bp >> 2) & (MQ_RING_DW - 1)] = wb;
-    q.wbuf = wb & ~(put & mz((bp & 3) ^ 3u));
+    q.wbuf = wb & ~(bo & mz((bp & 3) ^ 3u));
     q.bp += (int32_t)(bo & 1u);
 }
 // BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127) where bo (a lane mask; CT has reached 0 there).
@@ -423,7 +425,8 @@ __device__ __forceinline__ void mq_byteout5(MqLane& q, MqLds& L, int lane, uint3
 __device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t s, uint32_t s_next, uint32_t enm) {
     // bytes past a block's symbols are arbitrary: their context is the spare row 19
     const uint32_t cx = min(s >> 1, 19u);
-    const uint32_t e = bsel(mz(cx ^ q.pcx1), q.pne1, bsel(mz(cx ^ q.pcx2), q.pne2, q.epref));
+    // (opq on the operands: the optimiser would turn the equality masks back into compares)
+    const uint32_t e = bsel(mz(opq(cx ^ q.pcx1)), q.pne1, bsel(mz(opq(cx ^ q.pcx2)), q.pne2, q.epref));
     L.ctx[q.pcx2][lane] = q.pne2;
     q.epref = L.ctx[min(s_next >> 1, 19u)][lane];
     const uint32_t mpsm = mneg(e), qe = e & 0xffff;
