@@ -90,3 +90,14 @@ static __constant__ uint32_t c_mq[47] = {
     0x0015 | (43u << 16) | (40u << 22), 0x0009 | (44u << 16) | (41u << 22), 0x0005 | (45u << 16) | (42u << 22),
     0x0001 | (45u << 16) | (43u << 22), 0x5601 | (46u << 16) | (46u << 22)};
 
+// The hot coders keep a context as the entry of its (state, MPS) pair: entry 2 s + m =
+// Qe | (2 NMPS + m) << 16 | (2 NLPS + (m ^ SWITCH)) << 23 | m << 31, so both successor entries,
+// MPS bit included, are one table read away and no MPS arithmetic follows the decision (94
+// entries; the initial states of mqc_resetstates are entries 2 s).
+#define MQ_PAIRS 94
+__device__ __forceinline__ uint32_t mq_pair_entry(uint32_t j) {
+    const uint32_t e = c_mq[j >> 1], m = j & 1;
+    return (e & 0xffffu) | ((2 * ((e >> 16) & 0x3f) + m) << 16) | ((2 * ((e >> 22) & 0x3f) + (m ^ ((e >> 28) & 1))) << 23) |
+           (m << 31);
+}
+

@@ -175,42 +175,9 @@ __device__ __forceinline__ void mq2_refill(Mq2& q, bool en) {
     q.nb4 = adv ? (q.nb4 >> 8) : q.nb4;
 }
 
-// DECODE (Annex C.3.2) for context cx, predicated on `en`; needs avail >= 15.
-// DECODE (Annex C.3.2) for context cx, predicated on `en`; needs avail >= 15.
-// Context states live in LDS per lane as their probability-table entry
-// (Qe | NMPS << 16 | NLPS << 22 | SWITCH << 28) with the MPS in bit 31, so one read
-// yields everything the decision needs; the new state's entry is looked up and
-// written back off the decision's dependency chain.
-__device__ __forceinline__ uint32_t mq2_decode(Mq2& q, uint32_t (*ctx)[64], int lane, const uint32_t* tab,
-                                               uint32_t cx, bool en, uint32_t& wb) {
-    const uint32_t e = ctx[cx][lane];
-    const uint32_t mps = e >> 31;
-    const uint32_t qe = e & 0xffff;
-    const uint32_t chi = (uint32_t)(q.c >> 32);
-    const uint32_t a1 = q.a - qe;
-    const bool lower = (chi >> 16) < qe;
-    const bool fast = !lower & ((a1 & 0x8000) != 0);
-    const bool mps_path = lower ^ (a1 >= qe);                // exchange rule
-    const uint32_t d = (fast | mps_path) ? mps : (mps ^ 1);
-    const uint32_t nidx = mps_path ? ((e >> 16) & 0x3f) : ((e >> 22) & 0x3f);
-    const uint32_t nmps = mps_path ? mps : (mps ^ ((e >> 28) & 1));
-    const bool upd = en & !fast;
-    const uint32_t an = en ? (lower ? qe : a1) : q.a;
-    const uint32_t ch = (en & !lower) ? chi - (qe << 16) : chi;
-    const uint32_t ne = tab[nidx] | (nmps << 31);
-    // written back by the caller at the end of the step (unconditionally: a branch would wait
-    // on the table read), so the table read's latency hides behind the step's state updates
-    wb = upd ? ne : e;
-    const uint32_t n = upd ? __clz(an) - 16 : 0u;   // RENORMD: all shifts at once
-    q.a = an << n;
-    q.c = (((uint64_t)ch << 32) | (uint32_t)q.c) << n;
-    q.avail -= n;
-    return d;
-}
-
 struct Dec2Lds {
-    uint32_t tab[48];
-    uint32_t ctx[19][64];            // per-lane context states as table entries (| MPS << 31)
+    uint32_t tab[96];                // (state, MPS) pair entries (mq_pair_entry)
+    uint32_t ctx[19][64];            // per-lane context states as their (state, MPS) pair entries
     uint8_t zc[4][512];
     uint8_t sc[256];                 // index bit0 N-neg 1 N-sig 2 W-neg 3 W-sig 4 E-neg 5 E-sig 6 S-neg 7 S-sig
     uint32_t ring[RING_DW + 1][64];
@@ -256,7 +223,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
     Dec2Lds& Ls = Lw[wv];
     const uint32_t gw = blockIdx.x * DEC_WAVES + wv;          // global wave: 64 slots
     const uint32_t nwaves = (nblocks + 63) / 64;
-    if (lane < 47) Ls.tab[lane] = c_mq[lane];
+    for (int i = lane; i < MQ_PAIRS; i += 64) Ls.tab[i] = mq_pair_entry((uint32_t)i);
     for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
     for (int i = lane; i < 256; i += 64)
         Ls.sc[i] = sc_rule((uint32_t)(((i >> 2) & 0xf) | ((i & 3) << 4) | (i & 0xc0)));
@@ -278,7 +245,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
     for (int i = 0; i < 8; ++i) { Ls.mu[i][lane] = 0; Ls.bt[i][lane] = 0; Ls.pv[i][lane] = 0; }
     // mqc_resetstates (mqc_dec.cpp:121-130): every context at state 0 except ZC0 = 4, AGG = 3, UNI = 46
     for (int c = 0; c < 19; ++c)
-        Ls.ctx[c][lane] = c_mq[c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))];
+        Ls.ctx[c][lane] = mq_pair_entry(2 * (c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))));
     uint32_t nstep = 0, nsym = 0, nevents = 0;
     unsigned long long cyc_ev = 0, cyc_step = 0, cyc_p[6] = {0, 0, 0, 0, 0, 0};
     Mq2 q;
@@ -637,7 +604,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             __builtin_amdgcn_sched_barrier(0);
             // ---- R2: the entry selected by the last decision; DECODE (Annex C.3.2; RENORMD as one shift)
             e = bsel(pend_v, bsel(pend_b, eBp, eAp), e);
-            const uint32_t tM = Ls.tab[(e >> 16) & 0x3f], tL = Ls.tab[(e >> 22) & 0x3f];   // MPS / LPS successors
+            const uint32_t tM = Ls.tab[(e >> 16) & 0x7f], tL = Ls.tab[(e >> 23) & 0x7f];   // MPS / LPS successor pairs
             const uint32_t mps = e >> 31, qe = e & 0xffff;
             const uint32_t chi = (uint32_t)(q.c >> 32);
             const uint32_t a1 = q.a - qe;
@@ -677,7 +644,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             const uint32_t rr = (rlhi << 1) | d;
             const uint32_t nph = bsel(toA, PH_FIND, bsel(mF, bsel(aggm, PH_UNI1, PH_SIGN), bsel(mU1, PH_UNI2, PH_SIGN)));
             const uint32_t consumed = bsel(mF & ~aggm, 1u << r, ((2u << rr) - 1) & mU2);
-            const uint32_t ne = bsel(mpsp, tM | (mps << 31), tL | ((mps ^ ((e >> 28) & 1)) << 31));
+            const uint32_t ne = bsel(mpsp, tM, tL);
             Ls.ctx[cx][lane] = bsel(upd, ne, e);
             // some lane must refill its code register, or fetch a SIGN context after UNI2, before its
             // next decision: decided here so the next step's branch does not wait for the compare

@@ -348,7 +348,6 @@ struct MqLane {
     uint32_t a, c, ct;
     int32_t bp;
     uint32_t cur;
-    uint32_t wbuf;
     uint8_t* out;
     uint32_t cap;
     uint32_t lf;             // first line of the stream not yet stored to HBM
@@ -357,7 +356,7 @@ struct MqLane {
     uint32_t pcx1, pne1, pcx2, pne2, epref;
 };
 struct MqLds {
-    uint32_t tab[48];
+    uint32_t tab[96];                     // (state, MPS) pair entries (mq_pair_entry)
     uint32_t ctx[20][64];                 // per-lane context states (table entry | MPS << 31); row 19 spare
     uint32_t ring[64][MQ_RING_DW + 1];    // per-lane output ring (row padded: conflict-free columns)
 };
@@ -383,16 +382,16 @@ __device__ __forceinline__ void mq_lines_out(MqLane& q, MqLds& L, int lane) {
     }
 }
 
-// byte `cur` to stream position bp where bo (a lane mask), bp advances.  The coder's dummy
-// byte at bp = -1 lands in the top byte of a dword that is dropped (it completes, so the
-// buffer restarts, and its ring slot is rewritten before its line goes out); bytes at or past
-// cap enter the ring but never HBM (line stores stop at cap; the final bp reports overflow).
+// byte `cur` to stream position bp where bo (a lane mask), bp advances.  The byte is stored into
+// the lane's ring unconditionally (one ds_write_b8): where bo is clear it lands at bp, past the
+// stream, and the lane's next byte overwrites it before its line goes out.  The coder's dummy
+// byte at bp = -1 lands in ring byte 127, rewritten by stream byte 127 before line 1 leaves;
+// bytes at or past cap enter the ring but never HBM (line stores stop at cap; the final bp
+// reports the overflow).
 __device__ __forceinline__ void mq_put5(MqLane& q, MqLds& L, int lane, uint32_t bo, uint32_t cur) {
-    const uint32_t bp = (uint32_t)q.bp;
-    const uint32_t wb = q.wbuf | ((cur << (8 * (bp & 3))) & bo);
-    L.ring[lane][(bp >> 2) & (MQ_RING_DW - 1)] = wb;
-    q.wbuf = wb & ~(bo & mz((bp & 3) ^ 3u));
-    q.bp += (int32_t)(bo & 1u);
+    uint8_t* row = reinterpret_cast<uint8_t*>(&L.ring[lane][0]);
+    row[(uint32_t)q.bp & (4 * MQ_RING_DW - 1)] = (uint8_t)cur;
+    q.bp -= (int32_t)bo;
 }
 // BYTEOUT (Annex C.2.6, mqc_enc.cpp:86-127) where bo (a lane mask; CT has reached 0 there).
 // The finished byte (cur plus the carry) goes to position bp: into the dword buffer and,
@@ -415,14 +414,18 @@ __device__ __forceinline__ void mq_byteout5(MqLane& q, MqLds& L, int lane, uint3
 // RENORME's n = clz shifts run as at most three straight shifts: up to the byte boundary
 // (CT = 0), BYTEOUT there, then the rest; C stays below 2^28 before a shift of at most CT, so
 // 32 bits hold it.  A second boundary needs n >= CT + 7 (rare; never a third for n <= 15).
-// One symbol (cx = s >> 1, decision s & 1); enm: 0 / -1, the lane has it.
+// One symbol (cx = s >> 1, decision s & 1).  A lane past its block's last symbol keeps coding
+// (zero bytes: context 0, decision 0) with CT parked at 2^30 by its flush, so it never reaches a
+// BYTEOUT again and its stream position, pending byte and lines stay as the flush left them; A
+// stays a valid interval for any symbol, so no per-symbol "lane has a symbol" mask is needed.
 // Context states reach LDS two symbols late: the entry of the next symbol's context is read
 // here, right after the update from two symbols back is written, and the next symbol takes the
 // updates of the last two symbols from registers when its context matches.  So neither the
 // context read nor the probability-table read of an update sits on the chain between
 // consecutive symbols (except for back-to-back symbols of one context, which wait for the
 // table read).
-__device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t s, uint32_t s_next, uint32_t enm) {
+#define MQ_CT_PARKED (1u << 30)
+__device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t s, uint32_t s_next) {
     // bytes past a block's symbols are arbitrary: their context is the spare row 19
     const uint32_t cx = min(s >> 1, 19u);
     // (opq on the operands: the optimiser would turn the equality masks back into compares)
@@ -434,16 +437,14 @@ __device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t
     const uint32_t ism = ~(mpsm ^ mbit(s, 0));            // the symbol is the MPS
     const uint32_t fast = ism & mbit(a1, 15);             // MPS without renormalisation
     const uint32_t x = ism ^ mlt(a1, qe);
-    const uint32_t nidx = bsel(ism, (e >> 16) & 0x3f, (e >> 22) & 0x3f);
-    const uint32_t nmps = bsel(ism, mpsm, mpsm ^ mbit(e, 28));
-    const uint32_t upd = enm & ~fast;
-    const uint32_t ne = L.tab[nidx] | (nmps & 0x80000000u);
+    // the successor pair entry (MPS bit included): NMPS for the MPS, NLPS (with SWITCH) for the LPS
+    const uint32_t ne = L.tab[bsel(ism, (e >> 16) & 0x7f, (e >> 23) & 0x7f)];
     q.pcx2 = q.pcx1; q.pne2 = q.pne1;
-    q.pcx1 = cx; q.pne1 = bsel(upd, ne, e);
-    const uint32_t an = bsel(enm, bsel(x, a1, qe), q.a);
-    const uint32_t n = (ffbh(an) - 16u) & upd;           // an != 0
+    q.pcx1 = cx; q.pne1 = bsel(fast, e, ne);
+    const uint32_t an = bsel(x, a1, qe);
+    const uint32_t n = ffbh(an) - 16u;                    // an != 0; 0 on the fast path (an = a1 >= 0x8000)
     q.a = an << n;
-    uint32_t c = q.c + (qe & enm & x);
+    uint32_t c = q.c + (qe & x);
     const uint32_t n1 = min(n, q.ct);
     uint32_t n2 = n - n1;
     const bool two = __any(n2 >= 7u);                      // known before the first BYTEOUT
@@ -482,7 +483,7 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
     extern __shared__ uint32_t pe_dyn[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     MqLds& L = Lw[wave];
-    if (lane < 47) L.tab[lane] = c_mq[lane];
+    for (int i = lane; i < MQ_PAIRS; i += 64) L.tab[i] = mq_pair_entry((uint32_t)i);
     // lane slot j = position base + j of `order` (index order without one)
     const uint32_t j = (blockIdx.x * 4 + wave) * nl + lane;
     const bool inr = (uint32_t)lane < nl && j < count;
@@ -504,11 +505,13 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
     const bool rc = (B.flags & 2) != 0;
     double cum = 0.0;
     MqLane q;
-    q.a = 0x8000; q.c = 0; q.ct = 12; q.bp = -1; q.cur = 0; q.wbuf = 0; q.out = bytes + B.data_off; q.cap = B.data_cap;
+    // a lane without passes starts parked (no BYTEOUT ever; cap 0: no line leaves)
+    q.a = 0x8000; q.c = 0; q.ct = npasses ? 12u : MQ_CT_PARKED; q.bp = -1; q.cur = 0; q.out = bytes + B.data_off;
+    q.cap = has ? B.data_cap : 0;
     q.lf = 0;
     // initial context states (mqc_resetstates): every context at state 0 except ZC0 = 4, AGG = 3, UNI = 46
     for (int c = 0; c < 19; ++c)
-        L.ctx[c][lane] = c_mq[c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))];
+        L.ctx[c][lane] = mq_pair_entry(2 * (c == CTX_ZC ? 4 : (c == CTX_AGG ? 3 : (c == CTX_UNI ? 46 : 0))));
     uint32_t maxsym = nsym;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxsym = max(maxsym, (uint32_t)__shfl_xor((int)maxsym, o));
@@ -529,6 +532,7 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
                     q.c = c; q.ct = ct;
                     if (q.cur != 0xff) { mq_put5(q, L, lane, ~0u, q.cur); q.cur = 0; }
                     P[p].rate = (uint32_t)q.bp;
+                    q.ct = MQ_CT_PARKED;   // the block is coded: no BYTEOUT from here on
                 } else {
                     P[p].rate = (uint32_t)q.bp + 5 + (q.ct < 5 ? 1 : 0);
                 }
@@ -565,7 +569,7 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
 #pragma unroll
         for (uint32_t j = 0; j < 16; ++j) {
             const uint32_t i = base + j;
-            mq_code5(q, L, lane, byte_of(cur4, j), byte_of(j < 15 ? cur4 : nxt4, (j + 1) & 15), mlt(i, nsym));
+            mq_code5(q, L, lane, byte_of(cur4, j), byte_of(j < 15 ? cur4 : nxt4, (j + 1) & 15));
             // the prefetch two chunks ahead is issued after the first symbol has consumed this
             // chunk's bytes, so the wait for them does not also wait for the prefetch
             if (j == 0) {
@@ -581,7 +585,7 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
     // the partial last line: whole dwords before bp, then the dword holding bp (pending byte)
     if (npasses && q.bp >= 0 && (uint32_t)q.bp < q.cap) {
         const uint32_t bp = (uint32_t)q.bp, cl = bp >> 6;
-        L.ring[lane][(bp >> 2) & (MQ_RING_DW - 1)] = q.wbuf | (q.cur << (8 * (bp & 3)));
+        reinterpret_cast<uint8_t*>(&L.ring[lane][0])[bp & (4 * MQ_RING_DW - 1)] = (uint8_t)q.cur;
         if (cl > q.lf) mq_line_store(q, L, lane, q.lf);
         const uint32_t o = (cl & 1) * 16, k = (bp >> 2) & 15;
         for (uint32_t i = 0; i <= k; ++i) *(uint32_t*)(q.out + (size_t)cl * 64 + 4 * i) = L.ring[lane][o + i];
