@@ -292,7 +292,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
     // the entries of the two possible next contexts, read by the last step; the next step's R2
     // takes the one its decision selected (pend_b) when that step decided (pend_v)
     uint32_t eAp = 0, eBp = 0;
-    uint32_t pend_v = 0, pend_b = 0, slow = 0, aggm = 0;   // lane masks
+    uint32_t pend_v = 0, pend_b = 0, aggm = 0;   // lane masks
     // First position of column x + 1 or later (the next column with a stripe-start candidate, or
     // x + 1 when propagation gave it rows nn0), given the current column's rows nib0 still to code.
     auto next_position = [&](uint32_t nib0, uint32_t nn0, uint32_t& xA, uint32_t& nibA, uint32_t& nnA) {
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
         if (sel) {
             x = xA; r = rA; nib = nibA; nn = nnA; ph = PH_FIND; agg = aggA; fs = fsA; sce = scA; cx = cxF; e = eF;
             aggm = aggA ? ~0u : 0u;
-            pend_v = 0; slow = 0;
+            pend_v = 0;
             parked = parked || nibA == 0;   // a stripe-pass without candidates ends at once
         }
     };
@@ -528,9 +528,9 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
         uint32_t actm = (!done && !parked) ? ~0u : 0u;
         const uint32_t mSP = mlt(t, 1), mMR = mbit(t, 0), mCL = mbit(t, 1);
         uint32_t parkm = 0;
-        // need: some lane must refill its code register or fetch a SIGN context after UNI2 before
-        // its next decision (computed at the end of the previous step, so the branch does not wait)
-        bool need = __any(((actm != 0) & (q.avail < 16)) | (slow != 0));
+        // need: some lane must refill its code register before its next decision (computed at the
+        // end of the previous step, so the branch does not wait)
+        bool need = __any((actm != 0) & (q.avail < 16));
 #pragma unroll
         for (int us = 0; us < T1DEC_UNROLL; ++us) {
             // ---------------- one decision per active lane.  While it is decoded, the next step's
@@ -543,27 +543,15 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             //   R1 position A, window reads | R2 this decision | R3 windows -> LUT reads |
             //   R4 state updates, context write-back | R5 contexts of A and B, entry reads |
             //   R6 next state (the entry is selected in the next step's R2)
-            // SIGN after UNI2 (a run-length interruption, rare) fetches its context before the step.
+            // SIGN after UNI2 (a run-length interruption) is a B outcome with a fixed context: the
+            // run-length column and its neighbours are insignificant (the aggregation condition),
+            // and so are the rows the run covered, so the sample's sign context is that of an
+            // all-insignificant neighbourhood (SC index 0: context CTX_SC, no sign flip).
             ++nstep;
             if (__builtin_expect(need, 0)) {
                 while (__any((actm != 0) & (q.avail < 16))) {   // a burst of long renormalisations
                     mq2_refill(q, (actm != 0) & (q.avail < 16));
                     q.nb4 = ring_get4(Ls.ring, lane, q.bp);
-                }
-                if (__any(slow != 0)) {   // SIGN at row rr after UNI2: its window, sign context and entry
-                    const uint32_t dxs = (x >> 5) & 1, sxs = x & 31, os = r * 3 + dxs;
-                    const uint32_t fss = (__builtin_amdgcn_alignbit(Ls.sg[os + 1][lane], Ls.sg[os][lane], sxs) & 7) |
-                                         ((__builtin_amdgcn_alignbit(Ls.sg[os + 4][lane], Ls.sg[os + 3][lane], sxs) & 7) << 3) |
-                                         ((__builtin_amdgcn_alignbit(Ls.sg[os + 7][lane], Ls.sg[os + 6][lane], sxs) & 7) << 6);
-                    const uint32_t fns = (__builtin_amdgcn_alignbit(Ls.ng[os + 1][lane], Ls.ng[os][lane], sxs) & 7) |
-                                         ((__builtin_amdgcn_alignbit(Ls.ng[os + 4][lane], Ls.ng[os + 3][lane], sxs) & 7) << 3) |
-                                         ((__builtin_amdgcn_alignbit(Ls.ng[os + 7][lane], Ls.ng[os + 6][lane], sxs) & 7) << 6);
-                    const uint32_t cxs = CTX_SC + (Ls.sc[(fss & 0xaa) | ((fns >> 1) & 0x55)] & 15);
-                    const uint32_t es = Ls.ctx[cxs][lane];
-                    fs = bsel(slow, fss, fs);
-                    cx = bsel(slow, cxs, cx);
-                    e = bsel(slow, es, e);
-                    slow = 0;
                 }
             }
             // ---- R1
@@ -648,7 +636,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             Ls.ctx[cx][lane] = bsel(upd, ne, e);
             // some lane must refill its code register, or fetch a SIGN context after UNI2, before its
             // next decision: decided here so the next step's branch does not wait for the compare
-            need = __any((actm & (mlt(q.avail, 16) | mU2)) != 0);
+            need = __any((actm & mlt(q.avail, 16)) != 0);
             __builtin_amdgcn_sched_barrier(0);
             // ---- R5: the sign, the contexts of A and B and their entries
             const uint32_t negs = sgn & mbit(d ^ (sce >> 4), 0);
@@ -660,7 +648,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             const uint32_t cxM = bsel(mbit(muw, sA), CTX_MAG + 2, bsel(mnz(fsA & 0x1ef), CTX_MAG + 1, CTX_MAG));
             const uint32_t cxF = bsel(mMR, cxM, bsel(aggA, CTX_AGG, CTX_ZC + zcA));
             const uint32_t cxA = bsel(mU1, CTX_UNI, cxF);
-            const uint32_t cxB = bsel(aggm, CTX_UNI, CTX_SC + (sce & 15));
+            const uint32_t cxB = bsel(mU2, CTX_SC, bsel(aggm, CTX_UNI, CTX_SC + (sce & 15)));
             eAp = Ls.ctx[cxA][lane];
             eBp = Ls.ctx[cxB][lane];
             __builtin_amdgcn_sched_barrier(0);
@@ -676,9 +664,8 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             ph = nph;
             const uint32_t np = actm & toA & ~mnz(nibA);   // no position left: the stripe-pass ends
             parkm |= np;
-            cx = bsel(actm, bsel(takeB, cxB, cxA), cx);
-            pend_v = actm & ~mU2; pend_b = takeB;
-            slow = actm & mU2;
+            cx = bsel(actm, bsel(takeB | mU2, cxB, cxA), cx);
+            pend_v = actm; pend_b = takeB | mU2;
             actm &= ~np;
             __builtin_amdgcn_sched_barrier(0);
         }
