@@ -39,7 +39,7 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t v) {   // lowest set bit, 0xff
 __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
 
 
-__device__ __forceinline__ uint8_t zc_rule(uint32_t orient, uint32_t f) {
+__host__ __device__ constexpr uint8_t zc_rule(uint32_t orient, uint32_t f) {
     int h = ((f >> 3) & 1) + ((f >> 5) & 1);
     int v = ((f >> 1) & 1) + ((f >> 7) & 1);
     int d = (f & 1) + ((f >> 2) & 1) + ((f >> 6) & 1) + ((f >> 8) & 1);
@@ -59,7 +59,7 @@ __device__ __forceinline__ uint8_t zc_rule(uint32_t orient, uint32_t f) {
     return 8;
 }
 // returns (ctx offset in 0..4) | (xorbit << 4)
-__device__ __forceinline__ uint8_t sc_rule(uint32_t f) {
+__host__ __device__ constexpr uint8_t sc_rule(uint32_t f) {
     auto c = [&](int sigbit, int negbit) { return ((f >> sigbit) & 1) ? (((f >> negbit) & 1) ? -1 : 1) : 0; };
     int H = c(1, 0) + c(3, 2), V = c(5, 4) + c(7, 6);
     H = H < -1 ? -1 : (H > 1 ? 1 : H);

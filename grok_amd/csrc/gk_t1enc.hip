@@ -50,25 +50,40 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) 
     return (uint32_t)inc - v;
 }
 
-// 9-bit neighbourhood pattern (bit0 NW bit1 N bit2 NE bit3 W bit5 E bit6 SW bit7 S bit8 SE) for
-// stripe row r given the left column (L), centre-above (CA), centre-below (CB), right column (R)
-// 6-bit windows (bit0 = row above the stripe, bit5 = row below).
-__device__ __forceinline__ uint32_t pat9(uint32_t L, uint32_t CA, uint32_t CB, uint32_t R, int r) {
-    return ((L >> r) & 1) | (((CA >> r) & 1) << 1) | (((R >> r) & 1) << 2) | (((L >> (r + 1)) & 1) << 3) |
-           (((R >> (r + 1)) & 1) << 5) | (((L >> (r + 2)) & 1) << 6) | (((CB >> (r + 2)) & 1) << 7) |
-           (((R >> (r + 2)) & 1) << 8);
+// 3x3 neighbourhood of stripe row r in column-major order: bits 0-2 the left column, 3-5 the
+// centre, 6-8 the right one, each as rows r-1, r, r+1 (6-bit column windows: bit0 = the row above
+// the stripe, bit5 = the row below, so row r - 1 + k is window bit r + k).  Three bit-field
+// extracts per row instead of nine single-bit moves; the context tables are built in this order.
+__device__ __forceinline__ uint32_t nb9(uint32_t L, uint32_t C, uint32_t R, int r) {
+    return ((L >> r) & 7u) | (((C >> r) & 7u) << 3) | (((R >> r) & 7u) << 6);
 }
-// sign-context index (bit0 W-neg bit1 W-sig bit2 E-neg bit3 E-sig bit4 N-neg bit5 N-sig bit6 S-neg bit7 S-sig)
-__device__ __forceinline__ uint32_t scidx(uint32_t L, uint32_t NL, uint32_t CA, uint32_t CB, uint32_t NC, uint32_t R,
-                                          uint32_t NR, int r) {
-    uint32_t wv = (L >> (r + 1)) & 1, wn = (NL >> (r + 1)) & 1;
-    uint32_t ev = (R >> (r + 1)) & 1, en = (NR >> (r + 1)) & 1;
-    uint32_t nv = (CA >> r) & 1, nn = (NC >> r) & 1;
-    uint32_t sv = (CB >> (r + 2)) & 1, sn = (NC >> (r + 2)) & 1;
-    return wn | (wv << 1) | (en << 2) | (ev << 3) | (nn << 4) | (nv << 5) | (sn << 6) | (sv << 7);
+// sign-context index from the significance (fs) and sign (fn) neighbourhoods of nb9:
+// bit0 W-neg bit1 W-sig bit2 N-neg bit3 N-sig bit4 S-neg bit5 S-sig bit6 E-neg bit7 E-sig
+__device__ __forceinline__ uint32_t sc8(uint32_t fs, uint32_t fn) { return (fs & 0xaau) | ((fn >> 1) & 0x55u); }
+// table index -> the rule functions' layouts (gk_t1_common.h)
+__host__ __device__ constexpr uint32_t zc_of_nb9(uint32_t i) {
+    return (i & 1u) | (((i >> 3) & 1u) << 1) | (((i >> 6) & 1u) << 2) | (((i >> 1) & 1u) << 3) | (((i >> 4) & 1u) << 4) |
+           (((i >> 7) & 1u) << 5) | (((i >> 2) & 1u) << 6) | (((i >> 5) & 1u) << 7) | (((i >> 8) & 1u) << 8);
 }
+__host__ __device__ constexpr uint32_t sc_of_sc8(uint32_t i) {
+    return (i & 3u) | (((i >> 6) & 3u) << 2) | (((i >> 2) & 3u) << 4) | (((i >> 4) & 3u) << 6);
+}
+// The context tables in nb9 / sc8 order, evaluated at compile time (a block's wave copies its
+// orientation's 768 bytes into LDS instead of evaluating the rules for 768 entries).
+struct alignas(16) CmTabs {
+    uint8_t zc[4][512];
+    uint8_t sc[256];
+};
+constexpr CmTabs make_cm_tabs() {
+    CmTabs t{};
+    for (uint32_t o = 0; o < 4; ++o)
+        for (uint32_t i = 0; i < 512; ++i) t.zc[o][i] = zc_rule(o, zc_of_nb9(i));
+    for (uint32_t i = 0; i < 256; ++i) t.sc[i] = sc_rule(sc_of_sc8(i));
+    return t;
+}
+__constant__ CmTabs c_cm_tabs = make_cm_tabs();
 
-struct CmLds {
+struct alignas(16) CmLds {
     uint8_t zc[512];
     uint8_t sc[256];
 };
@@ -103,8 +118,8 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
     const int lane = threadIdx.x;
     const GkBlock B = blocks[b];
     const uint32_t w = B.w, h = B.h;
-    for (int i = lane; i < 512; i += 64) L.zc[i] = zc_rule(B.orient, (uint32_t)i);
-    for (int i = lane; i < 256; i += 64) L.sc[i] = sc_rule((uint32_t)i);
+    reinterpret_cast<uint2*>(L.zc)[lane] = reinterpret_cast<const uint2*>(c_cm_tabs.zc[B.orient & 3])[lane];
+    reinterpret_cast<uint32_t*>(L.sc)[lane] = reinterpret_cast<const uint32_t*>(c_cm_tabs.sc)[lane];
     // ---- quantise + sign-magnitude (T1Part1.cpp:36-87), column `lane` into registers
     const bool irrev = B.flags & 1;
     uint32_t m[64];
@@ -216,19 +231,21 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                     ns = ns2; cd = cd2;
                     if (!__any(ch)) break;
                 }
-                // symbols
-                const uint32_t Lt = WL | (in << 1), CA = Wc | (ns << 1), CB = Wc;
+                // symbols.  The left column is coded before this one (its new significances count),
+                // the right one after; in this column the rows above r are coded before row r.
+                const uint32_t Lt = WL | (in << 1), Cn = ns << 1;
                 uint32_t cnt = __popc(cd) + __popc(ns);
                 uint32_t total, off = wave_excl_scan(cnt, total);
                 uint8_t* o = S + pos + off;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if ((cd >> r) & 1) {
-                        uint32_t d = (bit4 >> r) & 1;
-                        *o++ = (uint8_t)(((CTX_ZC + L.zc[pat9(Lt, CA, CB, WR, r)]) << 1) | d);
+                        const uint32_t d = (bit4 >> r) & 1;
+                        const uint32_t fs = nb9(Lt, Wc | (Cn & ((2u << r) - 1)), WR, r);
+                        *o++ = (uint8_t)(((CTX_ZC + L.zc[fs]) << 1) | d);
                         if (d) {
-                            uint32_t e = L.sc[scidx(Lt, NL, CA, CB, Nc, WR, NR, r)];
-                            uint32_t sg = (Nc >> (r + 1)) & 1;
+                            const uint32_t e = L.sc[sc8(fs, nb9(NL, Nc, NR, r))];
+                            const uint32_t sg = (Nc >> (r + 1)) & 1;
                             *o++ = (uint8_t)(((CTX_SC + (e & 15)) << 1) | (sg ^ (e >> 4)));
                         }
                     }
@@ -277,7 +294,7 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
             const uint32_t pL = lane_prev(pk), pR = lane_next(pk);
             const uint32_t WL = pL & 63, NL = (pL >> 6) & 63, ncL = (pL >> 12) & 15;
             const uint32_t WR = pR & 63, NR = (pR >> 6) & 63;
-            const uint32_t Lt = WL | (ncL << 1), CA = Wc | (nc << 1), CB = Wc;
+            const uint32_t Lt = WL | (ncL << 1), Cn = nc << 1;
             const bool agg = (valid4 == 15u) && (cl == 15u) && ((Lt | WR | (Wc & 0x21u)) == 0);
             uint32_t rl = nc ? (uint32_t)__ffs(nc) - 1 : 4u;
             uint32_t cnt;
@@ -299,19 +316,21 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
                 if (rl != 4) {
                     *o++ = (uint8_t)((CTX_UNI << 1) | (rl >> 1));
                     *o++ = (uint8_t)((CTX_UNI << 1) | (rl & 1));
-                    uint32_t e = L.sc[scidx(Lt, NL, CA, CB, Nc, WR, NR, (int)rl)];
-                    uint32_t sg = (Nc >> (rl + 1)) & 1;
-                    *o++ = (uint8_t)(((CTX_SC + (e & 15)) << 1) | (sg ^ (e >> 4)));
+                    // the run's column and its neighbours are insignificant, and so are the rows the
+                    // run covered: the sign context of an empty neighbourhood (CTX_SC, no flip)
+                    const uint32_t sg = (Nc >> (rl + 1)) & 1;
+                    *o++ = (uint8_t)((CTX_SC << 1) | sg);
                 }
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if ((codemask >> r) & 1) {
-                    uint32_t d = (bit4 >> r) & 1;
-                    *o++ = (uint8_t)(((CTX_ZC + L.zc[pat9(Lt, CA, CB, WR, r)]) << 1) | d);
+                    const uint32_t d = (bit4 >> r) & 1;
+                    const uint32_t fs = nb9(Lt, Wc | (Cn & ((2u << r) - 1)), WR, r);
+                    *o++ = (uint8_t)(((CTX_ZC + L.zc[fs]) << 1) | d);
                     if (d) {
-                        uint32_t e = L.sc[scidx(Lt, NL, CA, CB, Nc, WR, NR, r)];
-                        uint32_t sg = (Nc >> (r + 1)) & 1;
+                        const uint32_t e = L.sc[sc8(fs, nb9(NL, Nc, NR, r))];
+                        const uint32_t sg = (Nc >> (r + 1)) & 1;
                         *o++ = (uint8_t)(((CTX_SC + (e & 15)) << 1) | (sg ^ (e >> 4)));
                     }
                 }
