@@ -137,7 +137,9 @@ __global__ __launch_bounds__(256) void k_dc_inv(const int32_t* __restrict__ in, 
 // never makes a separate pass through HBM.
 // =============================================================================
 #define DWT_TW 128
+#ifndef DWT_TH
 #define DWT_TH 32
+#endif
 #define DWT_LW (DWT_TW + 3)
 #define DWT_LH (DWT_TH + 3)
 typedef int32_t Lds53[DWT_LH][DWT_LW + 1];
@@ -257,15 +259,18 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
 // Level 1 from the caller's planes: DC shift (TileProcessor.cpp:506-535) and, for NC = 3,
 // the RCT (mct.cpp:99-146) on load; outputs into the level-1 planes of the NC components
 // (dst + c * cstride).  One LDS tile: Y is transformed first while each thread keeps the U
-// and V of its input positions in registers (19 slots), then U, then V go through the same
-// tile, so a workgroup needs 18 KB of LDS, not 55 (occupancy).
-#define L1_SLOTS 19
+// and V of its input positions in registers (L1_SLOTS), then U, then V go through the same
+// tile, so a workgroup needs one LDS tile instead of three (occupancy).
+#define L1_ROWS ((DWT_LH + 3) / 4)                   // tile rows per thread (4 waves, interior)
+#define L1_SLOTS (2 * L1_ROWS + 1)                  // two columns per row + one halo column slot
+#define L1_EDGE ((DWT_LH * DWT_LW + 255) / 256)     // positions per thread on edge tiles
+static_assert(L1_EDGE <= L1_SLOTS, "edge-tile positions fit the register slots");
 template <class F>   // f(slot, ly, lx, gy, gx): the positions of fwd53_fill, slot = compile-time index
 __device__ __forceinline__ void fwd53_fill_slots(int x0, int y0, int w, int h, int tid, F f) {
     const int tx = tid & 63, ty = tid >> 6;
     if (x0 >= 2 && y0 >= 2 && x0 + DWT_TW < w && y0 + DWT_TH < h) {
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
+        for (int k = 0; k < L1_ROWS; ++k) {
             const int ly = ty + 4 * k;
             if (ly < DWT_LH) {
                 const int gy = y0 - 2 + ly;
@@ -275,11 +280,11 @@ __device__ __forceinline__ void fwd53_fill_slots(int x0, int y0, int w, int h, i
         }
         if (tid < 3 * DWT_LH) {
             const int ly = tid / 3, lx = 128 + tid % 3;
-            f(18, ly, lx, y0 - 2 + ly, x0 - 2 + lx);
+            f(2 * L1_ROWS, ly, lx, y0 - 2 + ly, x0 - 2 + lx);
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 18; ++k) {   // 18 x 256 >= 35 x 131
+        for (int k = 0; k < L1_EDGE; ++k) {
             const int i = tid + 256 * k;
             if (i < DWT_LH * DWT_LW) {
                 const int ly = i / DWT_LW, lx = i % DWT_LW;
@@ -424,7 +429,7 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
 // Last inverse level into the caller's planes: inverse RCT for NC = 3 (mct.cpp:221-283),
 // DC shift and clamp (TileProcessor.cpp:457-504), samples of type TO, only inside the
 // output window (region coordinates [wx0, wx1) x [wy0, wy1); out.p[c] addresses (wx0, wy0)).
-// One LDS tile: the Y and U results of each thread's 16 output samples wait in registers
+// One LDS tile: the Y and U results of each thread's DWT_TH / 2 output samples wait in registers
 // while the next component goes through the tile.
 template <class TO, int NC>
 __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict__ src, uint64_t cstride, uint32_t sstride,
@@ -437,7 +442,7 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
     tb.origin(tile, ox, oy);
     const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
     const int tx = tid & 63, ty = tid >> 6;
-    int32_t R0[16], R1[16];   // this thread's samples (ry = ty + 4 (k >> 1), column tx + 64 (k & 1))
+    int32_t R0[DWT_TH / 2], R1[DWT_TH / 2];   // this thread's samples (ry = ty + 4 (k >> 1), column tx + 64 (k & 1))
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         if (c) LDS_BARRIER();   // the previous component's samples have been read
@@ -448,7 +453,7 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
         inv53_lift(T, (int)w, (int)h, tid);
         if (c + 1 < NC) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) (c == 0 ? R0 : R1)[k] = T[ty + 4 * (k >> 1) + 1][tx + 64 * (k & 1) + 1];
+            for (int k = 0; k < DWT_TH / 2; ++k) (c == 0 ? R0 : R1)[k] = T[ty + 4 * (k >> 1) + 1][tx + 64 * (k & 1) + 1];
         }
     }
     TO* o0 = (TO*)out.p[0];
@@ -456,7 +461,7 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
     TO* o2 = (TO*)out.p[NC == 3 ? 2 : 0];
     auto cl = [&](int32_t v) { return (TO)(v < mn ? mn : (v > mx ? mx : v)); };
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < DWT_TH / 2; ++k) {
         const int ry = ty + 4 * (k >> 1), cx = tx + 64 * (k & 1);
         const int gy = y0 + ry, Y = oy + gy, gx = x0 + cx, X = ox + gx;
         if (gy >= (int)h || gx >= (int)w || Y < win.y0 || Y >= win.y1 || X < win.x0 || X >= win.x1) continue;
