@@ -208,7 +208,8 @@ __device__ __forceinline__ uint64_t h_get(uint32_t (*g)[64], int row, int lane) 
 
 // TIMING (diagnostic build, GK_T1_STATS=2): shader-clock cycles spent in stripe-boundary
 // events vs decision steps, summed into stats[4] / stats[5].
-template <bool TIMING>
+// MODE 0: decode; 1: also count decisions per lane (GK_T1_STATS); 2: also time events (=2).
+template <int MODE>
 // A workgroup is DEC_WAVES independent waves (one per SIMD) and the launch pads its LDS to the
 // CU's 160 KiB, so every decoding wave has its SIMD to itself (single waves per workgroup were
 // placed two to a SIMD on some CUs while other SIMDs idled).
@@ -218,6 +219,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
                                                 const uint32_t* __restrict__ order, uint64_t* __restrict__ scratch,
                                                 const uint64_t* __restrict__ wave_off, uint32_t nblocks,
                                                 unsigned long long* __restrict__ stats, uint32_t kpark) {
+    constexpr bool TIMING = MODE == 2, STATS = MODE >= 1;
     __shared__ Dec2Lds Lw[DEC_WAVES];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     Dec2Lds& Ls = Lw[wv];
@@ -276,7 +278,10 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
     // candidates.
     uint32_t nr = min(4u, h), x = 0xffffffffu, r = 0, ph = PH_FIND, rlhi = 0, nib = 0, nn = 0;
     uint32_t vr = (1u << nr) - 1;                 // valid rows of the stripe
-    uint64_t C0, C1, C2, C3, CU, E, fresh = 0;    // candidate rows, their union, run-length columns
+    uint64_t C0, C1, C2, C3, CU, E;               // candidate rows, their union, run-length columns
+    // lane masks: this stripe-pass set a bit in the plane's rows (write-back needed); the current
+    // column gained a significance in this pass (a run-length test of the next column)
+    uint32_t dirty = 0, colsig = 0;
     {
         const uint64_t v0 = nr > 0 ? colmask : 0, v1 = nr > 1 ? colmask : 0, v2 = nr > 2 ? colmask : 0,
                        v3 = nr > 3 ? colmask : 0;
@@ -402,11 +407,11 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
                 const uint64_t B0 = h_get(Ls.bt, 0, lane), B1 = h_get(Ls.bt, 1, lane), B2 = h_get(Ls.bt, 2, lane),
                                B3 = h_get(Ls.bt, 3, lane);
                 late = ns > 3;
-                // rows a stripe-pass left unchanged are not stored: `fresh` marks the columns that
-                // gained a 1 bit in this plane's bit rows (a new significance in SP / CL, a
-                // refinement 1 in MR); scratch starts zero-filled and SP is the first pass to touch
-                // a plane's bit rows
-                wdirty = fresh != 0;
+                // rows a stripe-pass left unchanged are not stored: `dirty` marks a stripe-pass that
+                // set a 1 bit in this plane's bit rows (a new significance in SP / CL, a refinement
+                // 1 in MR); scratch starts zero-filled and SP is the first pass to touch a plane's
+                // bit rows
+                wdirty = dirty != 0;
                 W0 = S1; W1 = S2; W2 = S3; W3 = S4; W4 = N1; W5 = N2; W6 = N3; W7 = N4;
                 WB0 = B0; WB1 = B1; WB2 = B2; WB3 = B3;
                 const uint64_t P0 = h_get(Ls.pv, 0, lane), P1 = h_get(Ls.pv, 1, lane), P2 = h_get(Ls.pv, 2, lane),
@@ -476,7 +481,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
                     uint64_t* mup = WS + 4 * ny0 + WS_M;
                     st2(mup, WM0, WM1); st2(mup + 2, WM2, WM3);
                 }
-                fresh = 0; nn = 0; ph = PH_FIND;
+                dirty = 0; colsig = 0; nn = 0; ph = PH_FIND;
                 if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[2] += t - tp0; tp0 = t; }
             }
             prep_stripe(switched && !done);
@@ -567,7 +572,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             const uint32_t cb = ((t3 << r) >> 1) & vr & spn & mlt(gx, w);
             const uint32_t nib0 = bsel(mF, nib & ~(1u << r) & ~aggm, nib | ca);
             const uint32_t nn0 = nn | cb;
-            const uint64_t fresh0 = fresh | ((uint64_t)(sgn & 1) << (x & 63));
+            const uint32_t cs0 = colsig | sgn;
             // next position: the current column's next row, else x + 1 (propagated rows) or the
             // next column with a stripe-start candidate
             const uint32_t x1 = x + 1;
@@ -607,7 +612,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             q.a = an << nsh;
             q.c = (((uint64_t)ch << 32) | (uint32_t)q.c) << nsh;
             q.avail -= nsh;
-            nsym += actm & 1;
+            if (STATS) nsym += actm & 1;
             __builtin_amdgcn_sched_barrier(0);
             // ---- R3: windows -> LUT reads (zero coding of A, sign context of the current position)
             const uint32_t fsA = (__builtin_amdgcn_alignbit(g0b, g0a, sA) & 7) | ((__builtin_amdgcn_alignbit(g1b, g1a, sA) & 7) << 3) |
@@ -624,7 +629,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             const uint32_t dx0 = (x >> 5) & 1, bx = 1u << (x & 31);
             atomicOr(&Ls.bt[r * 2 + dx0][lane], bx & pb);
             atomicOr(&Ls.pv[r * 2 + dx0][lane], bx & actm & mF & mSP);
-            fresh |= (uint64_t)(pb & 1) << (x & 63);
+            dirty |= pb;
             // next state: FIND at A after a 0 (FIND), always after MR and SIGN; SIGN after a ZC 1;
             // UNI1 after a run-length 1; UNI2 after UNI1; SIGN at row 2 rlhi + d after UNI2
             const uint32_t takeB = mF & ~mMR & md;
@@ -642,9 +647,10 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             const uint32_t negs = sgn & mbit(d ^ (sce >> 4), 0);
             atomicOr(&Ls.ng[(r + 1) * 3 + gd][lane], gb & negs);
             // a column starts in run-length mode when it was eligible at stripe start, is untouched
-            // and its left neighbour column gained no significance in this pass
-            const uint32_t aggA = mCL & mbit((uint32_t)(E >> XA), 0) & mbit(nibA + 1, 4) &
-                                  ~mbit((uint32_t)((fresh0 << 1) >> XA), 0);
+            // and its left neighbour column gained no significance in this pass.  A run-length
+            // column is a new column (nibA = all rows), and the columns between this one and it
+            // had no candidates, so only this column (the neighbour iff XA = x + 1) can have gained one
+            const uint32_t aggA = mCL & mbit((uint32_t)(E >> XA), 0) & mbit(nibA + 1, 4) & ~(cs0 & mz(XA ^ gx));
             const uint32_t cxM = bsel(mbit(muw, sA), CTX_MAG + 2, bsel(mnz(fsA & 0x1ef), CTX_MAG + 1, CTX_MAG));
             const uint32_t cxF = bsel(mMR, cxM, bsel(aggA, CTX_AGG, CTX_ZC + zcA));
             const uint32_t cxA = bsel(mU1, CTX_UNI, cxF);
@@ -655,6 +661,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             // ---- R6: next state (lanes that did not decide keep cx / e and are parked or done, so
             // their other fields are rebuilt at the next stripe boundary)
             fs = bsel(toA, fsA, fs);
+            colsig = cs0 & ~(toA & mnz(xA ^ x));   // a new column has gained nothing yet
             aggm = bsel(toA, aggA, aggm);
             x = bsel(toA, xA, x);
             r = bsel(toA, rA, bsel(mU2, rr, r));
@@ -798,11 +805,14 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     const uint32_t nwaves = (nblocks + 63) / 64, ngroups = (nwaves + DEC_WAVES - 1) / DEC_WAVES;
     const size_t pad = DEC_WAVES * sizeof(Dec2Lds) < 163840 ? 163840 - DEC_WAVES * sizeof(Dec2Lds) : 0;
     if (timing)
-        hipLaunchKernelGGL(k_t1_dec2<true>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order, scratch,
+        hipLaunchKernelGGL(k_t1_dec2<2>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order, scratch,
                            wave_off, nblocks, stats, (uint32_t)kpark);
+    else if (want)
+        hipLaunchKernelGGL(k_t1_dec2<1>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order,
+                           scratch, wave_off, nblocks, stats, (uint32_t)kpark);
     else
-        hipLaunchKernelGGL(k_t1_dec2<false>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order,
-                           scratch, wave_off, nblocks, want ? stats : nullptr, (uint32_t)kpark);
+        hipLaunchKernelGGL(k_t1_dec2<0>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order,
+                           scratch, wave_off, nblocks, nullptr, (uint32_t)kpark);
     if (want) {
         unsigned long long h[16];
         (void)hipMemcpyAsync(h, stats, 128, hipMemcpyDeviceToHost, st);

@@ -370,9 +370,9 @@ struct MqLane {
     uint8_t* out;
     uint32_t cap;
     uint32_t lf;             // first line of the stream not yet stored to HBM
-    // context-state updates of the last two symbols, not yet in LDS (cx 19 = none), and the
-    // entry of the next symbol's context read ahead of time (see mq_code5)
-    uint32_t pcx1, pne1, pcx2, pne2, epref;
+    // context-state update of the last symbol, not yet in LDS (cx 19 = none), and the entry of
+    // the next symbol's context read ahead of time (see mq_code5)
+    uint32_t pcx1, pne1, epref;
 };
 struct MqLds {
     uint32_t tab[96];                     // (state, MPS) pair entries (mq_pair_entry)
@@ -437,19 +437,18 @@ __device__ __forceinline__ void mq_byteout5(MqLane& q, MqLds& L, int lane, uint3
 // (zero bytes: context 0, decision 0) with CT parked at 2^30 by its flush, so it never reaches a
 // BYTEOUT again and its stream position, pending byte and lines stay as the flush left them; A
 // stays a valid interval for any symbol, so no per-symbol "lane has a symbol" mask is needed.
-// Context states reach LDS two symbols late: the entry of the next symbol's context is read
-// here, right after the update from two symbols back is written, and the next symbol takes the
-// updates of the last two symbols from registers when its context matches.  So neither the
-// context read nor the probability-table read of an update sits on the chain between
-// consecutive symbols (except for back-to-back symbols of one context, which wait for the
-// table read).
+// Context states reach LDS one symbol late: the entry of the next symbol's context is read
+// here, right after the previous symbol's update is written, and the next symbol takes this
+// symbol's update from registers when its context matches.  So neither the context read nor
+// the probability-table read of an update sits on the chain between consecutive symbols
+// (except for back-to-back symbols of one context, which wait for the table read).
 #define MQ_CT_PARKED (1u << 30)
 __device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t s, uint32_t s_next) {
     // bytes past a block's symbols are arbitrary: their context is the spare row 19
     const uint32_t cx = min(s >> 1, 19u);
     // (opq on the operands: the optimiser would turn the equality masks back into compares)
-    const uint32_t e = bsel(mz(opq(cx ^ q.pcx1)), q.pne1, bsel(mz(opq(cx ^ q.pcx2)), q.pne2, q.epref));
-    L.ctx[q.pcx2][lane] = q.pne2;
+    const uint32_t e = bsel(mz(opq(cx ^ q.pcx1)), q.pne1, q.epref);
+    L.ctx[q.pcx1][lane] = q.pne1;                         // the previous symbol's update
     q.epref = L.ctx[min(s_next >> 1, 19u)][lane];
     const uint32_t mpsm = mneg(e), qe = e & 0xffff;
     const uint32_t a1 = q.a - qe;
@@ -458,7 +457,6 @@ __device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t
     const uint32_t x = ism ^ mlt(a1, qe);
     // the successor pair entry (MPS bit included): NMPS for the MPS, NLPS (with SWITCH) for the LPS
     const uint32_t ne = L.tab[bsel(ism, (e >> 16) & 0x7f, (e >> 23) & 0x7f)];
-    q.pcx2 = q.pcx1; q.pne2 = q.pne1;
     q.pcx1 = cx; q.pne1 = bsel(fast, e, ne);
     const uint32_t an = bsel(x, a1, qe);
     const uint32_t n = ffbh(an) - 16u;                    // an != 0; 0 on the fast path (an = a1 >= 0x8000)
@@ -581,7 +579,7 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
     uint4 cur4 = make_uint4(0, 0, 0, 0), nxt4 = make_uint4(0, 0, 0, 0);
     if (nsym) cur4 = *(const uint4*)(sp);
     if (nsym > 16) nxt4 = *(const uint4*)(sp + 16);
-    q.pcx1 = q.pcx2 = 19; q.pne1 = q.pne2 = 0;
+    q.pcx1 = 19; q.pne1 = 0;
     q.epref = L.ctx[min(byte_of(cur4, 0) >> 1, 19u)][lane];
     for (uint32_t base = 0; base < maxsym; base += 16) {
         uint4 pre = make_uint4(0, 0, 0, 0);

@@ -22,7 +22,7 @@ def count(src):
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
                                "-I", os.path.dirname(src), src, "-o", out])
         lines = open(out).read().split("\n")
-    s = next(i for i, l in enumerate(lines) if re.match(r"^_Z9k_t1_dec2ILb0EE.*:", l))
+    s = next(i for i, l in enumerate(lines) if re.match(r"^_Z9k_t1_dec2IL(?:b0|i0)EE.*:", l))
     e = next(i for i in range(s, len(lines)) if lines[i].startswith(".Lfunc_end"))
     blocks, cur = [], None
     for l in lines[s:e]:
