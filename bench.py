@@ -45,7 +45,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
 CLOCK_GHZ = 2.4            # MI355X max engine clock (MI355X_MICROARCH.md)
-DEC_INSTR_PER_STEP = 276   # k_t1_dec2 decision step, gfx950 ISA (python tools/isa_step_count.py)
+DEC_INSTR_PER_STEP = 273   # k_t1_dec2 decision step, gfx950 ISA (python tools/isa_step_count.py)
 METRIC = "Mpixels/s encode+decode, 8K RGB 5/3 lossless + 9/7 lossy, 1/2/4/8 GPU"
 # Grok 9.2.0 on the survey container (8 vCPU), enc+dec Mpix/s
 GROK_CPU = {"C2p_8t": 5.99, "C2p_1t": 1.11, "C3p_8t": 2.87, "C3p_1t": 0.93, "C4_8t": 51.9, "C4_1t": 19.3,
@@ -602,7 +602,7 @@ def main():
         # events on the engine stream (encode: k_t1_cm + k_t1_mq, decode: k_t1_dec2 + k_t1_recon)
         stages = {
             "T1 decode (k_t1_dec2 + k_t1_recon)": (m["dec_t1_ms"], m["dec_t1_bytes"] + 4.0 * samples,
-                                                   ["void k_t1_dec2<false>", "k_t1_recon"]),
+                                                   ["void k_t1_dec2<0>", "k_t1_recon"]),
             "T1 encode (k_t1_cm + k_t1_mq)": (m["enc_t1_ms"], 4.0 * samples + m["enc_t1_bytes"],
                                               ["void k_t1_cm<false>", "k_t1_mq"]),
             "DWT 5/3 fwd+inv (all levels)": (m["enc_dwt_ms"] + m["dec_dwt_ms"], m["enc_dwt_bytes"] + m["dec_dwt_bytes"],

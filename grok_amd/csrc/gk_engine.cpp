@@ -2482,16 +2482,21 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         // still being modelled.  An MQ workgroup fills its CU's LDS, so the modelling waves never
         // share a SIMD with an MQ chain (sharing one slowed the chains more than the overlap
         // gained).  Each block is coded exactly as in one pass; only the launch order changes.
-        uint8_t* dw = (uint8_t*)ctx->dweight.get(nbr);
+        uint32_t* dw = (uint32_t*)ctx->dweight.get(4 * (size_t)nbr);
         gk_launch_t1_weight(st, arena, dblk, dw, nbr);
-        uint8_t* hw = (uint8_t*)ctx->hweight.get(nbr);
-        HIPCHK(hipMemcpyAsync(hw, dw, nbr, hipMemcpyDeviceToHost, st));
+        uint32_t* hw = (uint32_t*)ctx->hweight.get(4 * (size_t)nbr);
+        HIPCHK(hipMemcpyAsync(hw, dw, 4 * (size_t)nbr, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        uint32_t start[34] = {0};
-        for (uint32_t i = 0; i < nbr; ++i) start[32 - std::min<uint32_t>(hw[i], 32)]++;   // descending weight
-        for (uint32_t k = 0, acc = 0; k < 34; ++k) { const uint32_t c = start[k]; start[k] = acc; acc += c; }
+        // counting sort, descending, on the estimate quantised to 4096 buckets of the range
+        uint32_t wmax = 1;
+        for (uint32_t i = 0; i < nbr; ++i) wmax = std::max(wmax, hw[i]);
+        const uint32_t kB = 4096;
+        auto key = [&](uint32_t i) { return kB - 1 - (uint32_t)(((uint64_t)hw[i] * (kB - 1)) / wmax); };
+        std::vector<uint32_t> start(kB + 1, 0);
+        for (uint32_t i = 0; i < nbr; ++i) start[key(i)]++;
+        for (uint32_t k = 0, acc = 0; k <= kB; ++k) { const uint32_t c = start[k]; start[k] = acc; acc += c; }
         uint32_t* ho = (uint32_t*)ctx->hord_enc.get(4 * (size_t)nbr);
-        for (uint32_t i = 0; i < nbr; ++i) ho[start[32 - std::min<uint32_t>(hw[i], 32)]++] = i;
+        for (uint32_t i = 0; i < nbr; ++i) ho[start[key(i)]++] = i;
         uint32_t* dord = (uint32_t*)ctx->dord_enc.get(4 * (size_t)nbr);
         HIPCHK(hipMemcpyAsync(dord, ho, 4 * (size_t)nbr, hipMemcpyHostToDevice, st));
         // chunk ends as fractions of the blocks (GK_T1ENC_CUTS, up to three), rounded to whole MQ

@@ -144,6 +144,19 @@ __global__ __launch_bounds__(256) void k_dc_inv(const int32_t* __restrict__ in, 
 #define DWT_LH (DWT_TH + 3)
 typedef int32_t Lds53[DWT_LH][DWT_LW + 1];
 
+// XCD-aware tile order.  The dispatcher deals workgroups to the 8 XCDs round robin (linear id
+// mod 8), so row-major neighbours - which read each other's halo lines - land on different
+// XCDs, each with its own L2, and every halo line is fetched from HBM again (C2 level 1 read
+// 1.5x its input).  Remapped, XCD k takes the k-th contiguous run of tiles (row-major over x, y,
+// z), in order, so a tile's left and upper neighbours were just read through the same L2.
+__device__ __forceinline__ uint3 xcd_tile() {
+    const uint32_t gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+    const uint32_t lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const uint32_t q = n / 8, r = n % 8, k = lin % 8, j = lin / 8;
+    const uint32_t t = k < r ? k * (q + 1) + j : r * (q + 1) + (k - r) * q + j;
+    return make_uint3(t % gx, (t / gx) % gy, t / (gx * gy));
+}
+
 __device__ __forceinline__ int mirror(int i, int n) {
     if (n == 1) return 0;
     while (i < 0 || i >= n) {   // at most one reflection for halo <= 2 unless n tiny
@@ -155,19 +168,22 @@ __device__ __forceinline__ int mirror(int i, int n) {
 
 // Visit the forward tile's input positions: rows y0-2 .. y0+TH, cols x0-2 .. x0+TW,
 // f(ly, lx, gy, gx) with (gy, gx) mirrored at the resolution border.  4 waves x 64 lanes:
-// lane tx walks columns tx, tx+64 of rows ty, ty+4, ..., the halo columns 128..130 as
-// one extra pass (no index division on the interior path).
+// lane tx walks columns x0 + tx, x0 + 64 + tx of rows ty, ty+4, ... (two 256-byte segments
+// aligned to the row's cache lines: starting them at the halo column x0 - 2 made every
+// segment touch three 128-byte lines), the halo columns x0-2, x0-1, x0+TW as one extra pass
+// (no index division on the interior path).
+__device__ __forceinline__ int fwd53_halo_lx(int j) { return j < 2 ? j : DWT_TW + 2; }   // LDS columns 0, 1, TW+2
 template <class F>
 __device__ __forceinline__ void fwd53_fill(int x0, int y0, int w, int h, int tid, F f) {
     const int tx = tid & 63, ty = tid >> 6;
     if (x0 >= 2 && y0 >= 2 && x0 + DWT_TW < w && y0 + DWT_TH < h) {   // interior tile
         for (int ly = ty; ly < DWT_LH; ly += 4) {
             const int gy = y0 - 2 + ly;
-            f(ly, tx, gy, x0 - 2 + tx);
-            f(ly, tx + 64, gy, x0 + 62 + tx);
+            f(ly, tx + 2, gy, x0 + tx);
+            f(ly, tx + 66, gy, x0 + 64 + tx);
         }
-        for (int i = tid; i < 3 * DWT_LH; i += 256) {   // columns 128..130
-            const int ly = i / 3, lx = 128 + i % 3;
+        for (int i = tid; i < 3 * DWT_LH; i += 256) {   // halo columns x0-2, x0-1, x0+TW
+            const int ly = i / 3, lx = fwd53_halo_lx(i % 3);
             f(ly, lx, y0 - 2 + ly, x0 - 2 + lx);
         }
     } else {
@@ -245,10 +261,11 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
                                                          int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
                                                          uint32_t h, GkTiles tb, GkComps cs) {
     __shared__ Lds53 T;
-    const uint32_t tile = blockIdx.z % tb.count(), comp = blockIdx.z / tb.count();
+    const uint3 bi = xcd_tile();
+    const uint32_t tile = bi.z % tb.count(), comp = bi.z / tb.count();
     src += tb.offset(tile, sstride) + comp * cs.cstride;
     dst += tb.offset(tile, dstride) + comp * cs.cstride;
-    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
+    const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
     fwd53_fill(x0, y0, (int)w, (int)h, tid,
                [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; });
     LDS_BARRIER();
@@ -274,12 +291,12 @@ __device__ __forceinline__ void fwd53_fill_slots(int x0, int y0, int w, int h, i
             const int ly = ty + 4 * k;
             if (ly < DWT_LH) {
                 const int gy = y0 - 2 + ly;
-                f(2 * k, ly, tx, gy, x0 - 2 + tx);
-                f(2 * k + 1, ly, tx + 64, gy, x0 + 62 + tx);
+                f(2 * k, ly, tx + 2, gy, x0 + tx);
+                f(2 * k + 1, ly, tx + 66, gy, x0 + 64 + tx);
             }
         }
         if (tid < 3 * DWT_LH) {
-            const int ly = tid / 3, lx = 128 + tid % 3;
+            const int ly = tid / 3, lx = fwd53_halo_lx(tid % 3);
             f(2 * L1_ROWS, ly, lx, y0 - 2 + ly, x0 - 2 + lx);
         }
     } else {
@@ -299,13 +316,14 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_l1(GkPtr3 in, uint32_t sin, i
                                                       uint64_t cstride, uint32_t dstride, uint32_t w, uint32_t h,
                                                       GkTiles tb, int32_t shift) {
     __shared__ Lds53 T;
-    const uint32_t tile = blockIdx.z;
+    const uint3 bi = xcd_tile();
+    const uint32_t tile = bi.z;
     const uint64_t io = tb.offset(tile, sin);
     const TI* p0 = (const TI*)in.p[0] + io;
     const TI* p1 = (const TI*)in.p[NC == 3 ? 1 : 0] + io;
     const TI* p2 = (const TI*)in.p[NC == 3 ? 2 : 0] + io;
     dst += tb.offset(tile, dstride);
-    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
+    const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
     int32_t U[L1_SLOTS], V[L1_SLOTS];
     fwd53_fill_slots(x0, y0, (int)w, (int)h, tid, [&](int k, int ly, int lx, int gy, int gx) {
         const size_t i = (size_t)gy * sin + gx;
@@ -348,17 +366,19 @@ __device__ __forceinline__ void inv53_fill(int x0, int y0, int w, int h, int tid
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
     if (x0 >= 1 && y0 >= 1 && x0 + DWT_TW + 1 < w && y0 + DWT_TH + 1 < h) {   // interior tile
         // interleaved column gx = x0 - 1 + lx: odd lx <=> even gx (L sample x0/2 + k, lx = 1 + 2k),
-        // even lx <=> odd gx (H sample x0/2 - 1 + k, lx = 2k); both reads are contiguous
+        // even lx <=> odd gx (H sample x0/2 - 1 + k, lx = 2k).  The main pass reads L samples
+        // x0/2 + tx and H samples x0/2 + tx (lx = 2 + 2 tx), both segments starting on a line
+        // boundary when the band starts on one (snw a multiple of 32)
         for (int ly = ty; ly < IDWT_LH; ly += 4) {
             const int gy = y0 - 1 + ly;
             const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
             f(ly, 1 + 2 * tx, sy, (x0 >> 1) + tx);
-            f(ly, 2 * tx, sy, snw + (x0 >> 1) - 1 + tx);
+            f(ly, 2 + 2 * tx, sy, snw + (x0 >> 1) + tx);
         }
-        for (int i = tid; i < 3 * IDWT_LH; i += 256) {   // lx 128 (H), 129 (L), 130 (H)
+        for (int i = tid; i < 3 * IDWT_LH; i += 256) {   // lx 0 (H x0/2 - 1), 129 (L), 130 (H)
             const int ly = i / 3, j = i % 3, gy = y0 - 1 + ly;
             const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
-            f(ly, 128 + j, sy, (j == 1) ? (x0 >> 1) + 64 : snw + (x0 >> 1) + 63 + (j >> 1));
+            f(ly, j ? 128 + j : 0, sy, j == 0 ? snw + (x0 >> 1) - 1 : (j == 1 ? (x0 >> 1) + 64 : snw + (x0 >> 1) + 64));
         }
     } else {
         for (int i = tid; i < IDWT_LH * IDWT_LW; i += 256) {
@@ -407,10 +427,11 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
                                                          int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
                                                          uint32_t h, GkTiles tb, GkComps cs) {
     __shared__ Lds53 T;
-    const uint32_t tile = blockIdx.z % tb.count(), comp = blockIdx.z / tb.count();
+    const uint3 bi = xcd_tile();
+    const uint32_t tile = bi.z % tb.count(), comp = bi.z / tb.count();
     src += tb.offset(tile, sstride) + comp * cs.cstride;
     dst += tb.offset(tile, dstride) + comp * cs.cstride;
-    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
+    const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
     const int tx = tid & 63, ty = tid >> 6;
     inv53_fill(x0, y0, (int)w, (int)h, tid,
                [&](int ly, int lx, int sy, int sx) { T[ly][lx] = src[(size_t)sy * sstride + sx]; });
@@ -436,11 +457,12 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
                                                       GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h,
                                                       GkTiles tb, int32_t shift, int32_t mn, int32_t mx) {
     __shared__ Lds53 T;
-    const uint32_t tile = blockIdx.z;
+    const uint3 bi = xcd_tile();
+    const uint32_t tile = bi.z;
     src += tb.offset(tile, sstride);
     int32_t ox, oy;
     tb.origin(tile, ox, oy);
-    const int x0 = blockIdx.x * DWT_TW, y0 = blockIdx.y * DWT_TH, tid = threadIdx.x;
+    const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
     const int tx = tid & 63, ty = tid >> 6;
     int32_t R0[DWT_TH / 2], R1[DWT_TH / 2];   // this thread's samples (ry = ty + 4 (k >> 1), column tx + 64 (k & 1))
 #pragma unroll

@@ -46,7 +46,7 @@ void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off
                      uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter,
                      const uint32_t* order = nullptr, uint32_t base = 0, uint32_t count = 0xffffffffu);
 // per-block coded bit-plane count (weight of the chunked CM / MQ overlap)
-void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* weight, uint32_t nblocks);
+void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint32_t* weight, uint32_t nblocks);
 uint32_t gk_t1dec_lanes();
 // counters of the last k_t1_dec2 launch made with GK_T1_STATS set: max steps per wave, steps, symbols
 void gk_t1dec_stats(uint64_t out[3]);

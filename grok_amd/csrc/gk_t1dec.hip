@@ -536,8 +536,7 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
         // need: some lane must refill its code register before its next decision (computed at the
         // end of the previous step, so the branch does not wait)
         bool need = __any((actm != 0) & (q.avail < 16));
-#pragma unroll
-        for (int us = 0; us < T1DEC_UNROLL; ++us) {
+        auto step = [&]() __attribute__((always_inline)) {
             // ---------------- one decision per active lane.  While it is decoded, the next step's
             // context is fetched for both outcomes: A, the next FIND position (where a 0 leads, or
             // where MR and SIGN lead anyway) with its significance window, LUT entry and context
@@ -675,6 +674,15 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
             pend_v = actm; pend_b = takeB | mU2;
             actm &= ~np;
             __builtin_amdgcn_sched_barrier(0);
+        };
+#pragma unroll
+        for (int us = 0; us < T1DEC_UNROLL / 2; ++us) step();
+        // half-way through the group: when the lane with the most work left has parked, the group
+        // ends here and its boundary event runs now (that lane used to wait for the group's end,
+        // ~6 steps per stripe-pass, ~8 % of its wave's steps); kpark bit 9
+        if (!((kpark >> 9) & 1) || __builtin_amdgcn_readlane((int)parkm, (int)crit_lane) == 0) {
+#pragma unroll
+            for (int us = T1DEC_UNROLL / 2; us < T1DEC_UNROLL; ++us) step();
         }
         parked = parked || parkm != 0;
         agg = aggm != 0;
@@ -801,6 +809,9 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         // GK_T1DEC_CRIT=0: no event for the lane with the most work left alone (bit 8 of kpark)
         const char* kc = getenv("GK_T1DEC_CRIT");
         if (!kc || atoi(kc)) kpark |= 0x100;
+        // GK_T1DEC_MID=0: no half-group exit when that lane has parked (bit 9)
+        const char* km = getenv("GK_T1DEC_MID");
+        if (!km || atoi(km)) kpark |= 0x200;
     }
     const uint32_t nwaves = (nblocks + 63) / 64, ngroups = (nwaves + DEC_WAVES - 1) / DEC_WAVES;
     const size_t pad = DEC_WAVES * sizeof(Dec2Lds) < 163840 ? 163840 - DEC_WAVES * sizeof(Dec2Lds) : 0;

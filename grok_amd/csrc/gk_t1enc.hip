@@ -646,16 +646,21 @@ void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks,
                            cm_info, nblocks, err, nmse_tab, pass_nmse, order, base, count);
 }
 
-// Per block the bit-plane count T1 will code (the magnitude test of k_t1_cm's load), as the
-// weight that orders the chunked context-modelling / MQ overlap: one wave per block.
+// Per block an estimate of the MQ decisions T1 will code, as the weight that orders the chunked
+// context-modelling / MQ overlap (one wave per block).  With P coded bit-planes every sample
+// takes about one decision per plane - zero coding above its most significant bit, then the
+// significance, its sign and the refinements - except the zeros a run-length column codes four
+// at a time; samples with more magnitude bits leave fewer such zeros.  Weight, in eighths of a
+// decision: 5 P area + 3 (sum of the samples' magnitude bit counts), i.e. P decisions per sample
+// less 3/8 of the zeros above the samples' most significant bits.
 __global__ __launch_bounds__(64) void k_t1_weight(const int32_t* __restrict__ coef, const GkBlock* __restrict__ blocks,
-                                                  uint8_t* __restrict__ weight, uint32_t nblocks) {
+                                                  uint32_t* __restrict__ weight, uint32_t nblocks) {
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
     const int lane = threadIdx.x;
     const GkBlock B = blocks[b];
     const bool irrev = B.flags & 1;
-    uint32_t mx = 0;
+    uint32_t mx = 0, nbits = 0;
     if (lane < (int)B.w)
         for (uint32_t y = 0; y < B.h; ++y) {
             const int32_t raw = coef[B.band_off + (size_t)y * B.stride + lane];
@@ -663,15 +668,20 @@ __global__ __launch_bounds__(64) void k_t1_weight(const int32_t* __restrict__ co
                                       : (uint32_t)(raw < 0 ? -raw : raw) * 64u;
             const uint32_t a = ((a0 >> 6) << (6 + (B.flags >> 3))) | (a0 & 63u);   // ROI maxshift
             mx = a > mx ? a : mx;
+            nbits += (a >> 6) ? 32u - __clz(a >> 6) : 0u;
         }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { const uint32_t t = __shfl_xor(mx, o); mx = t > mx ? t : mx; }
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t t = __shfl_xor(mx, o); mx = t > mx ? t : mx;
+        nbits += __shfl_xor(nbits, o);
+    }
     if (lane == 0) {
         const uint32_t t = mx ? 32 - __clz(mx) : 0;
-        weight[b] = (uint8_t)(t <= 6 ? 0 : t - 6);
+        const uint32_t planes = t <= 6 ? 0 : t - 6;
+        weight[b] = planes * B.w * B.h * 5u + 3u * nbits;
     }
 }
-void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* weight, uint32_t nblocks) {
+void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint32_t* weight, uint32_t nblocks) {
     if (!nblocks) return;
     hipLaunchKernelGGL(k_t1_weight, dim3(nblocks), dim3(64), 0, st, coef, blocks, weight, nblocks);
 }
