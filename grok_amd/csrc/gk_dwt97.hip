@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "gk_common.h"
+#include "gk_xcd.h"
 
 #pragma clang fp contract(off)
 
@@ -189,10 +190,11 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict
                                                          float* __restrict__ dst, uint32_t dstride, uint32_t w,
                                                          uint32_t h, GkTiles tb, GkComps cs) {
     __shared__ Lds97 T;
-    const uint32_t tile = blockIdx.z % tb.count(), comp = blockIdx.z / tb.count();
+    const uint3 bi = xcd_tile();
+    const uint32_t tile = bi.z % tb.count(), comp = bi.z / tb.count();
     src += tb.offset(tile, sstride) + comp * cs.cstride;
     dst += tb.offset(tile, dstride) + comp * cs.cstride;
-    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H, tid = threadIdx.x;
+    const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
     fwd97_fill(x0, y0, (int)w, (int)h, tid,
                [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; });
     __syncthreads();
@@ -221,13 +223,14 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_l1(GkPtr3 in, uint32_t sin, f
                                                       uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb,
                                                       int32_t shift) {
     __shared__ Lds97 T;
-    const uint32_t tile = blockIdx.z;
+    const uint3 bi = xcd_tile();
+    const uint32_t tile = bi.z;
     const uint64_t io = tb.offset(tile, sin);
     const TI* p0 = (const TI*)in.p[0] + io;
     const TI* p1 = (const TI*)in.p[NC == 3 ? 1 : 0] + io;
     const TI* p2 = (const TI*)in.p[NC == 3 ? 2 : 0] + io;
     dst += tb.offset(tile, dstride);
-    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H, tid = threadIdx.x;
+    const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
     float U[L97_SLOTS], V[L97_SLOTS];
     fwd97_fill_slots(x0, y0, (int)w, (int)h, tid, [&](int k, int ly, int lx, int gy, int gx) {
         const size_t i = (size_t)gy * sin + gx;
@@ -323,10 +326,11 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict
                                                          float* __restrict__ dst, uint32_t dstride, uint32_t w,
                                                          uint32_t h, GkTiles tb, GkComps cs) {
     __shared__ Lds97 T;
-    const uint32_t tile = blockIdx.z % tb.count(), comp = blockIdx.z / tb.count();
+    const uint3 bi = xcd_tile();
+    const uint32_t tile = bi.z % tb.count(), comp = bi.z / tb.count();
     src += tb.offset(tile, sstride) + comp * cs.cstride;
     dst += tb.offset(tile, dstride) + comp * cs.cstride;
-    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H, tid = threadIdx.x;
+    const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
     inv97_fill(x0, y0, (int)w, (int)h, tid,
                [&](int ly, int lx, int sy, int sx) { T[ly][lx] = src[(size_t)sy * sstride + sx]; });
     __syncthreads();
@@ -347,11 +351,12 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ 
                                                       GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h,
                                                       GkTiles tb, int32_t shift, int32_t mn, int32_t mx) {
     __shared__ Lds97 T;
-    const uint32_t tile = blockIdx.z;
+    const uint3 bi = xcd_tile();
+    const uint32_t tile = bi.z;
     src += tb.offset(tile, sstride);
     int32_t ox, oy;
     tb.origin(tile, ox, oy);
-    const int x0 = blockIdx.x * T97_W, y0 = blockIdx.y * T97_H, tid = threadIdx.x;
+    const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
     float R0[16], R1[16];   // sample i = tid + 256 k of the 32 x 128 output tile
 #pragma unroll
     for (int c = 0; c < NC; ++c) {

@@ -3584,7 +3584,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             ctx->tm.t1_steps_max = sv[0]; ctx->tm.t1_steps_total = sv[1]; ctx->tm.t1_symbols = sv[2];
         }
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr);
+        uint32_t maxnp = 1;
+        for (const GkBlock& G : blk) maxnp = std::max<uint32_t>(maxnp, G.numbps);
+        gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr, maxnp);
     }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // ---- inverse DWT; its last level writes the output region through the inverse MCT + DC

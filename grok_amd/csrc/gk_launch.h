@@ -53,7 +53,8 @@ void gk_t1dec_stats(uint64_t out[3]);
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
                       uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks);
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
-                        const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks);
+                        const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks,
+                        uint32_t maxnp);   // maxnp: the blocks' largest numbps
 // irreversible path (gk_dwt97.hip)
 // code-blocks with mode switches (gk_t1ms.hip)
 void gk_launch_t1_enc_ms(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, GkPass* passes,

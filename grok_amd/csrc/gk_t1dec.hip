@@ -723,13 +723,16 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
 // significant bit-plane rows and sign rows are staged once through LDS with
 // coalesced row loads (lane = row); the column extraction then reads them as
 // LDS broadcasts instead of one uniform global load per (row, plane).
+// The staging holds the launch's largest plane count (dynamic LDS: 16 KB for 32 planes capped
+// a CU at 9 such waves; C2's 11 planes take 6 KB).
 __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blocks, const uint32_t* __restrict__ ids,
                                                  const uint32_t* __restrict__ pos,
                                                  const uint64_t* __restrict__ scratch,
                                                  const uint64_t* __restrict__ wave_off, int32_t* __restrict__ coef,
-                                                 uint32_t nblocks) {
-    __shared__ uint64_t Lr[32 * 64];
-    __shared__ uint64_t Ls[64];
+                                                 uint32_t nblocks, uint32_t npmax) {
+    extern __shared__ uint64_t Lrec[];
+    uint64_t* Lr = Lrec;                 // npmax plane rows x 64
+    uint64_t* Ls = Lrec + npmax * 64;    // sign rows
     const uint32_t q = blockIdx.x;
     if (q >= nblocks) return;
     const int x = threadIdx.x;
@@ -749,7 +752,7 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
         if (k > 3 * (int)numbps - 3) k = 3 * (int)numbps - 3;
         bpl = (int)numbps - 1 - (k + 2) / 3;
         t = (k + 2) % 3;
-        const int np = min((int)numbps - bpl, 32);   // planes numbps-1 .. bpl, row i = numbps-1-p
+        const int np = min((int)numbps - bpl, (int)npmax);   // planes numbps-1 .. bpl, row i = numbps-1-p
         if (x < (int)h) {
 #pragma unroll 4
             for (int i = 0; i < np; ++i) Lr[i * 64 + x] = WS[WS_BITS + (size_t)i * 64 + x];
@@ -758,7 +761,7 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
     }
     __syncthreads();
     if (x >= (int)B.w) return;
-    const int np = min((int)numbps - bpl, 32);
+    const int np = min((int)numbps - bpl, (int)npmax);
     for (uint32_t y = 0; y < h; ++y) {
         int32_t v = 0;
         if (any) {
@@ -846,7 +849,9 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     }
 }
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
-                        const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks) {
+                        const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks, uint32_t maxnp) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_t1_recon, dim3(nblocks), dim3(64), 0, st, blocks, ids, pos, scratch, wave_off, coef, nblocks);
+    const uint32_t npmax = maxnp < 1 ? 1 : (maxnp > 32 ? 32 : maxnp);
+    hipLaunchKernelGGL(k_t1_recon, dim3(nblocks), dim3(64), (size_t)(npmax + 1) * 64 * 8, st, blocks, ids, pos, scratch,
+                       wave_off, coef, nblocks, npmax);
 }
