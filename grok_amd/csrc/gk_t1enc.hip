@@ -172,16 +172,19 @@ __global__ __launch_bounds__(64) void k_t1_cm(const int32_t* __restrict__ coef, 
     uint32_t pos = 0, passno = 0;
     int32_t acc = 0;   // RC: this lane's nmsedec for the current pass
     // RC: nmsedec of the rows in mask (getnmsedec_sig: table 0/1, getnmsedec_ref: table 2/3)
+    // (8-row groups that no lane of the wave has in `mask` are skipped with one uniform branch:
+    // a pass's new significances are sparse at the upper planes)
     auto nm_rows = [&](uint64_t mask, int t, int bp) __attribute__((always_inline)) {
         if constexpr (RC) {
-            if (bp > 0) {
+            const int16_t* tab = R.nm[bp > 0 ? t : t + 1];
 #pragma unroll
-                for (int y = 0; y < 64; ++y)
-                    if ((mask >> y) & 1) acc += R.nm[t][(m[y] >> bp) & 127];
-            } else {
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t gm = (uint32_t)(mask >> (8 * g)) & 0xffu;
+                if (__any(gm != 0)) {
 #pragma unroll
-                for (int y = 0; y < 64; ++y)
-                    if ((mask >> y) & 1) acc += R.nm[t + 1][m[y] & 127];
+                    for (int k = 0; k < 8; ++k)
+                        if ((gm >> k) & 1) acc += tab[(m[8 * g + k] >> bp) & 127];
+                }
             }
         }
     };
