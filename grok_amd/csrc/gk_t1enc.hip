@@ -423,12 +423,12 @@ __device__ __forceinline__ void mq_byteout5(MqLane& q, MqLds& L, int lane, uint3
     const uint32_t carry = (c >> 27) & 1u & bo & ~mz(q.cur ^ 0xffu);
     const uint32_t cur = q.cur + carry;
     c &= ~(carry << 27);
-    const uint32_t ffm = mz(cur ^ 0xffu);
-    const uint32_t nb = (c >> (19u + (ffm & 1u))) & 0xffu;
+    const uint32_t ffm = mz(cur ^ 0xffu);                          // 0 / -1
+    const uint32_t nb = __builtin_amdgcn_ubfe(c, 19u - ffm, 8);    // C >> 20 after 0xFF, else C >> 19
     mq_put5(q, L, lane, bo, cur);
     q.cur = bsel(bo, nb, q.cur);
-    c &= bsel(bo, bsel(ffm, 0xfffffu, 0x7ffffu), ~0u);
-    ct = bsel(bo, 8u - (ffm & 1u), ct);
+    c &= (0x7ffffu | (ffm & 0x80000u)) | ~bo;
+    ct = bsel(bo, 8u + ffm, ct);                                    // 7 after 0xFF, else 8
 }
 
 // CODEMPS / CODELPS + RENORME (Annex C.2.4-C.2.7), branch-free.  With x = (MPS symbol) xor
@@ -459,7 +459,9 @@ __device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t
     const uint32_t fast = ism & mbit(a1, 15);             // MPS without renormalisation
     const uint32_t x = ism ^ mlt(a1, qe);
     // the successor pair entry (MPS bit included): NMPS for the MPS, NLPS (with SWITCH) for the LPS
-    const uint32_t ne = L.tab[bsel(ism, (e >> 16) & 0x7f, (e >> 23) & 0x7f)];
+    uint32_t nidx;   // one v_bfi (the compiler otherwise masks both fields and adds them scaled)
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(nidx) : "v"(ism), "v"(__builtin_amdgcn_ubfe(e, 16, 7)), "v"(__builtin_amdgcn_ubfe(e, 23, 7)));
+    const uint32_t ne = L.tab[nidx];
     q.pcx1 = cx; q.pne1 = bsel(fast, e, ne);
     const uint32_t an = bsel(x, a1, qe);
     const uint32_t n = ffbh(an) - 16u;                    // an != 0; 0 on the fast path (an = a1 >= 0x8000)
