@@ -1118,8 +1118,11 @@ struct T2Enc {
         }
         bw.flush();
         if (budget) {
-            if ((uint64_t)hdr.size() >= *budget) return false;   // bounded BitIO (BitIO.cpp:35-52)
-            *budget -= hdr.size();
+            // compressPacketSimulate (T2Compress.cpp:347-434) in its uint32 arithmetic: the bounded
+            // BitIO fails when its byte count reaches the bytes left (BitIO.cpp:35-52), which never
+            // happens with none left, so such a packet passes and the subtraction wraps
+            if (*budget != 0 && (uint64_t)hdr.size() >= *budget) return false;
+            *budget = (uint32_t)(*budget - hdr.size());
         }
         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
             const PrecG& PG = R.prc[bi][pi];
@@ -1131,7 +1134,7 @@ struct T2Enc {
                 uint32_t r1 = rate(b, inprev[b] + np - 1);
                 if (budget) {
                     if ((uint64_t)(r1 - r0) > *budget) return false;
-                    *budget -= (r1 - r0);
+                    *budget = (uint32_t)(*budget - (r1 - r0));
                 }
                 if (seg) { seg->push_back(b); seg->push_back(r0); seg->push_back(r1 - r0); }
                 if (body_bytes) *body_bytes += r1 - r0;
@@ -1182,10 +1185,10 @@ struct T2Enc {
         // the packet the progression order writes last decides the budget test
         last_chain = chains.empty() ? 0 : (uint32_t)chains.size() - 1;
         {
-            const std::vector<PacketRef> ord = packet_order(P, T, 1);
-            if (!ord.empty())
+            const std::vector<PacketRef> o1 = packet_order(P, T, 1);
+            if (!o1.empty())
                 for (uint32_t i = 0; i < (uint32_t)chains.size(); ++i)
-                    if (chains[i].r == ord.back().r && chains[i].c == ord.back().c && chains[i].pi == ord.back().pi) last_chain = i;
+                    if (chains[i].r == o1.back().r && chains[i].c == o1.back().c && chains[i].pi == o1.back().pi) last_chain = i;
         }
         cunits.assign(chains.size(), {});
         for (uint32_t i = 0; i < (uint32_t)chains.size(); ++i) {
@@ -1204,6 +1207,7 @@ struct T2Enc {
         ubody.assign(units.size(), 0);
         csize.assign(chains.size(), 0); chdr.assign(chains.size(), 0);
         prior = 0;
+        fsize.clear(); fhdr.clear(); ord_l = 0xffffffffu;
     }
     void restore_band(const PrecG& PG) {
         incl[PG.tree] = incl0[PG.tree]; imsb[PG.tree] = imsb0[PG.tree];
@@ -1330,17 +1334,61 @@ struct T2Enc {
     uint64_t prof_code = 0, prof_stuff = 0;   // GK_PROFILE: code_layer phases (us)
     bool skip_clean = false;
     std::vector<uint8_t> cdirty;
+    // The packets of layers <= l in progression order, as (chain, layer), and the final layers'
+    // packet sizes: compressPacketsSimulate's outcome is a walk over them (packet_walk).
+    std::vector<std::pair<uint32_t, uint32_t>> ord;
+    uint32_t ord_l = 0xffffffffu;
+    std::vector<std::vector<uint64_t>> fsize, fhdr;   // per final layer: each chain's packet bytes / header bytes
+    void ensure_order(uint32_t l) {
+        if (ord_l == l) return;
+        const TileG& T = P.tiles[t0];
+        std::vector<uint32_t> base((size_t)P.p.numres * P.nc, 0);   // first chain of (r, c)
+        for (uint32_t i = (uint32_t)chains.size(); i-- > 0;) base[(size_t)chains[i].r * P.nc + chains[i].c] = i;
+        ord.clear();
+        for (const PacketRef& pr : packet_order(P, T, l + 1))
+            ord.push_back({base[(size_t)pr.r * P.nc + pr.c] + pr.pi, pr.l});
+        ord_l = l;
+    }
+    // compressPacketsSimulate (T2Compress.cpp:59-112) over packet sizes: a header reaching the
+    // bytes left or a body past them fails the layer, and a packet met with no byte left passes
+    // with all after it (its uint32 subtraction wraps, see write_packet)
+    bool packet_walk(uint32_t l, uint64_t max_bytes) const {
+        uint64_t rem = max_bytes;
+        for (const auto& e : ord) {
+            if (rem == 0) return true;
+            const uint64_t h = e.second < l ? fhdr[e.second][e.first] : chdr[e.first];
+            const uint64_t sz = e.second < l ? fsize[e.second][e.first] : csize[e.first];
+            if (h >= rem) return false;
+            rem -= h;
+            if (sz - h > rem) return false;
+            rem -= sz - h;
+        }
+        return true;
+    }
+    // could a running size before the last packet equal max_bytes exactly (the wrap above)?
+    // lo / hi: per chain bounds of this layer's packet bytes
+    bool may_hit(uint32_t l, uint64_t max_bytes) const {
+        uint64_t slo = 0, shi = 0;
+        for (size_t k = 0; k + 1 < ord.size(); ++k) {
+            const auto& e = ord[k];
+            if (e.second < l) { slo += fsize[e.second][e.first]; shi += fsize[e.second][e.first]; }
+            else { slo += clo[e.first] + cbody[e.first]; shi += chi[e.first] + cbody[e.first]; }
+            if (slo > max_bytes) return false;
+            if (shi >= max_bytes) return true;
+        }
+        return false;
+    }
     bool simulate_layer(uint32_t l, uint64_t max_bytes) {
         if (max_bytes == 0xffffffffull) return true;
         code_layer(l);
-        uint64_t tot = prior;
-        for (uint64_t v : csize) tot += v;
-        const uint64_t last = csize[last_chain], lasth = chdr[last_chain];
-        return tot - last + lasth < max_bytes && tot <= max_bytes;
+        ensure_order(l);
+        return packet_walk(l, max_bytes);
     }
     void finish_layer(uint32_t l) {   // layer l is final: advance the snapshot past it
         code_layer(l);
         for (uint64_t v : csize) prior += v;
+        if (fsize.size() <= l) { fsize.resize(l + 1); fhdr.resize(l + 1); }
+        fsize[l] = csize; fhdr[l] = chdr;
         incl0 = incl; imsb0 = imsb; inprev0 = inprev; nlb0 = nlb;
     }
 
@@ -1467,13 +1515,14 @@ struct T2Enc {
             lo += clo[i] + body; hi += chi[i] + body;
             if (i == last_chain) last_body = body;
         }
-        // pass <=> S_(n-1) + hdr_n < max_bytes and S_n <= max_bytes, S_n - body_n = S_(n-1) + hdr_n
+        // pass <=> S_(n-1) + hdr_n < max_bytes and S_n <= max_bytes, S_n - body_n = S_(n-1) + hdr_n,
+        // unless a running size S_k (k < n) equals max_bytes: then the rest passes (packet_walk)
         if (hi <= max_bytes && hi - last_body < max_bytes) return 1;
-        if (lo > max_bytes || lo - last_body >= max_bytes) return -1;
+        if (lo > max_bytes || lo - last_body >= max_bytes) { ensure_order(l); return may_hit(l, max_bytes) ? 0 : -1; }
         return 0;
     }
     // decide() from the per-unit sums make_layer_inc keeps (same arithmetic, no pass over blocks)
-    int decide_inc(uint64_t max_bytes) {
+    int decide_inc(uint32_t l, uint64_t max_bytes) {
         if (max_bytes == 0xffffffffull) return 1;
         for (uint32_t u = 0; u < (uint32_t)units.size(); ++u) { ubitn[u] = ibits[u]; ubody[u] = ibody[u]; }
         uint64_t lo = prior, hi = prior, last_body = 0;
@@ -1486,7 +1535,7 @@ struct T2Enc {
             if (i == last_chain) last_body = body;
         }
         if (hi <= max_bytes && hi - last_body < max_bytes) return 1;
-        if (lo > max_bytes || lo - last_body >= max_bytes) return -1;
+        if (lo > max_bytes || lo - last_body >= max_bytes) { ensure_order(l); return may_hit(l, max_bytes) ? 0 : -1; }
         return 0;
     }
 
@@ -1797,7 +1846,7 @@ struct T2Enc {
                     if (has_hi && h == h_hi && same(c_hi, j_hi)) ok = true;
                     else if (has_lo && h == h_lo && same(c_lo, j_lo)) ok = false;
                     else {
-                        int d = bounds_on ? decide_inc(max_len) : 0;
+                        int d = bounds_on ? decide_inc(l, max_len) : 0;
                         if (bounds_on && check) {   // debug: the incremental sums must equal a full pass
                             const std::vector<uint64_t> b0v = ubitn, b1v = ubody;
                             if (decide(l, max_len, prev) != d || ubitn != b0v || ubody != b1v)

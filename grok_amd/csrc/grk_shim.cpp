@@ -205,12 +205,11 @@ struct CodecObj : Obj {
     uint32_t win[4] = {0, 0, 0, 0};
     bool has_win = false;
     ImageObj* out = nullptr;                 // composited image (owned by the codec)
-    ImageObj* tile_out = nullptr;            // last grk_decompress_tile image
+    bool tile_decoded = false;               // grk_decompress_tile cropped `out` to a tile
     ~CodecObj() override {
         if (stream) grk_object_unref(stream);
         if (image) grk_object_unref(&image->obj);
         if (out) grk_object_unref(&out->img.obj);
-        if (tile_out) grk_object_unref(&tile_out->img.obj);
     }
 };
 CodecObj* codec_of(grk_codec* c) { return c ? dynamic_cast<CodecObj*>(obj_of(c)) : nullptr; }
@@ -294,9 +293,29 @@ ImageObj* region_image(CodecObj* C, uint32_t x0, uint32_t y0, uint32_t x1, uint3
     }
     GRK_COLOR_SPACE cs = GRK_CLRSPC_UNKNOWN;
     if (C->coding.cod_format == 2) cs = C->info.numcomps < 3 ? GRK_CLRSPC_GRAY : GRK_CLRSPC_SRGB;
-    ImageObj* o = new_image((uint16_t)C->info.numcomps, p.data(), cs, true);
+    // sample memory is attached by the decompress call (Grok allocates the composite's planes
+    // at decompress time too), so a header read of a 32768^2 .jp2 holds no planes
+    ImageObj* o = new_image((uint16_t)C->info.numcomps, p.data(), cs, false);
     if (o) { o->img.x0 = x0; o->img.y0 = y0; o->img.x1 = x1; o->img.y1 = y1; }
     return o;
+}
+
+// Re-bound the composited image in place and give it planes: callers keep the pointer that
+// grk_decompress_get_composited_image returned after the header read (grk_decompress.cpp:1191
+// takes it before set_window / decompress), as Grok edits the one composite image in place
+// (CodeStreamDecompress.cpp:335-387, :451-481).
+bool reshape_image(ImageObj* o, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    o->img.x0 = x0; o->img.y0 = y0; o->img.x1 = x1; o->img.y1 = y1;
+    for (auto& c : o->comps) {
+        const uint32_t stride = aligned_stride(x1 - x0);
+        if (c.data && (c.w != x1 - x0 || c.h != y1 - y0 || c.stride != stride)) { free(c.data); c.data = nullptr; }
+        c.x0 = x0; c.y0 = y0; c.w = x1 - x0; c.h = y1 - y0; c.stride = stride;
+        if (!c.data && c.w && c.h) {
+            c.data = (int32_t*)aligned_alloc(64, ((size_t)c.stride * c.h * 4 + 63) / 64 * 64);
+            if (!c.data) { error("out of memory for a %ux%u component", c.w, c.h); return false; }
+        }
+    }
+    return true;
 }
 
 }  // namespace
@@ -305,10 +324,12 @@ extern "C" {
 
 const char* grk_version(void) { return "9.2.0"; }   // the codestream COM text names this version
 
+// grok.cpp:71-86 sizes the thread pool and loads the plugin.  The engine (and its HIP context)
+// is created by the first call that codes, so an initialise on a host without a GPU succeeds and
+// the refusal comes from that call, as Grok's own CPU path would only fail there.
 bool grk_initialize(const char* pluginPath, uint32_t numthreads) {
     (void)pluginPath; (void)numthreads;   // no separate plugin; host T2 threads are sized by the engine
-    std::lock_guard<std::mutex> lk(g_eng_m);
-    return engine() != nullptr;
+    return true;
 }
 
 void grk_deinitialize(void) {
@@ -581,13 +602,21 @@ bool grk_decompress_read_header(grk_codec* codec, grk_header_info* hi) {
     return true;
 }
 
+// CodeStreamDecompress::setDecompressWindow (CodeStreamDecompress.cpp:295-398): (0,0,0,0) is the
+// whole image — grk_decompress.cpp:1259 always calls this, with the -d values or zeros; a left or
+// top edge past the image is an error; a right or bottom edge past it is clamped with a warning.
 bool grk_decompress_set_window(grk_codec* codec, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
     CodecObj* C = codec_of(codec);
-    if (!C || C->compress || !C->header_read) return false;
-    if (x0 >= x1 || y0 >= y1 || x1 > C->info.w || y1 > C->info.h) {
-        error("decompress window (%u,%u,%u,%u) is outside the image", x0, y0, x1, y1);
-        return false;
-    }
+    if (!C || C->compress) return false;
+    if (!C->header_read) { error("Need to read the main header before setting decompress window"); return false; }
+    if (!x0 && !y0 && !x1 && !y1) { C->has_win = false; return true; }
+    const uint32_t W = C->info.w, H = C->info.h;
+    if (x0 > W) { error("Left position of the decompress window (%u) is outside of the image area (Xsiz=%u).", x0, W); return false; }
+    if (y0 > H) { error("Top position of the decompress window (%u) is outside of the image area (Ysiz=%u).", y0, H); return false; }
+    if (x1 > W) { warn("Right position of the decompress window (%u) is outside the image area (Xsiz=%u).", x1, W); x1 = W; }
+    if (y1 > H) { warn("Bottom position of the decompress window (%u) is outside of the image area (Ysiz=%u).", y1, H); y1 = H; }
+    if (x0 >= x1 || y0 >= y1) { error("decompress window (%u,%u,%u,%u) is empty", x0, y0, x1, y1); return false; }
+    if (C->dp.cp_reduce) { error("reduced-resolution decode of a window is not supported on this path"); return false; }
     C->win[0] = x0; C->win[1] = y0; C->win[2] = x1; C->win[3] = y1;
     C->has_win = true;
     return true;
@@ -599,36 +628,51 @@ bool grk_decompress(grk_codec* codec, grk_plugin_tile* tile) {
     if (tile) { error("plugin tiles are not used: the tile pipeline runs in this library"); return false; }
     if (!C->header_read && !grk_decompress_read_header(codec, nullptr)) return false;
     if (C->has_win) {
-        // the composited image covers the window (CodeStreamDecompress::setDecompressWindow)
-        ImageObj* o = region_image(C, C->win[0], C->win[1], C->win[2], C->win[3]);
-        if (!o) return false;
-        if (C->out) grk_object_unref(&C->out->img.obj);
-        C->out = o;
-        return run_decode(C, o, C->win);
+        if (!reshape_image(C->out, C->win[0], C->win[1], C->win[2], C->win[3])) return false;
+        return run_decode(C, C->out, C->win);
     }
+    const uint32_t r = C->dp.cp_reduce;   // the composited image is ceil(size / 2^reduce)
+    if (!reshape_image(C->out, 0, 0, (uint32_t)(((uint64_t)C->info.w + (1ull << r) - 1) >> r),
+                       (uint32_t)(((uint64_t)C->info.h + (1ull << r) - 1) >> r)))
+        return false;
     return run_decode(C, C->out, nullptr);
 }
 
+// CodeStreamDecompress::decompressTile (CodeStreamDecompress.cpp:416-493): the composited image
+// is cropped to the tile (intersected with the window when one is set) and the tile decodes
+// into it; grk_decompress_get_tile_image then returns that image.
 bool grk_decompress_tile(grk_codec* codec, uint16_t tileIndex) {
     CodecObj* C = codec_of(codec);
     if (!C || C->compress) return false;
     if (!C->header_read && !grk_decompress_read_header(codec, nullptr)) return false;
+    if (C->dp.cp_reduce) { error("reduced-resolution decode of a tile is not supported on this path"); return false; }
     const uint32_t tw = C->coding.t_width, th = C->coding.t_height;
     const uint32_t ntx = (C->info.w + tw - 1) / tw, nty = (C->info.h + th - 1) / th;
-    if (tileIndex >= ntx * nty) { error("tile index %u out of range", tileIndex); return false; }
-    const uint32_t x0 = (tileIndex % ntx) * tw, y0 = (tileIndex / ntx) * th;
-    const uint32_t w[4] = {x0, y0, std::min(x0 + tw, C->info.w), std::min(y0 + th, C->info.h)};
-    ImageObj* o = region_image(C, w[0], w[1], w[2], w[3]);
-    if (!o) return false;
-    if (C->tile_out) grk_object_unref(&C->tile_out->img.obj);
-    C->tile_out = o;
-    return run_decode(C, o, w);
+    if (tileIndex >= ntx * nty) {
+        error("Tile index %u is greater than maximum tile index %u", tileIndex, ntx * nty - 1);
+        return false;
+    }
+    const uint32_t tx0 = (tileIndex % ntx) * tw, ty0 = (tileIndex / ntx) * th;
+    uint32_t w[4] = {tx0, ty0, std::min(tx0 + tw, C->info.w), std::min(ty0 + th, C->info.h)};
+    if (C->has_win) {
+        const uint32_t c[4] = {std::max(w[0], C->win[0]), std::max(w[1], C->win[1]), std::min(w[2], C->win[2]),
+                               std::min(w[3], C->win[3])};
+        if (c[0] < c[2] && c[1] < c[3]) { w[0] = c[0]; w[1] = c[1]; w[2] = c[2]; w[3] = c[3]; }
+        else {
+            warn("Decompress bounds <%u,%u,%u,%u> do not overlap with requested tile %u. Decompressing full image",
+                 C->win[0], C->win[1], C->win[2], C->win[3], tileIndex);
+            w[0] = C->win[0]; w[1] = C->win[1]; w[2] = C->win[2]; w[3] = C->win[3];
+        }
+    }
+    if (!reshape_image(C->out, w[0], w[1], w[2], w[3])) return false;
+    C->tile_decoded = true;
+    return run_decode(C, C->out, w);
 }
 
 grk_image* grk_decompress_get_tile_image(grk_codec* codec, uint16_t tileIndex) {
     (void)tileIndex;
     CodecObj* C = codec_of(codec);
-    return C && C->tile_out ? &C->tile_out->img : nullptr;
+    return C && C->tile_decoded ? &C->out->img : nullptr;
 }
 
 grk_image* grk_decompress_get_composited_image(grk_codec* codec) {

@@ -384,84 +384,82 @@ static void dc_ict_fwd(std::vector<std::vector<float>>& f, const std::vector<std
 // first then horizontal, in-place Mallat deinterleave).  Parity 0 only
 // (tile origin even at every level, which holds for single-tile images).
 // ----------------------------------------------------------------------------
-static void fwd53_1d(int32_t* x, uint32_t n, std::vector<int32_t>& tmp) {
-    if (n < 2) return;                       // width 1, even parity: unchanged
-    uint32_t sn = (n + 1) >> 1, dn = n >> 1;
+// A resolution whose first sample sits on an odd coordinate (tile origins off the 2^L grid,
+// e.g. -t 200,160) starts with a high-pass sample: WaveletFwd.cpp's parity_row / parity_col
+// (:486-489) select the odd ("cas1") lifting, and WaveletReverse.cpp:559-663 its inverse.
+// Written once for both parities: sample i is high-pass when (i + parity) is odd, with
+// whole-sample symmetric extension at both ends of the line; lows then highs on output.
+static inline int64_t mirror(int64_t i, uint32_t n) {
+    if (i < 0) i = -i;
+    if (i >= (int64_t)n) i = 2 * (int64_t)n - 2 - i;
+    return i;
+}
+static void fwd53_1d(int32_t* x, uint32_t n, std::vector<int32_t>& tmp, uint32_t par, bool) {
+    if (n == 1) { if (par) x[0] *= 2; return; }   // odd single sample: 2x (WaveletFwd.cpp:932-935)
+    if (n < 2) return;
+    const uint32_t sn = (n + 1 - par) >> 1;       // low-pass count
+    // predict on the high positions, then update the low positions
+    for (uint32_t i = 1 - par; i < n; i += 2) x[i] -= (x[mirror((int64_t)i - 1, n)] + x[mirror((int64_t)i + 1, n)]) >> 1;
+    for (uint32_t i = par; i < n; i += 2) x[i] += (x[mirror((int64_t)i - 1, n)] + x[mirror((int64_t)i + 1, n)] + 2) >> 2;
     tmp.resize(n);
-    // predict: d[i] = x[2i+1] - floor((x[2i] + x[2i+2]) / 2), mirror x[n] = x[n-2]
-    for (uint32_t i = 0; i < dn; ++i) {
-        int32_t a = x[2 * i];
-        int32_t b = (2 * i + 2 < n) ? x[2 * i + 2] : x[2 * i];
-        tmp[sn + i] = x[2 * i + 1] - ((a + b) >> 1);
-    }
-    // update: s[i] = x[2i] + floor((d[i-1] + d[i] + 2) / 4), mirror d[-1] = d[0], d[dn] = d[dn-1]
-    for (uint32_t i = 0; i < sn; ++i) {
-        int32_t dl = (i > 0) ? tmp[sn + i - 1] : tmp[sn];
-        int32_t dr = (i < dn) ? tmp[sn + i] : tmp[sn + dn - 1];
-        tmp[i] = x[2 * i] + ((dl + dr + 2) >> 2);
-    }
+    uint32_t k = 0;
+    for (uint32_t i = par; i < n; i += 2) tmp[k++] = x[i];
+    for (uint32_t i = 1 - par; i < n; i += 2) tmp[k++] = x[i];
+    (void)sn;
     memcpy(x, tmp.data(), n * sizeof(int32_t));
 }
-static void inv53_1d(int32_t* x, uint32_t n, std::vector<int32_t>& tmp) {
+static void inv53_1d(int32_t* x, uint32_t n, std::vector<int32_t>& tmp, uint32_t par, bool vertical) {
+    if (n == 1) {
+        // odd single sample: horizontal bandH[0] / 2, vertical bandL[0] >> 1 (WaveletReverse.cpp:583, :636)
+        if (par) x[0] = vertical ? (x[0] >> 1) : (x[0] / 2);
+        return;
+    }
     if (n < 2) return;
-    uint32_t sn = (n + 1) >> 1, dn = n >> 1;
+    const uint32_t sn = (n + 1 - par) >> 1;
     tmp.resize(n);
-    const int32_t* s = x; const int32_t* d = x + sn;
-    for (uint32_t i = 0; i < sn; ++i) {
-        int32_t dl = (i > 0) ? d[i - 1] : d[0];
-        int32_t dr = (i < dn) ? d[i] : d[dn - 1];
-        tmp[2 * i] = s[i] - ((dl + dr + 2) >> 2);
-    }
-    for (uint32_t i = 0; i < dn; ++i) {
-        int32_t a = tmp[2 * i];
-        int32_t b = (2 * i + 2 < n) ? tmp[2 * i + 2] : tmp[2 * i];
-        tmp[2 * i + 1] = d[i] + ((a + b) >> 1);
-    }
+    uint32_t k = 0;
+    for (uint32_t i = par; i < n; i += 2) tmp[i] = x[k++];
+    for (uint32_t i = 1 - par; i < n; i += 2) tmp[i] = x[k++];
+    (void)sn;
+    for (uint32_t i = par; i < n; i += 2) tmp[i] -= (tmp[mirror((int64_t)i - 1, n)] + tmp[mirror((int64_t)i + 1, n)] + 2) >> 2;
+    for (uint32_t i = 1 - par; i < n; i += 2) tmp[i] += (tmp[mirror((int64_t)i - 1, n)] + tmp[mirror((int64_t)i + 1, n)]) >> 1;
     memcpy(x, tmp.data(), n * sizeof(int32_t));
 }
 
 // ----------------------------------------------------------------------------
 // 9/7 irreversible DWT (Annex F.4.8.2; WaveletFwd.cpp:39-44, 964-1025 and
-// WaveletReverse.cpp:882-1024, 1272-1351).  Float lifting.
+// WaveletReverse.cpp:882-1024, 1272-1351).  Float lifting; a single sample is left as it is
+// for either parity (WaveletFwd.cpp:973-976, 1018-1021; WaveletReverse.cpp:1012-1014).
 // ----------------------------------------------------------------------------
 static const float A97 = -1.586134342f, B97 = -0.052980118f, G97 = 0.882911075f, D97 = 0.443506852f;
 static const float K97 = 1.230174105f, INVK97 = (float)(1.0 / 1.230174105), TWO_INVK97 = 1.625732422f;
 
-static void fwd97_1d(float* x, uint32_t n, std::vector<float>& tmp) {
+static void fwd97_1d(float* x, uint32_t n, std::vector<float>& tmp, uint32_t par, bool) {
     if (n < 2) return;
-    uint32_t sn = (n + 1) >> 1, dn = n >> 1;
     tmp.resize(n);
-    auto X = [&](int64_t i) -> float& {   // symmetric extension on the interleaved signal
-        if (i < 0) i = -i;
-        if (i >= (int64_t)n) i = 2 * (int64_t)n - 2 - i;
-        return x[i];
-    };
-    // work on a copy with lifting in place (odd = d, even = s)
-    auto lift = [&](int64_t start, float c) {
+    auto X = [&](int64_t i) -> float& { return x[mirror(i, n)]; };
+    auto lift = [&](uint32_t start, float c) {   // (left + right) * c added (encode_step2, :135-163)
         for (int64_t i = start; i < (int64_t)n; i += 2) { float t = (X(i - 1) + X(i + 1)) * c; x[i] = x[i] + t; }
     };
-    lift(1, A97); lift(0, B97); lift(1, G97); lift(0, D97);
-    for (uint32_t i = 0; i < sn; ++i) tmp[i] = x[2 * i] * INVK97;
-    for (uint32_t i = 0; i < dn; ++i) tmp[sn + i] = x[2 * i + 1] * K97;
+    lift(1 - par, A97); lift(par, B97); lift(1 - par, G97); lift(par, D97);
+    uint32_t k = 0;
+    for (uint32_t i = par; i < n; i += 2) tmp[k++] = x[i] * INVK97;
+    for (uint32_t i = 1 - par; i < n; i += 2) tmp[k++] = x[i] * K97;
     memcpy(x, tmp.data(), n * sizeof(float));
 }
-static void inv97_1d(float* x, uint32_t n, std::vector<float>& tmp) {
+static void inv97_1d(float* x, uint32_t n, std::vector<float>& tmp, uint32_t par, bool) {
     if (n < 2) return;
-    uint32_t sn = (n + 1) >> 1, dn = n >> 1;
     tmp.resize(n);
-    for (uint32_t i = 0; i < sn; ++i) tmp[2 * i] = x[i] * K97;
+    uint32_t k = 0;
+    for (uint32_t i = par; i < n; i += 2) tmp[i] = x[k++] * K97;
     // high band scaled by 2/K: Grok's decoder step sizes omit the band gain
     // (Quantizer.cpp:31-36, "BUG_WEIRD_TWO_INVK"), WaveletReverse.cpp:365-371
-    for (uint32_t i = 0; i < dn; ++i) tmp[2 * i + 1] = x[sn + i] * TWO_INVK97;
-    auto X = [&](int64_t i) -> float& {
-        if (i < 0) i = -i;
-        if (i >= (int64_t)n) i = 2 * (int64_t)n - 2 - i;
-        return tmp[i];
-    };
-    for (int64_t i = 0; i < (int64_t)n; i += 2) tmp[i] -= D97 * (X(i - 1) + X(i + 1));
-    for (int64_t i = 1; i < (int64_t)n; i += 2) tmp[i] -= G97 * (X(i - 1) + X(i + 1));
-    for (int64_t i = 0; i < (int64_t)n; i += 2) tmp[i] -= B97 * (X(i - 1) + X(i + 1));
-    for (int64_t i = 1; i < (int64_t)n; i += 2) tmp[i] -= A97 * (X(i - 1) + X(i + 1));
+    for (uint32_t i = 1 - par; i < n; i += 2) tmp[i] = x[k++] * TWO_INVK97;
+    auto X = [&](int64_t i) -> float& { return tmp[mirror(i, n)]; };
+    for (int64_t i = par; i < (int64_t)n; i += 2) tmp[i] -= D97 * (X(i - 1) + X(i + 1));
+    for (int64_t i = 1 - par; i < (int64_t)n; i += 2) tmp[i] -= G97 * (X(i - 1) + X(i + 1));
+    for (int64_t i = par; i < (int64_t)n; i += 2) tmp[i] -= B97 * (X(i - 1) + X(i + 1));
+    for (int64_t i = 1 - par; i < (int64_t)n; i += 2) tmp[i] -= A97 * (X(i - 1) + X(i + 1));
     memcpy(x, tmp.data(), n * sizeof(float));
 }
 
@@ -471,22 +469,21 @@ static void dwt2d(T* buf, uint32_t stride, const Comp& c, uint32_t numres, bool 
     auto level = [&](uint32_t r) {  // transform resolution r (rw x rh) <-> r-1 + 3 bands
         const Res& R = c.res[r];
         uint32_t rw = R.x1 - R.x0, rh = R.y1 - R.y0;
-        if (forward) {
-            col.resize(rh);
-            for (uint32_t x = 0; x < rw; ++x) {       // vertical first
-                for (uint32_t y = 0; y < rh; ++y) col[y] = buf[(size_t)y * stride + x];
-                f1d(col.data(), rh, tmp);
-                for (uint32_t y = 0; y < rh; ++y) buf[(size_t)y * stride + x] = col[y];
-            }
-            for (uint32_t y = 0; y < rh; ++y) f1d(buf + (size_t)y * stride, rw, tmp);
-        } else {
-            for (uint32_t y = 0; y < rh; ++y) f1d(buf + (size_t)y * stride, rw, tmp);  // horizontal first
+        const uint32_t px = R.x0 & 1, py = R.y0 & 1;   // parity_row / parity_col
+        auto vpass = [&]() {
             col.resize(rh);
             for (uint32_t x = 0; x < rw; ++x) {
                 for (uint32_t y = 0; y < rh; ++y) col[y] = buf[(size_t)y * stride + x];
-                f1d(col.data(), rh, tmp);
+                f1d(col.data(), rh, tmp, py, true);
                 for (uint32_t y = 0; y < rh; ++y) buf[(size_t)y * stride + x] = col[y];
             }
+        };
+        if (forward) {
+            vpass();                                   // vertical first
+            for (uint32_t y = 0; y < rh; ++y) f1d(buf + (size_t)y * stride, rw, tmp, px, false);
+        } else {
+            for (uint32_t y = 0; y < rh; ++y) f1d(buf + (size_t)y * stride, rw, tmp, px, false);  // horizontal first
+            vpass();
         }
     };
     if (forward) for (uint32_t r = numres - 1; r >= 1; --r) level(r);
@@ -1453,9 +1450,12 @@ static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t 
     }
     bw.flush();
     if (budget) {
-        // BitIO::writeByte fails when the byte count reaches the budget (BitIO.cpp:35-52)
-        if ((uint64_t)hdr.size() >= *budget) return false;
-        *budget -= hdr.size();
+        // compressPacketSimulate (T2Compress.cpp:347-434) in its own uint32 arithmetic: the header's
+        // BitIO fails when its byte count reaches the bytes left (BitIO::writeByte, BitIO.cpp:35-52),
+        // a test that never fires when no byte is left (offset starts above 0), so a packet met
+        // with 0 bytes left passes and the subtraction wraps: everything after it fits
+        if (*budget != 0 && (uint64_t)hdr.size() >= *budget) return false;
+        *budget = (uint32_t)(*budget - hdr.size());
     }
     if (o) o->insert(o->end(), hdr.begin(), hdr.end());
     for (size_t bi = 0; bi < R.bands.size(); ++bi) {   // packet body
@@ -1468,7 +1468,7 @@ static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t 
             uint32_t r1 = K.passes[K.passes_in_prev + np - 1].rate;
             if (budget) {
                 if ((uint64_t)(r1 - r0) > *budget) return false;
-                *budget -= (r1 - r0);
+                *budget = (uint32_t)(*budget - (r1 - r0));
             }
             if (o) o->insert(o->end(), K.data.begin() + r0, K.data.begin() + r1);
             K.passes_in_prev += np;

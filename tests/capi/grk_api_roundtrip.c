@@ -5,8 +5,9 @@
  * include/grk_abi.h (layout-identical to grok.h) and linked with libgrok_amd.so by
  * tests/test_gpu_grk_api.py.  Raw files are planar int32 samples, component after component.
  *
- *   enc RAW W H C PREC OUT [-n N] [-b W,H] [-I] [-r R1,R2,..] [-M 64] [-t W,H] [-X] [-L] [-jp2] [-tiles]
- *   dec IN RAWOUT [-d X0,Y0,X1,Y1] [-tile T]
+ *   enc RAW W H C PREC OUT [-n N] [-b W,H] [-I] [-r R1,R2,..] [-M 64] [-t W,H] [-X] [-L] [-jp2] [-tiles] [-file]
+ *   dec IN RAWOUT [-d X0,Y0,X1,Y1] [-tile T] [-r REDUCE] [-l LAYERS] [-mapped]
+ *   dump IN [FLAGS]
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -15,6 +16,7 @@
 #include "grk_abi.h"
 
 static void on_error(const char* msg, void* ud) { (void)ud; fprintf(stderr, "[grk error] %s\n", msg); }
+static void on_warning(const char* msg, void* ud) { (void)ud; fprintf(stderr, "[grk warning] %s\n", msg); }
 
 static int enc(int argc, char** argv) {
     const char* raw = argv[2];
@@ -23,6 +25,9 @@ static int enc(int argc, char** argv) {
     const char* out = argv[7];
     grk_cparameters p;
     grk_compress_set_default_params(&p);
+    p.mct = 255;                    /* pluginMain (grk_compress.cpp:2180-2184): resolved per image below */
+    p.rateControlAlgorithm = 255;
+    int to_file = 0;
     GRK_CODEC_FORMAT fmt = GRK_CODEC_J2K;
     int raw_tiles = 0;
     for (int i = 8; i < argc; ++i) {
@@ -40,15 +45,22 @@ static int enc(int argc, char** argv) {
         else if (!strcmp(argv[i], "-L")) p.writePLT = true;
         else if (!strcmp(argv[i], "-jp2")) fmt = GRK_CODEC_JP2;
         else if (!strcmp(argv[i], "-tiles")) raw_tiles = 1;
+        else if (!strcmp(argv[i], "-file")) to_file = 1;
         else if (!strcmp(argv[i], "-c")) {   /* one precinct size for every resolution: [W,H] */
             unsigned pw, ph;
             sscanf(argv[++i], "[%u,%u]", &pw, &ph);
             p.csty |= 1; p.res_spec = 1; p.prcw_init[0] = pw; p.prch_init[0] = ph;
         }
     }
-    if (c >= 3) p.mct = 1;   /* grk_compress.cpp:1978-1995: RGB input switches the MCT on */
-    grk_initialize(NULL, 0);
-    grk_set_error_handler(on_error, NULL);
+    if (p.mct == 255) p.mct = c >= 3 ? 1 : 0;   /* grk_compress.cpp:1978-1995: RGB input switches the MCT on */
+    if (p.rateControlAlgorithm == 255) p.rateControlAlgorithm = 0;
+    grk_initialize(NULL, p.numThreads);
+    {   /* pluginMain: grk_plugin_init fails without a plugin and the CLI falls back (:2209, :2281-2289) */
+        grk_plugin_init_info initInfo;
+        initInfo.deviceId = p.deviceId;
+        initInfo.verbose = false;
+        if (grk_plugin_init(initInfo)) return 20;
+    }
     grk_image_cmptparm cp[4];
     memset(cp, 0, sizeof cp);
     for (uint32_t k = 0; k < c; ++k) { cp[k].dx = cp[k].dy = 1; cp[k].w = w; cp[k].h = h; cp[k].prec = (uint8_t)prec; }
@@ -62,11 +74,17 @@ static int enc(int argc, char** argv) {
             memcpy(img->comps[k].data + (size_t)y * img->comps[k].stride, row, 4 * w);
         }
     fclose(f);
-    size_t cap = (size_t)w * h * c * 4 + (1 << 20);
-    uint8_t* buf = malloc(cap);
-    grk_stream* st = grk_stream_create_mem_stream(buf, cap, false, false);
+    /* compress() :2055-2066: a memory stream the size of 1.5x the raw image, or the output file */
+    size_t cap = (size_t)w * h * c * ((prec + 7) / 8) * 3 / 2 + (1 << 16);
+    uint8_t* buf = to_file ? NULL : malloc(cap);
+    grk_stream* st = to_file ? grk_stream_create_file_stream(out, 1024 * 1024, false)
+                             : grk_stream_create_mem_stream(buf, cap, false, false);
+    if (!st) return 4;
     grk_codec* codec = grk_compress_create(fmt, st);
-    if (!codec || !grk_compress_init(codec, &p, img) || !grk_compress_start(codec)) return 4;
+    if (!codec) return 4;
+    grk_set_warning_handler(on_warning, NULL);
+    grk_set_error_handler(on_error, NULL);
+    if (!grk_compress_init(codec, &p, img) || !grk_compress_start(codec)) return 4;
     int ok;
     if (raw_tiles) {   /* grk_compress_tile: planar 8/16-bit samples tile by tile */
         uint32_t tw = p.tile_size_on ? p.t_width : w, th = p.tile_size_on ? p.t_height : h;
@@ -87,13 +105,15 @@ static int enc(int argc, char** argv) {
             free(tb);
         }
     } else {
-        ok = grk_compress(codec);
+        ok = grk_compress_with_plugin(codec, NULL);   /* :2112, info->tile is NULL without a plugin */
     }
     if (!ok || !grk_compress_end(codec)) return 5;
-    size_t n = grk_stream_get_write_mem_stream_length(st);
-    f = fopen(out, "wb");
-    fwrite(buf, 1, n, f);
-    fclose(f);
+    if (!to_file) {
+        size_t n = grk_stream_get_write_mem_stream_length(st);
+        f = fopen(out, "wb");
+        fwrite(buf, 1, n, f);
+        fclose(f);
+    }
     grk_object_unref(codec);
     grk_object_unref(st);
     grk_object_unref(&img->obj);
@@ -103,38 +123,60 @@ static int enc(int argc, char** argv) {
     return 0;
 }
 
+/* grk_decompress's call sequence (GrkDecompress::pluginMain grk_decompress.cpp:897-921, then the
+ * CPU fallback main :1590-1613 -> decompress -> preProcess :1041-1295 -> postProcess):
+ *   grk_initialize; grk_plugin_init (false: no plugin, fall back); grk_decompress_set_default_params;
+ *   -d sets dparameters.DA_*; stream; create; handlers; init; read_header; the composited image is
+ *   taken right after the header (:1191) and written out at the end; set_window is called
+ *   UNCONDITIONALLY with the DA values, zeros when -d is absent (:1259); then grk_decompress +
+ *   grk_decompress_end, or grk_decompress_tile for -t. */
 static int dec(int argc, char** argv) {
     const char* in = argv[2];
     const char* out = argv[3];
-    grk_initialize(NULL, 0);
-    grk_set_error_handler(on_error, NULL);
-    grk_dparameters dp;
-    grk_decompress_set_default_params(&dp);
-    int win = 0, tile = -1;
-    uint32_t x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    grk_decompress_parameters params;
+    memset(&params, 0, sizeof params);
+    grk_decompress_set_default_params(&params.core);
+    int mapped = 0;
     for (int i = 4; i < argc; ++i) {
-        if (!strcmp(argv[i], "-d")) { sscanf(argv[++i], "%u,%u,%u,%u", &x0, &y0, &x1, &y1); win = 1; }
-        else if (!strcmp(argv[i], "-tile")) tile = atoi(argv[++i]);
+        if (!strcmp(argv[i], "-d"))
+            sscanf(argv[++i], "%u,%u,%u,%u", &params.core.DA_x0, &params.core.DA_y0, &params.core.DA_x1, &params.core.DA_y1);
+        else if (!strcmp(argv[i], "-tile")) { params.tileIndex = (uint16_t)atoi(argv[++i]); params.nb_tile_to_decompress = 1; }
+        else if (!strcmp(argv[i], "-r")) params.core.cp_reduce = (uint32_t)atoi(argv[++i]);
+        else if (!strcmp(argv[i], "-l")) params.core.cp_layer = (uint16_t)atoi(argv[++i]);
+        else if (!strcmp(argv[i], "-mapped")) mapped = 1;
     }
+    grk_initialize(NULL, 0);
+    grk_plugin_init_info initInfo;
+    initInfo.deviceId = 0;
+    initInfo.verbose = false;
+    if (grk_plugin_init(initInfo)) return 20;   /* no plugin: the CLI takes its CPU-API path */
     const size_t L = strlen(in);
     GRK_CODEC_FORMAT fmt = L > 4 && !strcmp(in + L - 4, ".jp2") ? GRK_CODEC_JP2 : GRK_CODEC_J2K;
-    grk_stream* st = grk_stream_create_file_stream(in, 1 << 20, true);
+    grk_stream* st = mapped ? grk_stream_create_mapped_file_stream(in, true) : grk_stream_create_file_stream(in, 1024 * 1024, true);
+    if (!st) return 6;
     grk_codec* codec = grk_decompress_create(fmt, st);
+    if (!codec) return 6;
+    grk_set_warning_handler(on_warning, NULL);
+    grk_set_error_handler(on_error, NULL);
+    if (!grk_decompress_init(codec, &params.core)) return 6;
     grk_header_info hi;
     memset(&hi, 0, sizeof hi);
-    if (!codec || !grk_decompress_init(codec, &dp) || !grk_decompress_read_header(codec, &hi)) return 6;
+    if (!grk_decompress_read_header(codec, &hi)) return 6;
+    grk_image* img = grk_decompress_get_composited_image(codec);
+    if (!img) return 10;
     fprintf(stdout, "header cblk %ux%u numres %u layers %u irrev %d tiles %ux%u\n", hi.cblockw_init, hi.cblockh_init,
             hi.numresolutions, hi.numlayers, (int)hi.irreversible, hi.t_grid_width, hi.t_grid_height);
-    grk_image* img;
-    if (tile >= 0) {
-        if (!grk_decompress_tile(codec, (uint16_t)tile)) return 7;
-        img = grk_decompress_get_tile_image(codec, (uint16_t)tile);
+    for (uint32_t i = 0; i < img->numcomps; ++i)
+        if (img->comps[i].prec > 16) return 11;
+    if (!grk_decompress_set_window(codec, params.core.DA_x0, params.core.DA_y0, params.core.DA_x1, params.core.DA_y1))
+        return 8;
+    if (!params.nb_tile_to_decompress) {
+        if (!(grk_decompress(codec, NULL) && grk_decompress_end(codec))) return 9;
     } else {
-        if (win && !grk_decompress_set_window(codec, x0, y0, x1, y1)) return 8;
-        if (!grk_decompress(codec, NULL) || !grk_decompress_end(codec)) return 9;
-        img = grk_decompress_get_composited_image(codec);
+        if (!grk_decompress_tile(codec, params.tileIndex)) return 7;
+        if (grk_decompress_get_tile_image(codec, params.tileIndex) != img) return 12;
     }
-    if (!img) return 10;
+    grk_object_unref(st);
     fprintf(stdout, "image %u %u %u %u comps %u\n", img->x0, img->y0, img->x1, img->y1, img->numcomps);
     FILE* f = fopen(out, "wb");
     for (uint32_t k = 0; k < img->numcomps; ++k)
@@ -142,12 +184,36 @@ static int dec(int argc, char** argv) {
             fwrite(img->comps[k].data + (size_t)y * img->comps[k].stride, 4, img->comps[k].w, f);
     fclose(f);
     grk_object_unref(codec);
+    grk_deinitialize();
+    return 0;
+}
+
+/* grk_dump's call sequence (grk_dump.cpp:342-504): initialize, handlers, default params, file
+ * stream, create, init, read_header(codec, NULL), grk_dump_codec, unref.  Needs no GPU. */
+static int dump(int argc, char** argv) {
+    const char* in = argv[2];
+    uint32_t flag = argc >= 4 ? (uint32_t)strtoul(argv[3], NULL, 0) : (GRK_IMG_INFO | GRK_J2K_MH_INFO);
+    grk_initialize(NULL, 0);
+    grk_set_warning_handler(on_warning, NULL);
+    grk_set_error_handler(on_error, NULL);
+    grk_dparameters parameters;
+    grk_decompress_set_default_params(&parameters);
+    grk_stream* st = grk_stream_create_file_stream(in, 1024 * 1024, 1);
+    if (!st) return 30;
+    const size_t L = strlen(in);
+    grk_codec* codec = grk_decompress_create(L > 4 && !strcmp(in + L - 4, ".jp2") ? GRK_CODEC_JP2 : GRK_CODEC_J2K, st);
+    if (!codec) { grk_object_unref(st); return 31; }
+    if (!grk_decompress_init(codec, &parameters)) return 32;
+    if (!grk_decompress_read_header(codec, NULL)) return 33;
+    grk_dump_codec(codec, flag, stdout);
     grk_object_unref(st);
+    grk_object_unref(codec);
     grk_deinitialize();
     return 0;
 }
 
 int main(int argc, char** argv) {
+    if (argc >= 3 && !strcmp(argv[1], "dump")) return dump(argc, argv);
     if (argc >= 8 && !strcmp(argv[1], "enc")) return enc(argc, argv);
     if (argc >= 4 && !strcmp(argv[1], "dec")) return dec(argc, argv);
     fprintf(stderr, "usage: enc RAW W H C PREC OUT [opts] | dec IN RAWOUT [-d x0,y0,x1,y1] [-tile t]\n");

@@ -83,12 +83,12 @@ def test_fullsize_97_vs_grok(eng, name):
 
 def test_fullsize_c3_exact_config_vs_oracle(eng):
     """C3 exactly as BASELINE configures it (8192^2 RGB12, -I -r 40,20,10, single precinct):
-    no Grok hash exists here (Grok is not rebuilt; its decoder is broken on this stream,
-    SURVEY R-BUG-3), so the reference is the Grok-pinned oracle's stream
-    (full_size.json oracle_fullsize.C3, make_oracle_fullsize.py)."""
+    the reference is full_size.json C3: recorded from the oracle by make_oracle_fullsize.py
+    and reproduced byte for byte by Grok 9.2.0's grk_compress in the round-3 review (Grok's
+    decoder is broken on this stream, SURVEY R-BUG-3, so the decode is checked by PSNR)."""
     import torch
     import grok_amd as G
-    cfg = FULL["oracle_fullsize"]["C3"]
+    cfg = FULL["C3"]
     img = _img(cfg)
     params = G.default_params(irreversible=True, layer_rate=[40.0, 20.0, 10.0])
     x = torch.from_numpy(img).cuda()

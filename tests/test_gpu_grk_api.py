@@ -82,3 +82,43 @@ def test_grk_api_compress_tile_raw_samples(tool, name):
     fx = next(f for f in FIXTURES if f.name == name)
     cs, _ = _enc(tool, fx.img, fx.bits, fx.flags, fx.name + "_raw", extra=("-tiles",))
     assert cs == fx.cs
+
+
+def test_grk_api_cli_window_semantics(tool):
+    # grk_decompress.cpp:1259 calls set_window with the -d values or zeros: (0,0,0,0) is the
+    # whole image; right / bottom edges past the image clamp with a warning
+    # (CodeStreamDecompress.cpp:309-316, :355-388); the composited image pointer taken after
+    # the header read is the one decoded into
+    fx = next(f for f in FIXTURES if f.name == "rgb8_tiles_xl")
+    cs, path = _enc(tool, fx.img, fx.bits, fx.flags, fx.name + "_cli")
+    c, h, w = fx.img.shape
+    dec, _ = _dec(tool, path, fx.img.shape, ("-d", "0,0,0,0"))
+    np.testing.assert_array_equal(dec, fx.img)
+    x0, y0 = 17, 33
+    dec, info = _dec(tool, path, (c, h - y0, w - x0), ("-d", "%d,%d,%d,%d" % (x0, y0, w + 100, h + 7)))
+    np.testing.assert_array_equal(dec, fx.img[:, y0:, x0:])
+    assert "image %d %d %d %d" % (x0, y0, w, h) in info
+    # a tile decode crops the composited image to the tile, intersected with the window
+    tw, th = fx.kw["tiles"]
+    dec, info = _dec(tool, path, (c, th - 5, tw - 9), ("-tile", 0, "-d", "9,5,%d,%d" % (w, h)))
+    np.testing.assert_array_equal(dec, fx.img[:, 5:th, 9:tw])
+
+
+@pytest.mark.parametrize("name,red,layers", [("rgb8_64", 2, 0), ("rgb12_97_r", 1, 2), ("rgb8_tiles_xl", 1, 0)])
+def test_grk_api_cli_reduce_and_layers(tool, name, red, layers):
+    # -r / -l through grk_dparameters (cp_reduce, cp_layer), with the CLI's set_window(0,0,0,0)
+    fx = next(f for f in FIXTURES if f.name == name)
+    exe, d = tool
+    p = d / (name + "_rl.j2k")
+    p.write_bytes(fx.cs)
+    c, h, w = fx.img.shape
+    shape = (c, (h + (1 << red) - 1) >> red, (w + (1 << red) - 1) >> red)
+    dec, _ = _dec(tool, p, shape, ("-r", red, "-l", layers))
+    O.set_decode_reduce(red)
+    O.set_decode_layers(layers)
+    try:
+        want, _ = O.decode(fx.cs)
+    finally:
+        O.set_decode_reduce(0)
+        O.set_decode_layers(0)
+    np.testing.assert_array_equal(dec, want)

@@ -133,3 +133,23 @@ def test_ht_rate_control_vs_oracle(eng, tiles):
     cs = eng.encode(img, 8, params=_params(**dict(kw)))
     assert cs == ref
     np.testing.assert_array_equal(eng.decode(cs), img)
+
+
+# The round-3 review's Grok runs on synth_image(384, 520, 3, 8, 7): the oracle equals Grok's
+# sizes on these (tests/test_oracle_grok_sizes.py), so the HIP path must equal the oracle —
+# including the 8-px edge tiles whose simulated budget wraps (T2Compress.cpp:347-434).
+@pytest.mark.parametrize("kw,grok_bytes", [
+    (dict(tiles=(256, 256), layer_rate=[20.0, 5.0], tlm=True), 118560),
+    (dict(tiles=(128, 128), layer_rate=[30.0]), 22142),
+    (dict(tiles=(256, 256), layer_rate=[20.0, 5.0]), None),
+], ids=["t256_r20_5_X", "t128_r30", "t256_r20_5"])
+def test_tiled_rate_control_grok_sizes(eng, kw, grok_bytes):
+    img = _img(7, 3, 384, 520, 8)
+    ref = O.encode(img, 8, **kw)
+    if grok_bytes:
+        assert len(ref) == grok_bytes
+    cs = eng.encode(img, 8, params=_params(**dict(kw)))
+    assert cs == ref
+    dec = eng.decode(cs)
+    want, _ = O.decode(cs)
+    np.testing.assert_array_equal(dec, want)
