@@ -45,7 +45,6 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak
 CLOCK_GHZ = 2.4            # MI355X max engine clock (MI355X_MICROARCH.md)
-DEC_INSTR_PER_STEP = 273   # k_t1_dec2 decision step, gfx950 ISA (python tools/isa_step_count.py)
 METRIC = "Mpixels/s encode+decode, 8K RGB 5/3 lossless + 9/7 lossy, 1/2/4/8 GPU"
 # Grok 9.2.0 on the survey container (8 vCPU), enc+dec Mpix/s
 GROK_CPU = {"C2p_8t": 5.99, "C2p_1t": 1.11, "C3p_8t": 2.87, "C3p_1t": 0.93, "C4_8t": 51.9, "C4_1t": 19.3,
@@ -151,21 +150,23 @@ def cpu_baseline(nthreads):
                                              "single-precinct 8K streams)", **GROK_CPU}}
 
 
-def pmc_traffic(kernels):
-    """HBM bytes per launch of `kernels` from the newest committed PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py from rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this benchmark; FETCH_SIZE doubled per
-    MI355X_MICROARCH.md's gfx950 note).  (None, None) if no summary exists."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+def pmc_traffic(kernels, config="C2"):
+    """HBM bytes per launch of `kernels` from the newest committed PMC summary of this config
+    (profiles/rNN_<config>_pmc.json, written by tools/pmc_summary.py from rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this benchmark, tools/gpu_profile_all.sh; FETCH_SIZE
+    doubled per MI355X_MICROARCH.md's gfx950 note).  (None, None) if no summary exists."""
+    files = [f for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))
+             if os.path.basename(f).lower().endswith("_%s_pmc.json" % config.lower())]
     if not files:
         return None, None
-    d = json.load(open(files[-1]))
+    f = sorted(files, key=lambda p: os.path.basename(p).lower())[-1]
+    d = json.load(open(f))
     tot = 0.0
     for k in kernels:
         if k not in d:
             return None, None
         tot += d[k]["hbm_bytes_per_launch"]
-    return tot, os.path.basename(files[-1])
+    return tot, os.path.basename(f)
 
 
 # ----------------------------------------------------------------------------- runners
@@ -600,18 +601,25 @@ def main():
     if rank == 0:
         # dominant kernel: the T1 stage with the largest average duration, measured with HIP
         # events on the engine stream (encode: k_t1_cm + k_t1_mq, decode: k_t1_dec2 + k_t1_recon)
+        cp = CONFIGS[args.config]["params"]
+        if cp.get("cblk_sty"):   # HTJ2K: one cleanup-pass coder kernel each way
+            dec_k, enc_k = ("T1 decode (k_ht_dec)", ["k_ht_dec"]), ("T1 encode (k_ht_enc)", ["k_ht_enc"])
+        else:
+            dec_k = ("T1 decode (k_t1_dec2 + k_t1_recon)", ["void k_t1_dec2<0>", "k_t1_recon"])
+            cm = "void k_t1_cm<true>" if cp.get("irreversible") else "void k_t1_cm<false>"
+            enc_k = ("T1 encode (k_t1_cm + k_t1_mq)", [cm, "k_t1_mq"])
+        dw = "97" if cp.get("irreversible") else "53"
         stages = {
-            "T1 decode (k_t1_dec2 + k_t1_recon)": (m["dec_t1_ms"], m["dec_t1_bytes"] + 4.0 * samples,
-                                                   ["void k_t1_dec2<0>", "k_t1_recon"]),
-            "T1 encode (k_t1_cm + k_t1_mq)": (m["enc_t1_ms"], 4.0 * samples + m["enc_t1_bytes"],
-                                              ["void k_t1_cm<false>", "k_t1_mq"]),
-            "DWT 5/3 fwd+inv (all levels)": (m["enc_dwt_ms"] + m["dec_dwt_ms"], m["enc_dwt_bytes"] + m["dec_dwt_bytes"],
-                                             ["k_dwt53_fwd_level", "k_dwt53_inv_level"]),
+            dec_k[0]: (m["dec_t1_ms"], m["dec_t1_bytes"] + 4.0 * samples, dec_k[1]),
+            enc_k[0]: (m["enc_t1_ms"], 4.0 * samples + m["enc_t1_bytes"], enc_k[1]),
+            "DWT %s fwd+inv (all levels)" % ("9/7" if dw == "97" else "5/3"):
+                (m["enc_dwt_ms"] + m["dec_dwt_ms"], m["enc_dwt_bytes"] + m["dec_dwt_bytes"],
+                 ["k_dwt%s_fwd_level" % dw, "k_dwt%s_inv_level" % dw]),
         }
         dom = max(stages, key=lambda k: stages[k][0])
         t_ms, nbytes, kern = stages[dom]
         achieved = nbytes / 1e9 / (t_ms / 1e3)
-        traffic, traffic_src = pmc_traffic(kern)
+        traffic, traffic_src = pmc_traffic(kern, args.config)
         dwt_gbs = (m["enc_dwt_bytes"] + m["dec_dwt_bytes"]) / 1e9 / ((m["enc_dwt_ms"] + m["dec_dwt_ms"]) / 1e3)
         res = {
             "metric": METRIC,
@@ -646,12 +654,20 @@ def main():
         if dec_steps and dec_steps[0]:
             # issue roofline of the chain-bound decoder: one wave per SIMD issues one instruction
             # per 4 cycles, so the kernel takes at least (steps of its longest wave) x
-            # (instructions per step) x 4 cycles; DEC_INSTR_PER_STEP from tools/isa_step_count.py
-            floor_ms = dec_steps[0] * DEC_INSTR_PER_STEP * 4 / (CLOCK_GHZ * 1e6)
+            # (instructions per step) x 4 cycles; instructions per step read from the loaded
+            # library's gfx950 code object (tools/isa_step_count.py, ROCm llvm-objdump)
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import isa_step_count
+            import grok_amd as G
+            _, dec_ips, dec_by = isa_step_count.count_so(G.LIB_PATH)
+            dec_ips = int(dec_ips)
+            floor_ms = dec_steps[0] * dec_ips * 4 / (CLOCK_GHZ * 1e6)
             dec2_ms = m.get("dec_t1_coder_ms", m["dec_t1_ms"])
             res["issue_roofline"] = {
                 "kernel": "k_t1_dec2 (T1 decode chain)", "bound": "instruction issue of the longest wave",
-                "max_steps_per_wave": dec_steps[0], "instructions_per_step": DEC_INSTR_PER_STEP,
+                "max_steps_per_wave": dec_steps[0], "instructions_per_step": dec_ips,
+                "instructions_per_step_source": "llvm-objdump of %s (k_t1_dec2<0> step bodies: %s)" % (
+                    os.path.relpath(G.LIB_PATH, ROOT), ", ".join("%s %d" % kv for kv in dec_by.items())),
                 "clock_ghz": CLOCK_GHZ, "floor_ms": round(floor_ms, 3), "measured_ms": round(dec2_ms, 3),
                 "frac": round(floor_ms / dec2_ms, 3), "steps_total": dec_steps[1], "symbols": dec_steps[2],
                 "lane_efficiency": round(dec_steps[2] / (64.0 * dec_steps[1]), 3) if dec_steps[1] else None}
