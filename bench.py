@@ -245,184 +245,148 @@ class BatchRunner:
 
 
 class ShardRunner:
-    """C4 on N ranks: tile rows split across ranks (grok_amd/shard.py).  One step =
-    every rank encodes its tiles from its slab (HBM -> tile parts in HBM); the tile-part
-    lengths are all-gathered; rank 0 gathers the payloads (RCCL) and assembles the
-    codestream in HBM under the main header with its TLM filled; every rank decodes its
-    own tile parts (main header with a TLM listing just those parts) back into its slab."""
+    """C4 on N ranks through grok_amd.shard.TileRowShard: rank 0 holds the
+    16-bit image in HBM.  One step = rank 0 scatters the tile rows (RCCL) -> every rank
+    encodes its tiles -> rank 0 gathers the tile parts and assembles the codestream (main
+    header, TLM filled) -> rank 0 locates each rank's tile parts through TLM and scatters them
+    -> every rank decodes its rows -> rank 0 gathers the decoded rows.  Samples travel as
+    16-bit (u16 held in int16 tensors, the engine's 2-byte sample type).
+    coder: per-rank coder (grok_amd.shard.EngineCoder by default; tests pass the CPU oracle)."""
 
-    def __init__(self, name, size, rank, world, device, dist):
+    def __init__(self, name, size, rank, world, device, dist, coder=None):
         import torch
-        import grok_amd as G
         from grok_amd import shard
         from grok_amd.synth import synth_slab
         cfg = CONFIGS[name]
         size = size or cfg["size"]
         self.name, self.cfg, self.size, self.rank, self.world, self.dist = name, cfg, size, rank, world, dist
         self.device = device
-        tw, th = cfg["params"]["tiles"]
-        self.ntx, self.nty = shard.tile_grid(size, size, th, tw)
-        self.tb, self.te, j0, j1 = shard.rank_tiles(self.ntx, self.nty, rank, world)
-        if self.te <= self.tb:
-            raise SystemExit("C4 sharding needs at least one tile row per rank")
-        self.maxt = max(shard.rank_tiles(self.ntx, self.nty, r, world)[1] - shard.rank_tiles(self.ntx, self.nty, r, world)[0]
-                        for r in range(world))
-        self.y0, self.y1 = j0 * th, min(size, j1 * th)
-        slab = synth_slab(self.y0, self.y1, size, size, cfg["comps"], cfg["bits"], cfg["seed"])
-        self.x = torch.from_numpy(slab.astype(np.int32)).to(device).contiguous()
+        C, bits = cfg["comps"], cfg["bits"]
+        shape = (C, size, size)
+        if coder is None:
+            import grok_amd as G
+            self.eng = G.Engine(device.index or 0)
+            coder = shard.EngineCoder(self.eng, shape, bits, G.default_params(**cfg["params"]))
+        else:
+            self.eng = None
+        self.coder = coder
+        self.sh = shard.TileRowShard(dist, rank, world, coder, shape, cfg["params"]["tiles"], device)
+        dt = torch.int16 if bits > 8 else torch.uint8
+        self.full = self.y_full = None
+        if rank == 0:
+            self.full = torch.empty(shape, dtype=dt, device=device)
+            th = cfg["params"]["tiles"][1]
+            for y0 in range(0, size, th):   # rank 0's image, generated by tile rows
+                y1 = min(size, y0 + th)
+                sl = synth_slab(y0, y1, size, size, C, bits, cfg["seed"])
+                sl = sl.view(np.int16) if bits > 8 else sl.astype(np.uint8)
+                self.full[:, y0:y1] = torch.from_numpy(np.ascontiguousarray(sl)).to(device)
+            self.y_full = torch.empty_like(self.full)
+        self.y0, self.y1 = self.sh.y0, self.sh.y1
+        self.x = torch.empty((C, self.y1 - self.y0, size), dtype=dt, device=device)
         self.y = torch.empty_like(self.x)
-        self.eng = G.Engine(device.index or 0)
-        self.params = G.default_params(**cfg["params"])
-        self.hdr, self.tlm, _ = self.eng.main_header((cfg["comps"], size, size), cfg["bits"], params=self.params)
-        self.eoc = torch.tensor([0xFF, 0xD9], dtype=torch.uint8, device=device)
-        self.parts = torch.empty(self.x.numel() * 4 + (1 << 22), dtype=torch.uint8, device=device)
+        self.parts = torch.empty(max(self.x.numel() * 4, 1) + (1 << 22), dtype=torch.uint8, device=device)
         self.n = 0
         self.cs = None
         self.pixels = size * size
 
+    def _timings(self):
+        return self.eng.timings() if self.eng is not None else None
+
     def step(self):
-        import struct
-        import torch
-        from grok_amd import shard
-        n, lens = self.eng.encode_tiles(self.x, self.cfg["bits"], self.tb, self.te, image_hw=(self.size, self.size),
-                                        row0=self.y0, params=self.params, out=self.parts)
-        te = self.eng.timings()
-        # tile-part lengths of every rank (padded to the largest tile count), then payloads to rank 0
-        ln = torch.zeros(self.maxt + 1, dtype=torch.int64, device=self.device)
-        ln[0] = n
-        ln[1:1 + len(lens)] = torch.tensor(lens, dtype=torch.int64)
-        lns = [torch.zeros_like(ln) for _ in range(self.world)]
-        self.dist.all_gather(lns, ln)
-        lns = [v.cpu().tolist() for v in lns]
-        mx = int(max(v[0] for v in lns))
-        payload = self.parts[:mx]
-        if self.rank == 0:
-            bufs = [torch.empty(mx, dtype=torch.uint8, device=self.device) for _ in range(self.world)]
-            self.dist.gather(payload, bufs, dst=0)
-            h = bytearray(self.hdr)
-            if self.tlm:
-                for r in range(self.world):
-                    rtb, rte, _, _ = shard.rank_tiles(self.ntx, self.nty, r, self.world)
-                    for k in range(rte - rtb):
-                        t = rtb + k
-                        h[self.tlm + 6 * t:self.tlm + 6 * t + 6] = struct.pack(">HI", t, int(lns[r][1 + k]))
-            hd = torch.frombuffer(h, dtype=torch.uint8).to(self.device)
-            self.cs = torch.cat([hd] + [b[:int(v[0])] for b, v in zip(bufs, lns)] + [self.eoc])
-            self.n = int(self.cs.numel())
-        else:
-            self.dist.gather(payload, None, dst=0)
-        # each rank decodes its own tile parts: main header with a TLM of just those parts
-        sub_hdr = shard.retlm(self.hdr, [(self.tb + k, int(v)) for k, v in enumerate(lens)])
-        sh = torch.frombuffer(bytearray(sub_hdr), dtype=torch.uint8).to(self.device)
-        sub = torch.cat([sh, self.parts[:n], self.eoc])
-        self.eng.decode(sub, length=int(sub.numel()), out=self.y, row0=self.y0)
-        td = self.eng.timings()
-        return te, td
+        self.sh.scatter_input(self.full, self.x)
+        self.cs, self.n = self.sh.encode(self.x, self.parts)
+        te = self._timings()
+        self.sh.decode(self.cs, self.n, self.y, self.y_full)
+        td = self._timings()
+        return (te, td) if te is not None else {}
 
     def check(self):
         import torch
         self.step()
-        torch.cuda.synchronize()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
         if not torch.equal(self.x, self.y):
-            raise SystemExit("sharded lossless round trip FAILED (%s)" % self.name)
-        if self.rank == 0 and self.tlm:
-            # the assembled stream is a valid codestream: decode a few tiles from it through its TLM
-            probe = torch.empty((self.x.shape[0], 64, 64), dtype=torch.int32, device=self.device)
-            self.eng.decode_window(self.cs, (0, 0, 64, 64), length=self.n, out=probe)
-            if not torch.equal(probe, self.x[:, :64, :64]):
-                raise SystemExit("assembled sharded codestream does not decode (%s)" % self.name)
+            raise SystemExit("sharded lossless round trip FAILED (%s, rank %d rows)" % (self.name, self.rank))
+        if self.rank == 0 and not torch.equal(self.full, self.y_full):
+            raise SystemExit("sharded lossless round trip FAILED (%s, gathered image)" % self.name)
         return None
 
     def close(self):
-        self.eng.close()
+        if self.eng is not None:
+            self.eng.close()
 
 
 class C5Runner:
-    """C5: decode-only random windows of a 32768^2 RGB8 tiled .jp2 held in HBM.  Rank 0
-    builds the file on its GPU from tile-row slabs (grok_amd.bigimage) and broadcasts it
-    (a shared file); one step decodes the four SURVEY windows.  With N ranks the tile rows
-    of each window are split into contiguous ranges, each rank decodes its band of the
-    window (TLM finds the tiles, PLT the packets, out-of-reach code-blocks are skipped)
-    into u8 planes, and rank 0 gathers the bands."""
+    """C5: decode-only random windows of a tiled RGB8 .jp2 held in rank 0's HBM (built on its
+    GPU from tile-row slabs, grok_amd.bigimage).  One step decodes the four SURVEY windows
+    through grok_amd.shard.WindowShard: with N ranks each window's tile rows are split into
+    bands, rank 0 scatters to each rank the tile parts its band needs (located through TLM;
+    no rank holds the whole file), every rank decodes its band into u8 planes and rank 0
+    gathers the bands.  size / windows / coder / file: overrides for the CPU tests."""
 
-    def __init__(self, rank, world, device, dist):
+    def __init__(self, rank, world, device, dist, size=None, windows=None, coder=None, file=None, n=0):
         import torch
-        import grok_amd as G
-        from grok_amd import bigimage
+        from grok_amd import shard
         cfg = CONFIGS["C5"]
         self.cfg, self.rank, self.world, self.device, self.dist = cfg, rank, world, device, dist
-        S = cfg["size"]
-        self.eng = G.Engine(device.index or 0)
-        p = G.default_params(**cfg["params"])
+        S = size or cfg["size"]
+        self.windows = windows or C5_WINDOWS
         self.crops = None
+        self.eng = None
         t0 = time.perf_counter()
-        if rank == 0:
-            it = bigimage.slabs(S, S, cfg["comps"], cfg["bits"], cfg["seed"], 1024, threads=16)
-            crops = {k: w for k, w in enumerate(C5_WINDOWS)}
-            self.file, self.n, self.crops = bigimage.encode_tiled(self.eng, (cfg["comps"], S, S), cfg["bits"], p, it,
-                                                                  device, crops=crops)
+        if coder is None:
+            import grok_amd as G
+            from grok_amd import bigimage
+            self.eng = G.Engine(device.index or 0)
+            p = G.default_params(**cfg["params"])
+            coder = shard.EngineCoder(self.eng, (cfg["comps"], S, S), cfg["bits"], p)
+            if rank == 0:
+                it = bigimage.slabs(S, S, cfg["comps"], cfg["bits"], cfg["seed"], 1024, threads=16)
+                crops = {k: w for k, w in enumerate(self.windows)}
+                file, n, self.crops = bigimage.encode_tiled(self.eng, (cfg["comps"], S, S), cfg["bits"], p, it,
+                                                            device, crops=crops)
+        self.file, self.n = file, n
         self.build_s = time.perf_counter() - t0
+        self.ws = shard.WindowShard(dist, rank, world, coder, device, file if rank == 0 else None, n)
+        nb = torch.zeros(1, dtype=torch.int64, device=device)
+        if rank == 0:
+            nb[0] = n
         if world > 1:
-            n = torch.tensor([self.n if rank == 0 else 0], dtype=torch.int64, device=device)
-            dist.broadcast(n, 0)
-            if rank != 0:
-                self.n = int(n.item())
-                self.file = torch.empty(self.n, dtype=torch.uint8, device=device)
-            dist.broadcast(self.file[:self.n], 0)
-        self.pixels = sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in C5_WINDOWS)
-        self.outs = [torch.empty((3, y1 - y0, x1 - x0), dtype=torch.uint8, device=device)
-                     for x0, y0, x1, y1 in C5_WINDOWS]
-        self.bands = [self._band(w) for w in C5_WINDOWS]
-
-    def _band(self, win):
-        x0, y0, x1, y1 = win
-        j0, j1 = y0 // 1024, (y1 - 1) // 1024 + 1
-        per, extra = divmod(j1 - j0, self.world)
-        rows = []
-        for r in range(self.world):
-            a = j0 + r * per + min(r, extra)
-            b = a + per + (1 if r < extra else 0)
-            rows.append((max(y0, a * 1024), min(y1, b * 1024)) if b > a else (y0, y0))
-        return rows
+            dist.broadcast(nb, 0)
+        self.n = int(nb.item())
+        self.pixels = sum((x1 - x0) * (y1 - y0) for x0, y0, x1, y1 in self.windows)
+        self.outs, self.bufs = [], []
+        for w in self.windows:
+            x0, y0, x1, y1 = w
+            hmax = max(b - a for a, b in self.ws.bands(w))
+            self.outs.append(torch.empty((3, y1 - y0, x1 - x0), dtype=torch.uint8, device=device) if rank == 0 else None)
+            self.bufs.append(torch.empty((3, max(hmax, 1), x1 - x0), dtype=torch.uint8, device=device)
+                             if rank != 0 else None)
 
     def step(self):
-        import torch
         acc = {}
-        for k, (x0, y0, x1, y1) in enumerate(C5_WINDOWS):
-            ry0, ry1 = self.bands[k][self.rank]
-            out = self.outs[k]
-            if ry1 > ry0:
-                self.eng.decode_window(self.file, (x0, ry0, x1, ry1), length=self.n, out=out[:, ry0 - y0:ry1 - y0])
+        for k, w in enumerate(self.windows):
+            self.ws.decode(w, self.outs[k], self.bufs[k])
+            if self.eng is not None:
                 t = self.eng.timings()
                 for f in ("t1_ms", "dwt_ms", "mct_ms", "t2_ms", "total_ms"):
                     acc["dec_" + f] = acc.get("dec_" + f, 0.0) + float(getattr(t, f))
-            if self.world > 1:
-                # rank 0 gathers the window's row bands (padded to the tallest band)
-                hmax = max(b - a for a, b in self.bands[k])
-                pad = torch.zeros((3, hmax, x1 - x0), dtype=torch.uint8, device=self.device)
-                if ry1 > ry0:
-                    pad[:, :ry1 - ry0] = out[:, ry0 - y0:ry1 - y0]
-                if self.rank == 0:
-                    bufs = [torch.empty_like(pad) for _ in range(self.world)]
-                    self.dist.gather(pad, bufs, dst=0)
-                    for r, (a, b) in enumerate(self.bands[k]):
-                        if b > a and r:
-                            out[:, a - y0:b - y0] = bufs[r][:, :b - a]
-                else:
-                    self.dist.gather(pad, None, dst=0)
         return acc
 
     def check(self):
         import torch
         self.step()
-        torch.cuda.synchronize()
-        if self.rank == 0:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        if self.rank == 0 and self.crops is not None:
             for k, o in enumerate(self.outs):
                 if not np.array_equal(o.cpu().numpy(), self.crops[k]):
-                    raise SystemExit("C5 window %s decode differs from the source" % (C5_WINDOWS[k],))
+                    raise SystemExit("C5 window %s decode differs from the source" % (self.windows[k],))
 
     def close(self):
-        self.eng.close()
+        if self.eng is not None:
+            self.eng.close()
 
 
 def timed(r, steps, warmup, world, dist, device, sync=True):
@@ -573,7 +537,9 @@ def main():
         aux["C4"] = {"config": "C4: " + CONFIGS["C4"]["desc"], "value": round(S4 * S4 / 1e6 * 3 / el4, 3),
                      "unit": "Mpixels/s", "ms_per_step": round(el4 * 1000.0 / 3, 3),
                      "codestream_bytes": int(r4.n),
-                     "parallelism": ("tile rows sharded over %d ranks, RCCL gather of tile parts to rank 0" % world)
+                     "parallelism": ("tile rows sharded over %d ranks (grok_amd.shard.TileRowShard): RCCL scatter of "
+                                     "the 16-bit rows from rank 0, gather of the tile parts, scatter of the "
+                                     "TLM-located parts, gather of the decoded rows" % world)
                      if world > 1 else "1 GPU, all 256 tiles batched",
                      "scaling": "strong",
                      "stages_ms": {k: round(v, 3) for k, v in m4.items() if k.endswith("_ms") and v > 0},
@@ -588,7 +554,9 @@ def main():
             aux["C5"] = {"config": "C5: " + CONFIGS["C5"]["desc"], "value": round(r5.pixels / 1e6 * 3 / el5, 3),
                          "unit": "Mpixels/s (window output samples)", "ms_per_step": round(el5 * 1000.0 / 3, 3),
                          "window_mpix_per_step": round(r5.pixels / 1e6, 3), "file_bytes": int(r5.n),
-                         "parallelism": ("each window's tile rows split over %d ranks, RCCL gather of the rows" % world)
+                         "parallelism": ("each window's tile rows split over %d ranks (grok_amd.shard.WindowShard): "
+                                         "RCCL scatter of the TLM-located tile parts each band needs, gather of the "
+                                         "decoded rows" % world)
                          if world > 1 else "1 GPU",
                          "scaling": "strong", "build_s": round(r5.build_s, 1),
                          "stages_ms_rank0": {k: round(v, 3) for k, v in m5.items() if v > 0},

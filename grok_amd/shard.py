@@ -214,3 +214,367 @@ def decode_sharded(dist, rank, world, cs, decode, ntx, nty, th, shape, device=No
         return full
     dist.gather(pad, None, dst=0)
     return None
+
+
+# ------------------------------------------------------- device-resident sharding (bench / drop-in)
+# The classes below keep every byte in device tensors (torch uint8 on the rank's GPU, or CPU
+# tensors under gloo in the tests): collectives move tensors, and only a codestream's main
+# header (a few KiB) is read on the host.  A "coder" does the per-rank coding:
+#   main_header() -> (header bytes, TLM entry offset or 0)
+#   encode_tiles(x_slab, tile_begin, tile_end, row0, out) -> (bytes written to out, [Psot per tile])
+#   decode_rows(sub, n, out_slab, row0)        sub: header + the rank's tile parts + EOC
+#   decode_window(cs, n, window, out)          window = (x0, y0, x1, y1)
+# EngineCoder (below) runs the HIP engine; tests/test_shard.py drives the same classes with the
+# CPU oracle standing in.
+SIZ = 0xFF51
+
+
+def parse_main_header(head):
+    """A codestream's main header from its first bytes: (length = offset of the first SOT,
+    SIZ fields {w, h, tw, th, nc}, [(tile, Psot)] from its TLM markers in order).
+    TLM field widths follow Stlm (TileLengthMarkers::read, cache/LengthCache.cpp): ST = 0
+    (tiles in order), 1 (u8) or 2 (u16) tile indices; SP = 0 (u16) or 1 (u32) lengths."""
+    h = bytes(head)
+    i, siz, entries = 2, None, []
+    while i + 4 <= len(h):
+        m, L = struct.unpack(">HH", h[i:i + 4])
+        if m == SOT:
+            if siz is None:
+                raise ValueError("main header without SIZ")
+            return i, siz, entries
+        if i + 2 + L > len(h):
+            break
+        if m == SIZ:
+            w, hh, x0, y0, tw, th, tx0, ty0, nc = struct.unpack(">IIIIIIIIH", h[i + 6:i + 40])
+            siz = dict(w=w - x0, h=hh - y0, tw=tw, th=th, nc=nc)
+        elif m == TLM:
+            stlm = h[i + 5]
+            st, sp = (stlm >> 4) & 3, (stlm >> 6) & 1
+            j, tnext = i + 6, entries[-1][0] + 1 if entries else 0
+            while j < i + 2 + L:
+                if st == 0:
+                    t = tnext
+                elif st == 1:
+                    t = h[j]
+                    j += 1
+                else:
+                    t = struct.unpack(">H", h[j:j + 2])[0]
+                    j += 2
+                if sp:
+                    n = struct.unpack(">I", h[j:j + 4])[0]
+                    j += 4
+                else:
+                    n = struct.unpack(">H", h[j:j + 2])[0]
+                    j += 2
+                entries.append((t, n))
+                tnext = t + 1
+        i += 2 + L
+    raise ValueError("the main header does not end within %d bytes" % len(h))
+
+
+def codestream_start(head):
+    """Offset of the codestream in a .jp2 (the jp2c box contents) or 0 for a raw codestream."""
+    h = bytes(head)
+    if h[:2] == b"\xff\x4f":
+        return 0
+    i = 0
+    while i + 8 <= len(h):
+        lbox, tbox = struct.unpack(">I4s", h[i:i + 8])
+        hl = 8
+        if lbox == 1:
+            lbox, hl = struct.unpack(">Q", h[i + 8:i + 16])[0], 16
+        if tbox == b"jp2c":
+            return i + hl
+        if lbox == 0:
+            break
+        i += lbox
+    raise ValueError("no jp2c box in the first %d bytes" % len(h))
+
+
+def _read_header(cs, n):
+    """(codestream offset, header length, SIZ, TLM entries, header bytes) of the stream held in
+    the uint8 tensor cs[:n]; only the header bytes are copied to the host."""
+    k = min(n, 1 << 16)
+    while True:
+        head = cs[:k].cpu().numpy().tobytes()
+        try:
+            off = codestream_start(head)
+            hl, siz, ent = parse_main_header(head[off:])
+            return off, hl, siz, ent, head[off:off + hl]
+        except (ValueError, struct.error):
+            if k >= n:
+                raise
+            k = min(n, 4 * k)
+
+
+def _tensor(b, device):
+    import torch
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(device)
+
+
+def _scatter_tensors(dist, rank, world, parts, device):
+    """Rank 0's list of per-rank uint8 tensors to every rank (lengths, then the payloads padded
+    to the longest): returns (this rank's buffer, its length)."""
+    import torch
+    n = torch.zeros(1, dtype=torch.int64, device=device)
+    dist.scatter(n, [torch.tensor([int(p.numel())], dtype=torch.int64, device=device) for p in parts]
+                 if rank == 0 else None, src=0)
+    mx = n.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    mx = max(int(mx.item()), 1)
+    buf = torch.empty(mx, dtype=torch.uint8, device=device)
+    if rank == 0:
+        srcs = []
+        for p in parts:
+            if p.numel() == mx:
+                srcs.append(p.contiguous())
+            else:
+                t = torch.zeros(mx, dtype=torch.uint8, device=device)
+                t[:p.numel()] = p
+                srcs.append(t)
+        dist.scatter(buf, srcs, src=0)
+    else:
+        dist.scatter(buf, None, src=0)
+    return buf, int(n.item())
+
+
+def _as_bytes(t):
+    """A sample tensor viewed as bytes along its last axis: the collectives move uint8 (RCCL has
+    no 16-bit integer type; gloo none either)."""
+    import torch
+    return t if t is None or t.element_size() == 1 else t.view(torch.uint8)
+
+
+def _gather_rows(dist, rank, world, slab, rows, bands, full):
+    """Each rank's (C, rows, W) slab into rank 0's `full` at its row band [a, b) (padded to the
+    tallest band for the collective)."""
+    import torch
+    slab, full = _as_bytes(slab), _as_bytes(full)
+    hmax = max(max(b - a for a, b in bands), 1)
+    if rows == hmax and slab.shape[1] == hmax:
+        pad = slab.contiguous()
+    else:
+        pad = torch.zeros((slab.shape[0], hmax, slab.shape[2]), dtype=slab.dtype, device=slab.device)
+        if rows:
+            pad[:, :rows] = slab[:, :rows]
+    if rank == 0:
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.gather(pad, bufs, dst=0)
+        y0 = bands[0][0]
+        for r, (a, b) in enumerate(bands):
+            if b > a and (r or full.data_ptr() != slab.data_ptr()):
+                full[:, a - y0:b - y0] = bufs[r][:, :b - a]
+    else:
+        dist.gather(pad, None, dst=0)
+
+
+class TileRowShard:
+    """A tiled image (single tile-part tiles) coded on `world` ranks, tile rows split into
+    contiguous ranges.
+
+    encode(x_slab): every rank codes its tiles from its row slab; the tile-part lengths are
+    all-gathered and rank 0 gathers the payloads and writes main header (TLM filled) + tile
+    parts in tile order + EOC: the codestream equals a one-GPU encode byte for byte.
+    decode(cs, n, out_slab, full): rank 0 reads the main header of its codestream, locates
+    every tile part through TLM (no SOT walk), and scatters to each rank a sub-stream (main
+    header with a TLM of just its parts + those parts + EOC); each rank decodes its rows into
+    out_slab and rank 0 gathers the row slabs into `full`.
+    scatter_input(full, slab): rank 0's image rows to every rank's slab."""
+
+    def __init__(self, dist, rank, world, coder, shape, tile_hw, device):
+        import torch
+        self.dist, self.rank, self.world, self.coder, self.device = dist, rank, world, coder, device
+        self.C, self.H, self.W = shape
+        self.tw, self.th = tile_hw
+        self.ntx, self.nty = tile_grid(self.H, self.W, self.th, self.tw)
+        self.ranges = [rank_tiles(self.ntx, self.nty, r, world) for r in range(world)]
+        self.tb, self.te = self.ranges[rank][:2]
+        self.bands = [(min(self.H, j0 * self.th), min(self.H, j1 * self.th)) for _, _, j0, j1 in self.ranges]
+        self.y0, self.y1 = self.bands[rank]
+        self.maxt = max(max(te - tb for tb, te, _, _ in self.ranges), 1)
+        self.hdr, self.tlm = coder.main_header()
+        self.hdr_t = _tensor(self.hdr, device)
+        self.eoc = torch.tensor([0xFF, 0xD9], dtype=torch.uint8, device=device)
+
+    def scatter_input(self, full, slab):
+        """full: rank 0's (C, H, W) image; slab: this rank's (C, y1-y0, W) rows."""
+        import torch
+        if self.world == 1:
+            if slab.data_ptr() != full.data_ptr():
+                slab.copy_(full)
+            return
+        hmax = max(max(b - a for a, b in self.bands), 1)
+        slab, full = _as_bytes(slab), _as_bytes(full)
+        buf = torch.empty((self.C, hmax, slab.shape[2]), dtype=torch.uint8, device=self.device)
+        srcs = None
+        if self.rank == 0:
+            srcs = []
+            for a, b in self.bands:
+                t = torch.zeros_like(buf)
+                t[:, :b - a] = full[:, a:b]
+                srcs.append(t)
+        self.dist.scatter(buf, srcs, src=0)
+        slab.copy_(buf[:, :self.y1 - self.y0])
+
+    def encode(self, x_slab, parts):
+        """Returns (codestream tensor, length) on rank 0, (None, length) elsewhere."""
+        import torch
+        n, lens = self.coder.encode_tiles(x_slab, self.tb, self.te, self.y0, parts) if self.te > self.tb else (0, [])
+        if self.world == 1:
+            h = bytearray(self.hdr)
+            if self.tlm:
+                for k, v in enumerate(lens):
+                    h[self.tlm + 6 * (self.tb + k):self.tlm + 6 * (self.tb + k) + 6] = struct.pack(">HI", self.tb + k, int(v))
+            cs = torch.cat([_tensor(h, self.device), parts[:n], self.eoc])
+            return cs, int(cs.numel())
+        ln = torch.zeros(self.maxt + 1, dtype=torch.int64, device=self.device)
+        ln[0] = n
+        if lens:
+            ln[1:1 + len(lens)] = torch.tensor(lens, dtype=torch.int64)
+        lns = [torch.zeros_like(ln) for _ in range(self.world)]
+        self.dist.all_gather(lns, ln)
+        lns = [v.cpu().tolist() for v in lns]
+        mx = max(int(max(v[0] for v in lns)), 1)
+        payload = parts[:mx]
+        if self.rank != 0:
+            self.dist.gather(payload, None, dst=0)
+            return None, 0
+        bufs = [torch.empty(mx, dtype=torch.uint8, device=self.device) for _ in range(self.world)]
+        self.dist.gather(payload, bufs, dst=0)
+        h = bytearray(self.hdr)
+        if self.tlm:
+            for r, (tb, te, _, _) in enumerate(self.ranges):
+                for k in range(te - tb):
+                    h[self.tlm + 6 * (tb + k):self.tlm + 6 * (tb + k) + 6] = struct.pack(">HI", tb + k, int(lns[r][1 + k]))
+        cs = torch.cat([_tensor(h, self.device)] + [b[:int(v[0])] for b, v in zip(bufs, lns)] + [self.eoc])
+        return cs, int(cs.numel())
+
+    def substreams(self, cs, n):
+        """Rank 0: per-rank sub-streams of the codestream cs[:n], located through its TLM."""
+        off, hl, siz, ent, hdr = _read_header(cs, n)
+        if not ent:
+            raise ValueError("sharded decode needs a TLM marker to locate the tile parts")
+        pos, where = off + hl, {}
+        for t, L in ent:
+            where.setdefault(t, []).append((pos, L))
+            pos += L
+        subs = []
+        for tb, te, _, _ in self.ranges:
+            mine = [(t, p, L) for t in range(tb, te) for p, L in where.get(t, [])]
+            if not mine:
+                subs.append(cs[:0])
+                continue
+            # a rank's tiles are contiguous in the stream: one slice
+            a, b = mine[0][1], mine[-1][1] + mine[-1][2]
+            subs.append(torch_cat([_tensor(retlm(hdr, [(t, L) for t, _, L in mine]), cs.device), cs[a:b], self.eoc]))
+        return subs
+
+    def decode(self, cs, n, out_slab, full=None, gather=True):
+        """cs[:n] on rank 0 (ignored elsewhere); out_slab: this rank's (C, y1-y0, W) rows;
+        gather (the same on every rank): rank 0 collects the slabs into full, its (C, H, W)."""
+        if self.world == 1:
+            self.coder.decode_rows(cs, n, out_slab, self.y0)
+            if gather and full is not None and full.data_ptr() != out_slab.data_ptr():
+                full.copy_(out_slab)
+            return
+        subs = self.substreams(cs, n) if self.rank == 0 else None
+        sub, m = _scatter_tensors(self.dist, self.rank, self.world, subs, self.device)
+        if self.y1 > self.y0:
+            self.coder.decode_rows(sub, m, out_slab, self.y0)
+        if gather:
+            _gather_rows(self.dist, self.rank, self.world, out_slab, self.y1 - self.y0, self.bands, full)
+
+
+def torch_cat(ts):
+    import torch
+    return torch.cat(ts)
+
+
+class WindowShard:
+    """Random-access window decode of a tiled codestream / .jp2 held on rank 0 (C5): the window's
+    tile rows are split into contiguous bands, one per rank; rank 0 locates the tile parts each
+    band needs through TLM and scatters them (main header with a TLM of just those parts + the
+    parts + EOC) — no rank holds the whole file; each rank decodes its band of the window
+    (PLT finds the packets, out-of-reach code-blocks are skipped) and rank 0 gathers the bands."""
+
+    def __init__(self, dist, rank, world, coder, device, file=None, n=0):
+        import torch
+        self.dist, self.rank, self.world, self.coder, self.device = dist, rank, world, coder, device
+        self.file, self.n = file, n
+        self.eoc = torch.tensor([0xFF, 0xD9], dtype=torch.uint8, device=device)
+        if rank == 0:
+            off, hl, siz, ent, hdr = _read_header(file, n)
+            self.hdr, self.siz = hdr, siz
+            pos, self.where = off + hl, {}
+            for t, L in ent:
+                self.where.setdefault(t, []).append((pos, L))
+                pos += L
+            if not ent:
+                raise ValueError("window sharding needs a TLM marker")
+        meta = torch.zeros(3, dtype=torch.int64, device=device)
+        if rank == 0:
+            meta[:] = torch.tensor([self.siz["tw"], self.siz["th"], self.siz["w"]])
+        if world > 1:
+            dist.broadcast(meta, 0)
+        self.tw, self.th, self.W = (int(v) for v in meta.tolist())
+
+    def bands(self, win):
+        x0, y0, x1, y1 = win
+        j0, j1 = y0 // self.th, (y1 - 1) // self.th + 1
+        per, extra = divmod(j1 - j0, self.world)
+        out = []
+        for r in range(self.world):
+            a = j0 + r * per + min(r, extra)
+            b = a + per + (1 if r < extra else 0)
+            out.append((max(y0, a * self.th), min(y1, b * self.th)) if b > a else (y0, y0))
+        return out
+
+    def decode(self, win, out, band_buf=None):
+        """out: rank 0's (C, y1-y0, x1-x0) window; band_buf: a (C, >= tallest band, x1-x0) buffer
+        on the other ranks (rank 0 decodes its band straight into out)."""
+        x0, y0, x1, y1 = win
+        if self.world == 1:
+            self.coder.decode_window(self.file, self.n, win, out)
+            return
+        bands = self.bands(win)
+        subs = None
+        if self.rank == 0:
+            ntx = (self.W + self.tw - 1) // self.tw
+            i0, i1 = x0 // self.tw, (x1 - 1) // self.tw + 1
+            subs = []
+            for a, b in bands:
+                if b <= a:
+                    subs.append(self.file[:0])
+                    continue
+                tiles = [j * ntx + i for j in range(a // self.th, (b - 1) // self.th + 1) for i in range(i0, i1)]
+                mine = [(t, p, L) for t in tiles for p, L in self.where.get(t, [])]
+                subs.append(torch_cat([_tensor(retlm(self.hdr, [(t, L) for t, _, L in mine]), self.device)] +
+                                      [self.file[p:p + L] for _, p, L in mine] + [self.eoc]))
+        sub, m = _scatter_tensors(self.dist, self.rank, self.world, subs, self.device)
+        a, b = bands[self.rank]
+        dst = out[:, a - y0:b - y0] if self.rank == 0 else band_buf[:, :b - a]
+        if b > a:
+            self.coder.decode_window(sub, m, (x0, a, x1, b), dst)
+        slab = out[:, a - y0:b - y0] if self.rank == 0 else band_buf
+        _gather_rows(self.dist, self.rank, self.world, slab, b - a, bands, out if self.rank == 0 else None)
+
+
+class EngineCoder:
+    """The coder interface over a grok_amd.Engine (one per rank / GPU)."""
+
+    def __init__(self, engine, image_shape, prec, params):
+        self.eng, self.shape, self.prec, self.params = engine, image_shape, prec, params
+
+    def main_header(self):
+        h, tlm, _ = self.eng.main_header(self.shape, self.prec, params=self.params)
+        return h, tlm
+
+    def encode_tiles(self, x, tb, te, row0, out):
+        return self.eng.encode_tiles(x, self.prec, tb, te, image_hw=self.shape[1:], row0=row0, params=self.params,
+                                     out=out)
+
+    def decode_rows(self, sub, n, out, row0):
+        self.eng.decode(sub, length=n, out=out, row0=row0)
+
+    def decode_window(self, cs, n, win, out):
+        self.eng.decode_window(cs, win, length=n, out=out)

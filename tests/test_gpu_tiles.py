@@ -10,7 +10,7 @@ parity 0), which covers the C4/C5 configurations (1024 x 1024 tiles).
 import numpy as np
 import pytest
 
-from conftest import FIXTURES, fixture_ids
+from conftest import FIXTURES, ROOT, fixture_ids
 import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -247,3 +247,115 @@ def test_decode_window_single_tile(eng):
     np.testing.assert_array_equal(eng.decode_window(fx.cs, (5, 7, w - 3, h - 11)), fx.img[:, 7:h - 11, 5:w - 3])
     with pytest.raises(RuntimeError):
         eng.decode_window(fx.cs, (0, 0, w + 1, h))
+
+
+class _HostEngineCoder:
+    """grok_amd.shard.EngineCoder behind host tensors: lets the gloo (CPU-tensor) collectives of
+    two processes sharing this box's one GPU drive bench.py's runners with the real engine."""
+
+    def __init__(self, shape, bits, params):
+        import grok_amd as G
+        from grok_amd import shard
+        self.eng = G.Engine(0)
+        self.ec = shard.EngineCoder(self.eng, shape, bits, params)
+
+    def main_header(self):
+        return self.ec.main_header()
+
+    def encode_tiles(self, x, tb, te, row0, out):
+        import torch
+        od = torch.empty(out.numel(), dtype=torch.uint8, device="cuda")
+        n, lens = self.ec.encode_tiles(x.cuda(), tb, te, row0, od)
+        out[:n] = od[:n].cpu()
+        return n, lens
+
+    def decode_rows(self, sub, n, out, row0):
+        import torch
+        od = torch.empty(out.shape, dtype=out.dtype, device="cuda")
+        self.ec.decode_rows(sub[:n].cuda(), n, od, row0)
+        out.copy_(od.cpu())
+
+    def decode_window(self, cs, n, win, out):
+        import torch
+        od = torch.empty(out.shape, dtype=out.dtype, device="cuda")
+        self.ec.decode_window(cs[:n].cuda(), n, win, od)
+        out.copy_(od.cpu())
+
+
+def _bench_runner_worker(rank, world, port, q):
+    import os
+    import sys
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        import grok_amd as G
+        from grok_amd.synth import synth_image
+        size, tiles = 512, (128, 128)
+        bench.CONFIGS["C4"] = dict(bench.CONFIGS["C4"], params=dict(bench.CONFIGS["C4"]["params"], tiles=tiles))
+        cfg = bench.CONFIGS["C4"]
+        coder = _HostEngineCoder((1, size, size), 16, G.default_params(**cfg["params"]))
+        r = bench.ShardRunner("C4", size, rank, world, torch.device("cpu"), dist, coder=coder)
+        r.check()
+        ok4 = True
+        if rank == 0:
+            img = synth_image(size, size, 1, 16, cfg["seed"]).astype(np.int32)
+            ok4 = r.cs[:r.n].numpy().tobytes() == O.encode(img, 16, cblk_sty=64, tiles=tiles, tlm=True, plt=True)
+        # C5: windows of a tiled RGB8 .jp2 on rank 0, each rank given only its band's tile parts
+        S = 384
+        kw5 = dict(tiles=(128, 128), tlm=True, plt=True, jp2=True)
+        img5 = synth_image(S, S, 3, 8, 30).astype(np.int32)
+        file = n = None
+        if rank == 0:
+            cs = O.encode(img5, 8, **kw5)
+            file, n = torch.frombuffer(bytearray(cs), dtype=torch.uint8), len(cs)
+        wins = [(0, 0, 128, 128), (37, 50, 301, 350), (300, 300, 384, 384)]
+        coder5 = _HostEngineCoder((3, S, S), 8, G.default_params(tiles=(128, 128), tlm=True, plt=True, jp2=True))
+        r5 = bench.C5Runner(rank, world, torch.device("cpu"), dist, size=S, windows=wins, coder=coder5, file=file, n=n)
+        r5.check()
+        ok5 = True
+        if rank == 0:
+            ok5 = all(np.array_equal(o.numpy(), img5[:, y0:y1, x0:x1]) for o, (x0, y0, x1, y1) in zip(r5.outs, wins))
+            q.put((bool(ok4), bool(ok5)))
+        coder.eng.close()
+        coder5.eng.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_runners_two_processes_one_gpu():
+    # bench.py's ShardRunner (C4) and C5Runner step() with the HIP engine in two rank processes
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_runner_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == (True, True)
+
+
+def test_bench_runners_world1_device():
+    # the same runners at world size 1 on device tensors (the collective-free path bench.py takes on one GPU)
+    import torch
+    import bench
+    from grok_amd.synth import synth_image
+    dev = torch.device("cuda", 0)
+    r = bench.ShardRunner("C4", 2048, 0, 1, dev, None)
+    r.check()
+    r.close()
+    r5 = bench.C5Runner(0, 1, dev, None, size=4096, windows=[(0, 0, 1024, 1024), (1234, 2345, 3001, 4000)])
+    r5.check()
+    r5.close()
