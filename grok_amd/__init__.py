@@ -51,6 +51,7 @@ class CParameters(ctypes.Structure):
         ("enableTilePartGeneration", ctypes.c_uint8), ("newTilePartProgressionDivider", ctypes.c_char),
         ("roi_compno", ctypes.c_int32), ("roi_shift", ctypes.c_uint32),
         ("numpocs", ctypes.c_uint32), ("pocs", Poc * 32),
+        ("allocationByQuality", ctypes.c_uint8), ("layer_distortion", ctypes.c_double * GK_MAX_LAYERS),
     ]
 
 
@@ -128,7 +129,7 @@ PROG_ORDERS = ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"]   # GRK_PROG_ORDER (grok.
 
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
                    precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False,
-                   prog_order="LRCP", tile_parts=None, pocs=None, roi=None):
+                   prog_order="LRCP", tile_parts=None, pocs=None, roi=None, sop=False, eph=False, quality=None):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
     prog_order: "LRCP", "RLCP", "RPCL", "PCRL", "CPRL" or 0..4 (grk_compress -p).
@@ -168,6 +169,12 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
     if tile_parts:   # grk_compress -u L|R|C: a new tile part whenever that index changes
         p.enableTilePartGeneration = 1
         p.newTilePartProgressionDivider = tile_parts.encode()
+    p.csty |= (2 if sop else 0) | (4 if eph else 0)   # grk_compress -S / -E
+    if quality:   # grk_compress -q PSNR,PSNR,...: fixed-quality layers
+        p.allocationByQuality = 1
+        p.numlayers = len(quality)
+        for i, q in enumerate(quality):
+            p.layer_distortion[i] = q
     return p
 
 

@@ -146,8 +146,14 @@ struct Params {
     uint32_t tw = 0, th = 0;             // nominal tile size (grk_cparameters::t_width/t_height; 0 = image)
     bool tlm = false, plt = false;       // grk_cparameters::writeTLM / writePLT
     bool jp2 = false;                    // grk_cparameters::cod_format == GRK_CODEC_JP2 (file format boxes)
-    bool rate_control() const {          // TileProcessor::needsRateControl (TileProcessor.cpp:952-967)
-        for (uint32_t l = 0; l < nlayers; ++l) if (rates[l] > 0.0) return true;
+    uint32_t sop_eph = 0;                // Scod bits: 2 = SOP before every packet (-S), 4 = EPH after its header (-E)
+    bool quality = false;                // fixed-quality layers (grk_cparameters::allocationByQuality, -q)
+    double dist[GK_MAX_LAYERS] = {0};    // PSNR target per layer (0 = the remaining passes)
+    bool layer_rc(uint32_t l) const {    // TileProcessor::layerNeedsRateControl (TileProcessor.cpp:952-957)
+        return quality ? dist[l] > 0.0 : rates[l] > 0.0;
+    }
+    bool rate_control() const {          // TileProcessor::needsRateControl (TileProcessor.cpp:958-966)
+        for (uint32_t l = 0; l < nlayers; ++l) if (layer_rc(l)) return true;
         return false;
     }
 };
@@ -1118,11 +1124,14 @@ struct T2Enc {
         }
         bw.flush();
         if (budget) {
-            // compressPacketSimulate (T2Compress.cpp:347-434) in its uint32 arithmetic: the bounded
-            // BitIO fails when its byte count reaches the bytes left (BitIO.cpp:35-52), which never
-            // happens with none left, so such a packet passes and the subtraction wraps
+            // compressPacketSimulate (T2Compress.cpp:347-434) in its uint32 arithmetic: SOP's 6 and
+            // EPH's 2 bytes are taken untested; the bounded BitIO fails when its byte count reaches
+            // the bytes left (BitIO.cpp:35-52), which never happens with none left, so such a
+            // packet passes and the subtraction wraps
+            if (P.p.sop_eph & 2) *budget = (uint32_t)(*budget - 6);
             if (*budget != 0 && (uint64_t)hdr.size() >= *budget) return false;
             *budget = (uint32_t)(*budget - hdr.size());
+            if (P.p.sop_eph & 4) *budget = (uint32_t)(*budget - 2);
         }
         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
             const PrecG& PG = R.prc[bi][pi];
@@ -1353,28 +1362,33 @@ struct T2Enc {
     // bytes left or a body past them fails the layer, and a packet met with no byte left passes
     // with all after it (its uint32 subtraction wraps, see write_packet)
     bool packet_walk(uint32_t l, uint64_t max_bytes) const {
-        uint64_t rem = max_bytes;
+        const bool sop = P.p.sop_eph & 2, eph = P.p.sop_eph & 4;
+        uint32_t rem = (uint32_t)max_bytes;
         for (const auto& e : ord) {
-            if (rem == 0) return true;
             const uint64_t h = e.second < l ? fhdr[e.second][e.first] : chdr[e.first];
             const uint64_t sz = e.second < l ? fsize[e.second][e.first] : csize[e.first];
-            if (h >= rem) return false;
-            rem -= h;
+            if (sop) rem -= 6;
+            if (rem != 0 && h >= rem) return false;
+            rem -= (uint32_t)h;
+            if (eph) rem -= 2;
             if (sz - h > rem) return false;
-            rem -= sz - h;
+            rem -= (uint32_t)(sz - h);
         }
         return true;
     }
-    // could a running size before the last packet equal max_bytes exactly (the wrap above)?
-    // lo / hi: per chain bounds of this layer's packet bytes
+    // Could the walk above wrap before it fails?  That needs the bytes left in front of some
+    // packet k to be 0 (0..5 with SOP) or, with EPH, 1 after its header: the running size
+    // before k within [max_bytes - 8 - k's header bytes, max_bytes].  Bounds per chain (clo /
+    // chi header bytes, cbody body bytes) for this layer, exact sizes for the final layers.
     bool may_hit(uint32_t l, uint64_t max_bytes) const {
+        const uint64_t ovh = ((P.p.sop_eph & 2) ? 6 : 0) + ((P.p.sop_eph & 4) ? 2 : 0);
         uint64_t slo = 0, shi = 0;
-        for (size_t k = 0; k + 1 < ord.size(); ++k) {
-            const auto& e = ord[k];
-            if (e.second < l) { slo += fsize[e.second][e.first]; shi += fsize[e.second][e.first]; }
-            else { slo += clo[e.first] + cbody[e.first]; shi += chi[e.first] + cbody[e.first]; }
+        for (const auto& e : ord) {
+            const uint64_t hmax = e.second < l ? fhdr[e.second][e.first] : chi[e.first];
             if (slo > max_bytes) return false;
-            if (shi >= max_bytes) return true;
+            if (shi + hmax + 8 >= max_bytes) return true;
+            if (e.second < l) { slo += fsize[e.second][e.first] + ovh; shi += fsize[e.second][e.first] + ovh; }
+            else { slo += clo[e.first] + cbody[e.first] + ovh; shi += chi[e.first] + cbody[e.first] + ovh; }
         }
         return false;
     }
@@ -1506,37 +1520,33 @@ struct T2Enc {
             }
             ubitn[u] = bits; ubody[u] = body;
         });
-        uint64_t lo = prior, hi = prior, last_body = 0;
+        return bounds_decision(l, max_bytes, [&](uint32_t u) { return ubitn[u]; });
+    }
+    // The bounds test shared by decide / decide_inc.  With S the running size over the packets
+    // of layers <= l in progression order (SOP / EPH bytes included) and the last packet's
+    // header bytes h_n, the walk passes iff S_(n-1) + [6] + h_n < max_bytes and S_n <= max_bytes
+    // (S_n - body_n - [2] = S_(n-1) + [6] + h_n), unless it wraps first (may_hit).
+    template <class F> int bounds_decision(uint32_t l, uint64_t max_bytes, F bits_of) {
+        ensure_order(l);
+        const uint64_t ovh = ((P.p.sop_eph & 2) ? 6 : 0) + ((P.p.sop_eph & 4) ? 2 : 0);
+        uint64_t lo = prior + ovh * ord.size(), hi = lo, last_tail = 0;
         clo.resize(chains.size()); chi.resize(chains.size()); cbody.resize(chains.size());
         for (size_t i = 0; i < chains.size(); ++i) {
             uint64_t R = 1, body = 0;
-            for (uint32_t u : cunits[i]) { R += ubitn[u]; body += ubody[u]; }
+            for (uint32_t u : cunits[i]) { R += bits_of(u); body += ubody[u]; }
             clo[i] = (R + 7) / 8; chi[i] = (R + 6) / 7 + 2; cbody[i] = body;
             lo += clo[i] + body; hi += chi[i] + body;
-            if (i == last_chain) last_body = body;
+            if (i == last_chain) last_tail = body + ((P.p.sop_eph & 4) ? 2 : 0);
         }
-        // pass <=> S_(n-1) + hdr_n < max_bytes and S_n <= max_bytes, S_n - body_n = S_(n-1) + hdr_n,
-        // unless a running size S_k (k < n) equals max_bytes: then the rest passes (packet_walk)
-        if (hi <= max_bytes && hi - last_body < max_bytes) return 1;
-        if (lo > max_bytes || lo - last_body >= max_bytes) { ensure_order(l); return may_hit(l, max_bytes) ? 0 : -1; }
+        if (hi <= max_bytes && hi - last_tail < max_bytes) return 1;
+        if (lo > max_bytes || lo - last_tail >= max_bytes) return may_hit(l, max_bytes) ? 0 : -1;
         return 0;
     }
     // decide() from the per-unit sums make_layer_inc keeps (same arithmetic, no pass over blocks)
     int decide_inc(uint32_t l, uint64_t max_bytes) {
         if (max_bytes == 0xffffffffull) return 1;
         for (uint32_t u = 0; u < (uint32_t)units.size(); ++u) { ubitn[u] = ibits[u]; ubody[u] = ibody[u]; }
-        uint64_t lo = prior, hi = prior, last_body = 0;
-        clo.resize(chains.size()); chi.resize(chains.size()); cbody.resize(chains.size());
-        for (size_t i = 0; i < chains.size(); ++i) {
-            uint64_t R = 1, body = 0;
-            for (uint32_t u : cunits[i]) { R += ibits[u]; body += ibody[u]; }
-            clo[i] = (R + 7) / 8; chi[i] = (R + 6) / 7 + 2; cbody[i] = body;
-            lo += clo[i] + body; hi += chi[i] + body;
-            if (i == last_chain) last_body = body;
-        }
-        if (hi <= max_bytes && hi - last_body < max_bytes) return 1;
-        if (lo > max_bytes || lo - last_body >= max_bytes) { ensure_order(l); return may_hit(l, max_bytes) ? 0 : -1; }
-        return 0;
+        return bounds_decision(l, max_bytes, [&](uint32_t u) { return ibits[u]; });
     }
 
     // ---- incremental bisection (bounds_on layers).  prev[] is fixed while layer l is
@@ -1788,9 +1798,36 @@ struct T2Enc {
         double min_slope = 1.7976931348623157e308, max_slope = -1;
         for (uint32_t ci = 0; ci < nsch; ++ci) { min_slope = std::min(min_slope, smin[ci]); max_slope = std::max(max_slope, smax[ci]); }
         double upper = max_slope;
+        // fixed quality (TileProcessor.cpp:1263-1267, 1299-1322): a layer's target is the tile's
+        // distortion less maxSE / 10^(PSNR/10), maxSE = sum over components of (2^prec - 1)^2 x
+        // the component's code-block area; tile->distortion is the blocks' total distortion
+        // decrease summed in block order (T1CompressScheduler::compress, single-threaded order)
+        double tile_dist = 0.0, maxSE = 0.0;
+        std::vector<double> cum(L, 0.0);
+        if (P.p.quality) {
+            std::vector<uint64_t> npix(P.nc, 0);
+            for (uint32_t b = b0; b < b1; ++b) {
+                npix[P.blocks[b].comp] += (uint64_t)P.blocks[b].w * P.blocks[b].h;
+                if (npasses(b)) tile_dist += dist(b, npasses(b) - 1);
+            }
+            const double m = (double)((1ull << P.prec) - 1);
+            for (uint32_t c = 0; c < P.nc; ++c) maxSE += m * m * (double)npix[c];
+        }
+        // a layer's distortion decrease at the current counts, tile->layerDistoration (makeLayerSimple,
+        // TileProcessor.cpp:1367-1458), summed in block order; p0 = passes in before the layer
+        auto layer_dist = [&](uint32_t l, bool after_final) {
+            double ld = 0.0;
+            for (uint32_t b = b0; b < b1; ++b) {
+                const uint32_t np = lnp[(size_t)b * L + l];
+                if (!np) continue;
+                const uint32_t p0 = after_final ? prev[b] - np : prev[b];
+                ld += p0 ? dist(b, p0 + np - 1) - dist(b, p0 - 1) : dist(b, np - 1);
+            }
+            return ld;
+        };
         // (with progression order changes the last packet of a layer's budget test is not
         // known per chain: every bisection step runs the serial simulation)
-        const bool fast = t1 == t0 + 1 && !getenv("GK_T2_SERIAL_SIM") && P.p.pocs.empty();
+        const bool fast = t1 == t0 + 1 && !getenv("GK_T2_SERIAL_SIM") && P.p.pocs.empty() && !P.p.quality;
         static const bool prof = getenv("GK_PROFILE") != nullptr;
         using clk = std::chrono::steady_clock;
         auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1805,13 +1842,14 @@ struct T2Enc {
         for (uint32_t l = 0; l < L; ++l) {
             uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
             bounds_on = bounds && rates[l] > 0.0;
+            const double target = P.p.quality ? tile_dist - maxSE / pow(10.0, P.p.dist[l] / 10.0) : 0.0;
             if (bounds_on) {
                 const auto tp = clk::now();
                 count_state(nb);
                 bounds_prep(l, prev);
                 t_prep += msd(tp, clk::now());
             }
-            if (rates[l] > 0.0) {
+            if (P.p.layer_rc(l)) {
                 double lower = min_slope, prevthresh = -1, thresh = 0;
                 // pass counts equal to those at an end of the bisection interval give that end's
                 // outcome (the simulation depends on nothing else): the simulation is skipped
@@ -1845,7 +1883,11 @@ struct T2Enc {
                     };
                     if (has_hi && h == h_hi && same(c_hi, j_hi)) ok = true;
                     else if (has_lo && h == h_lo && same(c_lo, j_lo)) ok = false;
-                    else {
+                    else if (P.p.quality) {
+                        // below the target: upperBound = thresh (TileProcessor.cpp:1311-1322)
+                        const double ld = layer_dist(l, false);
+                        ok = (l == 0 ? ld : cum[l - 1] + ld) < target;
+                    } else {
                         int d = bounds_on ? decide_inc(l, max_len) : 0;
                         if (bounds_on && check) {   // debug: the incremental sums must equal a full pass
                             const std::vector<uint64_t> b0v = ubitn, b1v = ubody;
@@ -1883,6 +1925,7 @@ struct T2Enc {
                     for (uint32_t b = b0; b < b1; ++b) { prev[b] = (uint16_t)(prev[b] + lnp[(size_t)b * L + l]); vld[b] = 0; }
                     t_make += msd(tm, clk::now());
                 } else make_layer(l, fin, true, prev);
+                if (P.p.quality) { const double ld = layer_dist(l, true); cum[l] = l == 0 ? ld : cum[l - 1] + ld; }
                 upper = lower - 1;
             } else {
                 make_layer(l, -1.0, true, prev);
@@ -1933,7 +1976,7 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
         put16(o, 0xff50); put16(o, 8); put32(o, 0x00020000); put16(o, (P.p.irrev ? 0x20 : 0) | Bp);
     }
     put16(o, 0xff52); put16(o, 12 + (P.p.custom_prc ? P.p.numres : 0));
-    o.push_back(P.p.custom_prc ? 1 : 0);
+    o.push_back((uint8_t)((P.p.custom_prc ? 1 : 0) | P.p.sop_eph));   // Scod: precincts, SOP, EPH
     o.push_back((uint8_t)P.p.prog);   // progression order
     put16(o, P.p.nlayers);
     o.push_back((uint8_t)((P.p.mct && P.nc >= 3) ? 1 : 0));
@@ -2126,7 +2169,15 @@ static void set_params(Params& P, const gk_cparameters* cp, uint32_t nc) {
     P.numgbits = cp->numgbits ? cp->numgbits : 2;
     P.nlayers = cp->numlayers ? cp->numlayers : 1;
     if (P.nlayers > GK_MAX_LAYERS) P.nlayers = GK_MAX_LAYERS;
-    for (uint32_t l = 0; l < P.nlayers; ++l) P.rates[l] = cp->layer_rate[l] > 0.0 ? cp->layer_rate[l] : 0.0;
+    // a tile takes the PSNR targets under allocationByQuality, the compression ratios otherwise
+    // (CodeStreamCompress.cpp:387-393)
+    P.quality = cp->allocationByQuality != 0;
+    for (uint32_t l = 0; l < GK_MAX_LAYERS; ++l) {
+        P.rates[l] = (l < P.nlayers && !P.quality && cp->layer_rate[l] > 0.0) ? cp->layer_rate[l] : 0.0;
+        P.dist[l] = (l < P.nlayers && P.quality && cp->layer_distortion[l] > 0.0) ? cp->layer_distortion[l] : 0.0;
+    }
+    if (cp->csty & ~7u) throw GkError("unknown coding style bits (csty)");
+    P.sop_eph = cp->csty & 6u;
     P.write_com = cp->write_comment;
     P.cblk_sty = cp->cblk_sty;
     if (cp->prog_order < 0 || cp->prog_order > 4) throw GkError("unknown progression order");
@@ -2748,7 +2799,15 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
                 const TileOut& C = co[q];
                 Pk k = C.pk[l];
                 const uint32_t h0 = (uint32_t)O.phdr.size(), s0 = (uint32_t)O.bsegs.size();
+                if (P.p.sop_eph & 2) {   // SOP: FF91, Lsop 4, Nsop = the packet's index in the tile (T2Compress.cpp:286-303)
+                    const uint32_t nsop = (uint32_t)O.pk.size() & 0xffff;
+                    const uint8_t sop[6] = {0xff, 0x91, 0, 4, (uint8_t)(nsop >> 8), (uint8_t)nsop};
+                    O.phdr.insert(O.phdr.end(), sop, sop + 6);
+                }
                 O.phdr.insert(O.phdr.end(), C.phdr.begin() + k.hoff, C.phdr.begin() + k.hoff + k.hlen);
+                if (P.p.sop_eph & 4) { O.phdr.push_back(0xff); O.phdr.push_back(0x92); }   // EPH (:312-319)
+                const uint32_t ovh = ((P.p.sop_eph & 2) ? 6 : 0) + ((P.p.sop_eph & 4) ? 2 : 0);
+                k.hlen += ovh; k.len += ovh;
                 O.bsegs.insert(O.bsegs.end(), C.bsegs.begin() + k.s0, C.bsegs.begin() + k.s1);
                 k.hoff = h0; k.s1 = s0 + (k.s1 - k.s0); k.s0 = s0;
                 O.pk.push_back(k);
@@ -2966,7 +3025,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             uint32_t scod = S.at(s);
             if (S.at(s + 1) > 4) throw GkError("corrupt COD marker (progression order)");
             W.p.prog = S.at(s + 1);
-            if (scod & 6) throw GkError("SOP/EPH markers not supported");
+            W.p.sop_eph = scod & 6;
             W.p.nlayers = S.be16(s + 2);
             W.p.mct = S.at(s + 4);
             W.p.numres = S.at(s + 5) + 1;
@@ -3136,7 +3195,7 @@ static void prefetch_packet_headers(gk_ctx* ctx, ByteSrc& S, const Plan& P, cons
             for (uint32_t bi = 0; bi < R.bands.size(); ++bi) nblk += (size_t)R.prc[bi][pr.pi].cw * R.prc[bi][pr.pi].ch;
             const size_t len = TP.plt[k++];
             if (pos + len > end) return;   // inconsistent PLT: fall back to page fetches
-            rg.push_back({pos, std::min(len, 64 + 16 * nblk)});
+            rg.push_back({pos, std::min(len, 72 + 16 * nblk)});   // (SOP / EPH included)
             pos += len;
         }
     }
@@ -3353,6 +3412,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                             }
                             if (!any) { pos += TPt.plt[pk]; continue; }
                         }
+                        if (P.p.sop_eph & 2) {   // SOP: FF91 0004 Nsop (T2Decompress::readPacketHeader :226-250)
+                            if (tile_end - pos < 6 || BS.be16(pos) != 0xff91) throw GkError("expected SOP marker");
+                            if (BS.be16(pos + 4) != (pk & 0xffff)) throw GkError("SOP marker packet counter mismatch");
+                            pos += 6;
+                        }
                         BitReader br(BS, pos, tile_end);
                         std::vector<std::pair<uint32_t, uint32_t>> contrib;
                         if (br.read(1)) {
@@ -3419,6 +3483,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         }
                         br.align();
                         pos = br.off;
+                        if (P.p.sop_eph & 4) {   // EPH after the header (:469-486)
+                            if (tile_end - pos < 2 || BS.be16(pos) != 0xff92) throw GkError("expected EPH marker");
+                            pos += 2;
+                        }
                         for (auto& ct : contrib) {
                             const uint32_t n = (uint32_t)std::min<size_t>(ct.second, tile_end > pos ? tile_end - pos : 0);
                             if (n && need[ct.first] && !skip_l) {
@@ -3971,7 +4039,7 @@ int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, gk_cpara
             coding->irreversible = (uint8_t)p.irrev;
             coding->mct = (uint8_t)p.mct;
             coding->numgbits = (uint8_t)p.numgbits;
-            coding->csty = p.custom_prc ? 1 : 0;
+            coding->csty = (uint8_t)((p.custom_prc ? 1 : 0) | p.sop_eph);
             coding->res_spec = p.custom_prc ? p.numres : 0;
             for (uint32_t r = 0; r < p.numres; ++r) {   // highest resolution first, as grk_cparameters
                 coding->prcw_init[r] = 1u << p.prcw[p.numres - 1 - r];

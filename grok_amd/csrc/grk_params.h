@@ -26,9 +26,8 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     // mct 255 = not set on the command line: grk_compress resolves it from the component count
     // once the image is loaded (grk_compress.cpp:1977-1981), as the engine does (>= 3 -> RCT/ICT)
     if (g.mct_data || (g.mct > 1 && g.mct != 255)) return refuse("Part-2 array MCT is not supported");
-    if (g.allocationByQuality && g.numlayers) return refuse("fixed-quality layers are not supported (use rates)");
     if (g.num_comments) return refuse("custom COM markers are not supported (the default comment is written)");
-    if (g.csty & ~1u) return refuse("SOP/EPH markers are not supported");
+    if (g.csty & ~7u) return refuse("unknown coding style bits (csty)");
     const uint32_t sty = (g.isHT ? GRK_CBLKSTY_HT : 0) | g.cblk_sty;
     if (sty > 0x7f || ((sty & GRK_CBLKSTY_HT) && sty != GRK_CBLKSTY_HT)) {
         snprintf(msg, sizeof msg, "code-block style 0x%x is not supported on this path", sty);
@@ -39,7 +38,14 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
         return refuse(msg);
     }
     p.numlayers = g.numlayers ? g.numlayers : 1;
-    for (uint32_t l = 0; l < p.numlayers && l < GRK_MAX_LAYERS; ++l) p.layer_rate[l] = g.numlayers ? g.layer_rate[l] : 0.0;
+    // a tile takes the PSNR targets under allocationByQuality, the compression ratios otherwise
+    // (CodeStreamCompress.cpp:387-393)
+    const bool q = g.allocationByQuality && g.numlayers;
+    p.allocationByQuality = q ? 1 : 0;
+    for (uint32_t l = 0; l < p.numlayers && l < GRK_MAX_LAYERS; ++l) {
+        p.layer_rate[l] = (g.numlayers && !q) ? g.layer_rate[l] : 0.0;
+        p.layer_distortion[l] = q ? g.layer_distortion[l] : 0.0;
+    }
     p.numresolution = g.numresolution;
     p.cblockw_init = g.cblockw_init; p.cblockh_init = g.cblockh_init;
     p.cblk_sty = (uint8_t)sty;

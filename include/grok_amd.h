@@ -45,7 +45,8 @@ typedef struct gk_cparameters {
     uint8_t irreversible;                /* grk_cparameters::irreversible */
     uint8_t mct;                         /* grk_cparameters::mct (RCT/ICT for >= 3 components) */
     uint8_t numgbits;                    /* grk_cparameters::numgbits (default 2) */
-    uint8_t csty;                        /* grk_cparameters::csty (bit0: user precincts) */
+    uint8_t csty;                        /* grk_cparameters::csty: bit0 user precincts, 2 SOP before every packet
+                                            (grk_compress -S), 4 EPH after every packet header (-E) */
     uint32_t res_spec;                   /* grk_cparameters::res_spec */
     uint32_t prcw_init[GK_MAXRLVLS];     /* grk_cparameters::prcw_init */
     uint32_t prch_init[GK_MAXRLVLS];     /* grk_cparameters::prch_init */
@@ -64,6 +65,8 @@ typedef struct gk_cparameters {
     uint32_t numpocs;                    /* progression order changes, written as a POC marker in each tile's
                                             first tile-part header (CodeStreamCompress::writePoc) */
     gk_poc pocs[32];
+    uint8_t allocationByQuality;         /* grk_cparameters::allocationByQuality (grk_compress -q): layers by PSNR */
+    double layer_distortion[GK_MAX_LAYERS]; /* grk_cparameters::layer_distortion: PSNR per layer (0 = the rest) */
 } gk_cparameters;
 
 /* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to

@@ -94,6 +94,9 @@ struct Params {
     uint32_t roi(uint32_t c) const { return c < roishift.size() ? roishift[c] : 0u; }
     uint32_t tw = 0, th = 0;    // nominal tile size (0 = one tile covering the image), grk_cparameters::t_width/t_height
     int tlm = 0, plt = 0;       // write TLM (-X) / PLT (-L) markers
+    uint32_t sop_eph = 0;       // Scod bits: 2 = SOP before every packet, 4 = EPH after every packet header (-S / -E)
+    bool quality = false;       // fixed-quality layers (-q, grk_cparameters::allocationByQuality)
+    double dist[100] = {0};     // per-layer PSNR targets (layer_distortion; 0 = every remaining pass)
     bool ht() const { return (cblk_sty & 0x40) != 0; }
     Params() { for (int i = 0; i < 33; ++i) { prcw_exp[i] = 15; prch_exp[i] = 15; } }
 };
@@ -1224,7 +1227,7 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
     bool custom_prc = false;
     for (uint32_t r = 0; r < p.numres; ++r) if (p.prcw_exp[r] != 15 || p.prch_exp[r] != 15) custom_prc = true;
     put16(o, 0xff52); put16(o, 12 + (custom_prc ? p.numres : 0));  // COD
-    o.push_back(custom_prc ? 1 : 0);                // Scod
+    o.push_back((uint8_t)((custom_prc ? 1 : 0) | p.sop_eph));   // Scod: precincts, SOP, EPH
     o.push_back((uint8_t)p.prog);                   // progression order
     put16(o, p.nlayers);
     o.push_back((uint8_t)((p.mct && im.nc >= 3) ? 1 : 0));
@@ -1398,8 +1401,10 @@ static uint32_t tile_part_of(const Params& p, uint32_t nc, const PktRef& k) {
 
 struct PrecTrees { std::vector<TagTree> incl, imsb; };
 
+// sop_eph: Scod's SOP (2) / EPH (4) bits; pkt: the packet's index in its tile (SOP's Nsop,
+// tile->numProcessedPackets, T2Compress.cpp:286-320)
 static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t layno, PrecTrees& T,
-                         uint64_t* budget) {
+                         uint64_t* budget, uint32_t sop_eph = 0, uint32_t pkt = 0) {
     if (layno == 0) {
         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
             Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
@@ -1450,14 +1455,23 @@ static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t 
     }
     bw.flush();
     if (budget) {
-        // compressPacketSimulate (T2Compress.cpp:347-434) in its own uint32 arithmetic: the header's
-        // BitIO fails when its byte count reaches the bytes left (BitIO::writeByte, BitIO.cpp:35-52),
-        // a test that never fires when no byte is left (offset starts above 0), so a packet met
-        // with 0 bytes left passes and the subtraction wraps: everything after it fits
+        // compressPacketSimulate (T2Compress.cpp:347-434) in its own uint32 arithmetic: SOP's 6
+        // and EPH's 2 bytes are taken without a test; the header's BitIO fails when its byte
+        // count reaches the bytes left (BitIO::writeByte, BitIO.cpp:35-52), a test that never
+        // fires when no byte is left (its count starts above 0), so a packet met with 0 bytes
+        // left passes and the subtraction wraps: everything after it fits
+        if (sop_eph & 2) *budget = (uint32_t)(*budget - 6);
         if (*budget != 0 && (uint64_t)hdr.size() >= *budget) return false;
         *budget = (uint32_t)(*budget - hdr.size());
+        if (sop_eph & 4) *budget = (uint32_t)(*budget - 2);
     }
-    if (o) o->insert(o->end(), hdr.begin(), hdr.end());
+    if (o) {
+        if (sop_eph & 2) {   // SOP: FF91, Lsop 4, Nsop = packet index mod 2^16
+            put16(*o, 0xff91); put16(*o, 4); put16(*o, pkt & 0xffff);
+        }
+        o->insert(o->end(), hdr.begin(), hdr.end());
+        if (sop_eph & 4) put16(*o, 0xff92);   // EPH
+    }
     for (size_t bi = 0; bi < R.bands.size(); ++bi) {   // packet body
         Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
         if (B.empty() || P.cblks.empty()) continue;
@@ -1855,6 +1869,9 @@ typedef struct {
     uint32_t pocs[32][6];
     int32_t roi_compno;    // grk_cparameters::roi_compno (-1 none) / roi_shift
     uint32_t roi_shift;
+    uint32_t csty;         // grk_cparameters::csty SOP (2) / EPH (4) bits (the precinct bit follows prcw_exp)
+    uint32_t by_quality;   // grk_cparameters::allocationByQuality: layer_distortion holds PSNR targets
+    double layer_distortion[100];
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -1879,7 +1896,12 @@ static Params to_params(const orc_cparams* cp) {
         p.pocs.push_back({cp->pocs[i][0], cp->pocs[i][1], cp->pocs[i][2], cp->pocs[i][3], cp->pocs[i][4], cp->pocs[i][5]});
     if (p.ht()) p.numgbits = 1;   // grk_compress.cpp:1123-1124
     p.tw = cp->tile_w; p.th = cp->tile_h; p.tlm = (int)cp->tlm; p.plt = (int)cp->plt;
-    for (uint32_t i = 0; i < 100; ++i) p.rates[i] = i < p.nlayers ? cp->layer_rate[i] : 0.0;
+    p.sop_eph = cp->csty & 6;
+    p.quality = cp->by_quality != 0;
+    // CodeStreamCompress.cpp:387-393: a tile takes the PSNR targets under allocationByQuality,
+    // the compression ratios otherwise
+    for (uint32_t i = 0; i < 100; ++i) p.rates[i] = (i < p.nlayers && !p.quality) ? cp->layer_rate[i] : 0.0;
+    for (uint32_t i = 0; i < 100; ++i) p.dist[i] = (i < p.nlayers && p.quality) ? cp->layer_distortion[i] : 0.0;
     for (int i = 0; i < 33; ++i) { p.prcw_exp[i] = cp->prcw_exp[i] ? cp->prcw_exp[i] : 15; p.prch_exp[i] = cp->prch_exp[i] ? cp->prch_exp[i] : 15; }
     return p;
 }
@@ -1908,8 +1930,11 @@ struct EncodeState {
 };
 
 // Rate control is active when any layer has a target rate (TileProcessor.cpp:952-967).
+static bool layer_needs_rc(const Params& p, uint32_t l) {   // TileProcessor::layerNeedsRateControl (:952-957)
+    return p.quality ? p.dist[l] > 0.0 : p.rates[l] > 0.0;
+}
 static bool needs_rate_control(const Params& p) {
-    for (uint32_t l = 0; l < p.nlayers; ++l) if (p.rates[l] > 0.0) return true;
+    for (uint32_t l = 0; l < p.nlayers; ++l) if (layer_needs_rc(p, l)) return true;
     return false;
 }
 
@@ -2065,21 +2090,25 @@ static bool simulate(EncodeState& E, uint32_t max_layers, uint64_t max_bytes) {
     uint64_t budget = max_bytes;
     uint64_t* bp = (max_bytes == 0xffffffffull) ? nullptr : &budget;
     for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, max_layers, &E.p.pocs))
-        if (!write_packet(nullptr, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], bp)) return false;
+        if (!write_packet(nullptr, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], bp, E.p.sop_eph)) return false;
     return true;
 }
 
-// makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0)
-static void make_layer(EncodeState& E, uint32_t layno, double thresh, bool final_attempt,
-                       std::vector<uint32_t>& prev) {
+// makeLayerSimple (thresh >= 0) / makeLayerFinal (thresh < 0); returns the layer's distortion
+// decrease, tile->layerDistoration[layno], summed in block order as there
+static double make_layer(EncodeState& E, uint32_t layno, double thresh, bool final_attempt,
+                         std::vector<uint32_t>& prev) {
     size_t i = 0;
+    double ld = 0.0;
     for_blocks(E, [&](Cblk& K) {
         if (layno == 0) prev[i] = 0;
         uint32_t inc = thresh < 0 ? std::max(prev[i], K.npasses) : included_passes(K, prev[i], thresh);
         K.layer_np[layno] = inc - prev[i];
+        if (inc > prev[i]) ld += prev[i] ? K.passes[inc - 1].dist - K.passes[prev[i] - 1].dist : K.passes[inc - 1].dist;
         if (final_attempt) prev[i] = inc;
         ++i;
     });
+    return ld;
 }
 
 // CodeStreamCompress::updateRates (:951-1025): compression ratios -> cumulative byte budgets of
@@ -2116,6 +2145,26 @@ static void rate_allocate(EncodeState& E) {
     }
     double rates[100];
     update_rates(E, rates);
+    // fixed quality (TileProcessor.cpp:1263-1267, 1299-1322): the layer's target is the tile's
+    // distortion less maxSE / 10^(PSNR/10), maxSE = sum over components of (2^prec - 1)^2 x
+    // the component's code-block area; tile->distortion is the blocks' total distortion
+    // decrease in block order (T1CompressScheduler::compress, single-threaded order)
+    double tile_dist = 0.0, maxSE = 0.0;
+    if (E.p.quality) {
+        for (uint32_t c = 0; c < E.im.nc; ++c) {
+            uint64_t numpix = 0;
+            for (uint32_t r = 0; r < E.p.numres; ++r)
+                for (auto& B : E.comps[c].res[r].bands)
+                    for (auto& P : B.prcs)
+                        for (auto& K : P.cblks) {
+                            numpix += (uint64_t)(K.x1 - K.x0) * (K.y1 - K.y0);
+                            if (K.npasses) tile_dist += K.passes[K.npasses - 1].dist;
+                        }
+            const double m = (double)((1ull << E.im.prec) - 1);
+            maxSE += m * m * (double)numpix;
+        }
+    }
+    double cum[100] = {0};
     double min_slope = 1.7976931348623157e308, max_slope = -1;
     for_blocks(E, [&](Cblk& K) {
         for (uint32_t q = 0; q < K.npasses; ++q) {
@@ -2130,18 +2179,26 @@ static void rate_allocate(EncodeState& E) {
     double upper = max_slope;
     for (uint32_t l = 0; l < E.p.nlayers; ++l) {
         uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
-        if (rates[l] > 0.0) {
+        if (layer_needs_rc(E.p, l)) {
             double lower = min_slope, prevthresh = -1, thresh = 0;
+            const double target = E.p.quality ? tile_dist - maxSE / pow(10.0, E.p.dist[l] / 10.0) : 0.0;
             for (uint32_t it = 0; it < 128; ++it) {
                 thresh = (upper == -1) ? lower : (lower + upper) / 2;
-                make_layer(E, l, thresh, false, prev);
+                const double ld = make_layer(E, l, thresh, false, prev);
                 if (prevthresh != -1 && fabs(prevthresh - thresh) < 0.001) break;
                 prevthresh = thresh;
-                if (!simulate(E, l + 1, max_len)) { lower = thresh; continue; }
-                upper = thresh;
+                if (E.p.quality) {
+                    const double achieved = l == 0 ? ld : cum[l - 1] + ld;
+                    if (achieved < target) { upper = thresh; continue; }
+                    lower = thresh;
+                } else {
+                    if (!simulate(E, l + 1, max_len)) { lower = thresh; continue; }
+                    upper = thresh;
+                }
             }
             double good = (upper == -1) ? thresh : upper;
-            make_layer(E, l, good, true, prev);
+            const double ld = make_layer(E, l, good, true, prev);
+            cum[l] = l == 0 ? ld : cum[l - 1] + ld;
             upper = lower - 1;
         } else {
             make_layer(E, l, -1.0, true, prev);
@@ -2156,7 +2213,8 @@ static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector
     auto trees = make_trees(E);
     for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, E.p.nlayers, &E.p.pocs)) {
         size_t before = body.size();
-        write_packet(&body, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], nullptr);
+        write_packet(&body, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], nullptr, E.p.sop_eph,
+                     (uint32_t)plens.size());
         plens.push_back((uint32_t)(body.size() - before));
         if (pparts) pparts->push_back(tile_part_of(E.p, E.im.nc, k));
     }
@@ -2500,6 +2558,7 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
         }
     }
     size_t pos = i;
+    uint32_t npkt = 0;   // tile->numProcessedPackets: SOP's expected Nsop (T2Decompress.cpp:114, 239-246)
     for (const PktRef& pk : packet_iter(comps, p, tx0, ty0, tx1, ty1, nlayers, tpocs && !tpocs->empty() ? tpocs : &p.pocs)) {
                 const uint32_t l = pk.l, r = pk.r, c = pk.c, pi = pk.pi;
                 Res& R = comps[c].res[r];
@@ -2511,6 +2570,12 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
                         pos = ranges[next_range].first; tile_end = ranges[next_range].second; ++next_range;
                     }
                     if (pos >= tile_end) goto t2done;
+                    if (p.sop_eph & 2) {   // SOP: FF91 0004 Nsop (T2Decompress::readPacketHeader :226-250)
+                        if (tile_end - pos < 6 || cs[pos] != 0xff || cs[pos + 1] != 0x91) return -5;
+                        if (get16(cs + pos + 4) != (npkt & 0xffff)) return -5;
+                        pos += 6;
+                    }
+                    ++npkt;
                     BitReader br; br.p = cs + pos; br.len = tile_end - pos;
                     std::vector<std::pair<Cblk*, uint32_t>> contrib;  // block, bytes in this packet
                     if (br.read(1)) {
@@ -2557,6 +2622,10 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
                     }
                     br.align();
                     pos += br.off;
+                    if (p.sop_eph & 4) {   // EPH after the header (:469-486)
+                        if (tile_end - pos < 2 || cs[pos] != 0xff || cs[pos + 1] != 0x92) return -5;
+                        pos += 2;
+                    }
                     for (auto& ct : contrib) {
                         const bool skip = ct.second > 0x7fffffffu;   // skipped layer: ~bytes
                         const uint32_t want = skip ? ~ct.second : ct.second;
@@ -2704,6 +2773,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             im.prec = (s[36] & 0x7f) + 1; im.sgnd = (s[36] & 0x80) != 0;
         } else if (m == 0xff52) {
             uint32_t scod = s[0];
+            p.sop_eph = scod & 6;
             p.nlayers = get16(s + 2); p.mct = s[4];
             p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
             p.cblk_sty = s[8];

@@ -26,6 +26,7 @@ class CParams(ctypes.Structure):
         ("cod_format", ctypes.c_uint32), ("prog_order", ctypes.c_uint32), ("tp_div", ctypes.c_uint32),
         ("numpocs", ctypes.c_uint32), ("pocs", (ctypes.c_uint32 * 6) * 32),
         ("roi_compno", ctypes.c_int32), ("roi_shift", ctypes.c_uint32),
+        ("csty", ctypes.c_uint32), ("by_quality", ctypes.c_uint32), ("layer_distortion", ctypes.c_double * 100),
     ]
 
 
@@ -95,7 +96,8 @@ def get_threads():
 
 
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
-           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None, roi=None):
+           layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None, roi=None,
+           sop=False, eph=False, quality=None):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -122,6 +124,13 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
         p.nlayers = len(layer_rate)
         for i, r in enumerate(layer_rate):
             p.layer_rate[i] = r
+    # grk_compress -S / -E (csty SOP / EPH bits) and -q PSNR layers (allocationByQuality)
+    p.csty = (2 if sop else 0) | (4 if eph else 0)
+    if quality:
+        p.by_quality = 1
+        p.nlayers = len(quality)
+        for i, q in enumerate(quality):
+            p.layer_distortion[i] = q
     if precincts:
         # Grok CLI semantics: list of (w, h) from the highest resolution down; the last repeats
         exps = [(int(w).bit_length() - 1, int(h).bit_length() - 1) for (w, h) in precincts]

@@ -5,7 +5,8 @@
  * include/grk_abi.h (layout-identical to grok.h) and linked with libgrok_amd.so by
  * tests/test_gpu_grk_api.py.  Raw files are planar int32 samples, component after component.
  *
- *   enc RAW W H C PREC OUT [-n N] [-b W,H] [-I] [-r R1,R2,..] [-M 64] [-t W,H] [-X] [-L] [-jp2] [-tiles] [-file]
+ *   enc RAW W H C PREC OUT [-n N] [-b W,H] [-I] [-r R1,R2,..] [-q Q1,Q2,..] [-S] [-E] [-M 64] [-t W,H] [-X] [-L]
+ *       [-jp2] [-tiles] [-file]
  *   dec IN RAWOUT [-d X0,Y0,X1,Y1] [-tile T] [-r REDUCE] [-l LAYERS] [-mapped]
  *   dump IN [FLAGS]
  */
@@ -46,6 +47,14 @@ static int enc(int argc, char** argv) {
         else if (!strcmp(argv[i], "-jp2")) fmt = GRK_CODEC_JP2;
         else if (!strcmp(argv[i], "-tiles")) raw_tiles = 1;
         else if (!strcmp(argv[i], "-file")) to_file = 1;
+        else if (!strcmp(argv[i], "-S")) p.csty |= 0x02;   /* grk_compress.cpp:529-531: SOP / EPH */
+        else if (!strcmp(argv[i], "-E")) p.csty |= 0x04;
+        else if (!strcmp(argv[i], "-q")) {   /* :788-800: PSNR per layer, fixed-quality allocation */
+            char* s = argv[++i];
+            p.numlayers = 0;
+            for (char* t = strtok(s, ","); t; t = strtok(NULL, ",")) p.layer_distortion[p.numlayers++] = atof(t);
+            p.allocationByQuality = true;
+        }
         else if (!strcmp(argv[i], "-c")) {   /* one precinct size for every resolution: [W,H] */
             unsigned pw, ph;
             sscanf(argv[++i], "[%u,%u]", &pw, &ph);

@@ -47,6 +47,12 @@ def parse_flags(flags):
         kw["tiles"] = tuple(int(v) for v in t[t.index("-t") + 1].split(","))
     if "-X" in t:
         kw["tlm"] = True
+    if "-S" in t:
+        kw["sop"] = True
+    if "-E" in t:
+        kw["eph"] = True
+    if "-q" in t:
+        kw["quality"] = [float(v) for v in t[t.index("-q") + 1].split(",")]
     if "-L" in t:
         kw["plt"] = True
     return kw

@@ -122,3 +122,16 @@ def test_grk_api_cli_reduce_and_layers(tool, name, red, layers):
         O.set_decode_reduce(0)
         O.set_decode_layers(0)
     np.testing.assert_array_equal(dec, want)
+
+
+@pytest.mark.parametrize("flags", ["-S -E", "-S -r 20,5", "-q 30,40", "-E -q 28,36,0 -t 128,128 -X"])
+def test_grk_api_sop_eph_quality(tool, flags):
+    # grk_compress -S / -E / -q through grk_cparameters (csty, allocationByQuality, layer_distortion)
+    from grok_amd.synth import synth_image
+    img = synth_image(200, 300, 3, 8, 77).astype(np.int32)
+    cs, path = _enc(tool, img, 8, flags, "sq_" + flags.replace(" ", "_").replace(",", "_"))
+    from conftest import parse_flags
+    assert cs == O.encode(img, 8, **parse_flags(flags))
+    dec, _ = _dec(tool, path, img.shape)
+    want, _ = O.decode(cs)
+    np.testing.assert_array_equal(dec, want)
