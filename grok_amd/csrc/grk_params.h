@@ -10,7 +10,9 @@
 #include "../../include/grk_abi.h"
 #include "../../include/grok_amd.h"
 
-inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters& p, std::string& why) {
+// ntiles: the image's tile count (progression order changes are given per tile).
+inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters& p, std::string& why,
+                             uint32_t ntiles = 1) {
     char msg[256];
     auto refuse = [&](const char* m) { why = m; return false; };
     gk_set_default_params(&p);
@@ -19,7 +21,6 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
                  GRK_J2K_MAXRLVLS);
         return refuse(msg);
     }
-    if (g.numpocs) return refuse("progression order changes (POC) are not supported on this path");
     if (g.prog_order < GRK_LRCP || g.prog_order > GRK_CPRL) return refuse("unknown progression order");
     if (g.tx0 || g.ty0 || g.image_offset_x0 || g.image_offset_y0) return refuse("image/tile offsets are not supported");
     if (g.tile_size_on && (!g.t_width || !g.t_height)) return refuse("tile size must be non-zero when tiling is on");
@@ -64,5 +65,30 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     p.roi_compno = g.roi_compno; p.roi_shift = g.roi_shift;
     p.enableTilePartGeneration = g.enableTilePartGeneration ? 1 : 0;
     p.newTilePartProgressionDivider = g.newTilePartProgressionDivider;
+    if (g.numpocs) {
+        // CodeStreamCompress.cpp:397-427: numpocs + 1 entries (grk_compress -P T<t>=...); tile t
+        // takes as many entries as name it - copied from the head of the list (the loop indexes
+        // by its own counter) - and a tile named by none is an error.  One entry is no change
+        // (tcp->numpocs = 0: the tile keeps prog_order).  The engine codes one list for every tile.
+        const uint32_t n = g.numpocs + 1;
+        if (n > GRK_J2K_MAXRLVLS || n > 32) return refuse("too many progression order changes");
+        uint32_t k = 0;
+        for (uint32_t t = 0; t < ntiles; ++t) {
+            uint32_t c = 0;
+            for (uint32_t i = 0; i < n; ++i) c += g.progression[i].tileno == t;
+            if (!c) return refuse("Problem with specified progression order changes");
+            if (t && c != k) return refuse("progression order changes that differ between tiles are not supported");
+            k = c;
+        }
+        if (k > 1) {
+            p.numpocs = k;
+            for (uint32_t i = 0; i < k; ++i) {
+                const grk_progression& e = g.progression[i];
+                p.pocs[i].resS = e.resS; p.pocs[i].compS = e.compS; p.pocs[i].layE = e.layE;
+                p.pocs[i].resE = e.resE; p.pocs[i].compE = e.compE;
+                p.pocs[i].prog = (int32_t)e.specifiedCompressionPocProg;
+            }
+        }
+    }
     return true;
 }

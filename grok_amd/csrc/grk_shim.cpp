@@ -215,9 +215,14 @@ struct CodecObj : Obj {
 CodecObj* codec_of(grk_codec* c) { return c ? dynamic_cast<CodecObj*>(obj_of(c)) : nullptr; }
 
 // grk_cparameters -> gk_cparameters (grk_params.h); a refusal goes to the error callback
-bool to_gk(const grk_cparameters& g, GRK_CODEC_FORMAT fmt, gk_cparameters& p) {
+bool to_gk(const grk_cparameters& g, GRK_CODEC_FORMAT fmt, gk_cparameters& p, const grk_image* im = nullptr) {
     std::string why;
-    if (grk_params_to_gk(g, fmt == GRK_CODEC_JP2, p, why)) return true;
+    uint32_t ntiles = 1;
+    if (im && im->numcomps && g.tile_size_on && g.t_width && g.t_height) {
+        const uint64_t w = im->comps[0].w, h = im->comps[0].h;
+        ntiles = (uint32_t)(((w + g.t_width - 1) / g.t_width) * ((h + g.t_height - 1) / g.t_height));
+    }
+    if (grk_params_to_gk(g, fmt == GRK_CODEC_JP2, p, why, ntiles)) return true;
     error("%s", why.c_str());
     return false;
 }
@@ -241,7 +246,7 @@ bool image_geometry(const grk_image* im, gk_image_info& info) {
 
 bool run_encode(CodecObj* C, const void* const* planes, const uint32_t* strides, uint32_t sample_bytes) {
     gk_cparameters p;
-    if (!to_gk(C->cp, C->fmt, p)) return false;
+    if (!to_gk(C->cp, C->fmt, p, C->image)) return false;
     gk_image_info info;
     if (!image_geometry(C->image, info)) return false;
     info.sample_bytes = sample_bytes;
@@ -444,7 +449,7 @@ bool grk_compress_init(grk_codec* codec, grk_cparameters* parameters, grk_image*
     CodecObj* C = codec_of(codec);
     if (!C || !C->compress || !parameters || !image) return false;
     gk_cparameters probe;
-    if (!to_gk(*parameters, C->fmt, probe)) return false;
+    if (!to_gk(*parameters, C->fmt, probe, image)) return false;
     gk_image_info info;
     if (!image_geometry(image, info)) return false;
     C->cp = *parameters;

@@ -6,7 +6,7 @@
  * tests/test_gpu_grk_api.py.  Raw files are planar int32 samples, component after component.
  *
  *   enc RAW W H C PREC OUT [-n N] [-b W,H] [-I] [-r R1,R2,..] [-q Q1,Q2,..] [-S] [-E] [-M 64] [-t W,H] [-X] [-L]
- *       [-jp2] [-tiles] [-file]
+ *       [-p PROG] [-P T0=..,PROG/T0=..] [-jp2] [-tiles] [-file]
  *   dec IN RAWOUT [-d X0,Y0,X1,Y1] [-tile T] [-r REDUCE] [-l LAYERS] [-mapped]
  *   dump IN [FLAGS]
  */
@@ -19,6 +19,13 @@
 static void on_error(const char* msg, void* ud) { (void)ud; fprintf(stderr, "[grk error] %s\n", msg); }
 static void on_warning(const char* msg, void* ud) { (void)ud; fprintf(stderr, "[grk warning] %s\n", msg); }
 
+static GRK_PROG_ORDER prog_of(const char* s) {   /* grk_compress.cpp:331-347 */
+    static const char* names[] = {"LRCP", "RLCP", "RPCL", "PCRL", "CPRL"};
+    for (int k = 0; k < 5; ++k)
+        if (!strncmp(s, names[k], 4)) return (GRK_PROG_ORDER)k;
+    return GRK_PROG_UNKNOWN;
+}
+
 static int enc(int argc, char** argv) {
     const char* raw = argv[2];
     uint32_t w = (uint32_t)atoi(argv[3]), h = (uint32_t)atoi(argv[4]), c = (uint32_t)atoi(argv[5]);
@@ -28,6 +35,7 @@ static int enc(int argc, char** argv) {
     grk_compress_set_default_params(&p);
     p.mct = 255;                    /* pluginMain (grk_compress.cpp:2180-2184): resolved per image below */
     p.rateControlAlgorithm = 255;
+    p.numlayers = 1;                /* :823-828: no -r / -q is one lossless layer (set before -P is read) */
     int to_file = 0;
     GRK_CODEC_FORMAT fmt = GRK_CODEC_J2K;
     int raw_tiles = 0;
@@ -47,6 +55,26 @@ static int enc(int argc, char** argv) {
         else if (!strcmp(argv[i], "-jp2")) fmt = GRK_CODEC_JP2;
         else if (!strcmp(argv[i], "-tiles")) raw_tiles = 1;
         else if (!strcmp(argv[i], "-file")) to_file = 1;
+        else if (!strcmp(argv[i], "-p")) p.prog_order = prog_of(argv[++i]);
+        else if (!strcmp(argv[i], "-P")) {   /* grk_compress.cpp:1001-1057: T<t>=resS,compS,layE,resE,compE,PROG/... */
+            char* s = argv[++i];
+            uint32_t n = 0, rs, cs, le, re, ce;
+            char prog[5];
+            while (sscanf(s, "T%u=%u,%u,%u,%u,%u,%4s", &p.progression[n].tileno, &rs, &cs, &le, &re, &ce, prog) == 7) {
+                p.progression[n].resS = (uint8_t)rs; p.progression[n].compS = (uint16_t)cs;
+                p.progression[n].layE = (uint16_t)le; p.progression[n].resE = (uint8_t)re;
+                p.progression[n].compE = (uint16_t)ce;
+                p.progression[n].specifiedCompressionPocProg = prog_of(prog);
+                if (p.progression[n].layE > p.numlayers) p.progression[n].layE = p.numlayers;
+                if (p.progression[n].resE > p.numresolution) p.progression[n].resE = (uint8_t)(p.numresolution - 1);
+                ++n;
+                while (*s && *s != '/') s++;
+                if (!*s) break;
+                s++;
+            }
+            if (n <= 1) return 21;
+            p.numpocs = n - 1;
+        }
         else if (!strcmp(argv[i], "-S")) p.csty |= 0x02;   /* grk_compress.cpp:529-531: SOP / EPH */
         else if (!strcmp(argv[i], "-E")) p.csty |= 0x04;
         else if (!strcmp(argv[i], "-q")) {   /* :788-800: PSNR per layer, fixed-quality allocation */

@@ -53,6 +53,19 @@ def parse_flags(flags):
         kw["eph"] = True
     if "-q" in t:
         kw["quality"] = [float(v) for v in t[t.index("-q") + 1].split(",")]
+    if "-p" in t:
+        kw["prog_order"] = t[t.index("-p") + 1]
+    if "-P" in t:   # grk_compress.cpp:1001-1057 with its clamps; every tile takes the list's head
+        nl = len(kw.get("layer_rate") or kw.get("quality") or [0])
+        nr = kw.get("numres", 6)
+        pocs = []
+        for e in t[t.index("-P") + 1].split("/"):
+            m = re.match(r"T(\d+)=(\d+),(\d+),(\d+),(\d+),(\d+),(\w{4})", e)
+            rs, cs, le, re_, ce = (int(v) for v in m.groups()[1:6])
+            pocs.append((m.group(1), rs, cs, min(le, nl), re_ if re_ <= nr else nr - 1, ce, m.group(7)))
+        k = sum(1 for q in pocs if q[0] == "0")
+        if k > 1:
+            kw["pocs"] = [q[1:] for q in pocs[:k]]
     if "-L" in t:
         kw["plt"] = True
     return kw

@@ -135,3 +135,17 @@ def test_grk_api_sop_eph_quality(tool, flags):
     dec, _ = _dec(tool, path, img.shape)
     want, _ = O.decode(cs)
     np.testing.assert_array_equal(dec, want)
+
+
+@pytest.mark.parametrize("flags", ["-r 20,10,5 -P T0=0,0,1,3,3,RLCP/T0=3,0,3,6,3,LRCP/T0=0,0,3,6,3,RPCL",
+                                   "-p CPRL -c [64,64],[32,32]", "-n 4 -P T0=0,0,1,4,3,PCRL/T0=0,0,1,5,3,LRCP"])
+def test_grk_api_progression_changes(tool, flags):
+    # grk_cparameters::progression / numpocs (grk_compress -P) and prog_order (-p)
+    from grok_amd.synth import synth_image
+    img = synth_image(160, 224, 3, 8, 78).astype(np.int32)
+    cs, path = _enc(tool, img, 8, flags, "poc_%d" % (abs(hash(flags)) % 10000))
+    from conftest import parse_flags
+    assert cs == O.encode(img, 8, **parse_flags(flags))
+    dec, _ = _dec(tool, path, img.shape)
+    want, _ = O.decode(cs)
+    np.testing.assert_array_equal(dec, want)
