@@ -2975,19 +2975,47 @@ static void parse_poc(Src& S, size_t s, uint32_t L, uint32_t nc, std::vector<Poc
 // Tile-part header markers that would change how the tile decodes (CodeStreamDecompress's
 // tile-part handlers: COD :1725, COC, QCD, QCC, RGN read_rgn :1480-1520) are refused here
 // rather than skipped, so a stream that carries them fails instead of decoding wrongly.
-static void check_tile_part_marker(uint32_t m) {
-    if (m == 0xff52 || m == 0xff53 || m == 0xff5c || m == 0xff5d)
-        throw GkError("COD/COC/QCD/QCC in a tile-part header are not supported on this path");
-    if (m == 0xff5e) throw GkError("RGN in a tile-part header is not supported on this path");
-}
 struct Header {
     Plan want;
     std::vector<std::pair<uint32_t, uint32_t>> qcd;
     size_t first_sot = 0;
     std::vector<TilePart> parts;
     std::vector<std::pair<uint32_t, uint32_t>> tlm;   // (tile, tile-part length) from TLM markers
+    std::vector<uint8_t> cod, qcd_body;               // main COD / QCD marker bodies (after Lxxx)
 };
 
+static std::vector<uint8_t> marker_body(ByteSrc& S, size_t s, uint32_t L) {
+    std::vector<uint8_t> v(L - 2);
+    for (uint32_t k = 0; k + 2 < L; ++k) v[k] = S.at(s + k);
+    return v;
+}
+
+// COC / QCC (main or tile-part header) and tile-part COD / QCD override the main COD / QCD for
+// one component or one tile (CodeStreamDecompress read_coc / read_qcc, TileCodingParams).
+// This path codes every tile-component with the main header's parameters, so such a marker is
+// accepted when it restates them (some encoders write them even when nothing differs) and
+// refused otherwise.  COC: Ccoc (1 byte below 257 components, else 2), Scoc (precinct flag),
+// then SPcoc laid out as COD's SPcod; QCC: Cqcc, then Sqcc/SPqcc as QCD's body.
+static void check_override_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, const Header& Hd, bool tile) {
+    if (m == 0xff5e && tile) throw GkError("RGN in a tile-part header is not supported on this path");
+    if (m != 0xff52 && m != 0xff53 && m != 0xff5c && m != 0xff5d) return;
+    if (L < 3) throw GkError("corrupt COD/COC/QCD/QCC marker");
+    const std::vector<uint8_t> b = marker_body(S, s, L);
+    const uint32_t nc = Hd.want.nc, cw = nc <= 256 ? 1 : 2;
+    bool same = false;
+    if (m == 0xff52) same = b == Hd.cod;
+    else if (m == 0xff5c) same = b == Hd.qcd_body;
+    else if (b.size() > cw) {
+        const uint32_t c = cw == 1 ? b[0] : (uint32_t)b[0] << 8 | b[1];
+        if (c >= nc) throw GkError("bad component number in COC/QCC");
+        if (m == 0xff5d) same = std::equal(b.begin() + cw, b.end(), Hd.qcd_body.begin(), Hd.qcd_body.end());
+        else same = Hd.cod.size() > 5 && (b[cw] & 1) == (Hd.cod[0] & 1) &&
+                    std::equal(b.begin() + cw + 1, b.end(), Hd.cod.begin() + 5, Hd.cod.end());
+    }
+    if (!same)
+        throw GkError(tile ? "tile-part COD/COC/QCD/QCC that differ from the main header are not supported on this path"
+                           : "COC/QCC that differ from COD/QCD are not supported on this path");
+}
 static void parse_header(ByteSrc& S, Header& Hd) {
     size_t i = 0;
     if (S.len < 4 || S.be16(0) != 0xff4f) throw GkError("not a J2K codestream (no SOC)");
@@ -2995,6 +3023,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     Plan& W = Hd.want;
     for (int k = 0; k < GK_MAXRLVLS; ++k) { W.p.prcw[k] = 15; W.p.prch[k] = 15; }
     bool have_siz = false, have_cod = false;
+    std::vector<size_t> coc_qcc;   // checked against COD / QCD once the main header is read
     while (i + 4 <= S.len) {
         uint32_t m = S.be16(i);
         if (m == 0xff90) { Hd.first_sot = i; break; }
@@ -3044,6 +3073,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
                 for (uint32_t r = 0; r < W.p.numres; ++r) { uint32_t v = S.at(s + 10 + r); W.p.prcw[r] = v & 15; W.p.prch[r] = v >> 4; }
             }
             have_cod = true;
+            Hd.cod = marker_body(S, s, L);
         } else if (m == 0xff5c) {
             if (L < 4) throw GkError("corrupt QCD marker");
             uint32_t sq = S.at(s);
@@ -3053,6 +3083,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             if (qt == 0) for (uint32_t k = 1; k < L - 2; ++k) Hd.qcd.push_back({(uint32_t)S.at(s + k) >> 3, 0u});
             else if (qt == 2) for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = S.be16(s + k); Hd.qcd.push_back({v >> 11, v & 0x7ff}); }
             else throw GkError("scalar-derived quantisation not supported");
+            Hd.qcd_body = marker_body(S, s, L);
         } else if (m == 0xff55) {   // TLM (TileLengthMarkers::read, cache/LengthCache.cpp)
             const uint32_t stlm = S.at(s + 1), st = (stlm >> 4) & 3, sp = (stlm >> 6) & 1;
             const uint32_t esz = st + (sp ? 4 : 2);
@@ -3078,11 +3109,12 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             if (W.p.roishift.size() < W.nc) W.p.roishift.resize(W.nc, 0);
             W.p.roishift[c] = (uint8_t)shift;
         } else if (m == 0xff5d || m == 0xff53) {
-            throw GkError("QCC/COC markers not supported on this path yet");
+            coc_qcc.push_back(i);
         }
         i += 2 + L;
     }
     if (!have_siz || !have_cod || Hd.qcd.empty() || !Hd.first_sot) throw GkError("incomplete main header");
+    for (size_t k : coc_qcc) check_override_marker(S, k + 4, S.be16(k), S.be16(k + 2), Hd, false);
     // tile parts: SOT (Isot, Psot, TPsot, TNsot), tile-part header markers (PLT, ...), SOD, packets
     // (CodeStreamDecompress SOT/SOD handlers; TLM and PLT are only needed for random access)
     size_t pos = Hd.first_sot;
@@ -3109,7 +3141,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             std::vector<Poc> tpoc;
             while (j + 4 <= end && S.be16(j) != 0xff93) {
                 if (S.be16(j) == 0xff5f) parse_poc(S, j + 4, S.be16(j + 2), W.nc, tpoc);   // tile-part POC
-                check_tile_part_marker(S.be16(j));
+                check_override_marker(S, j + 4, S.be16(j), S.be16(j + 2), Hd, true);
                 j += 2 + S.be16(j + 2);
             }
             if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
@@ -3163,7 +3195,7 @@ static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
         while (j + 4 <= TP.end && S.be16(j) != 0xff93) {
             const uint32_t m = S.be16(j), L = S.be16(j + 2);
             if (m == 0xff5f) parse_poc(S, j + 4, L, nc, TP.pocs);   // tile-part POC
-            check_tile_part_marker(m);
+            check_override_marker(S, j + 4, m, L, Hd, true);
             if (m == 0xff58) {
                 uint32_t v = 0;
                 for (size_t q = j + 5; q < j + 2 + L; ++q) {

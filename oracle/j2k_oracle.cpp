@@ -2739,6 +2739,21 @@ t2done:
     return 0;
 }
 
+// COC / QCC and tile-part COD / QCD (CodeStreamDecompress read_coc / read_qcc override the main
+// COD / QCD per component or per tile): this restatement codes every tile-component with the
+// main header's parameters, so it accepts such a marker only when it restates them.
+static bool restates_main(const uint8_t* b, uint32_t L, uint32_t m, uint32_t nc, const std::vector<uint8_t>& cod,
+                          const std::vector<uint8_t>& qcd) {
+    if (L < 3) return false;
+    const std::vector<uint8_t> v(b, b + L - 2);
+    if (m == 0xff52) return v == cod;
+    if (m == 0xff5c) return v == qcd;
+    const uint32_t cw = nc <= 256 ? 1 : 2;
+    if (v.size() <= cw || (cw == 1 ? v[0] : get16(b)) >= nc) return false;
+    if (m == 0xff5d) return std::equal(v.begin() + cw, v.end(), qcd.begin(), qcd.end());
+    return cod.size() > 5 && (v[cw] & 1) == (cod[0] & 1) && std::equal(v.begin() + cw + 1, v.end(), cod.begin() + 5, cod.end());
+}
+
 int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_t* H, uint32_t* NC, uint32_t* PREC) {
     size_t i = 0;
     if (len >= 12 && get32(cs) == 12 && get32(cs + 4) == 0x6a502020) {   // JP2: find the jp2c box
@@ -2760,6 +2775,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     Image im{}; Params p; p.write_com = 0;
     std::vector<std::pair<uint32_t, uint32_t>> qcd;
     size_t first_sot = 0;
+    std::vector<uint8_t> cod_body, qcd_body;
+    std::vector<size_t> coc_qcc;
     while (i + 4 <= len) {
         uint32_t m = get16(cs + i);
         if (m == 0xff90) { first_sot = i; break; }
@@ -2773,6 +2790,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             im.prec = (s[36] & 0x7f) + 1; im.sgnd = (s[36] & 0x80) != 0;
         } else if (m == 0xff52) {
             uint32_t scod = s[0];
+            cod_body.assign(s, s + L - 2);
             p.sop_eph = scod & 6;
             p.nlayers = get16(s + 2); p.mct = s[4];
             p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
@@ -2792,13 +2810,18 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             p.roishift[c] = s[cw + 1];
         } else if (m == 0xff5c) {
             uint32_t sq = s[0]; p.numgbits = sq >> 5;
+            qcd_body.assign(s, s + L - 2);
             uint32_t qt = sq & 0x1f;
             if (qt == 0) for (uint32_t k = 1; k + 0 < L - 2; ++k) qcd.push_back({(uint32_t)s[k] >> 3, 0u});
             else for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = get16(s + k); qcd.push_back({v >> 11, v & 0x7ff}); }
+        } else if (m == 0xff53 || m == 0xff5d) {
+            coc_qcc.push_back(i);
         }
         i += 2 + L;   // CAP, TLM, COM and other main-header markers are skipped
     }
     if (!first_sot) return -3;
+    for (size_t k : coc_qcc)
+        if (!restates_main(cs + k + 4, get16(cs + k + 2), get16(cs + k), im.nc, cod_body, qcd_body)) return -2;
     if (g_dec_reduce >= p.numres) return -7;   // reduce must leave one resolution
     *W = ceildivpow2(im.w, g_dec_reduce); *H = ceildivpow2(im.h, g_dec_reduce); *NC = im.nc; *PREC = im.prec;
     if (!out) return 0;
@@ -2816,7 +2839,11 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         size_t j = pos + 12;   // tile-part header markers (PLT, POC, ...) until SOD
         std::vector<PocE> tp_pocs;
         while (j + 2 <= tile_end && get16(cs + j) != 0xff93) {
-            if (get16(cs + j) == 0xff5f && !read_poc(cs + j + 4, get16(cs + j + 2), im.nc, tp_pocs)) return -5;
+            const uint32_t tm = get16(cs + j);
+            if (tm == 0xff5f && !read_poc(cs + j + 4, get16(cs + j + 2), im.nc, tp_pocs)) return -5;
+            if ((tm == 0xff52 || tm == 0xff53 || tm == 0xff5c || tm == 0xff5d) &&
+                !restates_main(cs + j + 4, get16(cs + j + 2), tm, im.nc, cod_body, qcd_body)) return -2;
+            if (tm == 0xff5e) return -2;   // tile-part RGN
             j += 2 + get16(cs + j + 2);
         }
         if (j + 2 > tile_end) return -5;

@@ -1,0 +1,59 @@
+"""COC / QCC and tile-part COD / QCD markers in the oracle decoder.
+
+Grok reads COC / QCC (CodeStreamDecompress read_coc / read_qcc) and tile-part COD / QCD as
+per-component / per-tile overrides of the main COD / QCD.  This path codes every tile-component
+with the main header's parameters, so a marker that restates them decodes exactly as the stream
+without it (some encoders write them unconditionally), and one that changes them is refused
+rather than ignored.  Streams: the committed Grok fixtures with markers spliced in
+(tests/j2k_markers.py).  The engine half is tests/test_gpu_override_markers.py.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import FIXTURES, ROOT
+import j2k_markers as J
+
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle as O  # noqa: E402
+
+NAMES = ["rgb8_tiles_xl", "rgb12_97_r", "mono16_ht_tiles", "rgb8_prc"]
+
+
+def _fx(name):
+    return next(f for f in FIXTURES if f.name == name)
+
+
+def restating(cs):
+    n = J.ncomp(cs)
+    segs = b"".join(J.coc(cs, c) + J.qcc(cs, c) for c in range(n))
+    return J.insert_tile_part(J.insert_main(cs, segs), J.cod(cs) + J.qcd(cs) + J.coc(cs, n - 1) + J.qcc(cs, 0))
+
+
+def changing(cs):
+    yield "main COC", J.insert_main(cs, J.coc(cs, 0, sty_xor=0x02))
+    yield "main QCC", J.insert_main(cs, J.qcc(cs, J.ncomp(cs) - 1, guard_add=1))
+    yield "tile COD", J.insert_tile_part(cs, J.cod(cs, layers_add=1))
+    yield "tile COC", J.insert_tile_part(cs, J.coc(cs, 0, sty_xor=0x08))
+    yield "tile QCC", J.insert_tile_part(cs, J.qcc(cs, 0, guard_add=1))
+    yield "COC bad component", J.insert_main(cs, J.coc(cs, J.ncomp(cs)))
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_restating_markers_decode_as_without(name):
+    fx = _fx(name)
+    want, prec = O.decode(fx.cs)
+    got, prec2 = O.decode(restating(fx.cs))
+    assert prec == prec2
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got, fx.grok_decoded)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_changing_markers_refused(name):
+    fx = _fx(name)
+    for what, cs in changing(fx.cs):
+        with pytest.raises(RuntimeError, match="failed: -2"):
+            O.decode(cs)
