@@ -30,6 +30,7 @@
 
 #include "../../include/grok_amd.h"
 #include "gk_common.h"
+#include "gk_bitio.h"
 #include "gk_launch.h"
 
 namespace {
@@ -526,24 +527,8 @@ static void build_plan(Plan& P) {
 // ---------------------------------------------------------------------------
 // Packet-header bit writer / reader (t2/BitIO.cpp) and tag trees (t2/TagTree.h)
 // ---------------------------------------------------------------------------
-struct BitWriter {
-    std::vector<uint8_t>& o;
-    uint32_t buf = 0; int ct = 8;
-    explicit BitWriter(std::vector<uint8_t>& out) : o(out) {}
-    inline void wbyte() { o.push_back((uint8_t)buf); ct = (buf == 0xff) ? 7 : 8; buf = 0; }
-    inline void putbit(uint32_t b) { if (ct == 0) wbyte(); --ct; buf |= b << ct; }
-    inline void write(uint32_t v, int n) { for (int i = n - 1; i >= 0; --i) putbit((v >> i) & 1); }
-    inline void put(uint32_t v, uint32_t k) { write(v, (int)k); }
-    void flush() { wbyte(); if (ct == 7) wbyte(); }
-    void commacode(uint32_t n) { for (uint32_t i = 0; i < n; ++i) putbit(1); putbit(0); }
-    void numpasses(uint32_t n) {
-        if (n == 1) write(0, 1);
-        else if (n == 2) write(2, 2);
-        else if (n <= 5) write(0xc | (n - 3), 4);
-        else if (n <= 36) write(0x1e0 | (n - 6), 9);
-        else write(0xff80 | (n - 37), 16);
-    }
-};
+// bit-stuffed writer (gk_bitio.h)
+using BitWriter = PktBitWriter;
 
 struct TagTree {
     std::vector<int32_t> parent;
@@ -741,60 +726,9 @@ struct ByteSrc {
     }
 };
 std::atomic<uint64_t> ByteSrc::fetch_ns{0}, ByteSrc::fetch_cnt{0};
-// Packet-header bit reader (T2Decompress / BitIO: a byte after 0xFF carries 7 bits).  Bytes
-// come from a cached contiguous span of the source; bits are taken several at a time.
-struct BitReader {
-    ByteSrc& s; size_t off; size_t end; uint32_t buf = 0; int ct = 0;
-    const uint8_t* wp = nullptr; size_t wlo = 0, whi = 0;   // empty window
-    BitReader(ByteSrc& src, size_t o, size_t e) : s(src), off(o), end(e) {}
-    inline uint8_t byte_at(size_t i) {
-        if (i - wlo >= whi - wlo) {
-            if (i >= s.len) return 0;
-            wp = s.span(i, wlo, whi);
-        }
-        return wp[i - wlo];
-    }
-    inline void bytein() { ct = (buf == 0xff) ? 7 : 8; buf = off < end ? byte_at(off) : 0; ++off; }
-    inline uint32_t getbit() { if (ct == 0) bytein(); --ct; return (buf >> ct) & 1; }
-    inline uint32_t read(int n) {
-        uint32_t v = 0;
-        while (n > 0) {
-            if (ct == 0) bytein();
-            const int k = n < ct ? n : ct;
-            v = (v << k) | ((buf >> (ct - k)) & ((1u << k) - 1));
-            ct -= k; n -= k;
-        }
-        return v;
-    }
-    void align() { if (buf == 0xff) bytein(); ct = 0; }
-    uint32_t numpasses() {
-        if (!read(1)) return 1;
-        if (!read(1)) return 2;
-        uint32_t n = read(2);
-        if (n != 3) return n + 3;
-        n = read(5);
-        if (n != 31) return n + 6;
-        return read(7) + 37;
-    }
-    // Up to `limit` bits equal to `bit`, counted a byte at a time; when a different bit comes
-    // first it is consumed too and `ended` is set (what a read(1) loop would have read).
-    uint32_t run(uint32_t bit, uint32_t limit, bool& ended) {
-        uint32_t n = 0;
-        ended = false;
-        while (n < limit) {
-            if (ct == 0) bytein();
-            const uint32_t mask = (1u << ct) - 1;
-            const uint32_t r = (bit ? ~buf : buf) & mask;   // differing bits in the unread window
-            if (!r) { const uint32_t k = std::min<uint32_t>((uint32_t)ct, limit - n); n += k; ct -= (int)k; continue; }
-            const uint32_t z = (uint32_t)ct - 1 - (uint32_t)floorlog2(r);
-            if (n + z >= limit) { ct -= (int)(limit - n); return limit; }
-            n += z; ct -= (int)z + 1; ended = true;
-            return n;
-        }
-        return n;
-    }
-    uint32_t commacode() { bool e; return run(1, 0xffffffffu, e); }
-};
+// Packet-header bit reader (T2Decompress / BitIO: a byte after 0xFF carries 7 bits): up to 64
+// unread bits in one register (gk_bitio.h), bytes from the source's cached windows.
+using BitReader = PktBitReader<ByteSrc>;
 
 struct DecTree {   // decoder-side tag tree
     std::vector<int32_t> parent;
@@ -3541,7 +3475,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     const auto h2 = now();
     // ---- the decode table: the needed blocks of the rectangle's tiles, compacted, with offsets
     // into this call's planes and staging slots, band quantisation from QCD (decoder semantics)
-    std::vector<GkBlock> blk;
+    // (written straight into the pinned upload buffer: no vector growth, no extra copy)
+    size_t nmax = 0;
+    for (const auto& nd : part_need) nmax += (size_t)std::count(nd.begin(), nd.end(), (uint8_t)1);
+    GkBlock* blk = (GkBlock*)ctx->hinfo.get(sizeof(GkBlock) * std::max<size_t>(nmax, 1));
+    uint32_t nblk = 0;
     std::vector<uint32_t> hseglen;   // BYPASS / TERMALL: segment lengths, a block's at G.data_cap
     std::vector<std::vector<int32_t>> part_idx(Hd.parts.size());   // tile-local block -> table entry
     uint64_t o = 0, t1_bytes = 0;
@@ -3563,7 +3501,8 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                             for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
                                 const uint32_t lb = PG.first_block + k - T.b0;
                                 if (!need[lb]) continue;
-                                GkBlock G = P.blocks[T.b0 + lb];
+                                GkBlock& G = blk[nblk];
+                                G = P.blocks[T.b0 + lb];
                                 G.band_off = relocate(P, RG, G.band_off);
                                 G.stride = RG.stride;
                                 G.band_numbps = (uint8_t)R.bands[bi].numbps;
@@ -3583,13 +3522,12 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                 t1_bytes += G.len;
                                 o += (((uint64_t)G.len + 15) & ~15ull) + 32;
                                 G.len = 0;   // reused as the fill cursor below
-                                idx[lb] = (int32_t)blk.size();
-                                blk.push_back(G);
+                                idx[lb] = (int32_t)nblk++;
                             }
                         }
                 }
         }
-    const uint32_t nbr = (uint32_t)blk.size(), nbx = std::max(nbr, 1u);
+    const uint32_t nbr = nblk, nbx = std::max(nbr, 1u);
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     // ---- stage compressed bytes on the device.  A host stream of which the selected blocks
     // use a small part (window decode of a large file) is gathered on the host and only those
@@ -3604,18 +3542,21 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // gather every selected block's segments into a 16-byte aligned slot followed by >= 32
     // bytes of 0xFF (the T1 decoders read their bytes through aligned windows; the Part-1
     // decoder takes the padding as the MQ end-of-data bytes)
-    std::vector<uint64_t> seg;
+    // (pos, slot position, length) triples, straight into the pinned upload buffer
+    size_t nseg = 0;
+    uint64_t* seg = nullptr;
     {
         size_t nch = 0;
         for (auto& p2 : ps) nch += p2.chunks.size();
-        seg.reserve(3 * nch);
+        seg = (uint64_t*)ctx->hseg.get(3 * nch * 8 + 8);
         for (size_t q = 0; q < ps.size(); ++q)
             for (const Chunk& ch : ps[q].chunks) {   // stream order = layer order within a block
                 if (part_idx[q].empty()) continue;
                 const int32_t k = part_idx[q][ch.b];
                 if (k < 0) continue;
                 GkBlock& G = blk[k];
-                seg.push_back(ch.pos); seg.push_back(G.data_off + G.len); seg.push_back(ch.len);
+                seg[nseg] = ch.pos; seg[nseg + 1] = G.data_off + G.len; seg[nseg + 2] = ch.len;
+                nseg += 3;
                 G.len += ch.len;
             }
     }
@@ -3624,16 +3565,14 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipStreamSynchronize(st));   // the pinned staging buffer may still feed an earlier copy
         uint8_t* hst = (uint8_t*)ctx->hstage2.get(o + 256);
         if (!P.p.ht()) memset(hst, 0xff, o);
-        for (size_t k = 0; k < seg.size(); k += 3) memcpy(hst + seg[k + 1], cs + seg[k], seg[k + 2]);
+        for (size_t k = 0; k < nseg; k += 3) memcpy(hst + seg[k + 1], cs + seg[k], seg[k + 2]);
         HIPCHK(hipMemcpyAsync(stg, hst, o, hipMemcpyHostToDevice, st));
     } else {
     if (!P.p.ht()) HIPCHK(hipMemsetAsync(stg, 0xff, o, st));
-    if (!seg.empty()) {
-        uint64_t* hs = (uint64_t*)ctx->hseg.get(seg.size() * 8 + 8);
-        memcpy(hs, seg.data(), seg.size() * 8);
-        uint64_t* ds = (uint64_t*)ctx->dseg.get(seg.size() * 8 + 8);
-        HIPCHK(hipMemcpyAsync(ds, hs, seg.size() * 8, hipMemcpyHostToDevice, st));
-        gk_launch_gather(st, dcs, stg, ds, (uint32_t)(seg.size() / 3));
+    if (nseg) {
+        uint64_t* ds = (uint64_t*)ctx->dseg.get(nseg * 8 + 8);
+        HIPCHK(hipMemcpyAsync(ds, seg, nseg * 8, hipMemcpyHostToDevice, st));
+        gk_launch_gather(st, dcs, stg, ds, (uint32_t)(nseg / 3));
     }
     }
     const uint8_t* src_bytes = stg;
@@ -3643,9 +3582,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 ms(h0, h1), ms(h1, h2), ms(h2, now()), Hd.parts.size(), nbr,
                 (unsigned long long)ByteSrc::fetch_cnt.load(), ByteSrc::fetch_ns.load() * 1e-6);
     GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * nbx);
-    GkBlock* hblk = (GkBlock*)ctx->hinfo.get(sizeof(GkBlock) * nbx);
-    memcpy(hblk, blk.data(), sizeof(GkBlock) * nbr);
-    HIPCHK(hipMemcpyAsync(dblk, hblk, sizeof(GkBlock) * nbr, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dblk, blk, sizeof(GkBlock) * nbr, hipMemcpyHostToDevice, st));
     ctx->blocks_uploaded = false;   // the encode table must be re-uploaded
     int32_t* arena = (int32_t*)ctx->arena.get(RG.plane * P.nc * 2 * sizeof(int32_t));
     // tiles of the rectangle without a tile part decode as zero; blocks skipped by the window
@@ -3696,7 +3633,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         {
             std::fill(hord, hord + nslots, 0xffffffffu);
             std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
-            for (const GkBlock& G : blk) cnt[std::min<uint32_t>(G.npasses, GK_MAX_PASSES + 1)]++;
+            for (uint32_t q = 0; q < nbr; ++q) cnt[std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1)]++;
             std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
             uint32_t acc = 0;
             for (int k = GK_MAX_PASSES + 1; k >= 0; --k) { start[k] = acc; acc += cnt[k]; }
@@ -3734,7 +3671,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         }
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         uint32_t maxnp = 1;
-        for (const GkBlock& G : blk) maxnp = std::max<uint32_t>(maxnp, G.numbps);
+        for (uint32_t q = 0; q < nbr; ++q) maxnp = std::max<uint32_t>(maxnp, blk[q].numbps);
         gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr, maxnp);
     }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
