@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgrok_amd.so")
 # Grok's plugin loader opens <pluginPath>/libgrokj2k_plugin.so (grok.cpp:579-605)
 PLUGIN = os.path.join(HERE, "libgrokj2k_plugin.so")
-ENGINE = ["gk_kernels.hip", "gk_dwt97.hip", "gk_t1enc.hip", "gk_t1dec.hip", "gk_t1ms.hip", "gk_ht.hip", "gk_engine.cpp"]
+ENGINE = ["gk_kernels.hip", "gk_dwt97.hip", "gk_dwt_any.hip", "gk_t1enc.hip", "gk_t1dec.hip", "gk_t1ms.hip", "gk_ht.hip", "gk_engine.cpp"]
 SOURCES = ENGINE + ["grk_shim.cpp", "grk_plugin.cpp"]
 
 

@@ -192,10 +192,16 @@ struct TileG {
     std::vector<CompG> comps;
     uint32_t b0 = 0, b1 = 0;             // code-block range in Plan::blocks
 };
-// A rectangular batch of equally-sized tiles: one DWT launch per level (grid.z = tile).
+// A class of tiles with the same geometry at every level (size, and resolution origins of the
+// same parity): one DWT launch per level (grid.z = tile).  On a grid whose tile sizes are
+// multiples of 2^L there are at most four (interior / last column x interior / last row); other
+// sizes split the columns (rows) by tile origin modulo 2^L, so a class is the tile columns
+// ci + k * si (rows cj + k * sj), k < tb.nx (tb.ny), and tb.dx = si * tw.
 struct ShapeG {
     uint32_t w, h;
     std::vector<uint32_t> resw, resh;    // resolution sizes by level l = 0..L (l=0: full tile)
+    std::vector<uint8_t> parx, pary;     // parity of the resolution origins by level (odd: cas1 lifting)
+    uint32_t ci = 0, cj = 0, si = 1, sj = 1;
     GkTiles tb;
 };
 
@@ -207,6 +213,7 @@ struct Plan {
     uint32_t ntx = 1, nty = 1, tw = 0, th = 0;   // tile grid
     std::vector<TileG> tiles;            // raster order
     std::vector<ShapeG> shapes;
+    bool l1_fusable = true;              // every tile origin even: level 1 fuses with DC shift / MCT
     std::vector<GkBlock> blocks;         // tile order, then canonical: comp, res, band, precinct, cblk
     std::vector<uint32_t> bxy;           // per block: top-left (x, y) in its band's coordinates
     uint64_t slot_bytes = 0;
@@ -471,26 +478,43 @@ static void build_plan(Plan& P) {
     P.tw = P.p.tw ? std::min(P.p.tw, P.w) : P.w;
     P.th = P.p.th ? std::min(P.p.th, P.h) : P.h;
     P.ntx = (P.w + P.tw - 1) / P.tw; P.nty = (P.h + P.th - 1) / P.th;
-    // every tile origin must sit on the 2^L grid so each tile's DWT has even parity at all levels
-    if ((P.ntx > 1 && (P.tw & ((1u << L) - 1))) || (P.nty > 1 && (P.th & ((1u << L) - 1))))
-        throw GkError("tile sizes must be multiples of 2^(numresolution-1) on this path");
     if ((size_t)P.ntx * P.nty > 65535) throw GkError("too many tiles");
-    // shape classes: {interior, last column} x {interior, last row}
+    // tile classes: along each axis the tiles before the last fall into classes by origin
+    // modulo 2^L (m = 2^L / gcd(t, 2^L) of them, an arithmetic progression each); the last
+    // tile (a different size) is a class of its own
+    struct Axis { uint32_t first, step, count, size; };
+    auto classes = [&](uint32_t n, uint32_t t, uint32_t last) {
+        std::vector<Axis> v;
+        const uint32_t G = 1u << L, g = (t & (0u - t)) < G ? (t & (0u - t)) : G;   // gcd(t, 2^L)
+        const uint32_t m = G / g;
+        for (uint32_t c = 0; c < std::min(m, n - 1); ++c) v.push_back({c, m, (n - 1 - c + m - 1) / m, t});
+        v.push_back({n - 1, 1, 1, last});
+        return v;
+    };
     const uint32_t lw = P.w - (P.ntx - 1) * P.tw, lh = P.h - (P.nty - 1) * P.th;
+    const std::vector<Axis> cx = classes(P.ntx, P.tw, lw), cy = classes(P.nty, P.th, lh);
     P.shapes.clear();
+    P.l1_fusable = true;
     std::vector<int> shape_of((size_t)P.ntx * P.nty, -1);
-    for (int cj = 0; cj < 2; ++cj)
-        for (int ci = 0; ci < 2; ++ci) {
-            uint32_t i0 = ci ? P.ntx - 1 : 0, nx = ci ? 1 : P.ntx - 1;
-            uint32_t j0 = cj ? P.nty - 1 : 0, ny = cj ? 1 : P.nty - 1;
-            if (!nx || !ny) continue;
+    for (const Axis& ay : cy)
+        for (const Axis& ax : cx) {
             ShapeG S;
-            S.w = ci ? lw : P.tw; S.h = cj ? lh : P.th;
-            S.resw.resize(L + 1); S.resh.resize(L + 1);
-            for (uint32_t l = 0; l <= L; ++l) { S.resw[l] = ceildivpow2(S.w, l); S.resh[l] = ceildivpow2(S.h, l); }
-            S.tb.nx = nx; S.tb.ny = ny; S.tb.i0 = i0; S.tb.j0 = j0; S.tb.dx = P.tw; S.tb.dy = P.th;
-            for (uint32_t j = j0; j < j0 + ny; ++j)
-                for (uint32_t i = i0; i < i0 + nx; ++i) shape_of[(size_t)j * P.ntx + i] = (int)P.shapes.size();
+            S.w = ax.size; S.h = ay.size;
+            const uint32_t x0 = ax.first * P.tw, y0 = ay.first * P.th;   // any member: the same geometry
+            S.resw.resize(L + 1); S.resh.resize(L + 1); S.parx.resize(L + 1); S.pary.resize(L + 1);
+            for (uint32_t l = 0; l <= L; ++l) {
+                S.resw[l] = ceildivpow2(x0 + S.w, l) - ceildivpow2(x0, l);
+                S.resh[l] = ceildivpow2(y0 + S.h, l) - ceildivpow2(y0, l);
+                S.parx[l] = (uint8_t)(ceildivpow2(x0, l) & 1);
+                S.pary[l] = (uint8_t)(ceildivpow2(y0, l) & 1);
+            }
+            if (S.parx[0] || S.pary[0]) P.l1_fusable = false;
+            S.ci = ax.first; S.si = ax.step; S.cj = ay.first; S.sj = ay.step;
+            S.tb.nx = ax.count; S.tb.ny = ay.count; S.tb.i0 = 0; S.tb.j0 = 0;
+            S.tb.dx = ax.step * P.tw; S.tb.dy = ay.step * P.th;
+            for (uint32_t b = 0; b < ay.count; ++b)
+                for (uint32_t a = 0; a < ax.count; ++a)
+                    shape_of[(size_t)(ay.first + b * ay.step) * P.ntx + ax.first + a * ax.step] = (int)P.shapes.size();
             P.shapes.push_back(S);
         }
     P.tiles.assign((size_t)P.ntx * P.nty, TileG());
@@ -2239,15 +2263,37 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
     const uint32_t nlev = forward ? L : (L + 1 > lstop ? L + 1 - lstop : 0);
     for (uint32_t i = 0; i < nlev; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
-        for (const ShapeG& S0 : P.shapes) {       // one launch per tile shape, grid.z = tiles of that shape
+        for (const ShapeG& S0 : P.shapes) {       // one launch per tile class, grid.z = its tiles
             ShapeG S = S0;                        // restricted to tile rows [jb, je), columns [ib, ie)
-            const uint32_t sj0 = std::max(S.tb.j0, jb), sj1 = std::min(S.tb.j0 + S.tb.ny, je);
-            const uint32_t si0 = std::max(S.tb.i0, ib), si1 = std::min(S.tb.i0 + S.tb.nx, ie);
-            if (sj0 >= sj1 || si0 >= si1) continue;
-            S.tb.j0 = sj0; S.tb.ny = sj1 - sj0;
-            S.tb.i0 = si0; S.tb.nx = si1 - si0;
-            S.tb.ox = RG.x0; S.tb.oy = RG.y0;
+            // members k of the class: tile column ci + k si; those in [ib, ie) are k in [k0, k1)
+            auto krange = [](uint64_t c, uint64_t st, uint32_t n, uint64_t b, uint64_t e, uint32_t& k0, uint32_t& k1) {
+                k0 = (uint32_t)std::min<uint64_t>(n, b > c ? (b - c + st - 1) / st : 0);
+                k1 = (uint32_t)(e > c ? std::min<uint64_t>(n, (e - c + st - 1) / st) : 0);
+            };
+            uint32_t ki0, ki1, kj0, kj1;
+            krange(S.ci, S.si, S.tb.nx, ib, ie, ki0, ki1);
+            krange(S.cj, S.sj, S.tb.ny, jb, je, kj0, kj1);
+            if (ki0 >= ki1 || kj0 >= kj1) continue;
+            S.tb.i0 = ki0; S.tb.nx = ki1 - ki0;
+            S.tb.j0 = kj0; S.tb.ny = kj1 - kj0;
+            // x = (ci + si k) tw - RG.x0 = k dx - ox (modulo 2^32; the true value is >= 0)
+            S.tb.ox = RG.x0 - S.ci * P.tw; S.tb.oy = RG.y0 - S.cj * P.th;
             const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
+            // a level whose input resolution starts on an odd coordinate (either axis), or every
+            // level under GK_DWT_ANY: the parity-general kernels (gk_dwt_any.hip)
+            static const bool force_any = getenv("GK_DWT_ANY") != nullptr;
+            if ((S.parx[l - 1] || S.pary[l - 1] || force_any) && !(l == 1 && io)) {
+                int32_t* A = arena;
+                int32_t* B = A + RG.plane;
+                int32_t* src_l = (l & 1) ? A : B;
+                int32_t* dst_l = (l & 1) ? B : A;
+                const uint64_t area = (uint64_t)w * h * S.tb.count();
+                gk_launch_dwt_any(ctx->st, P.p.irrev, forward, forward ? src_l : dst_l, forward ? dst_l : src_l, RG.stride,
+                                  w, h, S.parx[l - 1], S.pary[l - 1], S.tb, GkComps{cst, P.nc});
+                ctx->tm.dwt_launches += 3;
+                ctx->tm.dwt_bytes += area * 8 * P.nc;
+                continue;
+            }
             const uint64_t area = (uint64_t)w * h * S.tb.count();
             int32_t* A = arena;
             int32_t* B = A + RG.plane;
@@ -2446,7 +2492,9 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const bool mct3 = P.p.mct && P.nc >= 3;
     if (mct3 && (sstr[1] != sstr[0] || sstr[2] != sstr[0])) throw GkError("the first three components must share a stride");
     L1Io io;
-    const bool fused = P.p.numres > 1;   // DC shift + MCT run inside the first DWT level
+    // DC shift + MCT run inside the first DWT level (unless a tile starts on an odd coordinate:
+    // then they run first and level 1 takes the parity-general kernels)
+    const bool fused = P.p.numres > 1 && P.l1_fusable;
     if (fused) {
         io.stype = stype; io.mct3 = mct3; io.shift = shift;
         io.planes.assign(src.begin(), src.end());
@@ -2460,6 +2508,17 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     run_dwt(ctx, RG, true, jb, je, 0, 0xffffffffu, fused ? &io : nullptr);
+    if (const char* dp = getenv("GK_DUMP_DWT")) {   // debug: the work planes after the forward DWT
+        std::vector<int32_t> hv((size_t)P.nc * 2 * RG.plane);
+        HIPCHK(hipMemcpyAsync(hv.data(), arena, hv.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        if (FILE* f = fopen(dp, "wb")) {
+            const uint32_t hd[4] = {P.nc, RG.stride, RG.h, RG.w};
+            fwrite(hd, 4, 4, f);
+            fwrite(hv.data(), 4, hv.size(), f);
+            fclose(f);
+        }
+    }
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // T1 over the block range [b0, b1): every per-block device array is range-local
     const bool do_rc = P.p.rate_control();
@@ -3686,11 +3745,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     if (red) {
         // reduced resolution: undo levels L .. red+1; resolution numres-1-red of each tile is
         // then at the tile's corner of plane (red odd ? B : A); the inverse MCT + DC + clamp
-        // writes it per tile into the ceil(size / 2^red) output (tile origins lie on the
-        // 2^levels grid, so a tile's reduced origin is its origin >> red)
+        // writes it per tile into the ceil(size / 2^red) output (a tile's reduced origin is
+        // ceil(origin / 2^red), B.5)
         run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr, red + 1);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
-        const uint32_t qx0 = RG.x0 >> red, qy0 = RG.y0 >> red;
+        const uint32_t qx0 = ceildivpow2(RG.x0, red), qy0 = ceildivpow2(RG.y0, red);
         const uint32_t qcols = ceildivpow2(RG.x0 + RG.w, red) - qx0, qrows = ceildivpow2(RG.y0 + RG.h, red) - qy0;
         std::vector<uint8_t*> qd(P.nc);
         std::vector<uint32_t> qs(P.nc);
@@ -3703,7 +3762,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         for (uint32_t j = jb; j < je; ++j)
             for (uint32_t i = ib; i < ie; ++i) {
                 const TileG& T = P.tiles[(size_t)j * P.ntx + i];
-                const uint32_t tx0 = T.x0 >> red, ty0 = T.y0 >> red;
+                const uint32_t tx0 = ceildivpow2(T.x0, red), ty0 = ceildivpow2(T.y0, red);
                 const uint32_t tw = ceildivpow2(T.x1, red) - tx0, th = ceildivpow2(T.y1, red) - ty0;
                 auto src = [&](uint32_t c) {
                     return arena + (size_t)c * 2 * RG.plane + ((red & 1) ? RG.plane : 0) +
@@ -3753,7 +3812,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
     const bool mct3 = P.p.mct && P.nc >= 3;
-    if (P.p.numres > 1) {
+    if (P.p.numres > 1 && !P.l1_fusable) {   // levels first, then the inverse MCT + DC shift + clamp below
+        run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr);
+    }
+    if (P.p.numres > 1 && P.l1_fusable) {
         L1Io io;
         io.stype = stype; io.mct3 = mct3; io.shift = shift; io.mn = mn; io.mx = mx;
         io.planes.assign(dst.begin(), dst.end());

@@ -2418,7 +2418,9 @@ void orc_forward_coefs(const int32_t* planes, uint32_t w, uint32_t h, uint32_t n
                        const orc_cparams* cp, int32_t* out) {
     EncodeState E;
     prepare_encode(E, planes, w, h, nc, prec, sgnd, cp);
-    for (uint32_t c = 0; c < nc; ++c) memcpy(out + (size_t)c * w * h, E.coefs[c].data(), (size_t)w * h * 4);
+    for (uint32_t c = 0; c < nc; ++c)   // 9/7: the float coefficients' bits
+        memcpy(out + (size_t)c * w * h, E.p.irreversible ? (const void*)E.fcoefs[c].data() : (const void*)E.coefs[c].data(),
+               (size_t)w * h * 4);
 }
 
 // Stage dump: per-block T1 results in canonical order.  Two calls: first with

@@ -4,8 +4,8 @@ in one T1 launch, per-tile T2, SOT/TLM/PLT) vs Grok and the oracle.
 Bar: codestreams byte-identical to
 Grok's `-t W,H [-X] [-L]` output (fixtures) and to the oracle on seeded random
 tilings (ragged edge tiles, 1-tile-wide strips, Part 1 and HT, TLM/PLT on and
-off); decodes sample-exact.  Tile sizes are multiples of 2^(levels) (tile DWT
-parity 0), which covers the C4/C5 configurations (1024 x 1024 tiles).
+off); decodes sample-exact.  These tilings are multiples of 2^(levels) (tile DWT parity 0,
+the C4/C5 configurations); other tile sizes are tests/test_gpu_odd_tiles.py.
 """
 import numpy as np
 import pytest
@@ -89,10 +89,11 @@ def test_tiled_97(eng):
 
 
 def test_tile_grid_rules(eng):
-    # tile sizes off the 2^levels grid are refused (the tile DWT would need odd parity)
-    img = np.zeros((1, 100, 100), np.int32)
-    with pytest.raises(RuntimeError):
-        eng.encode(img, 8, params=_params(tiles=(48, 48)))
+    # tile sizes off the 2^levels grid: odd-parity levels (tests/test_gpu_odd_tiles.py)
+    img = (np.arange(100 * 100, dtype=np.int32).reshape(1, 100, 100) * 7) % 251
+    cs = eng.encode(img, 8, params=_params(tiles=(48, 48)))
+    assert cs == O.encode(img, 8, tiles=(48, 48))
+    np.testing.assert_array_equal(eng.decode(cs), img)
     # a tile larger than the image is a single tile
     cs = eng.encode(img, 8, params=_params(tiles=(4096, 4096)))
     np.testing.assert_array_equal(eng.decode(cs), img)
