@@ -52,12 +52,13 @@ class CParameters(ctypes.Structure):
         ("roi_compno", ctypes.c_int32), ("roi_shift", ctypes.c_uint32),
         ("numpocs", ctypes.c_uint32), ("pocs", Poc * 32),
         ("allocationByQuality", ctypes.c_uint8), ("layer_distortion", ctypes.c_double * GK_MAX_LAYERS),
+        ("tx0", ctypes.c_uint32), ("ty0", ctypes.c_uint32),
     ]
 
 
 class ImageInfo(ctypes.Structure):
     """gk_image_info; sample_bytes: 0/4 = int32 planes, 1/2 = planar 8/16-bit samples."""
-    _fields_ = [(n, ctypes.c_uint32) for n in ("w", "h", "numcomps", "prec", "sgnd", "sample_bytes")]
+    _fields_ = [(n, ctypes.c_uint32) for n in ("w", "h", "numcomps", "prec", "sgnd", "sample_bytes", "x0", "y0")]
 
 
 class Timings(ctypes.Structure):
@@ -129,7 +130,8 @@ PROG_ORDERS = ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"]   # GRK_PROG_ORDER (grok.
 
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
                    precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False,
-                   prog_order="LRCP", tile_parts=None, pocs=None, roi=None, sop=False, eph=False, quality=None):
+                   prog_order="LRCP", tile_parts=None, pocs=None, roi=None, sop=False, eph=False, quality=None,
+                   tile_origin=None):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
     prog_order: "LRCP", "RLCP", "RPCL", "PCRL", "CPRL" or 0..4 (grk_compress -p).
@@ -139,6 +141,8 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
     p = CParameters()
     lib.gk_set_default_params(ctypes.byref(p))
     p.numresolution = numresolution
+    if tile_origin:   # grk_compress -T: the tile grid's canvas origin (the image origin is Engine.encode's `origin`)
+        p.tx0, p.ty0 = int(tile_origin[0]), int(tile_origin[1])
     p.cblockw_init, p.cblockh_init = cblk
     p.irreversible = int(irreversible)
     p.mct = int(mct)
@@ -251,10 +255,12 @@ class Engine:
         return t
 
     # ------------------------------------------------------------------ encode
-    def encode(self, planes, prec, signed=False, params=None, out=None):
+    def encode(self, planes, prec, signed=False, params=None, out=None, origin=None):
         """planes: (C, H, W) int32 numpy array (host) or torch cuda tensor (device).
         Returns bytes (host) or, when ``out`` (a torch cuda uint8 tensor) is given,
-        the codestream length written into it on the device."""
+        the codestream length written into it on the device.  origin: the image area's
+        canvas origin (grk_image::x0 / y0, grk_compress -d); without it the image sits at
+        the tile grid origin (-T alone moves the image there, grk_compress.cpp:1547-1551)."""
         if params is None:
             params = default_params()
         c, h, w = planes.shape
@@ -268,6 +274,10 @@ class Engine:
         sb = _sample_bytes(planes)
         es = sb or 4
         info = ImageInfo(w, h, c, prec, int(signed), sb)
+        if origin is not None:
+            info.x0, info.y0 = int(origin[0]), int(origin[1])
+        else:
+            info.x0, info.y0 = params.tx0, params.ty0
         ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * es for k in range(c)])
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         n = ctypes.c_size_t()
@@ -315,6 +325,7 @@ class Engine:
         assert W == w
         ptrs, keep = self._planes_ptrs(planes, row0, prec)
         info = ImageInfo(W, H, c, prec, int(signed), _sample_bytes(keep))
+        info.x0, info.y0 = params.tx0, params.ty0
         on_dev = _is_torch_cuda(planes)
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         lens = (ctypes.c_uint32 * (tile_end - tile_begin))()
@@ -351,6 +362,7 @@ class Engine:
             params = default_params()
         c, h, w = image_shape
         info = ImageInfo(w, h, c, prec, int(signed), 0)
+        info.x0, info.y0 = params.tx0, params.ty0
         buf = np.empty(1 << 20, np.uint8)
         n, tlm, nt = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_uint32()
         rc = self.lib.gk_main_header(self.ctx, ctypes.byref(info), ctypes.byref(params), buf.ctypes.data, buf.size,
@@ -427,8 +439,9 @@ class Engine:
         info = self.read_header(cs, length)
         c, h, w = info.numcomps, info.h, info.w
         red = getattr(self, "_reduce", 0)
-        if red:   # reduced-resolution output: ceil(size / 2^reduce)
-            h, w = -(-h // (1 << red)), -(-w // (1 << red))
+        if red:   # reduced-resolution output: the image area on the reduced canvas (ceil(x / 2^reduce))
+            cd = lambda v: -(-v // (1 << red))
+            h, w = cd(info.y0 + h) - cd(info.y0), cd(info.x0 + w) - cd(info.x0)
         strides = (ctypes.c_uint32 * c)(*([w] * c))
         if out is not None:
             sample_bytes = _sample_bytes(out)

@@ -202,11 +202,16 @@ struct ShapeG {
     std::vector<uint32_t> resw, resh;    // resolution sizes by level l = 0..L (l=0: full tile)
     std::vector<uint8_t> parx, pary;     // parity of the resolution origins by level (odd: cas1 lifting)
     uint32_t ci = 0, cj = 0, si = 1, sj = 1;
+    uint32_t px0 = 0, py0 = 0;           // plane position of the first member's top-left
     GkTiles tb;
 };
 
 struct Plan {
     uint32_t w = 0, h = 0, nc = 0, prec = 0, sgnd = 0;
+    // canvas (B.2-B.3): the image area starts at (x0, y0), the tile grid at (gx0, gy0) <= (x0, y0).
+    // Tile and band geometry are canvas coordinates; work planes hold the image area, so a plane
+    // position is a canvas position less (x0, y0).
+    uint32_t x0 = 0, y0 = 0, gx0 = 0, gy0 = 0;
     Params p;
     uint32_t stride = 0;                 // work-plane stride (samples)
     size_t plane_elems = 0;              // per plane
@@ -444,7 +449,8 @@ static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
                         const uint32_t x1 = std::min(kx0 + (1u << R.cbw), px1), y1 = std::min(ky0 + (1u << R.cbh), py1);
                         GkBlock G{};
                         const size_t plane_base = ((size_t)c * 2 + B.plane) * P.plane_elems;
-                        G.band_off = plane_base + (size_t)(T.y0 + B.offy + y0 - B.y0) * P.stride + (T.x0 + B.offx + x0 - B.x0);
+                        G.band_off = plane_base + (size_t)(T.y0 - P.y0 + B.offy + y0 - B.y0) * P.stride +
+                                     (T.x0 - P.x0 + B.offx + x0 - B.x0);
                         G.stride = P.stride;
                         G.w = (uint16_t)(x1 - x0); G.h = (uint16_t)(y1 - y0);
                         G.orient = (uint8_t)B.orient; G.comp = (uint8_t)c;
@@ -475,24 +481,32 @@ static void build_plan(Plan& P) {
     const uint32_t L = P.p.numres - 1;
     P.stride = align_up(std::max(P.w, 1u), 64);
     P.plane_elems = (size_t)P.stride * P.h;
-    P.tw = P.p.tw ? std::min(P.p.tw, P.w) : P.w;
-    P.th = P.p.th ? std::min(P.p.th, P.h) : P.h;
-    P.ntx = (P.w + P.tw - 1) / P.tw; P.nty = (P.h + P.th - 1) / P.th;
+    // canvas extent of the image: [x0, X1) x [y0, Y1); without tiling one tile from the grid origin
+    // (CodeStreamCompress.cpp:352-363)
+    const uint32_t X1 = P.x0 + P.w, Y1 = P.y0 + P.h;
+    P.tw = P.p.tw ? std::min(P.p.tw, X1 - P.gx0) : X1 - P.gx0;
+    P.th = P.p.th ? std::min(P.p.th, Y1 - P.gy0) : Y1 - P.gy0;
+    P.ntx = (X1 - P.gx0 + P.tw - 1) / P.tw; P.nty = (Y1 - P.gy0 + P.th - 1) / P.th;
     if ((size_t)P.ntx * P.nty > 65535) throw GkError("too many tiles");
-    // tile classes: along each axis the tiles before the last fall into classes by origin
-    // modulo 2^L (m = 2^L / gcd(t, 2^L) of them, an arithmetic progression each); the last
-    // tile (a different size) is a class of its own
-    struct Axis { uint32_t first, step, count, size; };
-    auto classes = [&](uint32_t n, uint32_t t, uint32_t last) {
+    // tile classes: along each axis tile k spans [max(g + k t, o), min(g + (k + 1) t, end)); the
+    // last tile (and a first tile cut by the image origin) is a class of its own, the others fall
+    // into classes by origin modulo 2^L (m = 2^L / gcd(t, 2^L) of them, an arithmetic progression
+    // each; one class on a 2^L-aligned grid)
+    struct Axis { uint32_t first, step, count, size, origin; };   // origin: canvas position of the first member
+    auto classes = [&](uint32_t n, uint32_t t, uint32_t g, uint32_t o, uint32_t end) {
         std::vector<Axis> v;
-        const uint32_t G = 1u << L, g = (t & (0u - t)) < G ? (t & (0u - t)) : G;   // gcd(t, 2^L)
-        const uint32_t m = G / g;
-        for (uint32_t c = 0; c < std::min(m, n - 1); ++c) v.push_back({c, m, (n - 1 - c + m - 1) / m, t});
-        v.push_back({n - 1, 1, 1, last});
+        auto lo = [&](uint32_t k) { return std::max(g + k * t, o); };
+        auto hi = [&](uint32_t k) { return std::min(g + (k + 1) * t, end); };
+        // a first tile on the grid with the nominal size joins its residue class
+        const uint32_t c0 = (o == g && n > 1) ? 0 : 1;
+        if (c0) v.push_back({0, 1, 1, hi(0) - lo(0), lo(0)});
+        if (n == 1) return v;
+        const uint32_t G = 1u << L, lb = t & (0u - t), m = G / (lb < G ? lb : G);   // gcd(t, 2^L) = lowest set bit, capped
+        for (uint32_t c = c0; c < std::min(c0 + m, n - 1); ++c) v.push_back({c, m, (n - 1 - c + m - 1) / m, t, lo(c)});
+        v.push_back({n - 1, 1, 1, hi(n - 1) - lo(n - 1), lo(n - 1)});
         return v;
     };
-    const uint32_t lw = P.w - (P.ntx - 1) * P.tw, lh = P.h - (P.nty - 1) * P.th;
-    const std::vector<Axis> cx = classes(P.ntx, P.tw, lw), cy = classes(P.nty, P.th, lh);
+    const std::vector<Axis> cx = classes(P.ntx, P.tw, P.gx0, P.x0, X1), cy = classes(P.nty, P.th, P.gy0, P.y0, Y1);
     P.shapes.clear();
     P.l1_fusable = true;
     std::vector<int> shape_of((size_t)P.ntx * P.nty, -1);
@@ -500,7 +514,7 @@ static void build_plan(Plan& P) {
         for (const Axis& ax : cx) {
             ShapeG S;
             S.w = ax.size; S.h = ay.size;
-            const uint32_t x0 = ax.first * P.tw, y0 = ay.first * P.th;   // any member: the same geometry
+            const uint32_t x0 = ax.origin, y0 = ay.origin;   // any member: the same geometry
             S.resw.resize(L + 1); S.resh.resize(L + 1); S.parx.resize(L + 1); S.pary.resize(L + 1);
             for (uint32_t l = 0; l <= L; ++l) {
                 S.resw[l] = ceildivpow2(x0 + S.w, l) - ceildivpow2(x0, l);
@@ -510,6 +524,7 @@ static void build_plan(Plan& P) {
             }
             if (S.parx[0] || S.pary[0]) P.l1_fusable = false;
             S.ci = ax.first; S.si = ax.step; S.cj = ay.first; S.sj = ay.step;
+            S.px0 = x0 - P.x0; S.py0 = y0 - P.y0;
             S.tb.nx = ax.count; S.tb.ny = ay.count; S.tb.i0 = 0; S.tb.j0 = 0;
             S.tb.dx = ax.step * P.tw; S.tb.dy = ay.step * P.th;
             for (uint32_t b = 0; b < ay.count; ++b)
@@ -524,8 +539,8 @@ static void build_plan(Plan& P) {
     for (uint32_t t = 0; t < P.tiles.size(); ++t) {
         TileG& T = P.tiles[t];
         const uint32_t i = t % P.ntx, j = t / P.ntx;
-        T.x0 = i * P.tw; T.y0 = j * P.th;
-        T.x1 = std::min(T.x0 + P.tw, P.w); T.y1 = std::min(T.y0 + P.th, P.h);
+        T.x0 = std::max(P.gx0 + i * P.tw, P.x0); T.y0 = std::max(P.gy0 + j * P.th, P.y0);
+        T.x1 = std::min(P.gx0 + (i + 1) * P.tw, X1); T.y1 = std::min(P.gy0 + (j + 1) * P.th, Y1);
         build_tile(P, T, P.shapes[shape_of[t]]);
     }
     // encode slots: w*h*4 + 64 bytes each, 64-byte aligned (the MQ coder stores whole 64-byte lines)
@@ -1917,8 +1932,9 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
     put16(o, 0xff4f);
     put16(o, 0xff51); put16(o, 38 + 3 * P.nc);
     put16(o, P.p.ht() ? 0x4000 : 0);   // Rsiz: GRK_JPH_RSIZ_FLAG for HT (CodeStreamCompress.cpp:216-219)
-    put32(o, P.w); put32(o, P.h); put32(o, 0); put32(o, 0);
-    put32(o, P.p.tw ? P.p.tw : P.w); put32(o, P.p.th ? P.p.th : P.h); put32(o, 0); put32(o, 0);   // XTsiz YTsiz XTOsiz YTOsiz
+    put32(o, P.x0 + P.w); put32(o, P.y0 + P.h); put32(o, P.x0); put32(o, P.y0);   // Xsiz Ysiz XOsiz YOsiz
+    put32(o, P.p.tw ? P.p.tw : P.x0 + P.w - P.gx0); put32(o, P.p.th ? P.p.th : P.y0 + P.h - P.gy0);
+    put32(o, P.gx0); put32(o, P.gy0);                                              // XTsiz YTsiz XTOsiz YTOsiz
     put16(o, P.nc);
     for (uint32_t i = 0; i < P.nc; ++i) { o.push_back((uint8_t)((P.prec - 1) | (P.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
     if (P.p.ht()) {   // CAP (CodeStreamCompress::write_cap :1064-1111): Pcap bit 15, Ccap = MAGBp code
@@ -2206,6 +2222,7 @@ static std::string plan_key(const Plan& P) {
              P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0, P.p.rate_control() ? 1 : 0);
     std::string k(buf);
     k += " sty" + std::to_string(P.p.cblk_sty) + " t" + std::to_string(P.p.tw) + "x" + std::to_string(P.p.th);
+    k += " o" + std::to_string(P.x0) + "," + std::to_string(P.y0) + "," + std::to_string(P.gx0) + "," + std::to_string(P.gy0);
     for (size_t c = 0; c < P.p.roishift.size(); ++c)   // non-zero (component, shift) pairs only
         if (P.p.roishift[c]) k += " roi" + std::to_string(c) + ":" + std::to_string(P.p.roishift[c]);
     for (uint32_t r = 0; r < P.p.numres; ++r) k += " " + std::to_string(P.p.prcw[r]) + "," + std::to_string(P.p.prch[r]);
@@ -2276,8 +2293,8 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
             if (ki0 >= ki1 || kj0 >= kj1) continue;
             S.tb.i0 = ki0; S.tb.nx = ki1 - ki0;
             S.tb.j0 = kj0; S.tb.ny = kj1 - kj0;
-            // x = (ci + si k) tw - RG.x0 = k dx - ox (modulo 2^32; the true value is >= 0)
-            S.tb.ox = RG.x0 - S.ci * P.tw; S.tb.oy = RG.y0 - S.cj * P.th;
+            // member k's region position: px0 + k dx - RG.x0 = k dx - ox (modulo 2^32; the true value >= 0)
+            S.tb.ox = RG.x0 - S.px0; S.tb.oy = RG.y0 - S.py0;
             const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
             // a level whose input resolution starts on an odd coordinate (either axis), or every
             // level under GK_DWT_ANY: the parity-general kernels (gk_dwt_any.hip)
@@ -2359,6 +2376,16 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     Plan want;
     want.w = info->w; want.h = info->h; want.nc = info->numcomps; want.prec = info->prec; want.sgnd = info->sgnd;
     set_params(want.p, cp, want.nc);
+    // canvas offsets: image origin (grk_image::x0 / y0) and tile grid origin (grk_cparameters::tx0 / ty0);
+    // grk_compress.cpp:1554-1576 / B.3: the grid starts at or above-left of the image, its first
+    // tile reaches into the image area
+    want.x0 = info->x0; want.y0 = info->y0;
+    want.gx0 = cp ? cp->tx0 : 0; want.gy0 = cp ? cp->ty0 : 0;
+    if (want.gx0 > want.x0 || want.gy0 > want.y0) throw GkError("tile grid origin must lie at or above-left of the image origin");
+    if ((uint64_t)want.x0 + want.w > 0xffffffffull || (uint64_t)want.y0 + want.h > 0xffffffffull)
+        throw GkError("image area past the 32-bit canvas");
+    if (want.p.tw && ((uint64_t)want.gx0 + want.p.tw <= want.x0 || (uint64_t)want.gy0 + want.p.th <= want.y0))
+        throw GkError("the first tile must overlap the image area");
     if (want.nc < 3) want.p.mct = 0;
     check_poc_coverage(want.p, want.nc);
     if ((want.p.cblk_sty & GK_STY_HT) && want.p.cblk_sty != GK_STY_HT)
@@ -2459,7 +2486,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const uint32_t nb = (uint32_t)P.blocks.size();
     const uint32_t b0 = P.tiles[tb].b0, b1 = P.tiles[te - 1].b1, nbr = b1 - b0;   // block range of the tiles
     const uint32_t jb = tb / P.ntx, je = (te - 1) / P.ntx + 1;                     // tile rows touched
-    const uint32_t ry0 = P.tiles[jb * P.ntx].y0, ry1 = P.tiles[(je - 1) * P.ntx].y1;  // sample rows touched
+    const uint32_t ry0 = P.tiles[jb * P.ntx].y0 - P.y0, ry1 = P.tiles[(je - 1) * P.ntx].y1 - P.y0;  // image rows touched
     hipStream_t st = ctx->st;
 
     HIPCHK(hipEventRecord(ctx->ev[0], st));
@@ -3025,12 +3052,17 @@ static void parse_header(ByteSrc& S, Header& Hd) {
         if (L < 2 || i + 2 + L > S.len) throw GkError("corrupt main header (marker length)");
         if (m == 0xff51) {
             if (L < 41) throw GkError("corrupt SIZ marker");
-            W.w = S.be32(s + 2) - S.be32(s + 10); W.h = S.be32(s + 6) - S.be32(s + 14);
-            if (S.be32(s + 10) || S.be32(s + 14)) throw GkError("image offsets not supported");
-            if (S.be32(s + 26) || S.be32(s + 30)) throw GkError("tile grid offsets not supported");
+            const uint32_t X1 = S.be32(s + 2), Y1 = S.be32(s + 6);
+            W.x0 = S.be32(s + 10); W.y0 = S.be32(s + 14); W.gx0 = S.be32(s + 26); W.gy0 = S.be32(s + 30);
+            if (X1 <= W.x0 || Y1 <= W.y0) throw GkError("corrupt SIZ marker (empty image)");
+            W.w = X1 - W.x0; W.h = Y1 - W.y0;
             W.p.tw = S.be32(s + 18); W.p.th = S.be32(s + 22);
             if (!W.p.tw || !W.p.th) throw GkError("bad tile size");
-            if (W.p.tw >= W.w && W.p.th >= W.h) W.p.tw = W.p.th = 0;   // one tile
+            // B.3 (CodeStreamDecompress::read_siz): grid origin at or above-left of the image, the
+            // first tile overlapping it
+            if (W.gx0 > W.x0 || W.gy0 > W.y0 || (uint64_t)W.gx0 + W.p.tw <= W.x0 || (uint64_t)W.gy0 + W.p.th <= W.y0)
+                throw GkError("corrupt SIZ marker (tile grid offset)");
+            if ((uint64_t)W.gx0 + W.p.tw >= X1 && (uint64_t)W.gy0 + W.p.th >= Y1) W.p.tw = W.p.th = 0;   // one tile
             W.nc = S.be16(s + 34);
             if (W.nc == 0 || W.nc > 255 || L < 38 + 3 * W.nc) throw GkError("corrupt SIZ marker (component count)");
             if (!W.w || !W.h) throw GkError("corrupt SIZ marker (empty image)");
@@ -3294,8 +3326,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         std::vector<TilePart> keep;
         for (auto& TP : Hd.parts) {
             if (TP.tile >= P.tiles.size()) throw GkError("corrupt SOT (tile index)");
-            const TileG& T = P.tiles[TP.tile];
-            if (T.x0 < win[2] && win[0] < T.x1 && T.y0 < win[3] && win[1] < T.y1) keep.push_back(std::move(TP));
+            const TileG& T = P.tiles[TP.tile];   // (canvas tile against the image-relative window)
+            if (T.x0 - P.x0 < win[2] && win[0] < T.x1 - P.x0 && T.y0 - P.y0 < win[3] && win[1] < T.y1 - P.y0)
+                keep.push_back(std::move(TP));
         }
         Hd.parts.swap(keep);
         if (Hd.parts.empty()) throw GkError("no tile part intersects the window");
@@ -3321,7 +3354,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // decode as zero); the output region is the rectangle, clipped to the window
     const TileG& Tfirst = P.tiles[(size_t)jb * P.ntx + ib];
     const TileG& Tlast = P.tiles[(size_t)(je - 1) * P.ntx + ie - 1];
-    const Region RG = make_region(Tfirst.x0, Tfirst.y0, Tlast.x1, Tlast.y1);
+    const Region RG = make_region(Tfirst.x0 - P.x0, Tfirst.y0 - P.y0, Tlast.x1 - P.x0, Tlast.y1 - P.y0);   // image-relative
     uint32_t rx0 = RG.x0, ry0 = RG.y0, rx1 = RG.x0 + RG.w, ry1 = RG.y0 + RG.h, ox = 0, oy = 0;
     if (win) {
         rx0 = std::max(rx0, win[0]); ry0 = std::max(ry0, win[1]); rx1 = std::min(rx1, win[2]); ry1 = std::min(ry1, win[3]);
@@ -3336,15 +3369,17 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // outside are not decoded (their samples only feed outputs outside the window), and with
     // PLT a packet none of whose blocks is needed is skipped unparsed.
     const uint32_t Lv = P.p.numres - 1, pad = P.p.irrev ? 4 : 2;
+    // (on the canvas: the output rectangle moved by the image origin)
+    const uint32_t cx0 = rx0 + P.x0, cy0 = ry0 + P.y0, cx1 = rx1 + P.x0, cy1 = ry1 + P.y0;
     auto block_needed = [&](const TileG& T, std::vector<uint8_t>& need) {
         need.assign(T.b1 - T.b0, 1);
-        if (!win || (rx0 <= T.x0 && T.x1 <= rx1 && ry0 <= T.y0 && T.y1 <= ry1)) return;
+        if (!win || (cx0 <= T.x0 && T.x1 <= cx1 && cy0 <= T.y0 && T.y1 <= cy1)) return;
         // lo[a][l], hi[a][l]: needed [begin, end) in level-l low / high band coordinates, axis a
         uint32_t lo[2][GK_MAXRLVLS + 1][2], hi[2][GK_MAXRLVLS + 1][2];
         const CompG& C0 = T.comps[0];
         for (int ax = 0; ax < 2; ++ax) {
-            uint32_t s0 = ax ? std::max(ry0, T.y0) : std::max(rx0, T.x0);
-            uint32_t s1 = ax ? std::min(ry1, T.y1) : std::min(rx1, T.x1);
+            uint32_t s0 = ax ? std::max(cy0, T.y0) : std::max(cx0, T.x0);
+            uint32_t s1 = ax ? std::min(cy1, T.y1) : std::min(cx1, T.x1);
             lo[ax][0][0] = s0; lo[ax][0][1] = s1;
             for (uint32_t l = 1; l <= Lv; ++l) {
                 const ResG& Rl = C0.res[P.p.numres - l];       // resolution holding level-l bands
@@ -3749,8 +3784,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // ceil(origin / 2^red), B.5)
         run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr, red + 1);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
-        const uint32_t qx0 = ceildivpow2(RG.x0, red), qy0 = ceildivpow2(RG.y0, red);
-        const uint32_t qcols = ceildivpow2(RG.x0 + RG.w, red) - qx0, qrows = ceildivpow2(RG.y0 + RG.h, red) - qy0;
+        // reduced canvas: positions ceil(x / 2^red); output index = that less the image origin's
+        const uint32_t rox = ceildivpow2(P.x0, red), roy = ceildivpow2(P.y0, red);
+        const uint32_t qx0 = ceildivpow2(RG.x0 + P.x0, red) - rox, qy0 = ceildivpow2(RG.y0 + P.y0, red) - roy;
+        const uint32_t qcols = ceildivpow2(RG.x0 + P.x0 + RG.w, red) - rox - qx0;
+        const uint32_t qrows = ceildivpow2(RG.y0 + P.y0 + RG.h, red) - roy - qy0;
         std::vector<uint8_t*> qd(P.nc);
         std::vector<uint32_t> qs(P.nc);
         if (!out_on_device) {
@@ -3762,11 +3800,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         for (uint32_t j = jb; j < je; ++j)
             for (uint32_t i = ib; i < ie; ++i) {
                 const TileG& T = P.tiles[(size_t)j * P.ntx + i];
-                const uint32_t tx0 = ceildivpow2(T.x0, red), ty0 = ceildivpow2(T.y0, red);
-                const uint32_t tw = ceildivpow2(T.x1, red) - tx0, th = ceildivpow2(T.y1, red) - ty0;
+                const uint32_t tx0 = ceildivpow2(T.x0, red) - rox, ty0 = ceildivpow2(T.y0, red) - roy;
+                const uint32_t tw = ceildivpow2(T.x1, red) - ceildivpow2(T.x0, red), th = ceildivpow2(T.y1, red) - ceildivpow2(T.y0, red);
                 auto src = [&](uint32_t c) {
                     return arena + (size_t)c * 2 * RG.plane + ((red & 1) ? RG.plane : 0) +
-                           (size_t)(T.y0 - RG.y0) * RG.stride + (T.x0 - RG.x0);
+                           (size_t)(T.y0 - P.y0 - RG.y0) * RG.stride + (T.x0 - P.x0 - RG.x0);
                 };
                 auto srcf = [&](uint32_t c) { return reinterpret_cast<const float*>(src(c)); };
                 auto dst = [&](uint32_t c) { return qd[c] + ((size_t)(ty0 - qy0) * qs[c] + (tx0 - qx0)) * es; };
@@ -4021,7 +4059,7 @@ int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
         Header Hd;
         parse_header(S, Hd);
         info->w = Hd.want.w; info->h = Hd.want.h; info->numcomps = Hd.want.nc; info->prec = Hd.want.prec;
-        info->sgnd = Hd.want.sgnd;
+        info->sgnd = Hd.want.sgnd; info->x0 = Hd.want.x0; info->y0 = Hd.want.y0;
         return 0;
     } catch (const GkError& e) {
         ctx->err = e.msg;
@@ -4058,7 +4096,7 @@ int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, gk_cpara
         Header Hd;
         parse_header(S, Hd);
         info->w = Hd.want.w; info->h = Hd.want.h; info->numcomps = Hd.want.nc; info->prec = Hd.want.prec;
-        info->sgnd = Hd.want.sgnd;
+        info->sgnd = Hd.want.sgnd; info->x0 = Hd.want.x0; info->y0 = Hd.want.y0;
         info->sample_bytes = 0;
         if (coding) {
             const Params& p = Hd.want.p;
@@ -4077,7 +4115,9 @@ int gk_probe_header(const uint8_t* cs, size_t len, gk_image_info* info, gk_cpara
                 coding->prch_init[r] = 1u << p.prch[p.numres - 1 - r];
             }
             coding->tile_size_on = p.tw != 0;
-            coding->t_width = p.tw ? p.tw : Hd.want.w; coding->t_height = p.th ? p.th : Hd.want.h;
+            coding->t_width = p.tw ? p.tw : Hd.want.x0 + Hd.want.w - Hd.want.gx0;
+            coding->t_height = p.th ? p.th : Hd.want.y0 + Hd.want.h - Hd.want.gy0;
+            coding->tx0 = Hd.want.gx0; coding->ty0 = Hd.want.gy0;
             coding->writeTLM = !Hd.tlm.empty();
             coding->writePLT = 0;
             coding->cod_format = jp2 ? 2 : 0;

@@ -22,7 +22,9 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
         return refuse(msg);
     }
     if (g.prog_order < GRK_LRCP || g.prog_order > GRK_CPRL) return refuse("unknown progression order");
-    if (g.tx0 || g.ty0 || g.image_offset_x0 || g.image_offset_y0) return refuse("image/tile offsets are not supported");
+    // tile grid origin (-T); the image origin travels with the image (grk_image::x0 / y0: the CLI's
+    // readers set it from image_offset_x0 / y0, which the library itself does not read)
+    p.tx0 = g.tx0; p.ty0 = g.ty0;
     if (g.tile_size_on && (!g.t_width || !g.t_height)) return refuse("tile size must be non-zero when tiling is on");
     // mct 255 = not set on the command line: grk_compress resolves it from the component count
     // once the image is loaded (grk_compress.cpp:1977-1981), as the engine does (>= 3 -> RCT/ICT)

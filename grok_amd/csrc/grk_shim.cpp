@@ -218,8 +218,9 @@ CodecObj* codec_of(grk_codec* c) { return c ? dynamic_cast<CodecObj*>(obj_of(c))
 bool to_gk(const grk_cparameters& g, GRK_CODEC_FORMAT fmt, gk_cparameters& p, const grk_image* im = nullptr) {
     std::string why;
     uint32_t ntiles = 1;
-    if (im && im->numcomps && g.tile_size_on && g.t_width && g.t_height) {
-        const uint64_t w = im->comps[0].w, h = im->comps[0].h;
+    if (im && im->numcomps && g.tile_size_on && g.t_width && g.t_height) {   // grid from (tx0, ty0) to the image's far corner
+        const uint64_t w = (uint64_t)im->x0 + im->comps[0].w - std::min(g.tx0, im->x0);
+        const uint64_t h = (uint64_t)im->y0 + im->comps[0].h - std::min(g.ty0, im->y0);
         ntiles = (uint32_t)(((w + g.t_width - 1) / g.t_width) * ((h + g.t_height - 1) / g.t_height));
     }
     if (grk_params_to_gk(g, fmt == GRK_CODEC_JP2, p, why, ntiles)) return true;
@@ -230,7 +231,6 @@ bool to_gk(const grk_cparameters& g, GRK_CODEC_FORMAT fmt, gk_cparameters& p, co
 bool image_geometry(const grk_image* im, gk_image_info& info) {
     if (!im || !im->numcomps || !im->comps) { error("empty image"); return false; }
     const grk_image_comp& c0 = im->comps[0];
-    if (im->x0 || im->y0) { error("image offsets are not supported"); return false; }
     for (uint16_t i = 0; i < im->numcomps; ++i) {
         const grk_image_comp& c = im->comps[i];
         if (c.dx != 1 || c.dy != 1) { error("component subsampling is not supported"); return false; }
@@ -241,6 +241,7 @@ bool image_geometry(const grk_image* im, gk_image_info& info) {
     }
     info.w = c0.w; info.h = c0.h; info.numcomps = im->numcomps; info.prec = c0.prec; info.sgnd = c0.sgnd;
     info.sample_bytes = 0;
+    info.x0 = im->x0; info.y0 = im->y0;   // the image area's canvas origin (SIZ XOsiz / YOsiz)
     return true;
 }
 
@@ -287,6 +288,15 @@ bool run_decode(CodecObj* C, ImageObj* o, const uint32_t* w) {
                : gk_decode(e, C->data.data(), C->data.size(), 0, planes.data(), strides.data(), 0, 0);
     if (rc != 0) { error("%s", gk_last_error(e)); return false; }
     return true;
+}
+
+// the composited image without a window: the image area, on the canvas reduced by cp_reduce
+// (GrkImage::subsampleAndReduce: ceil(x / 2^reduce))
+void full_bounds(const CodecObj* C, uint32_t b[4]) {
+    const uint32_t r = C->dp.cp_reduce;
+    auto cd = [r](uint64_t v) { return (uint32_t)((v + (1ull << r) - 1) >> r); };
+    b[0] = cd(C->info.x0); b[1] = cd(C->info.y0);
+    b[2] = cd((uint64_t)C->info.x0 + C->info.w); b[3] = cd((uint64_t)C->info.y0 + C->info.h);
 }
 
 ImageObj* region_image(CodecObj* C, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
@@ -492,12 +502,17 @@ bool grk_compress_tile(grk_codec* codec, uint16_t tileIndex, uint8_t* data, uint
     const uint32_t es = (info.prec + 7) / 8;
     if (es > 2) { error("raw tiles of more than 16 bits per sample are not supported"); return false; }
     if (C->cp.tile_size_on && (!C->cp.t_width || !C->cp.t_height)) { error("tile size must be non-zero"); return false; }
-    const uint32_t tw = C->cp.tile_size_on ? std::min(C->cp.t_width, info.w) : info.w;
-    const uint32_t th = C->cp.tile_size_on ? std::min(C->cp.t_height, info.h) : info.h;
-    const uint32_t ntx = (info.w + tw - 1) / tw, nty = (info.h + th - 1) / th;
+    // tile grid from (tx0, ty0) over the image area [X0, X1) x [Y0, Y1) (B.3); x0, y0 below are
+    // image-relative
+    const uint32_t X0 = info.x0, Y0 = info.y0, X1 = X0 + info.w, Y1 = Y0 + info.h;
+    const uint32_t gx = std::min(C->cp.tx0, X0), gy = std::min(C->cp.ty0, Y0);
+    const uint32_t tw = C->cp.tile_size_on ? C->cp.t_width : X1 - gx;
+    const uint32_t th = C->cp.tile_size_on ? C->cp.t_height : Y1 - gy;
+    const uint32_t ntx = (X1 - gx + tw - 1) / tw, nty = (Y1 - gy + th - 1) / th;
     if (tileIndex >= ntx * nty) { error("tile index %u out of range", tileIndex); return false; }
-    const uint32_t x0 = (tileIndex % ntx) * tw, y0 = (tileIndex / ntx) * th;
-    const uint32_t w = std::min(tw, info.w - x0), h = std::min(th, info.h - y0);
+    const uint32_t x0 = std::max(gx + (tileIndex % ntx) * tw, X0) - X0, y0 = std::max(gy + (tileIndex / ntx) * th, Y0) - Y0;
+    const uint32_t w = std::min(gx + (tileIndex % ntx + 1) * tw, X1) - X0 - x0;
+    const uint32_t h = std::min(gy + (tileIndex / ntx + 1) * th, Y1) - Y0 - y0;
     if (data_size != (uint64_t)w * h * info.numcomps * es) { error("tile %u: wrong data size", tileIndex); return false; }
     if (C->tile_buf.empty()) {
         C->tile_buf.assign((size_t)info.w * info.h * info.numcomps * es, 0);
@@ -578,10 +593,10 @@ bool grk_decompress_read_header(grk_codec* codec, grk_header_info* hi) {
             error("reduced-resolution decode of a window is not supported on this path");
             return false;
         }
-        {   // cp_reduce: the composited image is ceil(size / 2^reduce)
-            const uint32_t r = C->dp.cp_reduce;
-            C->out = region_image(C, 0, 0, (uint32_t)(((uint64_t)C->info.w + (1ull << r) - 1) >> r),
-                                  (uint32_t)(((uint64_t)C->info.h + (1ull << r) - 1) >> r));
+        {   // the composited image: the image area on the canvas, reduced by cp_reduce (ceil(x / 2^reduce))
+            uint32_t b[4];
+            full_bounds(C, b);
+            C->out = region_image(C, b[0], b[1], b[2], b[3]);
         }
         if (!C->out) return false;
     }
@@ -595,10 +610,10 @@ bool grk_decompress_read_header(grk_codec* codec, grk_header_info* hi) {
         hi->csty = k.csty;
         hi->cblk_sty = k.cblk_sty;
         for (int r = 0; r < GRK_J2K_MAXRLVLS; ++r) { hi->prcw_init[r] = k.prcw_init[r]; hi->prch_init[r] = k.prch_init[r]; }
-        hi->tx0 = 0; hi->ty0 = 0;
+        hi->tx0 = k.tx0; hi->ty0 = k.ty0;
         hi->t_width = k.t_width; hi->t_height = k.t_height;
-        hi->t_grid_width = (C->info.w + k.t_width - 1) / k.t_width;
-        hi->t_grid_height = (C->info.h + k.t_height - 1) / k.t_height;
+        hi->t_grid_width = (C->info.x0 + C->info.w - k.tx0 + k.t_width - 1) / k.t_width;
+        hi->t_grid_height = (C->info.y0 + C->info.h - k.ty0 + k.t_height - 1) / k.t_height;
         hi->numlayers = k.numlayers;
         hi->xml_data = nullptr; hi->xml_data_len = 0;
         hi->num_comments = 0;
@@ -615,11 +630,12 @@ bool grk_decompress_set_window(grk_codec* codec, uint32_t x0, uint32_t y0, uint3
     if (!C || C->compress) return false;
     if (!C->header_read) { error("Need to read the main header before setting decompress window"); return false; }
     if (!x0 && !y0 && !x1 && !y1) { C->has_win = false; return true; }
-    const uint32_t W = C->info.w, H = C->info.h;
-    if (x0 > W) { error("Left position of the decompress window (%u) is outside of the image area (Xsiz=%u).", x0, W); return false; }
-    if (y0 > H) { error("Top position of the decompress window (%u) is outside of the image area (Ysiz=%u).", y0, H); return false; }
-    if (x1 > W) { warn("Right position of the decompress window (%u) is outside the image area (Xsiz=%u).", x1, W); x1 = W; }
-    if (y1 > H) { warn("Bottom position of the decompress window (%u) is outside of the image area (Ysiz=%u).", y1, H); y1 = H; }
+    // the window is relative to the image origin; Grok reports canvas positions (window + origin)
+    const uint32_t W = C->info.w, H = C->info.h, OX = C->info.x0, OY = C->info.y0;
+    if (x0 > W) { error("Left position of the decompress window (%u) is outside of the image area (Xsiz=%u).", x0 + OX, W + OX); return false; }
+    if (y0 > H) { error("Top position of the decompress window (%u) is outside of the image area (Ysiz=%u).", y0 + OY, H + OY); return false; }
+    if (x1 > W) { warn("Right position of the decompress window (%u) is outside the image area (Xsiz=%u).", x1 + OX, W + OX); x1 = W; }
+    if (y1 > H) { warn("Bottom position of the decompress window (%u) is outside of the image area (Ysiz=%u).", y1 + OY, H + OY); y1 = H; }
     if (x0 >= x1 || y0 >= y1) { error("decompress window (%u,%u,%u,%u) is empty", x0, y0, x1, y1); return false; }
     if (C->dp.cp_reduce) { error("reduced-resolution decode of a window is not supported on this path"); return false; }
     C->win[0] = x0; C->win[1] = y0; C->win[2] = x1; C->win[3] = y1;
@@ -632,14 +648,14 @@ bool grk_decompress(grk_codec* codec, grk_plugin_tile* tile) {
     if (!C || C->compress) return false;
     if (tile) { error("plugin tiles are not used: the tile pipeline runs in this library"); return false; }
     if (!C->header_read && !grk_decompress_read_header(codec, nullptr)) return false;
+    const uint32_t OX = C->info.x0, OY = C->info.y0;   // composited images are canvas rectangles
     if (C->has_win) {
-        if (!reshape_image(C->out, C->win[0], C->win[1], C->win[2], C->win[3])) return false;
+        if (!reshape_image(C->out, C->win[0] + OX, C->win[1] + OY, C->win[2] + OX, C->win[3] + OY)) return false;
         return run_decode(C, C->out, C->win);
     }
-    const uint32_t r = C->dp.cp_reduce;   // the composited image is ceil(size / 2^reduce)
-    if (!reshape_image(C->out, 0, 0, (uint32_t)(((uint64_t)C->info.w + (1ull << r) - 1) >> r),
-                       (uint32_t)(((uint64_t)C->info.h + (1ull << r) - 1) >> r)))
-        return false;
+    uint32_t b[4];
+    full_bounds(C, b);
+    if (!reshape_image(C->out, b[0], b[1], b[2], b[3])) return false;
     return run_decode(C, C->out, nullptr);
 }
 
@@ -652,13 +668,17 @@ bool grk_decompress_tile(grk_codec* codec, uint16_t tileIndex) {
     if (!C->header_read && !grk_decompress_read_header(codec, nullptr)) return false;
     if (C->dp.cp_reduce) { error("reduced-resolution decode of a tile is not supported on this path"); return false; }
     const uint32_t tw = C->coding.t_width, th = C->coding.t_height;
-    const uint32_t ntx = (C->info.w + tw - 1) / tw, nty = (C->info.h + th - 1) / th;
+    const uint32_t OX = C->info.x0, OY = C->info.y0, X1 = OX + C->info.w, Y1 = OY + C->info.h;
+    const uint32_t gx = C->coding.tx0, gy = C->coding.ty0;
+    const uint32_t ntx = (X1 - gx + tw - 1) / tw, nty = (Y1 - gy + th - 1) / th;
     if (tileIndex >= ntx * nty) {
         error("Tile index %u is greater than maximum tile index %u", tileIndex, ntx * nty - 1);
         return false;
     }
-    const uint32_t tx0 = (tileIndex % ntx) * tw, ty0 = (tileIndex / ntx) * th;
-    uint32_t w[4] = {tx0, ty0, std::min(tx0 + tw, C->info.w), std::min(ty0 + th, C->info.h)};
+    // the tile's rectangle on the canvas, clipped to the image area, made image-relative
+    const uint32_t i = tileIndex % ntx, j = tileIndex / ntx;
+    uint32_t w[4] = {std::max(gx + i * tw, OX) - OX, std::max(gy + j * th, OY) - OY, std::min(gx + (i + 1) * tw, X1) - OX,
+                     std::min(gy + (j + 1) * th, Y1) - OY};
     if (C->has_win) {
         const uint32_t c[4] = {std::max(w[0], C->win[0]), std::max(w[1], C->win[1]), std::min(w[2], C->win[2]),
                                std::min(w[3], C->win[3])};
@@ -669,7 +689,7 @@ bool grk_decompress_tile(grk_codec* codec, uint16_t tileIndex) {
             w[0] = C->win[0]; w[1] = C->win[1]; w[2] = C->win[2]; w[3] = C->win[3];
         }
     }
-    if (!reshape_image(C->out, w[0], w[1], w[2], w[3])) return false;
+    if (!reshape_image(C->out, w[0] + OX, w[1] + OY, w[2] + OX, w[3] + OY)) return false;
     C->tile_decoded = true;
     return run_decode(C, C->out, w);
 }
@@ -694,8 +714,9 @@ void grk_dump_codec(grk_codec* codec, uint32_t info_flag, FILE* f) {
     CodecObj* C = codec_of(codec);
     if (!C || C->compress || !C->header_read || !f) return;
     if (info_flag & GRK_IMG_INFO)
-        fprintf(f, "Image info {\n\t x0=0, y0=0\n\t x1=%u, y1=%u\n\t numcomps=%u\n\t prec=%u sgnd=%u\n}\n", C->info.w,
-                C->info.h, C->info.numcomps, C->info.prec, C->info.sgnd);
+        fprintf(f, "Image info {\n\t x0=%u, y0=%u\n\t x1=%u, y1=%u\n\t numcomps=%u\n\t prec=%u sgnd=%u\n}\n",
+                C->info.x0, C->info.y0, C->info.x0 + C->info.w, C->info.y0 + C->info.h, C->info.numcomps, C->info.prec,
+                C->info.sgnd);
     if (info_flag & GRK_J2K_MH_INFO)
         fprintf(f, "Codestream info from main header: {\n\t tdx=%u, tdy=%u\n\t numresolutions=%u\n\t cblkw=%u cblkh=%u "
                    "cblksty=0x%x\n\t qmfbid=%u mct=%u numlayers=%u\n}\n",

@@ -67,13 +67,15 @@ typedef struct gk_cparameters {
     gk_poc pocs[32];
     uint8_t allocationByQuality;         /* grk_cparameters::allocationByQuality (grk_compress -q): layers by PSNR */
     double layer_distortion[GK_MAX_LAYERS]; /* grk_cparameters::layer_distortion: PSNR per layer (0 = the rest) */
+    uint32_t tx0, ty0;                   /* grk_cparameters::tx0 / ty0 (grk_compress -T): tile grid origin on the
+                                            canvas, at or above-left of the image origin (B.3) */
 } gk_cparameters;
 
 /* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to
  * what the tile pipeline reads.  Component planes are int32 (grk_image_comp::data),
  * row stride in samples (grk_image_comp::stride). */
 typedef struct gk_image_info {
-    uint32_t w, h;          /* grk_image::x1 - x0, y1 - y0 (image at the origin; tiles per gk_cparameters) */
+    uint32_t w, h;          /* grk_image::x1 - x0, y1 - y0: the image area (tiles per gk_cparameters) */
     uint32_t numcomps;      /* grk_image::numcomps */
     uint32_t prec;          /* grk_image_comp::prec (same for every component) */
     uint32_t sgnd;          /* grk_image_comp::sgnd */
@@ -81,6 +83,8 @@ typedef struct gk_image_info {
                                8 / 16-bit samples, signed iff sgnd, as grk_compress_tile's buffer
                                (TileProcessor::ingestUncompressedData, TileProcessor.cpp:779-835);
                                must be 4 or (prec + 7) / 8.  Decode writes the same type. */
+    uint32_t x0, y0;        /* grk_image::x0 / y0 (grk_compress -d): the image area's canvas origin (SIZ
+                               XOsiz / YOsiz); planes hold the area only, windows are relative to it */
 } gk_image_info;
 
 /* Per-stage device times of the last call (HIP events on the engine stream). */

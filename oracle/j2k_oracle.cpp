@@ -93,6 +93,9 @@ struct Params {
     std::vector<uint32_t> roishift;   // per component ROI maxshift (RGN); empty = none
     uint32_t roi(uint32_t c) const { return c < roishift.size() ? roishift[c] : 0u; }
     uint32_t tw = 0, th = 0;    // nominal tile size (0 = one tile covering the image), grk_cparameters::t_width/t_height
+    // canvas offsets (B.2, B.3): the image area starts at (x0, y0) (grk_image::x0 / y0, CLI -d), the
+    // tile grid at (gx0, gy0) <= (x0, y0) (grk_cparameters::tx0 / ty0, CLI -T); w x h is the image area
+    uint32_t x0 = 0, y0 = 0, gx0 = 0, gy0 = 0;
     int tlm = 0, plt = 0;       // write TLM (-X) / PLT (-L) markers
     uint32_t sop_eph = 0;       // Scod bits: 2 = SOP before every packet, 4 = EPH after every packet header (-S / -E)
     bool quality = false;       // fixed-quality layers (-q, grk_cparameters::allocationByQuality)
@@ -1154,17 +1157,21 @@ struct Image {
     uint32_t w, h, nc, prec; bool sgnd;
 };
 
-// Tile grid (B.3): nominal tile size (tw, th) anchored at the image origin.
+// Tile grid (B.3, CodeStreamCompress.cpp:352-363): nominal tile size (tw, th) anchored at the grid
+// origin (gx0, gy0); without tiling one tile from the grid origin to the image's far corner.  Tile
+// rectangles are canvas coordinates clipped to the image area [x0, x0 + W) x [y0, y0 + H).
 static uint32_t tile_count(const Params& p, uint32_t W, uint32_t H) {
-    uint32_t tw = p.tw ? p.tw : W, th = p.th ? p.th : H;
-    return ((W + tw - 1) / tw) * ((H + th - 1) / th);
+    const uint32_t X1 = p.x0 + W, Y1 = p.y0 + H;
+    uint32_t tw = p.tw ? p.tw : X1 - p.gx0, th = p.th ? p.th : Y1 - p.gy0;
+    return ((X1 - p.gx0 + tw - 1) / tw) * ((Y1 - p.gy0 + th - 1) / th);
 }
 static void tile_rect(const Params& p, uint32_t W, uint32_t H, uint32_t t, uint32_t& x0, uint32_t& y0, uint32_t& x1,
                       uint32_t& y1) {
-    uint32_t tw = p.tw ? p.tw : W, th = p.th ? p.th : H;
-    uint32_t ntx = (W + tw - 1) / tw;
-    x0 = (t % ntx) * tw; y0 = (t / ntx) * th;
-    x1 = std::min(x0 + tw, W); y1 = std::min(y0 + th, H);
+    const uint32_t X1 = p.x0 + W, Y1 = p.y0 + H;
+    uint32_t tw = p.tw ? p.tw : X1 - p.gx0, th = p.th ? p.th : Y1 - p.gy0;
+    uint32_t ntx = (X1 - p.gx0 + tw - 1) / tw;
+    x0 = std::max(p.gx0 + (t % ntx) * tw, p.x0); y0 = std::max(p.gy0 + (t / ntx) * th, p.y0);
+    x1 = std::min(p.gx0 + (t % ntx + 1) * tw, X1); y1 = std::min(p.gy0 + (t / ntx + 1) * th, Y1);
 }
 
 // Main header: SOC SIZ [CAP] COD QCD [TLM] [COM] (CodeStreamCompress::init_header_writing
@@ -1207,8 +1214,9 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
     put16(o, 0xff4f);                               // SOC
     put16(o, 0xff51); put16(o, 38 + 3 * im.nc);     // SIZ
     put16(o, p.ht() ? 0x4000 : 0);                  // Rsiz (GRK_JPH_RSIZ_FLAG for HT, CodeStreamCompress.cpp:216-219)
-    put32(o, im.w); put32(o, im.h); put32(o, 0); put32(o, 0);
-    put32(o, p.tw ? p.tw : im.w); put32(o, p.th ? p.th : im.h); put32(o, 0); put32(o, 0);
+    put32(o, p.x0 + im.w); put32(o, p.y0 + im.h); put32(o, p.x0); put32(o, p.y0);   // Xsiz Ysiz XOsiz YOsiz
+    put32(o, p.tw ? p.tw : p.x0 + im.w - p.gx0); put32(o, p.th ? p.th : p.y0 + im.h - p.gy0);
+    put32(o, p.gx0); put32(o, p.gy0);                                                 // XTOsiz YTOsiz
     put16(o, im.nc);
     for (uint32_t i = 0; i < im.nc; ++i) { o.push_back((uint8_t)((im.prec - 1) | (im.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
     if (p.ht()) {                                   // CAP (CodeStreamCompress::write_cap :1064-1111)
@@ -1872,6 +1880,8 @@ typedef struct {
     uint32_t csty;         // grk_cparameters::csty SOP (2) / EPH (4) bits (the precinct bit follows prcw_exp)
     uint32_t by_quality;   // grk_cparameters::allocationByQuality: layer_distortion holds PSNR targets
     double layer_distortion[100];
+    uint32_t image_x0, image_y0;   // canvas offset of the image area (grk_image::x0 / y0, -d)
+    uint32_t tile_x0, tile_y0;     // tile grid origin (grk_cparameters::tx0 / ty0, -T)
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -1896,6 +1906,7 @@ static Params to_params(const orc_cparams* cp) {
         p.pocs.push_back({cp->pocs[i][0], cp->pocs[i][1], cp->pocs[i][2], cp->pocs[i][3], cp->pocs[i][4], cp->pocs[i][5]});
     if (p.ht()) p.numgbits = 1;   // grk_compress.cpp:1123-1124
     p.tw = cp->tile_w; p.th = cp->tile_h; p.tlm = (int)cp->tlm; p.plt = (int)cp->plt;
+    p.x0 = cp->image_x0; p.y0 = cp->image_y0; p.gx0 = cp->tile_x0; p.gy0 = cp->tile_y0;
     p.sop_eph = cp->csty & 6;
     p.quality = cp->by_quality != 0;
     // CodeStreamCompress.cpp:387-393: a tile takes the PSNR targets under allocationByQuality,
@@ -2021,7 +2032,8 @@ static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, ui
     for (uint32_t c = 0; c < nc; ++c) {   // tile-local copy (TileProcessor::ingestImage, TileProcessor.cpp:410-431)
         E.coefs[c].resize((size_t)tw * th);
         for (uint32_t y = 0; y < th; ++y)
-            memcpy(&E.coefs[c][(size_t)y * tw], planes + (size_t)c * w * rows + (size_t)(E.ty0 - row0 + y) * w + E.tx0,
+            memcpy(&E.coefs[c][(size_t)y * tw],
+                   planes + (size_t)c * w * rows + (size_t)(E.ty0 - E.p.y0 - row0 + y) * w + (E.tx0 - E.p.x0),
                    (size_t)tw * 4);
     }
     if (!E.p.irreversible) {
@@ -2709,9 +2721,11 @@ t2done:
     }
     int32_t shift = im.sgnd ? 0 : (1 << (im.prec - 1));
     int32_t mn = im.sgnd ? -(1 << (im.prec - 1)) : 0, mxv = im.sgnd ? (1 << (im.prec - 1)) - 1 : (1 << im.prec) - 1;
-    const uint32_t Wr = ceildivpow2(im.w, red), Hr = ceildivpow2(im.h, red);
-    const uint32_t tx0r = ceildivpow2(tx0, red), ty0r = ceildivpow2(ty0, red);
-    const uint32_t TWr = ceildivpow2(tx1, red) - tx0r, THr = ceildivpow2(ty1, red) - ty0r;
+    // reduced image area: [ceil(x0 / 2^r), ceil((x0 + w) / 2^r)) on the reduced canvas
+    const uint32_t Wr = ceildivpow2(p.x0 + im.w, red) - ceildivpow2(p.x0, red);
+    const uint32_t Hr = ceildivpow2(p.y0 + im.h, red) - ceildivpow2(p.y0, red);
+    const uint32_t tx0r = ceildivpow2(tx0, red) - ceildivpow2(p.x0, red), ty0r = ceildivpow2(ty0, red) - ceildivpow2(p.y0, red);
+    const uint32_t TWr = ceildivpow2(tx1, red) - ceildivpow2(tx0, red), THr = ceildivpow2(ty1, red) - ceildivpow2(ty0, red);
     const size_t n = (size_t)TW * TH, N = (size_t)Wr * Hr;
     auto put = [&](uint32_t c, size_t k, int32_t v) {
         const uint32_t x = (uint32_t)(k % TW), y = (uint32_t)(k / TW);
@@ -2786,8 +2800,12 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         const uint8_t* s = cs + i + 4;
         if (m == 0xff51) {
             im.w = get32(s + 2) - get32(s + 10); im.h = get32(s + 6) - get32(s + 14);
-            if (get32(s + 10) || get32(s + 14) || get32(s + 26) || get32(s + 30)) return -2;  // origins unsupported
+            p.x0 = get32(s + 10); p.y0 = get32(s + 14); p.gx0 = get32(s + 26); p.gy0 = get32(s + 30);
+            // B.3: the tile grid origin lies at or above-left of the image origin, its first tile reaches it
             p.tw = get32(s + 18); p.th = get32(s + 22);
+            if (get32(s + 2) <= p.x0 || get32(s + 6) <= p.y0 || p.gx0 > p.x0 || p.gy0 > p.y0 || !p.tw || !p.th ||
+                (uint64_t)p.gx0 + p.tw <= p.x0 || (uint64_t)p.gy0 + p.th <= p.y0)
+                return -2;
             im.nc = get16(s + 34);
             im.prec = (s[36] & 0x7f) + 1; im.sgnd = (s[36] & 0x80) != 0;
         } else if (m == 0xff52) {
@@ -2825,9 +2843,11 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     for (size_t k : coc_qcc)
         if (!restates_main(cs + k + 4, get16(cs + k + 2), get16(cs + k), im.nc, cod_body, qcd_body)) return -2;
     if (g_dec_reduce >= p.numres) return -7;   // reduce must leave one resolution
-    *W = ceildivpow2(im.w, g_dec_reduce); *H = ceildivpow2(im.h, g_dec_reduce); *NC = im.nc; *PREC = im.prec;
+    *W = ceildivpow2(p.x0 + im.w, g_dec_reduce) - ceildivpow2(p.x0, g_dec_reduce);
+    *H = ceildivpow2(p.y0 + im.h, g_dec_reduce) - ceildivpow2(p.y0, g_dec_reduce);
+    *NC = im.nc; *PREC = im.prec;
     if (!out) return 0;
-    if (p.tw == im.w && p.th == im.h) p.tw = p.th = 0;
+    if (p.gx0 + p.tw >= p.x0 + im.w && p.gy0 + p.th >= p.y0 + im.h) p.tw = p.th = 0;   // one tile
     std::fill(out, out + (size_t)im.nc * *W * *H, 0);
     const uint32_t nt = tile_count(p, im.w, im.h);
     size_t pos = first_sot;

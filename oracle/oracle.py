@@ -27,6 +27,8 @@ class CParams(ctypes.Structure):
         ("numpocs", ctypes.c_uint32), ("pocs", (ctypes.c_uint32 * 6) * 32),
         ("roi_compno", ctypes.c_int32), ("roi_shift", ctypes.c_uint32),
         ("csty", ctypes.c_uint32), ("by_quality", ctypes.c_uint32), ("layer_distortion", ctypes.c_double * 100),
+        ("image_x0", ctypes.c_uint32), ("image_y0", ctypes.c_uint32), ("tile_x0", ctypes.c_uint32),
+        ("tile_y0", ctypes.c_uint32),
     ]
 
 
@@ -97,7 +99,7 @@ def get_threads():
 
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
            layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None, roi=None,
-           sop=False, eph=False, quality=None):
+           sop=False, eph=False, quality=None, origin=None, tile_origin=None):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -118,6 +120,14 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
     p.roi_compno, p.roi_shift = (int(roi[0]), int(roi[1])) if roi else (-1, 0)
     if tiles:
         p.tile_w, p.tile_h = int(tiles[0]), int(tiles[1])
+    # canvas offsets: image area at origin (grk_compress -d), tile grid at tile_origin (-T; -T alone
+    # also moves the image origin there, grk_compress.cpp:1547-1551)
+    if tile_origin:
+        p.tile_x0, p.tile_y0 = int(tile_origin[0]), int(tile_origin[1])
+    if origin:
+        p.image_x0, p.image_y0 = int(origin[0]), int(origin[1])
+    elif tile_origin:
+        p.image_x0, p.image_y0 = p.tile_x0, p.tile_y0
     p.tlm, p.plt = int(tlm), int(plt)
     p.cod_format = 2 if jp2 else 0
     if layer_rate:

@@ -38,7 +38,7 @@ static int enc(int argc, char** argv) {
     p.numlayers = 1;                /* :823-828: no -r / -q is one lossless layer (set before -P is read) */
     int to_file = 0;
     GRK_CODEC_FORMAT fmt = GRK_CODEC_J2K;
-    int raw_tiles = 0;
+    int raw_tiles = 0, tile_off = 0, img_off = 0;
     for (int i = 8; i < argc; ++i) {
         if (!strcmp(argv[i], "-n")) p.numresolution = (uint8_t)atoi(argv[++i]);
         else if (!strcmp(argv[i], "-b")) sscanf(argv[++i], "%u,%u", &p.cblockw_init, &p.cblockh_init);
@@ -83,11 +83,21 @@ static int enc(int argc, char** argv) {
             for (char* t = strtok(s, ","); t; t = strtok(NULL, ",")) p.layer_distortion[p.numlayers++] = atof(t);
             p.allocationByQuality = true;
         }
+        else if (!strcmp(argv[i], "-T")) { sscanf(argv[++i], "%u,%u", &p.tx0, &p.ty0); tile_off = 1; }   /* :1512-1529 */
+        else if (!strcmp(argv[i], "-d")) {   /* :1530-1545 image offset */
+            sscanf(argv[++i], "%u,%u", &p.image_offset_x0, &p.image_offset_y0);
+            img_off = 1;
+        }
         else if (!strcmp(argv[i], "-c")) {   /* one precinct size for every resolution: [W,H] */
             unsigned pw, ph;
             sscanf(argv[++i], "[%u,%u]", &pw, &ph);
             p.csty |= 1; p.res_spec = 1; p.prcw_init[0] = pw; p.prch_init[0] = ph;
         }
+    }
+    if (!img_off && tile_off) {   /* :1547-1551: -T alone puts the image at the tile origin */
+        p.image_offset_x0 = p.tx0; p.image_offset_y0 = p.ty0;
+    } else if (p.tx0 > p.image_offset_x0 || p.ty0 > p.image_offset_y0) {
+        return 22;   /* :1554-1562 "Tile offset must be top left of image offset" */
     }
     if (p.mct == 255) p.mct = c >= 3 ? 1 : 0;   /* grk_compress.cpp:1978-1995: RGB input switches the MCT on */
     if (p.rateControlAlgorithm == 255) p.rateControlAlgorithm = 0;
@@ -100,7 +110,11 @@ static int enc(int argc, char** argv) {
     }
     grk_image_cmptparm cp[4];
     memset(cp, 0, sizeof cp);
-    for (uint32_t k = 0; k < c; ++k) { cp[k].dx = cp[k].dy = 1; cp[k].w = w; cp[k].h = h; cp[k].prec = (uint8_t)prec; }
+    /* the image readers place the image at the -d offset (RAWFormat.cpp:309-312, PNMFormat.cpp:474-477) */
+    for (uint32_t k = 0; k < c; ++k) {
+        cp[k].dx = cp[k].dy = 1; cp[k].w = w; cp[k].h = h; cp[k].prec = (uint8_t)prec;
+        cp[k].x0 = p.image_offset_x0; cp[k].y0 = p.image_offset_y0;
+    }
     grk_image* img = grk_image_new((uint16_t)c, cp, c >= 3 ? GRK_CLRSPC_SRGB : GRK_CLRSPC_GRAY, true);
     if (!img) return 2;
     FILE* f = fopen(raw, "rb");

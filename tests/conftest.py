@@ -55,6 +55,10 @@ def parse_flags(flags):
         kw["quality"] = [float(v) for v in t[t.index("-q") + 1].split(",")]
     if "-p" in t:
         kw["prog_order"] = t[t.index("-p") + 1]
+    if "-d" in t:   # image offset (the readers set grk_image::x0 / y0 from it)
+        kw["origin"] = tuple(int(v) for v in t[t.index("-d") + 1].split(","))
+    if "-T" in t:   # tile grid offset; alone it also moves the image there (grk_compress.cpp:1547-1551)
+        kw["tile_origin"] = tuple(int(v) for v in t[t.index("-T") + 1].split(","))
     if "-P" in t:   # grk_compress.cpp:1001-1057 with its clamps; every tile takes the list's head
         nl = len(kw.get("layer_rate") or kw.get("quality") or [0])
         nr = kw.get("numres", 6)

@@ -149,3 +149,15 @@ def test_grk_api_progression_changes(tool, flags):
     dec, _ = _dec(tool, path, img.shape)
     want, _ = O.decode(cs)
     np.testing.assert_array_equal(dec, want)
+
+
+@pytest.mark.parametrize("flags", ["-d 17,9 -T 5,2 -t 32,48", "-T 7,3 -t 40,40", "-d 3,5", "-d 65,33 -T 64,32 -t 32,32 -X -L"])
+def test_grk_api_offsets(tool, flags):
+    # grk_compress -d (image offset: grk_image::x0 / y0) and -T (grk_cparameters::tx0 / ty0)
+    from grok_amd.synth import synth_image
+    img = synth_image(90, 110, 3, 8, 79).astype(np.int32)
+    cs, path = _enc(tool, img, 8, flags, "off_%d" % (abs(hash(flags)) % 10000))
+    from conftest import parse_flags
+    assert cs == O.encode(img, 8, **parse_flags(flags))
+    dec, _ = _dec(tool, path, img.shape)
+    np.testing.assert_array_equal(dec, img)
