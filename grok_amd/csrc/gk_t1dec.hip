@@ -226,21 +226,20 @@ __device__ __forceinline__ uint64_t h_get(uint32_t (*g)[64], int row, int lane) 
 // TIMING (diagnostic build, GK_T1_STATS=2): shader-clock cycles spent in stripe-boundary
 // events vs decision steps, summed into stats[4] / stats[5].
 // MODE 0: decode; 1: also count decisions per lane (GK_T1_STATS); 2: also time events (=2).
-template <int MODE>
-// A workgroup is DEC_WAVES independent waves (one per SIMD) and the launch pads its LDS to the
+// A workgroup is W independent waves (one per SIMD, W <= 4) and the launch pads its LDS to the
 // CU's 160 KiB, so every decoding wave has its SIMD to itself (single waves per workgroup were
 // placed two to a SIMD on some CUs while other SIMDs idled).
-#define DEC_WAVES 4
-__global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __restrict__ bytes,
+template <int MODE, int W>
+__global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ bytes,
                                                 const GkBlock* __restrict__ blocks,
                                                 const uint32_t* __restrict__ order, uint64_t* __restrict__ scratch,
                                                 const uint64_t* __restrict__ wave_off, uint32_t nblocks,
                                                 unsigned long long* __restrict__ stats, uint32_t kpark) {
     constexpr bool TIMING = MODE == 2, STATS = MODE >= 1;
-    __shared__ Dec2Lds Lw[DEC_WAVES];
+    __shared__ Dec2Lds Lw[W];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     Dec2Lds& Ls = Lw[wv];
-    const uint32_t gw = blockIdx.x * DEC_WAVES + wv;          // global wave: 64 slots
+    const uint32_t gw = blockIdx.x * W + wv;          // global wave: 64 slots
     const uint32_t nwaves = (nblocks + 63) / 64;
     for (int i = lane; i < MQ_PAIRS; i += 64) Ls.tab[i] = mq_pair_entry((uint32_t)i);
     for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
@@ -364,7 +363,11 @@ __global__ __launch_bounds__(64 * DEC_WAVES) void k_t1_dec2(const uint8_t* __res
 
     // the lane with the most stripe-passes left (the wave lasts as long as it does), wave-uniform
     auto critical_lane = [&]() -> uint32_t {
-        const uint32_t rem = done ? 0u : (npasses - pidx) * ns - s;
+        // work left: stripe-passes (default), compressed bytes (GK_T1DEC_CRIT=2) or 8 x bytes +
+        // 4 x stripe-passes (GK_T1DEC_CRIT=3); kpark bits 10-11
+        const uint32_t sp = (npasses - pidx) * ns - s, nb = q.len > q.bp ? q.len - q.bp : 0u;
+        const uint32_t mode = (kpark >> 10) & 3;
+        const uint32_t rem = done ? 0u : min(mode == 0 ? sp : (mode == 1 ? nb : 8 * nb + 4 * sp), 0x3ffffffu);
         // wave max through DPP (row_shr 1/2/4/8, row_bcast 15/31): lane 63 ends with it
         uint32_t key = (rem << 6) | (uint32_t)lane;
         key = max(key, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x111, 0xf, 0xf, false));
@@ -829,21 +832,31 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         // GK_T1DEC_CRIT=0: no event for the lane with the most work left alone (bit 8 of kpark)
         const char* kc = getenv("GK_T1DEC_CRIT");
         if (!kc || atoi(kc)) kpark |= 0x100;
+        if (kc && atoi(kc) >= 2) kpark |= (atoi(kc) - 1) << 10;
         // GK_T1DEC_MID=0: no half-group exit when that lane has parked (bit 9)
         const char* km = getenv("GK_T1DEC_MID");
         if (!km || atoi(km)) kpark |= 0x200;
     }
-    const uint32_t nwaves = (nblocks + 63) / 64, ngroups = (nwaves + DEC_WAVES - 1) / DEC_WAVES;
-    const size_t pad = DEC_WAVES * sizeof(Dec2Lds) < 163840 ? 163840 - DEC_WAVES * sizeof(Dec2Lds) : 0;
+    // waves per workgroup (GK_T1DEC_WPG, 3 or 4): 3 spreads up to 3 x 256 waves one CU each with a
+    // SIMD spare, 4 packs them onto fewer CUs
+    static int wpg = -1;
+    if (wpg < 0) {
+        const char* v = getenv("GK_T1DEC_WPG");
+        wpg = (v && atoi(v) == 3) ? 3 : 4;
+    }
+    const uint32_t nwaves = (nblocks + 63) / 64;
+    auto launch = [&](auto kern, uint32_t W, unsigned long long* stp) {
+        const uint32_t ngroups = (nwaves + W - 1) / W;
+        const size_t pad = W * sizeof(Dec2Lds) < 163840 ? 163840 - W * sizeof(Dec2Lds) : 0;
+        hipLaunchKernelGGL(kern, dim3(ngroups), dim3(64 * W), pad, st, bytes, blocks, order, scratch, wave_off, nblocks,
+                           stp, (uint32_t)kpark);
+    };
     if (timing)
-        hipLaunchKernelGGL(k_t1_dec2<2>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order, scratch,
-                           wave_off, nblocks, stats, (uint32_t)kpark);
+        launch(k_t1_dec2<2, 4>, 4, stats);
     else if (want)
-        hipLaunchKernelGGL(k_t1_dec2<1>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order,
-                           scratch, wave_off, nblocks, stats, (uint32_t)kpark);
+        wpg == 3 ? launch(k_t1_dec2<1, 3>, 3, stats) : launch(k_t1_dec2<1, 4>, 4, stats);
     else
-        hipLaunchKernelGGL(k_t1_dec2<0>, dim3(ngroups), dim3(64 * DEC_WAVES), pad, st, bytes, blocks, order,
-                           scratch, wave_off, nblocks, nullptr, (uint32_t)kpark);
+        wpg == 3 ? launch(k_t1_dec2<0, 3>, 3, nullptr) : launch(k_t1_dec2<0, 4>, 4, nullptr);
     if (want) {
         unsigned long long h[16];
         (void)hipMemcpyAsync(h, stats, 128, hipMemcpyDeviceToHost, st);

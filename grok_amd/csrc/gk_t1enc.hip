@@ -419,10 +419,16 @@ __device__ __forceinline__ void mq_put5(MqLane& q, MqLds& L, int lane, uint32_t 
 // The finished byte (cur plus the carry) goes to position bp: into the dword buffer and,
 // unconditionally, into the ring (bp = -1 is the coder's dummy byte before the buffer, and
 // bytes at or past cap are dropped: the final bp reports the overflow).
+// CARRY = false: C is known to be below 2^27 (a second BYTEOUT in one renormalisation: the first
+// left C below 2^20 and at most 8 shifts followed), so the carry test is left out.
+template <bool CARRY = true>
 __device__ __forceinline__ void mq_byteout5(MqLane& q, MqLds& L, int lane, uint32_t bo, uint32_t& c, uint32_t& ct) {
-    const uint32_t carry = (c >> 27) & 1u & bo & ~mz(q.cur ^ 0xffu);
-    const uint32_t cur = q.cur + carry;
-    c &= ~(carry << 27);
+    uint32_t cur = q.cur;
+    if constexpr (CARRY) {
+        const uint32_t carry = (c >> 27) & 1u & bo & ~mz(q.cur ^ 0xffu);
+        cur += carry;
+        c &= ~(carry << 27);
+    }
     const uint32_t ffm = mz(cur ^ 0xffu);                          // 0 / -1
     const uint32_t nb = __builtin_amdgcn_ubfe(c, 19u - ffm, 8);    // C >> 20 after 0xFF, else C >> 19
     mq_put5(q, L, lane, bo, cur);
@@ -476,7 +482,7 @@ __device__ __forceinline__ void mq_code5(MqLane& q, MqLds& L, int lane, uint32_t
     if (two) {
         const uint32_t n2a = min(n2, ct);
         c <<= n2a; ct -= n2a; n2 -= n2a;
-        mq_byteout5(q, L, lane, mz(ct), c, ct);
+        mq_byteout5<false>(q, L, lane, mz(ct), c, ct);
     }
     q.c = c << n2;
     q.ct = ct - n2;
