@@ -481,7 +481,8 @@ def main():
         try:
             r.eng.decode(r.out, length=r.n, out=r.y)
             t = r.eng.timings()
-            dec_steps = (int(t.t1_steps_max), int(t.t1_steps_total), int(t.t1_symbols))
+            dec_steps = (int(t.t1_steps_max), int(t.t1_steps_total), int(t.t1_symbols), int(t.t1_solo_blocks),
+                         int(t.t1_solo_decisions), int(t.t1_solo_decisions_max))
         finally:
             del os.environ["GK_T1_STATS"]
     r.close()
@@ -573,7 +574,7 @@ def main():
         if cp.get("cblk_sty"):   # HTJ2K: one cleanup-pass coder kernel each way
             dec_k, enc_k = ("T1 decode (k_ht_dec)", ["k_ht_dec"]), ("T1 encode (k_ht_enc)", ["k_ht_enc"])
         else:
-            dec_k = ("T1 decode (k_t1_dec2 + k_t1_recon)", ["void k_t1_dec2<0>", "k_t1_recon"])
+            dec_k = ("T1 decode (k_t1_dec2 + k_t1_recon)", ["void k_t1_dec2<0, 4>", "k_t1_recon"])
             cm = "void k_t1_cm<true>" if cp.get("irreversible") else "void k_t1_cm<false>"
             enc_k = ("T1 encode (k_t1_cm + k_t1_mq)", [cm, "k_t1_mq"])
         dw = "97" if cp.get("irreversible") else "53"
@@ -634,11 +635,14 @@ def main():
             res["issue_roofline"] = {
                 "kernel": "k_t1_dec2 (T1 decode chain)", "bound": "instruction issue of the longest wave",
                 "max_steps_per_wave": dec_steps[0], "instructions_per_step": dec_ips,
-                "instructions_per_step_source": "llvm-objdump of %s (k_t1_dec2<0> step bodies: %s)" % (
+                "instructions_per_step_source": "llvm-objdump of %s (k_t1_dec2<0, 4> step bodies: %s)" % (
                     os.path.relpath(G.LIB_PATH, ROOT), ", ".join("%s %d" % kv for kv in dec_by.items())),
                 "clock_ghz": CLOCK_GHZ, "floor_ms": round(floor_ms, 3), "measured_ms": round(dec2_ms, 3),
                 "frac": round(floor_ms / dec2_ms, 3), "steps_total": dec_steps[1], "symbols": dec_steps[2],
-                "lane_efficiency": round(dec_steps[2] / (64.0 * dec_steps[1]), 3) if dec_steps[1] else None}
+                "lane_efficiency": round(dec_steps[2] / (64.0 * dec_steps[1]), 3) if dec_steps[1] else None,
+                "solo": {"blocks": dec_steps[3], "decisions": dec_steps[4], "max_decisions_per_wave": dec_steps[5],
+                         "note": "heaviest blocks decoded one per wave on the SIMDs the lane-parallel waves leave "
+                                 "(gk_t1dec.hip solo_block); the steps above are the lane-parallel waves'"}}
         if aux:
             res["aux"] = aux
         if not args.no_cpu_baseline:

@@ -66,7 +66,8 @@ class Timings(ctypes.Structure):
                                               "t1_cm_ms", "t1_coder_ms")] + \
                [("dwt_launches", ctypes.c_uint32), ("t1_blocks", ctypes.c_uint32)] + \
                [(n, ctypes.c_uint64) for n in ("dwt_bytes", "cs_bytes", "t1_bytes", "t1_steps_max", "t1_steps_total",
-                                               "t1_symbols")]
+                                               "t1_symbols", "t1_solo_blocks", "t1_solo_decisions",
+                                               "t1_solo_decisions_max")]
 
 
 _lib = None

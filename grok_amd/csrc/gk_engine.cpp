@@ -45,6 +45,14 @@ struct GkError {
     std::string msg;
     explicit GkError(std::string m) : msg(std::move(m)) {}
 };
+// Kernel launches report a bad configuration only through hipGetLastError: each stage of an
+// encode / decode ends with this check, so such an error fails the call that made it (with the
+// engine source line of the stage) instead of surfacing in a later, unrelated HIP call.
+static void launch_check(int line) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        throw GkError("kernel launch before gk_engine.cpp:" + std::to_string(line) + ": " + hipGetErrorString(e));
+}
 
 // Persistent host worker pool for the T2 stages (tiles, precinct chains, blocks).
 // run(n, f) calls f(0..n-1) across the workers and the caller, and returns when all
@@ -2489,6 +2497,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const uint32_t ry0 = P.tiles[jb * P.ntx].y0 - P.y0, ry1 = P.tiles[(je - 1) * P.ntx].y1 - P.y0;  // image rows touched
     hipStream_t st = ctx->st;
 
+    launch_check(__LINE__);
+
     HIPCHK(hipEventRecord(ctx->ev[0], st));
     // work planes for the sample rows of the selected tiles only
     const Region RG = make_region(0, ry0, P.w, ry1);
@@ -2512,6 +2522,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             src[c] = (const uint8_t*)comps[c] + (size_t)ry0 * strides[c] * es; sstr[c] = strides[c];
         }
     }
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
     auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * RG.plane; };
@@ -2533,6 +2544,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         if (mct3) gk_launch_dc_ict_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), RG.stride, P.w, nrows, shift);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, stype, src[c], sstr[c], planeAf(c), RG.stride, P.w, nrows, shift);
     }
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     run_dwt(ctx, RG, true, jb, je, 0, 0xffffffffu, fused ? &io : nullptr);
     if (const char* dp = getenv("GK_DUMP_DWT")) {   // debug: the work planes after the forward DWT
@@ -2546,6 +2558,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             fclose(f);
         }
     }
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // T1 over the block range [b0, b1): every per-block device array is range-local
     const bool do_rc = P.p.rate_control();
@@ -2584,15 +2597,18 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     if (P.p.ht()) {
         // HT cleanup pass (T1HT::compress, T1HT.cpp:109-133); MEL bytes staged in the symbol buffer
         uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nbx * GK_HT_MEL_CAP + 256);
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_ht_enc(st, arena, dblk, dbytes, mel, GK_HT_MEL_CAP, dinfo, nbr, derr);
     } else if (P.p.cblk_sty & 0x3f) {
         // mode switches: lane-per-block coder with per-pass termination rules (gk_t1ms.hip)
         uint8_t* mst = (uint8_t*)ctx->dmsstate.get(gk_t1ms_state_bytes(nbx));
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_t1_enc_ms(st, arena, dblk, dbytes, dps, dinfo, nbr, derr, ctx->nmse_tab, dpcount, mst, P.p.cblk_sty & 0x3f);
     } else if (nbr < 8192 || getenv("GK_T1ENC_SERIAL")) {
         gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nbr, derr, ctx->nmse_tab, dnmse);
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount);
     } else {
@@ -2650,6 +2666,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
                                 dord, base, cnt);
                 HIPCHK(hipEventRecord(ctx->xev[3 + k], ctx->aux[k]));
             } else {
+                launch_check(__LINE__);
                 HIPCHK(hipEventRecord(ctx->ev[8], st));
                 gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount, dord,
                                 base, cnt);
@@ -2657,6 +2674,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         }
         for (int k = 0; k + 1 < nch; ++k) HIPCHK(hipStreamWaitEvent(st, ctx->xev[3 + k], 0));
     }
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[4], st));
     // GK_PROFILE=1: host phase times of the encode's T2 (stderr)
     static const bool eprof = getenv("GK_PROFILE") != nullptr;
@@ -2920,6 +2938,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         write_jp2_prefix(J, P, total - jp2_prefix_size(P));
         memcpy(hdrs.data(), J.data(), J.size());
     }
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (eprof)
         fprintf(stderr, "encode t2: fetch %.2f ms, allocate %.2f ms, packets %.2f ms, segments %.2f ms\n", ems(te0, te1),
@@ -2936,8 +2955,10 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     HIPCHK(hipMemcpyAsync(ds, hs, seg.size() * 8, hipMemcpyHostToDevice, st));
     uint8_t* dst = out_on_device ? out : (uint8_t*)ctx->dout.get(total);
     gk_launch_gather(st, dbytes, dst, ds, (uint32_t)(seg.size() / 3));
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[6], st));
     if (!out_on_device) HIPCHK(hipMemcpyAsync(out, dst, total, hipMemcpyDeviceToHost, st));
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[7], st));
     HIPCHK(hipStreamSynchronize(st));
     ctx->tm.mct_ms = ev_ms(ctx, 1, 2);
@@ -3285,6 +3306,7 @@ static void merge_tile_parts(Header& Hd) {
 static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void* const* comps,
                         const uint32_t* strides, uint32_t sample_bytes, int out_on_device, const uint32_t* win = nullptr) {
     hipStream_t st = ctx->st;
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[0], st));
     // GK_PROFILE=1: host phase times of the decode (stderr)
     static const bool prof = getenv("GK_PROFILE") != nullptr;
@@ -3622,6 +3644,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 }
         }
     const uint32_t nbr = nblk, nbx = std::max(nbr, 1u);
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     // ---- stage compressed bytes on the device.  A host stream of which the selected blocks
     // use a small part (window decode of a large file) is gathered on the host and only those
@@ -3683,6 +3706,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // need no clearing (they only feed samples outside the output region)
     if (Hd.parts.size() < (size_t)(ie - ib) * (je - jb))
         HIPCHK(hipMemsetAsync(arena, 0, RG.plane * P.nc * 2 * sizeof(int32_t), st));
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     if (nbr == 0) {
         // nothing to decode (all-zero tiles)
@@ -3695,6 +3719,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         int* derr = (int*)ctx->derr.get(64);
         HIPCHK(hipMemsetAsync(derr, 0, 64, st));
         gk_launch_ht_dec(st, src_bytes, dblk, dsel, arena, nbr, derr);
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         int herr = 0;
         HIPCHK(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st));
@@ -3711,6 +3736,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         }
         uint8_t* mst = (uint8_t*)ctx->dmsstate.get(gk_t1ms_state_bytes(nbx));
         gk_launch_t1_dec_ms(st, src_bytes, dblk, dsl, arena, nbr, mst, P.p.cblk_sty & 0x3f);
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         if (multiseg && !hseglen.empty()) HIPCHK(hipStreamSynchronize(st));   // the pinned table is reused
     } else {
@@ -3719,31 +3745,54 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // `L` lanes of each 64-lane wave carry a block (gk_t1dec_lanes): fewer lanes per wave
         // give more waves, so every SIMD of the chip holds waves and can hide latency.
         const uint32_t L = gk_t1dec_lanes();
-        const uint32_t nw = (nbr + L - 1) / L, nslots = nw * 64;
+        // the heaviest blocks (most compressed bytes: decisions follow the bytes closely) go to
+        // solo waves, one block each, first in the grid (gk_t1dec.hip, solo_block)
+        const uint32_t nsb = nbr ? gk_t1dec_solo_blocks(nbr, L) : 0;
+        const uint32_t nsw = (nsb + 11) / 12 * 12;
+        const uint32_t nw = nsw + (nbr - nsb + L - 1) / L, nslots = nw * 64;
         uint32_t* hord = (uint32_t*)ctx->hord.get(4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
         uint32_t* hpos = hord + nslots;               // slot of block k
         uint32_t* hids = hpos + nbr;                  // identity (compact table)
         uint64_t* hwo = (uint64_t*)(hids + nbr + 2);
         {
             std::fill(hord, hord + nslots, 0xffffffffu);
+            std::vector<uint8_t> solo(nbr, 0);
+            if (nsb) {
+                std::vector<uint32_t> byl(nbr);
+                for (uint32_t q = 0; q < nbr; ++q) byl[q] = q;
+                auto heavier = [&](uint32_t x, uint32_t y) {
+                    const uint32_t lx = blk[x].npasses ? blk[x].len : 0, ly = blk[y].npasses ? blk[y].len : 0;
+                    return lx != ly ? lx > ly : x < y;
+                };
+                std::nth_element(byl.begin(), byl.begin() + (nsb - 1), byl.end(), heavier);
+                std::sort(byl.begin(), byl.begin() + nsb, heavier);
+                for (uint32_t j = 0; j < nsb; ++j) {
+                    const uint32_t q = byl[j];
+                    solo[q] = 1;
+                    hord[(size_t)j * 64] = q; hpos[q] = j * 64;
+                }
+            }
             std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
-            for (uint32_t q = 0; q < nbr; ++q) cnt[std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1)]++;
+            for (uint32_t q = 0; q < nbr; ++q)
+                if (!solo[q]) cnt[std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1)]++;
             std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
             uint32_t acc = 0;
             for (int k = GK_MAX_PASSES + 1; k >= 0; --k) { start[k] = acc; acc += cnt[k]; }
             for (uint32_t q = 0; q < nbr; ++q) {
+                hids[q] = q;
+                if (solo[q]) continue;
                 const uint32_t k = std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1);
                 const uint32_t idx = start[k]++;
-                const uint32_t slot = (idx / L) * 64 + idx % L;
+                const uint32_t slot = (nsw + idx / L) * 64 + idx % L;
                 hord[slot] = q; hpos[q] = slot;
-                hids[q] = q;
             }
             uint64_t wo = 0;
             for (uint32_t wv = 0; wv < nw; ++wv) {
                 hwo[wv] = wo;
                 uint32_t mp = 0;
-                for (uint32_t i = wv * 64; i < wv * 64 + L; ++i)
+                for (uint32_t i = wv * 64; i < wv * 64 + (wv < nsw ? 1 : L); ++i)
                     if (hord[i] != 0xffffffffu) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
+                if (wv < nsw && hord[wv * 64] == 0xffffffffu) continue;   // a solo wave without a block
                 wo += (272 + (uint64_t)mp * 64) * 64;   // per-lane slab: WS_FIXED + planes (gk_t1dec.hip), 128 B lines
             }
             hwo[nw] = wo;
@@ -3755,19 +3804,25 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         const uint32_t* dids = dpos + nbr;
         const uint64_t* dwo = (const uint64_t*)(dids + nbr + 2);
         uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
-        HIPCHK(hipMemsetAsync(dscr, 0, 8 * hwo[nw], st));   // decoder state rows start at zero
-        gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nslots);
+        // lane-parallel decoder state rows start at zero; solo waves write every row recon reads
+        HIPCHK(hipMemsetAsync(dscr + hwo[nsw], 0, 8 * (hwo[nw] - hwo[nsw]), st));
+        gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nslots, nsw);
         ctx->tm.t1_steps_max = ctx->tm.t1_steps_total = ctx->tm.t1_symbols = 0;
+        ctx->tm.t1_solo_decisions = ctx->tm.t1_solo_decisions_max = 0;
+        ctx->tm.t1_solo_blocks = nsb;
         if (getenv("GK_T1_STATS")) {
-            uint64_t sv[3];
+            uint64_t sv[5];
             gk_t1dec_stats(sv);
             ctx->tm.t1_steps_max = sv[0]; ctx->tm.t1_steps_total = sv[1]; ctx->tm.t1_symbols = sv[2];
+            ctx->tm.t1_solo_decisions = sv[3]; ctx->tm.t1_solo_decisions_max = sv[4];
         }
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         uint32_t maxnp = 1;
         for (uint32_t q = 0; q < nbr; ++q) maxnp = std::max<uint32_t>(maxnp, blk[q].numbps);
         gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr, maxnp);
     }
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // ---- inverse DWT; its last level writes the output region through the inverse MCT + DC
     // shift + clamp into the output planes (without decomposition levels a separate pass does)
@@ -3783,6 +3838,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // writes it per tile into the ceil(size / 2^red) output (a tile's reduced origin is
         // ceil(origin / 2^red), B.5)
         run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr, red + 1);
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
         // reduced canvas: positions ceil(x / 2^red); output index = that less the image origin's
         const uint32_t rox = ceildivpow2(P.x0, red), roy = ceildivpow2(P.y0, red);
@@ -3821,11 +3877,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 }
             }
         if (mct3r && (qs[1] != qs[0] || qs[2] != qs[0])) throw GkError("the first three components must share a stride");
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[5], st));
         if (!out_on_device)
             for (uint32_t c = 0; c < P.nc; ++c)
                 HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)qy0 * strides[c] + qx0) * es, (size_t)strides[c] * es,
                                         qd[c], (size_t)qcols * es, (size_t)qcols * es, qrows, hipMemcpyDeviceToHost, st));
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[6], st));
         HIPCHK(hipStreamSynchronize(st));
         ctx->tm.t2_ms = ev_ms(ctx, 0, 1); ctx->tm.t1_ms = ev_ms(ctx, 2, 3); ctx->tm.t1_cm_ms = 0.f;
@@ -3862,20 +3920,24 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         io.win.x1 = io.win.x0 + (int32_t)ncols; io.win.y1 = io.win.y0 + (int32_t)nrows;
         if (mct3 && (dstr[1] != dstr[0] || dstr[2] != dstr[0])) throw GkError("the first three components must share a stride");
         run_dwt(ctx, RG, false, jb, je, ib, ie, &io);
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
     } else if (!P.p.irrev) {
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
         if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
                                        ncols, nrows, shift, mn, mx);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
             gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
     } else {
+        launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
         if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
                                        ncols, nrows, shift, mn, mx);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
             gk_launch_dc_inv_f(st, planeAf(c), RG.stride, stype, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
     }
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (!out_on_device) {
         for (uint32_t c = 0; c < P.nc; ++c)
@@ -3883,6 +3945,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                     (size_t)strides[c] * es, dst[c], (size_t)ncols * es, (size_t)ncols * es, nrows,
                                     hipMemcpyDeviceToHost, st));
     }
+    launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[6], st));
     HIPCHK(hipStreamSynchronize(st));
     ctx->tm.t2_ms = ev_ms(ctx, 0, 1);

@@ -48,10 +48,14 @@ void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off
 // per-block coded bit-plane count (weight of the chunked CM / MQ overlap)
 void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint32_t* weight, uint32_t nblocks);
 uint32_t gk_t1dec_lanes();
-// counters of the last k_t1_dec2 launch made with GK_T1_STATS set: max steps per wave, steps, symbols
-void gk_t1dec_stats(uint64_t out[3]);
+// counters of the last k_t1_dec2 launch made with GK_T1_STATS set: max steps per wave, steps,
+// symbols (lane-parallel waves), decisions of the solo waves and of the busiest one
+void gk_t1dec_stats(uint64_t out[5]);
+// blocks decoded by solo waves (one wave per block, on the SIMDs the lane-parallel waves leave)
+uint32_t gk_t1dec_solo_blocks(uint32_t nblocks, uint32_t lanes);
+// the first nsolo waves of `order` are solo waves (a multiple of 12)
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
-                      uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks);
+                      uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks, uint32_t nsolo);
 void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* ids, const uint32_t* pos,
                         const uint64_t* scratch, const uint64_t* wave_off, int32_t* coef, uint32_t nblocks,
                         uint32_t maxnp);   // maxnp: the blocks' largest numbps

@@ -37,6 +37,7 @@
 #include "gk_t1_common.h"
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 
 // per-lane scratch (uint64 words, one contiguous slab per lane, 128-byte aligned).  A stripe's
 // state rows are one 128-byte line: stripe s at 16 s holds significance, sign, visited (SP of the
@@ -223,6 +224,260 @@ __device__ __forceinline__ uint64_t h_get(uint32_t (*g)[64], int row, int lane) 
     return ((uint64_t)g[row * 2 + 1][lane] << 32) | g[row * 2][lane];
 }
 
+// ------------------------------------------------------------------ solo decoding
+// The wave's time is its heaviest lane's: the LL and low-resolution blocks (C2: 31.9 k decisions
+// against a plateau of ~28 k for the level-1 bands; C3 without truncation 65 k against ~37 k) set
+// the kernel time while a quarter of the SIMDs idle.  Those blocks are decoded by "solo" waves
+// that run on the spare SIMDs, one block at a time: the control flow and the MQ registers are
+// wave-uniform (scalar branches, SALU), so a decision costs what its own path needs instead of
+// the lane-parallel step's every-case select chain.  The block's state sits in the lanes
+// (lane = column x, bit y = row y): significance, sign, refined, visited-in-SP and the plane's
+// bits, as 64-bit columns.  A stripe-pass packs each column's window into one dword per lane and
+// walks the columns with three of them in SGPRs (left, current, right); a column's word goes
+// back with v_writelane and the stripe's rows are merged into the columns by VALU at its end.
+// Context states, the (state, MPS) pair table and the ZC / SC rule tables live in VGPR lanes
+// and are read with v_readlane.  Output: the plane-bit rows and the sign rows of the lane slab
+// layout above (WS_BITS, WS_N), transposed with ballots, so k_t1_recon is shared.
+// Same algorithm as the lane-parallel step (T1::decompress_cblk, T1.cpp:934-1446; Annex C.3 /
+// D restated in oracle/j2k_oracle.cpp t1_decode_block), default code-block style only.
+//
+// Column word (per lane, rows relative to the stripe's first row y0):
+//   bits 0-5   significance of rows y0-1 .. y0+4
+//   bits 6-17  (significance, sign) pairs of rows y0-1 .. y0+4 (pair j at 6 + 2 j)
+//   bits 18-21 visited in SP of this plane, rows y0 .. y0+3
+//   bits 22-25 refined in an earlier plane
+//   bits 26-29 bits of this plane
+#define SW_PI 18
+#define SW_MU 22
+#define SW_BT 26
+__device__ __forceinline__ uint32_t srl(uint32_t v, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+__device__ __forceinline__ uint32_t swl(uint32_t old, uint32_t val, uint32_t lane) {   // v_writelane_b32
+    // (gfx9 reads one SGPR per VALU op besides M0: the lane select goes through M0)
+    asm("v_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(val), "{m0}"(lane));
+    return old;
+}
+// rows y0-1 .. y0+4 of a column (bit 0 = row y0-1)
+__device__ __forceinline__ uint32_t win6(uint64_t v, uint32_t y0) {
+    return y0 ? (uint32_t)(v >> (y0 - 1)) & 0x3fu : (uint32_t)(v << 1) & 0x3fu;
+}
+__device__ __forceinline__ uint32_t spread6(uint32_t v) {   // bit j -> bit 2 j
+    return (v & 1u) | ((v & 2u) << 1) | ((v & 4u) << 2) | ((v & 8u) << 3) | ((v & 16u) << 4) | ((v & 32u) << 5);
+}
+// ballot transpose: row y (bit x = lane x's bit y) into lane y of the result
+__device__ __forceinline__ uint64_t rows_of(uint64_t col, uint32_t h, int lane) {
+    uint32_t lo = 0, hi = 0;
+    for (uint32_t y = 0; y < h; ++y) {
+        const uint64_t r = __ballot((col >> y) & 1);
+        lo = swl(lo, (uint32_t)r, y);
+        hi = swl(hi, (uint32_t)(r >> 32), y);
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <bool STATS>
+__device__ void solo_block(const uint8_t* __restrict__ bytes, const GkBlock& B, uint64_t* __restrict__ WS, int lane,
+                           unsigned long long* __restrict__ stats) {
+    const uint32_t numbps = B.numbps, npasses = B.numbps ? B.npasses : 0;
+    if (!npasses) return;
+    const uint32_t w = B.w, h = B.h, ns = (h + 3) >> 2, orient = B.orient & 3;
+    // rule tables in lanes: ZC 8 entries of 4 bits per lane, index = left | centre << 3 | right << 6
+    // (3 rows each, bit 0 = the row above); SC 4 entries of 8 bits per lane, index = (sig, sign)
+    // pairs of N | W << 2 | S << 4 | E << 6
+    uint32_t ZCL = 0, SCL = 0;
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t i = (uint32_t)lane * 8 + k;
+        const uint32_t l = i & 7, c = (i >> 3) & 7, r = (i >> 6) & 7;
+        // zc_rule: bit0 NW 1 N 2 NE 3 W 4 self 5 E 6 SW 7 S 8 SE
+        const uint32_t f = (l & 1) | ((c & 1) << 1) | ((r & 1) << 2) | (((l >> 1) & 1) << 3) | (((c >> 1) & 1) << 4) |
+                           (((r >> 1) & 1) << 5) | (((l >> 2) & 1) << 6) | (((c >> 2) & 1) << 7) | (((r >> 2) & 1) << 8);
+        ZCL |= (uint32_t)zc_rule(orient, f) << (4 * k);
+    }
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t i = (uint32_t)lane * 4 + k;
+        // sc_rule: bit0 W-neg 1 W-sig 2 E-neg 3 E-sig 4 N-neg 5 N-sig 6 S-neg 7 S-sig
+        const uint32_t N = i & 3, Wp = (i >> 2) & 3, S = (i >> 4) & 3, E = (i >> 6) & 3;
+        const uint32_t f = (Wp >> 1) | ((Wp & 1) << 1) | ((E >> 1) << 2) | ((E & 1) << 3) | ((N >> 1) << 4) |
+                           ((N & 1) << 5) | ((S >> 1) << 6) | ((S & 1) << 7);
+        SCL |= (uint32_t)sc_rule(f) << (8 * k);
+    }
+    const uint32_t TAB0 = mq_pair_entry((uint32_t)lane), TAB1 = lane < MQ_PAIRS - 64 ? mq_pair_entry(64u + lane) : 0u;
+    // mqc_resetstates (mqc_dec.cpp:121-130)
+    uint32_t CTX = mq_pair_entry(2u * (lane == CTX_ZC ? 4u : (lane == CTX_AGG ? 3u : (lane == CTX_UNI ? 46u : 0u))));
+
+    // compressed bytes: a 256-byte window in the lanes (4 per lane); bytes at or past the length
+    // read 0xFF (the host pads every block with >= 32 bytes of 0xFF)
+    const uint8_t* p = bytes + B.data_off;
+    const uint32_t len = B.len;
+    uint32_t wb = 0, BW = 0;
+    auto load_window = [&](uint32_t at) {
+        wb = at;
+        const uint32_t o = at + 4u * (uint32_t)lane;
+        BW = o < len ? *reinterpret_cast<const uint32_t*>(p + o) : 0xffffffffu;
+    };
+    load_window(0);
+    // MQ code register (INITDEC / BYTEIN, Annex C.3.4-C.3.5, as Mq2 above): bits 63:48 = Chigh,
+    // `avail` valid bits below; the queue starts with a 0 bit, then the bytes (7 bits after an
+    // 0xFF, 1s for ever from a marker on)
+    uint64_t c = 0;
+    int32_t avail = -15;
+    uint32_t a = 0x8000, bp = 0;
+    bool prevff = false, ones = false;
+    auto refill = [&]() {
+        uint32_t off = bp - wb;
+        if (off > 248) { load_window(bp); off = 0; }
+        const uint32_t j = off >> 2, sh = (off & 3) * 8;
+        const uint64_t two = ((uint64_t)srl(BW, j + 1) << 32) | srl(BW, j);
+        const uint32_t word = (uint32_t)(two >> sh);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t b = (word >> (8 * k)) & 0xffu;
+            if (!ones && prevff && b > 0x8f) ones = true;
+            if (ones) {
+                c += (uint64_t)0xffu << (40 - avail);
+                avail += 8;
+            } else if (prevff) {
+                c += (uint64_t)b << (41 - avail);
+                avail += 7;
+                prevff = false;
+                ++bp;
+            } else {
+                c += (uint64_t)b << (40 - avail);
+                avail += 8;
+                prevff = b == 0xffu;
+                ++bp;
+            }
+        }
+    };
+    while (avail < 16) refill();
+    uint32_t ndec = 0;
+    auto tab = [&](uint32_t i) { return i < 64 ? srl(TAB0, i) : srl(TAB1, i - 64); };
+    // DECODE (Annex C.3.2) with RENORMD as one shift
+    auto dec = [&](uint32_t cx) -> uint32_t {
+        if (STATS) ++ndec;
+        const uint32_t e = srl(CTX, cx);
+        const uint32_t qe = e & 0xffffu;
+        uint32_t d = e >> 31;
+        a -= qe;
+        // lower sub-interval (Chigh < Qe): A = Qe, the exchange rule picks the symbol; upper: C -=
+        // Qe, renormalisation only when A fell below 0x8000
+        const uint32_t lower = (uint32_t)(c >> 48) < qe ? 1u : 0u;
+        const uint32_t lps = lower ^ (a < qe ? 1u : 0u);
+        const bool upd = lower || (a & 0x8000u) == 0;
+        c -= lower ? 0ull : (uint64_t)qe << 48;
+        a = lower ? qe : a;
+        if (upd) {
+            d ^= lps;
+            CTX = swl(CTX, tab(lps ? (e >> 23) & 0x7fu : (e >> 16) & 0x7fu), cx);
+            const uint32_t n = (uint32_t)__builtin_clz(a) - 16u;
+            a <<= n;
+            c <<= n;
+            avail -= (int32_t)n;
+            if (avail < 16) refill();
+        }
+        return d;
+    };
+
+    // block state: columns (bit y = row y)
+    uint64_t SG = 0, NG = 0, PI = 0, MU = 0, BT = 0;
+    uint32_t k = 0, t = 2;   // plane (0 = most significant) and pass type (0 SP, 1 MR, 2 CL)
+    auto flush_plane = [&](uint32_t kk) {
+        const uint64_t rows = rows_of(BT, h, lane);
+        if ((uint32_t)lane < h) WS[WS_BITS + (size_t)kk * 64 + lane] = rows;
+    };
+    for (uint32_t pidx = 0; pidx < npasses && k < numbps; ++pidx) {
+        for (uint32_t s = 0; s < ns; ++s) {
+            const uint32_t y0 = 4 * s, nr = min(4u, h - y0);
+            uint32_t W = win6(SG, y0) | (spread6(win6(SG, y0)) << 6) | (spread6(win6(NG, y0)) << 7) |
+                         (((uint32_t)(PI >> y0) & 15u) << SW_PI) | (((uint32_t)(MU >> y0) & 15u) << SW_MU) |
+                         (((uint32_t)(BT >> y0) & 15u) << SW_BT);
+            uint32_t Wl = 0, Wc = srl(W, 0), Wr = w > 1 ? srl(W, 1) : 0u;
+            for (uint32_t x = 0; x < w; ++x) {
+                const uint32_t Wn = x + 2 < w ? srl(W, x + 2) : 0u;
+                auto zidx = [&](uint32_t i) {
+                    return ((Wl >> i) & 7u) | (((Wc >> i) & 7u) << 3) | (((Wr >> i) & 7u) << 6);
+                };
+                // a decision 1 in ZC / run-length: the sign, then the sample is significant
+                auto sign = [&](uint32_t i) {
+                    const uint32_t si = ((Wc >> (6 + 2 * i)) & 0x33u) | (((Wl >> (8 + 2 * i)) & 3u) << 2) |
+                                        (((Wr >> (8 + 2 * i)) & 3u) << 6);
+                    const uint32_t sce = (srl(SCL, si >> 2) >> (8 * (si & 3))) & 0xffu;
+                    const uint32_t sg = dec(CTX_SC + (sce & 15u)) ^ (sce >> 4);
+                    Wc |= (1u << (1 + i)) | (1u << (8 + 2 * i)) | (sg << (9 + 2 * i)) | (1u << (SW_BT + i));
+                };
+                if (t == 0) {   // significance propagation (T1.cpp dec_sigpass)
+                    for (uint32_t i = 0; i < nr; ++i) {
+                        if ((Wc >> (1 + i)) & 1u) continue;
+                        const uint32_t zi = zidx(i);
+                        if (!zi) continue;
+                        if (dec(CTX_ZC + ((srl(ZCL, zi >> 3) >> (4 * (zi & 7))) & 15u))) sign(i);
+                        Wc |= 1u << (SW_PI + i);
+                    }
+                } else if (t == 1) {   // magnitude refinement (dec_refpass)
+                    for (uint32_t i = 0; i < nr; ++i) {
+                        if (((Wc >> (1 + i)) & 1u) == 0 || ((Wc >> (SW_PI + i)) & 1u)) continue;
+                        const uint32_t cx = ((Wc >> (SW_MU + i)) & 1u) ? CTX_MAG + 2
+                                            : ((zidx(i) & ~0x10u) ? CTX_MAG + 1 : CTX_MAG);
+                        if (dec(cx)) Wc |= 1u << (SW_BT + i);
+                        Wc |= 1u << (SW_MU + i);
+                    }
+                } else {   // cleanup (dec_clnpass), run-length mode on whole insignificant columns
+                    uint32_t i = 0;
+                    bool partial = false, skip = false;
+                    if (nr == 4 && (((Wl | Wc | Wr) & 0x3fu) | ((Wc >> SW_PI) & 15u)) == 0) {
+                        if (!dec(CTX_AGG)) {
+                            skip = true;
+                        } else {
+                            i = dec(CTX_UNI) << 1;
+                            i |= dec(CTX_UNI);
+                            partial = true;
+                        }
+                    }
+                    if (!skip) {
+                        for (; i < nr; ++i) {
+                            if (!partial) {
+                                if (((Wc >> (1 + i)) & 1u) || ((Wc >> (SW_PI + i)) & 1u)) continue;
+                                const uint32_t zi = zidx(i);
+                                if (!dec(CTX_ZC + ((srl(ZCL, zi >> 3) >> (4 * (zi & 7))) & 15u))) continue;
+                            }
+                            partial = false;
+                            sign(i);
+                        }
+                    }
+                    Wc &= ~(15u << SW_PI);
+                }
+                W = swl(W, Wc, x);
+                Wl = Wc; Wc = Wr; Wr = Wn;
+            }
+            // the stripe's rows back into the columns
+            const uint64_t m = ~((uint64_t)15 << y0);
+            const uint32_t nb = ((W >> 9) & 1u) | ((W >> 10) & 2u) | ((W >> 11) & 4u) | ((W >> 12) & 8u);
+            SG = (SG & m) | ((uint64_t)((W >> 1) & 15u) << y0);
+            NG = (NG & m) | ((uint64_t)nb << y0);
+            PI = (PI & m) | ((uint64_t)((W >> SW_PI) & 15u) << y0);
+            MU = (MU & m) | ((uint64_t)((W >> SW_MU) & 15u) << y0);
+            BT = (BT & m) | ((uint64_t)((W >> SW_BT) & 15u) << y0);
+        }
+        if (t == 2) {
+            flush_plane(k);
+            BT = 0;
+            ++k;
+            t = 0;
+        } else {
+            ++t;
+        }
+    }
+    if (t != 0 && k < numbps) flush_plane(k);   // a plane left after SP or MR
+    // sign rows (where significant) in the stripe lines
+    const uint64_t nrow = rows_of(NG, h, lane);
+    if ((uint32_t)lane < h) WS[16 * (lane >> 2) + WS_N + (lane & 3)] = nrow;
+    if (STATS && lane == 0) {
+        atomicAdd(&stats[13], (unsigned long long)ndec);
+        atomicMax(&stats[14], (unsigned long long)ndec);
+    }
+}
+
 // TIMING (diagnostic build, GK_T1_STATS=2): shader-clock cycles spent in stripe-boundary
 // events vs decision steps, summed into stats[4] / stats[5].
 // MODE 0: decode; 1: also count decisions per lane (GK_T1_STATS); 2: also time events (=2).
@@ -234,13 +489,27 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
                                                 const GkBlock* __restrict__ blocks,
                                                 const uint32_t* __restrict__ order, uint64_t* __restrict__ scratch,
                                                 const uint64_t* __restrict__ wave_off, uint32_t nblocks,
-                                                unsigned long long* __restrict__ stats, uint32_t kpark) {
+                                                unsigned long long* __restrict__ stats, uint32_t kpark,
+                                                uint32_t nsolo) {
     constexpr bool TIMING = MODE == 2, STATS = MODE >= 1;
     __shared__ Dec2Lds Lw[W];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     Dec2Lds& Ls = Lw[wv];
     const uint32_t gw = blockIdx.x * W + wv;          // global wave: 64 slots
     const uint32_t nwaves = (nblocks + 63) / 64;
+    if (gw < nsolo) {   // solo wave: its blocks one after another (nsolo is a whole number of workgroups)
+        // the wave index as a scalar, so everything derived from it stays in SGPRs and branches
+        // stay scalar
+        const uint32_t sgw = (uint32_t)__builtin_amdgcn_readfirstlane((int)gw);
+        const uint64_t lstride = (wave_off[sgw + 1] - wave_off[sgw]) / 64;
+        for (uint32_t i = 0; i < 64; ++i) {
+            const uint32_t bid = order[sgw * 64 + i];
+            if (bid == 0xffffffffu) break;
+            const GkBlock B = blocks[bid];
+            solo_block<STATS>(bytes, B, scratch + wave_off[sgw] + i * lstride, lane, stats);
+        }
+        return;
+    }
     for (int i = lane; i < MQ_PAIRS; i += 64) Ls.tab[i] = mq_pair_entry((uint32_t)i);
     for (int i = lane; i < 2048; i += 64) Ls.zc[i >> 9][i & 511] = zc_rule((uint32_t)(i >> 9), (uint32_t)(i & 511));
     for (int i = lane; i < 256; i += 64)
@@ -815,10 +1084,32 @@ uint32_t gk_t1dec_lanes() {
     }
     return lanes;
 }
-static uint64_t g_last_stats[3] = {0, 0, 0};   // max steps per wave, steps, symbols (GK_T1_STATS)
-void gk_t1dec_stats(uint64_t out[3]) { out[0] = g_last_stats[0]; out[1] = g_last_stats[1]; out[2] = g_last_stats[2]; }
+// max steps per wave, steps, symbols, solo decisions, solo decisions of the busiest solo wave (GK_T1_STATS)
+static uint64_t g_last_stats[5] = {0, 0, 0, 0, 0};
+void gk_t1dec_stats(uint64_t out[5]) { for (int i = 0; i < 5; ++i) out[i] = g_last_stats[i]; }
+// Solo blocks of a decode of nblocks blocks at `lanes` per wave: the spare SIMDs of the chip (4
+// per CU, less the lane-parallel waves), at most a quarter of the blocks; GK_T1DEC_SOLO=n forces
+// n (0: none).  The host gives each its own wave, first in the grid, in a multiple of 12 waves
+// (whole workgroups of 3 or 4).
+uint32_t gk_t1dec_solo_blocks(uint32_t nblocks, uint32_t lanes) {
+    static int ncu = -1, force = -2;
+    if (ncu < 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 0;
+        ncu = n;
+        const char* v = getenv("GK_T1DEC_SOLO");
+        force = v ? atoi(v) : -1;
+    }
+    if (force >= 0) return std::min<uint32_t>((uint32_t)force, nblocks);
+    const uint32_t simds = 4u * (uint32_t)ncu, nw = (nblocks + lanes - 1) / lanes;
+    if (nw + 12 > simds) return 0;
+    const uint32_t k = std::min<uint32_t>({(simds - nw) / 12 * 12, 512u, nblocks / 4});
+    return k;
+}
+
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
-                      uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks) {
+                      uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks, uint32_t nsolo) {
     if (!nblocks) return;
     static unsigned long long* stats = nullptr;
     const char* sv = getenv("GK_T1_STATS");
@@ -849,7 +1140,7 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         const uint32_t ngroups = (nwaves + W - 1) / W;
         const size_t pad = W * sizeof(Dec2Lds) < 163840 ? 163840 - W * sizeof(Dec2Lds) : 0;
         hipLaunchKernelGGL(kern, dim3(ngroups), dim3(64 * W), pad, st, bytes, blocks, order, scratch, wave_off, nblocks,
-                           stp, (uint32_t)kpark);
+                           stp, (uint32_t)kpark, nsolo);
     };
     if (timing)
         launch(k_t1_dec2<2, 4>, 4, stats);
@@ -862,10 +1153,13 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         (void)hipMemcpyAsync(h, stats, 128, hipMemcpyDeviceToHost, st);
         (void)hipStreamSynchronize(st);
         g_last_stats[0] = h[2]; g_last_stats[1] = h[0]; g_last_stats[2] = h[1];
+        g_last_stats[3] = h[13]; g_last_stats[4] = h[14];
         fprintf(stderr, "t1dec stats: waves %u steps_total %llu symbols %llu max_steps %llu avg_steps/wave %.0f lane_eff %.3f events/wave %.0f"
                         " busiest lane %llu decisions in a wave of %llu steps\n",
                 (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]),
                 (double)h[3] / ((nblocks + 63) / 64), h[12] >> 32, h[12] & 0xffffffffull);
+        if (nsolo)
+            fprintf(stderr, "t1dec solo: %u waves, decisions %llu, max per wave %llu\n", nsolo, h[13], h[14]);
         if (timing)
             fprintf(stderr, "t1dec timing: cycles/event %.0f cycles/step %.0f (event share %.3f)\n",
                     (double)h[4] / (double)(h[3] ? h[3] : 1), (double)h[5] / (double)(h[0] ? h[0] : 1),

@@ -99,6 +99,9 @@ typedef struct gk_timings {
     /* Part-1 decode with GK_T1_STATS set in the environment (0 otherwise): decision steps of
        the longest-running wave, all steps issued, symbols decoded (the T1 chain's work) */
     uint64_t t1_steps_max, t1_steps_total, t1_symbols;
+    /* Part-1 decode: code-blocks given to solo waves (one wave per block on the SIMDs the
+       lane-parallel waves leave); with GK_T1_STATS, their decisions and the largest per wave */
+    uint64_t t1_solo_blocks, t1_solo_decisions, t1_solo_decisions_max;
 } gk_timings;
 
 typedef struct gk_ctx gk_ctx;

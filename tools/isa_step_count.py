@@ -21,7 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
-KERNEL = re.compile(r"^[0-9a-f]+ <_Z9k_t1_dec2ILi0EE.*>:")
+KERNEL = re.compile(r"^[0-9a-f]+ <_Z9k_t1_dec2ILi0ELi4EE.*>:")   # k_t1_dec2<0, 4>
 
 
 def _classify(blocks, lines):
@@ -50,7 +50,7 @@ def _summarise(blocks):
 
 
 def count_so(so):
-    """Step count of k_t1_dec2<0> in the built library's gfx950 code object."""
+    """Step count of k_t1_dec2<0, 4> in the built library's gfx950 code object."""
     with tempfile.TemporaryDirectory() as d:
         lib = os.path.join(d, "lib.so")
         with open(so, "rb") as f, open(lib, "wb") as g:
@@ -69,7 +69,7 @@ def count_so(so):
             blocks = []
             _classify(blocks, lines[s + 1:e])
             return _summarise(blocks)
-    raise RuntimeError("k_t1_dec2<0> not found in the gfx950 code objects of " + so)
+    raise RuntimeError("k_t1_dec2<0, 4> not found in the gfx950 code objects of " + so)
 
 
 def count(src):
@@ -78,7 +78,7 @@ def count(src):
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
                                "-I", os.path.dirname(src), src, "-o", out])
         lines = open(out).read().split("\n")
-    s = next(i for i, l in enumerate(lines) if re.match(r"^_Z9k_t1_dec2IL(?:b0|i0)EE.*:", l))
+    s = next(i for i, l in enumerate(lines) if re.match(r"^_Z9k_t1_dec2ILi0ELi4EE.*:", l))
     e = next(i for i in range(s, len(lines)) if lines[i].startswith(".Lfunc_end"))
     blocks = []
     _classify(blocks, lines[s:e])
