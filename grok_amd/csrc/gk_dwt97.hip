@@ -402,12 +402,14 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ 
 
 void gk_launch_dc_ict_fwd(hipStream_t st, int stype, const void* r, const void* g, const void* b, uint32_t sin, float* y,
                           float* u, float* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift) {
+    if (!w || !h) return;   // an empty region (a resolution of zero width or height): no launch
     GK_SAMPLE_DISPATCH(stype, T,
         hipLaunchKernelGGL(k_dc_ict_fwd<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, (const T*)r, (const T*)g,
                            (const T*)b, sin, y, u, v, sout, w, h, shift))
 }
 void gk_launch_dc_fwd_f(hipStream_t st, int stype, const void* in, uint32_t sin, float* out, uint32_t sout, uint32_t w,
                         uint32_t h, int32_t shift) {
+    if (!w || !h) return;   // an empty region (a resolution of zero width or height): no launch
     GK_SAMPLE_DISPATCH(stype, T,
         hipLaunchKernelGGL(k_dc_fwd_f<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, (const T*)in, sin, out, sout, w, h,
                            shift))
@@ -415,12 +417,14 @@ void gk_launch_dc_fwd_f(hipStream_t st, int stype, const void* in, uint32_t sin,
 void gk_launch_ict_inv_dc(hipStream_t st, const float* y, const float* u, const float* v, uint32_t sin, int stype, void* r,
                           void* g, void* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift, int32_t mn,
                           int32_t mx) {
+    if (!w || !h) return;   // an empty region (a resolution of zero width or height): no launch
     GK_SAMPLE_DISPATCH(stype, T,
         hipLaunchKernelGGL(k_ict_inv_dc<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, y, u, v, sin, (T*)r, (T*)g, (T*)b,
                            sout, w, h, shift, mn, mx))
 }
 void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                         uint32_t h, int32_t shift, int32_t mn, int32_t mx) {
+    if (!w || !h) return;   // an empty region (a resolution of zero width or height): no launch
     GK_SAMPLE_DISPATCH(stype, T,
         hipLaunchKernelGGL(k_dc_inv_f<T>, dim3((w + 255) / 256, h), dim3(256), 0, st, in, sin, (T*)out, sout, w, h, shift,
                            mn, mx))
@@ -428,6 +432,7 @@ void gk_launch_dc_inv_f(hipStream_t st, const float* in, uint32_t sin, int stype
 static uint32_t comps_in_grid97(GkTiles tb, GkComps cs) { return tb.count() * cs.n <= 65535u ? cs.n : 1u; }
 void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb, GkComps cs) {
+    if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     const uint32_t ng = comps_in_grid97(tb, cs);
     for (uint32_t c = 0; c < cs.n; c += ng) {
         GkComps g = cs; g.n = ng;
@@ -438,6 +443,7 @@ void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, flo
 }
 void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb, GkComps cs) {
+    if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     const uint32_t ng = comps_in_grid97(tb, cs);
     for (uint32_t c = 0; c < cs.n; c += ng) {
         GkComps g = cs; g.n = ng;
@@ -448,6 +454,7 @@ void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, flo
 }
 void gk_launch_dwt97_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32_t sin, float* dst, uint64_t cstride,
                             uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb, int32_t shift) {
+    if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
     if (nc == 3)
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_fwd_l1<T, 3>), grid, dim3(256), 0, st, in, sin, dst,
@@ -459,6 +466,7 @@ void gk_launch_dwt97_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32
 void gk_launch_dwt97_inv_l1(hipStream_t st, int stype, int nc, const float* src, uint64_t cstride, uint32_t sstride,
                             GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
                             int32_t mn, int32_t mx) {
+    if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
     if (nc == 3)
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_inv_l1<T, 3>), grid, dim3(256), 0, st, src, cstride,

@@ -538,6 +538,7 @@ static int vec_ok(uint32_t es_a, const void* a0, const void* a1, const void* a2,
 }
 void gk_launch_dc_rct_fwd(hipStream_t st, int stype, const void* r, const void* g, const void* b, uint32_t sin,
                           int32_t* y, int32_t* u, int32_t* v, uint32_t sout, uint32_t w, uint32_t h, int32_t shift) {
+    if (!w || !h) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + 1023) / 1024, h);
     const int vec = vec_ok(gk_sample_size(stype), r, g, b, sin, 4, y, u, v, sout);
     GK_SAMPLE_DISPATCH(stype, T,
@@ -546,6 +547,7 @@ void gk_launch_dc_rct_fwd(hipStream_t st, int stype, const void* r, const void* 
 }
 void gk_launch_dc_fwd(hipStream_t st, int stype, const void* in, uint32_t sin, int32_t* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift) {
+    if (!w || !h) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + 255) / 256, h);
     GK_SAMPLE_DISPATCH(stype, T,
         hipLaunchKernelGGL(k_dc_fwd<T>, grid, dim3(256), 0, st, (const T*)in, sin, out, sout, w, h, shift))
@@ -553,6 +555,7 @@ void gk_launch_dc_fwd(hipStream_t st, int stype, const void* in, uint32_t sin, i
 void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, const int32_t* v, uint32_t sin, int stype,
                           void* r, void* g, void* b, uint32_t sout, uint32_t w, uint32_t h, int32_t shift,
                           int32_t mn, int32_t mx) {
+    if (!w || !h) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + 1023) / 1024, h);
     const int vec = vec_ok(4, y, u, v, sin, gk_sample_size(stype), r, g, b, sout);
     GK_SAMPLE_DISPATCH(stype, T,
@@ -561,6 +564,7 @@ void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, co
 }
 void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift, int32_t mn, int32_t mx) {
+    if (!w || !h) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + 255) / 256, h);
     GK_SAMPLE_DISPATCH(stype, T,
         hipLaunchKernelGGL(k_dc_inv<T>, grid, dim3(256), 0, st, in, sin, (T*)out, sout, w, h, shift, mn, mx))
@@ -568,6 +572,7 @@ void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int stype
 static uint32_t comps_in_grid(GkTiles tb, GkComps cs) { return tb.count() * cs.n <= 65535u ? cs.n : 1u; }
 void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb, GkComps cs) {
+    if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     const uint32_t ng = comps_in_grid(tb, cs);   // components per launch
     for (uint32_t c = 0; c < cs.n; c += ng) {
         GkComps g = cs; g.n = ng;
@@ -578,6 +583,7 @@ void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, i
 }
 void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb, GkComps cs) {
+    if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     const uint32_t ng = comps_in_grid(tb, cs);
     for (uint32_t c = 0; c < cs.n; c += ng) {
         GkComps g = cs; g.n = ng;
@@ -588,6 +594,7 @@ void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, i
 }
 void gk_launch_dwt53_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32_t sin, int32_t* dst, uint64_t cstride,
                             uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb, int32_t shift) {
+    if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
     if (nc == 3)
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_fwd_l1<T, 3>), grid, dim3(256), 0, st, in, sin, dst,
@@ -599,6 +606,7 @@ void gk_launch_dwt53_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32
 void gk_launch_dwt53_inv_l1(hipStream_t st, int stype, int nc, const int32_t* src, uint64_t cstride, uint32_t sstride,
                             GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
                             int32_t mn, int32_t mx) {
+    if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
     if (nc == 3)
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_inv_l1<T, 3>), grid, dim3(256), 0, st, src, cstride,

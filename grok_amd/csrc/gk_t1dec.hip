@@ -38,6 +38,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <string>
 
 // per-lane scratch (uint64 words, one contiguous slab per lane, 128-byte aligned).  A stripe's
 // state rows are one 128-byte line: stripe s at 16 s holds significance, sign, visited (SP of the
@@ -233,7 +234,8 @@ __device__ __forceinline__ uint64_t h_get(uint32_t (*g)[64], int row, int lane) 
 // the lane-parallel step's every-case select chain.  The block's state sits in the lanes
 // (lane = column x, bit y = row y): significance, sign, refined, visited-in-SP and the plane's
 // bits, as 64-bit columns.  A stripe-pass packs each column's window into one dword per lane and
-// walks the columns with three of them in SGPRs (left, current, right); a column's word goes
+// walks the columns that have something to code (a ballot per stripe-pass) with three words in
+// SGPRs (left, current, right); a column's word goes
 // back with v_writelane and the stripe's rows are merged into the columns by VALU at its end.
 // Context states, the (state, MPS) pair table and the ZC / SC rule tables live in VGPR lanes
 // and are read with v_readlane.  Output: the plane-bit rows and the sign rows of the lane slab
@@ -265,6 +267,12 @@ __device__ __forceinline__ uint32_t win6(uint64_t v, uint32_t y0) {
 __device__ __forceinline__ uint32_t spread6(uint32_t v) {   // bit j -> bit 2 j
     return (v & 1u) | ((v & 2u) << 1) | ((v & 4u) << 2) | ((v & 8u) << 3) | ((v & 16u) << 4) | ((v & 32u) << 5);
 }
+__device__ __forceinline__ uint32_t solo_prev(uint32_t v) {   // lane - 1's value, 0 at lane 0 (wave_shr:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t solo_next(uint32_t v) {   // lane + 1's value, 0 at lane 63 (wave_shl:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
 // ballot transpose: row y (bit x = lane x's bit y) into lane y of the result
 __device__ __forceinline__ uint64_t rows_of(uint64_t col, uint32_t h, int lane) {
     uint32_t lo = 0, hi = 0;
@@ -276,11 +284,12 @@ __device__ __forceinline__ uint64_t rows_of(uint64_t col, uint32_t h, int lane) 
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <bool STATS>
+template <bool STATS, bool TIMING>
 __device__ void solo_block(const uint8_t* __restrict__ bytes, const GkBlock& B, uint64_t* __restrict__ WS, int lane,
                            unsigned long long* __restrict__ stats) {
     const uint32_t numbps = B.numbps, npasses = B.numbps ? B.npasses : 0;
     if (!npasses) return;
+    const uint64_t t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t w = B.w, h = B.h, ns = (h + 3) >> 2, orient = B.orient & 3;
     // rule tables in lanes: ZC 8 entries of 4 bits per lane, index = left | centre << 3 | right << 6
     // (3 rows each, bit 0 = the row above); SC 4 entries of 8 bits per lane, index = (sig, sign)
@@ -392,9 +401,30 @@ __device__ void solo_block(const uint8_t* __restrict__ bytes, const GkBlock& B, 
             uint32_t W = win6(SG, y0) | (spread6(win6(SG, y0)) << 6) | (spread6(win6(NG, y0)) << 7) |
                          (((uint32_t)(PI >> y0) & 15u) << SW_PI) | (((uint32_t)(MU >> y0) & 15u) << SW_MU) |
                          (((uint32_t)(BT >> y0) & 15u) << SW_BT);
-            uint32_t Wl = 0, Wc = srl(W, 0), Wr = w > 1 ? srl(W, 1) : 0u;
-            for (uint32_t x = 0; x < w; ++x) {
-                const uint32_t Wn = x + 2 < w ? srl(W, x + 2) : 0u;
+            // columns with something to code in this pass (SP: an insignificant sample with a
+            // significant neighbour; MR: a significant sample not coded in SP; CL: an insignificant
+            // sample not coded in SP); SP adds the column right of one that gains a significance
+            uint64_t M;
+            {
+                const uint32_t S6 = W & 0x3fu, PI4 = (W >> SW_PI) & 15u, rows = (1u << nr) - 1u;
+                const uint32_t D = solo_prev(S6) | solo_next(S6);
+                const uint32_t nbr = D | (D >> 1) | (D >> 2) | S6 | (S6 >> 2);
+                const uint32_t ins = ~(S6 >> 1) & rows;
+                const uint32_t cr = t == 0 ? (nbr & ins) : (t == 1 ? ((S6 >> 1) & ~PI4 & rows) : (ins & ~PI4));
+                M = __ballot(cr != 0 && (uint32_t)lane < w);
+            }
+            uint32_t Wl = 0, Wc = 0, Wr = 0, xp = 0xfffffffeu;   // no column before the first
+            while (M) {
+                const uint32_t x = (uint32_t)__builtin_ctzll(M);
+                M &= M - 1;
+                if (x == xp + 1) {
+                    Wl = Wc; Wc = Wr;
+                } else {
+                    Wl = x ? srl(W, x - 1) : 0u;
+                    Wc = srl(W, x);
+                }
+                Wr = x + 1 < w ? srl(W, x + 1) : 0u;
+                const uint32_t sig0 = Wc & 0x1eu;
                 auto zidx = [&](uint32_t i) {
                     return ((Wl >> i) & 7u) | (((Wc >> i) & 7u) << 3) | (((Wr >> i) & 7u) << 6);
                 };
@@ -448,14 +478,16 @@ __device__ void solo_block(const uint8_t* __restrict__ bytes, const GkBlock& B, 
                     Wc &= ~(15u << SW_PI);
                 }
                 W = swl(W, Wc, x);
-                Wl = Wc; Wc = Wr; Wr = Wn;
+                if (t == 0 && (Wc & 0x1eu) != sig0 && x + 1 < w) M |= 2ull << x;
+                xp = x;
             }
             // the stripe's rows back into the columns
             const uint64_t m = ~((uint64_t)15 << y0);
             const uint32_t nb = ((W >> 9) & 1u) | ((W >> 10) & 2u) | ((W >> 11) & 4u) | ((W >> 12) & 8u);
             SG = (SG & m) | ((uint64_t)((W >> 1) & 15u) << y0);
             NG = (NG & m) | ((uint64_t)nb << y0);
-            PI = (PI & m) | ((uint64_t)((W >> SW_PI) & 15u) << y0);
+            // (a cleanup pass clears the visited flags of every column, skipped ones included)
+            PI = (PI & m) | (t == 2 ? 0ull : (uint64_t)((W >> SW_PI) & 15u) << y0);
             MU = (MU & m) | ((uint64_t)((W >> SW_MU) & 15u) << y0);
             BT = (BT & m) | ((uint64_t)((W >> SW_BT) & 15u) << y0);
         }
@@ -475,6 +507,7 @@ __device__ void solo_block(const uint8_t* __restrict__ bytes, const GkBlock& B, 
     if (STATS && lane == 0) {
         atomicAdd(&stats[13], (unsigned long long)ndec);
         atomicMax(&stats[14], (unsigned long long)ndec);
+        if (TIMING) atomicMax(&stats[15], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
     }
 }
 
@@ -506,7 +539,7 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
             const uint32_t bid = order[sgw * 64 + i];
             if (bid == 0xffffffffu) break;
             const GkBlock B = blocks[bid];
-            solo_block<STATS>(bytes, B, scratch + wave_off[sgw] + i * lstride, lane, stats);
+            solo_block<STATS, TIMING>(bytes, B, scratch + wave_off[sgw] + i * lstride, lane, stats);
         }
         return;
     }
@@ -1159,7 +1192,8 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
                 (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]),
                 (double)h[3] / ((nblocks + 63) / 64), h[12] >> 32, h[12] & 0xffffffffull);
         if (nsolo)
-            fprintf(stderr, "t1dec solo: %u waves, decisions %llu, max per wave %llu\n", nsolo, h[13], h[14]);
+            fprintf(stderr, "t1dec solo: %u waves, decisions %llu, max per wave %llu%s\n", nsolo, h[13], h[14],
+                    timing ? (", longest block " + std::to_string(h[15]) + " cycles").c_str() : "");
         if (timing)
             fprintf(stderr, "t1dec timing: cycles/event %.0f cycles/step %.0f (event share %.3f)\n",
                     (double)h[4] / (double)(h[3] ? h[3] : 1), (double)h[5] / (double)(h[0] ? h[0] : 1),
