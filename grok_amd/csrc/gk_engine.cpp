@@ -27,6 +27,7 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+#include <queue>
 
 #include "../../include/grok_amd.h"
 #include "gk_common.h"
@@ -3745,10 +3746,71 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // `L` lanes of each 64-lane wave carry a block (gk_t1dec_lanes): fewer lanes per wave
         // give more waves, so every SIMD of the chip holds waves and can hide latency.
         const uint32_t L = gk_t1dec_lanes();
-        // the heaviest blocks (most compressed bytes: decisions follow the bytes closely) go to
-        // solo waves, one block each, first in the grid (gk_t1dec.hip, solo_block)
-        const uint32_t nsb = nbr ? gk_t1dec_solo_blocks(nbr, L) : 0;
-        const uint32_t nsw = (nsb + 11) / 12 * 12;
+        // The heaviest blocks go to solo waves (gk_t1dec.hip solo_block) on the SIMDs the
+        // lane-parallel waves leave.  Weight = compressed bytes (decisions follow them within
+        // ~10 %).  K, the number of solo blocks, balances the two sides: the lane-parallel
+        // waves last as long as the heaviest block left to them (weight w[K]), a solo wave as
+        // long as its blocks' sum / ratio; the top K are packed longest-first into the solo
+        // waves (LPT) and K is the crossing point of the two (binary search: the first falls,
+        // the second grows with K).  GK_T1DEC_SOLO=n: the n heaviest, one per wave.
+        const GkSoloPlan sp = nbr ? gk_t1dec_solo_plan(nbr, L) : GkSoloPlan{0, -1, 1.f};
+        uint32_t nsb = 0;
+        std::vector<uint32_t> byl;
+        std::vector<std::vector<uint32_t>> bins;
+        auto weight = [&](uint32_t q) -> uint64_t { return blk[q].npasses ? blk[q].len : 0; };
+        if (sp.waves) {
+            // (at most 4 blocks per solo wave: the search stays a fraction of a millisecond of host time)
+            const uint32_t kmax = sp.forced >= 0 ? (uint32_t)sp.forced : std::min<uint32_t>(nbr / 4, 4u * sp.waves);
+            byl.resize(nbr);
+            for (uint32_t q = 0; q < nbr; ++q) byl[q] = q;
+            auto heavier = [&](uint32_t x, uint32_t y) { return weight(x) != weight(y) ? weight(x) > weight(y) : x < y; };
+            const uint32_t top = std::min<uint32_t>(kmax + 1, nbr);
+            if (top) {
+                std::nth_element(byl.begin(), byl.begin() + (top - 1), byl.end(), heavier);
+                std::sort(byl.begin(), byl.begin() + top, heavier);
+            }
+            // longest-first packing of the k heaviest into the solo waves; returns the largest load
+            auto pack = [&](uint32_t k, std::vector<std::vector<uint32_t>>* out) -> uint64_t {
+                std::vector<uint64_t> load(sp.waves, 0);
+                std::vector<uint32_t> cnt(sp.waves, 0);
+                if (out) out->assign(sp.waves, {});
+                using E = std::pair<uint64_t, uint32_t>;
+                std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
+                for (uint32_t b = 0; b < sp.waves; ++b) pq.push({0, b});
+                uint64_t mx = 0;
+                for (uint32_t j = 0; j < k && !pq.empty(); ++j) {
+                    const E e = pq.top();
+                    pq.pop();
+                    load[e.second] = e.first + weight(byl[j]);
+                    mx = std::max(mx, load[e.second]);
+                    if (out) (*out)[e.second].push_back(byl[j]);
+                    if (++cnt[e.second] < 64) pq.push({load[e.second], e.second});
+                }
+                return mx;
+            };
+            uint32_t k = 0;
+            if (sp.forced >= 0) {
+                k = (uint32_t)sp.forced;
+                bins.assign(sp.waves, {});
+                for (uint32_t j = 0; j < k; ++j) bins[j].push_back(byl[j]);
+            } else {
+                auto lane_side = [&](uint32_t kk) -> double { return kk < nbr ? (double)weight(byl[kk]) : 0.0; };
+                auto solo_side = [&](uint32_t kk) -> double { return (double)pack(kk, nullptr) / sp.ratio; };
+                uint32_t lo = 0, hi = kmax;   // first k with solo_side(k) >= lane_side(k)
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) / 2;
+                    if (solo_side(mid) >= lane_side(mid)) hi = mid; else lo = mid + 1;
+                }
+                k = lo;
+                if (k > 0 && std::max(solo_side(k - 1), lane_side(k - 1)) <= std::max(solo_side(k), lane_side(k))) --k;
+                if (k) pack(k, &bins);
+            }
+            nsb = k;
+        }
+        uint32_t nsw = 0;   // solo waves holding a block, rounded up to whole workgroups of 12
+        for (uint32_t b = 0; b < bins.size(); ++b)
+            if (!bins[b].empty()) nsw = b + 1;
+        nsw = (nsw + 11) / 12 * 12;
         const uint32_t nw = nsw + (nbr - nsb + L - 1) / L, nslots = nw * 64;
         uint32_t* hord = (uint32_t*)ctx->hord.get(4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
         uint32_t* hpos = hord + nslots;               // slot of block k
@@ -3757,21 +3819,12 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         {
             std::fill(hord, hord + nslots, 0xffffffffu);
             std::vector<uint8_t> solo(nbr, 0);
-            if (nsb) {
-                std::vector<uint32_t> byl(nbr);
-                for (uint32_t q = 0; q < nbr; ++q) byl[q] = q;
-                auto heavier = [&](uint32_t x, uint32_t y) {
-                    const uint32_t lx = blk[x].npasses ? blk[x].len : 0, ly = blk[y].npasses ? blk[y].len : 0;
-                    return lx != ly ? lx > ly : x < y;
-                };
-                std::nth_element(byl.begin(), byl.begin() + (nsb - 1), byl.end(), heavier);
-                std::sort(byl.begin(), byl.begin() + nsb, heavier);
-                for (uint32_t j = 0; j < nsb; ++j) {
-                    const uint32_t q = byl[j];
+            for (uint32_t b = 0; b < bins.size() && b < nsw; ++b)
+                for (uint32_t i = 0; i < bins[b].size(); ++i) {
+                    const uint32_t q = bins[b][i];
                     solo[q] = 1;
-                    hord[(size_t)j * 64] = q; hpos[q] = j * 64;
+                    hord[(size_t)b * 64 + i] = q; hpos[q] = b * 64 + i;
                 }
-            }
             std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
             for (uint32_t q = 0; q < nbr; ++q)
                 if (!solo[q]) cnt[std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1)]++;
@@ -3790,7 +3843,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             for (uint32_t wv = 0; wv < nw; ++wv) {
                 hwo[wv] = wo;
                 uint32_t mp = 0;
-                for (uint32_t i = wv * 64; i < wv * 64 + (wv < nsw ? 1 : L); ++i)
+                for (uint32_t i = wv * 64; i < wv * 64 + (wv < nsw ? 64 : L); ++i)
                     if (hord[i] != 0xffffffffu) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
                 if (wv < nsw && hord[wv * 64] == 0xffffffffu) continue;   // a solo wave without a block
                 wo += (272 + (uint64_t)mp * 64) * 64;   // per-lane slab: WS_FIXED + planes (gk_t1dec.hip), 128 B lines

@@ -51,8 +51,10 @@ uint32_t gk_t1dec_lanes();
 // counters of the last k_t1_dec2 launch made with GK_T1_STATS set: max steps per wave, steps,
 // symbols (lane-parallel waves), decisions of the solo waves and of the busiest one
 void gk_t1dec_stats(uint64_t out[5]);
-// blocks decoded by solo waves (one wave per block, on the SIMDs the lane-parallel waves leave)
-uint32_t gk_t1dec_solo_blocks(uint32_t nblocks, uint32_t lanes);
+// solo waves (gk_t1dec.hip solo_block) for a decode: how many the spare SIMDs hold (a multiple
+// of 12), a forced block count (one per wave; -1: the host packs), the host's cost ratio
+struct GkSoloPlan { uint32_t waves; int forced; float ratio; };
+GkSoloPlan gk_t1dec_solo_plan(uint32_t nblocks, uint32_t lanes);
 // the first nsolo waves of `order` are solo waves (a multiple of 12)
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
                       uint64_t* scratch, const uint64_t* wave_off, uint32_t nblocks, uint32_t nsolo);

@@ -284,12 +284,11 @@ __device__ __forceinline__ uint64_t rows_of(uint64_t col, uint32_t h, int lane) 
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <bool STATS, bool TIMING>
-__device__ void solo_block(const uint8_t* __restrict__ bytes, const GkBlock& B, uint64_t* __restrict__ WS, int lane,
-                           unsigned long long* __restrict__ stats) {
+// returns the decisions decoded (counted when STATS)
+template <bool STATS>
+__device__ uint32_t solo_block(const uint8_t* __restrict__ bytes, const GkBlock& B, uint64_t* __restrict__ WS, int lane) {
     const uint32_t numbps = B.numbps, npasses = B.numbps ? B.npasses : 0;
-    if (!npasses) return;
-    const uint64_t t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    if (!npasses) return 0;
     const uint32_t w = B.w, h = B.h, ns = (h + 3) >> 2, orient = B.orient & 3;
     // rule tables in lanes: ZC 8 entries of 4 bits per lane, index = left | centre << 3 | right << 6
     // (3 rows each, bit 0 = the row above); SC 4 entries of 8 bits per lane, index = (sig, sign)
@@ -504,11 +503,7 @@ __device__ void solo_block(const uint8_t* __restrict__ bytes, const GkBlock& B, 
     // sign rows (where significant) in the stripe lines
     const uint64_t nrow = rows_of(NG, h, lane);
     if ((uint32_t)lane < h) WS[16 * (lane >> 2) + WS_N + (lane & 3)] = nrow;
-    if (STATS && lane == 0) {
-        atomicAdd(&stats[13], (unsigned long long)ndec);
-        atomicMax(&stats[14], (unsigned long long)ndec);
-        if (TIMING) atomicMax(&stats[15], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
-    }
+    return ndec;
 }
 
 // TIMING (diagnostic build, GK_T1_STATS=2): shader-clock cycles spent in stripe-boundary
@@ -535,11 +530,24 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
         // stay scalar
         const uint32_t sgw = (uint32_t)__builtin_amdgcn_readfirstlane((int)gw);
         const uint64_t lstride = (wave_off[sgw + 1] - wave_off[sgw]) / 64;
+        const uint64_t t0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
+        uint32_t nd = 0;
         for (uint32_t i = 0; i < 64; ++i) {
             const uint32_t bid = order[sgw * 64 + i];
             if (bid == 0xffffffffu) break;
             const GkBlock B = blocks[bid];
-            solo_block<STATS, TIMING>(bytes, B, scratch + wave_off[sgw] + i * lstride, lane, stats);
+            nd += solo_block<STATS>(bytes, B, scratch + wave_off[sgw] + i * lstride, lane);
+        }
+        // solo counters: decisions (all waves, busiest wave), cycles (all waves, longest wave
+        // with its decisions: cycles << 20 | decisions)
+        if (STATS && lane == 0 && nd) {
+            atomicAdd(&stats[13], (unsigned long long)nd);
+            atomicMax(&stats[14], (unsigned long long)nd);
+            if (TIMING) {
+                const uint64_t cyc = __builtin_amdgcn_s_memtime() - t0;
+                atomicAdd(&stats[16], (unsigned long long)cyc);
+                atomicMax(&stats[15], (unsigned long long)((cyc << 20) | min(nd, 0xfffffu)));
+            }
         }
         return;
     }
@@ -1120,12 +1128,14 @@ uint32_t gk_t1dec_lanes() {
 // max steps per wave, steps, symbols, solo decisions, solo decisions of the busiest solo wave (GK_T1_STATS)
 static uint64_t g_last_stats[5] = {0, 0, 0, 0, 0};
 void gk_t1dec_stats(uint64_t out[5]) { for (int i = 0; i < 5; ++i) out[i] = g_last_stats[i]; }
-// Solo blocks of a decode of nblocks blocks at `lanes` per wave: the spare SIMDs of the chip (4
-// per CU, less the lane-parallel waves), at most a quarter of the blocks; GK_T1DEC_SOLO=n forces
-// n (0: none).  The host gives each its own wave, first in the grid, in a multiple of 12 waves
-// (whole workgroups of 3 or 4).
-uint32_t gk_t1dec_solo_blocks(uint32_t nblocks, uint32_t lanes) {
+// Solo waves for a decode of nblocks blocks at `lanes` per wave: the SIMDs the lane-parallel
+// waves leave (4 per CU), in whole workgroups of 12 waves (3 or 4 per group), at most 512.
+// GK_T1DEC_SOLO=n forces n solo blocks, one per wave (0: none); GK_T1DEC_SOLO_R sets the cost
+// ratio the host packs with (gk_engine.cpp: a lane-parallel wave's cycles per decision of its
+// busiest lane over a solo wave's cycles per decision; C2 measured ~1,675 / 572).
+GkSoloPlan gk_t1dec_solo_plan(uint32_t nblocks, uint32_t lanes) {
     static int ncu = -1, force = -2;
+    static float ratio = 2.5f;
     if (ncu < 0) {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1133,12 +1143,18 @@ uint32_t gk_t1dec_solo_blocks(uint32_t nblocks, uint32_t lanes) {
         ncu = n;
         const char* v = getenv("GK_T1DEC_SOLO");
         force = v ? atoi(v) : -1;
+        if (const char* r = getenv("GK_T1DEC_SOLO_R")) ratio = (float)atof(r);
     }
-    if (force >= 0) return std::min<uint32_t>((uint32_t)force, nblocks);
+    GkSoloPlan sp{0, -1, ratio};
+    if (force >= 0) {
+        sp.forced = (int)std::min<uint32_t>((uint32_t)force, nblocks);
+        sp.waves = ((uint32_t)sp.forced + 11) / 12 * 12;
+        return sp;
+    }
     const uint32_t simds = 4u * (uint32_t)ncu, nw = (nblocks + lanes - 1) / lanes;
-    if (nw + 12 > simds) return 0;
-    const uint32_t k = std::min<uint32_t>({(simds - nw) / 12 * 12, 512u, nblocks / 4});
-    return k;
+    if (nw + 12 > simds || nblocks < 8) return sp;
+    sp.waves = std::min<uint32_t>((simds - nw) / 12 * 12, 512u);
+    return sp;
 }
 
 void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* order,
@@ -1147,8 +1163,8 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     static unsigned long long* stats = nullptr;
     const char* sv = getenv("GK_T1_STATS");
     const bool want = sv != nullptr, timing = sv && atoi(sv) == 2;
-    if (want && !stats) { (void)hipMalloc(&stats, 128); }
-    if (want) (void)hipMemsetAsync(stats, 0, 128, st);
+    if (want && !stats) { (void)hipMalloc(&stats, 256); }
+    if (want) (void)hipMemsetAsync(stats, 0, 256, st);
     static int kpark = -1;
     if (kpark < 0) {
         const char* kp = getenv("GK_T1DEC_PARK");   // parked lanes that trigger a stripe boundary
@@ -1182,8 +1198,8 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
     else
         wpg == 3 ? launch(k_t1_dec2<0, 3>, 3, nullptr) : launch(k_t1_dec2<0, 4>, 4, nullptr);
     if (want) {
-        unsigned long long h[16];
-        (void)hipMemcpyAsync(h, stats, 128, hipMemcpyDeviceToHost, st);
+        unsigned long long h[32];
+        (void)hipMemcpyAsync(h, stats, 256, hipMemcpyDeviceToHost, st);
         (void)hipStreamSynchronize(st);
         g_last_stats[0] = h[2]; g_last_stats[1] = h[0]; g_last_stats[2] = h[1];
         g_last_stats[3] = h[13]; g_last_stats[4] = h[14];
@@ -1193,7 +1209,9 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
                 (double)h[3] / ((nblocks + 63) / 64), h[12] >> 32, h[12] & 0xffffffffull);
         if (nsolo)
             fprintf(stderr, "t1dec solo: %u waves, decisions %llu, max per wave %llu%s\n", nsolo, h[13], h[14],
-                    timing ? (", longest block " + std::to_string(h[15]) + " cycles").c_str() : "");
+                    timing ? (", cycles/decision " + std::to_string((double)h[16] / (double)(h[13] ? h[13] : 1)) +
+                              ", longest wave " + std::to_string(h[15] >> 20) + " cycles for " +
+                              std::to_string(h[15] & 0xfffff) + " decisions").c_str() : "");
         if (timing)
             fprintf(stderr, "t1dec timing: cycles/event %.0f cycles/step %.0f (event share %.3f)\n",
                     (double)h[4] / (double)(h[3] ? h[3] : 1), (double)h[5] / (double)(h[0] ? h[0] : 1),
