@@ -674,7 +674,8 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
     // the lane with the most stripe-passes left (the wave lasts as long as it does), wave-uniform
     auto critical_lane = [&]() -> uint32_t {
         // work left: stripe-passes (default), compressed bytes (GK_T1DEC_CRIT=2) or 8 x bytes +
-        // 4 x stripe-passes (GK_T1DEC_CRIT=3); kpark bits 10-11
+        // 4 x stripe-passes (GK_T1DEC_CRIT=3); kpark bits 10-11.  C2 max steps per wave:
+        // 32,136 / 34,128 / 33,900 (round 4, with solo waves)
         const uint32_t sp = (npasses - pidx) * ns - s, nb = q.len > q.bp ? q.len - q.bp : 0u;
         const uint32_t mode = (kpark >> 10) & 3;
         const uint32_t rem = done ? 0u : min(mode == 0 ? sp : (mode == 1 ? nb : 8 * nb + 4 * sp), 0x3ffffffu);
@@ -1177,13 +1178,6 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         const char* km = getenv("GK_T1DEC_MID");
         if (!km || atoi(km)) kpark |= 0x200;
     }
-    // waves per workgroup (GK_T1DEC_WPG, 3 or 4): 3 spreads up to 3 x 256 waves one CU each with a
-    // SIMD spare, 4 packs them onto fewer CUs
-    static int wpg = -1;
-    if (wpg < 0) {
-        const char* v = getenv("GK_T1DEC_WPG");
-        wpg = (v && atoi(v) == 3) ? 3 : 4;
-    }
     const uint32_t nwaves = (nblocks + 63) / 64;
     auto launch = [&](auto kern, uint32_t W, unsigned long long* stp) {
         const uint32_t ngroups = (nwaves + W - 1) / W;
@@ -1191,12 +1185,14 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
         hipLaunchKernelGGL(kern, dim3(ngroups), dim3(64 * W), pad, st, bytes, blocks, order, scratch, wave_off, nblocks,
                            stp, (uint32_t)kpark, nsolo);
     };
+    // four waves per workgroup (three per group was measured: C2 decode 20.5 -> 31.9 ms, the
+    // groups no longer fit one per CU next to the solo waves' groups)
     if (timing)
         launch(k_t1_dec2<2, 4>, 4, stats);
     else if (want)
-        wpg == 3 ? launch(k_t1_dec2<1, 3>, 3, stats) : launch(k_t1_dec2<1, 4>, 4, stats);
+        launch(k_t1_dec2<1, 4>, 4, stats);
     else
-        wpg == 3 ? launch(k_t1_dec2<0, 3>, 3, nullptr) : launch(k_t1_dec2<0, 4>, 4, nullptr);
+        launch(k_t1_dec2<0, 4>, 4, nullptr);
     if (want) {
         unsigned long long h[32];
         (void)hipMemcpyAsync(h, stats, 256, hipMemcpyDeviceToHost, st);
