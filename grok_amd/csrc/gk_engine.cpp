@@ -28,6 +28,7 @@
 #include <unordered_map>
 #include <vector>
 #include <queue>
+#include <map>
 
 #include "../../include/grok_amd.h"
 #include "gk_common.h"
@@ -54,6 +55,18 @@ static void launch_check(int line) {
     if (e != hipSuccess)
         throw GkError("kernel launch before gk_engine.cpp:" + std::to_string(line) + ": " + hipGetErrorString(e));
 }
+
+// Engines alive per device in this process.  Solo T1 waves use the SIMDs a decode leaves idle;
+// when several engines share a device their kernels overlap and no SIMD is idle, so solo waves
+// only stretch the tail (C2 with two images in flight: 2,555 -> 2,394 Mpix/s with them).
+static std::mutex g_dev_mu;
+static std::map<int, int> g_dev_engines;
+static int engines_on(int dev) {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    auto it = g_dev_engines.find(dev);
+    return it == g_dev_engines.end() ? 0 : it->second;
+}
+
 
 // Persistent host worker pool for the T2 stages (tiles, precinct chains, blocks).
 // run(n, f) calls f(0..n-1) across the workers and the caller, and returns when all
@@ -2100,6 +2113,7 @@ struct gk_ctx {
     uint32_t dec_layers = 0;   // quality layers to decode (0 = all; grk_dparameters::cp_layer)
     uint32_t dec_reduce = 0;   // highest resolutions discarded on decode (grk_dparameters::cp_reduce)
     int device = 0;
+    bool registered = false;   // counted in g_dev_engines
     hipStream_t st = nullptr;
     hipStream_t aux[3] = {nullptr, nullptr, nullptr};   // encode T1: MQ chunks overlapping context modelling
     hipEvent_t xev[6];
@@ -3753,7 +3767,8 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // long as its blocks' sum / ratio; the top K are packed longest-first into the solo
         // waves (LPT) and K is the crossing point of the two (binary search: the first falls,
         // the second grows with K).  GK_T1DEC_SOLO=n: the n heaviest, one per wave.
-        const GkSoloPlan sp = nbr ? gk_t1dec_solo_plan(nbr, L) : GkSoloPlan{0, -1, 1.f};
+        GkSoloPlan sp = nbr ? gk_t1dec_solo_plan(nbr, L) : GkSoloPlan{0, -1, 1.f};
+        if (sp.forced < 0 && engines_on(ctx->device) > 1) sp.waves = 0;   // the device is shared
         uint32_t nsb = 0;
         std::vector<uint32_t> byl;
         std::vector<std::vector<uint32_t>> bins;
@@ -4047,11 +4062,20 @@ gk_ctx* gk_create(int device_id) {
         gk_destroy(ctx);
         return nullptr;
     }
+    {
+        std::lock_guard<std::mutex> g(g_dev_mu);
+        ++g_dev_engines[device_id];
+        ctx->registered = true;
+    }
     return ctx;
 }
 
 void gk_destroy(gk_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->registered) {
+        std::lock_guard<std::mutex> g(g_dev_mu);
+        if (--g_dev_engines[ctx->device] <= 0) g_dev_engines.erase(ctx->device);
+    }
     (void)hipSetDevice(ctx->device);
     if (ctx->st) (void)hipStreamSynchronize(ctx->st);
     for (auto& a : ctx->aux)
