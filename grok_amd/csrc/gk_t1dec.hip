@@ -1010,7 +1010,9 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
         for (int us = 0; us < T1DEC_UNROLL / 2; ++us) step();
         // half-way through the group: when the lane with the most work left has parked, the group
         // ends here and its boundary event runs now (that lane used to wait for the group's end,
-        // ~6 steps per stripe-pass, ~8 % of its wave's steps); kpark bit 9
+        // ~6 steps per stripe-pass, ~8 % of its wave's steps); kpark bit 9.  Tests at every
+        // quarter were measured in round 4: 32,136 -> 32,049 steps but 20.5 -> 21.1 ms (the two
+        // extra tests and the broken-up unrolled body cost more than the steps saved)
         if (!((kpark >> 9) & 1) || __builtin_amdgcn_readlane((int)parkm, (int)crit_lane) == 0) {
 #pragma unroll
             for (int us = T1DEC_UNROLL / 2; us < T1DEC_UNROLL; ++us) step();

@@ -12,7 +12,7 @@ cp -r include "$T/"
 cp grok_amd/csrc/* "$T/grok_amd/csrc/"
 cp "$REPL" "$T/grok_amd/csrc/$NAME"
 cd "$T/grok_amd/csrc"
-SRCS="gk_kernels.hip gk_dwt97.hip gk_t1enc.hip gk_t1dec.hip gk_t1ms.hip gk_ht.hip gk_engine.cpp grk_shim.cpp"
+SRCS="gk_kernels.hip gk_dwt97.hip gk_dwt_any.hip gk_t1enc.hip gk_t1dec.hip gk_t1ms.hip gk_ht.hip gk_engine.cpp grk_shim.cpp"
 for f in $SRCS; do
     hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -c $f -o ${f%.*}.o &
 done
