@@ -150,6 +150,34 @@ def cpu_baseline(nthreads):
                                              "single-precinct 8K streams)", **GROK_CPU}}
 
 
+def ht_issue_roofline(stages, config="C4"):
+    """Issue roofline of the HTJ2K coders (one lane per code-block, branchy per-lane chains):
+    instructions issued per wave (VALU + SALU + LDS) from the newest committed SQ counter summary
+    of this config (profiles/rNN_<config>_sq.json, tools/sq_counters.sh + tools/sq_summary.py),
+    times 4 cycles (a lone wave issues one instruction per 4 cycles), times the waves a SIMD
+    holds (ceil(waves / 1,024)), over the live coder time.  None if no summary exists."""
+    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "*_sq.json"))
+                    if os.path.basename(f).lower().endswith("_%s_sq.json" % config.lower())),
+                   key=lambda p: os.path.basename(p).lower())
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    out = {}
+    for kern, ms_key in (("k_ht_dec", "dec_t1_coder_ms"), ("k_ht_enc", "enc_t1_coder_ms")):
+        if kern not in d or not stages.get(ms_key):
+            continue
+        k = d[kern]
+        insts = sum(k["insts_per_wave"].get(t, 0.0) for t in ("valu", "salu", "lds"))
+        per_simd = -(-int(k["waves"]) // 1024)
+        floor_ms = per_simd * insts * 4 / (CLOCK_GHZ * 1e6)
+        out[kern] = {"bound": "instruction issue of the longest chain (one lane per block)",
+                     "instructions_per_wave": round(insts), "waves": int(k["waves"]), "waves_per_simd": per_simd,
+                     "floor_ms": round(floor_ms, 3), "measured_ms": round(stages[ms_key], 3),
+                     "frac": round(floor_ms / stages[ms_key], 3),
+                     "wait_any": round(k["wait_any"], 3), "source": os.path.basename(files[-1])}
+    return out or None
+
+
 def pmc_traffic(kernels, config="C2"):
     """HBM bytes per launch of `kernels` from the newest committed PMC summary of this config
     (profiles/rNN_<config>_pmc.json, written by tools/pmc_summary.py from rocprofv3 --pmc
@@ -544,7 +572,8 @@ def main():
                      if world > 1 else "1 GPU, all 256 tiles batched",
                      "scaling": "strong",
                      "stages_ms": {k: round(v, 3) for k, v in m4.items() if k.endswith("_ms") and v > 0},
-                     "t1_blocks": int(m4.get("enc_t1_blocks", 0))}
+                     "t1_blocks": int(m4.get("enc_t1_blocks", 0)),
+                     "issue_roofline": ht_issue_roofline(m4)}
         r4.close()
         del r4
         torch.cuda.empty_cache()
@@ -620,6 +649,8 @@ def main():
                    "enc_blocks_per_s": round(m["enc_t1_blocks"] / (m["enc_t1_ms"] / 1e3)),
                    "dec_blocks_per_s": round(m["dec_t1_blocks"] / (m["dec_t1_ms"] / 1e3))},
         }
+        if cp.get("cblk_sty"):   # HTJ2K coders: issue roofline from the committed SQ counter summary
+            res["issue_roofline"] = ht_issue_roofline(m, args.config)
         if dec_steps and dec_steps[0]:
             # issue roofline of the chain-bound decoder: one wave per SIMD issues one instruction
             # per 4 cycles, so the kernel takes at least (steps of its longest wave) x
