@@ -61,7 +61,7 @@
 // At the end of every step each lane reads the 4 bytes at its position (nb4).
 #define RING_DW 32
 #ifndef T1DEC_UNROLL
-#define T1DEC_UNROLL 12   // decision steps per stripe-boundary test (C2 decoder: 1 -> 33.5 ms, 8 -> 26.4, 12 -> 25.8, 16 -> 26.3)
+#define T1DEC_UNROLL 16   // decision steps per stripe-boundary test (round 2, C2 decoder: 1 -> 33.5 ms, 8 -> 26.4, 12 -> 25.8, 16 -> 26.3; round 4 with solo waves: 10 -> 20.6, 12 -> 20.5, 16 -> 20.3, 20 -> 20.2-20.3, 24 -> 20.4)
 #endif
 __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
     // per-lane select; a plain ternary lets the compiler keep c as the compare's lane mask (an
