@@ -891,8 +891,13 @@ static void order_ranges(const Plan& P, const TileG& T, uint32_t prog, uint32_t 
 // A.6.6; PacketIter over the tile's progressions, each packet at most once: update_include)
 // the concatenation of every entry's progression over its ranges, clamped to the stream's
 // layers / resolutions / components, skipping packets an earlier entry already emitted.
+// entry (optional) receives per packet the emitting entry and the packet's position in the
+// entries' concatenated sequences, skipped packets counted: Grok's final pass runs each
+// entry's iterator afresh, skips a packet written before through the tile's packet tracker
+// (T2Compress.cpp:46-54, 278-280) and still counts it in tile->numProcessedPackets (SOP's Nsop).
 static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32_t L,
-                                           const std::vector<Poc>* pocs = nullptr) {
+                                           const std::vector<Poc>* pocs = nullptr,
+                                           std::vector<uint32_t>* entry = nullptr) {
     std::vector<PacketRef> out;
     if (!pocs || pocs->empty()) {
         order_ranges(P, T, P.p.prog, L, 0, P.p.numres, 0, P.nc, out);
@@ -904,16 +909,20 @@ static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32
         for (uint32_t r = 0; r < P.p.numres; ++r) maxprc = std::max(maxprc, T.comps[c].res[r].pw * T.comps[c].res[r].ph);
     std::vector<uint8_t> seen((size_t)P.nc * P.p.numres * maxprc * L, 0);
     std::vector<PacketRef> sub;
-    for (const Poc& q : *pocs) {
+    uint32_t iter = 0;
+    for (uint32_t ei = 0; ei < (uint32_t)pocs->size(); ++ei) {
+        const Poc& q = (*pocs)[ei];
         sub.clear();
         const uint32_t le = std::min(q.lye, L), r1 = std::min(q.re, P.p.numres), c1 = std::min(q.ce, P.nc);
         if (q.rs >= r1 || q.cs >= c1 || !le) continue;
         order_ranges(P, T, q.prog, le, q.rs, r1, q.cs, c1, sub);
         for (const PacketRef& pr : sub) {
             uint8_t& sflag = seen[(((size_t)pr.c * P.p.numres + pr.r) * maxprc + pr.pi) * L + pr.l];
+            const uint32_t it = iter++;
             if (sflag) continue;
             sflag = 1;
             out.push_back(pr);
+            if (entry) { entry->push_back(ei); entry->push_back(it); }
         }
     }
     return out;
@@ -927,6 +936,7 @@ static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32
 // index (P) is refused.  tp_key(pr) = the part of packet pr.
 struct TilePartSplit {
     uint32_t n = 1;
+    bool poc = false;   // one part per progression order change (part = the entry that emits the packet)
     int depth = -1;   // last progression-string position that splits
     const char* prog = "LRCP";
     uint32_t L = 1, R = 1, C = 1;
@@ -945,8 +955,14 @@ static TilePartSplit tile_part_split(const Plan& P) {
     static const char* names[5] = {"LRCP", "RLCP", "RPCL", "PCRL", "CPRL"};
     TilePartSplit S;
     S.prog = names[P.p.prog]; S.L = P.p.nlayers; S.R = P.p.numres; S.C = P.nc;
+    if (!P.p.pocs.empty()) {
+        // CodeStreamCompress::writeTileParts (:902-946): without a divider every progression
+        // is a tile part of its own (getNumTilePartsForProgression returns 1 for each)
+        if (P.p.tp_div) throw GkError("tile-part generation with progression order changes is not supported");
+        S.n = (uint32_t)P.p.pocs.size(); S.poc = true;
+        return S;
+    }
     if (!P.p.tp_div) return S;
-    if (!P.p.pocs.empty()) throw GkError("tile-part generation with progression order changes is not supported");
     for (int j = 0; j < 4; ++j) {
         const char ch = S.prog[j];
         if (ch == 'P') throw GkError("a tile-part divider behind the position index is not supported");
@@ -1148,10 +1164,15 @@ struct T2Enc {
         return true;
     }
 
+    // T2Compress::compressPacketsSimulate (:59-112) walks every packet in the tile's own
+    // progression whatever the progression order changes say: its THRESH_CALC PacketManager
+    // sets each entry's progression to tcp->prg and its ranges to the whole tile
+    // (updateCompressTcpProgressions, PacketManager.cpp:123-125, 565-589) and runs only the first
+    // iterator (pocno = 1 outside Cinema 4K)
     bool simulate(uint32_t max_layers, uint64_t max_bytes) {
         uint64_t budget = max_bytes;
         uint64_t* bp = max_bytes == 0xffffffffull ? nullptr : &budget;
-        for (const PacketRef& pr : packet_order(P, P.tiles[t0], max_layers, &P.p.pocs))   // rate control: one tile
+        for (const PacketRef& pr : packet_order(P, P.tiles[t0], max_layers))   // rate control: one tile
             if (!write_packet(P.tiles[t0].comps[pr.c].res[pr.r], pr.pi, pr.l, bp, nullptr)) return false;
         return true;
     }
@@ -1820,9 +1841,7 @@ struct T2Enc {
             }
             return ld;
         };
-        // (with progression order changes the last packet of a layer's budget test is not
-        // known per chain: every bisection step runs the serial simulation)
-        const bool fast = t1 == t0 + 1 && !getenv("GK_T2_SERIAL_SIM") && P.p.pocs.empty() && !P.p.quality;
+        const bool fast = t1 == t0 + 1 && !getenv("GK_T2_SERIAL_SIM") && !P.p.quality;
         static const bool prof = getenv("GK_PROFILE") != nullptr;
         using clk = std::chrono::steady_clock;
         auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1948,7 +1967,29 @@ struct T2Enc {
 static void put16(std::vector<uint8_t>& o, uint32_t v) { o.push_back((uint8_t)(v >> 8)); o.push_back((uint8_t)v); }
 static void put32(std::vector<uint8_t>& o, uint32_t v) { put16(o, v >> 16); put16(o, v & 0xffff); }
 
-// Main header: SOC SIZ [CAP] COD QCD [TLM] [COM]  (CodeStreamCompress::init_header_writing
+// POC marker (A.6.6, CodeStreamCompress::writePoc :1278-1340): per entry RSpoc, CSpoc (1 or 2
+// bytes), LYEpoc (2), REpoc, CEpoc (1 or 2), Ppoc.  clamp (a tile-part POC): layers /
+// resolutions / components clamped to the tile's, as the main header's writePoc leaves them,
+// and every progression replaced by *clamp (see build_tile_part) unless it is ~0u.
+static void write_poc(std::vector<uint8_t>& o, const std::vector<Poc>& pocs, uint32_t nc, const Plan* clamp,
+                      uint32_t prog = ~0u) {
+    const uint32_t cw = nc <= 256 ? 1 : 2;
+    put16(o, 0xff5f); put16(o, 2 + (uint32_t)pocs.size() * (5 + 2 * cw));
+    for (Poc e : pocs) {
+        if (clamp) {
+            e.lye = std::min(e.lye, clamp->p.nlayers); e.re = std::min(e.re, clamp->p.numres); e.ce = std::min(e.ce, nc);
+            if (prog != ~0u) e.prog = prog;
+        }
+        o.push_back((uint8_t)e.rs);
+        if (cw == 1) o.push_back((uint8_t)e.cs); else put16(o, e.cs);
+        put16(o, e.lye);
+        o.push_back((uint8_t)e.re);
+        if (cw == 1) o.push_back((uint8_t)e.ce); else put16(o, e.ce);
+        o.push_back((uint8_t)e.prog);
+    }
+}
+
+// Main header: SOC SIZ [CAP] COD QCD [TLM] [POC] [RGN] [COM]  (CodeStreamCompress::init_header_writing
 // :822-860; marker writers :1054-1685)
 static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tlm_pos = nullptr) {
     put16(o, 0xff4f);
@@ -2003,6 +2044,9 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
         if (tlm_pos) *tlm_pos = o.size();
         o.insert(o.end(), (size_t)(6 * ne), 0);
     }
+    // POC of tile 0 in the main header (init_header_writing :839-840), entries as given: writePoc
+    // (:1278-1340) writes each before clamping it to the tile's layers / resolutions / components
+    if (!P.p.pocs.empty()) write_poc(o, P.p.pocs, P.nc, nullptr);
     for (uint32_t c = 0; c < P.nc; ++c)   // RGN (CodeStreamCompress::write_regions / write_rgn :746-780, 1397-1410)
         if (P.p.roi(c)) {
             const uint32_t cw = P.nc <= 256 ? 1 : 2;
@@ -2845,15 +2889,18 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         std::vector<uint32_t> chain_at(P.p.numres * P.nc + 1, 0);
         for (uint32_t r = 0, q = 0; r < P.p.numres; ++r)
             for (uint32_t c = 0; c < P.nc; ++c) { chain_at[r * P.nc + c] = q; q += T.comps[c].res[r].pw * T.comps[c].res[r].ph; }
-        for (const PacketRef& pr : packet_order(P, T, L, &P.p.pocs)) {
-                O.pkey.push_back(TPS.key(pr));
+        std::vector<uint32_t> entry;
+        const std::vector<PacketRef> order = packet_order(P, T, L, &P.p.pocs, TPS.poc ? &entry : nullptr);
+        for (size_t oi = 0; oi < order.size(); ++oi) {
+                const PacketRef& pr = order[oi];
+                O.pkey.push_back(TPS.poc ? entry[2 * oi] : TPS.key(pr));
                 const size_t q = chain_at[pr.r * P.nc + pr.c] + pr.pi;
                 const uint32_t l = pr.l;
                 const TileOut& C = co[q];
                 Pk k = C.pk[l];
                 const uint32_t h0 = (uint32_t)O.phdr.size(), s0 = (uint32_t)O.bsegs.size();
                 if (P.p.sop_eph & 2) {   // SOP: FF91, Lsop 4, Nsop = the packet's index in the tile (T2Compress.cpp:286-303)
-                    const uint32_t nsop = (uint32_t)O.pk.size() & 0xffff;
+                    const uint32_t nsop = (TPS.poc ? entry[2 * oi + 1] : (uint32_t)O.pk.size()) & 0xffff;
                     const uint8_t sop[6] = {0xff, 0x91, 0, 4, (uint8_t)(nsop >> 8), (uint8_t)nsop};
                     O.phdr.insert(O.phdr.end(), sop, sop + 6);
                 }
@@ -2876,23 +2923,27 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             O.tp_off.push_back((uint32_t)h0); O.pk_first.push_back((uint32_t)pk0);
             put16(tp, 0xff90); put16(tp, 10); put16(tp, t); put32(tp, 0); tp.push_back((uint8_t)part);
             tp.push_back((uint8_t)TPS.n);
-            if (part == 0 && !P.p.pocs.empty()) {   // POC in the first tile part (CodeStreamCompress::writePoc :1278-1340)
-                const uint32_t cw = P.nc <= 256 ? 1 : 2;
-                put16(tp, 0xff5f); put16(tp, 2 + (uint32_t)P.p.pocs.size() * (5 + 2 * cw));
-                for (const Poc& e : P.p.pocs) {
-                    tp.push_back((uint8_t)e.rs);
-                    if (cw == 1) tp.push_back((uint8_t)e.cs); else put16(tp, e.cs);
-                    put16(tp, e.lye);
-                    tp.push_back((uint8_t)e.re);
-                    if (cw == 1) tp.push_back((uint8_t)e.ce); else put16(tp, e.ce);
-                    tp.push_back((uint8_t)e.prog);
-                }
-            }
+            // POC in the tile's first tile part (writeTilePart :870-875): writePoc writes tile 0's
+            // list (tcp = m_cp.tcps) as the main header's writePoc clamped it, each entry's
+            // progression being what tile 0's last PacketManager left: for tile 0 its own
+            // rate-control simulation (THRESH_CALC: tcp->prg), for later tiles tile 0's final pass
+            // (the given progressions)
+            if (part == 0 && !P.p.pocs.empty()) write_poc(tp, P.p.pocs, P.nc, &P, t == 0 ? P.p.prog : ~0u);
             if (P.p.plt && part == 0) {   // PacketLengthMarkers::write (PacketLengthMarkers.cpp:107-175): Zplt 0, 7-bit groups MSB first
+                // the lengths come from the final simulation (compressPacketSimulate :427-428), so
+                // with progression order changes they are listed in the tile's own progression
+                std::vector<uint32_t> lens;
+                if (!TPS.poc) {
+                    for (const Pk& k : O.pk) lens.push_back(k.len);
+                } else {
+                    const uint32_t ovh = ((P.p.sop_eph & 2) ? 6 : 0) + ((P.p.sop_eph & 4) ? 2 : 0);
+                    for (const PacketRef& pr : packet_order(P, T, L))
+                        lens.push_back(co[chain_at[pr.r * P.nc + pr.c] + pr.pi].pk[pr.l].len + ovh);
+                }
                 std::vector<uint8_t> v;
-                for (const Pk& k : O.pk) {
-                    const int nbits = floorlog2(k.len) + 1, nbytes = (nbits + 6) / 7;
-                    for (int q = nbytes - 1; q >= 0; --q) v.push_back((uint8_t)(((k.len >> (7 * q)) & 0x7F) | (q ? 0x80 : 0)));
+                for (const uint32_t len : lens) {
+                    const int nbits = floorlog2(len) + 1, nbytes = (nbits + 6) / 7;
+                    for (int q = nbytes - 1; q >= 0; --q) v.push_back((uint8_t)(((len >> (7 * q)) & 0x7F) | (q ? 0x80 : 0)));
                 }
                 if (3 + v.size() > 65535) throw GkError("PLT marker overflow (too many packets in one tile)");
                 put16(tp, 0xff58); put16(tp, (uint32_t)(3 + v.size())); tp.push_back(0);
@@ -3006,15 +3057,16 @@ struct TilePart {                  // packet bytes [data, end) of one tile part
     // parts in order); their PLT lengths are appended to plt
     std::vector<std::pair<size_t, size_t>> more;
     uint32_t tpsot = 0;
-    std::vector<Poc> pocs;          // POC in the tile's first tile-part header (overrides the main header's)
+    std::vector<Poc> pocs;          // after merge_tile_parts: the tile's progression order changes (empty: the main header's)
 };
 // POC marker body (A.6.6): per entry RSpoc, CSpoc (1 or 2 bytes), LYEpoc (2), REpoc, CEpoc
-// (1 or 2; 0 = 256 with one byte), Ppoc (CodeStreamDecompress::read_poc)
+// (1 or 2; 0 = 256 with one byte), Ppoc.  Appended to out: CodeStreamDecompress::read_poc
+// (:1148-1231) appends to the tcp's list (:1171-1172), so a tile-part POC extends the main
+// header's list the tile's tcp was copied from (merge_tile_parts).
 template <class Src>
 static void parse_poc(Src& S, size_t s, uint32_t L, uint32_t nc, std::vector<Poc>& out) {
     const uint32_t cw = nc <= 256 ? 1 : 2, esz = 5 + 2 * cw;
     if (L < 2 + esz || (L - 2) % esz) throw GkError("corrupt POC marker");
-    out.clear();
     for (size_t q = s; q + esz <= s + L - 2; q += esz) {
         Poc e;
         e.rs = S.at(q);
@@ -3298,7 +3350,12 @@ static void prefetch_packet_headers(gk_ctx* ctx, ByteSrc& S, const Plan& P, cons
 // win (optional): x0, y0, x1, y1 — decode only the tiles intersecting the window and write
 // the window into comps (whose element 0 is the window's top-left sample).
 // A tile's tile parts in TPsot order become one entry: the first part's range, the others
-// in `more`, PLT lengths concatenated (packets never straddle tile parts, A.4.2).
+// in `more`, PLT lengths concatenated (packets never straddle tile parts, A.4.2).  The tile's
+// progression order changes are the main header's list extended by each part's POC in turn
+// (read_poc appends to the tile's copy of the main tcp, CodeStreamDecompress.cpp:1171-1172;
+// OpenJPEG's opj_j2k_read_poc does the same).  PLT is not used for such a tile: Grok lists its
+// lengths in the tile's own progression, not in the order the packets are written
+// (TileProcessor::pcrdBisectSimple's final simulation, T2Compress.cpp:427-428).
 static void merge_tile_parts(Header& Hd) {
     std::unordered_map<uint32_t, size_t> first;
     std::vector<TilePart> out;
@@ -3314,6 +3371,13 @@ static void merge_tile_parts(Header& Hd) {
         if (TP.tpsot != H.more.size() + 1) throw GkError("tile parts out of order (TPsot)");
         H.more.push_back({TP.data, TP.end});
         H.plt.insert(H.plt.end(), TP.plt.begin(), TP.plt.end());
+        H.pocs.insert(H.pocs.end(), TP.pocs.begin(), TP.pocs.end());
+    }
+    const std::vector<Poc>& main_pocs = Hd.want.p.pocs;
+    for (TilePart& H : out) {
+        if (!H.pocs.empty()) H.pocs.insert(H.pocs.begin(), main_pocs.begin(), main_pocs.end());
+        if (H.pocs.size() > GK_MAXRLVLS) throw GkError("too many progression order changes (read_poc: at most 33)");
+        if (!H.pocs.empty() || !main_pocs.empty()) H.plt.clear();
     }
     Hd.parts.swap(out);
 }

@@ -40,6 +40,8 @@
 #include <algorithm>
 #include <atomic>
 #include <functional>
+#include <map>
+#include <tuple>
 #include <thread>
 
 namespace orc {
@@ -1047,19 +1049,52 @@ static void t1_decode_block(const uint8_t* data, uint32_t len, uint32_t npasses,
 // ----------------------------------------------------------------------------
 struct BitWriter {
     std::vector<uint8_t>* out; uint8_t buf = 0; int ct = 8;
+    // ops (optional): every write() call as (value, bits, whether the caller checks its result),
+    // for replaying the header through Grok's bounded BitIO (GrkSimBitIO below)
+    std::vector<uint64_t>* ops = nullptr;
     void wbyte() { out->push_back(buf); ct = (buf == 0xff) ? 7 : 8; buf = 0; }
     void putbit(uint32_t b) { if (ct == 0) wbyte(); --ct; buf |= (uint8_t)(b << ct); }
-    void write(uint32_t v, int n) { for (int i = n - 1; i >= 0; --i) putbit((v >> i) & 1); }
+    void write(uint32_t v, int n, bool checked = true) {
+        if (ops) ops->push_back((uint64_t)v | ((uint64_t)n << 32) | ((uint64_t)checked << 40));
+        for (int i = n - 1; i >= 0; --i) putbit((v >> i) & 1);
+    }
     void flush() { wbyte(); if (ct == 7) wbyte(); }
-    void commacode(uint32_t n) { for (uint32_t i = 0; i < n; ++i) write(1, 1); write(0, 1); }
+    // BitIO::putcommacode / putnumpasses (BitIO.cpp:144-178) return nothing: the callers never
+    // see a failed write inside them
+    void commacode(uint32_t n) { for (uint32_t i = 0; i < n; ++i) write(1, 1, false); write(0, 1, false); }
     void numpasses(uint32_t n) {
-        if (n == 1) write(0, 1);
-        else if (n == 2) write(2, 2);
-        else if (n <= 5) write(0xc | (n - 3), 4);
-        else if (n <= 36) write(0x1e0 | (n - 6), 9);
-        else if (n <= 164) write(0xff80 | (n - 37), 16);
+        if (n == 1) write(0, 1, false);
+        else if (n == 2) write(2, 2, false);
+        else if (n <= 5) write(0xc | (n - 3), 4, false);
+        else if (n <= 36) write(0x1e0 | (n - 6), 9, false);
+        else if (n <= 164) write(0xff80 | (n - 37), 16, false);
     }
 };
+
+// Grok's bounded BitIO as compressPacketSimulate uses it (BitIO(nullptr, max_bytes, true),
+// BitIO.cpp:24-52, 80-122): writeByte counts a byte and fails when the count reaches buf_len
+// (never when buf_len is 0: the count starts above it), leaving the pending byte and ct as they
+// were; putbit fails when that writeByte fails, and write() returns at the first failed bit,
+// dropping the rest of its value.  A failure inside putcommacode / putnumpasses is ignored, so
+// the header goes on: the next writeByte counts the same byte again (count buf_len + 1 != buf_len
+// succeeds) and nothing fails after it.  Replays a header's write() calls; returns false when a
+// checked write or the flush fails, else the byte count (BitIO::numBytes) in *nbytes.
+struct GrkSimBitIO {
+    uint64_t offset = 0, buf_len; uint8_t buf = 0; int ct = 8;
+    explicit GrkSimBitIO(uint64_t len) : buf_len(len) {}
+    bool write_byte() { ++offset; if (offset == buf_len) return false; ct = buf == 0xff ? 7 : 8; buf = 0; return true; }
+    bool putbit(uint32_t b) { if (ct == 0 && !write_byte()) return false; --ct; buf = (uint8_t)(buf | (b << ct)); return true; }
+    bool write(uint32_t v, int n) { for (int i = n - 1; i >= 0; --i) if (!putbit((v >> i) & 1)) return false; return true; }
+    bool flush() { if (!write_byte()) return false; return ct == 7 ? write_byte() : true; }
+};
+static bool grk_sim_header(const std::vector<uint64_t>& ops, uint64_t buf_len, uint64_t* nbytes) {
+    GrkSimBitIO b(buf_len);
+    for (uint64_t op : ops)
+        if (!b.write((uint32_t)op, (int)((op >> 32) & 0xff)) && (op >> 40)) return false;
+    if (!b.flush()) return false;
+    *nbytes = b.offset;
+    return true;
+}
 struct BitReader {
     const uint8_t* p; size_t len; size_t off = 0; uint8_t buf = 0; int ct = 0;
     void bytein() {
@@ -1177,14 +1212,17 @@ static void tile_rect(const Params& p, uint32_t W, uint32_t H, uint32_t t, uint3
 // Main header: SOC SIZ [CAP] COD QCD [TLM] [COM] (CodeStreamCompress::init_header_writing
 // :822-860).  *tlm_pos receives the offset of the first TLM entry (6 bytes per tile
 // part: Ttlm u16, Ptlm u32; Stlm = 0x60, LengthCache.cpp:437-482), patched later.
-static int tile_parts(const Params& p, uint32_t nc);   // tile parts per tile (below)
+static int tile_parts(const Params& p, uint32_t nc);   // tile parts per tile from the divider (below)
+static int num_parts(const Params& p, uint32_t nc);    // tile parts per tile (divider or POC entries)
 
 // POC marker (A.6.6): RSpoc, CSpoc, LYEpoc (16 bit), REpoc, CEpoc, Ppoc per entry; CSpoc /
-// CEpoc take two bytes when there are more than 256 components, CEpoc 0 means 256.
+// CEpoc take two bytes when there are more than 256 components, CEpoc 0 means 256.  The
+// entries are appended to `out` (CodeStreamDecompress::read_poc :1148-1231 appends to the
+// tcp's list at :1171-1172: a tile-part POC extends the main header's list the tile's tcp
+// was copied from, and a later tile part's POC extends it again).
 static bool read_poc(const uint8_t* s, uint32_t L, uint32_t nc, std::vector<PocE>& out) {
     const uint32_t cw = nc <= 256 ? 1 : 2, esz = 5 + 2 * cw;
     if (L < 2 + esz || (L - 2) % esz) return false;
-    out.clear();
     for (uint32_t q = 0; q + esz <= L - 2; q += esz) {
         const uint8_t* e = s + q;
         PocE v;
@@ -1256,11 +1294,15 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
         for (uint32_t r = 0; r < p.numres; ++r) for (auto& B : c0.res[r].bands) put16(o, (B.expn << 11) | B.mant);
     }
     if (p.tlm) {                                     // TLM (TileLengthMarkers::writeBegin)
-        uint32_t nt = tile_count(p, im.w, im.h) * (uint32_t)std::max(1, tile_parts(p, im.nc));   // entries per tile part
+        uint32_t nt = tile_count(p, im.w, im.h) * (uint32_t)std::max(1, num_parts(p, im.nc));   // entries per tile part
         put16(o, 0xff55); put16(o, 4 + 6 * nt); o.push_back(0); o.push_back(0x60);
         if (tlm_pos) *tlm_pos = o.size();
         o.insert(o.end(), (size_t)6 * nt, 0);
     }
+    // POC of tile 0 in the main header (init_header_writing :839-840), as given: writePoc
+    // (:1278-1340) writes each entry before clamping it to the tile's layers / resolutions /
+    // components; every tile here shares tile 0's list
+    if (!p.pocs.empty()) write_poc(o, p.pocs, im.nc);
     for (uint32_t c = 0; c < im.nc; ++c)            // RGN (CodeStreamCompress::write_rgn :746-780)
         if (p.roi(c)) {
             const uint32_t cw = im.nc <= 256 ? 1 : 2;
@@ -1291,7 +1333,8 @@ struct PktRef { uint32_t l, r, c, pi; };
 static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uint32_t prog, uint32_t tx0, uint32_t ty0,
                             uint32_t tx1, uint32_t ty1, uint32_t nlayers, uint32_t L, uint32_t r0, uint32_t r1,
                             uint32_t c0, uint32_t c1, std::vector<uint8_t>& seen, const std::vector<uint32_t>& base,
-                            std::vector<PktRef>& v) {
+                            std::vector<PktRef>& v, std::vector<uint32_t>* entry = nullptr, uint32_t ei = 0,
+                            uint32_t* iter = nullptr) {
     const uint32_t nc = (uint32_t)comps.size(), nr = p.numres;
     auto nprc = [&](uint32_t c, uint32_t r) {
         const Res& R = comps[c].res[r];
@@ -1299,9 +1342,11 @@ static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uin
     };
     auto put = [&](uint32_t l, uint32_t r, uint32_t c, uint32_t pi) {
         uint8_t& f = seen[((size_t)base[c * nr + r] + pi) * L + l];
+        const uint32_t it = iter ? (*iter)++ : 0;
         if (f) return;
         f = 1;
         v.push_back({l, r, c, pi});
+        if (entry) { entry->push_back(ei); entry->push_back(it); }
     };
     if (prog == 0 || prog == 1) {
         for (uint32_t a = (prog == 0 ? 0 : r0); a < (prog == 0 ? nlayers : r1); ++a)
@@ -1355,10 +1400,14 @@ static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uin
 }
 
 // The tile's packet sequence: its progression, or the POC entries' progressions in turn
-// (layers clamped to the stream's, each packet once).
+// (layers clamped to the stream's, each packet once); entry (optional) receives, per packet,
+// the index of the POC entry that emits it and its position in the entries' concatenated
+// sequences, packets already written counted (Grok's final pass runs each entry's iterator
+// afresh and skips a packet written before through the tile's packet tracker,
+// T2Compress.cpp:46-54, 278-280, still counting it in tile->numProcessedPackets: SOP's Nsop).
 static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Params& p, uint32_t tx0, uint32_t ty0,
                                        uint32_t tx1, uint32_t ty1, uint32_t nlayers,
-                                       const std::vector<PocE>* pocs = nullptr) {
+                                       const std::vector<PocE>* pocs = nullptr, std::vector<uint32_t>* entry = nullptr) {
     std::vector<PktRef> v;
     const uint32_t nc = (uint32_t)comps.size(), nr = p.numres;
     std::vector<uint32_t> base(nc * nr + 1, 0);
@@ -1372,10 +1421,13 @@ static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Par
         packet_iter_one(comps, p, p.prog, tx0, ty0, tx1, ty1, nlayers, nlayers, 0, nr, 0, nc, seen, base, v);
         return v;
     }
-    for (const PocE& e : *pocs) {
+    uint32_t iter = 0;
+    for (uint32_t ei = 0; ei < (uint32_t)pocs->size(); ++ei) {
+        const PocE& e = (*pocs)[ei];
         const uint32_t le = std::min(e.lye, nlayers), r1 = std::min(e.re, nr), c1 = std::min(e.ce, nc);
         if (e.rs >= r1 || e.cs >= c1 || !le) continue;
-        packet_iter_one(comps, p, e.prog, tx0, ty0, tx1, ty1, le, nlayers, e.rs, r1, e.cs, c1, seen, base, v);
+        packet_iter_one(comps, p, e.prog, tx0, ty0, tx1, ty1, le, nlayers, e.rs, r1, e.cs, c1, seen, base, v, entry, ei,
+                        &iter);
     }
     return v;
 }
@@ -1393,6 +1445,13 @@ static int tile_parts(const Params& p, uint32_t nc) {
         if (*q == p.tp_div) return n;
     }
     return -1;
+}
+// With progression order changes each entry is a tile part of its own
+// (CodeStreamCompress::writeTileParts :902-946: one part per progression when no divider
+// is given, getNumTilePartsForProgression :1899-1958 returning 1 for each).
+static int num_parts(const Params& p, uint32_t nc) {
+    if (!p.pocs.empty()) return p.tp_div ? -1 : (int)p.pocs.size();
+    return tile_parts(p, nc);
 }
 static uint32_t tile_part_of(const Params& p, uint32_t nc, const PktRef& k) {
     if (!p.tp_div) return 0;
@@ -1412,7 +1471,7 @@ struct PrecTrees { std::vector<TagTree> incl, imsb; };
 // sop_eph: Scod's SOP (2) / EPH (4) bits; pkt: the packet's index in its tile (SOP's Nsop,
 // tile->numProcessedPackets, T2Compress.cpp:286-320)
 static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t layno, PrecTrees& T,
-                         uint64_t* budget, uint32_t sop_eph = 0, uint32_t pkt = 0) {
+                         uint64_t* budget, uint32_t sop_eph = 0, uint32_t pkt = 0, uint64_t* counted_bytes = nullptr) {
     if (layno == 0) {
         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
             Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
@@ -1425,6 +1484,8 @@ static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t 
         }
     }
     BitWriter bw; std::vector<uint8_t> hdr; bw.out = &hdr;
+    std::vector<uint64_t> ops;
+    if (budget) bw.ops = &ops;
     bw.write(1, 1);  // non-empty packet (Grok always writes 1)
     for (size_t bi = 0; bi < R.bands.size(); ++bi) {
         Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
@@ -1468,10 +1529,32 @@ static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t 
         // count reaches the bytes left (BitIO::writeByte, BitIO.cpp:35-52), a test that never
         // fires when no byte is left (its count starts above 0), so a packet met with 0 bytes
         // left passes and the subtraction wraps: everything after it fits
-        if (sop_eph & 2) *budget = (uint32_t)(*budget - 6);
-        if (*budget != 0 && (uint64_t)hdr.size() >= *budget) return false;
-        *budget = (uint32_t)(*budget - hdr.size());
-        if (sop_eph & 4) *budget = (uint32_t)(*budget - 2);
+        // (GrkSimBitIO: a budget reached inside a number-of-passes or comma code is not seen, the
+        // header's count passes it and the subtraction wraps as well).  M is the packet's bytes
+        // left, decremented unless it is UINT_MAX; *budget (compressPacketsSimulate's maxBytes)
+        // takes the packet's counted bytes at the end, under the same guard.
+        uint32_t M = (uint32_t)*budget;
+        if (sop_eph & 2) { if (M != 0xffffffffu) M -= 6; }
+        uint64_t nb = 0;
+        if (!grk_sim_header(ops, M, &nb)) return false;
+        if (M != 0xffffffffu) M -= (uint32_t)nb;
+        if (sop_eph & 4) { if (M != 0xffffffffu) M -= 2; }
+        uint64_t counted = ((sop_eph & 2) ? 6 : 0) + nb + ((sop_eph & 4) ? 2 : 0);
+        for (size_t bi = 0; bi < R.bands.size(); ++bi) {
+            Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
+            if (B.empty() || P.cblks.empty()) continue;
+            for (auto& K : P.cblks) {
+                const uint32_t np = K.layer_np[layno];
+                if (!np) continue;
+                const uint32_t r0 = K.passes_in_prev ? K.passes[K.passes_in_prev - 1].rate : 0;
+                const uint32_t len = K.passes[K.passes_in_prev + np - 1].rate - r0;
+                if (len > M) return false;
+                if (M != 0xffffffffu) M -= len;
+                counted += len;
+            }
+        }
+        if (*budget != 0xffffffffu) *budget = (uint32_t)(*budget - counted);
+        if (counted_bytes) *counted_bytes = counted;
     }
     if (o) {
         if (sop_eph & 2) {   // SOP: FF91, Lsop 4, Nsop = packet index mod 2^16
@@ -1488,10 +1571,6 @@ static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t 
             if (!np) continue;
             uint32_t r0 = K.passes_in_prev ? K.passes[K.passes_in_prev - 1].rate : 0;
             uint32_t r1 = K.passes[K.passes_in_prev + np - 1].rate;
-            if (budget) {
-                if ((uint64_t)(r1 - r0) > *budget) return false;
-                *budget = (uint32_t)(*budget - (r1 - r0));
-            }
             if (o) o->insert(o->end(), K.data.begin() + r0, K.data.begin() + r1);
             K.passes_in_prev += np;
         }
@@ -1938,6 +2017,13 @@ struct EncodeState {
     std::vector<std::vector<int32_t>> coefs;   // reversible Mallat coefficients
     std::vector<std::vector<float>> fcoefs;    // irreversible Mallat coefficients
     size_t header_size = 0;
+    // the rate control's final simulation (pcrdBisectSimple :1352-1357): each packet's length as
+    // compressPacketSimulate counts it, in the tile's progression; they fill the PLT marker
+    // (pushNextPacketLength) and their sum the tile-part length written in SOT / TLM
+    // (preCalculatedTileLen, TileProcessor.cpp:243-259) - not always the bytes written, see
+    // GrkSimBitIO
+    std::vector<uint32_t> sim_lens;
+    bool have_sim = false;
 };
 
 // Rate control is active when any layer has a target rate (TileProcessor.cpp:952-967).
@@ -2096,13 +2182,24 @@ static std::vector<std::vector<std::vector<PrecTrees>>> make_trees(EncodeState& 
     return trees;
 }
 
-// T2Compress::compressPacketsSimulate: do layers [0, max_layers) fit in max_bytes?
-static bool simulate(EncodeState& E, uint32_t max_layers, uint64_t max_bytes) {
+// T2Compress::compressPacketsSimulate (:59-112): do layers [0, max_layers) fit in max_bytes?
+// The simulation walks every packet in the tile's own progression (COD's), whatever the
+// progression order changes say: its PacketManager is built in THRESH_CALC mode, where
+// updateCompressTcpProgressions (PacketManager.cpp:565-589, called at :123-125 with poc =
+// false) sets each entry's progression to tcp->prg and its ranges to the whole tile, and
+// only the first iterator runs (pocno = 1 outside Cinema 4K).
+static bool simulate(EncodeState& E, uint32_t max_layers, uint64_t max_bytes, std::vector<uint32_t>* lens = nullptr) {
     auto trees = make_trees(E);
     uint64_t budget = max_bytes;
     uint64_t* bp = (max_bytes == 0xffffffffull) ? nullptr : &budget;
-    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, max_layers, &E.p.pocs))
-        if (!write_packet(nullptr, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], bp, E.p.sop_eph)) return false;
+    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, max_layers)) {
+        std::vector<uint8_t> tmp;
+        uint64_t counted = 0;
+        if (!write_packet(lens && !bp ? &tmp : nullptr, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], bp,
+                          E.p.sop_eph, 0, &counted))
+            return false;
+        if (lens) lens->push_back((uint32_t)(bp ? counted : tmp.size()));
+    }
     return true;
 }
 
@@ -2189,8 +2286,18 @@ static void rate_allocate(EncodeState& E) {
         }
     });
     double upper = max_slope;
+    uint64_t last_len = 0xffffffffull;   // maxLayerLength after the loop: the last layer's
     for (uint32_t l = 0; l < E.p.nlayers; ++l) {
         uint64_t max_len = rates[l] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[l]) : 0xffffffffull;
+        last_len = max_len;
+        if (const char* fb = getenv("ORC_FORCE_BUDGET")) {   // debugging aid: "tile:layer:bytes,..."
+            for (const char* q = fb; *q;) {
+                unsigned ft, fl; unsigned long long fv; int n = 0;
+                if (sscanf(q, "%u:%u:%llu%n", &ft, &fl, &fv, &n) != 3) break;
+                if (ft == E.tile && fl == l) max_len = fv;
+                q += n; if (*q == ',') ++q;
+            }
+        }
         if (layer_needs_rc(E.p, l)) {
             double lower = min_slope, prevthresh = -1, thresh = 0;
             const double target = E.p.quality ? tile_dist - maxSE / pow(10.0, E.p.dist[l] / 10.0) : 0.0;
@@ -2204,11 +2311,26 @@ static void rate_allocate(EncodeState& E) {
                     if (achieved < target) { upper = thresh; continue; }
                     lower = thresh;
                 } else {
-                    if (!simulate(E, l + 1, max_len)) { lower = thresh; continue; }
+                    const bool fits = simulate(E, l + 1, max_len);
+                    if (getenv("ORC_RC_TRACE"))   // debugging aid: the bisection's steps
+                        fprintf(stderr, "  tile %u layer %u it %u thresh %.17g lower %.17g upper %.17g %s budget %llu\n",
+                                E.tile, l, it, thresh, lower, upper, fits ? "fits" : "fails", (unsigned long long)max_len);
+                    if (!fits) { lower = thresh; continue; }
                     upper = thresh;
                 }
             }
             double good = (upper == -1) ? thresh : upper;
+            if (const char* ft = getenv("ORC_FORCE_THRESH")) {   // debugging aid: "layer:thresh,..."
+                for (const char* q = ft; *q;) {
+                    unsigned fl, ftile; double fv; int n = 0;
+                    if (sscanf(q, "%u:%u:%lf%n", &ftile, &fl, &fv, &n) == 3) {
+                        if (fl == l && ftile == E.tile) good = fv;
+                    } else if (sscanf(q, "%u:%lf%n", &fl, &fv, &n) == 2) {
+                        if (fl == l) good = fv;
+                    } else break;
+                    q += n; if (*q == ',') ++q;
+                }
+            }
             const double ld = make_layer(E, l, good, true, prev);
             cum[l] = l == 0 ? ld : cum[l - 1] + ld;
             upper = lower - 1;
@@ -2216,20 +2338,56 @@ static void rate_allocate(EncodeState& E) {
             make_layer(E, l, -1.0, true, prev);
         }
     }
+    if (!E.p.quality) {   // the final simulation (with fixed quality maxLayerLength stays UINT_MAX there too)
+        E.sim_lens.clear();
+        E.have_sim = simulate(E, E.p.nlayers, last_len, &E.sim_lens);
+    }
 }
 
 // One tile's packets in LRCP order (T2Compress::compressPackets); packet lengths
 // are recorded for PLT.
+// With progression order changes the packets of entry k form tile part k, and the PLT lengths
+// (plt) are listed in the tile's own progression: Grok's PLT is filled by the rate-control
+// simulation (compressPacketSimulate :427-428, THRESH_CALC order, see simulate()), not by the
+// packets as written.
 static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector<uint32_t>& plens,
-                         std::vector<uint32_t>* pparts = nullptr) {
+                         std::vector<uint32_t>* pparts = nullptr, std::vector<uint32_t>* plt = nullptr) {
     auto trees = make_trees(E);
-    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, E.p.nlayers, &E.p.pocs)) {
+    const bool poc = !E.p.pocs.empty();
+    std::vector<uint32_t> entry;
+    const std::vector<PktRef> order =
+        packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, E.p.nlayers, &E.p.pocs, poc ? &entry : nullptr);
+    for (size_t i = 0; i < order.size(); ++i) {
+        const PktRef& k = order[i];
         size_t before = body.size();
         write_packet(&body, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], nullptr, E.p.sop_eph,
-                     (uint32_t)plens.size());
+                     poc ? entry[2 * i + 1] : (uint32_t)plens.size());
         plens.push_back((uint32_t)(body.size() - before));
-        if (pparts) pparts->push_back(tile_part_of(E.p, E.im.nc, k));
+        if (pparts) pparts->push_back(poc ? entry[2 * i] : tile_part_of(E.p, E.im.nc, k));
     }
+    if (!plt) return;
+    if (!poc) { *plt = plens; return; }
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, uint32_t> len;   // (c, r, pi, l) -> bytes
+    for (size_t i = 0; i < order.size(); ++i) len[{order[i].c, order[i].r, order[i].pi, order[i].l}] = plens[i];
+    plt->clear();
+    for (const PktRef& k : packet_iter(E.comps, E.p, E.tx0, E.ty0, E.tx1, E.ty1, E.p.nlayers)) {
+        auto it = len.find({k.c, k.r, k.pi, k.l});
+        if (it != len.end()) plt->push_back(it->second);
+    }
+}
+
+// A POC list must name every packet of the tile: CodeStreamCompress::validateProgressionOrders
+// (:1685-1747) refuses a list that misses one.  (A packet two entries name is written once, in
+// the first entry's part: the tile's packet tracker, T2Compress.cpp:278-280.)
+static bool pocs_cover(const Params& p, uint32_t nc) {
+    if (p.pocs.empty()) return true;
+    std::vector<uint8_t> n((size_t)p.nlayers * p.numres * nc, 0);
+    for (const PocE& e : p.pocs)
+        for (uint32_t l = 0; l < std::min(e.lye, p.nlayers); ++l)
+            for (uint32_t r = e.rs; r < std::min(e.re, p.numres); ++r)
+                for (uint32_t c = e.cs; c < std::min(e.ce, nc); ++c) n[((size_t)l * p.numres + r) * nc + c] = 1;
+    for (uint8_t v : n) if (!v) return false;
+    return true;
 }
 
 // Tile part: SOT [PLT] SOD packets (CodeStreamCompress::writeTilePart :862-900; SOT with
@@ -2239,18 +2397,35 @@ static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector
 // (TPsot = part, TNsot = parts) [PLT of every packet of the tile, first part only
 // (TileProcessor::writeTilePartT2)] SOD, packets.  Returns each part's Psot.
 static std::vector<uint32_t> write_tile_part(std::vector<uint8_t>& o, EncodeState& E) {
-    std::vector<uint8_t> body; std::vector<uint32_t> plens, pparts;
-    tile_packets(E, body, plens, &pparts);
-    const int np = tile_parts(E.p, E.im.nc);
+    std::vector<uint8_t> body; std::vector<uint32_t> plens, pparts, plt;
+    tile_packets(E, body, plens, &pparts, &plt);
+    if (E.have_sim) plt = E.sim_lens;   // PLT from the rate control's final simulation
+    const int np = num_parts(E.p, E.im.nc);
+    // CodeStreamCompress::writeTilePart (:858-900): a tile in one part with one progression
+    // writes the length TileProcessor precalculated (SOT + [PLT] + SOD + the simulation's
+    // packet bytes) as Psot and in TLM (canPreCalculateTileLen :54-57)
+    const bool precalc = np == 1 && E.p.pocs.empty();
     std::vector<uint32_t> psots;
     size_t pk = 0, boff = 0;
     for (int part = 0; part < np; ++part) {
         size_t sot = o.size();
         put16(o, 0xff90); put16(o, 10); put16(o, E.tile); put32(o, 0); o.push_back((uint8_t)part); o.push_back((uint8_t)np);
-        if (part == 0 && !E.p.pocs.empty()) write_poc(o, E.p.pocs, E.im.nc);   // POC in the first tile part
+        if (part == 0 && !E.p.pocs.empty()) {
+            // POC in the tile's first tile part (writeTilePart :870-875): writePoc writes tile 0's
+            // list (tcp = m_cp.tcps), clamped by the main header's writePoc; each entry's
+            // progression is what tile 0's last PacketManager left there - for tile 0 its own
+            // rate-control simulation (THRESH_CALC: tcp->prg), for later tiles tile 0's final
+            // pass (the given progression)
+            std::vector<PocE> w = E.p.pocs;
+            for (PocE& e : w) {
+                e.lye = std::min(e.lye, E.p.nlayers); e.re = std::min(e.re, E.p.numres); e.ce = std::min(e.ce, E.im.nc);
+                if (E.tile == 0) e.prog = E.p.prog;
+            }
+            write_poc(o, w, E.im.nc);
+        }
         if (E.p.plt && part == 0) {
             std::vector<uint8_t> v;
-            for (uint32_t L : plens) {
+            for (uint32_t L : plt) {
                 int nbits = floorlog2(L) + 1, nbytes = (nbits + 6) / 7;
                 for (int k = nbytes - 1; k >= 0; --k) v.push_back((uint8_t)(((L >> (7 * k)) & 0x7F) | (k ? 0x80 : 0)));
             }
@@ -2263,6 +2438,11 @@ static std::vector<uint32_t> write_tile_part(std::vector<uint8_t>& o, EncodeStat
         o.insert(o.end(), body.begin() + boff, body.begin() + boff + bl);
         boff += bl;
         uint32_t psot = (uint32_t)(o.size() - sot);
+        if (precalc && E.have_sim) {
+            uint64_t sum = 0;
+            for (uint32_t L : E.sim_lens) sum += L;
+            psot = (uint32_t)(psot - bl + sum);
+        }
         o[sot + 6] = (uint8_t)(psot >> 24); o[sot + 7] = (uint8_t)(psot >> 16); o[sot + 8] = (uint8_t)(psot >> 8); o[sot + 9] = (uint8_t)psot;
         psots.push_back(psot);
     }
@@ -2280,6 +2460,7 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
     size_t tlm_pos = 0;
     uint32_t nt = 0;
     const Params p0 = to_params(cp);
+    if (!pocs_cover(p0, nc) || num_parts(p0, nc) < 1) return 0;
     if (!needs_rate_control(p0) && tile_count(p0, w, h) > 1) {
         // independent tiles coded in parallel, written in tile order
         nt = tile_count(p0, w, h);
@@ -2573,7 +2754,7 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
     }
     size_t pos = i;
     uint32_t npkt = 0;   // tile->numProcessedPackets: SOP's expected Nsop (T2Decompress.cpp:114, 239-246)
-    for (const PktRef& pk : packet_iter(comps, p, tx0, ty0, tx1, ty1, nlayers, tpocs && !tpocs->empty() ? tpocs : &p.pocs)) {
+    for (const PktRef& pk : packet_iter(comps, p, tx0, ty0, tx1, ty1, nlayers, tpocs ? tpocs : &p.pocs)) {
                 const uint32_t l = pk.l, r = pk.r, c = pk.c, pi = pk.pi;
                 Res& R = comps[c].res[r];
                 // layers past the limit and resolutions past the reduction: header parsed for
@@ -2875,14 +3056,20 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     // a tile's parts in order (TPsot 0, 1, ...)
     std::vector<uint32_t> tiles;
     std::vector<std::vector<std::pair<size_t, size_t>>> ranges;
-    std::vector<std::vector<PocE>> tpocs;   // POC of the tile's first tile-part header
+    // a tile's progression order changes: the main header's list, extended by the POC of each of
+    // its tile-part headers in turn (read_poc appends to the tile's tcp, a copy of the main
+    // header's, CodeStreamDecompress.cpp:1171-1172; OpenJPEG's opj_j2k_read_poc does the same)
+    std::vector<std::vector<PocE>> tpocs;
     std::vector<int> slot(nt, -1);
     for (Part& q : parts) {
         if (slot[q.tile] < 0) {
             if (q.tpsot != 0) return -5;
             slot[q.tile] = (int)tiles.size(); tiles.push_back(q.tile); ranges.emplace_back();
-            tpocs.push_back(std::move(q.pocs));
+            tpocs.push_back(p.pocs);
         } else if (q.tpsot != ranges[slot[q.tile]].size()) return -5;
+        std::vector<PocE>& tl = tpocs[slot[q.tile]];
+        tl.insert(tl.end(), q.pocs.begin(), q.pocs.end());
+        if (tl.size() > 33) return -5;   // GRK_J2K_MAXRLVLS progressions (read_poc :1173-1178)
         ranges[slot[q.tile]].push_back({q.data, q.end});
     }
     std::vector<int> rcs(tiles.size(), 0);   // tiles write disjoint rectangles of out

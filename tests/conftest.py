@@ -39,8 +39,8 @@ def parse_flags(flags):
         kw["precincts"] = [tuple(map(int, m)) for m in re.findall(r"\[(\d+),(\d+)\]", t[t.index("-c") + 1])]
     if "-I" in t:
         kw["irreversible"] = True
-    if "-r" in t:
-        kw["layer_rate"] = [float(v) for v in t[t.index("-r") + 1].split(",")]
+    if "-r" in t:   # a ratio of 1 means lossless (0) (grk_compress.cpp:781-786)
+        kw["layer_rate"] = [0.0 if float(v) == 1 else float(v) for v in t[t.index("-r") + 1].split(",")]
     if "-M" in t:
         kw["cblk_sty"] = int(t[t.index("-M") + 1])
     if "-t" in t:
@@ -72,6 +72,8 @@ def parse_flags(flags):
             kw["pocs"] = [q[1:] for q in pocs[:k]]
     if "-L" in t:
         kw["plt"] = True
+    if "-u" in t:   # tile-part divider (grk_compress -u L|R|C)
+        kw["tile_parts"] = t[t.index("-u") + 1]
     return kw
 
 
