@@ -151,3 +151,67 @@ struct PktBitWriter {
         else put(0xff80 | (n - 37), 16);
     }
 };
+
+// Grok's bounded packet-header BitIO as T2Compress::compressPacketSimulate uses it
+// (BitIO(nullptr, max_bytes, true); BitIO.cpp:24-52, 80-122), emulated bit by bit for the
+// rate control's budget test: writeByte counts a byte and fails when the count reaches buf_len
+// (never when buf_len is 0, the count starting above it), leaving the pending byte and ct as
+// they were; putbit fails with it, and write() returns at the first failed bit, dropping the
+// rest of its value.  compressHeader checks every write but those inside putnumpasses and
+// putcommacode (BitIO.cpp:144-178 return nothing): a failure there is swallowed, the header
+// goes on (the next writeByte counts the same byte again, count buf_len + 1, and succeeds) and
+// the count it reports runs past the budget.  Same interface as PktBitWriter.
+struct GrkSimWriter {
+    uint64_t offset = 0, buf_len;
+    uint32_t buf = 0;
+    int ct = 8;
+    bool failed = false;      // a checked write or the flush reached the budget: the packet fails
+    bool swallowed = false;   // the budget was reached inside a number-of-passes / comma code
+    explicit GrkSimWriter(uint64_t len) : buf_len(len) {}
+    inline bool write_byte() {
+        ++offset;
+        if (offset == buf_len) return false;
+        ct = buf == 0xff ? 7 : 8;
+        buf = 0;
+        return true;
+    }
+    inline bool bit(uint32_t b) {
+        if (ct == 0 && !write_byte()) return false;
+        --ct;
+        buf |= b << ct;
+        return true;
+    }
+    inline bool bits(uint32_t v, uint32_t k) {
+        for (int i = (int)k - 1; i >= 0; --i)
+            if (!bit((v >> i) & 1)) return false;
+        return true;
+    }
+    // checked writes (a run of tag-tree bits is a run of one-bit writes: failing at its first
+    // failed bit is the same)
+    inline void put(uint32_t v, uint32_t k) { if (!failed && !bits(v, k)) failed = true; }
+    inline void putbit(uint32_t b) { put(b, 1); }
+    inline void write(uint32_t v, int n) {
+        if (n > 32) { put(0, (uint32_t)n - 32); n = 32; }
+        put(n == 32 ? v : (v & ((1u << n) - 1)), (uint32_t)n);
+    }
+    void flush() {
+        if (failed) return;
+        if (!write_byte() || (ct == 7 && !write_byte())) failed = true;
+    }
+    // unchecked: BitIO::putcommacode writes one bit per call, putnumpasses its code in one call
+    void commacode(uint32_t n) {
+        if (failed) return;
+        for (uint32_t i = 0; i < n; ++i) if (!bit(1)) swallowed = true;
+        if (!bit(0)) swallowed = true;
+    }
+    void numpasses(uint32_t n) {
+        if (failed) return;
+        bool ok;
+        if (n == 1) ok = bits(0, 1);
+        else if (n == 2) ok = bits(2, 2);
+        else if (n <= 5) ok = bits(0xc | (n - 3), 4);
+        else if (n <= 36) ok = bits(0x1e0 | (n - 6), 9);
+        else ok = bits(0xff80 | (n - 37), 16);
+        if (!ok) swallowed = true;
+    }
+};

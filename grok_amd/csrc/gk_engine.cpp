@@ -590,6 +590,16 @@ static void build_plan(Plan& P) {
 // ---------------------------------------------------------------------------
 // bit-stuffed writer (gk_bitio.h)
 using BitWriter = PktBitWriter;
+// one header coded into two writers at once
+template <class A, class B> struct TeeWriter {
+    A& a; B& b;
+    inline void put(uint32_t v, uint32_t k) { a.put(v, k); b.put(v, k); }
+    inline void putbit(uint32_t v) { a.putbit(v); b.putbit(v); }
+    inline void write(uint32_t v, int n) { a.write(v, n); b.write(v, n); }
+    void flush() { a.flush(); b.flush(); }
+    void commacode(uint32_t n) { a.commacode(n); b.commacode(n); }
+    void numpasses(uint32_t n) { a.numpasses(n); b.numpasses(n); }
+};
 
 struct TagTree {
     std::vector<int32_t> parent;
@@ -1118,31 +1128,53 @@ struct T2Enc {
         return write_packet(R, pi, l, budget, seg, hdr);
     }
     // hdr_out: the packet header bytes (a per-thread buffer when tiles are written in parallel;
-    // all other state touched is per code-block / per precinct, i.e. disjoint across tiles)
+    // all other state touched is per code-block / per precinct, i.e. disjoint across tiles).
+    // With a budget the header is only counted, as compressPacketSimulate (T2Compress.cpp:
+    // 347-434) does in its uint32 arithmetic: M, the packet's bytes left, loses SOP's 6 bytes
+    // untested, the header goes through Grok's bounded BitIO (GrkSimWriter: fails when its count
+    // reaches M - never with none left, so such a packet passes and the subtraction wraps - and
+    // misses a budget reached inside a number-of-passes or comma code), EPH's 2 bytes untested,
+    // then each body must fit; M is not decremented once it is UINT_MAX.  The caller's budget
+    // (compressPacketsSimulate's maxBytes) takes the packet's counted bytes, under the same
+    // guard.  *sw (optional) reports a swallowed failure: the packet's counted header bytes.
     bool write_packet(const ResG& R, uint32_t pi, uint32_t l, uint64_t* budget,
-                      std::vector<uint32_t>* seg, std::vector<uint8_t>& hdr, uint64_t* body_bytes = nullptr) {
+                      std::vector<uint32_t>* seg, std::vector<uint8_t>& hdr, uint64_t* body_bytes = nullptr,
+                      uint64_t* hdr_count = nullptr, bool* swallowed = nullptr) {
         if (l == 0)
             for (size_t bi = 0; bi < R.bands.size(); ++bi) {
                 const PrecG& PG = R.prc[bi][pi];
                 if (PG.cw && PG.ch) band_init(PG, R.bands[bi].numbps);
             }
         hdr.clear();
-        BitWriter bw(hdr);
-        bw.putbit(1);
-        for (size_t bi = 0; bi < R.bands.size(); ++bi) {
-            const PrecG& PG = R.prc[bi][pi];
-            if (PG.cw && PG.ch) band_header(PG, l, bw);
-        }
-        bw.flush();
+        constexpr uint32_t UMAX = 0xffffffffu;
+        uint32_t M = 0;
+        uint64_t counted = 0;
         if (budget) {
-            // compressPacketSimulate (T2Compress.cpp:347-434) in its uint32 arithmetic: SOP's 6 and
-            // EPH's 2 bytes are taken untested; the bounded BitIO fails when its byte count reaches
-            // the bytes left (BitIO.cpp:35-52), which never happens with none left, so such a
-            // packet passes and the subtraction wraps
-            if (P.p.sop_eph & 2) *budget = (uint32_t)(*budget - 6);
-            if (*budget != 0 && (uint64_t)hdr.size() >= *budget) return false;
-            *budget = (uint32_t)(*budget - hdr.size());
-            if (P.p.sop_eph & 4) *budget = (uint32_t)(*budget - 2);
+            M = (uint32_t)*budget;
+            if (P.p.sop_eph & 2) { if (M != UMAX) M -= 6; counted += 6; }
+            GrkSimWriter sw(M);
+            BitWriter bw(hdr);   // the real header too (its length when a failure is swallowed)
+            TeeWriter<GrkSimWriter, BitWriter> tw{sw, bw};
+            tw.putbit(1);
+            for (size_t bi = 0; bi < R.bands.size(); ++bi) {
+                const PrecG& PG = R.prc[bi][pi];
+                if (PG.cw && PG.ch) band_header(PG, l, tw);
+            }
+            tw.flush();
+            if (sw.failed) return false;
+            if (hdr_count) *hdr_count = sw.offset;
+            if (swallowed) *swallowed = sw.swallowed;
+            if (M != UMAX) M -= (uint32_t)sw.offset;
+            counted += sw.offset;
+            if (P.p.sop_eph & 4) { if (M != UMAX) M -= 2; counted += 2; }
+        } else {
+            BitWriter bw(hdr);
+            bw.putbit(1);
+            for (size_t bi = 0; bi < R.bands.size(); ++bi) {
+                const PrecG& PG = R.prc[bi][pi];
+                if (PG.cw && PG.ch) band_header(PG, l, bw);
+            }
+            bw.flush();
         }
         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
             const PrecG& PG = R.prc[bi][pi];
@@ -1153,27 +1185,43 @@ struct T2Enc {
                 uint32_t r0 = inprev[b] ? rate(b, inprev[b] - 1) : 0;
                 uint32_t r1 = rate(b, inprev[b] + np - 1);
                 if (budget) {
-                    if ((uint64_t)(r1 - r0) > *budget) return false;
-                    *budget = (uint32_t)(*budget - (r1 - r0));
+                    if (r1 - r0 > M) return false;
+                    if (M != UMAX) M -= r1 - r0;
+                    counted += r1 - r0;
                 }
                 if (seg) { seg->push_back(b); seg->push_back(r0); seg->push_back(r1 - r0); }
                 if (body_bytes) *body_bytes += r1 - r0;
                 inprev[b] = (uint16_t)(inprev[b] + np);
             }
         }
+        if (budget && *budget != UMAX) *budget = (uint32_t)(*budget - counted);
         return true;
     }
+
+    // A budget failure the simulation did not see (GrkSimWriter::swallowed): the packet, the
+    // header bytes Grok's BitIO counted for it and its real header bytes.  When the final
+    // simulation (pcrdBisectSimple :1352-1357) meets one, that count goes into the packet's PLT
+    // entry and the tile part's precalculated length (SOT Psot / TLM, TileProcessor.cpp:243-259).
+    struct Swallow { bool on = false; uint32_t c = 0, r = 0, pi = 0, l = 0; uint64_t hcnt = 0, hreal = 0; };
+    Swallow final_sw;   // the final simulation's, once allocate() has run
+    bool final_sw_pending = false;
 
     // T2Compress::compressPacketsSimulate (:59-112) walks every packet in the tile's own
     // progression whatever the progression order changes say: its THRESH_CALC PacketManager
     // sets each entry's progression to tcp->prg and its ranges to the whole tile
     // (updateCompressTcpProgressions, PacketManager.cpp:123-125, 565-589) and runs only the first
     // iterator (pocno = 1 outside Cinema 4K)
-    bool simulate(uint32_t max_layers, uint64_t max_bytes) {
+    bool simulate(uint32_t max_layers, uint64_t max_bytes, Swallow* swo = nullptr) {
         uint64_t budget = max_bytes;
         uint64_t* bp = max_bytes == 0xffffffffull ? nullptr : &budget;
-        for (const PacketRef& pr : packet_order(P, P.tiles[t0], max_layers))   // rate control: one tile
-            if (!write_packet(P.tiles[t0].comps[pr.c].res[pr.r], pr.pi, pr.l, bp, nullptr)) return false;
+        if (swo) *swo = Swallow();
+        for (const PacketRef& pr : packet_order(P, P.tiles[t0], max_layers)) {   // rate control: one tile
+            const ResG& R = P.tiles[t0].comps[pr.c].res[pr.r];
+            uint64_t hc = 0;
+            bool sw = false;
+            if (!write_packet(R, pr.pi, pr.l, bp, nullptr, hdr, nullptr, &hc, &sw)) return false;
+            if (sw && swo && !swo->on) *swo = Swallow{true, pr.c, pr.r, pr.pi, pr.l, hc, hdr.size()};
+        }
         return true;
     }
 
@@ -1374,23 +1422,56 @@ struct T2Enc {
             ord.push_back({base[(size_t)pr.r * P.nc + pr.c] + pr.pi, pr.l});
         ord_l = l;
     }
-    // compressPacketsSimulate (T2Compress.cpp:59-112) over packet sizes: a header reaching the
-    // bytes left or a body past them fails the layer, and a packet met with no byte left passes
-    // with all after it (its uint32 subtraction wraps, see write_packet)
-    bool packet_walk(uint32_t l, uint64_t max_bytes) const {
+    // compressPacketsSimulate (T2Compress.cpp:59-112) over packet sizes, in write_packet's
+    // arithmetic: a body past the bytes left fails the layer, a packet met with no byte left
+    // passes with all after it (its uint32 subtraction wraps), and a header reaching the bytes
+    // left fails it unless that happens inside a number-of-passes or comma code, where Grok's
+    // BitIO misses it and the count wraps as well (header_reaches).  Returns 1 (fits), 0 (fails)
+    // or -1 when a final layer's packet header reaches the budget (its coding state is gone:
+    // the caller runs the serial simulation).  *swo: a swallowed failure, if any.
+    int packet_walk(uint32_t l, uint64_t max_bytes, Swallow* swo) {
         const bool sop = P.p.sop_eph & 2, eph = P.p.sop_eph & 4;
+        constexpr uint32_t UMAX = 0xffffffffu;
         uint32_t rem = (uint32_t)max_bytes;
+        *swo = Swallow();
         for (const auto& e : ord) {
             const uint64_t h = e.second < l ? fhdr[e.second][e.first] : chdr[e.first];
             const uint64_t sz = e.second < l ? fsize[e.second][e.first] : csize[e.first];
-            if (sop) rem -= 6;
-            if (rem != 0 && h >= rem) return false;
-            rem -= (uint32_t)h;
-            if (eph) rem -= 2;
-            if (sz - h > rem) return false;
-            rem -= (uint32_t)(sz - h);
+            uint32_t M = rem;
+            if (sop && M != UMAX) M -= 6;
+            uint64_t hc = h;
+            if (M != 0 && h >= M) {
+                if (e.second < l) return -1;
+                if (!header_reaches(e.first, l, M, &hc)) return 0;
+                if (!swo->on) {
+                    const Chain& ch = chains[e.first];
+                    *swo = Swallow{true, ch.c, ch.r, ch.pi, l, hc, h};
+                }
+            }
+            if (M != UMAX) M -= (uint32_t)hc;
+            if (eph && M != UMAX) M -= 2;
+            const uint64_t body = sz - h;
+            if (body > M) return 0;
+            if (rem != UMAX) rem -= (uint32_t)(((sop ? 6 : 0) + hc + (eph ? 2 : 0) + body) & 0xffffffffu);
         }
-        return true;
+        return 1;
+    }
+    // Layer l's packet of chain i, coded again from the snapshot through Grok's bounded BitIO
+    // with M bytes left (GrkSimWriter): false if it fails, else true with the byte count it
+    // reports (the failure swallowed).  The coding state ends as code_layer left it.
+    bool header_reaches(uint32_t i, uint32_t l, uint32_t M, uint64_t* count) {
+        GrkSimWriter sw(M);
+        sw.putbit(1);
+        for (uint32_t u : cunits[i]) {
+            uint32_t numbps;
+            const PrecG& PG = unit_prec(units[u], &numbps);
+            if (l) restore_band(PG); else band_init(PG, numbps);
+            band_header(PG, l, sw);
+            band_body(PG, l);
+        }
+        sw.flush();
+        *count = sw.offset;
+        return !sw.failed;
     }
     // Could the walk above wrap before it fails?  That needs the bytes left in front of some
     // packet k to be 0 (0..5 with SOP) or, with EPH, 1 after its header: the running size
@@ -1408,11 +1489,20 @@ struct T2Enc {
         }
         return false;
     }
-    bool simulate_layer(uint32_t l, uint64_t max_bytes) {
+    bool simulate_layer(uint32_t l, uint64_t max_bytes, Swallow* swo) {
+        *swo = Swallow();
         if (max_bytes == 0xffffffffull) return true;
         code_layer(l);
         ensure_order(l);
-        return packet_walk(l, max_bytes);
+        const int r = packet_walk(l, max_bytes, swo);
+        if (r >= 0) return r > 0;
+        // the serial simulation, on a copy of the coding state the fast path keeps
+        const std::vector<TagTree> si = incl, sm = imsb;
+        const std::vector<uint16_t> sp = inprev;
+        const std::vector<uint8_t> sn = nlb;
+        const bool ok = simulate(l + 1, max_bytes, swo);
+        incl = si; imsb = sm; inprev = sp; nlb = sn;
+        return ok;
     }
     void finish_layer(uint32_t l) {   // layer l is final: advance the snapshot past it
         code_layer(l);
@@ -1780,8 +1870,9 @@ struct T2Enc {
         if (t1 != t0 + 1) throw GkError("rate control runs on one tile at a time");
         const TileG& TT = P.tiles[t0];
         const double size_pixel = (double)P.nc * P.prec, npix = (double)((uint64_t)(TT.x1 - TT.x0) * (TT.y1 - TT.y0));
-        // tile-part generation: 14 bytes (SOT + SOD) per extra part, spread over the layers
-        const double tp_offset = (double)((tile_part_split(P).n - 1) * 14) / (double)L;
+        // tile-part generation: 14 bytes (SOT + SOD) per extra part, spread over the layers (the
+        // parts of progression order changes do not count: `stride` needs m_enableTilePartGeneration)
+        const double tp_offset = P.p.tp_div ? (double)((tile_part_split(P).n - 1) * 14) / (double)L : 0.0;
         for (uint32_t k = 0; k < L; ++k)
             rates[k] = P.p.rates[k] > 0.0 ? (size_pixel * npix) / (P.p.rates[k] * 8.0) - tp_offset : 0.0;
         const double sot_adjust = (npix * (double)header_size) / ((double)P.w * (double)P.h);
@@ -1868,6 +1959,7 @@ struct T2Enc {
                 // pass counts equal to those at an end of the bisection interval give that end's
                 // outcome (the simulation depends on nothing else): the simulation is skipped
                 bool has_lo = false, has_hi = false;
+                Swallow sw_hi;
                 uint64_t h_lo = 0, h_hi = 0;
                 size_t j_lo = 0, j_hi = 0;   // journal positions of the counts at lower / upper
                 // the hash only nominates a match: the layer's pass counts are compared exactly
@@ -1889,13 +1981,14 @@ struct T2Enc {
                     if (prevthresh != -1 && fabs(prevthresh - thresh) < 0.001) break;
                     prevthresh = thresh;
                     bool ok;
+                    Swallow sw_now;   // a fit through a swallowed failure (Swallow)
                     // (bounds_on: the exact compare from the change journal, no count copies)
                     auto same = [&](const std::vector<uint16_t>& c, size_t pos) {
                         if (bounds_on) return same_counts_since(pos, l);
                         counts(c_now);
                         return c_now == c;
                     };
-                    if (has_hi && h == h_hi && same(c_hi, j_hi)) ok = true;
+                    if (has_hi && h == h_hi && same(c_hi, j_hi)) { ok = true; sw_now = sw_hi; }
                     else if (has_lo && h == h_lo && same(c_lo, j_lo)) ok = false;
                     else if (P.p.quality) {
                         // below the target: upperBound = thresh (TileProcessor.cpp:1311-1322)
@@ -1911,7 +2004,7 @@ struct T2Enc {
                         if (d && !check) { ok = d > 0; ++n_bound; }
                         else {
                             skip_clean = bounds_on;
-                            ok = fast ? simulate_layer(l, max_len) : simulate(l + 1, max_len);
+                            ok = fast ? simulate_layer(l, max_len, &sw_now) : simulate(l + 1, max_len, &sw_now);
                             skip_clean = false;
                             ++n_sim;
                             if (bounds_on && check && max_len != 0xffffffffull) {
@@ -1928,8 +2021,14 @@ struct T2Enc {
                         if (bounds_on) j_lo = jlog.size(); else counts(c_lo);
                         continue;
                     }
-                    upper = thresh; h_hi = h; has_hi = true;
+                    upper = thresh; h_hi = h; has_hi = true; sw_hi = sw_now;
                     if (bounds_on) j_hi = jlog.size(); else counts(c_hi);
+                }
+                // the final simulation (all layers, this layer's budget when it is the last)
+                // replays the step that set upper; without one it runs here
+                if (l + 1 == L) {
+                    if (has_hi) final_sw = sw_hi;
+                    else final_sw_pending = true;
                 }
                 const double fin = upper == -1 ? thresh : upper;
                 if (bounds_on) {   // incrementally too (fin is an end of the interval), then final
@@ -1952,6 +2051,10 @@ struct T2Enc {
                 t_fin += msd(tf, clk::now());
             }
             bounds_on = false;
+        }
+        if (final_sw_pending) {   // (the coding state is not needed after allocate: packets restart it)
+            const uint64_t last = rates[L - 1] > 0.0f ? (uint64_t)(uint32_t)ceil(rates[L - 1]) : 0xffffffffull;
+            simulate(L, last, &final_sw);
         }
         if (prof)
             fprintf(stderr, "pcrd: %u bisection steps, %u simulated, %u decided by bounds; make_layer %.2f ms, simulation %.2f ms, bounds setup %.2f ms, "
@@ -2792,8 +2895,11 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         }
     }
     T2Enc T2(P, hinfo, hpasses, tb, te);
-    if (te - tb == 1 || !P.p.rate_control()) T2.allocate(rc_header_size);
-    else {
+    std::vector<T2Enc::Swallow> tsw(te - tb);   // per tile: the final simulation's swallowed failure
+    if (te - tb == 1 || !P.p.rate_control()) {
+        T2.allocate(rc_header_size);
+        tsw[0] = T2.final_sw;
+    } else {
         // rate control per tile (TileProcessor::pcrdBisectSimple runs per tile): many tiles run
         // side by side on one thread each, a few run one after the other on the whole pool
         const bool par = te - tb >= host_pool().size();
@@ -2802,6 +2908,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             T2Enc Tt(P, hinfo, hpasses, t, t + 1);
             Tt.serial = par;
             Tt.allocate(rc_header_size);
+            tsw[q] = Tt.final_sw;
             const TileG& TG = P.tiles[t];
             std::copy(Tt.lnp.begin() + (size_t)TG.b0 * T2.L, Tt.lnp.begin() + (size_t)TG.b1 * T2.L,
                       T2.lnp.begin() + (size_t)TG.b0 * T2.L);
@@ -2847,6 +2954,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const bool par_chains = te - tb == 1;   // one tile: its precinct chains run in parallel instead
     auto build_tile_part = [&](uint32_t t, TileOut& O) {
         const TileG& T = P.tiles[t];
+        const T2Enc::Swallow& sw = tsw[t - tb];
         // A (resolution, component, precinct) chain owns its code-blocks and tag trees, so chains
         // are independent; within a chain the layers are sequential (T2 state carries over).
         struct Chain { uint32_t r, c, pi; };
@@ -2930,15 +3038,16 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             // (the given progressions)
             if (part == 0 && !P.p.pocs.empty()) write_poc(tp, P.p.pocs, P.nc, &P, t == 0 ? P.p.prog : ~0u);
             if (P.p.plt && part == 0) {   // PacketLengthMarkers::write (PacketLengthMarkers.cpp:107-175): Zplt 0, 7-bit groups MSB first
-                // the lengths come from the final simulation (compressPacketSimulate :427-428), so
-                // with progression order changes they are listed in the tile's own progression
+                // the lengths come from the final simulation (compressPacketSimulate :427-428):
+                // with progression order changes they are listed in the tile's own progression,
+                // and a swallowed failure there counted its packet's header as Grok's BitIO did
                 std::vector<uint32_t> lens;
-                if (!TPS.poc) {
-                    for (const Pk& k : O.pk) lens.push_back(k.len);
-                } else {
-                    const uint32_t ovh = ((P.p.sop_eph & 2) ? 6 : 0) + ((P.p.sop_eph & 4) ? 2 : 0);
-                    for (const PacketRef& pr : packet_order(P, T, L))
-                        lens.push_back(co[chain_at[pr.r * P.nc + pr.c] + pr.pi].pk[pr.l].len + ovh);
+                const uint32_t ovh = ((P.p.sop_eph & 2) ? 6 : 0) + ((P.p.sop_eph & 4) ? 2 : 0);
+                for (const PacketRef& pr : packet_order(P, T, L)) {
+                    uint32_t len = co[chain_at[pr.r * P.nc + pr.c] + pr.pi].pk[pr.l].len + ovh;
+                    if (sw.on && pr.c == sw.c && pr.r == sw.r && pr.pi == sw.pi && pr.l == sw.l)
+                        len = (uint32_t)(len + sw.hcnt - sw.hreal);
+                    lens.push_back(len);
                 }
                 std::vector<uint8_t> v;
                 for (const uint32_t len : lens) {
@@ -2952,6 +3061,9 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             put16(tp, 0xff93);
             uint64_t psot = tp.size() - h0;
             for (size_t q = pk0; q < pk1; ++q) psot += O.pk[q].len;
+            // a tile in one part with one progression writes the length TileProcessor precalculated
+            // from the final simulation (canPreCalculateTileLen, TileProcessor.cpp:54-57, 243-259)
+            if (TPS.n == 1 && sw.on) psot = psot + sw.hcnt - sw.hreal;
             if (psot > 0xffffffffull) throw GkError("tile part exceeds 4 GiB");
             tp[h0 + 6] = (uint8_t)(psot >> 24); tp[h0 + 7] = (uint8_t)(psot >> 16); tp[h0 + 8] = (uint8_t)(psot >> 8);
             tp[h0 + 9] = (uint8_t)psot;
@@ -3124,6 +3236,53 @@ static void check_override_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, 
         throw GkError(tile ? "tile-part COD/COC/QCD/QCC that differ from the main header are not supported on this path"
                            : "COC/QCC that differ from COD/QCD are not supported on this path");
 }
+// The tiles of the canvas tile grid (B.3)
+static uint32_t grid_tiles(const Plan& W) {
+    const uint64_t tw = W.p.tw ? W.p.tw : 1, th = W.p.th ? W.p.th : 1;
+    return (uint32_t)(((uint64_t)W.x0 + W.w - W.gx0 + tw - 1) / tw * (((uint64_t)W.y0 + W.h - W.gy0 + th - 1) / th));
+}
+// A tile part's end from its Psot, checked: the next SOT (Lsot 10, a tile index of the grid) or
+// EOC must start there, or the stream end.  Grok writes Psot (and TLM) from its rate-control
+// simulation's count when its BitIO swallowed a budget failure, a few bytes
+// off the part's real length; the nearest such marker within 8 bytes is taken instead.
+static size_t resync_part_end(ByteSrc& S, size_t pos, size_t end, uint32_t nt) {
+    auto ok = [&](size_t q) {
+        if (q == S.len || (q + 2 == S.len && S.be16(q) == 0xffd9)) return true;
+        return q + 12 <= S.len && S.be16(q) == 0xff90 && S.be16(q + 2) == 10 && S.be16(q + 4) < nt;
+    };
+    if (end <= S.len && ok(end)) return end;
+    for (size_t d = 1; d <= 8; ++d) {
+        if (end >= pos + 14 + d && end - d <= S.len && ok(end - d)) return end - d;
+        if (end + d <= S.len && ok(end + d)) return end + d;
+    }
+    return end;
+}
+// The tile parts by the SOT chain (Psot of each), their tile-part header markers read
+template <class Hdr> static void walk_sot_chain(ByteSrc& S, Hdr& Hd) {
+    Plan& W = Hd.want;
+    const uint32_t nt = grid_tiles(W);
+    size_t pos = Hd.first_sot;
+    while (pos + 12 <= S.len && S.be16(pos) == 0xff90) {
+        const uint32_t isot = S.be16(pos + 4), psot = S.be32(pos + 6);
+        size_t end = psot ? pos + psot : (S.len >= 2 ? S.len - 2 : S.len);
+        if (end > S.len + 8 || end < pos + 14) throw GkError("corrupt SOT (Psot)");
+        end = resync_part_end(S, pos, end, nt);
+        if (end > S.len) throw GkError("corrupt SOT (Psot)");
+        size_t j = pos + 12;
+        std::vector<Poc> tpoc;
+        while (j + 4 <= end && S.be16(j) != 0xff93) {
+            if (S.be16(j) == 0xff5f) parse_poc(S, j + 4, S.be16(j + 2), W.nc, tpoc);   // tile-part POC
+            check_override_marker(S, j + 4, S.be16(j), S.be16(j + 2), Hd, true);
+            j += 2 + S.be16(j + 2);
+        }
+        if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
+        Hd.parts.push_back({isot, pos, j + 2, end, {}, {}, S.at(pos + 10), std::move(tpoc)});
+        pos = end;
+    }
+}
+// A TLM whose lengths do not lead from SOT to SOT (read_tile_part_headers)
+struct TlmMismatch : GkError { TlmMismatch() : GkError("TLM does not match the SOT markers") {} };
+
 static void parse_header(ByteSrc& S, Header& Hd) {
     size_t i = 0;
     if (S.len < 4 || S.be16(0) != 0xff4f) throw GkError("not a J2K codestream (no SOC)");
@@ -3245,23 +3404,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
         }
         if (!tlm_ok) { Hd.parts.clear(); pos = Hd.first_sot; }
     }
-    if (!tlm_ok) {
-        while (pos + 12 <= S.len && S.be16(pos) == 0xff90) {
-            const uint32_t isot = S.be16(pos + 4), psot = S.be32(pos + 6);
-            const size_t end = psot ? pos + psot : (S.len >= 2 ? S.len - 2 : S.len);
-            if (end > S.len || end < pos + 14) throw GkError("corrupt SOT (Psot)");
-            size_t j = pos + 12;
-            std::vector<Poc> tpoc;
-            while (j + 4 <= end && S.be16(j) != 0xff93) {
-                if (S.be16(j) == 0xff5f) parse_poc(S, j + 4, S.be16(j + 2), W.nc, tpoc);   // tile-part POC
-                check_override_marker(S, j + 4, S.be16(j), S.be16(j + 2), Hd, true);
-                j += 2 + S.be16(j + 2);
-            }
-            if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
-            Hd.parts.push_back({isot, pos, j + 2, end, {}, {}, S.at(pos + 10), std::move(tpoc)});
-            pos = end;
-        }
-    }
+    if (!tlm_ok) walk_sot_chain(S, Hd);
     if (Hd.parts.empty()) throw GkError("no tile parts");
     for (uint8_t v : W.p.roishift)   // Grok's RoiShiftHTFilter keeps only the sign of a shifted sample
         if (v && W.p.ht()) throw GkError("ROI with HTJ2K is not supported on this path");
@@ -3302,7 +3445,7 @@ static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
     for (auto& TP : Hd.parts) {
         if (TP.data) continue;
         if (S.be16(TP.sot) != 0xff90 || S.be16(TP.sot + 4) != TP.tile || S.be32(TP.sot + 6) != TP.end - TP.sot)
-            throw GkError("TLM does not match the SOT markers");
+            throw TlmMismatch();
         TP.tpsot = S.at(TP.sot + 10);
         size_t j = TP.sot + 12;
         while (j + 4 <= TP.end && S.be16(j) != 0xff93) {
@@ -3375,6 +3518,11 @@ static void merge_tile_parts(Header& Hd) {
     }
     const std::vector<Poc>& main_pocs = Hd.want.p.pocs;
     for (TilePart& H : out) {
+        // PLT lengths that do not add up to the tile's data are not used (R-BUG-8 streams)
+        uint64_t plt_sum = 0, data = H.end - H.data;
+        for (uint32_t v : H.plt) plt_sum += v;
+        for (auto& m : H.more) data += m.second - m.first;
+        if (!H.plt.empty() && plt_sum != data) H.plt.clear();
         if (!H.pocs.empty()) H.pocs.insert(H.pocs.begin(), main_pocs.begin(), main_pocs.end());
         if (H.pocs.size() > GK_MAXRLVLS) throw GkError("too many progression order changes (read_poc: at most 33)");
         if (!H.pocs.empty() || !main_pocs.empty()) H.plt.clear();
@@ -3422,7 +3570,8 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     const uint32_t red = ctx->dec_reduce;
     if (red >= P.p.numres) throw GkError("reduce must be less than the number of resolutions");
     if (red && win) throw GkError("reduced-resolution decode of a window is not supported");
-    if (win) {   // keep only the tile parts of tiles intersecting the window
+    auto keep_window = [&]() {   // keep only the tile parts of tiles intersecting the window
+        if (!win) return;
         if (win[0] >= win[2] || win[1] >= win[3] || win[2] > P.w || win[3] > P.h) throw GkError("bad decode window");
         std::vector<TilePart> keep;
         for (auto& TP : Hd.parts) {
@@ -3433,8 +3582,17 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         }
         Hd.parts.swap(keep);
         if (Hd.parts.empty()) throw GkError("no tile part intersects the window");
+    };
+    keep_window();
+    if (S.dev) {
+        try {
+            read_tile_part_headers(ctx, S, Hd);
+        } catch (const TlmMismatch&) {   // (R-BUG-8 streams) the SOT chain instead
+            Hd.parts.clear();
+            walk_sot_chain(S, Hd);
+            keep_window();
+        }
     }
-    if (S.dev) read_tile_part_headers(ctx, S, Hd);
     merge_tile_parts(Hd);
     if (S.dev) prefetch_packet_headers(ctx, S, P, Hd);
     // ---- tiles present, their rectangle, and the code-blocks that reach the output

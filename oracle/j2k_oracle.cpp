@@ -2951,6 +2951,23 @@ static bool restates_main(const uint8_t* b, uint32_t L, uint32_t m, uint32_t nc,
     return cod.size() > 5 && (v[cw] & 1) == (cod[0] & 1) && std::equal(v.begin() + cw + 1, v.end(), cod.begin() + 5, cod.end());
 }
 
+// A tile part's end from its Psot, checked: the next SOT (Lsot 10, a tile index below nt) or
+// EOC must start there, or the data end.  Grok writes Psot from its rate-control simulation's
+// count when its BitIO swallowed a failure, a few bytes off the part's
+// real length; the nearest such marker within 8 bytes is taken instead.
+static size_t resync_part_end(const uint8_t* cs, size_t len, size_t pos, size_t end, uint32_t nt) {
+    auto ok = [&](size_t q) {
+        if (q == len || (q + 2 == len && get16(cs + q) == 0xffd9)) return true;
+        return q + 12 <= len && get16(cs + q) == 0xff90 && get16(cs + q + 2) == 10 && get16(cs + q + 4) < nt;
+    };
+    if (end <= len && ok(end)) return end;
+    for (size_t d = 1; d <= 8; ++d) {
+        if (end >= pos + 14 + d && end - d <= len && ok(end - d)) return end - d;
+        if (end + d <= len && ok(end + d)) return end + d;
+    }
+    return end;
+}
+
 int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_t* H, uint32_t* NC, uint32_t* PREC) {
     size_t i = 0;
     if (len >= 12 && get32(cs) == 12 && get32(cs + 4) == 0x6a502020) {   // JP2: find the jp2c box
@@ -3038,7 +3055,9 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         const uint8_t* s = cs + pos + 4;
         uint32_t isot = get16(s), psot = get32(s + 2);
         size_t tile_end = psot ? pos + psot : len - 2;
-        if (tile_end > len || isot >= nt) return -5;
+        if (tile_end > len + 8 || isot >= nt) return -5;
+        tile_end = resync_part_end(cs, len, pos, tile_end, nt);
+        if (tile_end > len) return -5;
         size_t j = pos + 12;   // tile-part header markers (PLT, POC, ...) until SOD
         std::vector<PocE> tp_pocs;
         while (j + 2 <= tile_end && get16(cs + j) != 0xff93) {

@@ -117,10 +117,12 @@ POCS = [
 
 @pytest.mark.parametrize("pi", range(len(POCS)))
 def test_progression_order_changes(eng, pi):
-    """POC (A.6.6; PacketIter over the tile's progressions, update_include): a POC marker in
-    each tile's first tile-part header (CodeStreamCompress::writePoc), packets ordered entry
-    by entry, each once.  Encode byte-identical to the oracle, decodes equal (whole, window,
-    PCRD layers through the serial simulation)."""
+    """POC (A.6.6; PacketIter over the tile's progressions, update_include) as Grok writes it:
+    tile 0's list in the main header and in each tile's first tile part, one tile part per
+    entry (CodeStreamCompress.cpp:839-840, 870-875, 902-946), packets entry by entry, each once
+    (overlapping entries: the later ones' parts skip what was written), the rate control's
+    simulation in the tile's own progression.  Encode byte-identical to the oracle, decodes
+    equal (whole, window)."""
     import grok_amd as G
     img = _img(20 + pi, 3, 150, 170)
     for kw in (dict(tiles=(64, 96), plt=True, tlm=True), dict(precincts=[(32, 32)], layer_rate=[20, 5, 0])):

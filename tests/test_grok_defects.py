@@ -1,0 +1,71 @@
+"""Grok 9.2.0 defects found by the reviews and what this
+repository does instead, checked on the CPU: the oracle's streams against the source image and
+cross-decoded by OpenJPEG 2.5.4 (Pillow), an independent decoder.
+
+  R-BUG-5  -T 5,3 -t 128,128 (tile grid offset): Grok's "lossless" stream decodes to 41.3 dB in
+           Grok, the oracle and OpenJPEG.  Ours is lossless in all three senses below.
+  R-BUG-6  HT -M 64 -t 100,70 (odd-parity tiles, mono16): Grok's stream decodes to 18.1 dB.
+  R-BUG-7  -t 24,40: Grok's decoder gives 23.1 dB on a stream (byte-equal to ours) that the
+           oracle and OpenJPEG decode losslessly.
+  R-BUG-8  rate control whose budget is reached inside a number-of-passes / comma code: Grok's
+           simulation misses the failure and writes SOT Psot / TLM / PLT lengths from its own
+           count, a few bytes off the tile part.  Reproduced byte for byte (the known answers in
+           test_oracle_grok_sizes.py); OpenJPEG rejects such streams, the oracle (and the engine,
+           test_gpu_grok_known.py) resynchronise on the next SOT.
+"""
+import io
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import parse_flags
+from grok_amd.synth import synth_image
+
+Image = pytest.importorskip("PIL.Image")
+
+
+def _openjpeg(cs):
+    im = Image.open(io.BytesIO(cs))
+    im.load()
+    a = np.asarray(im).astype(np.int64)
+    return a.transpose(2, 0, 1) if a.ndim == 3 else a[None]
+
+
+def _psnr(a, b, peak):
+    mse = ((np.asarray(a, np.float64) - b) ** 2).mean()
+    return float("inf") if mse == 0 else 10 * np.log10(peak ** 2 / mse)
+
+
+@pytest.mark.parametrize("args,bits,flags", [
+    ((384, 520, 3, 8, 7), 8, "-T 5,3 -t 128,128"),     # R-BUG-5
+    ((300, 260, 1, 16, 21), 16, "-M 64 -t 100,70"),    # R-BUG-6
+    ((384, 520, 3, 8, 7), 8, "-t 24,40"),              # R-BUG-7
+])
+def test_lossless_where_grok_is_not(args, bits, flags):
+    img = synth_image(*args).astype(np.int32)
+    cs = O.encode(img, bits, **parse_flags(flags))
+    dec, _ = O.decode(cs)
+    np.testing.assert_array_equal(dec, img)
+    np.testing.assert_array_equal(_openjpeg(cs), img)
+
+
+@pytest.mark.parametrize("flags", ["-t 64,64 -r 40,10", "-t 64,64 -r 40,10 -X -L"])
+def test_simulation_counted_lengths_decode(flags):
+    # R-BUG-8: at least one tile part's Psot does not lead to the next marker; the oracle's
+    # decode resynchronises and gives the layers' quality (about 30.7 dB at 40:1 / 10:1)
+    img = synth_image(384, 520, 3, 8, 7).astype(np.int32)
+    cs = O.encode(img, 8, **parse_flags(flags))
+    pos, bad = cs.find(b"\xff\x90"), 0
+    while cs[pos:pos + 2] == b"\xff\x90":
+        nxt = pos + int.from_bytes(cs[pos + 6:pos + 10], "big")
+        if cs[nxt:nxt + 2] not in (b"\xff\x90", b"\xff\xd9"):
+            bad += 1
+            nxt = min((q for q in range(nxt - 8, nxt + 9) if cs[q:q + 2] in (b"\xff\x90", b"\xff\xd9")),
+                      key=lambda q: abs(q - nxt))
+        pos = nxt
+    assert bad >= 1
+    dec, _ = O.decode(cs)
+    assert _psnr(dec, img, 255) > 30.5
+    with pytest.raises(Exception):   # OpenJPEG 2.5.4: "broken data stream"
+        _openjpeg(cs)
