@@ -30,7 +30,6 @@ With --gpus N > 1 and no WORLD_SIZE in the environment the script starts N rank
 processes itself (torch.distributed.run) before touching the GPU.
 """
 import argparse
-import glob
 import json
 import os
 import socket
@@ -150,18 +149,30 @@ def cpu_baseline(nthreads):
                                              "single-precinct 8K streams)", **GROK_CPU}}
 
 
+def profile_file(config, kind):
+    """The committed counter summary bench.py reports for (config, kind = "pmc" | "sq"): the file
+    named in profiles/current.json ({"C2_pmc": "r05_C2_pmc.json", ...}, written with the profiles
+    of the build they were measured on), else None.  An explicit manifest, not the newest-sorting
+    name, so adding a profile never silently changes which counters a bench line carries."""
+    man = os.path.join(ROOT, "profiles", "current.json")
+    try:
+        name = json.load(open(man)).get("%s_%s" % (config, kind))
+    except (OSError, ValueError):
+        return None
+    f = os.path.join(ROOT, "profiles", name) if name else None
+    return f if f and os.path.exists(f) else None
+
+
 def ht_issue_roofline(stages, config="C4"):
     """Issue roofline of the HTJ2K coders (one lane per code-block, branchy per-lane chains):
-    instructions issued per wave (VALU + SALU + LDS) from the newest committed SQ counter summary
-    of this config (profiles/rNN_<config>_sq.json, tools/sq_counters.sh + tools/sq_summary.py),
+    instructions issued per wave (VALU + SALU + LDS) from the committed SQ counter summary of this
+    config named in profiles/current.json (tools/sq_counters.sh + tools/sq_summary.py),
     times 4 cycles (a lone wave issues one instruction per 4 cycles), times the waves a SIMD
     holds (ceil(waves / 1,024)), over the live coder time.  None if no summary exists."""
-    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "*_sq.json"))
-                    if os.path.basename(f).lower().endswith("_%s_sq.json" % config.lower())),
-                   key=lambda p: os.path.basename(p).lower())
-    if not files:
+    f = profile_file(config, "sq")
+    if not f:
         return None
-    d = json.load(open(files[-1]))
+    d = json.load(open(f))
     out = {}
     for kern, ms_key in (("k_ht_dec", "dec_t1_coder_ms"), ("k_ht_enc", "enc_t1_coder_ms")):
         if kern not in d or not stages.get(ms_key):
@@ -174,20 +185,18 @@ def ht_issue_roofline(stages, config="C4"):
                      "instructions_per_wave": round(insts), "waves": int(k["waves"]), "waves_per_simd": per_simd,
                      "floor_ms": round(floor_ms, 3), "measured_ms": round(stages[ms_key], 3),
                      "frac": round(floor_ms / stages[ms_key], 3),
-                     "wait_any": round(k["wait_any"], 3), "source": os.path.basename(files[-1])}
+                     "wait_any": round(k["wait_any"], 3), "source": os.path.basename(f)}
     return out or None
 
 
 def pmc_traffic(kernels, config="C2"):
-    """HBM bytes per launch of `kernels` from the newest committed PMC summary of this config
-    (profiles/rNN_<config>_pmc.json, written by tools/pmc_summary.py from rocprofv3 --pmc
+    """HBM bytes per launch of `kernels` from the committed PMC summary of this config named in
+    profiles/current.json (written by tools/pmc_summary.py from rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE passes of this benchmark, tools/gpu_profile_all.sh; FETCH_SIZE
     doubled per MI355X_MICROARCH.md's gfx950 note).  (None, None) if no summary exists."""
-    files = [f for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))
-             if os.path.basename(f).lower().endswith("_%s_pmc.json" % config.lower())]
-    if not files:
+    f = profile_file(config, "pmc")
+    if not f:
         return None, None
-    f = sorted(files, key=lambda p: os.path.basename(p).lower())[-1]
     d = json.load(open(f))
     tot = 0.0
     for k in kernels:

@@ -124,21 +124,40 @@ def encode_sharded(dist, rank, world, encode_tiles, main_header, ntx, nty, devic
     return assemble(header, tlm, parts)
 
 
+TLM_MAX_ENTRIES = (0xFFFF - 4) // 6   # Ltlm is 16 bits: 10,921 six-byte entries per marker
+
+
 def retlm(header, entries):
-    """The main header with its TLM marker rewritten to list exactly `entries` [(tile, Psot)]
-    (Ttlm u16, Ptlm u32: Stlm = 0x60, TileLengthMarkers::writeBegin).  A rank's sub-stream
+    """The main header with its TLM markers replaced by ones listing exactly `entries`
+    [(tile, Psot)] (Ttlm u16, Ptlm u32: Stlm = 0x60, TileLengthMarkers::writeBegin), split over
+    consecutive markers (Ztlm 0, 1, ...) of at most 10,921 entries each.  A rank's sub-stream
     (main header + its own tile parts) then carries a TLM that matches it.  Headers without
     TLM are returned unchanged."""
     h = bytes(header)
-    i = 2
+    i, first, out = 2, None, [h[:2]]
     while i + 4 <= len(h):
         m, L = struct.unpack(">HH", h[i:i + 4])
+        if m == SOT:
+            break
         if m == TLM:
-            seg = struct.pack(">HHBB", TLM, 4 + 6 * len(entries), 0, 0x60) + \
-                b"".join(struct.pack(">HI", t, n) for t, n in entries)
-            return h[:i] + seg + h[i + 2 + L:]
+            if first is None:
+                first = len(out)
+                out.append(b"")   # the new markers go where the first one was
+        else:
+            out.append(h[i:i + 2 + L])
         i += 2 + L
-    return h
+    out.append(h[i:])
+    if first is None:
+        return h
+    segs = []
+    for z, k in enumerate(range(0, max(len(entries), 1), TLM_MAX_ENTRIES)):
+        chunk = entries[k:k + TLM_MAX_ENTRIES]
+        if z > 255:
+            raise ValueError("more than 256 TLM markers")
+        segs.append(struct.pack(">HHBB", TLM, 4 + 6 * len(chunk), z, 0x60) +
+                    b"".join(struct.pack(">HI", t, n) for t, n in chunk))
+    out[first] = b"".join(segs)
+    return b"".join(out)
 
 
 def _scatter_bytes(dist, rank, world, payloads, device):
@@ -246,7 +265,8 @@ def parse_main_header(head):
             break
         if m == SIZ:
             w, hh, x0, y0, tw, th, tx0, ty0, nc = struct.unpack(">IIIIIIIIH", h[i + 6:i + 40])
-            siz = dict(w=w - x0, h=hh - y0, tw=tw, th=th, nc=nc)
+            # the image area [x0, w) x [y0, hh) of the canvas, the tile grid anchored at (tx0, ty0)
+            siz = dict(w=w - x0, h=hh - y0, tw=tw, th=th, nc=nc, x0=x0, y0=y0, tx0=tx0, ty0=ty0)
         elif m == TLM:
             stlm = h[i + 5]
             st, sp = (stlm >> 4) & 3, (stlm >> 6) & 1
@@ -312,13 +332,20 @@ def _tensor(b, device):
     return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(device)
 
 
-def _scatter_tensors(dist, rank, world, parts, device):
+def _scatter_tensors(dist, rank, world, parts, device, error=None):
     """Rank 0's list of per-rank uint8 tensors to every rank (lengths, then the payloads padded
-    to the longest): returns (this rank's buffer, its length)."""
+    to the longest): returns (this rank's buffer, its length).  error (rank 0): an exception
+    rank 0 met while building `parts`: every rank then raises it (the lengths carry -1), so no
+    rank waits in a collective rank 0 never enters."""
     import torch
     n = torch.zeros(1, dtype=torch.int64, device=device)
-    dist.scatter(n, [torch.tensor([int(p.numel())], dtype=torch.int64, device=device) for p in parts]
-                 if rank == 0 else None, src=0)
+    ns = None
+    if rank == 0:
+        ns = [torch.tensor([-1 if error is not None else int(p.numel())], dtype=torch.int64, device=device)
+              for p in (parts if error is None else range(world))]
+    dist.scatter(n, ns, src=0)
+    if int(n.item()) < 0:
+        raise error if error is not None else RuntimeError("rank 0 could not build the sub-streams")
     mx = n.clone()
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     mx = max(int(mx.item()), 1)
@@ -450,23 +477,29 @@ class TileRowShard:
         return cs, int(cs.numel())
 
     def substreams(self, cs, n):
-        """Rank 0: per-rank sub-streams of the codestream cs[:n], located through its TLM."""
+        """Rank 0: per-rank sub-streams of the codestream cs[:n], located through its TLM: the
+        main header with a TLM of the rank's tile parts, those parts in stream order (each
+        located on its own, so tile parts that interleave across tiles stay right), EOC."""
         off, hl, siz, ent, hdr = _read_header(cs, n)
         if not ent:
             raise ValueError("sharded decode needs a TLM marker to locate the tile parts")
-        pos, where = off + hl, {}
+        if siz["x0"] or siz["y0"] or siz["tx0"] or siz["ty0"]:
+            raise ValueError("tile-row sharding of a stream with image / tile-grid offsets is not supported")
+        owner = {t: r for r, (tb, te, _, _) in enumerate(self.ranges) for t in range(tb, te)}
+        pos, mine_of = off + hl, [[] for _ in self.ranges]
         for t, L in ent:
-            where.setdefault(t, []).append((pos, L))
+            if t in owner:
+                mine_of[owner[t]].append((t, pos, L))
             pos += L
+        if pos > n:
+            raise ValueError("TLM lengths run past the codestream")
         subs = []
-        for tb, te, _, _ in self.ranges:
-            mine = [(t, p, L) for t in range(tb, te) for p, L in where.get(t, [])]
+        for mine in mine_of:
             if not mine:
                 subs.append(cs[:0])
                 continue
-            # a rank's tiles are contiguous in the stream: one slice
-            a, b = mine[0][1], mine[-1][1] + mine[-1][2]
-            subs.append(torch_cat([_tensor(retlm(hdr, [(t, L) for t, _, L in mine]), cs.device), cs[a:b], self.eoc]))
+            subs.append(torch_cat([_tensor(retlm(hdr, [(t, L) for t, _, L in mine]), cs.device)] +
+                                  [cs[p:p + L] for _, p, L in mine] + [self.eoc]))
         return subs
 
     def decode(self, cs, n, out_slab, full=None, gather=True):
@@ -477,8 +510,13 @@ class TileRowShard:
             if gather and full is not None and full.data_ptr() != out_slab.data_ptr():
                 full.copy_(out_slab)
             return
-        subs = self.substreams(cs, n) if self.rank == 0 else None
-        sub, m = _scatter_tensors(self.dist, self.rank, self.world, subs, self.device)
+        subs, err = None, None
+        if self.rank == 0:
+            try:
+                subs = self.substreams(cs, n)
+            except (ValueError, struct.error) as e:
+                err = e
+        sub, m = _scatter_tensors(self.dist, self.rank, self.world, subs, self.device, err)
         if self.y1 > self.y0:
             self.coder.decode_rows(sub, m, out_slab, self.y0)
         if gather:
@@ -502,31 +540,41 @@ class WindowShard:
         self.dist, self.rank, self.world, self.coder, self.device = dist, rank, world, coder, device
         self.file, self.n = file, n
         self.eoc = torch.tensor([0xFF, 0xD9], dtype=torch.uint8, device=device)
+        meta = torch.zeros(8, dtype=torch.int64, device=device)
+        err = None
         if rank == 0:
-            off, hl, siz, ent, hdr = _read_header(file, n)
-            self.hdr, self.siz = hdr, siz
-            pos, self.where = off + hl, {}
-            for t, L in ent:
-                self.where.setdefault(t, []).append((pos, L))
-                pos += L
-            if not ent:
-                raise ValueError("window sharding needs a TLM marker")
-        meta = torch.zeros(3, dtype=torch.int64, device=device)
-        if rank == 0:
-            meta[:] = torch.tensor([self.siz["tw"], self.siz["th"], self.siz["w"]])
+            try:
+                off, hl, siz, ent, hdr = _read_header(file, n)
+                if not ent:
+                    raise ValueError("window sharding needs a TLM marker")
+                self.hdr, self.siz = hdr, siz
+                pos, self.where = off + hl, {}
+                for t, L in ent:
+                    self.where.setdefault(t, []).append((pos, L))
+                    pos += L
+                meta[:7] = torch.tensor([siz[k] for k in ("tw", "th", "w", "x0", "y0", "tx0", "ty0")])
+                meta[7] = 1
+            except (ValueError, struct.error) as e:   # every rank raises below, none waits
+                err = e
         if world > 1:
             dist.broadcast(meta, 0)
-        self.tw, self.th, self.W = (int(v) for v in meta.tolist())
+        if not int(meta[7].item()):
+            raise err if err is not None else RuntimeError("rank 0 could not read the window stream's header")
+        self.tw, self.th, self.W, self.X0, self.Y0, self.TX0, self.TY0 = (int(v) for v in meta[:7].tolist())
 
     def bands(self, win):
+        """The window's rows [y0, y1) (image coordinates) split into per-rank bands along tile
+        rows of the canvas grid: tile row j covers canvas rows [TY0 + j th, TY0 + (j+1) th)."""
         x0, y0, x1, y1 = win
-        j0, j1 = y0 // self.th, (y1 - 1) // self.th + 1
+        j0 = (y0 + self.Y0 - self.TY0) // self.th
+        j1 = (y1 - 1 + self.Y0 - self.TY0) // self.th + 1
+        edge = lambda j: self.TY0 + j * self.th - self.Y0   # image row where tile row j starts
         per, extra = divmod(j1 - j0, self.world)
         out = []
         for r in range(self.world):
             a = j0 + r * per + min(r, extra)
             b = a + per + (1 if r < extra else 0)
-            out.append((max(y0, a * self.th), min(y1, b * self.th)) if b > a else (y0, y0))
+            out.append((max(y0, edge(a)), min(y1, edge(b))) if b > a else (y0, y0))
         return out
 
     def decode(self, win, out, band_buf=None):
@@ -539,14 +587,17 @@ class WindowShard:
         bands = self.bands(win)
         subs = None
         if self.rank == 0:
-            ntx = (self.W + self.tw - 1) // self.tw
-            i0, i1 = x0 // self.tw, (x1 - 1) // self.tw + 1
+            # canvas tile grid (B.3): ntx columns from TX0 to the image's right edge X0 + W
+            ntx = (self.X0 + self.W - self.TX0 + self.tw - 1) // self.tw
+            cx, cy = self.X0 - self.TX0, self.Y0 - self.TY0   # image -> grid coordinates
+            i0, i1 = (x0 + cx) // self.tw, (x1 - 1 + cx) // self.tw + 1
             subs = []
             for a, b in bands:
                 if b <= a:
                     subs.append(self.file[:0])
                     continue
-                tiles = [j * ntx + i for j in range(a // self.th, (b - 1) // self.th + 1) for i in range(i0, i1)]
+                tiles = [j * ntx + i for j in range((a + cy) // self.th, (b - 1 + cy) // self.th + 1)
+                         for i in range(i0, i1)]
                 mine = [(t, p, L) for t in tiles for p, L in self.where.get(t, [])]
                 subs.append(torch_cat([_tensor(retlm(self.hdr, [(t, L) for t, _, L in mine]), self.device)] +
                                       [self.file[p:p + L] for _, p, L in mine] + [self.eoc]))
