@@ -16,14 +16,15 @@
 #include <stdint.h>
 #include "gk_common.h"
 #include "gk_xcd.h"
+#include "gk_vec.h"
 
 #pragma clang fp contract(off)
 
 #define T97_W 128
 #define T97_H 32
 #define T97_HALO 4
-#define T97_LW (T97_W + 2 * T97_HALO)
-#define T97_LH (T97_H + 2 * T97_HALO)
+#define T97_LW (T97_W + 2 * T97_HALO)   // 136
+#define T97_LH (T97_H + 2 * T97_HALO)   // 40
 
 // WaveletFwd.cpp:39-44 (float constants; invK computed in double then rounded)
 #define F97_A (-1.586134342f)
@@ -113,10 +114,26 @@ __global__ __launch_bounds__(256) void k_dc_inv_f(const float* __restrict__ in, 
 // Forward 9/7, one level (WaveletFwd.cpp:964-1025): vertical then horizontal.
 // Components in grid.z (GkComps); level 1 fused with DC + ICT (k_dwt97_fwd_l1) and the
 // last inverse level with the inverse ICT + DC + clamp (k_dwt97_inv_l1), as for the 5/3.
+//
+// The tile is 136 x 40 samples in LDS (a 4-sample halo around the 128 x 32 outputs).  Work is
+// mapped without index division: a wave takes rows (ty, ty + 4, ...), its lanes columns tx and
+// tx + 64, and the few halo columns / rows past 64 updates go in one extra pass.  The scalings
+// are folded into neighbouring passes, multiplying each value exactly where Grok's separate
+// pass would have (the same float products, so the results are unchanged):
+//  * forward: the vertical K / 1/K of a row into horizontal steps 0 and 1 (every value those
+//    steps read is scaled as it is read until step 1 has written it), the horizontal one into
+//    the store;
+//  * inverse: the horizontal K / 2/K into the fill, the vertical one into vertical steps 0
+//    and 1 in the same way.
+// Interior tiles (no mirrored sample) read and write the caller's planes four samples per lane.
 // =============================================================================
 typedef float Lds97[T97_LH][T97_LW + 1];
 
-// f(ly, lx, gy, gx): the sample at mirrored input position (gy, gx) into LDS (ly, lx)
+__device__ __forceinline__ bool interior97(int x0, int y0, int w, int h) {
+    return x0 >= T97_HALO && y0 >= T97_HALO && x0 + T97_W + T97_HALO <= w && y0 + T97_H + T97_HALO <= h;
+}
+
+// f(ly, lx, gy, gx): the sample at mirrored input position (gy, gx) into LDS (ly, lx) (edge tiles)
 template <class F>
 __device__ __forceinline__ void fwd97_fill(int x0, int y0, int w, int h, int tid, F f) {
     for (int i = tid; i < T97_LH * T97_LW; i += 256) {
@@ -124,65 +141,86 @@ __device__ __forceinline__ void fwd97_fill(int x0, int y0, int w, int h, int tid
         f(ly, lx, mirror97(y0 - T97_HALO + ly, h), mirror97(x0 - T97_HALO + lx, w));
     }
 }
-
-__device__ __forceinline__ void fwd97_lift(Lds97& T, int w, int h, int tid) {
-    // local row ly <-> global y0 - 4 + ly; parity of global y == parity of ly (y0 even)
-    if (h > 1) {
-        const float cs[4] = {F97_A, F97_B, F97_G, F97_D};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int par = (s & 1) ? 0 : 1;          // alpha/gamma update odd rows, beta/delta even rows
-            const int lo = 1 + s, hi = T97_LH - 2 - s;  // rows with both neighbours still valid
-            const int first = lo + ((lo & 1) != par);
-            const int nrows = first > hi ? 0 : (hi - first) / 2 + 1;
-            for (int i = tid; i < nrows * T97_LW; i += 256) {
-                int ly = first + 2 * (i / T97_LW), lx = i % T97_LW;
-                float t = (T[ly - 1][lx] + T[ly + 1][lx]) * cs[s];
-                T[ly][lx] = T[ly][lx] + t;
-            }
-            __syncthreads();
-        }
-        for (int i = tid; i < T97_H * T97_LW; i += 256) {
-            int ly = T97_HALO + i / T97_LW, lx = i % T97_LW;
-            T[ly][lx] = T[ly][lx] * ((ly & 1) ? F97_K : F97_INVK);
-        }
-        __syncthreads();
+// interior tile: LDS columns 4..131 by the lanes, halo columns 0..3 / 132..135 in one pass
+template <class F>
+__device__ __forceinline__ void fwd97_fill_inner(int x0, int y0, int tid, F f) {
+    const int tx = tid & 63, ty = tid >> 6;
+    for (int ly = ty; ly < T97_LH; ly += 4) {
+        f(ly, 4 + tx, y0 - T97_HALO + ly, x0 + tx);
+        f(ly, 68 + tx, y0 - T97_HALO + ly, x0 + 64 + tx);
     }
-    if (w > 1) {
-        const float cs[4] = {F97_A, F97_B, F97_G, F97_D};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int par = (s & 1) ? 0 : 1;
-            const int lo = 1 + s, hi = T97_LW - 2 - s;
-            const int first = lo + ((lo & 1) != par);
-            const int ncols = first > hi ? 0 : (hi - first) / 2 + 1;
-            for (int i = tid; i < T97_H * ncols; i += 256) {
-                int ly = T97_HALO + i / ncols, lx = first + 2 * (i % ncols);
-                float t = (T[ly][lx - 1] + T[ly][lx + 1]) * cs[s];
-                T[ly][lx] = T[ly][lx] + t;
-            }
-            __syncthreads();
-        }
-        for (int i = tid; i < T97_H * T97_W; i += 256) {
-            int ly = T97_HALO + i / T97_W, lx = T97_HALO + i % T97_W;
-            T[ly][lx] = T[ly][lx] * ((lx & 1) ? F97_K : F97_INVK);
-        }
-        __syncthreads();
+    for (int i = tid; i < 8 * T97_LH; i += 256) {
+        const int ly = i >> 3, j = i & 7, lx = j < 4 ? j : 128 + j;
+        f(ly, lx, y0 - T97_HALO + ly, x0 - T97_HALO + lx);
     }
 }
 
+__device__ __forceinline__ void fwd97_lift(Lds97& T, int w, int h, int tid) {
+    const int tx = tid & 63, ty = tid >> 6;
+    // local row ly <-> global y0 - 4 + ly; parity of global y == parity of ly (y0 even)
+    if (h > 1) {
+        // step s (alpha, beta, gamma, delta) updates rows 1 + s, 3 + s, ... (19 - s rows) of every column
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const float c = s == 0 ? F97_A : (s == 1 ? F97_B : (s == 2 ? F97_G : F97_D));
+            const int first = 1 + s, nrows = 19 - s;
+            auto upd = [&](int ly, int lx) {
+                const float t = (T[ly - 1][lx] + T[ly + 1][lx]) * c;
+                T[ly][lx] = T[ly][lx] + t;
+            };
+            for (int m = ty; m < nrows; m += 4) { upd(first + 2 * m, tx); upd(first + 2 * m, 64 + tx); }
+            if (tid < nrows * 8) upd(first + 2 * (tid >> 3), 128 + (tid & 7));
+            __syncthreads();
+        }
+        if (w <= 1) {   // no horizontal pass to fold the scaling into
+            for (int i = tid; i < T97_H * T97_LW; i += 256) {
+                const int ly = T97_HALO + i / T97_LW, lx = i % T97_LW;
+                T[ly][lx] = T[ly][lx] * ((ly & 1) ? F97_K : F97_INVK);
+            }
+            __syncthreads();
+        }
+    }
+    if (w > 1) {
+        const bool vs = h > 1;   // the vertical scaling of rows 4..35 is still to apply
+        // step s updates columns 1 + s, 3 + s, ... (67 - s columns) of the output rows 4..35
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const float c = s == 0 ? F97_A : (s == 1 ? F97_B : (s == 2 ? F97_G : F97_D));
+            const int first = 1 + s, e = 3 - s;   // e: columns past the lanes' 64
+            auto upd = [&](int ly, int lx) {
+                const float f = vs ? ((ly & 1) ? F97_K : F97_INVK) : 1.0f;
+                if (s == 0 && vs) {   // nothing in the row is scaled yet
+                    const float t = (T[ly][lx - 1] * f + T[ly][lx + 1] * f) * c;
+                    T[ly][lx] = T[ly][lx] * f + t;
+                } else if (s == 1 && vs) {   // the odd columns are (step 0 wrote them)
+                    const float t = (T[ly][lx - 1] + T[ly][lx + 1]) * c;
+                    T[ly][lx] = T[ly][lx] * f + t;
+                } else {
+                    const float t = (T[ly][lx - 1] + T[ly][lx + 1]) * c;
+                    T[ly][lx] = T[ly][lx] + t;
+                }
+            };
+            for (int ly = T97_HALO + ty; ly < T97_HALO + T97_H; ly += 4) upd(ly, first + 2 * tx);
+            if (e && tid < T97_H * e) upd(T97_HALO + tid / e, first + 2 * (64 + tid % e));
+            __syncthreads();
+        }
+    }
+}
+
+// the four Mallat quadrants; the horizontal scaling (K odd, 1/K even columns) on the way out
 __device__ __forceinline__ void fwd97_store(const Lds97& T, float* __restrict__ dst, uint32_t dstride, int x0, int y0,
                                             int w, int h, int tid) {
+    const int tx = tid & 63, ty = tid >> 6;
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
-    for (int i = tid; i < T97_H * T97_W; i += 256) {
-        int ry = i / T97_W, rx = i % T97_W;
-        int q = rx / (T97_W / 2), k = rx % (T97_W / 2);
-        int gx = x0 + 2 * k + q, gy = y0 + ry;
-        if (gx >= w || gy >= h) continue;
-        float v = T[ry + T97_HALO][2 * k + q + T97_HALO];
-        int ox = (q == 0) ? (gx >> 1) : (snw + (gx >> 1));
-        int oy = ((gy & 1) == 0) ? (gy >> 1) : (snh + (gy >> 1));
-        dst[(size_t)oy * dstride + ox] = v;
+    const float fl = w > 1 ? F97_INVK : 1.0f, fh = w > 1 ? F97_K : 1.0f;
+    const int gx = x0 + 2 * tx;
+    for (int ry = ty; ry < T97_H; ry += 4) {
+        const int gy = y0 + ry;
+        if (gy >= h) break;
+        const int oy = ((gy & 1) == 0) ? (gy >> 1) : (snh + (gy >> 1));
+        float* drow = dst + (size_t)oy * dstride;
+        if (gx < w) drow[gx >> 1] = T[ry + T97_HALO][T97_HALO + 2 * tx] * fl;
+        if (gx + 1 < w) drow[snw + (gx >> 1)] = T[ry + T97_HALO][T97_HALO + 1 + 2 * tx] * fh;
     }
 }
 
@@ -195,21 +233,24 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict
     src += tb.offset(tile, sstride) + comp * cs.cstride;
     dst += tb.offset(tile, dstride) + comp * cs.cstride;
     const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
-    fwd97_fill(x0, y0, (int)w, (int)h, tid,
-               [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; });
+    auto ld = [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; };
+    if (interior97(x0, y0, (int)w, (int)h)) fwd97_fill_inner(x0, y0, tid, ld);
+    else fwd97_fill(x0, y0, (int)w, (int)h, tid, ld);
     __syncthreads();
     fwd97_lift(T, (int)w, (int)h, tid);
     fwd97_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
 }
 
 // Level 1 from the caller's planes: DC shift and, for NC = 3, the ICT (mct.cpp:147-219) on load.
-// One LDS tile: Y goes first while each thread keeps U and V of its positions in registers
-// (22 slots = ceil(40 x 136 / 256)), then U, then V (as k_dwt53_fwd_l1).
-#define L97_SLOTS 22
-template <class F>   // f(slot, ly, lx, gy, gx) over fwd97_fill's positions
+// One LDS tile: Y goes first while each thread keeps U and V of its positions in registers,
+// then U, then V (as k_dwt53_fwd_l1).  Interior tiles: six groups of four consecutive samples per
+// thread (five of the 40 x 32 main groups, one of the 80 halo groups), one vector load per group
+// and plane; edge tiles: 22 mirrored positions per thread.
+#define L97_SLOTS 24
+template <class F>   // f(slot, ly, lx, gy, gx): edge-tile positions, slot < 22
 __device__ __forceinline__ void fwd97_fill_slots(int x0, int y0, int w, int h, int tid, F f) {
 #pragma unroll
-    for (int k = 0; k < L97_SLOTS; ++k) {
+    for (int k = 0; k < 22; ++k) {
         const int i = tid + 256 * k;
         if (i < T97_LH * T97_LW) {
             const int ly = i / T97_LW, lx = i % T97_LW;
@@ -217,11 +258,20 @@ __device__ __forceinline__ void fwd97_fill_slots(int x0, int y0, int w, int h, i
         }
     }
 }
+template <class F>   // f(group, ly, lx): interior groups of four positions (ly, lx .. lx + 3)
+__device__ __forceinline__ void fwd97_groups(int tid, F f) {
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {
+        const int i = tid + 256 * g;
+        if (g < 5) f(g, i >> 5, T97_HALO + 4 * (i & 31));
+        else if (tid < 2 * T97_LH) f(g, tid >> 1, (tid & 1) ? T97_HALO + T97_W : 0);
+    }
+}
 
 template <class TI, int NC>
 __global__ __launch_bounds__(256) void k_dwt97_fwd_l1(GkPtr3 in, uint32_t sin, float* __restrict__ dst, uint64_t cstride,
                                                       uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb,
-                                                      int32_t shift) {
+                                                      int32_t shift, int vec) {
     __shared__ Lds97 T;
     const uint3 bi = xcd_tile();
     const uint32_t tile = bi.z;
@@ -232,22 +282,39 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_l1(GkPtr3 in, uint32_t sin, f
     dst += tb.offset(tile, dstride);
     const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
     float U[L97_SLOTS], V[L97_SLOTS];
-    fwd97_fill_slots(x0, y0, (int)w, (int)h, tid, [&](int k, int ly, int lx, int gy, int gx) {
-        const size_t i = (size_t)gy * sin + gx;
+    auto put = [&](int k, int ly, int lx, int32_t r0, int32_t g0, int32_t b0) {
         if (NC == 3) {
             const float a_r = 0.299f, a_g = 0.587f, a_b = 0.114f;
             const float cb = 0.5f / (1.0f - a_b), cr = 0.5f / (1.0f - a_r);
-            const float r = (float)((int32_t)p0[i] - shift), g = (float)((int32_t)p1[i] - shift),
-                        b = (float)((int32_t)p2[i] - shift);
+            const float r = (float)(r0 - shift), g = (float)(g0 - shift), b = (float)(b0 - shift);
             const float t0 = a_r * r, t1 = a_g * g, t2 = a_b * b;
             const float Y = (t0 + t1) + t2;
             T[ly][lx] = Y;
             U[k] = cb * (b - Y);
             V[k] = cr * (r - Y);
         } else {
-            T[ly][lx] = (float)((int32_t)p0[i] - shift);
+            T[ly][lx] = (float)(r0 - shift);
         }
-    });
+    };
+    const bool inner = interior97(x0, y0, (int)w, (int)h);
+    if (inner) {
+        // (x0 is a multiple of 128, so every group is aligned when the plane rows are)
+        const bool v = vec && al4(p0) && al4(p1) && al4(p2);
+        fwd97_groups(tid, [&](int g, int ly, int lx) {
+            const size_t i = (size_t)(y0 - T97_HALO + ly) * sin + (x0 - T97_HALO + lx);
+            const int4 a = ld4v(p0 + i, v);
+            const int4 b = NC == 3 ? ld4v(p1 + i, v) : a, c = NC == 3 ? ld4v(p2 + i, v) : a;
+            put(4 * g, ly, lx, a.x, b.x, c.x);
+            put(4 * g + 1, ly, lx + 1, a.y, b.y, c.y);
+            put(4 * g + 2, ly, lx + 2, a.z, b.z, c.z);
+            put(4 * g + 3, ly, lx + 3, a.w, b.w, c.w);
+        });
+    } else {
+        fwd97_fill_slots(x0, y0, (int)w, (int)h, tid, [&](int k, int ly, int lx, int gy, int gx) {
+            const size_t i = (size_t)gy * sin + gx;
+            put(k, ly, lx, (int32_t)p0[i], (int32_t)p1[i], (int32_t)p2[i]);
+        });
+    }
     __syncthreads();
     fwd97_lift(T, (int)w, (int)h, tid);
     fwd97_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
@@ -255,8 +322,15 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_l1(GkPtr3 in, uint32_t sin, f
 #pragma unroll
         for (int c = 1; c < 3; ++c) {
             __syncthreads();
-            fwd97_fill_slots(x0, y0, (int)w, (int)h, tid,
-                             [&](int k, int ly, int lx, int, int) { T[ly][lx] = c == 1 ? U[k] : V[k]; });
+            if (inner) {
+                fwd97_groups(tid, [&](int g, int ly, int lx) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) T[ly][lx + j] = c == 1 ? U[4 * g + j] : V[4 * g + j];
+                });
+            } else {
+                fwd97_fill_slots(x0, y0, (int)w, (int)h, tid,
+                                 [&](int k, int ly, int lx, int, int) { T[ly][lx] = c == 1 ? U[k] : V[k]; });
+            }
             __syncthreads();
             fwd97_lift(T, (int)w, (int)h, tid);
             fwd97_store(T, dst + c * cstride, dstride, x0, y0, (int)w, (int)h, tid);
@@ -268,54 +342,74 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_l1(GkPtr3 in, uint32_t sin, f
 // Inverse 9/7, one level (WaveletReverse.cpp:1010-1022, 1272-1351):
 // horizontal then vertical, on the interleaved signal.
 // =============================================================================
+// f(ly, lx, sy, sx, fac): interleaved position (ly, lx) from Mallat position (sy, sx), times the
+// horizontal scaling of its column (2/K odd, K even; 1 when there is no horizontal pass)
 template <class F>
 __device__ __forceinline__ void inv97_fill(int x0, int y0, int w, int h, int tid, F f) {
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
-    for (int i = tid; i < T97_LH * T97_LW; i += 256) {
-        int ly = i / T97_LW, lx = i % T97_LW;
-        int gy = mirror97(y0 - T97_HALO + ly, h), gx = mirror97(x0 - T97_HALO + lx, w);
-        f(ly, lx, (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1), (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1));
+    const float fe = w > 1 ? F97_K : 1.0f, fo = w > 1 ? I97_TWO_INVK : 1.0f;
+    if (interior97(x0, y0, w, h)) {
+        // even interleaved columns (lx even) are L samples x0/2 - 2 + lx/2, odd ones H samples
+        const int tx = tid & 63, ty = tid >> 6, hx = x0 >> 1;
+        for (int ly = ty; ly < T97_LH; ly += 4) {
+            const int gy = y0 - T97_HALO + ly, sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
+            f(ly, T97_HALO + 2 * tx, sy, hx + tx, fe);
+            f(ly, T97_HALO + 1 + 2 * tx, sy, snw + hx + tx, fo);
+        }
+        for (int i = tid; i < 8 * T97_LH; i += 256) {
+            const int ly = i >> 3, j = i & 7, lx = j < 4 ? j : 128 + j;
+            const int gy = y0 - T97_HALO + ly, sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
+            f(ly, lx, sy, (lx & 1) ? snw + hx - 2 + (lx >> 1) : hx - 2 + (lx >> 1), (lx & 1) ? fo : fe);
+        }
+    } else {
+        for (int i = tid; i < T97_LH * T97_LW; i += 256) {
+            const int ly = i / T97_LW, lx = i % T97_LW;
+            const int gy = mirror97(y0 - T97_HALO + ly, h), gx = mirror97(x0 - T97_HALO + lx, w);
+            f(ly, lx, (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1), (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1), (lx & 1) ? fo : fe);
+        }
     }
 }
 
 __device__ __forceinline__ void inv97_lift(Lds97& T, int w, int h, int tid) {
-    const float cs[4] = {I97_D, I97_G, I97_B, I97_A};
+    const int tx = tid & 63, ty = tid >> 6;
     if (w > 1) {
-        for (int i = tid; i < T97_LH * T97_LW; i += 256) {
-            int ly = i / T97_LW, lx = i % T97_LW;
-            T[ly][lx] = T[ly][lx] * ((lx & 1) ? I97_TWO_INVK : F97_K);
-        }
-        __syncthreads();
+        // step s (delta, gamma, beta, alpha) updates columns 2 + s, 4 + s, ... (67 - s) of every row
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            const int par = (s & 1) ? 1 : 0;            // delta/beta on even samples, gamma/alpha on odd
-            const int lo = 1 + s, hi = T97_LW - 2 - s;
-            const int first = lo + ((lo & 1) != par);
-            const int ncols = first > hi ? 0 : (hi - first) / 2 + 1;
-            for (int i = tid; i < T97_LH * ncols; i += 256) {
-                int ly = i / ncols, lx = first + 2 * (i % ncols);
-                float t = (T[ly][lx - 1] + T[ly][lx + 1]) * cs[s];
+            const float c = s == 0 ? I97_D : (s == 1 ? I97_G : (s == 2 ? I97_B : I97_A));
+            const int first = 2 + s, e = 3 - s;
+            auto upd = [&](int ly, int lx) {
+                const float t = (T[ly][lx - 1] + T[ly][lx + 1]) * c;
                 T[ly][lx] = T[ly][lx] + t;
-            }
+            };
+            for (int ly = ty; ly < T97_LH; ly += 4) upd(ly, first + 2 * tx);
+            if (e && tid < T97_LH * e) upd(tid / e, first + 2 * (64 + tid % e));
             __syncthreads();
         }
     }
     if (h > 1) {
-        for (int i = tid; i < T97_LH * T97_W; i += 256) {
-            int ly = i / T97_W, lx = T97_HALO + i % T97_W;
-            T[ly][lx] = T[ly][lx] * ((ly & 1) ? I97_TWO_INVK : F97_K);
-        }
-        __syncthreads();
+        // step s updates rows 2 + s, 4 + s, ... (19 - s rows) of the output columns 4..131; the
+        // vertical scaling (2/K odd, K even rows) of every value steps 0 and 1 read is applied as
+        // it is read, until that step has written it
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            const int par = (s & 1) ? 1 : 0;
-            const int lo = 1 + s, hi = T97_LH - 2 - s;
-            const int first = lo + ((lo & 1) != par);
-            const int nrows = first > hi ? 0 : (hi - first) / 2 + 1;
-            for (int i = tid; i < nrows * T97_W; i += 256) {
-                int ly = first + 2 * (i / T97_W), lx = T97_HALO + i % T97_W;
-                float t = (T[ly - 1][lx] + T[ly + 1][lx]) * cs[s];
-                T[ly][lx] = T[ly][lx] + t;
+            const float c = s == 0 ? I97_D : (s == 1 ? I97_G : (s == 2 ? I97_B : I97_A));
+            const int first = 2 + s, nrows = 19 - s;
+            auto upd = [&](int ly, int lx) {
+                if (s == 0) {   // even row, odd neighbours: nothing scaled yet
+                    const float t = (T[ly - 1][lx] * I97_TWO_INVK + T[ly + 1][lx] * I97_TWO_INVK) * c;
+                    T[ly][lx] = T[ly][lx] * F97_K + t;
+                } else if (s == 1) {   // odd row; its even neighbours were written by step 0
+                    const float t = (T[ly - 1][lx] + T[ly + 1][lx]) * c;
+                    T[ly][lx] = T[ly][lx] * I97_TWO_INVK + t;
+                } else {
+                    const float t = (T[ly - 1][lx] + T[ly + 1][lx]) * c;
+                    T[ly][lx] = T[ly][lx] + t;
+                }
+            };
+            for (int m = ty; m < nrows; m += 4) {
+                upd(first + 2 * m, T97_HALO + tx);
+                upd(first + 2 * m, T97_HALO + 64 + tx);
             }
             __syncthreads();
         }
@@ -331,25 +425,30 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict
     src += tb.offset(tile, sstride) + comp * cs.cstride;
     dst += tb.offset(tile, dstride) + comp * cs.cstride;
     const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
+    const int tx = tid & 63, ty = tid >> 6;
     inv97_fill(x0, y0, (int)w, (int)h, tid,
-               [&](int ly, int lx, int sy, int sx) { T[ly][lx] = src[(size_t)sy * sstride + sx]; });
+               [&](int ly, int lx, int sy, int sx, float f) { T[ly][lx] = src[(size_t)sy * sstride + sx] * f; });
     __syncthreads();
     inv97_lift(T, (int)w, (int)h, tid);
-    for (int i = tid; i < T97_H * T97_W; i += 256) {
-        int ry = i / T97_W, rx = i % T97_W;
-        int gx = x0 + rx, gy = y0 + ry;
-        if (gx >= (int)w || gy >= (int)h) continue;
-        dst[(size_t)gy * dstride + gx] = T[ry + T97_HALO][rx + T97_HALO];
+    for (int ry = ty; ry < T97_H; ry += 4) {
+        const int gy = y0 + ry;
+        if (gy >= (int)h) break;
+        float* drow = dst + (size_t)gy * dstride + x0;
+        if (x0 + tx < (int)w) drow[tx] = T[ry + T97_HALO][T97_HALO + tx];
+        if (x0 + 64 + tx < (int)w) drow[64 + tx] = T[ry + T97_HALO][T97_HALO + 64 + tx];
     }
 }
 
 // Last inverse level into the caller's planes: inverse ICT for NC = 3 (mct.cpp:284-364,
 // lrintf rounding), DC shift and clamp, only inside the output window (GkWin).  One LDS
-// tile; the Y and U results of each thread's 16 output samples wait in registers.
+// tile; the Y and U results of each thread's 16 output samples wait in registers.  A thread
+// owns four groups of four consecutive columns (row i >> 5, columns 4 (i & 31) .. + 3 of
+// group i = tid + 256 j), written as one vector store per plane where the window and the
+// planes allow.
 template <class TO, int NC>
 __global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ src, uint64_t cstride, uint32_t sstride,
                                                       GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h,
-                                                      GkTiles tb, int32_t shift, int32_t mn, int32_t mx) {
+                                                      GkTiles tb, int32_t shift, int32_t mn, int32_t mx, int vec) {
     __shared__ Lds97 T;
     const uint3 bi = xcd_tile();
     const uint32_t tile = bi.z;
@@ -357,43 +456,59 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ 
     int32_t ox, oy;
     tb.origin(tile, ox, oy);
     const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
-    float R0[16], R1[16];   // sample i = tid + 256 k of the 32 x 128 output tile
+    float R0[16], R1[16];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         if (c) __syncthreads();
         const float* sc = src + c * cstride;
         inv97_fill(x0, y0, (int)w, (int)h, tid,
-                   [&](int ly, int lx, int sy, int sx) { T[ly][lx] = sc[(size_t)sy * sstride + sx]; });
+                   [&](int ly, int lx, int sy, int sx, float f) { T[ly][lx] = sc[(size_t)sy * sstride + sx] * f; });
         __syncthreads();
         inv97_lift(T, (int)w, (int)h, tid);
         if (c + 1 < NC) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int i = tid + 256 * k;
-                (c == 0 ? R0 : R1)[k] = T[i / T97_W + T97_HALO][i % T97_W + T97_HALO];
+            for (int j = 0; j < 4; ++j) {
+                const int i = tid + 256 * j;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    (c == 0 ? R0 : R1)[4 * j + e] = T[(i >> 5) + T97_HALO][4 * (i & 31) + e + T97_HALO];
             }
         }
     }
     TO* o0 = (TO*)out.p[0];
     TO* o1 = (TO*)out.p[NC == 3 ? 1 : 0];
     TO* o2 = (TO*)out.p[NC == 3 ? 2 : 0];
-    auto cl = [&](float f) { int32_t v = (int32_t)rintf(f) + shift; return (TO)(v < mn ? mn : (v > mx ? mx : v)); };
+    auto cl = [&](float f) { int32_t v = (int32_t)rintf(f) + shift; return v < mn ? mn : (v > mx ? mx : v); };
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int i = tid + 256 * k;
-        const int ry = i / T97_W, rx = i % T97_W;
-        const int gx = x0 + rx, gy = y0 + ry, X = ox + gx, Y = oy + gy;
-        if (gx >= (int)w || gy >= (int)h || X < win.x0 || X >= win.x1 || Y < win.y0 || Y >= win.y1) continue;
+    for (int j = 0; j < 4; ++j) {
+        const int i = tid + 256 * j, ry = i >> 5, rx = 4 * (i & 31);
+        const int gy = y0 + ry, gx = x0 + rx, X = ox + gx, Y = oy + gy;
+        if (gy >= (int)h || Y < win.y0 || Y >= win.y1) continue;
+        int32_t r[4], g[4], b[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float last = T[ry + T97_HALO][rx + e + T97_HALO];
+            if (NC == 3) {
+                const float Yv = R0[4 * j + e], U = R1[4 * j + e], V = last;
+                const float R = Yv + 1.402f * V;
+                const float G = (Yv - 0.34413f * U) - 0.71414f * V;
+                const float B = Yv + 1.772f * U;
+                r[e] = cl(R); g[e] = cl(G); b[e] = cl(B);
+            } else {
+                r[e] = cl(last);
+            }
+        }
         const size_t o = (size_t)(Y - win.y0) * ostride + (X - win.x0);
-        const float last = T[ry + T97_HALO][rx + T97_HALO];
-        if (NC == 3) {
-            const float Yv = R0[k], U = R1[k], V = last;
-            const float R = Yv + 1.402f * V;
-            const float G = (Yv - 0.34413f * U) - 0.71414f * V;
-            const float B = Yv + 1.772f * U;
-            o0[o] = cl(R); o1[o] = cl(G); o2[o] = cl(B);
+        if (vec && gx + 3 < (int)w && X >= win.x0 && X + 3 < win.x1 && ((X - win.x0) & 3) == 0) {
+            st4(o0 + o, make_int4(r[0], r[1], r[2], r[3]));
+            if (NC == 3) { st4(o1 + o, make_int4(g[0], g[1], g[2], g[3])); st4(o2 + o, make_int4(b[0], b[1], b[2], b[3])); }
         } else {
-            o0[o] = cl(last);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (gx + e >= (int)w || X + e < win.x0 || X + e >= win.x1) continue;
+                o0[o + e] = (TO)r[e];
+                if (NC == 3) { o1[o + e] = (TO)g[e]; o2[o + e] = (TO)b[e]; }
+            }
         }
     }
 }
@@ -456,22 +571,24 @@ void gk_launch_dwt97_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32
                             uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb, int32_t shift) {
     if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
+    const int vec = (sin & 3) == 0;   // (the kernel checks each tile's row pointers)
     if (nc == 3)
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_fwd_l1<T, 3>), grid, dim3(256), 0, st, in, sin, dst,
-                                                        cstride, dstride, w, h, tb, shift))
+                                                        cstride, dstride, w, h, tb, shift, vec))
     else
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_fwd_l1<T, 1>), grid, dim3(256), 0, st, in, sin, dst,
-                                                        cstride, dstride, w, h, tb, shift))
+                                                        cstride, dstride, w, h, tb, shift, vec))
 }
 void gk_launch_dwt97_inv_l1(hipStream_t st, int stype, int nc, const float* src, uint64_t cstride, uint32_t sstride,
                             GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
                             int32_t mn, int32_t mx) {
     if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count());
+    const int vec = gk_vec_ok(gk_sample_size(stype), out, nc, ostride);
     if (nc == 3)
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_inv_l1<T, 3>), grid, dim3(256), 0, st, src, cstride,
-                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx))
+                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx, vec))
     else
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt97_inv_l1<T, 1>), grid, dim3(256), 0, st, src, cstride,
-                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx))
+                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx, vec))
 }

@@ -29,6 +29,10 @@
 #include <vector>
 #include <queue>
 #include <map>
+#include <climits>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "../../include/grok_amd.h"
 #include "gk_common.h"
@@ -70,57 +74,83 @@ static int engines_on(int dev) {
 
 // Persistent host worker pool for the T2 stages (tiles, precinct chains, blocks).
 // run(n, f) calls f(0..n-1) across the workers and the caller, and returns when all
-// calls finished; the first GkError thrown by any call is rethrown.
+// calls finished; the first GkError thrown by any call is rethrown.  Host phases are short (a
+// rate-control bisection step is ~100 us on 16 threads), so a dispatch must cost little:
+//  * items are claimed from a (generation, index) word and run() waits for the items to
+//    finish, not for every worker to have woken (a worker that wakes after its generation's
+//    items are all claimed never touches that job);
+//  * workers sleep on the generation word itself (futex), so a wake-up takes no mutex: with a
+//    mutex and a condition variable, 15 woken workers queued on the mutex the next dispatch
+//    needed.  Empty dispatch on the GPU box (tools/pcrd_bench.cpp): ~30 us with
+//    notify_all and a wait for every worker, ~12 us with item completion alone.
 class HostPool {
     std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    const std::function<void(size_t)>* job_ = nullptr;
-    std::atomic<size_t> next_{0};
-    size_t n_ = 0;
-    int busy_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::atomic<const std::function<void(size_t)>*> job_{nullptr};   // published before gen_ (release)
+    std::atomic<size_t> n_{0};
+    std::atomic<uint32_t> gen_{0};           // futex word: a new job
+    std::atomic<uint64_t> claim_{0};         // generation << 32 | next item
+    std::atomic<size_t> done_{0};            // items of the current generation finished
+    std::atomic<uint32_t> fin_{0};           // futex word: the caller sleeps until done_ == n
+    std::atomic<bool> stop_{false}, has_err_{false};
+    std::mutex err_m_;
     std::string err_;
     std::mutex run_m_;
-    void drain(const std::function<void(size_t)>& f, size_t n) {
+    static void fwait(std::atomic<uint32_t>& w, uint32_t v) {
+        syscall(SYS_futex, reinterpret_cast<uint32_t*>(&w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+    }
+    static void fwake(std::atomic<uint32_t>& w) {
+        syscall(SYS_futex, reinterpret_cast<uint32_t*>(&w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+    }
+    int64_t claim(uint32_t g, size_t n) {    // an item of generation g, or -1
+        uint64_t c = claim_.load(std::memory_order_acquire);
         for (;;) {
-            const size_t i = next_.fetch_add(1);
-            if (i >= n) break;
-            try { f(i); } catch (const GkError& e) {
-                std::lock_guard<std::mutex> lk(m_);
-                if (err_.empty()) err_ = e.msg;
+            if ((uint32_t)(c >> 32) != g || (c & 0xffffffffull) >= n) return -1;
+            if (claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel)) return (int64_t)(c & 0xffffffffull);
+        }
+    }
+    void fail(const std::string& e) {
+        std::lock_guard<std::mutex> lk(err_m_);
+        if (err_.empty()) err_ = e;
+        has_err_ = true;
+    }
+    void work(uint32_t g, const std::function<void(size_t)>& f, size_t n) {
+        for (int64_t i; (i = claim(g, n)) >= 0;) {
+            try { f((size_t)i); } catch (const GkError& e) {
+                fail(e.msg);
             } catch (const std::exception& e) {   // e.g. std::bad_alloc: recorded, never escapes a worker
-                std::lock_guard<std::mutex> lk(m_);
-                if (err_.empty()) err_ = std::string("host worker: ") + e.what();
+                fail(std::string("host worker: ") + e.what());
             } catch (...) {
-                std::lock_guard<std::mutex> lk(m_);
-                if (err_.empty()) err_ = "host worker: unknown exception";
+                fail("host worker: unknown exception");
+            }
+            if (done_.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {   // the last item
+                fin_.fetch_add(1, std::memory_order_release);
+                fwake(fin_);
             }
         }
     }
     void worker() {
-        uint64_t seen = 0;
+        uint32_t seen = 0;
         for (;;) {
-            const std::function<void(size_t)>* f;
-            size_t n;
-            {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_; f = job_; n = n_;
-            }
-            drain(*f, n);
-            std::lock_guard<std::mutex> lk(m_);
-            if (--busy_ == 0) done_.notify_all();
+            uint32_t g;
+            while ((g = gen_.load(std::memory_order_acquire)) == seen && !stop_.load(std::memory_order_acquire)) fwait(gen_, seen);
+            if (stop_.load(std::memory_order_acquire)) return;
+            seen = g;
+            // job_ / n_ of generation g (written before gen_); a later generation may have
+            // replaced them already, and then every claim of g fails and f is not called
+            const std::function<void(size_t)>* f = job_.load(std::memory_order_relaxed);
+            const size_t n = n_.load(std::memory_order_relaxed);
+            const uint64_t c = claim_.load(std::memory_order_acquire);
+            if ((uint32_t)(c >> 32) != g) continue;
+            work(g, *f, n);
         }
     }
 
 public:
     explicit HostPool(unsigned k) { for (unsigned i = 0; i < k; ++i) th_.emplace_back([this] { worker(); }); }
     ~HostPool() {
-        { std::lock_guard<std::mutex> lk(m_); stop_ = true; }
-        cv_.notify_all();
+        stop_.store(true, std::memory_order_release);
+        gen_.fetch_add(1, std::memory_order_release);
+        fwake(gen_);
         for (auto& t : th_) t.join();
     }
     unsigned size() const { return (unsigned)th_.size() + 1; }
@@ -129,16 +159,26 @@ public:
     void run(size_t n, const std::function<void(size_t)>& f) {
         if (n == 0) return;
         std::unique_lock<std::mutex> own(run_m_, std::try_to_lock);
-        if (n == 1 || th_.empty() || !own.owns_lock()) { for (size_t i = 0; i < n; ++i) f(i); return; }
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            job_ = &f; n_ = n; next_ = 0; busy_ = (int)th_.size(); ++gen_; err_.clear();
+        if (n == 1 || th_.empty() || !own.owns_lock() || n > 0xffffffffull) { for (size_t i = 0; i < n; ++i) f(i); return; }
+        { std::lock_guard<std::mutex> lk(err_m_); err_.clear(); }
+        has_err_ = false;
+        job_.store(&f, std::memory_order_relaxed);
+        n_.store(n, std::memory_order_relaxed);
+        done_.store(0, std::memory_order_relaxed);
+        const uint32_t g = gen_.load(std::memory_order_relaxed) + 1;
+        claim_.store((uint64_t)g << 32, std::memory_order_release);
+        gen_.store(g, std::memory_order_release);
+        fwake(gen_);
+        work(g, f, n);
+        for (uint32_t v; done_.load(std::memory_order_acquire) != n;) {   // items still running on workers
+            v = fin_.load(std::memory_order_acquire);
+            if (done_.load(std::memory_order_acquire) == n) break;
+            fwait(fin_, v);
         }
-        cv_.notify_all();
-        drain(f, n);
-        std::unique_lock<std::mutex> lk(m_);
-        done_.wait(lk, [&] { return busy_ == 0; });
-        if (!err_.empty()) throw GkError(err_);
+        if (has_err_.load(std::memory_order_acquire)) {
+            std::lock_guard<std::mutex> lk(err_m_);
+            throw GkError(err_);
+        }
     }
 };
 static HostPool& host_pool() {   // one pool per process, sized to the CPU share (at most 16 threads)
@@ -1584,11 +1624,12 @@ struct T2Enc {
             for (uint32_t u = 0; u < (uint32_t)units.size(); ++u) {
                 const uint32_t fb = unit_prec(units[u]).first_block;
                 for (uint32_t k = 0; k < units[u].nblk; k += kChunk)
-                    chunks.push_back({u, fb + k, fb + std::min(units[u].nblk, k + kChunk), {}, {}, 0});
+                    chunks.push_back({u, fb + k, fb + std::min(units[u].nblk, k + kChunk), {}, {}, 0, HUGE_VAL, -HUGE_VAL});
             }
         if (ulock.size() != units.size()) ulock = std::vector<std::mutex>(units.size());
         nact = 0;
         for (ChunkI& C : chunks) {
+            C.mslo = HUGE_VAL; C.mshi = -HUGE_VAL;
             C.act.resize(C.e - C.s);
             for (uint32_t b = C.s; b < C.e; ++b) C.act[b - C.s] = b;
             nact += C.act.size();
@@ -1668,7 +1709,12 @@ struct T2Enc {
     // unit's blocks (recount in parallel; changes applied under the unit's lock, since units
     // own disjoint trees and sums).
     // act: blocks whose count may still change; log: this step's changes (block, old count)
-    struct ChunkI { uint32_t u, s, e; std::vector<uint32_t> act, log; uint64_t hd; };
+    // mslo / mshi: the largest slo and smallest shi over the chunk's active blocks as the last
+    // step that ran it left them (+inf / -inf when some block has no valid interval): a
+    // threshold that passes the reuse test against both passes it for every active block
+    // (t - s and the comparisons are monotone in s), so the chunk keeps its counts unread
+    // (the early steps of a layer, thresholds far above every block's slopes)
+    struct ChunkI { uint32_t u, s, e; std::vector<uint32_t> act, log; uint64_t hd; double mslo, mshi; };
     static constexpr uint32_t kChunk = 512;
     std::vector<ChunkI> chunks;
     std::vector<std::mutex> ulock;               // per unit
@@ -1691,7 +1737,6 @@ struct T2Enc {
         }
     }
     uint64_t make_layer_inc(uint32_t l, double thresh, double lo, double hi, const std::vector<uint16_t>& prev) {
-        prof_act += nact;
 #ifdef PCRD_TRACE
         fprintf(stderr, "l %u t %.6g [%.6g, %.6g] active %zu\n", l, thresh, lo, hi, nact);
 #endif
@@ -1699,10 +1744,12 @@ struct T2Enc {
             ChunkI& C = chunks[c];
             C.hd = 0;
             if (C.act.empty()) return;
+            if (thresh > 0 && thresh - C.mshi < kEps && !(thresh - C.mslo < kEps)) return;
             thread_local std::vector<uint32_t> chg;   // (block, new count) pairs
             chg.clear();
             size_t w = 0;
             const size_t n = C.act.size();
+            double mslo = -HUGE_VAL, mshi = HUGE_VAL;
             for (size_t i = 0; i < n; ++i) {
                 const uint32_t b = C.act[i];
                 // the reuse test holds on an interval: at both ends, for every later threshold
@@ -1715,8 +1762,12 @@ struct T2Enc {
                 }
                 const uint32_t cur = lnp[(size_t)b * L + l], inc = count_at(b, thresh, prev[b], cur);
                 if (inc != prev[b] + cur) { chg.push_back(b); chg.push_back(inc); }
+                if (vld[b]) { mslo = std::max(mslo, slo[b]); mshi = std::min(mshi, shi[b]); }
+                else { mslo = HUGE_VAL; mshi = -HUGE_VAL; }
             }
             C.act.resize(w);
+            if (mslo == HUGE_VAL) mshi = -HUGE_VAL;   // (a block without an interval keeps the chunk live)
+            C.mslo = mslo; C.mshi = mshi;
             if (chg.empty()) return;
             const PrecG& PG = unit_prec(units[C.u]);
             std::lock_guard<std::mutex> lk(ulock[C.u]);
@@ -1736,7 +1787,11 @@ struct T2Enc {
             C.hd = hd;
         };
         const auto tp0 = std::chrono::steady_clock::now();
-        const bool par = nact >= 2048;
+        size_t nwork = 0;   // active blocks of the chunks the reuse test does not skip
+        for (const ChunkI& C : chunks)
+            if (!(thresh > 0 && thresh - C.mshi < kEps && !(thresh - C.mslo < kEps))) nwork += C.act.size();
+        const bool par = nwork >= 2048;
+        prof_act += nwork;
         if (par) prun(chunks.size(), run_chunk);
         else for (size_t c = 0; c < chunks.size(); ++c) run_chunk(c);
         const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count();

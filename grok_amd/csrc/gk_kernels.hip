@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include "gk_common.h"
 #include "gk_xcd.h"
+#include "gk_vec.h"
 
 #define LDS_BARRIER() __syncthreads()
 
@@ -19,19 +20,7 @@
 // Sample access for the caller's planes: int32 (Grok image components) or the
 // planar 8/16-bit buffers of grk_compress_tile (TileProcessor.cpp:779-835).
 // Four consecutive samples move as one vector access (16 B int32, 4 B u8,
-// 8 B u16) when the host found every pointer and stride aligned (vec != 0).
-// =============================================================================
-__device__ __forceinline__ int4 ld4(const int32_t* p) { return *(const int4*)p; }
-__device__ __forceinline__ int4 ld4(const uint8_t* p) { const uchar4 v = *(const uchar4*)p; return make_int4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ int4 ld4(const int8_t* p) { const char4 v = *(const char4*)p; return make_int4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ int4 ld4(const uint16_t* p) { const ushort4 v = *(const ushort4*)p; return make_int4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ int4 ld4(const int16_t* p) { const short4 v = *(const short4*)p; return make_int4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ void st4(int32_t* p, int4 v) { *(int4*)p = v; }
-__device__ __forceinline__ void st4(uint8_t* p, int4 v) { *(uchar4*)p = make_uchar4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ void st4(int8_t* p, int4 v) { *(char4*)p = make_char4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ void st4(uint16_t* p, int4 v) { *(ushort4*)p = make_ushort4(v.x, v.y, v.z, v.w); }
-__device__ __forceinline__ void st4(int16_t* p, int4 v) { *(short4*)p = make_short4(v.x, v.y, v.z, v.w); }
-
+// 8 B u16, gk_vec.h) when the host found every pointer and stride aligned (vec != 0).
 // =============================================================================
 // DC level shift + RCT (forward).  In: 3 caller planes (stride sin), out: 3
 // int32 work planes (stride sout).  mct.cpp:99-146, TileProcessor.cpp:506-535.
@@ -264,45 +253,32 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
 // Level 1 from the caller's planes: DC shift (TileProcessor.cpp:506-535) and, for NC = 3,
 // the RCT (mct.cpp:99-146) on load; outputs into the level-1 planes of the NC components
 // (dst + c * cstride).  One LDS tile: Y is transformed first while each thread keeps the U
-// and V of its input positions in registers (L1_SLOTS), then U, then V go through the same
-// tile, so a workgroup needs one LDS tile instead of three (occupancy).
-#define L1_ROWS ((DWT_LH + 3) / 4)                   // tile rows per thread (4 waves, interior)
-#define L1_SLOTS (2 * L1_ROWS + 1)                  // two columns per row + one halo column slot
+// and V of its input positions in registers, then U, then V go through the same tile, so a
+// workgroup needs one LDS tile instead of three (occupancy).  Interior tiles read the planes
+// four samples per lane: five groups of four consecutive samples per thread cover the 35 x 128
+// main positions (one vector load per group and plane, 128 contiguous samples per half wave),
+// one more slot the 3 x 35 halo columns; edge tiles take L1_EDGE mirrored positions per thread.
+#define L1_GROUPS 5                                 // ceil(35 x 32 / 256) groups of four
+#define L1_SLOTS (4 * L1_GROUPS + 1)                // + one halo column slot
 #define L1_EDGE ((DWT_LH * DWT_LW + 255) / 256)     // positions per thread on edge tiles
 static_assert(L1_EDGE <= L1_SLOTS, "edge-tile positions fit the register slots");
-template <class F>   // f(slot, ly, lx, gy, gx): the positions of fwd53_fill, slot = compile-time index
-__device__ __forceinline__ void fwd53_fill_slots(int x0, int y0, int w, int h, int tid, F f) {
-    const int tx = tid & 63, ty = tid >> 6;
-    if (x0 >= 2 && y0 >= 2 && x0 + DWT_TW < w && y0 + DWT_TH < h) {
+static_assert(32 * DWT_LH <= 256 * L1_GROUPS, "interior groups fit");
+__device__ __forceinline__ bool interior53(int x0, int y0, int w, int h) {
+    return x0 >= 2 && y0 >= 2 && x0 + DWT_TW < w && y0 + DWT_TH < h;
+}
+template <class F>   // f(group, ly, lx): interior groups of four positions (ly, lx .. lx + 3)
+__device__ __forceinline__ void fwd53_groups(int tid, F f) {
 #pragma unroll
-        for (int k = 0; k < L1_ROWS; ++k) {
-            const int ly = ty + 4 * k;
-            if (ly < DWT_LH) {
-                const int gy = y0 - 2 + ly;
-                f(2 * k, ly, tx + 2, gy, x0 + tx);
-                f(2 * k + 1, ly, tx + 66, gy, x0 + 64 + tx);
-            }
-        }
-        if (tid < 3 * DWT_LH) {
-            const int ly = tid / 3, lx = fwd53_halo_lx(tid % 3);
-            f(2 * L1_ROWS, ly, lx, y0 - 2 + ly, x0 - 2 + lx);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < L1_EDGE; ++k) {
-            const int i = tid + 256 * k;
-            if (i < DWT_LH * DWT_LW) {
-                const int ly = i / DWT_LW, lx = i % DWT_LW;
-                f(k, ly, lx, mirror(y0 - 2 + ly, h), mirror(x0 - 2 + lx, w));
-            }
-        }
+    for (int g = 0; g < L1_GROUPS; ++g) {
+        const int i = tid + 256 * g;
+        if (i < 32 * DWT_LH) f(g, i >> 5, 2 + 4 * (i & 31));
     }
 }
 
 template <class TI, int NC>
 __global__ __launch_bounds__(256) void k_dwt53_fwd_l1(GkPtr3 in, uint32_t sin, int32_t* __restrict__ dst,
                                                       uint64_t cstride, uint32_t dstride, uint32_t w, uint32_t h,
-                                                      GkTiles tb, int32_t shift) {
+                                                      GkTiles tb, int32_t shift, int vec) {
     __shared__ Lds53 T;
     const uint3 bi = xcd_tile();
     const uint32_t tile = bi.z;
@@ -313,17 +289,45 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_l1(GkPtr3 in, uint32_t sin, i
     dst += tb.offset(tile, dstride);
     const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
     int32_t U[L1_SLOTS], V[L1_SLOTS];
-    fwd53_fill_slots(x0, y0, (int)w, (int)h, tid, [&](int k, int ly, int lx, int gy, int gx) {
-        const size_t i = (size_t)gy * sin + gx;
+    auto put = [&](int k, int ly, int lx, int32_t r0, int32_t g0, int32_t b0) {
         if (NC == 3) {
-            const int32_t r = (int32_t)p0[i] - shift, g = (int32_t)p1[i] - shift, b = (int32_t)p2[i] - shift;
+            const int32_t r = r0 - shift, g = g0 - shift, b = b0 - shift;
             T[ly][lx] = (r + 2 * g + b) >> 2;
             U[k] = b - g;
             V[k] = r - g;
         } else {
-            T[ly][lx] = (int32_t)p0[i] - shift;
+            T[ly][lx] = r0 - shift;
         }
-    });
+    };
+    const bool inner = interior53(x0, y0, (int)w, (int)h);
+    if (inner) {
+        // (x0 is a multiple of 128, so every group is aligned when the plane rows are)
+        const bool v = vec && al4(p0) && al4(p1) && al4(p2);
+        fwd53_groups(tid, [&](int g, int ly, int lx) {
+            const size_t i = (size_t)(y0 - 2 + ly) * sin + (x0 - 2 + lx);
+            const int4 a = ld4v(p0 + i, v);
+            const int4 b = NC == 3 ? ld4v(p1 + i, v) : a, c = NC == 3 ? ld4v(p2 + i, v) : a;
+            put(4 * g, ly, lx, a.x, b.x, c.x);
+            put(4 * g + 1, ly, lx + 1, a.y, b.y, c.y);
+            put(4 * g + 2, ly, lx + 2, a.z, b.z, c.z);
+            put(4 * g + 3, ly, lx + 3, a.w, b.w, c.w);
+        });
+        if (tid < 3 * DWT_LH) {   // halo columns x0-2, x0-1, x0+TW
+            const int ly = tid / 3, lx = fwd53_halo_lx(tid % 3);
+            const size_t i = (size_t)(y0 - 2 + ly) * sin + (x0 - 2 + lx);
+            put(4 * L1_GROUPS, ly, lx, (int32_t)p0[i], (int32_t)p1[i], (int32_t)p2[i]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < L1_EDGE; ++k) {
+            const int i = tid + 256 * k;
+            if (i < DWT_LH * DWT_LW) {
+                const int ly = i / DWT_LW, lx = i % DWT_LW;
+                const size_t o = (size_t)mirror(y0 - 2 + ly, (int)h) * sin + mirror(x0 - 2 + lx, (int)w);
+                put(k, ly, lx, (int32_t)p0[o], (int32_t)p1[o], (int32_t)p2[o]);
+            }
+        }
+    }
     LDS_BARRIER();
     fwd53_lift(T, (int)w, (int)h, tid);
     fwd53_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
@@ -331,8 +335,19 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_l1(GkPtr3 in, uint32_t sin, i
 #pragma unroll
         for (int c = 1; c < 3; ++c) {
             LDS_BARRIER();   // the previous component's stores have read the tile
-            fwd53_fill_slots(x0, y0, (int)w, (int)h, tid,
-                             [&](int k, int ly, int lx, int, int) { T[ly][lx] = c == 1 ? U[k] : V[k]; });
+            if (inner) {
+                fwd53_groups(tid, [&](int g, int ly, int lx) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) T[ly][lx + j] = c == 1 ? U[4 * g + j] : V[4 * g + j];
+                });
+                if (tid < 3 * DWT_LH) T[tid / 3][fwd53_halo_lx(tid % 3)] = c == 1 ? U[4 * L1_GROUPS] : V[4 * L1_GROUPS];
+            } else {
+#pragma unroll
+                for (int k = 0; k < L1_EDGE; ++k) {
+                    const int i = tid + 256 * k;
+                    if (i < DWT_LH * DWT_LW) T[i / DWT_LW][i % DWT_LW] = c == 1 ? U[k] : V[k];
+                }
+            }
             LDS_BARRIER();
             fwd53_lift(T, (int)w, (int)h, tid);
             fwd53_store(T, dst + c * cstride, dstride, x0, y0, (int)w, (int)h, tid);
@@ -438,12 +453,14 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restri
 // Last inverse level into the caller's planes: inverse RCT for NC = 3 (mct.cpp:221-283),
 // DC shift and clamp (TileProcessor.cpp:457-504), samples of type TO, only inside the
 // output window (region coordinates [wx0, wx1) x [wy0, wy1); out.p[c] addresses (wx0, wy0)).
-// One LDS tile: the Y and U results of each thread's DWT_TH / 2 output samples wait in registers
-// while the next component goes through the tile.
+// One LDS tile: the Y and U results of each thread's 16 output samples wait in registers
+// while the next component goes through the tile.  A thread owns four groups of four
+// consecutive columns (row i >> 5, columns 4 (i & 31) .. + 3 of group i = tid + 256 j), written
+// as one vector store per plane where the window and the planes allow.
 template <class TO, int NC>
 __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict__ src, uint64_t cstride, uint32_t sstride,
                                                       GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h,
-                                                      GkTiles tb, int32_t shift, int32_t mn, int32_t mx) {
+                                                      GkTiles tb, int32_t shift, int32_t mn, int32_t mx, int vec) {
     __shared__ Lds53 T;
     const uint3 bi = xcd_tile();
     const uint32_t tile = bi.z;
@@ -451,8 +468,8 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
     int32_t ox, oy;
     tb.origin(tile, ox, oy);
     const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
-    const int tx = tid & 63, ty = tid >> 6;
-    int32_t R0[DWT_TH / 2], R1[DWT_TH / 2];   // this thread's samples (ry = ty + 4 (k >> 1), column tx + 64 (k & 1))
+    static_assert(DWT_TW * DWT_TH == 4 * 4 * 256, "four groups of four per thread");
+    int32_t R0[16], R1[16];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         if (c) LDS_BARRIER();   // the previous component's samples have been read
@@ -463,27 +480,46 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
         inv53_lift(T, (int)w, (int)h, tid);
         if (c + 1 < NC) {
 #pragma unroll
-            for (int k = 0; k < DWT_TH / 2; ++k) (c == 0 ? R0 : R1)[k] = T[ty + 4 * (k >> 1) + 1][tx + 64 * (k & 1) + 1];
+            for (int j = 0; j < 4; ++j) {
+                const int i = tid + 256 * j;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) (c == 0 ? R0 : R1)[4 * j + e] = T[(i >> 5) + 1][4 * (i & 31) + e + 1];
+            }
         }
     }
     TO* o0 = (TO*)out.p[0];
     TO* o1 = (TO*)out.p[NC == 3 ? 1 : 0];
     TO* o2 = (TO*)out.p[NC == 3 ? 2 : 0];
-    auto cl = [&](int32_t v) { return (TO)(v < mn ? mn : (v > mx ? mx : v)); };
+    auto cl = [&](int32_t v) { return v < mn ? mn : (v > mx ? mx : v); };
 #pragma unroll
-    for (int k = 0; k < DWT_TH / 2; ++k) {
-        const int ry = ty + 4 * (k >> 1), cx = tx + 64 * (k & 1);
-        const int gy = y0 + ry, Y = oy + gy, gx = x0 + cx, X = ox + gx;
-        if (gy >= (int)h || gx >= (int)w || Y < win.y0 || Y >= win.y1 || X < win.x0 || X >= win.x1) continue;
+    for (int j = 0; j < 4; ++j) {
+        const int i = tid + 256 * j, ry = i >> 5, rx = 4 * (i & 31);
+        const int gy = y0 + ry, Y = oy + gy, gx = x0 + rx, X = ox + gx;
+        if (gy >= (int)h || Y < win.y0 || Y >= win.y1) continue;
+        int32_t r[4], g[4], b[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int32_t last = T[ry + 1][rx + e + 1];
+            if (NC == 3) {
+                const int32_t G = R0[4 * j + e] - ((R1[4 * j + e] + last) >> 2);
+                r[e] = cl(last + G + shift);
+                g[e] = cl(G + shift);
+                b[e] = cl(R1[4 * j + e] + G + shift);
+            } else {
+                r[e] = cl(last + shift);
+            }
+        }
         const size_t o = (size_t)(Y - win.y0) * ostride + (X - win.x0);
-        const int32_t last = T[ry + 1][cx + 1];
-        if (NC == 3) {
-            const int32_t G = R0[k] - ((R1[k] + last) >> 2);
-            o0[o] = cl(last + G + shift);
-            o1[o] = cl(G + shift);
-            o2[o] = cl(R1[k] + G + shift);
+        if (vec && gx + 3 < (int)w && X >= win.x0 && X + 3 < win.x1 && ((X - win.x0) & 3) == 0) {
+            st4(o0 + o, make_int4(r[0], r[1], r[2], r[3]));
+            if (NC == 3) { st4(o1 + o, make_int4(g[0], g[1], g[2], g[3])); st4(o2 + o, make_int4(b[0], b[1], b[2], b[3])); }
         } else {
-            o0[o] = cl(last + shift);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (gx + e >= (int)w || X + e < win.x0 || X + e >= win.x1) continue;
+                o0[o + e] = (TO)r[e];
+                if (NC == 3) { o1[o + e] = (TO)g[e]; o2[o + e] = (TO)b[e]; }
+            }
         }
     }
 }
@@ -596,24 +632,26 @@ void gk_launch_dwt53_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32
                             uint32_t dstride, uint32_t w, uint32_t h, GkTiles tb, int32_t shift) {
     if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
+    const int vec = (sin & 3) == 0;   // (the kernel checks each tile's row pointers)
     if (nc == 3)
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_fwd_l1<T, 3>), grid, dim3(256), 0, st, in, sin, dst,
-                                                        cstride, dstride, w, h, tb, shift))
+                                                        cstride, dstride, w, h, tb, shift, vec))
     else
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_fwd_l1<T, 1>), grid, dim3(256), 0, st, in, sin, dst,
-                                                        cstride, dstride, w, h, tb, shift))
+                                                        cstride, dstride, w, h, tb, shift, vec))
 }
 void gk_launch_dwt53_inv_l1(hipStream_t st, int stype, int nc, const int32_t* src, uint64_t cstride, uint32_t sstride,
                             GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
                             int32_t mn, int32_t mx) {
     if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
     dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count());
+    const int vec = gk_vec_ok(gk_sample_size(stype), out, nc, ostride);
     if (nc == 3)
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_inv_l1<T, 3>), grid, dim3(256), 0, st, src, cstride,
-                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx))
+                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx, vec))
     else
         GK_SAMPLE_DISPATCH(stype, T, hipLaunchKernelGGL((k_dwt53_inv_l1<T, 1>), grid, dim3(256), 0, st, src, cstride,
-                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx))
+                                                        sstride, out, ostride, win, w, h, tb, shift, mn, mx, vec))
 }
 void gk_launch_gather(hipStream_t st, const uint8_t* src, uint8_t* dst, const uint64_t* seg, uint32_t nseg) {
     if (!nseg) return;

@@ -663,7 +663,10 @@ void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks,
 // significance, its sign and the refinements - except the zeros a run-length column codes four
 // at a time; samples with more magnitude bits leave fewer such zeros.  Weight, in eighths of a
 // decision: 5 P area + 3 (sum of the samples' magnitude bit counts), i.e. P decisions per sample
-// less 3/8 of the zeros above the samples' most significant bits.
+// less 3/8 of the zeros above the samples' most significant bits.  The estimate only orders the
+// blocks (each is coded the same whatever the order), so it is taken over every fourth row - a
+// quarter of the coefficient lines - with the bit count scaled back (a full pass was 0.28 ms of
+// C2's encode, `profiles/r04z_C2_kernel_stats.txt`).
 __global__ __launch_bounds__(64) void k_t1_weight(const int32_t* __restrict__ coef, const GkBlock* __restrict__ blocks,
                                                   uint32_t* __restrict__ weight, uint32_t nblocks) {
     const uint32_t b = blockIdx.x;
@@ -673,7 +676,8 @@ __global__ __launch_bounds__(64) void k_t1_weight(const int32_t* __restrict__ co
     const bool irrev = B.flags & 1;
     uint32_t mx = 0, nbits = 0;
     if (lane < (int)B.w)
-        for (uint32_t y = 0; y < B.h; ++y) {
+#pragma unroll 4
+        for (uint32_t y = 0; y < B.h; y += 4) {
             const int32_t raw = coef[B.band_off + (size_t)y * B.stride + lane];
             const uint32_t a0 = irrev ? (uint32_t)fabsf(rintf((__int_as_float(raw) / B.step) * 64.0f))
                                       : (uint32_t)(raw < 0 ? -raw : raw) * 64u;
@@ -689,7 +693,8 @@ __global__ __launch_bounds__(64) void k_t1_weight(const int32_t* __restrict__ co
     if (lane == 0) {
         const uint32_t t = mx ? 32 - __clz(mx) : 0;
         const uint32_t planes = t <= 6 ? 0 : t - 6;
-        weight[b] = planes * B.w * B.h * 5u + 3u * nbits;
+        const uint32_t rows = (B.h + 3) / 4;   // rows sampled
+        weight[b] = planes * B.w * B.h * 5u + (uint32_t)((3ull * nbits * B.h) / (rows ? rows : 1));
     }
 }
 void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint32_t* weight, uint32_t nblocks) {

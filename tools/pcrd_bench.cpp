@@ -40,7 +40,22 @@ int main(int argc, char** argv) {
         fclose(f);
     }
     printf("blocks %u passes %zu\n", nb, passes.size());
-    for (int it = 0; it < 5; ++it) {
+    {   // host pool dispatch: an empty job over the pool's threads, and a 49,152-item light job
+        const size_t n = host_pool().size();
+        std::atomic<uint64_t> sink{0};
+        for (int rep = 0; rep < 4; ++rep) {
+            auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < 1000; ++i) host_pool().run(n, [&](size_t q) { sink += q; });
+            auto t1 = std::chrono::steady_clock::now();
+            for (int i = 0; i < 100; ++i)
+                host_pool().run(24, [&](size_t q) { uint64_t a = 0; for (size_t k = 0; k < 2048; ++k) a += k * q; sink += a; });
+            auto t2 = std::chrono::steady_clock::now();
+            printf("pool %zu threads: empty dispatch %.2f us, 24 x 2048 items %.2f us\n", n,
+                   std::chrono::duration<double, std::micro>(t1 - t0).count() / 1000,
+                   std::chrono::duration<double, std::micro>(t2 - t1).count() / 100);
+        }
+    }
+    for (int it = 0; it < 8; ++it) {
         T2Enc T2(P, info.data(), passes.data(), 0, 1);
         T2.serial = getenv("PCRD_SERIAL") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
