@@ -129,11 +129,12 @@ __global__ __launch_bounds__(256) void k_dc_inv_f(const float* __restrict__ in, 
 // =============================================================================
 typedef float Lds97[T97_LH][T97_LW + 1];
 
-__device__ __forceinline__ bool interior97(int x0, int y0, int w, int h) {
-    return x0 >= T97_HALO && y0 >= T97_HALO && x0 + T97_W + T97_HALO <= w && y0 + T97_H + T97_HALO <= h;
-}
+// a tile whose 128 columns lie inside the resolution takes the lane-mapped paths (rows and
+// halo columns mirrored where they fall outside: a tile-grid border); a last, partial tile
+// column the general per-position one
+__device__ __forceinline__ bool fullw97(int x0, int w) { return x0 + T97_W <= w; }
 
-// f(ly, lx, gy, gx): the sample at mirrored input position (gy, gx) into LDS (ly, lx) (edge tiles)
+// f(ly, lx, gy, gx): the sample at mirrored input position (gy, gx) into LDS (ly, lx) (partial tiles)
 template <class F>
 __device__ __forceinline__ void fwd97_fill(int x0, int y0, int w, int h, int tid, F f) {
     for (int i = tid; i < T97_LH * T97_LW; i += 256) {
@@ -141,17 +142,18 @@ __device__ __forceinline__ void fwd97_fill(int x0, int y0, int w, int h, int tid
         f(ly, lx, mirror97(y0 - T97_HALO + ly, h), mirror97(x0 - T97_HALO + lx, w));
     }
 }
-// interior tile: LDS columns 4..131 by the lanes, halo columns 0..3 / 132..135 in one pass
+// full-width tile: LDS columns 4..131 by the lanes, halo columns 0..3 / 132..135 in one pass
 template <class F>
-__device__ __forceinline__ void fwd97_fill_inner(int x0, int y0, int tid, F f) {
+__device__ __forceinline__ void fwd97_fill_inner(int x0, int y0, int w, int h, int tid, F f) {
     const int tx = tid & 63, ty = tid >> 6;
     for (int ly = ty; ly < T97_LH; ly += 4) {
-        f(ly, 4 + tx, y0 - T97_HALO + ly, x0 + tx);
-        f(ly, 68 + tx, y0 - T97_HALO + ly, x0 + 64 + tx);
+        const int gy = mirror97(y0 - T97_HALO + ly, h);
+        f(ly, 4 + tx, gy, x0 + tx);
+        f(ly, 68 + tx, gy, x0 + 64 + tx);
     }
     for (int i = tid; i < 8 * T97_LH; i += 256) {
         const int ly = i >> 3, j = i & 7, lx = j < 4 ? j : 128 + j;
-        f(ly, lx, y0 - T97_HALO + ly, x0 - T97_HALO + lx);
+        f(ly, lx, mirror97(y0 - T97_HALO + ly, h), mirror97(x0 - T97_HALO + lx, w));
     }
 }
 
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict
     dst += tb.offset(tile, dstride) + comp * cs.cstride;
     const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
     auto ld = [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; };
-    if (interior97(x0, y0, (int)w, (int)h)) fwd97_fill_inner(x0, y0, tid, ld);
+    if (fullw97(x0, (int)w)) fwd97_fill_inner(x0, y0, (int)w, (int)h, tid, ld);
     else fwd97_fill(x0, y0, (int)w, (int)h, tid, ld);
     __syncthreads();
     fwd97_lift(T, (int)w, (int)h, tid);
@@ -296,14 +298,27 @@ __global__ __launch_bounds__(256) void k_dwt97_fwd_l1(GkPtr3 in, uint32_t sin, f
             T[ly][lx] = (float)(r0 - shift);
         }
     };
-    const bool inner = interior97(x0, y0, (int)w, (int)h);
+    const bool inner = fullw97(x0, (int)w);
     if (inner) {
-        // (x0 is a multiple of 128, so every group is aligned when the plane rows are)
+        // (x0 is a multiple of 128, so every main group is aligned when the plane rows are; a
+        // halo group outside the resolution is read one mirrored sample at a time)
         const bool v = vec && al4(p0) && al4(p1) && al4(p2);
         fwd97_groups(tid, [&](int g, int ly, int lx) {
-            const size_t i = (size_t)(y0 - T97_HALO + ly) * sin + (x0 - T97_HALO + lx);
-            const int4 a = ld4v(p0 + i, v);
-            const int4 b = NC == 3 ? ld4v(p1 + i, v) : a, c = NC == 3 ? ld4v(p2 + i, v) : a;
+            const size_t r = (size_t)mirror97(y0 - T97_HALO + ly, (int)h) * sin;
+            const int gx = x0 - T97_HALO + lx;
+            int4 a, b, c;
+            if (gx >= 0 && gx + 3 < (int)w) {
+                const size_t i = r + gx;
+                a = ld4v(p0 + i, v);
+                b = NC == 3 ? ld4v(p1 + i, v) : a; c = NC == 3 ? ld4v(p2 + i, v) : a;
+            } else {
+                int ga[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ga[j] = mirror97(gx + j, (int)w);
+                a = make_int4((int32_t)p0[r + ga[0]], (int32_t)p0[r + ga[1]], (int32_t)p0[r + ga[2]], (int32_t)p0[r + ga[3]]);
+                b = NC == 3 ? make_int4((int32_t)p1[r + ga[0]], (int32_t)p1[r + ga[1]], (int32_t)p1[r + ga[2]], (int32_t)p1[r + ga[3]]) : a;
+                c = NC == 3 ? make_int4((int32_t)p2[r + ga[0]], (int32_t)p2[r + ga[1]], (int32_t)p2[r + ga[2]], (int32_t)p2[r + ga[3]]) : a;
+            }
             put(4 * g, ly, lx, a.x, b.x, c.x);
             put(4 * g + 1, ly, lx + 1, a.y, b.y, c.y);
             put(4 * g + 2, ly, lx + 2, a.z, b.z, c.z);
@@ -348,18 +363,19 @@ template <class F>
 __device__ __forceinline__ void inv97_fill(int x0, int y0, int w, int h, int tid, F f) {
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
     const float fe = w > 1 ? F97_K : 1.0f, fo = w > 1 ? I97_TWO_INVK : 1.0f;
-    if (interior97(x0, y0, w, h)) {
+    if (fullw97(x0, w)) {   // (rows and halo columns mirrored)
         // even interleaved columns (lx even) are L samples x0/2 - 2 + lx/2, odd ones H samples
         const int tx = tid & 63, ty = tid >> 6, hx = x0 >> 1;
         for (int ly = ty; ly < T97_LH; ly += 4) {
-            const int gy = y0 - T97_HALO + ly, sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
+            const int gy = mirror97(y0 - T97_HALO + ly, h), sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
             f(ly, T97_HALO + 2 * tx, sy, hx + tx, fe);
             f(ly, T97_HALO + 1 + 2 * tx, sy, snw + hx + tx, fo);
         }
         for (int i = tid; i < 8 * T97_LH; i += 256) {
             const int ly = i >> 3, j = i & 7, lx = j < 4 ? j : 128 + j;
-            const int gy = y0 - T97_HALO + ly, sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
-            f(ly, lx, sy, (lx & 1) ? snw + hx - 2 + (lx >> 1) : hx - 2 + (lx >> 1), (lx & 1) ? fo : fe);
+            const int gy = mirror97(y0 - T97_HALO + ly, h), sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
+            const int gx = mirror97(x0 - T97_HALO + lx, w);
+            f(ly, lx, sy, (gx & 1) ? snw + (gx >> 1) : (gx >> 1), (lx & 1) ? fo : fe);
         }
     } else {
         for (int i = tid; i < T97_LH * T97_LW; i += 256) {

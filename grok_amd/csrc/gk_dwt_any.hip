@@ -8,7 +8,9 @@
 // kernels for that level instead.  They follow the restated line transforms exactly: sample i
 // of a line is high-pass when (i + parity) is odd, whole-sample symmetric extension at both
 // ends, lows then highs on output; a single sample is doubled (5/3 forward, odd parity) or
-// halved (5/3 inverse: bandH / 2 across, bandL >> 1 down, WaveletReverse.cpp:583, :636) and
+// halved (5/3 inverse: bandH / 2 across, bandL >> 1 down, WaveletReverse.cpp:583, :636; a
+// windowed decode takes Grok's partial-tile path, whose horizontal case shifts too,
+// S(buf, 0) >>= 1 at :1551-1554, and differs from / 2 for a negative odd coefficient) and
 // left as it is by the 9/7.  9/7 steps are rounded one operation at a time (no contraction),
 // as the tiled kernels and Grok's scalar path do.
 //
@@ -70,10 +72,10 @@ __device__ void deinterleave(const T* x, size_t sx, T* y, size_t sy, int n, int 
     }
 }
 // Mallat line x (lows then highs) interleaved into line y, then inverse lifting in place
-__device__ void inv53_line(const int32_t* x, size_t sx, int32_t* y, size_t sy, int n, int par, bool vertical) {
+__device__ void inv53_line(const int32_t* x, size_t sx, int32_t* y, size_t sy, int n, int par, bool shift) {
     if (n == 1) {
         int32_t v = x[0];
-        if (par) v = vertical ? (v >> 1) : (v / 2);
+        if (par) v = shift ? (v >> 1) : (v / 2);
         y[0] = v;
         return;
     }
@@ -99,6 +101,7 @@ __device__ void inv97_line(const float* x, size_t sx, float* y, size_t sy, int n
 
 struct AnyLevel {
     uint32_t w, h, px, py;
+    uint32_t partial;   // a windowed decode (Grok's partial-tile inverse)
     GkTiles tb;
     uint64_t cstride;
     uint32_t stride;
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(64) void k_any_inv_rows(int32_t* src, int32_t* dst,
     if constexpr (IRREV)
         inv97_line(reinterpret_cast<const float*>(src) + o, 1, reinterpret_cast<float*>(dst) + o, 1, (int)a.w, (int)a.px);
     else
-        inv53_line(src + o, 1, dst + o, 1, (int)a.w, (int)a.px, false);
+        inv53_line(src + o, 1, dst + o, 1, (int)a.w, (int)a.px, a.partial != 0);
 }
 template <bool IRREV>
 __global__ __launch_bounds__(64) void k_any_inv_cols(int32_t* src, int32_t* dst, AnyLevel a) {
@@ -171,12 +174,12 @@ __global__ __launch_bounds__(256) void k_any_copy(const int32_t* src, int32_t* d
 // region of `in` and leaves the Mallat output in `out`; inverse the other way round.  `in` /
 // `out` are component 0's planes (components cstride apart, grid.y = components x tiles).
 void gk_launch_dwt_any(hipStream_t st, bool irrev, bool forward, int32_t* in, int32_t* out, uint32_t stride, uint32_t w,
-                       uint32_t h, uint32_t px, uint32_t py, GkTiles tb, GkComps cs) {
+                       uint32_t h, uint32_t px, uint32_t py, GkTiles tb, GkComps cs, bool partial) {
     if (!w || !h || !tb.count() || !cs.n) return;
     // grid.y = components x tiles (at most 65535: larger sets go one component at a time)
     const uint32_t ng = tb.count() * cs.n <= 65535u ? cs.n : 1u;
     for (uint32_t c = 0; c < cs.n; c += ng) {
-        const AnyLevel a{w, h, px, py, tb, cs.cstride, stride};
+        const AnyLevel a{w, h, px, py, partial ? 1u : 0u, tb, cs.cstride, stride};
         const uint32_t nz = tb.count() * ng;
         int32_t* i2 = in + (uint64_t)c * cs.cstride;
         int32_t* o2 = out + (uint64_t)c * cs.cstride;

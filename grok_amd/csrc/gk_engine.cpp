@@ -76,36 +76,41 @@ static int engines_on(int dev) {
 // run(n, f) calls f(0..n-1) across the workers and the caller, and returns when all
 // calls finished; the first GkError thrown by any call is rethrown.  Host phases are short (a
 // rate-control bisection step is ~100 us on 16 threads), so a dispatch must cost little:
-//  * items are claimed from a (generation, index) word and run() waits for the items to
-//    finish, not for every worker to have woken (a worker that wakes after its generation's
-//    items are all claimed never touches that job);
+//  * items are claimed from one word holding (generation, item count, next item) and run()
+//    waits for the items to finish, not for every worker to have woken; a worker reads the job
+//    only after a successful claim, when no later job can have replaced it (a worker that
+//    wakes after its generation's items are all claimed never touches that job);
 //  * workers sleep on the generation word itself (futex), so a wake-up takes no mutex: with a
 //    mutex and a condition variable, 15 woken workers queued on the mutex the next dispatch
 //    needed.  Empty dispatch on the GPU box (tools/pcrd_bench.cpp): ~30 us with
-//    notify_all and a wait for every worker, ~12 us with item completion alone.
+//    notify_all and a wait for every worker, ~5 us now.
 class HostPool {
     std::vector<std::thread> th_;
-    std::atomic<const std::function<void(size_t)>*> job_{nullptr};   // published before gen_ (release)
-    std::atomic<size_t> n_{0};
+    std::atomic<const std::function<void(size_t)>*> job_{nullptr};   // written before the claim word
     std::atomic<uint32_t> gen_{0};           // futex word: a new job
-    std::atomic<uint64_t> claim_{0};         // generation << 32 | next item
+    std::atomic<uint64_t> claim_{0};         // generation (16 bits) | items (24) | next item (24)
     std::atomic<size_t> done_{0};            // items of the current generation finished
-    std::atomic<uint32_t> fin_{0};           // futex word: the caller sleeps until done_ == n
+    std::atomic<uint32_t> fin_{0};           // futex word: the caller sleeps until done_ == items
     std::atomic<bool> stop_{false}, has_err_{false};
     std::mutex err_m_;
     std::string err_;
     std::mutex run_m_;
+    static constexpr uint64_t kMaxItems = (1u << 24) - 1;
     static void fwait(std::atomic<uint32_t>& w, uint32_t v) {
         syscall(SYS_futex, reinterpret_cast<uint32_t*>(&w), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
     }
     static void fwake(std::atomic<uint32_t>& w) {
         syscall(SYS_futex, reinterpret_cast<uint32_t*>(&w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
     }
-    int64_t claim(uint32_t g, size_t n) {    // an item of generation g, or -1
+    // an item of generation g: its index and the generation's item count, or false
+    bool claim(uint32_t g, size_t& i, size_t& n) {
         uint64_t c = claim_.load(std::memory_order_acquire);
         for (;;) {
-            if ((uint32_t)(c >> 32) != g || (c & 0xffffffffull) >= n) return -1;
-            if (claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel)) return (int64_t)(c & 0xffffffffull);
+            if ((uint32_t)(c >> 48) != (g & 0xffffu)) return false;
+            n = (size_t)((c >> 24) & kMaxItems);
+            i = (size_t)(c & kMaxItems);
+            if (i >= n) return false;
+            if (claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel)) return true;
         }
     }
     void fail(const std::string& e) {
@@ -113,9 +118,11 @@ class HostPool {
         if (err_.empty()) err_ = e;
         has_err_ = true;
     }
-    void work(uint32_t g, const std::function<void(size_t)>& f, size_t n) {
-        for (int64_t i; (i = claim(g, n)) >= 0;) {
-            try { f((size_t)i); } catch (const GkError& e) {
+    void work(uint32_t g) {
+        for (size_t i, n; claim(g, i, n);) {
+            // (the claim synchronises with the caller's publication, and this item keeps the job alive)
+            const std::function<void(size_t)>& f = *job_.load(std::memory_order_relaxed);
+            try { f(i); } catch (const GkError& e) {
                 fail(e.msg);
             } catch (const std::exception& e) {   // e.g. std::bad_alloc: recorded, never escapes a worker
                 fail(std::string("host worker: ") + e.what());
@@ -135,13 +142,7 @@ class HostPool {
             while ((g = gen_.load(std::memory_order_acquire)) == seen && !stop_.load(std::memory_order_acquire)) fwait(gen_, seen);
             if (stop_.load(std::memory_order_acquire)) return;
             seen = g;
-            // job_ / n_ of generation g (written before gen_); a later generation may have
-            // replaced them already, and then every claim of g fails and f is not called
-            const std::function<void(size_t)>* f = job_.load(std::memory_order_relaxed);
-            const size_t n = n_.load(std::memory_order_relaxed);
-            const uint64_t c = claim_.load(std::memory_order_acquire);
-            if ((uint32_t)(c >> 32) != g) continue;
-            work(g, *f, n);
+            work(g);
         }
     }
 
@@ -159,17 +160,16 @@ public:
     void run(size_t n, const std::function<void(size_t)>& f) {
         if (n == 0) return;
         std::unique_lock<std::mutex> own(run_m_, std::try_to_lock);
-        if (n == 1 || th_.empty() || !own.owns_lock() || n > 0xffffffffull) { for (size_t i = 0; i < n; ++i) f(i); return; }
+        if (n == 1 || th_.empty() || !own.owns_lock() || n > kMaxItems) { for (size_t i = 0; i < n; ++i) f(i); return; }
         { std::lock_guard<std::mutex> lk(err_m_); err_.clear(); }
         has_err_ = false;
         job_.store(&f, std::memory_order_relaxed);
-        n_.store(n, std::memory_order_relaxed);
         done_.store(0, std::memory_order_relaxed);
         const uint32_t g = gen_.load(std::memory_order_relaxed) + 1;
-        claim_.store((uint64_t)g << 32, std::memory_order_release);
+        claim_.store(((uint64_t)(g & 0xffffu) << 48) | ((uint64_t)n << 24), std::memory_order_release);
         gen_.store(g, std::memory_order_release);
         fwake(gen_);
-        work(g, f, n);
+        work(g);
         for (uint32_t v; done_.load(std::memory_order_acquire) != n;) {   // items still running on workers
             v = fin_.load(std::memory_order_acquire);
             if (done_.load(std::memory_order_acquire) == n) break;
@@ -1066,12 +1066,16 @@ struct T2Enc {
         b0 = P.tiles[tb].b0; b1 = P.tiles[te - 1].b1;
         lnp.assign(nb * L, 0); inprev.assign(nb, 0); nlb.assign(nb, 0);
         incl.resize(P.ntrees); imsb.resize(P.ntrees);
-        for (uint32_t t = tb; t < te; ++t)
-        for (auto& C : P.tiles[t].comps)
-            for (auto& R : C.res)
-                for (size_t bi = 0; bi < R.bands.size(); ++bi)
-                    for (auto& PG : R.prc[bi])
-                        if (PG.cw && PG.ch) { incl[PG.tree].build(PG.cw, PG.ch); imsb[PG.tree].build(PG.cw, PG.ch); }
+        // the tiles' tag trees are disjoint: many tiles (C4: 256 x ~18 trees) build in parallel
+        auto build_tile = [&](size_t q) {
+            for (auto& C : P.tiles[tb + (uint32_t)q].comps)
+                for (auto& R : C.res)
+                    for (size_t bi = 0; bi < R.bands.size(); ++bi)
+                        for (auto& PG : R.prc[bi])
+                            if (PG.cw && PG.ch) { incl[PG.tree].build(PG.cw, PG.ch); imsb[PG.tree].build(PG.cw, PG.ch); }
+        };
+        if (te - tb > 1) host_pool().run(te - tb, build_tile);
+        else build_tile(0);
     }
     uint32_t npasses(uint32_t b) const { return info[4 * (size_t)b + 1]; }
     uint32_t rate(uint32_t b, uint32_t q) const {   // cumulative bytes after pass q (q < npasses)
@@ -2313,6 +2317,10 @@ struct HostBuf {
 
 struct gk_ctx {
     uint32_t dec_layers = 0;   // quality layers to decode (0 = all; grk_dparameters::cp_layer)
+    // the decode in progress has a window: Grok then takes its partial-tile inverse
+    // (CodeStreamDecompress.cpp:389, WaveletReverse.cpp:2237-2246), whose 5/3 single odd sample
+    // across is H >> 1 (:1551-1554) where the whole-tile path has H / 2 (:583)
+    bool dwt_partial = false;
     uint32_t dec_reduce = 0;   // highest resolutions discarded on decode (grk_dparameters::cp_reduce)
     int device = 0;
     bool registered = false;   // counted in g_dev_engines
@@ -2531,7 +2539,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                 int32_t* dst_l = (l & 1) ? B : A;
                 const uint64_t area = (uint64_t)w * h * S.tb.count();
                 gk_launch_dwt_any(ctx->st, P.p.irrev, forward, forward ? src_l : dst_l, forward ? dst_l : src_l, RG.stride,
-                                  w, h, S.parx[l - 1], S.pary[l - 1], S.tb, GkComps{cst, P.nc});
+                                  w, h, S.parx[l - 1], S.pary[l - 1], S.tb, GkComps{cst, P.nc}, !forward && ctx->dwt_partial);
                 ctx->tm.dwt_launches += 3;
                 ctx->tm.dwt_bytes += area * 8 * P.nc;
                 continue;
@@ -3590,6 +3598,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     hipStream_t st = ctx->st;
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[0], st));
+    ctx->dwt_partial = win != nullptr;
     // GK_PROFILE=1: host phase times of the decode (stderr)
     static const bool prof = getenv("GK_PROFILE") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -3891,25 +3900,29 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     std::vector<uint32_t> hseglen;   // BYPASS / TERMALL: segment lengths, a block's at G.data_cap
     std::vector<std::vector<int32_t>> part_idx(Hd.parts.size());   // tile-local block -> table entry
     uint64_t o = 0, t1_bytes = 0;
-    for (uint32_t j = jb; j < je; ++j)
-        for (uint32_t i = ib; i < ie; ++i) {
-            const int32_t q = part_of[(size_t)j * P.ntx + i];
-            if (q < 0) continue;
-            const TileG& T = P.tiles[(size_t)j * P.ntx + i];
-            const PartState& st2 = ps[q];
-            const std::vector<uint8_t>& need = part_need[q];
-            std::vector<int32_t>& idx = part_idx[q];
-            idx.assign(T.b1 - T.b0, -1);
-            for (uint32_t c = 0; c < P.nc; ++c)
-                for (uint32_t r = 0; r < P.p.numres; ++r) {
-                    const ResG& R = T.comps[c].res[r];
-                    for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
-                        for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                            const PrecG& PG = R.prc[bi][pi];
-                            for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                                const uint32_t lb = PG.first_block + k - T.b0;
-                                if (!need[lb]) continue;
-                                GkBlock& G = blk[nblk];
+    // one tile's needed blocks into blk[nb0 ..) with staging offsets from o0 (its blocks in
+    // (component, resolution, band, precinct, block) order); count-only when blk is null
+    struct TileFill { int32_t q; uint32_t t, nb; uint64_t bytes, t1; };
+    auto fill_tile = [&](const TileFill& tf, uint32_t nb0, uint64_t o0, bool count_only, TileFill* out) {
+        const TileG& T = P.tiles[tf.t];
+        const PartState& st2 = ps[tf.q];
+        const std::vector<uint8_t>& need = part_need[tf.q];
+        std::vector<int32_t>& idx = part_idx[tf.q];
+        if (!count_only) idx.assign(T.b1 - T.b0, -1);
+        uint32_t n = 0;
+        uint64_t oo = o0, t1 = 0;
+        for (uint32_t c = 0; c < P.nc; ++c)
+            for (uint32_t r = 0; r < P.p.numres; ++r) {
+                const ResG& R = T.comps[c].res[r];
+                for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
+                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
+                        const PrecG& PG = R.prc[bi][pi];
+                        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                            const uint32_t lb = PG.first_block + k - T.b0;
+                            if (!need[lb]) continue;
+                            const uint32_t len = st2.len[lb];
+                            if (!count_only) {
+                                GkBlock& G = blk[nb0 + n];
                                 G = P.blocks[T.b0 + lb];
                                 G.band_off = relocate(P, RG, G.band_off);
                                 G.stride = RG.stride;
@@ -3920,21 +3933,47 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                     G.step = R.bands[bi].step_dec / (float)(1u << (31 - R.bands[bi].numbps));
                                 }
                                 G.numbps = st2.numbps[lb];
-                                G.len = st2.len[lb];
-                                G.npasses = G.len ? st2.npasses[lb] : 0;
+                                G.npasses = len ? st2.npasses[lb] : 0;
                                 if (multiseg) {
                                     G.data_cap = (uint32_t)hseglen.size();
                                     hseglen.insert(hseglen.end(), st2.seglens[lb].begin(), st2.seglens[lb].end());
                                 }
-                                G.data_off = o;
-                                t1_bytes += G.len;
-                                o += (((uint64_t)G.len + 15) & ~15ull) + 32;
+                                G.data_off = oo;
                                 G.len = 0;   // reused as the fill cursor below
-                                idx[lb] = (int32_t)nblk++;
+                                idx[lb] = (int32_t)(nb0 + n);
                             }
+                            t1 += len;
+                            oo += (((uint64_t)len + 15) & ~15ull) + 32;
+                            ++n;
                         }
-                }
+                    }
+            }
+        if (out) { out->nb = n; out->bytes = oo - o0; out->t1 = t1; }
+    };
+    std::vector<TileFill> tiles_in;
+    for (uint32_t j = jb; j < je; ++j)
+        for (uint32_t i = ib; i < ie; ++i) {
+            const int32_t q = part_of[(size_t)j * P.ntx + i];
+            if (q >= 0) tiles_in.push_back({q, j * P.ntx + i, 0, 0, 0});
         }
+    // many tiles (C4: 256) fill in parallel from per-tile counts; BYPASS / TERMALL segment
+    // lengths append in table order, so those streams take the serial pass
+    const bool par_fill = !multiseg && tiles_in.size() >= 8;
+    std::vector<uint32_t> tb0(tiles_in.size() + 1, 0);
+    std::vector<uint64_t> to0(tiles_in.size() + 1, 0);
+    if (par_fill) {
+        host_pool().run(tiles_in.size(), [&](size_t k) { fill_tile(tiles_in[k], 0, 0, true, &tiles_in[k]); });
+        for (size_t k = 0; k < tiles_in.size(); ++k) {
+            tb0[k + 1] = tb0[k] + tiles_in[k].nb; to0[k + 1] = to0[k] + tiles_in[k].bytes; t1_bytes += tiles_in[k].t1;
+        }
+        host_pool().run(tiles_in.size(), [&](size_t k) { fill_tile(tiles_in[k], tb0[k], to0[k], false, nullptr); });
+        nblk = tb0.back(); o = to0.back();
+    } else {
+        for (TileFill& tf : tiles_in) {
+            fill_tile(tf, nblk, o, false, &tf);
+            nblk += tf.nb; o += tf.bytes; t1_bytes += tf.t1;
+        }
+    }
     const uint32_t nbr = nblk, nbx = std::max(nbr, 1u);
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[1], st));
@@ -3951,23 +3990,35 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // gather every selected block's segments into a 16-byte aligned slot followed by >= 32
     // bytes of 0xFF (the T1 decoders read their bytes through aligned windows; the Part-1
     // decoder takes the padding as the MQ end-of-data bytes)
-    // (pos, slot position, length) triples, straight into the pinned upload buffer
+    // (pos, slot position, length) triples, straight into the pinned upload buffer; a part's
+    // chunks are those of its own blocks, so parts fill disjoint ranges
     size_t nseg = 0;
     uint64_t* seg = nullptr;
     {
-        size_t nch = 0;
-        for (auto& p2 : ps) nch += p2.chunks.size();
-        seg = (uint64_t*)ctx->hseg.get(3 * nch * 8 + 8);
-        for (size_t q = 0; q < ps.size(); ++q)
+        std::vector<size_t> sb(ps.size() + 1, 0);
+        for (size_t q = 0; q < ps.size(); ++q) sb[q + 1] = sb[q] + (part_idx[q].empty() ? 0 : 3 * ps[q].chunks.size());
+        seg = (uint64_t*)ctx->hseg.get(sb.back() * 8 + 8);
+        std::vector<size_t> used(ps.size(), 0);
+        auto segs = [&](size_t q) {
+            if (part_idx[q].empty()) return;
+            size_t w = sb[q];
             for (const Chunk& ch : ps[q].chunks) {   // stream order = layer order within a block
-                if (part_idx[q].empty()) continue;
                 const int32_t k = part_idx[q][ch.b];
                 if (k < 0) continue;
                 GkBlock& G = blk[k];
-                seg[nseg] = ch.pos; seg[nseg + 1] = G.data_off + G.len; seg[nseg + 2] = ch.len;
-                nseg += 3;
+                seg[w] = ch.pos; seg[w + 1] = G.data_off + G.len; seg[w + 2] = ch.len;
+                w += 3;
                 G.len += ch.len;
             }
+            used[q] = w - sb[q];
+        };
+        if (par_fill) host_pool().run(ps.size(), segs);
+        else for (size_t q = 0; q < ps.size(); ++q) segs(q);
+        // compact (a part's unused tail: chunks of blocks the table does not hold)
+        for (size_t q = 0; q < ps.size(); ++q) {
+            if (nseg != sb[q]) memmove(seg + nseg, seg + sb[q], used[q] * 8);
+            nseg += used[q];
+        }
     }
     uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 256);   // decoder window loads read up to 48 B past a block
     if (host_gather) {

@@ -71,25 +71,50 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
     uint8_t* mel = mel_scratch + (size_t)b * mel_cap;
     bool ovf = false;
 
-    // ---- MagSgn: LSB-first, a byte after 0xFF carries 7 bits; bytes packed into dwords
-    uint64_t ms_acc = 0; int ms_n = 0, ms_k = 8; uint32_t ms_pos = 0, ms_word = 0;
+    // Output bytes leave in whole 16-byte lines: each stream collects its bytes in a 16-byte
+    // register line aligned like its destination and stores the line once complete (one
+    // 16-byte store per lane instead of one store per byte or per dword: a wave's byte stores
+    // touched 64 lines each and the encoder wrote 3.4x its output, `profiles/r04s_C4_pmc.txt`).
+    // ---- MagSgn: LSB-first, a byte after 0xFF carries 7 bits; forward from the slot start
+    // (64-byte aligned)
+    uint64_t ms_acc = 0; int ms_n = 0, ms_k = 8; uint32_t ms_pos = 0;
+    uint64_t ms_l0 = 0, ms_l1 = 0;   // the current line, bytes ms_pos & ~15 ..
+    auto ms_byte = [&](uint32_t byte) {
+        const uint32_t o = ms_pos & 15;
+        if (o < 8) ms_l0 |= (uint64_t)byte << (8 * o); else ms_l1 |= (uint64_t)byte << (8 * (o - 8));
+        ++ms_pos;
+        if ((ms_pos & 15) == 0) {
+            *(uint4*)(slot + ms_pos - 16) = make_uint4((uint32_t)ms_l0, (uint32_t)(ms_l0 >> 32), (uint32_t)ms_l1, (uint32_t)(ms_l1 >> 32));
+            ms_l0 = ms_l1 = 0;
+        }
+    };
     auto ms_put = [&](uint32_t v, int m) {
         ms_acc |= (uint64_t)v << ms_n; ms_n += m;
         while (ms_n >= ms_k) {
             uint32_t byte = (uint32_t)ms_acc & ((1u << ms_k) - 1);
             ms_acc >>= ms_k; ms_n -= ms_k;
-            ms_word |= byte << (8 * (ms_pos & 3));
-            ++ms_pos;
-            if ((ms_pos & 3) == 0) { *(uint32_t*)(slot + ms_pos - 4) = ms_word; ms_word = 0; }
+            ms_byte(byte);
             ms_k = (byte == 0xFF) ? 7 : 8;
         }
     };
     // ---- VLC: LSB-first, grows backward from the slot end; after a byte > 0x8F the
-    // next byte's MSB is a stuffed 0 unless its low 7 bits differ from 0x7F
+    // next byte's MSB is a stuffed 0 unless its low 7 bits differ from 0x7F.  Byte i goes to
+    // tail_end - 2 - i; the register line holds the 16-byte aligned line of the current byte and
+    // is stored when the stream moves below it.  (A line above the slot end is padding before
+    // the next 64-byte aligned slot; the locator bytes are stored last.)
     uint64_t v_acc = 0xF; int v_n = 4; bool v_gt = true; uint32_t v_cnt = 0, v_first = 0;
+    uint64_t v_l0 = 0, v_l1 = 0;
+    uint8_t* v_line = (uint8_t*)((uintptr_t)(tail_end - 2) & ~(uintptr_t)15);
     auto v_emit = [&](uint32_t byte) {
         if (v_cnt == 0) v_first = byte;
-        tail_end[-2 - (int)v_cnt] = (uint8_t)byte;
+        uint8_t* a = tail_end - 2 - (int)v_cnt;
+        if (a < v_line) {   // the line above is complete
+            *(uint4*)v_line = make_uint4((uint32_t)v_l0, (uint32_t)(v_l0 >> 32), (uint32_t)v_l1, (uint32_t)(v_l1 >> 32));
+            v_l0 = v_l1 = 0;
+            v_line -= 16;
+        }
+        const uint32_t o = (uint32_t)(a - v_line);
+        if (o < 8) v_l0 |= (uint64_t)byte << (8 * o); else v_l1 |= (uint64_t)byte << (8 * (o - 8));
         ++v_cnt;
     };
     auto vlc_put = [&](uint32_t cw, int len) {
@@ -104,10 +129,15 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
         }
     };
     // ---- MEL: MSB-first bits, a byte after 0xFF carries 7 bits
-    uint32_t m_tmp = 0, m_cnt = 0; int m_rem = 8, m_run = 0, m_k = 0, m_thr = 1;
+    // (staged in the block's scratch a dword at a time; copied into place once Scup is known)
+    uint32_t m_tmp = 0, m_cnt = 0, m_word = 0; int m_rem = 8, m_run = 0, m_k = 0, m_thr = 1;
     auto mel_store = [&](uint32_t byte) {
-        if (m_cnt < mel_cap) mel[m_cnt] = (uint8_t)byte; else ovf = true;
+        m_word |= byte << (8 * (m_cnt & 3));
         ++m_cnt;
+        if ((m_cnt & 3) == 0) {
+            if (m_cnt <= mel_cap) *(uint32_t*)(mel + m_cnt - 4) = m_word; else ovf = true;
+            m_word = 0;
+        }
     };
     auto mel_bit = [&](int v) {
         m_tmp = (m_tmp << 1) | (uint32_t)v;
@@ -276,21 +306,30 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
     if (ms_n > 0) {
         const int t = ms_k - ms_n;
         const uint32_t byte = ((uint32_t)ms_acc | (((1u << t) - 1) << ms_n)) & 0xFF;
-        if (byte != 0xFF) {
-            ms_word |= byte << (8 * (ms_pos & 3));
-            ++ms_pos;
-            if ((ms_pos & 3) == 0) { *(uint32_t*)(slot + ms_pos - 4) = ms_word; ms_word = 0; }
-        }
-        if (ms_pos & 3) *(uint32_t*)(slot + (ms_pos & ~3u)) = ms_word;
-    } else {
-        if (ms_pos & 3) *(uint32_t*)(slot + (ms_pos & ~3u)) = ms_word;
-        if (ms_k == 7) --ms_pos;   // a trailing 0xFF is dropped
+        if (byte != 0xFF) ms_byte(byte);
+    }
+    // the MagSgn line in progress: its dwords up to ms_pos (a line just completed is stored)
+    for (uint32_t d = 0; d < ((ms_pos & 15) + 3) / 4; ++d)
+        *(uint32_t*)(slot + (ms_pos & ~15u) + 4 * d) = (uint32_t)((d < 2 ? ms_l0 : ms_l1) >> (32 * (d & 1)));
+    if (ms_n == 0 && ms_k == 7) --ms_pos;   // a trailing 0xFF is dropped (it stays stored, past ms_pos)
+    if (m_cnt & 3) {   // the MEL dword in progress
+        if (m_cnt <= mel_cap) *(uint32_t*)(mel + (m_cnt & ~3u)) = m_word; else ovf = true;
     }
     const uint32_t scup = m_cnt + v_cnt + 1;
     if (ovf || (uint64_t)ms_pos + scup > G.data_cap || scup > 4079) {
         atomicOr(err, 1);
         info[4 * (size_t)b + 0] = 1; info[4 * (size_t)b + 1] = 0; info[4 * (size_t)b + 2] = 0; info[4 * (size_t)b + 3] = 0;
         return;
+    }
+    // the VLC line in progress: its bytes from the last one down to the line's top (or the
+    // slot end), one by one - MEL bytes go right below them
+    {
+        uint8_t* lo = tail_end - 1 - (int)v_cnt;   // the last VLC byte
+        uint8_t* hi = v_line + 16 < tail_end ? v_line + 16 : tail_end;
+        for (uint8_t* a = lo; a < hi; ++a) {
+            const uint32_t o = (uint32_t)(a - v_line);
+            *a = (uint8_t)((o < 8 ? v_l0 >> (8 * o) : v_l1 >> (8 * (o - 8))) & 0xFF);
+        }
     }
     uint8_t* tail = tail_end - scup;
     for (uint32_t i = 0; i < m_cnt; ++i) tail[i] = mel[i];
@@ -351,15 +390,27 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     const uint32_t pcup = lcup - scup;
     const int umax = (int)G.band_numbps - (int)G.numbps + 2;   // k_msbs + 2
 
+    // The three streams are read through 16-byte aligned register windows, the next window of
+    // each loaded one window ahead (its latency hides behind the 16 bytes in hand): a load per
+    // byte or dword on the lane's dependent chain left the wave waiting (SQ_WAIT_ANY 0.67,
+    // `profiles/r04_C4_sq.txt`).  The staging slot is 16-byte aligned and followed by >= 32
+    // bytes (and the buffer by 256), so the windows never leave the buffer going forward;
+    // going backward they stop at the slot start.
+    auto byte_of = [](const uint4& q, uint32_t o) -> uint32_t {   // byte o (0..15) of q
+        const uint32_t wd = o < 8 ? (o < 4 ? q.x : q.y) : (o < 12 ? q.z : q.w);
+        return (wd >> (8 * (o & 3))) & 0xFF;
+    };
+    const uint4* dq = reinterpret_cast<const uint4*>(d);
     // ---- MagSgn reader: forward, LSB first, 7 bits after 0xFF, 0xFF past Pcup
     uint64_t ms_acc = 0; int ms_n = 0; bool ms_ff = false; uint32_t ms_p = 0;
-    uint32_t ms_w = 0; int ms_wb = 0;
+    uint4 ms_cur = dq[0], ms_nxt = dq[1];   // bytes [ms_base, ms_base + 16), and the next 16
+    uint32_t ms_base = 0;
     auto ms_get = [&](int m) -> uint32_t {
         while (ms_n < m) {
             uint32_t byte;
             if (ms_p < pcup) {
-                if (ms_wb == 0) { ms_w = *(const uint32_t*)(d + (ms_p & ~3u)); ms_w >>= 8 * (ms_p & 3); ms_wb = 4 - (int)(ms_p & 3); }
-                byte = ms_w & 0xFF; ms_w >>= 8; --ms_wb;
+                if (ms_p - ms_base >= 16) { ms_cur = ms_nxt; ms_base += 16; ms_nxt = dq[(ms_base >> 4) + 1]; }
+                byte = byte_of(ms_cur, ms_p - ms_base);
             } else byte = 0xFF;
             ++ms_p;
             const int k = ms_ff ? 7 : 8;
@@ -374,9 +425,15 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     // ---- MEL reader: forward from Pcup, MSB first, 7 bits after 0xFF
     uint32_t mel_p = pcup, mel_cur = 0; int mel_bits = 0; bool mel_ff = false;
     int mel_k = 0, mel_run = 0; bool mel_one = false;
+    uint32_t mel_base = pcup & ~15u;
+    uint4 mel_w = dq[mel_base >> 4], mel_nxt = dq[(mel_base >> 4) + 1];
     auto mel_bit = [&]() -> int {
         if (mel_bits == 0) {
-            const uint32_t byte = mel_p < lcup ? d[mel_p] : 0xFF;
+            uint32_t byte = 0xFF;   // past Lcup
+            if (mel_p < lcup) {
+                if (mel_p - mel_base >= 16) { mel_w = mel_nxt; mel_base += 16; mel_nxt = dq[(mel_base >> 4) + 1]; }
+                byte = byte_of(mel_w, mel_p - mel_base);
+            }
             ++mel_p;
             mel_bits = mel_ff ? 7 : 8;
             mel_cur = byte & ((1u << mel_bits) - 1);
@@ -410,9 +467,16 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
         v_acc = t & ((1u << v_n) - 1);
         v_gt = d0 > 0x8F;
     }
+    // backward window: bytes [v_base, v_base + 16) and the 16 below (none below the slot start)
+    int v_base = (v_p >= 0 ? v_p : 0) & ~15;
+    uint4 v_cur = dq[v_base >> 4], v_prv = v_base >= 16 ? dq[(v_base >> 4) - 1] : make_uint4(0, 0, 0, 0);
     auto v_fill = [&]() {
         while (v_n <= 32) {
-            const uint32_t byte = v_p >= (int)pcup ? d[v_p] : 0u;
+            if (v_p < v_base && v_base > 0) {
+                v_cur = v_prv; v_base -= 16;
+                v_prv = v_base >= 16 ? dq[(v_base >> 4) - 1] : make_uint4(0, 0, 0, 0);
+            }
+            const uint32_t byte = v_p >= (int)pcup ? byte_of(v_cur, (uint32_t)(v_p - v_base)) : 0u;
             --v_p;
             const int k = (v_gt && (byte & 0x7F) == 0x7F) ? 7 : 8;
             v_acc |= (uint64_t)(byte & ((1u << k) - 1)) << v_n;

@@ -148,20 +148,23 @@ __device__ __forceinline__ int mirror(int i, int n) {
 // lane tx walks columns x0 + tx, x0 + 64 + tx of rows ty, ty+4, ... (two 256-byte segments
 // aligned to the row's cache lines: starting them at the halo column x0 - 2 made every
 // segment touch three 128-byte lines), the halo columns x0-2, x0-1, x0+TW as one extra pass
-// (no index division on the interior path).
+// (no index division on this path).  Every tile whose TW columns lie inside the resolution
+// takes it - rows and halo columns mirrored where they fall outside (a tile-grid border) -
+// and only a last, partial tile column the general per-position path.
 __device__ __forceinline__ int fwd53_halo_lx(int j) { return j < 2 ? j : DWT_TW + 2; }   // LDS columns 0, 1, TW+2
+__device__ __forceinline__ bool fullw53(int x0, int w) { return x0 + DWT_TW <= w; }
 template <class F>
 __device__ __forceinline__ void fwd53_fill(int x0, int y0, int w, int h, int tid, F f) {
     const int tx = tid & 63, ty = tid >> 6;
-    if (x0 >= 2 && y0 >= 2 && x0 + DWT_TW < w && y0 + DWT_TH < h) {   // interior tile
+    if (fullw53(x0, w)) {
         for (int ly = ty; ly < DWT_LH; ly += 4) {
-            const int gy = y0 - 2 + ly;
+            const int gy = mirror(y0 - 2 + ly, h);
             f(ly, tx + 2, gy, x0 + tx);
             f(ly, tx + 66, gy, x0 + 64 + tx);
         }
         for (int i = tid; i < 3 * DWT_LH; i += 256) {   // halo columns x0-2, x0-1, x0+TW
             const int ly = i / 3, lx = fwd53_halo_lx(i % 3);
-            f(ly, lx, y0 - 2 + ly, x0 - 2 + lx);
+            f(ly, lx, mirror(y0 - 2 + ly, h), mirror(x0 - 2 + lx, w));
         }
     } else {
         for (int i = tid; i < DWT_LH * DWT_LW; i += 256) {
@@ -263,9 +266,6 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restri
 #define L1_EDGE ((DWT_LH * DWT_LW + 255) / 256)     // positions per thread on edge tiles
 static_assert(L1_EDGE <= L1_SLOTS, "edge-tile positions fit the register slots");
 static_assert(32 * DWT_LH <= 256 * L1_GROUPS, "interior groups fit");
-__device__ __forceinline__ bool interior53(int x0, int y0, int w, int h) {
-    return x0 >= 2 && y0 >= 2 && x0 + DWT_TW < w && y0 + DWT_TH < h;
-}
 template <class F>   // f(group, ly, lx): interior groups of four positions (ly, lx .. lx + 3)
 __device__ __forceinline__ void fwd53_groups(int tid, F f) {
 #pragma unroll
@@ -299,12 +299,12 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_l1(GkPtr3 in, uint32_t sin, i
             T[ly][lx] = r0 - shift;
         }
     };
-    const bool inner = interior53(x0, y0, (int)w, (int)h);
+    const bool inner = fullw53(x0, (int)w);   // (rows and halo columns mirrored)
     if (inner) {
         // (x0 is a multiple of 128, so every group is aligned when the plane rows are)
         const bool v = vec && al4(p0) && al4(p1) && al4(p2);
         fwd53_groups(tid, [&](int g, int ly, int lx) {
-            const size_t i = (size_t)(y0 - 2 + ly) * sin + (x0 - 2 + lx);
+            const size_t i = (size_t)mirror(y0 - 2 + ly, (int)h) * sin + (x0 - 2 + lx);
             const int4 a = ld4v(p0 + i, v);
             const int4 b = NC == 3 ? ld4v(p1 + i, v) : a, c = NC == 3 ? ld4v(p2 + i, v) : a;
             put(4 * g, ly, lx, a.x, b.x, c.x);
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) void k_dwt53_fwd_l1(GkPtr3 in, uint32_t sin, i
         });
         if (tid < 3 * DWT_LH) {   // halo columns x0-2, x0-1, x0+TW
             const int ly = tid / 3, lx = fwd53_halo_lx(tid % 3);
-            const size_t i = (size_t)(y0 - 2 + ly) * sin + (x0 - 2 + lx);
+            const size_t i = (size_t)mirror(y0 - 2 + ly, (int)h) * sin + mirror(x0 - 2 + lx, (int)w);
             put(4 * L1_GROUPS, ly, lx, (int32_t)p0[i], (int32_t)p1[i], (int32_t)p2[i]);
         }
     } else {
@@ -367,27 +367,29 @@ template <class F>
 __device__ __forceinline__ void inv53_fill(int x0, int y0, int w, int h, int tid, F f) {
     const int tx = tid & 63, ty = tid >> 6;
     const int snw = (w + 1) >> 1, snh = (h + 1) >> 1;
-    if (x0 >= 1 && y0 >= 1 && x0 + DWT_TW + 1 < w && y0 + DWT_TH + 1 < h) {   // interior tile
+    auto sxo = [&](int gx) { return (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1); };
+    if (fullw53(x0, w)) {   // (rows and halo columns mirrored, as fwd53_fill)
         // interleaved column gx = x0 - 1 + lx: odd lx <=> even gx (L sample x0/2 + k, lx = 1 + 2k),
         // even lx <=> odd gx (H sample x0/2 - 1 + k, lx = 2k).  The main pass reads L samples
         // x0/2 + tx and H samples x0/2 + tx (lx = 2 + 2 tx), both segments starting on a line
         // boundary when the band starts on one (snw a multiple of 32)
         for (int ly = ty; ly < IDWT_LH; ly += 4) {
-            const int gy = y0 - 1 + ly;
+            const int gy = mirror(y0 - 1 + ly, h);
             const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
             f(ly, 1 + 2 * tx, sy, (x0 >> 1) + tx);
             f(ly, 2 + 2 * tx, sy, snw + (x0 >> 1) + tx);
         }
-        for (int i = tid; i < 3 * IDWT_LH; i += 256) {   // lx 0 (H x0/2 - 1), 129 (L), 130 (H)
-            const int ly = i / 3, j = i % 3, gy = y0 - 1 + ly;
+        for (int i = tid; i < 3 * IDWT_LH; i += 256) {   // lx 0 (gx x0 - 1), 129 (x0 + TW), 130 (x0 + TW + 1)
+            const int ly = i / 3, j = i % 3, gy = mirror(y0 - 1 + ly, h);
             const int sy = (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1);
-            f(ly, j ? 128 + j : 0, sy, j == 0 ? snw + (x0 >> 1) - 1 : (j == 1 ? (x0 >> 1) + 64 : snw + (x0 >> 1) + 64));
+            const int lx = j ? 128 + j : 0;
+            f(ly, lx, sy, sxo(mirror(x0 - 1 + lx, w)));
         }
     } else {
         for (int i = tid; i < IDWT_LH * IDWT_LW; i += 256) {
             const int ly = i / IDWT_LW, lx = i % IDWT_LW;
             const int gy = mirror(y0 - 1 + ly, h), gx = mirror(x0 - 1 + lx, w);
-            f(ly, lx, (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1), (gx & 1) ? (snw + (gx >> 1)) : (gx >> 1));
+            f(ly, lx, (gy & 1) ? (snh + (gy >> 1)) : (gy >> 1), sxo(gx));
         }
     }
 }

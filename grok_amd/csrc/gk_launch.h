@@ -64,7 +64,7 @@ void gk_launch_t1_recon(hipStream_t st, const GkBlock* blocks, const uint32_t* i
 // one DWT level of any parity, either filter, one line per thread (gk_dwt_any.hip): forward
 // reads the input region of `in` and leaves the Mallat level in `out`, inverse the reverse
 void gk_launch_dwt_any(hipStream_t st, bool irrev, bool forward, int32_t* in, int32_t* out, uint32_t stride, uint32_t w,
-                       uint32_t h, uint32_t px, uint32_t py, GkTiles tb, GkComps cs);
+                       uint32_t h, uint32_t px, uint32_t py, GkTiles tb, GkComps cs, bool partial = false);
 // irreversible path (gk_dwt97.hip)
 // code-blocks with mode switches (gk_t1ms.hip)
 void gk_launch_t1_enc_ms(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, GkPass* passes,

@@ -416,10 +416,14 @@ static void fwd53_1d(int32_t* x, uint32_t n, std::vector<int32_t>& tmp, uint32_t
     (void)sn;
     memcpy(x, tmp.data(), n * sizeof(int32_t));
 }
+// A decode with a window (grk_decompress_set_window) runs Grok's partial-tile inverse for every
+// tile (CodeStreamDecompress.cpp:389, WaveletReverse.cpp:2237-2246); its single odd sample
+// across is shifted, S(buf, 0) >>= 1 (:1551-1554), where the whole-tile path divides (:583).
+static bool g_partial_inverse = false;
 static void inv53_1d(int32_t* x, uint32_t n, std::vector<int32_t>& tmp, uint32_t par, bool vertical) {
     if (n == 1) {
         // odd single sample: horizontal bandH[0] / 2, vertical bandL[0] >> 1 (WaveletReverse.cpp:583, :636)
-        if (par) x[0] = vertical ? (x[0] >> 1) : (x[0] / 2);
+        if (par) x[0] = (vertical || g_partial_inverse) ? (x[0] >> 1) : (x[0] / 2);
         return;
     }
     if (n < 2) return;
@@ -2968,6 +2972,17 @@ static size_t resync_part_end(const uint8_t* cs, size_t len, size_t pos, size_t 
     return end;
 }
 
+// the next decodes as through a decode window (Grok's partial-tile inverse), or not
+extern "C" void orc_set_partial(int on) { g_partial_inverse = on != 0; }
+// the inverse 5/3 of a single-sample line holding v (test hook for the rule above)
+extern "C" int32_t orc_inv53_single(int32_t v, uint32_t par, int vertical, int partial) {
+    const bool was = g_partial_inverse;
+    g_partial_inverse = partial != 0;
+    std::vector<int32_t> tmp;
+    inv53_1d(&v, 1, tmp, par, vertical != 0);
+    g_partial_inverse = was;
+    return v;
+}
 int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_t* H, uint32_t* NC, uint32_t* PREC) {
     size_t i = 0;
     if (len >= 12 && get32(cs) == 12 && get32(cs + 4) == 0x6a502020) {   // JP2: find the jp2c box

@@ -56,6 +56,9 @@ def lib():
                                     ctypes.c_uint32, ctypes.c_int, P(CParams), ctypes.c_void_p, ctypes.c_size_t]
         _lib.orc_decode.restype = ctypes.c_int
         _lib.orc_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p] + [P(ctypes.c_uint32)] * 4
+        _lib.orc_set_partial.argtypes = [ctypes.c_int]
+        _lib.orc_inv53_single.argtypes = [ctypes.c_int32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+        _lib.orc_inv53_single.restype = ctypes.c_int32
         _lib.orc_forward_coefs.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_uint32, ctypes.c_int, P(CParams), P(ctypes.c_int32)]
         _lib.orc_encode_blocks.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -221,7 +224,10 @@ def set_decode_reduce(n):
     lib().orc_set_decode_reduce(ctypes.c_uint32(int(n)))
 
 
-def decode(cs):
+def decode(cs, partial=False):
+    """Decode the whole image.  partial: as Grok decodes once a window is set (its partial-tile
+    inverse for every tile, which shifts a single odd 5/3 sample across instead of halving it);
+    crop the result to the window."""
     buf = np.frombuffer(cs, dtype=np.uint8).copy()
     buf = np.concatenate([buf, np.zeros(8, np.uint8)])
     W, H, NC, PREC = (ctypes.c_uint32() for _ in range(4))
@@ -230,8 +236,12 @@ def decode(cs):
     if rc != 0:
         raise RuntimeError("oracle decode header failed: %d" % rc)
     out = np.empty((NC.value, H.value, W.value), dtype=np.int32)
-    rc = lib().orc_decode(buf.ctypes.data, len(cs), out.ctypes.data, ctypes.byref(W), ctypes.byref(H),
-                          ctypes.byref(NC), ctypes.byref(PREC))
+    lib().orc_set_partial(int(bool(partial)))
+    try:
+        rc = lib().orc_decode(buf.ctypes.data, len(cs), out.ctypes.data, ctypes.byref(W), ctypes.byref(H),
+                              ctypes.byref(NC), ctypes.byref(PREC))
+    finally:
+        lib().orc_set_partial(0)
     if rc != 0:
         raise RuntimeError("oracle decode failed: %d" % rc)
     return out, PREC.value

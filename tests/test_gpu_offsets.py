@@ -104,3 +104,23 @@ def test_offsets_refused(eng):
         eng.encode(img, 8, params=G.default_params(tiles=(16, 16), tile_origin=(9, 9)), origin=(5, 5))
     with pytest.raises(RuntimeError, match="first tile"):
         eng.encode(img, 8, params=G.default_params(tiles=(16, 16), tile_origin=(0, 0)), origin=(20, 20))
+
+
+def test_window_takes_partial_inverse_rule(eng):
+    # A tile one column wide on an odd canvas coordinate (image origin x 63, 64-wide tiles) has a
+    # single odd sample across at its top resolution.  Grok decodes through a window with its
+    # partial-tile inverse (S >>= 1) and without one with bandH / 2; the engine follows
+    # (ctx->dwt_partial) and so does the oracle (decode(partial=True)); the two can differ only
+    # on a negative odd coefficient of a lossy stream, so both rules are also checked directly
+    # (test_grok_defects.py::test_single_odd_sample_rule)
+    import grok_amd as G
+    img = _img(90, 110, 3, 8, 77)
+    kw = dict(tiles=(64, 64), layer_rate=[3.0])
+    p = G.default_params(tiles=(64, 64), numlayers=1, layer_rate=[3.0])
+    cs = eng.encode(img, 8, params=p, origin=(63, 0))
+    assert cs == O.encode(img, 8, origin=(63, 0), **kw)
+    whole, _ = O.decode(cs)
+    part, _ = O.decode(cs, partial=True)
+    np.testing.assert_array_equal(eng.decode(cs), whole)
+    win = (0, 5, 40, 80)
+    np.testing.assert_array_equal(eng.decode_window(cs, win), part[:, win[1]:win[3], win[0]:win[2]])

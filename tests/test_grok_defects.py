@@ -69,3 +69,17 @@ def test_simulation_counted_lengths_decode(flags):
     assert _psnr(dec, img, 255) > 30.5
     with pytest.raises(Exception):   # OpenJPEG 2.5.4: "broken data stream"
         _openjpeg(cs)
+
+
+@pytest.mark.parametrize("v,vertical,partial,want", [
+    (-3, False, False, -1),   # whole-tile decode: bandH[0] / 2 (WaveletReverse.cpp:583)
+    (-3, False, True, -2),    # decode window: Grok's partial-tile path, S(buf, 0) >>= 1 (:1551-1554)
+    (-3, True, False, -2),    # down a column both paths shift (:636, :1735)
+    (-3, True, True, -2),
+    (5, False, False, 2), (5, False, True, 2),
+])
+def test_single_odd_sample_rule(v, vertical, partial, want):
+    # a one-sample line on an odd coordinate holds a high-pass coefficient; Grok halves it
+    # differently in its whole-tile and window decodes, and so do the oracle and the engine
+    # (gk_dwt_any.hip inv53_line, ctx->dwt_partial)
+    assert O.lib().orc_inv53_single(v, 1, int(vertical), int(partial)) == want
