@@ -50,7 +50,7 @@ __device__ __forceinline__ void uvlc_code(int u, uint32_t& pre, int& plen, uint3
 __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ coef, const GkBlock* __restrict__ blocks,
                                                   uint8_t* __restrict__ bytes, uint8_t* __restrict__ mel_scratch,
                                                   uint32_t mel_cap, uint32_t* __restrict__ info, uint32_t nblocks,
-                                                  int* __restrict__ err) {
+                                                  int* __restrict__ err, uint32_t nl) {
     __shared__ uint16_t s_tab[2][2048];
     __shared__ uint8_t s_e[HT_LINE][HT_WG];
     __shared__ uint8_t s_cx[HT_LINE][HT_WG];
@@ -60,8 +60,10 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
     const int tid = threadIdx.x;
     for (int i = tid; i < 2048; i += HT_WG) { s_tab[0][i] = HT_VLC_ENC0[i]; s_tab[1][i] = HT_VLC_ENC1[i]; }
     __syncthreads();
-    const uint32_t b = blockIdx.x * HT_WG + tid;
-    if (b >= nblocks) return;
+    // nl blocks per wave (the other lanes idle): more, thinner waves per SIMD hide the serial
+    // coder's memory waits behind each other (GK_HT_LANES)
+    const uint32_t b = (blockIdx.x * (HT_WG / 64) + (tid >> 6)) * nl + (tid & 63);
+    if ((uint32_t)(tid & 63) >= nl || b >= nblocks) return;
 
     const GkBlock G = blocks[b];
     const int32_t* src = coef + G.band_off;
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
 // =============================================================================
 __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ bytes, const GkBlock* __restrict__ blocks,
                                                   const uint32_t* __restrict__ ids, int32_t* __restrict__ coef,
-                                                  uint32_t nblocks, int* __restrict__ err) {
+                                                  uint32_t nblocks, int* __restrict__ err, uint32_t nl) {
     __shared__ uint16_t s_tab[2][1024];
     __shared__ uint8_t s_e[HT_LINE][HT_WG];
     __shared__ uint8_t s_cx[HT_LINE][HT_WG];
@@ -357,8 +359,10 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     const int tid = threadIdx.x;
     for (int i = tid; i < 1024; i += HT_WG) { s_tab[0][i] = HT_VLC_DEC0[i]; s_tab[1][i] = HT_VLC_DEC1[i]; }
     __syncthreads();
-    const uint32_t b = blockIdx.x * HT_WG + tid;
-    if (b >= nblocks) return;
+    // nl blocks per wave (the other lanes idle): more, thinner waves per SIMD hide the serial
+    // coder's memory waits behind each other (GK_HT_LANES)
+    const uint32_t b = (blockIdx.x * (HT_WG / 64) + (tid >> 6)) * nl + (tid & 63);
+    if ((uint32_t)(tid & 63) >= nl || b >= nblocks) return;
 
     const GkBlock G = blocks[ids ? ids[b] : b];
     int32_t* dst = coef + G.band_off;
@@ -390,27 +394,15 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     const uint32_t pcup = lcup - scup;
     const int umax = (int)G.band_numbps - (int)G.numbps + 2;   // k_msbs + 2
 
-    // The three streams are read through 16-byte aligned register windows, the next window of
-    // each loaded one window ahead (its latency hides behind the 16 bytes in hand): a load per
-    // byte or dword on the lane's dependent chain left the wave waiting (SQ_WAIT_ANY 0.67,
-    // `profiles/r04_C4_sq.txt`).  The staging slot is 16-byte aligned and followed by >= 32
-    // bytes (and the buffer by 256), so the windows never leave the buffer going forward;
-    // going backward they stop at the slot start.
-    auto byte_of = [](const uint4& q, uint32_t o) -> uint32_t {   // byte o (0..15) of q
-        const uint32_t wd = o < 8 ? (o < 4 ? q.x : q.y) : (o < 12 ? q.z : q.w);
-        return (wd >> (8 * (o & 3))) & 0xFF;
-    };
-    const uint4* dq = reinterpret_cast<const uint4*>(d);
     // ---- MagSgn reader: forward, LSB first, 7 bits after 0xFF, 0xFF past Pcup
     uint64_t ms_acc = 0; int ms_n = 0; bool ms_ff = false; uint32_t ms_p = 0;
-    uint4 ms_cur = dq[0], ms_nxt = dq[1];   // bytes [ms_base, ms_base + 16), and the next 16
-    uint32_t ms_base = 0;
+    uint32_t ms_w = 0; int ms_wb = 0;
     auto ms_get = [&](int m) -> uint32_t {
         while (ms_n < m) {
             uint32_t byte;
             if (ms_p < pcup) {
-                if (ms_p - ms_base >= 16) { ms_cur = ms_nxt; ms_base += 16; ms_nxt = dq[(ms_base >> 4) + 1]; }
-                byte = byte_of(ms_cur, ms_p - ms_base);
+                if (ms_wb == 0) { ms_w = *(const uint32_t*)(d + (ms_p & ~3u)); ms_w >>= 8 * (ms_p & 3); ms_wb = 4 - (int)(ms_p & 3); }
+                byte = ms_w & 0xFF; ms_w >>= 8; --ms_wb;
             } else byte = 0xFF;
             ++ms_p;
             const int k = ms_ff ? 7 : 8;
@@ -425,15 +417,9 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     // ---- MEL reader: forward from Pcup, MSB first, 7 bits after 0xFF
     uint32_t mel_p = pcup, mel_cur = 0; int mel_bits = 0; bool mel_ff = false;
     int mel_k = 0, mel_run = 0; bool mel_one = false;
-    uint32_t mel_base = pcup & ~15u;
-    uint4 mel_w = dq[mel_base >> 4], mel_nxt = dq[(mel_base >> 4) + 1];
     auto mel_bit = [&]() -> int {
         if (mel_bits == 0) {
-            uint32_t byte = 0xFF;   // past Lcup
-            if (mel_p < lcup) {
-                if (mel_p - mel_base >= 16) { mel_w = mel_nxt; mel_base += 16; mel_nxt = dq[(mel_base >> 4) + 1]; }
-                byte = byte_of(mel_w, mel_p - mel_base);
-            }
+            const uint32_t byte = mel_p < lcup ? d[mel_p] : 0xFF;
             ++mel_p;
             mel_bits = mel_ff ? 7 : 8;
             mel_cur = byte & ((1u << mel_bits) - 1);
@@ -467,16 +453,9 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
         v_acc = t & ((1u << v_n) - 1);
         v_gt = d0 > 0x8F;
     }
-    // backward window: bytes [v_base, v_base + 16) and the 16 below (none below the slot start)
-    int v_base = (v_p >= 0 ? v_p : 0) & ~15;
-    uint4 v_cur = dq[v_base >> 4], v_prv = v_base >= 16 ? dq[(v_base >> 4) - 1] : make_uint4(0, 0, 0, 0);
     auto v_fill = [&]() {
         while (v_n <= 32) {
-            if (v_p < v_base && v_base > 0) {
-                v_cur = v_prv; v_base -= 16;
-                v_prv = v_base >= 16 ? dq[(v_base >> 4) - 1] : make_uint4(0, 0, 0, 0);
-            }
-            const uint32_t byte = v_p >= (int)pcup ? byte_of(v_cur, (uint32_t)(v_p - v_base)) : 0u;
+            const uint32_t byte = v_p >= (int)pcup ? d[v_p] : 0u;
             --v_p;
             const int k = (v_gt && (byte & 0x7F) == 0x7F) ? 7 : 8;
             v_acc |= (uint64_t)(byte & ((1u << k) - 1)) << v_n;
@@ -621,16 +600,28 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     if (bad) { atomicOr(err, 4); zero_block(); }
 }
 
+// blocks per 64-lane wave (1..64).  C4 (66,304 blocks), T1 encode / decode: 64 lanes 3.13 / 5.50
+// ms, 48 lanes 3.04 / 5.17, 32 lanes 3.27 / 5.23, 16 lanes 5.38 / 8.33 (one wave per SIMD leaves
+// each serial coder's memory waits exposed; 48 lanes put a second wave on a third of the SIMDs)
+static uint32_t ht_lanes(const char* var) {
+    const char* v = getenv(var);
+    const int n = v ? atoi(v) : 48;
+    return (uint32_t)(n < 1 ? 1 : (n > 64 ? 64 : n));
+}
 void gk_launch_ht_enc(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, uint8_t* mel_scratch,
                       uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_ht_enc, dim3((nblocks + HT_WG - 1) / HT_WG), dim3(HT_WG), 0, st, coef, blocks, bytes,
-                       mel_scratch, mel_cap, info, nblocks, err);
+    static const uint32_t nl = ht_lanes("GK_HT_ENC_LANES");
+    const uint32_t per = (HT_WG / 64) * nl;
+    hipLaunchKernelGGL(k_ht_enc, dim3((nblocks + per - 1) / per), dim3(HT_WG), 0, st, coef, blocks, bytes,
+                       mel_scratch, mel_cap, info, nblocks, err, nl);
 }
 
 void gk_launch_ht_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* ids, int32_t* coef,
                       uint32_t nblocks, int* err) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(k_ht_dec, dim3((nblocks + HT_WG - 1) / HT_WG), dim3(HT_WG), 0, st, bytes, blocks, ids, coef,
-                       nblocks, err);
+    static const uint32_t nl = ht_lanes("GK_HT_DEC_LANES");
+    const uint32_t per = (HT_WG / 64) * nl;
+    hipLaunchKernelGGL(k_ht_dec, dim3((nblocks + per - 1) / per), dim3(HT_WG), 0, st, bytes, blocks, ids, coef,
+                       nblocks, err, nl);
 }

@@ -123,8 +123,8 @@ __device__ __forceinline__ uint32_t col4(uint64_t a, uint64_t b, uint64_t c, uin
 }
 enum { PH_FIND = 1, PH_SIGN = 2, PH_UNI1 = 4, PH_UNI2 = 8 };   // one-hot: the step tests bits
 
-struct Rows22 {   // one stripe's rows: S1..S5 / N1..N5 (rows y0..y0+4), P/M/B (rows y0..y0+3), S0 / N0 (row y0-1)
-    uint64_t s0, s1, s2, s3, s4, s5, n0, n1, n2, n3, n4, n5, p0, p1, p2, p3, m0, m1, m2, m3, b0, b1, b2, b3;
+struct Rows22 {   // one stripe's rows: S1..S5 / N1..N5 (rows y0..y0+4), P/M/B (rows y0..y0+3)
+    uint64_t s1, s2, s3, s4, s5, n1, n2, n3, n4, n5, p0, p1, p2, p3, m0, m1, m2, m3, b0, b1, b2, b3;
 };
 // rows of stripe y0 / plane `k` from the lane's scratch slab (consecutive words per field)
 __device__ __forceinline__ void ld2(const uint64_t* p, uint64_t& a, uint64_t& b) {   // 16-byte aligned pair
@@ -135,14 +135,10 @@ __device__ __forceinline__ void st2(uint64_t* p, uint64_t a, uint64_t b) { *(ulo
 // Only the rows the stripe-pass of type t (0 SP, 1 MR, 2 CL) reads are fetched: SP starts a
 // plane (no plane-bit or visited rows) and ignores refinement rows; MR ignores signs; CL
 // ignores refinement rows; the first cleanup pass (k == 0) has no plane or visited rows yet.
-// `above`: also the row above (the previous stripe's last row), for a stripe-pass not entered
-// from the stripe above it (empty stripe-passes skipped in between)
-__device__ __forceinline__ void load_rows(Rows22& R, const uint64_t* WS, uint32_t k, uint32_t t, uint32_t y0,
-                                          bool above = false) {
+__device__ __forceinline__ void load_rows(Rows22& R, const uint64_t* WS, uint32_t k, uint32_t t, uint32_t y0) {
     const uint64_t* st = WS + 4 * y0;   // this stripe's line (y0 = 4 s)
     const uint64_t* bt = WS + WS_BITS + (size_t)k * 64 + y0;
     ld2(st + WS_S, R.s1, R.s2); ld2(st + WS_S + 2, R.s3, R.s4); R.s5 = st[16 + WS_S];
-    if (above && y0) { R.s0 = st[WS_S + 3 - 16]; R.n0 = st[WS_N + 3 - 16]; }
     if (t != 1) { ld2(st + WS_N, R.n1, R.n2); ld2(st + WS_N + 2, R.n3, R.n4); R.n5 = st[16 + WS_N]; }
     if (t != 0 && k != 0) { ld2(st + WS_P, R.p0, R.p1); ld2(st + WS_P + 2, R.p2, R.p3); ld2(bt, R.b0, R.b1); ld2(bt + 2, R.b2, R.b3); }
     if (t == 1) { ld2(st + WS_M, R.m0, R.m1); ld2(st + WS_M + 2, R.m2, R.m3); }
@@ -669,31 +665,11 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
         }
     };
     Rows22 X = {};
-    // Empty stripe-passes are skipped: a magnitude-refinement stripe-pass codes the samples
-    // significant before the plane (prevS: a bit per stripe, taken when the plane's SP starts),
-    // a cleanup stripe-pass the samples neither significant nor visited by the plane's SP (clF:
-    // the stripe was full after its SP).  Both are known before the stripe-pass starts, so the
-    // stripe-pass the lane goes to next (nk, nt, nss, npi) - and the rows it prefetches - skip
-    // them; skipping changes no state (such a pass would set no bit).  C2's level-1 blocks: ~21 %
-    // of stripe-passes empty, mostly cleanup ones in the low planes, each costing its lane a
-    // wait for the next boundary event.
-    uint32_t anyS = 0, prevS = 0, clF = 0;     // per stripe: any significant sample; prevS; clF
-    uint32_t nk = k, nt = t, nss = s, npi = pidx;
-    uint32_t fprev = 0xffffffffu;               // the stripe finished at the previous switch,
-    bool lprev = false;                         // and whether its rows were stored late
-    auto target = [&]() {   // the next non-empty stripe-pass after (k, t, s) into (nk, nt, nss, npi)
-        nk = k; nt = t; nss = s; npi = pidx;
-        for (uint32_t g = 0; g < 2 * 16 + 2; ++g) {
-            next_pos3(nk, nt, nss, npi, ns);
-            if (npi >= npasses || nk >= numbps) break;
-            const bool emr = nt == 1 && !((prevS >> nss) & 1);
-            // (a cleanup stripe whose SP of this plane has not run yet has no clF bit)
-            const bool ecl = nt == 2 && ((clF >> nss) & 1) && !(nk == k && t == 0 && nss >= s);
-            if (!emr && !ecl) break;
-        }
-    };
-    target();
-    if (!done && npi < npasses && nk < numbps) load_rows(X, WS, nk, nt, 4 * nss, nss != s + 1);
+    {
+        uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
+        next_pos3(k2, t2, s2, p2, ns);
+        if (!done && p2 < npasses && k2 < numbps) load_rows(X, WS, k2, t2, 4 * s2);
+    }
 
     // the lane with the most stripe-passes left (the wave lasts as long as it does), wave-uniform
     auto critical_lane = [&]() -> uint32_t {
@@ -753,7 +729,7 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
             if (parked) {
                 parked = false;
                 switched = true;
-                const uint32_t y0 = 4 * s, f = s;
+                const uint32_t y0 = 4 * s;
                 // the finished stripe: rows back to scratch
                 const uint64_t S1 = g_get(Ls.sg, 1, lane), S2 = g_get(Ls.sg, 2, lane), S3 = g_get(Ls.sg, 3, lane),
                                S4 = g_get(Ls.sg, 4, lane);
@@ -761,13 +737,7 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
                                N4 = g_get(Ls.ng, 4, lane);
                 const uint64_t B0 = h_get(Ls.bt, 0, lane), B1 = h_get(Ls.bt, 1, lane), B2 = h_get(Ls.bt, 2, lane),
                                B3 = h_get(Ls.bt, 3, lane);
-                // the landing stripe-pass (prefetched into X) and whether X predates rows stored
-                // since: this stripe's (stored now) or the previous switch's late store
-                const uint32_t ft = t;
-                const bool ldone = npi >= npasses || nk >= numbps;
-                const bool stale = !ldone && (nss == f || nss + 1 == f ||
-                                              (lprev && (nss == fprev || nss + 1 == fprev || nss == fprev + 1)));
-                late = ns > 3 && !stale;
+                late = ns > 3;
                 // rows a stripe-pass left unchanged are not stored: `dirty` marks a stripe-pass that
                 // set a 1 bit in this plane's bit rows (a new significance in SP / CL, a refinement
                 // 1 in MR); scratch starts zero-filled and SP is the first pass to touch a plane's
@@ -778,15 +748,6 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
                 const uint64_t P0 = h_get(Ls.pv, 0, lane), P1 = h_get(Ls.pv, 1, lane), P2 = h_get(Ls.pv, 2, lane),
                                P3 = h_get(Ls.pv, 3, lane);
                 WP0 = P0; WP1 = P1; WP2 = P2; WP3 = P3;
-                // stripe masks: significance after SP / cleanup; full after SP (cleanup has nothing
-                // to code where every valid sample is significant or was visited)
-                if (ft != 1) anyS = (anyS & ~(1u << f)) | ((S1 | S2 | S3 | S4) != 0 ? 1u << f : 0u);
-                if (ft == 0) {
-                    const uint64_t u0 = nr > 0 ? colmask : 0, u1 = nr > 1 ? colmask : 0, u2 = nr > 2 ? colmask : 0,
-                                   u3 = nr > 3 ? colmask : 0;
-                    const bool full = ((~(S1 | P0) & u0) | (~(S2 | P1) & u1) | (~(S3 | P2) & u2) | (~(S4 | P3) & u3)) == 0;
-                    clF = (clF & ~(1u << f)) | (full ? 1u << f : 0u);
-                }
                 wy0 = y0; wk = k; wt = t;
                 if (!late) {
                     uint64_t* sgp = WS + 4 * y0 + WS_S;
@@ -801,23 +762,19 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
                     if (wdirty) { st2(btp, B0, B1); st2(btp + 2, B2, B3); }
                 }
                 if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[0] += t - tp0; tp0 = t; }
-                k = nk; t = nt; s = nss; pidx = npi;
-                done = ldone;
-                fprev = f; lprev = late;
-                if (!done && t == 0 && s == 0) prevS = anyS;   // a plane's SP starts: MR's candidates
+                next_pos3(k, t, s, pidx, ns);
+                done = pidx >= npasses || k >= numbps;
                 // New stripe rows come from the prefetch X, issued when the finished stripe
-                // started.  When that prefetch overlapped rows stored since (1-stripe blocks,
-                // 2-stripe blocks at a pass change, a skip that wrapped round to the finished
-                // stripe or its neighbours), the lane stored early above and reloads them now
-                // (rare: the smallest bands).
-                const bool resync = stale;
+                // started.  For 1-stripe blocks (and 2-stripe blocks at a pass change) that
+                // prefetch overlapped the finished stripe's rows, so those lanes reload them
+                // now, after the write-back above (rare: only the smallest bands).
+                const bool resync = !done && (ns == 1 || (ns == 2 && s == 0));
                 if (__any(resync)) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (resync) load_rows(X, WS, k, t, 4 * s, s != f + 1);
+                    if (resync) load_rows(X, WS, k, t, 4 * s);
                 }
                 const bool newplane = t == 0 || k == 0;
-                // the row above: the finished stripe's last row when it is the stripe above
-                const uint64_t nS0 = s == 0 ? 0ull : (s == f + 1 ? S4 : X.s0), nN0 = s == 0 ? 0ull : (s == f + 1 ? N4 : X.n0);
+                const uint64_t nS0 = s ? S4 : 0ull, nN0 = s ? N4 : 0ull;
                 const uint64_t nS1 = X.s1, nS2 = X.s2, nS3 = X.s3, nS4 = X.s4, nS5 = X.s5;
                 const uint64_t nN1 = X.n1, nN2 = X.n2, nN3 = X.n3, nN4 = X.n4, nN5 = X.n5;
                 const uint64_t nM0 = X.m0, nM1 = X.m1, nM2 = X.m2, nM3 = X.m3;
@@ -865,10 +822,10 @@ __global__ __launch_bounds__(64 * W) void k_t1_dec2(const uint8_t* __restrict__ 
             uint64_t tq0 = TIMING ? __builtin_amdgcn_s_memtime() : 0;
             if (q.sbase != q.fill) { q.sbase = q.fill; stage_load(q); }
             if (TIMING) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc_p[4] += t - tq0; tq0 = t; }
-            if (switched && !done) {
-                target();
-                if (npi < npasses && nk < numbps) load_rows(X, WS, nk, nt, 4 * nss, nss != s + 1);
-            }
+            uint32_t k2 = k, t2 = t, s2 = s, p2 = pidx;
+            next_pos3(k2, t2, s2, p2, ns);
+            if (switched && !done && p2 < npasses && k2 < numbps)
+                load_rows(X, WS, k2, t2, 4 * s2);
             if (late) {
                 uint64_t* sgp = WS + 4 * wy0 + WS_S;
                 uint64_t* ngp = WS + 4 * wy0 + WS_N;
