@@ -57,8 +57,13 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
     // Input staging: a lane's 8 columns x 2 rows, loaded as two 16-byte pieces per row when its
     // quads reach them (a 4-byte load per sample was a 64-line gather, one block per lane).
     __shared__ int32_t s_in[2][8][HT_WG];
+    // Output staging: the lane's current 64-byte block of the MagSgn and of the VLC stream
+    // (four 16-byte lines each), stored to HBM as four consecutive 16-byte stores once complete
+    __shared__ uint4 s_ms[4][HT_WG], s_v[4][HT_WG];
     const int tid = threadIdx.x;
     for (int i = tid; i < 2048; i += HT_WG) { s_tab[0][i] = HT_VLC_ENC0[i]; s_tab[1][i] = HT_VLC_ENC1[i]; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s_v[i][tid] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     // nl blocks per wave (the other lanes idle): more, thinner waves per SIMD hide the serial
     // coder's memory waits behind each other (GK_HT_LANES)
@@ -73,10 +78,12 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
     uint8_t* mel = mel_scratch + (size_t)b * mel_cap;
     bool ovf = false;
 
-    // Output bytes leave in whole 16-byte lines: each stream collects its bytes in a 16-byte
-    // register line aligned like its destination and stores the line once complete (one
-    // 16-byte store per lane instead of one store per byte or per dword: a wave's byte stores
-    // touched 64 lines each and the encoder wrote 3.4x its output, `profiles/r04s_C4_pmc.txt`).
+    // Output bytes leave in whole 64-byte blocks: each stream collects its bytes in a 16-byte
+    // register line aligned like its destination, a complete line goes to the lane's LDS block,
+    // and a complete block leaves as four consecutive 16-byte stores.  (One block per lane
+    // makes every store instruction a 64-line scatter; byte stores, and then single 16-byte
+    // lines, left partial lines in L2 that were written back more than once: the encoder wrote
+    // 3.4x its output, `profiles/r04s_C4_pmc.txt`, `r05_C4_pmc.txt`.)
     // ---- MagSgn: LSB-first, a byte after 0xFF carries 7 bits; forward from the slot start
     // (64-byte aligned)
     uint64_t ms_acc = 0; int ms_n = 0, ms_k = 8; uint32_t ms_pos = 0;
@@ -86,8 +93,12 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
         if (o < 8) ms_l0 |= (uint64_t)byte << (8 * o); else ms_l1 |= (uint64_t)byte << (8 * (o - 8));
         ++ms_pos;
         if ((ms_pos & 15) == 0) {
-            *(uint4*)(slot + ms_pos - 16) = make_uint4((uint32_t)ms_l0, (uint32_t)(ms_l0 >> 32), (uint32_t)ms_l1, (uint32_t)(ms_l1 >> 32));
+            s_ms[((ms_pos - 16) >> 4) & 3][tid] = make_uint4((uint32_t)ms_l0, (uint32_t)(ms_l0 >> 32), (uint32_t)ms_l1, (uint32_t)(ms_l1 >> 32));
             ms_l0 = ms_l1 = 0;
+            if ((ms_pos & 63) == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) *(uint4*)(slot + ms_pos - 64 + 16 * i) = s_ms[i][tid];
+            }
         }
     };
     auto ms_put = [&](uint32_t v, int m) {
@@ -101,9 +112,10 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
     };
     // ---- VLC: LSB-first, grows backward from the slot end; after a byte > 0x8F the
     // next byte's MSB is a stuffed 0 unless its low 7 bits differ from 0x7F.  Byte i goes to
-    // tail_end - 2 - i; the register line holds the 16-byte aligned line of the current byte and
-    // is stored when the stream moves below it.  (A line above the slot end is padding before
-    // the next 64-byte aligned slot; the locator bytes are stored last.)
+    // tail_end - 2 - i; the register line holds the 16-byte aligned line of the current byte, a
+    // line the stream moves below goes to the LDS block, and the block leaves once its lowest
+    // line is complete.  (Lines of a block above the slot end lie in the padding before the
+    // next 64-byte aligned slot; the locator bytes are stored last.)
     uint64_t v_acc = 0xF; int v_n = 4; bool v_gt = true; uint32_t v_cnt = 0, v_first = 0;
     uint64_t v_l0 = 0, v_l1 = 0;
     uint8_t* v_line = (uint8_t*)((uintptr_t)(tail_end - 2) & ~(uintptr_t)15);
@@ -111,7 +123,11 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
         if (v_cnt == 0) v_first = byte;
         uint8_t* a = tail_end - 2 - (int)v_cnt;
         if (a < v_line) {   // the line above is complete
-            *(uint4*)v_line = make_uint4((uint32_t)v_l0, (uint32_t)(v_l0 >> 32), (uint32_t)v_l1, (uint32_t)(v_l1 >> 32));
+            s_v[((uintptr_t)v_line >> 4) & 3][tid] = make_uint4((uint32_t)v_l0, (uint32_t)(v_l0 >> 32), (uint32_t)v_l1, (uint32_t)(v_l1 >> 32));
+            if (((uintptr_t)v_line & 63) == 0) {   // its block is complete
+#pragma unroll
+                for (int i = 0; i < 4; ++i) *(uint4*)(v_line + 16 * i) = s_v[i][tid];
+            }
             v_l0 = v_l1 = 0;
             v_line -= 16;
         }
@@ -310,7 +326,9 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
         const uint32_t byte = ((uint32_t)ms_acc | (((1u << t) - 1) << ms_n)) & 0xFF;
         if (byte != 0xFF) ms_byte(byte);
     }
-    // the MagSgn line in progress: its dwords up to ms_pos (a line just completed is stored)
+    // the MagSgn block in progress: its complete lines from LDS, then the line in progress up to
+    // ms_pos, dword by dword (a block just completed has been stored)
+    for (uint32_t i = 0; i < ((ms_pos & 63) >> 4); ++i) *(uint4*)(slot + (ms_pos & ~63u) + 16 * i) = s_ms[i][tid];
     for (uint32_t d = 0; d < ((ms_pos & 15) + 3) / 4; ++d)
         *(uint32_t*)(slot + (ms_pos & ~15u) + 4 * d) = (uint32_t)((d < 2 ? ms_l0 : ms_l1) >> (32 * (d & 1)));
     if (ms_n == 0 && ms_k == 7) --ms_pos;   // a trailing 0xFF is dropped (it stays stored, past ms_pos)
@@ -323,8 +341,11 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
         info[4 * (size_t)b + 0] = 1; info[4 * (size_t)b + 1] = 0; info[4 * (size_t)b + 2] = 0; info[4 * (size_t)b + 3] = 0;
         return;
     }
-    // the VLC line in progress: its bytes from the last one down to the line's top (or the
-    // slot end), one by one - MEL bytes go right below them
+    // the VLC block in progress: its complete lines above the current one from LDS (lines above
+    // the stream's first are zero: padding or the locator bytes stored below), then the line in
+    // progress: its bytes from the last one up to the line's top (or the slot end), one by one -
+    // MEL bytes go right below them
+    for (uint8_t* L = v_line + 16; ((uintptr_t)L & 63) != 0; L += 16) *(uint4*)L = s_v[((uintptr_t)L >> 4) & 3][tid];
     {
         uint8_t* lo = tail_end - 1 - (int)v_cnt;   // the last VLC byte
         uint8_t* hi = v_line + 16 < tail_end ? v_line + 16 : tail_end;
