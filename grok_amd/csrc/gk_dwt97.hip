@@ -473,13 +473,63 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ 
     tb.origin(tile, ox, oy);
     const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
     float R0[16], R1[16];
+    // Full-width tiles: the next component's input is loaded into registers (PF, the positions
+    // inv97_fill's full-width path visits) while the current one lifts (as k_dwt53_inv_l1).
+    constexpr int PF_ROWS = (T97_LH + 3) / 4, PF_HALO = (8 * T97_LH + 255) / 256;
+    float PF[2 * PF_ROWS + PF_HALO];
+    const bool inner = fullw97(x0, (int)w);
+    const int tx = tid & 63, ty = tid >> 6, hx = x0 >> 1;
+    const int snw = ((int)w + 1) >> 1, snh = ((int)h + 1) >> 1;
+    const float fe = w > 1 ? F97_K : 1.0f, fo = w > 1 ? I97_TWO_INVK : 1.0f;
+    auto srow = [&](int ly) {
+        const int gy = mirror97(y0 - T97_HALO + ly, (int)h);
+        return (size_t)((gy & 1) ? (snh + (gy >> 1)) : (gy >> 1)) * sstride;
+    };
+    auto hlx = [](int i) { const int j = i & 7; return j < 4 ? j : 128 + j; };
+    auto fetch = [&](const float* sc) {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < T97_LH) {
+                const float* r = sc + srow(ly) + hx + tx;
+                PF[2 * m] = r[0];
+                PF[2 * m + 1] = r[snw];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PF_HALO; ++k) {
+            const int i = tid + 256 * k;
+            if (i < 8 * T97_LH) {
+                const int gx = mirror97(x0 - T97_HALO + hlx(i), (int)w);
+                PF[2 * PF_ROWS + k] = sc[srow(i >> 3) + ((gx & 1) ? snw + (gx >> 1) : (gx >> 1))];
+            }
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < T97_LH) {
+                T[ly][T97_HALO + 2 * tx] = PF[2 * m] * fe;
+                T[ly][T97_HALO + 1 + 2 * tx] = PF[2 * m + 1] * fo;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PF_HALO; ++k) {
+            const int i = tid + 256 * k;
+            if (i < 8 * T97_LH) T[i >> 3][hlx(i)] = PF[2 * PF_ROWS + k] * ((hlx(i) & 1) ? fo : fe);
+        }
+    };
+    if (inner) fetch(src);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         if (c) __syncthreads();
         const float* sc = src + c * cstride;
-        inv97_fill(x0, y0, (int)w, (int)h, tid,
-                   [&](int ly, int lx, int sy, int sx, float f) { T[ly][lx] = sc[(size_t)sy * sstride + sx] * f; });
+        if (inner) put();
+        else inv97_fill(x0, y0, (int)w, (int)h, tid,
+                        [&](int ly, int lx, int sy, int sx, float f) { T[ly][lx] = sc[(size_t)sy * sstride + sx] * f; });
         __syncthreads();
+        if (inner && c + 1 < NC) fetch(sc + cstride);
         inv97_lift(T, (int)w, (int)h, tid);
         if (c + 1 < NC) {
 #pragma unroll

@@ -472,13 +472,52 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
     const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
     static_assert(DWT_TW * DWT_TH == 4 * 4 * 256, "four groups of four per thread");
     int32_t R0[16], R1[16];
+    // Full-width tiles: the next component's input is loaded into registers (PF, the positions
+    // inv53_fill's full-width path visits) while the current one lifts, so its HBM latency
+    // overlaps the lifting instead of following it.
+    constexpr int PF_ROWS = (IDWT_LH + 3) / 4;
+    int32_t PF[2 * PF_ROWS + 1];
+    const bool inner = fullw53(x0, (int)w);
+    const int tx = tid & 63, ty = tid >> 6;
+    const int snw = ((int)w + 1) >> 1, snh = ((int)h + 1) >> 1;
+    auto srow = [&](int ly) {
+        const int gy = mirror(y0 - 1 + ly, (int)h);
+        return (size_t)((gy & 1) ? (snh + (gy >> 1)) : (gy >> 1)) * sstride;
+    };
+    auto fetch = [&](const int32_t* sc) {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < IDWT_LH) {
+                const int32_t* r = sc + srow(ly) + (x0 >> 1) + tx;
+                PF[2 * m] = r[0];
+                PF[2 * m + 1] = r[snw];
+            }
+        }
+        if (tid < 3 * IDWT_LH) {   // lx 0, 129, 130 (as inv53_fill)
+            const int ly = tid / 3, j = tid % 3, lx = j ? 128 + j : 0;
+            const int gx = mirror(x0 - 1 + lx, (int)w);
+            PF[2 * PF_ROWS] = sc[srow(ly) + ((gx & 1) ? (snw + (gx >> 1)) : (gx >> 1))];
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < IDWT_LH) { T[ly][1 + 2 * tx] = PF[2 * m]; T[ly][2 + 2 * tx] = PF[2 * m + 1]; }
+        }
+        if (tid < 3 * IDWT_LH) { const int j = tid % 3; T[tid / 3][j ? 128 + j : 0] = PF[2 * PF_ROWS]; }
+    };
+    if (inner) fetch(src);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         if (c) LDS_BARRIER();   // the previous component's samples have been read
         const int32_t* sc = src + c * cstride;
-        inv53_fill(x0, y0, (int)w, (int)h, tid,
-                   [&](int ly, int lx, int sy, int sx) { T[ly][lx] = sc[(size_t)sy * sstride + sx]; });
+        if (inner) put();
+        else inv53_fill(x0, y0, (int)w, (int)h, tid,
+                        [&](int ly, int lx, int sy, int sx) { T[ly][lx] = sc[(size_t)sy * sstride + sx]; });
         LDS_BARRIER();
+        if (inner && c + 1 < NC) fetch(sc + cstride);
         inv53_lift(T, (int)w, (int)h, tid);
         if (c + 1 < NC) {
 #pragma unroll
