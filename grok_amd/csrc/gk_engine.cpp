@@ -3741,7 +3741,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // ---- T2 (T2Decompress.cpp:216-570), LRCP, per tile part.  Tile parts are independent
     // (own precincts, tag trees and code-blocks), so they are parsed in parallel host threads
     // into tile-local state (index = block - tile's first block).
-    struct Chunk { uint64_t pos; uint32_t b, len; };
+    struct Chunk { uint64_t pos; uint32_t b, len, boff; };   // boff: the block's bytes before this chunk
     struct PartState {
         std::vector<Chunk> chunks;
         std::vector<uint8_t> included, numbps;
@@ -3873,7 +3873,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         for (auto& ct : contrib) {
                             const uint32_t n = (uint32_t)std::min<size_t>(ct.second, tile_end > pos ? tile_end - pos : 0);
                             if (n && need[ct.first] && !skip_l) {
-                                st2.chunks.push_back({pos, ct.first, n});
+                                st2.chunks.push_back({pos, ct.first, n, st2.len[ct.first]});
                                 st2.len[ct.first] += n;
                             }
                             pos += ct.second;
@@ -3903,50 +3903,55 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // one tile's needed blocks into blk[nb0 ..) with staging offsets from o0 (its blocks in
     // (component, resolution, band, precinct, block) order); count-only when blk is null
     struct TileFill { int32_t q; uint32_t t, nb; uint64_t bytes, t1; };
-    auto fill_tile = [&](const TileFill& tf, uint32_t nb0, uint64_t o0, bool count_only, TileFill* out) {
+    // the blocks of one precinct-band (c, r, bi, pi) of a tile, continuing n / oo / t1
+    auto fill_prec = [&](const TileFill& tf, uint32_t c, uint32_t r, uint32_t bi, uint32_t pi, uint32_t nb0,
+                         bool count_only, uint32_t& n, uint64_t& oo, uint64_t& t1) {
         const TileG& T = P.tiles[tf.t];
         const PartState& st2 = ps[tf.q];
         const std::vector<uint8_t>& need = part_need[tf.q];
         std::vector<int32_t>& idx = part_idx[tf.q];
-        if (!count_only) idx.assign(T.b1 - T.b0, -1);
+        const ResG& R = T.comps[c].res[r];
+        const PrecG& PG = R.prc[bi][pi];
+        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+            const uint32_t lb = PG.first_block + k - T.b0;
+            if (!need[lb]) continue;
+            const uint32_t len = st2.len[lb];
+            if (!count_only) {
+                GkBlock& G = blk[nb0 + n];
+                G = P.blocks[T.b0 + lb];
+                G.band_off = relocate(P, RG, G.band_off);
+                G.stride = RG.stride;
+                G.band_numbps = (uint8_t)R.bands[bi].numbps;
+                G.step = R.bands[bi].step_dec / 2.0f;
+                if (P.p.ht() && P.p.irrev) {   // ScaleHTFilter: stepsize / 2^(31 - numbps) (Quantizer.cpp:52-62)
+                    if (R.bands[bi].numbps > 31) throw GkError("unsupported number of band bit-planes");
+                    G.step = R.bands[bi].step_dec / (float)(1u << (31 - R.bands[bi].numbps));
+                }
+                G.numbps = st2.numbps[lb];
+                G.npasses = len ? st2.npasses[lb] : 0;
+                if (multiseg) {
+                    G.data_cap = (uint32_t)hseglen.size();
+                    hseglen.insert(hseglen.end(), st2.seglens[lb].begin(), st2.seglens[lb].end());
+                }
+                G.data_off = oo;
+                G.len = len;
+                idx[lb] = (int32_t)(nb0 + n);
+            }
+            t1 += len;
+            oo += (((uint64_t)len + 15) & ~15ull) + 32;
+            ++n;
+        }
+    };
+    auto fill_tile = [&](const TileFill& tf, uint32_t nb0, uint64_t o0, bool count_only, TileFill* out) {
+        const TileG& T = P.tiles[tf.t];
+        if (!count_only) part_idx[tf.q].assign(T.b1 - T.b0, -1);
         uint32_t n = 0;
         uint64_t oo = o0, t1 = 0;
         for (uint32_t c = 0; c < P.nc; ++c)
             for (uint32_t r = 0; r < P.p.numres; ++r) {
                 const ResG& R = T.comps[c].res[r];
                 for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
-                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
-                        const PrecG& PG = R.prc[bi][pi];
-                        for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
-                            const uint32_t lb = PG.first_block + k - T.b0;
-                            if (!need[lb]) continue;
-                            const uint32_t len = st2.len[lb];
-                            if (!count_only) {
-                                GkBlock& G = blk[nb0 + n];
-                                G = P.blocks[T.b0 + lb];
-                                G.band_off = relocate(P, RG, G.band_off);
-                                G.stride = RG.stride;
-                                G.band_numbps = (uint8_t)R.bands[bi].numbps;
-                                G.step = R.bands[bi].step_dec / 2.0f;
-                                if (P.p.ht() && P.p.irrev) {   // ScaleHTFilter: stepsize / 2^(31 - numbps) (Quantizer.cpp:52-62)
-                                    if (R.bands[bi].numbps > 31) throw GkError("unsupported number of band bit-planes");
-                                    G.step = R.bands[bi].step_dec / (float)(1u << (31 - R.bands[bi].numbps));
-                                }
-                                G.numbps = st2.numbps[lb];
-                                G.npasses = len ? st2.npasses[lb] : 0;
-                                if (multiseg) {
-                                    G.data_cap = (uint32_t)hseglen.size();
-                                    hseglen.insert(hseglen.end(), st2.seglens[lb].begin(), st2.seglens[lb].end());
-                                }
-                                G.data_off = oo;
-                                G.len = 0;   // reused as the fill cursor below
-                                idx[lb] = (int32_t)(nb0 + n);
-                            }
-                            t1 += len;
-                            oo += (((uint64_t)len + 15) & ~15ull) + 32;
-                            ++n;
-                        }
-                    }
+                    for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) fill_prec(tf, c, r, bi, pi, nb0, count_only, n, oo, t1);
             }
         if (out) { out->nb = n; out->bytes = oo - o0; out->t1 = t1; }
     };
@@ -3968,6 +3973,36 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         }
         host_pool().run(tiles_in.size(), [&](size_t k) { fill_tile(tiles_in[k], tb0[k], to0[k], false, nullptr); });
         nblk = tb0.back(); o = to0.back();
+    } else if (!multiseg) {
+        // few tiles (C2 / C3: one, 49 k blocks): the same two passes over precinct-bands
+        struct Unit { uint32_t k, c, r, bi, pi, nb; uint64_t bytes, t1; };
+        std::vector<Unit> units;
+        for (uint32_t k = 0; k < tiles_in.size(); ++k) {
+            const TileG& T = P.tiles[tiles_in[k].t];
+            part_idx[tiles_in[k].q].assign(T.b1 - T.b0, -1);
+            for (uint32_t c = 0; c < P.nc; ++c)
+                for (uint32_t r = 0; r < P.p.numres; ++r) {
+                    const ResG& R = T.comps[c].res[r];
+                    for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
+                        for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi)
+                            if (R.prc[bi][pi].cw * R.prc[bi][pi].ch) units.push_back({k, c, r, bi, pi, 0, 0, 0});
+                }
+        }
+        auto run_unit = [&](size_t i, uint32_t nb0, uint64_t o0, bool count_only) {
+            Unit& u = units[i];
+            uint32_t n = 0;
+            uint64_t oo = o0, t1 = 0;
+            fill_prec(tiles_in[u.k], u.c, u.r, u.bi, u.pi, nb0, count_only, n, oo, t1);
+            if (count_only) { u.nb = n; u.bytes = oo - o0; u.t1 = t1; }
+        };
+        host_pool().run(units.size(), [&](size_t i) { run_unit(i, 0, 0, true); });
+        std::vector<uint32_t> ub(units.size());
+        std::vector<uint64_t> uo(units.size());
+        for (size_t i = 0; i < units.size(); ++i) {
+            ub[i] = nblk; uo[i] = o;
+            nblk += units[i].nb; o += units[i].bytes; t1_bytes += units[i].t1;
+        }
+        host_pool().run(units.size(), [&](size_t i) { run_unit(i, ub[i], uo[i], false); });
     } else {
         for (TileFill& tf : tiles_in) {
             fill_tile(tf, nblk, o, false, &tf);
@@ -3992,33 +4027,36 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // decoder takes the padding as the MQ end-of-data bytes)
     // (pos, slot position, length) triples, straight into the pinned upload buffer; a part's
     // chunks are those of its own blocks, so parts fill disjoint ranges
+    // (a chunk lands at its block's slot + the block's bytes before it, recorded by the parse, so
+    // pieces of one part's chunk list fill in parallel; a chunk of a block the table does not
+    // hold becomes an empty triple)
     size_t nseg = 0;
     uint64_t* seg = nullptr;
     {
         std::vector<size_t> sb(ps.size() + 1, 0);
         for (size_t q = 0; q < ps.size(); ++q) sb[q + 1] = sb[q] + (part_idx[q].empty() ? 0 : 3 * ps[q].chunks.size());
         seg = (uint64_t*)ctx->hseg.get(sb.back() * 8 + 8);
-        std::vector<size_t> used(ps.size(), 0);
-        auto segs = [&](size_t q) {
-            if (part_idx[q].empty()) return;
-            size_t w = sb[q];
-            for (const Chunk& ch : ps[q].chunks) {   // stream order = layer order within a block
-                const int32_t k = part_idx[q][ch.b];
-                if (k < 0) continue;
-                GkBlock& G = blk[k];
-                seg[w] = ch.pos; seg[w + 1] = G.data_off + G.len; seg[w + 2] = ch.len;
-                w += 3;
-                G.len += ch.len;
-            }
-            used[q] = w - sb[q];
-        };
-        if (par_fill) host_pool().run(ps.size(), segs);
-        else for (size_t q = 0; q < ps.size(); ++q) segs(q);
-        // compact (a part's unused tail: chunks of blocks the table does not hold)
+        struct Piece { size_t q, b, e; };
+        std::vector<Piece> pieces;
         for (size_t q = 0; q < ps.size(); ++q) {
-            if (nseg != sb[q]) memmove(seg + nseg, seg + sb[q], used[q] * 8);
-            nseg += used[q];
+            if (part_idx[q].empty()) continue;
+            const size_t n = ps[q].chunks.size(), step = std::max<size_t>(4096, n / 32);
+            for (size_t b = 0; b < n; b += step) pieces.push_back({q, b, std::min(n, b + step)});
         }
+        host_pool().run(pieces.size(), [&](size_t i) {
+            const Piece& pc = pieces[i];
+            const std::vector<Chunk>& chs = ps[pc.q].chunks;
+            const std::vector<int32_t>& idx = part_idx[pc.q];
+            for (size_t j = pc.b; j < pc.e; ++j) {
+                const Chunk& ch = chs[j];
+                const int32_t k = idx[ch.b];
+                uint64_t* w = seg + sb[pc.q] + 3 * j;
+                w[0] = ch.pos;
+                w[1] = k < 0 ? 0 : blk[k].data_off + ch.boff;
+                w[2] = k < 0 ? 0 : ch.len;
+            }
+        });
+        nseg = sb.back();
     }
     uint8_t* stg = (uint8_t*)ctx->bytes.get(o + 256);   // decoder window loads read up to 48 B past a block
     if (host_gather) {
