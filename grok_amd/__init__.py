@@ -387,11 +387,18 @@ class Engine:
     def decode_window(self, cs, window, length=None, out=None, sample_bytes=0):
         """gk_decode_window: window = (x0, y0, x1, y1).  Returns a (C, y1-y0, x1-x0) numpy
         array (int32, or 8/16-bit with sample_bytes 1/2), or fills ``out`` (a torch cuda
-        tensor of that shape; its element size selects the sample type) in place."""
+        tensor of that shape; its element size selects the sample type) in place.  With
+        set_decode_reduce(r) the window (full-resolution coordinates) is returned at the
+        reduced resolution: its canvas rectangle with every edge ceil(x / 2^r)."""
         on_dev = _is_torch_cuda(cs)
         info = self.read_header(cs, length)
         x0, y0, x1, y1 = window
         c, h, w = info.numcomps, y1 - y0, x1 - x0
+        red = getattr(self, "_reduce", 0)
+        if red:   # the window's canvas rectangle reduced: ceil(x / 2^reduce) (set_decode_reduce)
+            cd = lambda v: -(-v >> red)
+            w = cd(x1 + info.x0) - cd(x0 + info.x0)
+            h = cd(y1 + info.y0) - cd(y0 + info.y0)
         if out is not None:
             # any (C, h, w) view with unit column stride (e.g. a row band of a larger window)
             assert tuple(out.shape) == (c, h, w) and out.stride(2) == 1

@@ -3633,7 +3633,6 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                     if (B.numbps > 30) throw GkError("more than 30 band bit-planes (ROI shift included) not supported");
     const uint32_t red = ctx->dec_reduce;
     if (red >= P.p.numres) throw GkError("reduce must be less than the number of resolutions");
-    if (red && win) throw GkError("reduced-resolution decode of a window is not supported");
     auto keep_window = [&]() {   // keep only the tile parts of tiles intersecting the window
         if (!win) return;
         if (win[0] >= win[2] || win[1] >= win[3] || win[2] > P.w || win[3] > P.h) throw GkError("bad decode window");
@@ -4285,30 +4284,48 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr, red + 1);
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
-        // reduced canvas: positions ceil(x / 2^red); output index = that less the image origin's
+        // reduced canvas: positions ceil(x / 2^red); output index = that less the image origin's.
+        // A window (image-relative, full resolution) reduces the same way (the composite
+        // component bounds of CodeStreamDecompress.cpp:471-481, rectceildivpow2): the output is
+        // the reduced tile rectangle clipped to it, the caller's planes addressing its origin
         const uint32_t rox = ceildivpow2(P.x0, red), roy = ceildivpow2(P.y0, red);
-        const uint32_t qx0 = ceildivpow2(RG.x0 + P.x0, red) - rox, qy0 = ceildivpow2(RG.y0 + P.y0, red) - roy;
-        const uint32_t qcols = ceildivpow2(RG.x0 + P.x0 + RG.w, red) - rox - qx0;
-        const uint32_t qrows = ceildivpow2(RG.y0 + P.y0 + RG.h, red) - roy - qy0;
+        uint32_t qx0 = ceildivpow2(RG.x0 + P.x0, red) - rox, qy0 = ceildivpow2(RG.y0 + P.y0, red) - roy;
+        uint32_t qx1 = ceildivpow2(RG.x0 + P.x0 + RG.w, red) - rox, qy1 = ceildivpow2(RG.y0 + P.y0 + RG.h, red) - roy;
+        uint32_t wx0 = 0, wy0 = 0;   // the caller's origin in the reduced image
+        if (win) {
+            wx0 = ceildivpow2(win[0] + P.x0, red) - rox; wy0 = ceildivpow2(win[1] + P.y0, red) - roy;
+            qx0 = std::max(qx0, wx0); qy0 = std::max(qy0, wy0);
+            qx1 = std::min(qx1, ceildivpow2(win[2] + P.x0, red) - rox); qy1 = std::min(qy1, ceildivpow2(win[3] + P.y0, red) - roy);
+            if (qx1 <= qx0 || qy1 <= qy0) throw GkError("the window is empty at this reduction");
+        }
+        const uint32_t qcols = qx1 - qx0, qrows = qy1 - qy0;
         std::vector<uint8_t*> qd(P.nc);
         std::vector<uint32_t> qs(P.nc);
         if (!out_on_device) {
             uint8_t* stage = (uint8_t*)ctx->dplanes.get((size_t)qcols * qrows * P.nc * es + 16);
             for (uint32_t c = 0; c < P.nc; ++c) { qd[c] = stage + (size_t)c * qcols * qrows * es; qs[c] = qcols; }
         } else {
-            for (uint32_t c = 0; c < P.nc; ++c) { qd[c] = (uint8_t*)comps[c] + ((size_t)qy0 * strides[c] + qx0) * es; qs[c] = strides[c]; }
+            for (uint32_t c = 0; c < P.nc; ++c) {
+                qd[c] = (uint8_t*)comps[c] + ((size_t)(qy0 - wy0) * strides[c] + (qx0 - wx0)) * es;
+                qs[c] = strides[c];
+            }
         }
         for (uint32_t j = jb; j < je; ++j)
             for (uint32_t i = ib; i < ie; ++i) {
                 const TileG& T = P.tiles[(size_t)j * P.ntx + i];
                 const uint32_t tx0 = ceildivpow2(T.x0, red) - rox, ty0 = ceildivpow2(T.y0, red) - roy;
-                const uint32_t tw = ceildivpow2(T.x1, red) - ceildivpow2(T.x0, red), th = ceildivpow2(T.y1, red) - ceildivpow2(T.y0, red);
+                const uint32_t tx1 = ceildivpow2(T.x1, red) - rox, ty1 = ceildivpow2(T.y1, red) - roy;
+                // the part of the tile's reduced rectangle inside the output
+                const uint32_t ix0 = std::max(tx0, qx0), iy0 = std::max(ty0, qy0);
+                const uint32_t ix1 = std::min(tx1, qx1), iy1 = std::min(ty1, qy1);
+                if (ix1 <= ix0 || iy1 <= iy0) continue;
+                const uint32_t tw = ix1 - ix0, th = iy1 - iy0;
                 auto src = [&](uint32_t c) {
                     return arena + (size_t)c * 2 * RG.plane + ((red & 1) ? RG.plane : 0) +
-                           (size_t)(T.y0 - P.y0 - RG.y0) * RG.stride + (T.x0 - P.x0 - RG.x0);
+                           (size_t)(T.y0 - P.y0 - RG.y0 + (iy0 - ty0)) * RG.stride + (T.x0 - P.x0 - RG.x0 + (ix0 - tx0));
                 };
                 auto srcf = [&](uint32_t c) { return reinterpret_cast<const float*>(src(c)); };
-                auto dst = [&](uint32_t c) { return qd[c] + ((size_t)(ty0 - qy0) * qs[c] + (tx0 - qx0)) * es; };
+                auto dst = [&](uint32_t c) { return qd[c] + ((size_t)(iy0 - qy0) * qs[c] + (ix0 - qx0)) * es; };
                 if (!P.p.irrev) {
                     if (mct3r) gk_launch_rct_inv_dc(st, src(0), src(1), src(2), RG.stride, stype, dst(0), dst(1), dst(2), qs[0],
                                                     tw, th, shift, mn, mx);
@@ -4326,8 +4343,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipEventRecord(ctx->ev[5], st));
         if (!out_on_device)
             for (uint32_t c = 0; c < P.nc; ++c)
-                HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)qy0 * strides[c] + qx0) * es, (size_t)strides[c] * es,
-                                        qd[c], (size_t)qcols * es, (size_t)qcols * es, qrows, hipMemcpyDeviceToHost, st));
+                HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)(qy0 - wy0) * strides[c] + (qx0 - wx0)) * es,
+                                        (size_t)strides[c] * es, qd[c], (size_t)qcols * es, (size_t)qcols * es, qrows,
+                                        hipMemcpyDeviceToHost, st));
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[6], st));
         HIPCHK(hipStreamSynchronize(st));

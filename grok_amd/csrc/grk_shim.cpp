@@ -282,7 +282,7 @@ bool run_decode(CodecObj* C, ImageObj* o, const uint32_t* w) {
     std::vector<uint32_t> strides(o->img.numcomps);
     for (uint16_t i = 0; i < o->img.numcomps; ++i) { planes[i] = o->comps[i].data; strides[i] = o->comps[i].stride; }
     gk_set_decode_layers(e, C->dp.cp_layer);   // 0 = every layer
-    gk_set_decode_reduce(e, C->dp.cp_reduce);   // the engine refuses it with a window
+    gk_set_decode_reduce(e, C->dp.cp_reduce);
     int rc = w ? gk_decode_window(e, C->data.data(), C->data.size(), 0, w[0], w[1], w[2], w[3], planes.data(),
                                   strides.data(), 0, 0)
                : gk_decode(e, C->data.data(), C->data.size(), 0, planes.data(), strides.data(), 0, 0);
@@ -290,20 +290,19 @@ bool run_decode(CodecObj* C, ImageObj* o, const uint32_t* w) {
     return true;
 }
 
-// the composited image without a window: the image area, on the canvas reduced by cp_reduce
-// (GrkImage::subsampleAndReduce: ceil(x / 2^reduce))
-void full_bounds(const CodecObj* C, uint32_t b[4]) {
-    const uint32_t r = C->dp.cp_reduce;
-    auto cd = [r](uint64_t v) { return (uint32_t)((v + (1ull << r) - 1) >> r); };
-    b[0] = cd(C->info.x0); b[1] = cd(C->info.y0);
-    b[2] = cd((uint64_t)C->info.x0 + C->info.w); b[3] = cd((uint64_t)C->info.y0 + C->info.h);
-}
+// The composited image keeps its canvas bounds (the image area, or the window) at full
+// resolution while its components take them reduced by cp_reduce, ceil(x / 2^reduce)
+// (GrkImage::subsampleAndReduce, GrkImage.cpp:74-113; SIZMarker.cpp:292 for the header image,
+// CodeStreamDecompress.cpp:390 after a window)
+static inline uint32_t reduced(uint64_t v, uint32_t r) { return (uint32_t)((v + (1ull << r) - 1) >> r); }
 
 ImageObj* region_image(CodecObj* C, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    const uint32_t r = C->dp.cp_reduce;
     std::vector<grk_image_cmptparm> p(C->info.numcomps);
     for (auto& q : p) {
         q = grk_image_cmptparm{};
-        q.dx = q.dy = 1; q.w = x1 - x0; q.h = y1 - y0; q.x0 = x0; q.y0 = y0;
+        q.dx = q.dy = 1; q.x0 = reduced(x0, r); q.y0 = reduced(y0, r);
+        q.w = reduced(x1, r) - q.x0; q.h = reduced(y1, r) - q.y0;
         q.prec = (uint8_t)C->info.prec; q.sgnd = C->info.sgnd != 0;
     }
     GRK_COLOR_SPACE cs = GRK_CLRSPC_UNKNOWN;
@@ -318,13 +317,16 @@ ImageObj* region_image(CodecObj* C, uint32_t x0, uint32_t y0, uint32_t x1, uint3
 // Re-bound the composited image in place and give it planes: callers keep the pointer that
 // grk_decompress_get_composited_image returned after the header read (grk_decompress.cpp:1191
 // takes it before set_window / decompress), as Grok edits the one composite image in place
-// (CodeStreamDecompress.cpp:335-387, :451-481).
-bool reshape_image(ImageObj* o, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+// (CodeStreamDecompress.cpp:335-387, :451-481).  (x0, y0, x1, y1): canvas bounds at full
+// resolution; the components take them reduced by r.
+bool reshape_image(ImageObj* o, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t r) {
     o->img.x0 = x0; o->img.y0 = y0; o->img.x1 = x1; o->img.y1 = y1;
+    const uint32_t cx0 = reduced(x0, r), cy0 = reduced(y0, r), cw = reduced(x1, r) - cx0, ch = reduced(y1, r) - cy0;
+    if (!cw || !ch) { error("the decompress region is empty at reduction %u", r); return false; }
     for (auto& c : o->comps) {
-        const uint32_t stride = aligned_stride(x1 - x0);
-        if (c.data && (c.w != x1 - x0 || c.h != y1 - y0 || c.stride != stride)) { free(c.data); c.data = nullptr; }
-        c.x0 = x0; c.y0 = y0; c.w = x1 - x0; c.h = y1 - y0; c.stride = stride;
+        const uint32_t stride = aligned_stride(cw);
+        if (c.data && (c.w != cw || c.h != ch || c.stride != stride)) { free(c.data); c.data = nullptr; }
+        c.x0 = cx0; c.y0 = cy0; c.w = cw; c.h = ch; c.stride = stride;
         if (!c.data && c.w && c.h) {
             c.data = (int32_t*)aligned_alloc(64, ((size_t)c.stride * c.h * 4 + 63) / 64 * 64);
             if (!c.data) { error("out of memory for a %ux%u component", c.w, c.h); return false; }
@@ -589,15 +591,8 @@ bool grk_decompress_read_header(grk_codec* codec, grk_header_info* hi) {
             error("reduce %u must be less than the number of resolutions %u", C->dp.cp_reduce, C->coding.numresolution);
             return false;
         }
-        if (C->dp.cp_reduce && C->has_win) {
-            error("reduced-resolution decode of a window is not supported on this path");
-            return false;
-        }
-        {   // the composited image: the image area on the canvas, reduced by cp_reduce (ceil(x / 2^reduce))
-            uint32_t b[4];
-            full_bounds(C, b);
-            C->out = region_image(C, b[0], b[1], b[2], b[3]);
-        }
+        // the composited image: the image area on the canvas (components reduced by cp_reduce)
+        C->out = region_image(C, C->info.x0, C->info.y0, C->info.x0 + C->info.w, C->info.y0 + C->info.h);
         if (!C->out) return false;
     }
     if (hi) {
@@ -637,7 +632,6 @@ bool grk_decompress_set_window(grk_codec* codec, uint32_t x0, uint32_t y0, uint3
     if (x1 > W) { warn("Right position of the decompress window (%u) is outside the image area (Xsiz=%u).", x1 + OX, W + OX); x1 = W; }
     if (y1 > H) { warn("Bottom position of the decompress window (%u) is outside of the image area (Ysiz=%u).", y1 + OY, H + OY); y1 = H; }
     if (x0 >= x1 || y0 >= y1) { error("decompress window (%u,%u,%u,%u) is empty", x0, y0, x1, y1); return false; }
-    if (C->dp.cp_reduce) { error("reduced-resolution decode of a window is not supported on this path"); return false; }
     C->win[0] = x0; C->win[1] = y0; C->win[2] = x1; C->win[3] = y1;
     C->has_win = true;
     return true;
@@ -650,12 +644,12 @@ bool grk_decompress(grk_codec* codec, grk_plugin_tile* tile) {
     if (!C->header_read && !grk_decompress_read_header(codec, nullptr)) return false;
     const uint32_t OX = C->info.x0, OY = C->info.y0;   // composited images are canvas rectangles
     if (C->has_win) {
-        if (!reshape_image(C->out, C->win[0] + OX, C->win[1] + OY, C->win[2] + OX, C->win[3] + OY)) return false;
+        // (the components: the window's canvas rectangle reduced by cp_reduce)
+        if (!reshape_image(C->out, C->win[0] + OX, C->win[1] + OY, C->win[2] + OX, C->win[3] + OY, C->dp.cp_reduce))
+            return false;
         return run_decode(C, C->out, C->win);
     }
-    uint32_t b[4];
-    full_bounds(C, b);
-    if (!reshape_image(C->out, b[0], b[1], b[2], b[3])) return false;
+    if (!reshape_image(C->out, OX, OY, OX + C->info.w, OY + C->info.h, C->dp.cp_reduce)) return false;
     return run_decode(C, C->out, nullptr);
 }
 
@@ -689,7 +683,7 @@ bool grk_decompress_tile(grk_codec* codec, uint16_t tileIndex) {
             w[0] = C->win[0]; w[1] = C->win[1]; w[2] = C->win[2]; w[3] = C->win[3];
         }
     }
-    if (!reshape_image(C->out, w[0] + OX, w[1] + OY, w[2] + OX, w[3] + OY)) return false;
+    if (!reshape_image(C->out, w[0] + OX, w[1] + OY, w[2] + OX, w[3] + OY, 0)) return false;
     C->tile_decoded = true;
     return run_decode(C, C->out, w);
 }

@@ -124,6 +124,27 @@ def test_grk_api_cli_reduce_and_layers(tool, name, red, layers):
     np.testing.assert_array_equal(dec, want)
 
 
+@pytest.mark.parametrize("name,red", [("rgb8_tiles_xl", 1), ("rgb12_97_r", 2)])
+def test_grk_api_cli_reduce_window(tool, name, red):
+    # -r with -d: the window's canvas rectangle on the reduced canvas (ceil(x / 2^r) per edge,
+    # CodeStreamDecompress.cpp:471-481), decoded under the partial-tile rule a window selects
+    fx = next(f for f in FIXTURES if f.name == name)
+    exe, d = tool
+    p = d / (name + "_rw.j2k")
+    p.write_bytes(fx.cs)
+    c, h, w = fx.img.shape
+    x0, y0, x1, y1 = 17, 33, w - 5, h - 3
+    cd = lambda v: -(-v >> red)
+    dec, info = _dec(tool, p, (c, cd(y1) - cd(y0), cd(x1) - cd(x0)), ("-r", red, "-d", "%d,%d,%d,%d" % (x0, y0, x1, y1)))
+    O.set_decode_reduce(red)
+    try:
+        want, _ = O.decode(fx.cs, partial=True)
+    finally:
+        O.set_decode_reduce(0)
+    np.testing.assert_array_equal(dec, want[:, cd(y0):cd(y1), cd(x0):cd(x1)])
+    assert "image %d %d %d %d" % (x0, y0, x1, y1) in info   # (the image keeps its full-resolution bounds)
+
+
 @pytest.mark.parametrize("flags", ["-S -E", "-S -r 20,5", "-q 30,40", "-E -q 28,36,0 -t 128,128 -X"])
 def test_grk_api_sop_eph_quality(tool, flags):
     # grk_compress -S / -E / -q through grk_cparameters (csty, allocationByQuality, layer_distortion)

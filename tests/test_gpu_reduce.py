@@ -81,3 +81,37 @@ def test_reduce_flat_level(eng):
             eng.decode(cs)
     finally:
         eng.set_decode_reduce(0)
+
+
+# reduced-resolution windows (grk_decompress -r n -d x0,y0,x1,y1): the window is given at full
+# resolution and returned on the reduced canvas, every edge ceil(x / 2^n) (the composite
+# component bounds, CodeStreamDecompress.cpp:471-481); the samples are the oracle's reduced
+# decode under the partial-tile rule a window selects (WaveletReverse.cpp:1551-1554), cropped
+WINDOWS = [(0, 0, 37, 41), (13, 7, 101, 66), (33, 29, 34, 30), (5, 50, 170, 150), (64, 0, 128, 64)]
+
+
+@pytest.mark.parametrize("ci", [0, 1, 2, 3, 5])
+def test_reduce_window_vs_oracle(eng, ci):
+    case = CASES[ci]
+    bits = case.get("bits", 8)
+    img = _img(ci, case["c"], case["h"], case["w"], bits)
+    cs = eng.encode(img, bits, params=_gk(case["kw"]))
+    cd = lambda v, r: -(-v >> r)
+    try:
+        for red in range(1, case["kw"]["numres"]):
+            eng.set_decode_reduce(red)
+            O.set_decode_reduce(red)
+            ref = O.decode(cs, partial=True)[0]
+            for (x0, y0, x1, y1) in WINDOWS:
+                x1, y1 = min(x1, case["w"]), min(y1, case["h"])
+                if x0 >= x1 or y0 >= y1:
+                    continue
+                qx0, qy0, qx1, qy1 = cd(x0, red), cd(y0, red), cd(x1, red), cd(y1, red)
+                if qx0 >= qx1 or qy0 >= qy1:
+                    continue   # (nothing left at this reduction)
+                dec = eng.decode_window(cs, (x0, y0, x1, y1))
+                assert dec.shape == (case["c"], qy1 - qy0, qx1 - qx0)
+                np.testing.assert_array_equal(dec, ref[:, qy0:qy1, qx0:qx1], err_msg=f"red {red} window {(x0, y0, x1, y1)}")
+    finally:
+        eng.set_decode_reduce(0)
+        O.set_decode_reduce(0)
