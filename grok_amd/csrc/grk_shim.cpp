@@ -660,7 +660,6 @@ bool grk_decompress_tile(grk_codec* codec, uint16_t tileIndex) {
     CodecObj* C = codec_of(codec);
     if (!C || C->compress) return false;
     if (!C->header_read && !grk_decompress_read_header(codec, nullptr)) return false;
-    if (C->dp.cp_reduce) { error("reduced-resolution decode of a tile is not supported on this path"); return false; }
     const uint32_t tw = C->coding.t_width, th = C->coding.t_height;
     const uint32_t OX = C->info.x0, OY = C->info.y0, X1 = OX + C->info.w, Y1 = OY + C->info.h;
     const uint32_t gx = C->coding.tx0, gy = C->coding.ty0;
@@ -683,7 +682,8 @@ bool grk_decompress_tile(grk_codec* codec, uint16_t tileIndex) {
             w[0] = C->win[0]; w[1] = C->win[1]; w[2] = C->win[2]; w[3] = C->win[3];
         }
     }
-    if (!reshape_image(C->out, w[0] + OX, w[1] + OY, w[2] + OX, w[3] + OY, 0)) return false;
+    // (with cp_reduce the components take the tile's rectangle reduced, CodeStreamDecompress.cpp:471-481)
+    if (!reshape_image(C->out, w[0] + OX, w[1] + OY, w[2] + OX, w[3] + OY, C->dp.cp_reduce)) return false;
     C->tile_decoded = true;
     return run_decode(C, C->out, w);
 }

@@ -143,6 +143,11 @@ def test_grk_api_cli_reduce_window(tool, name, red):
         O.set_decode_reduce(0)
     np.testing.assert_array_equal(dec, want[:, cd(y0):cd(y1), cd(x0):cd(x1)])
     assert "image %d %d %d %d" % (x0, y0, x1, y1) in info   # (the image keeps its full-resolution bounds)
+    if fx.tiled:   # -r with -tile: the tile's rectangle reduced the same way
+        tw, th = fx.kw["tiles"]
+        tx0, ty0, tx1, ty1 = tw, 0, min(2 * tw, w), min(th, h)
+        dec, _ = _dec(tool, p, (c, cd(ty1) - cd(ty0), cd(tx1) - cd(tx0)), ("-r", red, "-tile", 1))
+        np.testing.assert_array_equal(dec, want[:, cd(ty0):cd(ty1), cd(tx0):cd(tx1)])
 
 
 @pytest.mark.parametrize("flags", ["-S -E", "-S -r 20,5", "-q 30,40", "-E -q 28,36,0 -t 128,128 -X"])
