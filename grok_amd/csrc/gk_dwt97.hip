@@ -226,21 +226,64 @@ __device__ __forceinline__ void fwd97_store(const Lds97& T, float* __restrict__ 
     }
 }
 
+// One level, cpw components per workgroup; full-width tiles prefetch the next component's input
+// into registers while the current one lifts (as k_dwt53_fwd_level)
 __global__ __launch_bounds__(256) void k_dwt97_fwd_level(const float* __restrict__ src, uint32_t sstride,
                                                          float* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h, GkTiles tb, GkComps cs) {
+                                                         uint32_t h, GkTiles tb, GkComps cs, uint32_t cpw) {
     __shared__ Lds97 T;
     const uint3 bi = xcd_tile();
-    const uint32_t tile = bi.z % tb.count(), comp = bi.z / tb.count();
-    src += tb.offset(tile, sstride) + comp * cs.cstride;
-    dst += tb.offset(tile, dstride) + comp * cs.cstride;
+    const uint32_t tile = bi.z % tb.count(), c0 = bi.z / tb.count() * cpw, c1 = min(cs.n, c0 + cpw);
+    src += tb.offset(tile, sstride);
+    dst += tb.offset(tile, dstride);
     const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
-    auto ld = [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; };
-    if (fullw97(x0, (int)w)) fwd97_fill_inner(x0, y0, (int)w, (int)h, tid, ld);
-    else fwd97_fill(x0, y0, (int)w, (int)h, tid, ld);
-    __syncthreads();
-    fwd97_lift(T, (int)w, (int)h, tid);
-    fwd97_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
+    const int tx = tid & 63, ty = tid >> 6;
+    constexpr int PF_ROWS = (T97_LH + 3) / 4, PF_HALO = (8 * T97_LH + 255) / 256;
+    float PF[2 * PF_ROWS + PF_HALO];
+    const bool inner = fullw97(x0, (int)w);
+    auto hlx = [](int i) { const int j = i & 7; return j < 4 ? j : 128 + j; };
+    auto fetch = [&](const float* sc) {   // (fwd97_fill_inner's positions)
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < T97_LH) {
+                const float* r = sc + (size_t)mirror97(y0 - T97_HALO + ly, (int)h) * sstride + x0 + tx;
+                PF[2 * m] = r[0];
+                PF[2 * m + 1] = r[64];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PF_HALO; ++k) {
+            const int i = tid + 256 * k;
+            if (i < 8 * T97_LH)
+                PF[2 * PF_ROWS + k] = sc[(size_t)mirror97(y0 - T97_HALO + (i >> 3), (int)h) * sstride +
+                                         mirror97(x0 - T97_HALO + hlx(i), (int)w)];
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < T97_LH) { T[ly][4 + tx] = PF[2 * m]; T[ly][68 + tx] = PF[2 * m + 1]; }
+        }
+#pragma unroll
+        for (int k = 0; k < PF_HALO; ++k) {
+            const int i = tid + 256 * k;
+            if (i < 8 * T97_LH) T[i >> 3][hlx(i)] = PF[2 * PF_ROWS + k];
+        }
+    };
+    if (inner) fetch(src + c0 * cs.cstride);
+    for (uint32_t c = c0; c < c1; ++c) {
+        if (c != c0) __syncthreads();   // the previous component's stores have read the tile
+        const float* sc = src + c * cs.cstride;
+        if (inner) put();
+        else fwd97_fill(x0, y0, (int)w, (int)h, tid,
+                        [&](int ly, int lx, int gy, int gx) { T[ly][lx] = sc[(size_t)gy * sstride + gx]; });
+        __syncthreads();
+        if (inner && c + 1 < c1) fetch(sc + cs.cstride);
+        fwd97_lift(T, (int)w, (int)h, tid);
+        fwd97_store(T, dst + c * cs.cstride, dstride, x0, y0, (int)w, (int)h, tid);
+    }
 }
 
 // Level 1 from the caller's planes: DC shift and, for NC = 3, the ICT (mct.cpp:147-219) on load.
@@ -432,26 +475,80 @@ __device__ __forceinline__ void inv97_lift(Lds97& T, int w, int h, int tid) {
     }
 }
 
+// One level, cpw components per workgroup with the next one's input prefetched (as
+// k_dwt97_fwd_level; the positions and scalings of inv97_fill's full-width path)
 __global__ __launch_bounds__(256) void k_dwt97_inv_level(const float* __restrict__ src, uint32_t sstride,
                                                          float* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h, GkTiles tb, GkComps cs) {
+                                                         uint32_t h, GkTiles tb, GkComps cs, uint32_t cpw) {
     __shared__ Lds97 T;
     const uint3 bi = xcd_tile();
-    const uint32_t tile = bi.z % tb.count(), comp = bi.z / tb.count();
-    src += tb.offset(tile, sstride) + comp * cs.cstride;
-    dst += tb.offset(tile, dstride) + comp * cs.cstride;
+    const uint32_t tile = bi.z % tb.count(), c0 = bi.z / tb.count() * cpw, c1 = min(cs.n, c0 + cpw);
+    src += tb.offset(tile, sstride);
+    dst += tb.offset(tile, dstride);
     const int x0 = bi.x * T97_W, y0 = bi.y * T97_H, tid = threadIdx.x;
-    const int tx = tid & 63, ty = tid >> 6;
-    inv97_fill(x0, y0, (int)w, (int)h, tid,
-               [&](int ly, int lx, int sy, int sx, float f) { T[ly][lx] = src[(size_t)sy * sstride + sx] * f; });
-    __syncthreads();
-    inv97_lift(T, (int)w, (int)h, tid);
-    for (int ry = ty; ry < T97_H; ry += 4) {
-        const int gy = y0 + ry;
-        if (gy >= (int)h) break;
-        float* drow = dst + (size_t)gy * dstride + x0;
-        if (x0 + tx < (int)w) drow[tx] = T[ry + T97_HALO][T97_HALO + tx];
-        if (x0 + 64 + tx < (int)w) drow[64 + tx] = T[ry + T97_HALO][T97_HALO + 64 + tx];
+    const int tx = tid & 63, ty = tid >> 6, hx = x0 >> 1;
+    constexpr int PF_ROWS = (T97_LH + 3) / 4, PF_HALO = (8 * T97_LH + 255) / 256;
+    float PF[2 * PF_ROWS + PF_HALO];
+    const bool inner = fullw97(x0, (int)w);
+    const int snw = ((int)w + 1) >> 1, snh = ((int)h + 1) >> 1;
+    const float fe = w > 1 ? F97_K : 1.0f, fo = w > 1 ? I97_TWO_INVK : 1.0f;
+    auto srow = [&](int ly) {
+        const int gy = mirror97(y0 - T97_HALO + ly, (int)h);
+        return (size_t)((gy & 1) ? (snh + (gy >> 1)) : (gy >> 1)) * sstride;
+    };
+    auto hlx = [](int i) { const int j = i & 7; return j < 4 ? j : 128 + j; };
+    auto fetch = [&](const float* sc) {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < T97_LH) {
+                const float* r = sc + srow(ly) + hx + tx;
+                PF[2 * m] = r[0];
+                PF[2 * m + 1] = r[snw];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PF_HALO; ++k) {
+            const int i = tid + 256 * k;
+            if (i < 8 * T97_LH) {
+                const int gx = mirror97(x0 - T97_HALO + hlx(i), (int)w);
+                PF[2 * PF_ROWS + k] = sc[srow(i >> 3) + ((gx & 1) ? snw + (gx >> 1) : (gx >> 1))];
+            }
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < T97_LH) {
+                T[ly][T97_HALO + 2 * tx] = PF[2 * m] * fe;
+                T[ly][T97_HALO + 1 + 2 * tx] = PF[2 * m + 1] * fo;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PF_HALO; ++k) {
+            const int i = tid + 256 * k;
+            if (i < 8 * T97_LH) T[i >> 3][hlx(i)] = PF[2 * PF_ROWS + k] * ((hlx(i) & 1) ? fo : fe);
+        }
+    };
+    if (inner) fetch(src + c0 * cs.cstride);
+    for (uint32_t c = c0; c < c1; ++c) {
+        if (c != c0) __syncthreads();   // the previous component's stores have read the tile
+        const float* sc = src + c * cs.cstride;
+        if (inner) put();
+        else inv97_fill(x0, y0, (int)w, (int)h, tid,
+                        [&](int ly, int lx, int sy, int sx, float f) { T[ly][lx] = sc[(size_t)sy * sstride + sx] * f; });
+        __syncthreads();
+        if (inner && c + 1 < c1) fetch(sc + cs.cstride);
+        inv97_lift(T, (int)w, (int)h, tid);
+        float* dc = dst + c * cs.cstride;
+        for (int ry = ty; ry < T97_H; ry += 4) {
+            const int gy = y0 + ry;
+            if (gy >= (int)h) break;
+            float* drow = dc + (size_t)gy * dstride + x0;
+            if (x0 + tx < (int)w) drow[tx] = T[ry + T97_HALO][T97_HALO + tx];
+            if (x0 + 64 + tx < (int)w) drow[64 + tx] = T[ry + T97_HALO][T97_HALO + 64 + tx];
+        }
     }
 }
 
@@ -614,23 +711,27 @@ static uint32_t comps_in_grid97(GkTiles tb, GkComps cs) { return tb.count() * cs
 void gk_launch_dwt97_fwd(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb, GkComps cs) {
     if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
-    const uint32_t ng = comps_in_grid97(tb, cs);
+    const uint32_t gx = (w + T97_W - 1) / T97_W, gy = (h + T97_H - 1) / T97_H;
+    const uint32_t cpw = gk_dwt_cpw(gx * gy * tb.count(), cs.n, true);   // (gk_kernels.hip)
+    const uint32_t ng = cpw > 1 ? cs.n : comps_in_grid97(tb, cs);
     for (uint32_t c = 0; c < cs.n; c += ng) {
         GkComps g = cs; g.n = ng;
-        dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count() * ng);
+        dim3 grid(gx, gy, tb.count() * (ng / cpw));
         hipLaunchKernelGGL(k_dwt97_fwd_level, grid, dim3(256), 0, st, src + c * cs.cstride, sstride, dst + c * cs.cstride,
-                           dstride, w, h, tb, g);
+                           dstride, w, h, tb, g, cpw);
     }
 }
 void gk_launch_dwt97_inv(hipStream_t st, const float* src, uint32_t sstride, float* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb, GkComps cs) {
     if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
-    const uint32_t ng = comps_in_grid97(tb, cs);
+    const uint32_t gx = (w + T97_W - 1) / T97_W, gy = (h + T97_H - 1) / T97_H;
+    const uint32_t cpw = gk_dwt_cpw(gx * gy * tb.count(), cs.n, false);   // (gk_kernels.hip)
+    const uint32_t ng = cpw > 1 ? cs.n : comps_in_grid97(tb, cs);
     for (uint32_t c = 0; c < cs.n; c += ng) {
         GkComps g = cs; g.n = ng;
-        dim3 grid((w + T97_W - 1) / T97_W, (h + T97_H - 1) / T97_H, tb.count() * ng);
+        dim3 grid(gx, gy, tb.count() * (ng / cpw));
         hipLaunchKernelGGL(k_dwt97_inv_level, grid, dim3(256), 0, st, src + c * cs.cstride, sstride, dst + c * cs.cstride,
-                           dstride, w, h, tb, g);
+                           dstride, w, h, tb, g, cpw);
     }
 }
 void gk_launch_dwt97_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32_t sin, float* dst, uint64_t cstride,

@@ -237,20 +237,58 @@ __device__ __forceinline__ void fwd53_store(const Lds53& T, int32_t* __restrict_
     }
 }
 
+// One level, cpw components per workgroup (grid z: tile + count * component group).  With
+// several, full-width tiles load the next component's input into registers (the positions
+// fwd53_fill's full-width path visits) while the current one lifts, as k_dwt53_inv_l1 does;
+// the launcher takes one component per workgroup when the grid would not fill the chip.
 __global__ __launch_bounds__(256) void k_dwt53_fwd_level(const int32_t* __restrict__ src, uint32_t sstride,
                                                          int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h, GkTiles tb, GkComps cs) {
+                                                         uint32_t h, GkTiles tb, GkComps cs, uint32_t cpw) {
     __shared__ Lds53 T;
     const uint3 bi = xcd_tile();
-    const uint32_t tile = bi.z % tb.count(), comp = bi.z / tb.count();
-    src += tb.offset(tile, sstride) + comp * cs.cstride;
-    dst += tb.offset(tile, dstride) + comp * cs.cstride;
+    const uint32_t tile = bi.z % tb.count(), c0 = bi.z / tb.count() * cpw, c1 = min(cs.n, c0 + cpw);
+    src += tb.offset(tile, sstride);
+    dst += tb.offset(tile, dstride);
     const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
-    fwd53_fill(x0, y0, (int)w, (int)h, tid,
-               [&](int ly, int lx, int gy, int gx) { T[ly][lx] = src[(size_t)gy * sstride + gx]; });
-    LDS_BARRIER();
-    fwd53_lift(T, (int)w, (int)h, tid);
-    fwd53_store(T, dst, dstride, x0, y0, (int)w, (int)h, tid);
+    const int tx = tid & 63, ty = tid >> 6;
+    constexpr int PF_ROWS = (DWT_LH + 3) / 4;
+    int32_t PF[2 * PF_ROWS + 1];
+    const bool inner = fullw53(x0, (int)w);
+    auto fetch = [&](const int32_t* sc) {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < DWT_LH) {
+                const int32_t* r = sc + (size_t)mirror(y0 - 2 + ly, (int)h) * sstride + x0 + tx;
+                PF[2 * m] = r[0];
+                PF[2 * m + 1] = r[64];
+            }
+        }
+        if (tid < 3 * DWT_LH) {   // halo columns x0-2, x0-1, x0+TW (as fwd53_fill)
+            const int ly = tid / 3, lx = fwd53_halo_lx(tid % 3);
+            PF[2 * PF_ROWS] = sc[(size_t)mirror(y0 - 2 + ly, (int)h) * sstride + mirror(x0 - 2 + lx, (int)w)];
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < DWT_LH) { T[ly][tx + 2] = PF[2 * m]; T[ly][tx + 66] = PF[2 * m + 1]; }
+        }
+        if (tid < 3 * DWT_LH) T[tid / 3][fwd53_halo_lx(tid % 3)] = PF[2 * PF_ROWS];
+    };
+    if (inner) fetch(src + c0 * cs.cstride);
+    for (uint32_t c = c0; c < c1; ++c) {
+        if (c != c0) LDS_BARRIER();   // the previous component's stores have read the tile
+        const int32_t* sc = src + c * cs.cstride;
+        if (inner) put();
+        else fwd53_fill(x0, y0, (int)w, (int)h, tid,
+                        [&](int ly, int lx, int gy, int gx) { T[ly][lx] = sc[(size_t)gy * sstride + gx]; });
+        LDS_BARRIER();
+        if (inner && c + 1 < c1) fetch(sc + cs.cstride);
+        fwd53_lift(T, (int)w, (int)h, tid);
+        fwd53_store(T, dst + c * cs.cstride, dstride, x0, y0, (int)w, (int)h, tid);
+    }
 }
 
 // Level 1 from the caller's planes: DC shift (TileProcessor.cpp:506-535) and, for NC = 3,
@@ -428,27 +466,69 @@ __device__ __forceinline__ void inv53_lift(Lds53& T, int w, int h, int tid) {
     }
 }
 
+// One level, cpw components per workgroup with the next one's input prefetched (as
+// k_dwt53_fwd_level)
 __global__ __launch_bounds__(256) void k_dwt53_inv_level(const int32_t* __restrict__ src, uint32_t sstride,
                                                          int32_t* __restrict__ dst, uint32_t dstride, uint32_t w,
-                                                         uint32_t h, GkTiles tb, GkComps cs) {
+                                                         uint32_t h, GkTiles tb, GkComps cs, uint32_t cpw) {
     __shared__ Lds53 T;
     const uint3 bi = xcd_tile();
-    const uint32_t tile = bi.z % tb.count(), comp = bi.z / tb.count();
-    src += tb.offset(tile, sstride) + comp * cs.cstride;
-    dst += tb.offset(tile, dstride) + comp * cs.cstride;
+    const uint32_t tile = bi.z % tb.count(), c0 = bi.z / tb.count() * cpw, c1 = min(cs.n, c0 + cpw);
+    src += tb.offset(tile, sstride);
+    dst += tb.offset(tile, dstride);
     const int x0 = bi.x * DWT_TW, y0 = bi.y * DWT_TH, tid = threadIdx.x;
     const int tx = tid & 63, ty = tid >> 6;
-    inv53_fill(x0, y0, (int)w, (int)h, tid,
-               [&](int ly, int lx, int sy, int sx) { T[ly][lx] = src[(size_t)sy * sstride + sx]; });
-    LDS_BARRIER();
-    inv53_lift(T, (int)w, (int)h, tid);
+    constexpr int PF_ROWS = (IDWT_LH + 3) / 4;
+    int32_t PF[2 * PF_ROWS + 1];
+    const bool inner = fullw53(x0, (int)w);
+    const int snw = ((int)w + 1) >> 1, snh = ((int)h + 1) >> 1;
+    auto srow = [&](int ly) {
+        const int gy = mirror(y0 - 1 + ly, (int)h);
+        return (size_t)((gy & 1) ? (snh + (gy >> 1)) : (gy >> 1)) * sstride;
+    };
+    auto fetch = [&](const int32_t* sc) {   // (inv53_fill's full-width positions)
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < IDWT_LH) {
+                const int32_t* r = sc + srow(ly) + (x0 >> 1) + tx;
+                PF[2 * m] = r[0];
+                PF[2 * m + 1] = r[snw];
+            }
+        }
+        if (tid < 3 * IDWT_LH) {
+            const int ly = tid / 3, j = tid % 3, lx = j ? 128 + j : 0;
+            const int gx = mirror(x0 - 1 + lx, (int)w);
+            PF[2 * PF_ROWS] = sc[srow(ly) + ((gx & 1) ? (snw + (gx >> 1)) : (gx >> 1))];
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int m = 0; m < PF_ROWS; ++m) {
+            const int ly = ty + 4 * m;
+            if (ly < IDWT_LH) { T[ly][1 + 2 * tx] = PF[2 * m]; T[ly][2 + 2 * tx] = PF[2 * m + 1]; }
+        }
+        if (tid < 3 * IDWT_LH) { const int j = tid % 3; T[tid / 3][j ? 128 + j : 0] = PF[2 * PF_ROWS]; }
+    };
     const bool full = x0 + DWT_TW <= (int)w && y0 + DWT_TH <= (int)h;
-    for (int ry = ty; ry < DWT_TH; ry += 4) {
-        const int gy = y0 + ry;
-        if (!full && gy >= (int)h) break;
-        int32_t* drow = dst + (size_t)gy * dstride + x0;
-        for (int c = tx; c < DWT_TW; c += 64)
-            if (full || x0 + c < (int)w) drow[c] = T[ry + 1][c + 1];
+    if (inner) fetch(src + c0 * cs.cstride);
+    for (uint32_t c = c0; c < c1; ++c) {
+        if (c != c0) LDS_BARRIER();   // the previous component's stores have read the tile
+        const int32_t* sc = src + c * cs.cstride;
+        if (inner) put();
+        else inv53_fill(x0, y0, (int)w, (int)h, tid,
+                        [&](int ly, int lx, int sy, int sx) { T[ly][lx] = sc[(size_t)sy * sstride + sx]; });
+        LDS_BARRIER();
+        if (inner && c + 1 < c1) fetch(sc + cs.cstride);
+        inv53_lift(T, (int)w, (int)h, tid);
+        int32_t* dc = dst + c * cs.cstride;
+        for (int ry = ty; ry < DWT_TH; ry += 4) {
+            const int gy = y0 + ry;
+            if (!full && gy >= (int)h) break;
+            int32_t* drow = dc + (size_t)gy * dstride + x0;
+            for (int cc = tx; cc < DWT_TW; cc += 64)
+                if (full || x0 + cc < (int)w) drow[cc] = T[ry + 1][cc + 1];
+        }
     }
 }
 
@@ -647,26 +727,41 @@ void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int stype
         hipLaunchKernelGGL(k_dc_inv<T>, grid, dim3(256), 0, st, in, sin, (T*)out, sout, w, h, shift, mn, mx))
 }
 static uint32_t comps_in_grid(GkTiles tb, GkComps cs) { return tb.count() * cs.n <= 65535u ? cs.n : 1u; }
+// components per workgroup of a level launch.  One, unless `multi` (the kernel measured faster
+// with the next component prefetched) and the grid still gives every CU 8 workgroups of all the
+// components: C2 (5/3) levels 2-5 one per workgroup 125 / 139 µs forward / inverse per step,
+// all three 146 / 163 (the register-staged fill alone is the gain over the per-position fill,
+// 164 / 193); C3 (9/7) forward 210 / 222 µs with all / one.  GK_DWT_CPW=1 / 3 forces one / all.
+uint32_t gk_dwt_cpw(uint32_t wgs, uint32_t n, bool multi) {
+    static const int force = getenv("GK_DWT_CPW") ? atoi(getenv("GK_DWT_CPW")) : 0;
+    if (force == 1) multi = false;
+    if (force > 1) multi = true;
+    return (multi && n > 1 && wgs >= 8u * 256u) ? n : 1u;
+}
 void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb, GkComps cs) {
     if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
-    const uint32_t ng = comps_in_grid(tb, cs);   // components per launch
+    const uint32_t gx = (w + DWT_TW - 1) / DWT_TW, gy = (h + DWT_TH - 1) / DWT_TH;
+    const uint32_t cpw = gk_dwt_cpw(gx * gy * tb.count(), cs.n, false);
+    const uint32_t ng = cpw > 1 ? cs.n : comps_in_grid(tb, cs);   // components per launch
     for (uint32_t c = 0; c < cs.n; c += ng) {
         GkComps g = cs; g.n = ng;
-        dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count() * ng);
+        dim3 grid(gx, gy, tb.count() * (ng / cpw));
         hipLaunchKernelGGL(k_dwt53_fwd_level, grid, dim3(256), 0, st, src + c * cs.cstride, sstride, dst + c * cs.cstride,
-                           dstride, w, h, tb, g);
+                           dstride, w, h, tb, g, cpw);
     }
 }
 void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride, uint32_t w,
                          uint32_t h, GkTiles tb, GkComps cs) {
     if (!w || !h || !tb.count()) return;   // an empty region (a resolution of zero width or height): no launch
-    const uint32_t ng = comps_in_grid(tb, cs);
+    const uint32_t gx = (w + DWT_TW - 1) / DWT_TW, gy = (h + DWT_TH - 1) / DWT_TH;
+    const uint32_t cpw = gk_dwt_cpw(gx * gy * tb.count(), cs.n, false);
+    const uint32_t ng = cpw > 1 ? cs.n : comps_in_grid(tb, cs);
     for (uint32_t c = 0; c < cs.n; c += ng) {
         GkComps g = cs; g.n = ng;
-        dim3 grid((w + DWT_TW - 1) / DWT_TW, (h + DWT_TH - 1) / DWT_TH, tb.count() * ng);
+        dim3 grid(gx, gy, tb.count() * (ng / cpw));
         hipLaunchKernelGGL(k_dwt53_inv_level, grid, dim3(256), 0, st, src + c * cs.cstride, sstride, dst + c * cs.cstride,
-                           dstride, w, h, tb, g);
+                           dstride, w, h, tb, g, cpw);
     }
 }
 void gk_launch_dwt53_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32_t sin, int32_t* dst, uint64_t cstride,

@@ -25,6 +25,8 @@ void gk_launch_rct_inv_dc(hipStream_t st, const int32_t* y, const int32_t* u, co
 void gk_launch_dc_inv(hipStream_t st, const int32_t* in, uint32_t sin, int stype, void* out, uint32_t sout, uint32_t w,
                       uint32_t h, int32_t shift, int32_t mn, int32_t mx);
 // one DWT level of cs.n components (planes cs.cstride apart), every tile of tb
+// components per workgroup of a DWT level launch (gk_kernels.hip)
+uint32_t gk_dwt_cpw(uint32_t wgs, uint32_t n, bool multi);
 void gk_launch_dwt53_fwd(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
                          uint32_t w, uint32_t h, GkTiles tb = GkTiles(), GkComps cs = GkComps());
 void gk_launch_dwt53_inv(hipStream_t st, const int32_t* src, uint32_t sstride, int32_t* dst, uint32_t dstride,
