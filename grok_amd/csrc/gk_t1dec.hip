@@ -1095,11 +1095,14 @@ __global__ __launch_bounds__(64) void k_t1_recon(const GkBlock* __restrict__ blo
     __syncthreads();
     if (x >= (int)B.w) return;
     const int np = min((int)numbps - bpl, (int)npmax);
+    // the lane's half of each 64-bit row: one 32-bit LDS read and a bit-field extract per plane
+    const uint32_t* Lh = reinterpret_cast<const uint32_t*>(Lr) + (x >> 5);
+    const uint32_t xb = x & 31;
     for (uint32_t y = 0; y < h; ++y) {
         int32_t v = 0;
         if (any) {
             uint32_t M = 0;
-            for (int i = 0; i < np; ++i) M |= (uint32_t)((Lr[i * 64 + y] >> x) & 1) << ((int)numbps - 1 - i);
+            for (int i = 0; i < np; ++i) M |= __builtin_amdgcn_ubfe(Lh[2 * (i * 64 + y)], xb, 1) << ((int)numbps - 1 - i);
             if (M) {
                 int qq = (t == 0 && (M >> (bpl + 1)) != 0) ? bpl + 1 : bpl;
                 int32_t mag = (int32_t)(((M >> qq) << 1 | 1) << qq);
