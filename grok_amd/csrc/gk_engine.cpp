@@ -86,11 +86,14 @@ static int engines_on(int dev) {
 //    notify_all and a wait for every worker, ~5 us now.
 class HostPool {
     std::vector<std::thread> th_;
+    // (the claim word and the finished count on lines of their own: every item touches both,
+    // from every thread)
     std::atomic<const std::function<void(size_t)>*> job_{nullptr};   // written before the claim word
     std::atomic<uint32_t> gen_{0};           // futex word: a new job
-    std::atomic<uint64_t> claim_{0};         // generation (16 bits) | items (24) | next item (24)
-    std::atomic<size_t> done_{0};            // items of the current generation finished
     std::atomic<uint32_t> fin_{0};           // futex word: the caller sleeps until done_ == items
+    alignas(128) std::atomic<uint64_t> claim_{0};   // generation (16 bits) | items (24) | next item (24)
+    alignas(128) std::atomic<size_t> done_{0};      // items of the current generation finished
+    char pad_[128 - sizeof(std::atomic<size_t>)];
     std::atomic<bool> stop_{false}, has_err_{false};
     std::mutex err_m_;
     std::string err_;
@@ -118,8 +121,12 @@ class HostPool {
         if (err_.empty()) err_ = e;
         has_err_ = true;
     }
+    // A thread counts the items it ran and adds them to done_ once it finds nothing left to
+    // claim (the job stays alive until done_ reaches the item count, so the count is added
+    // before this thread lets go of it).
     void work(uint32_t g) {
-        for (size_t i, n; claim(g, i, n);) {
+        size_t ran = 0, n = 0;
+        for (size_t i; claim(g, i, n);) {
             // (the claim synchronises with the caller's publication, and this item keeps the job alive)
             const std::function<void(size_t)>& f = *job_.load(std::memory_order_relaxed);
             try { f(i); } catch (const GkError& e) {
@@ -129,10 +136,11 @@ class HostPool {
             } catch (...) {
                 fail("host worker: unknown exception");
             }
-            if (done_.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {   // the last item
-                fin_.fetch_add(1, std::memory_order_release);
-                fwake(fin_);
-            }
+            ++ran;
+        }
+        if (ran && done_.fetch_add(ran, std::memory_order_acq_rel) + ran == n) {   // the last items
+            fin_.fetch_add(1, std::memory_order_release);
+            fwake(fin_);
         }
     }
     void worker() {
@@ -1627,10 +1635,9 @@ struct T2Enc {
         if (chunks.empty())
             for (uint32_t u = 0; u < (uint32_t)units.size(); ++u) {
                 const uint32_t fb = unit_prec(units[u]).first_block;
-                for (uint32_t k = 0; k < units[u].nblk; k += kChunk)
-                    chunks.push_back({u, fb + k, fb + std::min(units[u].nblk, k + kChunk), {}, {}, 0, HUGE_VAL, -HUGE_VAL});
+                for (uint32_t k = 0; k < units[u].nblk; k += chunk_blocks())
+                    chunks.push_back({u, fb + k, fb + std::min(units[u].nblk, k + chunk_blocks()), {}, {}, 0, HUGE_VAL, -HUGE_VAL});
             }
-        if (ulock.size() != units.size()) ulock = std::vector<std::mutex>(units.size());
         nact = 0;
         for (ChunkI& C : chunks) {
             C.mslo = HUGE_VAL; C.mshi = -HUGE_VAL;
@@ -1710,34 +1717,39 @@ struct T2Enc {
     // non-zero adds its zero-bit-plane bits (V[n] - V[parent] + 1) and one bit for each
     // child with no block in packets (decide()'s two tree terms), and the walk stops at the
     // first ancestor already counting one.  A step is one parallel pass over chunks of a
-    // unit's blocks (recount in parallel; changes applied under the unit's lock, since units
-    // own disjoint trees and sums).
+    // unit's blocks (recount in parallel; the changes applied by each chunk, the tree counts and
+    // the unit's sums updated atomically).
     // act: blocks whose count may still change; log: this step's changes (block, old count)
     // mslo / mshi: the largest slo and smallest shi over the chunk's active blocks as the last
     // step that ran it left them (+inf / -inf when some block has no valid interval): a
     // threshold that passes the reuse test against both passes it for every active block
     // (t - s and the comparisons are monotone in s), so the chunk keeps its counts unread
     // (the early steps of a layer, thresholds far above every block's slopes)
-    struct ChunkI { uint32_t u, s, e; std::vector<uint32_t> act, log; uint64_t hd; double mslo, mshi; };
-    static constexpr uint32_t kChunk = 512;
+    struct alignas(128) ChunkI { uint32_t u, s, e; std::vector<uint32_t> act, log; uint64_t hd; double mslo, mshi; };   // (a line pair each: chunks of one step are written by different threads)
+    static uint32_t chunk_blocks() {   // GK_PCRD_CHUNK (tuning)
+        static const uint32_t v = getenv("GK_PCRD_CHUNK") ? (uint32_t)atoi(getenv("GK_PCRD_CHUNK")) : 512u;
+        return v ? v : 512u;
+    }
     std::vector<ChunkI> chunks;
-    std::vector<std::mutex> ulock;               // per unit
     size_t nact = 0;                             // active blocks over all chunks
     std::vector<std::vector<uint32_t>> tN, tC;   // per tree node: included new blocks below; children with A == 0
     std::vector<uint64_t> ibits, ibody;          // per unit: header bits (tag trees + blocks), body bytes
     std::vector<uint8_t> udirty;                 // per unit: counts changed since it was last coded
     uint64_t lay_hash = 0, prof_act = 0, prof_npar = 0;
     double prof_par_ms = 0, prof_ser_ms = 0;
+    // (N[n] is updated atomically: chunks of one unit apply their changes concurrently; a
+    // node's count and the bits of its 0 <-> non-zero transitions add up to the same totals in
+    // any order)
     void tree_toggle(uint32_t tree, uint32_t k, bool enter, uint64_t& bits) {
         const std::vector<int32_t>& par = incl[tree].parent;
         const std::vector<uint8_t>& A = tA[tree];
         const std::vector<uint32_t>& V = tV[tree];
         const std::vector<uint32_t>& C = tC[tree];
-        std::vector<uint32_t>& N = tN[tree];
+        uint32_t* N = tN[tree].data();
         for (int32_t n = (int32_t)k; n >= 0 && !A[n]; n = par[n]) {
             const uint64_t w = (uint64_t)(V[n] - (par[n] < 0 ? 0u : V[par[n]]) + 1) + C[n];
-            if (enter) { if (N[n]++) break; bits += w; }
-            else { if (--N[n]) break; bits -= w; }
+            if (enter) { if (__atomic_fetch_add(&N[n], 1u, __ATOMIC_RELAXED)) break; bits += w; }
+            else { if (__atomic_sub_fetch(&N[n], 1u, __ATOMIC_RELAXED)) break; bits -= w; }
         }
     }
     uint64_t make_layer_inc(uint32_t l, double thresh, double lo, double hi, const std::vector<uint16_t>& prev) {
@@ -1774,8 +1786,9 @@ struct T2Enc {
             C.mslo = mslo; C.mshi = mshi;
             if (chg.empty()) return;
             const PrecG& PG = unit_prec(units[C.u]);
-            std::lock_guard<std::mutex> lk(ulock[C.u]);
-            uint64_t hd = 0, bits = ibits[C.u], body = ibody[C.u];
+            // (the unit's sums take this chunk's deltas atomically; blocks, their costs and the
+            // journal are the chunk's own)
+            uint64_t hd = 0, bits = 0, body = 0;
             for (size_t j = 0; j < chg.size(); j += 2) {
                 const uint32_t b = chg[j], inc = chg[j + 1];
                 const uint16_t vo = lnp[(size_t)b * L + l], vn = (uint16_t)(inc - prev[b]);
@@ -1787,7 +1800,9 @@ struct T2Enc {
                 lnp[(size_t)b * L + l] = vn;
                 if (!prev[b] && (vo == 0) != (vn == 0)) tree_toggle(PG.tree, b - PG.first_block, vn != 0, bits);
             }
-            ibits[C.u] = bits; ibody[C.u] = body; udirty[C.u] = 1;
+            __atomic_fetch_add(&ibits[C.u], bits, __ATOMIC_RELAXED);
+            __atomic_fetch_add(&ibody[C.u], body, __ATOMIC_RELAXED);
+            __atomic_store_n(&udirty[C.u], (uint8_t)1, __ATOMIC_RELAXED);
             C.hd = hd;
         };
         const auto tp0 = std::chrono::steady_clock::now();
