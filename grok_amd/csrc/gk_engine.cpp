@@ -3166,7 +3166,41 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             e[2] = (uint8_t)(psot >> 24); e[3] = (uint8_t)(psot >> 16); e[4] = (uint8_t)(psot >> 8); e[5] = (uint8_t)psot;
         }
         add_host(O.tp.data() + O.tp_off[part], O.tp_off[part + 1] - O.tp_off[part]);
-        for (uint32_t pq = O.pk_first[part]; pq < O.pk_first[part + 1]; ++pq) {
+        const uint32_t pa = O.pk_first[part], pe = O.pk_first[part + 1];
+        if (!ht && te - tb == 1 && (size_t)O.bsegs.size() >= 3 * 8192) {
+            // one tile's many body segments (C2 / C3: 49 k per layer) in parallel per packet: a
+            // packet's triples, header bytes and stream position follow from the ones before it
+            const uint32_t np = pe - pa;
+            std::vector<size_t> sb(np + 1), hb(np + 1);
+            std::vector<uint64_t> pb(np + 1);
+            sb[0] = seg.size(); hb[0] = hdrs.size(); pb[0] = pos;
+            for (uint32_t i = 0; i < np; ++i) {
+                const Pk& k = O.pk[pa + i];
+                sb[i + 1] = sb[i] + (k.hlen ? 3 : 0) + (k.s1 - k.s0);
+                hb[i + 1] = hb[i] + k.hlen;
+                pb[i + 1] = pb[i] + k.len;
+            }
+            seg.resize(sb[np]);
+            hdrs.resize(hb[np]);
+            host_pool().run(np, [&](size_t i) {
+                const Pk& k = O.pk[pa + i];
+                uint64_t* w = seg.data() + sb[i];
+                uint64_t p = pb[i];
+                if (k.hlen) {
+                    w[0] = slot_span + hb[i]; w[1] = p; w[2] = k.hlen; w += 3;
+                    memcpy(hdrs.data() + hb[i], O.phdr.data() + k.hoff, k.hlen);
+                    p += k.hlen;
+                }
+                for (uint32_t q = k.s0; q < k.s1; q += 3) {
+                    const uint32_t b = O.bsegs[q], off = O.bsegs[q + 1], n = O.bsegs[q + 2];
+                    w[0] = P.blocks[b].data_off - slot0 + off; w[1] = p; w[2] = n; w += 3;
+                    p += n;
+                }
+            });
+            pos = pb[np];
+            continue;
+        }
+        for (uint32_t pq = pa; pq < pe; ++pq) {
             const Pk& k = O.pk[pq];
             add_host(O.phdr.data() + k.hoff, k.hlen);
             for (uint32_t q = k.s0; q < k.s1; q += 3) {
