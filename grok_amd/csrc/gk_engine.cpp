@@ -3063,10 +3063,77 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             }
         };
         if (par_chains && chains.size() > 1) {
-            // largest chains (highest resolutions) first for the dynamic schedule
-            std::vector<size_t> ord(chains.size());
-            for (size_t i = 0; i < ord.size(); ++i) ord[i] = ord.size() - 1 - i;
-            host_pool().run(ord.size(), [&](size_t i) { run_chain(ord[i]); });
+            // One tile: (chain, band) units in parallel - a band's tag trees and code-blocks are
+            // its own, so each codes its part of every layer's header as raw bits and its body
+            // segments; per (chain, layer) the header is then the bit 1, the bands' bits in band
+            // order and a flush through the stuffing writer (the same bit sequence write_packet
+            // writes), the body the bands' segments in band order.  The top resolution's three
+            // bands (C2: 4,096 blocks each) no longer run as one chain.
+            struct BandU { uint32_t q, bi; };
+            std::vector<BandU> bu;
+            std::vector<uint32_t> bu0(chains.size() + 1, 0);
+            for (size_t q = 0; q < chains.size(); ++q) {
+                const ResG& R = T.comps[chains[q].c].res[chains[q].r];
+                for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
+                    if (R.prc[bi][chains[q].pi].cw && R.prc[bi][chains[q].pi].ch) bu.push_back({(uint32_t)q, bi});
+                bu0[q + 1] = (uint32_t)bu.size();
+            }
+            std::vector<std::vector<RawBits>> ubit(bu.size(), std::vector<RawBits>(L));
+            std::vector<std::vector<uint32_t>> useg(bu.size());     // (block, first byte, length)
+            std::vector<std::vector<uint32_t>> uend(bu.size(), std::vector<uint32_t>(L));   // useg end per layer
+            std::vector<size_t> bord(bu.size());
+            for (size_t i = 0; i < bord.size(); ++i) bord[i] = bord.size() - 1 - i;   // largest first
+            host_pool().run(bord.size(), [&](size_t j) {
+                const size_t u = bord[j];
+                const Chain& ch = chains[bu[u].q];
+                const ResG& R = T.comps[ch.c].res[ch.r];
+                const PrecG& PG = R.prc[bu[u].bi][ch.pi];
+                T2.band_init(PG, R.bands[bu[u].bi].numbps);
+                std::vector<uint32_t>& sg = useg[u];
+                for (uint32_t l = 0; l < L; ++l) {
+                    RawBits& rb = ubit[u][l];
+                    T2.band_header(PG, l, rb);
+                    rb.finish();
+                    for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
+                        const uint32_t b = PG.first_block + k;
+                        const uint32_t np = T2.lnp[(size_t)b * L + l];
+                        if (!np) continue;
+                        const uint32_t r0 = T2.inprev[b] ? T2.rate(b, T2.inprev[b] - 1) : 0, r1 = T2.rate(b, T2.inprev[b] + np - 1);
+                        if (r1 > r0) { sg.push_back(b); sg.push_back(r0); sg.push_back(r1 - r0); }
+                        T2.inprev[b] = (uint16_t)(T2.inprev[b] + np);
+                    }
+                    uend[u][l] = (uint32_t)sg.size();
+                }
+            });
+            host_pool().run(chains.size(), [&](size_t q) {
+                TileOut& C = co[q];
+                for (uint32_t l = 0; l < L; ++l) {
+                    const uint32_t h0 = (uint32_t)C.phdr.size();
+                    PktBitWriter bw(C.phdr);
+                    bw.putbit(1);
+                    for (uint32_t u = bu0[q]; u < bu0[q + 1]; ++u) {
+                        const RawBits& rb = ubit[u][l];
+                        const size_t full = (size_t)(rb.n / 64);
+                        const uint32_t rem = (uint32_t)(rb.n % 64);
+                        for (size_t i = 0; i < full; ++i) { bw.put((uint32_t)(rb.w[i] >> 32), 32); bw.put((uint32_t)rb.w[i], 32); }
+                        if (rem) {
+                            const uint64_t x = rb.w[full] >> (64 - rem);
+                            if (rem > 32) { bw.put((uint32_t)(x >> 32), rem - 32); bw.put((uint32_t)x, 32); }
+                            else bw.put((uint32_t)x, rem);
+                        }
+                    }
+                    bw.flush();
+                    const uint32_t hlen = (uint32_t)C.phdr.size() - h0;
+                    Pk k{h0, hlen, (uint32_t)C.bsegs.size(), 0, hlen};
+                    for (uint32_t u = bu0[q]; u < bu0[q + 1]; ++u) {
+                        const uint32_t s0 = l ? uend[u][l - 1] : 0, s1 = uend[u][l];
+                        for (uint32_t i = s0; i < s1; i += 3) k.len += useg[u][i + 2];
+                        C.bsegs.insert(C.bsegs.end(), useg[u].begin() + s0, useg[u].begin() + s1);
+                    }
+                    k.s1 = (uint32_t)C.bsegs.size();
+                    C.pk.push_back(k);
+                }
+            });
         } else {
             for (size_t q = 0; q < chains.size(); ++q) run_chain(q);
         }
