@@ -2876,11 +2876,15 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         uint32_t* dord = (uint32_t*)ctx->dord_enc.get(4 * (size_t)nbr);
         HIPCHK(hipMemcpyAsync(dord, ho, 4 * (size_t)nbr, hipMemcpyHostToDevice, st));
         // chunk ends as fractions of the blocks (GK_T1ENC_CUTS, up to three), rounded to whole MQ
-        // workgroups (4 x 64 blocks); the last chunk's MQ runs on the main stream
-        static std::vector<double> fr;
+        // workgroups (4 x 64 blocks); the last chunk's MQ runs on the main stream.  Defaults
+        // measured per workload (bench enc_t1): without rate control 0.125, 0.375 (C2 9.18 ms;
+        // 0.08, 0.25: 9.3), with it, where the modelling also sums distortions, 0.08, 0.25 (C3
+        // 14.96-15.22 ms against 15.6-15.8)
+        static std::vector<double> frs[2];
+        std::vector<double>& fr = frs[do_rc ? 1 : 0];
         if (fr.empty()) {
             const char* cv = getenv("GK_T1ENC_CUTS");
-            std::string cs = cv ? cv : "0.125,0.375";
+            std::string cs = cv ? cv : (do_rc ? "0.08,0.25" : "0.125,0.375");
             for (size_t q = 0; q < cs.size();) {
                 size_t e = cs.find(',', q);
                 if (e == std::string::npos) e = cs.size();
