@@ -767,7 +767,25 @@ struct ByteSrc {
     size_t len = 0;
     hipStream_t st = nullptr;
     static const size_t PG = 1 << 16;
-    std::unordered_map<size_t, std::vector<uint8_t>> pages;
+    // pages in pinned host memory from a process-wide pool (a pageable destination made each
+    // synchronous 64 KiB fetch go through the runtime's bounce buffer)
+    struct PinnedPages {
+        std::mutex m;
+        std::vector<uint8_t*> free;
+        uint8_t* get() {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                if (!free.empty()) { uint8_t* p = free.back(); free.pop_back(); return p; }
+            }
+            void* p = nullptr;
+            if (hipHostMalloc(&p, PG, hipHostMallocDefault) != hipSuccess) return nullptr;
+            return (uint8_t*)p;
+        }
+        void put(uint8_t* p) { std::lock_guard<std::mutex> lk(m); free.push_back(p); }
+    };
+    static PinnedPages& pinned() { static PinnedPages* pp = new PinnedPages(); return *pp; }   // (never destroyed)
+    struct PageDel { void operator()(uint8_t* p) const { if (p) pinned().put(p); } };
+    std::unordered_map<size_t, std::unique_ptr<uint8_t, PageDel>> pages;
     size_t last_pg = ~(size_t)0;             // fast path: the page of the previous access
     const uint8_t* last = nullptr;
     // host copies of scattered ranges fetched in one batch (tile-part and packet headers),
@@ -807,14 +825,16 @@ struct ByteSrc {
         if (it == pages.end()) {
             const auto t0 = std::chrono::steady_clock::now();
             size_t o = pg * PG, n = std::min(PG, len - o);
-            std::vector<uint8_t> v(n);
-            HIPCHK(hipMemcpyAsync(v.data(), dev + o, n, hipMemcpyDeviceToHost, st));
+            uint8_t* v = pinned().get();
+            if (!v) throw GkError("out of pinned host memory for codestream pages");
+            std::unique_ptr<uint8_t, PageDel> hold(v);
+            HIPCHK(hipMemcpyAsync(v, dev + o, n, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
-            it = pages.emplace(pg, std::move(v)).first;
+            it = pages.emplace(pg, std::move(hold)).first;
             fetch_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
             ++fetch_cnt;
         }
-        return it->second.data();
+        return it->second.get();
     }
     inline uint8_t at(size_t i) {
         if (i >= len) return 0;
