@@ -174,14 +174,17 @@ int gk_set_decode_layers(gk_ctx* ctx, uint32_t max_layers);
 /* grk_dparameters::cp_reduce (CodeStreamDecompress / TileComponent resolutions_to_decompress):
  * later gk_decode calls discard the `reduce` highest resolutions: packets of those resolutions
  * are skipped, the inverse DWT stops `reduce` levels early and the output planes are
- * ceil(w / 2^reduce) x ceil(h / 2^reduce) (0 = full resolution; not with gk_decode_window). */
+ * ceil(w / 2^reduce) x ceil(h / 2^reduce) (0 = full resolution); gk_decode_window then returns
+ * the window on the reduced canvas (every edge of its canvas rectangle ceil(x / 2^reduce),
+ * CodeStreamDecompress.cpp:471-481). */
 int gk_set_decode_reduce(gk_ctx* ctx, uint32_t reduce);
 
 /* grk_decompress_set_window + grk_decompress (grok.h:1082-1657; CodeStreamDecompress
  * window decode): decode the window [x0, x1) x [y0, y1) of the image.
  * Only the tile parts of tiles intersecting the window are read (located through TLM
  * when present, their packet headers through PLT), decoded and inverse-transformed;
- * comps[c][0] receives sample (x0, y0) of component c, row stride strides[c]. */
+ * comps[c][0] receives sample (x0, y0) of component c, row stride strides[c] (with
+ * gk_set_decode_reduce: the reduced window's first sample, see there). */
 int gk_decode_window(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, uint32_t x0, uint32_t y0,
                      uint32_t x1, uint32_t y1, void* const* comps, const uint32_t* strides, uint32_t sample_bytes,
                      int out_on_device);
