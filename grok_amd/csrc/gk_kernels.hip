@@ -432,7 +432,15 @@ __device__ __forceinline__ void inv53_fill(int x0, int y0, int w, int h, int tid
     }
 }
 
-__device__ __forceinline__ void inv53_lift(Lds53& T, int w, int h, int tid) {
+// k_dwt53_inv_l1's tile: rows start 3 dwords in, so output column c (LDS column c + 1) of a
+// 4-column group sits on a 16-byte boundary and a group is one ds_read_b128
+struct alignas(16) Lds53A {
+    int32_t a[DWT_LH][DWT_LW + 5];
+    __device__ __forceinline__ int32_t* operator[](int r) { return a[r] + 3; }
+    __device__ __forceinline__ const int32_t* operator[](int r) const { return a[r] + 3; }
+};
+template <class TT>
+__device__ __forceinline__ void inv53_lift(TT& T, int w, int h, int tid) {
     const int tx = tid & 63, ty = tid >> 6;
     if (w > 1) {
         // horizontal step 1: even interleaved cols x (lx = x - x0 + 1): x even <=> lx odd, lx in [1, TW+1]
@@ -543,7 +551,7 @@ template <class TO, int NC>
 __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict__ src, uint64_t cstride, uint32_t sstride,
                                                       GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h,
                                                       GkTiles tb, int32_t shift, int32_t mn, int32_t mx, int vec) {
-    __shared__ Lds53 T;
+    __shared__ Lds53A T;
     const uint3 bi = xcd_tile();
     const uint32_t tile = bi.z;
     src += tb.offset(tile, sstride);
@@ -603,8 +611,9 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int i = tid + 256 * j;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) (c == 0 ? R0 : R1)[4 * j + e] = T[(i >> 5) + 1][4 * (i & 31) + e + 1];
+                const int4 v = *(const int4*)&T[(i >> 5) + 1][4 * (i & 31) + 1];
+                int32_t* R = c == 0 ? R0 : R1;
+                R[4 * j] = v.x; R[4 * j + 1] = v.y; R[4 * j + 2] = v.z; R[4 * j + 3] = v.w;
             }
         }
     }
@@ -618,9 +627,11 @@ __global__ __launch_bounds__(256) void k_dwt53_inv_l1(const int32_t* __restrict_
         const int gy = y0 + ry, Y = oy + gy, gx = x0 + rx, X = ox + gx;
         if (gy >= (int)h || Y < win.y0 || Y >= win.y1) continue;
         int32_t r[4], g[4], b[4];
+        const int4 lv = *(const int4*)&T[ry + 1][rx + 1];
+        const int32_t lastv[4] = {lv.x, lv.y, lv.z, lv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int32_t last = T[ry + 1][rx + e + 1];
+            const int32_t last = lastv[e];
             if (NC == 3) {
                 const int32_t G = R0[4 * j + e] - ((R1[4 * j + e] + last) >> 2);
                 r[e] = cl(last + G + shift);
