@@ -429,7 +429,11 @@ __device__ __forceinline__ void inv97_fill(int x0, int y0, int w, int h, int tid
     }
 }
 
-__device__ __forceinline__ void inv97_lift(Lds97& T, int w, int h, int tid) {
+// k_dwt97_inv_l1's tile: rows of 140 floats (a multiple of four), so output column c (LDS
+// column c + 4) of a 4-column group sits on a 16-byte boundary: one ds_read_b128 per group
+typedef float Lds97i[T97_LH][T97_LW + 4];
+template <class TT>
+__device__ __forceinline__ void inv97_lift(TT& T, int w, int h, int tid) {
     const int tx = tid & 63, ty = tid >> 6;
     if (w > 1) {
         // step s (delta, gamma, beta, alpha) updates columns 2 + s, 4 + s, ... (67 - s) of every row
@@ -562,7 +566,7 @@ template <class TO, int NC>
 __global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ src, uint64_t cstride, uint32_t sstride,
                                                       GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h,
                                                       GkTiles tb, int32_t shift, int32_t mn, int32_t mx, int vec) {
-    __shared__ Lds97 T;
+    __shared__ __attribute__((aligned(16))) Lds97i T;
     const uint3 bi = xcd_tile();
     const uint32_t tile = bi.z;
     src += tb.offset(tile, sstride);
@@ -632,9 +636,9 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ 
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int i = tid + 256 * j;
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    (c == 0 ? R0 : R1)[4 * j + e] = T[(i >> 5) + T97_HALO][4 * (i & 31) + e + T97_HALO];
+                const float4 v = *(const float4*)&T[(i >> 5) + T97_HALO][4 * (i & 31) + T97_HALO];
+                float* R = c == 0 ? R0 : R1;
+                R[4 * j] = v.x; R[4 * j + 1] = v.y; R[4 * j + 2] = v.z; R[4 * j + 3] = v.w;
             }
         }
     }
@@ -648,9 +652,11 @@ __global__ __launch_bounds__(256) void k_dwt97_inv_l1(const float* __restrict__ 
         const int gy = y0 + ry, gx = x0 + rx, X = ox + gx, Y = oy + gy;
         if (gy >= (int)h || Y < win.y0 || Y >= win.y1) continue;
         int32_t r[4], g[4], b[4];
+        const float4 lv = *(const float4*)&T[ry + T97_HALO][rx + T97_HALO];
+        const float lastv[4] = {lv.x, lv.y, lv.z, lv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const float last = T[ry + T97_HALO][rx + e + T97_HALO];
+            const float last = lastv[e];
             if (NC == 3) {
                 const float Yv = R0[4 * j + e], U = R1[4 * j + e], V = last;
                 const float R = Yv + 1.402f * V;
