@@ -23,7 +23,8 @@ GK_MAX_LAYERS = 100
 # Exported symbols declared in include/grok_amd.h (checked by tests/test_capi.py).
 EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_encode_tiles", "gk_main_header",
            "gk_jp2_header", "gk_decode_header", "gk_probe_header", "gk_decode", "gk_decode_window", "gk_get_timings",
-           "gk_last_error", "gk_version", "gk_set_decode_layers", "gk_set_decode_reduce")
+           "gk_last_error", "gk_version", "gk_set_decode_layers", "gk_set_decode_reduce",
+           "gk_set_window_rule")
 
 
 class Poc(ctypes.Structure):
@@ -112,6 +113,8 @@ def load_library(build_if_missing=True):
     lib.gk_decode_header.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, P(ImageInfo)]
     lib.gk_set_decode_reduce.restype = ctypes.c_int
     lib.gk_set_decode_reduce.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    lib.gk_set_window_rule.restype = ctypes.c_int
+    lib.gk_set_window_rule.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.gk_set_decode_layers.restype = ctypes.c_int
     lib.gk_set_decode_layers.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     lib.gk_decode.restype = ctypes.c_int
@@ -436,6 +439,12 @@ class Engine:
         if self.lib.gk_set_decode_reduce(self.ctx, int(reduce)) != 0:
             self._err("gk_set_decode_reduce")
         self._reduce = int(reduce)
+
+    def set_window_rule(self, whole_tile):
+        """gk_set_window_rule: later windows use Grok's whole-tile inverse 5/3 rule (True, as
+        decompressTile without a window) or its partial-tile rule (False, the default)."""
+        if self.lib.gk_set_window_rule(self.ctx, int(bool(whole_tile))) != 0:
+            self._err("gk_set_window_rule")
 
     def decode(self, cs, length=None, out=None, row0=0, sample_bytes=0):
         """cs: bytes (host) or torch cuda uint8 tensor (+length).  Returns a (C, H, W)

@@ -24,15 +24,21 @@ def needs_build():
 def build(force=False, verbose=False):
     if not force and not needs_build():
         return LIB
+    from concurrent.futures import ThreadPoolExecutor
     objs = {}
+    cmds = []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(CSRC, s.rsplit(".", 1)[0] + ".o")
-        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj]
+        cmds.append(["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj])
         if verbose:
-            print(" ".join(cmd), file=sys.stderr)
-        subprocess.check_call(cmd)
+            print(" ".join(cmds[-1]), file=sys.stderr)
         objs[s] = obj
+    # one compiler per source, at most 8 at a time (container: 8 CPUs; the box sets MAX_JOBS)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "8")), 8))
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(subprocess.check_call, c) for c in cmds]:
+            f.result()
     engine = [objs[s] for s in ENGINE]
     # the grk_* drop-in, and the T1 plugin a Grok host loads (its own copy of the engine: a
     # host process already holds Grok's grk_* symbols)

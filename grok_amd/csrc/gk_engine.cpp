@@ -214,6 +214,11 @@ struct Params {
     std::vector<uint8_t> roishift;       // per component ROI shift (RGN, maxshift; empty = none)
     uint32_t roi(uint32_t c) const { return c < roishift.size() ? roishift[c] : 0u; }
     bool ht() const { return (cblk_sty & 0x40) != 0; }
+    // a code-block side above 64 (128 x 32 ... 1024 x 4): Part-1 blocks take the lane-per-block
+    // coders of gk_t1ms.hip, whose state is sized by the block (T1::alloc, T1.cpp:337-398), HT
+    // blocks the wide-line HT kernels; the headline kernels keep their 64-column layouts
+    bool wide() const { return cbw > 6 || cbh > 6; }
+    bool t1_generic() const { return (cblk_sty & 0x3f) != 0 || (wide() && !ht()); }
     uint32_t tw = 0, th = 0;             // nominal tile size (grk_cparameters::t_width/t_height; 0 = image)
     bool tlm = false, plt = false;       // grk_cparameters::writeTLM / writePLT
     bool jp2 = false;                    // grk_cparameters::cod_format == GRK_CODEC_JP2 (file format boxes)
@@ -2357,6 +2362,7 @@ struct gk_ctx {
     // across is H >> 1 (:1551-1554) where the whole-tile path has H / 2 (:583)
     bool dwt_partial = false;
     uint32_t dec_reduce = 0;   // highest resolutions discarded on decode (grk_dparameters::cp_reduce)
+    bool win_whole_tile = false;   // gk_set_window_rule: windows keep the whole-tile inverse DWT rule
     int device = 0;
     bool registered = false;   // counted in g_dev_engines
     hipStream_t st = nullptr;
@@ -2464,6 +2470,10 @@ static void set_params(Params& P, const gk_cparameters* cp, uint32_t nc) {
             }
             P.prcw[r] = pw < 1 ? 1 : (uint32_t)floorlog2(pw);
             P.prch[r] = ph < 1 ? 1 : (uint32_t)floorlog2(ph);
+            // a size of exactly 1 gives exponent 0: legal at resolution 0 (1 x 1 code-blocks),
+            // without a band partition (B.6: PPx - 1) above it
+            if (r > 0 && (!P.prcw[r] || !P.prch[r]))
+                throw GkError("precinct size 1 above resolution 0 (exponent 0 has no band partition)");
         }
     }
 }
@@ -2664,7 +2674,9 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if (want.prec == 0 || want.prec > 31) throw GkError("component precision must be 1..31 bits");
     if (want.w == 0 || want.h == 0) throw GkError("empty image");
-    if ((1u << want.p.cbw) > 64 || (1u << want.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
+    // grk_compress.cpp:981-988 (and A.6.1's xcb, ycb): 4 <= side <= 1024, at most 4096 samples
+    if (want.p.cbw < 2 || want.p.cbh < 2 || want.p.cbw > 10 || want.p.cbh > 10 || want.p.cbw + want.p.cbh > 12)
+        throw GkError("code-block size must be 4..1024 per side with at most 4096 samples");
     ensure_plan(ctx, want);
     restore_native_qcd(ctx);
     // encode: ROI-scaled indices keep 6 fractional bits below them in a 31-bit magnitude
@@ -2859,8 +2871,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nbx * GK_HT_MEL_CAP + 256);
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_ht_enc(st, arena, dblk, dbytes, mel, GK_HT_MEL_CAP, dinfo, nbr, derr);
-    } else if (P.p.cblk_sty & 0x3f) {
+        gk_launch_ht_enc(st, arena, dblk, dbytes, mel, GK_HT_MEL_CAP, dinfo, nbr, derr, P.p.wide());
+    } else if (P.p.t1_generic()) {
         // mode switches: lane-per-block coder with per-pass termination rules (gk_t1ms.hip)
         uint8_t* mst = (uint8_t*)ctx->dmsstate.get(gk_t1ms_state_bytes(nbx));
         launch_check(__LINE__);
@@ -2976,7 +2988,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const size_t rc_header_size = H.size() + (P.p.jp2 ? jp2_prefix_size(P) : 0);
     if (!with_header) H.clear();
     const auto te1 = eclk::now();
-    if (const char* ds = getenv("GK_DUMP_SYMS"); ds && dsym && !(P.p.cblk_sty & 0x3f)) {
+    if (const char* ds = getenv("GK_DUMP_SYMS"); ds && dsym && !P.p.t1_generic()) {
         // debug: per-block MQ symbol counts (decisions) and coded bit-planes, u32 pairs
         std::vector<uint32_t> pe((size_t)GK_MAX_PASSES * nbr), cm(2 * (size_t)nbr), out(2 * (size_t)nbr);
         HIPCHK(hipMemcpy(pe.data(), dpe, 4 * pe.size(), hipMemcpyDeviceToHost));
@@ -3545,7 +3557,10 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             if (scod & 1) {
                 if (L < 12 + W.p.numres) throw GkError("corrupt COD marker (precinct sizes)");
                 W.p.custom_prc = true;
-                for (uint32_t r = 0; r < W.p.numres; ++r) { uint32_t v = S.at(s + 10 + r); W.p.prcw[r] = v & 15; W.p.prch[r] = v >> 4; }
+                for (uint32_t r = 0; r < W.p.numres; ++r) {
+                    uint32_t v = S.at(s + 10 + r); W.p.prcw[r] = v & 15; W.p.prch[r] = v >> 4;
+                    if (r > 0 && (!W.p.prcw[r] || !W.p.prch[r])) throw GkError("COD: precinct exponent 0 above resolution 0");
+                }
             }
             have_cod = true;
             Hd.cod = marker_body(S, s, L);
@@ -3611,7 +3626,6 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     if (Hd.parts.empty()) throw GkError("no tile parts");
     for (uint8_t v : W.p.roishift)   // Grok's RoiShiftHTFilter keeps only the sign of a shifted sample
         if (v && W.p.ht()) throw GkError("ROI with HTJ2K is not supported on this path");
-    if ((1u << W.p.cbw) > 64 || (1u << W.p.cbh) > 64) throw GkError("code-block sides > 64 not supported yet");
 }
 
 // Device-resident codestream: copy scattered ranges (tile-part headers, packet headers) to
@@ -3738,7 +3752,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     hipStream_t st = ctx->st;
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[0], st));
-    ctx->dwt_partial = win != nullptr;
+    // Grok's partial-tile inverse (its single odd 5/3 sample shifted, not halved) follows a window
+    // set with setDecompressWindow; decompressTile without one keeps the whole-tile rule
+    ctx->dwt_partial = win != nullptr && !ctx->win_whole_tile;
     // GK_PROFILE=1: host phase times of the decode (stderr)
     static const bool prof = getenv("GK_PROFILE") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -4238,15 +4254,16 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipMemcpyAsync(dsel, hsel, 4 * (size_t)nbr, hipMemcpyHostToDevice, st));
         int* derr = (int*)ctx->derr.get(64);
         HIPCHK(hipMemsetAsync(derr, 0, 64, st));
-        gk_launch_ht_dec(st, src_bytes, dblk, dsel, arena, nbr, derr);
+        gk_launch_ht_dec(st, src_bytes, dblk, dsel, arena, nbr, derr, P.p.wide());
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
         int herr = 0;
         HIPCHK(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (herr) throw GkError("corrupt HT code-block segment");
-    } else if (P.p.cblk_sty & 0x3f) {
-        // mode switches: lane-per-block decoder over the codeword segments (gk_t1ms.hip)
+    } else if (P.p.t1_generic()) {
+        // mode switches or wide code-blocks: lane-per-block decoder over the codeword segments
+        // (gk_t1ms.hip)
         uint32_t* dsl = nullptr;
         if (multiseg && !hseglen.empty()) {
             uint32_t* hsl = (uint32_t*)ctx->hord.get(4 * hseglen.size());
@@ -4816,6 +4833,12 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void
         ctx->err = e.msg;
         return -1;
     }
+}
+
+int gk_set_window_rule(gk_ctx* ctx, int whole_tile) {
+    if (!ctx) return -1;
+    ctx->win_whole_tile = whole_tile != 0;
+    return 0;
 }
 
 int gk_set_decode_reduce(gk_ctx* ctx, uint32_t reduce) {

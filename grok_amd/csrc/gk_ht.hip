@@ -24,8 +24,13 @@
 #define GK_HT_TABLE_QUAL __constant__
 #include "gk_ht_tables.h"
 
-#define HT_WG 256
-#define HT_LINE 36          // line-state entries per lane: w/2 + 4 for w <= 64
+// Workgroup size and line-state entries per lane (w/2 + 4): 256 lanes x 36 entries for blocks up
+// to 64 wide; code-blocks up to 1024 wide (Grok accepts 4 <= w, h <= 1024 with w * h <= 4096,
+// grk_compress.cpp:981-988) take 64-lane workgroups with 516 entries (66 KB of line state)
+#define HT_WG_STD 256
+#define HT_LINE_STD 36
+#define HT_WG_WIDE 64
+#define HT_LINE_WIDE 516
 
 // MEL exponent table {0,0,0,1,1,1,2,2,2,3,3,4,5} packed 3 bits per state
 __device__ __forceinline__ int mel_exp(int k) {
@@ -47,6 +52,7 @@ __device__ __forceinline__ void uvlc_code(int u, uint32_t& pre, int& plen, uint3
 // =============================================================================
 // Encoder
 // =============================================================================
+template <int HT_WG, int HT_LINE>
 __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ coef, const GkBlock* __restrict__ blocks,
                                                   uint8_t* __restrict__ bytes, uint8_t* __restrict__ mel_scratch,
                                                   uint32_t mel_cap, uint32_t* __restrict__ info, uint32_t nblocks,
@@ -367,6 +373,7 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
 // =============================================================================
 // Decoder
 // =============================================================================
+template <int HT_WG, int HT_LINE>
 __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ bytes, const GkBlock* __restrict__ blocks,
                                                   const uint32_t* __restrict__ ids, int32_t* __restrict__ coef,
                                                   uint32_t nblocks, int* __restrict__ err, uint32_t nl) {
@@ -630,19 +637,31 @@ static uint32_t ht_lanes(const char* var) {
     return (uint32_t)(n < 1 ? 1 : (n > 64 ? 64 : n));
 }
 void gk_launch_ht_enc(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, uint8_t* mel_scratch,
-                      uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err) {
+                      uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err, bool wide) {
     if (!nblocks) return;
     static const uint32_t nl = ht_lanes("GK_HT_ENC_LANES");
-    const uint32_t per = (HT_WG / 64) * nl;
-    hipLaunchKernelGGL(k_ht_enc, dim3((nblocks + per - 1) / per), dim3(HT_WG), 0, st, coef, blocks, bytes,
+    if (wide) {
+        const uint32_t per = (HT_WG_WIDE / 64) * nl;
+        hipLaunchKernelGGL((k_ht_enc<HT_WG_WIDE, HT_LINE_WIDE>), dim3((nblocks + per - 1) / per), dim3(HT_WG_WIDE), 0, st,
+                           coef, blocks, bytes, mel_scratch, mel_cap, info, nblocks, err, nl);
+        return;
+    }
+    const uint32_t per = (HT_WG_STD / 64) * nl;
+    hipLaunchKernelGGL((k_ht_enc<HT_WG_STD, HT_LINE_STD>), dim3((nblocks + per - 1) / per), dim3(HT_WG_STD), 0, st, coef, blocks, bytes,
                        mel_scratch, mel_cap, info, nblocks, err, nl);
 }
 
 void gk_launch_ht_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* ids, int32_t* coef,
-                      uint32_t nblocks, int* err) {
+                      uint32_t nblocks, int* err, bool wide) {
     if (!nblocks) return;
     static const uint32_t nl = ht_lanes("GK_HT_DEC_LANES");
-    const uint32_t per = (HT_WG / 64) * nl;
-    hipLaunchKernelGGL(k_ht_dec, dim3((nblocks + per - 1) / per), dim3(HT_WG), 0, st, bytes, blocks, ids, coef,
-                       nblocks, err, nl);
+    if (wide) {
+        const uint32_t per = (HT_WG_WIDE / 64) * nl;
+        hipLaunchKernelGGL((k_ht_dec<HT_WG_WIDE, HT_LINE_WIDE>), dim3((nblocks + per - 1) / per), dim3(HT_WG_WIDE), 0, st,
+                           bytes, blocks, ids, coef, nblocks, err, nl);
+        return;
+    }
+    const uint32_t per = (HT_WG_STD / 64) * nl;
+    hipLaunchKernelGGL((k_ht_dec<HT_WG_STD, HT_LINE_STD>), dim3((nblocks + per - 1) / per), dim3(HT_WG_STD), 0, st, bytes, blocks, ids,
+                       coef, nblocks, err, nl);
 }

@@ -94,8 +94,8 @@ void gk_launch_dwt97_fwd_l1(hipStream_t st, int stype, int nc, GkPtr3 in, uint32
 void gk_launch_dwt97_inv_l1(hipStream_t st, int stype, int nc, const float* src, uint64_t cstride, uint32_t sstride,
                             GkPtr3 out, uint32_t ostride, GkWin win, uint32_t w, uint32_t h, GkTiles tb, int32_t shift,
                             int32_t mn, int32_t mx);
-// HTJ2K cleanup-pass block coder (gk_ht.hip)
+// HTJ2K cleanup-pass block coder (gk_ht.hip); wide: some block is wider than 64 samples
 void gk_launch_ht_enc(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint8_t* bytes, uint8_t* mel_scratch,
-                      uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err);
+                      uint32_t mel_cap, uint32_t* info, uint32_t nblocks, int* err, bool wide = false);
 void gk_launch_ht_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* blocks, const uint32_t* ids, int32_t* coef,
-                      uint32_t nblocks, int* err);
+                      uint32_t nblocks, int* err, bool wide = false);

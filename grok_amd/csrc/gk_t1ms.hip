@@ -20,7 +20,9 @@
 
 enum { MS_LAZY = 0x01, MS_RESET = 0x02, MS_TERMALL = 0x04, MS_VSC = 0x08, MS_PTERM = 0x10, MS_SEGSYM = 0x20 };
 enum { F_SIG = 1, F_NEG = 2, F_PI = 4, F_MU = 8 };
-#define MS_STATE_BYTES 4608u   // (64 + 2) x (64 + 2) state bytes, rounded up
+// (w + 2) x (h + 2) state bytes, rounded up: at most 1026 x 6 for the code-block shapes Grok
+// accepts (4 <= w, h <= 1024, w * h <= 4096; grk_compress.cpp:981-988)
+#define MS_STATE_BYTES 6208u
 #define MS_CT_INIT 0xDEADBEEFu // BYPASS_CT_INIT (mqc_inl.h:24): no raw bit written yet
 
 // Block state with a one-sample border; VSC: the last row of a stripe sees the next

@@ -273,8 +273,9 @@ bool run_encode(CodecObj* C, const void* const* planes, const uint32_t* strides,
     return true;
 }
 
-// decode into `o` (its comps sized for the region) — the whole image or the window `w`
-bool run_decode(CodecObj* C, ImageObj* o, const uint32_t* w) {
+// decode into `o` (its comps sized for the region) — the whole image or the window `w`;
+// whole_tile: a tile decode with no window set keeps Grok's whole-tile inverse rule
+bool run_decode(CodecObj* C, ImageObj* o, const uint32_t* w, bool whole_tile = false) {
     std::lock_guard<std::mutex> lk(g_eng_m);
     gk_ctx* e = engine();
     if (!e) return false;
@@ -283,9 +284,11 @@ bool run_decode(CodecObj* C, ImageObj* o, const uint32_t* w) {
     for (uint16_t i = 0; i < o->img.numcomps; ++i) { planes[i] = o->comps[i].data; strides[i] = o->comps[i].stride; }
     gk_set_decode_layers(e, C->dp.cp_layer);   // 0 = every layer
     gk_set_decode_reduce(e, C->dp.cp_reduce);
+    gk_set_window_rule(e, whole_tile ? 1 : 0);
     int rc = w ? gk_decode_window(e, C->data.data(), C->data.size(), 0, w[0], w[1], w[2], w[3], planes.data(),
                                   strides.data(), 0, 0)
                : gk_decode(e, C->data.data(), C->data.size(), 0, planes.data(), strides.data(), 0, 0);
+    gk_set_window_rule(e, 0);
     if (rc != 0) { error("%s", gk_last_error(e)); return false; }
     return true;
 }
@@ -685,7 +688,8 @@ bool grk_decompress_tile(grk_codec* codec, uint16_t tileIndex) {
     // (with cp_reduce the components take the tile's rectangle reduced, CodeStreamDecompress.cpp:471-481)
     if (!reshape_image(C->out, w[0] + OX, w[1] + OY, w[2] + OX, w[3] + OY, C->dp.cp_reduce)) return false;
     C->tile_decoded = true;
-    return run_decode(C, C->out, w);
+    // wholeTileDecompress stays set unless a window was (CodeStreamDecompress.cpp:389)
+    return run_decode(C, C->out, w, !C->has_win);
 }
 
 grk_image* grk_decompress_get_tile_image(grk_codec* codec, uint16_t tileIndex) {

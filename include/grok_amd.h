@@ -179,6 +179,14 @@ int gk_set_decode_layers(gk_ctx* ctx, uint32_t max_layers);
  * CodeStreamDecompress.cpp:471-481). */
 int gk_set_decode_reduce(gk_ctx* ctx, uint32_t reduce);
 
+/* Inverse 5/3 rule of later gk_decode_window calls.  whole_tile = 0 (default): Grok's partial-tile
+ * inverse, which a window set through setDecompressWindow selects for every tile
+ * (CodeStreamDecompress.cpp:389; a one-sample-wide resolution on an odd coordinate shifts its
+ * sample, WaveletReverse.cpp:1551-1554).  whole_tile = 1: the whole-tile rule (that sample halved,
+ * WaveletReverse.cpp:583), which CodeStreamDecompress::decompressTile keeps when no window is set
+ * (grk_decompress_tile with the CLI's set_window(0,0,0,0), :309-316, 416-493). */
+int gk_set_window_rule(gk_ctx* ctx, int whole_tile);
+
 /* grk_decompress_set_window + grk_decompress (grok.h:1082-1657; CodeStreamDecompress
  * window decode): decode the window [x0, x1) x [y0, y1) of the image.
  * Only the tile parts of tiles intersecting the window are read (located through TLM

@@ -1996,7 +1996,10 @@ static Params to_params(const orc_cparams* cp) {
     // the compression ratios otherwise
     for (uint32_t i = 0; i < 100; ++i) p.rates[i] = (i < p.nlayers && !p.quality) ? cp->layer_rate[i] : 0.0;
     for (uint32_t i = 0; i < 100; ++i) p.dist[i] = (i < p.nlayers && p.quality) ? cp->layer_distortion[i] : 0.0;
-    for (int i = 0; i < 33; ++i) { p.prcw_exp[i] = cp->prcw_exp[i] ? cp->prcw_exp[i] : 15; p.prch_exp[i] = cp->prch_exp[i] ? cp->prch_exp[i] : 15; }
+    // exponents as given: 15 (orc_default_params) is the default 2^15 partition, 0 is a legal
+    // exponent at resolution 0 (CodeStreamCompress.cpp:573-590 writes it when the halved size
+    // reaches 1); at a higher resolution it has no band partition (B.6 PPx - 1) and is refused
+    for (int i = 0; i < 33; ++i) { p.prcw_exp[i] = cp->prcw_exp[i] & 15; p.prch_exp[i] = cp->prch_exp[i] & 15; }
     return p;
 }
 
@@ -2383,6 +2386,15 @@ static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector
 // A POC list must name every packet of the tile: CodeStreamCompress::validateProgressionOrders
 // (:1685-1747) refuses a list that misses one.  (A packet two entries name is written once, in
 // the first entry's part: the tile's packet tracker, T2Compress.cpp:278-280.)
+// B.6: a resolution above 0 splits its precinct partition among the bands at PPx - 1, so its
+// exponent must be at least 1 (Grok never writes 0 there; CodeStreamCompress.cpp:575-590 clamps
+// sizes below 1 to exponent 1 and only a size of exactly 1 reaches 0, at the lowest resolution)
+static bool prc_exps_ok(const Params& p) {
+    for (uint32_t r = 1; r < p.numres; ++r)
+        if (p.prcw_exp[r] == 0 || p.prch_exp[r] == 0) return false;
+    return true;
+}
+
 static bool pocs_cover(const Params& p, uint32_t nc) {
     if (p.pocs.empty()) return true;
     std::vector<uint8_t> n((size_t)p.nlayers * p.numres * nc, 0);
@@ -2464,7 +2476,7 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
     size_t tlm_pos = 0;
     uint32_t nt = 0;
     const Params p0 = to_params(cp);
-    if (!pocs_cover(p0, nc) || num_parts(p0, nc) < 1) return 0;
+    if (!prc_exps_ok(p0) || !pocs_cover(p0, nc) || num_parts(p0, nc) < 1) return 0;
     if (!needs_rate_control(p0) && tile_count(p0, w, h) > 1) {
         // independent tiles coded in parallel, written in tile order
         nt = tile_count(p0, w, h);
@@ -2592,6 +2604,7 @@ size_t orc_main_header(uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int s
 size_t orc_encode_tile_parts(const int32_t* slab, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
                              const orc_cparams* cp, uint32_t row0, uint32_t rows, uint32_t tb, uint32_t te,
                              uint8_t* out, size_t cap, uint32_t* part_lens) {
+    if (!prc_exps_ok(to_params(cp))) return 0;
     std::vector<std::vector<uint8_t>> parts(te - tb);
     par_for(te - tb, [&](size_t q) {
         EncodeState E;
@@ -3033,6 +3046,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             if ((s[8] & 0x40) && s[8] != 0x40) return -2;  // HT with Part-1 mode switches (CodeStreamDecompress.cpp:1781)
             if (s[8] & 0x80) return -2;
             if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
+            if (!prc_exps_ok(p)) return -2;
         } else if (m == 0xff5f) {
             if (!read_poc(s, L, im.nc, p.pocs)) return -2;
         } else if (m == 0xff5e) {                          // RGN: Crgn, Srgn (0), SPrgn

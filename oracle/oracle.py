@@ -145,15 +145,20 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
         for i, q in enumerate(quality):
             p.layer_distortion[i] = q
     if precincts:
-        # Grok CLI semantics: list of (w, h) from the highest resolution down; the last repeats
-        exps = [(int(w).bit_length() - 1, int(h).bit_length() - 1) for (w, h) in precincts]
-        for r in range(numres):
-            k = numres - 1 - r
-            e = exps[min(k, len(exps) - 1)]
-            if k >= len(exps):
-                # Grok halves the last specified precinct per lower resolution (min 1 = 2^1? keep >= cblk)
-                e = (max(exps[-1][0] - (k - len(exps) + 1), 1), max(exps[-1][1] - (k - len(exps) + 1), 1))
-            p.prcw_exp[r], p.prch_exp[r] = e
+        # Grok CLI semantics (CodeStreamCompress.cpp:542-590): sizes from the highest resolution
+        # down; past the list, the last size shifted right once per resolution; a size below 1
+        # takes exponent 1, any other floorlog2(size) -- so a shift that reaches exactly 1 gives
+        # exponent 0 (1 x 1 code-blocks at resolution 0)
+        def _exp(s):
+            return 1 if s < 1 else int(s).bit_length() - 1
+        ns = len(precincts)
+        for k in range(numres):
+            r = numres - 1 - k
+            if k < ns:
+                w, h = precincts[k]
+            else:
+                w, h = precincts[-1][0] >> (k - (ns - 1)), precincts[-1][1] >> (k - (ns - 1))
+            p.prcw_exp[r], p.prch_exp[r] = _exp(int(w)), _exp(int(h))
     return p
 
 

@@ -187,3 +187,46 @@ def test_grk_api_offsets(tool, flags):
     assert cs == O.encode(img, 8, **parse_flags(flags))
     dec, _ = _dec(tool, path, img.shape)
     np.testing.assert_array_equal(dec, img)
+
+
+def test_grk_api_tile_rule_without_window(tool):
+    # grk_decompress -tile t with no -d decodes the tile with Grok's whole-tile
+    # inverse (decompressTile keeps wholeTileDecompress), a -d window with the partial-tile one;
+    # the fixture makes the two rules differ inside tile 3 (tests/window_rule_case.py)
+    from window_rule_case import LAYERS, TILE, case
+    img, kw = case()
+    cs = O.encode(img, 8, **kw)
+    exe, d = tool
+    p = d / "tile_rule.j2k"
+    p.write_bytes(cs)
+    O.set_decode_layers(LAYERS)
+    try:
+        whole, _ = O.decode(cs)
+        part, _ = O.decode(cs, partial=True)
+    finally:
+        O.set_decode_layers(0)
+    tw, h = kw["tiles"]
+    x0, x1 = TILE * tw, min((TILE + 1) * tw, img.shape[2])
+    assert (whole[:, :, x0:x1] != part[:, :, x0:x1]).any()
+    dec, _ = _dec(tool, p, (1, h, x1 - x0), ("-tile", TILE, "-l", LAYERS))
+    np.testing.assert_array_equal(dec, whole[:, :, x0:x1])
+    dec, _ = _dec(tool, p, (1, h, x1 - x0), ("-d", "%d,0,%d,%d" % (x0, x1, h), "-l", LAYERS))
+    np.testing.assert_array_equal(dec, part[:, :, x0:x1])
+    dec, _ = _dec(tool, p, (1, h, x1 - x0), ("-tile", TILE, "-d", "%d,0,%d,%d" % (x0, x1, h), "-l", LAYERS))
+    np.testing.assert_array_equal(dec, part[:, :, x0:x1])
+    dec, _ = _dec(tool, p, img.shape, ("-l", LAYERS))
+    np.testing.assert_array_equal(dec, whole)
+
+
+@pytest.mark.parametrize("flags,grok_bytes,grok_sha", [("-b 128,32", 410963, "69f2f8af6486a243"),
+                                                       ("-b 1024,4 -r 20,5", 119723, "e7f7599fcd9dc5ef")])
+def test_grk_api_wide_code_blocks(tool, flags, grok_bytes, grok_sha):
+    # grk_compress -b W,H with a side above 64 (grk_compress.cpp:981-988) through the drop-in
+    import hashlib
+    from grok_amd.synth import synth_image
+    img = synth_image(384, 520, 3, 8, 7).astype(np.int32)
+    cs, path = _enc(tool, img, 8, flags, "wide_" + flags.split()[1].replace(",", "x"))
+    assert len(cs) == grok_bytes and hashlib.sha256(cs).hexdigest()[:16] == grok_sha
+    dec, _ = _dec(tool, path, img.shape)
+    want, _ = O.decode(cs)
+    np.testing.assert_array_equal(dec, want)

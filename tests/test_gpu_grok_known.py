@@ -13,7 +13,7 @@ import pytest
 
 import oracle as O
 from conftest import parse_flags
-from test_oracle_grok_sizes import IMAGES, KNOWN
+from test_oracle_grok_sizes import DECODES, IMAGES, KNOWN, oracle_reduced, u16_sha
 
 pytestmark = pytest.mark.gpu
 
@@ -73,3 +73,21 @@ def test_fast_and_serial_simulation_agree(eng, images, monkeypatch):
         serial = eng.encode(img, bits, params=gk_params(kw))
         monkeypatch.delenv("GK_T2_SERIAL_SIM")
         assert fast == serial, flags
+
+
+@pytest.mark.parametrize("which,flags,red,win,shape,grok_sha", DECODES, ids=["%s %s -r %d" % (d[0], d[1], d[2]) for d in DECODES])
+def test_engine_decode_equals_grok(eng, images, which, flags, red, win, shape, grok_sha):
+    # Grok's grk_decompress -r / -d on Grok's own streams (round-5 review hashes): the engine's
+    # reduced and windowed decodes equal them and the oracle's
+    img, bits = images[which]
+    kw = parse_flags(flags)
+    cs = eng.encode(img, bits, params=gk_params(kw))
+    assert cs == O.encode(img, bits, **kw)
+    eng.set_decode_reduce(red)
+    try:
+        dec = eng.decode_window(cs, win) if win else eng.decode(cs)
+    finally:
+        eng.set_decode_reduce(0)
+    assert dec.shape == shape
+    assert u16_sha(dec) == grok_sha
+    np.testing.assert_array_equal(dec, oracle_reduced(cs, red, win))

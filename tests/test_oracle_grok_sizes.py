@@ -49,8 +49,51 @@ KNOWN = [
     ("A", "-t 200,160 -r 30,10", 59002, "233358c512356ea7"),
     ("A", "-p CPRL -c [64,64],[32,32] -r 20,5,1", 430903, "4b2a4e73b5768a8a"),
     ("B", "-t 96,96 -r 30,5", 31004, "a484a6cb530b7307"),
+    # precinct sizes halved down to 1 at resolution 0: Grok writes exponent 0 there (1 x 1
+    # code-blocks; CodeStreamCompress.cpp:573-590 clamps only a size below 1 to exponent 1)
+    ("A", "-c [32,32]", 460644, "1a20eebb14e5bdae"),
+    ("A", "-c [128,128] -n 8", 414895, "a579b4e7db961bcc"),
+    ("A", "-c [32,32] -t 128,128 -r 25,8", 81116, "d1d86b10027d07d8"),
 ]
-IMAGES = {"A": ((384, 520, 3, 8, 7), 8), "B": ((300, 260, 1, 16, 21), 16)}
+# code-blocks with a side above 64 (grk_compress.cpp:981-988 accepts 4 <= w, h <= 1024 with
+# w * h <= 4096; T1.cpp:337-398 sizes the flags from the block)
+KNOWN_WIDE = [
+    ("A", "-b 128,32", 410963, "69f2f8af6486a243"),
+    ("A", "-b 1024,4 -r 20,5", 119723, "e7f7599fcd9dc5ef"),
+    ("A", "-b 256,16 -t 256,256 -r 30,10 -X -L", 60250, "3181016eaffb0732"),
+    ("B", "-b 512,8", 134945, "f208992db5ed0200"),
+]
+# Grok 9.2.0's grk_decompress on Grok's own streams (round-5 review): (input, encode flags,
+# reduce -r, window -d at full resolution or None, output shape, SHA-256 prefix of the decoded
+# C x H x W array as little-endian uint16).  A window is returned on the reduced canvas with every
+# edge ceil(x / 2^r) (CodeStreamDecompress.cpp:390, 471-481) and decoded under the partial-tile
+# rule a window selects (WaveletReverse.cpp:1551-1554).
+DECODES = [
+    ("A", "-t 128,128", 2, (37, 51, 300, 333), (3, 71, 65), "8e8e070182473ca1"),
+    ("A", "", 1, (10, 20, 200, 170), (3, 75, 95), "2116a8a1fc0a78b3"),
+    ("A", "-I -t 128,128", 2, (37, 51, 300, 333), (3, 71, 65), "d14027a6df793e4f"),
+    ("D", "-p RPCL -c [128,128],[64,64] -t 256,256", 1, (100, 200, 650, 611), (3, 206, 275), "292c11071aec9bbf"),
+    ("A", "-I -t 128,128 -r 40,20,10", 0, (37, 51, 300, 333), (3, 282, 263), "867ec517e1d2a93d"),
+    ("B", "-M 64", 2, None, (1, 75, 65), "6351293e6e33fed7"),
+]
+IMAGES = {"A": ((384, 520, 3, 8, 7), 8), "B": ((300, 260, 1, 16, 21), 16), "D": ((700, 900, 3, 8, 55), 8)}
+
+
+def u16_sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a.astype("<u2")).tobytes()).hexdigest()[:16]
+
+
+def oracle_reduced(cs, red, win):
+    """The oracle's decode of cs at reduction red, cropped to the full-resolution window win."""
+    O.set_decode_reduce(red)
+    try:
+        dec, _ = O.decode(cs, partial=win is not None)
+    finally:
+        O.set_decode_reduce(0)
+    if win is None:
+        return dec
+    cd = lambda v: -(-v >> red)
+    return dec[:, cd(win[1]):cd(win[3]), cd(win[0]):cd(win[2])]
 
 
 @pytest.fixture(scope="module")
@@ -58,13 +101,38 @@ def images():
     return {k: (synth_image(*a).astype(np.int32), bits) for k, (a, bits) in IMAGES.items()}
 
 
-@pytest.mark.parametrize("which,flags,grok_bytes,grok_sha", KNOWN, ids=[k[1] for k in KNOWN])
+@pytest.mark.parametrize("which,flags,grok_bytes,grok_sha", KNOWN + KNOWN_WIDE, ids=[k[1] for k in KNOWN + KNOWN_WIDE])
 def test_oracle_equals_grok(images, which, flags, grok_bytes, grok_sha):
     img, bits = images[which]
     cs = O.encode(img, bits, **parse_flags(flags))
     assert len(cs) == grok_bytes, flags
     if grok_sha:
         assert hashlib.sha256(cs).hexdigest()[:16] == grok_sha, flags
+
+
+@pytest.mark.parametrize("which,flags,red,win,shape,grok_sha", DECODES, ids=["%s %s -r %d" % (d[0], d[1], d[2]) for d in DECODES])
+def test_oracle_decode_equals_grok(images, which, flags, red, win, shape, grok_sha):
+    img, bits = images[which]
+    dec = oracle_reduced(O.encode(img, bits, **parse_flags(flags)), red, win)
+    assert dec.shape == shape
+    assert u16_sha(dec) == grok_sha
+
+
+def test_oracle_precinct_exponent_zero(images):
+    # -c [32,32] with 6 resolutions: 32, 16, 8, 4, 2, 1 -> exponents 5 .. 0; the COD's last
+    # precinct byte (resolution 0) is 0x00 and the stream decodes losslessly
+    img, bits = images["A"]
+    p = O.params(precincts=[(32, 32)])
+    assert [p.prcw_exp[r] for r in range(6)] == [0, 1, 2, 3, 4, 5]
+    p = O.params(precincts=[(2, 2)], numres=4)   # 2, 1, 0 -> exponents 1, 0, then clamped 1
+    assert [p.prcw_exp[r] for r in range(4)] == [1, 1, 0, 1]
+    cs = O.encode(img, bits, precincts=[(32, 32)])
+    i = cs.index(b"\xff\x52")
+    assert cs[i + 2 + 2 + 10:i + 2 + 2 + 16] == bytes([0x00, 0x11, 0x22, 0x33, 0x44, 0x55])
+    np.testing.assert_array_equal(O.decode(cs)[0], img)
+    # exponent 0 above resolution 0 has no band partition (B.6): refused, as the engine does
+    with pytest.raises(RuntimeError):
+        O.encode(img, bits, precincts=[(2, 2)], numres=4)
 
 
 def test_grok_poc_stream_decodes(images):
