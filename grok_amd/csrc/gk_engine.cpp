@@ -773,23 +773,45 @@ struct ByteSrc {
     hipStream_t st = nullptr;
     static const size_t PG = 1 << 16;
     // pages in pinned host memory from a process-wide pool (a pageable destination made each
-    // synchronous 64 KiB fetch go through the runtime's bounce buffer)
+    // synchronous 64 KiB fetch go through the runtime's bounce buffer).  At most kLive pinned
+    // pages exist at once (256 MiB; past that a page is ordinary heap memory) and at most kKeep
+    // of them stay pooled between decodes (64 MiB; the rest are freed when returned)
     struct PinnedPages {
+        static const size_t kLive = 4096, kKeep = 1024;
         std::mutex m;
         std::vector<uint8_t*> free;
-        uint8_t* get() {
+        size_t live = 0;
+        uint8_t* get(bool& pinned) {
             {
                 std::lock_guard<std::mutex> lk(m);
-                if (!free.empty()) { uint8_t* p = free.back(); free.pop_back(); return p; }
+                if (!free.empty()) { uint8_t* p = free.back(); free.pop_back(); pinned = true; return p; }
+                if (live >= kLive) { pinned = false; return (uint8_t*)malloc(PG); }
+                ++live;
             }
             void* p = nullptr;
-            if (hipHostMalloc(&p, PG, hipHostMallocDefault) != hipSuccess) return nullptr;
+            if (hipHostMalloc(&p, PG, hipHostMallocDefault) != hipSuccess) {
+                std::lock_guard<std::mutex> lk(m);
+                --live;
+                pinned = false;
+                return (uint8_t*)malloc(PG);
+            }
+            pinned = true;
             return (uint8_t*)p;
         }
-        void put(uint8_t* p) { std::lock_guard<std::mutex> lk(m); free.push_back(p); }
+        void put(uint8_t* p) {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                if (free.size() < kKeep) { free.push_back(p); return; }
+                --live;
+            }
+            (void)hipHostFree(p);
+        }
     };
     static PinnedPages& pinned() { static PinnedPages* pp = new PinnedPages(); return *pp; }   // (never destroyed)
-    struct PageDel { void operator()(uint8_t* p) const { if (p) pinned().put(p); } };
+    struct PageDel {
+        bool pin = true;
+        void operator()(uint8_t* p) const { if (!p) return; if (pin) pinned().put(p); else ::free(p); }
+    };
     std::unordered_map<size_t, std::unique_ptr<uint8_t, PageDel>> pages;
     size_t last_pg = ~(size_t)0;             // fast path: the page of the previous access
     const uint8_t* last = nullptr;
@@ -830,9 +852,10 @@ struct ByteSrc {
         if (it == pages.end()) {
             const auto t0 = std::chrono::steady_clock::now();
             size_t o = pg * PG, n = std::min(PG, len - o);
-            uint8_t* v = pinned().get();
-            if (!v) throw GkError("out of pinned host memory for codestream pages");
-            std::unique_ptr<uint8_t, PageDel> hold(v);
+            bool pin = true;
+            uint8_t* v = pinned().get(pin);
+            if (!v) throw GkError("out of host memory for codestream pages");
+            std::unique_ptr<uint8_t, PageDel> hold(v, PageDel{pin});
             HIPCHK(hipMemcpyAsync(v, dev + o, n, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
             it = pages.emplace(pg, std::move(hold)).first;

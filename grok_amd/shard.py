@@ -514,7 +514,7 @@ class TileRowShard:
         if self.rank == 0:
             try:
                 subs = self.substreams(cs, n)
-            except (ValueError, struct.error) as e:
+            except Exception as e:   # any failure: every rank raises in the scatter, none waits
                 err = e
         sub, m = _scatter_tensors(self.dist, self.rank, self.world, subs, self.device, err)
         if self.y1 > self.y0:
@@ -554,7 +554,7 @@ class WindowShard:
                     pos += L
                 meta[:7] = torch.tensor([siz[k] for k in ("tw", "th", "w", "x0", "y0", "tx0", "ty0")])
                 meta[7] = 1
-            except (ValueError, struct.error) as e:   # every rank raises below, none waits
+            except Exception as e:   # every rank raises below, none waits
                 err = e
         if world > 1:
             dist.broadcast(meta, 0)
@@ -577,6 +577,25 @@ class WindowShard:
             out.append((max(y0, edge(a)), min(y1, edge(b))) if b > a else (y0, y0))
         return out
 
+    def _band_streams(self, win, bands):
+        """Rank 0: each band's sub-stream (main header with a TLM of its tile parts, the parts, EOC)."""
+        x0, y0, x1, y1 = win
+        # canvas tile grid (B.3): ntx columns from TX0 to the image's right edge X0 + W
+        ntx = (self.X0 + self.W - self.TX0 + self.tw - 1) // self.tw
+        cx, cy = self.X0 - self.TX0, self.Y0 - self.TY0   # image -> grid coordinates
+        i0, i1 = (x0 + cx) // self.tw, (x1 - 1 + cx) // self.tw + 1
+        subs = []
+        for a, b in bands:
+            if b <= a:
+                subs.append(self.file[:0])
+                continue
+            tiles = [j * ntx + i for j in range((a + cy) // self.th, (b - 1 + cy) // self.th + 1)
+                     for i in range(i0, i1)]
+            mine = [(t, p, L) for t in tiles for p, L in self.where.get(t, [])]
+            subs.append(torch_cat([_tensor(retlm(self.hdr, [(t, L) for t, _, L in mine]), self.device)] +
+                                  [self.file[p:p + L] for _, p, L in mine] + [self.eoc]))
+        return subs
+
     def decode(self, win, out, band_buf=None):
         """out: rank 0's (C, y1-y0, x1-x0) window; band_buf: a (C, >= tallest band, x1-x0) buffer
         on the other ranks (rank 0 decodes its band straight into out)."""
@@ -585,23 +604,13 @@ class WindowShard:
             self.coder.decode_window(self.file, self.n, win, out)
             return
         bands = self.bands(win)
-        subs = None
+        subs, err = None, None
         if self.rank == 0:
-            # canvas tile grid (B.3): ntx columns from TX0 to the image's right edge X0 + W
-            ntx = (self.X0 + self.W - self.TX0 + self.tw - 1) // self.tw
-            cx, cy = self.X0 - self.TX0, self.Y0 - self.TY0   # image -> grid coordinates
-            i0, i1 = (x0 + cx) // self.tw, (x1 - 1 + cx) // self.tw + 1
-            subs = []
-            for a, b in bands:
-                if b <= a:
-                    subs.append(self.file[:0])
-                    continue
-                tiles = [j * ntx + i for j in range((a + cy) // self.th, (b - 1 + cy) // self.th + 1)
-                         for i in range(i0, i1)]
-                mine = [(t, p, L) for t in tiles for p, L in self.where.get(t, [])]
-                subs.append(torch_cat([_tensor(retlm(self.hdr, [(t, L) for t, _, L in mine]), self.device)] +
-                                      [self.file[p:p + L] for _, p, L in mine] + [self.eoc]))
-        sub, m = _scatter_tensors(self.dist, self.rank, self.world, subs, self.device)
+            try:
+                subs = self._band_streams(win, bands)
+            except Exception as e:   # (e.g. retlm: more than 256 TLM entries) every rank raises
+                err = e
+        sub, m = _scatter_tensors(self.dist, self.rank, self.world, subs, self.device, err)
         a, b = bands[self.rank]
         dst = out[:, a - y0:b - y0] if self.rank == 0 else band_buf[:, :b - a]
         if b > a:

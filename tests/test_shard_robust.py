@@ -173,3 +173,44 @@ def test_retlm_splits_over_markers():
         i += 2 + L
     assert zs == [0, 1, 2] and seen == entries
     assert shard.parse_main_header(h + b"\xff\x90\x00\x0a")[2] == entries
+
+
+def _w_window_errors(rank, world, port, q):
+    # rank 0 failing while it cuts a window's band sub-streams (any exception type: an IndexError
+    # from a bad TLM offset here) reaches every rank through the scatter
+    dist = _init(rank, world, port)
+    try:
+        from test_bench_shard import OracleCoder
+        rng = np.random.default_rng(8)
+        C, H, W = 1, 128, 128
+        img = rng.integers(0, 256, size=(C, H, W)).astype(np.int32)
+        kw = dict(tiles=(32, 32), tlm=True)
+        cs = O.encode(img, 8, **kw)
+        dev = torch.device("cpu")
+        src = torch.frombuffer(bytearray(cs), dtype=torch.uint8) if rank == 0 else None
+        ws = shard.WindowShard(dist, rank, world, OracleCoder((C, H, W), 8, kw), dev, file=src,
+                               n=len(cs) if rank == 0 else 0)
+        if rank == 0:
+            def bad(win, bands):
+                raise IndexError("tile part offset past the file")
+            ws._band_streams = bad
+        out = torch.zeros((C, H, W), dtype=torch.uint8) if rank == 0 else None
+        band = torch.zeros((C, H, W), dtype=torch.uint8)
+        got = None
+        try:
+            ws.decode((0, 0, W, H), out, band)
+        except (IndexError, RuntimeError) as e:
+            got = type(e).__name__
+        # the group is still usable afterwards: a clean window decodes
+        if rank == 0:
+            del ws._band_streams
+        ws.decode((0, 0, W, H), out, band)
+        ok = bool((out.numpy().astype(np.int32) == img).all()) if rank == 0 else True
+        q.put((rank, got, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_window_band_errors_reach_every_rank():
+    res = sorted(_run(_w_window_errors, (), nres=2))
+    assert res == [(0, "IndexError", True), (1, "RuntimeError", True)]
