@@ -1,18 +1,19 @@
 """Benchmark: Mpixels/s encode+decode, JPEG 2000 tile pipeline on MI355X.
 
-Headline workload (BASELINE.json configs[1], "C2"): 8192x8192 8-bit RGB, 5/3
-reversible lossless + RCT, 64x64 code-blocks, 6 resolutions, single tile, one
-quality layer — Grok's default coding parameters.  Synthetic input from the
-survey's seeded generator (grok_amd/synth.py, seed 10 + rank).
-
-One step = encode (image resident in HBM -> codestream resident in HBM) +
-decode (codestream in HBM -> image in HBM); host T2 (packet headers, rate
-allocation) runs inside the step.  value = pixels of all ranks / max-over-ranks
-wall time.  Single-tile configs run as replicas (one image per GPU, no
-collective on the data path): scaling = "weak".
+Headline workload = BASELINE.json's metric as named, "8K RGB 5/3 lossless + 9/7 lossy": one
+step encodes and decodes one image of each of
+  C2  configs[1]: 8192x8192 8-bit RGB, 5/3 reversible lossless + RCT, 64x64 code-blocks,
+      6 resolutions, single tile, one quality layer (Grok's default coding parameters), and
+  C3  configs[2]: 8192x8192 12-bit RGB, 9/7 irreversible + ICT, 3 quality layers -r 40,20,10
+      (PCRD rate control),
+synthetic input from the survey's seeded generator (grok_amd/synth.py, seeds 10 / 11 + rank).
+Encode = image resident in HBM -> codestream resident in HBM; decode = codestream in HBM ->
+image in HBM; host T2 (packet headers, rate allocation) runs inside the step.  value = pixels
+of all ranks (2 x 8192^2 per rank per step) / max-over-ranks wall time.  Single-tile configs run
+as replicas (one C2 + C3 pair per GPU, no collective on the data path): scaling = "weak".  The
+line also carries C2 and C3 timed alone (`per_config`).
 
 The same JSON line carries auxiliary measurements:
-  C3  configs[2]: 8192^2 12-bit RGB, 9/7 + ICT, 3 quality layers -r 40,20,10;
   C4  configs[3]: 16384^2 16-bit mono, HTJ2K, 1024^2 tiles, TLM + PLT — with N > 1
       ranks tile rows are sharded (strong scaling): each rank codes its tile rows,
       rank 0 gathers the tile parts over RCCL, each rank decodes its own parts;
@@ -73,7 +74,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size", type=int, default=0, help="override the config's image side")
-    ap.add_argument("--config", default="C2", choices=["C2", "C3", "C4"])
+    ap.add_argument("--config", default="C2+C3", choices=["C2+C3", "C2", "C3", "C4"],
+                    help="C2+C3: the headline metric (one 5/3 and one 9/7 image per step)")
     ap.add_argument("--no-aux", action="store_true", help="skip the auxiliary C3/C4/C5/batch measurements")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 window-decode measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -103,9 +105,17 @@ def launch(args):
 
 
 def host_threads(args):
+    """Threads of the N-thread CPU baseline: the host CPU share this process may use.  The GPU
+    box gives one GPU's job a 16-CPU share (it exports OMP_NUM_THREADS=16) while os.cpu_count()
+    reports the whole machine, so the share, not os.cpu_count(), is what the baseline can use."""
     if args.cpu_threads:
         return args.cpu_threads
-    return max(1, min(int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count() or 1, 16))
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0) or aff
+    return max(1, min(share, aff, os.cpu_count() or 1))
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -139,10 +149,17 @@ def cpu_baseline(nthreads):
                 assert (dec == img).all()
             per[name]["%dt" % th] = round(h * w / 1e6 / float(np.median(runs)), 4)
     O.set_threads(1)
-    return {"value": per["C2"]["%dt" % nthreads], "unit": "Mpixels/s", "cores": nthreads, "cores_list": sorted({1, nthreads}),
+    # the headline's unit of work: one C2 pixel and one C3 pixel (harmonic mean of the two rates)
+    comb = lambda t: round(2.0 / (1.0 / per["C2"][t] + 1.0 / per["C3"][t]), 4)
+    return {"value": comb("%dt" % nthreads), "unit": "Mpixels/s", "cores": nthreads,
+            "cores_list": sorted({1, nthreads}), "value_1t": comb("1t"),
+            "host_cpu_count": os.cpu_count(),
+            "cores_note": "threads = the CPU share of this GPU's job (OMP_NUM_THREADS / affinity); os.cpu_count() "
+                          "reports the whole host, which the box shares between GPUs",
             "kind": "port",
             "sample": "oracle/j2k_oracle.cpp encode+decode, median of 3, on crops: C2 2048^2, C3 1024^2, C4 2048^2; "
-                      "value = C2 crop at %d threads" % nthreads,
+                      "value = C2 + C3 crops combined as the headline (one 5/3 and one 9/7 pixel per unit) at %d "
+                      "threads" % nthreads,
             "per_config": per,
             "grok_container_8vcpu": {"note": "BASELINE.md section 2, Grok 9.2.0 CLI on the survey container (8 vCPU), "
                                              "enc+dec Mpix/s; C2p/C3p = -c [256,256] variants (Grok cannot decode the "
@@ -426,6 +443,62 @@ class C5Runner:
             self.eng.close()
 
 
+class PairRunner:
+    """The headline step: one C2 image (5/3 lossless) and one C3 image (9/7 lossy) encoded and
+    decoded, one after the other on one engine each.  Stage timings are reported per config
+    (keys prefixed "C2_" / "C3_")."""
+
+    def __init__(self, r2, r3):
+        self.rs = (("C2", r2), ("C3", r3))
+        self.pixels = r2.pixels + r3.pixels
+        self.n = r2.n
+        self.name = "C2+C3"
+
+    def step(self):
+        acc = {}
+        for name, r in self.rs:
+            te, td = r.step()
+            for pre, t in (("enc", te), ("dec", td)):
+                for f, _ in t._fields_:
+                    acc["%s_%s_%s" % (name, pre, f)] = float(getattr(t, f))
+        self.n = self.rs[0][1].n + self.rs[1][1].n
+        return acc
+
+    def check(self):
+        self.rs[0][1].check()
+        psnr = self.rs[1][1].check()
+        self.n = self.rs[0][1].n + self.rs[1][1].n
+        return psnr
+
+    def close(self):
+        for _, r in self.rs:
+            r.close()
+
+
+def stage_rooflines(name, m, cfg, size=0):
+    """HBM roofline candidates of one config's timed stages (per step averages of the engine's
+    HIP-event timings m): T1 decode (compressed bytes + 4 B/sample), T1 encode (4 B/sample +
+    compressed bytes), DWT (the engine's per-level algorithmic bytes)."""
+    cp = cfg["params"]
+    samples = cfg["comps"] * (size or cfg["size"]) ** 2
+    if cp.get("cblk_sty"):   # HTJ2K: one cleanup-pass coder kernel each way
+        dec_k, enc_k = ("T1 decode (k_ht_dec)", ["k_ht_dec"]), ("T1 encode (k_ht_enc)", ["k_ht_enc"])
+    else:
+        dec_k = ("T1 decode (k_t1_dec2 + k_t1_recon)", ["void k_t1_dec2<0, 4>", "k_t1_recon"])
+        cm = "void k_t1_cm<true>" if cp.get("irreversible") else "void k_t1_cm<false>"
+        enc_k = ("T1 encode (k_t1_cm + k_t1_mq)", [cm, "k_t1_mq"])
+    dw = "97" if cp.get("irreversible") else "53"
+    return [
+        {"config": name, "stage": "%s %s" % (name, dec_k[0]), "avg_ms": m["dec_t1_ms"],
+         "bytes_per_launch": m["dec_t1_bytes"] + 4.0 * samples, "kernels": dec_k[1]},
+        {"config": name, "stage": "%s %s" % (name, enc_k[0]), "avg_ms": m["enc_t1_ms"],
+         "bytes_per_launch": 4.0 * samples + m["enc_t1_bytes"], "kernels": enc_k[1]},
+        {"config": name, "stage": "%s DWT %s fwd+inv (all levels)" % (name, "9/7" if dw == "97" else "5/3"),
+         "avg_ms": m["enc_dwt_ms"] + m["dec_dwt_ms"], "bytes_per_launch": m["enc_dwt_bytes"] + m["dec_dwt_bytes"],
+         "kernels": ["k_dwt%s_fwd_level" % dw, "k_dwt%s_inv_level" % dw]},
+    ]
+
+
 def timed(r, steps, warmup, world, dist, device, sync=True):
     import torch
     for _ in range(warmup):
@@ -501,45 +574,56 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
 
-    r = Runner(args.config, args.size, rank, device) if args.config != "C4" or world == 1 else \
-        ShardRunner("C4", args.size, rank, world, device, dist)
-    S = r.size
-    r.check()
+    if args.config == "C2+C3":
+        r2 = Runner("C2", args.size, rank, device)
+        r3 = Runner("C3", args.size, rank, device)
+        r = PairRunner(r2, r3)
+    elif args.config != "C4" or world == 1:
+        r = Runner(args.config, args.size, rank, device)
+    else:
+        r = ShardRunner("C4", args.size, rank, world, device, dist)
+    psnr = r.check()
     el, m = timed(r, args.steps, args.warmup, world, dist, device)
     ms = el * 1000.0 / args.steps
-    samples = S * S * r.cfg["comps"]
-    per_rank = world if isinstance(r, Runner) else 1   # replicas: every rank codes its own image
-    value = S * S / 1e6 * per_rank * args.steps / el
+    per_rank = world if not isinstance(r, ShardRunner) else 1   # replicas: every rank codes its own images
+    value = r.pixels / 1e6 * per_rank * args.steps / el
+    r_pixels = int(r.pixels)
+    per_config = None
+    if isinstance(r, PairRunner):
+        # each config of the pair timed alone as well (same engines, same images)
+        per_config = {}
+        for name, rr in (("C2", r2), ("C3", r3)):
+            elx, _ = timed(rr, args.steps, 1, world, dist, device)
+            per_config[name] = {"config": "%s: %s" % (name, CONFIGS[name]["desc"]),
+                                "value": round(rr.pixels / 1e6 * world * args.steps / elx, 3), "unit": "Mpixels/s",
+                                "ms_per_step": round(elx * 1000.0 / args.steps, 3),
+                                "codestream_bytes": int(rr.n),
+                                "stages_ms": {k[3:]: round(v, 3) for k, v in m.items()
+                                              if k.startswith(name + "_") and k.endswith("_ms") and v > 0}}
+        per_config["C3"]["psnr_db"] = round(psnr, 3)
+        per_config["C3"]["psnr_note"] = "decode vs source, 12-bit peak (tolerance check: >= 30 dB in bench)"
     codestream_bytes = int(r.n)
     # the T1 decoder's chain length: one more (untimed) decode with the step counters on
     dec_steps = None
-    if isinstance(r, Runner) and not r.cfg["params"].get("cblk_sty"):
+    rs = r2 if isinstance(r, PairRunner) else r
+    if isinstance(rs, Runner) and not rs.cfg["params"].get("cblk_sty"):
         os.environ["GK_T1_STATS"] = "1"
         try:
-            r.eng.decode(r.out, length=r.n, out=r.y)
-            t = r.eng.timings()
+            rs.eng.decode(rs.out, length=rs.n, out=rs.y)
+            t = rs.eng.timings()
             dec_steps = (int(t.t1_steps_max), int(t.t1_steps_total), int(t.t1_symbols), int(t.t1_solo_blocks),
                          int(t.t1_solo_decisions), int(t.t1_solo_decisions_max))
         finally:
             del os.environ["GK_T1_STATS"]
     r.close()
-    del r
+    del r, rs
+    if args.config == "C2+C3":
+        del r2, r3
     torch.cuda.empty_cache()
 
     aux = None
-    if not args.no_aux and args.config == "C2":
+    if not args.no_aux and args.config == "C2+C3":
         aux = {}
-        r3 = Runner("C3", args.size, rank, device)
-        psnr = r3.check()
-        el3, m3 = timed(r3, 2, 1, world, dist, device)
-        S3 = r3.size
-        aux["C3"] = {"config": "C3: " + CONFIGS["C3"]["desc"], "value": round(S3 * S3 / 1e6 * world * 2 / el3, 3),
-                     "unit": "Mpixels/s", "ms_per_step": round(el3 * 500.0, 3), "psnr_db": round(psnr, 3),
-                     "codestream_bytes": int(r3.n), "parallelism": "replicas x%d" % world,
-                     "stages_ms": {k: round(v, 3) for k, v in m3.items() if k.endswith("_ms") and v > 0}}
-        r3.close()
-        del r3
-        torch.cuda.empty_cache()
         # C2 with two images in flight per GPU (throughput of overlapped independent jobs)
         rb = BatchRunner("C2", 2, rank, device)
         rb.check()
@@ -606,58 +690,72 @@ def main():
             torch.cuda.empty_cache()
 
     if rank == 0:
-        # dominant kernel: the T1 stage with the largest average duration, measured with HIP
-        # events on the engine stream (encode: k_t1_cm + k_t1_mq, decode: k_t1_dec2 + k_t1_recon)
-        cp = CONFIGS[args.config]["params"]
-        if cp.get("cblk_sty"):   # HTJ2K: one cleanup-pass coder kernel each way
-            dec_k, enc_k = ("T1 decode (k_ht_dec)", ["k_ht_dec"]), ("T1 encode (k_ht_enc)", ["k_ht_enc"])
-        else:
-            dec_k = ("T1 decode (k_t1_dec2 + k_t1_recon)", ["void k_t1_dec2<0, 4>", "k_t1_recon"])
-            cm = "void k_t1_cm<true>" if cp.get("irreversible") else "void k_t1_cm<false>"
-            enc_k = ("T1 encode (k_t1_cm + k_t1_mq)", [cm, "k_t1_mq"])
-        dw = "97" if cp.get("irreversible") else "53"
-        stages = {
-            dec_k[0]: (m["dec_t1_ms"], m["dec_t1_bytes"] + 4.0 * samples, dec_k[1]),
-            enc_k[0]: (m["enc_t1_ms"], 4.0 * samples + m["enc_t1_bytes"], enc_k[1]),
-            "DWT %s fwd+inv (all levels)" % ("9/7" if dw == "97" else "5/3"):
-                (m["enc_dwt_ms"] + m["dec_dwt_ms"], m["enc_dwt_bytes"] + m["dec_dwt_bytes"],
-                 ["k_dwt%s_fwd_level" % dw, "k_dwt%s_inv_level" % dw]),
-        }
-        dom = max(stages, key=lambda k: stages[k][0])
-        t_ms, nbytes, kern = stages[dom]
-        achieved = nbytes / 1e9 / (t_ms / 1e3)
-        traffic, traffic_src = pmc_traffic(kern, args.config)
-        dwt_gbs = (m["enc_dwt_bytes"] + m["dec_dwt_bytes"]) / 1e9 / ((m["enc_dwt_ms"] + m["dec_dwt_ms"]) / 1e3)
+        # dominant kernel: the T1 / DWT stage with the largest average duration per step, measured
+        # with HIP events on the engine stream, over the configs of the step
+        names = ["C2", "C3"] if args.config == "C2+C3" else [args.config]
+        cands = []
+        for name in names:
+            mm = {k[3:]: v for k, v in m.items() if k.startswith(name + "_")} if len(names) > 1 else m
+            cands += stage_rooflines(name, mm, CONFIGS[name], args.size)
+        dom = max(cands, key=lambda c: c["avg_ms"])
+        achieved = dom["bytes_per_launch"] / 1e9 / (dom["avg_ms"] / 1e3)
+        traffic, traffic_src = pmc_traffic(dom["kernels"], dom["config"])
+        dwt = {}
+        for name in names:
+            mm = {k[3:]: v for k, v in m.items() if k.startswith(name + "_")} if len(names) > 1 else m
+            smp = CONFIGS[name]["comps"] * (args.size or CONFIGS[name]["size"]) ** 2
+            gbs = (mm["enc_dwt_bytes"] + mm["dec_dwt_bytes"]) / 1e9 / ((mm["enc_dwt_ms"] + mm["dec_dwt_ms"]) / 1e3)
+            dwt[name] = {"stage": "DC shift + MCT + DWT (%s), encode and decode (level 1 fused with the sample stage, "
+                                  "all levels)" % ("9/7 + ICT" if CONFIGS[name]["params"].get("irreversible") else
+                                                   "5/3 + RCT"),
+                         "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "ms": round(mm["enc_dwt_ms"] + mm["dec_dwt_ms"], 3),
+                         "bytes_per_sample": round((mm["enc_dwt_bytes"] + mm["dec_dwt_bytes"]) / (2.0 * smp), 3)}
+        grok_ref = GROK_CPU["C2p_8t"] if args.config == "C2" else (
+            2.0 / (1.0 / GROK_CPU["C2p_8t"] + 1.0 / GROK_CPU["C3p_8t"]) if args.config == "C2+C3" else None)
         res = {
             "metric": METRIC,
             "value": round(value, 3), "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
             "scaling": "weak" if args.config != "C4" else "strong",
-            "vs_baseline": round(value / GROK_CPU["C2p_8t"], 2) if args.config == "C2" else None,
-            "vs_baseline_ref": "Grok 9.2.0 CPU enc+dec of C2' (-c [256,256]) on 8 vCPU, 5.99 Mpix/s (BASELINE.md "
-                               "section 2; no published GPU number exists)",
-            "dtype": "int32",
-            "data": "synthetic (seeded survey generator grok_amd/synth.py, seed %d+rank)" % CONFIGS[args.config]["seed"],
-            "config": {"workload": "%s: %s; encode+decode, image and codestream resident in HBM" % (
-                args.config, CONFIGS[args.config]["desc"]),
-                "parallelism": "replicas x%d (one image per GPU)" % world if args.config != "C4" or world == 1 else
-                "C4 tile rows sharded over %d ranks" % world,
-                "codestream_bytes": codestream_bytes},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            # the reference publishes no number for this metric
+            "vs_baseline": None,
+            "dtype": "int32 (5/3) + f32 (9/7)" if args.config == "C2+C3" else
+                     ("f32" if CONFIGS[args.config]["params"].get("irreversible") else "int32"),
+            "data": "synthetic (seeded survey generator grok_amd/synth.py, seeds %s + rank)" % (
+                "10 (C2) / 11 (C3)" if args.config == "C2+C3" else str(CONFIGS[args.config]["seed"])),
+            "config": {"workload": ("C2+C3: one 8192x8192 8-bit RGB 5/3 lossless image (C2: %s) and one 8192x8192 "
+                                    "12-bit RGB 9/7 lossy image (C3: %s) encoded + decoded per step, images and "
+                                    "codestreams resident in HBM" % (CONFIGS["C2"]["desc"], CONFIGS["C3"]["desc"]))
+                                   if args.config == "C2+C3" else
+                                   "%s: %s; encode+decode, image and codestream resident in HBM" % (
+                                       args.config, CONFIGS[args.config]["desc"]),
+                       "parallelism": "replicas x%d (one image per GPU)" % world if args.config != "C4" or world == 1
+                       else "C4 tile rows sharded over %d ranks" % world,
+                       "pixels_per_step_per_rank": r_pixels,
+                       "codestream_bytes": codestream_bytes},
+            "roofline": {"bound": "hbm", "kernel": dom["stage"], "config": dom["config"], "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": None if traffic is None else round(traffic), "traffic_source": traffic_src,
-                         "bytes_per_launch": round(nbytes), "avg_ms": round(t_ms, 3),
+                         "bytes_per_launch": round(dom["bytes_per_launch"]), "avg_ms": round(dom["avg_ms"], 3),
                          "note": "T1 is a serial MQ chain per code-block; bytes = compressed bytes + 4 B/sample"},
-            "dwt_roofline": {"stage": "DC shift + MCT + DWT, encode and decode (level 1 fused with the sample "
-                                      "stage, all levels)",
-                             "achieved": round(dwt_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(dwt_gbs / HBM_PEAK_GBS, 4),
-                             "bytes_per_sample": round((m["enc_dwt_bytes"] + m["dec_dwt_bytes"]) / (2.0 * samples), 3)},
+            "dwt_roofline": dwt[names[0]] if len(names) == 1 else dwt,
             "stages_ms": {k: round(v, 3) for k, v in m.items() if k.endswith("_ms") and v > 0},
-            "t1": {"blocks": int(m["enc_t1_blocks"]),
-                   "enc_blocks_per_s": round(m["enc_t1_blocks"] / (m["enc_t1_ms"] / 1e3)),
-                   "dec_blocks_per_s": round(m["dec_t1_blocks"] / (m["dec_t1_ms"] / 1e3))},
         }
+        if per_config:
+            res["per_config"] = per_config
+        if grok_ref:
+            res["vs_grok_cpu_container"] = {"ratio": round(value / grok_ref, 1), "grok_mpix_s": round(grok_ref, 3),
+                                            "ref": "Grok 9.2.0 CPU enc+dec on the survey container (8 vCPU), BASELINE.md "
+                                                   "section 2 (C2' / C3' -c [256,256] variants: Grok cannot decode its "
+                                                   "single-precinct 8K streams); not a published number"}
+        t1m = {k[3:]: v for k, v in m.items() if k.startswith("C2_")} if args.config == "C2+C3" else m
+        if "enc_t1_blocks" in t1m:
+            res["t1"] = {"blocks": int(t1m["enc_t1_blocks"]),
+                         "enc_blocks_per_s": round(t1m["enc_t1_blocks"] / (t1m["enc_t1_ms"] / 1e3)),
+                         "dec_blocks_per_s": round(t1m["dec_t1_blocks"] / (t1m["dec_t1_ms"] / 1e3))}
+        cp = CONFIGS[args.config]["params"] if args.config in CONFIGS else {}
         if cp.get("cblk_sty"):   # HTJ2K coders: issue roofline from the committed SQ counter summary
             res["issue_roofline"] = ht_issue_roofline(m, args.config)
         if dec_steps and dec_steps[0]:
@@ -671,9 +769,9 @@ def main():
             _, dec_ips, dec_by = isa_step_count.count_so(G.LIB_PATH)
             dec_ips = int(dec_ips)
             floor_ms = dec_steps[0] * dec_ips * 4 / (CLOCK_GHZ * 1e6)
-            dec2_ms = m.get("dec_t1_coder_ms", m["dec_t1_ms"])
+            dec2_ms = t1m.get("dec_t1_coder_ms", t1m["dec_t1_ms"])
             res["issue_roofline"] = {
-                "kernel": "k_t1_dec2 (T1 decode chain)", "bound": "instruction issue of the longest wave",
+                "kernel": "k_t1_dec2 (T1 decode chain, C2)", "bound": "instruction issue of the longest wave",
                 "max_steps_per_wave": dec_steps[0], "instructions_per_step": dec_ips,
                 "instructions_per_step_source": "llvm-objdump of %s (k_t1_dec2<0, 4> step bodies: %s)" % (
                     os.path.relpath(G.LIB_PATH, ROOT), ", ".join("%s %d" % kv for kv in dec_by.items())),
