@@ -65,11 +65,19 @@ static void launch_check(int line) {
 // only stretch the tail (C2 with two images in flight: 2,555 -> 2,394 Mpix/s with them).
 static std::mutex g_dev_mu;
 static std::map<int, int> g_dev_engines;
-static int engines_on(int dev) {
+// Engines of a device inside an encode / decode call right now (every call returns after its
+// stream has drained): a second one means another image's kernels share the chip with this one
+static std::map<int, int> g_dev_busy;
+static int engines_busy(int dev) {
     std::lock_guard<std::mutex> g(g_dev_mu);
-    auto it = g_dev_engines.find(dev);
-    return it == g_dev_engines.end() ? 0 : it->second;
+    auto it = g_dev_busy.find(dev);
+    return it == g_dev_busy.end() ? 0 : it->second;
 }
+struct DevBusy {
+    int dev;
+    explicit DevBusy(int d) : dev(d) { std::lock_guard<std::mutex> g(g_dev_mu); ++g_dev_busy[dev]; }
+    ~DevBusy() { std::lock_guard<std::mutex> g(g_dev_mu); if (--g_dev_busy[dev] <= 0) g_dev_busy.erase(dev); }
+};
 
 
 // Persistent host worker pool for the T2 stages (tiles, precinct chains, blocks).
@@ -4313,11 +4321,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // waves (LPT) and K is the crossing point of the two (binary search: the first falls,
         // the second grows with K).  GK_T1DEC_SOLO=n: the n heaviest, one per wave.
         GkSoloPlan sp = nbr ? gk_t1dec_solo_plan(nbr, L) : GkSoloPlan{0, -1, 1.f};
-        // Device shared with other engines (e.g. two images in flight): no SIMD is idle, so a solo
+        // Device shared with another engine's call in progress (e.g. two images in flight; engines
+        // that merely exist, like the bench's C2 + C3 pair run one after the other, do not count):
+        // no SIMD is idle, so a solo
         // wave's time is taken from the other decodes; only clear outliers (> 1.3 x the weight of
         // the block at rank 1,024) go solo, one per wave.  C2 (LL blocks 1.06 x the plateau): none,
         // 2,394 -> 2,548 Mpix/s with two images in flight; C3 (LL ~1.6 x): kept (1,761 -> 2,056).
-        const bool shared = sp.forced < 0 && engines_on(ctx->device) > 1;
+        const bool shared = sp.forced < 0 && engines_busy(ctx->device) > 1;
         uint32_t nsb = 0;
         std::vector<uint32_t> byl;
         std::vector<std::vector<uint32_t>> bins;
@@ -4679,6 +4689,7 @@ int gk_encode(gk_ctx* ctx, const gk_image_info* info, const void* const* comps, 
     if (!ctx || !info || !comps || !strides || !out) return -1;
     try {
         (void)hipSetDevice(ctx->device);
+        DevBusy busy(ctx->device);
         int rc = 0;
         size_t n = encode_impl(ctx, info, comps, strides, comps_on_device, p, out, cap, out_on_device, &rc);
         if (out_len) *out_len = n;
@@ -4696,6 +4707,7 @@ int gk_encode_tiles(gk_ctx* ctx, const gk_image_info* info, const void* const* c
     if (!ctx || !info || !comps || !strides || !out || !part_lens || tile_end <= tile_begin) return -1;
     try {
         (void)hipSetDevice(ctx->device);
+        DevBusy busy(ctx->device);
         int rc = 0;
         size_t n = encode_impl(ctx, info, comps, strides, comps_on_device, p, out, cap, out_on_device, &rc,
                                tile_begin, tile_end, false, part_lens);
@@ -4714,6 +4726,7 @@ int gk_encode_blocks(gk_ctx* ctx, const gk_image_info* info, const void* const* 
     if (!ctx || !info || !comps || !strides) return -1;
     try {
         (void)hipSetDevice(ctx->device);
+        DevBusy busy(ctx->device);
         if (p && p->tile_size_on && (p->t_width < info->w || p->t_height < info->h))
             throw GkError("code-block results are produced for single-tile images only (Grok's plugin tile is one tile)");
         int rc = 0;
@@ -4850,6 +4863,7 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void
     if (!ctx || !cs || !comps || !strides) return -1;
     try {
         (void)hipSetDevice(ctx->device);
+        DevBusy busy(ctx->device);
         decode_impl(ctx, cs, len, cs_on_device, comps, strides, sample_bytes, out_on_device);
         return 0;
     } catch (const GkError& e) {
@@ -4882,6 +4896,7 @@ int gk_decode_window(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
     if (!ctx || !cs || !comps || !strides) return -1;
     try {
         (void)hipSetDevice(ctx->device);
+        DevBusy busy(ctx->device);
         const uint32_t win[4] = {x0, y0, x1, y1};
         decode_impl(ctx, cs, len, cs_on_device, comps, strides, sample_bytes, out_on_device, win);
         return 0;
