@@ -539,7 +539,9 @@ static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
                         G.orient = (uint8_t)B.orient; G.comp = (uint8_t)c;
                         G.band_numbps = (uint8_t)B.numbps;
                         // bits 3..7: the component's ROI shift (RGN; RoiShiftFilter on decode)
-                        G.flags = (P.p.irrev ? 1 : 0) | (P.p.rate_control() ? 2 : 0) | (uint8_t)(P.p.roi(c) << 3);
+                        // (bit 1, rate control: set when an encode uploads the table, so one plan
+                        // serves the encode and the decode of a rate-controlled stream)
+                        G.flags = (P.p.irrev ? 1 : 0) | (uint8_t)(P.p.roi(c) << 3);
                         G.step = B.step_enc;
                         // T1::getwmsedec weight w1 * w2 * stepsize (T1.cpp:418-436): w1 = MCT basis norm
                         // (mct.cpp:689-704) when the MCT is on, w2 = DWT band norm (T1.cpp:264-277)
@@ -2424,6 +2426,7 @@ struct gk_ctx {
     hipEvent_t ev[32];
     bool blocks_uploaded = false;
     uint32_t enc_b0 = 0, enc_b1 = 0;   // block range of the uploaded encode table
+    bool enc_rc = false;                // its rate-control flag (GkBlock::flags bit 1)
     // band quantisation held by the cached plan's bands: the plan's own (encoder, native_qcd)
     // or that of the last decoded stream (band_qcd)
     std::vector<std::pair<uint32_t, uint32_t>> native_qcd, band_qcd;
@@ -2527,8 +2530,8 @@ static void check_poc_coverage(const Params& P, uint32_t nc) {
 
 static std::string plan_key(const Plan& P) {
     char buf[256];
-    snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
-             P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0, P.p.rate_control() ? 1 : 0);
+    snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
+             P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0);
     std::string k(buf);
     k += " sty" + std::to_string(P.p.cblk_sty) + " t" + std::to_string(P.p.tw) + "x" + std::to_string(P.p.th);
     k += " o" + std::to_string(P.x0) + "," + std::to_string(P.y0) + "," + std::to_string(P.gx0) + "," + std::to_string(P.gy0);
@@ -2880,7 +2883,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     uint32_t* dpe = (uint32_t*)ctx->dpassend.get(4 * GK_MAX_PASSES * (size_t)nbx);
     uint32_t* dcm = (uint32_t*)ctx->dcminfo.get(8 * (size_t)nbx);
     int32_t* dnmse = do_rc ? (int32_t*)ctx->dnmse.get(4 * GK_MAX_PASSES * (size_t)nbx) : nullptr;
-    if (!ctx->blocks_uploaded || ctx->enc_b0 != b0 || ctx->enc_b1 != b1) {
+    if (!ctx->blocks_uploaded || ctx->enc_b0 != b0 || ctx->enc_b1 != b1 || ctx->enc_rc != do_rc) {
         // the range's blocks with offsets into this call's planes and slots
         GkBlock* hb = (GkBlock*)ctx->hpasses.get(sizeof(GkBlock) * nbx + 8 * ((size_t)nbr + 1));
         uint64_t* hso = (uint64_t*)(hb + nbx);
@@ -2889,12 +2892,13 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
             hb[i].band_off = relocate(P, RG, hb[i].band_off);
             hb[i].stride = RG.stride;
             hb[i].data_off -= slot0;
+            hb[i].flags = (uint8_t)((hb[i].flags & ~2u) | (do_rc ? 2u : 0u));
         }
         for (uint32_t i = 0; i <= nbr; ++i) hso[i] = P.sym_off[b0 + i] - P.sym_off[b0];
         HIPCHK(hipMemcpyAsync(dblk, hb, sizeof(GkBlock) * nbr, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(dsymoff, hso, 8 * ((size_t)nbr + 1), hipMemcpyHostToDevice, st));
         HIPCHK(hipStreamSynchronize(st));   // the staging buffer is reused below
-        ctx->blocks_uploaded = true; ctx->enc_b0 = b0; ctx->enc_b1 = b1;
+        ctx->blocks_uploaded = true; ctx->enc_b0 = b0; ctx->enc_b1 = b1; ctx->enc_rc = do_rc;
     }
     HIPCHK(hipMemsetAsync(derr, 0, 64, st));
     if (P.p.ht()) {
