@@ -23,7 +23,7 @@ static inline __host__ __device__ uint32_t gk_sample_size(int t) { return t == G
 struct GkBlock {
     uint64_t band_off;     // element offset of the block's top-left sample in the coefficient arena
     uint32_t stride;       // row stride in elements
-    uint16_t w, h;         // block size (w <= 64, h <= 64 in this round)
+    uint16_t w, h;         // block size: 4..1024 per side, w * h <= 4096 (sides above 64: gk_t1ms.hip / wide HT)
     uint8_t orient;        // 0 LL, 1 HL, 2 LH, 3 HH
     uint8_t comp;
     uint8_t band_numbps;   // Quantizer.cpp:45-49 (decode: numbps - k_msbs)

@@ -2901,6 +2901,9 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         ctx->blocks_uploaded = true; ctx->enc_b0 = b0; ctx->enc_b1 = b1; ctx->enc_rc = do_rc;
     }
     HIPCHK(hipMemsetAsync(derr, 0, 64, st));
+    // solo MQ waves (gk_t1enc.hip mq_solo_block): GK_T1ENC_SOLO = how many of the heaviest blocks
+    // of the first chunk they code (without chunks: the first blocks in index order; tests)
+    const uint32_t nsolo_env = []() { const char* v = getenv("GK_T1ENC_SOLO"); return v ? (uint32_t)atoi(v) : 0u; }();
     if (P.p.ht()) {
         // HT cleanup pass (T1HT::compress, T1HT.cpp:109-133); MEL bytes staged in the symbol buffer
         uint8_t* mel = (uint8_t*)ctx->dsym.get((size_t)nbx * GK_HT_MEL_CAP + 256);
@@ -2917,7 +2920,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         gk_launch_t1_cm(st, arena, dblk, dsymoff, dsym, dpe, dcm, nbr, derr, ctx->nmse_tab, dnmse);
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[8], st));
-        gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount);
+        gk_launch_t1_mq(st, dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount, nullptr, 0,
+                        0xffffffffu, std::min(nsolo_env, nbr));
     } else {
         // Context modelling and MQ coding overlap.  Blocks go heaviest first (most coded
         // bit-planes, k_t1_weight) in three chunks; chunk i's MQ kernel starts on its own stream
@@ -2974,7 +2978,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
                 HIPCHK(hipEventRecord(ctx->xev[k], st));
                 HIPCHK(hipStreamWaitEvent(ctx->aux[k], ctx->xev[k], 0));
                 gk_launch_t1_mq(ctx->aux[k], dsym, dsymoff, dpe, dcm, dblk, dbytes, dps, dinfo, nbr, derr, dnmse, dpcount,
-                                dord, base, cnt);
+                                dord, base, cnt, k == 0 ? std::min(nsolo_env, cnt) : 0u);
                 HIPCHK(hipEventRecord(ctx->xev[3 + k], ctx->aux[k]));
             } else {
                 launch_check(__LINE__);

@@ -46,7 +46,8 @@ void gk_launch_t1_cm(hipStream_t st, const int32_t* coef, const GkBlock* blocks,
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
                      uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter,
-                     const uint32_t* order = nullptr, uint32_t base = 0, uint32_t count = 0xffffffffu);
+                     const uint32_t* order = nullptr, uint32_t base = 0, uint32_t count = 0xffffffffu,
+                     uint32_t nsolo = 0);   // nsolo: the first positions coded by solo waves, one block each
 // per-block coded bit-plane count (weight of the chunked CM / MQ overlap)
 void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blocks, uint32_t* weight, uint32_t nblocks);
 uint32_t gk_t1dec_lanes();

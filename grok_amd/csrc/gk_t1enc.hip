@@ -493,6 +493,183 @@ __device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t j) {
     return (w >> (8 * (j & 3))) & 0xff;
 }
 
+// ------------------------------------------------------------------ solo MQ coding
+// The heaviest blocks set the lane-parallel kernel's time: a lane codes one symbol per ~440
+// cycles whatever its own path (every lane runs every select of the step), and the LL and
+// low-resolution blocks of C3's 12-bit 9/7 data carry ~65 k symbols against a ~37 k plateau.
+// Solo waves code one such block each with the coder wave-uniform: A, C, CT and the byte
+// position in SGPRs, SALU selects instead of lane masks, the context states in lanes 0..18 of a
+// VGPR and the (state, MPS) pair table in two VGPRs (v_readlane / v_writelane), the symbols
+// arriving 64 at a time as 16 dwords in lanes 0..15, finished bytes gathered into a dword that
+// lane 0 stores.  The coder is the standard one of Annex C.2 in Grok's 32-bit arithmetic
+// (mqc_enc.cpp:86-330: C with its carry at bit 27, as gk_t1ms.hip's MsEnc), the pass bookkeeping
+// k_t1_mq's (T1.cpp:856-930); outputs are the same records, so T2 and rate control are shared.
+__device__ __forceinline__ uint32_t srl(uint32_t v, uint32_t lane) {   // v_readlane_b32
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+__device__ __forceinline__ uint32_t swl(uint32_t old, uint32_t val, uint32_t lane) {   // v_writelane_b32
+    // (gfx9 reads one SGPR per VALU op besides M0: the lane select goes through M0)
+    asm("v_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(val), "{m0}"(lane));
+    return old;
+}
+// Output: finished bytes gather into a dword (wacc, SGPR) written into a 256-byte ring held as one
+// VGPR (lane k = ring dword k) with v_writelane after every byte; at the end of every 64-symbol
+// chunk the 64-byte lines the stream has passed leave as one 16-lane store each (a chunk emits at
+// most 128 bytes).  No divergent branch sits in the symbol loop.
+struct MqSolo {
+    uint32_t a, c, ct;
+    int32_t bp;          // position of the pending byte `cur` (-1: the coder's dummy byte)
+    uint32_t cur;
+    uint32_t wacc;       // finished bytes of the dword holding position bp
+    uint32_t ring;       // (VGPR) 256-byte ring of the stream, lane k = dword k
+    // BYTEOUT (mqc_byteout, mqc_enc.cpp:86-127) without branches: a carry (C bit 27, unless the
+    // pending byte is 0xFF) goes into the pending byte, which is then final; the next byte takes 7
+    // bits of C after an 0xFF, else 8
+    __device__ __forceinline__ void byteout() {
+        const bool ff = cur == 0xffu;
+        const bool carry = !ff && (c & 0x8000000u);
+        const uint32_t cur2 = cur + (carry ? 1u : 0u);
+        const bool seven = cur2 == 0xffu;
+        const uint32_t cc = carry ? c & 0x7ffffffu : c;
+        const uint32_t nb = seven ? (cc >> 20) & 0xffu : (cc >> 19) & 0xffu;
+        // cur2 is final at bp (bp = -1: the dummy byte lands in ring dword 63, rewritten by stream
+        // bytes 252..255 before that line leaves)
+        wacc |= cur2 << (8u * ((uint32_t)bp & 3u));
+        ring = swl(ring, wacc, ((uint32_t)bp >> 2) & 63u);
+        ++bp;
+        wacc = ((uint32_t)bp & 3u) ? wacc : 0u;
+        cur = nb;
+        c = seven ? cc & 0xfffffu : cc & 0x7ffffu;
+        ct = seven ? 7u : 8u;
+    }
+};
+
+__device__ void mq_solo_block(uint32_t b, const uint8_t* __restrict__ sym, const uint64_t* __restrict__ sym_off,
+                              const uint32_t* __restrict__ pass_end, const uint32_t* __restrict__ cm_info,
+                              const GkBlock* __restrict__ blocks, uint8_t* __restrict__ bytes,
+                              GkPass* __restrict__ passes, uint32_t* __restrict__ info, int* err,
+                              const int32_t* __restrict__ pass_nmse, uint32_t* __restrict__ pass_counter, int lane) {
+    const uint32_t numbps = cm_info[2 * b], npasses = cm_info[2 * b + 1];
+    if (npasses == 0) {
+        if (lane == 0) { info[4 * b] = 0; info[4 * b + 1] = 0; info[4 * b + 2] = 0; info[4 * b + 3] = 0; }
+        return;
+    }
+    const uint32_t* PE = pass_end + (size_t)b * GK_MAX_PASSES;
+    const uint32_t nsym = PE[npasses - 1];
+    const GkBlock B = blocks[b];
+    const uint8_t* sp = sym + sym_off[b];
+    uint8_t* out = bytes + B.data_off;
+    const uint32_t cap = B.data_cap;
+    uint32_t poff = 0;
+    if (lane == 0) poff = atomicAdd(pass_counter, npasses);
+    poff = srl(poff, 0);
+    GkPass* P = passes + poff;
+    const bool rc = (B.flags & 2) != 0;
+    double cum = 0.0;
+    // the pair table and the context states in lanes (mqc_resetstates: ZC0 = 4, AGG = 3, UNI = 46)
+    const uint32_t TAB0 = mq_pair_entry((uint32_t)lane), TAB1 = lane < MQ_PAIRS - 64 ? mq_pair_entry(64u + lane) : 0u;
+    uint32_t CTX = mq_pair_entry(2u * (lane == CTX_ZC ? 4u : (lane == CTX_AGG ? 3u : (lane == CTX_UNI ? 46u : 0u))));
+    MqSolo q;
+    q.a = 0x8000; q.c = 0; q.ct = 12; q.bp = -1; q.cur = 0; q.wacc = 0; q.ring = 0;
+    uint32_t lf = 0;   // first 64-byte line not yet stored
+    auto lines_out = [&](uint32_t upto) {   // lines [lf, upto) from the ring, 16 lanes each
+        for (; lf < upto; ++lf)
+            if ((uint32_t)(lane >> 4) == (lf & 3u) && lf * 64 + 64 <= cap)
+                *reinterpret_cast<uint32_t*>(out + (size_t)lf * 64 + 4 * (lane & 15)) = q.ring;
+    };
+    auto chunk = [&](uint32_t k) -> uint32_t {   // symbols [64 k, 64 k + 64) as dwords in lanes 0..15
+        return (lane < 16 && 64 * k < nsym) ? *reinterpret_cast<const uint32_t*>(sp + 64 * k + 4 * lane) : 0u;
+    };
+    uint32_t p = 0, next_end = PE[0];
+    auto close_pass = [&]() {   // pass p ends here (T1.cpp:856-897)
+        uint32_t rate;
+        if (p == npasses - 1) {   // FLUSH (mqc_enc.cpp:213-227); the last pass is the one terminated
+            const uint32_t tempc = q.c + q.a;
+            q.c |= 0xffffu;
+            if (q.c >= tempc) q.c -= 0x8000u;
+            q.c <<= q.ct; q.byteout();
+            q.c <<= q.ct; q.byteout();
+            // a final 0xFF is not part of the stream; any other pending byte is
+            if (q.cur != 0xffu) {
+                q.wacc |= q.cur << (8u * ((uint32_t)q.bp & 3u));
+                q.ring = swl(q.ring, q.wacc, ((uint32_t)q.bp >> 2) & 63u);
+                ++q.bp;
+            }
+            rate = (uint32_t)q.bp;
+        } else {
+            rate = (uint32_t)q.bp + 5u + (q.ct < 5 ? 1u : 0u);
+        }
+        if (rc) {
+            const int bpno = p == 0 ? (int)numbps - 1 : (int)numbps - 2 - (int)(p - 1) / 3;
+            double wm = __dmul_rn(B.wmse, (double)(1 << bpno));
+            wm = __dmul_rn(wm, __dmul_rn(wm, (double)pass_nmse[(size_t)b * GK_MAX_PASSES + p]) / 8192.0);
+            cum = __dadd_rn(cum, wm);
+        }
+        if (lane == 0) { P[p].rate = rate; P[p].dist = cum; }
+        ++p;
+        next_end = p < npasses ? PE[p] : 0xffffffffu;
+    };
+    while (p < npasses && next_end == 0) close_pass();   // passes without symbols
+    uint32_t NX = chunk(0);
+    for (uint32_t k = 0; 64 * k < nsym; ++k) {
+        const uint32_t CH = NX;
+        NX = chunk(k + 1);
+        const uint32_t i1 = min(64 * k + 64, nsym);
+        for (uint32_t i = 64 * k; i < i1; ++i) {
+            const uint32_t s = (srl(CH, (i >> 2) & 15u) >> (8u * (i & 3u))) & 0xffu;
+            // CODEMPS / CODELPS (Annex C.2.4-C.2.5) + RENORME: with x = (MPS symbol) xor (A - Qe <
+            // Qe), C takes Qe and A keeps A - Qe iff x, else A = Qe; the state moves unless the
+            // symbol is an MPS that needs no renormalisation
+            const uint32_t cx = s >> 1;
+            const uint32_t e = srl(CTX, cx);
+            const uint32_t qe = e & 0xffffu;
+            const uint32_t a1 = q.a - qe;
+            const bool ism = (s & 1u) == (e >> 31);
+            const bool x = ism != (a1 < qe);
+            const bool fast = ism && (a1 & 0x8000u);
+            const uint32_t nidx = ism ? (e >> 16) & 0x7fu : (e >> 23) & 0x7fu;
+            const uint32_t t0 = srl(TAB0, nidx & 63u), t1 = srl(TAB1, nidx & 63u);
+            CTX = swl(CTX, fast ? e : ((nidx & 64u) ? t1 : t0), cx);
+            const uint32_t an = x ? a1 : qe;
+            q.c += x ? qe : 0u;
+            uint32_t n = (uint32_t)__builtin_clz(an) - 16u;   // <= 15
+            q.a = an << n;
+            if (n >= q.ct) {   // a byte boundary: shift up to it, BYTEOUT (CT >= 7 after), maybe once more
+                q.c <<= q.ct; n -= q.ct; q.byteout();
+                if (n >= q.ct) { q.c <<= q.ct; n -= q.ct; q.byteout(); }
+            }
+            q.c <<= n; q.ct -= n;
+            if (i + 1 == next_end)
+                do close_pass(); while (p < npasses && next_end == i + 1);
+        }
+        lines_out((uint32_t)max(q.bp, 0) >> 6);
+    }
+    // the partial last line (bytes before bp are final; the stream ends at bp)
+    const uint32_t nbytes = (uint32_t)q.bp;
+    if (lf * 64 < nbytes && (uint32_t)(lane >> 4) == (lf & 3u) && lf * 64 + 4 * (lane & 15) + 4 <= cap &&
+        (uint32_t)(lane & 15) * 4 < nbytes - lf * 64)
+        *reinterpret_cast<uint32_t*>(out + (size_t)lf * 64 + 4 * (lane & 15)) = q.ring;
+    __threadfence();
+    if (lane != 0) return;
+    uint32_t last = nbytes;
+    for (int k = (int)npasses; k > 0;) {   // monotone rates (T1.cpp:907-919)
+        GkPass& ps = P[--k];
+        if (ps.rate > last) ps.rate = last; else last = ps.rate;
+    }
+    uint32_t prev = 0;
+    for (uint32_t k = 0; k < npasses; ++k) {   // FF back-off (T1.cpp:920-930)
+        GkPass& ps = P[k];
+        if (ps.rate > 0 && ps.rate <= cap && out[ps.rate - 1] == 0xff) ps.rate--;
+        ps.len = ps.rate - prev;
+        prev = ps.rate;
+    }
+    info[4 * b] = numbps;
+    info[4 * b + 1] = npasses;
+    info[4 * b + 2] = P[npasses - 1].rate;
+    info[4 * b + 3] = poff;
+    if (nbytes > cap) atomicOr(err, 1);
+}
+
 // Outputs: info[4b..4b+3] = (numbps, npasses, bytes, offset of the block's
 // passes in `passes`); pass records are packed (atomic offset allocation) so
 // the host copies only the passes that exist.  With rate control the
@@ -503,17 +680,28 @@ __global__ __launch_bounds__(256) void k_t1_mq(const uint8_t* __restrict__ sym, 
                                               GkPass* __restrict__ passes, uint32_t* __restrict__ info,
                                               uint32_t nblocks, int* err, const int32_t* __restrict__ pass_nmse,
                                               uint32_t* __restrict__ pass_counter, uint32_t nl,
-                                              const uint32_t* __restrict__ order, uint32_t base, uint32_t count) {
+                                              const uint32_t* __restrict__ order, uint32_t base, uint32_t count,
+                                              uint32_t nsolo) {
     // nl = blocks per wave (lanes >= nl idle; gk_t1enc_lanes); pass ends staged in LDS [pass][lane].
     // A workgroup is four independent waves (one per SIMD) and takes a whole CU's LDS (the
     // launch pads it), so no other kernel's waves share a SIMD with an MQ chain.
     __shared__ MqLds Lw[4];
     extern __shared__ uint32_t pe_dyn[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the first nsolo waves (whole workgroups) are solo waves: position base + wave of `order`
+    const uint32_t gw = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + wave));
+    if (gw < nsolo) {
+        if (gw < count)
+            mq_solo_block(order ? order[base + gw] : base + gw, sym, sym_off, pass_end, cm_info, blocks, bytes, passes,
+                          info, err, pass_nmse, pass_counter, lane);
+        return;
+    }
     MqLds& L = Lw[wave];
     for (int i = lane; i < MQ_PAIRS; i += 64) L.tab[i] = mq_pair_entry((uint32_t)i);
-    // lane slot j = position base + j of `order` (index order without one)
-    const uint32_t j = (blockIdx.x * 4 + wave) * nl + lane;
+    // lane slot j = position base + nsolo + j of `order` (index order without one)
+    base += nsolo;
+    count = count > nsolo ? count - nsolo : 0;
+    const uint32_t j = (gw - nsolo) * nl + lane;
     const bool inr = (uint32_t)lane < nl && j < count;
     const uint32_t b = inr ? (order ? order[base + j] : base + j) : 0xffffffffu;
     const bool has = inr && b < nblocks;
@@ -704,10 +892,11 @@ void gk_launch_t1_weight(hipStream_t st, const int32_t* coef, const GkBlock* blo
 void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off, const uint32_t* pass_end,
                      const uint32_t* cm_info, const GkBlock* blocks, uint8_t* bytes, GkPass* passes, uint32_t* info,
                      uint32_t nblocks, int* err, const int32_t* pass_nmse, uint32_t* pass_counter, const uint32_t* order,
-                     uint32_t base, uint32_t count) {
+                     uint32_t base, uint32_t count, uint32_t nsolo) {
     if (!nblocks) return;
     if (count == 0xffffffffu) count = nblocks;
     if (!count) return;
+    nsolo = std::min((nsolo + 3) / 4 * 4, (count + 3) / 4 * 4);   // whole workgroups of solo waves
     static uint32_t nl = 0;
     if (!nl) {   // blocks per 64-lane wave (GK_T1ENC_LANES, 1..64)
         const char* v = getenv("GK_T1ENC_LANES");
@@ -717,6 +906,8 @@ void gk_launch_t1_mq(hipStream_t st, const uint8_t* sym, const uint64_t* sym_off
     // dynamic LDS: the four waves' pass ends, padded so one workgroup fills the CU's 160 KiB
     const size_t pe = (size_t)(GK_MAX_PASSES + 1) * nl * 4 * 4;
     const size_t lds = std::max(pe, (size_t)163840 - 4 * sizeof(MqLds));
-    hipLaunchKernelGGL(k_t1_mq, dim3((count + 4 * nl - 1) / (4 * nl)), dim3(256), lds, st, sym, sym_off, pass_end,
-                       cm_info, blocks, bytes, passes, info, nblocks, err, pass_nmse, pass_counter, nl, order, base, count);
+    const uint32_t rest = count > nsolo ? count - nsolo : 0;
+    hipLaunchKernelGGL(k_t1_mq, dim3(nsolo / 4 + (rest + 4 * nl - 1) / (4 * nl)), dim3(256), lds, st, sym, sym_off,
+                       pass_end, cm_info, blocks, bytes, passes, info, nblocks, err, pass_nmse, pass_counter, nl, order,
+                       base, count, nsolo);
 }
