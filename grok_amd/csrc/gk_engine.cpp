@@ -436,22 +436,52 @@ static void assign_steps_tile(Plan& P, TileG& T) {
     }
 }
 
-static void apply_qcd(Plan& P, const std::vector<std::pair<uint32_t, uint32_t>>& q) {
+// A stream's quantisation per component (QCD, replaced per component by a main-header QCC, A.6.4-
+// A.6.5) as one flat list: for each component a (guard bits, ~0u) entry, then the (expn, mant) of
+// its bands, LL first then (HL, LH, HH) per resolution, scalar-derived steps already expanded.
+typedef std::vector<std::pair<uint32_t, uint32_t>> QuantList;
+static void apply_qcd(Plan& P, const QuantList& q) {
+    // the start of each component's entries
+    std::vector<size_t> at;
+    for (size_t k = 0; k < q.size(); ++k) if (q[k].second == ~0u) at.push_back(k);
+    if (at.size() != P.nc) throw GkError("quantisation list does not match the component count");
     for (auto& T : P.tiles)
     for (uint32_t ci = 0; ci < (uint32_t)T.comps.size(); ++ci) {
         CompG& C = T.comps[ci];
+        const size_t k0 = at[ci] + 1, k1 = ci + 1 < at.size() ? at[ci + 1] : q.size();
+        if (k1 <= k0) throw GkError("QCD / QCC without step sizes");
+        const uint32_t gb = q[at[ci]].first;
         uint32_t bandno = 0;
         for (uint32_t r = 0; r < P.p.numres; ++r)
             for (auto& B : C.res[r].bands) {
-                size_t k = std::min<size_t>(bandno, q.size() - 1);
+                size_t k = std::min<size_t>(k0 + bandno, k1 - 1);
                 B.expn = q[k].first; B.mant = q[k].second;
                 uint32_t lg_enc = B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1);
                 uint32_t lg_dec = P.p.irrev ? 0 : lg_enc;
                 B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
                 B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
-                B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1);
+                B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, (int)B.expn + (int)gb - 1);
                 ++bandno;
             }
+    }
+}
+// Sqcd / Sqcc + SPqcd / SPqcc -> guard bits and band steps (Quantizer::read_SQcd_SQcc,
+// Quantizer.cpp:185-334): no quantisation (one byte per band, exponent << 3), scalar expounded
+// (16 bits per band), scalar derived (the LL step only; band b > 0 takes expn_0 - floor((b - 1) / 3)
+// and mant_0, :319-331, i.e. E-5's epsilon_0 - N_L + n_b)
+static void parse_quant(const std::vector<uint8_t>& b, uint32_t numres, QuantList& out) {
+    if (b.size() < 2) throw GkError("corrupt QCD / QCC marker");
+    const uint32_t sq = b[0], qt = sq & 0x1f, nb = 3 * numres - 2;
+    out.push_back({sq >> 5, ~0u});
+    const size_t k0 = out.size();
+    if (qt == 0) for (size_t k = 1; k < b.size(); ++k) out.push_back({(uint32_t)b[k] >> 3, 0u});
+    else if (qt == 1 || qt == 2) for (size_t k = 1; k + 1 < b.size(); k += 2) { uint32_t v = (uint32_t)b[k] << 8 | b[k + 1]; out.push_back({v >> 11, v & 0x7ff}); }
+    else throw GkError("corrupt QCD / QCC marker (quantisation style)");
+    if (out.size() == k0) throw GkError("QCD / QCC without step sizes");
+    if (qt == 1) {
+        const auto s0 = out[k0];
+        out.resize(k0 + nb);
+        for (uint32_t k = 1; k < nb; ++k) out[k0 + k] = {s0.first > (k - 1) / 3 ? s0.first - (k - 1) / 3 : 0u, s0.second};
     }
 }
 
@@ -2554,8 +2584,11 @@ static void ensure_plan(gk_ctx* ctx, const Plan& want) {
     ctx->plan_key = k;
     ctx->blocks_uploaded = false;
     ctx->native_qcd.clear();
-    for (const ResG& R : ctx->plan.tiles[0].comps[0].res)
-        for (const BandG& B : R.bands) ctx->native_qcd.push_back({B.expn, B.mant});
+    for (const CompG& C : ctx->plan.tiles[0].comps) {
+        ctx->native_qcd.push_back({ctx->plan.p.numgbits, ~0u});
+        for (const ResG& R : C.res)
+            for (const BandG& B : R.bands) ctx->native_qcd.push_back({B.expn, B.mant});
+    }
     ctx->band_qcd = ctx->native_qcd;
 }
 // Encode uses the plan's own quantisation: undo a decoded stream's QCD if one was applied.
@@ -3451,7 +3484,8 @@ static void parse_poc(Src& S, size_t s, uint32_t L, uint32_t nc, std::vector<Poc
 // rather than skipped, so a stream that carries them fails instead of decoding wrongly.
 struct Header {
     Plan want;
-    std::vector<std::pair<uint32_t, uint32_t>> qcd;
+    QuantList qcd;                                    // per component (apply_qcd)
+    std::vector<std::vector<uint8_t>> qbody;          // per component: its main QCC body, else the QCD's
     size_t first_sot = 0;
     std::vector<TilePart> parts;
     std::vector<std::pair<uint32_t, uint32_t>> tlm;   // (tile, tile-part length) from TLM markers
@@ -3464,10 +3498,11 @@ static std::vector<uint8_t> marker_body(ByteSrc& S, size_t s, uint32_t L) {
     return v;
 }
 
-// COC / QCC (main or tile-part header) and tile-part COD / QCD override the main COD / QCD for
-// one component or one tile (CodeStreamDecompress read_coc / read_qcc, TileCodingParams).
-// This path codes every tile-component with the main header's parameters, so such a marker is
-// accepted when it restates them (some encoders write them even when nothing differs) and
+// COC (main or tile-part header), tile-part QCC and tile-part COD / QCD override the main header's
+// coding or quantisation for one component or one tile (CodeStreamDecompress read_coc /
+// read_qcc, TileCodingParams).  A main-header QCC is applied per component (apply_qcd); every
+// tile-component is otherwise coded with the main header's parameters, so these markers are
+// accepted when they restate them (some encoders write them even when nothing differs) and
 // refused otherwise.  COC: Ccoc (1 byte below 257 components, else 2), Scoc (precinct flag),
 // then SPcoc laid out as COD's SPcod; QCC: Cqcc, then Sqcc/SPqcc as QCD's body.
 static void check_override_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, const Header& Hd, bool tile) {
@@ -3478,17 +3513,19 @@ static void check_override_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, 
     const uint32_t nc = Hd.want.nc, cw = nc <= 256 ? 1 : 2;
     bool same = false;
     if (m == 0xff52) same = b == Hd.cod;
-    else if (m == 0xff5c) same = b == Hd.qcd_body;
-    else if (b.size() > cw) {
+    else if (m == 0xff5c) {   // (a tile QCD replaces every component's QCD / QCC)
+        same = true;
+        for (const auto& q : Hd.qbody) same = same && b == q;
+    } else if (b.size() > cw) {
         const uint32_t c = cw == 1 ? b[0] : (uint32_t)b[0] << 8 | b[1];
         if (c >= nc) throw GkError("bad component number in COC/QCC");
-        if (m == 0xff5d) same = std::equal(b.begin() + cw, b.end(), Hd.qcd_body.begin(), Hd.qcd_body.end());
+        if (m == 0xff5d) same = std::equal(b.begin() + cw, b.end(), Hd.qbody[c].begin(), Hd.qbody[c].end());
         else same = Hd.cod.size() > 5 && (b[cw] & 1) == (Hd.cod[0] & 1) &&
                     std::equal(b.begin() + cw + 1, b.end(), Hd.cod.begin() + 5, Hd.cod.end());
     }
     if (!same)
         throw GkError(tile ? "tile-part COD/COC/QCD/QCC that differ from the main header are not supported on this path"
-                           : "COC/QCC that differ from COD/QCD are not supported on this path");
+                           : "COC that differs from COD is not supported on this path");
 }
 // The tiles of the canvas tile grid (B.3)
 static uint32_t grid_tiles(const Plan& W) {
@@ -3544,7 +3581,8 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     Plan& W = Hd.want;
     for (int k = 0; k < GK_MAXRLVLS; ++k) { W.p.prcw[k] = 15; W.p.prch[k] = 15; }
     bool have_siz = false, have_cod = false;
-    std::vector<size_t> coc_qcc;   // checked against COD / QCD once the main header is read
+    std::vector<size_t> coc_qcc;   // COC: checked against COD once the main header is read
+    std::vector<std::pair<uint32_t, std::vector<uint8_t>>> qcc;   // main-header QCC: (component, Sqcc + SPqcc)
     while (i + 4 <= S.len) {
         uint32_t m = S.be16(i);
         if (m == 0xff90) { Hd.first_sot = i; break; }
@@ -3605,13 +3643,8 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             Hd.cod = marker_body(S, s, L);
         } else if (m == 0xff5c) {
             if (L < 4) throw GkError("corrupt QCD marker");
-            uint32_t sq = S.at(s);
-            W.p.numgbits = sq >> 5;
-            uint32_t qt = sq & 0x1f;
-            Hd.qcd.clear();
-            if (qt == 0) for (uint32_t k = 1; k < L - 2; ++k) Hd.qcd.push_back({(uint32_t)S.at(s + k) >> 3, 0u});
-            else if (qt == 2) for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = S.be16(s + k); Hd.qcd.push_back({v >> 11, v & 0x7ff}); }
-            else throw GkError("scalar-derived quantisation not supported");
+            W.p.numgbits = S.at(s) >> 5;
+            if ((S.at(s) & 0x1f) > 2) throw GkError("corrupt QCD marker (quantisation style)");
             Hd.qcd_body = marker_body(S, s, L);
         } else if (m == 0xff55) {   // TLM (TileLengthMarkers::read, cache/LengthCache.cpp)
             const uint32_t stlm = S.at(s + 1), st = (stlm >> 4) & 3, sp = (stlm >> 6) & 1;
@@ -3637,12 +3670,26 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             if (shift >= 32) throw GkError("unsupported ROI shift");
             if (W.p.roishift.size() < W.nc) W.p.roishift.resize(W.nc, 0);
             W.p.roishift[c] = (uint8_t)shift;
-        } else if (m == 0xff5d || m == 0xff53) {
+        } else if (m == 0xff5d) {   // QCC (A.6.5): one component's quantisation replaces the QCD's
+            if (!have_siz) throw GkError("QCC before SIZ");
+            const uint32_t cw = W.nc <= 256 ? 1 : 2;
+            if (L < 4 + cw) throw GkError("corrupt QCC marker");
+            const uint32_t c = cw == 1 ? S.at(s) : S.be16(s);
+            if (c >= W.nc) throw GkError("bad component number in QCC");
+            std::vector<uint8_t> b = marker_body(S, s, L);
+            qcc.push_back({c, std::vector<uint8_t>(b.begin() + cw, b.end())});
+        } else if (m == 0xff53) {
             coc_qcc.push_back(i);
         }
         i += 2 + L;
     }
-    if (!have_siz || !have_cod || Hd.qcd.empty() || !Hd.first_sot) throw GkError("incomplete main header");
+    if (!have_siz || !have_cod || Hd.qcd_body.empty() || !Hd.first_sot) throw GkError("incomplete main header");
+    // per component: the QCD's quantisation, replaced by its main-header QCC (a main QCC takes
+    // precedence over the main QCD in any marker order, Quantizer.cpp:215-235)
+    Hd.qbody.assign(W.nc, Hd.qcd_body);
+    for (auto& q : qcc) Hd.qbody[q.first] = q.second;
+    Hd.qcd.clear();
+    for (uint32_t c = 0; c < W.nc; ++c) parse_quant(Hd.qbody[c], W.p.numres, Hd.qcd);
     for (size_t k : coc_qcc) check_override_marker(S, k + 4, S.be16(k), S.be16(k + 2), Hd, false);
     // tile parts: SOT (Isot, Psot, TPsot, TNsot), tile-part header markers (PLT, ...), SOD, packets
     // (CodeStreamDecompress SOT/SOD handlers; TLM and PLT are only needed for random access)

@@ -103,8 +103,22 @@ struct Params {
     bool quality = false;       // fixed-quality layers (-q, grk_cparameters::allocationByQuality)
     double dist[100] = {0};     // per-layer PSNR targets (layer_distortion; 0 = every remaining pass)
     bool ht() const { return (cblk_sty & 0x40) != 0; }
+    // per-component quantisation of third-party encoders (written as QCC markers, A.6.5; Grok's own
+    // encoder pushes one QCD to every component, CodeStreamCompress.cpp:382-384): guard bits per
+    // component (empty: numgbits), irreversible exponents lowered by qshift[c] (a step 2^qshift
+    // times coarser), and scalar-derived quantisation (Sqcd style 1: only the LL step is written,
+    // the others follow E-5 as Quantizer.cpp:319-331 expands them)
+    std::vector<uint32_t> comp_gb;
+    std::vector<int32_t> comp_qshift;
+    bool qderived = false;
+    uint32_t gb(uint32_t c) const { return c < comp_gb.size() ? comp_gb[c] : numgbits; }
+    int32_t qshift(uint32_t c) const { return c < comp_qshift.size() ? comp_qshift[c] : 0; }
     Params() { for (int i = 0; i < 33; ++i) { prcw_exp[i] = 15; prch_exp[i] = 15; } }
 };
+
+// A component's quantisation as decoded from QCD / QCC (A.6.4-A.6.5): guard bits and the (expn,
+// mant) of every band, LL first then (HL, LH, HH) per resolution, scalar-derived steps expanded
+struct Quant { uint32_t gb = 2; std::vector<std::pair<uint32_t, uint32_t>> steps; };
 
 // ----------------------------------------------------------------------------
 // Tile geometry (Annex B; Grok: Resolution.h:37-72, Precinct.h:59-68,
@@ -301,21 +315,39 @@ static void ht_irrev_quant(uint32_t prec, int sgnd, uint32_t nd, uint32_t r, uin
     expn = e;
 }
 
-static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress,
-                         const std::vector<std::pair<uint32_t,uint32_t>>* qcd, int sgnd = 0, uint32_t roishift = 0) {
-    // qcd: per band (expn, mant) in band order LL, (HL,LH,HH) per resolution, when decoding.
+// Expand a QCD / QCC body's steps (Sqcd, then SPqcd) into a Quant for numres resolutions:
+// scalar derived (style 1) as Grok's read_SQcd_SQcc (Quantizer.cpp:319-331), band b > 0 taking
+// expn_0 - floor((b - 1) / 3) (E-5: epsilon_0 - N_L + n_b) and mant_0.  false: malformed.
+static bool parse_quant(const uint8_t* s, size_t n, uint32_t numres, Quant& q) {
+    if (n < 1) return false;
+    const uint32_t sq = s[0], qt = sq & 0x1f, nb = 3 * numres - 2;
+    q.gb = sq >> 5;
+    q.steps.clear();
+    if (qt == 0) for (size_t k = 1; k < n; ++k) q.steps.push_back({(uint32_t)s[k] >> 3, 0u});
+    else if (qt == 1 || qt == 2) for (size_t k = 1; k + 1 < n; k += 2) { uint32_t v = ((uint32_t)s[k] << 8) | s[k + 1]; q.steps.push_back({v >> 11, v & 0x7ff}); }
+    else return false;
+    if (q.steps.empty()) return false;
+    if (qt == 1) {
+        const auto s0 = q.steps[0];
+        q.steps.assign(nb, s0);
+        for (uint32_t b = 1; b < nb; ++b) q.steps[b] = {s0.first > (b - 1) / 3 ? s0.first - (b - 1) / 3 : 0u, s0.second};
+    }
+    return true;
+}
+
+static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress, const Quant* qd, int sgnd = 0,
+                         uint32_t roishift = 0, uint32_t comp = 0) {
+    // qd (decoding): the component's guard bits and band steps, band order LL, (HL,LH,HH) per
+    // resolution; encoding: p's guard bits, exponent shift and derived style of component comp
     uint32_t bandno = 0;
+    const uint32_t gbits = qd ? qd->gb : p.gb(comp);
+    uint32_t e0 = 0, m0 = 0;   // the LL step (scalar derived)
     for (uint32_t r = 0; r < p.numres; ++r) {
         for (auto& B : c.res[r].bands) {
             uint32_t expn, mant;
-            if (qcd) {
-                expn = (*qcd)[std::min<size_t>(bandno, qcd->size() - 1)].first;
-                mant = (*qcd)[std::min<size_t>(bandno, qcd->size() - 1)].second;
-                if (qcd->size() == 1 && bandno > 0) {  // scalar derived (E-5)
-                    uint32_t nb = p.numres - r;
-                    expn = (*qcd)[0].first - (p.numres - 1) + (nb - 1) + 0;  // rarely used
-                    (void)nb;
-                }
+            if (qd) {
+                expn = qd->steps[std::min<size_t>(bandno, qd->steps.size() - 1)].first;
+                mant = qd->steps[std::min<size_t>(bandno, qd->steps.size() - 1)].second;
             } else if (p.ht() && p.irreversible) {
                 ht_irrev_quant(prec, sgnd, p.numres - 1, r, B.orient, expn, mant);
             } else if (p.ht() && !p.irreversible) {
@@ -332,13 +364,17 @@ static void assign_steps(Comp& c, const Params& p, uint32_t prec, bool compress,
                 int pp = floorlog2(step) - 13;
                 int n = 11 - floorlog2(step);
                 mant = (n < 0 ? step >> -n : step << n) & 0x7ff;
-                expn = (uint32_t)((int)(prec + gain) - pp);
+                expn = (uint32_t)std::max(0, (int)(prec + gain) - pp - (p.irreversible ? p.qshift(comp) : 0));
+                if (p.irreversible && p.qderived) {   // E-5 from the LL step
+                    if (bandno == 0) { e0 = expn; m0 = mant; }
+                    else { expn = e0 > (bandno - 1) / 3 ? e0 - (bandno - 1) / 3 : 0u; mant = m0; }
+                }
             }
             B.expn = expn; B.mant = mant;
             uint32_t log2_gain = (!compress && p.irreversible) ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
             uint32_t nbps = prec + log2_gain;
             B.stepsize = (float)((1.0 + mant / 2048.0) * pow(2.0, (int)nbps - (int)expn));
-            int v = (int)expn + (int)p.numgbits - 1;
+            int v = (int)expn + (int)gbits - 1;
             B.numbps = roishift + (uint32_t)std::max(0, v);   // Quantizer.cpp:47: roishift + expn + guard - 1
             ++bandno;
         }
@@ -1287,15 +1323,38 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
     o.push_back(p.irreversible ? 0 : 1);
     if (custom_prc) for (uint32_t r = 0; r < p.numres; ++r) o.push_back((uint8_t)(p.prcw_exp[r] | (p.prch_exp[r] << 4)));
     uint32_t nbands = 3 * p.numres - 2;              // QCD
-    put16(o, 0xff5c);
-    if (!p.irreversible) {
-        put16(o, 3 + nbands);
-        o.push_back((uint8_t)(p.numgbits << 5));
-        for (uint32_t r = 0; r < p.numres; ++r) for (auto& B : c0.res[r].bands) o.push_back((uint8_t)(B.expn << 3));
-    } else {
-        put16(o, 3 + 2 * nbands);
-        o.push_back((uint8_t)((p.numgbits << 5) | 2));
-        for (uint32_t r = 0; r < p.numres; ++r) for (auto& B : c0.res[r].bands) put16(o, (B.expn << 11) | B.mant);
+    // Sqcd + SPqcd of a component: no quantisation (5/3), scalar expounded, or scalar derived (LL only)
+    auto quant_body = [&](const Comp& cc, uint32_t gbits) {
+        std::vector<uint8_t> q;
+        if (!p.irreversible) {
+            q.push_back((uint8_t)(gbits << 5));
+            for (uint32_t r = 0; r < p.numres; ++r) for (auto& B : cc.res[r].bands) q.push_back((uint8_t)(B.expn << 3));
+        } else {
+            q.push_back((uint8_t)((gbits << 5) | (p.qderived ? 1 : 2)));
+            for (uint32_t r = 0; r < (p.qderived ? 1u : p.numres); ++r)
+                for (auto& B : cc.res[r].bands) {
+                    const uint32_t v = (B.expn << 11) | B.mant;
+                    q.push_back((uint8_t)(v >> 8)); q.push_back((uint8_t)(v & 0xff));
+                }
+        }
+        return q;
+    };
+    (void)nbands;
+    const std::vector<uint8_t> q0 = quant_body(c0, p.gb(0));
+    put16(o, 0xff5c); put16(o, (uint32_t)(2 + q0.size()));
+    o.insert(o.end(), q0.begin(), q0.end());
+    // QCC for every component whose quantisation differs from component 0's (write_all_qcc,
+    // CodeStreamCompress.cpp:1384-1396): Cqcc (one byte below 257 components), Sqcc, SPqcc
+    for (uint32_t c = 1; c < im.nc; ++c) {
+        if (p.gb(c) == p.gb(0) && p.qshift(c) == p.qshift(0)) continue;
+        Comp cc = c0;
+        assign_steps(cc, p, im.prec, true, nullptr, im.sgnd ? 1 : 0, 0, c);
+        const std::vector<uint8_t> qc = quant_body(cc, p.gb(c));
+        if (qc == q0) continue;
+        const uint32_t cw = im.nc <= 256 ? 1 : 2;
+        put16(o, 0xff5d); put16(o, (uint32_t)(2 + cw + qc.size()));
+        if (cw == 2) put16(o, c); else o.push_back((uint8_t)c);
+        o.insert(o.end(), qc.begin(), qc.end());
     }
     if (p.tlm) {                                     // TLM (TileLengthMarkers::writeBegin)
         uint32_t nt = tile_count(p, im.w, im.h) * (uint32_t)std::max(1, num_parts(p, im.nc));   // entries per tile part
@@ -1965,6 +2024,11 @@ typedef struct {
     double layer_distortion[100];
     uint32_t image_x0, image_y0;   // canvas offset of the image area (grk_image::x0 / y0, -d)
     uint32_t tile_x0, tile_y0;     // tile grid origin (grk_cparameters::tx0 / ty0, -T)
+    // per-component quantisation (QCC; Params::comp_gb / comp_qshift / qderived), first nq components
+    uint32_t nq;
+    uint32_t comp_gb[16];
+    int32_t comp_qshift[16];
+    uint32_t qderived;
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -2000,6 +2064,8 @@ static Params to_params(const orc_cparams* cp) {
     // exponent at resolution 0 (CodeStreamCompress.cpp:573-590 writes it when the halved size
     // reaches 1); at a higher resolution it has no band partition (B.6 PPx - 1) and is refused
     for (int i = 0; i < 33; ++i) { p.prcw_exp[i] = cp->prcw_exp[i] & 15; p.prch_exp[i] = cp->prch_exp[i] & 15; }
+    for (uint32_t c = 0; c < cp->nq && c < 16; ++c) { p.comp_gb.push_back(cp->comp_gb[c]); p.comp_qshift.push_back(cp->comp_qshift[c]); }
+    p.qderived = cp->qderived != 0;
     return p;
 }
 
@@ -2119,7 +2185,7 @@ static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, ui
     E.comps.assign(nc, Comp());
     for (uint32_t c = 0; c < nc; ++c) {
         build_geometry(E.comps[c], E.tx0, E.ty0, E.tx1, E.ty1, E.p);
-        assign_steps(E.comps[c], E.p, prec, true, nullptr, sgnd, E.p.roi(c));
+        assign_steps(E.comps[c], E.p, prec, true, nullptr, sgnd, E.p.roi(c), c);
     }
     E.coefs.assign(nc, {});
     for (uint32_t c = 0; c < nc; ++c) {   // tile-local copy (TileProcessor::ingestImage, TileProcessor.cpp:410-431)
@@ -2740,7 +2806,7 @@ void orc_t1_decode_cblk(const uint8_t* data, uint32_t len, uint32_t npasses, uin
 // ranges: the packet bytes [data, end) of the tile's tile parts in TPsot order (a tile's
 // packet sequence continues across its parts, A.4.2)
 static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, size_t>>& ranges, const Params& p,
-                       const Image& im, const std::vector<std::pair<uint32_t, uint32_t>>& qcd, uint32_t tile,
+                       const Image& im, const std::vector<Quant>& cq, uint32_t tile,
                        int32_t* out, const std::vector<PocE>* tpocs = nullptr) {
     size_t data = ranges[0].first, tile_end = ranges[0].second, next_range = 1;
     uint32_t tx0, ty0, tx1, ty1;
@@ -2750,7 +2816,7 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
     const uint32_t red = g_dec_reduce;   // grk_dparameters::cp_reduce
     size_t i = data;
     std::vector<Comp> comps(im.nc);
-    for (uint32_t c = 0; c < im.nc; ++c) { build_geometry(comps[c], tx0, ty0, tx1, ty1, p); assign_steps(comps[c], p, im.prec, false, &qcd, 0, p.roi(c)); }
+    for (uint32_t c = 0; c < im.nc; ++c) { build_geometry(comps[c], tx0, ty0, tx1, ty1, p); assign_steps(comps[c], p, im.prec, false, &cq[c], 0, p.roi(c)); }
     // T2 decode (LRCP)
     struct TT { std::vector<TagTree> incl, imsb; };
     std::vector<std::vector<std::vector<TT>>> trees(im.nc);
@@ -2956,15 +3022,20 @@ t2done:
 // COC / QCC and tile-part COD / QCD (CodeStreamDecompress read_coc / read_qcc override the main
 // COD / QCD per component or per tile): this restatement codes every tile-component with the
 // main header's parameters, so it accepts such a marker only when it restates them.
+// qcc: the main header's quantisation body per component (its QCC, else the QCD)
 static bool restates_main(const uint8_t* b, uint32_t L, uint32_t m, uint32_t nc, const std::vector<uint8_t>& cod,
-                          const std::vector<uint8_t>& qcd) {
+                          const std::vector<uint8_t>& qcd, const std::vector<std::vector<uint8_t>>& qcc) {
     if (L < 3) return false;
     const std::vector<uint8_t> v(b, b + L - 2);
     if (m == 0xff52) return v == cod;
-    if (m == 0xff5c) return v == qcd;
+    if (m == 0xff5c) {
+        for (const auto& q : qcc) if (q != qcd) return false;   // a tile QCD would replace differing QCCs
+        return v == qcd;
+    }
     const uint32_t cw = nc <= 256 ? 1 : 2;
     if (v.size() <= cw || (cw == 1 ? v[0] : get16(b)) >= nc) return false;
-    if (m == 0xff5d) return std::equal(v.begin() + cw, v.end(), qcd.begin(), qcd.end());
+    const uint32_t c = cw == 1 ? v[0] : get16(b);
+    if (m == 0xff5d) return std::equal(v.begin() + cw, v.end(), qcc[c].begin(), qcc[c].end());
     return cod.size() > 5 && (v[cw] & 1) == (cod[0] & 1) && std::equal(v.begin() + cw + 1, v.end(), cod.begin() + 5, cod.end());
 }
 
@@ -3015,10 +3086,10 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     if (len < 4 || get16(cs) != 0xff4f) return -1;
     i = 2;
     Image im{}; Params p; p.write_com = 0;
-    std::vector<std::pair<uint32_t, uint32_t>> qcd;
     size_t first_sot = 0;
     std::vector<uint8_t> cod_body, qcd_body;
     std::vector<size_t> coc_qcc;
+    std::vector<std::pair<uint32_t, std::vector<uint8_t>>> qccs;   // main-header QCC: (component, Sqcc + SPqcc)
     while (i + 4 <= len) {
         uint32_t m = get16(cs + i);
         if (m == 0xff90) { first_sot = i; break; }
@@ -3056,19 +3127,30 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             if (p.roishift.size() < im.nc) p.roishift.resize(im.nc, 0);
             p.roishift[c] = s[cw + 1];
         } else if (m == 0xff5c) {
-            uint32_t sq = s[0]; p.numgbits = sq >> 5;
+            if (L < 3) return -2;
+            p.numgbits = s[0] >> 5;
             qcd_body.assign(s, s + L - 2);
-            uint32_t qt = sq & 0x1f;
-            if (qt == 0) for (uint32_t k = 1; k + 0 < L - 2; ++k) qcd.push_back({(uint32_t)s[k] >> 3, 0u});
-            else for (uint32_t k = 1; k + 1 < L - 2; k += 2) { uint32_t v = get16(s + k); qcd.push_back({v >> 11, v & 0x7ff}); }
-        } else if (m == 0xff53 || m == 0xff5d) {
+        } else if (m == 0xff5d) {   // QCC (A.6.5): this component's quantisation replaces the QCD's
+            const uint32_t cw = im.nc <= 256 ? 1 : 2;
+            if (!im.nc || L < 3 + cw) return -2;
+            const uint32_t c = cw == 1 ? s[0] : get16(s);
+            if (c >= im.nc) return -2;
+            qccs.push_back({c, std::vector<uint8_t>(s + cw, s + L - 2)});
+        } else if (m == 0xff53) {
             coc_qcc.push_back(i);
         }
         i += 2 + L;   // CAP, TLM, COM and other main-header markers are skipped
     }
-    if (!first_sot) return -3;
+    if (!first_sot || qcd_body.empty()) return -3;
+    // per component: the QCD's quantisation, replaced by a main-header QCC (read_SQcd_SQcc with
+    // Grok's precedence: a main QCC wins over the main QCD, Quantizer.cpp:215-235)
+    std::vector<std::vector<uint8_t>> qbody(im.nc, qcd_body);
+    for (const auto& q : qccs) qbody[q.first] = q.second;
+    std::vector<Quant> cq(im.nc);
+    for (uint32_t c = 0; c < im.nc; ++c)
+        if (!parse_quant(qbody[c].data(), qbody[c].size(), p.numres, cq[c])) return -2;
     for (size_t k : coc_qcc)
-        if (!restates_main(cs + k + 4, get16(cs + k + 2), get16(cs + k), im.nc, cod_body, qcd_body)) return -2;
+        if (!restates_main(cs + k + 4, get16(cs + k + 2), get16(cs + k), im.nc, cod_body, qcd_body, qbody)) return -2;
     if (g_dec_reduce >= p.numres) return -7;   // reduce must leave one resolution
     *W = ceildivpow2(p.x0 + im.w, g_dec_reduce) - ceildivpow2(p.x0, g_dec_reduce);
     *H = ceildivpow2(p.y0 + im.h, g_dec_reduce) - ceildivpow2(p.y0, g_dec_reduce);
@@ -3093,7 +3175,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             const uint32_t tm = get16(cs + j);
             if (tm == 0xff5f && !read_poc(cs + j + 4, get16(cs + j + 2), im.nc, tp_pocs)) return -5;
             if ((tm == 0xff52 || tm == 0xff53 || tm == 0xff5c || tm == 0xff5d) &&
-                !restates_main(cs + j + 4, get16(cs + j + 2), tm, im.nc, cod_body, qcd_body)) return -2;
+                !restates_main(cs + j + 4, get16(cs + j + 2), tm, im.nc, cod_body, qcd_body, qbody)) return -2;
             if (tm == 0xff5e) return -2;   // tile-part RGN
             j += 2 + get16(cs + j + 2);
         }
@@ -3121,7 +3203,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         ranges[slot[q.tile]].push_back({q.data, q.end});
     }
     std::vector<int> rcs(tiles.size(), 0);   // tiles write disjoint rectangles of out
-    par_for(tiles.size(), [&](size_t q) { rcs[q] = decode_tile(cs, ranges[q], p, im, qcd, tiles[q], out, &tpocs[q]); });
+    par_for(tiles.size(), [&](size_t q) { rcs[q] = decode_tile(cs, ranges[q], p, im, cq, tiles[q], out, &tpocs[q]); });
     for (int rc : rcs) if (rc) return rc;
     return 0;
 }

@@ -29,6 +29,8 @@ class CParams(ctypes.Structure):
         ("csty", ctypes.c_uint32), ("by_quality", ctypes.c_uint32), ("layer_distortion", ctypes.c_double * 100),
         ("image_x0", ctypes.c_uint32), ("image_y0", ctypes.c_uint32), ("tile_x0", ctypes.c_uint32),
         ("tile_y0", ctypes.c_uint32),
+        ("nq", ctypes.c_uint32), ("comp_gb", ctypes.c_uint32 * 16), ("comp_qshift", ctypes.c_int32 * 16),
+        ("qderived", ctypes.c_uint32),
     ]
 
 
@@ -102,7 +104,8 @@ def get_threads():
 
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
            layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None, roi=None,
-           sop=False, eph=False, quality=None, origin=None, tile_origin=None):
+           sop=False, eph=False, quality=None, origin=None, tile_origin=None, comp_guard_bits=None, comp_qshift=None,
+           qderived=False):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -132,6 +135,14 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
     elif tile_origin:
         p.image_x0, p.image_y0 = p.tile_x0, p.tile_y0
     p.tlm, p.plt = int(tlm), int(plt)
+    # per-component quantisation, written as QCC markers (third-party encoders; Grok writes none)
+    if comp_guard_bits or comp_qshift:
+        n = max(len(comp_guard_bits or []), len(comp_qshift or []))
+        p.nq = n
+        for c in range(n):
+            p.comp_gb[c] = int((comp_guard_bits or [])[c]) if c < len(comp_guard_bits or []) else 2
+            p.comp_qshift[c] = int((comp_qshift or [])[c]) if c < len(comp_qshift or []) else 0
+    p.qderived = int(bool(qderived))
     p.cod_format = 2 if jp2 else 0
     if layer_rate:
         p.nlayers = len(layer_rate)

@@ -40,3 +40,12 @@ def test_changing_markers_engine_refuses(eng, name):
         with pytest.raises(RuntimeError, match="not supported on this path|bad component number"):
             eng.decode(cs)
     np.testing.assert_array_equal(eng.decode(fx.cs), fx.grok_decoded)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_main_qcc_engine_equals_oracle(eng, name):
+    import j2k_markers as J
+    import oracle as O
+    fx = _fx(name)
+    cs = J.insert_main(fx.cs, J.qcc(fx.cs, J.ncomp(fx.cs) - 1, guard_add=1))
+    np.testing.assert_array_equal(eng.decode(cs), O.decode(cs)[0])

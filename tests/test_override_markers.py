@@ -1,10 +1,11 @@
 """COC / QCC and tile-part COD / QCD markers in the oracle decoder.
 
 Grok reads COC / QCC (CodeStreamDecompress read_coc / read_qcc) and tile-part COD / QCD as
-per-component / per-tile overrides of the main COD / QCD.  This path codes every tile-component
-with the main header's parameters, so a marker that restates them decodes exactly as the stream
-without it (some encoders write them unconditionally), and one that changes them is refused
-rather than ignored.  Streams: the committed Grok fixtures with markers spliced in
+per-component / per-tile overrides of the main COD / QCD.  A main-header QCC is applied to its
+component (tests/test_qcc.py); otherwise this path codes every tile-component with the main
+header's parameters, so a marker that restates them decodes exactly as the stream without it
+(some encoders write them unconditionally), and one that changes them is refused rather than
+ignored.  Streams: the committed Grok fixtures with markers spliced in
 (tests/j2k_markers.py).  The engine half is tests/test_gpu_override_markers.py.
 """
 import os
@@ -34,7 +35,6 @@ def restating(cs):
 
 def changing(cs):
     yield "main COC", J.insert_main(cs, J.coc(cs, 0, sty_xor=0x02))
-    yield "main QCC", J.insert_main(cs, J.qcc(cs, J.ncomp(cs) - 1, guard_add=1))
     yield "tile COD", J.insert_tile_part(cs, J.cod(cs, layers_add=1))
     yield "tile COC", J.insert_tile_part(cs, J.coc(cs, 0, sty_xor=0x08))
     yield "tile QCC", J.insert_tile_part(cs, J.qcc(cs, 0, guard_add=1))
@@ -57,3 +57,19 @@ def test_changing_markers_refused(name):
     for what, cs in changing(fx.cs):
         with pytest.raises(RuntimeError, match="failed: -2"):
             O.decode(cs)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_main_qcc_applies_to_its_component(name):
+    # a main-header QCC with one more guard bit raises that component's band bit-plane counts
+    # (Quantizer.cpp:47), so a Part-1 block's bit-planes (band count less the packet header's zero
+    # bit-planes) move up one: the stream decodes, differently; HT places the magnitude by the
+    # zero bit-plane count alone (k_msbs), so its samples stay
+    fx = _fx(name)
+    n = J.ncomp(fx.cs)
+    got, _ = O.decode(J.insert_main(fx.cs, J.qcc(fx.cs, n - 1, guard_add=1)))
+    assert got.shape == fx.grok_decoded.shape
+    if fx.ht:
+        np.testing.assert_array_equal(got, fx.grok_decoded)
+    else:
+        assert not np.array_equal(got, fx.grok_decoded)
