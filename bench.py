@@ -268,6 +268,35 @@ class Runner:
         self.eng.close()
 
 
+class InFlightRunner:
+    """Runners driven concurrently, each from its own host thread with its own engine (HIP stream
+    and buffers): one step = every runner's step once.  With the headline pair (one C2 and one
+    C3 image) the host phases of one image (PCRD, packet headers) overlap the other's kernels."""
+
+    def __init__(self, runners):
+        from concurrent.futures import ThreadPoolExecutor
+        self.rs = runners
+        self.pixels = sum(r.pixels for r in runners)
+        self.n = sum(r.n for r in runners)
+        self.pool = ThreadPoolExecutor(len(runners))
+
+    def step(self):
+        for f in [self.pool.submit(r.step) for r in self.rs]:
+            f.result()
+        self.n = sum(r.n for r in self.rs)
+        return {}
+
+    def check(self):
+        for r in self.rs:
+            r.check()
+        self.n = sum(r.n for r in self.rs)
+
+    def close(self):
+        self.pool.shutdown()
+        for r in self.rs:
+            r.close()
+
+
 class BatchRunner:
     """`nimg` images in flight on one GPU: each has its own engine (own HIP stream and
     buffers) and is driven from its own host thread, so one image's host T2 and
@@ -624,6 +653,18 @@ def main():
     aux = None
     if not args.no_aux and args.config == "C2+C3":
         aux = {}
+        # the headline pair with both images in flight (one host thread and engine each)
+        rp = InFlightRunner([Runner("C2", args.size, rank, device), Runner("C3", args.size, rank, device)])
+        rp.check()
+        elp, _ = timed(rp, 3, 1, world, dist, device)
+        aux["C2+C3_inflight"] = {"config": "the headline step (one C2 and one C3 image encoded + decoded) with both images "
+                                           "in flight on the GPU (2 engines / HIP streams, one host thread each: the "
+                                           "host PCRD and packet phases of one image overlap the other's kernels)",
+                                 "value": round(rp.pixels / 1e6 * world * 3 / elp, 3), "unit": "Mpixels/s",
+                                 "ms_per_step": round(elp * 1000.0 / 3, 3), "parallelism": "replicas x%d" % world}
+        rp.close()
+        del rp
+        torch.cuda.empty_cache()
         # C2 with two images in flight per GPU (throughput of overlapped independent jobs)
         rb = BatchRunner("C2", 2, rank, device)
         rb.check()
