@@ -2274,6 +2274,11 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
                 const uint32_t nb = P.p.irrev ? (P.p.numres - 1) - (r ? r - 1 : 0) : 1u;
                 B = std::max(B, Bd.expn + P.p.numgbits - nb);
             }
+        // an ROI upshift adds its bit-planes to the coded magnitudes (15444-15 A.2: MAGBp bounds
+        // them; Grok's encoder never applies the shift to HT blocks)
+        uint32_t rmax = 0;
+        for (uint32_t c = 0; c < P.nc; ++c) rmax = std::max(rmax, P.p.roi(c));
+        B += rmax;
         uint32_t Bp = B <= 8 ? 0 : B < 28 ? B - 8 : B < 48 ? 13 + (B >> 2) : 31;
         put16(o, 0xff50); put16(o, 8); put32(o, 0x00020000); put16(o, (P.p.irrev ? 0x20 : 0) | Bp);
     }
@@ -2735,8 +2740,6 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     check_poc_coverage(want.p, want.nc);
     if ((want.p.cblk_sty & GK_STY_HT) && want.p.cblk_sty != GK_STY_HT)
         throw GkError("HTJ2K cannot be combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781
-    for (uint8_t v : want.p.roishift)
-        if (v && want.p.ht()) throw GkError("ROI with HTJ2K is not supported on this path");
     if (want.p.cblk_sty > 0x7f) throw GkError("unknown code-block style bits");
     if (want.nc > 255 || want.nc == 0) throw GkError("bad component count");
     if (want.prec == 0 || want.prec > 31) throw GkError("component precision must be 1..31 bits");
@@ -3710,8 +3713,6 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     }
     if (!tlm_ok) walk_sot_chain(S, Hd);
     if (Hd.parts.empty()) throw GkError("no tile parts");
-    for (uint8_t v : W.p.roishift)   // Grok's RoiShiftHTFilter keeps only the sign of a shifted sample
-        if (v && W.p.ht()) throw GkError("ROI with HTJ2K is not supported on this path");
 }
 
 // Device-resident codestream: copy scattered ranges (tile-part headers, packet headers) to

@@ -31,6 +31,9 @@
 #define HT_LINE_STD 36
 #define HT_WG_WIDE 64
 #define HT_LINE_WIDE 516
+#ifndef HT_OUTC
+#define HT_OUTC 16          // decoder output staging: columns per flush (8 or 16)
+#endif
 
 // MEL exponent table {0,0,0,1,1,1,2,2,2,3,3,4,5} packed 3 bits per state
 __device__ __forceinline__ int mel_exp(int k) {
@@ -181,6 +184,9 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
     // coefficient, trunc(x * (1 / stepsize)) (R-BUG-2: Grok reads the float bits as an int)
     const bool irrev = G.flags & 1;
     const float inv_step = irrev ? 1.0f / G.step : 0.0f;
+    // ROI maxshift (the component is the region): every index magnitude scaled up by 2^shift, the
+    // band's bit-plane count raised by it (standard-correct; Grok's encoder only raises the count)
+    const uint32_t rshift = G.flags >> 3;
     // columns [x8, x8 + 8) of rows y, y + 1 into the staging (zeros outside the block)
     auto stage = [&](uint32_t x8, uint32_t y) {
         const uint32_t nc = x8 < w ? min(8u, w - x8) : 0u;
@@ -198,7 +204,8 @@ __global__ __launch_bounds__(HT_WG) void k_ht_enc(const int32_t* __restrict__ co
     };
     auto ld = [&](uint32_t x, uint32_t y) -> int32_t {
         const int32_t raw = s_in[y & 1][x & 7][tid];
-        return irrev ? (int32_t)(__int_as_float(raw) * inv_step) : raw;
+        const int32_t v = irrev ? (int32_t)(__int_as_float(raw) * inv_step) : raw;
+        return v < 0 ? -(int32_t)((uint32_t)-v << rshift) : (int32_t)((uint32_t)v << rshift);
     };
     // one quad: samples (x,y) (x,y+1) (x+1,y) (x+1,y+1) -> rho, exponents, MagSgn values
     auto quad = [&](uint32_t x, uint32_t y, int& rho, int* e, uint32_t* sv, int& emax) {
@@ -380,10 +387,12 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     __shared__ uint16_t s_tab[2][1024];
     __shared__ uint8_t s_e[HT_LINE][HT_WG];
     __shared__ uint8_t s_cx[HT_LINE][HT_WG];
-    // Output staging: a lane's samples of 8 columns x 2 rows, stored as two 16-byte pieces per row
-    // once the 8 columns are decoded.  Storing each sample as it is decoded made every store a
-    // 64-line scatter (one block per lane): C4 k_ht_dec 9.0 ms, 4.9 ms with no stores at all.
-    __shared__ uint32_t s_out[2][8][HT_WG];
+    // Output staging: a lane's samples of HT_OUTC columns x 2 rows, stored as HT_OUTC / 4 16-byte
+    // pieces per row once those columns are decoded.  Storing each sample as it is decoded made
+    // every store a 64-line scatter (one block per lane): C4 k_ht_dec 9.0 ms, 4.9 ms with no stores
+    // at all; 8 columns (32 bytes per row and flush) wrote 1.5x the samples (partial 128-byte lines
+    // written back more than once, `profiles/r05b_C4_pmc.txt`), 16 columns write half lines.
+    __shared__ uint32_t s_out[2][HT_OUTC][HT_WG];
     const int tid = threadIdx.x;
     for (int i = tid; i < 1024; i += HT_WG) { s_tab[0][i] = HT_VLC_DEC0[i]; s_tab[1][i] = HT_VLC_DEC1[i]; }
     __syncthreads();
@@ -411,6 +420,10 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
     const uint32_t kmsbs = (uint32_t)G.band_numbps - (uint32_t)G.numbps;
     if (G.npasses && lcup && kmsbs > 29) { atomicOr(err, 4); zero_block(); return; }
     const uint32_t pbit = 30 - kmsbs;
+    // ROI maxshift on the indices: a magnitude at or above 2^shift is the region's and scales back
+    // down (standard-correct; Grok's RoiShiftHTFilter / RoiScaleHTFilter, PostDecompressFilters.h:
+    // 92-158, AND the shifted magnitude with the sign bit, R-BUG-9, and are not reproduced)
+    const uint32_t rshift = G.flags >> 3;
     if (!G.npasses || lcup < 2) {
         if (lcup == 1 || (G.npasses && lcup)) atomicOr(err, 4);
         zero_block();
@@ -522,7 +535,8 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
                 else v = (m ? ms_get(m) : 0u) | ((uint32_t)((e1 >> n) & 1) << m);
                 const uint32_t mu = (v >> 1) + 1;
                 e[n] = 32 - __clz(2 * mu - 1);
-                val = (v & 1) ? -(int32_t)mu : (int32_t)mu;
+                const uint32_t mo = (rshift && mu >= (1u << rshift)) ? mu >> rshift : mu;
+                val = (v & 1) ? -(int32_t)mo : (int32_t)mo;
             }
             uint32_t bits = (uint32_t)val;
             if (irrev) {
@@ -530,17 +544,19 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
                 const float f = (float)mag * G.step;
                 bits = __float_as_uint(val < 0 ? -f : f);
             }
-            s_out[yy & 1][xx & 7][tid] = bits;
+            s_out[yy & 1][xx & (HT_OUTC - 1)][tid] = bits;
         }
     };
-    // columns [x8, x8 + 8) of rows y, y + 1 (those inside the block) from the staging
+    // columns [x8, x8 + HT_OUTC) of rows y, y + 1 (those inside the block) from the staging
     auto flush = [&](uint32_t x8, uint32_t y) {
-        const uint32_t nc = min(8u, w - x8);
+        const uint32_t nc = min((uint32_t)HT_OUTC, w - x8);
         for (uint32_t r = 0; r < 2 && y + r < h; ++r) {
             uint32_t* row = reinterpret_cast<uint32_t*>(dst + (size_t)(y + r) * stride + x8);
-            if (nc == 8 && ((uintptr_t)row & 15) == 0) {
-                reinterpret_cast<uint4*>(row)[0] = make_uint4(s_out[r][0][tid], s_out[r][1][tid], s_out[r][2][tid], s_out[r][3][tid]);
-                reinterpret_cast<uint4*>(row)[1] = make_uint4(s_out[r][4][tid], s_out[r][5][tid], s_out[r][6][tid], s_out[r][7][tid]);
+            if (nc == HT_OUTC && ((uintptr_t)row & 15) == 0) {
+#pragma unroll
+                for (uint32_t k = 0; k < HT_OUTC; k += 4)
+                    reinterpret_cast<uint4*>(row)[k / 4] =
+                        make_uint4(s_out[r][k][tid], s_out[r][k + 1][tid], s_out[r][k + 2][tid], s_out[r][k + 3][tid]);
             } else {
                 for (uint32_t k = 0; k < nc; ++k) row[k] = s_out[r][k][tid];
             }
@@ -621,7 +637,7 @@ __global__ __launch_bounds__(HT_WG) void k_ht_dec(const uint8_t* __restrict__ by
             }
             if (first) c_q0 = (rho[1] >> 1) | (rho[1] & 1);
             else c_q0 |= ((rho[1] & 4) >> 1) | ((rho[1] & 8) >> 2);
-            if ((x & 4) || x + 4 >= w) flush(x & ~7u, y);
+            if ((x & (HT_OUTC - 4)) == HT_OUTC - 4 || x + 4 >= w) flush(x & ~(uint32_t)(HT_OUTC - 1), y);
         }
         if (first) s_e[li + 1][tid] = 0;
     }

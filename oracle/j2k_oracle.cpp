@@ -1307,6 +1307,11 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
                 const uint32_t nb = p.irreversible ? (p.numres - 1) - (r ? r - 1 : 0) : 1u;
                 B = std::max(B, Bd.expn + p.numgbits - nb);
             }
+        // an ROI upshift adds its bit-planes to the magnitudes (15444-15 A.2: MAGBp bounds the
+        // coded magnitude bit-planes; Grok's encoder never applies the shift)
+        uint32_t rmax = 0;
+        for (uint32_t c = 0; c < im.nc; ++c) rmax = std::max(rmax, p.roi(c));
+        B += rmax;
         uint32_t Bp = B <= 8 ? 0 : B < 28 ? B - 8 : B < 48 ? 13 + (B >> 2) : 31;
         put16(o, 0xff50); put16(o, 8); put32(o, 0x00020000); put16(o, (p.irreversible ? 0x20 : 0) | Bp);
     }
@@ -2128,14 +2133,23 @@ static void t1_encode_all(EncodeState& E) {
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
                         if (E.p.ht()) {   // T1HT::compress (T1HT.cpp:109-133): one cleanup pass
                             const size_t o0 = (size_t)(B.offy + K.y0 - B.y0) * C.w + (B.offx + K.x0 - B.x0);
-                            if (E.p.irreversible) {
+                            // ROI maxshift (standard-correct, the component is the region: every
+                            // index magnitude scaled up by 2^shift, the band's bit-plane count raised
+                            // by it; Grok refuses nothing but its encoder only raises the count,
+                            // CodeStreamCompress.cpp:538-541)
+                            const uint32_t rs = E.p.roi(c);
+                            auto roi_up = [&](int32_t v) { return rs ? (v < 0 ? -(int32_t)((uint32_t)-v << rs) : (int32_t)((uint32_t)v << rs)) : v; };
+                            if (E.p.irreversible || rs) {
                                 // T1HT::preCompress irreversible branch (T1HT.cpp:88-104) on the 9/7
                                 // coefficients as floats (R-BUG-2: Grok reads the float bits as
                                 // int32): index = trunc(x * (1 / stepsize))
-                                const float inv = 1.0f / B.stepsize;
+                                const float inv = E.p.irreversible ? 1.0f / B.stepsize : 0.0f;
                                 std::vector<int32_t> q((size_t)w * h);
                                 for (uint32_t y = 0; y < h; ++y)
-                                    for (uint32_t x = 0; x < w; ++x) q[(size_t)y * w + x] = (int32_t)(E.fcoefs[c][o0 + (size_t)y * C.w + x] * inv);
+                                    for (uint32_t x = 0; x < w; ++x) {
+                                        const size_t o = o0 + (size_t)y * C.w + x;
+                                        q[(size_t)y * w + x] = roi_up(E.p.irreversible ? (int32_t)(E.fcoefs[c][o] * inv) : E.coefs[c][o]);
+                                    }
                                 K.data = ht_encode_block(q.data(), w, h, w);
                             } else
                             K.data = ht_encode_block(E.coefs[c].data() + o0, w, h, C.w);
@@ -2944,7 +2958,21 @@ t2done:
                                 jrc[ji] = -4;
                                 return;
                             }
-                            if (!p.irreversible) for (auto& v : blk) v *= 2;   // same ShiftFilter below
+                            // ROI maxshift on the indices (standard-correct: a magnitude at or above
+                            // 2^shift is the region's, scaled back down; Grok's RoiShiftHTFilter /
+                            // RoiScaleHTFilter, PostDecompressFilters.h:92-158, AND the shifted
+                            // magnitude with the sign bit, R-BUG-9, and are not reproduced)
+                            if (const uint32_t rs = p.roi(c))
+                                for (auto& v : blk) {
+                                    const uint32_t m = (uint32_t)(v < 0 ? -v : v);
+                                    if (m >= (1u << rs)) v = v < 0 ? -(int32_t)(m >> rs) : (int32_t)(m >> rs);
+                                }
+                            if (!p.irreversible) {   // ShiftHTFilter: the index is the coefficient
+                                for (uint32_t y = 0; y < h; ++y)
+                                    for (uint32_t x = 0; x < w; ++x)
+                                        ip[c][(size_t)(B.offy + K.y0 - B.y0 + y) * TW + (B.offx + K.x0 - B.x0 + x)] = blk[y * w + x];
+                                return;
+                            }
                             else {
                                 // ScaleHTFilter (PostDecompressFilters.h:161-176): the decoder's 32-bit
                                 // sample (magnitude LSB at p = 30 - k_msbs, ojph_block_decoder.cpp:1222)

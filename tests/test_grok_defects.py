@@ -12,6 +12,13 @@ cross-decoded by OpenJPEG 2.5.4 (Pillow), an independent decoder (SURVEY.md sect
            count, a few bytes off the tile part.  Reproduced byte for byte (the known answers in
            test_oracle_grok_sizes.py); OpenJPEG rejects such streams, the oracle (and the engine,
            test_gpu_grok_known.py) resynchronise on the next SOT.
+  R-BUG-9  ROI with the HT block coder: Grok's RoiShiftHTFilter / RoiScaleHTFilter
+           (PostDecompressFilters.h:92-158) test the raw 32-bit decoder sample against 2^shift
+           and AND the shifted magnitude with the sign bit, so every region sample decodes to
+           zero; its encoder only raises the band bit-plane count (CodeStreamCompress.cpp:538-541).
+           Ours is the standard maxshift on the HT indices (test_roi_htj2k_round_trip below); no
+           independent decoder pins it (OpenJPEG 2.5.4 refuses RGN with HT), so it is oracle-
+           restated and GPU-tested against the oracle (tests/test_gpu_roi.py).
 """
 import io
 
@@ -83,3 +90,17 @@ def test_single_odd_sample_rule(v, vertical, partial, want):
     # differently in its whole-tile and window decodes, and so do the oracle and the engine
     # (gk_dwt_any.hip inv53_line, ctx->dwt_partial)
     assert O.lib().orc_inv53_single(v, 1, int(vertical), int(partial)) == want
+
+
+@pytest.mark.parametrize("roi,irr", [((0, 4), False), ((1, 6), False), ((2, 3), True)])
+def test_roi_htj2k_round_trip(roi, irr):
+    # R-BUG-9: the standard maxshift on HT indices; 5/3 lossless, 9/7 at its usual distortion, and
+    # the same image without ROI decodes alike (the shift only lifts the region above background)
+    img = synth_image(120, 136, 3, 8, 90 + roi[1]).astype(np.int32)
+    cs = O.encode(img, 8, numres=4, irreversible=irr, roi=roi, cblk_sty=0x40)
+    assert b"\xff\x5e" in cs
+    dec, _ = O.decode(cs)
+    plain, _ = O.decode(O.encode(img, 8, numres=4, irreversible=irr, cblk_sty=0x40))
+    if not irr:
+        np.testing.assert_array_equal(dec, img)
+    np.testing.assert_array_equal(dec, plain)
