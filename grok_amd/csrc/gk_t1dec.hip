@@ -1208,11 +1208,13 @@ void gk_launch_t1_dec(hipStream_t st, const uint8_t* bytes, const GkBlock* block
                         " busiest lane %llu decisions in a wave of %llu steps\n",
                 (nblocks + 63) / 64, h[0], h[1], h[2], (double)h[0] / ((nblocks + 63) / 64), (double)h[1] / (64.0 * h[0]),
                 (double)h[3] / ((nblocks + 63) / 64), h[12] >> 32, h[12] & 0xffffffffull);
-        if (nsolo)
-            fprintf(stderr, "t1dec solo: %u waves, decisions %llu, max per wave %llu%s\n", nsolo, h[13], h[14],
-                    timing ? (", cycles/decision " + std::to_string((double)h[16] / (double)(h[13] ? h[13] : 1)) +
-                              ", longest wave " + std::to_string(h[15] >> 20) + " cycles for " +
-                              std::to_string(h[15] & 0xfffff) + " decisions").c_str() : "");
+        if (nsolo) {
+            const std::string tail = timing ? ", cycles/decision " + std::to_string((double)h[16] / (double)(h[13] ? h[13] : 1)) +
+                                                  ", longest wave " + std::to_string(h[15] >> 20) + " cycles for " +
+                                                  std::to_string(h[15] & 0xfffff) + " decisions"
+                                            : std::string();
+            fprintf(stderr, "t1dec solo: %u waves, decisions %llu, max per wave %llu%s\n", nsolo, h[13], h[14], tail.c_str());
+        }
         if (timing)
             fprintf(stderr, "t1dec timing: cycles/event %.0f cycles/step %.0f (event share %.3f)\n",
                     (double)h[4] / (double)(h[3] ? h[3] : 1), (double)h[5] / (double)(h[0] ? h[0] : 1),
