@@ -24,7 +24,7 @@ GK_MAX_LAYERS = 100
 EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_encode_tiles", "gk_main_header",
            "gk_jp2_header", "gk_decode_header", "gk_probe_header", "gk_decode", "gk_decode_window", "gk_get_timings",
            "gk_last_error", "gk_version", "gk_set_decode_layers", "gk_set_decode_reduce",
-           "gk_set_window_rule")
+           "gk_set_window_rule", "gk_set_subsampling", "gk_probe_components", "gk_header_subsampling")
 
 
 class Poc(ctypes.Structure):
@@ -115,6 +115,13 @@ def load_library(build_if_missing=True):
     lib.gk_set_decode_reduce.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     lib.gk_set_window_rule.restype = ctypes.c_int
     lib.gk_set_window_rule.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.gk_set_subsampling.restype = ctypes.c_int
+    lib.gk_set_subsampling.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_uint32), P(ctypes.c_uint32)]
+    lib.gk_probe_components.restype = ctypes.c_int
+    lib.gk_probe_components.argtypes = [ctypes.c_void_p, ctypes.c_size_t, P(ctypes.c_uint32), P(ctypes.c_uint32),
+                                        ctypes.c_uint32]
+    lib.gk_header_subsampling.restype = ctypes.c_int
+    lib.gk_header_subsampling.argtypes = [ctypes.c_void_p, P(ctypes.c_uint32), P(ctypes.c_uint32), ctypes.c_uint32]
     lib.gk_set_decode_layers.restype = ctypes.c_int
     lib.gk_set_decode_layers.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     lib.gk_decode.restype = ctypes.c_int
@@ -197,6 +204,27 @@ def probe_header(cs):
     return info
 
 
+def probe_components(cs):
+    """gk_probe_components: [(dx, dy)] per component of host codestream / JP2 bytes (SIZ XRsiz / YRsiz)."""
+    lib = load_library()
+    b = np.frombuffer(bytes(cs), np.uint8)
+    dx, dy = (ctypes.c_uint32 * 16384)(), (ctypes.c_uint32 * 16384)()
+    n = lib.gk_probe_components(b.ctypes.data, len(b), dx, dy, 16384)
+    if n < 0:
+        raise ValueError("gk_probe_components failed")
+    return [(dx[c], dy[c]) for c in range(n)]
+
+
+def comp_shape(w, h, dx, dy, origin=(0, 0), reduce=0):
+    """(rows, cols) of a component sampled every (dx, dy) canvas positions over the image area
+    [x0, x0 + w) x [y0, y0 + h) (grk_image_comp h / w), reduced by `reduce` resolutions."""
+    x0, y0 = origin
+    cd = lambda a, b: -(-a // b)
+    cx0, cy0, cx1, cy1 = cd(x0, dx), cd(y0, dy), cd(x0 + w, dx), cd(y0 + h, dy)
+    r = 1 << reduce
+    return cd(cy1, r) - cd(cy0, r), cd(cx1, r) - cd(cx0, r)
+
+
 def _sample_bytes(x):
     """gk_image_info::sample_bytes of a plane array (numpy or torch): 0 for 32-bit, else its item size."""
     n = x.element_size() if hasattr(x, "element_size") else x.dtype.itemsize
@@ -259,14 +287,18 @@ class Engine:
         return t
 
     # ------------------------------------------------------------------ encode
-    def encode(self, planes, prec, signed=False, params=None, out=None, origin=None):
+    def encode(self, planes, prec, signed=False, params=None, out=None, origin=None, subsampling=None, size=None):
         """planes: (C, H, W) int32 numpy array (host) or torch cuda tensor (device).
         Returns bytes (host) or, when ``out`` (a torch cuda uint8 tensor) is given,
         the codestream length written into it on the device.  origin: the image area's
         canvas origin (grk_image::x0 / y0, grk_compress -d); without it the image sits at
-        the tile grid origin (-T alone moves the image there, grk_compress.cpp:1547-1551)."""
+        the tile grid origin (-T alone moves the image there, grk_compress.cpp:1547-1551).
+        subsampling=[(dx, dy), ...] (grk_image_comp::dx / dy): planes is then a list of 2-D
+        planes of comp_shape(W, H, dx, dy, origin) each and size=(W, H) the image area."""
         if params is None:
             params = default_params()
+        if subsampling:
+            return self._encode_subsampled(planes, prec, signed, params, out, origin, subsampling, size)
         c, h, w = planes.shape
         on_dev = _is_torch_cuda(planes)
         if on_dev:
@@ -302,6 +334,49 @@ class Engine:
         if rc != 0:
             self._err("gk_encode")
         return buf[:n.value].tobytes()
+
+    def _encode_subsampled(self, planes, prec, signed, params, out, origin, subsampling, size):
+        c = len(planes)
+        w, h = size
+        on_dev = _is_torch_cuda(planes[0])
+        keep = [p if on_dev else _host_planes(p, prec) for p in planes]
+        sb = _sample_bytes(keep[0])
+        info = ImageInfo(w, h, c, prec, int(signed), sb)
+        if origin is not None:
+            info.x0, info.y0 = int(origin[0]), int(origin[1])
+        else:
+            info.x0, info.y0 = params.tx0, params.ty0
+        for k, (dx, dy) in enumerate(subsampling):
+            assert tuple(keep[k].shape) == comp_shape(w, h, dx, dy, (info.x0, info.y0)), (k, tuple(keep[k].shape))
+        ptrs = (ctypes.c_void_p * c)(*[p.data_ptr() if on_dev else p.ctypes.data for p in keep])
+        strides = (ctypes.c_uint32 * c)(*[p.shape[1] for p in keep])
+        dxs = (ctypes.c_uint32 * c)(*[int(d[0]) for d in subsampling])
+        dys = (ctypes.c_uint32 * c)(*[int(d[1]) for d in subsampling])
+        if self.lib.gk_set_subsampling(self.ctx, c, dxs, dys) != 0:
+            self._err("gk_set_subsampling")
+        try:
+            n = ctypes.c_size_t()
+            if out is not None:
+                rc = self.lib.gk_encode(self.ctx, ctypes.byref(info), ptrs, strides, int(on_dev), ctypes.byref(params),
+                                        ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(n), 1)
+                if rc != 0:
+                    self._err("gk_encode")
+                return n.value
+            cap = c * h * w * 4 + (1 << 20)
+            buf = np.empty(cap, np.uint8)
+            rc = self.lib.gk_encode(self.ctx, ctypes.byref(info), ptrs, strides, int(on_dev), ctypes.byref(params),
+                                    buf.ctypes.data, cap, ctypes.byref(n), 0)
+            if rc != 0:
+                self._err("gk_encode")
+            return buf[:n.value].tobytes()
+        finally:
+            self.lib.gk_set_subsampling(self.ctx, 0, None, None)
+
+    def subsampling(self):
+        """[(dx, dy)] per component of the stream the last read_header / decode read."""
+        dx, dy = (ctypes.c_uint32 * 16384)(), (ctypes.c_uint32 * 16384)()
+        n = self.lib.gk_header_subsampling(self.ctx, dx, dy, 16384)
+        return [(dx[c], dy[c]) for c in range(max(n, 0))]
 
     def _planes_ptrs(self, planes, row0=0, prec=32):
         """Component base pointers addressing image row 0 for a (C, rows, W) slab whose
@@ -456,6 +531,9 @@ class Engine:
         info = self.read_header(cs, length)
         c, h, w = info.numcomps, info.h, info.w
         red = getattr(self, "_reduce", 0)
+        sub = self.subsampling()
+        if any(d != (1, 1) for d in sub):
+            return self._decode_subsampled(cs, length, out, sample_bytes, info, sub, red)
         if red:   # reduced-resolution output: the image area on the reduced canvas (ceil(x / 2^reduce))
             cd = lambda v: -(-v // (1 << red))
             h, w = cd(info.y0 + h) - cd(info.y0), cd(info.x0 + w) - cd(info.x0)
@@ -474,6 +552,32 @@ class Engine:
             ptrs = (ctypes.c_void_p * c)(*[base + k * h * w * es for k in range(c)])
             out_dev = 0
         if on_dev:
+            rc = self.lib.gk_decode(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, ptrs, strides, sample_bytes,
+                                    out_dev)
+        else:
+            b = np.frombuffer(cs, np.uint8)
+            rc = self.lib.gk_decode(self.ctx, b.ctypes.data, len(cs), 0, ptrs, strides, sample_bytes, out_dev)
+        if rc != 0:
+            self._err("gk_decode")
+        return res
+
+    def _decode_subsampled(self, cs, length, out, sample_bytes, info, sub, red):
+        """Subsampled components: a list of 2-D planes, component c of comp_shape(W, H, dx, dy,
+        origin, reduce); ``out`` (torch cuda) is then a list of such tensors filled in place."""
+        c = info.numcomps
+        shapes = [comp_shape(info.w, info.h, dx, dy, (info.x0, info.y0), red) for dx, dy in sub]
+        if out is not None:
+            assert len(out) == c and all(tuple(o.shape) == s for o, s in zip(out, shapes))
+            sample_bytes = _sample_bytes(out[0])
+            res, out_dev = out, 1
+            ptrs = (ctypes.c_void_p * c)(*[o.data_ptr() for o in out])
+            strides = (ctypes.c_uint32 * c)(*[o.stride(0) for o in out])
+        else:
+            res = [np.empty(s, _np_sample_dtype(sample_bytes, info)) for s in shapes]
+            out_dev = 0
+            ptrs = (ctypes.c_void_p * c)(*[r.ctypes.data for r in res])
+            strides = (ctypes.c_uint32 * c)(*[s[1] for s in shapes])
+        if _is_torch_cuda(cs):
             rc = self.lib.gk_decode(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, ptrs, strides, sample_bytes,
                                     out_dev)
         else:

@@ -289,8 +289,34 @@ struct ShapeG {
     GkTiles tb;
 };
 
+// Components sampled on one grid (SIZ XRsiz / YRsiz; grk_image_comp::dx / dy): their
+// tile-components are the tiles divided by (dx, dy), rounded up (TileProcessor.cpp:116-131), so
+// they share one set of tile classes and DWT launches.  Without subsampling there is one group
+// holding every component.
+struct SGroup {
+    uint32_t dx = 1, dy = 1;
+    uint32_t ox = 0, oy = 0;             // the image area's origin on the group's grid: ceil(x0 / dx), ceil(y0 / dy)
+    uint32_t w = 0, h = 0;               // its extent there (grk_image_comp w / h): a component plane's size
+    std::vector<ShapeG> shapes;          // tile classes on the group's grid
+    std::vector<int> shape_of;           // tile -> class
+    std::vector<std::pair<uint32_t, uint32_t>> runs;   // its components as contiguous ranges [c0, c1)
+};
+
 struct Plan {
     uint32_t w = 0, h = 0, nc = 0, prec = 0, sgnd = 0;
+    std::vector<uint8_t> cdx, cdy;       // per component subsampling (empty: none)
+    uint32_t sx(uint32_t c) const { return c < cdx.size() ? cdx[c] : 1u; }
+    uint32_t sy(uint32_t c) const { return c < cdy.size() ? cdy[c] : 1u; }
+    bool subsampled() const {
+        for (uint32_t c = 0; c < nc; ++c) if (sx(c) != 1 || sy(c) != 1) return true;
+        return false;
+    }
+    // the inverse / forward MCT: COD's flag, three components or more, the first three on one
+    // grid (Grok's encoder clears the flag otherwise, CodeStreamCompress.cpp:501-512; its decoder
+    // skips the transform, TileProcessor::needsMctDecompress :432-456)
+    bool mct3() const {
+        return p.mct && nc >= 3 && sx(1) == sx(0) && sx(2) == sx(0) && sy(1) == sy(0) && sy(2) == sy(0);
+    }
     // canvas (B.2-B.3): the image area starts at (x0, y0), the tile grid at (gx0, gy0) <= (x0, y0).
     // Tile and band geometry are canvas coordinates; work planes hold the image area, so a plane
     // position is a canvas position less (x0, y0).
@@ -300,8 +326,9 @@ struct Plan {
     size_t plane_elems = 0;              // per plane
     uint32_t ntx = 1, nty = 1, tw = 0, th = 0;   // tile grid
     std::vector<TileG> tiles;            // raster order
-    std::vector<ShapeG> shapes;
-    bool l1_fusable = true;              // every tile origin even: level 1 fuses with DC shift / MCT
+    std::vector<SGroup> groups;          // sampling grids (one without subsampling)
+    std::vector<uint32_t> group_of;      // component -> group
+    bool l1_fusable = true;              // every tile(-component) origin even: level 1 fuses with DC shift / MCT
     std::vector<GkBlock> blocks;         // tile order, then canonical: comp, res, band, precinct, cblk
     std::vector<uint32_t> bxy;           // per block: top-left (x, y) in its band's coordinates
     uint64_t slot_bytes = 0;
@@ -485,18 +512,28 @@ static void parse_quant(const std::vector<uint8_t>& b, uint32_t numres, QuantLis
     }
 }
 
-static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
+static inline uint32_t ceildiv(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + b - 1) / b); }
+
+static void build_tile(Plan& P, TileG& T, uint32_t t) {
     const uint32_t L = P.p.numres - 1;
     T.comps.assign(P.nc, CompG());
     T.b0 = (uint32_t)P.blocks.size();
+    // tile-component c: the tile divided by its component's subsampling (the tile itself without)
+    std::vector<uint32_t> tcx0(P.nc), tcy0(P.nc), tcx1(P.nc), tcy1(P.nc);
+    for (uint32_t c = 0; c < P.nc; ++c) {
+        tcx0[c] = ceildiv(T.x0, P.sx(c)); tcy0[c] = ceildiv(T.y0, P.sy(c));
+        tcx1[c] = ceildiv(T.x1, P.sx(c)); tcy1[c] = ceildiv(T.y1, P.sy(c));
+    }
     for (uint32_t c = 0; c < P.nc; ++c) {
         CompG& C = T.comps[c];
+        const SGroup& G = P.groups[P.group_of[c]];
+        const ShapeG& S = G.shapes[G.shape_of[t]];
         C.res.assign(P.p.numres, ResG());
         for (uint32_t r = 0; r < P.p.numres; ++r) {
             ResG& R = C.res[r];
             const uint32_t nb = L - r;
-            R.x0 = ceildivpow2(T.x0, nb); R.y0 = ceildivpow2(T.y0, nb);
-            R.w = ceildivpow2(T.x1, nb) - R.x0; R.h = ceildivpow2(T.y1, nb) - R.y0;
+            R.x0 = ceildivpow2(tcx0[c], nb); R.y0 = ceildivpow2(tcy0[c], nb);
+            R.w = ceildivpow2(tcx1[c], nb) - R.x0; R.h = ceildivpow2(tcy1[c], nb) - R.y0;
             const uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
             R.px0 = (R.x0 >> pwe) << pwe; R.py0 = (R.y0 >> phe) << phe;
             R.pw = R.w ? ((ceildivpow2(R.x0 + R.w, pwe) << pwe) - R.px0) >> pwe : 0;
@@ -521,7 +558,7 @@ static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
                         if (!o) return ceildivpow2((uint32_t)t, lev);
                         return t <= half ? 0 : ceildivpow2((uint32_t)(t - half), lev);
                     };
-                    B.x0 = cb(T.x0, xo); B.y0 = cb(T.y0, yo); B.x1 = cb(T.x1, xo); B.y1 = cb(T.y1, yo);
+                    B.x0 = cb(tcx0[c], xo); B.y0 = cb(tcy0[c], yo); B.x1 = cb(tcx1[c], xo); B.y1 = cb(tcy1[c], yo);
                     B.level = lev;
                     B.plane = (lev & 1) ? 1 : 0;
                     B.offx = xo ? S.resw[lev] : 0;   // Mallat placement inside the tile rectangle
@@ -534,6 +571,7 @@ static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
     // code-blocks, canonical order (T1CompressScheduler.cpp:31-94); grids are absolute
     for (uint32_t c = 0; c < P.nc; ++c) {
         CompG& C = T.comps[c];
+        const SGroup& SG = P.groups[P.group_of[c]];
         for (uint32_t r = 0; r < P.p.numres; ++r) {
             ResG& R = C.res[r];
             const uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
@@ -562,8 +600,9 @@ static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
                         const uint32_t x1 = std::min(kx0 + (1u << R.cbw), px1), y1 = std::min(ky0 + (1u << R.cbh), py1);
                         GkBlock G{};
                         const size_t plane_base = ((size_t)c * 2 + B.plane) * P.plane_elems;
-                        G.band_off = plane_base + (size_t)(T.y0 - P.y0 + B.offy + y0 - B.y0) * P.stride +
-                                     (T.x0 - P.x0 + B.offx + x0 - B.x0);
+                        // (plane positions on the component's grid, less the image origin there)
+                        G.band_off = plane_base + (size_t)(tcy0[c] - SG.oy + B.offy + y0 - B.y0) * P.stride +
+                                     (tcx0[c] - SG.ox + B.offx + x0 - B.x0);
                         G.stride = P.stride;
                         G.w = (uint16_t)(x1 - x0); G.h = (uint16_t)(y1 - y0);
                         G.orient = (uint8_t)B.orient; G.comp = (uint8_t)c;
@@ -578,7 +617,7 @@ static void build_tile(Plan& P, TileG& T, const ShapeG& S) {
                         {
                             static const double norms_irrev[3] = {1.732, 1.805, 1.573};
                             static const double norms_rev[3] = {1.732, .8292, .8292};
-                            const bool mct = P.p.mct && P.nc >= 3;
+                            const bool mct = P.mct3();
                             double w1 = (mct && c < 3) ? (P.p.irrev ? norms_irrev[c] : norms_rev[c]) : 1.0;
                             G.wmse = w1 * band_norm(P.p.numres - 1 - r, B.orient, !P.p.irrev) * (double)B.step_enc;
                         }
@@ -621,32 +660,54 @@ static void build_plan(Plan& P) {
         v.push_back({n - 1, 1, 1, hi(n - 1) - lo(n - 1), lo(n - 1)});
         return v;
     };
-    const std::vector<Axis> cx = classes(P.ntx, P.tw, P.gx0, P.x0, X1), cy = classes(P.nty, P.th, P.gy0, P.y0, Y1);
-    P.shapes.clear();
+    // sampling groups: components by (XRsiz, YRsiz), in order of first appearance
+    P.groups.clear();
+    P.group_of.assign(P.nc, 0);
+    for (uint32_t c = 0; c < P.nc; ++c) {
+        uint32_t g = 0;
+        while (g < P.groups.size() && (P.groups[g].dx != P.sx(c) || P.groups[g].dy != P.sy(c))) ++g;
+        if (g == P.groups.size()) { P.groups.emplace_back(); P.groups[g].dx = P.sx(c); P.groups[g].dy = P.sy(c); }
+        P.group_of[c] = g;
+        auto& runs = P.groups[g].runs;
+        if (!runs.empty() && runs.back().second == c) runs.back().second = c + 1;
+        else runs.push_back({c, c + 1});
+    }
     P.l1_fusable = true;
-    std::vector<int> shape_of((size_t)P.ntx * P.nty, -1);
-    for (const Axis& ay : cy)
-        for (const Axis& ax : cx) {
-            ShapeG S;
-            S.w = ax.size; S.h = ay.size;
-            const uint32_t x0 = ax.origin, y0 = ay.origin;   // any member: the same geometry
-            S.resw.resize(L + 1); S.resh.resize(L + 1); S.parx.resize(L + 1); S.pary.resize(L + 1);
-            for (uint32_t l = 0; l <= L; ++l) {
-                S.resw[l] = ceildivpow2(x0 + S.w, l) - ceildivpow2(x0, l);
-                S.resh[l] = ceildivpow2(y0 + S.h, l) - ceildivpow2(y0, l);
-                S.parx[l] = (uint8_t)(ceildivpow2(x0, l) & 1);
-                S.pary[l] = (uint8_t)(ceildivpow2(y0, l) & 1);
+    for (SGroup& G : P.groups) {
+        // the tile grid on the group's grid: tile k spans ceil(edge / d) of the canvas tile, a regular
+        // grid (origin ceil(g / d), pitch t / d) when d divides the nominal tile size
+        if ((P.ntx > 1 && P.tw % G.dx) || (P.nty > 1 && P.th % G.dy))
+            throw GkError("a component subsampling factor that does not divide the tile size is not supported on this path");
+        const uint32_t tw = P.ntx > 1 ? P.tw / G.dx : ceildiv(P.tw, G.dx), th = P.nty > 1 ? P.th / G.dy : ceildiv(P.th, G.dy);
+        G.ox = ceildiv(P.x0, G.dx); G.oy = ceildiv(P.y0, G.dy);
+        G.w = ceildiv(X1, G.dx) - G.ox; G.h = ceildiv(Y1, G.dy) - G.oy;
+        const std::vector<Axis> cx = classes(P.ntx, tw, ceildiv(P.gx0, G.dx), G.ox, ceildiv(X1, G.dx));
+        const std::vector<Axis> cy = classes(P.nty, th, ceildiv(P.gy0, G.dy), G.oy, ceildiv(Y1, G.dy));
+        G.shapes.clear();
+        G.shape_of.assign((size_t)P.ntx * P.nty, -1);
+        for (const Axis& ay : cy)
+            for (const Axis& ax : cx) {
+                ShapeG S;
+                S.w = ax.size; S.h = ay.size;
+                const uint32_t x0 = ax.origin, y0 = ay.origin;   // any member: the same geometry
+                S.resw.resize(L + 1); S.resh.resize(L + 1); S.parx.resize(L + 1); S.pary.resize(L + 1);
+                for (uint32_t l = 0; l <= L; ++l) {
+                    S.resw[l] = ceildivpow2(x0 + S.w, l) - ceildivpow2(x0, l);
+                    S.resh[l] = ceildivpow2(y0 + S.h, l) - ceildivpow2(y0, l);
+                    S.parx[l] = (uint8_t)(ceildivpow2(x0, l) & 1);
+                    S.pary[l] = (uint8_t)(ceildivpow2(y0, l) & 1);
+                }
+                if (S.parx[0] || S.pary[0]) P.l1_fusable = false;
+                S.ci = ax.first; S.si = ax.step; S.cj = ay.first; S.sj = ay.step;
+                S.px0 = x0 - G.ox; S.py0 = y0 - G.oy;
+                S.tb.nx = ax.count; S.tb.ny = ay.count; S.tb.i0 = 0; S.tb.j0 = 0;
+                S.tb.dx = ax.step * tw; S.tb.dy = ay.step * th;
+                for (uint32_t b = 0; b < ay.count; ++b)
+                    for (uint32_t a = 0; a < ax.count; ++a)
+                        G.shape_of[(size_t)(ay.first + b * ay.step) * P.ntx + ax.first + a * ax.step] = (int)G.shapes.size();
+                G.shapes.push_back(S);
             }
-            if (S.parx[0] || S.pary[0]) P.l1_fusable = false;
-            S.ci = ax.first; S.si = ax.step; S.cj = ay.first; S.sj = ay.step;
-            S.px0 = x0 - P.x0; S.py0 = y0 - P.y0;
-            S.tb.nx = ax.count; S.tb.ny = ay.count; S.tb.i0 = 0; S.tb.j0 = 0;
-            S.tb.dx = ax.step * P.tw; S.tb.dy = ay.step * P.th;
-            for (uint32_t b = 0; b < ay.count; ++b)
-                for (uint32_t a = 0; a < ax.count; ++a)
-                    shape_of[(size_t)(ay.first + b * ay.step) * P.ntx + ax.first + a * ax.step] = (int)P.shapes.size();
-            P.shapes.push_back(S);
-        }
+    }
     P.tiles.assign((size_t)P.ntx * P.nty, TileG());
     P.blocks.clear();
     P.bxy.clear();
@@ -656,7 +717,7 @@ static void build_plan(Plan& P) {
         const uint32_t i = t % P.ntx, j = t / P.ntx;
         T.x0 = std::max(P.gx0 + i * P.tw, P.x0); T.y0 = std::max(P.gy0 + j * P.th, P.y0);
         T.x1 = std::min(P.gx0 + (i + 1) * P.tw, X1); T.y1 = std::min(P.gy0 + (j + 1) * P.th, Y1);
-        build_tile(P, T, P.shapes[shape_of[t]]);
+        build_tile(P, T, t);
     }
     // encode slots: w*h*4 + 64 bytes each, 64-byte aligned (the MQ coder stores whole 64-byte lines)
     uint64_t off = 0;
@@ -1015,10 +1076,17 @@ static void order_ranges(const Plan& P, const TileG& T, uint32_t prog, uint32_t 
         for (uint32_t r = r0; r < r1; ++r) {
             const ResG& R = T.comps[c].res[r];
             const uint32_t n = np(c, r), lv = nr - 1 - r, pwe = P.p.prcw[r], phe = P.p.prch[r];
+            // where Grok's walk (PacketIter::generatePrecinctIndex, PacketIter.cpp:287-335) first
+            // meets precinct (i, j): the canvas position XRsiz * 2^(PPx + level) * (its grid index),
+            // except a first precinct whose resolution starts off its precinct grid, which the
+            // walk takes at the tile origin (that test without XRsiz, as there)
+            const uint64_t sxc = P.sx(c), syc = P.sy(c);
+            const bool offx = (((uint64_t)R.x0 << lv) & ((1ull << (pwe + lv)) - 1)) != 0;
+            const bool offy = (((uint64_t)R.y0 << lv) & ((1ull << (phe + lv)) - 1)) != 0;
             for (uint32_t pi = 0; pi < n; ++pi) {
                 const uint32_t i = pi % R.pw, j = pi / R.pw;
-                const uint64_t ax = i ? ((uint64_t)(R.px0 >> pwe) + i) << (pwe + lv) : T.x0;
-                const uint64_t ay = j ? ((uint64_t)(R.py0 >> phe) + j) << (phe + lv) : T.y0;
+                const uint64_t ax = (i || !offx) ? sxc * (((uint64_t)(R.px0 >> pwe) + i) << (pwe + lv)) : T.x0;
+                const uint64_t ay = (j || !offy) ? syc * (((uint64_t)(R.py0 >> phe) + j) << (phe + lv)) : T.y0;
                 v.push_back({ay, ax, r, c, pi});
             }
         }
@@ -2036,7 +2104,8 @@ struct T2Enc {
         // parts of progression order changes do not count: `stride` needs m_enableTilePartGeneration)
         const double tp_offset = P.p.tp_div ? (double)((tile_part_split(P).n - 1) * 14) / (double)L : 0.0;
         for (uint32_t k = 0; k < L; ++k)
-            rates[k] = P.p.rates[k] > 0.0 ? (size_pixel * npix) / (P.p.rates[k] * 8.0) - tp_offset : 0.0;
+            // bits_empty = 8 x component 0's subsampling (updateRates, CodeStreamCompress.cpp:961)
+            rates[k] = P.p.rates[k] > 0.0 ? (size_pixel * npix) / (P.p.rates[k] * 8.0 * P.sx(0) * P.sy(0)) - tp_offset : 0.0;
         const double sot_adjust = (npix * (double)header_size) / ((double)P.w * (double)P.h);
         if (rates[0] > 0.0) { rates[0] -= sot_adjust; if (rates[0] < 30.0f) rates[0] = 30.0f; }
         for (uint32_t k = 1; k + 1 < L; ++k)
@@ -2264,7 +2333,10 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
     put32(o, P.p.tw ? P.p.tw : P.x0 + P.w - P.gx0); put32(o, P.p.th ? P.p.th : P.y0 + P.h - P.gy0);
     put32(o, P.gx0); put32(o, P.gy0);                                              // XTsiz YTsiz XTOsiz YTOsiz
     put16(o, P.nc);
-    for (uint32_t i = 0; i < P.nc; ++i) { o.push_back((uint8_t)((P.prec - 1) | (P.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
+    for (uint32_t i = 0; i < P.nc; ++i) {   // Ssiz, XRsiz, YRsiz
+        o.push_back((uint8_t)((P.prec - 1) | (P.sgnd ? 0x80 : 0)));
+        o.push_back((uint8_t)P.sx(i)); o.push_back((uint8_t)P.sy(i));
+    }
     if (P.p.ht()) {   // CAP (CodeStreamCompress::write_cap :1064-1111): Pcap bit 15, Ccap = MAGBp code
         uint32_t B = 0;
         // param_qcd::get_MAGBp (HTParams.cpp:318-336): scalar expounded bands count from their
@@ -2461,6 +2533,8 @@ struct gk_ctx {
     hipEvent_t ev[32];
     bool blocks_uploaded = false;
     uint32_t enc_b0 = 0, enc_b1 = 0;   // block range of the uploaded encode table
+    std::vector<uint8_t> enc_dx, enc_dy;   // gk_set_subsampling: the next encodes' component subsampling
+    std::vector<uint32_t> hdr_dx, hdr_dy;  // the last gk_decode_header's component subsampling
     bool enc_rc = false;                // its rate-control flag (GkBlock::flags bit 1)
     // band quantisation held by the cached plan's bands: the plan's own (encoder, native_qcd)
     // or that of the last decoded stream (band_qcd)
@@ -2568,6 +2642,8 @@ static std::string plan_key(const Plan& P) {
     snprintf(buf, sizeof buf, "%u %u %u %u %u %u %u %u %u %u %u %u", P.w, P.h, P.nc, P.prec, P.sgnd, P.p.numres, P.p.cbw,
              P.p.cbh, P.p.irrev, P.p.mct, P.p.numgbits, P.p.custom_prc ? 1 : 0);
     std::string k(buf);
+    if (P.subsampled())
+        for (uint32_t c = 0; c < P.nc; ++c) k += " s" + std::to_string(P.sx(c)) + "x" + std::to_string(P.sy(c));
     k += " sty" + std::to_string(P.p.cblk_sty) + " t" + std::to_string(P.p.tw) + "x" + std::to_string(P.p.th);
     k += " o" + std::to_string(P.x0) + "," + std::to_string(P.y0) + "," + std::to_string(P.gx0) + "," + std::to_string(P.gy0);
     for (size_t c = 0; c < P.p.roishift.size(); ++c)   // non-zero (component, shift) pairs only
@@ -2630,7 +2706,12 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
     const uint32_t nlev = forward ? L : (L + 1 > lstop ? L + 1 - lstop : 0);
     for (uint32_t i = 0; i < nlev; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
-        for (const ShapeG& S0 : P.shapes) {       // one launch per tile class, grid.z = its tiles
+        // per sampling group (one without subsampling) and run of its components
+        for (const SGroup& G : P.groups)
+        for (const auto& run : G.runs)
+        for (const ShapeG& S0 : G.shapes) {       // one launch per tile class, grid.z = its tiles
+            const uint32_t c0 = run.first, ncr = run.second - run.first;
+            int32_t* const base = arena + (size_t)c0 * cst;   // component c0's plane pair
             ShapeG S = S0;                        // restricted to tile rows [jb, je), columns [ib, ie)
             // members k of the class: tile column ci + k si; those in [ib, ie) are k in [k0, k1)
             auto krange = [](uint64_t c, uint64_t st, uint32_t n, uint64_t b, uint64_t e, uint32_t& k0, uint32_t& k1) {
@@ -2644,51 +2725,56 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
             S.tb.i0 = ki0; S.tb.nx = ki1 - ki0;
             S.tb.j0 = kj0; S.tb.ny = kj1 - kj0;
             // member k's region position: px0 + k dx - RG.x0 = k dx - ox (modulo 2^32; the true value >= 0)
+            // (a subsampled stream's regions are the whole image: origin 0 on every grid)
             S.tb.ox = RG.x0 - S.px0; S.tb.oy = RG.y0 - S.py0;
             const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
             // a level whose input resolution starts on an odd coordinate (either axis), or every
             // level under GK_DWT_ANY: the parity-general kernels (gk_dwt_any.hip)
             static const bool force_any = getenv("GK_DWT_ANY") != nullptr;
             if ((S.parx[l - 1] || S.pary[l - 1] || force_any) && !(l == 1 && io)) {
-                int32_t* A = arena;
+                int32_t* A = base;
                 int32_t* B = A + RG.plane;
                 int32_t* src_l = (l & 1) ? A : B;
                 int32_t* dst_l = (l & 1) ? B : A;
                 const uint64_t area = (uint64_t)w * h * S.tb.count();
                 gk_launch_dwt_any(ctx->st, P.p.irrev, forward, forward ? src_l : dst_l, forward ? dst_l : src_l, RG.stride,
-                                  w, h, S.parx[l - 1], S.pary[l - 1], S.tb, GkComps{cst, P.nc}, !forward && ctx->dwt_partial);
+                                  w, h, S.parx[l - 1], S.pary[l - 1], S.tb, GkComps{cst, ncr}, !forward && ctx->dwt_partial);
                 ctx->tm.dwt_launches += 3;
-                ctx->tm.dwt_bytes += area * 8 * P.nc;
+                ctx->tm.dwt_bytes += area * 8 * ncr;
                 continue;
             }
             const uint64_t area = (uint64_t)w * h * S.tb.count();
-            int32_t* A = arena;
+            int32_t* A = base;
             int32_t* B = A + RG.plane;
             int32_t* src_l = (l & 1) ? A : B;     // D_{l-1}: level l input plane (l-1 odd -> B)
             int32_t* dst_l = (l & 1) ? B : A;     // D_l
             if (l == 1 && io) {
                 // fused level 1: three components through the MCT, the others one by one
                 const uint64_t es = gk_sample_size(io->stype);
-                for (uint32_t c = 0; c < P.nc;) {
-                    const int nc = (io->mct3 && c == 0) ? 3 : 1;
+                // the output window on this grid (a subsampled stream decodes whole images)
+                GkWin win = io->win;
+                if (P.subsampled()) { win.x0 = 0; win.y0 = 0; win.x1 = (int32_t)G.w; win.y1 = (int32_t)G.h; }
+                for (uint32_t c = c0; c < run.second;) {
+                    const int nc = (io->mct3 && c == 0 && run.second >= 3) ? 3 : 1;
+                    int32_t* dl = dst_l + (size_t)(c - c0) * cst;
                     GkPtr3 pp;
                     for (int k = 0; k < nc; ++k) pp.p[k] = io->planes[c + k];
                     if (forward) {
                         if (P.p.irrev)
                             gk_launch_dwt97_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c],
-                                                   reinterpret_cast<float*>(dst_l + c * cst), cst, RG.stride, w, h, S.tb,
+                                                   reinterpret_cast<float*>(dl), cst, RG.stride, w, h, S.tb,
                                                    io->shift);
                         else
-                            gk_launch_dwt53_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c], dst_l + c * cst, cst,
+                            gk_launch_dwt53_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c], dl, cst,
                                                    RG.stride, w, h, S.tb, io->shift);
                     } else {
                         if (P.p.irrev)
-                            gk_launch_dwt97_inv_l1(ctx->st, io->stype, nc, reinterpret_cast<const float*>(dst_l + c * cst),
-                                                   cst, RG.stride, pp, io->strides[c], io->win, w, h, S.tb, io->shift,
+                            gk_launch_dwt97_inv_l1(ctx->st, io->stype, nc, reinterpret_cast<const float*>(dl),
+                                                   cst, RG.stride, pp, io->strides[c], win, w, h, S.tb, io->shift,
                                                    io->mn, io->mx);
                         else
-                            gk_launch_dwt53_inv_l1(ctx->st, io->stype, nc, dst_l + c * cst, cst, RG.stride, pp,
-                                                   io->strides[c], io->win, w, h, S.tb, io->shift, io->mn, io->mx);
+                            gk_launch_dwt53_inv_l1(ctx->st, io->stype, nc, dl, cst, RG.stride, pp,
+                                                   io->strides[c], win, w, h, S.tb, io->shift, io->mn, io->mx);
                     }
                     ctx->tm.dwt_launches++;
                     ctx->tm.dwt_bytes += area * (4 + es) * nc;
@@ -2696,7 +2782,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                 }
                 continue;
             }
-            const GkComps cs{cst, P.nc};
+            const GkComps cs{cst, ncr};
             if (P.p.irrev) {
                 float* fs = reinterpret_cast<float*>(src_l);
                 float* fd = reinterpret_cast<float*>(dst_l);
@@ -2707,7 +2793,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                 else gk_launch_dwt53_inv(ctx->st, dst_l, RG.stride, src_l, RG.stride, w, h, S.tb, cs);
             }
             ctx->tm.dwt_launches++;
-            ctx->tm.dwt_bytes += area * 8 * P.nc;
+            ctx->tm.dwt_bytes += area * 8 * ncr;
         }
     }
 }
@@ -2731,12 +2817,19 @@ static void setup_plan(gk_ctx* ctx, const gk_image_info* info, const gk_cparamet
     // tile reaches into the image area
     want.x0 = info->x0; want.y0 = info->y0;
     want.gx0 = cp ? cp->tx0 : 0; want.gy0 = cp ? cp->ty0 : 0;
+    if (!ctx->enc_dx.empty()) {   // gk_set_subsampling
+        if (ctx->enc_dx.size() != want.nc) throw GkError("gk_set_subsampling was given a different component count");
+        want.cdx = ctx->enc_dx; want.cdy = ctx->enc_dy;
+        if (!want.subsampled()) { want.cdx.clear(); want.cdy.clear(); }
+    }
     if (want.gx0 > want.x0 || want.gy0 > want.y0) throw GkError("tile grid origin must lie at or above-left of the image origin");
     if ((uint64_t)want.x0 + want.w > 0xffffffffull || (uint64_t)want.y0 + want.h > 0xffffffffull)
         throw GkError("image area past the 32-bit canvas");
     if (want.p.tw && ((uint64_t)want.gx0 + want.p.tw <= want.x0 || (uint64_t)want.gy0 + want.p.th <= want.y0))
         throw GkError("the first tile must overlap the image area");
     if (want.nc < 3) want.p.mct = 0;
+    // CodeStreamCompress.cpp:501-512: no MCT unless the first three components share a grid
+    if (want.p.mct && !want.mct3()) want.p.mct = 0;
     check_poc_coverage(want.p, want.nc);
     if ((want.p.cblk_sty & GK_STY_HT) && want.p.cblk_sty != GK_STY_HT)
         throw GkError("HTJ2K cannot be combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781
@@ -2833,6 +2926,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const uint32_t ntiles = (uint32_t)P.tiles.size();
     if (te == 0) { tb = 0; te = ntiles; }
     if (tb >= te || te > ntiles) throw GkError("bad tile range");
+    const bool sub = P.subsampled();
+    if (sub && (tb != 0 || te != ntiles)) throw GkError("tile-range encodes of subsampled components are not supported on this path");
     const uint32_t nb = (uint32_t)P.blocks.size();
     const uint32_t b0 = P.tiles[tb].b0, b1 = P.tiles[te - 1].b1, nbr = b1 - b0;   // block range of the tiles
     const uint32_t jb = tb / P.ntx, je = (te - 1) / P.ntx + 1;                     // tile rows touched
@@ -2851,7 +2946,21 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const size_t es = gk_sample_size(stype);
     std::vector<const void*> src(P.nc);
     std::vector<uint32_t> sstr(P.nc);
-    if (!comps_on_device) {
+    if (sub) {
+        // subsampled components: each plane at its own size (the whole image), staged back to back
+        size_t tot = 0;
+        for (uint32_t c = 0; c < P.nc; ++c) tot += (size_t)P.groups[P.group_of[c]].w * P.groups[P.group_of[c]].h;
+        uint8_t* dp = comps_on_device ? nullptr : (uint8_t*)ctx->dplanes.get(tot * es + 16);
+        size_t o = 0;
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            const SGroup& G = P.groups[P.group_of[c]];
+            if (comps_on_device) { src[c] = comps[c]; sstr[c] = strides[c]; continue; }
+            HIPCHK(hipMemcpy2DAsync(dp + o * es, (size_t)G.w * es, comps[c], (size_t)strides[c] * es, (size_t)G.w * es, G.h,
+                                    hipMemcpyHostToDevice, st));
+            src[c] = dp + o * es; sstr[c] = G.w;
+            o += (size_t)G.w * G.h;
+        }
+    } else if (!comps_on_device) {
         uint8_t* dp = (uint8_t*)ctx->dplanes.get((size_t)P.w * nrows * P.nc * es);
         for (uint32_t c = 0; c < P.nc; ++c) {
             HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * nrows * es, (size_t)P.w * es,
@@ -2869,7 +2978,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
     auto planeA = [&](uint32_t c) { return arena + (size_t)c * 2 * RG.plane; };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<float*>(planeA(c)); };
-    const bool mct3 = P.p.mct && P.nc >= 3;
+    const bool mct3 = P.mct3();
     if (mct3 && (sstr[1] != sstr[0] || sstr[2] != sstr[0])) throw GkError("the first three components must share a stride");
     L1Io io;
     // DC shift + MCT run inside the first DWT level (unless a tile starts on an odd coordinate:
@@ -2879,12 +2988,18 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         io.stype = stype; io.mct3 = mct3; io.shift = shift;
         io.planes.assign(src.begin(), src.end());
         io.strides = sstr;
-    } else if (!P.p.irrev) {   // no decomposition: DC shift + MCT into plane A of each component
-        if (mct3) gk_launch_dc_rct_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), RG.stride, P.w, nrows, shift);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, stype, src[c], sstr[c], planeA(c), RG.stride, P.w, nrows, shift);
     } else {
-        if (mct3) gk_launch_dc_ict_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), RG.stride, P.w, nrows, shift);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, stype, src[c], sstr[c], planeAf(c), RG.stride, P.w, nrows, shift);
+        // no decomposition (or a tile on an odd origin): DC shift + MCT into plane A of each
+        // component (each component's plane at its own size)
+        auto cw = [&](uint32_t c) { return sub ? P.groups[P.group_of[c]].w : P.w; };
+        auto ch = [&](uint32_t c) { return sub ? P.groups[P.group_of[c]].h : nrows; };
+        if (!P.p.irrev) {
+            if (mct3) gk_launch_dc_rct_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), RG.stride, cw(0), ch(0), shift);
+            for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, stype, src[c], sstr[c], planeA(c), RG.stride, cw(c), ch(c), shift);
+        } else {
+            if (mct3) gk_launch_dc_ict_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeAf(0), planeAf(1), planeAf(2), RG.stride, cw(0), ch(0), shift);
+            for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd_f(st, stype, src[c], sstr[c], planeAf(c), RG.stride, cw(c), ch(c), shift);
+        }
     }
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[2], st));
@@ -3611,10 +3726,15 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             uint32_t sz = S.at(s + 36);
             W.prec = (sz & 0x7f) + 1; W.sgnd = (sz & 0x80) ? 1 : 0;
             if (W.prec > 31) throw GkError("component precision > 31 bits not supported");
+            W.cdx.assign(W.nc, 1); W.cdy.assign(W.nc, 1);
             for (uint32_t c = 0; c < W.nc; ++c) {
-                if (S.at(s + 37 + 3 * c) != 1 || S.at(s + 38 + 3 * c) != 1) throw GkError("component subsampling not supported");
+                // XRsiz / YRsiz: 1..255 (read_siz)
+                W.cdx[c] = S.at(s + 37 + 3 * c); W.cdy[c] = S.at(s + 38 + 3 * c);
+                if (!W.cdx[c] || !W.cdy[c]) throw GkError("corrupt SIZ marker (component subsampling 0)");
                 if (((S.at(s + 36 + 3 * c) & 0x7f) + 1) != W.prec) throw GkError("mixed component precision not supported");
+                if ((S.at(s + 36 + 3 * c) >> 7) != W.sgnd) throw GkError("mixed component signedness not supported");
             }
+            if (!W.subsampled()) { W.cdx.clear(); W.cdy.clear(); }
             have_siz = true;
         } else if (m == 0xff52) {
             if (L < 12) throw GkError("corrupt COD marker");
@@ -3876,6 +3996,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                     if (B.numbps > 30) throw GkError("more than 30 band bit-planes (ROI shift included) not supported");
     const uint32_t red = ctx->dec_reduce;
     if (red >= P.p.numres) throw GkError("reduce must be less than the number of resolutions");
+    // subsampled components decode whole images (every component plane at its own size)
+    const bool sub = P.subsampled();
+    if (sub && win) throw GkError("window decodes of subsampled components are not supported on this path");
     auto keep_window = [&]() {   // keep only the tile parts of tiles intersecting the window
         if (!win) return;
         if (win[0] >= win[2] || win[1] >= win[3] || win[2] > P.w || win[3] > P.h) throw GkError("bad decode window");
@@ -3915,6 +4038,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         ib = std::min(ib, t % P.ntx); ie = std::max(ie, t % P.ntx + 1);
         jb = std::min(jb, t / P.ntx); je = std::max(je, t / P.ntx + 1);
     }
+    if (sub) { ib = 0; ie = P.ntx; jb = 0; je = P.nty; }   // (tiles without a tile part decode as zero)
     // work planes cover the tile rectangle only (tiles of the rectangle without a tile part
     // decode as zero); the output region is the rectangle, clipped to the window
     const TileG& Tfirst = P.tiles[(size_t)jb * P.ntx + ib];
@@ -4521,12 +4645,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     int32_t mx = P.sgnd ? (1 << (P.prec - 1)) - 1 : (int32_t)((1u << P.prec) - 1);
     const int stype = sample_type(sample_bytes, P.prec, P.sgnd != 0);
     const size_t es = gk_sample_size(stype);
-    const bool mct3r = P.p.mct && P.nc >= 3;
+    const bool mct3r = P.mct3();
     if (red) {
         // reduced resolution: undo levels L .. red+1; resolution numres-1-red of each tile is
         // then at the tile's corner of plane (red odd ? B : A); the inverse MCT + DC + clamp
         // writes it per tile into the ceil(size / 2^red) output (a tile's reduced origin is
-        // ceil(origin / 2^red), B.5)
+        // ceil(origin / 2^red), B.5).  Subsampled components: the same on each component's grid
+        // (tile-component ceil(tile / XRsiz), then reduced), one plane each.
         run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr, red + 1);
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
@@ -4534,64 +4659,86 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // A window (image-relative, full resolution) reduces the same way (the composite
         // component bounds of CodeStreamDecompress.cpp:471-481, rectceildivpow2): the output is
         // the reduced tile rectangle clipped to it, the caller's planes addressing its origin
-        const uint32_t rox = ceildivpow2(P.x0, red), roy = ceildivpow2(P.y0, red);
-        uint32_t qx0 = ceildivpow2(RG.x0 + P.x0, red) - rox, qy0 = ceildivpow2(RG.y0 + P.y0, red) - roy;
-        uint32_t qx1 = ceildivpow2(RG.x0 + P.x0 + RG.w, red) - rox, qy1 = ceildivpow2(RG.y0 + P.y0 + RG.h, red) - roy;
-        uint32_t wx0 = 0, wy0 = 0;   // the caller's origin in the reduced image
-        if (win) {
-            wx0 = ceildivpow2(win[0] + P.x0, red) - rox; wy0 = ceildivpow2(win[1] + P.y0, red) - roy;
-            qx0 = std::max(qx0, wx0); qy0 = std::max(qy0, wy0);
-            qx1 = std::min(qx1, ceildivpow2(win[2] + P.x0, red) - rox); qy1 = std::min(qy1, ceildivpow2(win[3] + P.y0, red) - roy);
-            if (qx1 <= qx0 || qy1 <= qy0) throw GkError("the window is empty at this reduction");
+        std::vector<uint32_t> rox(P.nc), roy(P.nc), qx0(P.nc), qy0(P.nc), qx1(P.nc), qy1(P.nc), wx0(P.nc, 0), wy0(P.nc, 0);
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            const SGroup& G = P.groups[P.group_of[c]];
+            rox[c] = ceildivpow2(G.ox, red); roy[c] = ceildivpow2(G.oy, red);
+            if (sub) {   // the whole component
+                qx0[c] = 0; qy0[c] = 0; qx1[c] = ceildivpow2(G.ox + G.w, red) - rox[c]; qy1[c] = ceildivpow2(G.oy + G.h, red) - roy[c];
+                continue;
+            }
+            qx0[c] = ceildivpow2(RG.x0 + P.x0, red) - rox[c]; qy0[c] = ceildivpow2(RG.y0 + P.y0, red) - roy[c];
+            qx1[c] = ceildivpow2(RG.x0 + P.x0 + RG.w, red) - rox[c]; qy1[c] = ceildivpow2(RG.y0 + P.y0 + RG.h, red) - roy[c];
+            if (win) {
+                wx0[c] = ceildivpow2(win[0] + P.x0, red) - rox[c]; wy0[c] = ceildivpow2(win[1] + P.y0, red) - roy[c];
+                qx0[c] = std::max(qx0[c], wx0[c]); qy0[c] = std::max(qy0[c], wy0[c]);
+                qx1[c] = std::min(qx1[c], ceildivpow2(win[2] + P.x0, red) - rox[c]);
+                qy1[c] = std::min(qy1[c], ceildivpow2(win[3] + P.y0, red) - roy[c]);
+                if (qx1[c] <= qx0[c] || qy1[c] <= qy0[c]) throw GkError("the window is empty at this reduction");
+            }
         }
-        const uint32_t qcols = qx1 - qx0, qrows = qy1 - qy0;
         std::vector<uint8_t*> qd(P.nc);
         std::vector<uint32_t> qs(P.nc);
         if (!out_on_device) {
-            uint8_t* stage = (uint8_t*)ctx->dplanes.get((size_t)qcols * qrows * P.nc * es + 16);
-            for (uint32_t c = 0; c < P.nc; ++c) { qd[c] = stage + (size_t)c * qcols * qrows * es; qs[c] = qcols; }
+            size_t tot = 0;
+            for (uint32_t c = 0; c < P.nc; ++c) tot += (size_t)(qx1[c] - qx0[c]) * (qy1[c] - qy0[c]);
+            uint8_t* stage = (uint8_t*)ctx->dplanes.get(tot * es + 16);
+            size_t o2 = 0;
+            for (uint32_t c = 0; c < P.nc; ++c) {
+                qd[c] = stage + o2 * es; qs[c] = qx1[c] - qx0[c];
+                o2 += (size_t)(qx1[c] - qx0[c]) * (qy1[c] - qy0[c]);
+            }
         } else {
             for (uint32_t c = 0; c < P.nc; ++c) {
-                qd[c] = (uint8_t*)comps[c] + ((size_t)(qy0 - wy0) * strides[c] + (qx0 - wx0)) * es;
+                qd[c] = (uint8_t*)comps[c] + ((size_t)(qy0[c] - wy0[c]) * strides[c] + (qx0[c] - wx0[c])) * es;
                 qs[c] = strides[c];
             }
         }
         for (uint32_t j = jb; j < je; ++j)
             for (uint32_t i = ib; i < ie; ++i) {
                 const TileG& T = P.tiles[(size_t)j * P.ntx + i];
-                const uint32_t tx0 = ceildivpow2(T.x0, red) - rox, ty0 = ceildivpow2(T.y0, red) - roy;
-                const uint32_t tx1 = ceildivpow2(T.x1, red) - rox, ty1 = ceildivpow2(T.y1, red) - roy;
-                // the part of the tile's reduced rectangle inside the output
-                const uint32_t ix0 = std::max(tx0, qx0), iy0 = std::max(ty0, qy0);
-                const uint32_t ix1 = std::min(tx1, qx1), iy1 = std::min(ty1, qy1);
-                if (ix1 <= ix0 || iy1 <= iy0) continue;
-                const uint32_t tw = ix1 - ix0, th = iy1 - iy0;
-                auto src = [&](uint32_t c) {
-                    return arena + (size_t)c * 2 * RG.plane + ((red & 1) ? RG.plane : 0) +
-                           (size_t)(T.y0 - P.y0 - RG.y0 + (iy0 - ty0)) * RG.stride + (T.x0 - P.x0 - RG.x0 + (ix0 - tx0));
-                };
-                auto srcf = [&](uint32_t c) { return reinterpret_cast<const float*>(src(c)); };
-                auto dst = [&](uint32_t c) { return qd[c] + ((size_t)(iy0 - qy0) * qs[c] + (ix0 - qx0)) * es; };
-                if (!P.p.irrev) {
-                    if (mct3r) gk_launch_rct_inv_dc(st, src(0), src(1), src(2), RG.stride, stype, dst(0), dst(1), dst(2), qs[0],
-                                                    tw, th, shift, mn, mx);
-                    for (uint32_t c = mct3r ? 3 : 0; c < P.nc; ++c)
-                        gk_launch_dc_inv(st, src(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
-                } else {
-                    if (mct3r) gk_launch_ict_inv_dc(st, srcf(0), srcf(1), srcf(2), RG.stride, stype, dst(0), dst(1), dst(2),
-                                                    qs[0], tw, th, shift, mn, mx);
-                    for (uint32_t c = mct3r ? 3 : 0; c < P.nc; ++c)
-                        gk_launch_dc_inv_f(st, srcf(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
+                for (uint32_t c = 0; c < P.nc;) {
+                    const bool m3 = mct3r && c == 0;
+                    const SGroup& G = P.groups[P.group_of[c]];
+                    // the tile-component and its reduced rectangle on the component's grid
+                    const uint32_t cx0 = ceildiv(T.x0, G.dx), cy0 = ceildiv(T.y0, G.dy);
+                    const uint32_t tx0 = ceildivpow2(cx0, red) - rox[c], ty0 = ceildivpow2(cy0, red) - roy[c];
+                    const uint32_t tx1 = ceildivpow2(ceildiv(T.x1, G.dx), red) - rox[c];
+                    const uint32_t ty1 = ceildivpow2(ceildiv(T.y1, G.dy), red) - roy[c];
+                    // the part of the tile's reduced rectangle inside the output
+                    const uint32_t ix0 = std::max(tx0, qx0[c]), iy0 = std::max(ty0, qy0[c]);
+                    const uint32_t ix1 = std::min(tx1, qx1[c]), iy1 = std::min(ty1, qy1[c]);
+                    const uint32_t cn = m3 ? 3 : 1;
+                    if (ix1 <= ix0 || iy1 <= iy0) { c += cn; continue; }
+                    const uint32_t tw = ix1 - ix0, th = iy1 - iy0;
+                    auto src = [&](uint32_t k) {
+                        return arena + (size_t)k * 2 * RG.plane + ((red & 1) ? RG.plane : 0) +
+                               (size_t)(cy0 - G.oy - RG.y0 + (iy0 - ty0)) * RG.stride + (cx0 - G.ox - RG.x0 + (ix0 - tx0));
+                    };
+                    auto srcf = [&](uint32_t k) { return reinterpret_cast<const float*>(src(k)); };
+                    auto dst = [&](uint32_t k) { return qd[k] + ((size_t)(iy0 - qy0[k]) * qs[k] + (ix0 - qx0[k])) * es; };
+                    if (!P.p.irrev) {
+                        if (m3) gk_launch_rct_inv_dc(st, src(0), src(1), src(2), RG.stride, stype, dst(0), dst(1), dst(2), qs[0],
+                                                     tw, th, shift, mn, mx);
+                        else gk_launch_dc_inv(st, src(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
+                    } else {
+                        if (m3) gk_launch_ict_inv_dc(st, srcf(0), srcf(1), srcf(2), RG.stride, stype, dst(0), dst(1), dst(2),
+                                                     qs[0], tw, th, shift, mn, mx);
+                        else gk_launch_dc_inv_f(st, srcf(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
+                    }
+                    c += cn;
                 }
             }
         if (mct3r && (qs[1] != qs[0] || qs[2] != qs[0])) throw GkError("the first three components must share a stride");
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[5], st));
         if (!out_on_device)
-            for (uint32_t c = 0; c < P.nc; ++c)
-                HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)(qy0 - wy0) * strides[c] + (qx0 - wx0)) * es,
+            for (uint32_t c = 0; c < P.nc; ++c) {
+                const uint32_t qcols = qx1[c] - qx0[c], qrows = qy1[c] - qy0[c];
+                HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)(qy0[c] - wy0[c]) * strides[c] + (qx0[c] - wx0[c])) * es,
                                         (size_t)strides[c] * es, qd[c], (size_t)qcols * es, (size_t)qcols * es, qrows,
                                         hipMemcpyDeviceToHost, st));
+            }
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[6], st));
         HIPCHK(hipStreamSynchronize(st));
@@ -4601,11 +4748,20 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         ctx->tm.total_ms = ev_ms(ctx, 0, 6); ctx->tm.t1_blocks = nbr;
         return;
     }
+    // the output rectangle of component c (a subsampled component: its whole plane, on its grid)
+    auto ocols = [&](uint32_t c) { return sub ? P.groups[P.group_of[c]].w : ncols; };
+    auto orows = [&](uint32_t c) { return sub ? P.groups[P.group_of[c]].h : nrows; };
     std::vector<void*> dst(P.nc);
     std::vector<uint32_t> dstr(P.nc);
     if (!out_on_device) {
-        uint8_t* stage = (uint8_t*)ctx->dplanes.get((size_t)ncols * nrows * P.nc * es + 16);
-        for (uint32_t c = 0; c < P.nc; ++c) { dst[c] = stage + (size_t)c * ncols * nrows * es; dstr[c] = ncols; }
+        size_t tot = 0;
+        for (uint32_t c = 0; c < P.nc; ++c) tot += (size_t)ocols(c) * orows(c);
+        uint8_t* stage = (uint8_t*)ctx->dplanes.get(tot * es + 16);
+        size_t o2 = 0;
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            dst[c] = stage + o2 * es; dstr[c] = ocols(c);
+            o2 += (size_t)ocols(c) * orows(c);
+        }
     } else {
         for (uint32_t c = 0; c < P.nc; ++c) {
             dst[c] = (uint8_t*)comps[c] + ((size_t)(ry0 - oy) * strides[c] + (rx0 - ox)) * es;
@@ -4616,7 +4772,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         return arena + (size_t)c * 2 * RG.plane + (size_t)(ry0 - RG.y0) * RG.stride + (rx0 - RG.x0);
     };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
-    const bool mct3 = P.p.mct && P.nc >= 3;
+    const bool mct3 = P.mct3();
     if (P.p.numres > 1 && !P.l1_fusable) {   // levels first, then the inverse MCT + DC shift + clamp below
         run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr);
     }
@@ -4635,23 +4791,23 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
         if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
-                                       ncols, nrows, shift, mn, mx);
+                                       ocols(0), orows(0), shift, mn, mx);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
-            gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
+            gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shift, mn, mx);
     } else {
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
         if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
-                                       ncols, nrows, shift, mn, mx);
+                                       ocols(0), orows(0), shift, mn, mx);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
-            gk_launch_dc_inv_f(st, planeAf(c), RG.stride, stype, dst[c], dstr[c], ncols, nrows, shift, mn, mx);
+            gk_launch_dc_inv_f(st, planeAf(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shift, mn, mx);
     }
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (!out_on_device) {
         for (uint32_t c = 0; c < P.nc; ++c)
             HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)(ry0 - oy) * strides[c] + (rx0 - ox)) * es,
-                                    (size_t)strides[c] * es, dst[c], (size_t)ncols * es, (size_t)ncols * es, nrows,
+                                    (size_t)strides[c] * es, dst[c], (size_t)ocols(c) * es, (size_t)ocols(c) * es, orows(c),
                                     hipMemcpyDeviceToHost, st));
     }
     launch_check(__LINE__);
@@ -4844,6 +5000,8 @@ int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
         parse_header(S, Hd);
         info->w = Hd.want.w; info->h = Hd.want.h; info->numcomps = Hd.want.nc; info->prec = Hd.want.prec;
         info->sgnd = Hd.want.sgnd; info->x0 = Hd.want.x0; info->y0 = Hd.want.y0;
+        ctx->hdr_dx.assign(Hd.want.nc, 1); ctx->hdr_dy.assign(Hd.want.nc, 1);
+        for (uint32_t c = 0; c < Hd.want.nc; ++c) { ctx->hdr_dx[c] = Hd.want.sx(c); ctx->hdr_dy[c] = Hd.want.sy(c); }
         return 0;
     } catch (const GkError& e) {
         ctx->err = e.msg;
@@ -4926,6 +5084,46 @@ int gk_decode(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void
         ctx->err = e.msg;
         return -1;
     }
+}
+
+int gk_set_subsampling(gk_ctx* ctx, uint32_t numcomps, const uint32_t* dx, const uint32_t* dy) {
+    if (!ctx) return -1;
+    ctx->enc_dx.clear(); ctx->enc_dy.clear();
+    if (!numcomps) return 0;
+    if (!dx || !dy || numcomps > 255) { ctx->err = "bad subsampling"; return -1; }
+    for (uint32_t c = 0; c < numcomps; ++c) {
+        if (!dx[c] || !dy[c] || dx[c] > 255 || dy[c] > 255) { ctx->err = "subsampling factors must be 1..255"; return -1; }
+        ctx->enc_dx.push_back((uint8_t)dx[c]); ctx->enc_dy.push_back((uint8_t)dy[c]);
+    }
+    ctx->plan_key.clear();
+    return 0;
+}
+
+int gk_probe_components(const uint8_t* cs, size_t len, uint32_t* dx, uint32_t* dy, uint32_t cap) {
+    if (!cs) return -1;
+    try {
+        ByteSrc S; S.len = len; S.host = cs;
+        size_t joff = 0, jlen = 0;
+        if (jp2_locate(S, joff, jlen)) { S = ByteSrc(); S.len = jlen; S.host = cs + joff; }
+        Header Hd;
+        parse_header(S, Hd);
+        for (uint32_t c = 0; c < Hd.want.nc && c < cap; ++c) {
+            if (dx) dx[c] = Hd.want.sx(c);
+            if (dy) dy[c] = Hd.want.sy(c);
+        }
+        return (int)Hd.want.nc;
+    } catch (const GkError&) {
+        return -1;
+    }
+}
+
+int gk_header_subsampling(gk_ctx* ctx, uint32_t* dx, uint32_t* dy, uint32_t cap) {
+    if (!ctx) return -1;
+    for (uint32_t c = 0; c < ctx->hdr_dx.size() && c < cap; ++c) {
+        if (dx) dx[c] = ctx->hdr_dx[c];
+        if (dy) dy[c] = ctx->hdr_dy[c];
+    }
+    return (int)ctx->hdr_dx.size();
 }
 
 int gk_set_window_rule(gk_ctx* ctx, int whole_tile) {

@@ -206,6 +206,7 @@ struct CodecObj : Obj {
     bool has_win = false;
     ImageObj* out = nullptr;                 // composited image (owned by the codec)
     bool tile_decoded = false;               // grk_decompress_tile cropped `out` to a tile
+    std::vector<uint32_t> cdx, cdy;          // the stream's component subsampling (SIZ XRsiz / YRsiz)
     ~CodecObj() override {
         if (stream) grk_object_unref(stream);
         if (image) grk_object_unref(&image->obj);
@@ -228,18 +229,32 @@ bool to_gk(const grk_cparameters& g, GRK_CODEC_FORMAT fmt, gk_cparameters& p, co
     return false;
 }
 
+inline uint32_t ceil_div(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + b - 1) / b); }
+bool subsampled(const grk_image* im) {
+    for (uint16_t i = 0; i < im->numcomps; ++i)
+        if (im->comps[i].dx > 1 || im->comps[i].dy > 1) return true;
+    return false;
+}
+
 bool image_geometry(const grk_image* im, gk_image_info& info) {
     if (!im || !im->numcomps || !im->comps) { error("empty image"); return false; }
     const grk_image_comp& c0 = im->comps[0];
+    // subsampled components (grk_image_comp::dx / dy): component c covers the image area
+    // [x0, x1) sampled every dx, ceil(x1 / dx) - ceil(x0 / dx) columns (GrkImage.cpp:74-113)
+    const bool sub = subsampled(im);
+    if (sub && (im->x1 <= im->x0 || im->y1 <= im->y0)) { error("subsampled image without its area (x1, y1)"); return false; }
     for (uint16_t i = 0; i < im->numcomps; ++i) {
         const grk_image_comp& c = im->comps[i];
-        if (c.dx != 1 || c.dy != 1) { error("component subsampling is not supported"); return false; }
-        if (c.w != c0.w || c.h != c0.h || c.prec != c0.prec || c.sgnd != c0.sgnd) {
-            error("components must share size and precision on this path");
+        const uint32_t dx = c.dx ? c.dx : 1, dy = c.dy ? c.dy : 1;
+        const bool size_ok = sub ? (c.w == ceil_div(im->x1, dx) - ceil_div(im->x0, dx) && c.h == ceil_div(im->y1, dy) - ceil_div(im->y0, dy))
+                                 : (c.w == c0.w && c.h == c0.h);
+        if (!size_ok || c.prec != c0.prec || c.sgnd != c0.sgnd) {
+            error("components must share precision, and their sizes follow the image area and subsampling, on this path");
             return false;
         }
     }
-    info.w = c0.w; info.h = c0.h; info.numcomps = im->numcomps; info.prec = c0.prec; info.sgnd = c0.sgnd;
+    info.w = sub ? im->x1 - im->x0 : c0.w; info.h = sub ? im->y1 - im->y0 : c0.h;
+    info.numcomps = im->numcomps; info.prec = c0.prec; info.sgnd = c0.sgnd;
     info.sample_bytes = 0;
     info.x0 = im->x0; info.y0 = im->y0;   // the image area's canvas origin (SIZ XOsiz / YOsiz)
     return true;
@@ -259,6 +274,14 @@ bool run_encode(CodecObj* C, const void* const* planes, const uint32_t* strides,
     std::lock_guard<std::mutex> lk(g_eng_m);
     gk_ctx* e = engine();
     if (!e) return false;
+    std::vector<uint32_t> dx(info.numcomps), dy(info.numcomps);
+    for (uint32_t c = 0; c < info.numcomps; ++c) {
+        dx[c] = C->image->comps[c].dx ? C->image->comps[c].dx : 1; dy[c] = C->image->comps[c].dy ? C->image->comps[c].dy : 1;
+    }
+    if (gk_set_subsampling(e, subsampled(C->image) ? info.numcomps : 0, dx.data(), dy.data()) != 0) {
+        error("%s", gk_last_error(e));
+        return false;
+    }
     std::vector<uint8_t> out((size_t)info.w * info.h * info.numcomps * 4 + (1 << 20));
     size_t n = 0;
     int rc = gk_encode(e, &info, planes, strides, 0, &p, out.data(), out.size(), &n, 0);
@@ -266,6 +289,7 @@ bool run_encode(CodecObj* C, const void* const* planes, const uint32_t* strides,
         out.resize(n);
         rc = gk_encode(e, &info, planes, strides, 0, &p, out.data(), out.size(), &n, 0);
     }
+    gk_set_subsampling(e, 0, nullptr, nullptr);
     if (rc != 0) { error("%s", gk_last_error(e)); return false; }
     StreamObj* s = stream_of(C->stream);
     if (!s || !s->write_all(out.data(), n)) return false;
@@ -302,10 +326,13 @@ static inline uint32_t reduced(uint64_t v, uint32_t r) { return (uint32_t)((v + 
 ImageObj* region_image(CodecObj* C, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
     const uint32_t r = C->dp.cp_reduce;
     std::vector<grk_image_cmptparm> p(C->info.numcomps);
-    for (auto& q : p) {
+    for (uint32_t k = 0; k < p.size(); ++k) {
+        grk_image_cmptparm& q = p[k];
         q = grk_image_cmptparm{};
-        q.dx = q.dy = 1; q.x0 = reduced(x0, r); q.y0 = reduced(y0, r);
-        q.w = reduced(x1, r) - q.x0; q.h = reduced(y1, r) - q.y0;
+        // (a subsampled component: the rectangle on its grid, then reduced; GrkImage.cpp:74-113)
+        q.dx = C->cdx[k]; q.dy = C->cdy[k];
+        q.x0 = reduced(ceil_div(x0, q.dx), r); q.y0 = reduced(ceil_div(y0, q.dy), r);
+        q.w = reduced(ceil_div(x1, q.dx), r) - q.x0; q.h = reduced(ceil_div(y1, q.dy), r) - q.y0;
         q.prec = (uint8_t)C->info.prec; q.sgnd = C->info.sgnd != 0;
     }
     GRK_COLOR_SPACE cs = GRK_CLRSPC_UNKNOWN;
@@ -324,9 +351,11 @@ ImageObj* region_image(CodecObj* C, uint32_t x0, uint32_t y0, uint32_t x1, uint3
 // resolution; the components take them reduced by r.
 bool reshape_image(ImageObj* o, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t r) {
     o->img.x0 = x0; o->img.y0 = y0; o->img.x1 = x1; o->img.y1 = y1;
-    const uint32_t cx0 = reduced(x0, r), cy0 = reduced(y0, r), cw = reduced(x1, r) - cx0, ch = reduced(y1, r) - cy0;
-    if (!cw || !ch) { error("the decompress region is empty at reduction %u", r); return false; }
     for (auto& c : o->comps) {
+        const uint32_t dx = c.dx ? c.dx : 1, dy = c.dy ? c.dy : 1;
+        const uint32_t cx0 = reduced(ceil_div(x0, dx), r), cy0 = reduced(ceil_div(y0, dy), r);
+        const uint32_t cw = reduced(ceil_div(x1, dx), r) - cx0, ch = reduced(ceil_div(y1, dy), r) - cy0;
+        if (!cw || !ch) { error("the decompress region is empty at reduction %u", r); return false; }
         const uint32_t stride = aligned_stride(cw);
         if (c.data && (c.w != cw || c.h != ch || c.stride != stride)) { free(c.data); c.data = nullptr; }
         c.x0 = cx0; c.y0 = cy0; c.w = cw; c.h = ch; c.stride = stride;
@@ -504,6 +533,7 @@ bool grk_compress_tile(grk_codec* codec, uint16_t tileIndex, uint8_t* data, uint
     if (!C || !C->compress || !C->image || !data) return false;
     gk_image_info info;
     if (!image_geometry(C->image, info)) return false;
+    if (subsampled(C->image)) { error("raw tiles of subsampled components are not supported on this path"); return false; }
     const uint32_t es = (info.prec + 7) / 8;
     if (es > 2) { error("raw tiles of more than 16 bits per sample are not supported"); return false; }
     if (C->cp.tile_size_on && (!C->cp.t_width || !C->cp.t_height)) { error("tile size must be non-zero"); return false; }
@@ -587,6 +617,11 @@ bool grk_decompress_read_header(grk_codec* codec, grk_header_info* hi) {
         char msg[256];
         if (gk_probe_header(C->data.data(), C->data.size(), &C->info, &C->coding, msg, sizeof msg) != 0) {
             error("%s", msg);
+            return false;
+        }
+        C->cdx.assign(C->info.numcomps, 1); C->cdy.assign(C->info.numcomps, 1);
+        if (gk_probe_components(C->data.data(), C->data.size(), C->cdx.data(), C->cdy.data(), C->info.numcomps) < 0) {
+            error("cannot read the component subsampling");
             return false;
         }
         C->header_read = true;

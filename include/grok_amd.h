@@ -179,6 +179,27 @@ int gk_set_decode_layers(gk_ctx* ctx, uint32_t max_layers);
  * CodeStreamDecompress.cpp:471-481). */
 int gk_set_decode_reduce(gk_ctx* ctx, uint32_t reduce);
 
+/* grk_image_comp::dx / dy of the components of later gk_encode / gk_main_header calls (SIZ XRsiz /
+ * YRsiz, 1..255; numcomps = 0 clears it).  Component c's plane then holds the image area sampled
+ * every (dx[c], dy[c]) canvas positions: ceil((x0 + w) / dx) - ceil(x0 / dx) columns and the same
+ * in y (grk_image_comp w / h), row stride strides[c].  Its tile-components are the tiles divided
+ * by (dx, dy), rounded up (TileProcessor.cpp:116-131); the MCT is cleared unless the first three
+ * components share a grid (CodeStreamCompress.cpp:501-512); rate control takes component 0's
+ * factors (updateRates :961).  Tiled images need each factor to divide the tile size; whole images
+ * only (no gk_encode_tiles). */
+int gk_set_subsampling(gk_ctx* ctx, uint32_t numcomps, const uint32_t* dx, const uint32_t* dy);
+
+/* A stream's component subsampling (SIZ XRsiz / YRsiz) from its header, no device needed: fills
+ * dx[c], dy[c] for the first cap components and returns the component count (< 0 on error).
+ * gk_decode writes component c into a plane of its own size: the image area divided by (dx, dy)
+ * as in gk_set_subsampling, then reduced by cp_reduce (ceil of both edges / 2^reduce).  Windows
+ * of subsampled streams are refused. */
+int gk_probe_components(const uint8_t* cs, size_t len, uint32_t* dx, uint32_t* dy, uint32_t cap);
+
+/* The component subsampling of the stream the last gk_decode_header read (host or device bytes):
+ * dx[c], dy[c] for the first cap components; returns the component count. */
+int gk_header_subsampling(gk_ctx* ctx, uint32_t* dx, uint32_t* dy, uint32_t cap);
+
 /* Inverse 5/3 rule of later gk_decode_window calls.  whole_tile = 0 (default): Grok's partial-tile
  * inverse, which a window set through setDecompressWindow selects for every tile
  * (CodeStreamDecompress.cpp:389; a one-sample-wide resolution on an odd coordinate shifts its

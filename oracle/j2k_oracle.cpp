@@ -71,6 +71,7 @@ template <class F> static void par_for(size_t n, F f) {
 
 static inline uint32_t ceildivpow2(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + (1ull << b) - 1) >> b); }
 static inline uint32_t floordivpow2(uint32_t a, uint32_t b) { return a >> b; }
+static inline uint32_t ceildiv(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + b - 1) / b); }
 static inline int floorlog2(uint32_t a) { int l = 0; while (a > 1) { a >>= 1; ++l; } return l; }
 
 // ----------------------------------------------------------------------------
@@ -112,6 +113,17 @@ struct Params {
     std::vector<int32_t> comp_qshift;
     bool qderived = false;
     uint32_t gb(uint32_t c) const { return c < comp_gb.size() ? comp_gb[c] : numgbits; }
+    // component subsampling (SIZ XRsiz / YRsiz, grk_image_comp::dx / dy; empty = 1): component c
+    // samples the canvas at multiples of (sx(c), sy(c)), its tile-components are the tiles'
+    // rectangles divided by them, rounded up (TileProcessor.cpp:116-131)
+    std::vector<uint32_t> cdx, cdy;
+    uint32_t sx(uint32_t c) const { return c < cdx.size() ? cdx[c] : 1u; }
+    uint32_t sy(uint32_t c) const { return c < cdy.size() ? cdy[c] : 1u; }
+    bool subsampled() const {
+        for (uint32_t v : cdx) if (v != 1) return true;
+        for (uint32_t v : cdy) if (v != 1) return true;
+        return false;
+    }
     int32_t qshift(uint32_t c) const { return c < comp_qshift.size() ? comp_qshift[c] : 0; }
     Params() { for (int i = 0; i < 33; ++i) { prcw_exp[i] = 15; prch_exp[i] = 15; } }
 };
@@ -1249,6 +1261,27 @@ static void tile_rect(const Params& p, uint32_t W, uint32_t H, uint32_t t, uint3
     x1 = std::min(p.gx0 + (t % ntx + 1) * tw, X1); y1 = std::min(p.gy0 + (t / ntx + 1) * th, Y1);
 }
 
+// Component c's plane: the image area divided by its subsampling, each edge rounded up
+// (grk_image_comp w / h; the caller's planes are these sizes, back to back)
+static void comp_size(const Params& p, uint32_t W, uint32_t H, uint32_t c, uint32_t& cw, uint32_t& ch) {
+    cw = ceildiv(p.x0 + W, p.sx(c)) - ceildiv(p.x0, p.sx(c));
+    ch = ceildiv(p.y0 + H, p.sy(c)) - ceildiv(p.y0, p.sy(c));
+}
+static std::vector<size_t> plane_offsets(const Params& p, uint32_t W, uint32_t H, uint32_t nc) {
+    std::vector<size_t> o(nc + 1, 0);
+    for (uint32_t c = 0; c < nc; ++c) {
+        uint32_t cw, ch;
+        comp_size(p, W, H, c, cw, ch);
+        o[c + 1] = o[c] + (size_t)cw * ch;
+    }
+    return o;
+}
+// The MCT needs the first three components on one sampling grid: Grok disables it otherwise
+// (CodeStreamCompress.cpp:501-512), and below three components
+static void settle_mct(Params& p, uint32_t nc) {
+    if (nc < 3 || p.sx(0) != p.sx(1) || p.sx(0) != p.sx(2) || p.sy(0) != p.sy(1) || p.sy(0) != p.sy(2)) p.mct = 0;
+}
+
 // Main header: SOC SIZ [CAP] COD QCD [TLM] [COM] (CodeStreamCompress::init_header_writing
 // :822-860).  *tlm_pos receives the offset of the first TLM entry (6 bytes per tile
 // part: Ttlm u16, Ptlm u32; Stlm = 0x60, LengthCache.cpp:437-482), patched later.
@@ -1296,7 +1329,10 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
     put32(o, p.tw ? p.tw : p.x0 + im.w - p.gx0); put32(o, p.th ? p.th : p.y0 + im.h - p.gy0);
     put32(o, p.gx0); put32(o, p.gy0);                                                 // XTOsiz YTOsiz
     put16(o, im.nc);
-    for (uint32_t i = 0; i < im.nc; ++i) { o.push_back((uint8_t)((im.prec - 1) | (im.sgnd ? 0x80 : 0))); o.push_back(1); o.push_back(1); }
+    for (uint32_t i = 0; i < im.nc; ++i) {          // Ssiz, XRsiz, YRsiz
+        o.push_back((uint8_t)((im.prec - 1) | (im.sgnd ? 0x80 : 0)));
+        o.push_back((uint8_t)p.sx(i)); o.push_back((uint8_t)p.sy(i));
+    }
     if (p.ht()) {                                   // CAP (CodeStreamCompress::write_cap :1064-1111)
         uint32_t B = 0;
         // param_qcd::get_MAGBp (HTParams.cpp:318-336): reversible expn + guard - 1; scalar
@@ -1425,22 +1461,31 @@ static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uin
                 }
         return;
     }
+    // the walk's step: the smallest precinct on the canvas, XRsiz * 2^(PPx + level) over the
+    // components (update_dxy, PacketIter.cpp:366-388; CPRL takes its component's alone, :63-65)
     uint64_t dx = ~0ull, dy = ~0ull;
-    for (uint32_t c = 0; c < nc; ++c)
-        for (uint32_t r = 0; r < nr; ++r) {
-            const uint32_t lv = nr - 1 - r;
-            dx = std::min<uint64_t>(dx, 1ull << (comps[c].res[r].prcw_exp + lv));
-            dy = std::min<uint64_t>(dy, 1ull << (comps[c].res[r].prch_exp + lv));
-        }
+    auto steps = [&](uint32_t ca, uint32_t cb) {
+        dx = ~0ull; dy = ~0ull;
+        for (uint32_t c = ca; c < cb; ++c)
+            for (uint32_t r = 0; r < nr; ++r) {
+                const uint32_t lv = nr - 1 - r;
+                dx = std::min<uint64_t>(dx, (uint64_t)p.sx(c) << (comps[c].res[r].prcw_exp + lv));
+                dy = std::min<uint64_t>(dy, (uint64_t)p.sy(c) << (comps[c].res[r].prch_exp + lv));
+            }
+    };
+    steps(0, nc);
+    // generatePrecinctIndex (:287-335): a precinct of resolution r of component c starts where the
+    // canvas position is a multiple of XRsiz * 2^(PPx + level), or at the tile origin when the
+    // resolution's origin is off its precinct grid (that test without XRsiz, as there)
     auto prc_at = [&](uint32_t c, uint32_t r, uint64_t x, uint64_t y, uint32_t& pi) {
         const Res& R = comps[c].res[r];
         if (!nprc(c, r)) return false;
         const uint32_t lv = nr - 1 - r;
-        const uint64_t rpx = R.prcw_exp + lv, rpy = R.prch_exp + lv;
-        if (!((x % (1ull << rpx)) == 0 || (x == tx0 && (((uint64_t)R.x0 << lv) % (1ull << rpx)) != 0))) return false;
-        if (!((y % (1ull << rpy)) == 0 || (y == ty0 && (((uint64_t)R.y0 << lv) % (1ull << rpy)) != 0))) return false;
-        const uint64_t i = (((x + (1ull << lv) - 1) >> lv) >> R.prcw_exp) - (R.x0 >> R.prcw_exp);
-        const uint64_t j = (((y + (1ull << lv) - 1) >> lv) >> R.prch_exp) - (R.y0 >> R.prch_exp);
+        const uint64_t rpx = R.prcw_exp + lv, rpy = R.prch_exp + lv, sxc = p.sx(c), syc = p.sy(c);
+        if (!((x % (sxc << rpx)) == 0 || (x == tx0 && (((uint64_t)R.x0 << lv) % (1ull << rpx)) != 0))) return false;
+        if (!((y % (syc << rpy)) == 0 || (y == ty0 && (((uint64_t)R.y0 << lv) % (1ull << rpy)) != 0))) return false;
+        const uint64_t i = (((x + (sxc << lv) - 1) / (sxc << lv)) >> R.prcw_exp) - (R.x0 >> R.prcw_exp);
+        const uint64_t j = (((y + (syc << lv) - 1) / (syc << lv)) >> R.prch_exp) - (R.y0 >> R.prch_exp);
         if (i >= R.pw || j >= R.ph) return false;
         pi = (uint32_t)(i + j * R.pw);
         return true;
@@ -1462,8 +1507,10 @@ static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uin
             for (uint32_t c = c0; c < c1; ++c) for (uint32_t r = r0; r < r1; ++r) emit(c, r, x, y);
         });
     } else {                  // CPRL
-        for (uint32_t c = c0; c < c1; ++c)
+        for (uint32_t c = c0; c < c1; ++c) {
+            steps(c, c + 1);
             walk([&](uint64_t x, uint64_t y) { for (uint32_t r = r0; r < r1; ++r) emit(c, r, x, y); });
+        }
     }
 }
 
@@ -2034,6 +2081,9 @@ typedef struct {
     uint32_t comp_gb[16];
     int32_t comp_qshift[16];
     uint32_t qderived;
+    // component subsampling (grk_image_comp::dx / dy), first nsub components (others 1)
+    uint32_t nsub;
+    uint32_t sub_dx[16], sub_dy[16];
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -2071,6 +2121,7 @@ static Params to_params(const orc_cparams* cp) {
     for (int i = 0; i < 33; ++i) { p.prcw_exp[i] = cp->prcw_exp[i] & 15; p.prch_exp[i] = cp->prch_exp[i] & 15; }
     for (uint32_t c = 0; c < cp->nq && c < 16; ++c) { p.comp_gb.push_back(cp->comp_gb[c]); p.comp_qshift.push_back(cp->comp_qshift[c]); }
     p.qderived = cp->qderived != 0;
+    for (uint32_t c = 0; c < cp->nsub && c < 16; ++c) { p.cdx.push_back(std::max(1u, cp->sub_dx[c])); p.cdy.push_back(std::max(1u, cp->sub_dy[c])); }
     return p;
 }
 
@@ -2192,31 +2243,40 @@ static void prepare_encode(EncodeState& E, const int32_t* planes, uint32_t w, ui
     if (!rows) rows = h;
     E.im = Image{w, h, nc, prec, sgnd != 0};
     E.p = to_params(cp);
-    if (nc < 3) E.p.mct = 0;
+    settle_mct(E.p, nc);
     E.tile = tile;
     tile_rect(E.p, w, h, tile, E.tx0, E.ty0, E.tx1, E.ty1);
-    const uint32_t tw = E.tx1 - E.tx0, th = E.ty1 - E.ty0;
     E.comps.assign(nc, Comp());
+    // tile-component c: the tile's rectangle divided by the subsampling (TileProcessor.cpp:116-131)
+    std::vector<uint32_t> tcx0(nc), tcy0(nc);
     for (uint32_t c = 0; c < nc; ++c) {
-        build_geometry(E.comps[c], E.tx0, E.ty0, E.tx1, E.ty1, E.p);
+        const uint32_t sx = E.p.sx(c), sy = E.p.sy(c);
+        tcx0[c] = ceildiv(E.tx0, sx); tcy0[c] = ceildiv(E.ty0, sy);
+        build_geometry(E.comps[c], tcx0[c], tcy0[c], ceildiv(E.tx1, sx), ceildiv(E.ty1, sy), E.p);
         assign_steps(E.comps[c], E.p, prec, true, nullptr, sgnd, E.p.roi(c), c);
     }
+    // planes: subsampled components back to back at their own sizes (the whole image only)
+    const std::vector<size_t> off = plane_offsets(E.p, w, h, nc);
     E.coefs.assign(nc, {});
     for (uint32_t c = 0; c < nc; ++c) {   // tile-local copy (TileProcessor::ingestImage, TileProcessor.cpp:410-431)
-        E.coefs[c].resize((size_t)tw * th);
-        for (uint32_t y = 0; y < th; ++y)
-            memcpy(&E.coefs[c][(size_t)y * tw],
-                   planes + (size_t)c * w * rows + (size_t)(E.ty0 - E.p.y0 - row0 + y) * w + (E.tx0 - E.p.x0),
-                   (size_t)tw * 4);
+        const Comp& C = E.comps[c];
+        uint32_t cw = w, ch = h;
+        size_t coff = (size_t)c * w * rows;
+        if (E.p.subsampled()) { comp_size(E.p, w, h, c, cw, ch); coff = off[c]; }
+        const uint32_t ox = ceildiv(E.p.x0, E.p.sx(c)), oy = ceildiv(E.p.y0, E.p.sy(c));
+        E.coefs[c].resize((size_t)C.w * C.h);
+        for (uint32_t y = 0; y < C.h; ++y)
+            memcpy(&E.coefs[c][(size_t)y * C.w], planes + coff + (size_t)(tcy0[c] - oy - row0 + y) * cw + (tcx0[c] - ox),
+                   (size_t)C.w * 4);
     }
     if (!E.p.irreversible) {
         dc_rct_fwd(E.coefs, prec, sgnd != 0, E.p.mct != 0);
         for (uint32_t c = 0; c < nc; ++c)
-            dwt2d<int32_t>(E.coefs[c].data(), tw, E.comps[c], E.p.numres, true, fwd53_1d);
+            dwt2d<int32_t>(E.coefs[c].data(), E.comps[c].w, E.comps[c], E.p.numres, true, fwd53_1d);
     } else {
         dc_ict_fwd(E.fcoefs, E.coefs, prec, sgnd != 0, E.p.mct != 0);
         for (uint32_t c = 0; c < nc; ++c)
-            dwt2d<float>(E.fcoefs[c].data(), tw, E.comps[c], E.p.numres, true, fwd97_1d);
+            dwt2d<float>(E.fcoefs[c].data(), E.comps[c].w, E.comps[c], E.p.numres, true, fwd97_1d);
     }
 }
 
@@ -2312,7 +2372,8 @@ static double make_layer(EncodeState& E, uint32_t layno, double thresh, bool fin
 // first tile (JP2 boxes, jp2c box header, main header: the stream position) by tile area.
 static void update_rates(const EncodeState& E, double* rates) {
     const Params& p = E.p;
-    const double size_pixel = (double)E.im.nc * E.im.prec, bits_empty = 8.0;
+    // bits_empty = 8 x component 0's subsampling (updateRates, CodeStreamCompress.cpp:961)
+    const double size_pixel = (double)E.im.nc * E.im.prec, bits_empty = 8.0 * p.sx(0) * p.sy(0);
     const double npix = (double)((uint64_t)(E.tx1 - E.tx0) * (E.ty1 - E.ty0));
     // tile-part generation: (parts - 1) x 14 bytes of SOT + SOD, spread over the layers
     const double offset = (double)((std::max(1, tile_parts(p, E.im.nc)) - 1) * 14) / (double)p.nlayers;
@@ -2564,7 +2625,7 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
             EncodeState E0;
             E0.im = Image{w, h, nc, prec, sgnd != 0};
             E0.p = p0;
-            if (nc < 3) E0.p.mct = 0;
+            settle_mct(E0.p, nc);
             E0.comps.assign(1, Comp());
             uint32_t x0, y0, x1, y1;
             tile_rect(E0.p, w, h, 0, x0, y0, x1, y1);
@@ -2663,7 +2724,7 @@ size_t orc_main_header(uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int s
     EncodeState E0;
     E0.im = Image{w, h, nc, prec, sgnd != 0};
     E0.p = to_params(cp);
-    if (nc < 3) E0.p.mct = 0;
+    settle_mct(E0.p, nc);
     E0.comps.assign(1, Comp());
     uint32_t x0, y0, x1, y1;
     tile_rect(E0.p, w, h, 0, x0, y0, x1, y1);
@@ -2684,7 +2745,7 @@ size_t orc_main_header(uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int s
 size_t orc_encode_tile_parts(const int32_t* slab, uint32_t w, uint32_t h, uint32_t nc, uint32_t prec, int sgnd,
                              const orc_cparams* cp, uint32_t row0, uint32_t rows, uint32_t tb, uint32_t te,
                              uint8_t* out, size_t cap, uint32_t* part_lens) {
-    if (!prc_exps_ok(to_params(cp))) return 0;
+    if (!prc_exps_ok(to_params(cp)) || to_params(cp).subsampled()) return 0;   // (whole-image planes only)
     std::vector<std::vector<uint8_t>> parts(te - tb);
     par_for(te - tb, [&](size_t q) {
         EncodeState E;
@@ -2825,12 +2886,18 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
     size_t data = ranges[0].first, tile_end = ranges[0].second, next_range = 1;
     uint32_t tx0, ty0, tx1, ty1;
     tile_rect(p, im.w, im.h, tile, tx0, ty0, tx1, ty1);
-    const uint32_t TW = tx1 - tx0, TH = ty1 - ty0;
     const uint32_t nlayers = p.nlayers;
     const uint32_t red = g_dec_reduce;   // grk_dparameters::cp_reduce
     size_t i = data;
+    // tile-component c: the tile divided by the component's subsampling (TileProcessor.cpp:116-131)
     std::vector<Comp> comps(im.nc);
-    for (uint32_t c = 0; c < im.nc; ++c) { build_geometry(comps[c], tx0, ty0, tx1, ty1, p); assign_steps(comps[c], p, im.prec, false, &cq[c], 0, p.roi(c)); }
+    std::vector<uint32_t> tcx0(im.nc), tcy0(im.nc), tcx1(im.nc), tcy1(im.nc);
+    for (uint32_t c = 0; c < im.nc; ++c) {
+        tcx0[c] = ceildiv(tx0, p.sx(c)); tcy0[c] = ceildiv(ty0, p.sy(c));
+        tcx1[c] = ceildiv(tx1, p.sx(c)); tcy1[c] = ceildiv(ty1, p.sy(c));
+        build_geometry(comps[c], tcx0[c], tcy0[c], tcx1[c], tcy1[c], p);
+        assign_steps(comps[c], p, im.prec, false, &cq[c], 0, p.roi(c));
+    }
     // T2 decode (LRCP)
     struct TT { std::vector<TagTree> incl, imsb; };
     std::vector<std::vector<std::vector<TT>>> trees(im.nc);
@@ -2934,7 +3001,8 @@ t2done:
     struct Job { uint32_t c; Band* B; Cblk* K; };
     std::vector<Job> jobs;
     for (uint32_t c = 0; c < im.nc; ++c) {
-        if (!p.irreversible) ip[c].assign((size_t)TW * TH, 0); else fp[c].assign((size_t)TW * TH, 0.f);
+        const size_t n = (size_t)comps[c].w * comps[c].h;
+        if (!p.irreversible) ip[c].assign(n, 0); else fp[c].assign(n, 0.f);
         for (uint32_t r = 0; r < p.numres; ++r)
             for (auto& B : comps[c].res[r].bands)
                 for (auto& P : B.prcs)
@@ -2945,6 +3013,7 @@ t2done:
                         const uint32_t c = jobs[ji].c;
                         Band& B = *jobs[ji].B;
                         Cblk& K = *jobs[ji].K;
+                        const uint32_t TW = comps[c].w;   // tile-component row stride
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
                         std::vector<int32_t> blk(w * h);
                         if (p.ht()) {   // T1HT::decompress: k_msbs = band numbps - cblk numbps
@@ -3008,33 +3077,45 @@ t2done:
         Comp& C = comps[c];
         // reduced-resolution decode: the inverse transform stops at resolution numres-1-reduce,
         // whose samples sit at the tile buffer's corner (resolutions_to_decompress)
-        if (!p.irreversible) dwt2d<int32_t>(ip[c].data(), TW, C, p.numres - red, false, inv53_1d);
-        else dwt2d<float>(fp[c].data(), TW, C, p.numres - red, false, inv97_1d);
+        if (!p.irreversible) dwt2d<int32_t>(ip[c].data(), C.w, C, p.numres - red, false, inv53_1d);
+        else dwt2d<float>(fp[c].data(), C.w, C, p.numres - red, false, inv97_1d);
     }
     int32_t shift = im.sgnd ? 0 : (1 << (im.prec - 1));
     int32_t mn = im.sgnd ? -(1 << (im.prec - 1)) : 0, mxv = im.sgnd ? (1 << (im.prec - 1)) - 1 : (1 << im.prec) - 1;
-    // reduced image area: [ceil(x0 / 2^r), ceil((x0 + w) / 2^r)) on the reduced canvas
-    const uint32_t Wr = ceildivpow2(p.x0 + im.w, red) - ceildivpow2(p.x0, red);
-    const uint32_t Hr = ceildivpow2(p.y0 + im.h, red) - ceildivpow2(p.y0, red);
-    const uint32_t tx0r = ceildivpow2(tx0, red) - ceildivpow2(p.x0, red), ty0r = ceildivpow2(ty0, red) - ceildivpow2(p.y0, red);
-    const uint32_t TWr = ceildivpow2(tx1, red) - ceildivpow2(tx0, red), THr = ceildivpow2(ty1, red) - ceildivpow2(ty0, red);
-    const size_t n = (size_t)TW * TH, N = (size_t)Wr * Hr;
+    // component c's reduced area: [ceil(ceil(x0 / XRsiz) / 2^r), ...) on its reduced grid, the
+    // output planes back to back (one image-sized plane each without subsampling)
+    std::vector<size_t> ooff(im.nc + 1, 0);
+    std::vector<uint32_t> Wr(im.nc), tx0r(im.nc), ty0r(im.nc), TWr(im.nc), THr(im.nc);
+    for (uint32_t c = 0; c < im.nc; ++c) {
+        const uint32_t ox = ceildivpow2(ceildiv(p.x0, p.sx(c)), red), oy = ceildivpow2(ceildiv(p.y0, p.sy(c)), red);
+        Wr[c] = ceildivpow2(ceildiv(p.x0 + im.w, p.sx(c)), red) - ox;
+        const uint32_t Hr = ceildivpow2(ceildiv(p.y0 + im.h, p.sy(c)), red) - oy;
+        ooff[c + 1] = ooff[c] + (size_t)Wr[c] * Hr;
+        tx0r[c] = ceildivpow2(tcx0[c], red) - ox; ty0r[c] = ceildivpow2(tcy0[c], red) - oy;
+        TWr[c] = ceildivpow2(tcx1[c], red) - ceildivpow2(tcx0[c], red); THr[c] = ceildivpow2(tcy1[c], red) - ceildivpow2(tcy0[c], red);
+    }
     auto put = [&](uint32_t c, size_t k, int32_t v) {
-        const uint32_t x = (uint32_t)(k % TW), y = (uint32_t)(k / TW);
-        if (x >= TWr || y >= THr) return;
-        out[c * N + (size_t)(ty0r + y) * Wr + tx0r + x] = std::min(mxv, std::max(mn, v + shift));
+        const uint32_t x = (uint32_t)(k % comps[c].w), y = (uint32_t)(k / comps[c].w);
+        if (x >= TWr[c] || y >= THr[c]) return;
+        out[ooff[c] + (size_t)(ty0r[c] + y) * Wr[c] + tx0r[c] + x] = std::min(mxv, std::max(mn, v + shift));
     };
+    // the inverse MCT needs the first three tile-components of one size (needsMctDecompress,
+    // TileProcessor.cpp:432-456: Grok skips it with a warning otherwise)
+    const bool mct = p.mct && im.nc >= 3 && comps[1].w == comps[0].w && comps[2].w == comps[0].w &&
+                     comps[1].h == comps[0].h && comps[2].h == comps[0].h;
+    const size_t n = (size_t)comps[0].w * comps[0].h;
+    auto nof = [&](uint32_t c) { return (size_t)comps[c].w * comps[c].h; };
     if (!p.irreversible) {
-        if (p.mct && im.nc >= 3)
+        if (mct)
             for (size_t k = 0; k < n; ++k) {
                 int32_t y = ip[0][k], u = ip[1][k], v = ip[2][k];
                 int32_t g = y - ((u + v) >> 2), rr = v + g, b = u + g;
                 ip[0][k] = rr; ip[1][k] = g; ip[2][k] = b;
             }
         for (uint32_t c = 0; c < im.nc; ++c)
-            for (size_t k = 0; k < n; ++k) put(c, k, ip[c][k]);
+            for (size_t k = 0; k < nof(c); ++k) put(c, k, ip[c][k]);
     } else {
-        if (p.mct && im.nc >= 3)
+        if (mct)
             for (size_t k = 0; k < n; ++k) {
                 float y = fp[0][k], u = fp[1][k], v = fp[2][k];
                 fp[0][k] = y + 1.402f * v;
@@ -3042,7 +3123,7 @@ t2done:
                 fp[2][k] = y + 1.772f * u;
             }
         for (uint32_t c = 0; c < im.nc; ++c)
-            for (size_t k = 0; k < n; ++k) put(c, k, (int32_t)lrintf(fp[c][k]));
+            for (size_t k = 0; k < nof(c); ++k) put(c, k, (int32_t)lrintf(fp[c][k]));
     }
     return 0;
 }
@@ -3084,6 +3165,12 @@ static size_t resync_part_end(const uint8_t* cs, size_t len, size_t pos, size_t 
     return end;
 }
 
+// the (reduced) plane sizes of the last orc_decode's components, (w, h) each; returns the count
+static thread_local std::vector<uint32_t> t_comp_dims;
+uint32_t orc_last_comp_dims(uint32_t* out) {
+    if (out) std::copy(t_comp_dims.begin(), t_comp_dims.end(), out);
+    return (uint32_t)(t_comp_dims.size() / 2);
+}
 // the next decodes as through a decode window (Grok's partial-tile inverse), or not
 extern "C" void orc_set_partial(int on) { g_partial_inverse = on != 0; }
 // the inverse 5/3 of a single-sample line holding v (test hook for the rule above)
@@ -3132,7 +3219,13 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
                 (uint64_t)p.gx0 + p.tw <= p.x0 || (uint64_t)p.gy0 + p.th <= p.y0)
                 return -2;
             im.nc = get16(s + 34);
+            if (!im.nc || L < 38 + 3 * im.nc) return -2;
             im.prec = (s[36] & 0x7f) + 1; im.sgnd = (s[36] & 0x80) != 0;
+            p.cdx.assign(im.nc, 1); p.cdy.assign(im.nc, 1);
+            for (uint32_t c = 0; c < im.nc; ++c) {   // XRsiz / YRsiz (1..255)
+                p.cdx[c] = s[37 + 3 * c]; p.cdy[c] = s[38 + 3 * c];
+                if (!p.cdx[c] || !p.cdy[c]) return -2;
+            }
         } else if (m == 0xff52) {
             uint32_t scod = s[0];
             cod_body.assign(s, s + L - 2);
@@ -3183,9 +3276,19 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     *W = ceildivpow2(p.x0 + im.w, g_dec_reduce) - ceildivpow2(p.x0, g_dec_reduce);
     *H = ceildivpow2(p.y0 + im.h, g_dec_reduce) - ceildivpow2(p.y0, g_dec_reduce);
     *NC = im.nc; *PREC = im.prec;
+    // each component's (reduced) plane size: orc_last_comp_dims
+    t_comp_dims.clear();
+    size_t total = 0;
+    for (uint32_t c = 0; c < im.nc; ++c) {
+        const uint32_t sx = p.sx(c), sy = p.sy(c);
+        const uint32_t cw = ceildivpow2(ceildiv(p.x0 + im.w, sx), g_dec_reduce) - ceildivpow2(ceildiv(p.x0, sx), g_dec_reduce);
+        const uint32_t ch = ceildivpow2(ceildiv(p.y0 + im.h, sy), g_dec_reduce) - ceildivpow2(ceildiv(p.y0, sy), g_dec_reduce);
+        t_comp_dims.push_back(cw); t_comp_dims.push_back(ch);
+        total += (size_t)cw * ch;
+    }
     if (!out) return 0;
     if (p.gx0 + p.tw >= p.x0 + im.w && p.gy0 + p.th >= p.y0 + im.h) p.tw = p.th = 0;   // one tile
-    std::fill(out, out + (size_t)im.nc * *W * *H, 0);
+    std::fill(out, out + total, 0);
     const uint32_t nt = tile_count(p, im.w, im.h);
     size_t pos = first_sot;
     struct Part { size_t data, end; uint32_t tile, tpsot; std::vector<PocE> pocs; };

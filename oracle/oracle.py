@@ -31,6 +31,7 @@ class CParams(ctypes.Structure):
         ("tile_y0", ctypes.c_uint32),
         ("nq", ctypes.c_uint32), ("comp_gb", ctypes.c_uint32 * 16), ("comp_qshift", ctypes.c_int32 * 16),
         ("qderived", ctypes.c_uint32),
+        ("nsub", ctypes.c_uint32), ("sub_dx", ctypes.c_uint32 * 16), ("sub_dy", ctypes.c_uint32 * 16),
     ]
 
 
@@ -59,6 +60,8 @@ def lib():
         _lib.orc_decode.restype = ctypes.c_int
         _lib.orc_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p] + [P(ctypes.c_uint32)] * 4
         _lib.orc_set_partial.argtypes = [ctypes.c_int]
+        _lib.orc_last_comp_dims.restype = ctypes.c_uint32
+        _lib.orc_last_comp_dims.argtypes = [ctypes.c_void_p]
         _lib.orc_inv53_single.argtypes = [ctypes.c_int32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
         _lib.orc_inv53_single.restype = ctypes.c_int32
         _lib.orc_forward_coefs.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -105,7 +108,7 @@ def get_threads():
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
            layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None, roi=None,
            sop=False, eph=False, quality=None, origin=None, tile_origin=None, comp_guard_bits=None, comp_qshift=None,
-           qderived=False):
+           qderived=False, subsampling=None):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -143,6 +146,11 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
             p.comp_gb[c] = int((comp_guard_bits or [])[c]) if c < len(comp_guard_bits or []) else 2
             p.comp_qshift[c] = int((comp_qshift or [])[c]) if c < len(comp_qshift or []) else 0
     p.qderived = int(bool(qderived))
+    # component subsampling [(dx, dy), ...] (grk_image_comp::dx / dy; SIZ XRsiz / YRsiz)
+    if subsampling:
+        p.nsub = len(subsampling)
+        for c, (dx, dy) in enumerate(subsampling):
+            p.sub_dx[c], p.sub_dy[c] = int(dx), int(dy)
     p.cod_format = 2 if jp2 else 0
     if layer_rate:
         p.nlayers = len(layer_rate)
@@ -180,9 +188,25 @@ def _planes(img):
     return a
 
 
-def encode(img, prec, signed=False, **kw):
-    a = _planes(img)
-    c, h, w = a.shape
+def comp_shape(w, h, dx, dy, origin=(0, 0)):
+    """(rows, cols) of a component sampled every (dx, dy) on the canvas (grk_image_comp h / w)."""
+    x0, y0 = origin
+    return -(-(y0 + h) // dy) - -(-y0 // dy), -(-(x0 + w) // dx) - -(-x0 // dx)
+
+
+def encode(img, prec, signed=False, size=None, **kw):
+    """img: (C, H, W) int32 array; with subsampling=[(dx, dy), ...], a list of per-component 2-D
+    planes of comp_shape(W, H, dx, dy, origin) and size=(W, H), the image area."""
+    if kw.get("subsampling"):
+        planes = [np.ascontiguousarray(x, dtype=np.int32) for x in img]
+        w, h = size
+        c = len(planes)
+        for k, (dx, dy) in enumerate(kw["subsampling"]):
+            assert planes[k].shape == comp_shape(w, h, dx, dy, kw.get("origin") or (0, 0)), (k, planes[k].shape)
+        a = np.concatenate([x.ravel() for x in planes])
+    else:
+        a = _planes(img)
+        c, h, w = a.shape
     p = params(**kw)
     cap = a.nbytes * 2 + (1 << 16)
     out = np.empty(cap, dtype=np.uint8)
@@ -251,15 +275,25 @@ def decode(cs, partial=False):
                           ctypes.byref(PREC))
     if rc != 0:
         raise RuntimeError("oracle decode header failed: %d" % rc)
-    out = np.empty((NC.value, H.value, W.value), dtype=np.int32)
+    dims = (ctypes.c_uint32 * (2 * NC.value))()
+    lib().orc_last_comp_dims(dims)
+    shapes = [(dims[2 * c + 1], dims[2 * c]) for c in range(NC.value)]
+    flat = np.empty(sum(a * b for a, b in shapes), dtype=np.int32)
     lib().orc_set_partial(int(bool(partial)))
     try:
-        rc = lib().orc_decode(buf.ctypes.data, len(cs), out.ctypes.data, ctypes.byref(W), ctypes.byref(H),
+        rc = lib().orc_decode(buf.ctypes.data, len(cs), flat.ctypes.data, ctypes.byref(W), ctypes.byref(H),
                               ctypes.byref(NC), ctypes.byref(PREC))
     finally:
         lib().orc_set_partial(0)
     if rc != 0:
         raise RuntimeError("oracle decode failed: %d" % rc)
+    if all(sh == (H.value, W.value) for sh in shapes):
+        return flat.reshape(NC.value, H.value, W.value), PREC.value
+    # subsampled components: one plane each, at its own size
+    out, o = [], 0
+    for sh in shapes:
+        out.append(flat[o:o + sh[0] * sh[1]].reshape(sh))
+        o += sh[0] * sh[1]
     return out, PREC.value
 
 
