@@ -39,6 +39,7 @@ static int enc(int argc, char** argv) {
     int to_file = 0;
     GRK_CODEC_FORMAT fmt = GRK_CODEC_J2K;
     int raw_tiles = 0, tile_off = 0, img_off = 0;
+    uint32_t sdx[4] = {1, 1, 1, 1}, sdy[4] = {1, 1, 1, 1};
     for (int i = 8; i < argc; ++i) {
         if (!strcmp(argv[i], "-n")) p.numresolution = (uint8_t)atoi(argv[++i]);
         else if (!strcmp(argv[i], "-b")) sscanf(argv[++i], "%u,%u", &p.cblockw_init, &p.cblockh_init);
@@ -84,6 +85,16 @@ static int enc(int argc, char** argv) {
             p.allocationByQuality = true;
         }
         else if (!strcmp(argv[i], "-T")) { sscanf(argv[++i], "%u,%u", &p.tx0, &p.ty0); tile_off = 1; }   /* :1512-1529 */
+        else if (!strcmp(argv[i], "-sub")) {   /* API-level subsampling (grk_image_comp dx / dy): dx1xdy1:dx2xdy2:...
+                                                  (the CLI's raw reader refuses it, RAWFormat.cpp:293-298) */
+            char* s = argv[++i];
+            for (uint32_t k = 0; k < 4 && *s; ++k) {
+                sscanf(s, "%ux%u", &sdx[k], &sdy[k]);
+                char* q = strchr(s, ':');
+                if (!q) break;
+                s = q + 1;
+            }
+        }
         else if (!strcmp(argv[i], "-d")) {   /* :1530-1545 image offset */
             sscanf(argv[++i], "%u,%u", &p.image_offset_x0, &p.image_offset_y0);
             img_off = 1;
@@ -110,19 +121,25 @@ static int enc(int argc, char** argv) {
     }
     grk_image_cmptparm cp[4];
     memset(cp, 0, sizeof cp);
-    /* the image readers place the image at the -d offset (RAWFormat.cpp:309-312, PNMFormat.cpp:474-477) */
+    /* the image readers place the image at the -d offset (RAWFormat.cpp:309-312, PNMFormat.cpp:474-477);
+       a subsampled component holds the image area sampled every (dx, dy): ceil(x1 / dx) - ceil(x0 / dx)
+       columns (GrkImage.cpp:74-113) */
+    const uint32_t X0 = p.image_offset_x0, Y0 = p.image_offset_y0;
     for (uint32_t k = 0; k < c; ++k) {
-        cp[k].dx = cp[k].dy = 1; cp[k].w = w; cp[k].h = h; cp[k].prec = (uint8_t)prec;
-        cp[k].x0 = p.image_offset_x0; cp[k].y0 = p.image_offset_y0;
+        cp[k].dx = sdx[k]; cp[k].dy = sdy[k]; cp[k].prec = (uint8_t)prec;
+        cp[k].w = (X0 + w + sdx[k] - 1) / sdx[k] - (X0 + sdx[k] - 1) / sdx[k];
+        cp[k].h = (Y0 + h + sdy[k] - 1) / sdy[k] - (Y0 + sdy[k] - 1) / sdy[k];
+        cp[k].x0 = X0; cp[k].y0 = Y0;
     }
     grk_image* img = grk_image_new((uint16_t)c, cp, c >= 3 ? GRK_CLRSPC_SRGB : GRK_CLRSPC_GRAY, true);
     if (!img) return 2;
+    img->x0 = X0; img->y0 = Y0; img->x1 = X0 + w; img->y1 = Y0 + h;
     FILE* f = fopen(raw, "rb");
     int32_t* row = malloc(sizeof(int32_t) * w);
     for (uint32_t k = 0; k < c; ++k)
-        for (uint32_t y = 0; y < h; ++y) {
-            if (fread(row, 4, w, f) != w) return 3;
-            memcpy(img->comps[k].data + (size_t)y * img->comps[k].stride, row, 4 * w);
+        for (uint32_t y = 0; y < cp[k].h; ++y) {
+            if (fread(row, 4, cp[k].w, f) != cp[k].w) return 3;
+            memcpy(img->comps[k].data + (size_t)y * img->comps[k].stride, row, 4 * cp[k].w);
         }
     fclose(f);
     /* compress() :2055-2066: a memory stream the size of 1.5x the raw image, or the output file */

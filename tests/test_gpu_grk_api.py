@@ -230,3 +230,27 @@ def test_grk_api_wide_code_blocks(tool, flags, grok_bytes, grok_sha):
     dec, _ = _dec(tool, path, img.shape)
     want, _ = O.decode(cs)
     np.testing.assert_array_equal(dec, want)
+
+
+@pytest.mark.parametrize("name, flags", [("420_53", "-n 3"), ("tiled_pcrl", "-n 3 -t 64,32 -p PCRL -c [16,16]"),
+                                         ("422_97", "-n 4 -I")])
+def test_grk_api_subsampled_components(tool, name, flags):
+    # an API user's grk_image with subsampled components (grk_image_comp dx / dy): the shim codes
+    # the oracle's bytes and decodes each component at its own size (the CLI's raw reader itself
+    # refuses subsampling, RAWFormat.cpp:293-298, so this is the library-level call sequence)
+    from subsampling_cases import CASES, planes, oracle_kw
+    W, H, sub, prec, kw = CASES[name]
+    exe, d = tool
+    src = planes(name)
+    raw = d / (name + "_sub.raw")
+    np.concatenate([p.ravel() for p in src]).astype(np.int32).tofile(raw)
+    out = d / (name + "_sub.j2k")
+    subarg = ":".join("%dx%d" % s for s in sub)
+    _run(exe, "enc", raw, W, H, len(sub), prec, out, *flags.split(), "-sub", subarg)
+    ref = O.encode(src, prec, size=(W, H), **oracle_kw(name))
+    assert out.read_bytes() == ref
+    dec = d / (name + "_sub.dec")
+    _run(exe, "dec", out, dec)
+    flat = np.fromfile(dec, np.int32)
+    want, _ = O.decode(ref)
+    np.testing.assert_array_equal(flat, np.concatenate([w.ravel() for w in want]))
