@@ -1439,8 +1439,14 @@ static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uin
                             uint32_t c0, uint32_t c1, std::vector<uint8_t>& seen, const std::vector<uint32_t>& base,
                             std::vector<PktRef>& v, std::vector<uint32_t>* entry = nullptr, uint32_t ei = 0,
                             uint32_t* iter = nullptr) {
-    const uint32_t nc = (uint32_t)comps.size(), nr = p.numres;
+    // (per-component resolution counts: a COC may give a component fewer decomposition levels;
+    // resolution r of a component without it has no packets, PacketIter.cpp:160-162)
+    const uint32_t nc = (uint32_t)comps.size();
+    uint32_t nr = 0;
+    for (const Comp& C : comps) nr = std::max<uint32_t>(nr, (uint32_t)C.res.size());
+    auto nres = [&](uint32_t c) { return (uint32_t)comps[c].res.size(); };
     auto nprc = [&](uint32_t c, uint32_t r) {
+        if (r >= nres(c)) return 0u;
         const Res& R = comps[c].res[r];
         return (R.x1 > R.x0 && R.y1 > R.y0) ? R.pw * R.ph : 0u;
     };
@@ -1467,8 +1473,8 @@ static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uin
     auto steps = [&](uint32_t ca, uint32_t cb) {
         dx = ~0ull; dy = ~0ull;
         for (uint32_t c = ca; c < cb; ++c)
-            for (uint32_t r = 0; r < nr; ++r) {
-                const uint32_t lv = nr - 1 - r;
+            for (uint32_t r = 0; r < nres(c); ++r) {
+                const uint32_t lv = nres(c) - 1 - r;
                 dx = std::min<uint64_t>(dx, (uint64_t)p.sx(c) << (comps[c].res[r].prcw_exp + lv));
                 dy = std::min<uint64_t>(dy, (uint64_t)p.sy(c) << (comps[c].res[r].prch_exp + lv));
             }
@@ -1478,9 +1484,9 @@ static void packet_iter_one(const std::vector<Comp>& comps, const Params& p, uin
     // canvas position is a multiple of XRsiz * 2^(PPx + level), or at the tile origin when the
     // resolution's origin is off its precinct grid (that test without XRsiz, as there)
     auto prc_at = [&](uint32_t c, uint32_t r, uint64_t x, uint64_t y, uint32_t& pi) {
-        const Res& R = comps[c].res[r];
         if (!nprc(c, r)) return false;
-        const uint32_t lv = nr - 1 - r;
+        const Res& R = comps[c].res[r];
+        const uint32_t lv = nres(c) - 1 - r;
         const uint64_t rpx = R.prcw_exp + lv, rpy = R.prch_exp + lv, sxc = p.sx(c), syc = p.sy(c);
         if (!((x % (sxc << rpx)) == 0 || (x == tx0 && (((uint64_t)R.x0 << lv) % (1ull << rpx)) != 0))) return false;
         if (!((y % (syc << rpy)) == 0 || (y == ty0 && (((uint64_t)R.y0 << lv) % (1ull << rpy)) != 0))) return false;
@@ -1524,12 +1530,15 @@ static std::vector<PktRef> packet_iter(const std::vector<Comp>& comps, const Par
                                        uint32_t tx1, uint32_t ty1, uint32_t nlayers,
                                        const std::vector<PocE>* pocs = nullptr, std::vector<uint32_t>* entry = nullptr) {
     std::vector<PktRef> v;
-    const uint32_t nc = (uint32_t)comps.size(), nr = p.numres;
+    const uint32_t nc = (uint32_t)comps.size();
+    uint32_t nr = 0;
+    for (const Comp& C : comps) nr = std::max<uint32_t>(nr, (uint32_t)C.res.size());
     std::vector<uint32_t> base(nc * nr + 1, 0);
     for (uint32_t c = 0, k = 0; c < nc; ++c)
         for (uint32_t r = 0; r < nr; ++r, ++k) {
-            const Res& R = comps[c].res[r];
-            base[k + 1] = base[k] + ((R.x1 > R.x0 && R.y1 > R.y0) ? R.pw * R.ph : 0u);
+            const bool has = r < comps[c].res.size();
+            const Res* R = has ? &comps[c].res[r] : nullptr;
+            base[k + 1] = base[k] + ((has && R->x1 > R->x0 && R->y1 > R->y0) ? R->pw * R->ph : 0u);
         }
     std::vector<uint8_t> seen((size_t)base[nc * nr] * nlayers + 1, 0);
     if (!pocs || pocs->empty()) {
@@ -2881,7 +2890,7 @@ void orc_t1_decode_cblk(const uint8_t* data, uint32_t len, uint32_t npasses, uin
 // ranges: the packet bytes [data, end) of the tile's tile parts in TPsot order (a tile's
 // packet sequence continues across its parts, A.4.2)
 static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, size_t>>& ranges, const Params& p,
-                       const Image& im, const std::vector<Quant>& cq, uint32_t tile,
+                       const std::vector<Params>& pcs, const Image& im, const std::vector<Quant>& cq, uint32_t tile,
                        int32_t* out, const std::vector<PocE>* tpocs = nullptr) {
     size_t data = ranges[0].first, tile_end = ranges[0].second, next_range = 1;
     uint32_t tx0, ty0, tx1, ty1;
@@ -2895,15 +2904,15 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
     for (uint32_t c = 0; c < im.nc; ++c) {
         tcx0[c] = ceildiv(tx0, p.sx(c)); tcy0[c] = ceildiv(ty0, p.sy(c));
         tcx1[c] = ceildiv(tx1, p.sx(c)); tcy1[c] = ceildiv(ty1, p.sy(c));
-        build_geometry(comps[c], tcx0[c], tcy0[c], tcx1[c], tcy1[c], p);
-        assign_steps(comps[c], p, im.prec, false, &cq[c], 0, p.roi(c));
+        build_geometry(comps[c], tcx0[c], tcy0[c], tcx1[c], tcy1[c], pcs[c]);
+        assign_steps(comps[c], pcs[c], im.prec, false, &cq[c], 0, p.roi(c));
     }
     // T2 decode (LRCP)
     struct TT { std::vector<TagTree> incl, imsb; };
     std::vector<std::vector<std::vector<TT>>> trees(im.nc);
     for (uint32_t c = 0; c < im.nc; ++c) {
-        trees[c].resize(p.numres);
-        for (uint32_t r = 0; r < p.numres; ++r) {
+        trees[c].resize(pcs[c].numres);
+        for (uint32_t r = 0; r < pcs[c].numres; ++r) {
             Res& R = comps[c].res[r];
             trees[c][r].resize(R.pw * R.ph);
             for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
@@ -2923,7 +2932,8 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
                 Res& R = comps[c].res[r];
                 // layers past the limit and resolutions past the reduction: header parsed for
                 // the coding state, data skipped (T2Decompress::processPacket, T2Decompress.cpp:55-116)
-                const bool skip_l = (g_dec_layers && l >= g_dec_layers) || r + red >= p.numres;
+                const bool skip_l = (g_dec_layers && l >= g_dec_layers) || r + red >= pcs[c].numres;
+                const uint32_t sty = pcs[c].cblk_sty;
                 {
                     while (pos >= tile_end && next_range < ranges.size()) {
                         pos = ranges[next_range].first; tile_end = ranges[next_range].second; ++next_range;
@@ -2964,10 +2974,10 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
                                 // when the last one holds its maximum pass count
                                 uint32_t nb = 0, left = np;
                                 while (left) {
-                                    if (K.segpasses.empty() || K.segpasses.back() == seg_maxpasses(p.cblk_sty, (uint32_t)K.segpasses.size() - 1)) {
+                                    if (K.segpasses.empty() || K.segpasses.back() == seg_maxpasses(sty, (uint32_t)K.segpasses.size() - 1)) {
                                         K.segpasses.push_back(0); K.seglens.push_back(0);
                                     }
-                                    const uint32_t room = seg_maxpasses(p.cblk_sty, (uint32_t)K.segpasses.size() - 1) - K.segpasses.back();
+                                    const uint32_t room = seg_maxpasses(sty, (uint32_t)K.segpasses.size() - 1) - K.segpasses.back();
                                     const uint32_t n = std::min(room, left);
                                     const uint32_t sl = br.read((int)K.numlenbits + floorlog2(n));
                                     K.segpasses.back() += n;
@@ -3002,8 +3012,8 @@ t2done:
     std::vector<Job> jobs;
     for (uint32_t c = 0; c < im.nc; ++c) {
         const size_t n = (size_t)comps[c].w * comps[c].h;
-        if (!p.irreversible) ip[c].assign(n, 0); else fp[c].assign(n, 0.f);
-        for (uint32_t r = 0; r < p.numres; ++r)
+        if (!pcs[c].irreversible) ip[c].assign(n, 0); else fp[c].assign(n, 0.f);
+        for (uint32_t r = 0; r < pcs[c].numres; ++r)
             for (auto& B : comps[c].res[r].bands)
                 for (auto& P : B.prcs)
                     for (auto& K : P.cblks) jobs.push_back({c, &B, &K});
@@ -3014,6 +3024,7 @@ t2done:
                         Band& B = *jobs[ji].B;
                         Cblk& K = *jobs[ji].K;
                         const uint32_t TW = comps[c].w;   // tile-component row stride
+                        const Params& p = pcs[c];         // the component's coding (COD / COC)
                         uint32_t w = K.x1 - K.x0, h = K.y1 - K.y0;
                         std::vector<int32_t> blk(w * h);
                         if (p.ht()) {   // T1HT::decompress: k_msbs = band numbps - cblk numbps
@@ -3077,8 +3088,8 @@ t2done:
         Comp& C = comps[c];
         // reduced-resolution decode: the inverse transform stops at resolution numres-1-reduce,
         // whose samples sit at the tile buffer's corner (resolutions_to_decompress)
-        if (!p.irreversible) dwt2d<int32_t>(ip[c].data(), C.w, C, p.numres - red, false, inv53_1d);
-        else dwt2d<float>(fp[c].data(), C.w, C, p.numres - red, false, inv97_1d);
+        if (!pcs[c].irreversible) dwt2d<int32_t>(ip[c].data(), C.w, C, pcs[c].numres - red, false, inv53_1d);
+        else dwt2d<float>(fp[c].data(), C.w, C, pcs[c].numres - red, false, inv97_1d);
     }
     int32_t shift = im.sgnd ? 0 : (1 << (im.prec - 1));
     int32_t mn = im.sgnd ? -(1 << (im.prec - 1)) : 0, mxv = im.sgnd ? (1 << (im.prec - 1)) - 1 : (1 << im.prec) - 1;
@@ -3105,26 +3116,21 @@ t2done:
                      comps[1].h == comps[0].h && comps[2].h == comps[0].h;
     const size_t n = (size_t)comps[0].w * comps[0].h;
     auto nof = [&](uint32_t c) { return (size_t)comps[c].w * comps[c].h; };
-    if (!p.irreversible) {
-        if (mct)
-            for (size_t k = 0; k < n; ++k) {
-                int32_t y = ip[0][k], u = ip[1][k], v = ip[2][k];
-                int32_t g = y - ((u + v) >> 2), rr = v + g, b = u + g;
-                ip[0][k] = rr; ip[1][k] = g; ip[2][k] = b;
-            }
-        for (uint32_t c = 0; c < im.nc; ++c)
-            for (size_t k = 0; k < nof(c); ++k) put(c, k, ip[c][k]);
-    } else {
-        if (mct)
-            for (size_t k = 0; k < n; ++k) {
-                float y = fp[0][k], u = fp[1][k], v = fp[2][k];
-                fp[0][k] = y + 1.402f * v;
-                fp[1][k] = y - 0.34413f * u - 0.71414f * v;
-                fp[2][k] = y + 1.772f * u;
-            }
-        for (uint32_t c = 0; c < im.nc; ++c)
-            for (size_t k = 0; k < nof(c); ++k) put(c, k, (int32_t)lrintf(fp[c][k]));
-    }
+    if (mct && !pcs[0].irreversible)
+        for (size_t k = 0; k < n; ++k) {
+            int32_t y = ip[0][k], u = ip[1][k], v = ip[2][k];
+            int32_t g = y - ((u + v) >> 2), rr = v + g, b = u + g;
+            ip[0][k] = rr; ip[1][k] = g; ip[2][k] = b;
+        }
+    if (mct && pcs[0].irreversible)
+        for (size_t k = 0; k < n; ++k) {
+            float y = fp[0][k], u = fp[1][k], v = fp[2][k];
+            fp[0][k] = y + 1.402f * v;
+            fp[1][k] = y - 0.34413f * u - 0.71414f * v;
+            fp[2][k] = y + 1.772f * u;
+        }
+    for (uint32_t c = 0; c < im.nc; ++c)   // (each component by its own transform)
+        for (size_t k = 0; k < nof(c); ++k) put(c, k, pcs[c].irreversible ? (int32_t)lrintf(fp[c][k]) : ip[c][k]);
     return 0;
 }
 
@@ -3132,11 +3138,22 @@ t2done:
 // COD / QCD per component or per tile): this restatement codes every tile-component with the
 // main header's parameters, so it accepts such a marker only when it restates them.
 // qcc: the main header's quantisation body per component (its QCC, else the QCD)
+// ccod: each component's coding as a COC body would state it (Scoc precinct flag, then SPcoc):
+// its main COC, else the COD's
+static std::vector<uint8_t> cod_as_coc(const std::vector<uint8_t>& cod) {
+    std::vector<uint8_t> v{(uint8_t)(cod[0] & 1)};
+    v.insert(v.end(), cod.begin() + 5, cod.end());
+    return v;
+}
 static bool restates_main(const uint8_t* b, uint32_t L, uint32_t m, uint32_t nc, const std::vector<uint8_t>& cod,
-                          const std::vector<uint8_t>& qcd, const std::vector<std::vector<uint8_t>>& qcc) {
+                          const std::vector<uint8_t>& qcd, const std::vector<std::vector<uint8_t>>& qcc,
+                          const std::vector<std::vector<uint8_t>>& ccod) {
     if (L < 3) return false;
     const std::vector<uint8_t> v(b, b + L - 2);
-    if (m == 0xff52) return v == cod;
+    if (m == 0xff52) {   // (a tile COD would replace the main COCs too)
+        for (const auto& q : ccod) if (q != cod_as_coc(cod)) return false;
+        return v == cod;
+    }
     if (m == 0xff5c) {
         for (const auto& q : qcc) if (q != qcd) return false;   // a tile QCD would replace differing QCCs
         return v == qcd;
@@ -3145,7 +3162,25 @@ static bool restates_main(const uint8_t* b, uint32_t L, uint32_t m, uint32_t nc,
     if (v.size() <= cw || (cw == 1 ? v[0] : get16(b)) >= nc) return false;
     const uint32_t c = cw == 1 ? v[0] : get16(b);
     if (m == 0xff5d) return std::equal(v.begin() + cw, v.end(), qcc[c].begin(), qcc[c].end());
-    return cod.size() > 5 && (v[cw] & 1) == (cod[0] & 1) && std::equal(v.begin() + cw + 1, v.end(), cod.begin() + 5, cod.end());
+    return (v[cw] & 1) == ccod[c][0] && std::equal(v.begin() + cw + 1, v.end(), ccod[c].begin() + 1, ccod[c].end());
+}
+
+// A component's coding parameters from its COC-form body (Scoc, SPcoc: decomposition levels,
+// code-block size and style, transform, [precinct sizes]; CodeStreamDecompress read_coc /
+// read_SPCod_SPCoc), over the stream's parameters; false when malformed
+static bool comp_params(const std::vector<uint8_t>& v, Params& pc) {
+    if (v.size() < 6) return false;
+    pc.numres = v[1] + 1u; pc.cbw_exp = v[2] + 2u; pc.cbh_exp = v[3] + 2u; pc.cblk_sty = v[4];
+    pc.irreversible = v[5] == 0;
+    if (pc.numres > 33 || pc.cbw_exp > 10 || pc.cbh_exp > 10 || pc.cbw_exp + pc.cbh_exp > 12) return false;
+    if ((pc.cblk_sty & 0x40) && pc.cblk_sty != 0x40) return false;
+    if (pc.cblk_sty & 0x80) return false;
+    for (uint32_t r = 0; r < 33; ++r) { pc.prcw_exp[r] = 15; pc.prch_exp[r] = 15; }
+    if (v[0] & 1) {
+        if (v.size() < 6 + pc.numres) return false;
+        for (uint32_t r = 0; r < pc.numres; ++r) { pc.prcw_exp[r] = v[6 + r] & 15; pc.prch_exp[r] = v[6 + r] >> 4; }
+    }
+    return prc_exps_ok(pc);
 }
 
 // A tile part's end from its Psot, checked: the next SOT (Lsot 10, a tile index below nt) or
@@ -3267,12 +3302,32 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     // Grok's precedence: a main QCC wins over the main QCD, Quantizer.cpp:215-235)
     std::vector<std::vector<uint8_t>> qbody(im.nc, qcd_body);
     for (const auto& q : qccs) qbody[q.first] = q.second;
+    // per component: the COD's coding, replaced by its main-header COC (A.6.2; Grok's read_coc
+    // fills the component's tccp, a main COC winning over the main COD in either order)
+    if (cod_body.size() < 10) return -3;
+    std::vector<std::vector<uint8_t>> ccod(im.nc, cod_as_coc(cod_body));
+    for (size_t k : coc_qcc) {
+        const uint32_t L = get16(cs + k + 2), cw = im.nc <= 256 ? 1 : 2;
+        if (L < 2 + cw + 6) return -2;
+        const uint8_t* b = cs + k + 4;
+        const uint32_t c = cw == 1 ? b[0] : get16(b);
+        if (c >= im.nc) return -2;
+        ccod[c].assign(b + cw, b + L - 2);
+    }
+    std::vector<Params> pcs(im.nc, p);
+    uint32_t min_res = 33;
+    for (uint32_t c = 0; c < im.nc; ++c) {
+        if (!comp_params(ccod[c], pcs[c])) return -2;
+        min_res = std::min(min_res, pcs[c].numres);
+    }
+    // the inverse MCT picks RCT / ICT by component 0's transform (TileProcessor::mctDecompress):
+    // first three components coded with different transforms are refused
+    if (p.mct && im.nc >= 3 && (pcs[1].irreversible != pcs[0].irreversible || pcs[2].irreversible != pcs[0].irreversible))
+        return -2;
     std::vector<Quant> cq(im.nc);
     for (uint32_t c = 0; c < im.nc; ++c)
-        if (!parse_quant(qbody[c].data(), qbody[c].size(), p.numres, cq[c])) return -2;
-    for (size_t k : coc_qcc)
-        if (!restates_main(cs + k + 4, get16(cs + k + 2), get16(cs + k), im.nc, cod_body, qcd_body, qbody)) return -2;
-    if (g_dec_reduce >= p.numres) return -7;   // reduce must leave one resolution
+        if (!parse_quant(qbody[c].data(), qbody[c].size(), pcs[c].numres, cq[c])) return -2;
+    if (g_dec_reduce >= min_res) return -7;   // reduce must leave one resolution of every component
     *W = ceildivpow2(p.x0 + im.w, g_dec_reduce) - ceildivpow2(p.x0, g_dec_reduce);
     *H = ceildivpow2(p.y0 + im.h, g_dec_reduce) - ceildivpow2(p.y0, g_dec_reduce);
     *NC = im.nc; *PREC = im.prec;
@@ -3306,7 +3361,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             const uint32_t tm = get16(cs + j);
             if (tm == 0xff5f && !read_poc(cs + j + 4, get16(cs + j + 2), im.nc, tp_pocs)) return -5;
             if ((tm == 0xff52 || tm == 0xff53 || tm == 0xff5c || tm == 0xff5d) &&
-                !restates_main(cs + j + 4, get16(cs + j + 2), tm, im.nc, cod_body, qcd_body, qbody)) return -2;
+                !restates_main(cs + j + 4, get16(cs + j + 2), tm, im.nc, cod_body, qcd_body, qbody, ccod)) return -2;
             if (tm == 0xff5e) return -2;   // tile-part RGN
             j += 2 + get16(cs + j + 2);
         }
@@ -3334,7 +3389,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         ranges[slot[q.tile]].push_back({q.data, q.end});
     }
     std::vector<int> rcs(tiles.size(), 0);   // tiles write disjoint rectangles of out
-    par_for(tiles.size(), [&](size_t q) { rcs[q] = decode_tile(cs, ranges[q], p, im, cq, tiles[q], out, &tpocs[q]); });
+    par_for(tiles.size(), [&](size_t q) { rcs[q] = decode_tile(cs, ranges[q], p, pcs, im, cq, tiles[q], out, &tpocs[q]); });
     for (int rc : rcs) if (rc) return rc;
     return 0;
 }

@@ -1,9 +1,9 @@
 """COC / QCC and tile-part COD / QCD markers in the oracle decoder.
 
 Grok reads COC / QCC (CodeStreamDecompress read_coc / read_qcc) and tile-part COD / QCD as
-per-component / per-tile overrides of the main COD / QCD.  A main-header QCC is applied to its
-component (tests/test_qcc.py); otherwise this path codes every tile-component with the main
-header's parameters, so a marker that restates them decodes exactly as the stream without it
+per-component / per-tile overrides of the main COD / QCD.  A main-header QCC / COC is applied to its
+component (tests/test_qcc.py, tests/test_coc.py); otherwise this path codes every tile with the
+main header's parameters, so a tile-part marker that restates them decodes exactly as the stream without it
 (some encoders write them unconditionally), and one that changes them is refused rather than
 ignored.  Streams: the committed Grok fixtures with markers spliced in
 (tests/j2k_markers.py).  The engine half is tests/test_gpu_override_markers.py.
@@ -34,7 +34,7 @@ def restating(cs):
 
 
 def changing(cs):
-    yield "main COC", J.insert_main(cs, J.coc(cs, 0, sty_xor=0x02))
+    # (a main-header COC that changes its component's coding is applied: tests/test_coc.py)
     yield "tile COD", J.insert_tile_part(cs, J.cod(cs, layers_add=1))
     yield "tile COC", J.insert_tile_part(cs, J.coc(cs, 0, sty_xor=0x08))
     yield "tile QCC", J.insert_tile_part(cs, J.qcc(cs, 0, guard_add=1))
