@@ -240,6 +240,29 @@ struct Params {
         for (uint32_t l = 0; l < nlayers; ++l) if (layer_rc(l)) return true;
         return false;
     }
+    // Per-component coding from main-header COC markers (A.6.2; CodeStreamDecompress read_coc):
+    // decomposition levels, code-block size and style, transform, precincts.  Empty: every
+    // component takes the COD's (always so on encode: grk_cparameters has one coding style).
+    struct CompCod {
+        uint32_t numres = 6, cbw = 6, cbh = 6, cblk_sty = 0, irrev = 0;
+        uint32_t prcw[GK_MAXRLVLS], prch[GK_MAXRLVLS];
+    };
+    std::vector<CompCod> cc;
+    uint32_t c_numres(uint32_t c) const { return cc.empty() ? numres : cc[c].numres; }
+    uint32_t c_cbw(uint32_t c) const { return cc.empty() ? cbw : cc[c].cbw; }
+    uint32_t c_cbh(uint32_t c) const { return cc.empty() ? cbh : cc[c].cbh; }
+    uint32_t c_sty(uint32_t c) const { return cc.empty() ? cblk_sty : cc[c].cblk_sty; }
+    uint32_t c_irrev(uint32_t c) const { return cc.empty() ? irrev : cc[c].irrev; }
+    uint32_t c_prcw(uint32_t c, uint32_t r) const { return cc.empty() ? prcw[r] : cc[c].prcw[r]; }
+    uint32_t c_prch(uint32_t c, uint32_t r) const { return cc.empty() ? prch[r] : cc[c].prch[r]; }
+    bool c_ht(uint32_t c) const { return (c_sty(c) & 0x40) != 0; }
+    bool c_wide(uint32_t c) const { return c_cbw(c) > 6 || c_cbh(c) > 6; }
+    // T1 kernel class of a component's blocks: 0 the headline Part-1 coders, 1 the lane-per-block
+    // coders of gk_t1ms.hip (mode switches or wide blocks), 2 HTJ2K; with the style bits and width
+    uint32_t c_class(uint32_t c) const {
+        const uint32_t k = c_ht(c) ? 2u : ((c_sty(c) & 0x3f) || c_wide(c)) ? 1u : 0u;
+        return k | (c_sty(c) & 0x3f) << 2 | (c_wide(c) ? 1u << 8 : 0u);
+    }
 };
 
 struct BandG {
@@ -289,12 +312,13 @@ struct ShapeG {
     GkTiles tb;
 };
 
-// Components sampled on one grid (SIZ XRsiz / YRsiz; grk_image_comp::dx / dy): their
-// tile-components are the tiles divided by (dx, dy), rounded up (TileProcessor.cpp:116-131), so
-// they share one set of tile classes and DWT launches.  Without subsampling there is one group
-// holding every component.
+// Components sampled on one grid (SIZ XRsiz / YRsiz; grk_image_comp::dx / dy) and transformed
+// alike (levels, 5/3 or 9/7: COD / COC): their tile-components are the tiles divided by
+// (dx, dy), rounded up (TileProcessor.cpp:116-131), so they share one set of tile classes and DWT
+// launches.  Without subsampling or COC there is one group holding every component.
 struct SGroup {
     uint32_t dx = 1, dy = 1;
+    uint32_t numres = 1, irrev = 0;      // the components' decomposition levels + 1 and transform (COD / COC)
     uint32_t ox = 0, oy = 0;             // the image area's origin on the group's grid: ceil(x0 / dx), ceil(y0 / dy)
     uint32_t w = 0, h = 0;               // its extent there (grk_image_comp w / h): a component plane's size
     std::vector<ShapeG> shapes;          // tile classes on the group's grid
@@ -328,6 +352,8 @@ struct Plan {
     std::vector<TileG> tiles;            // raster order
     std::vector<SGroup> groups;          // sampling grids (one without subsampling)
     std::vector<uint32_t> group_of;      // component -> group
+    uint32_t max_numres() const { uint32_t m = 0; for (const SGroup& G : groups) m = std::max(m, G.numres); return m; }
+    uint32_t min_numres() const { uint32_t m = 64; for (const SGroup& G : groups) m = std::min(m, G.numres); return m; }
     bool l1_fusable = true;              // every tile(-component) origin even: level 1 fuses with DC shift / MCT
     std::vector<GkBlock> blocks;         // tile order, then canonical: comp, res, band, precinct, cblk
     std::vector<uint32_t> bxy;           // per block: top-left (x, y) in its band's coordinates
@@ -429,23 +455,25 @@ static void ht_irrev_quant(uint32_t prec, bool sgnd, uint32_t nd, uint32_t r, ui
 static void assign_steps_tile(Plan& P, TileG& T) {
     for (uint32_t ci = 0; ci < (uint32_t)T.comps.size(); ++ci) {
         CompG& C = T.comps[ci];
-        for (uint32_t r = 0; r < P.p.numres; ++r) {
+        const uint32_t nres = P.p.c_numres(ci), irrev = P.p.c_irrev(ci);
+        const bool ht = P.p.c_ht(ci);
+        for (uint32_t r = 0; r < nres; ++r) {
             for (auto& B : C.res[r].bands) {
-                uint32_t level = P.p.numres - 1 - r;
-                if (P.p.ht() && !P.p.irrev) {
+                uint32_t level = nres - 1 - r;
+                if (ht && !irrev) {
                     B.mant = 0;
-                    B.expn = ht_rev_expn(P.prec, P.p.numres - 1, r, B.orient);
+                    B.expn = ht_rev_expn(P.prec, nres - 1, r, B.orient);
                     B.step_enc = B.step_dec = 1.0f;
                     B.numbps = (uint32_t)std::max(0, (int)B.expn + (int)P.p.numgbits - 1) + P.p.roi(ci);
                     continue;
                 }
-                uint32_t gain = P.p.irrev ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
-                if (P.p.ht()) {
-                    ht_irrev_quant(P.prec, P.sgnd != 0, P.p.numres - 1, r, B.orient, B.expn, B.mant);
+                uint32_t gain = irrev ? 0 : (B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1));
+                if (ht) {
+                    ht_irrev_quant(P.prec, P.sgnd != 0, nres - 1, r, B.orient, B.expn, B.mant);
                 } else {
                 // Part-1 QCD generation (HTParams.cpp:216-251)
                 double stepsize = 1.0;
-                if (P.p.irrev) stepsize = (double)(1u << gain) / band_norm(level, B.orient, false);
+                if (irrev) stepsize = (double)(1u << gain) / band_norm(level, B.orient, false);
                 uint32_t step = (uint32_t)floor(stepsize * 8192.0);
                 int pp = floorlog2(step) - 13, n = 11 - floorlog2(step);
                 B.mant = (n < 0 ? step >> -n : step << n) & 0x7ff;
@@ -453,7 +481,7 @@ static void assign_steps_tile(Plan& P, TileG& T) {
                 }
                 // Quantizer::setBandStepSizeAndBps (Quantizer.cpp:26-66)
                 uint32_t lg_enc = B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1);
-                uint32_t lg_dec = P.p.irrev ? 0 : lg_enc;
+                uint32_t lg_dec = irrev ? 0 : lg_enc;
                 B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
                 B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
                 int v = (int)B.expn + (int)P.p.numgbits - 1;
@@ -479,12 +507,12 @@ static void apply_qcd(Plan& P, const QuantList& q) {
         if (k1 <= k0) throw GkError("QCD / QCC without step sizes");
         const uint32_t gb = q[at[ci]].first;
         uint32_t bandno = 0;
-        for (uint32_t r = 0; r < P.p.numres; ++r)
+        for (uint32_t r = 0; r < P.p.c_numres(ci); ++r)
             for (auto& B : C.res[r].bands) {
                 size_t k = std::min<size_t>(k0 + bandno, k1 - 1);
                 B.expn = q[k].first; B.mant = q[k].second;
                 uint32_t lg_enc = B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1);
-                uint32_t lg_dec = P.p.irrev ? 0 : lg_enc;
+                uint32_t lg_dec = P.p.c_irrev(ci) ? 0 : lg_enc;
                 B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
                 B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
                 B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, (int)B.expn + (int)gb - 1);
@@ -515,7 +543,6 @@ static void parse_quant(const std::vector<uint8_t>& b, uint32_t numres, QuantLis
 static inline uint32_t ceildiv(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + b - 1) / b); }
 
 static void build_tile(Plan& P, TileG& T, uint32_t t) {
-    const uint32_t L = P.p.numres - 1;
     T.comps.assign(P.nc, CompG());
     T.b0 = (uint32_t)P.blocks.size();
     // tile-component c: the tile divided by its component's subsampling (the tile itself without)
@@ -528,18 +555,19 @@ static void build_tile(Plan& P, TileG& T, uint32_t t) {
         CompG& C = T.comps[c];
         const SGroup& G = P.groups[P.group_of[c]];
         const ShapeG& S = G.shapes[G.shape_of[t]];
-        C.res.assign(P.p.numres, ResG());
-        for (uint32_t r = 0; r < P.p.numres; ++r) {
+        const uint32_t nres = P.p.c_numres(c), L = nres - 1;   // the component's coding (COD / COC)
+        C.res.assign(nres, ResG());
+        for (uint32_t r = 0; r < nres; ++r) {
             ResG& R = C.res[r];
             const uint32_t nb = L - r;
             R.x0 = ceildivpow2(tcx0[c], nb); R.y0 = ceildivpow2(tcy0[c], nb);
             R.w = ceildivpow2(tcx1[c], nb) - R.x0; R.h = ceildivpow2(tcy1[c], nb) - R.y0;
-            const uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
+            const uint32_t pwe = P.p.c_prcw(c, r), phe = P.p.c_prch(c, r);
             R.px0 = (R.x0 >> pwe) << pwe; R.py0 = (R.y0 >> phe) << phe;
             R.pw = R.w ? ((ceildivpow2(R.x0 + R.w, pwe) << pwe) - R.px0) >> pwe : 0;
             R.ph = R.h ? ((ceildivpow2(R.y0 + R.h, phe) << phe) - R.py0) >> phe : 0;
             const uint32_t bpw = r ? pwe - 1 : pwe, bph = r ? phe - 1 : phe;
-            R.cbw = std::min(P.p.cbw, bpw); R.cbh = std::min(P.p.cbh, bph);
+            R.cbw = std::min(P.p.c_cbw(c), bpw); R.cbh = std::min(P.p.c_cbh(c), bph);
             const uint32_t nbands = r ? 3 : 1;
             R.bands.assign(nbands, BandG());
             R.prc.assign(nbands, std::vector<PrecG>(R.pw * R.ph));
@@ -551,7 +579,7 @@ static void build_tile(Plan& P, TileG& T, uint32_t t) {
                     B.level = L; B.offx = 0; B.offy = 0;
                     B.plane = L == 0 ? 0 : ((L & 1) ? 1 : 0);
                 } else {
-                    const uint32_t lev = P.p.numres - r;   // decomposition level of this band (1..L)
+                    const uint32_t lev = nres - r;   // decomposition level of this band (1..L)
                     const uint32_t xo = B.orient & 1, yo = B.orient >> 1;
                     const uint64_t half = 1ull << (lev - 1);
                     auto cb = [&](uint64_t t, uint32_t o) -> uint32_t {   // B-15
@@ -572,9 +600,10 @@ static void build_tile(Plan& P, TileG& T, uint32_t t) {
     for (uint32_t c = 0; c < P.nc; ++c) {
         CompG& C = T.comps[c];
         const SGroup& SG = P.groups[P.group_of[c]];
-        for (uint32_t r = 0; r < P.p.numres; ++r) {
+        const uint32_t nres = P.p.c_numres(c), irrev = P.p.c_irrev(c);
+        for (uint32_t r = 0; r < nres; ++r) {
             ResG& R = C.res[r];
-            const uint32_t pwe = P.p.prcw[r], phe = P.p.prch[r];
+            const uint32_t pwe = P.p.c_prcw(c, r), phe = P.p.c_prch(c, r);
             const uint32_t bpw = r ? pwe - 1 : pwe, bph = r ? phe - 1 : phe;
             const uint32_t tlx = r ? R.px0 >> 1 : R.px0, tly = r ? R.py0 >> 1 : R.py0;
             for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
@@ -610,7 +639,7 @@ static void build_tile(Plan& P, TileG& T, uint32_t t) {
                         // bits 3..7: the component's ROI shift (RGN; RoiShiftFilter on decode)
                         // (bit 1, rate control: set when an encode uploads the table, so one plan
                         // serves the encode and the decode of a rate-controlled stream)
-                        G.flags = (P.p.irrev ? 1 : 0) | (uint8_t)(P.p.roi(c) << 3);
+                        G.flags = (irrev ? 1 : 0) | (uint8_t)(P.p.roi(c) << 3);
                         G.step = B.step_enc;
                         // T1::getwmsedec weight w1 * w2 * stepsize (T1.cpp:418-436): w1 = MCT basis norm
                         // (mct.cpp:689-704) when the MCT is on, w2 = DWT band norm (T1.cpp:264-277)
@@ -618,8 +647,8 @@ static void build_tile(Plan& P, TileG& T, uint32_t t) {
                             static const double norms_irrev[3] = {1.732, 1.805, 1.573};
                             static const double norms_rev[3] = {1.732, .8292, .8292};
                             const bool mct = P.mct3();
-                            double w1 = (mct && c < 3) ? (P.p.irrev ? norms_irrev[c] : norms_rev[c]) : 1.0;
-                            G.wmse = w1 * band_norm(P.p.numres - 1 - r, B.orient, !P.p.irrev) * (double)B.step_enc;
+                            double w1 = (mct && c < 3) ? (irrev ? norms_irrev[c] : norms_rev[c]) : 1.0;
+                            G.wmse = w1 * band_norm(nres - 1 - r, B.orient, !irrev) * (double)B.step_enc;
                         }
                         P.blocks.push_back(G);
                         P.bxy.push_back(x0); P.bxy.push_back(y0);
@@ -632,7 +661,6 @@ static void build_tile(Plan& P, TileG& T, uint32_t t) {
 }
 
 static void build_plan(Plan& P) {
-    const uint32_t L = P.p.numres - 1;
     P.stride = align_up(std::max(P.w, 1u), 64);
     P.plane_elems = (size_t)P.stride * P.h;
     // canvas extent of the image: [x0, X1) x [y0, Y1); without tiling one tile from the grid origin
@@ -647,7 +675,7 @@ static void build_plan(Plan& P) {
     // into classes by origin modulo 2^L (m = 2^L / gcd(t, 2^L) of them, an arithmetic progression
     // each; one class on a 2^L-aligned grid)
     struct Axis { uint32_t first, step, count, size, origin; };   // origin: canvas position of the first member
-    auto classes = [&](uint32_t n, uint32_t t, uint32_t g, uint32_t o, uint32_t end) {
+    auto classes = [&](uint32_t n, uint32_t t, uint32_t g, uint32_t o, uint32_t end, uint32_t L) {
         std::vector<Axis> v;
         auto lo = [&](uint32_t k) { return std::max(g + k * t, o); };
         auto hi = [&](uint32_t k) { return std::min(g + (k + 1) * t, end); };
@@ -665,8 +693,15 @@ static void build_plan(Plan& P) {
     P.group_of.assign(P.nc, 0);
     for (uint32_t c = 0; c < P.nc; ++c) {
         uint32_t g = 0;
-        while (g < P.groups.size() && (P.groups[g].dx != P.sx(c) || P.groups[g].dy != P.sy(c))) ++g;
-        if (g == P.groups.size()) { P.groups.emplace_back(); P.groups[g].dx = P.sx(c); P.groups[g].dy = P.sy(c); }
+        auto same = [&](const SGroup& G) {
+            return G.dx == P.sx(c) && G.dy == P.sy(c) && G.numres == P.p.c_numres(c) && G.irrev == P.p.c_irrev(c);
+        };
+        while (g < P.groups.size() && !same(P.groups[g])) ++g;
+        if (g == P.groups.size()) {
+            P.groups.emplace_back();
+            SGroup& G = P.groups[g];
+            G.dx = P.sx(c); G.dy = P.sy(c); G.numres = P.p.c_numres(c); G.irrev = P.p.c_irrev(c);
+        }
         P.group_of[c] = g;
         auto& runs = P.groups[g].runs;
         if (!runs.empty() && runs.back().second == c) runs.back().second = c + 1;
@@ -681,8 +716,9 @@ static void build_plan(Plan& P) {
         const uint32_t tw = P.ntx > 1 ? P.tw / G.dx : ceildiv(P.tw, G.dx), th = P.nty > 1 ? P.th / G.dy : ceildiv(P.th, G.dy);
         G.ox = ceildiv(P.x0, G.dx); G.oy = ceildiv(P.y0, G.dy);
         G.w = ceildiv(X1, G.dx) - G.ox; G.h = ceildiv(Y1, G.dy) - G.oy;
-        const std::vector<Axis> cx = classes(P.ntx, tw, ceildiv(P.gx0, G.dx), G.ox, ceildiv(X1, G.dx));
-        const std::vector<Axis> cy = classes(P.nty, th, ceildiv(P.gy0, G.dy), G.oy, ceildiv(Y1, G.dy));
+        const uint32_t L = G.numres - 1;
+        const std::vector<Axis> cx = classes(P.ntx, tw, ceildiv(P.gx0, G.dx), G.ox, ceildiv(X1, G.dx), L);
+        const std::vector<Axis> cy = classes(P.nty, th, ceildiv(P.gy0, G.dy), G.oy, ceildiv(Y1, G.dy), L);
         G.shapes.clear();
         G.shape_of.assign((size_t)P.ntx * P.nty, -1);
         for (const Axis& ay : cy)
@@ -708,6 +744,10 @@ static void build_plan(Plan& P) {
                 G.shapes.push_back(S);
             }
     }
+    // level 1 fuses with the sample stage when every group has a level 1 and the MCT's three
+    // components share a group (COC can give them different levels)
+    for (const SGroup& G : P.groups) if (G.numres < 2) P.l1_fusable = false;
+    if (P.mct3() && (P.group_of[1] != P.group_of[0] || P.group_of[2] != P.group_of[0])) P.l1_fusable = false;
     P.tiles.assign((size_t)P.ntx * P.nty, TileG());
     P.blocks.clear();
     P.bxy.clear();
@@ -1059,8 +1099,13 @@ struct PacketRef { uint32_t l, r, c, pi; };
 // One progression over layers [0, L), resolutions [r0, r1), components [c0, c1).
 static void order_ranges(const Plan& P, const TileG& T, uint32_t prog, uint32_t L, uint32_t r0, uint32_t r1, uint32_t c0,
                          uint32_t c1, std::vector<PacketRef>& out) {
-    const uint32_t nr = P.p.numres;
-    auto np = [&](uint32_t c, uint32_t r) { const ResG& R = T.comps[c].res[r]; return R.w && R.h ? R.pw * R.ph : 0u; };
+    // (a component coded with fewer resolutions (COC) has no packets at the higher ones,
+    // PacketIter.cpp:160-162)
+    auto np = [&](uint32_t c, uint32_t r) {
+        if (r >= T.comps[c].res.size()) return 0u;
+        const ResG& R = T.comps[c].res[r];
+        return R.w && R.h ? R.pw * R.ph : 0u;
+    };
     if (prog == 0 || prog == 1) {   // LRCP / RLCP
         for (uint32_t a = (prog == 0 ? 0 : r0); a < (prog == 0 ? L : r1); ++a)
             for (uint32_t b = (prog == 0 ? r0 : 0); b < (prog == 0 ? r1 : L); ++b)
@@ -1073,9 +1118,10 @@ static void order_ranges(const Plan& P, const TileG& T, uint32_t prog, uint32_t 
     struct Pr { uint64_t ay, ax; uint32_t r, c, pi; };
     std::vector<Pr> v;
     for (uint32_t c = c0; c < c1; ++c)
-        for (uint32_t r = r0; r < r1; ++r) {
+        for (uint32_t r = r0; r < std::min<uint32_t>(r1, (uint32_t)T.comps[c].res.size()); ++r) {
             const ResG& R = T.comps[c].res[r];
-            const uint32_t n = np(c, r), lv = nr - 1 - r, pwe = P.p.prcw[r], phe = P.p.prch[r];
+            const uint32_t nr = (uint32_t)T.comps[c].res.size();
+            const uint32_t n = np(c, r), lv = nr - 1 - r, pwe = P.p.c_prcw(c, r), phe = P.p.c_prch(c, r);
             // where Grok's walk (PacketIter::generatePrecinctIndex, PacketIter.cpp:287-335) first
             // meets precinct (i, j): the canvas position XRsiz * 2^(PPx + level) * (its grid index),
             // except a first precinct whose resolution starts off its precinct grid, which the
@@ -1113,25 +1159,26 @@ static std::vector<PacketRef> packet_order(const Plan& P, const TileG& T, uint32
                                            const std::vector<Poc>* pocs = nullptr,
                                            std::vector<uint32_t>* entry = nullptr) {
     std::vector<PacketRef> out;
+    const uint32_t NR = P.max_numres();   // (COC: components may have fewer)
     if (!pocs || pocs->empty()) {
-        order_ranges(P, T, P.p.prog, L, 0, P.p.numres, 0, P.nc, out);
+        order_ranges(P, T, P.p.prog, L, 0, NR, 0, P.nc, out);
         return out;
     }
-    // packet id: ((c * numres + r) * maxprc + pi) * L + l
+    // packet id: ((c * NR + r) * maxprc + pi) * L + l
     uint32_t maxprc = 1;
     for (uint32_t c = 0; c < P.nc; ++c)
-        for (uint32_t r = 0; r < P.p.numres; ++r) maxprc = std::max(maxprc, T.comps[c].res[r].pw * T.comps[c].res[r].ph);
-    std::vector<uint8_t> seen((size_t)P.nc * P.p.numres * maxprc * L, 0);
+        for (const ResG& R : T.comps[c].res) maxprc = std::max(maxprc, R.pw * R.ph);
+    std::vector<uint8_t> seen((size_t)P.nc * NR * maxprc * L, 0);
     std::vector<PacketRef> sub;
     uint32_t iter = 0;
     for (uint32_t ei = 0; ei < (uint32_t)pocs->size(); ++ei) {
         const Poc& q = (*pocs)[ei];
         sub.clear();
-        const uint32_t le = std::min(q.lye, L), r1 = std::min(q.re, P.p.numres), c1 = std::min(q.ce, P.nc);
+        const uint32_t le = std::min(q.lye, L), r1 = std::min(q.re, NR), c1 = std::min(q.ce, P.nc);
         if (q.rs >= r1 || q.cs >= c1 || !le) continue;
         order_ranges(P, T, q.prog, le, q.rs, r1, q.cs, c1, sub);
         for (const PacketRef& pr : sub) {
-            uint8_t& sflag = seen[(((size_t)pr.c * P.p.numres + pr.r) * maxprc + pr.pi) * L + pr.l];
+            uint8_t& sflag = seen[(((size_t)pr.c * NR + pr.r) * maxprc + pr.pi) * L + pr.l];
             const uint32_t it = iter++;
             if (sflag) continue;
             sflag = 1;
@@ -2649,6 +2696,11 @@ static std::string plan_key(const Plan& P) {
     for (size_t c = 0; c < P.p.roishift.size(); ++c)   // non-zero (component, shift) pairs only
         if (P.p.roishift[c]) k += " roi" + std::to_string(c) + ":" + std::to_string(P.p.roishift[c]);
     for (uint32_t r = 0; r < P.p.numres; ++r) k += " " + std::to_string(P.p.prcw[r]) + "," + std::to_string(P.p.prch[r]);
+    for (const Params::CompCod& q : P.p.cc) {   // COC: every component's coding
+        k += " coc" + std::to_string(q.numres) + "," + std::to_string(q.cbw) + "," + std::to_string(q.cbh) + "," +
+             std::to_string(q.cblk_sty) + "," + std::to_string(q.irrev);
+        for (uint32_t r = 0; r < q.numres; ++r) k += ":" + std::to_string(q.prcw[r]) + "," + std::to_string(q.prch[r]);
+    }
     return k;
 }
 
@@ -2700,14 +2752,16 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                     uint32_t ib = 0, uint32_t ie = 0xffffffffu, const L1Io* io = nullptr, uint32_t lstop = 1) {
     Plan& P = ctx->plan;
     int32_t* arena = (int32_t*)ctx->arena.p;
-    const uint32_t L = P.p.numres - 1;
     const uint64_t cst = 2 * (uint64_t)RG.plane;   // component plane pairs
     ctx->tm.dwt_launches = 0; ctx->tm.dwt_bytes = 0;
+    // per group (sampling grid, levels and transform; one group without subsampling or COC), level
+    // by level, one launch per run of its components and tile class
+    for (const SGroup& G : P.groups) {
+    const uint32_t L = G.numres - 1;
+    const uint32_t irrev = G.irrev;
     const uint32_t nlev = forward ? L : (L + 1 > lstop ? L + 1 - lstop : 0);
     for (uint32_t i = 0; i < nlev; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
-        // per sampling group (one without subsampling) and run of its components
-        for (const SGroup& G : P.groups)
         for (const auto& run : G.runs)
         for (const ShapeG& S0 : G.shapes) {       // one launch per tile class, grid.z = its tiles
             const uint32_t c0 = run.first, ncr = run.second - run.first;
@@ -2737,7 +2791,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                 int32_t* src_l = (l & 1) ? A : B;
                 int32_t* dst_l = (l & 1) ? B : A;
                 const uint64_t area = (uint64_t)w * h * S.tb.count();
-                gk_launch_dwt_any(ctx->st, P.p.irrev, forward, forward ? src_l : dst_l, forward ? dst_l : src_l, RG.stride,
+                gk_launch_dwt_any(ctx->st, irrev, forward, forward ? src_l : dst_l, forward ? dst_l : src_l, RG.stride,
                                   w, h, S.parx[l - 1], S.pary[l - 1], S.tb, GkComps{cst, ncr}, !forward && ctx->dwt_partial);
                 ctx->tm.dwt_launches += 3;
                 ctx->tm.dwt_bytes += area * 8 * ncr;
@@ -2760,7 +2814,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                     GkPtr3 pp;
                     for (int k = 0; k < nc; ++k) pp.p[k] = io->planes[c + k];
                     if (forward) {
-                        if (P.p.irrev)
+                        if (irrev)
                             gk_launch_dwt97_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c],
                                                    reinterpret_cast<float*>(dl), cst, RG.stride, w, h, S.tb,
                                                    io->shift);
@@ -2768,7 +2822,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                             gk_launch_dwt53_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c], dl, cst,
                                                    RG.stride, w, h, S.tb, io->shift);
                     } else {
-                        if (P.p.irrev)
+                        if (irrev)
                             gk_launch_dwt97_inv_l1(ctx->st, io->stype, nc, reinterpret_cast<const float*>(dl),
                                                    cst, RG.stride, pp, io->strides[c], win, w, h, S.tb, io->shift,
                                                    io->mn, io->mx);
@@ -2783,7 +2837,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                 continue;
             }
             const GkComps cs{cst, ncr};
-            if (P.p.irrev) {
+            if (irrev) {
                 float* fs = reinterpret_cast<float*>(src_l);
                 float* fd = reinterpret_cast<float*>(dst_l);
                 if (forward) gk_launch_dwt97_fwd(ctx->st, fs, RG.stride, fd, RG.stride, w, h, S.tb, cs);
@@ -2795,6 +2849,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
             ctx->tm.dwt_launches++;
             ctx->tm.dwt_bytes += area * 8 * ncr;
         }
+    }
     }
 }
 
@@ -3608,7 +3663,33 @@ struct Header {
     std::vector<TilePart> parts;
     std::vector<std::pair<uint32_t, uint32_t>> tlm;   // (tile, tile-part length) from TLM markers
     std::vector<uint8_t> cod, qcd_body;               // main COD / QCD marker bodies (after Lxxx)
+    std::vector<std::vector<uint8_t>> ccod;           // per component: its coding as a COC body states it
+                                                      // (Scoc, SPcoc): its main COC, else the COD's
 };
+// The COD's coding in COC form: Scod's precinct flag, then SPcod from the decomposition levels on
+static std::vector<uint8_t> cod_as_coc(const std::vector<uint8_t>& cod) {
+    std::vector<uint8_t> v{(uint8_t)(cod[0] & 1)};
+    v.insert(v.end(), cod.begin() + 5, cod.end());
+    return v;
+}
+// A component's coding from its COC-form body (read_SPCod_SPCoc): levels, code-block size and
+// style, transform, precinct sizes (default 2^15 without the precinct flag)
+static void comp_coding(const std::vector<uint8_t>& v, Params::CompCod& k) {
+    if (v.size() < 6) throw GkError("corrupt COC marker");
+    k.numres = v[1] + 1u; k.cbw = v[2] + 2u; k.cbh = v[3] + 2u; k.cblk_sty = v[4]; k.irrev = v[5] == 0 ? 1 : 0;
+    if (k.numres > GK_MAXRLVLS) throw GkError("corrupt COC marker (more than 32 decomposition levels)");
+    if (k.cbw > 10 || k.cbh > 10 || k.cbw + k.cbh > 12) throw GkError("corrupt COC marker (code-block size)");
+    if ((k.cblk_sty & 0x40) && k.cblk_sty != 0x40) throw GkError("HTJ2K combined with Part-1 mode switches");
+    if (k.cblk_sty > 0x7f) throw GkError("unknown code-block style bits");
+    for (uint32_t r = 0; r < GK_MAXRLVLS; ++r) { k.prcw[r] = 15; k.prch[r] = 15; }
+    if (v[0] & 1) {
+        if (v.size() < 6 + k.numres) throw GkError("corrupt COC marker (precinct sizes)");
+        for (uint32_t r = 0; r < k.numres; ++r) {
+            k.prcw[r] = v[6 + r] & 15; k.prch[r] = v[6 + r] >> 4;
+            if (r > 0 && (!k.prcw[r] || !k.prch[r])) throw GkError("COC: precinct exponent 0 above resolution 0");
+        }
+    }
+}
 
 static std::vector<uint8_t> marker_body(ByteSrc& S, size_t s, uint32_t L) {
     std::vector<uint8_t> v(L - 2);
@@ -3616,12 +3697,11 @@ static std::vector<uint8_t> marker_body(ByteSrc& S, size_t s, uint32_t L) {
     return v;
 }
 
-// COC (main or tile-part header), tile-part QCC and tile-part COD / QCD override the main header's
-// coding or quantisation for one component or one tile (CodeStreamDecompress read_coc /
-// read_qcc, TileCodingParams).  A main-header QCC is applied per component (apply_qcd); every
-// tile-component is otherwise coded with the main header's parameters, so these markers are
-// accepted when they restate them (some encoders write them even when nothing differs) and
-// refused otherwise.  COC: Ccoc (1 byte below 257 components, else 2), Scoc (precinct flag),
+// Tile-part COD / COC / QCD / QCC override the main header's coding or quantisation for one tile
+// (CodeStreamDecompress read_coc / read_qcc, TileCodingParams).  Main-header COC / QCC are
+// applied per component (Params::cc, apply_qcd); every tile is coded with the main header's
+// parameters, so tile-part markers are accepted when they restate them (some encoders write them
+// even when nothing differs) and refused otherwise.  COC: Ccoc (1 byte below 257 components, else 2), Scoc (precinct flag),
 // then SPcoc laid out as COD's SPcod; QCC: Cqcc, then Sqcc/SPqcc as QCD's body.
 static void check_override_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, const Header& Hd, bool tile) {
     if (m == 0xff5e && tile) throw GkError("RGN in a tile-part header is not supported on this path");
@@ -3630,7 +3710,10 @@ static void check_override_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, 
     const std::vector<uint8_t> b = marker_body(S, s, L);
     const uint32_t nc = Hd.want.nc, cw = nc <= 256 ? 1 : 2;
     bool same = false;
-    if (m == 0xff52) same = b == Hd.cod;
+    if (m == 0xff52) {   // (a tile COD replaces the main COCs as well)
+        same = b == Hd.cod;
+        for (const auto& q : Hd.ccod) same = same && q == cod_as_coc(Hd.cod);
+    }
     else if (m == 0xff5c) {   // (a tile QCD replaces every component's QCD / QCC)
         same = true;
         for (const auto& q : Hd.qbody) same = same && b == q;
@@ -3638,12 +3721,9 @@ static void check_override_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, 
         const uint32_t c = cw == 1 ? b[0] : (uint32_t)b[0] << 8 | b[1];
         if (c >= nc) throw GkError("bad component number in COC/QCC");
         if (m == 0xff5d) same = std::equal(b.begin() + cw, b.end(), Hd.qbody[c].begin(), Hd.qbody[c].end());
-        else same = Hd.cod.size() > 5 && (b[cw] & 1) == (Hd.cod[0] & 1) &&
-                    std::equal(b.begin() + cw + 1, b.end(), Hd.cod.begin() + 5, Hd.cod.end());
+        else same = (b[cw] & 1) == Hd.ccod[c][0] && std::equal(b.begin() + cw + 1, b.end(), Hd.ccod[c].begin() + 1, Hd.ccod[c].end());
     }
-    if (!same)
-        throw GkError(tile ? "tile-part COD/COC/QCD/QCC that differ from the main header are not supported on this path"
-                           : "COC that differs from COD is not supported on this path");
+    if (!same) throw GkError("tile-part COD/COC/QCD/QCC that differ from the main header are not supported on this path");
 }
 // The tiles of the canvas tile grid (B.3)
 static uint32_t grid_tiles(const Plan& W) {
@@ -3811,9 +3891,29 @@ static void parse_header(ByteSrc& S, Header& Hd) {
     // precedence over the main QCD in any marker order, Quantizer.cpp:215-235)
     Hd.qbody.assign(W.nc, Hd.qcd_body);
     for (auto& q : qcc) Hd.qbody[q.first] = q.second;
+    // per component: the COD's coding, replaced by its main-header COC (A.6.2; read_coc fills the
+    // component's tccp, a main COC winning over the main COD in either order)
+    Hd.ccod.assign(W.nc, cod_as_coc(Hd.cod));
+    for (size_t k : coc_qcc) {
+        const uint32_t L = S.be16(k + 2), cw = W.nc <= 256 ? 1 : 2;
+        const std::vector<uint8_t> b = marker_body(S, k + 4, L);
+        if (b.size() < cw + 6) throw GkError("corrupt COC marker");
+        const uint32_t c = cw == 1 ? b[0] : (uint32_t)b[0] << 8 | b[1];
+        if (c >= W.nc) throw GkError("bad component number in COC/QCC");
+        Hd.ccod[c].assign(b.begin() + cw, b.end());
+    }
+    W.p.cc.clear();
+    bool differ = false;
+    for (uint32_t c = 0; c < W.nc; ++c) differ = differ || Hd.ccod[c] != Hd.ccod[0] || Hd.ccod[c] != cod_as_coc(Hd.cod);
+    if (differ) {
+        W.p.cc.resize(W.nc);
+        for (uint32_t c = 0; c < W.nc; ++c) comp_coding(Hd.ccod[c], W.p.cc[c]);
+        // the inverse MCT picks RCT / ICT by component 0's transform (TileProcessor::mctDecompress)
+        if (W.p.mct && W.nc >= 3 && (W.p.cc[1].irrev != W.p.cc[0].irrev || W.p.cc[2].irrev != W.p.cc[0].irrev))
+            throw GkError("MCT over components with different transforms is not supported");
+    }
     Hd.qcd.clear();
-    for (uint32_t c = 0; c < W.nc; ++c) parse_quant(Hd.qbody[c], W.p.numres, Hd.qcd);
-    for (size_t k : coc_qcc) check_override_marker(S, k + 4, S.be16(k), S.be16(k + 2), Hd, false);
+    for (uint32_t c = 0; c < W.nc; ++c) parse_quant(Hd.qbody[c], W.p.c_numres(c), Hd.qcd);
     // tile parts: SOT (Isot, Psot, TPsot, TNsot), tile-part header markers (PLT, ...), SOD, packets
     // (CodeStreamDecompress SOT/SOD handlers; TLM and PLT are only needed for random access)
     size_t pos = Hd.first_sot;
@@ -3989,16 +4089,17 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // the Part-1 decoders hold twice the magnitude plus the half-bit, (2M+1) << q, in an int32:
     // a band (ROI shift included) of more than 30 bit-planes cannot be held (every tile has the
     // same bands as tile 0)
-    if (!P.p.ht())
-        for (const CompG& C : P.tiles[0].comps)
-            for (const ResG& R : C.res)
+    for (uint32_t c = 0; c < P.nc; ++c)
+        if (!P.p.c_ht(c))
+            for (const ResG& R : P.tiles[0].comps[c].res)
                 for (const BandG& B : R.bands)
                     if (B.numbps > 30) throw GkError("more than 30 band bit-planes (ROI shift included) not supported");
     const uint32_t red = ctx->dec_reduce;
-    if (red >= P.p.numres) throw GkError("reduce must be less than the number of resolutions");
-    // subsampled components decode whole images (every component plane at its own size)
-    const bool sub = P.subsampled();
-    if (sub && win) throw GkError("window decodes of subsampled components are not supported on this path");
+    if (red >= P.min_numres()) throw GkError("reduce must be less than the number of resolutions");
+    // subsampled components, or components coded differently (COC), decode whole images (every
+    // component plane at its own size)
+    const bool sub = P.subsampled() || !P.p.cc.empty();
+    if (sub && win) throw GkError("window decodes of subsampled or COC-coded components are not supported on this path");
     auto keep_window = [&]() {   // keep only the tile parts of tiles intersecting the window
         if (!win) return;
         if (win[0] >= win[2] || win[1] >= win[3] || win[2] > P.w || win[3] > P.h) throw GkError("bad decode window");
@@ -4118,9 +4219,12 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         std::vector<std::vector<uint32_t>> seglens;
         std::vector<uint16_t> segp;
     };
-    const bool multiseg = (P.p.cblk_sty & (GK_STY_LAZY | GK_STY_TERMALL)) != 0;
-    auto seg_max = [&](uint32_t sg) -> uint32_t {
-        if (P.p.cblk_sty & GK_STY_TERMALL) return 1;
+    // BYPASS / TERMALL components: several codeword segments per block (per component with COC)
+    auto comp_multiseg = [&](uint32_t c) { return (P.p.c_sty(c) & (GK_STY_LAZY | GK_STY_TERMALL)) != 0; };
+    bool multiseg = false;
+    for (uint32_t c = 0; c < P.nc; ++c) multiseg = multiseg || comp_multiseg(c);
+    auto seg_max = [&](uint32_t c, uint32_t sg) -> uint32_t {
+        if (P.p.c_sty(c) & GK_STY_TERMALL) return 1;
         return sg == 0 ? 10 : ((sg & 1) ? 2 : 1);
     };
     std::vector<PartState> ps(Hd.parts.size());
@@ -4143,10 +4247,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // layer limit (tcp->numLayersToDecompress): packets of later layers are skipped through
         // PLT or parsed without their data (T2Decompress::processPacket, T2Decompress.cpp:55-116)
         const uint32_t maxl = ctx->dec_layers ? std::min(ctx->dec_layers, P.p.nlayers) : P.p.nlayers;
-        const uint32_t rmax = P.p.numres - ctx->dec_reduce;   // resolutions decoded
         for (size_t oi = 0; oi < order.size(); ++oi, ++pk) {
                         const uint32_t l = order[oi].l, r = order[oi].r, c = order[oi].c, pi = order[oi].pi;
                         const ResG& R = TG.comps[c].res[r];
+                        const uint32_t rmax = P.p.c_numres(c) - ctx->dec_reduce;   // resolutions decoded
+                        const bool mseg = comp_multiseg(c);
                         while (pos >= tile_end && nextp < TPt.more.size()) {   // the tile's next tile part
                             pos = TPt.more[nextp].first; tile_end = TPt.more[nextp].second; ++nextp;
                         }
@@ -4201,7 +4306,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                     const uint32_t np = br.numpasses();
                                     st2.numlenbits[b] += br.commacode();
                                     uint32_t sl = 0;
-                                    if (!multiseg) {
+                                    if (!mseg) {
                                         const uint32_t nbits = st2.numlenbits[b] + floorlog2(np);
                                         if (nbits > 32) throw GkError("corrupt packet header (segment length)");
                                         sl = br.read((int)nbits);
@@ -4210,11 +4315,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                                         // packets until it holds its maximum pass count
                                         std::vector<uint32_t>& SL = st2.seglens[b];
                                         for (uint32_t left = np; left;) {
-                                            if (SL.empty() || st2.segp[b] == seg_max((uint32_t)SL.size() - 1)) {
+                                            if (SL.empty() || st2.segp[b] == seg_max(c, (uint32_t)SL.size() - 1)) {
                                                 if (SL.size() >= GK_MAX_PASSES) throw GkError("corrupt packet header (segments)");
                                                 SL.push_back(0); st2.segp[b] = 0;
                                             }
-                                            const uint32_t n = std::min(seg_max((uint32_t)SL.size() - 1) - st2.segp[b], left);
+                                            const uint32_t n = std::min(seg_max(c, (uint32_t)SL.size() - 1) - st2.segp[b], left);
                                             const uint32_t nbits = st2.numlenbits[b] + floorlog2(n);
                                             if (nbits > 32) throw GkError("corrupt packet header (segment length)");
                                             const uint32_t part = br.read((int)nbits);
@@ -4289,7 +4394,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 G.stride = RG.stride;
                 G.band_numbps = (uint8_t)R.bands[bi].numbps;
                 G.step = R.bands[bi].step_dec / 2.0f;
-                if (P.p.ht() && P.p.irrev) {   // ScaleHTFilter: stepsize / 2^(31 - numbps) (Quantizer.cpp:52-62)
+                if (P.p.c_ht(c) && P.p.c_irrev(c)) {   // ScaleHTFilter: stepsize / 2^(31 - numbps) (Quantizer.cpp:52-62)
                     if (R.bands[bi].numbps > 31) throw GkError("unsupported number of band bit-planes");
                     G.step = R.bands[bi].step_dec / (float)(1u << (31 - R.bands[bi].numbps));
                 }
@@ -4314,7 +4419,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         uint32_t n = 0;
         uint64_t oo = o0, t1 = 0;
         for (uint32_t c = 0; c < P.nc; ++c)
-            for (uint32_t r = 0; r < P.p.numres; ++r) {
+            for (uint32_t r = 0; r < (uint32_t)T.comps[c].res.size(); ++r) {
                 const ResG& R = T.comps[c].res[r];
                 for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
                     for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) fill_prec(tf, c, r, bi, pi, nb0, count_only, n, oo, t1);
@@ -4347,7 +4452,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             const TileG& T = P.tiles[tiles_in[k].t];
             part_idx[tiles_in[k].q].assign(T.b1 - T.b0, -1);
             for (uint32_t c = 0; c < P.nc; ++c)
-                for (uint32_t r = 0; r < P.p.numres; ++r) {
+                for (uint32_t r = 0; r < (uint32_t)T.comps[c].res.size(); ++r) {
                     const ResG& R = T.comps[c].res[r];
                     for (uint32_t bi = 0; bi < R.bands.size(); ++bi)
                         for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi)
@@ -4445,8 +4550,31 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                         "%u blocks); %llu page fetches %.3f ms (cumulative)\n",
                 ms(h0, h1), ms(h1, h2), ms(h2, now()), Hd.parts.size(), nbr,
                 (unsigned long long)ByteSrc::fetch_cnt.load(), ByteSrc::fetch_ns.load() * 1e-6);
-    GkBlock* dblk = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * nbx);
-    HIPCHK(hipMemcpyAsync(dblk, blk, sizeof(GkBlock) * nbr, hipMemcpyHostToDevice, st));
+    // components coded with different T1 coders (COC: Part-1 / mode switches / HT): the table is
+    // grouped by coder class (a stable partition; entries keep their staging offsets and segment
+    // lists), one decoder launch per class below
+    std::vector<std::pair<uint32_t, uint32_t>> cls_range;   // (first entry, class) per class run
+    {
+        bool mixed = false;
+        for (uint32_t c = 1; c < P.nc; ++c) mixed = mixed || P.p.c_class(c) != P.p.c_class(0);
+        if (mixed && nbr) {
+            std::vector<GkBlock> tmp(blk, blk + nbr);
+            std::vector<uint32_t> classes;
+            for (uint32_t c = 0; c < P.nc; ++c)
+                if (std::find(classes.begin(), classes.end(), P.p.c_class(c)) == classes.end()) classes.push_back(P.p.c_class(c));
+            uint32_t k = 0;
+            for (uint32_t cl : classes) {
+                const uint32_t k0 = k;
+                for (const GkBlock& G : tmp)
+                    if (P.p.c_class(G.comp) == cl) blk[k++] = G;
+                if (k > k0) cls_range.push_back({k0, cl});
+            }
+        } else {
+            cls_range.push_back({0, P.p.c_class(0)});
+        }
+    }
+    GkBlock* dblk_all = (GkBlock*)ctx->dblocks.get(sizeof(GkBlock) * nbx);
+    HIPCHK(hipMemcpyAsync(dblk_all, blk, sizeof(GkBlock) * nbr, hipMemcpyHostToDevice, st));
     ctx->blocks_uploaded = false;   // the encode table must be re-uploaded
     int32_t* arena = (int32_t*)ctx->arena.get(RG.plane * P.nc * 2 * sizeof(int32_t));
     // tiles of the rectangle without a tile part decode as zero; blocks skipped by the window
@@ -4455,186 +4583,201 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipMemsetAsync(arena, 0, RG.plane * P.nc * 2 * sizeof(int32_t), st));
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[2], st));
-    if (nbr == 0) {
-        // nothing to decode (all-zero tiles)
-    } else if (P.p.ht()) {
-        // HT cleanup pass decode straight into the band windows (T1HT::decompress, T1HT.cpp:134-187)
-        uint32_t* dsel = (uint32_t*)ctx->dord.get(4 * (size_t)nbx + 16);
-        uint32_t* hsel = (uint32_t*)ctx->hord.get(4 * (size_t)nbx + 16);
-        for (uint32_t k = 0; k < nbr; ++k) hsel[k] = k;
-        HIPCHK(hipMemcpyAsync(dsel, hsel, 4 * (size_t)nbr, hipMemcpyHostToDevice, st));
-        int* derr = (int*)ctx->derr.get(64);
-        HIPCHK(hipMemsetAsync(derr, 0, 64, st));
-        gk_launch_ht_dec(st, src_bytes, dblk, dsel, arena, nbr, derr, P.p.wide());
-        launch_check(__LINE__);
-        HIPCHK(hipEventRecord(ctx->ev[8], st));
-        int herr = 0;
-        HIPCHK(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        if (herr) throw GkError("corrupt HT code-block segment");
-    } else if (P.p.t1_generic()) {
-        // mode switches or wide code-blocks: lane-per-block decoder over the codeword segments
-        // (gk_t1ms.hip)
-        uint32_t* dsl = nullptr;
-        if (multiseg && !hseglen.empty()) {
-            uint32_t* hsl = (uint32_t*)ctx->hord.get(4 * hseglen.size());
-            memcpy(hsl, hseglen.data(), 4 * hseglen.size());
-            dsl = (uint32_t*)ctx->dseglen.get(4 * hseglen.size());
-            HIPCHK(hipMemcpyAsync(dsl, hsl, 4 * hseglen.size(), hipMemcpyHostToDevice, st));
-        }
-        uint8_t* mst = (uint8_t*)ctx->dmsstate.get(gk_t1ms_state_bytes(nbx));
-        gk_launch_t1_dec_ms(st, src_bytes, dblk, dsl, arena, nbr, mst, P.p.cblk_sty & 0x3f);
-        launch_check(__LINE__);
-        HIPCHK(hipEventRecord(ctx->ev[8], st));
-        if (multiseg && !hseglen.empty()) HIPCHK(hipStreamSynchronize(st));   // the pinned table is reused
-    } else {
-        // lane assignment: blocks bucketed by pass count (descending), so the lanes of a
-        // wave decode similar amounts of work and the longest waves start first.  Only
-        // `L` lanes of each 64-lane wave carry a block (gk_t1dec_lanes): fewer lanes per wave
-        // give more waves, so every SIMD of the chip holds waves and can hide latency.
-        const uint32_t L = gk_t1dec_lanes();
-        // The heaviest blocks go to solo waves (gk_t1dec.hip solo_block) on the SIMDs the
-        // lane-parallel waves leave.  Weight = compressed bytes (decisions follow them within
-        // ~10 %).  K, the number of solo blocks, balances the two sides: the lane-parallel
-        // waves last as long as the heaviest block left to them (weight w[K]), a solo wave as
-        // long as its blocks' sum / ratio; the top K are packed longest-first into the solo
-        // waves (LPT) and K is the crossing point of the two (binary search: the first falls,
-        // the second grows with K).  GK_T1DEC_SOLO=n: the n heaviest, one per wave.
-        GkSoloPlan sp = nbr ? gk_t1dec_solo_plan(nbr, L) : GkSoloPlan{0, -1, 1.f};
-        // Device shared with another engine's call in progress (e.g. two images in flight; engines
-        // that merely exist, like the bench's C2 + C3 pair run one after the other, do not count):
-        // no SIMD is idle, so a solo
-        // wave's time is taken from the other decodes; only clear outliers (> 1.3 x the weight of
-        // the block at rank 1,024) go solo, one per wave.  C2 (LL blocks 1.06 x the plateau): none,
-        // 2,394 -> 2,548 Mpix/s with two images in flight; C3 (LL ~1.6 x): kept (1,761 -> 2,056).
-        const bool shared = sp.forced < 0 && engines_busy(ctx->device) > 1;
-        uint32_t nsb = 0;
-        std::vector<uint32_t> byl;
-        std::vector<std::vector<uint32_t>> bins;
-        auto weight = [&](uint32_t q) -> uint64_t { return blk[q].npasses ? blk[q].len : 0; };
-        if (sp.waves) {
-            // (at most 4 blocks per solo wave: the search stays a fraction of a millisecond of host time)
-            const uint32_t kmax = sp.forced >= 0 ? (uint32_t)sp.forced : std::min<uint32_t>(nbr / 4, 4u * sp.waves);
-            byl.resize(nbr);
-            for (uint32_t q = 0; q < nbr; ++q) byl[q] = q;
-            auto heavier = [&](uint32_t x, uint32_t y) { return weight(x) != weight(y) ? weight(x) > weight(y) : x < y; };
-            const uint32_t top = std::min<uint32_t>(kmax + 1, nbr);
-            if (top) {
-                std::nth_element(byl.begin(), byl.begin() + (top - 1), byl.end(), heavier);
-                std::sort(byl.begin(), byl.begin() + top, heavier);
+    // one class of the table: entries [s, s + n), decoder class cls (Params::c_class)
+    auto t1_class = [&](uint32_t s0, uint32_t n, uint32_t cls) {
+        const uint32_t nbr = n, nbx = std::max(n, 1u);
+        GkBlock* const blk_all = blk;
+        GkBlock* const blk = blk_all + s0;
+        GkBlock* const dblk = dblk_all + s0;
+        const bool cls_ht = (cls & 3) == 2, cls_generic = (cls & 3) == 1, cls_wide = (cls >> 8) & 1;
+        const uint32_t cls_sty = (cls >> 2) & 0x3f;
+        (void)blk_all;
+        if (nbr == 0) {
+            // nothing to decode (all-zero tiles)
+        } else if (cls_ht) {
+            // HT cleanup pass decode straight into the band windows (T1HT::decompress, T1HT.cpp:134-187)
+            uint32_t* dsel = (uint32_t*)ctx->dord.get(4 * (size_t)nbx + 16);
+            uint32_t* hsel = (uint32_t*)ctx->hord.get(4 * (size_t)nbx + 16);
+            for (uint32_t k = 0; k < nbr; ++k) hsel[k] = k;
+            HIPCHK(hipMemcpyAsync(dsel, hsel, 4 * (size_t)nbr, hipMemcpyHostToDevice, st));
+            int* derr = (int*)ctx->derr.get(64);
+            HIPCHK(hipMemsetAsync(derr, 0, 64, st));
+            gk_launch_ht_dec(st, src_bytes, dblk, dsel, arena, nbr, derr, cls_wide);
+            launch_check(__LINE__);
+            HIPCHK(hipEventRecord(ctx->ev[8], st));
+            int herr = 0;
+            HIPCHK(hipMemcpyAsync(&herr, derr, 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            if (herr) throw GkError("corrupt HT code-block segment");
+        } else if (cls_generic) {
+            // mode switches or wide code-blocks: lane-per-block decoder over the codeword segments
+            // (gk_t1ms.hip)
+            uint32_t* dsl = nullptr;   // (segment tables for BYPASS / TERMALL classes only: one segment otherwise)
+            if ((cls_sty & (GK_STY_LAZY | GK_STY_TERMALL)) && !hseglen.empty()) {
+                uint32_t* hsl = (uint32_t*)ctx->hord.get(4 * hseglen.size());
+                memcpy(hsl, hseglen.data(), 4 * hseglen.size());
+                dsl = (uint32_t*)ctx->dseglen.get(4 * hseglen.size());
+                HIPCHK(hipMemcpyAsync(dsl, hsl, 4 * hseglen.size(), hipMemcpyHostToDevice, st));
             }
-            // longest-first packing of the k heaviest into the solo waves; returns the largest load
-            auto pack = [&](uint32_t k, std::vector<std::vector<uint32_t>>* out) -> uint64_t {
-                std::vector<uint64_t> load(sp.waves, 0);
-                std::vector<uint32_t> cnt(sp.waves, 0);
-                if (out) out->assign(sp.waves, {});
-                using E = std::pair<uint64_t, uint32_t>;
-                std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
-                for (uint32_t b = 0; b < sp.waves; ++b) pq.push({0, b});
-                uint64_t mx = 0;
-                for (uint32_t j = 0; j < k && !pq.empty(); ++j) {
-                    const E e = pq.top();
-                    pq.pop();
-                    load[e.second] = e.first + weight(byl[j]);
-                    mx = std::max(mx, load[e.second]);
-                    if (out) (*out)[e.second].push_back(byl[j]);
-                    if (++cnt[e.second] < 64) pq.push({load[e.second], e.second});
+            uint8_t* mst = (uint8_t*)ctx->dmsstate.get(gk_t1ms_state_bytes(nbx));
+            gk_launch_t1_dec_ms(st, src_bytes, dblk, dsl, arena, nbr, mst, cls_sty);
+            launch_check(__LINE__);
+            HIPCHK(hipEventRecord(ctx->ev[8], st));
+            if (dsl) HIPCHK(hipStreamSynchronize(st));   // the pinned table is reused
+        } else {
+            // lane assignment: blocks bucketed by pass count (descending), so the lanes of a
+            // wave decode similar amounts of work and the longest waves start first.  Only
+            // `L` lanes of each 64-lane wave carry a block (gk_t1dec_lanes): fewer lanes per wave
+            // give more waves, so every SIMD of the chip holds waves and can hide latency.
+            const uint32_t L = gk_t1dec_lanes();
+            // The heaviest blocks go to solo waves (gk_t1dec.hip solo_block) on the SIMDs the
+            // lane-parallel waves leave.  Weight = compressed bytes (decisions follow them within
+            // ~10 %).  K, the number of solo blocks, balances the two sides: the lane-parallel
+            // waves last as long as the heaviest block left to them (weight w[K]), a solo wave as
+            // long as its blocks' sum / ratio; the top K are packed longest-first into the solo
+            // waves (LPT) and K is the crossing point of the two (binary search: the first falls,
+            // the second grows with K).  GK_T1DEC_SOLO=n: the n heaviest, one per wave.
+            GkSoloPlan sp = nbr ? gk_t1dec_solo_plan(nbr, L) : GkSoloPlan{0, -1, 1.f};
+            // Device shared with another engine's call in progress (e.g. two images in flight; engines
+            // that merely exist, like the bench's C2 + C3 pair run one after the other, do not count):
+            // no SIMD is idle, so a solo
+            // wave's time is taken from the other decodes; only clear outliers (> 1.3 x the weight of
+            // the block at rank 1,024) go solo, one per wave.  C2 (LL blocks 1.06 x the plateau): none,
+            // 2,394 -> 2,548 Mpix/s with two images in flight; C3 (LL ~1.6 x): kept (1,761 -> 2,056).
+            const bool shared = sp.forced < 0 && engines_busy(ctx->device) > 1;
+            uint32_t nsb = 0;
+            std::vector<uint32_t> byl;
+            std::vector<std::vector<uint32_t>> bins;
+            auto weight = [&](uint32_t q) -> uint64_t { return blk[q].npasses ? blk[q].len : 0; };
+            if (sp.waves) {
+                // (at most 4 blocks per solo wave: the search stays a fraction of a millisecond of host time)
+                const uint32_t kmax = sp.forced >= 0 ? (uint32_t)sp.forced : std::min<uint32_t>(nbr / 4, 4u * sp.waves);
+                byl.resize(nbr);
+                for (uint32_t q = 0; q < nbr; ++q) byl[q] = q;
+                auto heavier = [&](uint32_t x, uint32_t y) { return weight(x) != weight(y) ? weight(x) > weight(y) : x < y; };
+                const uint32_t top = std::min<uint32_t>(kmax + 1, nbr);
+                if (top) {
+                    std::nth_element(byl.begin(), byl.begin() + (top - 1), byl.end(), heavier);
+                    std::sort(byl.begin(), byl.begin() + top, heavier);
                 }
-                return mx;
-            };
-            uint32_t k = 0;
-            if (sp.forced >= 0) {
-                k = (uint32_t)sp.forced;
-                bins.assign(sp.waves, {});
-                for (uint32_t j = 0; j < k; ++j) bins[j].push_back(byl[j]);
-            } else if (shared) {
-                const uint32_t r = std::min<uint32_t>(std::max<uint32_t>(1024u, top), nbr - 1);
-                if (r >= top) std::nth_element(byl.begin() + top, byl.begin() + r, byl.end(), heavier);
-                const double ref = 1.3 * (double)weight(byl[r]);
-                while (k < std::min<uint32_t>(kmax, sp.waves) && (double)weight(byl[k]) > ref) ++k;
-                bins.assign(sp.waves, {});
-                for (uint32_t j = 0; j < k; ++j) bins[j].push_back(byl[j]);
-            } else {
-                auto lane_side = [&](uint32_t kk) -> double { return kk < nbr ? (double)weight(byl[kk]) : 0.0; };
-                auto solo_side = [&](uint32_t kk) -> double { return (double)pack(kk, nullptr) / sp.ratio; };
-                uint32_t lo = 0, hi = kmax;   // first k with solo_side(k) >= lane_side(k)
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) / 2;
-                    if (solo_side(mid) >= lane_side(mid)) hi = mid; else lo = mid + 1;
+                // longest-first packing of the k heaviest into the solo waves; returns the largest load
+                auto pack = [&](uint32_t k, std::vector<std::vector<uint32_t>>* out) -> uint64_t {
+                    std::vector<uint64_t> load(sp.waves, 0);
+                    std::vector<uint32_t> cnt(sp.waves, 0);
+                    if (out) out->assign(sp.waves, {});
+                    using E = std::pair<uint64_t, uint32_t>;
+                    std::priority_queue<E, std::vector<E>, std::greater<E>> pq;
+                    for (uint32_t b = 0; b < sp.waves; ++b) pq.push({0, b});
+                    uint64_t mx = 0;
+                    for (uint32_t j = 0; j < k && !pq.empty(); ++j) {
+                        const E e = pq.top();
+                        pq.pop();
+                        load[e.second] = e.first + weight(byl[j]);
+                        mx = std::max(mx, load[e.second]);
+                        if (out) (*out)[e.second].push_back(byl[j]);
+                        if (++cnt[e.second] < 64) pq.push({load[e.second], e.second});
+                    }
+                    return mx;
+                };
+                uint32_t k = 0;
+                if (sp.forced >= 0) {
+                    k = (uint32_t)sp.forced;
+                    bins.assign(sp.waves, {});
+                    for (uint32_t j = 0; j < k; ++j) bins[j].push_back(byl[j]);
+                } else if (shared) {
+                    const uint32_t r = std::min<uint32_t>(std::max<uint32_t>(1024u, top), nbr - 1);
+                    if (r >= top) std::nth_element(byl.begin() + top, byl.begin() + r, byl.end(), heavier);
+                    const double ref = 1.3 * (double)weight(byl[r]);
+                    while (k < std::min<uint32_t>(kmax, sp.waves) && (double)weight(byl[k]) > ref) ++k;
+                    bins.assign(sp.waves, {});
+                    for (uint32_t j = 0; j < k; ++j) bins[j].push_back(byl[j]);
+                } else {
+                    auto lane_side = [&](uint32_t kk) -> double { return kk < nbr ? (double)weight(byl[kk]) : 0.0; };
+                    auto solo_side = [&](uint32_t kk) -> double { return (double)pack(kk, nullptr) / sp.ratio; };
+                    uint32_t lo = 0, hi = kmax;   // first k with solo_side(k) >= lane_side(k)
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) / 2;
+                        if (solo_side(mid) >= lane_side(mid)) hi = mid; else lo = mid + 1;
+                    }
+                    k = lo;
+                    if (k > 0 && std::max(solo_side(k - 1), lane_side(k - 1)) <= std::max(solo_side(k), lane_side(k))) --k;
+                    if (k) pack(k, &bins);
                 }
-                k = lo;
-                if (k > 0 && std::max(solo_side(k - 1), lane_side(k - 1)) <= std::max(solo_side(k), lane_side(k))) --k;
-                if (k) pack(k, &bins);
+                nsb = k;
             }
-            nsb = k;
-        }
-        uint32_t nsw = 0;   // solo waves holding a block, rounded up to whole workgroups of 12
-        for (uint32_t b = 0; b < bins.size(); ++b)
-            if (!bins[b].empty()) nsw = b + 1;
-        nsw = (nsw + 11) / 12 * 12;
-        const uint32_t nw = nsw + (nbr - nsb + L - 1) / L, nslots = nw * 64;
-        uint32_t* hord = (uint32_t*)ctx->hord.get(4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
-        uint32_t* hpos = hord + nslots;               // slot of block k
-        uint32_t* hids = hpos + nbr;                  // identity (compact table)
-        uint64_t* hwo = (uint64_t*)(hids + nbr + 2);
-        {
-            std::fill(hord, hord + nslots, 0xffffffffu);
-            std::vector<uint8_t> solo(nbr, 0);
-            for (uint32_t b = 0; b < bins.size() && b < nsw; ++b)
-                for (uint32_t i = 0; i < bins[b].size(); ++i) {
-                    const uint32_t q = bins[b][i];
-                    solo[q] = 1;
-                    hord[(size_t)b * 64 + i] = q; hpos[q] = b * 64 + i;
+            uint32_t nsw = 0;   // solo waves holding a block, rounded up to whole workgroups of 12
+            for (uint32_t b = 0; b < bins.size(); ++b)
+                if (!bins[b].empty()) nsw = b + 1;
+            nsw = (nsw + 11) / 12 * 12;
+            const uint32_t nw = nsw + (nbr - nsb + L - 1) / L, nslots = nw * 64;
+            uint32_t* hord = (uint32_t*)ctx->hord.get(4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1));
+            uint32_t* hpos = hord + nslots;               // slot of block k
+            uint32_t* hids = hpos + nbr;                  // identity (compact table)
+            uint64_t* hwo = (uint64_t*)(hids + nbr + 2);
+            {
+                std::fill(hord, hord + nslots, 0xffffffffu);
+                std::vector<uint8_t> solo(nbr, 0);
+                for (uint32_t b = 0; b < bins.size() && b < nsw; ++b)
+                    for (uint32_t i = 0; i < bins[b].size(); ++i) {
+                        const uint32_t q = bins[b][i];
+                        solo[q] = 1;
+                        hord[(size_t)b * 64 + i] = q; hpos[q] = b * 64 + i;
+                    }
+                std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
+                for (uint32_t q = 0; q < nbr; ++q)
+                    if (!solo[q]) cnt[std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1)]++;
+                std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
+                uint32_t acc = 0;
+                for (int k = GK_MAX_PASSES + 1; k >= 0; --k) { start[k] = acc; acc += cnt[k]; }
+                for (uint32_t q = 0; q < nbr; ++q) {
+                    hids[q] = q;
+                    if (solo[q]) continue;
+                    const uint32_t k = std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1);
+                    const uint32_t idx = start[k]++;
+                    const uint32_t slot = (nsw + idx / L) * 64 + idx % L;
+                    hord[slot] = q; hpos[q] = slot;
                 }
-            std::vector<uint32_t> cnt(GK_MAX_PASSES + 2, 0);
-            for (uint32_t q = 0; q < nbr; ++q)
-                if (!solo[q]) cnt[std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1)]++;
-            std::vector<uint32_t> start(GK_MAX_PASSES + 2, 0);
-            uint32_t acc = 0;
-            for (int k = GK_MAX_PASSES + 1; k >= 0; --k) { start[k] = acc; acc += cnt[k]; }
-            for (uint32_t q = 0; q < nbr; ++q) {
-                hids[q] = q;
-                if (solo[q]) continue;
-                const uint32_t k = std::min<uint32_t>(blk[q].npasses, GK_MAX_PASSES + 1);
-                const uint32_t idx = start[k]++;
-                const uint32_t slot = (nsw + idx / L) * 64 + idx % L;
-                hord[slot] = q; hpos[q] = slot;
+                uint64_t wo = 0;
+                for (uint32_t wv = 0; wv < nw; ++wv) {
+                    hwo[wv] = wo;
+                    uint32_t mp = 0;
+                    for (uint32_t i = wv * 64; i < wv * 64 + (wv < nsw ? 64 : L); ++i)
+                        if (hord[i] != 0xffffffffu) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
+                    if (wv < nsw && hord[wv * 64] == 0xffffffffu) continue;   // a solo wave without a block
+                    wo += (272 + (uint64_t)mp * 64) * 64;   // per-lane slab: WS_FIXED + planes (gk_t1dec.hip), 128 B lines
+                }
+                hwo[nw] = wo;
             }
-            uint64_t wo = 0;
-            for (uint32_t wv = 0; wv < nw; ++wv) {
-                hwo[wv] = wo;
-                uint32_t mp = 0;
-                for (uint32_t i = wv * 64; i < wv * 64 + (wv < nsw ? 64 : L); ++i)
-                    if (hord[i] != 0xffffffffu) mp = std::max(mp, (uint32_t)blk[hord[i]].numbps);
-                if (wv < nsw && hord[wv * 64] == 0xffffffffu) continue;   // a solo wave without a block
-                wo += (272 + (uint64_t)mp * 64) * 64;   // per-lane slab: WS_FIXED + planes (gk_t1dec.hip), 128 B lines
+            const size_t obytes = 4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1);
+            uint32_t* dord = (uint32_t*)ctx->dord.get(obytes);
+            HIPCHK(hipMemcpyAsync(dord, hord, obytes, hipMemcpyHostToDevice, st));
+            const uint32_t* dpos = dord + nslots;
+            const uint32_t* dids = dpos + nbr;
+            const uint64_t* dwo = (const uint64_t*)(dids + nbr + 2);
+            uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
+            // lane-parallel decoder state rows start at zero; solo waves write every row recon reads
+            HIPCHK(hipMemsetAsync(dscr + hwo[nsw], 0, 8 * (hwo[nw] - hwo[nsw]), st));
+            gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nslots, nsw);
+            ctx->tm.t1_steps_max = ctx->tm.t1_steps_total = ctx->tm.t1_symbols = 0;
+            ctx->tm.t1_solo_decisions = ctx->tm.t1_solo_decisions_max = 0;
+            ctx->tm.t1_solo_blocks = nsb;
+            if (getenv("GK_T1_STATS")) {
+                uint64_t sv[5];
+                gk_t1dec_stats(sv);
+                ctx->tm.t1_steps_max = sv[0]; ctx->tm.t1_steps_total = sv[1]; ctx->tm.t1_symbols = sv[2];
+                ctx->tm.t1_solo_decisions = sv[3]; ctx->tm.t1_solo_decisions_max = sv[4];
             }
-            hwo[nw] = wo;
+            launch_check(__LINE__);
+            HIPCHK(hipEventRecord(ctx->ev[8], st));
+            uint32_t maxnp = 1;
+            for (uint32_t q = 0; q < nbr; ++q) maxnp = std::max<uint32_t>(maxnp, blk[q].numbps);
+            gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr, maxnp);
         }
-        const size_t obytes = 4 * ((size_t)nslots + 2 * (size_t)nbr + 2) + 8 * ((size_t)nw + 1);
-        uint32_t* dord = (uint32_t*)ctx->dord.get(obytes);
-        HIPCHK(hipMemcpyAsync(dord, hord, obytes, hipMemcpyHostToDevice, st));
-        const uint32_t* dpos = dord + nslots;
-        const uint32_t* dids = dpos + nbr;
-        const uint64_t* dwo = (const uint64_t*)(dids + nbr + 2);
-        uint64_t* dscr = (uint64_t*)ctx->dscratch.get(8 * hwo[nw] + 64);
-        // lane-parallel decoder state rows start at zero; solo waves write every row recon reads
-        HIPCHK(hipMemsetAsync(dscr + hwo[nsw], 0, 8 * (hwo[nw] - hwo[nsw]), st));
-        gk_launch_t1_dec(st, src_bytes, dblk, dord, dscr, dwo, nslots, nsw);
-        ctx->tm.t1_steps_max = ctx->tm.t1_steps_total = ctx->tm.t1_symbols = 0;
-        ctx->tm.t1_solo_decisions = ctx->tm.t1_solo_decisions_max = 0;
-        ctx->tm.t1_solo_blocks = nsb;
-        if (getenv("GK_T1_STATS")) {
-            uint64_t sv[5];
-            gk_t1dec_stats(sv);
-            ctx->tm.t1_steps_max = sv[0]; ctx->tm.t1_steps_total = sv[1]; ctx->tm.t1_symbols = sv[2];
-            ctx->tm.t1_solo_decisions = sv[3]; ctx->tm.t1_solo_decisions_max = sv[4];
-        }
-        launch_check(__LINE__);
-        HIPCHK(hipEventRecord(ctx->ev[8], st));
-        uint32_t maxnp = 1;
-        for (uint32_t q = 0; q < nbr; ++q) maxnp = std::max<uint32_t>(maxnp, blk[q].numbps);
-        gk_launch_t1_recon(st, dblk, dids, dpos, dscr, dwo, arena, nbr, maxnp);
+    };
+    for (size_t k = 0; k < cls_range.size(); ++k) {
+        const uint32_t s0 = cls_range[k].first, e0 = k + 1 < cls_range.size() ? cls_range[k + 1].first : nbr;
+        if (k) HIPCHK(hipStreamSynchronize(st));   // (the pinned staging tables are reused per class)
+        t1_class(s0, e0 - s0, cls_range[k].second);
     }
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[3], st));
@@ -4717,7 +4860,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                     };
                     auto srcf = [&](uint32_t k) { return reinterpret_cast<const float*>(src(k)); };
                     auto dst = [&](uint32_t k) { return qd[k] + ((size_t)(iy0 - qy0[k]) * qs[k] + (ix0 - qx0[k])) * es; };
-                    if (!P.p.irrev) {
+                    if (!P.p.c_irrev(c)) {
                         if (m3) gk_launch_rct_inv_dc(st, src(0), src(1), src(2), RG.stride, stype, dst(0), dst(1), dst(2), qs[0],
                                                      tw, th, shift, mn, mx);
                         else gk_launch_dc_inv(st, src(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
@@ -4773,10 +4916,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
     const bool mct3 = P.mct3();
-    if (P.p.numres > 1 && !P.l1_fusable) {   // levels first, then the inverse MCT + DC shift + clamp below
+    if (P.max_numres() > 1 && !P.l1_fusable) {   // levels first, then the inverse MCT + DC shift + clamp below
         run_dwt(ctx, RG, false, jb, je, ib, ie, nullptr);
     }
-    if (P.p.numres > 1 && P.l1_fusable) {
+    if (P.max_numres() > 1 && P.l1_fusable) {
         L1Io io;
         io.stype = stype; io.mct3 = mct3; io.shift = shift; io.mn = mn; io.mx = mx;
         io.planes.assign(dst.begin(), dst.end());
@@ -4787,20 +4930,20 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         run_dwt(ctx, RG, false, jb, je, ib, ie, &io);
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
-    } else if (!P.p.irrev) {
-        launch_check(__LINE__);
-        HIPCHK(hipEventRecord(ctx->ev[4], st));
-        if (mct3) gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
-                                       ocols(0), orows(0), shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
-            gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shift, mn, mx);
     } else {
+        // (each component by its own transform: COC may differ; the MCT's three share component 0's)
         launch_check(__LINE__);
         HIPCHK(hipEventRecord(ctx->ev[4], st));
-        if (mct3) gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
-                                       ocols(0), orows(0), shift, mn, mx);
-        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c)
-            gk_launch_dc_inv_f(st, planeAf(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shift, mn, mx);
+        if (mct3 && !P.p.c_irrev(0))
+            gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
+                                 ocols(0), orows(0), shift, mn, mx);
+        if (mct3 && P.p.c_irrev(0))
+            gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
+                                 ocols(0), orows(0), shift, mn, mx);
+        for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) {
+            if (!P.p.c_irrev(c)) gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shift, mn, mx);
+            else gk_launch_dc_inv_f(st, planeAf(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shift, mn, mx);
+        }
     }
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[5], st));
