@@ -472,6 +472,9 @@ class Engine:
         info = self.read_header(cs, length)
         x0, y0, x1, y1 = window
         c, h, w = info.numcomps, y1 - y0, x1 - x0
+        sub = self.subsampling()
+        if any(d != (1, 1) for d in sub):
+            return self._window_subsampled(cs, length, window, out, sample_bytes, info, sub)
         red = getattr(self, "_reduce", 0)
         if red:   # the window's canvas rectangle reduced: ceil(x / 2^reduce) (set_decode_reduce)
             cd = lambda v: -(-v >> red)
@@ -585,4 +588,38 @@ class Engine:
             rc = self.lib.gk_decode(self.ctx, b.ctypes.data, len(cs), 0, ptrs, strides, sample_bytes, out_dev)
         if rc != 0:
             self._err("gk_decode")
+        return res
+
+    def _window_subsampled(self, cs, length, window, out, sample_bytes, info, sub):
+        """Window of a stream with subsampled components: component c's plane is the window's
+        canvas rectangle on its grid (every edge ceil(x / dx), then reduced), a list of planes."""
+        x0, y0, x1, y1 = window
+        red = getattr(self, "_reduce", 0)
+        cd = lambda a, b: -(-a // b)
+        shapes = []
+        for dx, dy in sub:
+            gx = lambda v: cd(cd(v + info.x0, dx), 1 << red)
+            gy = lambda v: cd(cd(v + info.y0, dy), 1 << red)
+            shapes.append((gy(y1) - gy(y0), gx(x1) - gx(x0)))
+        c = info.numcomps
+        if out is not None:
+            assert len(out) == c and all(tuple(o.shape) == s for o, s in zip(out, shapes))
+            sample_bytes = _sample_bytes(out[0])
+            res, out_dev = out, 1
+            ptrs = (ctypes.c_void_p * c)(*[o.data_ptr() for o in out])
+            strides = (ctypes.c_uint32 * c)(*[o.stride(0) for o in out])
+        else:
+            res = [np.empty(s, _np_sample_dtype(sample_bytes, info)) for s in shapes]
+            out_dev = 0
+            ptrs = (ctypes.c_void_p * c)(*[r.ctypes.data for r in res])
+            strides = (ctypes.c_uint32 * c)(*[max(s[1], 1) for s in shapes])
+        if _is_torch_cuda(cs):
+            rc = self.lib.gk_decode_window(self.ctx, ctypes.c_void_p(cs.data_ptr()), length, 1, x0, y0, x1, y1, ptrs,
+                                           strides, sample_bytes, out_dev)
+        else:
+            b = np.frombuffer(cs, np.uint8)
+            rc = self.lib.gk_decode_window(self.ctx, b.ctypes.data, len(cs), 0, x0, y0, x1, y1, ptrs, strides,
+                                           sample_bytes, out_dev)
+        if rc != 0:
+            self._err("gk_decode_window")
         return res

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <tuple>
 #include <cmath>
 #include <cstdarg>
@@ -42,6 +43,7 @@
 namespace {
 
 static inline uint32_t ceildivpow2(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + (1ull << b) - 1) >> b); }
+static inline uint32_t ceildiv(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + b - 1) / b); }
 static inline int floorlog2(uint32_t a) { return a > 1 ? 31 - __builtin_clz(a) : 0; }
 static inline uint32_t align_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }
 
@@ -390,6 +392,15 @@ static inline uint64_t relocate(const Plan& P, const Region& R, uint64_t band_of
     const uint64_t y = rem / P.stride, x = rem % P.stride;
     return q * R.plane + (y - R.y0) * R.stride + (x - R.x0);
 }
+// The region R (image-relative, full-resolution canvas grid) on sampling group G's grid: its
+// canvas edges divided by (dx, dy), rounded up, less the group's image origin; the work planes
+// keep R's stride and size (a subsampled grid is never larger).  Without subsampling R itself.
+static inline Region group_region(const Plan& P, const Region& R, const SGroup& G) {
+    Region g = R;
+    g.x0 = ceildiv(R.x0 + P.x0, G.dx) - G.ox; g.y0 = ceildiv(R.y0 + P.y0, G.dy) - G.oy;
+    g.w = ceildiv(R.x0 + R.w + P.x0, G.dx) - G.ox - g.x0; g.h = ceildiv(R.y0 + R.h + P.y0, G.dy) - G.oy - g.y0;
+    return g;
+}
 
 // DWT basis-function norms (T1.cpp:264-277 getnorm_53 / getnorm_97; ISO 15444-1 Annex E)
 static double band_norm(uint32_t level, uint32_t orient, bool rev) {
@@ -539,8 +550,6 @@ static void parse_quant(const std::vector<uint8_t>& b, uint32_t numres, QuantLis
         for (uint32_t k = 1; k < nb; ++k) out[k0 + k] = {s0.first > (k - 1) / 3 ? s0.first - (k - 1) / 3 : 0u, s0.second};
     }
 }
-
-static inline uint32_t ceildiv(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a + b - 1) / b); }
 
 static void build_tile(Plan& P, TileG& T, uint32_t t) {
     T.comps.assign(P.nc, CompG());
@@ -2738,10 +2747,10 @@ static void restore_native_qcd(gk_ctx* ctx) {
 struct L1Io {
     int stype = GK_S32;
     bool mct3 = false;
-    std::vector<const void*> planes;
+    std::vector<const void*> planes;     // component c's plane at its output rectangle's origin
     std::vector<uint32_t> strides;
     int32_t shift = 0, mn = 0, mx = 0;
-    GkWin win;
+    uint32_t cx0 = 0, cy0 = 0, cx1 = 0, cy1 = 0;   // inverse: the output rectangle on the canvas
 };
 
 // Forward/inverse DWT over all components with the ping-pong placement of gk_common.h; every
@@ -2759,6 +2768,7 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
     for (const SGroup& G : P.groups) {
     const uint32_t L = G.numres - 1;
     const uint32_t irrev = G.irrev;
+    const Region RGg = group_region(P, RG, G);
     const uint32_t nlev = forward ? L : (L + 1 > lstop ? L + 1 - lstop : 0);
     for (uint32_t i = 0; i < nlev; ++i) {
         uint32_t l = forward ? i + 1 : L - i;     // level being (un)done
@@ -2779,8 +2789,8 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
             S.tb.i0 = ki0; S.tb.nx = ki1 - ki0;
             S.tb.j0 = kj0; S.tb.ny = kj1 - kj0;
             // member k's region position: px0 + k dx - RG.x0 = k dx - ox (modulo 2^32; the true value >= 0)
-            // (a subsampled stream's regions are the whole image: origin 0 on every grid)
-            S.tb.ox = RG.x0 - S.px0; S.tb.oy = RG.y0 - S.py0;
+            // (the region on the group's grid)
+            S.tb.ox = RGg.x0 - S.px0; S.tb.oy = RGg.y0 - S.py0;
             const uint32_t w = S.resw[l - 1], h = S.resh[l - 1];
             // a level whose input resolution starts on an odd coordinate (either axis), or every
             // level under GK_DWT_ANY: the parity-general kernels (gk_dwt_any.hip)
@@ -2805,9 +2815,12 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
             if (l == 1 && io) {
                 // fused level 1: three components through the MCT, the others one by one
                 const uint64_t es = gk_sample_size(io->stype);
-                // the output window on this grid (a subsampled stream decodes whole images)
-                GkWin win = io->win;
-                if (P.subsampled()) { win.x0 = 0; win.y0 = 0; win.x1 = (int32_t)G.w; win.y1 = (int32_t)G.h; }
+                // the output rectangle on this group's grid, relative to its region
+                GkWin win;
+                if (!forward) {
+                    win.x0 = (int32_t)(ceildiv(io->cx0, G.dx) - G.ox - RGg.x0); win.y0 = (int32_t)(ceildiv(io->cy0, G.dy) - G.oy - RGg.y0);
+                    win.x1 = (int32_t)(ceildiv(io->cx1, G.dx) - G.ox - RGg.x0); win.y1 = (int32_t)(ceildiv(io->cy1, G.dy) - G.oy - RGg.y0);
+                }
                 for (uint32_t c = c0; c < run.second;) {
                     const int nc = (io->mct3 && c == 0 && run.second >= 3) ? 3 : 1;
                     int32_t* dl = dst_l + (size_t)(c - c0) * cst;
@@ -3095,7 +3108,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
         uint64_t* hso = (uint64_t*)(hb + nbx);
         for (uint32_t i = 0; i < nbr; ++i) {
             hb[i] = P.blocks[b0 + i];
-            hb[i].band_off = relocate(P, RG, hb[i].band_off);
+            hb[i].band_off = relocate(P, group_region(P, RG, P.groups[P.group_of[hb[i].comp]]), hb[i].band_off);
             hb[i].stride = RG.stride;
             hb[i].data_off -= slot0;
             hb[i].flags = (uint8_t)((hb[i].flags & ~2u) | (do_rc ? 2u : 0u));
@@ -4096,10 +4109,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                     if (B.numbps > 30) throw GkError("more than 30 band bit-planes (ROI shift included) not supported");
     const uint32_t red = ctx->dec_reduce;
     if (red >= P.min_numres()) throw GkError("reduce must be less than the number of resolutions");
-    // subsampled components, or components coded differently (COC), decode whole images (every
-    // component plane at its own size)
-    const bool sub = P.subsampled() || !P.p.cc.empty();
-    if (sub && win) throw GkError("window decodes of subsampled or COC-coded components are not supported on this path");
+    // subsampled components: every component plane at its own size, rectangles on its grid
     auto keep_window = [&]() {   // keep only the tile parts of tiles intersecting the window
         if (!win) return;
         if (win[0] >= win[2] || win[1] >= win[3] || win[2] > P.w || win[3] > P.h) throw GkError("bad decode window");
@@ -4139,7 +4149,6 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         ib = std::min(ib, t % P.ntx); ie = std::max(ie, t % P.ntx + 1);
         jb = std::min(jb, t / P.ntx); je = std::max(je, t / P.ntx + 1);
     }
-    if (sub) { ib = 0; ie = P.ntx; jb = 0; je = P.nty; }   // (tiles without a tile part decode as zero)
     // work planes cover the tile rectangle only (tiles of the rectangle without a tile part
     // decode as zero); the output region is the rectangle, clipped to the window
     const TileG& Tfirst = P.tiles[(size_t)jb * P.ntx + ib];
@@ -4151,6 +4160,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         ox = win[0]; oy = win[1];
     }
     const uint32_t ncols = rx1 - rx0, nrows = ry1 - ry0;
+    // the region on each sampling group's grid (RG itself without subsampling)
+    std::vector<Region> RGg;
+    for (const SGroup& G : P.groups) RGg.push_back(group_region(P, RG, G));
     // Per tile: which code-blocks reach [rx0, rx1) x [ry0, ry1).  Inverse lifting reconstructs
     // sample n of a level from low/high coefficients within a few positions of n/2 (5/3: the
     // update/predict steps reach one neighbour each; 9/7: four steps), so the coefficients a
@@ -4158,22 +4170,35 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     // (the padded band window of TileComponentWindowBuffer / T2Decompress.cpp:55-116).  Blocks
     // outside are not decoded (their samples only feed outputs outside the window), and with
     // PLT a packet none of whose blocks is needed is skipped unparsed.
-    const uint32_t Lv = P.p.numres - 1, pad = P.p.irrev ? 4 : 2;
     // (on the canvas: the output rectangle moved by the image origin)
     const uint32_t cx0 = rx0 + P.x0, cy0 = ry0 + P.y0, cx1 = rx1 + P.x0, cy1 = ry1 + P.y0;
     auto block_needed = [&](const TileG& T, std::vector<uint8_t>& need) {
         need.assign(T.b1 - T.b0, 1);
         if (!win || (cx0 <= T.x0 && T.x1 <= cx1 && cy0 <= T.y0 && T.y1 <= cy1)) return;
-        // lo[a][l], hi[a][l]: needed [begin, end) in level-l low / high band coordinates, axis a
-        uint32_t lo[2][GK_MAXRLVLS + 1][2], hi[2][GK_MAXRLVLS + 1][2];
-        const CompG& C0 = T.comps[0];
+        // per sampling group (its grid, levels and transform; the components of a group share
+        // their geometry): lo[a][l], hi[a][l] = needed [begin, end) in level-l low / high band
+        // coordinates, axis a
+        const size_t ng = P.groups.size();
+        std::vector<std::array<std::array<std::array<uint32_t, 2>, GK_MAXRLVLS + 1>, 2>> LO(ng), HI(ng);
+        std::vector<uint8_t> done(ng, 0);
+        for (uint32_t c = 0; c < P.nc; ++c) {
+        const uint32_t g = P.group_of[c];
+        if (done[g]) continue;
+        done[g] = 1;
+        const SGroup& SG = P.groups[g];
+        const uint32_t Lv = SG.numres - 1, pad = SG.irrev ? 4 : 2;
+        auto& lo = LO[g];
+        auto& hi = HI[g];
+        const CompG& C0 = T.comps[c];
         for (int ax = 0; ax < 2; ++ax) {
-            uint32_t s0 = ax ? std::max(cy0, T.y0) : std::max(cx0, T.x0);
-            uint32_t s1 = ax ? std::min(cy1, T.y1) : std::min(cx1, T.x1);
+            // the window and the tile on the group's grid
+            const uint32_t d = ax ? SG.dy : SG.dx;
+            uint32_t s0 = ceildiv(ax ? std::max(cy0, T.y0) : std::max(cx0, T.x0), d);
+            uint32_t s1 = ceildiv(ax ? std::min(cy1, T.y1) : std::min(cx1, T.x1), d);
             lo[ax][0][0] = s0; lo[ax][0][1] = s1;
             for (uint32_t l = 1; l <= Lv; ++l) {
-                const ResG& Rl = C0.res[P.p.numres - l];       // resolution holding level-l bands
-                const ResG& Rlow = C0.res[P.p.numres - 1 - l]; // its low-pass image
+                const ResG& Rl = C0.res[SG.numres - l];       // resolution holding level-l bands
+                const ResG& Rlow = C0.res[SG.numres - 1 - l]; // its low-pass image
                 const uint32_t c0 = s0 / 2 > pad ? s0 / 2 - pad : 0, c1 = (s1 + 1) / 2 + pad;
                 const uint32_t lx0 = ax ? Rlow.y0 : Rlow.x0, lx1 = lx0 + (ax ? Rlow.h : Rlow.w);
                 const BandG& Bh = Rl.bands[ax ? 1 : 0];       // HL (high in x) / LH (high in y)
@@ -4183,14 +4208,18 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                 s0 = lo[ax][l][0]; s1 = std::max(lo[ax][l][0], lo[ax][l][1]);
             }
         }
-        for (uint32_t c = 0; c < P.nc; ++c)
-            for (uint32_t r = 0; r < P.p.numres; ++r) {
+        }
+        for (uint32_t c = 0; c < P.nc; ++c) {
+            const uint32_t g = P.group_of[c], nres = P.groups[g].numres;
+            const auto& lo = LO[g];
+            const auto& hi = HI[g];
+            for (uint32_t r = 0; r < nres; ++r) {
                 const ResG& R = T.comps[c].res[r];
-                const uint32_t lev = r ? P.p.numres - r : Lv;
+                const uint32_t lev = r ? nres - r : nres - 1;
                 for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
                     const uint32_t o = R.bands[bi].orient;
-                    const uint32_t* nx = (o & 1) ? hi[0][lev] : lo[0][lev];
-                    const uint32_t* ny = (o & 2) ? hi[1][lev] : lo[1][lev];
+                    const uint32_t* nx = (o & 1) ? hi[0][lev].data() : lo[0][lev].data();
+                    const uint32_t* ny = (o & 2) ? hi[1][lev].data() : lo[1][lev].data();
                     for (uint32_t pi = 0; pi < R.pw * R.ph; ++pi) {
                         const PrecG& PG = R.prc[bi][pi];
                         for (uint32_t k = 0; k < PG.cw * PG.ch; ++k) {
@@ -4202,6 +4231,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                     }
                 }
             }
+        }
     };
     std::vector<std::vector<uint8_t>> part_need(Hd.parts.size());
     host_pool().run(Hd.parts.size(), [&](size_t q) { block_needed(P.tiles[Hd.parts[q].tile], part_need[q]); });
@@ -4390,7 +4420,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             if (!count_only) {
                 GkBlock& G = blk[nb0 + n];
                 G = P.blocks[T.b0 + lb];
-                G.band_off = relocate(P, RG, G.band_off);
+                G.band_off = relocate(P, RGg[P.group_of[G.comp]], G.band_off);
                 G.stride = RG.stride;
                 G.band_numbps = (uint8_t)R.bands[bi].numbps;
                 G.step = R.bands[bi].step_dec / 2.0f;
@@ -4803,20 +4833,19 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         // component bounds of CodeStreamDecompress.cpp:471-481, rectceildivpow2): the output is
         // the reduced tile rectangle clipped to it, the caller's planes addressing its origin
         std::vector<uint32_t> rox(P.nc), roy(P.nc), qx0(P.nc), qy0(P.nc), qx1(P.nc), qy1(P.nc), wx0(P.nc, 0), wy0(P.nc, 0);
+        // (component c: canvas positions on its grid first, ceil(x / dx), then reduced)
         for (uint32_t c = 0; c < P.nc; ++c) {
             const SGroup& G = P.groups[P.group_of[c]];
+            auto rx = [&](uint32_t v) { return ceildivpow2(ceildiv(v, G.dx), red); };
+            auto ry = [&](uint32_t v) { return ceildivpow2(ceildiv(v, G.dy), red); };
             rox[c] = ceildivpow2(G.ox, red); roy[c] = ceildivpow2(G.oy, red);
-            if (sub) {   // the whole component
-                qx0[c] = 0; qy0[c] = 0; qx1[c] = ceildivpow2(G.ox + G.w, red) - rox[c]; qy1[c] = ceildivpow2(G.oy + G.h, red) - roy[c];
-                continue;
-            }
-            qx0[c] = ceildivpow2(RG.x0 + P.x0, red) - rox[c]; qy0[c] = ceildivpow2(RG.y0 + P.y0, red) - roy[c];
-            qx1[c] = ceildivpow2(RG.x0 + P.x0 + RG.w, red) - rox[c]; qy1[c] = ceildivpow2(RG.y0 + P.y0 + RG.h, red) - roy[c];
+            qx0[c] = rx(RG.x0 + P.x0) - rox[c]; qy0[c] = ry(RG.y0 + P.y0) - roy[c];
+            qx1[c] = rx(RG.x0 + P.x0 + RG.w) - rox[c]; qy1[c] = ry(RG.y0 + P.y0 + RG.h) - roy[c];
             if (win) {
-                wx0[c] = ceildivpow2(win[0] + P.x0, red) - rox[c]; wy0[c] = ceildivpow2(win[1] + P.y0, red) - roy[c];
+                wx0[c] = rx(win[0] + P.x0) - rox[c]; wy0[c] = ry(win[1] + P.y0) - roy[c];
                 qx0[c] = std::max(qx0[c], wx0[c]); qy0[c] = std::max(qy0[c], wy0[c]);
-                qx1[c] = std::min(qx1[c], ceildivpow2(win[2] + P.x0, red) - rox[c]);
-                qy1[c] = std::min(qy1[c], ceildivpow2(win[3] + P.y0, red) - roy[c]);
+                qx1[c] = std::min(qx1[c], rx(win[2] + P.x0) - rox[c]);
+                qy1[c] = std::min(qy1[c], ry(win[3] + P.y0) - roy[c]);
                 if (qx1[c] <= qx0[c] || qy1[c] <= qy0[c]) throw GkError("the window is empty at this reduction");
             }
         }
@@ -4854,9 +4883,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                     const uint32_t cn = m3 ? 3 : 1;
                     if (ix1 <= ix0 || iy1 <= iy0) { c += cn; continue; }
                     const uint32_t tw = ix1 - ix0, th = iy1 - iy0;
+                    const Region& Rg = RGg[P.group_of[c]];
                     auto src = [&](uint32_t k) {
                         return arena + (size_t)k * 2 * RG.plane + ((red & 1) ? RG.plane : 0) +
-                               (size_t)(cy0 - G.oy - RG.y0 + (iy0 - ty0)) * RG.stride + (cx0 - G.ox - RG.x0 + (ix0 - tx0));
+                               (size_t)(cy0 - G.oy - Rg.y0 + (iy0 - ty0)) * RG.stride + (cx0 - G.ox - Rg.x0 + (ix0 - tx0));
                     };
                     auto srcf = [&](uint32_t k) { return reinterpret_cast<const float*>(src(k)); };
                     auto dst = [&](uint32_t k) { return qd[k] + ((size_t)(iy0 - qy0[k]) * qs[k] + (ix0 - qx0[k])) * es; };
@@ -4891,9 +4921,17 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         ctx->tm.total_ms = ev_ms(ctx, 0, 6); ctx->tm.t1_blocks = nbr;
         return;
     }
-    // the output rectangle of component c (a subsampled component: its whole plane, on its grid)
-    auto ocols = [&](uint32_t c) { return sub ? P.groups[P.group_of[c]].w : ncols; };
-    auto orows = [&](uint32_t c) { return sub ? P.groups[P.group_of[c]].h : nrows; };
+    // the output rectangle of component c on its grid ([rx0, rx1) x [ry0, ry1) without
+    // subsampling), and the caller plane's origin there (the window's, or the image's)
+    std::vector<uint32_t> qx0(P.nc), qy0(P.nc), qx1(P.nc), qy1(P.nc), qox(P.nc), qoy(P.nc);
+    for (uint32_t c = 0; c < P.nc; ++c) {
+        const SGroup& G = P.groups[P.group_of[c]];
+        qx0[c] = ceildiv(rx0 + P.x0, G.dx) - G.ox; qx1[c] = ceildiv(rx1 + P.x0, G.dx) - G.ox;
+        qy0[c] = ceildiv(ry0 + P.y0, G.dy) - G.oy; qy1[c] = ceildiv(ry1 + P.y0, G.dy) - G.oy;
+        qox[c] = ceildiv(ox + P.x0, G.dx) - G.ox; qoy[c] = ceildiv(oy + P.y0, G.dy) - G.oy;
+    }
+    auto ocols = [&](uint32_t c) { return qx1[c] - qx0[c]; };
+    auto orows = [&](uint32_t c) { return qy1[c] - qy0[c]; };
     std::vector<void*> dst(P.nc);
     std::vector<uint32_t> dstr(P.nc);
     if (!out_on_device) {
@@ -4907,12 +4945,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         }
     } else {
         for (uint32_t c = 0; c < P.nc; ++c) {
-            dst[c] = (uint8_t*)comps[c] + ((size_t)(ry0 - oy) * strides[c] + (rx0 - ox)) * es;
+            dst[c] = (uint8_t*)comps[c] + ((size_t)(qy0[c] - qoy[c]) * strides[c] + (qx0[c] - qox[c])) * es;
             dstr[c] = strides[c];
         }
     }
     auto planeA = [&](uint32_t c) {
-        return arena + (size_t)c * 2 * RG.plane + (size_t)(ry0 - RG.y0) * RG.stride + (rx0 - RG.x0);
+        const Region& Rg = RGg[P.group_of[c]];
+        return arena + (size_t)c * 2 * RG.plane + (size_t)(qy0[c] - Rg.y0) * RG.stride + (qx0[c] - Rg.x0);
     };
     auto planeAf = [&](uint32_t c) { return reinterpret_cast<const float*>(planeA(c)); };
     const bool mct3 = P.mct3();
@@ -4924,8 +4963,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         io.stype = stype; io.mct3 = mct3; io.shift = shift; io.mn = mn; io.mx = mx;
         io.planes.assign(dst.begin(), dst.end());
         io.strides = dstr;
-        io.win.x0 = (int32_t)(rx0 - RG.x0); io.win.y0 = (int32_t)(ry0 - RG.y0);
-        io.win.x1 = io.win.x0 + (int32_t)ncols; io.win.y1 = io.win.y0 + (int32_t)nrows;
+        io.cx0 = rx0 + P.x0; io.cy0 = ry0 + P.y0; io.cx1 = rx1 + P.x0; io.cy1 = ry1 + P.y0;
         if (mct3 && (dstr[1] != dstr[0] || dstr[2] != dstr[0])) throw GkError("the first three components must share a stride");
         run_dwt(ctx, RG, false, jb, je, ib, ie, &io);
         launch_check(__LINE__);
@@ -4949,7 +4987,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     HIPCHK(hipEventRecord(ctx->ev[5], st));
     if (!out_on_device) {
         for (uint32_t c = 0; c < P.nc; ++c)
-            HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)(ry0 - oy) * strides[c] + (rx0 - ox)) * es,
+            HIPCHK(hipMemcpy2DAsync((uint8_t*)comps[c] + ((size_t)(qy0[c] - qoy[c]) * strides[c] + (qx0[c] - qox[c])) * es,
                                     (size_t)strides[c] * es, dst[c], (size_t)ocols(c) * es, (size_t)ocols(c) * es, orows(c),
                                     hipMemcpyDeviceToHost, st));
     }

@@ -1,7 +1,7 @@
 """Main-header COC on the HIP path (the oracle half, pinned by OpenJPEG, is tests/test_coc.py):
 components with their own decomposition levels, code-block size and style (Part-1, mode switches,
 HT, wide blocks), transform and precincts decode to the oracle's planes, i.e. to each
-component's own single-component decode; full and reduced, host and device streams."""
+component's own single-component decode; full and reduced, host and device streams, windows."""
 import numpy as np
 import pytest
 
@@ -52,6 +52,14 @@ def test_engine_coc_reduced(eng, name):
         np.testing.assert_array_equal(g, w)
 
 
-def test_engine_coc_window_refused(eng):
-    with pytest.raises(RuntimeError, match="COC-coded components"):
-        eng.decode_window(stream("ht_and_part1"), (0, 0, 16, 16))
+@pytest.mark.parametrize("name", ["levels_cblk_97_prc", "ht_and_part1", "mode_switches", "wide_block"])
+@pytest.mark.parametrize("win", [(0, 0, 16, 16), (7, 5, 45, 39), (33, 21, 60, 50)])
+def test_engine_coc_window(eng, name, win):
+    # each component's window equals the crop of the oracle's partial-rule decode (its own levels,
+    # code-blocks and transform project the window onto its bands)
+    cs = stream(name)
+    full, _ = O.decode(cs, partial=True)
+    x0, y0, x1, y1 = win
+    got = eng.decode_window(cs, win)
+    for g, f in zip(got, full):
+        np.testing.assert_array_equal(g, f[y0:y1, x0:x1])

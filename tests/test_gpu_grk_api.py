@@ -254,3 +254,24 @@ def test_grk_api_subsampled_components(tool, name, flags):
     flat = np.fromfile(dec, np.int32)
     want, _ = O.decode(ref)
     np.testing.assert_array_equal(flat, np.concatenate([w.ravel() for w in want]))
+
+
+def test_grk_api_subsampled_window(tool):
+    # grk_decompress -d on a 4:2:0 stream: each component of the composite takes the window's
+    # rectangle on its grid (GrkImage::subsampleAndReduce), decoded with the partial-tile rule
+    from subsampling_cases import CASES, planes, oracle_kw
+    name = "tiled_pcrl"
+    W, H, sub, prec, kw = CASES[name]
+    exe, d = tool
+    ref = O.encode(planes(name), prec, size=(W, H), **oracle_kw(name))
+    path = d / "sub_win.j2k"
+    path.write_bytes(ref)
+    x0, y0, x1, y1 = 9, 5, 101, 63
+    dec = d / "sub_win.dec"
+    _run(exe, "dec", path, dec, "-d", "%d,%d,%d,%d" % (x0, y0, x1, y1))
+    full, _ = O.decode(ref, partial=True)
+    want = []
+    for f, (dx, dy) in zip(full, sub):
+        cd = lambda a, b: -(-a // b)
+        want.append(f[cd(y0, dy):cd(y1, dy), cd(x0, dx):cd(x1, dx)].ravel())
+    np.testing.assert_array_equal(np.fromfile(dec, np.int32), np.concatenate(want))

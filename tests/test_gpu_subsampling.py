@@ -1,7 +1,7 @@
 """Subsampled components on the HIP path (the oracle half, pinned by OpenJPEG, is
 tests/test_subsampling.py): gk_encode with gk_set_subsampling writes the oracle's bytes, gk_decode
 returns the oracle's planes (each component at its own size, host or device, int32 or 8/16-bit,
-full or reduced resolution), and windows of such streams are refused."""
+full or reduced resolution), and windows return each component's window on its grid."""
 import os
 import sys
 
@@ -99,10 +99,57 @@ def test_engine_round_trip_lossless(eng):
         np.testing.assert_array_equal(g, s)
 
 
-def test_engine_subsampled_window_refused(eng):
-    cs = _oracle_cs("420_53")
-    with pytest.raises(RuntimeError, match="window decodes of subsampled"):
-        eng.decode_window(cs, (0, 0, 16, 16))
+def _crop(planes, window, sub, origin, reduce=0):
+    """Each component's window on its grid: canvas edges ceil(x / dx), then ceil(/ 2^reduce)."""
+    x0, y0, x1, y1 = window
+    X0, Y0 = origin
+    cd = lambda a, b: -(-a // b)
+    out = []
+    for p, (dx, dy) in zip(planes, sub):
+        gx = lambda v: cd(cd(v + X0, dx), 1 << reduce) - cd(cd(X0, dx), 1 << reduce)
+        gy = lambda v: cd(cd(v + Y0, dy), 1 << reduce) - cd(cd(Y0, dy), 1 << reduce)
+        out.append(p[gy(y0):gy(y1), gx(x0):gx(x1)])
+    return out
+
+
+WINDOWS = [(0, 0, 16, 16), (5, 3, 41, 37), (17, 11, 67, 45)]
+
+
+@pytest.mark.parametrize("name", ["420_53", "offset_odd", "tiled_pcrl", "tiled_rpcl_origin", "422_97", "ht_420",
+                                  "cprl_dx3"])
+@pytest.mark.parametrize("wi", range(len(WINDOWS)))
+def test_engine_subsampled_window(eng, name, wi):
+    # Grok's window semantics: the composite's component c is the window's canvas rectangle on its
+    # grid; a window decode takes the partial-tile inverse (the oracle's partial mode)
+    W, H, sub, prec, kw = CASES[name]
+    x0, y0, x1, y1 = WINDOWS[wi]
+    win = (x0, y0, min(x1, W), min(y1, H))
+    cs = _oracle_cs(name)
+    full, _ = O.decode(cs, partial=True)
+    origin = kw.get("origin") or kw.get("tile_origin") or (0, 0)
+    got = eng.decode_window(cs, win)
+    for g, w in zip(got, _crop(full, win, sub, origin)):
+        np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.parametrize("name", ["420_53_r6", "tiled_pcrl", "422_97"])
+def test_engine_subsampled_window_reduced(eng, name):
+    W, H, sub, prec, kw = CASES[name]
+    win = (5, 3, min(61, W), min(47, H))
+    cs = _oracle_cs(name)
+    O.set_decode_reduce(1)
+    try:
+        full, _ = O.decode(cs, partial=True)
+    finally:
+        O.set_decode_reduce(0)
+    eng.set_decode_reduce(1)
+    try:
+        got = eng.decode_window(cs, win)
+    finally:
+        eng.set_decode_reduce(0)
+    origin = kw.get("origin") or kw.get("tile_origin") or (0, 0)
+    for g, w in zip(got, _crop(full, win, sub, origin, reduce=1)):
+        np.testing.assert_array_equal(g, w)
 
 
 def test_engine_tile_pitch_must_divide(eng):
