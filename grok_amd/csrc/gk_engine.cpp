@@ -3643,6 +3643,11 @@ struct TilePart {                  // packet bytes [data, end) of one tile part
     std::vector<std::pair<size_t, size_t>> more;
     uint32_t tpsot = 0;
     std::vector<Poc> pocs;          // after merge_tile_parts: the tile's progression order changes (empty: the main header's)
+    // packed packet headers (A.7.4 / A.7.5): this part's PPT markers (Zppt, Ippt); after
+    // merge_tile_parts the tile's headers (its PPT data in Zppt order, or its PPM run) in hdrs
+    std::vector<std::pair<uint32_t, std::vector<uint8_t>>> ppt;
+    std::vector<uint8_t> hdrs;
+    bool packed = false;
 };
 // POC marker body (A.6.6): per entry RSpoc, CSpoc (1 or 2 bytes), LYEpoc (2), REpoc, CEpoc
 // (1 or 2; 0 = 256 with one byte), Ppoc.  Appended to out: CodeStreamDecompress::read_poc
@@ -3678,6 +3683,7 @@ struct Header {
     std::vector<uint8_t> cod, qcd_body;               // main COD / QCD marker bodies (after Lxxx)
     std::vector<std::vector<uint8_t>> ccod;           // per component: its coding as a COC body states it
                                                       // (Scoc, SPcoc): its main COC, else the COD's
+    std::map<uint32_t, std::vector<uint8_t>> ppm;     // PPM bodies by Zppm (PPMMarker::read)
 };
 // The COD's coding in COC form: Scod's precinct flag, then SPcod from the decomposition levels on
 static std::vector<uint8_t> cod_as_coc(const std::vector<uint8_t>& cod) {
@@ -3759,6 +3765,15 @@ static size_t resync_part_end(ByteSrc& S, size_t pos, size_t end, uint32_t nt) {
     }
     return end;
 }
+// PPT marker (A.7.5; CodeStreamDecompress::read_ppt): Zppt, then Ippt (packed packet headers of
+// the tile); not in a stream with PPM (read_ppt's error)
+template <class Hdr> static std::pair<uint32_t, std::vector<uint8_t>> read_ppt(ByteSrc& S, size_t s, uint32_t L, const Hdr& Hd) {
+    if (L < 3) throw GkError("corrupt PPT marker");
+    if (!Hd.ppm.empty()) throw GkError("PPT marker in a stream with PPM markers");
+    std::vector<uint8_t> v(L - 3);
+    for (uint32_t k = 0; k + 3 < L; ++k) v[k] = S.at(s + 1 + k);
+    return {S.at(s), std::move(v)};
+}
 // The tile parts by the SOT chain (Psot of each), their tile-part header markers read
 template <class Hdr> static void walk_sot_chain(ByteSrc& S, Hdr& Hd) {
     Plan& W = Hd.want;
@@ -3772,13 +3787,16 @@ template <class Hdr> static void walk_sot_chain(ByteSrc& S, Hdr& Hd) {
         if (end > S.len) throw GkError("corrupt SOT (Psot)");
         size_t j = pos + 12;
         std::vector<Poc> tpoc;
+        std::vector<std::pair<uint32_t, std::vector<uint8_t>>> tppt;
         while (j + 4 <= end && S.be16(j) != 0xff93) {
             if (S.be16(j) == 0xff5f) parse_poc(S, j + 4, S.be16(j + 2), W.nc, tpoc);   // tile-part POC
+            if (S.be16(j) == 0xff61) tppt.push_back(read_ppt(S, j + 4, S.be16(j + 2), Hd));
             check_override_marker(S, j + 4, S.be16(j), S.be16(j + 2), Hd, true);
             j += 2 + S.be16(j + 2);
         }
         if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
         Hd.parts.push_back({isot, pos, j + 2, end, {}, {}, S.at(pos + 10), std::move(tpoc)});
+        Hd.parts.back().ppt = std::move(tppt);
         pos = end;
     }
 }
@@ -3896,6 +3914,9 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             qcc.push_back({c, std::vector<uint8_t>(b.begin() + cw, b.end())});
         } else if (m == 0xff53) {
             coc_qcc.push_back(i);
+        } else if (m == 0xff60) {   // PPM (A.7.4): Zppm, then (Nppm, Ippm) runs
+            if (L < 3) throw GkError("corrupt PPM marker");
+            if (!Hd.ppm.emplace(S.at(s), marker_body(S, s + 1, L - 1)).second) throw GkError("PPM: Zppm read twice");
         }
         i += 2 + L;
     }
@@ -3988,6 +4009,7 @@ static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
         while (j + 4 <= TP.end && S.be16(j) != 0xff93) {
             const uint32_t m = S.be16(j), L = S.be16(j + 2);
             if (m == 0xff5f) parse_poc(S, j + 4, L, nc, TP.pocs);   // tile-part POC
+            if (m == 0xff61) TP.ppt.push_back(read_ppt(S, j + 4, L, Hd));
             check_override_marker(S, j + 4, m, L, Hd, true);
             if (m == 0xff58) {
                 uint32_t v = 0;
@@ -4050,8 +4072,39 @@ static void merge_tile_parts(Header& Hd) {
         TilePart& H = out[it->second];
         if (TP.tpsot != H.more.size() + 1) throw GkError("tile parts out of order (TPsot)");
         H.more.push_back({TP.data, TP.end});
+        for (auto& e : TP.ppt) H.ppt.push_back(std::move(e));
         H.plt.insert(H.plt.end(), TP.plt.begin(), TP.plt.end());
         H.pocs.insert(H.pocs.end(), TP.pocs.begin(), TP.pocs.end());
+    }
+    // packed packet headers: PPM's Nppm runs (PPMMarker::merge), the k-th taken by tile k (T2Decompress
+    // indexes m_tile_packet_headers by tile, :257-266: kept to one tile part per tile), or the tile's
+    // PPT data in Zppt order (merge_ppt, one index space per tile)
+    std::vector<std::vector<uint8_t>> runs;
+    if (!Hd.ppm.empty()) {
+        std::vector<uint8_t> v;
+        for (auto& kv : Hd.ppm) v.insert(v.end(), kv.second.begin(), kv.second.end());
+        for (size_t at = 0; at < v.size();) {
+            if (v.size() - at < 4) throw GkError("PPM: not enough bytes for Nppm");
+            const uint32_t n = (uint32_t)v[at] << 24 | (uint32_t)v[at + 1] << 16 | (uint32_t)v[at + 2] << 8 | v[at + 3];
+            at += 4;
+            if (v.size() - at < n) throw GkError("PPM: packed headers shorter than Nppm");
+            runs.emplace_back(v.begin() + at, v.begin() + at + n);
+            at += n;
+        }
+    }
+    for (TilePart& H : out) {
+        if (!Hd.ppm.empty()) {
+            if (!H.more.empty()) throw GkError("PPM with several tile parts per tile is not supported on this path");
+            if (H.tile >= runs.size()) throw GkError("PPM has no packed packet headers for a tile");
+            H.hdrs = runs[H.tile]; H.packed = true;
+        } else if (!H.ppt.empty()) {
+            std::map<uint32_t, std::vector<uint8_t>> z;
+            for (auto& e : H.ppt)
+                if (!z.emplace(e.first, std::move(e.second)).second) throw GkError("PPT: Zppt read twice");
+            for (auto& kv : z) H.hdrs.insert(H.hdrs.end(), kv.second.begin(), kv.second.end());
+            H.packed = true;
+        }
+        if (H.packed) H.plt.clear();   // (packet lengths are not used with packed headers)
     }
     const std::vector<Poc>& main_pocs = Hd.want.p.pocs;
     for (TilePart& H : out) {
@@ -4273,6 +4326,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         st2.chunks.reserve(ntb);
         size_t tile_end = TPt.end;
         size_t pos = TPt.data, pk = 0, nextp = 0;
+        ByteSrc HS;   // the tile's packed packet headers (PPM / PPT)
+        HS.host = TPt.hdrs.data(); HS.len = TPt.hdrs.size();
+        size_t hpos = 0;
         const std::vector<PacketRef> order = packet_order(P, TG, P.p.nlayers, TPt.pocs.empty() ? &P.p.pocs : &TPt.pocs);
         // layer limit (tcp->numLayersToDecompress): packets of later layers are skipped through
         // PLT or parsed without their data (T2Decompress::processPacket, T2Decompress.cpp:55-116)
@@ -4301,7 +4357,9 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                             if (BS.be16(pos + 4) != (pk & 0xffff)) throw GkError("SOP marker packet counter mismatch");
                             pos += 6;
                         }
-                        BitReader br(BS, pos, tile_end);
+                        // the header from the packed headers (PPM / PPT) when the tile has them, else in
+                        // front of the body (T2Decompress.cpp:255-270)
+                        BitReader br = TPt.packed ? BitReader(HS, hpos, HS.len) : BitReader(BS, pos, tile_end);
                         std::vector<std::pair<uint32_t, uint32_t>> contrib;
                         if (br.read(1)) {
                             for (uint32_t bi = 0; bi < R.bands.size(); ++bi) {
@@ -4366,10 +4424,19 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                             }
                         }
                         br.align();
+                        if (TPt.packed) {
+                            hpos = br.off;
+                            if (hpos > HS.len) throw GkError("corrupt packed packet headers");
+                            if (P.p.sop_eph & 4) {   // EPH after the header, in the packed headers
+                                if (HS.len - hpos < 2 || HS.be16(hpos) != 0xff92) throw GkError("expected EPH marker");
+                                hpos += 2;
+                            }
+                        } else {
                         pos = br.off;
                         if (P.p.sop_eph & 4) {   // EPH after the header (:469-486)
                             if (tile_end - pos < 2 || BS.be16(pos) != 0xff92) throw GkError("expected EPH marker");
                             pos += 2;
+                        }
                         }
                         for (auto& ct : contrib) {
                             const uint32_t n = (uint32_t)std::min<size_t>(ct.second, tile_end > pos ? tile_end - pos : 0);

@@ -117,6 +117,11 @@ struct Params {
     // samples the canvas at multiples of (sx(c), sy(c)), its tile-components are the tiles'
     // rectangles divided by them, rounded up (TileProcessor.cpp:116-131)
     std::vector<uint32_t> cdx, cdy;
+    // packed packet headers (A.7.4 / A.7.5): 1 = PPT (each tile's headers in its tile-part
+    // header), 2 = PPM (every tile's in the main header); the packets then carry their bodies only.
+    // Grok's encoder writes neither; they are third-party streams its decoder reads
+    // (CodeStreamDecompress read_ppm / read_ppt, T2Decompress.cpp:255-270)
+    uint32_t ppx = 0;
     uint32_t sx(uint32_t c) const { return c < cdx.size() ? cdx[c] : 1u; }
     uint32_t sy(uint32_t c) const { return c < cdy.size() ? cdy[c] : 1u; }
     bool subsampled() const {
@@ -1595,7 +1600,8 @@ struct PrecTrees { std::vector<TagTree> incl, imsb; };
 // sop_eph: Scod's SOP (2) / EPH (4) bits; pkt: the packet's index in its tile (SOP's Nsop,
 // tile->numProcessedPackets, T2Compress.cpp:286-320)
 static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t layno, PrecTrees& T,
-                         uint64_t* budget, uint32_t sop_eph = 0, uint32_t pkt = 0, uint64_t* counted_bytes = nullptr) {
+                         uint64_t* budget, uint32_t sop_eph = 0, uint32_t pkt = 0, uint64_t* counted_bytes = nullptr,
+                         std::vector<uint8_t>* ho = nullptr) {   // ho: the header (+ EPH) goes there (PPT / PPM)
     if (layno == 0) {
         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
             Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
@@ -1684,8 +1690,9 @@ static bool write_packet(std::vector<uint8_t>* o, Res& R, uint32_t pi, uint32_t 
         if (sop_eph & 2) {   // SOP: FF91, Lsop 4, Nsop = packet index mod 2^16
             put16(*o, 0xff91); put16(*o, 4); put16(*o, pkt & 0xffff);
         }
-        o->insert(o->end(), hdr.begin(), hdr.end());
-        if (sop_eph & 4) put16(*o, 0xff92);   // EPH
+        std::vector<uint8_t>& hd = ho ? *ho : *o;
+        hd.insert(hd.end(), hdr.begin(), hdr.end());
+        if (sop_eph & 4) put16(hd, 0xff92);   // EPH
     }
     for (size_t bi = 0; bi < R.bands.size(); ++bi) {   // packet body
         Band& B = R.bands[bi]; Precinct& P = B.prcs[pi];
@@ -2093,6 +2100,7 @@ typedef struct {
     // component subsampling (grk_image_comp::dx / dy), first nsub components (others 1)
     uint32_t nsub;
     uint32_t sub_dx[16], sub_dy[16];
+    uint32_t ppx;          // packed packet headers: 1 PPT, 2 PPM (Params::ppx)
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -2131,6 +2139,7 @@ static Params to_params(const orc_cparams* cp) {
     for (uint32_t c = 0; c < cp->nq && c < 16; ++c) { p.comp_gb.push_back(cp->comp_gb[c]); p.comp_qshift.push_back(cp->comp_qshift[c]); }
     p.qderived = cp->qderived != 0;
     for (uint32_t c = 0; c < cp->nsub && c < 16; ++c) { p.cdx.push_back(std::max(1u, cp->sub_dx[c])); p.cdy.push_back(std::max(1u, cp->sub_dy[c])); }
+    p.ppx = cp->ppx;
     return p;
 }
 
@@ -2162,6 +2171,7 @@ struct EncodeState {
     // GrkSimBitIO
     std::vector<uint32_t> sim_lens;
     bool have_sim = false;
+    std::vector<uint8_t> pkt_headers;   // PPT / PPM: the tile's packet headers in packet order
 };
 
 // Rate control is active when any layer has a target rate (TileProcessor.cpp:952-967).
@@ -2518,7 +2528,7 @@ static void tile_packets(EncodeState& E, std::vector<uint8_t>& body, std::vector
         const PktRef& k = order[i];
         size_t before = body.size();
         write_packet(&body, E.comps[k.c].res[k.r], k.pi, k.l, trees[k.c][k.r][k.pi], nullptr, E.p.sop_eph,
-                     poc ? entry[2 * i + 1] : (uint32_t)plens.size());
+                     poc ? entry[2 * i + 1] : (uint32_t)plens.size(), nullptr, E.p.ppx ? &E.pkt_headers : nullptr);
         plens.push_back((uint32_t)(body.size() - before));
         if (pparts) pparts->push_back(poc ? entry[2 * i] : tile_part_of(E.p, E.im.nc, k));
     }
@@ -2589,6 +2599,14 @@ static std::vector<uint32_t> write_tile_part(std::vector<uint8_t>& o, EncodeStat
             }
             write_poc(o, w, E.im.nc);
         }
+        if (E.p.ppx == 1) {   // PPT: the tile's packet headers, Zppt 0, 1, ... of at most 65533 bytes each
+            for (size_t at = 0, z = 0; at < E.pkt_headers.size() || z == 0; ++z) {
+                const size_t n = std::min<size_t>(65532, E.pkt_headers.size() - at);
+                put16(o, 0xff61); put16(o, (uint32_t)(3 + n)); o.push_back((uint8_t)z);
+                o.insert(o.end(), E.pkt_headers.begin() + at, E.pkt_headers.begin() + at + n);
+                at += n;
+            }
+        }
         if (E.p.plt && part == 0) {
             std::vector<uint8_t> v;
             for (uint32_t L : plt) {
@@ -2627,6 +2645,9 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
     uint32_t nt = 0;
     const Params p0 = to_params(cp);
     if (!prc_exps_ok(p0) || !pocs_cover(p0, nc) || num_parts(p0, nc) < 1) return 0;
+    // packed packet headers: one tile part per tile, no rate control or PLT (test streams)
+    if (p0.ppx && (num_parts(p0, nc) != 1 || needs_rate_control(p0) || p0.plt)) return 0;
+    std::vector<std::vector<uint8_t>> ppm_tiles;   // PPM: each tile's packet headers
     if (!needs_rate_control(p0) && tile_count(p0, w, h) > 1) {
         // independent tiles coded in parallel, written in tile order
         nt = tile_count(p0, w, h);
@@ -2644,12 +2665,14 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
         }
         std::vector<std::vector<uint8_t>> parts(nt);
         std::vector<std::vector<uint32_t>> psl(nt);
+        ppm_tiles.assign(nt, {});
         par_for(nt, [&](size_t t) {
             EncodeState E;
             prepare_encode(E, planes, w, h, nc, prec, sgnd, cp, (uint32_t)t);
             t1_encode_all(E);
             rate_allocate(E);
             psl[t] = write_tile_part(parts[t], E);
+            ppm_tiles[t].swap(E.pkt_headers);
         });
         for (uint32_t t = 0; t < nt; ++t) {
             for (size_t k = 0; p0.tlm && k < psl[t].size(); ++k) {
@@ -2681,6 +2704,7 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
         t1_encode_all(E);
         rate_allocate(E);
         const std::vector<uint32_t> psl = write_tile_part(o, E);
+        ppm_tiles.push_back(std::move(E.pkt_headers));
         for (size_t k = 0; E.p.tlm && k < psl.size(); ++k) {
             const uint32_t psot = psl[k];
             size_t q = tlm_pos + (size_t)6 * (t * psl.size() + k);
@@ -2689,6 +2713,22 @@ size_t orc_encode(const int32_t* planes, uint32_t w, uint32_t h, uint32_t nc, ui
         }
         if (t + 1 >= nt) { put16(o, 0xffd9); break; }
     }
+    }
+    if (p0.ppx == 2) {
+        // PPM in the main header, before the first SOT: Nppm (4 bytes) + the headers of each tile
+        // part in codestream order (one per tile here), split over markers of Zppm 0, 1, ...
+        std::vector<uint8_t> v, m;
+        for (const auto& t : ppm_tiles) { put32(v, (uint32_t)t.size()); v.insert(v.end(), t.begin(), t.end()); }
+        for (size_t at = 0, z = 0; at < v.size(); ++z) {
+            if (z > 255) return 0;
+            const size_t n = std::min<size_t>(65532, v.size() - at);
+            put16(m, 0xff60); put16(m, (uint32_t)(3 + n)); m.push_back((uint8_t)z);
+            m.insert(m.end(), v.begin() + at, v.begin() + at + n);
+            at += n;
+        }
+        size_t sot = 2;
+        while (get16(o.data() + sot) != 0xff90) sot += 2 + get16(o.data() + sot + 2);
+        o.insert(o.begin() + sot, m.begin(), m.end());
     }
     std::vector<uint8_t> J;
     if (cp && cp->cod_format == 2) jp2_prefix(J, w, h, nc, prec, sgnd, o.size());
@@ -2891,8 +2931,9 @@ void orc_t1_decode_cblk(const uint8_t* data, uint32_t len, uint32_t npasses, uin
 // packet sequence continues across its parts, A.4.2)
 static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, size_t>>& ranges, const Params& p,
                        const std::vector<Params>& pcs, const Image& im, const std::vector<Quant>& cq, uint32_t tile,
-                       int32_t* out, const std::vector<PocE>* tpocs = nullptr) {
+                       int32_t* out, const std::vector<PocE>* tpocs = nullptr, const std::vector<uint8_t>* hdr = nullptr) {
     size_t data = ranges[0].first, tile_end = ranges[0].second, next_range = 1;
+    size_t hpos = 0;   // read position in the packed packet headers (hdr: PPM / PPT)
     uint32_t tx0, ty0, tx1, ty1;
     tile_rect(p, im.w, im.h, tile, tx0, ty0, tx1, ty1);
     const uint32_t nlayers = p.nlayers;
@@ -2945,7 +2986,11 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
                         pos += 6;
                     }
                     ++npkt;
-                    BitReader br; br.p = cs + pos; br.len = tile_end - pos;
+                    // the header from the packed headers (PPM / PPT) when the stream has them, else
+                    // in front of the body (T2Decompress.cpp:255-270)
+                    BitReader br;
+                    if (hdr) { br.p = hdr->data() + hpos; br.len = hdr->size() - hpos; }
+                    else { br.p = cs + pos; br.len = tile_end - pos; }
                     std::vector<std::pair<Cblk*, uint32_t>> contrib;  // block, bytes in this packet
                     if (br.read(1)) {
                         for (size_t bi = 0; bi < R.bands.size(); ++bi) {
@@ -2990,10 +3035,19 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
                         }
                     }
                     br.align();
+                    if (hdr) {
+                        hpos += br.off;
+                        if (hpos > hdr->size()) return -5;
+                        if (p.sop_eph & 4) {   // EPH after the header, in the packed headers
+                            if (hdr->size() - hpos < 2 || (*hdr)[hpos] != 0xff || (*hdr)[hpos + 1] != 0x92) return -5;
+                            hpos += 2;
+                        }
+                    } else {
                     pos += br.off;
                     if (p.sop_eph & 4) {   // EPH after the header (:469-486)
                         if (tile_end - pos < 2 || cs[pos] != 0xff || cs[pos + 1] != 0x92) return -5;
                         pos += 2;
+                    }
                     }
                     for (auto& ct : contrib) {
                         const bool skip = ct.second > 0x7fffffffu;   // skipped layer: ~bytes
@@ -3240,6 +3294,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     std::vector<uint8_t> cod_body, qcd_body;
     std::vector<size_t> coc_qcc;
     std::vector<std::pair<uint32_t, std::vector<uint8_t>>> qccs;   // main-header QCC: (component, Sqcc + SPqcc)
+    std::map<uint32_t, std::vector<uint8_t>> ppm;                   // PPM bodies by Zppm
     while (i + 4 <= len) {
         uint32_t m = get16(cs + i);
         if (m == 0xff90) { first_sot = i; break; }
@@ -3294,6 +3349,9 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             qccs.push_back({c, std::vector<uint8_t>(s + cw, s + L - 2)});
         } else if (m == 0xff53) {
             coc_qcc.push_back(i);
+        } else if (m == 0xff60) {   // PPM (A.7.4): Zppm, then (Nppm, Ippm) runs (PPMMarker::read)
+            if (L < 3) return -2;
+            if (!ppm.emplace(s[0], std::vector<uint8_t>(s + 1, s + L - 2)).second) return -2;   // Zppm read twice
         }
         i += 2 + L;   // CAP, TLM, COM and other main-header markers are skipped
     }
@@ -3346,7 +3404,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     std::fill(out, out + total, 0);
     const uint32_t nt = tile_count(p, im.w, im.h);
     size_t pos = first_sot;
-    struct Part { size_t data, end; uint32_t tile, tpsot; std::vector<PocE> pocs; };
+    struct Part { size_t data, end; uint32_t tile, tpsot; std::vector<PocE> pocs;
+                  std::vector<std::pair<uint32_t, std::vector<uint8_t>>> ppt; };
     std::vector<Part> parts;
     while (pos + 12 <= len && get16(cs + pos) == 0xff90) {
         const uint8_t* s = cs + pos + 4;
@@ -3357,8 +3416,14 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         if (tile_end > len) return -5;
         size_t j = pos + 12;   // tile-part header markers (PLT, POC, ...) until SOD
         std::vector<PocE> tp_pocs;
+        std::vector<std::pair<uint32_t, std::vector<uint8_t>>> tp_ppt;
         while (j + 2 <= tile_end && get16(cs + j) != 0xff93) {
             const uint32_t tm = get16(cs + j);
+            if (tm == 0xff61) {   // PPT (A.7.5): Zppt, Ippt; not with PPM (read_ppt's error)
+                const uint32_t Lp = get16(cs + j + 2);
+                if (Lp < 3 || !ppm.empty()) return -2;
+                tp_ppt.push_back({cs[j + 4], std::vector<uint8_t>(cs + j + 5, cs + j + 2 + Lp)});
+            }
             if (tm == 0xff5f && !read_poc(cs + j + 4, get16(cs + j + 2), im.nc, tp_pocs)) return -5;
             if ((tm == 0xff52 || tm == 0xff53 || tm == 0xff5c || tm == 0xff5d) &&
                 !restates_main(cs + j + 4, get16(cs + j + 2), tm, im.nc, cod_body, qcd_body, qbody, ccod)) return -2;
@@ -3366,7 +3431,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             j += 2 + get16(cs + j + 2);
         }
         if (j + 2 > tile_end) return -5;
-        parts.push_back({j + 2, tile_end, isot, s[6], std::move(tp_pocs)});
+        parts.push_back({j + 2, tile_end, isot, s[6], std::move(tp_pocs), std::move(tp_ppt)});
         pos = tile_end;
     }
     // a tile's parts in order (TPsot 0, 1, ...)
@@ -3388,8 +3453,42 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         if (tl.size() > 33) return -5;   // GRK_J2K_MAXRLVLS progressions (read_poc :1173-1178)
         ranges[slot[q.tile]].push_back({q.data, q.end});
     }
+    // packed packet headers per tile: PPT markers of the tile's parts in Zppt order (merge_ppt, one
+    // index space per tile), or PPM's Nppm runs, the k-th taken by tile k (T2Decompress.cpp:257-266
+    // indexes m_tile_packet_headers by tile: kept to one tile part per tile here)
+    std::vector<std::vector<uint8_t>> hdrs(tiles.size());
+    std::vector<uint8_t> has_hdr(tiles.size(), 0);
+    if (!ppm.empty()) {
+        std::vector<uint8_t> v;
+        for (auto& kv : ppm) v.insert(v.end(), kv.second.begin(), kv.second.end());
+        std::vector<std::vector<uint8_t>> runs;
+        for (size_t at = 0; at < v.size();) {
+            if (v.size() - at < 4) return -2;
+            const uint32_t n = get32(v.data() + at);
+            at += 4;
+            if (v.size() - at < n) return -2;
+            runs.emplace_back(v.begin() + at, v.begin() + at + n);
+            at += n;
+        }
+        for (size_t q = 0; q < tiles.size(); ++q) {
+            if (ranges[q].size() != 1 || tiles[q] >= runs.size()) return -2;
+            hdrs[q] = runs[tiles[q]]; has_hdr[q] = 1;
+        }
+    }
+    for (const Part& pt : parts)
+        if (!pt.ppt.empty()) has_hdr[(size_t)slot[pt.tile]] = 1;
+    for (size_t q = 0; q < tiles.size(); ++q) {
+        if (!has_hdr[q] || !ppm.empty()) continue;
+        std::map<uint32_t, std::vector<uint8_t>> z;
+        for (const Part& pt : parts)
+            if (pt.tile == tiles[q])
+                for (const auto& e : pt.ppt) if (!z.emplace(e.first, e.second).second) return -2;   // Zppt read twice
+        for (auto& kv : z) hdrs[q].insert(hdrs[q].end(), kv.second.begin(), kv.second.end());
+    }
     std::vector<int> rcs(tiles.size(), 0);   // tiles write disjoint rectangles of out
-    par_for(tiles.size(), [&](size_t q) { rcs[q] = decode_tile(cs, ranges[q], p, pcs, im, cq, tiles[q], out, &tpocs[q]); });
+    par_for(tiles.size(), [&](size_t q) {
+        rcs[q] = decode_tile(cs, ranges[q], p, pcs, im, cq, tiles[q], out, &tpocs[q], has_hdr[q] ? &hdrs[q] : nullptr);
+    });
     for (int rc : rcs) if (rc) return rc;
     return 0;
 }

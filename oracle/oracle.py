@@ -32,6 +32,7 @@ class CParams(ctypes.Structure):
         ("nq", ctypes.c_uint32), ("comp_gb", ctypes.c_uint32 * 16), ("comp_qshift", ctypes.c_int32 * 16),
         ("qderived", ctypes.c_uint32),
         ("nsub", ctypes.c_uint32), ("sub_dx", ctypes.c_uint32 * 16), ("sub_dy", ctypes.c_uint32 * 16),
+        ("ppx", ctypes.c_uint32),
     ]
 
 
@@ -108,7 +109,7 @@ def get_threads():
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
            layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None, roi=None,
            sop=False, eph=False, quality=None, origin=None, tile_origin=None, comp_guard_bits=None, comp_qshift=None,
-           qderived=False, subsampling=None):
+           qderived=False, subsampling=None, packed_headers=None):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -151,6 +152,8 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
         p.nsub = len(subsampling)
         for c, (dx, dy) in enumerate(subsampling):
             p.sub_dx[c], p.sub_dy[c] = int(dx), int(dy)
+    # packed packet headers: "ppt" (tile-part headers) or "ppm" (main header); test streams only
+    p.ppx = {None: 0, "ppt": 1, "ppm": 2}[packed_headers]
     p.cod_format = 2 if jp2 else 0
     if layer_rate:
         p.nlayers = len(layer_rate)
