@@ -3855,6 +3855,9 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             W.p.sop_eph = scod & 6;
             W.p.nlayers = S.be16(s + 2);
             W.p.mct = S.at(s + 4);
+            // SGcod MCT: 0 none, 1 RCT / ICT; 2 = a Part-2 array transform (MCT / MCC / MCO markers,
+            // Grok's decompress_custom), not on this path
+            if (W.p.mct > 1) throw GkError("Part-2 array multiple-component transforms are not supported on this path");
             W.p.numres = S.at(s + 5) + 1;
             // at most 32 decomposition levels (CodeStreamDecompress.cpp:1733)
             if (W.p.numres > GK_MAXRLVLS) throw GkError("corrupt COD marker (more than 32 decomposition levels)");
@@ -3914,6 +3917,10 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             qcc.push_back({c, std::vector<uint8_t>(b.begin() + cw, b.end())});
         } else if (m == 0xff53) {
             coc_qcc.push_back(i);
+        } else if (m == 0xff72 || m == 0xff73 || (m >= 0xff74 && m <= 0xff79)) {
+            // Part-2 extensions (DFS, ADS, MCT, MCC, NLT, MCO, CBD, ATK: ISO 15444-2 A.2) change
+            // how the stream decodes; refused rather than ignored
+            throw GkError("Part-2 (ISO 15444-2) extension markers are not supported on this path");
         } else if (m == 0xff60) {   // PPM (A.7.4): Zppm, then (Nppm, Ippm) runs
             if (L < 3) throw GkError("corrupt PPM marker");
             if (!Hd.ppm.emplace(S.at(s), marker_body(S, s + 1, L - 1)).second) throw GkError("PPM: Zppm read twice");

@@ -3321,6 +3321,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             cod_body.assign(s, s + L - 2);
             p.sop_eph = scod & 6;
             p.nlayers = get16(s + 2); p.mct = s[4];
+            if (p.mct > 1) return -2;   // Part-2 array MCT (decompress_custom): not restated
             p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
             p.cblk_sty = s[8];
             if (s[1] > 4) return -2;                                 // progression order
@@ -3349,6 +3350,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             qccs.push_back({c, std::vector<uint8_t>(s + cw, s + L - 2)});
         } else if (m == 0xff53) {
             coc_qcc.push_back(i);
+        } else if (m == 0xff72 || m == 0xff73 || (m >= 0xff74 && m <= 0xff79)) {
+            return -2;   // Part-2 extension markers (ISO 15444-2 A.2): not restated
         } else if (m == 0xff60) {   // PPM (A.7.4): Zppm, then (Nppm, Ippm) runs (PPMMarker::read)
             if (L < 3) return -2;
             if (!ppm.emplace(s[0], std::vector<uint8_t>(s + 1, s + L - 2)).second) return -2;   // Zppm read twice

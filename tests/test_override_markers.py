@@ -73,3 +73,27 @@ def test_main_qcc_applies_to_its_component(name):
         np.testing.assert_array_equal(got, fx.grok_decoded)
     else:
         assert not np.array_equal(got, fx.grok_decoded)
+
+
+@pytest.mark.parametrize("marker", [0xFF74, 0xFF75, 0xFF77, 0xFF78, 0xFF79])
+def test_part2_markers_refused(marker):
+    # Part-2 extensions (MCT / MCC / MCO / CBD / ATK) change the decode; refused rather than ignored
+    fx = _fx("rgb8_tiles_xl")
+    cs = J.insert_main(fx.cs, bytes([marker >> 8, marker & 0xFF, 0, 4, 0, 0]))
+    with pytest.raises(RuntimeError, match="failed: -2"):
+        O.decode(cs)
+    import grok_amd as G
+    with pytest.raises(ValueError, match="Part-2"):
+        G.probe_header(cs)
+
+
+def test_part2_array_mct_refused():
+    fx = _fx("rgb8_tiles_xl")
+    cs = bytearray(fx.cs)
+    cod = cs.index(b"\xff\x52")
+    cs[cod + 4 + 4] = 2   # SGcod MCT = 2: a Part-2 array transform
+    with pytest.raises(RuntimeError, match="failed: -2"):
+        O.decode(bytes(cs))
+    import grok_amd as G
+    with pytest.raises(ValueError, match="Part-2"):
+        G.probe_header(bytes(cs))
