@@ -24,7 +24,7 @@ GK_MAX_LAYERS = 100
 EXPORTS = ("gk_create", "gk_destroy", "gk_set_default_params", "gk_encode", "gk_encode_tiles", "gk_main_header",
            "gk_jp2_header", "gk_decode_header", "gk_probe_header", "gk_decode", "gk_decode_window", "gk_get_timings",
            "gk_last_error", "gk_version", "gk_set_decode_layers", "gk_set_decode_reduce",
-           "gk_set_window_rule", "gk_set_subsampling", "gk_probe_components", "gk_header_subsampling")
+           "gk_set_window_rule", "gk_set_subsampling", "gk_probe_components", "gk_header_components")
 
 
 class Poc(ctypes.Structure):
@@ -118,10 +118,9 @@ def load_library(build_if_missing=True):
     lib.gk_set_subsampling.restype = ctypes.c_int
     lib.gk_set_subsampling.argtypes = [ctypes.c_void_p, ctypes.c_uint32, P(ctypes.c_uint32), P(ctypes.c_uint32)]
     lib.gk_probe_components.restype = ctypes.c_int
-    lib.gk_probe_components.argtypes = [ctypes.c_void_p, ctypes.c_size_t, P(ctypes.c_uint32), P(ctypes.c_uint32),
-                                        ctypes.c_uint32]
-    lib.gk_header_subsampling.restype = ctypes.c_int
-    lib.gk_header_subsampling.argtypes = [ctypes.c_void_p, P(ctypes.c_uint32), P(ctypes.c_uint32), ctypes.c_uint32]
+    lib.gk_probe_components.argtypes = [ctypes.c_void_p, ctypes.c_size_t] + [P(ctypes.c_uint32)] * 4 + [ctypes.c_uint32]
+    lib.gk_header_components.restype = ctypes.c_int
+    lib.gk_header_components.argtypes = [ctypes.c_void_p] + [P(ctypes.c_uint32)] * 4 + [ctypes.c_uint32]
     lib.gk_set_decode_layers.restype = ctypes.c_int
     lib.gk_set_decode_layers.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
     lib.gk_decode.restype = ctypes.c_int
@@ -204,14 +203,17 @@ def probe_header(cs):
     return info
 
 
-def probe_components(cs):
-    """gk_probe_components: [(dx, dy)] per component of host codestream / JP2 bytes (SIZ XRsiz / YRsiz)."""
+def probe_components(cs, precision=False):
+    """gk_probe_components: [(dx, dy)] per component of host codestream / JP2 bytes (SIZ XRsiz /
+    YRsiz); with precision=True [(dx, dy, prec, signed)]."""
     lib = load_library()
     b = np.frombuffer(bytes(cs), np.uint8)
-    dx, dy = (ctypes.c_uint32 * 16384)(), (ctypes.c_uint32 * 16384)()
-    n = lib.gk_probe_components(b.ctypes.data, len(b), dx, dy, 16384)
+    dx, dy, pr, sg = [(ctypes.c_uint32 * 16384)() for _ in range(4)]
+    n = lib.gk_probe_components(b.ctypes.data, len(b), dx, dy, pr, sg, 16384)
     if n < 0:
         raise ValueError("gk_probe_components failed")
+    if precision:
+        return [(dx[c], dy[c], pr[c], bool(sg[c])) for c in range(n)]
     return [(dx[c], dy[c]) for c in range(n)]
 
 
@@ -375,7 +377,7 @@ class Engine:
     def subsampling(self):
         """[(dx, dy)] per component of the stream the last read_header / decode read."""
         dx, dy = (ctypes.c_uint32 * 16384)(), (ctypes.c_uint32 * 16384)()
-        n = self.lib.gk_header_subsampling(self.ctx, dx, dy, 16384)
+        n = self.lib.gk_header_components(self.ctx, dx, dy, None, None, 16384)
         return [(dx[c], dy[c]) for c in range(max(n, 0))]
 
     def _planes_ptrs(self, planes, row0=0, prec=32):

@@ -331,6 +331,11 @@ struct SGroup {
 struct Plan {
     uint32_t w = 0, h = 0, nc = 0, prec = 0, sgnd = 0;
     std::vector<uint8_t> cdx, cdy;       // per component subsampling (empty: none)
+    // decode: per-component precision and signedness (SIZ Ssiz) when they differ (empty: prec /
+    // sgnd for every component; prec is then the largest)
+    std::vector<uint8_t> cprec, csgnd;
+    uint32_t c_prec(uint32_t c) const { return c < cprec.size() ? cprec[c] : prec; }
+    uint32_t c_sgnd(uint32_t c) const { return c < csgnd.size() ? csgnd[c] : sgnd; }
     uint32_t sx(uint32_t c) const { return c < cdx.size() ? cdx[c] : 1u; }
     uint32_t sy(uint32_t c) const { return c < cdy.size() ? cdy[c] : 1u; }
     bool subsampled() const {
@@ -524,8 +529,9 @@ static void apply_qcd(Plan& P, const QuantList& q) {
                 B.expn = q[k].first; B.mant = q[k].second;
                 uint32_t lg_enc = B.orient == 0 ? 0 : (B.orient == 3 ? 2 : 1);
                 uint32_t lg_dec = P.p.c_irrev(ci) ? 0 : lg_enc;
-                B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_enc) - (int)B.expn));
-                B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(P.prec + lg_dec) - (int)B.expn));
+                const uint32_t prec = P.c_prec(ci);   // (R_b = the component's precision + gain, Quantizer.cpp:40-42)
+                B.step_enc = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(prec + lg_enc) - (int)B.expn));
+                B.step_dec = (float)((1.0 + B.mant / 2048.0) * pow(2.0, (int)(prec + lg_dec) - (int)B.expn));
                 B.numbps = P.p.roi(ci) + (uint32_t)std::max(0, (int)B.expn + (int)gb - 1);
                 ++bandno;
             }
@@ -2590,7 +2596,7 @@ struct gk_ctx {
     bool blocks_uploaded = false;
     uint32_t enc_b0 = 0, enc_b1 = 0;   // block range of the uploaded encode table
     std::vector<uint8_t> enc_dx, enc_dy;   // gk_set_subsampling: the next encodes' component subsampling
-    std::vector<uint32_t> hdr_dx, hdr_dy;  // the last gk_decode_header's component subsampling
+    std::vector<uint32_t> hdr_dx, hdr_dy, hdr_prec, hdr_sgnd;   // the last gk_decode_header's components
     bool enc_rc = false;                // its rate-control flag (GkBlock::flags bit 1)
     // band quantisation held by the cached plan's bands: the plan's own (encoder, native_qcd)
     // or that of the last decoded stream (band_qcd)
@@ -2700,6 +2706,7 @@ static std::string plan_key(const Plan& P) {
     std::string k(buf);
     if (P.subsampled())
         for (uint32_t c = 0; c < P.nc; ++c) k += " s" + std::to_string(P.sx(c)) + "x" + std::to_string(P.sy(c));
+    for (size_t c = 0; c < P.cprec.size(); ++c) k += " p" + std::to_string(P.cprec[c]) + (P.csgnd[c] ? "s" : "u");
     k += " sty" + std::to_string(P.p.cblk_sty) + " t" + std::to_string(P.p.tw) + "x" + std::to_string(P.p.th);
     k += " o" + std::to_string(P.x0) + "," + std::to_string(P.y0) + "," + std::to_string(P.gx0) + "," + std::to_string(P.gy0);
     for (size_t c = 0; c < P.p.roishift.size(); ++c)   // non-zero (component, shift) pairs only
@@ -2749,7 +2756,7 @@ struct L1Io {
     bool mct3 = false;
     std::vector<const void*> planes;     // component c's plane at its output rectangle's origin
     std::vector<uint32_t> strides;
-    int32_t shift = 0, mn = 0, mx = 0;
+    std::vector<int32_t> shift, mn, mx;  // per component: DC shift, clamp range (its precision)
     uint32_t cx0 = 0, cy0 = 0, cx1 = 0, cy1 = 0;   // inverse: the output rectangle on the canvas
 };
 
@@ -2830,18 +2837,18 @@ static void run_dwt(gk_ctx* ctx, const Region& RG, bool forward, uint32_t jb = 0
                         if (irrev)
                             gk_launch_dwt97_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c],
                                                    reinterpret_cast<float*>(dl), cst, RG.stride, w, h, S.tb,
-                                                   io->shift);
+                                                   io->shift[c]);
                         else
                             gk_launch_dwt53_fwd_l1(ctx->st, io->stype, nc, pp, io->strides[c], dl, cst,
-                                                   RG.stride, w, h, S.tb, io->shift);
+                                                   RG.stride, w, h, S.tb, io->shift[c]);
                     } else {
                         if (irrev)
                             gk_launch_dwt97_inv_l1(ctx->st, io->stype, nc, reinterpret_cast<const float*>(dl),
-                                                   cst, RG.stride, pp, io->strides[c], win, w, h, S.tb, io->shift,
-                                                   io->mn, io->mx);
+                                                   cst, RG.stride, pp, io->strides[c], win, w, h, S.tb, io->shift[c],
+                                                   io->mn[c], io->mx[c]);
                         else
                             gk_launch_dwt53_inv_l1(ctx->st, io->stype, nc, dl, cst, RG.stride, pp,
-                                                   io->strides[c], win, w, h, S.tb, io->shift, io->mn, io->mx);
+                                                   io->strides[c], win, w, h, S.tb, io->shift[c], io->mn[c], io->mx[c]);
                     }
                     ctx->tm.dwt_launches++;
                     ctx->tm.dwt_bytes += area * (4 + es) * nc;
@@ -3053,7 +3060,7 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     // then they run first and level 1 takes the parity-general kernels)
     const bool fused = P.p.numres > 1 && P.l1_fusable;
     if (fused) {
-        io.stype = stype; io.mct3 = mct3; io.shift = shift;
+        io.stype = stype; io.mct3 = mct3; io.shift.assign(P.nc, shift);
         io.planes.assign(src.begin(), src.end());
         io.strides = sstr;
     } else {
@@ -3842,10 +3849,20 @@ static void parse_header(ByteSrc& S, Header& Hd) {
                 // XRsiz / YRsiz: 1..255 (read_siz)
                 W.cdx[c] = S.at(s + 37 + 3 * c); W.cdy[c] = S.at(s + 38 + 3 * c);
                 if (!W.cdx[c] || !W.cdy[c]) throw GkError("corrupt SIZ marker (component subsampling 0)");
-                if (((S.at(s + 36 + 3 * c) & 0x7f) + 1) != W.prec) throw GkError("mixed component precision not supported");
-                if ((S.at(s + 36 + 3 * c) >> 7) != W.sgnd) throw GkError("mixed component signedness not supported");
             }
             if (!W.subsampled()) { W.cdx.clear(); W.cdy.clear(); }
+            // Ssiz per component: precisions / signs may differ (each component DC-shifted and
+            // clamped by its own, Quantizer steps from its own); prec becomes the largest
+            W.cprec.assign(W.nc, 0); W.csgnd.assign(W.nc, 0);
+            bool mixed = false;
+            for (uint32_t c = 0; c < W.nc; ++c) {
+                const uint32_t v = S.at(s + 36 + 3 * c);
+                W.cprec[c] = (uint8_t)((v & 0x7f) + 1); W.csgnd[c] = (uint8_t)(v >> 7);
+                if (W.cprec[c] > 31) throw GkError("component precision > 31 bits not supported");
+                mixed = mixed || W.cprec[c] != W.prec || W.csgnd[c] != W.sgnd;
+                W.prec = std::max<uint32_t>(W.prec, W.cprec[c]);
+            }
+            if (!mixed) { W.cprec.clear(); W.csgnd.clear(); }
             have_siz = true;
         } else if (m == 0xff52) {
             if (L < 12) throw GkError("corrupt COD marker");
@@ -3953,6 +3970,9 @@ static void parse_header(ByteSrc& S, Header& Hd) {
         if (W.p.mct && W.nc >= 3 && (W.p.cc[1].irrev != W.p.cc[0].irrev || W.p.cc[2].irrev != W.p.cc[0].irrev))
             throw GkError("MCT over components with different transforms is not supported");
     }
+    if (W.p.mct && W.nc >= 3 && (W.c_prec(1) != W.c_prec(0) || W.c_prec(2) != W.c_prec(0) ||
+                                 W.c_sgnd(1) != W.c_sgnd(0) || W.c_sgnd(2) != W.c_sgnd(0)))
+        throw GkError("MCT over components of different precisions or signs is not supported on this path");
     Hd.qcd.clear();
     for (uint32_t c = 0; c < W.nc; ++c) parse_quant(Hd.qbody[c], W.p.c_numres(c), Hd.qcd);
     // tile parts: SOT (Isot, Psot, TPsot, TNsot), tile-part header markers (PLT, ...), SOD, packets
@@ -4887,9 +4907,18 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     HIPCHK(hipEventRecord(ctx->ev[3], st));
     // ---- inverse DWT; its last level writes the output region through the inverse MCT + DC
     // shift + clamp into the output planes (without decomposition levels a separate pass does)
-    int32_t shift = P.sgnd ? 0 : (1 << (P.prec - 1));
-    int32_t mn = P.sgnd ? -(1 << (P.prec - 1)) : 0;
-    int32_t mx = P.sgnd ? (1 << (P.prec - 1)) - 1 : (int32_t)((1u << P.prec) - 1);
+    // DC shift and clamp per component (its precision and sign: mct::decompress_dc_shift_* per
+    // component); 8 / 16-bit output takes the largest precision and one sign
+    std::vector<int32_t> shiftv(P.nc), mnv(P.nc), mxv(P.nc);
+    for (uint32_t c = 0; c < P.nc; ++c) {
+        const uint32_t pr = P.c_prec(c);
+        const bool sg = P.c_sgnd(c) != 0;
+        shiftv[c] = sg ? 0 : (1 << (pr - 1));
+        mnv[c] = sg ? -(1 << (pr - 1)) : 0;
+        mxv[c] = sg ? (1 << (pr - 1)) - 1 : (int32_t)((1u << pr) - 1);
+        if ((sample_bytes == 1 || sample_bytes == 2) && sg != (P.sgnd != 0))
+            throw GkError("8 / 16-bit output of components with different signs: use int32 planes");
+    }
     const int stype = sample_type(sample_bytes, P.prec, P.sgnd != 0);
     const size_t es = gk_sample_size(stype);
     const bool mct3r = P.mct3();
@@ -4966,12 +4995,12 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
                     auto dst = [&](uint32_t k) { return qd[k] + ((size_t)(iy0 - qy0[k]) * qs[k] + (ix0 - qx0[k])) * es; };
                     if (!P.p.c_irrev(c)) {
                         if (m3) gk_launch_rct_inv_dc(st, src(0), src(1), src(2), RG.stride, stype, dst(0), dst(1), dst(2), qs[0],
-                                                     tw, th, shift, mn, mx);
-                        else gk_launch_dc_inv(st, src(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
+                                                     tw, th, shiftv[c], mnv[c], mxv[c]);
+                        else gk_launch_dc_inv(st, src(c), RG.stride, stype, dst(c), qs[c], tw, th, shiftv[c], mnv[c], mxv[c]);
                     } else {
                         if (m3) gk_launch_ict_inv_dc(st, srcf(0), srcf(1), srcf(2), RG.stride, stype, dst(0), dst(1), dst(2),
-                                                     qs[0], tw, th, shift, mn, mx);
-                        else gk_launch_dc_inv_f(st, srcf(c), RG.stride, stype, dst(c), qs[c], tw, th, shift, mn, mx);
+                                                     qs[0], tw, th, shiftv[c], mnv[c], mxv[c]);
+                        else gk_launch_dc_inv_f(st, srcf(c), RG.stride, stype, dst(c), qs[c], tw, th, shiftv[c], mnv[c], mxv[c]);
                     }
                     c += cn;
                 }
@@ -5034,7 +5063,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     }
     if (P.max_numres() > 1 && P.l1_fusable) {
         L1Io io;
-        io.stype = stype; io.mct3 = mct3; io.shift = shift; io.mn = mn; io.mx = mx;
+        io.stype = stype; io.mct3 = mct3; io.shift = shiftv; io.mn = mnv; io.mx = mxv;
         io.planes.assign(dst.begin(), dst.end());
         io.strides = dstr;
         io.cx0 = rx0 + P.x0; io.cy0 = ry0 + P.y0; io.cx1 = rx1 + P.x0; io.cy1 = ry1 + P.y0;
@@ -5048,13 +5077,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         HIPCHK(hipEventRecord(ctx->ev[4], st));
         if (mct3 && !P.p.c_irrev(0))
             gk_launch_rct_inv_dc(st, planeA(0), planeA(1), planeA(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
-                                 ocols(0), orows(0), shift, mn, mx);
+                                 ocols(0), orows(0), shiftv[0], mnv[0], mxv[0]);
         if (mct3 && P.p.c_irrev(0))
             gk_launch_ict_inv_dc(st, planeAf(0), planeAf(1), planeAf(2), RG.stride, stype, dst[0], dst[1], dst[2], dstr[0],
-                                 ocols(0), orows(0), shift, mn, mx);
+                                 ocols(0), orows(0), shiftv[0], mnv[0], mxv[0]);
         for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) {
-            if (!P.p.c_irrev(c)) gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shift, mn, mx);
-            else gk_launch_dc_inv_f(st, planeAf(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shift, mn, mx);
+            if (!P.p.c_irrev(c)) gk_launch_dc_inv(st, planeA(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shiftv[c], mnv[c], mxv[c]);
+            else gk_launch_dc_inv_f(st, planeAf(c), RG.stride, stype, dst[c], dstr[c], ocols(c), orows(c), shiftv[c], mnv[c], mxv[c]);
         }
     }
     launch_check(__LINE__);
@@ -5256,7 +5285,11 @@ int gk_decode_header(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_devic
         info->w = Hd.want.w; info->h = Hd.want.h; info->numcomps = Hd.want.nc; info->prec = Hd.want.prec;
         info->sgnd = Hd.want.sgnd; info->x0 = Hd.want.x0; info->y0 = Hd.want.y0;
         ctx->hdr_dx.assign(Hd.want.nc, 1); ctx->hdr_dy.assign(Hd.want.nc, 1);
-        for (uint32_t c = 0; c < Hd.want.nc; ++c) { ctx->hdr_dx[c] = Hd.want.sx(c); ctx->hdr_dy[c] = Hd.want.sy(c); }
+        ctx->hdr_prec.assign(Hd.want.nc, 0); ctx->hdr_sgnd.assign(Hd.want.nc, 0);
+        for (uint32_t c = 0; c < Hd.want.nc; ++c) {
+            ctx->hdr_dx[c] = Hd.want.sx(c); ctx->hdr_dy[c] = Hd.want.sy(c);
+            ctx->hdr_prec[c] = Hd.want.c_prec(c); ctx->hdr_sgnd[c] = Hd.want.c_sgnd(c);
+        }
         return 0;
     } catch (const GkError& e) {
         ctx->err = e.msg;
@@ -5354,7 +5387,8 @@ int gk_set_subsampling(gk_ctx* ctx, uint32_t numcomps, const uint32_t* dx, const
     return 0;
 }
 
-int gk_probe_components(const uint8_t* cs, size_t len, uint32_t* dx, uint32_t* dy, uint32_t cap) {
+int gk_probe_components(const uint8_t* cs, size_t len, uint32_t* dx, uint32_t* dy, uint32_t* prec, uint32_t* sgnd,
+                        uint32_t cap) {
     if (!cs) return -1;
     try {
         ByteSrc S; S.len = len; S.host = cs;
@@ -5365,6 +5399,8 @@ int gk_probe_components(const uint8_t* cs, size_t len, uint32_t* dx, uint32_t* d
         for (uint32_t c = 0; c < Hd.want.nc && c < cap; ++c) {
             if (dx) dx[c] = Hd.want.sx(c);
             if (dy) dy[c] = Hd.want.sy(c);
+            if (prec) prec[c] = Hd.want.c_prec(c);
+            if (sgnd) sgnd[c] = Hd.want.c_sgnd(c);
         }
         return (int)Hd.want.nc;
     } catch (const GkError&) {
@@ -5372,11 +5408,13 @@ int gk_probe_components(const uint8_t* cs, size_t len, uint32_t* dx, uint32_t* d
     }
 }
 
-int gk_header_subsampling(gk_ctx* ctx, uint32_t* dx, uint32_t* dy, uint32_t cap) {
+int gk_header_components(gk_ctx* ctx, uint32_t* dx, uint32_t* dy, uint32_t* prec, uint32_t* sgnd, uint32_t cap) {
     if (!ctx) return -1;
     for (uint32_t c = 0; c < ctx->hdr_dx.size() && c < cap; ++c) {
         if (dx) dx[c] = ctx->hdr_dx[c];
         if (dy) dy[c] = ctx->hdr_dy[c];
+        if (prec) prec[c] = ctx->hdr_prec[c];
+        if (sgnd) sgnd[c] = ctx->hdr_sgnd[c];
     }
     return (int)ctx->hdr_dx.size();
 }

@@ -207,6 +207,7 @@ struct CodecObj : Obj {
     ImageObj* out = nullptr;                 // composited image (owned by the codec)
     bool tile_decoded = false;               // grk_decompress_tile cropped `out` to a tile
     std::vector<uint32_t> cdx, cdy;          // the stream's component subsampling (SIZ XRsiz / YRsiz)
+    std::vector<uint32_t> cprec, csgnd;      // and precision / signedness (Ssiz)
     ~CodecObj() override {
         if (stream) grk_object_unref(stream);
         if (image) grk_object_unref(&image->obj);
@@ -333,7 +334,7 @@ ImageObj* region_image(CodecObj* C, uint32_t x0, uint32_t y0, uint32_t x1, uint3
         q.dx = C->cdx[k]; q.dy = C->cdy[k];
         q.x0 = reduced(ceil_div(x0, q.dx), r); q.y0 = reduced(ceil_div(y0, q.dy), r);
         q.w = reduced(ceil_div(x1, q.dx), r) - q.x0; q.h = reduced(ceil_div(y1, q.dy), r) - q.y0;
-        q.prec = (uint8_t)C->info.prec; q.sgnd = C->info.sgnd != 0;
+        q.prec = (uint8_t)C->cprec[k]; q.sgnd = C->csgnd[k] != 0;
     }
     GRK_COLOR_SPACE cs = GRK_CLRSPC_UNKNOWN;
     if (C->coding.cod_format == 2) cs = C->info.numcomps < 3 ? GRK_CLRSPC_GRAY : GRK_CLRSPC_SRGB;
@@ -620,7 +621,9 @@ bool grk_decompress_read_header(grk_codec* codec, grk_header_info* hi) {
             return false;
         }
         C->cdx.assign(C->info.numcomps, 1); C->cdy.assign(C->info.numcomps, 1);
-        if (gk_probe_components(C->data.data(), C->data.size(), C->cdx.data(), C->cdy.data(), C->info.numcomps) < 0) {
+        C->cprec.assign(C->info.numcomps, C->info.prec); C->csgnd.assign(C->info.numcomps, C->info.sgnd);
+        if (gk_probe_components(C->data.data(), C->data.size(), C->cdx.data(), C->cdy.data(), C->cprec.data(),
+                                C->csgnd.data(), C->info.numcomps) < 0) {
             error("cannot read the component subsampling");
             return false;
         }

@@ -189,16 +189,19 @@ int gk_set_decode_reduce(gk_ctx* ctx, uint32_t reduce);
  * only (no gk_encode_tiles). */
 int gk_set_subsampling(gk_ctx* ctx, uint32_t numcomps, const uint32_t* dx, const uint32_t* dy);
 
-/* A stream's component subsampling (SIZ XRsiz / YRsiz) from its header, no device needed: fills
- * dx[c], dy[c] for the first cap components and returns the component count (< 0 on error).
- * gk_decode writes component c into a plane of its own size: the image area divided by (dx, dy)
- * as in gk_set_subsampling, then reduced by cp_reduce (ceil of both edges / 2^reduce).  Windows
- * of subsampled streams are refused. */
-int gk_probe_components(const uint8_t* cs, size_t len, uint32_t* dx, uint32_t* dy, uint32_t cap);
+/* A stream's components from its header, no device needed (SIZ XRsiz / YRsiz / Ssiz): fills dx[c],
+ * dy[c], prec[c], sgnd[c] (any may be NULL) for the first cap components and returns the component
+ * count (< 0 on error).  gk_decode writes component c into a plane of its own size: the image area
+ * divided by (dx, dy) as in gk_set_subsampling, then reduced by cp_reduce (ceil of both edges /
+ * 2^reduce); windows take the window's rectangle on each component's grid.  Components of
+ * different precisions are DC-shifted and clamped each by its own (gk_image_info::prec reports the
+ * largest; 8 / 16-bit output needs one sign). */
+int gk_probe_components(const uint8_t* cs, size_t len, uint32_t* dx, uint32_t* dy, uint32_t* prec, uint32_t* sgnd,
+                        uint32_t cap);
 
-/* The component subsampling of the stream the last gk_decode_header read (host or device bytes):
- * dx[c], dy[c] for the first cap components; returns the component count. */
-int gk_header_subsampling(gk_ctx* ctx, uint32_t* dx, uint32_t* dy, uint32_t cap);
+/* The same for the stream the last gk_decode_header read (host or device bytes); returns the
+ * component count. */
+int gk_header_components(gk_ctx* ctx, uint32_t* dx, uint32_t* dy, uint32_t* prec, uint32_t* sgnd, uint32_t cap);
 
 /* Inverse 5/3 rule of later gk_decode_window calls.  whole_tile = 0 (default): Grok's partial-tile
  * inverse, which a window set through setDecompressWindow selects for every tile

@@ -1247,6 +1247,11 @@ static uint32_t get32(const uint8_t* p) { return (get16(p) << 16) | get16(p + 2)
 
 struct Image {
     uint32_t w, h, nc, prec; bool sgnd;
+    // decode: per-component precision and signedness (SIZ Ssiz; empty = prec / sgnd for all)
+    std::vector<uint32_t> cprec;
+    std::vector<uint8_t> csgnd;
+    uint32_t pr(uint32_t c) const { return c < cprec.size() ? cprec[c] : prec; }
+    bool sg(uint32_t c) const { return c < csgnd.size() ? csgnd[c] != 0 : sgnd; }
 };
 
 // Tile grid (B.3, CodeStreamCompress.cpp:352-363): nominal tile size (tw, th) anchored at the grid
@@ -2946,7 +2951,7 @@ static int decode_tile(const uint8_t* cs, const std::vector<std::pair<size_t, si
         tcx0[c] = ceildiv(tx0, p.sx(c)); tcy0[c] = ceildiv(ty0, p.sy(c));
         tcx1[c] = ceildiv(tx1, p.sx(c)); tcy1[c] = ceildiv(ty1, p.sy(c));
         build_geometry(comps[c], tcx0[c], tcy0[c], tcx1[c], tcy1[c], pcs[c]);
-        assign_steps(comps[c], pcs[c], im.prec, false, &cq[c], 0, p.roi(c));
+        assign_steps(comps[c], pcs[c], im.pr(c), false, &cq[c], 0, p.roi(c));
     }
     // T2 decode (LRCP)
     struct TT { std::vector<TagTree> incl, imsb; };
@@ -3145,8 +3150,11 @@ t2done:
         if (!pcs[c].irreversible) dwt2d<int32_t>(ip[c].data(), C.w, C, pcs[c].numres - red, false, inv53_1d);
         else dwt2d<float>(fp[c].data(), C.w, C, pcs[c].numres - red, false, inv97_1d);
     }
-    int32_t shift = im.sgnd ? 0 : (1 << (im.prec - 1));
-    int32_t mn = im.sgnd ? -(1 << (im.prec - 1)) : 0, mxv = im.sgnd ? (1 << (im.prec - 1)) - 1 : (1 << im.prec) - 1;
+    // DC level shift and clamp per component (its precision and signedness, SIZ Ssiz;
+    // mct::decompress_dc_shift_rev / _irrev per component)
+    auto shift_of = [&](uint32_t c) { return im.sg(c) ? 0 : (1 << (im.pr(c) - 1)); };
+    auto mn_of = [&](uint32_t c) { return im.sg(c) ? -(1 << (im.pr(c) - 1)) : 0; };
+    auto mx_of = [&](uint32_t c) { return im.sg(c) ? (1 << (im.pr(c) - 1)) - 1 : (int32_t)((1u << im.pr(c)) - 1); };
     // component c's reduced area: [ceil(ceil(x0 / XRsiz) / 2^r), ...) on its reduced grid, the
     // output planes back to back (one image-sized plane each without subsampling)
     std::vector<size_t> ooff(im.nc + 1, 0);
@@ -3162,7 +3170,7 @@ t2done:
     auto put = [&](uint32_t c, size_t k, int32_t v) {
         const uint32_t x = (uint32_t)(k % comps[c].w), y = (uint32_t)(k / comps[c].w);
         if (x >= TWr[c] || y >= THr[c]) return;
-        out[ooff[c] + (size_t)(ty0r[c] + y) * Wr[c] + tx0r[c] + x] = std::min(mxv, std::max(mn, v + shift));
+        out[ooff[c] + (size_t)(ty0r[c] + y) * Wr[c] + tx0r[c] + x] = std::min(mx_of(c), std::max(mn_of(c), v + shift_of(c)));
     };
     // the inverse MCT needs the first three tile-components of one size (needsMctDecompress,
     // TileProcessor.cpp:432-456: Grok skips it with a warning otherwise)
@@ -3256,6 +3264,11 @@ static size_t resync_part_end(const uint8_t* cs, size_t len, size_t pos, size_t 
 
 // the (reduced) plane sizes of the last orc_decode's components, (w, h) each; returns the count
 static thread_local std::vector<uint32_t> t_comp_dims;
+static thread_local std::vector<uint32_t> t_comp_prec;   // precision | signed << 8 per component
+uint32_t orc_last_comp_prec(uint32_t* out) {
+    if (out) std::copy(t_comp_prec.begin(), t_comp_prec.end(), out);
+    return (uint32_t)t_comp_prec.size();
+}
 uint32_t orc_last_comp_dims(uint32_t* out) {
     if (out) std::copy(t_comp_dims.begin(), t_comp_dims.end(), out);
     return (uint32_t)(t_comp_dims.size() / 2);
@@ -3311,6 +3324,11 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             im.nc = get16(s + 34);
             if (!im.nc || L < 38 + 3 * im.nc) return -2;
             im.prec = (s[36] & 0x7f) + 1; im.sgnd = (s[36] & 0x80) != 0;
+            im.cprec.assign(im.nc, 0); im.csgnd.assign(im.nc, 0);
+            for (uint32_t c = 0; c < im.nc; ++c) {   // Ssiz per component (1..38 bits; 31 here)
+                im.cprec[c] = (s[36 + 3 * c] & 0x7f) + 1u; im.csgnd[c] = (s[36 + 3 * c] & 0x80) != 0;
+                if (im.cprec[c] > 31) return -2;
+            }
             p.cdx.assign(im.nc, 1); p.cdy.assign(im.nc, 1);
             for (uint32_t c = 0; c < im.nc; ++c) {   // XRsiz / YRsiz (1..255)
                 p.cdx[c] = s[37 + 3 * c]; p.cdy[c] = s[38 + 3 * c];
@@ -3385,6 +3403,9 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     // first three components coded with different transforms are refused
     if (p.mct && im.nc >= 3 && (pcs[1].irreversible != pcs[0].irreversible || pcs[2].irreversible != pcs[0].irreversible))
         return -2;
+    // (an MCT over components of different precisions or signs: refused, as by the engine)
+    if (p.mct && im.nc >= 3 && (im.pr(1) != im.pr(0) || im.pr(2) != im.pr(0) || im.sg(1) != im.sg(0) || im.sg(2) != im.sg(0)))
+        return -2;
     std::vector<Quant> cq(im.nc);
     for (uint32_t c = 0; c < im.nc; ++c)
         if (!parse_quant(qbody[c].data(), qbody[c].size(), pcs[c].numres, cq[c])) return -2;
@@ -3394,6 +3415,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     *NC = im.nc; *PREC = im.prec;
     // each component's (reduced) plane size: orc_last_comp_dims
     t_comp_dims.clear();
+    t_comp_prec.clear();
+    for (uint32_t c = 0; c < im.nc; ++c) t_comp_prec.push_back(im.pr(c) | (im.sg(c) ? 0x100u : 0u));
     size_t total = 0;
     for (uint32_t c = 0; c < im.nc; ++c) {
         const uint32_t sx = p.sx(c), sy = p.sy(c);

@@ -63,6 +63,8 @@ def lib():
         _lib.orc_set_partial.argtypes = [ctypes.c_int]
         _lib.orc_last_comp_dims.restype = ctypes.c_uint32
         _lib.orc_last_comp_dims.argtypes = [ctypes.c_void_p]
+        _lib.orc_last_comp_prec.restype = ctypes.c_uint32
+        _lib.orc_last_comp_prec.argtypes = [ctypes.c_void_p]
         _lib.orc_inv53_single.argtypes = [ctypes.c_int32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
         _lib.orc_inv53_single.restype = ctypes.c_int32
         _lib.orc_forward_coefs.argtypes = [P(ctypes.c_int32), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -298,6 +300,14 @@ def decode(cs, partial=False):
         out.append(flat[o:o + sh[0] * sh[1]].reshape(sh))
         o += sh[0] * sh[1]
     return out, PREC.value
+
+
+def last_comp_prec():
+    """[(precision, signed)] per component of the last decode (SIZ Ssiz)."""
+    n = lib().orc_last_comp_prec(None)
+    v = (ctypes.c_uint32 * max(n, 1))()
+    lib().orc_last_comp_prec(v)
+    return [(v[c] & 0xff, bool(v[c] >> 8)) for c in range(n)]
 
 
 def forward_coefs(img, prec, signed=False, **kw):

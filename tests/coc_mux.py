@@ -65,16 +65,18 @@ def _prc_exps(cod):
 
 
 def mux(planes, prec, comp_kw, nlayers=1):
-    """planes: list of (H, W) int32 arrays (one size); comp_kw: per component oracle.encode
-    keyword arguments (numres, cblk, irreversible, cblk_sty, precincts, layer_rate ...).
+    """planes: list of (H, W) int32 arrays (one size); prec: the precision, or one per component
+    (SIZ Ssiz; the QCD / QCC follow it); comp_kw: per component oracle.encode keyword arguments
+    (numres, cblk, irreversible, cblk_sty, precincts, layer_rate ...).
     Returns the multi-component codestream."""
     h, w = planes[0].shape
+    precs = list(prec) if isinstance(prec, (list, tuple)) else [prec] * len(planes)
     parts = []
-    for p, kw in zip(planes, comp_kw):
+    for p, kw, pr in zip(planes, comp_kw, precs):
         kw = dict(kw, plt=True, mct=False, write_com=False)
         if "layer_rate" not in kw:
             kw["nlayers"] = nlayers
-        cs = O.encode(p[None], prec, **kw)
+        cs = O.encode(p[None], pr, **kw)
         main, plt, data = _markers(cs)
         cod = main[0xFF52]
         assert cod[1] == 0 and struct.unpack(">H", cod[2:4])[0] == nlayers   # LRCP, the same layers
@@ -93,7 +95,7 @@ def mux(planes, prec, comp_kw, nlayers=1):
         parts.append((main, cod, npr, pk))
     nc = len(planes)
     siz0 = parts[0][0][0xFF51]
-    siz = bytearray(siz0[:34]) + struct.pack(">H", nc) + bytes([prec - 1, 1, 1]) * nc
+    siz = bytearray(siz0[:34]) + struct.pack(">H", nc) + b"".join(bytes([pr - 1, 1, 1]) for pr in precs)
     cod0 = bytearray(parts[0][1])
     cod0[4] = 0   # no MCT
     o = bytearray(b"\xff\x4f")

@@ -28,15 +28,23 @@ CASES = {
     "layers_rate": (96, 96, 8, [dict(numres=4, layer_rate=[20, 5]), dict(numres=3, layer_rate=[30, 8]),
                                 dict(numres=5, irreversible=True, layer_rate=[40, 10])], 2),
     "mono12_pair": (50, 66, 12, [dict(numres=5, cblk=(32, 32)), dict(numres=1)], 1),
+    # components of different precisions (SIZ Ssiz per component; QCC follows the precision)
+    "mixed_precision": (48, 60, [12, 8, 16, 4], [dict(numres=3), dict(numres=3), dict(numres=4, irreversible=True),
+                                                 dict(numres=2)], 1),
 }
+
+
+def _precs(name):
+    H, W, prec, kws, L = CASES[name]
+    return list(prec) if isinstance(prec, (list, tuple)) else [prec] * len(kws)
 
 
 def planes(name):
     H, W, prec, kws, L = CASES[name]
     rng = np.random.default_rng(sum(map(ord, name)))
     yy, xx = np.mgrid[0:H, 0:W]
-    return [((xx * (c + 2) + yy * 3 + rng.integers(0, 16, size=(H, W))) % (1 << prec)).astype(np.int32)
-            for c in range(len(kws))]
+    return [((xx * (c + 2) + yy * 3 + rng.integers(0, 16, size=(H, W))) % (1 << pr)).astype(np.int32)
+            for c, pr in enumerate(_precs(name))]
 
 
 def stream(name):
@@ -50,11 +58,11 @@ def single_decodes(name, reduce=0):
     out = []
     O.set_decode_reduce(reduce)
     try:
-        for p, kw in zip(planes(name), kws):
+        for p, kw, pr in zip(planes(name), kws, _precs(name)):
             kw = dict(kw, plt=True, mct=False, write_com=False)
             if "layer_rate" not in kw:
                 kw["nlayers"] = L
-            out.append(O.decode(O.encode(p[None], prec, **kw))[0][0])
+            out.append(O.decode(O.encode(p[None], pr, **kw))[0][0])
     finally:
         O.set_decode_reduce(0)
     return out
@@ -85,6 +93,14 @@ def test_oracle_coc_reduced(name):
         O.set_decode_reduce(0)
     for g, w in zip(got, single_decodes(name, reduce=1)):
         np.testing.assert_array_equal(g, w)
+
+
+def test_mixed_precision_reported():
+    O.decode(stream("mixed_precision"))
+    assert O.last_comp_prec() == [(12, False), (8, False), (16, False), (4, False)]
+    import grok_amd as G
+    assert [c[2] for c in G.probe_components(stream("mixed_precision"), precision=True)] == [12, 8, 16, 4]
+    assert G.probe_header(stream("mixed_precision")).prec == 16   # (the largest)
 
 
 def test_oracle_coc_reduce_past_a_component_refused():
