@@ -54,6 +54,8 @@ class CParameters(ctypes.Structure):
         ("numpocs", ctypes.c_uint32), ("pocs", Poc * 32),
         ("allocationByQuality", ctypes.c_uint8), ("layer_distortion", ctypes.c_double * GK_MAX_LAYERS),
         ("tx0", ctypes.c_uint32), ("ty0", ctypes.c_uint32),
+        ("num_comments", ctypes.c_uint32), ("comment", ctypes.c_char_p * 256), ("comment_len", ctypes.c_uint16 * 256),
+        ("is_binary_comment", ctypes.c_uint8 * 256),
     ]
 
 
@@ -141,7 +143,7 @@ PROG_ORDERS = ["LRCP", "RLCP", "RPCL", "PCRL", "CPRL"]   # GRK_PROG_ORDER (grok.
 def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True, numlayers=1, layer_rate=None,
                    precincts=None, write_comment=True, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False,
                    prog_order="LRCP", tile_parts=None, pocs=None, roi=None, sop=False, eph=False, quality=None,
-                   tile_origin=None):
+                   tile_origin=None, comments=None):
     """grk_compress_set_default_params + the CLI options used by the benchmark configs.
 
     prog_order: "LRCP", "RLCP", "RPCL", "PCRL", "CPRL" or 0..4 (grk_compress -p).
@@ -184,6 +186,13 @@ def default_params(numresolution=6, cblk=(64, 64), irreversible=False, mct=True,
         p.enableTilePartGeneration = 1
         p.newTilePartProgressionDivider = tile_parts.encode()
     p.csty |= (2 if sop else 0) | (4 if eph else 0)   # grk_compress -S / -E
+    if comments:   # grk_compress -C: [bytes or str, ...] (bytes = binary, Rcom 0); the buffers stay with p
+        p._comment_bufs = [c if isinstance(c, bytes) else c.encode() for c in comments]
+        p.num_comments = len(comments)
+        for i, c in enumerate(comments):
+            p.comment[i] = p._comment_bufs[i]
+            p.comment_len[i] = len(p._comment_bufs[i])
+            p.is_binary_comment[i] = 1 if isinstance(c, bytes) else 0
     if quality:   # grk_compress -q PSNR,PSNR,...: fixed-quality layers
         p.allocationByQuality = 1
         p.numlayers = len(quality)

@@ -222,6 +222,8 @@ struct Params {
     char tp_div = 0;                     // tile-part divider 'L' / 'R' / 'C' (grk_compress -u), 0 = one part per tile
     std::vector<Poc> pocs;               // progression order changes (every tile; empty = prog)
     std::vector<uint8_t> roishift;       // per component ROI shift (RGN, maxshift; empty = none)
+    // the caller's COM markers (Rcom 0 binary / 1 text, bytes) written instead of the default one
+    std::vector<std::pair<uint32_t, std::string>> comments;
     uint32_t roi(uint32_t c) const { return c < roishift.size() ? roishift[c] : 0u; }
     bool ht() const { return (cblk_sty & 0x40) != 0; }
     // a code-block side above 64 (128 x 32 ... 1024 x 4): Part-1 blocks take the lane-per-block
@@ -2459,7 +2461,12 @@ static void write_main_header(std::vector<uint8_t>& o, const Plan& P, size_t* tl
             o.push_back(0);   // Srgn: implicit (maxshift)
             o.push_back((uint8_t)P.p.roi(c));
         }
-    if (P.p.write_com) {
+    if (!P.p.comments.empty()) {   // (CodeStreamCompress::write_com :1114-1145)
+        for (const auto& c : P.p.comments) {
+            put16(o, 0xff64); put16(o, 4 + (uint32_t)c.second.size()); put16(o, c.first);
+            o.insert(o.end(), c.second.begin(), c.second.end());
+        }
+    } else if (P.p.write_com) {
         const char* txt = "Created by Grok     version 9.2.0";
         put16(o, 0xff64); put16(o, 4 + (uint32_t)strlen(txt)); put16(o, 1);
         o.insert(o.end(), txt, txt + strlen(txt));
@@ -2632,6 +2639,19 @@ static void set_params(Params& P, const gk_cparameters* cp, uint32_t nc) {
     if (cp->csty & ~7u) throw GkError("unknown coding style bits (csty)");
     P.sop_eph = cp->csty & 6u;
     P.write_com = cp->write_comment;
+    // caller comments (CodeStreamCompress.cpp:303-330): entry i is kept when non-empty and not longer
+    // than GRK_MAX_COMMENT_LENGTH; write_com then writes entries 0 .. kept - 1 that are valid (an
+    // entry skipped early shifts the count, as there).  Lengths that overflow Lcom are refused.
+    P.comments.clear();
+    if (cp->num_comments > GK_NUM_COMMENTS) throw GkError("at most 256 comments");
+    uint32_t kept = 0;
+    for (uint32_t i = 0; i < cp->num_comments; ++i)
+        if (cp->comment_len[i] && cp->comment[i]) ++kept;
+    for (uint32_t i = 0; i < kept; ++i) {
+        if (!cp->comment_len[i] || !cp->comment[i]) continue;
+        if (cp->comment_len[i] > 65531) throw GkError("comment longer than a COM marker holds (65531 bytes)");
+        P.comments.push_back({cp->is_binary_comment[i] ? 0u : 1u, std::string(cp->comment[i], cp->comment_len[i])});
+    }
     P.cblk_sty = cp->cblk_sty;
     if (cp->prog_order < 0 || cp->prog_order > 4) throw GkError("unknown progression order");
     P.prog = (uint32_t)cp->prog_order;

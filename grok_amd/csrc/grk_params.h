@@ -29,7 +29,11 @@ inline bool grk_params_to_gk(const grk_cparameters& g, bool jp2, gk_cparameters&
     // mct 255 = not set on the command line: grk_compress resolves it from the component count
     // once the image is loaded (grk_compress.cpp:1977-1981), as the engine does (>= 3 -> RCT/ICT)
     if (g.mct_data || (g.mct > 1 && g.mct != 255)) return refuse("Part-2 array MCT is not supported");
-    if (g.num_comments) return refuse("custom COM markers are not supported (the default comment is written)");
+    if (g.num_comments > GK_NUM_COMMENTS) return refuse("too many comments");
+    p.num_comments = (uint32_t)g.num_comments;   // grk_compress -C (CodeStreamCompress.cpp:303-330)
+    for (size_t i = 0; i < g.num_comments; ++i) {
+        p.comment[i] = g.comment[i]; p.comment_len[i] = g.comment_len[i]; p.is_binary_comment[i] = g.is_binary_comment[i];
+    }
     if (g.csty & ~7u) return refuse("unknown coding style bits (csty)");
     const uint32_t sty = (g.isHT ? GRK_CBLKSTY_HT : 0) | g.cblk_sty;
     if (sty > 0x7f || ((sty & GRK_CBLKSTY_HT) && sty != GRK_CBLKSTY_HT)) {

@@ -25,6 +25,7 @@ extern "C" {
 
 #define GK_MAXRLVLS 33
 #define GK_MAX_LAYERS 100
+#define GK_NUM_COMMENTS 256   /* GRK_NUM_COMMENTS_SUPPORTED */
 
 /* One progression order change (grk_progression's resS, compS, layE, resE, compE, progression;
  * POC marker A.6.6): layers [0, layE), resolutions [resS, resE), components [compS, compE). */
@@ -69,6 +70,13 @@ typedef struct gk_cparameters {
     double layer_distortion[GK_MAX_LAYERS]; /* grk_cparameters::layer_distortion: PSNR per layer (0 = the rest) */
     uint32_t tx0, ty0;                   /* grk_cparameters::tx0 / ty0 (grk_compress -T): tile grid origin on the
                                             canvas, at or above-left of the image origin (B.3) */
+    /* grk_cparameters::comment / comment_len / is_binary_comment / num_comments (grk_compress -C):
+       COM markers written instead of Grok's default one (CodeStreamCompress.cpp:303-330 keeps the
+       non-empty ones, write_com :1114-1145 writes Rcom 1 (text) or 0 (binary) and the bytes) */
+    uint32_t num_comments;
+    const char* comment[GK_NUM_COMMENTS];
+    uint16_t comment_len[GK_NUM_COMMENTS];
+    uint8_t is_binary_comment[GK_NUM_COMMENTS];
 } gk_cparameters;
 
 /* Image description: grk_image / grk_image_comp (grok.h:895-959) reduced to

@@ -122,6 +122,9 @@ struct Params {
     // Grok's encoder writes neither; they are third-party streams its decoder reads
     // (CodeStreamDecompress read_ppm / read_ppt, T2Decompress.cpp:255-270)
     uint32_t ppx = 0;
+    // caller COM markers (grk_compress -C; CodeStreamCompress.cpp:303-330, write_com :1114-1145):
+    // (Rcom, bytes), written instead of the default comment
+    std::vector<std::pair<uint32_t, std::string>> comments;
     uint32_t sx(uint32_t c) const { return c < cdx.size() ? cdx[c] : 1u; }
     uint32_t sy(uint32_t c) const { return c < cdy.size() ? cdy[c] : 1u; }
     bool subsampled() const {
@@ -1424,7 +1427,12 @@ static void write_main_header(std::vector<uint8_t>& o, const Image& im, const Pa
             if (cw == 1) o.push_back((uint8_t)c); else put16(o, c);
             o.push_back(0); o.push_back((uint8_t)p.roi(c));
         }
-    if (p.write_com) {                               // COM (CodeStreamCompress.cpp:334, 1114)
+    if (!p.comments.empty()) {
+        for (const auto& c : p.comments) {
+            put16(o, 0xff64); put16(o, 4 + (uint32_t)c.second.size()); put16(o, c.first);
+            o.insert(o.end(), c.second.begin(), c.second.end());
+        }
+    } else if (p.write_com) {                        // COM (CodeStreamCompress.cpp:334, 1114)
         const char* txt = "Created by Grok     version 9.2.0";
         put16(o, 0xff64); put16(o, 4 + (uint32_t)strlen(txt)); put16(o, 1);
         o.insert(o.end(), txt, txt + strlen(txt));
@@ -2106,6 +2114,10 @@ typedef struct {
     uint32_t nsub;
     uint32_t sub_dx[16], sub_dy[16];
     uint32_t ppx;          // packed packet headers: 1 PPT, 2 PPM (Params::ppx)
+    // caller comments: ncom entries, bytes back to back at com_data
+    uint32_t ncom;
+    const uint8_t* com_data;
+    uint32_t com_len[16], com_binary[16];
 } orc_cparams;
 
 void orc_set_threads(unsigned n) { g_threads = n ? n : 1; }
@@ -2145,6 +2157,8 @@ static Params to_params(const orc_cparams* cp) {
     p.qderived = cp->qderived != 0;
     for (uint32_t c = 0; c < cp->nsub && c < 16; ++c) { p.cdx.push_back(std::max(1u, cp->sub_dx[c])); p.cdy.push_back(std::max(1u, cp->sub_dy[c])); }
     p.ppx = cp->ppx;
+    for (uint32_t i = 0, at = 0; i < cp->ncom && i < 16; at += cp->com_len[i], ++i)
+        p.comments.push_back({cp->com_binary[i] ? 0u : 1u, std::string((const char*)cp->com_data + at, cp->com_len[i])});
     return p;
 }
 

@@ -33,6 +33,8 @@ class CParams(ctypes.Structure):
         ("qderived", ctypes.c_uint32),
         ("nsub", ctypes.c_uint32), ("sub_dx", ctypes.c_uint32 * 16), ("sub_dy", ctypes.c_uint32 * 16),
         ("ppx", ctypes.c_uint32),
+        ("ncom", ctypes.c_uint32), ("com_data", ctypes.c_char_p), ("com_len", ctypes.c_uint32 * 16),
+        ("com_binary", ctypes.c_uint32 * 16),
     ]
 
 
@@ -111,7 +113,7 @@ def get_threads():
 def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, write_com=True, precincts=None,
            layer_rate=None, cblk_sty=0, tiles=None, tlm=False, plt=False, jp2=False, prog_order=0, tile_parts=None, pocs=None, roi=None,
            sop=False, eph=False, quality=None, origin=None, tile_origin=None, comp_guard_bits=None, comp_qshift=None,
-           qderived=False, subsampling=None, packed_headers=None):
+           qderived=False, subsampling=None, packed_headers=None, comments=None):
     p = CParams()
     lib().orc_default_params(ctypes.byref(p))
     p.numres = numres
@@ -154,6 +156,14 @@ def params(numres=6, cblk=(64, 64), irreversible=False, mct=True, nlayers=1, wri
         p.nsub = len(subsampling)
         for c, (dx, dy) in enumerate(subsampling):
             p.sub_dx[c], p.sub_dy[c] = int(dx), int(dy)
+    # caller comments (grk_compress -C): [str (text) or bytes (binary)], written instead of the default
+    if comments:
+        bufs = [c if isinstance(c, bytes) else c.encode() for c in comments]
+        p._com = b"".join(bufs)
+        p.ncom = len(bufs)
+        p.com_data = p._com
+        for i, (b, c) in enumerate(zip(bufs, comments)):
+            p.com_len[i], p.com_binary[i] = len(b), int(isinstance(c, bytes))
     # packed packet headers: "ppt" (tile-part headers) or "ppm" (main header); test streams only
     p.ppx = {None: 0, "ppt": 1, "ppm": 2}[packed_headers]
     p.cod_format = 2 if jp2 else 0

@@ -85,6 +85,21 @@ static int enc(int argc, char** argv) {
             p.allocationByQuality = true;
         }
         else if (!strcmp(argv[i], "-T")) { sscanf(argv[++i], "%u,%u", &p.tx0, &p.ty0); tile_off = 1; }   /* :1512-1529 */
+        else if (!strcmp(argv[i], "-C")) {   /* grk_compress.cpp:1578-1608: '|'-separated ISO Latin comments */
+            char* str = argv[++i];
+            char* tok = strtok(str, "|");
+            while (tok && p.num_comments < GRK_NUM_COMMENTS_SUPPORTED) {
+                if (*tok) {
+                    size_t n = strlen(tok);
+                    p.is_binary_comment[p.num_comments] = false;
+                    p.comment[p.num_comments] = (char*)malloc(n);
+                    memcpy(p.comment[p.num_comments], tok, n);
+                    p.comment_len[p.num_comments] = (uint16_t)n;
+                    p.num_comments++;
+                }
+                tok = strtok(NULL, "|");
+            }
+        }
         else if (!strcmp(argv[i], "-sub")) {   /* API-level subsampling (grk_image_comp dx / dy): dx1xdy1:dx2xdy2:...
                                                   (the CLI's raw reader refuses it, RAWFormat.cpp:293-298) */
             char* s = argv[++i];

@@ -275,3 +275,16 @@ def test_grk_api_subsampled_window(tool):
         cd = lambda a, b: -(-a // b)
         want.append(f[cd(y0, dy):cd(y1, dy), cd(x0, dx):cd(x1, dx)].ravel())
     np.testing.assert_array_equal(np.fromfile(dec, np.int32), np.concatenate(want))
+
+
+@pytest.mark.parametrize("flags", ["-n 4", "-n 5 -r 40,10"])
+def test_grk_api_comments(tool, flags):
+    # grk_compress -C "a|b": COM markers instead of Grok's default one; with rate control the
+    # header's extra bytes move the layer budgets (updateRates' header size), as in Grok
+    from grok_amd.synth import synth_image
+    from conftest import parse_flags
+    img = synth_image(96, 120, 3, 8, 31).astype(np.int32)
+    cs, _ = _enc(tool, img, 8, flags, "com_%d" % len(flags), extra=("-C", "first|second comment"))
+    ref = O.encode(img, 8, comments=["first", "second comment"], **parse_flags(flags))
+    assert cs == ref
+    assert cs.count(b"\xff\x64") == 2 and b"Created by Grok" not in cs
