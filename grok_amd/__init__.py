@@ -383,6 +383,42 @@ class Engine:
         finally:
             self.lib.gk_set_subsampling(self.ctx, 0, None, None)
 
+    def encode_tiles_subsampled(self, planes, prec, tile_begin, tile_end, subsampling, size, signed=False, params=None,
+                                origin=None):
+        """gk_encode_tiles for an image with subsampled components: planes = whole component
+        planes (comp_shape each); only the rows of the selected tiles are read.  Returns
+        (bytes, part_lens); with main_header_subsampled and EOC the parts assemble the stream."""
+        if params is None:
+            params = default_params()
+        c = len(planes)
+        w, h = size
+        keep = [_host_planes(p, prec) for p in planes]
+        info = ImageInfo(w, h, c, prec, int(signed), _sample_bytes(keep[0]))
+        info.x0, info.y0 = (int(origin[0]), int(origin[1])) if origin is not None else (params.tx0, params.ty0)
+        ptrs = (ctypes.c_void_p * c)(*[p.ctypes.data for p in keep])
+        strides = (ctypes.c_uint32 * c)(*[p.shape[1] for p in keep])
+        dxs = (ctypes.c_uint32 * c)(*[int(d[0]) for d in subsampling])
+        dys = (ctypes.c_uint32 * c)(*[int(d[1]) for d in subsampling])
+        if self.lib.gk_set_subsampling(self.ctx, c, dxs, dys) != 0:
+            self._err("gk_set_subsampling")
+        try:
+            lens = (ctypes.c_uint32 * (tile_end - tile_begin))()
+            n = ctypes.c_size_t()
+            cap = sum(p.size for p in keep) * 4 + (1 << 20)
+            buf = np.empty(cap, np.uint8)
+            rc = self.lib.gk_encode_tiles(self.ctx, ctypes.byref(info), ptrs, strides, 0, ctypes.byref(params),
+                                          tile_begin, tile_end, buf.ctypes.data, cap, ctypes.byref(n), lens, 0)
+            if rc != 0:
+                self._err("gk_encode_tiles")
+            hdr = np.empty(1 << 20, np.uint8)
+            hn, tlm, nt = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_uint32()
+            if self.lib.gk_main_header(self.ctx, ctypes.byref(info), ctypes.byref(params), hdr.ctypes.data, hdr.size,
+                                       ctypes.byref(hn), ctypes.byref(tlm), ctypes.byref(nt)) != 0:
+                self._err("gk_main_header")
+            return hdr[:hn.value].tobytes(), buf[:n.value].tobytes(), list(lens)
+        finally:
+            self.lib.gk_set_subsampling(self.ctx, 0, None, None)
+
     def subsampling(self):
         """[(dx, dy)] per component of the stream the last read_header / decode read."""
         dx, dy = (ctypes.c_uint32 * 16384)(), (ctypes.c_uint32 * 16384)()

@@ -3022,7 +3022,6 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     if (te == 0) { tb = 0; te = ntiles; }
     if (tb >= te || te > ntiles) throw GkError("bad tile range");
     const bool sub = P.subsampled();
-    if (sub && (tb != 0 || te != ntiles)) throw GkError("tile-range encodes of subsampled components are not supported on this path");
     const uint32_t nb = (uint32_t)P.blocks.size();
     const uint32_t b0 = P.tiles[tb].b0, b1 = P.tiles[te - 1].b1, nbr = b1 - b0;   // block range of the tiles
     const uint32_t jb = tb / P.ntx, je = (te - 1) / P.ntx + 1;                     // tile rows touched
@@ -3041,31 +3040,23 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     const size_t es = gk_sample_size(stype);
     std::vector<const void*> src(P.nc);
     std::vector<uint32_t> sstr(P.nc);
-    if (sub) {
-        // subsampled components: each plane at its own size (the whole image), staged back to back
+    // component c reads the rows of the selected tiles on its grid (the region on its sampling
+    // group's grid: every row of the image width); host planes are staged back to back
+    std::vector<Region> RGg;
+    for (const SGroup& G : P.groups) RGg.push_back(group_region(P, RG, G));
+    {
         size_t tot = 0;
-        for (uint32_t c = 0; c < P.nc; ++c) tot += (size_t)P.groups[P.group_of[c]].w * P.groups[P.group_of[c]].h;
+        for (uint32_t c = 0; c < P.nc; ++c) tot += (size_t)RGg[P.group_of[c]].w * RGg[P.group_of[c]].h;
         uint8_t* dp = comps_on_device ? nullptr : (uint8_t*)ctx->dplanes.get(tot * es + 16);
         size_t o = 0;
         for (uint32_t c = 0; c < P.nc; ++c) {
-            const SGroup& G = P.groups[P.group_of[c]];
-            if (comps_on_device) { src[c] = comps[c]; sstr[c] = strides[c]; continue; }
-            HIPCHK(hipMemcpy2DAsync(dp + o * es, (size_t)G.w * es, comps[c], (size_t)strides[c] * es, (size_t)G.w * es, G.h,
+            const Region& R = RGg[P.group_of[c]];
+            const uint8_t* first = (const uint8_t*)comps[c] + (size_t)R.y0 * strides[c] * es;
+            if (comps_on_device) { src[c] = first; sstr[c] = strides[c]; continue; }
+            HIPCHK(hipMemcpy2DAsync(dp + o * es, (size_t)R.w * es, first, (size_t)strides[c] * es, (size_t)R.w * es, R.h,
                                     hipMemcpyHostToDevice, st));
-            src[c] = dp + o * es; sstr[c] = G.w;
-            o += (size_t)G.w * G.h;
-        }
-    } else if (!comps_on_device) {
-        uint8_t* dp = (uint8_t*)ctx->dplanes.get((size_t)P.w * nrows * P.nc * es);
-        for (uint32_t c = 0; c < P.nc; ++c) {
-            HIPCHK(hipMemcpy2DAsync(dp + (size_t)c * P.w * nrows * es, (size_t)P.w * es,
-                                    (const uint8_t*)comps[c] + (size_t)ry0 * strides[c] * es, (size_t)strides[c] * es,
-                                    (size_t)P.w * es, nrows, hipMemcpyHostToDevice, st));
-            src[c] = dp + (size_t)c * P.w * nrows * es; sstr[c] = P.w;
-        }
-    } else {
-        for (uint32_t c = 0; c < P.nc; ++c) {
-            src[c] = (const uint8_t*)comps[c] + (size_t)ry0 * strides[c] * es; sstr[c] = strides[c];
+            src[c] = dp + o * es; sstr[c] = R.w;
+            o += (size_t)R.w * R.h;
         }
     }
     launch_check(__LINE__);
@@ -3086,8 +3077,8 @@ static size_t encode_impl(gk_ctx* ctx, const gk_image_info* info, const void* co
     } else {
         // no decomposition (or a tile on an odd origin): DC shift + MCT into plane A of each
         // component (each component's plane at its own size)
-        auto cw = [&](uint32_t c) { return sub ? P.groups[P.group_of[c]].w : P.w; };
-        auto ch = [&](uint32_t c) { return sub ? P.groups[P.group_of[c]].h : nrows; };
+        auto cw = [&](uint32_t c) { return RGg[P.group_of[c]].w; };
+        auto ch = [&](uint32_t c) { return RGg[P.group_of[c]].h; };
         if (!P.p.irrev) {
             if (mct3) gk_launch_dc_rct_fwd(st, stype, src[0], src[1], src[2], sstr[0], planeA(0), planeA(1), planeA(2), RG.stride, cw(0), ch(0), shift);
             for (uint32_t c = mct3 ? 3 : 0; c < P.nc; ++c) gk_launch_dc_fwd(st, stype, src[c], sstr[c], planeA(c), RG.stride, cw(c), ch(c), shift);

@@ -160,3 +160,21 @@ def test_engine_tile_pitch_must_divide(eng):
     src = [np.zeros((48, 64), np.int32), np.zeros((24, 32), np.int32)]
     with pytest.raises(RuntimeError, match="does not divide the tile size"):
         eng.encode(src, 8, params=G.default_params(numresolution=2, tiles=(33, 48)), subsampling=sub, size=(W, H))
+
+
+@pytest.mark.parametrize("name", ["tiled_pcrl", "tiled_rpcl_origin"])
+def test_engine_subsampled_tile_ranges(eng, name):
+    # gk_encode_tiles on a subsampled image (tile sharding): the header plus the parts of two tile
+    # ranges assemble the whole-image stream
+    import grok_amd as G
+    W, H, sub, prec, kw = CASES[name]
+    pk, origin = engine_params(name)
+    params = G.default_params(**pk)
+    src = planes(name)
+    full = eng.encode(src, prec, params=params, origin=origin, subsampling=sub, size=(W, H))
+    ntiles = -(-(W + (origin or (0, 0))[0]) // kw["tiles"][0]) * -(-(H + (origin or (0, 0))[1]) // kw["tiles"][1])
+    k = ntiles // 2
+    hdr, a, _ = eng.encode_tiles_subsampled(src, prec, 0, k, sub, (W, H), params=params, origin=origin)
+    _, b, _ = eng.encode_tiles_subsampled(src, prec, k, ntiles, sub, (W, H), params=params, origin=origin)
+    assert hdr + a + b + b"\xff\xd9" == full
+
