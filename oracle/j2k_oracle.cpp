@@ -37,6 +37,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <memory>
 #include <algorithm>
 #include <atomic>
 #include <functional>
@@ -3211,9 +3212,7 @@ t2done:
 }
 
 // COC / QCC and tile-part COD / QCD (CodeStreamDecompress read_coc / read_qcc override the main
-// COD / QCD per component or per tile): this restatement codes every tile-component with the
-// main header's parameters, so it accepts such a marker only when it restates them.
-// qcc: the main header's quantisation body per component (its QCC, else the QCD)
+// COD / QCD per component or per tile).
 // ccod: each component's coding as a COC body would state it (Scoc precinct flag, then SPcoc):
 // its main COC, else the COD's
 static std::vector<uint8_t> cod_as_coc(const std::vector<uint8_t>& cod) {
@@ -3221,24 +3220,61 @@ static std::vector<uint8_t> cod_as_coc(const std::vector<uint8_t>& cod) {
     v.insert(v.end(), cod.begin() + 5, cod.end());
     return v;
 }
-static bool restates_main(const uint8_t* b, uint32_t L, uint32_t m, uint32_t nc, const std::vector<uint8_t>& cod,
-                          const std::vector<uint8_t>& qcd, const std::vector<std::vector<uint8_t>>& qcc,
-                          const std::vector<std::vector<uint8_t>>& ccod) {
-    if (L < 3) return false;
-    const std::vector<uint8_t> v(b, b + L - 2);
-    if (m == 0xff52) {   // (a tile COD would replace the main COCs too)
-        for (const auto& q : ccod) if (q != cod_as_coc(cod)) return false;
-        return v == cod;
+// COD body (Scod, SGcod, SPcod; CodeStreamDecompress::read_cod :2521-2623) into the stream-level
+// fields of p (SOP / EPH, layers, MCT, progression) and its default coding; false when malformed
+// or not restated here (a Part-2 array MCT)
+static bool read_cod(const std::vector<uint8_t>& v, Params& p) {
+    if (v.size() < 10) return false;
+    const uint8_t* s = v.data();
+    const uint32_t scod = s[0];
+    if (scod & ~7u) return false;            // unknown Scod bits (read_cod :2548)
+    p.sop_eph = scod & 6;
+    p.nlayers = get16(s + 2); p.mct = s[4];
+    if (!p.nlayers || p.mct > 1) return false;   // (MCT 2: Part-2 decompress_custom, not restated)
+    p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
+    p.cblk_sty = s[8];
+    if (s[1] > 4) return false;                                   // progression order
+    p.prog = s[1];
+    if ((s[8] & 0x40) && s[8] != 0x40) return false;  // HT with Part-1 mode switches (CodeStreamDecompress.cpp:1781)
+    if (s[8] & 0x80) return false;
+    if (p.numres > 33 || p.cbw_exp > 10 || p.cbh_exp > 10 || p.cbw_exp + p.cbh_exp > 12) return false;
+    for (uint32_t r = 0; r < 33; ++r) { p.prcw_exp[r] = 15; p.prch_exp[r] = 15; }
+    if (scod & 1) {
+        if (v.size() < 10 + p.numres) return false;
+        for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
     }
-    if (m == 0xff5c) {
-        for (const auto& q : qcc) if (q != qcd) return false;   // a tile QCD would replace differing QCCs
-        return v == qcd;
-    }
+    return prc_exps_ok(p);
+}
+
+// A tile's coding and quantisation: the main header's (cod, ccod, qbody) changed by the COD / COC /
+// QCD / QCC of its tile-part headers.  The tile's tcp starts as a copy of the main header's; read_cod
+// (CodeStreamDecompress.cpp:2521-2623) sets the tile's stream fields and copies its SPcod to every
+// component, read_coc (:2631-2670) sets one component's, both in marker order; quantisation follows
+// read_SQcd_SQcc's scoping (Quantizer.cpp:208-235): a tile QCC wins over a tile QCD, which wins over
+// the main header's QCC / QCD, in any marker order.
+struct TileCoding { std::vector<uint8_t> cod; std::vector<std::vector<uint8_t>> ccod, qbody; };
+static bool tile_coding(const std::vector<std::pair<uint32_t, std::vector<uint8_t>>>& marks, uint32_t nc, TileCoding& tc) {
     const uint32_t cw = nc <= 256 ? 1 : 2;
-    if (v.size() <= cw || (cw == 1 ? v[0] : get16(b)) >= nc) return false;
-    const uint32_t c = cw == 1 ? v[0] : get16(b);
-    if (m == 0xff5d) return std::equal(v.begin() + cw, v.end(), qcc[c].begin(), qcc[c].end());
-    return (v[cw] & 1) == ccod[c][0] && std::equal(v.begin() + cw + 1, v.end(), ccod[c].begin() + 1, ccod[c].end());
+    std::vector<uint8_t> tqcc(nc, 0);
+    for (const auto& mk : marks) {
+        const std::vector<uint8_t>& v = mk.second;
+        if (mk.first == 0xff52) {
+            if (v.size() < 10) return false;
+            tc.cod = v;
+            for (auto& q : tc.ccod) q = cod_as_coc(v);
+        } else if (mk.first == 0xff5c) {
+            if (v.size() < 2) return false;
+            for (uint32_t c = 0; c < nc; ++c) if (!tqcc[c]) tc.qbody[c] = v;
+        } else {
+            if (v.size() < cw + 2) return false;
+            const uint32_t c = cw == 1 ? v[0] : get16(v.data());
+            if (c >= nc) return false;
+            std::vector<uint8_t> b(v.begin() + cw, v.end());
+            if (mk.first == 0xff5d) { tc.qbody[c] = std::move(b); tqcc[c] = 1; }
+            else { if (b.size() < 6) return false; tc.ccod[c] = std::move(b); }
+        }
+    }
+    return true;
 }
 
 // A component's coding parameters from its COC-form body (Scoc, SPcoc: decomposition levels,
@@ -3349,19 +3385,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
                 if (!p.cdx[c] || !p.cdy[c]) return -2;
             }
         } else if (m == 0xff52) {
-            uint32_t scod = s[0];
             cod_body.assign(s, s + L - 2);
-            p.sop_eph = scod & 6;
-            p.nlayers = get16(s + 2); p.mct = s[4];
-            if (p.mct > 1) return -2;   // Part-2 array MCT (decompress_custom): not restated
-            p.numres = s[5] + 1; p.cbw_exp = s[6] + 2; p.cbh_exp = s[7] + 2; p.irreversible = s[9] == 0;
-            p.cblk_sty = s[8];
-            if (s[1] > 4) return -2;                                 // progression order
-            p.prog = s[1];
-            if ((s[8] & 0x40) && s[8] != 0x40) return -2;  // HT with Part-1 mode switches (CodeStreamDecompress.cpp:1781)
-            if (s[8] & 0x80) return -2;
-            if (scod & 1) for (uint32_t r = 0; r < p.numres; ++r) { p.prcw_exp[r] = s[10 + r] & 15; p.prch_exp[r] = s[10 + r] >> 4; }
-            if (!prc_exps_ok(p)) return -2;
+            if (!read_cod(cod_body, p)) return -2;
         } else if (m == 0xff5f) {
             if (!read_poc(s, L, im.nc, p.pocs)) return -2;
         } else if (m == 0xff5e) {                          // RGN: Crgn, Srgn (0), SPrgn
@@ -3407,22 +3432,34 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         if (c >= im.nc) return -2;
         ccod[c].assign(b + cw, b + L - 2);
     }
-    std::vector<Params> pcs(im.nc, p);
+    // a tile's parameters from its coding: stream fields from its COD, each component's from its
+    // COC-form body, quantisation per component; 0, or the error code
+    auto setup = [&](const TileCoding& tc, Params& pt, std::vector<Params>& pcs_t, std::vector<Quant>& cq_t,
+                     uint32_t& min_res) -> int {
+        if (!read_cod(tc.cod, pt)) return -2;
+        pcs_t.assign(im.nc, pt);
+        min_res = 33;
+        for (uint32_t c = 0; c < im.nc; ++c) {
+            if (!comp_params(tc.ccod[c], pcs_t[c])) return -2;
+            min_res = std::min(min_res, pcs_t[c].numres);
+        }
+        // the inverse MCT picks RCT / ICT by component 0's transform (TileProcessor::mctDecompress):
+        // first three components coded with different transforms are refused
+        if (pt.mct && im.nc >= 3 && (pcs_t[1].irreversible != pcs_t[0].irreversible || pcs_t[2].irreversible != pcs_t[0].irreversible))
+            return -2;
+        // (an MCT over components of different precisions or signs: refused, as by the engine)
+        if (pt.mct && im.nc >= 3 && (im.pr(1) != im.pr(0) || im.pr(2) != im.pr(0) || im.sg(1) != im.sg(0) || im.sg(2) != im.sg(0)))
+            return -2;
+        cq_t.assign(im.nc, Quant());
+        for (uint32_t c = 0; c < im.nc; ++c)
+            if (!parse_quant(tc.qbody[c].data(), tc.qbody[c].size(), pcs_t[c].numres, cq_t[c])) return -2;
+        return g_dec_reduce >= min_res ? -7 : 0;   // reduce must leave one resolution of every component
+    };
+    const TileCoding main_tc{cod_body, ccod, qbody};
+    std::vector<Params> pcs;
+    std::vector<Quant> cq;
     uint32_t min_res = 33;
-    for (uint32_t c = 0; c < im.nc; ++c) {
-        if (!comp_params(ccod[c], pcs[c])) return -2;
-        min_res = std::min(min_res, pcs[c].numres);
-    }
-    // the inverse MCT picks RCT / ICT by component 0's transform (TileProcessor::mctDecompress):
-    // first three components coded with different transforms are refused
-    if (p.mct && im.nc >= 3 && (pcs[1].irreversible != pcs[0].irreversible || pcs[2].irreversible != pcs[0].irreversible))
-        return -2;
-    // (an MCT over components of different precisions or signs: refused, as by the engine)
-    if (p.mct && im.nc >= 3 && (im.pr(1) != im.pr(0) || im.pr(2) != im.pr(0) || im.sg(1) != im.sg(0) || im.sg(2) != im.sg(0)))
-        return -2;
-    std::vector<Quant> cq(im.nc);
-    for (uint32_t c = 0; c < im.nc; ++c)
-        if (!parse_quant(qbody[c].data(), qbody[c].size(), pcs[c].numres, cq[c])) return -2;
+    if (int rc = setup(main_tc, p, pcs, cq, min_res)) return rc;
     if (g_dec_reduce >= min_res) return -7;   // reduce must leave one resolution of every component
     *W = ceildivpow2(p.x0 + im.w, g_dec_reduce) - ceildivpow2(p.x0, g_dec_reduce);
     *H = ceildivpow2(p.y0 + im.h, g_dec_reduce) - ceildivpow2(p.y0, g_dec_reduce);
@@ -3445,7 +3482,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     const uint32_t nt = tile_count(p, im.w, im.h);
     size_t pos = first_sot;
     struct Part { size_t data, end; uint32_t tile, tpsot; std::vector<PocE> pocs;
-                  std::vector<std::pair<uint32_t, std::vector<uint8_t>>> ppt; };
+                  std::vector<std::pair<uint32_t, std::vector<uint8_t>>> ppt, marks; };
     std::vector<Part> parts;
     while (pos + 12 <= len && get16(cs + pos) == 0xff90) {
         const uint8_t* s = cs + pos + 4;
@@ -3456,7 +3493,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         if (tile_end > len) return -5;
         size_t j = pos + 12;   // tile-part header markers (PLT, POC, ...) until SOD
         std::vector<PocE> tp_pocs;
-        std::vector<std::pair<uint32_t, std::vector<uint8_t>>> tp_ppt;
+        std::vector<std::pair<uint32_t, std::vector<uint8_t>>> tp_ppt, tp_marks;
         while (j + 2 <= tile_end && get16(cs + j) != 0xff93) {
             const uint32_t tm = get16(cs + j);
             if (tm == 0xff61) {   // PPT (A.7.5): Zppt, Ippt; not with PPM (read_ppt's error)
@@ -3465,13 +3502,16 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
                 tp_ppt.push_back({cs[j + 4], std::vector<uint8_t>(cs + j + 5, cs + j + 2 + Lp)});
             }
             if (tm == 0xff5f && !read_poc(cs + j + 4, get16(cs + j + 2), im.nc, tp_pocs)) return -5;
-            if ((tm == 0xff52 || tm == 0xff53 || tm == 0xff5c || tm == 0xff5d) &&
-                !restates_main(cs + j + 4, get16(cs + j + 2), tm, im.nc, cod_body, qcd_body, qbody, ccod)) return -2;
+            if (tm == 0xff52 || tm == 0xff53 || tm == 0xff5c || tm == 0xff5d) {   // the tile's coding / quantisation
+                const uint32_t Lm = get16(cs + j + 2);
+                if (Lm < 3 || j + 2 + Lm > tile_end) return -5;
+                tp_marks.push_back({tm, std::vector<uint8_t>(cs + j + 4, cs + j + 2 + Lm)});
+            }
             if (tm == 0xff5e) return -2;   // tile-part RGN
             j += 2 + get16(cs + j + 2);
         }
         if (j + 2 > tile_end) return -5;
-        parts.push_back({j + 2, tile_end, isot, s[6], std::move(tp_pocs), std::move(tp_ppt)});
+        parts.push_back({j + 2, tile_end, isot, s[6], std::move(tp_pocs), std::move(tp_ppt), std::move(tp_marks)});
         pos = tile_end;
     }
     // a tile's parts in order (TPsot 0, 1, ...)
@@ -3525,9 +3565,27 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
                 for (const auto& e : pt.ppt) if (!z.emplace(e.first, e.second).second) return -2;   // Zppt read twice
         for (auto& kv : z) hdrs[q].insert(hdrs[q].end(), kv.second.begin(), kv.second.end());
     }
+    // tiles with COD / COC / QCD / QCC in their tile-part headers: their own parameters
+    struct TileParams { Params p; std::vector<Params> pcs; std::vector<Quant> cq; };
+    std::vector<std::unique_ptr<TileParams>> own(tiles.size());
+    for (size_t q = 0; q < tiles.size(); ++q) {
+        std::vector<std::pair<uint32_t, std::vector<uint8_t>>> marks;
+        for (const Part& pt : parts)
+            if (pt.tile == tiles[q]) marks.insert(marks.end(), pt.marks.begin(), pt.marks.end());
+        if (marks.empty()) continue;
+        TileCoding tc = main_tc;
+        if (!tile_coding(marks, im.nc, tc)) return -2;
+        if (tc.cod == main_tc.cod && tc.ccod == main_tc.ccod && tc.qbody == main_tc.qbody) continue;   // restated
+        own[q].reset(new TileParams{p, {}, {}});
+        uint32_t tmin = 33;
+        if (int rc = setup(tc, own[q]->p, own[q]->pcs, own[q]->cq, tmin)) return rc;
+        own[q]->p.pocs = p.pocs;
+    }
     std::vector<int> rcs(tiles.size(), 0);   // tiles write disjoint rectangles of out
     par_for(tiles.size(), [&](size_t q) {
-        rcs[q] = decode_tile(cs, ranges[q], p, pcs, im, cq, tiles[q], out, &tpocs[q], has_hdr[q] ? &hdrs[q] : nullptr);
+        const TileParams* o = own[q].get();
+        rcs[q] = decode_tile(cs, ranges[q], o ? o->p : p, o ? o->pcs : pcs, im, o ? o->cq : cq, tiles[q], out, &tpocs[q],
+                             has_hdr[q] ? &hdrs[q] : nullptr);
     });
     for (int rc : rcs) if (rc) return rc;
     return 0;

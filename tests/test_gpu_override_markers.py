@@ -1,12 +1,13 @@
 """COC / QCC and tile-part COD / QCD markers in the HIP decoder (the oracle half and the
 rationale are in tests/test_override_markers.py): markers restating the main COD / QCD decode
 exactly as the stream without them, from host and from device-resident (TLM-located) streams;
-markers that change them are refused with the engine's message."""
+markers that change a tile's coding decode to the oracle's samples; bad component numbers are
+refused with the engine's message."""
 import numpy as np
 import pytest
 
 from conftest import FIXTURES
-from test_override_markers import NAMES, changing, restating
+from test_override_markers import NAMES, changing, refused, restating
 
 pytestmark = pytest.mark.gpu
 
@@ -34,10 +35,21 @@ def test_restating_markers_engine(eng, name):
 
 
 @pytest.mark.parametrize("name", NAMES)
-def test_changing_markers_engine_refuses(eng, name):
+def test_changing_tile_markers_engine(eng, name):
+    import oracle as O
+    import torch
     fx = _fx(name)
     for what, cs in changing(fx.cs):
-        with pytest.raises(RuntimeError, match="not supported on this path|bad component number"):
+        if fx.ht and what == "tile COC":
+            with pytest.raises(RuntimeError, match="HTJ2K combined with Part-1"):
+                eng.decode(cs)
+            continue
+        want = O.decode(cs)[0]
+        np.testing.assert_array_equal(eng.decode(cs), want, err_msg=what)
+        d = torch.frombuffer(bytearray(cs), dtype=torch.uint8).cuda()
+        np.testing.assert_array_equal(eng.decode(d, len(cs)), want, err_msg=what)
+    for what, cs in refused(fx.cs):
+        with pytest.raises(RuntimeError, match="bad component number"):
             eng.decode(cs)
     np.testing.assert_array_equal(eng.decode(fx.cs), fx.grok_decoded)
 

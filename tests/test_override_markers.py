@@ -1,12 +1,14 @@
 """COC / QCC and tile-part COD / QCD markers in the oracle decoder.
 
-Grok reads COC / QCC (CodeStreamDecompress read_coc / read_qcc) and tile-part COD / QCD as
-per-component / per-tile overrides of the main COD / QCD.  A main-header QCC / COC is applied to its
-component (tests/test_qcc.py, tests/test_coc.py); otherwise this path codes every tile with the
-main header's parameters, so a tile-part marker that restates them decodes exactly as the stream without it
-(some encoders write them unconditionally), and one that changes them is refused rather than
-ignored.  Streams: the committed Grok fixtures with markers spliced in
-(tests/j2k_markers.py).  The engine half is tests/test_gpu_override_markers.py.
+Grok reads COC / QCC (CodeStreamDecompress read_coc / read_qcc) and tile-part COD / COC / QCD / QCC
+as per-component / per-tile overrides of the main COD / QCD.  A main-header QCC / COC is applied
+to its component (tests/test_qcc.py, tests/test_coc.py); tile-part markers set the tile's own coding
+(tests/test_tile_coding.py for streams coded that way).  Here the committed Grok fixtures get
+markers spliced in (tests/j2k_markers.py): markers that restate the main header decode exactly as
+the stream without them (some encoders write them unconditionally); markers that change the first
+tile's code-block style or guard bits decode as OpenJPEG 2.5.4 decodes them (sample for sample,
+9/7 included); a tile COD with one more layer than the tile holds reads the tile as truncated, i.e.
+as before.  The engine half is tests/test_gpu_override_markers.py.
 """
 import os
 import sys
@@ -16,6 +18,7 @@ import pytest
 
 from conftest import FIXTURES, ROOT
 import j2k_markers as J
+import openjpeg
 
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import oracle as O  # noqa: E402
@@ -38,7 +41,11 @@ def changing(cs):
     yield "tile COD", J.insert_tile_part(cs, J.cod(cs, layers_add=1))
     yield "tile COC", J.insert_tile_part(cs, J.coc(cs, 0, sty_xor=0x08))
     yield "tile QCC", J.insert_tile_part(cs, J.qcc(cs, 0, guard_add=1))
+
+
+def refused(cs):
     yield "COC bad component", J.insert_main(cs, J.coc(cs, J.ncomp(cs)))
+    yield "tile COC bad component", J.insert_tile_part(cs, J.coc(cs, J.ncomp(cs)))
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -52,9 +59,28 @@ def test_restating_markers_decode_as_without(name):
 
 
 @pytest.mark.parametrize("name", NAMES)
-def test_changing_markers_refused(name):
+def test_changing_tile_markers_applied(name):
     fx = _fx(name)
     for what, cs in changing(fx.cs):
+        if what == "tile COD":   # (the extra layer's packets are absent: a truncated tile)
+            np.testing.assert_array_equal(O.decode(cs)[0], fx.grok_decoded)
+        elif fx.ht and what == "tile COC":   # HT with a Part-1 mode switch (CodeStreamDecompress.cpp:1781)
+            with pytest.raises(RuntimeError, match="failed: -2"):
+                O.decode(cs)
+        elif fx.ht:   # HT places magnitudes by the zero bit-plane count alone: guard bits do not move them
+            np.testing.assert_array_equal(O.decode(cs)[0], fx.grok_decoded)
+        else:
+            got, _ = O.decode(cs)
+            assert not np.array_equal(got, fx.grok_decoded), what
+            if openjpeg.available():
+                for (dx, dy, r), g in zip(openjpeg.decode(cs), got):
+                    np.testing.assert_array_equal(r, g, err_msg=what)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_bad_component_refused(name):
+    fx = _fx(name)
+    for what, cs in refused(fx.cs):
         with pytest.raises(RuntimeError, match="failed: -2"):
             O.decode(cs)
 
