@@ -3666,6 +3666,9 @@ struct TilePart {                  // packet bytes [data, end) of one tile part
     std::vector<std::pair<uint32_t, std::vector<uint8_t>>> ppt;
     std::vector<uint8_t> hdrs;
     bool packed = false;
+    // the part's COD / COC / QCD / QCC (marker, body), in stream order: the tile's own coding and
+    // quantisation (merge_tile_parts appends the later parts')
+    std::vector<std::pair<uint32_t, std::vector<uint8_t>>> cmark;
 };
 // POC marker body (A.6.6): per entry RSpoc, CSpoc (1 or 2 bytes), LYEpoc (2), REpoc, CEpoc
 // (1 or 2; 0 = 256 with one byte), Ppoc.  Appended to out: CodeStreamDecompress::read_poc
@@ -3688,9 +3691,9 @@ static void parse_poc(Src& S, size_t s, uint32_t L, uint32_t nc, std::vector<Poc
         out.push_back(e);
     }
 }
-// Tile-part header markers that would change how the tile decodes (CodeStreamDecompress's
-// tile-part handlers: COD :1725, COC, QCD, QCC, RGN read_rgn :1480-1520) are refused here
-// rather than skipped, so a stream that carries them fails instead of decoding wrongly.
+// The main header as read, with the tile parts' positions and their tile-part header markers
+// (CodeStreamDecompress's tile-part handlers: COD :1725, COC, QCD, QCC; a tile-part RGN,
+// read_rgn :1480-1520, is refused rather than skipped)
 struct Header {
     Plan want;
     QuantList qcd;                                    // per component (apply_qcd)
@@ -3734,33 +3737,53 @@ static std::vector<uint8_t> marker_body(ByteSrc& S, size_t s, uint32_t L) {
     return v;
 }
 
-// Tile-part COD / COC / QCD / QCC override the main header's coding or quantisation for one tile
-// (CodeStreamDecompress read_coc / read_qcc, TileCodingParams).  Main-header COC / QCC are
-// applied per component (Params::cc, apply_qcd); every tile is coded with the main header's
-// parameters, so tile-part markers are accepted when they restate them (some encoders write them
-// even when nothing differs) and refused otherwise.  COC: Ccoc (1 byte below 257 components, else 2), Scoc (precinct flag),
-// then SPcoc laid out as COD's SPcod; QCC: Cqcc, then Sqcc/SPqcc as QCD's body.
-static void check_override_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, const Header& Hd, bool tile) {
-    if (m == 0xff5e && tile) throw GkError("RGN in a tile-part header is not supported on this path");
+// Tile-part COD / COC / QCD / QCC set one tile's coding or quantisation (the tile's tcp, a copy of
+// the main header's: CodeStreamDecompress read_cod / read_coc / read_qcd / read_qcc); collected per
+// tile part here, applied by tile_coding.  COC: Ccoc (1 byte below 257 components, else 2), Scoc
+// (precinct flag), then SPcoc laid out as COD's SPcod; QCC: Cqcc, then Sqcc / SPqcc as QCD's body.
+// A tile-part RGN is refused.
+static void collect_coding_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, const Header& Hd,
+                                  std::vector<std::pair<uint32_t, std::vector<uint8_t>>>& out) {
+    if (m == 0xff5e) throw GkError("RGN in a tile-part header is not supported on this path");
     if (m != 0xff52 && m != 0xff53 && m != 0xff5c && m != 0xff5d) return;
     if (L < 3) throw GkError("corrupt COD/COC/QCD/QCC marker");
-    const std::vector<uint8_t> b = marker_body(S, s, L);
+    std::vector<uint8_t> b = marker_body(S, s, L);
     const uint32_t nc = Hd.want.nc, cw = nc <= 256 ? 1 : 2;
-    bool same = false;
-    if (m == 0xff52) {   // (a tile COD replaces the main COCs as well)
-        same = b == Hd.cod;
-        for (const auto& q : Hd.ccod) same = same && q == cod_as_coc(Hd.cod);
-    }
-    else if (m == 0xff5c) {   // (a tile QCD replaces every component's QCD / QCC)
-        same = true;
-        for (const auto& q : Hd.qbody) same = same && b == q;
-    } else if (b.size() > cw) {
+    if (m == 0xff53 || m == 0xff5d) {
+        if (b.size() <= cw) throw GkError("corrupt COC/QCC marker");
         const uint32_t c = cw == 1 ? b[0] : (uint32_t)b[0] << 8 | b[1];
         if (c >= nc) throw GkError("bad component number in COC/QCC");
-        if (m == 0xff5d) same = std::equal(b.begin() + cw, b.end(), Hd.qbody[c].begin(), Hd.qbody[c].end());
-        else same = (b[cw] & 1) == Hd.ccod[c][0] && std::equal(b.begin() + cw + 1, b.end(), Hd.ccod[c].begin() + 1, Hd.ccod[c].end());
+        if (m == 0xff53 && b.size() < cw + 6) throw GkError("corrupt COC marker");
     }
-    if (!same) throw GkError("tile-part COD/COC/QCD/QCC that differ from the main header are not supported on this path");
+    if (m == 0xff52 && b.size() < 10) throw GkError("corrupt COD marker");
+    out.push_back({m, std::move(b)});
+}
+// A tile's coding and quantisation: the main header's (cod, ccod, qbody) changed by its tile-part
+// markers.  read_cod (CodeStreamDecompress.cpp:2521-2623) sets the tile's stream fields and copies
+// its SPcod to every component, read_coc (:2631-2670) one component's, in marker order;
+// quantisation follows read_SQcd_SQcc's scoping (Quantizer.cpp:208-235): a tile QCC wins over a
+// tile QCD, which wins over the main header's QCC / QCD, in any marker order.  True when the tile
+// is coded differently from the main header.
+struct TileCoding { std::vector<uint8_t> cod; std::vector<std::vector<uint8_t>> ccod, qbody; };
+static bool tile_coding(const Header& Hd, const TilePart& H, TileCoding& tc) {
+    tc.cod = Hd.cod; tc.ccod = Hd.ccod; tc.qbody = Hd.qbody;
+    const uint32_t nc = Hd.want.nc, cw = nc <= 256 ? 1 : 2;
+    std::vector<uint8_t> tqcc(nc, 0);
+    for (const auto& mk : H.cmark) {
+        const std::vector<uint8_t>& v = mk.second;
+        if (mk.first == 0xff52) {
+            tc.cod = v;
+            for (auto& q : tc.ccod) q = cod_as_coc(v);
+        } else if (mk.first == 0xff5c) {
+            for (uint32_t c = 0; c < nc; ++c) if (!tqcc[c]) tc.qbody[c] = v;
+        } else {
+            const uint32_t c = cw == 1 ? v[0] : (uint32_t)v[0] << 8 | v[1];
+            std::vector<uint8_t> b(v.begin() + cw, v.end());
+            if (mk.first == 0xff5d) { tc.qbody[c] = std::move(b); tqcc[c] = 1; }
+            else tc.ccod[c] = std::move(b);
+        }
+    }
+    return tc.cod != Hd.cod || tc.ccod != Hd.ccod || tc.qbody != Hd.qbody;
 }
 // The tiles of the canvas tile grid (B.3)
 static uint32_t grid_tiles(const Plan& W) {
@@ -3805,21 +3828,78 @@ template <class Hdr> static void walk_sot_chain(ByteSrc& S, Hdr& Hd) {
         if (end > S.len) throw GkError("corrupt SOT (Psot)");
         size_t j = pos + 12;
         std::vector<Poc> tpoc;
-        std::vector<std::pair<uint32_t, std::vector<uint8_t>>> tppt;
+        std::vector<std::pair<uint32_t, std::vector<uint8_t>>> tppt, tmark;
         while (j + 4 <= end && S.be16(j) != 0xff93) {
             if (S.be16(j) == 0xff5f) parse_poc(S, j + 4, S.be16(j + 2), W.nc, tpoc);   // tile-part POC
             if (S.be16(j) == 0xff61) tppt.push_back(read_ppt(S, j + 4, S.be16(j + 2), Hd));
-            check_override_marker(S, j + 4, S.be16(j), S.be16(j + 2), Hd, true);
+            collect_coding_marker(S, j + 4, S.be16(j), S.be16(j + 2), Hd, tmark);
             j += 2 + S.be16(j + 2);
         }
         if (j + 2 > end || S.be16(j) != 0xff93) throw GkError("missing SOD");
         Hd.parts.push_back({isot, pos, j + 2, end, {}, {}, S.at(pos + 10), std::move(tpoc)});
         Hd.parts.back().ppt = std::move(tppt);
+        Hd.parts.back().cmark = std::move(tmark);
         pos = end;
     }
 }
 // A TLM whose lengths do not lead from SOT to SOT (read_tile_part_headers)
 struct TlmMismatch : GkError { TlmMismatch() : GkError("TLM does not match the SOT markers") {} };
+
+// COD body (Scod, SGcod, SPcod; read_cod :2521-2623) into the stream-level fields (progression,
+// SOP / EPH, layers, MCT) and the default coding of p
+static void read_cod_fields(const std::vector<uint8_t>& b, Params& p) {
+    if (b.size() < 10) throw GkError("corrupt COD marker");
+    const uint32_t scod = b[0];
+    if (b[1] > 4) throw GkError("corrupt COD marker (progression order)");
+    p.prog = b[1];
+    p.sop_eph = scod & 6;
+    p.nlayers = (uint32_t)b[2] << 8 | b[3];
+    if (!p.nlayers) throw GkError("corrupt COD marker (no layers)");
+    p.mct = b[4];
+    // SGcod MCT: 0 none, 1 RCT / ICT; 2 = a Part-2 array transform (MCT / MCC / MCO markers,
+    // Grok's decompress_custom), not on this path
+    if (p.mct > 1) throw GkError("Part-2 array multiple-component transforms are not supported on this path");
+    p.numres = b[5] + 1;
+    // at most 32 decomposition levels (CodeStreamDecompress.cpp:1733)
+    if (p.numres > GK_MAXRLVLS) throw GkError("corrupt COD marker (more than 32 decomposition levels)");
+    p.cbw = b[6] + 2; p.cbh = b[7] + 2;
+    if (p.cbw > 10 || p.cbh > 10 || p.cbw + p.cbh > 12) throw GkError("corrupt COD marker (code-block size)");
+    p.cblk_sty = b[8];
+    if ((p.cblk_sty & GK_STY_HT) && p.cblk_sty != GK_STY_HT)
+        throw GkError("HTJ2K combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781-1788
+    if (p.cblk_sty > 0x7f) throw GkError("unknown code-block style bits");
+    p.irrev = b[9] == 0 ? 1 : 0;
+    p.custom_prc = false;
+    for (int k = 0; k < GK_MAXRLVLS; ++k) { p.prcw[k] = 15; p.prch[k] = 15; }
+    if (scod & 1) {
+        if (b.size() < 10 + p.numres) throw GkError("corrupt COD marker (precinct sizes)");
+        p.custom_prc = true;
+        for (uint32_t r = 0; r < p.numres; ++r) {
+            const uint32_t v = b[10 + r]; p.prcw[r] = v & 15; p.prch[r] = v >> 4;
+            if (r > 0 && (!p.prcw[r] || !p.prch[r])) throw GkError("COD: precinct exponent 0 above resolution 0");
+        }
+    }
+}
+// The coding of every component (Params::cc when they differ) and the quantisation (Hd.qcd) from
+// the COD, the per-component COC-form bodies and the quantisation bodies; MCT restrictions checked
+static void apply_coding(Header& Hd) {
+    Plan& W = Hd.want;
+    W.p.cc.clear();
+    bool differ = false;
+    for (uint32_t c = 0; c < W.nc; ++c) differ = differ || Hd.ccod[c] != Hd.ccod[0] || Hd.ccod[c] != cod_as_coc(Hd.cod);
+    if (differ) {
+        W.p.cc.resize(W.nc);
+        for (uint32_t c = 0; c < W.nc; ++c) comp_coding(Hd.ccod[c], W.p.cc[c]);
+        // the inverse MCT picks RCT / ICT by component 0's transform (TileProcessor::mctDecompress)
+        if (W.p.mct && W.nc >= 3 && (W.p.cc[1].irrev != W.p.cc[0].irrev || W.p.cc[2].irrev != W.p.cc[0].irrev))
+            throw GkError("MCT over components with different transforms is not supported");
+    }
+    if (W.p.mct && W.nc >= 3 && (W.c_prec(1) != W.c_prec(0) || W.c_prec(2) != W.c_prec(0) ||
+                                 W.c_sgnd(1) != W.c_sgnd(0) || W.c_sgnd(2) != W.c_sgnd(0)))
+        throw GkError("MCT over components of different precisions or signs is not supported on this path");
+    Hd.qcd.clear();
+    for (uint32_t c = 0; c < W.nc; ++c) parse_quant(Hd.qbody[c], W.p.c_numres(c), Hd.qcd);
+}
 
 static void parse_header(ByteSrc& S, Header& Hd) {
     size_t i = 0;
@@ -3877,35 +3957,9 @@ static void parse_header(ByteSrc& S, Header& Hd) {
             have_siz = true;
         } else if (m == 0xff52) {
             if (L < 12) throw GkError("corrupt COD marker");
-            uint32_t scod = S.at(s);
-            if (S.at(s + 1) > 4) throw GkError("corrupt COD marker (progression order)");
-            W.p.prog = S.at(s + 1);
-            W.p.sop_eph = scod & 6;
-            W.p.nlayers = S.be16(s + 2);
-            W.p.mct = S.at(s + 4);
-            // SGcod MCT: 0 none, 1 RCT / ICT; 2 = a Part-2 array transform (MCT / MCC / MCO markers,
-            // Grok's decompress_custom), not on this path
-            if (W.p.mct > 1) throw GkError("Part-2 array multiple-component transforms are not supported on this path");
-            W.p.numres = S.at(s + 5) + 1;
-            // at most 32 decomposition levels (CodeStreamDecompress.cpp:1733)
-            if (W.p.numres > GK_MAXRLVLS) throw GkError("corrupt COD marker (more than 32 decomposition levels)");
-            W.p.cbw = S.at(s + 6) + 2; W.p.cbh = S.at(s + 7) + 2;
-            if (W.p.cbw > 10 || W.p.cbh > 10 || W.p.cbw + W.p.cbh > 12) throw GkError("corrupt COD marker (code-block size)");
-            W.p.cblk_sty = S.at(s + 8);
-            if ((W.p.cblk_sty & GK_STY_HT) && W.p.cblk_sty != GK_STY_HT)
-                throw GkError("HTJ2K combined with Part-1 mode switches");   // CodeStreamDecompress.cpp:1781-1788
-            if (W.p.cblk_sty > 0x7f) throw GkError("unknown code-block style bits");
-            W.p.irrev = S.at(s + 9) == 0 ? 1 : 0;
-            if (scod & 1) {
-                if (L < 12 + W.p.numres) throw GkError("corrupt COD marker (precinct sizes)");
-                W.p.custom_prc = true;
-                for (uint32_t r = 0; r < W.p.numres; ++r) {
-                    uint32_t v = S.at(s + 10 + r); W.p.prcw[r] = v & 15; W.p.prch[r] = v >> 4;
-                    if (r > 0 && (!W.p.prcw[r] || !W.p.prch[r])) throw GkError("COD: precinct exponent 0 above resolution 0");
-                }
-            }
-            have_cod = true;
             Hd.cod = marker_body(S, s, L);
+            read_cod_fields(Hd.cod, W.p);
+            have_cod = true;
         } else if (m == 0xff5c) {
             if (L < 4) throw GkError("corrupt QCD marker");
             W.p.numgbits = S.at(s) >> 5;
@@ -3971,21 +4025,7 @@ static void parse_header(ByteSrc& S, Header& Hd) {
         if (c >= W.nc) throw GkError("bad component number in COC/QCC");
         Hd.ccod[c].assign(b.begin() + cw, b.end());
     }
-    W.p.cc.clear();
-    bool differ = false;
-    for (uint32_t c = 0; c < W.nc; ++c) differ = differ || Hd.ccod[c] != Hd.ccod[0] || Hd.ccod[c] != cod_as_coc(Hd.cod);
-    if (differ) {
-        W.p.cc.resize(W.nc);
-        for (uint32_t c = 0; c < W.nc; ++c) comp_coding(Hd.ccod[c], W.p.cc[c]);
-        // the inverse MCT picks RCT / ICT by component 0's transform (TileProcessor::mctDecompress)
-        if (W.p.mct && W.nc >= 3 && (W.p.cc[1].irrev != W.p.cc[0].irrev || W.p.cc[2].irrev != W.p.cc[0].irrev))
-            throw GkError("MCT over components with different transforms is not supported");
-    }
-    if (W.p.mct && W.nc >= 3 && (W.c_prec(1) != W.c_prec(0) || W.c_prec(2) != W.c_prec(0) ||
-                                 W.c_sgnd(1) != W.c_sgnd(0) || W.c_sgnd(2) != W.c_sgnd(0)))
-        throw GkError("MCT over components of different precisions or signs is not supported on this path");
-    Hd.qcd.clear();
-    for (uint32_t c = 0; c < W.nc; ++c) parse_quant(Hd.qbody[c], W.p.c_numres(c), Hd.qcd);
+    apply_coding(Hd);
     // tile parts: SOT (Isot, Psot, TPsot, TNsot), tile-part header markers (PLT, ...), SOD, packets
     // (CodeStreamDecompress SOT/SOD handlers; TLM and PLT are only needed for random access)
     size_t pos = Hd.first_sot;
@@ -4048,7 +4088,7 @@ static void read_tile_part_headers(gk_ctx* ctx, ByteSrc& S, Header& Hd) {
             const uint32_t m = S.be16(j), L = S.be16(j + 2);
             if (m == 0xff5f) parse_poc(S, j + 4, L, nc, TP.pocs);   // tile-part POC
             if (m == 0xff61) TP.ppt.push_back(read_ppt(S, j + 4, L, Hd));
-            check_override_marker(S, j + 4, m, L, Hd, true);
+            collect_coding_marker(S, j + 4, m, L, Hd, TP.cmark);
             if (m == 0xff58) {
                 uint32_t v = 0;
                 for (size_t q = j + 5; q < j + 2 + L; ++q) {
@@ -4111,6 +4151,7 @@ static void merge_tile_parts(Header& Hd) {
         if (TP.tpsot != H.more.size() + 1) throw GkError("tile parts out of order (TPsot)");
         H.more.push_back({TP.data, TP.end});
         for (auto& e : TP.ppt) H.ppt.push_back(std::move(e));
+        for (auto& e : TP.cmark) H.cmark.push_back(std::move(e));
         H.plt.insert(H.plt.end(), TP.plt.begin(), TP.plt.end());
         H.pocs.insert(H.pocs.end(), TP.pocs.begin(), TP.pocs.end());
     }
@@ -4158,14 +4199,26 @@ static void merge_tile_parts(Header& Hd) {
     Hd.parts.swap(out);
 }
 
+// A pass over some of the stream's tiles (tiles coded with their own parameters): the tiles it
+// decodes, their coding (else the main header's), the output frame's origin (image-relative; the
+// caller's window origin) and the inverse rule of the whole call
+struct TilePass {
+    std::vector<uint8_t> tiles;   // by tile index: decoded in this pass
+    const TileCoding* coding = nullptr;
+    uint32_t fx = 0, fy = 0;
+    bool partial = false;
+};
 static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_device, void* const* comps,
-                        const uint32_t* strides, uint32_t sample_bytes, int out_on_device, const uint32_t* win = nullptr) {
+                        const uint32_t* strides, uint32_t sample_bytes, int out_on_device, const uint32_t* win = nullptr,
+                        const TilePass* pass = nullptr) {
     hipStream_t st = ctx->st;
     launch_check(__LINE__);
     HIPCHK(hipEventRecord(ctx->ev[0], st));
+    const uint8_t* const cs_in = cs;
+    const size_t len_in = len;
     // Grok's partial-tile inverse (its single odd 5/3 sample shifted, not halved) follows a window
     // set with setDecompressWindow; decompressTile without one keeps the whole-tile rule
-    ctx->dwt_partial = win != nullptr && !ctx->win_whole_tile;
+    ctx->dwt_partial = pass ? pass->partial : win != nullptr && !ctx->win_whole_tile;
     // GK_PROFILE=1: host phase times of the decode (stderr)
     static const bool prof = getenv("GK_PROFILE") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
@@ -4186,6 +4239,11 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     }
     Header Hd;
     parse_header(S, Hd);
+    if (pass && pass->coding) {   // the pass's tiles: their own coding and quantisation
+        Hd.cod = pass->coding->cod; Hd.ccod = pass->coding->ccod; Hd.qbody = pass->coding->qbody;
+        read_cod_fields(Hd.cod, Hd.want.p);
+        apply_coding(Hd);
+    }
     if (Hd.want.nc < 3) Hd.want.p.mct = 0;
     ensure_plan(ctx, Hd.want);
     Plan& P = ctx->plan;
@@ -4225,6 +4283,55 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         }
     }
     merge_tile_parts(Hd);
+    if (pass) {
+        std::vector<TilePart> keep;
+        for (auto& TP : Hd.parts)
+            if (TP.tile < pass->tiles.size() && pass->tiles[TP.tile]) keep.push_back(std::move(TP));
+        Hd.parts.swap(keep);
+        if (Hd.parts.empty()) throw GkError("internal: a tile pass without tiles");
+    } else {
+        // tiles coded with their own parameters (tile-part COD / COC / QCD / QCC): the tiles with
+        // the main header's coding in one pass, then each other tile in a pass of its own, through
+        // its rectangle (clipped to the window) into the same output frame.  Passes write disjoint
+        // tile rectangles in stream order on one HIP stream; a tile absent from a pass's tile
+        // rectangle is written as zero by that pass before its own pass writes it.
+        std::vector<TileCoding> own(Hd.parts.size());
+        std::vector<uint8_t> differs(Hd.parts.size(), 0);
+        bool any = false;
+        for (size_t q = 0; q < Hd.parts.size(); ++q) {
+            if (Hd.parts[q].cmark.empty()) continue;
+            differs[q] = tile_coding(Hd, Hd.parts[q], own[q]);
+            any = any || differs[q];
+        }
+        if (any) {
+            const size_t ntl = P.tiles.size();
+            const uint32_t full[4] = {0, 0, P.w, P.h};
+            const uint32_t* wv = win ? win : full;
+            TilePass base;
+            base.tiles.assign(ntl, 0);
+            base.fx = win ? win[0] : 0; base.fy = win ? win[1] : 0;
+            base.partial = ctx->dwt_partial;
+            bool main_tiles = false;
+            for (size_t q = 0; q < Hd.parts.size(); ++q)
+                if (!differs[q] && Hd.parts[q].tile < ntl) { base.tiles[Hd.parts[q].tile] = 1; main_tiles = true; }
+            if (main_tiles) decode_impl(ctx, cs_in, len_in, cs_on_device, comps, strides, sample_bytes, out_on_device, win, &base);
+            for (size_t q = 0; q < Hd.parts.size(); ++q) {
+                if (!differs[q]) continue;
+                const uint32_t t = Hd.parts[q].tile;
+                if (t >= ntl) throw GkError("corrupt SOT (tile index)");
+                const TileG& T = P.tiles[t];
+                const uint32_t tw[4] = {std::max(T.x0 - P.x0, wv[0]), std::max(T.y0 - P.y0, wv[1]),
+                                        std::min(T.x1 - P.x0, wv[2]), std::min(T.y1 - P.y0, wv[3])};
+                if (tw[0] >= tw[2] || tw[1] >= tw[3]) continue;
+                TilePass tp = base;
+                tp.tiles.assign(ntl, 0);
+                tp.tiles[t] = 1;
+                tp.coding = &own[q];
+                decode_impl(ctx, cs_in, len_in, cs_on_device, comps, strides, sample_bytes, out_on_device, tw, &tp);
+            }
+            return;
+        }
+    }
     if (S.dev) prefetch_packet_headers(ctx, S, P, Hd);
     // ---- tiles present, their rectangle, and the code-blocks that reach the output
     std::vector<int32_t> part_of(P.tiles.size(), -1);
@@ -4250,6 +4357,7 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
         rx0 = std::max(rx0, win[0]); ry0 = std::max(ry0, win[1]); rx1 = std::min(rx1, win[2]); ry1 = std::min(ry1, win[3]);
         ox = win[0]; oy = win[1];
     }
+    if (pass) { ox = pass->fx; oy = pass->fy; }
     const uint32_t ncols = rx1 - rx0, nrows = ry1 - ry0;
     // the region on each sampling group's grid (RG itself without subsampling)
     std::vector<Region> RGg;
