@@ -5064,12 +5064,13 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
             qx0[c] = rx(RG.x0 + P.x0) - rox[c]; qy0[c] = ry(RG.y0 + P.y0) - roy[c];
             qx1[c] = rx(RG.x0 + P.x0 + RG.w) - rox[c]; qy1[c] = ry(RG.y0 + P.y0 + RG.h) - roy[c];
             if (win) {
-                wx0[c] = rx(win[0] + P.x0) - rox[c]; wy0[c] = ry(win[1] + P.y0) - roy[c];
-                qx0[c] = std::max(qx0[c], wx0[c]); qy0[c] = std::max(qy0[c], wy0[c]);
+                qx0[c] = std::max(qx0[c], rx(win[0] + P.x0) - rox[c]); qy0[c] = std::max(qy0[c], ry(win[1] + P.y0) - roy[c]);
                 qx1[c] = std::min(qx1[c], rx(win[2] + P.x0) - rox[c]);
                 qy1[c] = std::min(qy1[c], ry(win[3] + P.y0) - roy[c]);
                 if (qx1[c] <= qx0[c] || qy1[c] <= qy0[c]) throw GkError("the window is empty at this reduction");
             }
+            // the caller plane's origin: the window's (a tile pass: the whole call's frame), or the image's
+            wx0[c] = rx(ox + P.x0) - rox[c]; wy0[c] = ry(oy + P.y0) - roy[c];
         }
         std::vector<uint8_t*> qd(P.nc);
         std::vector<uint32_t> qs(P.nc);
