@@ -288,3 +288,33 @@ def test_grk_api_comments(tool, flags):
     ref = O.encode(img, 8, comments=["first", "second comment"], **parse_flags(flags))
     assert cs == ref
     assert cs.count(b"\xff\x64") == 2 and b"Created by Grok" not in cs
+
+
+@pytest.mark.parametrize("kind", ["tile_coding", "coc", "ppm"])
+def test_grk_api_third_party_streams(tool, kind):
+    # grk_decompress's call sequence on streams Grok's encoder never writes but its decoder reads:
+    # tiles with their own coding (tile-part COD / QCD), per-component COC / QCC, PPM packed
+    # headers; the shim returns the oracle's samples, also through -tile (Grok's whole-tile rule)
+    exe, d = tool
+    if kind == "tile_coding":
+        import tile_coding
+        cs = tile_coding.stream("levels_cblk")
+    elif kind == "coc":
+        import test_coc
+        cs = test_coc.stream("levels_cblk_97_prc")
+    else:
+        import test_ppx
+        cs = test_ppx.stream("tiles_sop_eph", "ppm")
+    path = d / ("third_%s.j2k" % kind)
+    path.write_bytes(cs)
+    dec = d / ("third_%s.dec" % kind)
+    _run(exe, "dec", path, dec)
+    want, _ = O.decode(cs)
+    want = want if isinstance(want, list) else list(want)
+    np.testing.assert_array_equal(np.fromfile(dec, np.int32), np.concatenate([w.ravel() for w in want]))
+    if kind == "tile_coding":   # tile 1 (B-coded) alone
+        import tile_coding
+        x0, y0, x1, y1 = tile_coding.tile_rects("levels_cblk")[1]
+        _run(exe, "dec", path, dec, "-tile", "1")
+        full = tile_coding.expected("levels_cblk")
+        np.testing.assert_array_equal(np.fromfile(dec, np.int32), full[:, y0:y1, x0:x1].ravel())
