@@ -3741,11 +3741,10 @@ static std::vector<uint8_t> marker_body(ByteSrc& S, size_t s, uint32_t L) {
 // the main header's: CodeStreamDecompress read_cod / read_coc / read_qcd / read_qcc); collected per
 // tile part here, applied by tile_coding.  COC: Ccoc (1 byte below 257 components, else 2), Scoc
 // (precinct flag), then SPcoc laid out as COD's SPcod; QCC: Cqcc, then Sqcc / SPqcc as QCD's body.
-// A tile-part RGN is refused.
+// Tile-part RGN: the tile's ROI shift of one component (read_rgn :1476-1520).
 static void collect_coding_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, const Header& Hd,
                                   std::vector<std::pair<uint32_t, std::vector<uint8_t>>>& out) {
-    if (m == 0xff5e) throw GkError("RGN in a tile-part header is not supported on this path");
-    if (m != 0xff52 && m != 0xff53 && m != 0xff5c && m != 0xff5d) return;
+    if (m != 0xff52 && m != 0xff53 && m != 0xff5c && m != 0xff5d && m != 0xff5e) return;
     if (L < 3) throw GkError("corrupt COD/COC/QCD/QCC marker");
     std::vector<uint8_t> b = marker_body(S, s, L);
     const uint32_t nc = Hd.want.nc, cw = nc <= 256 ? 1 : 2;
@@ -3756,6 +3755,13 @@ static void collect_coding_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, 
         if (m == 0xff53 && b.size() < cw + 6) throw GkError("corrupt COC marker");
     }
     if (m == 0xff52 && b.size() < 10) throw GkError("corrupt COD marker");
+    if (m == 0xff5e) {   // Crgn, Srgn, SPrgn
+        if (b.size() != cw + 2) throw GkError("corrupt RGN marker");
+        const uint32_t c = cw == 1 ? b[0] : (uint32_t)b[0] << 8 | b[1];
+        if (c >= nc) throw GkError("bad component number in RGN");
+        if (b[cw] != 0) throw GkError("only the implicit (maxshift) ROI style is defined");
+        if (b[cw + 1] >= 32) throw GkError("unsupported ROI shift");
+    }
     out.push_back({m, std::move(b)});
 }
 // A tile's coding and quantisation: the main header's (cod, ccod, qbody) changed by its tile-part
@@ -3764,10 +3770,13 @@ static void collect_coding_marker(ByteSrc& S, size_t s, uint32_t m, uint32_t L, 
 // quantisation follows read_SQcd_SQcc's scoping (Quantizer.cpp:208-235): a tile QCC wins over a
 // tile QCD, which wins over the main header's QCC / QCD, in any marker order.  True when the tile
 // is coded differently from the main header.
-struct TileCoding { std::vector<uint8_t> cod; std::vector<std::vector<uint8_t>> ccod, qbody; };
+struct TileCoding { std::vector<uint8_t> cod; std::vector<std::vector<uint8_t>> ccod, qbody; std::vector<uint8_t> roi; };
 static bool tile_coding(const Header& Hd, const TilePart& H, TileCoding& tc) {
     tc.cod = Hd.cod; tc.ccod = Hd.ccod; tc.qbody = Hd.qbody;
     const uint32_t nc = Hd.want.nc, cw = nc <= 256 ? 1 : 2;
+    std::vector<uint8_t> main_roi(nc, 0);
+    for (uint32_t c = 0; c < nc && c < Hd.want.p.roishift.size(); ++c) main_roi[c] = Hd.want.p.roishift[c];
+    tc.roi = main_roi;
     std::vector<uint8_t> tqcc(nc, 0);
     for (const auto& mk : H.cmark) {
         const std::vector<uint8_t>& v = mk.second;
@@ -3776,6 +3785,8 @@ static bool tile_coding(const Header& Hd, const TilePart& H, TileCoding& tc) {
             for (auto& q : tc.ccod) q = cod_as_coc(v);
         } else if (mk.first == 0xff5c) {
             for (uint32_t c = 0; c < nc; ++c) if (!tqcc[c]) tc.qbody[c] = v;
+        } else if (mk.first == 0xff5e) {
+            tc.roi[cw == 1 ? v[0] : (uint32_t)v[0] << 8 | v[1]] = v[cw + 1];
         } else {
             const uint32_t c = cw == 1 ? v[0] : (uint32_t)v[0] << 8 | v[1];
             std::vector<uint8_t> b(v.begin() + cw, v.end());
@@ -3783,7 +3794,7 @@ static bool tile_coding(const Header& Hd, const TilePart& H, TileCoding& tc) {
             else tc.ccod[c] = std::move(b);
         }
     }
-    return tc.cod != Hd.cod || tc.ccod != Hd.ccod || tc.qbody != Hd.qbody;
+    return tc.cod != Hd.cod || tc.ccod != Hd.ccod || tc.qbody != Hd.qbody || tc.roi != main_roi;
 }
 // The tiles of the canvas tile grid (B.3)
 static uint32_t grid_tiles(const Plan& W) {
@@ -4242,6 +4253,10 @@ static void decode_impl(gk_ctx* ctx, const uint8_t* cs, size_t len, int cs_on_de
     if (pass && pass->coding) {   // the pass's tiles: their own coding and quantisation
         Hd.cod = pass->coding->cod; Hd.ccod = pass->coding->ccod; Hd.qbody = pass->coding->qbody;
         read_cod_fields(Hd.cod, Hd.want.p);
+        Hd.want.p.roishift.assign(pass->coding->roi.begin(), pass->coding->roi.end());
+        bool any_roi = false;
+        for (uint8_t r : pass->coding->roi) any_roi = any_roi || r;
+        if (!any_roi) Hd.want.p.roishift.clear();
         apply_coding(Hd);
     }
     if (Hd.want.nc < 3) Hd.want.p.mct = 0;

@@ -3252,7 +3252,8 @@ static bool read_cod(const std::vector<uint8_t>& v, Params& p) {
 // component, read_coc (:2631-2670) sets one component's, both in marker order; quantisation follows
 // read_SQcd_SQcc's scoping (Quantizer.cpp:208-235): a tile QCC wins over a tile QCD, which wins over
 // the main header's QCC / QCD, in any marker order.
-struct TileCoding { std::vector<uint8_t> cod; std::vector<std::vector<uint8_t>> ccod, qbody; };
+// A tile-part RGN sets the tile's ROI shift of its component (read_rgn, :1476-1520).
+struct TileCoding { std::vector<uint8_t> cod; std::vector<std::vector<uint8_t>> ccod, qbody; std::vector<uint32_t> roi; };
 static bool tile_coding(const std::vector<std::pair<uint32_t, std::vector<uint8_t>>>& marks, uint32_t nc, TileCoding& tc) {
     const uint32_t cw = nc <= 256 ? 1 : 2;
     std::vector<uint8_t> tqcc(nc, 0);
@@ -3265,6 +3266,11 @@ static bool tile_coding(const std::vector<std::pair<uint32_t, std::vector<uint8_
         } else if (mk.first == 0xff5c) {
             if (v.size() < 2) return false;
             for (uint32_t c = 0; c < nc; ++c) if (!tqcc[c]) tc.qbody[c] = v;
+        } else if (mk.first == 0xff5e) {   // Crgn, Srgn (0: implicit), SPrgn (< 32)
+            if (v.size() != cw + 2) return false;
+            const uint32_t c = cw == 1 ? v[0] : get16(v.data());
+            if (c >= nc || v[cw] != 0 || v[cw + 1] >= 32) return false;
+            tc.roi[c] = v[cw + 1];
         } else {
             if (v.size() < cw + 2) return false;
             const uint32_t c = cw == 1 ? v[0] : get16(v.data());
@@ -3437,6 +3443,7 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
     auto setup = [&](const TileCoding& tc, Params& pt, std::vector<Params>& pcs_t, std::vector<Quant>& cq_t,
                      uint32_t& min_res) -> int {
         if (!read_cod(tc.cod, pt)) return -2;
+        pt.roishift = tc.roi;
         pcs_t.assign(im.nc, pt);
         min_res = 33;
         for (uint32_t c = 0; c < im.nc; ++c) {
@@ -3455,7 +3462,9 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
             if (!parse_quant(tc.qbody[c].data(), tc.qbody[c].size(), pcs_t[c].numres, cq_t[c])) return -2;
         return g_dec_reduce >= min_res ? -7 : 0;   // reduce must leave one resolution of every component
     };
-    const TileCoding main_tc{cod_body, ccod, qbody};
+    std::vector<uint32_t> main_roi(im.nc, 0);
+    for (uint32_t c = 0; c < im.nc; ++c) main_roi[c] = p.roi(c);
+    const TileCoding main_tc{cod_body, ccod, qbody, main_roi};
     std::vector<Params> pcs;
     std::vector<Quant> cq;
     uint32_t min_res = 33;
@@ -3502,12 +3511,11 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
                 tp_ppt.push_back({cs[j + 4], std::vector<uint8_t>(cs + j + 5, cs + j + 2 + Lp)});
             }
             if (tm == 0xff5f && !read_poc(cs + j + 4, get16(cs + j + 2), im.nc, tp_pocs)) return -5;
-            if (tm == 0xff52 || tm == 0xff53 || tm == 0xff5c || tm == 0xff5d) {   // the tile's coding / quantisation
+            if (tm == 0xff52 || tm == 0xff53 || tm == 0xff5c || tm == 0xff5d || tm == 0xff5e) {   // the tile's coding / quantisation / ROI
                 const uint32_t Lm = get16(cs + j + 2);
                 if (Lm < 3 || j + 2 + Lm > tile_end) return -5;
                 tp_marks.push_back({tm, std::vector<uint8_t>(cs + j + 4, cs + j + 2 + Lm)});
             }
-            if (tm == 0xff5e) return -2;   // tile-part RGN
             j += 2 + get16(cs + j + 2);
         }
         if (j + 2 > tile_end) return -5;
@@ -3575,7 +3583,8 @@ int orc_decode(const uint8_t* cs, size_t len, int32_t* out, uint32_t* W, uint32_
         if (marks.empty()) continue;
         TileCoding tc = main_tc;
         if (!tile_coding(marks, im.nc, tc)) return -2;
-        if (tc.cod == main_tc.cod && tc.ccod == main_tc.ccod && tc.qbody == main_tc.qbody) continue;   // restated
+        if (tc.cod == main_tc.cod && tc.ccod == main_tc.ccod && tc.qbody == main_tc.qbody && tc.roi == main_tc.roi)
+            continue;   // restated
         own[q].reset(new TileParams{p, {}, {}});
         uint32_t tmin = 33;
         if (int rc = setup(tc, own[q]->p, own[q]->pcs, own[q]->cq, tmin)) return rc;

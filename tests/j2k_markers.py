@@ -49,6 +49,12 @@ def qcc(cs, comp, guard_add=0):
     return segment(0xff5d, comp.to_bytes(cw, "big") + bytes(q))
 
 
+def rgn(cs, comp, shift):
+    """RGN for `comp`: implicit (maxshift) style, ROI shift `shift` (A.6.3)."""
+    cw = 1 if ncomp(cs) <= 256 else 2
+    return segment(0xff5e, comp.to_bytes(cw, "big") + bytes([0, shift]))
+
+
 def cod(cs, layers_add=0):
     b = bytearray(body(cs, 0xff52))
     n = int.from_bytes(b[2:4], "big") + layers_add

@@ -6,7 +6,7 @@ to its component (tests/test_qcc.py, tests/test_coc.py); tile-part markers set t
 (tests/test_tile_coding.py for streams coded that way).  Here the committed Grok fixtures get
 markers spliced in (tests/j2k_markers.py): markers that restate the main header decode exactly as
 the stream without them (some encoders write them unconditionally); markers that change the first
-tile's code-block style or guard bits decode as OpenJPEG 2.5.4 decodes them (sample for sample,
+tile's code-block style, guard bits or ROI shift decode as OpenJPEG 2.5.4 decodes them (sample for sample,
 9/7 included); a tile COD with one more layer than the tile holds reads the tile as truncated, i.e.
 as before.  The engine half is tests/test_gpu_override_markers.py.
 """
@@ -41,6 +41,7 @@ def changing(cs):
     yield "tile COD", J.insert_tile_part(cs, J.cod(cs, layers_add=1))
     yield "tile COC", J.insert_tile_part(cs, J.coc(cs, 0, sty_xor=0x08))
     yield "tile QCC", J.insert_tile_part(cs, J.qcc(cs, 0, guard_add=1))
+    yield "tile RGN", J.insert_tile_part(cs, J.rgn(cs, 0, 3))
 
 
 def refused(cs):
@@ -67,6 +68,18 @@ def test_changing_tile_markers_applied(name):
         elif fx.ht and what == "tile COC":   # HT with a Part-1 mode switch (CodeStreamDecompress.cpp:1781)
             with pytest.raises(RuntimeError, match="failed: -2"):
                 O.decode(cs)
+        elif what == "tile RGN":
+            # maxshift ROI over data coded without one: every nonzero index is at or above the
+            # shift once the bit-planes move up, so the descale restores it (OpenJPEG agrees);
+            # the tile's shift is read, the samples stay.  (HT: OpenJPEG refuses; the engine
+            # half compares with the oracle.)
+            got, _ = O.decode(cs)
+            if fx.ht:
+                continue
+            np.testing.assert_array_equal(got, fx.grok_decoded)
+            if openjpeg.available():
+                for (dx, dy, r), g in zip(openjpeg.decode(cs), got):
+                    np.testing.assert_array_equal(r, g)
         elif fx.ht:   # HT places magnitudes by the zero bit-plane count alone: guard bits do not move them
             np.testing.assert_array_equal(O.decode(cs)[0], fx.grok_decoded)
         else:

@@ -13,6 +13,7 @@ Marker forms for a B tile:
   "coc":   COC(c, B) + QCC(c, B) for every c (B's Scod / SGcod must equal A's)
   "scope": QCC(c, B) for every c, COD(B), then QCD(A): a tile QCC wins over the tile QCD in any
            order (Quantizer.cpp:208-235), so A's QCD is ignored
+  "rgn":   B's RGN markers (B = A with an ROI shift: the tile's own ROI, read_rgn)
 """
 import os
 import struct
@@ -58,7 +59,7 @@ def _coc_form(cod):
     return bytes([cod[0] & 1]) + bytes(cod[5:])
 
 
-def marker_segments(a_main, b_main, nc, form):
+def marker_segments(a_main, b_main, nc, form, b_segs=()):
     cod_b, qcd_b, qcd_a = b_main[0xFF52], b_main[0xFF5C], a_main[0xFF5C]
     cw = 1 if nc <= 256 else 2
     cid = lambda c: c.to_bytes(cw, "big")
@@ -71,6 +72,8 @@ def marker_segments(a_main, b_main, nc, form):
     if form == "scope":
         return (b"".join(_seg(0xFF5D, cid(c) + qcd_b) for c in range(nc)) + _seg(0xFF52, cod_b) +
                 _seg(0xFF5C, qcd_a))
+    if form == "rgn":
+        return b"".join(seg for m, seg in b_segs if m == 0xFF5E)
     raise ValueError(form)
 
 
@@ -78,7 +81,7 @@ def splice(cs_a, cs_b, tiles, form="cod", tlm=False):
     """cs_a with the parts of `tiles` taken from cs_b, each behind the tile-part markers of `form`
     stating B's coding.  tlm: write a TLM marker (Ttlm 16 bits, Ptlm 32 bits) for the result."""
     a_main, a_segs, a_sot = _main(cs_a)
-    b_main, _, b_sot = _main(cs_b)
+    b_main, b_segs, b_sot = _main(cs_b)
     nc = struct.unpack(">H", a_main[0xFF51][34:36])[0]
     pa, pb = _parts(cs_a, a_sot), _parts(cs_b, b_sot)
     assert sorted(pa) == sorted(pb)
@@ -86,7 +89,7 @@ def splice(cs_a, cs_b, tiles, form="cod", tlm=False):
     for t in sorted(pa):
         hdr, data = pb[t] if t in tiles else pa[t]
         if t in tiles:
-            hdr = marker_segments(a_main, b_main, nc, form) + hdr
+            hdr = marker_segments(a_main, b_main, nc, form, b_segs) + hdr
         psot = 12 + len(hdr) + 2 + len(data)
         body += struct.pack(">HHHIBB", 0xFF90, 10, t, psot, 0, 1) + hdr + b"\xff\x93" + data
         lens.append((t, psot))
@@ -108,6 +111,7 @@ CASES = {
     "modes_tile": (80, 96, dict(numres=3, cblk=(32, 32)), dict(numres=3, cblk_sty=0x05), {3}, "cod"),
     "scope_irrev": (80, 96, dict(numres=3), dict(numres=3, irreversible=True), {1, 2}, "scope"),
     "ragged_tiles": (70, 101, dict(numres=3), dict(numres=2, cblk=(16, 16)), {2, 5}, "cod"),
+    "roi_tile": (80, 96, dict(numres=3), dict(numres=3, roi=(1, 9)), {0, 3}, "rgn"),
 }
 
 
