@@ -73,9 +73,10 @@ def _split_marker(cs, code):
         i += 2 + L
 
 
-def test_rgn_in_tile_part_header_refused(eng):
-    """RGN in a tile-part header (read_rgn accepts it there) would change the tile's samples;
-    the decoder refuses it instead of skipping it."""
+def test_rgn_in_tile_part_header(eng):
+    """RGN moved from the main header into the tile-part header: the tile's own ROI shift
+    (read_rgn on the tile's tcp, CodeStreamDecompress.cpp:1476-1520): the stream decodes as before,
+    as the oracle decodes it."""
     import grok_amd as G
     rng = np.random.default_rng(6)
     img = rng.integers(0, 256, size=(1, 40, 48)).astype(np.int32)
@@ -87,8 +88,8 @@ def test_rgn_in_tile_part_header_refused(eng):
     psot = int.from_bytes(body[sot + 6:sot + 10], "big")
     sot_new = body[sot:sot + 6] + ((psot + n) if psot else 0).to_bytes(4, "big") + body[sot + 10:sot + 12]
     spliced = body[:sot] + sot_new + rgn + body[sot + 12:]
-    with pytest.raises(RuntimeError, match="RGN in a tile-part header"):
-        eng.decode(spliced)
+    np.testing.assert_array_equal(eng.decode(spliced), O.decode(spliced)[0])
+    np.testing.assert_array_equal(eng.decode(spliced), img)
     np.testing.assert_array_equal(eng.decode(cs), img)
 
 
