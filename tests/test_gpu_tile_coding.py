@@ -83,3 +83,40 @@ def test_engine_tile_coding_reduce_past_a_tile_refused(eng):
             eng.decode(stream("ragged_tiles"))
     finally:
         eng.set_decode_reduce(0)
+
+
+@pytest.mark.parametrize("reduce", [0, 1])
+def test_engine_tile_coding_device_output(eng, reduce):
+    # the passes write straight into the caller's device planes (int16 samples here)
+    import torch
+    name = "levels_cblk"
+    want = expected(name, reduce=reduce)
+    out = torch.full(want.shape, -1, dtype=torch.int16, device="cuda")
+    eng.set_decode_reduce(reduce)
+    try:
+        eng.decode(stream(name), out=out)
+    finally:
+        eng.set_decode_reduce(0)
+    np.testing.assert_array_equal(out.cpu().numpy().astype(np.int32), want)
+
+
+def test_engine_tile_coding_subsampled():
+    # a 4:2:0 stream whose tile 1 is coded with its own levels and code-blocks
+    import grok_amd as G
+    import tile_coding as TC
+    from subsampling_cases import comp_shape
+    W, H, sub = 96, 80, [(1, 1), (2, 2), (2, 2)]
+    rng = np.random.default_rng(5)
+    src = [rng.integers(0, 256, size=comp_shape(W, H, dx, dy)).astype(np.int32) for dx, dy in sub]
+    a = O.encode(src, 8, size=(W, H), subsampling=sub, tiles=TC.TILES, numres=3)
+    b = O.encode(src, 8, size=(W, H), subsampling=sub, tiles=TC.TILES, numres=2, cblk=(16, 16))
+    cs = TC.splice(a, b, {1}, "cod")
+    want, _ = O.decode(cs)
+    e = G.Engine(0)
+    try:
+        got = e.decode(cs)
+    finally:
+        e.close()
+    for g, w, s in zip(got, want, src):
+        np.testing.assert_array_equal(g, w)
+        np.testing.assert_array_equal(g, s)   # (lossless either way)
