@@ -74,3 +74,17 @@ def test_tile_coding_reduce_past_a_tile_refused():
             O.decode(stream("ragged_tiles"))
     finally:
         O.set_decode_reduce(0)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_engine_header_reads_tile_coding(name):
+    # the engine's header reader (no GPU needed) takes the tile-part markers; a bad component
+    # number in one is refused
+    import grok_amd as G
+    import j2k_markers as J
+    cs = stream(name)
+    info = G.probe_header(cs)
+    H, W = CASES[name][:2]
+    assert (info.w, info.h, info.numcomps) == (W, H, 3)
+    with pytest.raises(ValueError, match="bad component number"):
+        G.probe_header(J.insert_tile_part(cs, J.coc(cs, 3)))
