@@ -87,17 +87,17 @@ def test_engine_tile_coding_reduce_past_a_tile_refused(eng):
 
 @pytest.mark.parametrize("reduce", [0, 1])
 def test_engine_tile_coding_device_output(eng, reduce):
-    # the passes write straight into the caller's device planes (int16 samples here)
+    # the passes write straight into the caller's device planes
     import torch
     name = "levels_cblk"
     want = expected(name, reduce=reduce)
-    out = torch.full(want.shape, -1, dtype=torch.int16, device="cuda")
+    out = torch.full(want.shape, -1, dtype=torch.int32, device="cuda")
     eng.set_decode_reduce(reduce)
     try:
         eng.decode(stream(name), out=out)
     finally:
         eng.set_decode_reduce(0)
-    np.testing.assert_array_equal(out.cpu().numpy().astype(np.int32), want)
+    np.testing.assert_array_equal(out.cpu().numpy(), want)
 
 
 def test_engine_tile_coding_subsampled():
