@@ -187,14 +187,15 @@ int gk_set_decode_layers(gk_ctx* ctx, uint32_t max_layers);
  * CodeStreamDecompress.cpp:471-481). */
 int gk_set_decode_reduce(gk_ctx* ctx, uint32_t reduce);
 
-/* grk_image_comp::dx / dy of the components of later gk_encode / gk_main_header calls (SIZ XRsiz /
+/* grk_image_comp::dx / dy of the components of later gk_encode / gk_encode_tiles / gk_main_header calls (SIZ XRsiz /
  * YRsiz, 1..255; numcomps = 0 clears it).  Component c's plane then holds the image area sampled
  * every (dx[c], dy[c]) canvas positions: ceil((x0 + w) / dx) - ceil(x0 / dx) columns and the same
  * in y (grk_image_comp w / h), row stride strides[c].  Its tile-components are the tiles divided
  * by (dx, dy), rounded up (TileProcessor.cpp:116-131); the MCT is cleared unless the first three
  * components share a grid (CodeStreamCompress.cpp:501-512); rate control takes component 0's
- * factors (updateRates :961).  Tiled images need each factor to divide the tile size; whole images
- * only (no gk_encode_tiles). */
+ * factors (updateRates :961).  Tiled images need each factor to divide the tile size.  With
+ * gk_encode_tiles, comps[c] addresses component c's plane at its row 0 and only the rows of the
+ * selected tiles (on that component's grid) are read. */
 int gk_set_subsampling(gk_ctx* ctx, uint32_t numcomps, const uint32_t* dx, const uint32_t* dy);
 
 /* A stream's components from its header, no device needed (SIZ XRsiz / YRsiz / Ssiz): fills dx[c],
