@@ -36,7 +36,7 @@ def test_engine_tile_coding_device_tlm(eng, name):
     np.testing.assert_array_equal(eng.decode(d, len(cs)), expected(name))
 
 
-@pytest.mark.parametrize("name", ["levels_cblk", "rev_to_irrev", "coc_form", "ht_tile", "ragged_tiles"])
+@pytest.mark.parametrize("name", ["levels_cblk", "rev_to_irrev", "coc_form", "ht_tile", "ragged_tiles", "origin_tiles"])
 def test_engine_tile_coding_reduced(eng, name):
     eng.set_decode_reduce(1)
     try:
@@ -52,7 +52,7 @@ def test_engine_tile_coding_u8(eng):
     np.testing.assert_array_equal(got.astype(np.int32), expected("ht_tile"))
 
 
-@pytest.mark.parametrize("name", ["levels_cblk", "rev_to_irrev", "modes_tile", "ragged_tiles"])
+@pytest.mark.parametrize("name", ["levels_cblk", "rev_to_irrev", "modes_tile", "ragged_tiles", "origin_tiles"])
 @pytest.mark.parametrize("win", [(5, 7, 61, 50), (40, 30, 60, 45), (0, 0, 20, 20)])
 def test_engine_tile_coding_window(eng, name, win):
     H, W = CASES[name][:2]

@@ -35,7 +35,7 @@ def test_oracle_tile_coding_tlm(name):
     np.testing.assert_array_equal(got, expected(name))
 
 
-@pytest.mark.parametrize("name", ["levels_cblk", "rev_to_irrev", "coc_form", "ht_tile", "ragged_tiles"])
+@pytest.mark.parametrize("name", ["levels_cblk", "rev_to_irrev", "coc_form", "ht_tile", "ragged_tiles", "origin_tiles"])
 def test_oracle_tile_coding_reduced(name):
     cs = stream(name)
     O.set_decode_reduce(1)

@@ -113,6 +113,9 @@ CASES = {
     "ragged_tiles": (70, 101, dict(numres=3), dict(numres=2, cblk=(16, 16)), {2, 5}, "cod"),
     "roi_tile": (80, 96, dict(numres=3), dict(numres=3, roi=(1, 9)), {0, 3}, "rgn"),
 }
+# an image area off the canvas origin, tile grid at (0, 0): the first tiles are clipped
+CASES["origin_tiles"] = (75, 90, dict(numres=3, origin=(13, 7), tile_origin=(0, 0)),
+                         dict(numres=4, cblk=(16, 16), origin=(13, 7), tile_origin=(0, 0)), {0, 4}, "cod")
 
 
 def image(name):
@@ -136,12 +139,17 @@ def stream(name, tlm=False):
 
 
 def tile_rects(name):
-    """{tile: (x0, y0, x1, y1)} of the case's tile grid (image at the origin)."""
-    H, W = CASES[name][:2]
+    """{tile: (x0, y0, x1, y1)} of the case's tile grid in image coordinates (B.3: the tiles of the
+    grid at the canvas origin, clipped to the image area)."""
+    H, W, ka = CASES[name][:3]
+    ox, oy = ka.get("origin") or (0, 0)
     tw, th = TILES
-    nx = -(-W // tw)
-    return {t: ((t % nx) * tw, (t // nx) * th, min(W, (t % nx + 1) * tw), min(H, (t // nx + 1) * th))
-            for t in range(nx * -(-H // th))}
+    nx, ny = -(-(ox + W) // tw), -(-(oy + H) // th)
+    out = {}
+    for t in range(nx * ny):
+        i, j = t % nx, t // nx
+        out[t] = (max(i * tw, ox) - ox, max(j * th, oy) - oy, min(ox + W, (i + 1) * tw) - ox, min(oy + H, (j + 1) * th) - oy)
+    return out
 
 
 def expected(name, partial=False, reduce=0):
@@ -155,8 +163,10 @@ def expected(name, partial=False, reduce=0):
         O.set_decode_reduce(0)
     out = da.copy()
     r = 1 << reduce
-    cd = lambda v: -(-v // r)
+    ox, oy = CASES[name][2].get("origin") or (0, 0)
+    cx = lambda v: -(-(v + ox) // r) - -(-ox // r)   # (reduced canvas edges, less the image origin's)
+    cy = lambda v: -(-(v + oy) // r) - -(-oy // r)
     for t, (x0, y0, x1, y1) in tile_rects(name).items():
         if t in CASES[name][4]:
-            out[:, cd(y0):cd(y1), cd(x0):cd(x1)] = db[:, cd(y0):cd(y1), cd(x0):cd(x1)]
+            out[:, cy(y0):cy(y1), cx(x0):cx(x1)] = db[:, cy(y0):cy(y1), cx(x0):cx(x1)]
     return out
