@@ -120,3 +120,13 @@ def test_engine_tile_coding_subsampled():
     for g, w, s in zip(got, want, src):
         np.testing.assert_array_equal(g, w)
         np.testing.assert_array_equal(g, s)   # (lossless either way)
+
+
+@pytest.mark.parametrize("name", ["ht_and_part1", "mode_switches", "wide_block"])
+def test_engine_tile_cod_resets_main_coc(eng, name):
+    import j2k_markers as J
+    import test_coc
+    cs = test_coc.stream(name)
+    t = J.insert_tile_part(cs, J.cod(cs))
+    for g, w in zip(eng.decode(t), O.decode(t)[0]):
+        np.testing.assert_array_equal(g, w)

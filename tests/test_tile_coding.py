@@ -88,3 +88,21 @@ def test_engine_header_reads_tile_coding(name):
     assert (info.w, info.h, info.numcomps) == (W, H, 3)
     with pytest.raises(ValueError, match="bad component number"):
         G.probe_header(J.insert_tile_part(cs, J.coc(cs, 3)))
+
+
+@pytest.mark.parametrize("name", ["ht_and_part1", "mode_switches", "wide_block"])
+def test_tile_cod_resets_main_coc(name):
+    # a tile COD copies its SPcod to every component of the tile, over the main header's COCs
+    # (read_cod :2603-2620; OpenJPEG's opj_j2k_read_cod likewise): the COC streams of
+    # tests/test_coc.py with the main COD restated in the tile-part header decode their COC'd
+    # components with component 0's coding, i.e. wrongly, and the same way in OpenJPEG 2.5.4
+    import j2k_markers as J
+    import test_coc
+    cs = test_coc.stream(name)
+    t = J.insert_tile_part(cs, J.cod(cs))
+    got, _ = O.decode(t)
+    want, _ = O.decode(cs)
+    assert any(not np.array_equal(g, w) for g, w in zip(got, want))
+    if openjpeg.available():
+        for (dx, dy, r), g in zip(openjpeg.decode(t), got):
+            np.testing.assert_array_equal(r, g)
